@@ -1,0 +1,251 @@
+/*
+ * tgsim.h — C ABI of the MI355X-native Testground network simulator (runner "local:mi355x").
+ *
+ * This is the drop-in boundary for Testground's per-message data path. Today that path is
+ *   sidecar.Network.ConfigureNetwork          (reference pkg/sidecar/instance.go:37-42)
+ *     -> NetlinkLink.Shape / AddRules          (pkg/sidecar/link.go:155-217)
+ *     -> handleRoutingPolicy                   (pkg/sidecar/route.go:102-117)
+ *     -> host-kernel HTB + netem + FIB per packet, and
+ *   sync.Client SignalEntry / Barrier          (sdk-go [EXT]; call sites pkg/sidecar/sidecar_handler.go:40-79)
+ * Every entry point below names the reference interface it replaces. A Go runner binds it through
+ * cgo; the Python package testground_amd binds it through ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no torch/HIP types. Host pointers unless a name says "_device".
+ *  - Return 0 on success, a negative TGSIM_E* code on error; tgsim_last_error() has the message.
+ *  - One ctx per OS thread (the HIP current device is per thread). A ctx is not thread-safe.
+ *  - Simulated time is int64 nanoseconds since run start, always >= 0.
+ *  - Instances are global ids 0..n_instances-1. A ctx owns shard [lo, hi) of them (sharding.md in
+ *    DESIGN.md): shaping state of senders in the shard, inboxes of receivers in the shard.
+ *  - The semantics of every call are pinned in DESIGN.md section 2 ("Pinned semantics").
+ */
+#ifndef TGSIM_H
+#define TGSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGSIM_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------------------------- */
+enum {
+  TGSIM_OK = 0,
+  TGSIM_EINVAL = -1,              /* bad argument (kernel/netlink would return EINVAL) */
+  TGSIM_ENOMEM = -2,              /* allocation failed */
+  TGSIM_EHIP = -3,                /* HIP runtime error */
+  TGSIM_ECAPACITY = -4,           /* a configured capacity was exceeded (resize and rerun) */
+  TGSIM_ECAUSALITY = -5,          /* a send/signal time lies before the current window start */
+  TGSIM_ENOTSUP = -6,             /* feature not supported by this build */
+  TGSIM_EUNSUPPORTED_NETWORK = -7,/* docker_network.go:52-55 "unsupported network: %s" */
+  TGSIM_ESTATE = -8,              /* call out of protocol order */
+  TGSIM_ENODEV = -9               /* no HIP device / library built without device code */
+};
+
+/* ---- sdk-go network types ----------------------------------------------------------------- */
+/* network.FilterAction (sdk-go network/types.go [EXT]): iota order Accept, Reject, Drop. */
+enum { TGSIM_FILTER_ACCEPT = 0, TGSIM_FILTER_REJECT = 1, TGSIM_FILTER_DROP = 2 };
+/* network.RoutingPolicyType: "allow_all" / "deny_all"; any other value (incl. "") acts as deny
+ * (route.go:105-113). */
+enum { TGSIM_POLICY_DENY_ALL = 0, TGSIM_POLICY_ALLOW_ALL = 1 };
+
+/* network.LinkShape (sdk-go [EXT]) field for field; consumed at link.go:155-181. */
+typedef struct tgsim_link_shape {
+  int64_t latency_ns;      /* time.Duration */
+  int64_t jitter_ns;       /* time.Duration */
+  uint64_t bandwidth_bps;  /* bits per second, 0 = unlimited (link.go:156-159) */
+  float loss;              /* percent */
+  float corrupt;
+  float corrupt_corr;
+  float reorder;
+  float reorder_corr;
+  float duplicate;
+  float duplicate_corr;
+  int32_t filter;          /* FilterAction; only meaningful inside a rule (link.go:185-186) */
+} tgsim_link_shape;
+
+/* network.LinkRule: Subnet + LinkShape. Only Shape.filter is used (link.go:185-186 TODO). */
+typedef struct tgsim_link_rule {
+  uint32_t subnet_ip;      /* IPv4, host byte order (a.b.c.d = a<<24|b<<16|c<<8|d) */
+  uint32_t prefix_len;     /* 0..32 */
+  tgsim_link_shape shape;
+} tgsim_link_rule;
+
+/* network.Config (sdk-go [EXT]) minus the callback fields, which the sidecar handler consumes
+ * (sidecar_handler.go:75-79) and which therefore live one layer up (testground_amd.sidecar). */
+typedef struct tgsim_network_config {
+  const char* network;         /* must be "default" */
+  int32_t enable;              /* bool */
+  int32_t routing_policy;      /* TGSIM_POLICY_* */
+  tgsim_link_shape default_shape;
+  const tgsim_link_rule* rules;
+  size_t n_rules;
+  int32_t has_ipv4;            /* cfg.IPv4 != nil */
+  uint32_t ipv4;               /* host byte order */
+} tgsim_network_config;
+
+/* ---- simulator configuration ---------------------------------------------------------------- */
+typedef struct tgsim_config {
+  uint32_t n_instances;        /* total instances in the run (all shards) */
+  uint32_t shard_id;           /* this ctx's shard (rank) */
+  uint32_t n_shards;           /* world size; instances split into contiguous ranges */
+  uint32_t device;             /* HIP device ordinal */
+  uint64_t seed;               /* Philox key (run seed) */
+  uint32_t data_subnet;        /* data network base address, host byte order (e.g. 16.0.0.0) */
+  uint32_t data_prefix_len;    /* e.g. 16 (runner/common.go:28-40) */
+  int64_t wheel_slot_ns;       /* timing-wheel slot width; 0 = default 1 ms */
+  uint32_t wheel_slots;        /* slots per wheel region; 0 = default 2048 */
+  uint32_t reserved0;
+  uint64_t max_msgs_per_window;/* staged-message capacity per window */
+  uint64_t max_records;        /* capacity of every per-window record batch and of the wheel arena */
+  uint64_t exchange_cap;       /* records per peer in one window's all-to-all (n_shards > 1) */
+  uint32_t max_states;         /* sync states (dense ids 0..max_states-1); 0 = default 4096 */
+  uint32_t max_waiters;        /* barrier waiters; 0 = default 65536 */
+  uint64_t max_signals;        /* signal log capacity over the run; 0 = default 2^24 */
+} tgsim_config;
+
+/* ---- message / delivery records --------------------------------------------------------------- */
+/* Input messages, struct of arrays (24 B per message). (src, seq) must be unique over a run. */
+typedef struct tgsim_msg_soa {
+  const uint32_t* src;     /* sender instance id */
+  const uint32_t* dst;     /* receiver instance id, or TGSIM_DST_EXTERNAL */
+  const uint32_t* seq;     /* per-sender message id (Philox counter word) */
+  const uint32_t* size;    /* bytes, < 2^31 */
+  const int64_t* t_send;   /* ns */
+} tgsim_msg_soa;
+
+#define TGSIM_DST_EXTERNAL 0xFFFFFFFFu  /* a host outside the data network (plans/network/traffic.go) */
+
+/* Per-message status (1 byte each, in enqueue order). Low nibble = code, high bits = flags. */
+enum {
+  TGSIM_ST_QUEUED = 0,      /* >= 1 copy entered the egress queue */
+  TGSIM_ST_LOST = 1,        /* netem loss draw (and no duplicate) */
+  TGSIM_ST_DROPPED = 2,     /* blackhole route: LinkRule Drop (link.go:209-210) */
+  TGSIM_ST_REJECTED = 3,    /* prohibit route: LinkRule Reject (link.go:206-207), sender gets EACCES */
+  TGSIM_ST_UNREACHABLE = 4, /* no route (disabled link / external under DenyAll) */
+  TGSIM_ST_EXTERNAL = 5,    /* routed out via the control network (AllowAll) - leaves the simulation */
+  TGSIM_ST_DEST_DOWN = 6,   /* receiver's data link disabled (Enable=false) at send time */
+  TGSIM_ST_LOCAL = 7,       /* src == dst: loopback, unshaped, delivered at t_send */
+  TGSIM_ST_FLAG_DUP = 0x10,         /* a duplicate clone was created */
+  TGSIM_ST_FLAG_CLONE_LOST = 0x20,  /* ... and the clone's own loss draw hit */
+  TGSIM_ST_FLAG_DUP_CANCEL = 0x40   /* duplicate and loss both hit: exactly one copy sent */
+};
+
+/* Delivery / in-flight record flags (tgsim_record.meta, tgsim_delivery_soa.flags). */
+enum {
+  TGSIM_F_CLONE = 1u << 0,      /* this copy is the netem duplicate */
+  TGSIM_F_CORRUPT = 1u << 1,    /* one bit flipped: byte corrupt_off, bit (flags>>4)&7 */
+  TGSIM_F_REORDERED = 1u << 2,  /* took the reorder path (sent without delay) */
+  TGSIM_F_STAGE_D = 1u << 3,    /* internal: t is the delivery time (else the netem ready time) */
+  TGSIM_F_LOCAL = 1u << 7       /* loopback delivery */
+};
+#define TGSIM_F_BIT_SHIFT 4
+
+/* In-flight record, 32 B. This is also the wire format of the cross-shard exchange. */
+typedef struct tgsim_record {
+  int64_t t;              /* stage A: netem time_to_send; stage D: delivery time */
+  uint32_t src, dst, seq, size;
+  uint32_t meta;          /* TGSIM_F_* | corrupt bit << 4 */
+  uint32_t corrupt_off;   /* corrupted byte offset */
+} tgsim_record;
+
+/* Deliveries of one window, struct of arrays, sorted by (dst, t_deliver, src, seq, clone-first). */
+typedef struct tgsim_delivery_soa {
+  int64_t* t_deliver;
+  uint32_t* src;
+  uint32_t* dst;
+  uint32_t* seq;
+  uint32_t* size;
+  uint32_t* flags;
+  uint32_t* corrupt_off;
+} tgsim_delivery_soa;
+
+/* Cumulative counters of a ctx (this shard). */
+typedef struct tgsim_stats {
+  uint64_t msgs_in, copies, lost, dropped, rejected, unreachable, external, dest_down, local;
+  uint64_t delivered, windows, inflight;
+} tgsim_stats;
+
+typedef struct tgsim_ctx tgsim_ctx;
+
+/* ---- lifecycle ----------------------------------------------------------------------------- */
+const char* tgsim_version(void);
+int tgsim_abi_version(void);
+/* Replaces: NewNetlinkLink per instance (link.go:47-115) + sidecar bring-up (docker_reactor.go:132-270).
+ * Every instance starts as after the sidecar's initial Config{Network:"default", Enable:true}
+ * (sidecar_handler.go:26-29): link enabled, unshaped, unlimited, external routing disabled
+ * (zero RoutingPolicy => deny, route.go:105-113), ip = data_subnet + 2 + id. */
+int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out);
+void tgsim_destroy(tgsim_ctx* ctx);
+const char* tgsim_last_error(const tgsim_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream) for all work. NULL = own stream. */
+int tgsim_set_stream(tgsim_ctx* ctx, void* hip_stream);
+int tgsim_shard_range(const tgsim_ctx* ctx, uint32_t* lo, uint32_t* hi);
+int tgsim_sync(tgsim_ctx* ctx); /* wait for the stream, surface device-side errors */
+int tgsim_get_stats(tgsim_ctx* ctx, tgsim_stats* out);
+int64_t tgsim_now(const tgsim_ctx* ctx); /* current window start (host view) */
+
+/* ---- network configuration (sidecar.Network, pkg/sidecar/instance.go:37-42) -------------------
+ * tgsim_configure_network replaces DockerNetwork.ConfigureNetwork (docker_network.go:51-148) for
+ * one instance, in docker apply order: policy -> enable/disable -> IP change -> Shape -> AddRules.
+ * Takes effect for messages sent at or after the current window start. In a sharded run call it on
+ * EVERY shard (ip/enable/policy tables are replicated; shape/rules are kept by the owning shard). */
+int tgsim_configure_network(tgsim_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg);
+/* Lower-level pieces of the same call. */
+int tgsim_set_shape(tgsim_ctx* ctx, uint32_t instance, const tgsim_link_shape* shape); /* Shape, link.go:155 */
+int tgsim_add_rules(tgsim_ctx* ctx, uint32_t instance, const tgsim_link_rule* rules, size_t n); /* AddRules, link.go:187 */
+int tgsim_set_policy(tgsim_ctx* ctx, uint32_t instance, int32_t policy); /* handleRoutingPolicy, route.go:102 */
+int tgsim_set_enabled(tgsim_ctx* ctx, uint32_t instance, int32_t enabled, int32_t has_ip, uint32_t ip);
+int tgsim_get_ip(const tgsim_ctx* ctx, uint32_t instance, uint32_t* ip);
+
+/* ---- data path (replaces the host kernel's HTB/netem/FIB per packet) ----------------------------- */
+/* Stage messages for the next window (host SoA, copied). t_send must be >= tgsim_now(). */
+int tgsim_enqueue(tgsim_ctx* ctx, const tgsim_msg_soa* msgs, size_t n);
+/* Stage messages already in device memory (SoA arrays of n elements). */
+int tgsim_enqueue_device(tgsim_ctx* ctx, const tgsim_msg_soa* dev_msgs, size_t n);
+/* Run one window [now, t_end): shape + route staged messages, token-bucket the copies whose netem
+ * time is < t_end, deliver everything due before t_end. Single-shard ctx only. */
+int tgsim_advance(tgsim_ctx* ctx, int64_t t_end);
+/* Same, with t_end = release time of a barrier waiter + offset, read on the device (no host sync). */
+int tgsim_advance_to_barrier(tgsim_ctx* ctx, uint32_t waiter, int64_t offset_ns);
+/* Sharded window protocol: begin (sender side) -> caller all-to-alls the exchange buffers
+ * (n_shards * exchange_cap records each way, peer-major; the first record of each peer block is a
+ * header whose .t holds the record count) on the same stream -> end (receiver side). */
+int tgsim_advance_begin(tgsim_ctx* ctx, int64_t t_end);
+int tgsim_exchange_buffers(tgsim_ctx* ctx, void** send_device, void** recv_device, size_t* bytes);
+int tgsim_advance_end(tgsim_ctx* ctx);
+/* Results of the last window. Copying forces a stream sync. */
+int tgsim_delivery_count(tgsim_ctx* ctx, size_t* n);
+int tgsim_copy_deliveries(tgsim_ctx* ctx, tgsim_delivery_soa* out, size_t cap, size_t* n);
+int tgsim_copy_inbox_offsets(tgsim_ctx* ctx, uint32_t* out, size_t cap); /* shard-local dst -> offset */
+int tgsim_copy_status(tgsim_ctx* ctx, uint8_t* out, size_t cap, size_t* n);
+int tgsim_deliveries_device(tgsim_ctx* ctx, tgsim_delivery_soa* out_device_ptrs);
+
+/* ---- sync service (sdk-go sync.Client [EXT]; sync-service v0.1.0) ------------------------------ */
+/* SignalEntry for a batch of (state, instance, t) events. seq_out[i] = 1-based sequence number in
+ * (t, instance) order among all signals of that state (NULL = not needed). Batches of one state
+ * must not go back in time. In a sharded run every shard receives the same (all-gathered) batch. */
+int tgsim_sync_signal(tgsim_ctx* ctx, const uint32_t* states, const uint32_t* instances,
+                      const int64_t* t, size_t n, uint32_t* seq_out);
+/* Barrier(state, target) registered at time t_wait: releases at max(t_wait, time of the
+ * target-th signal). Returns a waiter id. */
+int tgsim_sync_barrier(tgsim_ctx* ctx, uint32_t state, uint32_t target, int64_t t_wait,
+                       uint32_t* waiter_out);
+/* release_out = release time, or -1 while pending. */
+int tgsim_sync_poll(tgsim_ctx* ctx, uint32_t waiter, int64_t* release_out);
+int tgsim_sync_count(tgsim_ctx* ctx, uint32_t state, uint32_t* count_out);
+
+/* ---- synthetic workloads (device generators) --------------------------------------- */
+/* Gossip storm round (config 4): every instance of this shard sends `fanout` messages of `size`
+ * bytes to Philox-chosen distinct peers at t0 + U[0, spread_ns), seq = round*fanout + k, and signals
+ * `state` at its last send time. Staged for the next window; the signal batch is kept on the device. */
+int tgsim_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout,
+                          uint32_t size, int64_t spread_ns, uint32_t state);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TGSIM_H */

@@ -1,0 +1,859 @@
+/*
+ * tgsim_oracle.c — TEST INFRASTRUCTURE ONLY (see tgsim_oracle.h for the rules and parity status).
+ *
+ * Single-threaded, deliberately literal restatement of the pinned semantics in DESIGN.md section 2.
+ * Data structures are the obvious ones (sorted vectors, a binary heap, qsort), so that the GPU
+ * implementation, which uses radix bucketing, LDS bitonic sorts, max-plus scans and a slotted
+ * timing wheel, is checked against something independent of its own structure.
+ */
+#include "tgsim_oracle.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NEG_INF (INT64_MIN / 4)
+#define TB_CLAMP ((int64_t)1 << 61)
+#define COST_CLAMP ((uint64_t)1 << 52)
+#define EXTERNAL_IP 0x08080808u /* TGSIM_DST_EXTERNAL is modelled as 8.8.8.8 */
+
+/* ============================== primitives ================================================= */
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox.h). Constants are the published ones. */
+void tgo_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Go's uint32(x) of a float on amd64: CVTTS?2SQ to int64 (0x8000000000000000 when out of range or
+ * NaN), then the low 32 bits. */
+static uint32_t go_u32_of_double(double v) {
+  if (!(v > -9.2233720368547758e18 && v < 9.2233720368547758e18)) return 0u;
+  return (uint32_t)(uint64_t)(int64_t)v;
+}
+
+/* vishvananda/netlink v1.1.0 Percentage2u32 [EXT] (called for Loss/Duplicate/Reorder/Corrupt from
+ * NewNetem, which link.go:169-179 feeds): 100 -> MaxUint32, else uint32(MaxUint32 * (pct/100)) with
+ * the untyped constant converted to float32 and the product computed in float32. */
+uint32_t tgo_percentage2u32(float pct) {
+  if (pct == 100.0f) return 0xFFFFFFFFu;
+  volatile float q = pct / 100.0f;
+  volatile float v = 4294967296.0f * q;
+  return go_u32_of_double((double)v);
+}
+
+/* netlink time2Tick: uint32(float64(us) * tickInUsec), tickInUsec = 1000/64 = 15.625 from
+ * /proc/net/psched "000003e8 00000040 000f4240 3b9aca00" [EXT]. us*15.625 is exact in float64. */
+uint32_t tgo_time2tick(uint32_t us) { return (uint32_t)(((uint64_t)us * 125u) >> 3); }
+
+/* pkg/sidecar/link.go:143-151 toMicroseconds: Duration.Microseconds() (truncating division), capped
+ * at MaxUint32, then uint32() (negative values wrap). */
+uint32_t tgo_to_microseconds(int64_t ns) {
+  int64_t us = ns / 1000;
+  if (us > (int64_t)0xFFFFFFFFu) us = 0xFFFFFFFFu;
+  return (uint32_t)(uint64_t)us;
+}
+
+/* Linux psched_ratecfg_precompute__ [EXT] (net/sched/sch_generic.c): the HTB class rate as a
+ * multiply-shift of the byte count: l2t_ns(len) = (len * mult) >> shift. */
+void tgo_ratecfg(uint64_t rate, uint32_t* mult, uint32_t* shift) {
+  uint64_t factor = 1000000000ull;
+  *mult = 1; *shift = 0;
+  if (rate == 0) return;
+  for (;;) {
+    *mult = (uint32_t)(factor / rate);
+    if ((*mult & (1u << 31)) || (factor & (1ull << 63))) break;
+    factor <<= 1;
+    (*shift)++;
+  }
+}
+
+typedef struct {
+  int64_t mu;        /* netem latency, ns */
+  int32_t sigma;     /* netem jitter, ns, as the s32 argument of tabledist */
+  uint32_t loss_t, dup_t, corrupt_t, reorder_t;
+  uint32_t mult, shift; /* HTB rate */
+  int64_t tau;       /* HTB buffer, ns */
+  int limited;       /* Bandwidth != 0 */
+} oshape;
+
+/* LinkShape -> the netem/HTB state the kernel ends up with.
+ * link.go:155-181 (Shape), netlink NewHtbClass/NewNetem [EXT], sch_htb/sch_netem change paths [EXT]. */
+static int derive_shape(const tgsim_link_shape* s, oshape* o, char* err, size_t errlen) {
+  memset(o, 0, sizeof(*o));
+  /* Correlated loss/dup/corrupt/reorder are a sequential recurrence (netem get_crandom [EXT]);
+   * not in this build. */
+  if (s->corrupt_corr != 0.0f || s->reorder_corr != 0.0f || s->duplicate_corr != 0.0f) {
+    if (err) snprintf(err, errlen, "correlated netem parameters are not supported");
+    return TGSIM_ENOTSUP;
+  }
+  /* HTB: link.go:156-167; rate = Bandwidth/8 bytes/s (netlink NewHtbClass); the kernel refuses a
+   * zero rate (htb_change_class: !hopt->rate.rate && !rate64 -> EINVAL). */
+  uint64_t bw = s->bandwidth_bps == 0 ? UINT64_MAX : s->bandwidth_bps;
+  uint64_t rate = bw / 8;
+  if (rate == 0) {
+    if (err) snprintf(err, errlen, "invalid htb rate: %llu bits/s", (unsigned long long)s->bandwidth_bps);
+    return TGSIM_EINVAL;
+  }
+  o->limited = s->bandwidth_bps != 0;
+  tgo_ratecfg(rate, &o->mult, &o->shift);
+  /* buffer = uint32(rate/Hz + mtu) bytes, Hz = 1e9 (hrtimer psched), mtu = 1600; then
+   * Xmittime = time2Tick(uint32(1e6 * (buffer/rate))) ticks; kernel: ns = ticks << 6. */
+  uint32_t buf_bytes = go_u32_of_double((double)rate / 1e9 + 1600.0);
+  uint32_t buf_us = go_u32_of_double(1000000.0 * ((double)buf_bytes / (double)rate));
+  o->tau = (int64_t)tgo_time2tick(buf_us) << 6;
+  /* netem: link.go:169-179 -> netlink NewNetem: latency = time2Tick(us); jitter converted only when
+   * the converted latency is > 0; kernel stores ticks << 6 ns; tabledist takes sigma as s32. */
+  uint32_t lat_ticks = tgo_time2tick(tgo_to_microseconds(s->latency_ns));
+  uint32_t jit_us = tgo_to_microseconds(s->jitter_ns);
+  uint32_t jit_ticks = lat_ticks > 0 ? tgo_time2tick(jit_us) : jit_us;
+  o->mu = (int64_t)lat_ticks << 6;
+  o->sigma = (int32_t)(uint32_t)((uint64_t)jit_ticks << 6);
+  o->loss_t = tgo_percentage2u32(s->loss);
+  o->dup_t = tgo_percentage2u32(s->duplicate);
+  o->corrupt_t = tgo_percentage2u32(s->corrupt);
+  o->reorder_t = tgo_percentage2u32(s->reorder);
+  return TGSIM_OK;
+}
+
+int tgo_derive_shape(const tgsim_link_shape* s, int64_t out[10]) {
+  oshape o;
+  int rc = derive_shape(s, &o, NULL, 0);
+  if (rc) return rc;
+  out[0] = o.mu; out[1] = o.sigma; out[2] = o.loss_t; out[3] = o.dup_t; out[4] = o.corrupt_t;
+  out[5] = o.reorder_t; out[6] = o.mult; out[7] = o.shift; out[8] = o.tau; out[9] = o.limited;
+  return 0;
+}
+
+/* pkg/runner/common.go:28-40 nextDataNetwork: 16+n/256 . n%256 .0.0/16, gateway .1, >4095 exhausted. */
+int tgo_next_data_network(int n, uint32_t* subnet, uint32_t* prefix_len, uint32_t* gw) {
+  if (n > 4095 || n < 0) return TGSIM_EINVAL;
+  uint32_t a = 16u + (uint32_t)n / 256u, b = (uint32_t)n % 256u;
+  *subnet = (a << 24) | (b << 16);
+  *prefix_len = 16;
+  *gw = *subnet | 1u;
+  return TGSIM_OK;
+}
+
+/* Linux netem tabledist() uniform branch [EXT]: sigma==0 -> mu; else ((rnd % (2*(u32)sigma)) + mu) - sigma. */
+static int64_t tabledist(int64_t mu, int32_t sigma, uint32_t rnd) {
+  if (sigma == 0) return mu;
+  uint32_t m = 2u * (uint32_t)sigma;
+  if (m == 0) return mu;
+  return (int64_t)(rnd % m) + mu - (int64_t)sigma;
+}
+
+static uint64_t l2t_ns(const oshape* s, uint32_t len) {
+  uint64_t c = ((uint64_t)len * s->mult) >> s->shift;
+  return c > COST_CLAMP ? COST_CLAMP : c;
+}
+
+/* ============================== context ===================================================== */
+
+typedef struct { uint32_t prefix, plen; int32_t action; } orule;
+typedef struct { orule* v; size_t n, cap; } orules;
+typedef struct { uint32_t* src; uint32_t* dst; uint32_t* seq; uint32_t* size; int64_t* t; size_t n, cap; } omsgs;
+typedef struct { tgsim_record* v; size_t n, cap; } orecs;
+typedef struct { int64_t* t; size_t n, cap; } otimes;
+typedef struct { uint32_t state, target; int64_t t_wait; } owaiter;
+
+struct tgo_ctx {
+  tgsim_config cfg;
+  uint32_t N, lo, hi, nloc, S;
+  uint32_t data_net, data_mask, data_len;
+  uint64_t seed;
+  oshape* shape;      /* [nloc] */
+  int64_t* X;         /* [nloc] HTB token state as the time tokens reach 0 */
+  orules* rules;      /* [nloc] sorted by (plen desc, prefix asc) */
+  uint8_t* enabled;   /* [N] */
+  uint8_t* allow_ext; /* [N] */
+  uint32_t* ip;       /* [N] */
+  uint32_t* id_of;    /* [2^(32-len)] ip - data_net -> id, or UINT32_MAX */
+  size_t id_of_n;
+  int64_t now, t_end;
+  int in_window;
+  omsgs staged;
+  uint8_t* status; size_t n_status, status_cap;
+  orecs heap;         /* pending records, min-heap on t */
+  orecs A, D, newD;   /* per-window scratch */
+  orecs out;          /* deliveries of the last window (sorted) */
+  uint32_t* inbox;    /* [nloc+1] */
+  tgsim_record* xsend; tgsim_record* xrecv; size_t xcap;
+  orecs* outbox;      /* [S] */
+  tgsim_stats stats;
+  otimes* sig;        /* per state: signal times in seq order */
+  size_t n_states;
+  owaiter* waiters; size_t n_waiters, waiters_cap;
+  char err[512];
+};
+
+static int fail(tgo_ctx* c, int code, const char* fmt, ...) {
+  if (c) { va_list ap; va_start(ap, fmt); vsnprintf(c->err, sizeof(c->err), fmt, ap); va_end(ap); }
+  return code;
+}
+
+static int grow(void** p, size_t* cap, size_t need, size_t elem) {
+  if (need <= *cap) return 0;
+  size_t nc = *cap ? *cap : 64;
+  while (nc < need) nc *= 2;
+  void* q = realloc(*p, nc * elem);
+  if (!q) return TGSIM_ENOMEM;
+  *p = q; *cap = nc;
+  return 0;
+}
+static int recs_push(orecs* r, const tgsim_record* x) {
+  if (grow((void**)&r->v, &r->cap, r->n + 1, sizeof(tgsim_record))) return TGSIM_ENOMEM;
+  r->v[r->n++] = *x;
+  return 0;
+}
+
+/* min-heap on t */
+static int heap_push(orecs* h, const tgsim_record* x) {
+  if (recs_push(h, x)) return TGSIM_ENOMEM;
+  size_t i = h->n - 1;
+  while (i) {
+    size_t p = (i - 1) / 2;
+    if (h->v[p].t <= h->v[i].t) break;
+    tgsim_record t = h->v[p]; h->v[p] = h->v[i]; h->v[i] = t; i = p;
+  }
+  return 0;
+}
+static tgsim_record heap_pop(orecs* h) {
+  tgsim_record top = h->v[0];
+  h->v[0] = h->v[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    if (l < h->n && h->v[l].t < h->v[m].t) m = l;
+    if (r < h->n && h->v[r].t < h->v[m].t) m = r;
+    if (m == i) break;
+    tgsim_record t = h->v[m]; h->v[m] = h->v[i]; h->v[i] = t; i = m;
+  }
+  return top;
+}
+
+static uint32_t shard_of(const tgo_ctx* c, uint32_t g) {
+  /* shard k owns [floor(k*N/S), floor((k+1)*N/S)) */
+  uint32_t k = (uint32_t)(((uint64_t)g * c->S) / c->N);
+  while (k + 1 < c->S && (uint32_t)(((uint64_t)(k + 1) * c->N) / c->S) <= g) ++k;
+  while (k > 0 && (uint32_t)(((uint64_t)k * c->N) / c->S) > g) --k;
+  return k;
+}
+
+static const tgsim_link_shape ZERO_SHAPE;
+
+int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
+  *out = NULL;
+  if (!cfg || cfg->n_instances == 0 || cfg->n_shards == 0 || cfg->shard_id >= cfg->n_shards)
+    return TGSIM_EINVAL;
+  if (cfg->data_prefix_len < 1 || cfg->data_prefix_len > 30) return TGSIM_EINVAL;
+  tgo_ctx* c = (tgo_ctx*)calloc(1, sizeof(tgo_ctx));
+  if (!c) return TGSIM_ENOMEM;
+  c->cfg = *cfg;
+  c->N = cfg->n_instances; c->S = cfg->n_shards;
+  c->lo = (uint32_t)(((uint64_t)cfg->shard_id * c->N) / c->S);
+  c->hi = (uint32_t)(((uint64_t)(cfg->shard_id + 1) * c->N) / c->S);
+  c->nloc = c->hi - c->lo;
+  c->seed = cfg->seed;
+  c->data_len = cfg->data_prefix_len;
+  c->data_mask = 0xFFFFFFFFu << (32 - c->data_len);
+  c->data_net = cfg->data_subnet & c->data_mask;
+  c->id_of_n = (size_t)1 << (32 - c->data_len);
+  if ((uint64_t)c->N + 2 > c->id_of_n) { free(c); return TGSIM_EINVAL; }
+  c->shape = (oshape*)calloc(c->nloc ? c->nloc : 1, sizeof(oshape));
+  c->X = (int64_t*)calloc(c->nloc ? c->nloc : 1, sizeof(int64_t));
+  c->rules = (orules*)calloc(c->nloc ? c->nloc : 1, sizeof(orules));
+  c->enabled = (uint8_t*)calloc(c->N, 1);
+  c->allow_ext = (uint8_t*)calloc(c->N, 1);
+  c->ip = (uint32_t*)calloc(c->N, sizeof(uint32_t));
+  c->id_of = (uint32_t*)malloc(c->id_of_n * sizeof(uint32_t));
+  c->inbox = (uint32_t*)calloc(c->nloc + 1, sizeof(uint32_t));
+  c->outbox = (orecs*)calloc(c->S, sizeof(orecs));
+  c->xcap = cfg->exchange_cap ? cfg->exchange_cap : 1024;
+  c->xsend = (tgsim_record*)calloc((size_t)c->S * c->xcap, sizeof(tgsim_record));
+  c->xrecv = (tgsim_record*)calloc((size_t)c->S * c->xcap, sizeof(tgsim_record));
+  if (!c->shape || !c->X || !c->rules || !c->enabled || !c->allow_ext || !c->ip || !c->id_of ||
+      !c->inbox || !c->outbox || !c->xsend || !c->xrecv) {
+    tgo_destroy(c);
+    return TGSIM_ENOMEM;
+  }
+  memset(c->id_of, 0xFF, c->id_of_n * sizeof(uint32_t));
+  oshape z;
+  derive_shape(&ZERO_SHAPE, &z, NULL, 0);
+  for (uint32_t i = 0; i < c->nloc; ++i) { c->shape[i] = z; c->X[i] = NEG_INF; }
+  for (uint32_t g = 0; g < c->N; ++g) {
+    c->enabled[g] = 1;
+    c->allow_ext[g] = 0; /* sidecar init config has the zero RoutingPolicy => disable (route.go:105-113) */
+    c->ip[g] = c->data_net + 2u + g;
+    c->id_of[c->ip[g] - c->data_net] = g;
+  }
+  *out = c;
+  return TGSIM_OK;
+}
+
+void tgo_destroy(tgo_ctx* c) {
+  if (!c) return;
+  if (c->rules) for (uint32_t i = 0; i < c->nloc; ++i) free(c->rules[i].v);
+  if (c->outbox) for (uint32_t i = 0; i < c->S; ++i) free(c->outbox[i].v);
+  if (c->sig) for (size_t i = 0; i < c->n_states; ++i) free(c->sig[i].t);
+  free(c->sig); free(c->waiters);
+  free(c->shape); free(c->X); free(c->rules); free(c->enabled); free(c->allow_ext); free(c->ip);
+  free(c->id_of); free(c->inbox); free(c->outbox); free(c->xsend); free(c->xrecv);
+  free(c->staged.src); free(c->staged.dst); free(c->staged.seq); free(c->staged.size); free(c->staged.t);
+  free(c->status); free(c->heap.v); free(c->A.v); free(c->D.v); free(c->newD.v); free(c->out.v);
+  free(c);
+}
+
+const char* tgo_last_error(const tgo_ctx* c) { return c ? c->err : "null context"; }
+int64_t tgo_now(const tgo_ctx* c) { return c->now; }
+
+static int is_local(const tgo_ctx* c, uint32_t g) { return g >= c->lo && g < c->hi; }
+
+/* ============================== network configuration ======================================= */
+
+/* NetlinkLink.Shape, link.go:155-183: HTB first (setHtb), then netem. */
+int tgo_set_shape(tgo_ctx* c, uint32_t g, const tgsim_link_shape* s) {
+  if (g >= c->N || !s) return fail(c, TGSIM_EINVAL, "bad instance %u", g);
+  oshape o;
+  int rc = derive_shape(s, &o, c->err, sizeof(c->err));
+  if (rc) return rc;
+  if (is_local(c, g)) c->shape[g - c->lo] = o;
+  return TGSIM_OK;
+}
+
+static int rule_cmp(uint32_t pa, uint32_t la, uint32_t pb, uint32_t lb) {
+  if (la != lb) return la > lb ? -1 : 1; /* longer prefixes first */
+  if (pa != pb) return pa < pb ? -1 : 1;
+  return 0;
+}
+static size_t rule_find(const orules* r, uint32_t prefix, uint32_t plen, int* found) {
+  size_t lo = 0, hi = r->n;
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    int c = rule_cmp(r->v[mid].prefix, r->v[mid].plen, prefix, plen);
+    if (c < 0) lo = mid + 1; else hi = mid;
+  }
+  *found = lo < r->n && r->v[lo].prefix == prefix && r->v[lo].plen == plen;
+  return lo;
+}
+
+/* NetlinkLink.AddRules, link.go:187-217. Accept deletes the blackhole and prohibit routes for the
+ * subnet (errors ignored); Reject/Drop RouteReplace a PROHIBIT/BLACKHOLE route (the kernel rejects
+ * a prefix with host bits set: EINVAL, returned, later rules not applied). */
+int tgo_add_rules(tgo_ctx* c, uint32_t g, const tgsim_link_rule* rules, size_t n) {
+  if (g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance %u", g);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t plen = rules[i].prefix_len;
+    if (plen > 32) return fail(c, TGSIM_EINVAL, "invalid prefix length %u", plen);
+    uint32_t mask = plen ? 0xFFFFFFFFu << (32 - plen) : 0u;
+    uint32_t prefix = rules[i].subnet_ip;
+    int action = rules[i].shape.filter;
+    if (!is_local(c, g)) {
+      if (action != TGSIM_FILTER_ACCEPT && (prefix & ~mask)) return fail(c, TGSIM_EINVAL, "invalid prefix for given prefix length");
+      continue;
+    }
+    orules* r = &c->rules[g - c->lo];
+    int found;
+    if (action == TGSIM_FILTER_ACCEPT) {
+      size_t at = rule_find(r, prefix & mask, plen, &found);
+      if (found && (prefix & ~mask) == 0) {
+        memmove(&r->v[at], &r->v[at + 1], (r->n - at - 1) * sizeof(orule));
+        r->n--;
+      }
+      continue;
+    }
+    if (action != TGSIM_FILTER_REJECT && action != TGSIM_FILTER_DROP)
+      return fail(c, TGSIM_EINVAL, "unknown filter action %d", action);
+    if (prefix & ~mask) return fail(c, TGSIM_EINVAL, "invalid prefix for given prefix length");
+    size_t at = rule_find(r, prefix, plen, &found);
+    if (found) { r->v[at].action = action; continue; }
+    if (grow((void**)&r->v, &r->cap, r->n + 1, sizeof(orule))) return fail(c, TGSIM_ENOMEM, "oom");
+    memmove(&r->v[at + 1], &r->v[at], (r->n - at) * sizeof(orule));
+    r->v[at].prefix = prefix; r->v[at].plen = plen; r->v[at].action = action;
+    r->n++;
+  }
+  return TGSIM_OK;
+}
+
+/* route.go:102-117: AllowAll enables external routes, DenyAll and every other value disables. */
+int tgo_set_policy(tgo_ctx* c, uint32_t g, int32_t policy) {
+  if (g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance %u", g);
+  c->allow_ext[g] = policy == TGSIM_POLICY_ALLOW_ALL;
+  return TGSIM_OK;
+}
+
+static int set_ip(tgo_ctx* c, uint32_t g, uint32_t ip) {
+  if ((ip & c->data_mask) != c->data_net) return fail(c, TGSIM_EINVAL, "ip outside the data subnet");
+  uint32_t off = ip - c->data_net;
+  if (off == 0 || off == (uint32_t)(c->id_of_n - 1) || off == 1)
+    return fail(c, TGSIM_EINVAL, "reserved address");
+  if (c->id_of[off] != UINT32_MAX && c->id_of[off] != g) return fail(c, TGSIM_EINVAL, "address already in use");
+  c->id_of[c->ip[g] - c->data_net] = UINT32_MAX;
+  c->ip[g] = ip;
+  c->id_of[off] = g;
+  return TGSIM_OK;
+}
+
+/* Link disconnect / (re)connect, docker_network.go:65-133. A new link is a new HTB class + netem
+ * qdisc (link.go:47-115): unshaped, unlimited, bucket full. Blackhole/prohibit routes live in the
+ * netns routing table and survive. */
+int tgo_set_enabled(tgo_ctx* c, uint32_t g, int32_t enabled, int32_t has_ip, uint32_t ip) {
+  if (g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance %u", g);
+  if (!enabled) { c->enabled[g] = 0; return TGSIM_OK; }
+  if (c->enabled[g] && has_ip && ip != c->ip[g]) c->enabled[g] = 0; /* disconnect to change ip */
+  if (!c->enabled[g]) {
+    if (has_ip) { int rc = set_ip(c, g, ip); if (rc) return rc; }
+    c->enabled[g] = 1;
+    if (is_local(c, g)) {
+      derive_shape(&ZERO_SHAPE, &c->shape[g - c->lo], NULL, 0);
+      c->X[g - c->lo] = NEG_INF;
+    }
+  }
+  return TGSIM_OK;
+}
+
+/* DockerNetwork.ConfigureNetwork, docker_network.go:51-148, in its order. */
+int tgo_configure_network(tgo_ctx* c, uint32_t g, const tgsim_network_config* cfg) {
+  if (!cfg || g >= c->N) return fail(c, TGSIM_EINVAL, "bad arguments");
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return fail(c, TGSIM_EUNSUPPORTED_NETWORK, "unsupported network: %s", net);
+  int rc = tgo_set_policy(c, g, cfg->routing_policy);
+  if (rc) return rc;
+  if (!cfg->enable) return tgo_set_enabled(c, g, 0, 0, 0);
+  rc = tgo_set_enabled(c, g, 1, cfg->has_ipv4, cfg->ipv4);
+  if (rc) return rc;
+  rc = tgo_set_shape(c, g, &cfg->default_shape);
+  if (rc) return rc;
+  return tgo_add_rules(c, g, cfg->rules, cfg->n_rules);
+}
+
+int tgo_get_ip(const tgo_ctx* c, uint32_t g, uint32_t* ip) {
+  if (g >= c->N) return TGSIM_EINVAL;
+  *ip = c->ip[g];
+  return TGSIM_OK;
+}
+
+/* ============================== data path =================================================== */
+
+int tgo_enqueue(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
+  omsgs* s = &c->staged;
+  size_t need = s->n + n;
+  if (need > s->cap) {
+    size_t nc = s->cap ? s->cap : 1024;
+    while (nc < need) nc *= 2;
+    s->src = (uint32_t*)realloc(s->src, nc * 4); s->dst = (uint32_t*)realloc(s->dst, nc * 4);
+    s->seq = (uint32_t*)realloc(s->seq, nc * 4); s->size = (uint32_t*)realloc(s->size, nc * 4);
+    s->t = (int64_t*)realloc(s->t, nc * 8);
+    if (!s->src || !s->dst || !s->seq || !s->size || !s->t) return fail(c, TGSIM_ENOMEM, "oom");
+    s->cap = nc;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (m->src[i] >= c->N || (m->dst[i] >= c->N && m->dst[i] != TGSIM_DST_EXTERNAL))
+      return fail(c, TGSIM_EINVAL, "message %zu: bad instance id", i);
+    if (!is_local(c, m->src[i])) return fail(c, TGSIM_EINVAL, "message %zu: sender not in this shard", i);
+    if (m->t_send[i] < c->now) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before window start", i);
+    if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "message %zu: size too large", i);
+  }
+  memcpy(s->src + s->n, m->src, n * 4); memcpy(s->dst + s->n, m->dst, n * 4);
+  memcpy(s->seq + s->n, m->seq, n * 4); memcpy(s->size + s->n, m->size, n * 4);
+  memcpy(s->t + s->n, m->t_send, n * 8);
+  s->n = need;
+  return TGSIM_OK;
+}
+
+enum { R_NONE = 0, R_DATA, R_DEFAULT, R_DROP, R_REJECT };
+
+/* Longest-prefix match over the sender's netns routing table: its blackhole/prohibit routes
+ * (link.go:187-217), the data network's connected route (present while the link is enabled), the
+ * default route via the control network (present under AllowAll, route.go:68-100). An equal-length
+ * rule replaces the route it collides with (RouteReplace). Linear scan: obviously correct. */
+static int route_lookup(const tgo_ctx* c, uint32_t g, uint32_t dst_ip) {
+  int data_ok = c->enabled[g] && ((dst_ip & c->data_mask) == c->data_net);
+  const orules* r = &c->rules[g - c->lo];
+  for (size_t i = 0; i < r->n; ++i) {
+    uint32_t plen = r->v[i].plen;
+    if (data_ok && c->data_len > plen) return R_DATA;
+    uint32_t mask = plen ? 0xFFFFFFFFu << (32 - plen) : 0u;
+    if ((dst_ip & mask) == r->v[i].prefix) return r->v[i].action == TGSIM_FILTER_DROP ? R_DROP : R_REJECT;
+  }
+  if (data_ok) return R_DATA;
+  if (c->allow_ext[g]) return R_DEFAULT;
+  return R_NONE;
+}
+
+static void draw(const tgo_ctx* c, uint32_t seq, uint32_t src, uint32_t clone, uint32_t blk, uint32_t out[4]) {
+  uint32_t ctr[4] = {seq, src, clone | (blk << 1), 0x4E45544Du /* "NETM" */};
+  uint32_t key[2] = {(uint32_t)c->seed, (uint32_t)(c->seed >> 32)};
+  tgo_philox4x32_10(ctr, key, out);
+}
+
+static int route_record(tgo_ctx* c, tgsim_record* r); /* stage-D record -> local newD or outbox */
+
+/* One copy through the rest of netem_enqueue [EXT] after the duplicate/loss decision:
+ * (clone only) loss draw, corruption draw, reorder-or-delay. Returns 1 if a record was produced. */
+static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, uint32_t seq,
+                      uint32_t size, int64_t t_send, uint32_t clone, tgsim_record* rec) {
+  uint32_t r0[4];
+  draw(c, seq, src, clone, 0, r0);
+  if (clone && sh->loss_t && sh->loss_t >= r0[1]) return 0;
+  rec->src = src; rec->dst = dst; rec->seq = seq; rec->size = size;
+  rec->meta = clone ? TGSIM_F_CLONE : 0; rec->corrupt_off = 0;
+  if (sh->corrupt_t) {
+    uint32_t r1[4];
+    draw(c, seq, src, clone, 1, r1);
+    if (sh->corrupt_t >= r1[0] && size > 0) {
+      rec->meta |= TGSIM_F_CORRUPT | ((r1[2] % 8u) << TGSIM_F_BIT_SHIFT);
+      rec->corrupt_off = r1[1] % size;
+    }
+  }
+  if (sh->reorder_t && !(sh->reorder_t < r0[3])) { /* gap == 1 when reorder > 0 (netlink NewNetem) */
+    rec->meta |= TGSIM_F_REORDERED;
+    rec->t = t_send;
+  } else {
+    int64_t delay = tabledist(sh->mu, sh->sigma, r0[2]);
+    rec->t = t_send + (delay > 0 ? delay : 0);
+  }
+  if (!sh->limited) rec->meta |= TGSIM_F_STAGE_D; /* unlimited HTB: departs when netem releases it */
+  return 1;
+}
+
+static int cmp_tb(const void* a, const void* b) {
+  const tgsim_record* x = (const tgsim_record*)a; const tgsim_record* y = (const tgsim_record*)b;
+  if (x->src != y->src) return x->src < y->src ? -1 : 1;
+  if (x->t != y->t) return x->t < y->t ? -1 : 1;
+  if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+  uint32_t rx = (x->meta & TGSIM_F_CLONE) ? 0 : 1, ry = (y->meta & TGSIM_F_CLONE) ? 0 : 1;
+  return rx < ry ? -1 : rx > ry;
+}
+static int cmp_dl(const void* a, const void* b) {
+  const tgsim_record* x = (const tgsim_record*)a; const tgsim_record* y = (const tgsim_record*)b;
+  if (x->dst != y->dst) return x->dst < y->dst ? -1 : 1;
+  if (x->t != y->t) return x->t < y->t ? -1 : 1;
+  if (x->src != y->src) return x->src < y->src ? -1 : 1;
+  if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+  uint32_t rx = (x->meta & TGSIM_F_CLONE) ? 0 : 1, ry = (y->meta & TGSIM_F_CLONE) ? 0 : 1;
+  return rx < ry ? -1 : rx > ry;
+}
+
+static int route_record(tgo_ctx* c, tgsim_record* r) {
+  uint32_t p = shard_of(c, r->dst);
+  if (p == c->cfg.shard_id) return recs_push(&c->newD, r);
+  return recs_push(&c->outbox[p], r);
+}
+
+int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  omsgs* s = &c->staged;
+  for (size_t i = 0; i < s->n; ++i)
+    if (s->t[i] >= t_end) return fail(c, TGSIM_ECAUSALITY, "staged message %zu sent at/after t_end", i);
+  c->t_end = t_end;
+  c->A.n = c->D.n = c->newD.n = 0;
+  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
+  /* 1. due events from the pending set (netem-ready copies and deliveries before t_end) */
+  while (c->heap.n && c->heap.v[0].t < t_end) {
+    tgsim_record r = heap_pop(&c->heap);
+    if (r.meta & TGSIM_F_STAGE_D) { if (recs_push(&c->D, &r)) return TGSIM_ENOMEM; }
+    else if (recs_push(&c->A, &r)) return TGSIM_ENOMEM;
+  }
+  /* 2. route + netem for every staged message, in enqueue order */
+  if (grow((void**)&c->status, &c->status_cap, s->n + 1, 1)) return fail(c, TGSIM_ENOMEM, "oom");
+  c->n_status = s->n;
+  for (size_t i = 0; i < s->n; ++i) {
+    uint32_t src = s->src[i], dst = s->dst[i], seq = s->seq[i], size = s->size[i];
+    int64_t ts = s->t[i];
+    c->stats.msgs_in++;
+    if (dst == src) {
+      tgsim_record r = {ts, src, dst, seq, size, TGSIM_F_LOCAL | TGSIM_F_STAGE_D, 0};
+      c->status[i] = TGSIM_ST_LOCAL; c->stats.local++;
+      if (route_record(c, &r)) return TGSIM_ENOMEM;
+      continue;
+    }
+    int ext = dst == TGSIM_DST_EXTERNAL;
+    int rt = route_lookup(c, src, ext ? EXTERNAL_IP : c->ip[dst]);
+    if (rt == R_DROP) { c->status[i] = TGSIM_ST_DROPPED; c->stats.dropped++; continue; }
+    if (rt == R_REJECT) { c->status[i] = TGSIM_ST_REJECTED; c->stats.rejected++; continue; }
+    if (rt == R_DEFAULT) {
+      if (ext) { c->status[i] = TGSIM_ST_EXTERNAL; c->stats.external++; }
+      else { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; }
+      continue;
+    }
+    if (rt == R_NONE) { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; continue; }
+    if (!c->enabled[dst]) { c->status[i] = TGSIM_ST_DEST_DOWN; c->stats.dest_down++; continue; }
+    const oshape* sh = &c->shape[src - c->lo];
+    uint32_t r0[4];
+    draw(c, seq, src, 0, 0, r0);
+    int count = 1;
+    int dup = sh->dup_t && sh->dup_t >= r0[0];
+    if (dup) ++count;
+    int lost = sh->loss_t && sh->loss_t >= r0[1];
+    if (lost) --count;
+    if (count == 0) { c->status[i] = TGSIM_ST_LOST; c->stats.lost++; continue; }
+    uint8_t st = TGSIM_ST_QUEUED;
+    if (dup && lost) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+    tgsim_record rec;
+    if (count == 2) { /* the clone is enqueued first, through the root qdisc, duplicate disabled */
+      st |= TGSIM_ST_FLAG_DUP;
+      if (netem_copy(c, sh, src, dst, seq, size, ts, 1, &rec)) {
+        c->stats.copies++;
+        if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
+        else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
+        else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
+      } else st |= TGSIM_ST_FLAG_CLONE_LOST;
+    }
+    netem_copy(c, sh, src, dst, seq, size, ts, 0, &rec);
+    c->stats.copies++;
+    if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
+    else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
+    else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
+    c->status[i] = st;
+  }
+  s->n = 0;
+  /* 3. HTB token bucket (GCRA form): copies whose netem time is < t_end, per sender in
+   *    (time_to_send, seq, clone-first) order; d = max(e, X); X = min(max(X, e - tau) + cost, 2^61). */
+  if (c->A.n) qsort(c->A.v, c->A.n, sizeof(tgsim_record), cmp_tb);
+  for (size_t i = 0; i < c->A.n; ++i) {
+    tgsim_record r = c->A.v[i];
+    uint32_t l = r.src - c->lo;
+    const oshape* sh = &c->shape[l];
+    int64_t X = c->X[l];
+    int64_t d = r.t > X ? r.t : X;
+    int64_t base = X > r.t - sh->tau ? X : r.t - sh->tau;
+    int64_t nx = base + (int64_t)l2t_ns(sh, r.size);
+    c->X[l] = nx > TB_CLAMP ? TB_CLAMP : nx;
+    r.t = d;
+    r.meta |= TGSIM_F_STAGE_D;
+    if (route_record(c, &r)) return TGSIM_ENOMEM;
+  }
+  /* 4. pack the exchange (peer-major blocks, header record .t = count) */
+  memset(c->xsend, 0, (size_t)c->S * c->xcap * sizeof(tgsim_record));
+  for (uint32_t p = 0; p < c->S; ++p) {
+    orecs* o = &c->outbox[p];
+    if (o->n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "exchange capacity exceeded (%zu records to peer %u)", o->n, p);
+    c->xsend[(size_t)p * c->xcap].t = (int64_t)o->n;
+    memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
+  }
+  c->in_window = 1;
+  return TGSIM_OK;
+}
+
+int tgo_exchange_buffers(tgo_ctx* c, void** send, void** recv, size_t* bytes) {
+  *send = c->xsend; *recv = c->xrecv;
+  *bytes = (size_t)c->S * c->xcap * sizeof(tgsim_record);
+  return TGSIM_OK;
+}
+
+int tgo_advance_end(tgo_ctx* c) {
+  if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
+  /* 5. received stage-D records join this shard's own */
+  if (c->S > 1) {
+    for (uint32_t p = 0; p < c->S; ++p) {
+      if (p == c->cfg.shard_id) continue;
+      const tgsim_record* blk = &c->xrecv[(size_t)p * c->xcap];
+      size_t n = (size_t)blk[0].t;
+      if (n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "corrupt exchange header");
+      for (size_t i = 0; i < n; ++i) if (recs_push(&c->newD, &blk[1 + i])) return TGSIM_ENOMEM;
+    }
+  }
+  for (size_t i = 0; i < c->newD.n; ++i) {
+    const tgsim_record* r = &c->newD.v[i];
+    if (r->t < c->t_end) { if (recs_push(&c->D, r)) return TGSIM_ENOMEM; }
+    else if (heap_push(&c->heap, r)) return TGSIM_ENOMEM;
+  }
+  /* 6. deliveries: inbox order (dst, t, src, seq, clone-first) */
+  if (c->D.n) qsort(c->D.v, c->D.n, sizeof(tgsim_record), cmp_dl);
+  c->out.n = 0;
+  if (grow((void**)&c->out.v, &c->out.cap, c->D.n + 1, sizeof(tgsim_record))) return TGSIM_ENOMEM;
+  memcpy(c->out.v, c->D.v, c->D.n * sizeof(tgsim_record));
+  c->out.n = c->D.n;
+  memset(c->inbox, 0, (c->nloc + 1) * sizeof(uint32_t));
+  for (size_t i = 0; i < c->out.n; ++i) c->inbox[c->out.v[i].dst - c->lo + 1]++;
+  for (uint32_t i = 0; i < c->nloc; ++i) c->inbox[i + 1] += c->inbox[i];
+  c->stats.delivered += c->out.n;
+  c->stats.windows++;
+  c->stats.inflight = c->heap.n;
+  c->now = c->t_end;
+  c->in_window = 0;
+  return TGSIM_OK;
+}
+
+int tgo_advance(tgo_ctx* c, int64_t t_end) {
+  if (c->S != 1) return fail(c, TGSIM_ESTATE, "tgo_advance needs a single-shard context");
+  int rc = tgo_advance_begin(c, t_end);
+  if (rc) return rc;
+  return tgo_advance_end(c);
+}
+
+int tgo_delivery_count(tgo_ctx* c, size_t* n) { *n = c->out.n; return 0; }
+
+int tgo_copy_deliveries(tgo_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n) {
+  *n = c->out.n;
+  if (c->out.n > cap) return fail(c, TGSIM_ECAPACITY, "output capacity");
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    o->t_deliver[i] = r->t; o->src[i] = r->src; o->dst[i] = r->dst; o->seq[i] = r->seq;
+    o->size[i] = r->size; o->flags[i] = r->meta & ~(uint32_t)TGSIM_F_STAGE_D; o->corrupt_off[i] = r->corrupt_off;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_copy_inbox_offsets(tgo_ctx* c, uint32_t* out, size_t cap) {
+  if (cap < (size_t)c->nloc + 1) return TGSIM_ECAPACITY;
+  memcpy(out, c->inbox, (c->nloc + 1) * sizeof(uint32_t));
+  return 0;
+}
+
+int tgo_copy_status(tgo_ctx* c, uint8_t* out, size_t cap, size_t* n) {
+  *n = c->n_status;
+  if (c->n_status > cap) return TGSIM_ECAPACITY;
+  memcpy(out, c->status, c->n_status);
+  return 0;
+}
+
+int tgo_get_stats(tgo_ctx* c, tgsim_stats* out) { *out = c->stats; out->inflight = c->heap.n; return 0; }
+
+/* ============================== sync service ================================================ */
+/* sdk-go sync.Client [EXT]: SignalEntry increments the state's counter and returns the new value
+ * (1-based seq); Barrier(state, target) fires once the counter reaches target. Simulated: a batch
+ * is ordered by (t, instance); signal times per state never go backwards across batches. */
+
+typedef struct { uint32_t state, inst; int64_t t; size_t idx; } osig;
+static int cmp_sig(const void* a, const void* b) {
+  const osig* x = (const osig*)a; const osig* y = (const osig*)b;
+  if (x->state != y->state) return x->state < y->state ? -1 : 1;
+  if (x->t != y->t) return x->t < y->t ? -1 : 1;
+  if (x->inst != y->inst) return x->inst < y->inst ? -1 : 1;
+  return x->idx < y->idx ? -1 : x->idx > y->idx;
+}
+
+static int ensure_state(tgo_ctx* c, uint32_t st) {
+  if (st >= (1u << 24)) return fail(c, TGSIM_EINVAL, "state id too large");
+  if (st < c->n_states) return 0;
+  size_t nn = c->n_states ? c->n_states : 16;
+  while (nn <= st) nn *= 2;
+  otimes* v = (otimes*)realloc(c->sig, nn * sizeof(otimes));
+  if (!v) return TGSIM_ENOMEM;
+  memset(v + c->n_states, 0, (nn - c->n_states) * sizeof(otimes));
+  c->sig = v; c->n_states = nn;
+  return 0;
+}
+
+int tgo_sync_signal(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                    size_t n, uint32_t* seq_out) {
+  if (n == 0) return 0;
+  osig* v = (osig*)malloc(n * sizeof(osig));
+  if (!v) return TGSIM_ENOMEM;
+  for (size_t i = 0; i < n; ++i) {
+    int rc = ensure_state(c, states[i]);
+    if (rc) { free(v); return rc; }
+    otimes* ts = &c->sig[states[i]];
+    if (t[i] < 0 || (ts->n && t[i] < ts->t[ts->n - 1])) { free(v); return fail(c, TGSIM_ECAUSALITY, "signal %zu goes back in time", i); }
+    v[i].state = states[i]; v[i].inst = inst[i]; v[i].t = t[i]; v[i].idx = i;
+  }
+  qsort(v, n, sizeof(osig), cmp_sig);
+  for (size_t i = 0; i < n; ++i) {
+    otimes* ts = &c->sig[v[i].state];
+    if (grow((void**)&ts->t, &ts->cap, ts->n + 1, sizeof(int64_t))) { free(v); return TGSIM_ENOMEM; }
+    ts->t[ts->n++] = v[i].t;
+    if (seq_out) seq_out[v[i].idx] = (uint32_t)ts->n;
+  }
+  free(v);
+  return 0;
+}
+
+int tgo_sync_barrier(tgo_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w) {
+  int rc = ensure_state(c, state);
+  if (rc) return rc;
+  if (grow((void**)&c->waiters, &c->waiters_cap, c->n_waiters + 1, sizeof(owaiter))) return TGSIM_ENOMEM;
+  c->waiters[c->n_waiters].state = state; c->waiters[c->n_waiters].target = target;
+  c->waiters[c->n_waiters].t_wait = t_wait;
+  *w = (uint32_t)c->n_waiters++;
+  return 0;
+}
+
+int tgo_sync_poll(tgo_ctx* c, uint32_t w, int64_t* rel) {
+  if (w >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  owaiter* x = &c->waiters[w];
+  const otimes* ts = &c->sig[x->state];
+  if (x->target == 0) { *rel = x->t_wait; return 0; }
+  if (ts->n < x->target) { *rel = -1; return 0; }
+  int64_t tk = ts->t[x->target - 1];
+  *rel = tk > x->t_wait ? tk : x->t_wait;
+  return 0;
+}
+
+int tgo_sync_count(tgo_ctx* c, uint32_t state, uint32_t* count) {
+  *count = state < c->n_states ? (uint32_t)c->sig[state].n : 0;
+  return 0;
+}
+
+int tgo_advance_to_barrier(tgo_ctx* c, uint32_t w, int64_t offset) {
+  int64_t rel;
+  int rc = tgo_sync_poll(c, w, &rel);
+  if (rc) return rc;
+  if (rel < 0) return fail(c, TGSIM_ESTATE, "barrier not released");
+  return tgo_advance(c, rel + offset);
+}
+
+/* ============================== workload: gossip storm =============== */
+/* Instance g picks `fanout` distinct peers != g by Philox (rejection on repeats), sends `size` bytes
+ * to each at t0 + U[0, spread), and signals `state` at its last send (the SignalAndWait pattern of
+ * plans/benchmarks/benchmarks.go:122-141 around a storm round, plans/benchmarks/storm.go:150-197). */
+int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                        int64_t spread_ns, uint32_t state) {
+  if (fanout == 0 || fanout >= c->N || fanout > 64) return fail(c, TGSIM_EINVAL, "bad fanout");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "storm generator signals need a single-shard context");
+  size_t n = (size_t)c->nloc * fanout;
+  uint32_t* src = (uint32_t*)malloc(n * 4); uint32_t* dst = (uint32_t*)malloc(n * 4);
+  uint32_t* seq = (uint32_t*)malloc(n * 4); uint32_t* sz = (uint32_t*)malloc(n * 4);
+  int64_t* ts = (int64_t*)malloc(n * 8);
+  uint32_t* sst = (uint32_t*)malloc(c->nloc * 4); uint32_t* sin = (uint32_t*)malloc(c->nloc * 4);
+  int64_t* stt = (int64_t*)malloc(c->nloc * 8);
+  int rc = TGSIM_ENOMEM;
+  if (!src || !dst || !seq || !sz || !ts || !sst || !sin || !stt) goto out;
+  uint32_t key[2] = {(uint32_t)c->seed, (uint32_t)(c->seed >> 32)};
+  for (uint32_t l = 0; l < c->nloc; ++l) {
+    uint32_t g = c->lo + l;
+    uint32_t chosen[64];
+    int64_t tmax = t0;
+    for (uint32_t k = 0; k < fanout; ++k) {
+      uint32_t out[4], p;
+      uint32_t ctr[4] = {g, round, k << 16, 0x53544F52u /* "STOR" */};
+      tgo_philox4x32_10(ctr, key, out);
+      uint64_t u = ((uint64_t)out[2] << 32) | out[1];
+      int64_t t = t0 + (spread_ns > 0 ? (int64_t)(u % (uint64_t)spread_ns) : 0);
+      for (uint32_t attempt = 0;; ++attempt) {
+        if (attempt) { uint32_t ctr2[4] = {g, round, (k << 16) | attempt, 0x53544F52u}; tgo_philox4x32_10(ctr2, key, out); }
+        p = out[0] % (c->N - 1);
+        if (p >= g) ++p;
+        int dupl = 0;
+        for (uint32_t j = 0; j < k; ++j) dupl |= chosen[j] == p;
+        if (!dupl) break;
+      }
+      chosen[k] = p;
+      size_t i = (size_t)l * fanout + k;
+      src[i] = g; dst[i] = p; seq[i] = round * fanout + k; sz[i] = size; ts[i] = t;
+      if (t > tmax) tmax = t;
+    }
+    sst[l] = state; sin[l] = g; stt[l] = tmax;
+  }
+  tgsim_msg_soa m = {src, dst, seq, sz, ts};
+  rc = tgo_enqueue(c, &m, n);
+  if (!rc) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
+out:
+  free(src); free(dst); free(seq); free(sz); free(ts); free(sst); free(sin); free(stt);
+  return rc;
+}

@@ -1,0 +1,165 @@
+"""ctypes mirror of include/tgsim.h and the loader of the HIP library (testground_amd/libtgsim.so).
+
+The product path binds ONLY libtgsim.so. If it is missing or cannot find a HIP device, every call
+fails loudly (TgsimError); there is no CPU fallback. The CPU oracle (oracle/liboracle.so) exposes
+the same entry points with a ``tgo_`` prefix and is bound by test infrastructure only
+(oracle/pyoracle.py), through :func:`bind`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtgsim.so")
+
+# ---- constants (tgsim.h) -------------------------------------------------------------------
+OK = 0
+EINVAL, ENOMEM, EHIP, ECAPACITY, ECAUSALITY, ENOTSUP, EUNSUPPORTED_NETWORK, ESTATE, ENODEV = (
+    -1, -2, -3, -4, -5, -6, -7, -8, -9)
+ERROR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EHIP: "EHIP", ECAPACITY: "ECAPACITY",
+               ECAUSALITY: "ECAUSALITY", ENOTSUP: "ENOTSUP",
+               EUNSUPPORTED_NETWORK: "EUNSUPPORTED_NETWORK", ESTATE: "ESTATE", ENODEV: "ENODEV"}
+
+FILTER_ACCEPT, FILTER_REJECT, FILTER_DROP = 0, 1, 2
+POLICY_DENY_ALL, POLICY_ALLOW_ALL = 0, 1
+DST_EXTERNAL = 0xFFFFFFFF
+
+ST_QUEUED, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACHABLE, ST_EXTERNAL, ST_DEST_DOWN, ST_LOCAL = range(8)
+ST_FLAG_DUP, ST_FLAG_CLONE_LOST, ST_FLAG_DUP_CANCEL = 0x10, 0x20, 0x40
+F_CLONE, F_CORRUPT, F_REORDERED, F_STAGE_D, F_LOCAL = 1, 2, 4, 8, 128
+
+
+class TgsimError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class LinkShape(C.Structure):
+    _fields_ = [("latency_ns", C.c_int64), ("jitter_ns", C.c_int64), ("bandwidth_bps", C.c_uint64),
+                ("loss", C.c_float), ("corrupt", C.c_float), ("corrupt_corr", C.c_float),
+                ("reorder", C.c_float), ("reorder_corr", C.c_float), ("duplicate", C.c_float),
+                ("duplicate_corr", C.c_float), ("filter", C.c_int32)]
+
+
+class LinkRule(C.Structure):
+    _fields_ = [("subnet_ip", C.c_uint32), ("prefix_len", C.c_uint32), ("shape", LinkShape)]
+
+
+class NetworkConfig(C.Structure):
+    _fields_ = [("network", C.c_char_p), ("enable", C.c_int32), ("routing_policy", C.c_int32),
+                ("default_shape", LinkShape), ("rules", C.POINTER(LinkRule)), ("n_rules", C.c_size_t),
+                ("has_ipv4", C.c_int32), ("ipv4", C.c_uint32)]
+
+
+class Config(C.Structure):
+    _fields_ = [("n_instances", C.c_uint32), ("shard_id", C.c_uint32), ("n_shards", C.c_uint32),
+                ("device", C.c_uint32), ("seed", C.c_uint64), ("data_subnet", C.c_uint32),
+                ("data_prefix_len", C.c_uint32), ("wheel_slot_ns", C.c_int64), ("wheel_slots", C.c_uint32),
+                ("reserved0", C.c_uint32), ("max_msgs_per_window", C.c_uint64),
+                ("max_records", C.c_uint64), ("exchange_cap", C.c_uint64), ("max_states", C.c_uint32),
+                ("max_waiters", C.c_uint32), ("max_signals", C.c_uint64)]
+
+
+class MsgSoA(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("seq", C.c_void_p), ("size", C.c_void_p),
+                ("t_send", C.c_void_p)]
+
+
+class DeliverySoA(C.Structure):
+    _fields_ = [("t_deliver", C.c_void_p), ("src", C.c_void_p), ("dst", C.c_void_p), ("seq", C.c_void_p),
+                ("size", C.c_void_p), ("flags", C.c_void_p), ("corrupt_off", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("msgs_in", "copies", "lost", "dropped", "rejected", "unreachable",
+                                          "external", "dest_down", "local", "delivered", "windows",
+                                          "inflight")]
+
+
+RECORD_DTYPE_FIELDS = [("t", "<i8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("size", "<u4"),
+                       ("meta", "<u4"), ("corrupt_off", "<u4")]
+
+P = C.c_void_p
+_SIGS = {
+    "create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+    "destroy": (None, [P]),
+    "last_error": (C.c_char_p, [P]),
+    "now": (C.c_int64, [P]),
+    "configure_network": (C.c_int, [P, C.c_uint32, C.POINTER(NetworkConfig)]),
+    "set_shape": (C.c_int, [P, C.c_uint32, C.POINTER(LinkShape)]),
+    "add_rules": (C.c_int, [P, C.c_uint32, C.POINTER(LinkRule), C.c_size_t]),
+    "set_policy": (C.c_int, [P, C.c_uint32, C.c_int32]),
+    "set_enabled": (C.c_int, [P, C.c_uint32, C.c_int32, C.c_int32, C.c_uint32]),
+    "get_ip": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "enqueue": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
+    "advance": (C.c_int, [P, C.c_int64]),
+    "advance_begin": (C.c_int, [P, C.c_int64]),
+    "exchange_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_size_t)]),
+    "advance_end": (C.c_int, [P]),
+    "advance_to_barrier": (C.c_int, [P, C.c_uint32, C.c_int64]),
+    "delivery_count": (C.c_int, [P, C.POINTER(C.c_size_t)]),
+    "copy_deliveries": (C.c_int, [P, C.POINTER(DeliverySoA), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "copy_inbox_offsets": (C.c_int, [P, C.c_void_p, C.c_size_t]),
+    "copy_status": (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "get_stats": (C.c_int, [P, C.POINTER(Stats)]),
+    "sync_signal": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "sync_barrier": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_int64, C.POINTER(C.c_uint32)]),
+    "sync_poll": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_int64)]),
+    "sync_count": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
+}
+# entry points only the HIP library has
+_SIGS_HIP = {
+    "version": (C.c_char_p, []),
+    "abi_version": (C.c_int, []),
+    "set_stream": (C.c_int, [P, P]),
+    "shard_range": (C.c_int, [P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "sync": (C.c_int, [P]),
+    "enqueue_device": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
+    "deliveries_device": (C.c_int, [P, C.POINTER(DeliverySoA)]),
+}
+
+
+class Binding:
+    """A loaded library + its symbol prefix; attribute access returns the typed C function."""
+
+    def __init__(self, cdll: C.CDLL, prefix: str, name: str):
+        self.cdll = cdll
+        self.prefix = prefix
+        self.name = name
+        sigs = dict(_SIGS)
+        if prefix == "tgsim_":
+            sigs.update(_SIGS_HIP)
+        for short, (res, args) in sigs.items():
+            fn = getattr(cdll, prefix + short)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, short, fn)
+
+
+def bind(path: str, prefix: str, name: str) -> Binding:
+    return Binding(C.CDLL(path), prefix, name)
+
+
+_HIP: Binding | None = None
+
+
+def hip_library() -> Binding:
+    """The product library. Raises if it was not built (run __graft_entry__.build())."""
+    global _HIP
+    if _HIP is None:
+        if not os.path.exists(LIB_PATH):
+            raise TgsimError(ENODEV, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        _HIP = bind(LIB_PATH, "tgsim_", "hip")
+    return _HIP
+
+
+def header_symbols(header: str | None = None) -> list[str]:
+    """Every function the public header declares (for the ABI export test)."""
+    import re
+    header = header or os.path.join(os.path.dirname(HERE), "include", "tgsim.h")
+    text = open(header).read()
+    return sorted(set(re.findall(r"\b(tgsim_[a-z_0-9]+)\s*\(", text)))

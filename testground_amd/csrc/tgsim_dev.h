@@ -1,0 +1,88 @@
+// tgsim_dev.h — raw device view of one simulator context and the window pipeline entry points
+// implemented in tgsim_kernels.hip. The host runtime (tgsim_runtime.hip) owns allocation, table
+// uploads and the C ABI; everything here is plain pointers.
+#pragma once
+#include "tgsim_internal.h"
+
+namespace tgsim {
+
+struct Dev {
+  hipStream_t stream = nullptr;
+  uint32_t N = 0, S = 1, shard = 0, lo = 0, nloc = 0;
+  uint32_t data_net = 0, data_mask = 0, data_len = 0;
+  uint32_t key0 = 0, key1 = 0;
+  int64_t slot_ns = 1000000;
+  uint32_t slots = 1024;
+  uint32_t cap_msgs = 0, cap_rec = 0;
+  uint64_t cap_arena = 0;
+  uint32_t xcap = 0;
+  DevScalars* sc = nullptr;       // device
+  DevScalars* h_sc = nullptr;     // pinned host mirror (read at sync points)
+
+  // tables
+  ShapeDev* shape = nullptr;
+  int64_t* X = nullptr;
+  uint8_t* flags = nullptr;       // [N] bit0 link enabled, bit1 external routing allowed
+  uint32_t* ip = nullptr;         // [N]
+  uint32_t* rule_off = nullptr;   // [nloc+1]
+  RuleDev* rules = nullptr;
+
+  // staged messages (SoA) + per-message status
+  uint32_t *m_src = nullptr, *m_dst = nullptr, *m_seq = nullptr, *m_size = nullptr;
+  int64_t* m_t = nullptr;
+  uint8_t* status = nullptr;
+
+  // record batches and the wheel
+  tgsim_record *A = nullptr, *D = nullptr, *L = nullptr, *arena = nullptr;
+  tgsim_record *xsend = nullptr, *xrecv = nullptr;
+  RegionDev* regions = nullptr;
+  uint32_t* dirs = nullptr;
+  uint32_t* plan_start = nullptr;
+  uint32_t* plan_off = nullptr;
+
+  // sort scratch
+  uint32_t *keys0 = nullptr, *keys1 = nullptr, *vals0 = nullptr, *vals1 = nullptr;
+  uint32_t* hist = nullptr;
+  uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
+  LargeSeg* large = nullptr;
+  uint32_t* chunk_off = nullptr;
+  uint64_t *K1a = nullptr, *K1b = nullptr, *K2a = nullptr, *K2b = nullptr;
+  uint32_t *K3a = nullptr, *K3b = nullptr;
+
+  // outputs of the last window
+  int64_t* o_t = nullptr;
+  uint32_t *o_src = nullptr, *o_dst = nullptr, *o_seq = nullptr, *o_size = nullptr,
+           *o_flags = nullptr, *o_coff = nullptr;
+  uint32_t* inbox = nullptr;      // [nloc+1]
+
+  // sync service
+  uint32_t max_states = 0, max_waiters = 0;
+  uint64_t max_signals = 0;
+  uint32_t *s_state = nullptr, *s_inst = nullptr, *s_seq = nullptr;  // batch (device)
+  int64_t* s_t = nullptr;
+  uint32_t s_cap = 0;
+  uint32_t* st_count = nullptr;
+  int64_t* st_last = nullptr;
+  uint32_t* st_nchunks = nullptr;
+  SigChunk* st_chunks = nullptr;
+  int64_t* sig_log = nullptr;
+  uint32_t* w_state = nullptr;
+  uint32_t* w_target = nullptr;
+  int64_t* w_twait = nullptr;
+  int64_t* w_release = nullptr;
+};
+
+// Every function returns hipSuccess or the first HIP error; device-side capacity/ordering problems
+// are reported through DevScalars::err and surfaced by the host at the next sync.
+hipError_t launch_set_window(Dev& d, int64_t T, int64_t t_end);
+hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t offset_ns);
+hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
+hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
+hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
+hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)
+hipError_t signal_batch(Dev& d, uint32_t n, uint64_t log_base, uint32_t n_waiters);
+hipError_t resolve_waiters(Dev& d, uint32_t n_waiters);
+hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
+                            uint32_t size, int64_t spread_ns, uint32_t state);
+
+}  // namespace tgsim

@@ -1,0 +1,129 @@
+// tgsim_internal.h — device-side data layout and helpers shared by the gfx950 kernels and the host
+// runtime of libtgsim.so. Semantics: DESIGN.md section 2. Layout rationale: DESIGN.md section 4.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tgsim.h"
+
+namespace tgsim {
+
+constexpr int kBlock = 256;              // threads per workgroup (4 wave64)
+constexpr int kTile = 1024;              // small-segment tile: segments <= kTile sorted in LDS
+constexpr int kSpan = 2 * kTile;         // LDS capacity of one small-segment span
+constexpr int kChunk = 2048;             // large-segment chunk (LDS bitonic) and merge tile
+constexpr int kRadixBlocks = 512;        // fixed grid of the radix group-by passes
+constexpr int kMaxShards = 64;
+constexpr int kMaxRegions = 8192;        // live timing-wheel regions (one per window)
+constexpr int kStreamBlocks = 2048;      // grid of grid-stride streaming kernels
+constexpr int64_t kNegInf = INT64_MIN / 4;
+constexpr int64_t kTbClamp = (int64_t)1 << 61;
+constexpr uint64_t kCostClamp = (uint64_t)1 << 52;
+constexpr uint32_t kExternalIp = 0x08080808u;
+constexpr uint32_t kNetemSalt = 0x4E45544Du;  // "NETM": 4th Philox counter word of netem draws
+constexpr uint32_t kStormSalt = 0x53544F52u;  // "STOR": storm generator draws
+
+// device error bits (DevScalars::err)
+enum : uint32_t {
+  ERR_CAP_A = 1u << 0, ERR_CAP_D = 1u << 1, ERR_CAP_L = 1u << 2, ERR_CAP_X = 1u << 3,
+  ERR_ARENA = 1u << 4, ERR_REGIONS = 1u << 5, ERR_CAUSAL = 1u << 6, ERR_SIG_ORDER = 1u << 7,
+  ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
+  ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13
+};
+
+// Per-sender egress state derived from network.LinkShape (48 B; gathered by src).
+struct alignas(16) ShapeDev {
+  int64_t mu;        // netem latency (ns)
+  int64_t tau;       // HTB buffer (ns)
+  int32_t sigma;     // netem jitter (ns) as tabledist's s32
+  uint32_t loss_t, dup_t, corrupt_t, reorder_t;
+  uint32_t mult, shift, limited;  // HTB rate as multiply-shift; limited = Bandwidth != 0
+};
+static_assert(sizeof(ShapeDev) == 48, "ShapeDev layout");
+
+struct RuleDev {           // per-sender routing rule, CSR, sorted (plen desc, prefix asc)
+  uint32_t prefix;
+  uint32_t plen_action;    // plen | action << 8
+};
+
+// One live timing-wheel region: the "later" records of one window, bucketed by delivery/ready slot.
+struct RegionDev {
+  uint64_t arena_off;      // first record in the arena ring
+  uint32_t n;              // records
+  uint32_t consumed;       // records already extracted (a prefix in slot order)
+  int64_t base_slot;       // absolute slot of region slot 0 (= floor(window end / slot_ns))
+  uint32_t dir;            // directory index (slot offsets at dirs[dir * (slots + 1)])
+  uint32_t pad;
+};
+
+// Device-resident scalars of one ctx. Host writes them only through kernels / memsets.
+enum { Q_A = 0, Q_D = 1, Q_L = 2, Q_X0 = 3 };  // append queues: TB batch, deliveries, wheel, peers
+struct DevScalars {
+  int64_t T, t_end;                  // current window
+  // ---- per-window block: zeroed by one memset at window start (kWindowResetBegin..End) ----
+  uint32_t q[Q_X0 + kMaxShards];     // append cursors: A, D, L, exchange per peer
+  uint32_t n_extract;                // records extracted from the wheel this window
+  uint32_t plan_tail, plan_n;        // region ring range the extraction plan covers
+  uint32_t n_large, max_large, n_chunks;
+  uint32_t n_recv, n_out;
+  // ---- persistent ----
+  uint32_t err;                      // sticky ERR_* bits
+  uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)
+  uint32_t sig_n;                    // size of the signal batch being processed
+  uint64_t arena_head, arena_tail, arena_used, ins_off;  // arena ring (records)
+  uint64_t sig_log_used;             // signal log entries used
+  // cumulative statistics (tgsim_stats)
+  unsigned long long st[10];
+};
+enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_EXTERNAL, ST_DESTDOWN,
+       ST_LOCAL, ST_DELIVERED };
+
+struct LargeSeg { uint32_t seg, start, len, pad; };
+struct SigChunk { uint32_t seq_start, len; uint64_t log_pos; };
+constexpr int kMaxChunksPerState = 64;
+
+// Sort element of the segmented sorts: order (seg, k1, k2, k3).
+struct SortKey {
+  uint32_t seg;
+  uint64_t k1, k2;
+  uint32_t k3;
+};
+
+__host__ __device__ inline bool key_less(uint32_t sa, uint64_t a1, uint64_t a2, uint32_t a3,
+                                         uint32_t sb, uint64_t b1, uint64_t b2, uint32_t b3) {
+  if (sa != sb) return sa < sb;
+  if (a1 != b1) return a1 < b1;
+  if (a2 != b2) return a2 < b2;
+  return a3 < b3;
+}
+
+// Philox4x32-10 (Random123 constants). Counter-based: draws are a pure function of
+// (key = run seed, counter = (message id, sender, copy|block, salt)).
+__host__ __device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// Shard k owns [floor(kN/S), floor((k+1)N/S)); the owner of g is floor(((g+1)S - 1)/N).
+__host__ __device__ inline uint32_t shard_of(uint32_t g, uint32_t N, uint32_t S) {
+  return (uint32_t)((((uint64_t)g + 1) * S - 1) / N);
+}
+
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ inline uint32_t mask_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+}  // namespace tgsim

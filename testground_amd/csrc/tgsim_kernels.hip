@@ -1,0 +1,1429 @@
+// tgsim_kernels.hip — gfx950 kernels of the simulator's window pipeline.
+//
+//  (1) k_shape        fused route (CIDR LPM over per-sender rule CSR) + netem Philox draws
+//                     (duplicate, loss, corrupt, reorder, jitter) per message -> copy records,
+//                     compacted into per-destination queues with wave64 ballot/prefix appends.
+//  (2) token bucket   copies grouped by sender (stable LSD radix group-by), ordered by
+//                     (netem time, seq, clone-first) with an LDS bitonic sort per sender segment,
+//                     then the HTB GCRA recurrence as a max-plus block scan in LDS.
+//  (3) deliveries     due copies grouped by receiver, ordered (t, src, seq, clone-first) in LDS,
+//                     written as the inbox SoA; future events go to a timing-wheel region:
+//                     a counting (radix) sort on integer-ns slot, extracted by slot prefix later.
+//  (4) sync service   signal batches ordered by (state, t, instance) -> 1-based sequence numbers,
+//                     per-state counters and a signal log; barrier waiters resolved on device.
+// Segments longer than kTile go through a merge-path chunk sort (k_large_*).
+#include <algorithm>
+
+#include "tgsim_dev.h"
+
+namespace tgsim {
+
+// ============================================================================================
+// small device helpers
+// ============================================================================================
+
+__device__ __forceinline__ void load_rec(const tgsim_record* p, tgsim_record& r) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  r.t = (int64_t)(((uint64_t)a.y << 32) | a.x);
+  r.src = a.z; r.dst = a.w; r.seq = b.x; r.size = b.y; r.meta = b.z; r.corrupt_off = b.w;
+}
+__device__ __forceinline__ void store_rec(tgsim_record* p, const tgsim_record& r) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4((uint32_t)(uint64_t)r.t, (uint32_t)((uint64_t)r.t >> 32), r.src, r.dst);
+  q[1] = make_uint4(r.seq, r.size, r.meta, r.corrupt_off);
+}
+
+// Wave64 compaction: every lane with q >= 0 gets a slot in queue q. One atomic per distinct queue
+// per wave (ballot -> leader atomicAdd -> broadcast -> mbcnt rank).
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counters, int q) {
+  uint32_t pos = 0xFFFFFFFFu;
+  bool pending = q >= 0;
+  for (;;) {
+    const uint64_t m = __ballot(pending);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int lq = __shfl(q, leader);
+    const bool mine = pending && q == lq;
+    const uint64_t mm = __ballot(mine);
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(&counters[lq], (uint32_t)__popcll(mm));
+    base = __shfl(base, leader);
+    if (mine) { pos = base + mask_rank(mm); pending = false; }
+  }
+  return pos;
+}
+
+struct Queues {
+  DevScalars* sc;
+  tgsim_record *A, *D, *L, *X;
+  uint32_t cap, xcap;
+  // Wave-collective: all lanes of the wave must call it (q < 0 = nothing to push).
+  __device__ __forceinline__ void push(int q, const tgsim_record& r) const {
+    const uint32_t pos = wave_append(sc->q, q);
+    if (q < 0) return;
+    tgsim_record* buf;
+    uint32_t c = cap, eb;
+    if (q == Q_A) { buf = A; eb = ERR_CAP_A; }
+    else if (q == Q_D) { buf = D; eb = ERR_CAP_D; }
+    else if (q == Q_L) { buf = L; eb = ERR_CAP_L; }
+    else { buf = X + (size_t)(q - Q_X0) * xcap + 1; c = xcap - 1; eb = ERR_CAP_X; }
+    if (pos < c) store_rec(buf + pos, r);
+    else atomicOr(&sc->err, eb);
+  }
+};
+
+struct Geo { uint32_t N, S, shard; };
+
+// Queue of a stage-D record (its t is the delivery time): the receiver's shard, now or later.
+__device__ __forceinline__ int qid_stage_d(const Geo& g, uint32_t dst, int64_t t, int64_t t_end) {
+  if (g.S > 1) {
+    const uint32_t p = shard_of(dst, g.N, g.S);
+    if (p != g.shard) return Q_X0 + (int)p;
+  }
+  return t < t_end ? Q_D : Q_L;
+}
+
+__device__ __forceinline__ uint32_t clamp_n(const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = *n_ptr;
+  return n < cap ? n : cap;
+}
+
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
+  v = v < 2 ? 2 : v;
+  return 1u << (32 - __clz(v - 1));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ============================================================================================
+// window control
+// ============================================================================================
+
+__global__ void k_set_window(DevScalars* sc, int64_t T, int64_t t_end) {
+  sc->T = T;
+  sc->t_end = t_end;
+}
+
+// t_end = release time of a barrier waiter + offset, decided on the device (no host round trip).
+__global__ void k_set_window_barrier(DevScalars* sc, const int64_t* w_release, uint32_t waiter,
+                                     int64_t T, int64_t offset) {
+  const int64_t rel = w_release[waiter];
+  sc->T = T;
+  if (rel < 0) {
+    atomicOr(&sc->err, ERR_UNRELEASED);
+    sc->t_end = T;
+  } else {
+    const int64_t e = rel + offset;
+    sc->t_end = e < T ? T : e;
+  }
+}
+
+__global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
+
+__global__ void k_reset_tb(int64_t* X, const uint32_t* locals, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) X[locals[i]] = kNegInf;
+}
+
+// ============================================================================================
+// (1) route + netem: one thread per staged message
+// ============================================================================================
+
+enum { R_NONE = 0, R_DATA, R_DEFAULT, R_DROP, R_REJECT };
+
+struct ShapeArgs {
+  const uint32_t *src, *dst, *seq, *size;
+  const int64_t* t;
+  uint32_t n;
+  uint8_t* status;
+  const ShapeDev* shape;
+  const uint8_t* flags;
+  const uint32_t* ip;
+  const uint32_t* rule_off;
+  const RuleDev* rules;
+  uint32_t lo, nloc, data_net, data_mask, data_len, key0, key1;
+  Geo geo;
+  Queues Q;
+};
+
+// Longest-prefix match over the sender's routing table: rule groups by prefix
+// length (descending), each a sorted run searched by bisection; the data network's connected
+// route and the control network's default route compete at their own prefix lengths.
+__device__ int route_lookup(const ShapeArgs& a, uint32_t sl, uint32_t g, uint32_t dip) {
+  const uint8_t f = a.flags[g];
+  const bool data_ok = (f & 1u) && ((dip & a.data_mask) == a.data_net);
+  uint32_t pos = a.rule_off[sl];
+  const uint32_t end = a.rule_off[sl + 1];
+  while (pos < end) {
+    const uint32_t plen = a.rules[pos].plen_action & 0xFFu;
+    if (data_ok && a.data_len > plen) return R_DATA;
+    uint32_t lo = pos + 1, hi = end;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((a.rules[mid].plen_action & 0xFFu) == plen) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t gend = lo;
+    const uint32_t mask = plen ? 0xFFFFFFFFu << (32 - plen) : 0u;
+    const uint32_t target = dip & mask;
+    lo = pos; hi = gend;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.rules[mid].prefix < target) lo = mid + 1; else hi = mid;
+    }
+    if (lo < gend && a.rules[lo].prefix == target)
+      return ((a.rules[lo].plen_action >> 8) & 0xFFu) == TGSIM_FILTER_DROP ? R_DROP : R_REJECT;
+    pos = gend;
+  }
+  if (data_ok) return R_DATA;
+  if (f & 2u) return R_DEFAULT;
+  return R_NONE;
+}
+
+// netem tabledist() uniform branch [EXT].
+__device__ __forceinline__ int64_t tabledist(int64_t mu, int32_t sigma, uint32_t rnd) {
+  if (sigma == 0) return mu;
+  const uint32_t m = 2u * (uint32_t)sigma;
+  if (m == 0) return mu;
+  return (int64_t)(rnd % m) + mu - (int64_t)sigma;
+}
+
+// The part of netem_enqueue [EXT] after the duplicate/loss decision, for one copy.
+__device__ __forceinline__ bool netem_copy(const ShapeDev& sh, uint32_t src, uint32_t dst, uint32_t seq,
+                                           uint32_t size, int64_t ts, uint32_t clone, uint32_t k0,
+                                           uint32_t k1, tgsim_record& rec) {
+  uint32_t r0[4];
+  philox4x32_10(seq, src, clone, kNetemSalt, k0, k1, r0);
+  if (clone && sh.loss_t && sh.loss_t >= r0[1]) return false;
+  rec.src = src; rec.dst = dst; rec.seq = seq; rec.size = size;
+  rec.meta = clone ? TGSIM_F_CLONE : 0u;
+  rec.corrupt_off = 0;
+  if (sh.corrupt_t) {
+    uint32_t r1[4];
+    philox4x32_10(seq, src, clone | 2u, kNetemSalt, k0, k1, r1);
+    if (sh.corrupt_t >= r1[0] && size > 0) {
+      rec.meta |= TGSIM_F_CORRUPT | ((r1[2] % 8u) << TGSIM_F_BIT_SHIFT);
+      rec.corrupt_off = r1[1] % size;
+    }
+  }
+  if (sh.reorder_t && !(sh.reorder_t < r0[3])) {
+    rec.meta |= TGSIM_F_REORDERED;
+    rec.t = ts;
+  } else {
+    const int64_t delay = tabledist(sh.mu, sh.sigma, r0[2]);
+    rec.t = ts + (delay > 0 ? delay : 0);
+  }
+  if (!sh.limited) rec.meta |= TGSIM_F_STAGE_D;
+  return true;
+}
+
+__device__ __forceinline__ int qid_copy(const ShapeArgs& a, const tgsim_record& r, int64_t t_end) {
+  if (r.meta & TGSIM_F_STAGE_D) return qid_stage_d(a.geo, r.dst, r.t, t_end);
+  return r.t < t_end ? Q_A : Q_L;
+}
+
+__global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
+  DevScalars* sc = a.Q.sc;
+  const int64_t T = sc->T, t_end = sc->t_end;
+  uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
+    const int64_t ts = a.t[i];
+    tgsim_record r1, r2;
+    int q1 = -1, q2 = -1;
+    uint8_t st;
+    cnt[ST_MSGS]++;
+    const uint32_t sl = src - a.lo;
+    if (sl >= a.nloc || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
+      atomicOr(&sc->err, ERR_BAD_MSG);
+      st = TGSIM_ST_UNREACHABLE;
+      cnt[ST_UNREACH]++;
+    } else if (ts < T || ts >= t_end) {
+      atomicOr(&sc->err, ERR_CAUSAL);
+      st = TGSIM_ST_UNREACHABLE;
+      cnt[ST_UNREACH]++;
+    } else if (dst == src) {  // loopback: unshaped
+      r2.t = ts; r2.src = src; r2.dst = dst; r2.seq = seq; r2.size = size;
+      r2.meta = TGSIM_F_LOCAL | TGSIM_F_STAGE_D; r2.corrupt_off = 0;
+      q2 = qid_stage_d(a.geo, dst, ts, t_end);
+      st = TGSIM_ST_LOCAL;
+      cnt[ST_LOCAL]++;
+    } else {
+      const bool ext = dst == TGSIM_DST_EXTERNAL;
+      const int rt = route_lookup(a, sl, src, ext ? kExternalIp : a.ip[dst]);
+      if (rt == R_DROP) { st = TGSIM_ST_DROPPED; cnt[ST_DROPPED]++; }
+      else if (rt == R_REJECT) { st = TGSIM_ST_REJECTED; cnt[ST_REJECTED]++; }
+      else if (rt == R_DEFAULT && ext) { st = TGSIM_ST_EXTERNAL; cnt[ST_EXTERNAL]++; }
+      else if (rt != R_DATA) { st = TGSIM_ST_UNREACHABLE; cnt[ST_UNREACH]++; }
+      else if (!(a.flags[dst] & 1u)) { st = TGSIM_ST_DEST_DOWN; cnt[ST_DESTDOWN]++; }
+      else {
+        const ShapeDev sh = a.shape[sl];
+        uint32_t r0[4];
+        philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
+        int count = 1;
+        const bool dup = sh.dup_t && sh.dup_t >= r0[0];
+        if (dup) ++count;
+        const bool lost = sh.loss_t && sh.loss_t >= r0[1];
+        if (lost) --count;
+        if (count == 0) {
+          st = TGSIM_ST_LOST;
+          cnt[ST_LOST]++;
+        } else {
+          st = TGSIM_ST_QUEUED;
+          if (dup && lost) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+          if (count == 2) {
+            st |= TGSIM_ST_FLAG_DUP;
+            if (netem_copy(sh, src, dst, seq, size, ts, 1u, a.key0, a.key1, r1)) {
+              q1 = qid_copy(a, r1, t_end);
+              cnt[ST_COPIES]++;
+            } else {
+              st |= TGSIM_ST_FLAG_CLONE_LOST;
+            }
+          }
+          netem_copy(sh, src, dst, seq, size, ts, 0u, a.key0, a.key1, r2);
+          q2 = qid_copy(a, r2, t_end);
+          cnt[ST_COPIES]++;
+        }
+      }
+    }
+    a.status[i] = st;
+    a.Q.push(q1, r1);
+    a.Q.push(q2, r2);
+  }
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+    const uint32_t v = wave_sum(cnt[c]);
+    if (lane_id() == 0 && v) atomicAdd(&sc->st[c], (unsigned long long)v);
+  }
+}
+
+// ============================================================================================
+// timing wheel: plan (which slot prefixes of which live regions are due), extract, insert
+// ============================================================================================
+
+__global__ __launch_bounds__(kBlock) void k_plan(RegionDev* regions, const uint32_t* dirs, uint32_t slots,
+                                                 int64_t slot_ns, uint32_t* plan_start,
+                                                 uint32_t* plan_off, DevScalars* sc) {
+  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tail = sc->reg_tail, head = sc->reg_head, nlive = head - tail;
+  const int64_t t_end = sc->t_end;
+  const int64_t kabs = t_end > 0 ? (t_end - 1) / slot_ns : -1;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nlive; base += kBlock) {
+    const uint32_t k = base + tid;
+    uint32_t len = 0;
+    if (k < nlive) {
+      RegionDev& r = regions[(tail + k) % kMaxRegions];
+      const uint32_t start = r.consumed;
+      uint32_t hi = start;
+      if (kabs >= 0) {
+        const int64_t krel = kabs - r.base_slot;
+        if (krel >= (int64_t)slots - 1) hi = r.n;
+        else if (krel >= 0) hi = dirs[(size_t)r.dir * (slots + 1) + (uint32_t)krel + 1];
+      }
+      if (hi < start) hi = start;
+      len = hi - start;
+      r.consumed = hi;
+      plan_start[k] = start;
+    }
+    part[tid] = len;
+    __syncthreads();
+    for (uint32_t o = 1; o < kBlock; o <<= 1) {
+      const uint32_t v = tid >= o ? part[tid - o] : 0u;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    if (k < nlive) plan_off[k] = carry + part[tid] - len;
+    __syncthreads();
+    if (tid == kBlock - 1) carry += part[tid];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    plan_off[nlive] = carry;
+    sc->n_extract = carry;
+    sc->plan_tail = tail;
+    sc->plan_n = nlive;
+    uint32_t t = tail;
+    uint64_t freed = 0;
+    while (t != head) {
+      const RegionDev& r = regions[t % kMaxRegions];
+      if (r.consumed != r.n) break;
+      freed += r.n;
+      ++t;
+    }
+    sc->reg_tail = t;
+    sc->arena_used -= freed;
+    sc->arena_tail = (t == head) ? sc->arena_head : regions[t % kMaxRegions].arena_off;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, const uint32_t* plan_start,
+                                                    const uint32_t* plan_off, const tgsim_record* arena,
+                                                    Queues Q) {
+  DevScalars* sc = Q.sc;
+  const uint32_t total = sc->n_extract, tail = sc->plan_tail, nl = sc->plan_n;
+  const int64_t t_end = sc->t_end;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
+    uint32_t lo = 0, hi = nl;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (plan_off[mid] <= j) lo = mid; else hi = mid;
+    }
+    const RegionDev& r = regions[(tail + lo) % kMaxRegions];
+    tgsim_record rec;
+    load_rec(arena + r.arena_off + plan_start[lo] + (j - plan_off[lo]), rec);
+    const int q = rec.t < t_end ? ((rec.meta & TGSIM_F_STAGE_D) ? Q_D : Q_A) : Q_L;
+    Q.push(q, rec);
+  }
+}
+
+// Allocate this window's region in the arena ring (one thread).
+__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, uint32_t cap,
+                               int64_t slot_ns) {
+  const uint32_t n = min(sc->q[Q_L], cap);
+  if (sc->reg_head - sc->reg_tail >= (uint32_t)kMaxRegions) {
+    atomicOr(&sc->err, ERR_REGIONS);
+    sc->ins_off = ~0ull;
+    return;
+  }
+  uint64_t head = sc->arena_head, tail = sc->arena_tail, off;
+  if (sc->arena_used == 0) {
+    head = tail = 0;
+    sc->arena_tail = 0;
+    off = 0;
+    if (n > cap_arena) { atomicOr(&sc->err, ERR_ARENA); sc->ins_off = ~0ull; return; }
+  } else if (head > tail) {
+    if (head + n <= cap_arena) off = head;
+    else if (n <= tail) off = 0;
+    else { atomicOr(&sc->err, ERR_ARENA); sc->ins_off = ~0ull; return; }
+  } else {
+    if (head + n <= tail) off = head;
+    else { atomicOr(&sc->err, ERR_ARENA); sc->ins_off = ~0ull; return; }
+  }
+  const uint32_t slot = sc->reg_head % kMaxRegions;
+  RegionDev r;
+  r.arena_off = off; r.n = n; r.consumed = 0;
+  r.base_slot = sc->t_end / slot_ns;
+  r.dir = slot; r.pad = 0;
+  regions[slot] = r;
+  sc->reg_head += 1;
+  sc->arena_head = off + n;
+  sc->arena_used += n;
+  if (sc->reg_head - sc->reg_tail == 1) sc->arena_tail = off;
+  sc->ins_off = off;
+}
+
+__global__ __launch_bounds__(kBlock) void k_region_fill(const tgsim_record* L, const uint32_t* keys,
+                                                        const uint32_t* vals, tgsim_record* arena,
+                                                        uint32_t* dirs, uint32_t slots, uint32_t cap,
+                                                        const DevScalars* sc) {
+  const uint64_t off = sc->ins_off;
+  if (off == ~0ull) return;
+  const uint32_t n = min(sc->q[Q_L], cap);
+  const uint32_t dir = (sc->reg_head - 1) % kMaxRegions;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t i = tid; i < n; i += stride) {
+    tgsim_record r;
+    load_rec(L + vals[i], r);
+    store_rec(arena + off + i, r);
+  }
+  for (uint32_t s = tid; s <= slots; s += stride)
+    dirs[(size_t)dir * (slots + 1) + s] = lower_bound_u32(keys, n, s);
+}
+
+// ============================================================================================
+// stable LSD radix group-by on u32 keys (8-bit digits, wave64 ballot ranking)
+// ============================================================================================
+
+__device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_t& end) {
+  uint32_t chunk = (n + kRadixBlocks - 1) / kRadixBlocks;
+  chunk = (chunk + kBlock - 1) & ~(uint32_t)(kBlock - 1);
+  start = blockIdx.x * chunk;
+  end = min(start + chunk, n);
+  if (start > n) start = n;
+}
+
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t* keys, const uint32_t* n_ptr,
+                                                       uint32_t cap, int shift, uint32_t* hist) {
+  __shared__ uint32_t h[256];
+  const uint32_t n = clamp_n(n_ptr, cap);
+  uint32_t start, end;
+  radix_range(n, start, end);
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = start + threadIdx.x; i < end; i += kBlock) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+  __syncthreads();
+  hist[threadIdx.x * kRadixBlocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan over hist[256 * kRadixBlocks] (digit-major), one block of 1024 threads
+__global__ __launch_bounds__(1024) void k_radix_scan(uint32_t* hist) {
+  constexpr int N = 256 * kRadixBlocks, PER = N / 1024;
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x;
+  uint32_t s = 0;
+  for (int i = 0; i < PER; ++i) s += hist[t * PER + i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t v = hist[t * PER + i];
+    hist[t * PER + i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* kin, const uint32_t* vin,
+                                                          uint32_t* kout, uint32_t* vout,
+                                                          const uint32_t* n_ptr, uint32_t cap, int shift,
+                                                          const uint32_t* hist) {
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t wcnt[4][256];
+  const uint32_t n = clamp_n(n_ptr, cap);
+  uint32_t start, end;
+  radix_range(n, start, end);
+  const uint32_t tid = threadIdx.x, wave = tid >> 6;
+  base[tid] = hist[tid * kRadixBlocks + blockIdx.x];
+  for (uint32_t t0 = start; t0 < end; t0 += kBlock) {
+    const uint32_t i = t0 + tid;
+    const bool valid = i < end;
+    const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
+    const uint32_t d = (k >> shift) & 255u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(valid && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = mask_rank(peers);
+    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+    __syncthreads();
+    wcnt[0][tid] = 0; wcnt[1][tid] = c0; wcnt[2][tid] = c0 + c1; wcnt[3][tid] = c0 + c1 + c2;
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = base[d] + wcnt[wave][d] + rank;
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+    __syncthreads();
+    base[tid] += c0 + c1 + c2 + c3;
+    __syncthreads();
+  }
+}
+
+// keys of a record batch: 0 = sender (local), 1 = receiver (local), 2 = wheel slot
+__global__ __launch_bounds__(kBlock) void k_keys_rec(const tgsim_record* batch, const uint32_t* n_ptr,
+                                                     uint32_t cap, int mode, uint32_t lo, int64_t slot_ns,
+                                                     uint32_t slots, const DevScalars* sc, uint32_t* keys,
+                                                     uint32_t* vals) {
+  const uint32_t n = clamp_n(n_ptr, cap);
+  const int64_t base_slot = sc->t_end / slot_ns;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint4 a = reinterpret_cast<const uint4*>(batch + i)[0];
+    uint32_t k;
+    if (mode == 0) k = a.z - lo;
+    else if (mode == 1) k = a.w - lo;
+    else {
+      const int64_t t = (int64_t)(((uint64_t)a.y << 32) | a.x);
+      int64_t s = t / slot_ns - base_slot;
+      s = s < 0 ? 0 : (s > (int64_t)slots - 1 ? (int64_t)slots - 1 : s);
+      k = (uint32_t)s;
+    }
+    keys[i] = k;
+    vals[i] = i;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, uint32_t n, uint32_t* keys,
+                                                     uint32_t* vals) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    keys[i] = states[i];
+    vals[i] = i;
+  }
+}
+
+// Segment offsets off[k] = first position of key k (k = 0..K), and the list of segments longer
+// than kTile (handled by the merge-path path).
+__global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const uint32_t* n_ptr, uint32_t cap,
+                                                   uint32_t K, uint32_t* off, LargeSeg* large,
+                                                   DevScalars* sc) {
+  const uint32_t n = clamp_n(n_ptr, cap);
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= K; k += stride) {
+    const uint32_t lb = lower_bound_u32(keys, n, k);
+    off[k] = lb;
+    if (k < K) {
+      const uint32_t ub = lower_bound_u32(keys, n, k + 1);
+      const uint32_t len = ub - lb;
+      if (len > (uint32_t)kTile) {
+        const uint32_t i = atomicAdd(&sc->n_large, 1u);
+        LargeSeg L;
+        L.seg = k; L.start = lb; L.len = len; L.pad = 0;
+        large[i] = L;
+        atomicMax(&sc->max_large, len);
+      }
+    }
+  }
+}
+
+// ============================================================================================
+// segmented sorts: LDS bitonic for small segments, chunk sort + merge path for large ones
+// ============================================================================================
+
+struct SortSmem {
+  uint64_t k1[kSpan];
+  uint64_t k2[kSpan];
+  uint32_t sg[kSpan];
+  uint32_t k3[kSpan];
+  int64_t scA[kBlock];
+  int64_t scB[kBlock];
+  int64_t carry;
+  uint32_t pad[2];
+};
+
+__device__ __forceinline__ void bitonic_lds(SortSmem& s, uint32_t npad) {
+  for (uint32_t k = 2; k <= npad; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t p = threadIdx.x; p < (npad >> 1); p += kBlock) {
+        const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+        const uint32_t l = i + j;
+        const bool up = (i & k) == 0;
+        const bool lt = key_less(s.sg[l], s.k1[l], s.k2[l], s.k3[l], s.sg[i], s.k1[i], s.k2[i], s.k3[i]);
+        if (lt == up) {
+          uint32_t ts = s.sg[i]; s.sg[i] = s.sg[l]; s.sg[l] = ts;
+          uint64_t t1 = s.k1[i]; s.k1[i] = s.k1[l]; s.k1[l] = t1;
+          uint64_t t2 = s.k2[i]; s.k2[i] = s.k2[l]; s.k2[l] = t2;
+          uint32_t t3 = s.k3[i]; s.k3[i] = s.k3[l]; s.k3[l] = t3;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ void pad_key(SortSmem& s, uint32_t j) {
+  s.sg[j] = 0xFFFFFFFFu; s.k1[j] = ~0ull; s.k2[j] = ~0ull; s.k3[j] = 0xFFFFFFFFu;
+}
+
+template <class P>
+__global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys, const uint32_t* vals,
+                                                      const uint32_t* off, const uint32_t* n_ptr,
+                                                      uint32_t cap) {
+  __shared__ SortSmem s;
+  const uint32_t n = clamp_n(n_ptr, cap);
+  const uint32_t ntiles = (n + kTile - 1) / kTile;
+  for (uint32_t w = blockIdx.x; w < ntiles; w += gridDim.x) {
+    const uint32_t a = w * kTile, b = min(a + kTile, n);
+    const uint32_t s_begin = (a == 0 || keys[a] != keys[a - 1]) ? a : off[keys[a] + 1];
+    uint32_t s_next = (b >= n) ? n : ((keys[b] != keys[b - 1]) ? b : off[keys[b] + 1]);
+    if (s_begin >= s_next) continue;
+    const uint32_t kl = keys[s_next - 1];
+    if (off[kl + 1] - off[kl] > (uint32_t)kTile) s_next = off[kl];
+    if (s_next <= s_begin) continue;
+    const uint32_t m = s_next - s_begin;
+    const uint32_t npad = next_pow2(m);
+    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
+      if (j < m) {
+        const uint32_t i = s_begin + j;
+        p.key(keys[i], vals[i], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+      } else {
+        pad_key(s, j);
+      }
+    }
+    __syncthreads();
+    bitonic_lds(s, npad);
+    p.epilogue(s, m, npad, s_begin, off);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_large_prep(const LargeSeg* large, uint32_t* chunk_off,
+                                                       DevScalars* sc) {
+  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t carry;
+  const uint32_t nl = sc->n_large, tid = threadIdx.x;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nl; base += kBlock) {
+    const uint32_t i = base + tid;
+    const uint32_t c = i < nl ? (large[i].len + kChunk - 1) / kChunk : 0u;
+    part[tid] = c;
+    __syncthreads();
+    for (uint32_t o = 1; o < kBlock; o <<= 1) {
+      const uint32_t v = tid >= o ? part[tid - o] : 0u;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    if (i < nl) chunk_off[i] = carry + part[tid] - c;
+    __syncthreads();
+    if (tid == kBlock - 1) carry += part[tid];
+    __syncthreads();
+  }
+  if (tid == 0) { chunk_off[nl] = carry; sc->n_chunks = carry; }
+}
+
+__device__ __forceinline__ uint32_t chunk_owner(const uint32_t* chunk_off, uint32_t nl, uint32_t c) {
+  uint32_t lo = 0, hi = nl;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (chunk_off[mid] <= c) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <class P>
+__global__ __launch_bounds__(kBlock) void k_large_chunks(P p, const uint32_t* keys, const uint32_t* vals,
+                                                         const LargeSeg* large, const uint32_t* chunk_off,
+                                                         const DevScalars* sc, uint64_t* K1, uint64_t* K2,
+                                                         uint32_t* K3) {
+  __shared__ SortSmem s;
+  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
+  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+    const uint32_t li = chunk_owner(chunk_off, nl, c);
+    const LargeSeg L = large[li];
+    const uint32_t q = c - chunk_off[li];
+    const uint32_t st = L.start + q * kChunk;
+    const uint32_t cnt = min((uint32_t)kChunk, L.len - q * kChunk);
+    const uint32_t npad = next_pow2(cnt);
+    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
+      if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+      else pad_key(s, j);
+    }
+    __syncthreads();
+    bitonic_lds(s, npad);
+    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
+      K1[st + j] = s.k1[j]; K2[st + j] = s.k2[j]; K3[st + j] = s.k3[j];
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ bool kless(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3,
+                                      uint32_t x, uint32_t y) {
+  return key_less(0, K1[x], K2[x], K3[x], 0, K1[y], K2[y], K3[y]);
+}
+
+// One merge-path pass: runs of width W inside every large segment are merged pairwise; each work
+// item produces kChunk outputs, 8 per thread from its own diagonal search.
+__global__ __launch_bounds__(kBlock) void k_large_merge(const LargeSeg* large, const uint32_t* chunk_off,
+                                                        const DevScalars* sc, uint32_t W,
+                                                        const uint64_t* sK1, const uint64_t* sK2,
+                                                        const uint32_t* sK3, uint64_t* dK1, uint64_t* dK2,
+                                                        uint32_t* dK3) {
+  constexpr uint32_t IT = kChunk / kBlock;
+  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
+  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+    const uint32_t li = chunk_owner(chunk_off, nl, c);
+    const LargeSeg L = large[li];
+    const uint32_t q = c - chunk_off[li];
+    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
+    const uint32_t base = L.start;
+    if (L.len <= W) {
+      for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock) {
+        dK1[base + j] = sK1[base + j]; dK2[base + j] = sK2[base + j]; dK3[base + j] = sK3[base + j];
+      }
+      continue;
+    }
+    const uint32_t pair = o0 / (2 * W);
+    const uint32_t As = pair * 2 * W;
+    const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
+    const uint32_t nA = Ae - As, nB = Be - Ae;
+    const uint32_t dend = o1 - As;
+    const uint32_t d0 = o0 - As + threadIdx.x * IT;
+    if (d0 >= dend) continue;
+    const uint32_t a0 = base + As, b0 = base + Ae;
+    uint32_t lo = d0 > nB ? d0 - nB : 0u, hi = min(d0, nA);
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (!kless(sK1, sK2, sK3, b0 + (d0 - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
+    }
+    uint32_t ia = lo, ib = d0 - lo;
+    for (uint32_t k = 0; k < IT && d0 + k < dend; ++k) {
+      bool takeA;
+      if (ib >= nB) takeA = true;
+      else if (ia >= nA) takeA = false;
+      else takeA = !kless(sK1, sK2, sK3, b0 + ib, a0 + ia);
+      const uint32_t src = takeA ? a0 + ia++ : b0 + ib++;
+      const uint32_t dst = base + As + d0 + k;
+      dK1[dst] = sK1[src]; dK2[dst] = sK2[src]; dK3[dst] = sK3[src];
+    }
+  }
+}
+
+// ============================================================================================
+// (2) token bucket: HTB as GCRA, X_i = min(max(X_{i-1}, e_i - tau) + c_i, 2^61), d_i = max(e_i, X_{i-1}).
+// Each step is the max-plus affine map x -> max(min(x + A, K), B); maps compose associatively, so
+// a block scan over the sorted span gives every d_i. A == kNegInf marks a constant map (segment head).
+// ============================================================================================
+
+struct MP { int64_t A, B; };
+
+__device__ __forceinline__ int64_t sadd(int64_t a, int64_t b) {
+  if (a == kNegInf || b == kNegInf) return kNegInf;
+  const int64_t s = a + b;
+  return s > kTbClamp ? kTbClamp : s;
+}
+__device__ __forceinline__ MP mp_then(MP e, MP l) {  // l after e
+  MP r;
+  r.A = sadd(e.A, l.A);
+  const int64_t eb = sadd(e.B, l.A);
+  r.B = eb > l.B ? eb : l.B;
+  return r;
+}
+__device__ __forceinline__ int64_t mp_apply(MP f, int64_t x) {
+  if (f.A == kNegInf || x == kNegInf) return f.B;
+  int64_t v = x + f.A;
+  v = v > kTbClamp ? kTbClamp : v;
+  return v > f.B ? v : f.B;
+}
+
+__device__ __forceinline__ uint64_t l2t_ns(const ShapeDev& sh, uint32_t len) {
+  const uint64_t c = ((uint64_t)len * sh.mult) >> sh.shift;
+  return c > kCostClamp ? kCostClamp : c;
+}
+
+struct TBPolicy {
+  const tgsim_record* A;
+  const ShapeDev* shape;
+  int64_t* X;
+  uint32_t lo;
+  Geo geo;
+  Queues Q;
+  const DevScalars* sc;
+
+  __device__ __forceinline__ void key(uint32_t seg, uint32_t idx, uint32_t& sg, uint64_t& k1, uint64_t& k2,
+                                      uint32_t& k3) const {
+    const uint4 a = reinterpret_cast<const uint4*>(A + idx)[0];
+    const uint4 b = reinterpret_cast<const uint4*>(A + idx)[1];
+    sg = seg;
+    k1 = ((uint64_t)a.y << 32) | a.x;                          // netem time_to_send (>= 0)
+    k2 = ((uint64_t)b.x << 1) | ((b.z & TGSIM_F_CLONE) ? 0u : 1u);  // seq, clone first
+    k3 = idx;
+  }
+
+  // Scan m sorted items in LDS (segments contiguous). has_carry: the first item continues a
+  // segment whose X before it is `carry`. final: the last item ends its segment.
+  __device__ void scan(SortSmem& s, uint32_t m, uint32_t npad, bool has_carry, int64_t carry,
+                       bool final) const {
+    const int64_t t_end = sc->t_end;
+    const uint32_t IT = npad >= kBlock ? npad / kBlock : 1u;
+    const uint32_t j0 = threadIdx.x * IT;
+    // phase 1: per-thread aggregate
+    MP agg = {0, kNegInf};
+    for (uint32_t u = 0; u < IT; ++u) {
+      const uint32_t j = j0 + u;
+      if (j >= m) break;
+      const uint32_t sl = s.sg[j];
+      const ShapeDev& sh = shape[sl];
+      const int64_t e = (int64_t)s.k1[j];
+      const int64_t c = (int64_t)l2t_ns(sh, A[s.k3[j]].size);
+      const bool head = (j == 0) ? !has_carry : (s.sg[j - 1] != sl);
+      MP f;
+      if (head) {
+        const int64_t xs = X[sl];
+        const int64_t b = xs > e - sh.tau ? xs : e - sh.tau;
+        int64_t v = b + c;
+        f.A = kNegInf; f.B = v > kTbClamp ? kTbClamp : v;
+      } else {
+        f.A = c;
+        const int64_t v = e - sh.tau + c;
+        f.B = v > kTbClamp ? kTbClamp : v;
+      }
+      agg = mp_then(agg, f);
+    }
+    s.scA[threadIdx.x] = agg.A;
+    s.scB[threadIdx.x] = agg.B;
+    __syncthreads();
+    // phase 2: inclusive Hillis-Steele scan of the 256 aggregates
+    for (uint32_t o = 1; o < kBlock; o <<= 1) {
+      MP v = {0, kNegInf};
+      const bool has = threadIdx.x >= o;
+      if (has) { v.A = s.scA[threadIdx.x - o]; v.B = s.scB[threadIdx.x - o]; }
+      MP me = {s.scA[threadIdx.x], s.scB[threadIdx.x]};
+      __syncthreads();
+      if (has) { me = mp_then(v, me); s.scA[threadIdx.x] = me.A; s.scB[threadIdx.x] = me.B; }
+      __syncthreads();
+    }
+    MP P = {0, kNegInf};
+    if (has_carry) { P.A = kNegInf; P.B = carry; }
+    if (threadIdx.x > 0) {
+      const MP prev = {s.scA[threadIdx.x - 1], s.scB[threadIdx.x - 1]};
+      P = mp_then(P, prev);
+    }
+    // phase 3: per item d = max(e, X_prev), route the departed copy
+    for (uint32_t u = 0; u < IT; ++u) {
+      const uint32_t j = j0 + u;
+      tgsim_record rec;
+      int q = -1;
+      if (j < m) {
+        const uint32_t sl = s.sg[j];
+        const ShapeDev& sh = shape[sl];
+        const int64_t e = (int64_t)s.k1[j];
+        load_rec(A + s.k3[j], rec);
+        const int64_t c = (int64_t)l2t_ns(sh, rec.size);
+        const bool head = (j == 0) ? !has_carry : (s.sg[j - 1] != sl);
+        int64_t xprev;
+        MP f;
+        if (head) {
+          xprev = X[sl];
+          const int64_t b = xprev > e - sh.tau ? xprev : e - sh.tau;
+          const int64_t v = b + c;
+          f.A = kNegInf; f.B = v > kTbClamp ? kTbClamp : v;
+        } else {
+          xprev = mp_apply(P, kNegInf);
+          f.A = c;
+          const int64_t v = e - sh.tau + c;
+          f.B = v > kTbClamp ? kTbClamp : v;
+        }
+        P = mp_then(P, f);
+        s.k2[j] = (uint64_t)mp_apply(P, kNegInf);  // X after this item (written back below)
+        if (j + 1 == m) s.carry = mp_apply(P, kNegInf);
+        rec.t = e > xprev ? e : xprev;
+        rec.meta |= TGSIM_F_STAGE_D;
+        q = qid_stage_d(geo, rec.dst, rec.t, t_end);
+      }
+      Q.push(q, rec);
+    }
+    __syncthreads();  // every head has read X before any segment end overwrites it
+    for (uint32_t u = 0; u < IT; ++u) {
+      const uint32_t j = j0 + u;
+      if (j >= m) break;
+      const bool last = (j + 1 == m) ? final : (s.sg[j + 1] != s.sg[j]);
+      if (last) X[s.sg[j]] = (int64_t)s.k2[j];
+    }
+    __syncthreads();
+  }
+
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t npad, uint32_t, const uint32_t*) const {
+    scan(s, m, npad, false, 0, true);
+  }
+};
+
+// One block per large sender segment: sorted keys arrive in tiles of kChunk with a carried X.
+__global__ __launch_bounds__(kBlock) void k_tb_large(TBPolicy p, const LargeSeg* large,
+                                                     const uint64_t* K1, const uint32_t* K3) {
+  __shared__ SortSmem s;
+  const uint32_t nl = p.sc->n_large;
+  for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+    const LargeSeg L = large[li];
+    bool has_carry = false;
+    int64_t carry = 0;
+    for (uint32_t t0 = 0; t0 < L.len; t0 += kChunk) {
+      const uint32_t cnt = min((uint32_t)kChunk, L.len - t0);
+      const uint32_t npad = next_pow2(cnt);
+      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
+        s.sg[j] = L.seg; s.k1[j] = K1[L.start + t0 + j]; s.k3[j] = K3[L.start + t0 + j];
+      }
+      __syncthreads();
+      p.scan(s, cnt, npad, has_carry, carry, t0 + cnt == L.len);
+      carry = s.carry;
+      has_carry = true;
+      __syncthreads();
+    }
+  }
+}
+
+// ============================================================================================
+// (3) deliveries: inbox order (dst, t, src, seq, clone-first), written as SoA
+// ============================================================================================
+
+struct EmitPolicy {
+  const tgsim_record* D;
+  uint32_t lo;
+  int64_t* o_t;
+  uint32_t *o_src, *o_dst, *o_seq, *o_size, *o_flags, *o_coff;
+
+  __device__ __forceinline__ void key(uint32_t seg, uint32_t idx, uint32_t& sg, uint64_t& k1, uint64_t& k2,
+                                      uint32_t& k3) const {
+    const uint4 a = reinterpret_cast<const uint4*>(D + idx)[0];
+    const uint4 b = reinterpret_cast<const uint4*>(D + idx)[1];
+    sg = seg;
+    k1 = ((uint64_t)a.y << 32) | a.x;
+    k2 = ((uint64_t)a.z << 32) | b.x;
+    k3 = (((b.z & TGSIM_F_CLONE) ? 0u : 1u) << 31) | idx;
+  }
+  __device__ __forceinline__ void write(uint32_t pos, uint32_t k3) const {
+    tgsim_record r;
+    load_rec(D + (k3 & 0x7FFFFFFFu), r);
+    o_t[pos] = r.t; o_src[pos] = r.src; o_dst[pos] = r.dst; o_seq[pos] = r.seq; o_size[pos] = r.size;
+    o_flags[pos] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; o_coff[pos] = r.corrupt_off;
+  }
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t, uint32_t s_begin, const uint32_t*) const {
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s_begin + j, s.k3[j]);
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const LargeSeg* large,
+                                                       const uint32_t* chunk_off, const DevScalars* sc,
+                                                       const uint32_t* K3) {
+  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
+  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+    const uint32_t li = chunk_owner(chunk_off, nl, c);
+    const LargeSeg L = large[li];
+    const uint32_t q = c - chunk_off[li];
+    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
+    for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock) p.write(L.start + j, K3[L.start + j]);
+  }
+}
+
+// ============================================================================================
+// (4) sync service
+// ============================================================================================
+
+struct SigPolicy {
+  const uint32_t* inst;
+  const int64_t* t;
+  const uint32_t* count;
+  uint32_t* seq_out;
+  int64_t* log;
+  uint64_t log_base;
+
+  __device__ __forceinline__ void key(uint32_t seg, uint32_t idx, uint32_t& sg, uint64_t& k1, uint64_t& k2,
+                                      uint32_t& k3) const {
+    sg = seg;
+    k1 = (uint64_t)t[idx];
+    k2 = inst[idx];
+    k3 = idx;
+  }
+  __device__ __forceinline__ void write(uint32_t state, uint32_t gpos, uint32_t seg_start, uint64_t k1,
+                                        uint32_t idx) const {
+    seq_out[idx] = count[state] + (gpos - seg_start) + 1u;
+    log[log_base + gpos] = (int64_t)k1;
+  }
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t, uint32_t s_begin, const uint32_t* off) const {
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s.sg[j], s_begin + j, off[s.sg[j]], s.k1[j], s.k3[j]);
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void k_sig_large(SigPolicy p, const LargeSeg* large,
+                                                      const uint32_t* chunk_off, const DevScalars* sc,
+                                                      const uint64_t* K1, const uint32_t* K3) {
+  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
+  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+    const uint32_t li = chunk_owner(chunk_off, nl, c);
+    const LargeSeg L = large[li];
+    const uint32_t q = c - chunk_off[li];
+    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
+    for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock)
+      p.write(L.seg, L.start + j, L.start, K1[L.start + j], K3[L.start + j]);
+  }
+}
+
+// Commit a sorted batch: per present state, check time order, append a log chunk, bump the count.
+__global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint32_t K, uint64_t log_base,
+                                                       const int64_t* log, uint32_t* count, int64_t* last,
+                                                       uint32_t* nchunks, SigChunk* chunks, DevScalars* sc) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+    const uint32_t a = off[k], b = off[k + 1];
+    if (a == b) continue;
+    const int64_t first = log[log_base + a];
+    if (count[k] > 0 && first < last[k]) atomicOr(&sc->err, ERR_SIG_ORDER);
+    const uint32_t c = nchunks[k];
+    if (c >= (uint32_t)kMaxChunksPerState) {
+      atomicOr(&sc->err, ERR_STATE_CHUNKS);
+    } else {
+      SigChunk ch;
+      ch.seq_start = count[k] + 1u; ch.len = b - a; ch.log_pos = log_base + a;
+      chunks[(size_t)k * kMaxChunksPerState + c] = ch;
+      nchunks[k] = c + 1;
+    }
+    count[k] += b - a;
+    last[k] = log[log_base + b - 1];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_waiters(uint32_t nw, const uint32_t* w_state, const uint32_t* w_target,
+                                                    const int64_t* w_twait, int64_t* w_release,
+                                                    const uint32_t* count, const uint32_t* nchunks,
+                                                    const SigChunk* chunks, const int64_t* log) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+    if (w_release[w] >= 0) continue;
+    const uint32_t st = w_state[w], tg = w_target[w];
+    const int64_t tw = w_twait[w];
+    if (tg == 0) { w_release[w] = tw; continue; }
+    if (count[st] < tg) continue;
+    const uint32_t nc = nchunks[st];
+    for (uint32_t c = 0; c < nc; ++c) {
+      const SigChunk ch = chunks[(size_t)st * kMaxChunksPerState + c];
+      if (tg >= ch.seq_start && tg < ch.seq_start + ch.len) {
+        const int64_t t = log[ch.log_pos + (tg - ch.seq_start)];
+        w_release[w] = t > tw ? t : tw;
+        break;
+      }
+    }
+  }
+}
+
+// ============================================================================================
+// exchange (sharded runs)
+// ============================================================================================
+
+__global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const DevScalars* sc) {
+  const uint32_t p = threadIdx.x;
+  if (p >= S) return;
+  tgsim_record h;
+  const uint32_t n = min(sc->q[Q_X0 + p], xcap - 1);
+  h.t = (int64_t)n; h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
+  store_rec(xsend + (size_t)p * xcap, h);
+}
+
+__global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint32_t S, uint32_t shard,
+                                                 uint32_t xcap, Queues Q) {
+  const int64_t t_end = Q.sc->t_end;
+  const uint64_t total = (uint64_t)S * xcap;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint64_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
+    const uint32_t p = (uint32_t)(j / xcap), i = (uint32_t)(j % xcap);
+    int q = -1;
+    tgsim_record rec;
+    if (p != shard && i > 0) {
+      const int64_t n = xrecv[(size_t)p * xcap].t;
+      if (n < 0 || n >= (int64_t)xcap) {
+        if (i == 1) atomicOr(&Q.sc->err, ERR_EXCH_HDR);
+      } else if ((int64_t)i <= n) {
+        load_rec(xrecv + j, rec);
+        q = rec.t < t_end ? Q_D : Q_L;
+      }
+    }
+    Q.push(q, rec);
+  }
+}
+
+__global__ void k_finish(DevScalars* sc, uint32_t cap) {
+  const uint32_t n = min(sc->q[Q_D], cap);
+  sc->n_out = n;
+  sc->st[ST_DELIVERED] += n;
+}
+
+// ============================================================================================
+// workload generator: gossip storm round
+// ============================================================================================
+
+__global__ __launch_bounds__(kBlock) void k_gen_storm(uint32_t lo, uint32_t nloc, uint32_t N, uint32_t round,
+                                                      int64_t t0, uint32_t F, uint32_t size, int64_t spread,
+                                                      uint32_t state, uint32_t key0, uint32_t key1,
+                                                      uint32_t base, uint32_t* m_src, uint32_t* m_dst,
+                                                      uint32_t* m_seq, uint32_t* m_size, int64_t* m_t,
+                                                      uint32_t* s_state, uint32_t* s_inst, int64_t* s_t) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += stride) {
+    const uint32_t g = lo + l;
+    uint32_t chosen[32];
+    int64_t tmax = t0;
+    for (uint32_t k = 0; k < F; ++k) {
+      uint32_t out[4];
+      philox4x32_10(g, round, k << 16, kStormSalt, key0, key1, out);
+      const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
+      const int64_t t = t0 + (spread > 0 ? (int64_t)(u % (uint64_t)spread) : 0);
+      uint32_t p;
+      for (uint32_t attempt = 0;; ++attempt) {
+        if (attempt) philox4x32_10(g, round, (k << 16) | attempt, kStormSalt, key0, key1, out);
+        p = out[0] % (N - 1);
+        if (p >= g) ++p;
+        bool dupl = false;
+#pragma unroll
+        for (uint32_t j = 0; j < 32; ++j) dupl |= (j < k) && chosen[j] == p;
+        if (!dupl) break;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 32; ++j)
+        if (j == k) chosen[j] = p;
+      const uint32_t i = base + l * F + k;
+      m_src[i] = g; m_dst[i] = p; m_seq[i] = round * F + k; m_size[i] = size; m_t[i] = t;
+      if (t > tmax) tmax = t;
+    }
+    s_state[l] = state; s_inst[l] = g; s_t[l] = tmax;
+  }
+}
+
+// ============================================================================================
+// host-side pipeline drivers
+// ============================================================================================
+
+#define TG_CHECK(x)                  \
+  do {                               \
+    hipError_t e__ = (x);            \
+    if (e__ != hipSuccess) return e__; \
+  } while (0)
+
+static inline int bits_for(uint32_t K) { return K <= 1 ? 0 : 32 - __builtin_clz(K - 1); }
+
+hipError_t sync_scalars(Dev& d) {
+  TG_CHECK(hipMemcpyAsync(d.h_sc, d.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, d.stream));
+  return hipStreamSynchronize(d.stream);
+}
+
+hipError_t launch_set_window(Dev& d, int64_t T, int64_t t_end) {
+  hipLaunchKernelGGL(k_set_window, dim3(1), dim3(1), 0, d.stream, d.sc, T, t_end);
+  TG_CHECK(hipGetLastError());
+  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
+  return hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream);
+}
+
+hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t offset_ns) {
+  hipLaunchKernelGGL(k_set_window_barrier, dim3(1), dim3(1), 0, d.stream, d.sc, d.w_release, waiter, T,
+                     offset_ns);
+  TG_CHECK(hipGetLastError());
+  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
+  return hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream);
+}
+
+hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_reset_tb, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, d.X, locals_dev, n);
+  return hipGetLastError();
+}
+
+static inline unsigned grid_for(uint64_t n) {
+  uint64_t g = (n + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > (uint64_t)kStreamBlocks) g = kStreamBlocks;
+  return (unsigned)g;
+}
+
+static Queues make_queues(Dev& d) {
+  Queues Q;
+  Q.sc = d.sc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.cap = d.cap_rec; Q.xcap = d.xcap;
+  return Q;
+}
+
+// Stable group-by of (keys0, vals0)[0..*n_ptr) on keys < K; returns the buffers holding the result.
+static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t** keys, uint32_t** vals) {
+  const int bits = bits_for(K);
+  const int passes = (bits + 7) / 8;
+  uint32_t *ki = d.keys0, *vi = d.vals0, *ko = d.keys1, *vo = d.vals1;
+  for (int p = 0; p < passes; ++p) {
+    hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, 8 * p, d.hist);
+    hipLaunchKernelGGL(k_radix_scan, dim3(1), dim3(1024), 0, d.stream, d.hist);
+    hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
+                       d.cap_rec, 8 * p, d.hist);
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  TG_CHECK(hipGetLastError());
+  *keys = ki;
+  *vals = vi;
+  return hipSuccess;
+}
+
+static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, uint32_t K) {
+  const size_t b = offsetof(DevScalars, n_large), e = offsetof(DevScalars, n_recv);
+  TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
+  hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)K + 1)), dim3(kBlock), 0, d.stream, keys, n_ptr, d.cap_rec,
+                     K, d.seg_off, d.large, d.sc);
+  return hipGetLastError();
+}
+
+// Sort the large segments (if any) into (K1,K2,K3) scratch; returns which buffer holds the result.
+template <class P>
+static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uint32_t* vals, bool* any,
+                             uint64_t** K1, uint64_t** K2, uint32_t** K3) {
+  TG_CHECK(sync_scalars(d));
+  *any = d.h_sc->n_large > 0;
+  if (!*any) return hipSuccess;
+  const uint32_t max_len = d.h_sc->max_large;
+  const uint32_t nl = d.h_sc->n_large;
+  hipLaunchKernelGGL(k_large_prep, dim3(1), dim3(kBlock), 0, d.stream, d.large, d.chunk_off, d.sc);
+  uint64_t chunks_ub = 0;
+  (void)nl;
+  chunks_ub = (uint64_t)d.cap_rec / kChunk + nl + 1;
+  const unsigned g = (unsigned)std::min<uint64_t>(chunks_ub, (uint64_t)kStreamBlocks);
+  hipLaunchKernelGGL((k_large_chunks<P>), dim3(g), dim3(kBlock), 0, d.stream, p, keys, vals, d.large, d.chunk_off,
+                     d.sc, d.K1a, d.K2a, d.K3a);
+  uint64_t *s1 = d.K1a, *s2 = d.K2a, *d1 = d.K1b, *d2 = d.K2b;
+  uint32_t *s3 = d.K3a, *d3 = d.K3b;
+  for (uint64_t W = kChunk; W < max_len; W *= 2) {
+    hipLaunchKernelGGL(k_large_merge, dim3(g), dim3(kBlock), 0, d.stream, d.large, d.chunk_off, d.sc, (uint32_t)W,
+                       s1, s2, s3, d1, d2, d3);
+    std::swap(s1, d1); std::swap(s2, d2); std::swap(s3, d3);
+  }
+  TG_CHECK(hipGetLastError());
+  *K1 = s1; *K2 = s2; *K3 = s3;
+  return hipSuccess;
+}
+
+static hipError_t run_token_bucket(Dev& d) {
+  uint32_t* nA = &d.sc->q[Q_A];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, nA, d.cap_rec, 0, d.lo,
+                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  uint32_t *keys, *vals;
+  TG_CHECK(group_by(d, nA, d.nloc, &keys, &vals));
+  TG_CHECK(bounds(d, keys, nA, d.nloc));
+  TBPolicy p;
+  p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
+  p.sc = d.sc;
+  hipLaunchKernelGGL(k_seg_small<TBPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals, d.seg_off,
+                     nA, d.cap_rec);
+  TG_CHECK(hipGetLastError());
+  bool any;
+  uint64_t *K1, *K2;
+  uint32_t* K3;
+  TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
+  if (any) {
+    hipLaunchKernelGGL(k_tb_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, K1, K3);
+    TG_CHECK(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+hipError_t window_begin(Dev& d, uint32_t n_staged) {
+  Queues Q = make_queues(d);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kBlock), 0, d.stream, d.regions, d.dirs, d.slots, d.slot_ns,
+                     d.plan_start, d.plan_off, d.sc);
+  hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
+                     d.plan_off, d.arena, Q);
+  TG_CHECK(hipGetLastError());
+  if (n_staged) {
+    ShapeArgs a;
+    a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged;
+    a.status = d.status; a.shape = d.shape; a.flags = d.flags; a.ip = d.ip; a.rule_off = d.rule_off;
+    a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
+    a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
+    hipLaunchKernelGGL(k_shape, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, a);
+    TG_CHECK(hipGetLastError());
+  }
+  TG_CHECK(run_token_bucket(d));
+  if (d.S > 1) {
+    hipLaunchKernelGGL(k_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, d.xsend, d.S, d.xcap, d.sc);
+    TG_CHECK(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+static hipError_t run_deliveries(Dev& d) {
+  uint32_t* nD = &d.sc->q[Q_D];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, nD, d.cap_rec, 1, d.lo,
+                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  uint32_t *keys, *vals;
+  TG_CHECK(group_by(d, nD, d.nloc, &keys, &vals));
+  TG_CHECK(bounds(d, keys, nD, d.nloc));
+  TG_CHECK(hipMemcpyAsync(d.inbox, d.seg_off, ((size_t)d.nloc + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          d.stream));
+  EmitPolicy p;
+  p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
+  hipLaunchKernelGGL(k_seg_small<EmitPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                     d.seg_off, nD, d.cap_rec);
+  TG_CHECK(hipGetLastError());
+  bool any;
+  uint64_t *K1, *K2;
+  uint32_t* K3;
+  TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
+  if (any) {
+    hipLaunchKernelGGL(k_emit_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc, K3);
+    TG_CHECK(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+static hipError_t run_wheel_insert(Dev& d) {
+  uint32_t* nL = &d.sc->q[Q_L];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, nL, d.cap_rec, 2, d.lo,
+                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  uint32_t *keys, *vals;
+  TG_CHECK(group_by(d, nL, d.slots, &keys, &vals));
+  hipLaunchKernelGGL(k_region_alloc, dim3(1), dim3(1), 0, d.stream, d.sc, d.regions, d.cap_arena, d.cap_rec,
+                     d.slot_ns);
+  hipLaunchKernelGGL(k_region_fill, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, keys, vals, d.arena, d.dirs,
+                     d.slots, d.cap_rec, d.sc);
+  return hipGetLastError();
+}
+
+hipError_t window_end(Dev& d) {
+  if (d.S > 1) {
+    Queues Q = make_queues(d);
+    const uint64_t total = (uint64_t)d.S * d.xcap;
+    hipLaunchKernelGGL(k_recv, dim3(grid_for(total)), dim3(kBlock), 0, d.stream, d.xrecv, d.S, d.shard, d.xcap, Q);
+    TG_CHECK(hipGetLastError());
+  }
+  TG_CHECK(run_deliveries(d));
+  TG_CHECK(run_wheel_insert(d));
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, d.stream, d.sc, d.cap_rec);
+  return hipGetLastError();
+}
+
+hipError_t signal_batch(Dev& d, uint32_t n, uint64_t log_base, uint32_t n_waiters) {
+  if (n) {
+    hipLaunchKernelGGL(k_keys_sig, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_state, n, d.keys0, d.vals0);
+    // the batch count lives in a device word: reuse the Q_A cursor slot of a scratch scalar block
+    uint32_t* n_dev = &d.sc->sig_n;
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
+    uint32_t *keys, *vals;
+    TG_CHECK(group_by(d, n_dev, d.max_states, &keys, &vals));
+    TG_CHECK(bounds(d, keys, n_dev, d.max_states));
+    SigPolicy p;
+    p.inst = d.s_inst; p.t = d.s_t; p.count = d.st_count; p.seq_out = d.s_seq; p.log = d.sig_log;
+    p.log_base = log_base;
+    hipLaunchKernelGGL(k_seg_small<SigPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                       d.seg_off, n_dev, d.cap_rec);
+    TG_CHECK(hipGetLastError());
+    bool any;
+    uint64_t *K1, *K2;
+    uint32_t* K3;
+    TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
+    if (any) {
+      hipLaunchKernelGGL(k_sig_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc,
+                         K1, K3);
+      TG_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_sig_commit, dim3(grid_for(d.max_states)), dim3(kBlock), 0, d.stream, d.seg_off,
+                       d.max_states, log_base, d.sig_log, d.st_count, d.st_last, d.st_nchunks, d.st_chunks, d.sc);
+    TG_CHECK(hipGetLastError());
+  }
+  return resolve_waiters(d, n_waiters);
+}
+
+hipError_t resolve_waiters(Dev& d, uint32_t n_waiters) {
+  if (!n_waiters) return hipSuccess;
+  hipLaunchKernelGGL(k_waiters, dim3(grid_for(n_waiters)), dim3(kBlock), 0, d.stream, n_waiters, d.w_state,
+                     d.w_target, d.w_twait, d.w_release, d.st_count, d.st_nchunks, d.st_chunks, d.sig_log);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
+                            uint32_t size, int64_t spread_ns, uint32_t state) {
+  hipLaunchKernelGGL(k_gen_storm, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.lo, d.nloc, d.N, round, t0,
+                     fanout, size, spread_ns, state, d.key0, d.key1, staged_base, d.m_src, d.m_dst, d.m_seq,
+                     d.m_size, d.m_t, d.s_state, d.s_inst, d.s_t);
+  return hipGetLastError();
+}
+
+}  // namespace tgsim

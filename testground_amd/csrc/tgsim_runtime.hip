@@ -1,0 +1,788 @@
+// tgsim_runtime.hip — host runtime of libtgsim.so: context, table compilation (LinkShape -> netem/HTB
+// state, LinkRule -> per-sender LPM tables), uploads, and the C ABI declared in include/tgsim.h.
+//
+// The table compilation restates the reference's configuration path:
+//   pkg/sidecar/link.go:143-217 (toMicroseconds, Shape, AddRules), pkg/sidecar/route.go:102-117
+//   (routing policy), pkg/sidecar/docker_network.go:51-148 (apply order), plus the recalled
+//   vishvananda/netlink v1.1.0 and Linux sch_htb/sch_netem conversions marked [EXT] in DESIGN.md.
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tgsim_dev.h"
+
+using namespace tgsim;
+
+#define TGSIM_VERSION_STRING "tgsim-mi355x 0.1.0 (gfx950)"
+
+struct tgsim_ctx {
+  tgsim_config cfg{};
+  Dev d;
+  std::string err;
+  bool own_stream = false;
+  uint32_t N = 0, S = 1, shard = 0, lo = 0, hi = 0, nloc = 0;
+  uint32_t data_net = 0, data_mask = 0, data_len = 0;
+  std::vector<ShapeDev> shape_h;
+  std::vector<uint8_t> flags_h;
+  std::vector<uint32_t> ip_h;
+  std::vector<uint32_t> id_of_h;  // ip - data_net -> instance id
+  std::vector<std::vector<RuleDev>> rules_h;
+  std::vector<uint32_t> tb_reset;
+  bool shape_dirty = true, flags_dirty = true, ip_dirty = true, rules_dirty = true;
+  size_t rules_cap_dev = 0;
+  uint32_t* tb_reset_dev = nullptr;
+  uint32_t tb_reset_cap = 0;
+  int64_t now = 0;
+  uint32_t n_staged = 0, n_status_last = 0;
+  bool in_window = false;
+  bool now_from_device = false;
+  uint64_t sig_log_used = 0;
+  uint32_t n_waiters = 0;
+  std::vector<void*> allocs;
+};
+
+static int fail(tgsim_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+static int hipfail(tgsim_ctx* c, hipError_t e, const char* what) {
+  return fail(c, TGSIM_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIPCK(c, x, what)                          \
+  do {                                             \
+    hipError_t e__ = (x);                          \
+    if (e__ != hipSuccess) return hipfail(c, e__, what); \
+  } while (0)
+
+template <typename T>
+static int dalloc(tgsim_ctx* c, T** p, size_t n) {
+  void* q = nullptr;
+  size_t bytes = n * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess) return fail(c, TGSIM_ENOMEM, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+  c->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return 0;
+}
+
+// ============================== LinkShape -> device shape ====================================
+
+static uint32_t go_u32_of_double(double v) {  // Go uint32(float) on amd64: via int64, low 32 bits
+  if (!(v > -9.2233720368547758e18 && v < 9.2233720368547758e18)) return 0u;
+  return (uint32_t)(uint64_t)(int64_t)v;
+}
+static uint32_t pct2u32(float pct) {  // netlink Percentage2u32 [EXT]
+  if (pct == 100.0f) return 0xFFFFFFFFu;
+  volatile float q = pct / 100.0f;
+  volatile float v = 4294967296.0f * q;
+  return go_u32_of_double((double)v);
+}
+static uint32_t time2tick(uint32_t us) { return (uint32_t)(((uint64_t)us * 125u) >> 3); }  // us * 15.625
+static uint32_t to_us(int64_t ns) {  // link.go:143-151
+  int64_t us = ns / 1000;
+  if (us > (int64_t)0xFFFFFFFFu) us = 0xFFFFFFFFu;
+  return (uint32_t)(uint64_t)us;
+}
+
+static int compile_shape(const tgsim_link_shape& s, ShapeDev& o, std::string* err) {
+  memset(&o, 0, sizeof(o));
+  if (s.corrupt_corr != 0.0f || s.reorder_corr != 0.0f || s.duplicate_corr != 0.0f) {
+    if (err) *err = "correlated netem parameters are not supported";
+    return TGSIM_ENOTSUP;
+  }
+  const uint64_t bw = s.bandwidth_bps == 0 ? UINT64_MAX : s.bandwidth_bps;  // link.go:156-159
+  const uint64_t rate = bw / 8;                                               // netlink NewHtbClass
+  if (rate == 0) {
+    if (err) *err = "invalid htb rate";
+    return TGSIM_EINVAL;
+  }
+  o.limited = s.bandwidth_bps != 0;
+  // psched_ratecfg_precompute [EXT]
+  uint64_t factor = 1000000000ull;
+  uint32_t mult = 1, shift = 0;
+  for (;;) {
+    mult = (uint32_t)(factor / rate);
+    if ((mult & (1u << 31)) || (factor & (1ull << 63))) break;
+    factor <<= 1;
+    ++shift;
+  }
+  o.mult = mult;
+  o.shift = shift;
+  const uint32_t buf_bytes = go_u32_of_double((double)rate / 1e9 + 1600.0);
+  const uint32_t buf_us = go_u32_of_double(1000000.0 * ((double)buf_bytes / (double)rate));
+  o.tau = (int64_t)time2tick(buf_us) << 6;
+  const uint32_t lat_ticks = time2tick(to_us(s.latency_ns));
+  const uint32_t jit_us = to_us(s.jitter_ns);
+  const uint32_t jit_ticks = lat_ticks > 0 ? time2tick(jit_us) : jit_us;  // netlink NewNetem quirk [EXT]
+  o.mu = (int64_t)lat_ticks << 6;
+  o.sigma = (int32_t)(uint32_t)((uint64_t)jit_ticks << 6);
+  o.loss_t = pct2u32(s.loss);
+  o.dup_t = pct2u32(s.duplicate);
+  o.corrupt_t = pct2u32(s.corrupt);
+  o.reorder_t = pct2u32(s.reorder);
+  return TGSIM_OK;
+}
+
+static ShapeDev default_shape() {
+  tgsim_link_shape z;
+  memset(&z, 0, sizeof(z));
+  ShapeDev o;
+  compile_shape(z, o, nullptr);
+  return o;
+}
+
+// ============================== lifecycle ====================================================
+
+extern "C" const char* tgsim_version(void) { return TGSIM_VERSION_STRING; }
+extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
+
+extern "C" void tgsim_destroy(tgsim_ctx* c) {
+  if (!c) return;
+  if (c->d.stream) hipStreamSynchronize(c->d.stream);
+  for (void* p : c->allocs) hipFree(p);
+  if (c->d.h_sc) hipHostFree(c->d.h_sc);
+  if (c->own_stream && c->d.stream) hipStreamDestroy(c->d.stream);
+  delete c;
+}
+
+extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
+  if (!out) return TGSIM_EINVAL;
+  *out = nullptr;
+  if (!cfg || cfg->n_instances == 0 || cfg->n_shards == 0 || cfg->n_shards > (uint32_t)kMaxShards ||
+      cfg->shard_id >= cfg->n_shards || cfg->data_prefix_len < 1 || cfg->data_prefix_len > 30)
+    return TGSIM_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TGSIM_ENODEV;
+  if ((int)cfg->device >= ndev) return TGSIM_ENODEV;
+  if (hipSetDevice((int)cfg->device) != hipSuccess) return TGSIM_ENODEV;
+
+  tgsim_ctx* c = new tgsim_ctx();
+  c->cfg = *cfg;
+  c->N = cfg->n_instances;
+  c->S = cfg->n_shards;
+  c->shard = cfg->shard_id;
+  c->lo = (uint32_t)(((uint64_t)c->shard * c->N) / c->S);
+  c->hi = (uint32_t)(((uint64_t)(c->shard + 1) * c->N) / c->S);
+  c->nloc = c->hi - c->lo;
+  c->data_len = cfg->data_prefix_len;
+  c->data_mask = 0xFFFFFFFFu << (32 - c->data_len);
+  c->data_net = cfg->data_subnet & c->data_mask;
+  const uint64_t space = 1ull << (32 - c->data_len);
+  if ((uint64_t)c->N + 3 > space || (kExternalIp & c->data_mask) == c->data_net) {
+    delete c;
+    return TGSIM_EINVAL;
+  }
+  Dev& d = c->d;
+  d.N = c->N; d.S = c->S; d.shard = c->shard; d.lo = c->lo; d.nloc = c->nloc;
+  d.data_net = c->data_net; d.data_mask = c->data_mask; d.data_len = c->data_len;
+  d.key0 = (uint32_t)cfg->seed; d.key1 = (uint32_t)(cfg->seed >> 32);
+  d.slot_ns = cfg->wheel_slot_ns > 0 ? cfg->wheel_slot_ns : 1000000;
+  d.slots = cfg->wheel_slots ? cfg->wheel_slots : 1024;
+  const uint64_t cap_msgs = cfg->max_msgs_per_window ? cfg->max_msgs_per_window : (1u << 20);
+  const uint64_t cap_rec = cfg->max_records ? cfg->max_records : (1u << 22);
+  if (cap_msgs > 0x7FFFFFFFull || cap_rec > 0x7FFFFFFFull || d.slots < 2 || d.slots > (1u << 20)) {
+    delete c;
+    return TGSIM_EINVAL;
+  }
+  d.cap_msgs = (uint32_t)cap_msgs;
+  d.cap_rec = (uint32_t)cap_rec;
+  d.cap_arena = 2 * cap_rec;
+  d.xcap = c->S > 1 ? (uint32_t)(cfg->exchange_cap ? cfg->exchange_cap : 65536) : 1;
+  d.max_states = cfg->max_states ? cfg->max_states : 4096;
+  d.max_waiters = cfg->max_waiters ? cfg->max_waiters : 65536;
+  d.max_signals = cfg->max_signals ? cfg->max_signals : (1ull << 24);
+  d.s_cap = std::max<uint32_t>(c->nloc, 1u << 16);
+
+  hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { delete c; return TGSIM_EHIP; }
+  c->own_stream = true;
+  if (hipHostMalloc((void**)&d.h_sc, sizeof(DevScalars), hipHostMallocDefault) != hipSuccess) {
+    tgsim_destroy(c);
+    return TGSIM_ENOMEM;
+  }
+  memset(d.h_sc, 0, sizeof(DevScalars));
+
+  const size_t nl1 = (size_t)c->nloc + 1;
+  const size_t segK = std::max<size_t>(std::max<size_t>(c->nloc, d.slots), d.max_states) + 1;
+  int rc = 0;
+  rc |= dalloc(c, &d.sc, 1);
+  rc |= dalloc(c, &d.shape, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.flags, c->N);
+  rc |= dalloc(c, &d.ip, c->N);
+  rc |= dalloc(c, &d.rule_off, nl1);
+  rc |= dalloc(c, &d.rules, 1);
+  rc |= dalloc(c, &d.m_src, d.cap_msgs);
+  rc |= dalloc(c, &d.m_dst, d.cap_msgs);
+  rc |= dalloc(c, &d.m_seq, d.cap_msgs);
+  rc |= dalloc(c, &d.m_size, d.cap_msgs);
+  rc |= dalloc(c, &d.m_t, d.cap_msgs);
+  rc |= dalloc(c, &d.status, d.cap_msgs);
+  rc |= dalloc(c, &d.A, d.cap_rec);
+  rc |= dalloc(c, &d.D, d.cap_rec);
+  rc |= dalloc(c, &d.L, d.cap_rec);
+  rc |= dalloc(c, &d.arena, d.cap_arena);
+  rc |= dalloc(c, &d.xsend, (size_t)c->S * d.xcap);
+  rc |= dalloc(c, &d.xrecv, (size_t)c->S * d.xcap);
+  rc |= dalloc(c, &d.regions, kMaxRegions);
+  rc |= dalloc(c, &d.dirs, (size_t)kMaxRegions * (d.slots + 1));
+  rc |= dalloc(c, &d.plan_start, kMaxRegions + 1);
+  rc |= dalloc(c, &d.plan_off, kMaxRegions + 1);
+  rc |= dalloc(c, &d.keys0, d.cap_rec);
+  rc |= dalloc(c, &d.keys1, d.cap_rec);
+  rc |= dalloc(c, &d.vals0, d.cap_rec);
+  rc |= dalloc(c, &d.vals1, d.cap_rec);
+  rc |= dalloc(c, &d.hist, 256 * kRadixBlocks);
+  rc |= dalloc(c, &d.seg_off, segK);
+  rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
+  rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
+  rc |= dalloc(c, &d.K1a, d.cap_rec);
+  rc |= dalloc(c, &d.K1b, d.cap_rec);
+  rc |= dalloc(c, &d.K2a, d.cap_rec);
+  rc |= dalloc(c, &d.K2b, d.cap_rec);
+  rc |= dalloc(c, &d.K3a, d.cap_rec);
+  rc |= dalloc(c, &d.K3b, d.cap_rec);
+  rc |= dalloc(c, &d.o_t, d.cap_rec);
+  rc |= dalloc(c, &d.o_src, d.cap_rec);
+  rc |= dalloc(c, &d.o_dst, d.cap_rec);
+  rc |= dalloc(c, &d.o_seq, d.cap_rec);
+  rc |= dalloc(c, &d.o_size, d.cap_rec);
+  rc |= dalloc(c, &d.o_flags, d.cap_rec);
+  rc |= dalloc(c, &d.o_coff, d.cap_rec);
+  rc |= dalloc(c, &d.inbox, nl1);
+  rc |= dalloc(c, &d.s_state, d.s_cap);
+  rc |= dalloc(c, &d.s_inst, d.s_cap);
+  rc |= dalloc(c, &d.s_seq, d.s_cap);
+  rc |= dalloc(c, &d.s_t, d.s_cap);
+  rc |= dalloc(c, &d.st_count, d.max_states);
+  rc |= dalloc(c, &d.st_last, d.max_states);
+  rc |= dalloc(c, &d.st_nchunks, d.max_states);
+  rc |= dalloc(c, &d.st_chunks, (size_t)d.max_states * kMaxChunksPerState);
+  rc |= dalloc(c, &d.sig_log, d.max_signals);
+  rc |= dalloc(c, &d.w_state, d.max_waiters);
+  rc |= dalloc(c, &d.w_target, d.max_waiters);
+  rc |= dalloc(c, &d.w_twait, d.max_waiters);
+  rc |= dalloc(c, &d.w_release, d.max_waiters);
+  if (rc) { tgsim_destroy(c); return TGSIM_ENOMEM; }
+  c->rules_cap_dev = 1;
+
+  hipStream_t s = d.stream;
+  bool ok = hipMemsetAsync(d.sc, 0, sizeof(DevScalars), s) == hipSuccess &&
+            hipMemsetAsync(d.st_count, 0, d.max_states * sizeof(uint32_t), s) == hipSuccess &&
+            hipMemsetAsync(d.st_nchunks, 0, d.max_states * sizeof(uint32_t), s) == hipSuccess &&
+            hipMemsetAsync(d.st_last, 0, d.max_states * sizeof(int64_t), s) == hipSuccess &&
+            hipMemsetAsync(d.rule_off, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
+            hipMemsetAsync(d.inbox, 0, nl1 * sizeof(uint32_t), s) == hipSuccess;
+  if (!ok) { tgsim_destroy(c); return TGSIM_EHIP; }
+
+  // initial state = after the sidecar's Config{Network:"default", Enable:true} (sidecar_handler.go:26-29)
+  c->shape_h.assign(c->nloc, default_shape());
+  c->flags_h.assign(c->N, 1u);  // enabled, external routing off (zero RoutingPolicy -> disable)
+  c->ip_h.resize(c->N);
+  c->id_of_h.assign(space, UINT32_MAX);
+  for (uint32_t g = 0; g < c->N; ++g) {
+    c->ip_h[g] = c->data_net + 2u + g;
+    c->id_of_h[2u + g] = g;
+  }
+  c->rules_h.assign(c->nloc, {});
+  std::vector<int64_t> xs(std::max<uint32_t>(c->nloc, 1), kNegInf);
+  if (hipMemcpy(d.X, xs.data(), xs.size() * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
+    tgsim_destroy(c);
+    return TGSIM_EHIP;
+  }
+  *out = c;
+  return TGSIM_OK;
+}
+
+extern "C" const char* tgsim_last_error(const tgsim_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int tgsim_set_stream(tgsim_ctx* c, void* stream) {
+  if (!c) return TGSIM_EINVAL;
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  if (c->own_stream) hipStreamDestroy(c->d.stream);
+  if (stream) {
+    c->d.stream = (hipStream_t)stream;
+    c->own_stream = false;
+  } else {
+    HIPCK(c, hipStreamCreateWithFlags(&c->d.stream, hipStreamNonBlocking), "stream");
+    c->own_stream = true;
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_shard_range(const tgsim_ctx* c, uint32_t* lo, uint32_t* hi) {
+  if (!c) return TGSIM_EINVAL;
+  *lo = c->lo;
+  *hi = c->hi;
+  return TGSIM_OK;
+}
+
+static int check_device_errors(tgsim_ctx* c) {
+  const uint32_t e = c->d.h_sc->err;
+  if (!e) return TGSIM_OK;
+  if (e & (ERR_CAP_A | ERR_CAP_D | ERR_CAP_L | ERR_CAP_X | ERR_ARENA | ERR_REGIONS | ERR_SIG_CAP | ERR_STATE_CHUNKS))
+    return fail(c, TGSIM_ECAPACITY, "device capacity exceeded (err bits 0x%x)", e);
+  if (e & (ERR_CAUSAL | ERR_SIG_ORDER)) return fail(c, TGSIM_ECAUSALITY, "causality violation on device (err 0x%x)", e);
+  if (e & ERR_UNRELEASED) return fail(c, TGSIM_ESTATE, "advance_to_barrier: barrier not released");
+  return fail(c, TGSIM_EINVAL, "device error bits 0x%x", e);
+}
+
+static int sync_and_check(tgsim_ctx* c) {
+  HIPCK(c, sync_scalars(c->d), "sync");
+  if (c->now_from_device && !c->in_window) {
+    c->now = c->d.h_sc->t_end;
+    c->now_from_device = false;
+  }
+  return check_device_errors(c);
+}
+
+extern "C" int tgsim_sync(tgsim_ctx* c) {
+  if (!c) return TGSIM_EINVAL;
+  return sync_and_check(c);
+}
+
+extern "C" int tgsim_get_stats(tgsim_ctx* c, tgsim_stats* o) {
+  if (!c || !o) return TGSIM_EINVAL;
+  int rc = sync_and_check(c);
+  const DevScalars& h = *c->d.h_sc;
+  o->msgs_in = h.st[ST_MSGS]; o->copies = h.st[ST_COPIES]; o->lost = h.st[ST_LOST];
+  o->dropped = h.st[ST_DROPPED]; o->rejected = h.st[ST_REJECTED]; o->unreachable = h.st[ST_UNREACH];
+  o->external = h.st[ST_EXTERNAL]; o->dest_down = h.st[ST_DESTDOWN]; o->local = h.st[ST_LOCAL];
+  o->delivered = h.st[ST_DELIVERED];
+  o->windows = 0;
+  o->inflight = h.arena_used;
+  return rc;
+}
+
+extern "C" int64_t tgsim_now(const tgsim_ctx* c) { return c ? c->now : -1; }
+
+// ============================== network configuration ========================================
+
+static bool is_local(const tgsim_ctx* c, uint32_t g) { return g >= c->lo && g < c->hi; }
+
+extern "C" int tgsim_set_shape(tgsim_ctx* c, uint32_t g, const tgsim_link_shape* s) {
+  if (!c || !s || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
+  ShapeDev o;
+  std::string e;
+  int rc = compile_shape(*s, o, &e);
+  if (rc) return fail(c, rc, "%s", e.c_str());
+  if (is_local(c, g)) {
+    c->shape_h[g - c->lo] = o;
+    c->shape_dirty = true;
+  }
+  return TGSIM_OK;
+}
+
+static bool rule_before(const RuleDev& a, uint32_t prefix, uint32_t plen) {
+  const uint32_t la = a.plen_action & 0xFFu;
+  if (la != plen) return la > plen;
+  return a.prefix < prefix;
+}
+
+// NetlinkLink.AddRules (link.go:187-217)
+extern "C" int tgsim_add_rules(tgsim_ctx* c, uint32_t g, const tgsim_link_rule* rules, size_t n) {
+  if (!c || g >= c->N || (n && !rules)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t plen = rules[i].prefix_len;
+    if (plen > 32) return fail(c, TGSIM_EINVAL, "invalid prefix length %u", plen);
+    const uint32_t mask = plen ? 0xFFFFFFFFu << (32 - plen) : 0u;
+    const uint32_t prefix = rules[i].subnet_ip;
+    const int action = rules[i].shape.filter;
+    if (action != TGSIM_FILTER_ACCEPT && action != TGSIM_FILTER_REJECT && action != TGSIM_FILTER_DROP)
+      return fail(c, TGSIM_EINVAL, "unknown filter action %d", action);
+    if (action != TGSIM_FILTER_ACCEPT && (prefix & ~mask))
+      return fail(c, TGSIM_EINVAL, "invalid prefix for given prefix length");
+    if (!is_local(c, g)) continue;
+    auto& v = c->rules_h[g - c->lo];
+    if (action == TGSIM_FILTER_ACCEPT) {  // RouteDel blackhole + prohibit, errors ignored
+      if (prefix & ~mask) continue;
+      auto it = std::lower_bound(v.begin(), v.end(), 0, [&](const RuleDev& r, int) { return rule_before(r, prefix, plen); });
+      if (it != v.end() && it->prefix == prefix && (it->plen_action & 0xFFu) == plen) {
+        v.erase(it);
+        c->rules_dirty = true;
+      }
+      continue;
+    }
+    auto it = std::lower_bound(v.begin(), v.end(), 0, [&](const RuleDev& r, int) { return rule_before(r, prefix, plen); });
+    const uint32_t pa = plen | ((uint32_t)action << 8);
+    if (it != v.end() && it->prefix == prefix && (it->plen_action & 0xFFu) == plen) it->plen_action = pa;  // RouteReplace
+    else v.insert(it, RuleDev{prefix, pa});
+    c->rules_dirty = true;
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_set_policy(tgsim_ctx* c, uint32_t g, int32_t policy) {  // route.go:102-117
+  if (!c || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
+  const uint8_t f = (uint8_t)((c->flags_h[g] & 1u) | (policy == TGSIM_POLICY_ALLOW_ALL ? 2u : 0u));
+  if (f != c->flags_h[g]) { c->flags_h[g] = f; c->flags_dirty = true; }
+  return TGSIM_OK;
+}
+
+static int set_ip(tgsim_ctx* c, uint32_t g, uint32_t ip) {
+  if ((ip & c->data_mask) != c->data_net) return fail(c, TGSIM_EINVAL, "ip outside the data subnet");
+  const uint32_t off = ip - c->data_net;
+  if (off <= 1 || off == (uint32_t)(c->id_of_h.size() - 1)) return fail(c, TGSIM_EINVAL, "reserved address");
+  if (c->id_of_h[off] != UINT32_MAX && c->id_of_h[off] != g) return fail(c, TGSIM_EINVAL, "address already in use");
+  c->id_of_h[c->ip_h[g] - c->data_net] = UINT32_MAX;
+  c->ip_h[g] = ip;
+  c->id_of_h[off] = g;
+  c->ip_dirty = true;
+  return TGSIM_OK;
+}
+
+// docker_network.go:65-133: disconnect / (re)connect; a new link is a fresh HTB class + netem qdisc.
+extern "C" int tgsim_set_enabled(tgsim_ctx* c, uint32_t g, int32_t enabled, int32_t has_ip, uint32_t ip) {
+  if (!c || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
+  uint8_t& f = c->flags_h[g];
+  if (!enabled) {
+    if (f & 1u) { f &= ~1u; c->flags_dirty = true; }
+    return TGSIM_OK;
+  }
+  if ((f & 1u) && has_ip && ip != c->ip_h[g]) { f &= ~1u; c->flags_dirty = true; }
+  if (!(f & 1u)) {
+    if (has_ip) {
+      int rc = set_ip(c, g, ip);
+      if (rc) return rc;
+    }
+    f |= 1u;
+    c->flags_dirty = true;
+    if (is_local(c, g)) {
+      c->shape_h[g - c->lo] = default_shape();
+      c->shape_dirty = true;
+      c->tb_reset.push_back(g - c->lo);
+    }
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_configure_network(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg) {
+  if (!c || !cfg || g >= c->N) return fail(c, TGSIM_EINVAL, "bad arguments");
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return fail(c, TGSIM_EUNSUPPORTED_NETWORK, "unsupported network: %s", net);
+  int rc = tgsim_set_policy(c, g, cfg->routing_policy);
+  if (rc) return rc;
+  if (!cfg->enable) return tgsim_set_enabled(c, g, 0, 0, 0);
+  rc = tgsim_set_enabled(c, g, 1, cfg->has_ipv4, cfg->ipv4);
+  if (rc) return rc;
+  rc = tgsim_set_shape(c, g, &cfg->default_shape);
+  if (rc) return rc;
+  return tgsim_add_rules(c, g, cfg->rules, cfg->n_rules);
+}
+
+extern "C" int tgsim_get_ip(const tgsim_ctx* c, uint32_t g, uint32_t* ip) {
+  if (!c || !ip || g >= c->N) return TGSIM_EINVAL;
+  *ip = c->ip_h[g];
+  return TGSIM_OK;
+}
+
+static int upload_tables(tgsim_ctx* c) {
+  Dev& d = c->d;
+  bool copied = false;
+  if (c->shape_dirty && c->nloc) {
+    HIPCK(c, hipMemcpyAsync(d.shape, c->shape_h.data(), c->nloc * sizeof(ShapeDev), hipMemcpyHostToDevice, d.stream), "upload shapes");
+    copied = true;
+  }
+  if (c->flags_dirty) {
+    HIPCK(c, hipMemcpyAsync(d.flags, c->flags_h.data(), c->N, hipMemcpyHostToDevice, d.stream), "upload flags");
+    copied = true;
+  }
+  if (c->ip_dirty) {
+    HIPCK(c, hipMemcpyAsync(d.ip, c->ip_h.data(), c->N * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream), "upload ips");
+    copied = true;
+  }
+  std::vector<uint32_t> off;
+  std::vector<RuleDev> flat;
+  if (c->rules_dirty) {
+    off.resize((size_t)c->nloc + 1);
+    size_t total = 0;
+    for (uint32_t i = 0; i < c->nloc; ++i) { off[i] = (uint32_t)total; total += c->rules_h[i].size(); }
+    off[c->nloc] = (uint32_t)total;
+    if (total > 0xFFFFFFF0ull) return fail(c, TGSIM_ECAPACITY, "too many rules");
+    flat.reserve(total);
+    for (uint32_t i = 0; i < c->nloc; ++i) flat.insert(flat.end(), c->rules_h[i].begin(), c->rules_h[i].end());
+    if (total > c->rules_cap_dev) {
+      HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+      auto it = std::find(c->allocs.begin(), c->allocs.end(), (void*)d.rules);
+      if (it != c->allocs.end()) { hipFree(d.rules); c->allocs.erase(it); }
+      size_t cap = std::max<size_t>(total, 2 * c->rules_cap_dev);
+      if (dalloc(c, &d.rules, cap)) return TGSIM_ENOMEM;
+      c->rules_cap_dev = cap;
+    }
+    HIPCK(c, hipMemcpyAsync(d.rule_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream), "upload rules");
+    if (total)
+      HIPCK(c, hipMemcpyAsync(d.rules, flat.data(), total * sizeof(RuleDev), hipMemcpyHostToDevice, d.stream), "upload rules");
+    copied = true;
+  }
+  if (!c->tb_reset.empty()) {
+    const uint32_t n = (uint32_t)c->tb_reset.size();
+    if (n > c->tb_reset_cap) {
+      HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+      if (dalloc(c, &c->tb_reset_dev, n)) return TGSIM_ENOMEM;
+      c->tb_reset_cap = n;
+    }
+    HIPCK(c, hipMemcpyAsync(c->tb_reset_dev, c->tb_reset.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream), "upload resets");
+    HIPCK(c, launch_reset_tb(d, c->tb_reset_dev, n), "reset tb");
+    copied = true;
+  }
+  // host sources are pageable vectors that later calls may modify: wait for the copies
+  if (copied) HIPCK(c, hipStreamSynchronize(d.stream), "sync uploads");
+  c->tb_reset.clear();
+  c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = false;
+  return TGSIM_OK;
+}
+
+// ============================== data path ====================================================
+
+static int validate_msgs(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    if (m->src[i] >= c->N || (m->dst[i] >= c->N && m->dst[i] != TGSIM_DST_EXTERNAL))
+      return fail(c, TGSIM_EINVAL, "message %zu: bad instance id", i);
+    if (!is_local(c, m->src[i])) return fail(c, TGSIM_EINVAL, "message %zu: sender not in this shard", i);
+    if (m->t_send[i] < c->now) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before window start", i);
+    if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "message %zu: size too large", i);
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (!c || !m) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  if ((uint64_t)c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  int rc = validate_msgs(c, m, n);
+  if (rc) return rc;
+  if (!n) return TGSIM_OK;
+  Dev& d = c->d;
+  const size_t o = c->n_staged;
+  HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_dst + o, m->dst, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_seq + o, m->seq, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_size + o, m->size, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_t + o, m->t_send, n * 8, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipStreamSynchronize(d.stream), "enqueue");
+  c->n_staged += (uint32_t)n;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (!c || !m) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
+  if ((uint64_t)c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  if (!n) return TGSIM_OK;
+  Dev& d = c->d;
+  const size_t o = c->n_staged;
+  HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_dst + o, m->dst, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_seq + o, m->seq, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_size + o, m->size, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_t + o, m->t_send, n * 8, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  c->n_staged += (uint32_t)n;
+  return TGSIM_OK;
+}
+
+static int begin_common(tgsim_ctx* c) {
+  int rc = upload_tables(c);
+  if (rc) return rc;
+  HIPCK(c, window_begin(c->d, c->n_staged), "window_begin");
+  c->n_status_last = c->n_staged;
+  c->n_staged = 0;
+  c->in_window = true;
+  // window_begin synchronised once (token-bucket grouping); surface errors seen there
+  return check_device_errors(c);
+}
+
+extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
+  if (!c) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  HIPCK(c, launch_set_window(c->d, c->now, t_end), "set window");
+  return begin_common(c);
+}
+
+extern "C" int tgsim_exchange_buffers(tgsim_ctx* c, void** send, void** recv, size_t* bytes) {
+  if (!c || !send || !recv || !bytes) return TGSIM_EINVAL;
+  *send = c->d.xsend;
+  *recv = c->d.xrecv;
+  *bytes = (size_t)c->S * c->d.xcap * sizeof(tgsim_record);
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_advance_end(tgsim_ctx* c) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
+  HIPCK(c, window_end(c->d), "window_end");
+  c->in_window = false;
+  // window_end synchronised during the delivery sort; h_sc->t_end is this window's end
+  c->now = c->d.h_sc->t_end;
+  c->now_from_device = false;
+  return check_device_errors(c);
+}
+
+extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
+  if (!c) return TGSIM_EINVAL;
+  if (c->S != 1) return fail(c, TGSIM_ESTATE, "tgsim_advance needs a single-shard context; use begin/end");
+  int rc = tgsim_advance_begin(c, t_end);
+  if (rc) return rc;
+  return tgsim_advance_end(c);
+}
+
+extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
+  if (!c) return TGSIM_EINVAL;
+  if (c->S != 1) return fail(c, TGSIM_ESTATE, "single-shard context required");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  HIPCK(c, launch_set_window_barrier(c->d, c->now, waiter, offset_ns), "set window");
+  int rc = begin_common(c);
+  if (rc) return rc;
+  return tgsim_advance_end(c);
+}
+
+extern "C" int tgsim_delivery_count(tgsim_ctx* c, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  int rc = sync_and_check(c);
+  *n = c->d.h_sc->n_out;
+  return rc;
+}
+
+extern "C" int tgsim_copy_deliveries(tgsim_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n) {
+  if (!c || !o || !n) return TGSIM_EINVAL;
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  const size_t k = c->d.h_sc->n_out;
+  *n = k;
+  if (k > cap) return fail(c, TGSIM_ECAPACITY, "output capacity %zu < %zu deliveries", cap, k);
+  if (!k) return TGSIM_OK;
+  Dev& d = c->d;
+  HIPCK(c, hipMemcpy(o->t_deliver, d.o_t, k * 8, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->src, d.o_src, k * 4, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->dst, d.o_dst, k * 4, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->seq, d.o_seq, k * 4, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->size, d.o_size, k * 4, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->flags, d.o_flags, k * 4, hipMemcpyDeviceToHost), "copy");
+  HIPCK(c, hipMemcpy(o->corrupt_off, d.o_coff, k * 4, hipMemcpyDeviceToHost), "copy");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_copy_inbox_offsets(tgsim_ctx* c, uint32_t* out, size_t cap) {
+  if (!c || !out) return TGSIM_EINVAL;
+  if (cap < (size_t)c->nloc + 1) return fail(c, TGSIM_ECAPACITY, "inbox capacity");
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  HIPCK(c, hipMemcpy(out, c->d.inbox, ((size_t)c->nloc + 1) * 4, hipMemcpyDeviceToHost), "copy");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_copy_status(tgsim_ctx* c, uint8_t* out, size_t cap, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  *n = c->n_status_last;
+  if (c->n_status_last > cap) return fail(c, TGSIM_ECAPACITY, "status capacity");
+  if (c->n_status_last) HIPCK(c, hipMemcpy(out, c->d.status, c->n_status_last, hipMemcpyDeviceToHost), "copy");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_deliveries_device(tgsim_ctx* c, tgsim_delivery_soa* o) {
+  if (!c || !o) return TGSIM_EINVAL;
+  Dev& d = c->d;
+  o->t_deliver = d.o_t; o->src = d.o_src; o->dst = d.o_dst; o->seq = d.o_seq; o->size = d.o_size;
+  o->flags = d.o_flags; o->corrupt_off = d.o_coff;
+  return TGSIM_OK;
+}
+
+// ============================== sync service =================================================
+
+extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                                 size_t n, uint32_t* seq_out) {
+  if (!c || (n && (!states || !inst || !t))) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
+  if (n > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch larger than %u", c->d.s_cap);
+  if (c->sig_log_used + n > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
+  for (size_t i = 0; i < n; ++i) {
+    if (states[i] >= c->d.max_states) return fail(c, TGSIM_EINVAL, "state id %u >= max_states", states[i]);
+    if (t[i] < 0) return fail(c, TGSIM_ECAUSALITY, "negative signal time");
+  }
+  Dev& d = c->d;
+  if (n) {
+    HIPCK(c, hipMemcpyAsync(d.s_state, states, n * 4, hipMemcpyHostToDevice, d.stream), "signal");
+    HIPCK(c, hipMemcpyAsync(d.s_inst, inst, n * 4, hipMemcpyHostToDevice, d.stream), "signal");
+    HIPCK(c, hipMemcpyAsync(d.s_t, t, n * 8, hipMemcpyHostToDevice, d.stream), "signal");
+  }
+  const uint64_t base = c->sig_log_used;
+  HIPCK(c, signal_batch(d, (uint32_t)n, base, c->n_waiters), "signal batch");
+  c->sig_log_used += n;
+  if (seq_out && n) HIPCK(c, hipMemcpyAsync(seq_out, d.s_seq, n * 4, hipMemcpyDeviceToHost, d.stream), "seq");
+  return sync_and_check(c);
+}
+
+extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w) {
+  if (!c || !w) return TGSIM_EINVAL;
+  if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "state id %u >= max_states", state);
+  if (c->n_waiters >= c->d.max_waiters) return fail(c, TGSIM_ECAPACITY, "too many barrier waiters");
+  Dev& d = c->d;
+  const uint32_t i = c->n_waiters;
+  const int64_t minus1 = -1;
+  HIPCK(c, hipMemcpy(d.w_state + i, &state, 4, hipMemcpyHostToDevice), "barrier");
+  HIPCK(c, hipMemcpy(d.w_target + i, &target, 4, hipMemcpyHostToDevice), "barrier");
+  HIPCK(c, hipMemcpy(d.w_twait + i, &t_wait, 8, hipMemcpyHostToDevice), "barrier");
+  HIPCK(c, hipMemcpy(d.w_release + i, &minus1, 8, hipMemcpyHostToDevice), "barrier");
+  c->n_waiters++;
+  *w = i;
+  HIPCK(c, resolve_waiters(d, c->n_waiters), "barrier");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_sync_poll(tgsim_ctx* c, uint32_t w, int64_t* rel) {
+  if (!c || !rel) return TGSIM_EINVAL;
+  if (w >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  HIPCK(c, hipMemcpyAsync(rel, c->d.w_release + w, 8, hipMemcpyDeviceToHost, c->d.stream), "poll");
+  return sync_and_check(c);
+}
+
+extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
+  if (!c || !count) return TGSIM_EINVAL;
+  if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
+  HIPCK(c, hipMemcpyAsync(count, c->d.st_count + state, 4, hipMemcpyDeviceToHost, c->d.stream), "count");
+  return sync_and_check(c);
+}
+
+// ============================== workloads ====================================================
+
+extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                     int64_t spread_ns, uint32_t state) {
+  if (!c) return TGSIM_EINVAL;
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "storm generator signals need a single-shard context");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
+  if (size >= 0x80000000u || spread_ns < 0) return fail(c, TGSIM_EINVAL, "bad size/spread");
+  if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  if (t0 < c->now) return fail(c, TGSIM_ECAUSALITY, "t0 before window start");
+  const uint64_t n = (uint64_t)c->nloc * fanout;
+  if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
+  if (c->sig_log_used + c->nloc > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
+  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state), "gen storm");
+  c->n_staged += (uint32_t)n;
+  const uint64_t base = c->sig_log_used;
+  HIPCK(c, signal_batch(c->d, c->nloc, base, c->n_waiters), "storm signals");
+  c->sig_log_used += c->nloc;
+  return TGSIM_OK;
+}

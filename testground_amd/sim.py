@@ -1,0 +1,232 @@
+"""Python handle on one simulator context (one shard of one run).
+
+``Simulator`` drives libtgsim.so (the HIP path). It takes an optional ``binding`` so that test
+infrastructure can drive the CPU oracle through the identical interface; product code never
+passes one.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi as A
+
+DELIVERY_FIELDS = ("t_deliver", "src", "dst", "seq", "size", "flags", "corrupt_off")
+
+
+@dataclass
+class SimConfig:
+    n_instances: int
+    seed: int = 1
+    shard_id: int = 0
+    n_shards: int = 1
+    device: int = 0
+    data_subnet: str = "16.0.0.0"
+    data_prefix_len: int = 16
+    wheel_slot_ns: int = 1_000_000
+    wheel_slots: int = 1024
+    max_msgs_per_window: int = 1 << 20
+    max_records: int = 1 << 22
+    exchange_cap: int = 1 << 16
+    max_states: int = 4096
+    max_waiters: int = 65536
+    max_signals: int = 1 << 24
+
+    def to_c(self) -> A.Config:
+        c = A.Config()
+        c.n_instances = self.n_instances
+        c.shard_id = self.shard_id
+        c.n_shards = self.n_shards
+        c.device = self.device
+        c.seed = self.seed
+        c.data_subnet = ip_to_int(self.data_subnet)
+        c.data_prefix_len = self.data_prefix_len
+        c.wheel_slot_ns = self.wheel_slot_ns
+        c.wheel_slots = self.wheel_slots
+        c.max_msgs_per_window = self.max_msgs_per_window
+        c.max_records = self.max_records
+        c.exchange_cap = self.exchange_cap
+        c.max_states = self.max_states
+        c.max_waiters = self.max_waiters
+        c.max_signals = self.max_signals
+        return c
+
+
+def ip_to_int(ip: str) -> int:
+    a, b, c, d = (int(x) for x in ip.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def int_to_ip(v: int) -> str:
+    return f"{(v >> 24) & 255}.{(v >> 16) & 255}.{(v >> 8) & 255}.{v & 255}"
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Simulator:
+    def __init__(self, cfg: SimConfig, binding: A.Binding | None = None):
+        self.lib = binding or A.hip_library()
+        self.cfg = cfg
+        self._ctx = C.c_void_p()
+        c = cfg.to_c()
+        rc = self.lib.create(C.byref(c), C.byref(self._ctx))
+        if rc != A.OK:
+            raise A.TgsimError(rc, f"{self.lib.name}: create failed")
+        n, s, k = cfg.n_instances, cfg.n_shards, cfg.shard_id
+        self.lo, self.hi = (k * n) // s, ((k + 1) * n) // s
+
+    # ---- plumbing ---------------------------------------------------------------------------
+    def _check(self, rc: int) -> None:
+        if rc != A.OK:
+            msg = self.lib.last_error(self._ctx)
+            raise A.TgsimError(rc, msg.decode() if msg else "")
+
+    def close(self) -> None:
+        if self._ctx:
+            self.lib.destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def now(self) -> int:
+        return int(self.lib.now(self._ctx))
+
+    # ---- network configuration (sidecar.Network) ---------------------------------------------
+    def configure_network(self, instance: int, cfg: A.NetworkConfig) -> None:
+        self._check(self.lib.configure_network(self._ctx, instance, C.byref(cfg)))
+
+    def set_shape(self, instance: int, shape: A.LinkShape) -> None:
+        self._check(self.lib.set_shape(self._ctx, instance, C.byref(shape)))
+
+    def add_rules(self, instance: int, rules: list[A.LinkRule]) -> None:
+        arr = (A.LinkRule * max(1, len(rules)))(*rules)
+        self._check(self.lib.add_rules(self._ctx, instance, arr, len(rules)))
+
+    def set_policy(self, instance: int, policy: int) -> None:
+        self._check(self.lib.set_policy(self._ctx, instance, policy))
+
+    def set_enabled(self, instance: int, enabled: bool, ip: int | None = None) -> None:
+        self._check(self.lib.set_enabled(self._ctx, instance, int(enabled), int(ip is not None), ip or 0))
+
+    def get_ip(self, instance: int) -> int:
+        v = C.c_uint32()
+        self._check(self.lib.get_ip(self._ctx, instance, C.byref(v)))
+        return v.value
+
+    # ---- data path --------------------------------------------------------------------------
+    def enqueue(self, src, dst, seq, size, t_send) -> None:
+        arrs = [np.ascontiguousarray(x, dtype=np.uint32) for x in (src, dst, seq, size)]
+        t = np.ascontiguousarray(t_send, dtype=np.int64)
+        n = len(t)
+        assert all(len(a) == n for a in arrs)
+        m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
+        self._check(self.lib.enqueue(self._ctx, C.byref(m), n))
+
+    def advance(self, t_end: int) -> None:
+        self._check(self.lib.advance(self._ctx, int(t_end)))
+
+    def advance_begin(self, t_end: int) -> None:
+        self._check(self.lib.advance_begin(self._ctx, int(t_end)))
+
+    def advance_end(self) -> None:
+        self._check(self.lib.advance_end(self._ctx))
+
+    def exchange_buffers(self) -> tuple[int, int, int]:
+        s, r, b = C.c_void_p(), C.c_void_p(), C.c_size_t()
+        self._check(self.lib.exchange_buffers(self._ctx, C.byref(s), C.byref(r), C.byref(b)))
+        return s.value, r.value, b.value
+
+    def advance_to_barrier(self, waiter: int, offset_ns: int = 0) -> None:
+        self._check(self.lib.advance_to_barrier(self._ctx, waiter, int(offset_ns)))
+
+    def delivery_count(self) -> int:
+        n = C.c_size_t()
+        self._check(self.lib.delivery_count(self._ctx, C.byref(n)))
+        return n.value
+
+    def deliveries(self) -> dict[str, np.ndarray]:
+        n = self.delivery_count()
+        out = {"t_deliver": np.zeros(n, np.int64)}
+        for f in DELIVERY_FIELDS[1:]:
+            out[f] = np.zeros(n, np.uint32)
+        soa = A.DeliverySoA(*[_ptr(out[f]) if n else None for f in DELIVERY_FIELDS])
+        got = C.c_size_t()
+        self._check(self.lib.copy_deliveries(self._ctx, C.byref(soa), n, C.byref(got)))
+        assert got.value == n
+        return out
+
+    def inbox_offsets(self) -> np.ndarray:
+        out = np.zeros(self.hi - self.lo + 1, np.uint32)
+        self._check(self.lib.copy_inbox_offsets(self._ctx, _ptr(out), len(out)))
+        return out
+
+    def status(self) -> np.ndarray:
+        n = C.c_size_t()
+        buf = np.zeros(1 << 16, np.uint8)
+        rc = self.lib.copy_status(self._ctx, _ptr(buf), len(buf), C.byref(n))
+        if rc == A.ECAPACITY and n.value > len(buf):
+            buf = np.zeros(n.value, np.uint8)
+            rc = self.lib.copy_status(self._ctx, _ptr(buf), len(buf), C.byref(n))
+        self._check(rc)
+        return buf[: n.value].copy()
+
+    def stats(self) -> dict[str, int]:
+        s = A.Stats()
+        self._check(self.lib.get_stats(self._ctx, C.byref(s)))
+        return {name: getattr(s, name) for name, _ in A.Stats._fields_}
+
+    # ---- sync service -----------------------------------------------------------------------
+    def signal(self, states, instances, t, want_seq: bool = True) -> np.ndarray | None:
+        st = np.ascontiguousarray(states, dtype=np.uint32)
+        ins = np.ascontiguousarray(instances, dtype=np.uint32)
+        tt = np.ascontiguousarray(t, dtype=np.int64)
+        n = len(st)
+        seq = np.zeros(max(n, 1), np.uint32) if want_seq else None
+        self._check(self.lib.sync_signal(self._ctx, _ptr(st), _ptr(ins), _ptr(tt), n,
+                                         _ptr(seq) if want_seq else None))
+        return seq[:n] if want_seq else None
+
+    def barrier(self, state: int, target: int, t_wait: int) -> int:
+        w = C.c_uint32()
+        self._check(self.lib.sync_barrier(self._ctx, state, target, int(t_wait), C.byref(w)))
+        return w.value
+
+    def poll(self, waiter: int) -> int:
+        r = C.c_int64()
+        self._check(self.lib.sync_poll(self._ctx, waiter, C.byref(r)))
+        return r.value
+
+    def count(self, state: int) -> int:
+        v = C.c_uint32()
+        self._check(self.lib.sync_count(self._ctx, state, C.byref(v)))
+        return v.value
+
+    # ---- workloads --------------------------------------------------------------------------
+    def gen_storm_round(self, round_: int, t0: int, fanout: int, size: int, spread_ns: int, state: int) -> None:
+        self._check(self.lib.gen_storm_round(self._ctx, round_, int(t0), fanout, size, int(spread_ns), state))
+
+
+def make_shape(latency_ns=0, jitter_ns=0, bandwidth_bps=0, loss=0.0, corrupt=0.0, reorder=0.0, duplicate=0.0,
+               corrupt_corr=0.0, reorder_corr=0.0, duplicate_corr=0.0, filter=0) -> A.LinkShape:
+    return A.LinkShape(int(latency_ns), int(jitter_ns), int(bandwidth_bps), loss, corrupt, corrupt_corr, reorder,
+                       reorder_corr, duplicate, duplicate_corr, filter)
+
+
+def make_rule(subnet: str, filter: int) -> A.LinkRule:
+    ip, plen = subnet.split("/")
+    return A.LinkRule(ip_to_int(ip), int(plen), make_shape(filter=filter))

@@ -1,0 +1,175 @@
+"""Seeded scenario drivers shared by the parity tests: the same calls are made on the HIP simulator
+and on the CPU oracle, and every observable (statuses, deliveries, inbox offsets, stats, sync
+sequence numbers and barrier releases) is collected for bit-exact comparison."""
+from __future__ import annotations
+
+import numpy as np
+
+from testground_amd import _abi as A
+from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape, int_to_ip
+
+MS = 1_000_000
+
+
+def random_shape(rng, *, allow_bw=True):
+    lat = int(rng.choice([0, 1_000, 999_999, 5 * MS, 20 * MS, 100 * MS]))
+    jit = int(rng.choice([0, 0, 3 * MS, 10 * MS, 150 * MS]))
+    bw = int(rng.choice([0, 0, 1 << 20, 10_000_000, 800_000])) if allow_bw else 0
+    loss = float(rng.choice([0, 0, 1.0, 20.0, 100.0]))
+    dup = float(rng.choice([0, 0, 5.0, 50.0]))
+    cor = float(rng.choice([0, 0, 10.0]))
+    reo = float(rng.choice([0, 0, 25.0]))
+    return make_shape(latency_ns=lat, jitter_ns=jit, bandwidth_bps=bw, loss=loss, duplicate=dup,
+                      corrupt=cor, reorder=reo)
+
+
+def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_window: int = 300,
+               window_ns: int = 40 * MS, rules: bool = True, cfg_kw=None):
+    rng = np.random.default_rng(seed)
+    cfg = SimConfig(n_instances=n_inst, seed=1000 + seed, **(cfg_kw or {}))
+    sim = Simulator(cfg, binding=binding)
+    out = []
+    seqc = np.zeros(n_inst, np.int64)
+    for g in range(n_inst):
+        sim.set_shape(g, random_shape(rng))
+        if rng.random() < 0.3:
+            sim.set_policy(g, A.POLICY_ALLOW_ALL)
+    if rules:
+        for g in rng.choice(n_inst, size=n_inst // 3, replace=False):
+            rl = []
+            for _ in range(int(rng.integers(1, 6))):
+                tgt = int(rng.integers(0, n_inst))
+                ip = sim.get_ip(tgt)
+                plen = int(rng.choice([32, 32, 30, 24, 16, 0]))
+                mask = (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF if plen else 0
+                f = int(rng.choice([A.FILTER_DROP, A.FILTER_REJECT, A.FILTER_ACCEPT]))
+                rl.append(make_rule(f"{int_to_ip(ip & mask)}/{plen}", f))
+            sim.add_rules(int(g), rl)
+    t0 = 0
+    for w in range(windows):
+        if w == windows // 2:  # mid-run reconfiguration: shapes, an IP change, a disabled link
+            for g in rng.choice(n_inst, size=4, replace=False):
+                sim.set_shape(int(g), random_shape(rng))
+            g = int(rng.integers(0, n_inst))
+            sim.set_enabled(g, True, ip=sim.get_ip(g) + 1000)
+            sim.set_enabled(int((g + 3) % n_inst), False)
+        n = msgs_per_window
+        src = rng.integers(0, n_inst, n)
+        dst = rng.integers(0, n_inst, n)
+        dst[rng.random(n) < 0.03] = A.DST_EXTERNAL
+        loc = rng.random(n) < 0.02
+        dst[loc] = src[loc]
+        seq = np.zeros(n, np.int64)
+        for i in range(n):
+            seq[i] = seqc[src[i]]
+            seqc[src[i]] += 1
+        size = rng.choice([0, 1, 64, 1024, 4096, 65536], n)
+        t = t0 + np.sort(rng.integers(0, window_ns, n))
+        if rng.random() < 0.5:  # ties in send time
+            t[: n // 4] = t0
+        sim.enqueue(src, dst, seq, size, t)
+        t0 += window_ns
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    # drain
+    for w in range(3):
+        t0 += 10 * window_ns
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    st = sim.stats()
+    st.pop("windows", None)
+    st.pop("inflight", None)
+    out.append(dict(stats=st))
+    sim.close()
+    return out
+
+
+def run_heavy(binding, seed: int):
+    """One sender with a long backlog (token-bucket segment > LDS tile) and one receiver with a large
+    inbox (delivery segment > LDS tile): exercises the merge-path large-segment paths."""
+    rng = np.random.default_rng(seed)
+    n_inst = 64
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed), binding=binding)
+    for g in range(n_inst):
+        sim.set_shape(g, make_shape(latency_ns=10 * MS, jitter_ns=int(rng.choice([0, 5 * MS])),
+                                    bandwidth_bps=int(rng.choice([0, 100_000_000])), duplicate=2.0))
+    out = []
+    t0 = 0
+    for w in range(3):
+        n = 9000
+        src = np.where(rng.random(n) < 0.6, 0, rng.integers(1, n_inst, n))
+        dst = np.where(rng.random(n) < 0.6, 5, rng.integers(0, n_inst, n))
+        dst[dst == src] = (dst[dst == src] + 1) % n_inst
+        seq = np.arange(n) + w * n
+        size = rng.choice([100, 1500], n)
+        t = t0 + np.sort(rng.integers(0, 20 * MS, n))
+        t[:500] = t0
+        sim.enqueue(src, dst, seq, size, t)
+        t0 += 20 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    t0 += 5_000 * MS
+    sim.advance(t0)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats={k: v for k, v in sim.stats().items() if k not in ("windows", "inflight")}))
+    sim.close()
+    return out
+
+
+def run_sync(binding, seed: int):
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=8, seed=seed, max_states=64), binding=binding)
+    res = []
+    waiters = []
+    t = 0
+    for b in range(6):
+        n = int(rng.integers(1, 3000))
+        states = rng.integers(0, 5, n)
+        inst = rng.integers(0, 5000, n)
+        ts = t + rng.integers(0, 1000, n)
+        ts[rng.random(n) < 0.3] = t  # ties -> broken by instance
+        seq = sim.signal(states, inst, ts)
+        res.append(("seq", seq.copy()))
+        for _ in range(3):
+            waiters.append(sim.barrier(int(rng.integers(0, 5)), int(rng.integers(0, 4000)), int(t + rng.integers(0, 2000))))
+        res.append(("rel", [sim.poll(w) for w in waiters]))
+        res.append(("cnt", [sim.count(s) for s in range(6)]))
+        t += 1000
+    sim.close()
+    return res
+
+
+def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4):
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed), binding=binding)
+    rng = np.random.default_rng(seed)
+    for g in range(n_inst):
+        sim.set_shape(g, make_shape(latency_ns=int(rng.integers(20, 101)) * MS, jitter_ns=5 * MS,
+                                    bandwidth_bps=10_000_000, loss=0.5))
+    out = []
+    for r in range(rounds):
+        t0 = sim.now
+        sim.gen_storm_round(r, t0, fanout, 1024, 10 * MS, r)
+        w = sim.barrier(r, n_inst, t0)
+        sim.advance_to_barrier(w, 1 * MS)
+        out.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats={k: v for k, v in sim.stats().items() if k not in ("windows", "inflight")}))
+    sim.close()
+    return out
+
+
+def assert_same(a, b, path="out"):
+    if isinstance(a, dict):
+        assert set(a) == set(b), f"{path}: keys {set(a)} vs {set(b)}"
+        for k in a:
+            assert_same(a[k], b[k], f"{path}.{k}")
+    elif isinstance(a, (list, tuple)):
+        assert len(a) == len(b), f"{path}: len {len(a)} vs {len(b)}"
+        for i, (x, y) in enumerate(zip(a, b)):
+            assert_same(x, y, f"{path}[{i}]")
+    elif isinstance(a, np.ndarray):
+        assert a.shape == b.shape, f"{path}: shape {a.shape} vs {b.shape}"
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0][:10]
+            raise AssertionError(f"{path}: mismatch at {bad}: {a[bad]} vs {b[bad]}")
+    else:
+        assert a == b, f"{path}: {a} vs {b}"
