@@ -14,6 +14,7 @@ struct Dev {
   int64_t slot_ns = 1000000;
   uint32_t slots = 1024;
   uint32_t cap_msgs = 0, cap_rec = 0;
+  uint32_t subcap = 0;            // per sub-queue capacity of the A/D/L batches (kNSub sub-queues)
   uint64_t cap_arena = 0;
   uint32_t xcap = 0;
   DevScalars* sc = nullptr;       // device
@@ -42,7 +43,9 @@ struct Dev {
 
   // sort scratch
   uint32_t *keys0 = nullptr, *keys1 = nullptr, *vals0 = nullptr, *vals1 = nullptr;
-  uint32_t* hist = nullptr;
+  uint32_t* hist = nullptr;       // [kMaxBins * kRadixBlocks]
+  uint32_t* tot = nullptr;        // [kMaxBins]
+  uint32_t* qc = nullptr;         // [3][kNSub][32] append counters (128 B apart)
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;
   uint32_t* chunk_off = nullptr;
@@ -70,6 +73,7 @@ struct Dev {
   uint32_t* w_target = nullptr;
   int64_t* w_twait = nullptr;
   int64_t* w_release = nullptr;
+  int64_t* sig_red = nullptr;     // [4] count-only batch reduction: n, tmin, tmax
 };
 
 // Every function returns hipSuccess or the first HIP error; device-side capacity/ordering problems
@@ -80,7 +84,11 @@ hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)
-hipError_t signal_batch(Dev& d, uint32_t n, uint64_t log_base, uint32_t n_waiters);
+// Signal batch already in d.s_state/s_inst/s_t. States lie in [kmin, kmax]. count_only: the
+// batch has one state and no sequence numbers are materialised.
+hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
+                        bool count_only);
+hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait);
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters);
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
                             uint32_t size, int64_t spread_ns, uint32_t state);

@@ -12,7 +12,11 @@ constexpr int kBlock = 256;              // threads per workgroup (4 wave64)
 constexpr int kTile = 1024;              // small-segment tile: segments <= kTile sorted in LDS
 constexpr int kSpan = 2 * kTile;         // LDS capacity of one small-segment span
 constexpr int kChunk = 2048;             // large-segment chunk (LDS bitonic) and merge tile
-constexpr int kRadixBlocks = 512;        // fixed grid of the radix group-by passes
+constexpr int kRadixBlocks = 256;        // fixed grid of the radix group-by passes (== kBlock)
+constexpr int kMaxDigitBits = 11;        // radix digit width <= 11 bits (2048 bins)
+constexpr int kMaxBins = 1 << kMaxDigitBits;
+constexpr int kNSub = 64;                // append sub-queues per batch (contention sharding)
+constexpr int kRankSortMax = 64;         // segments up to this length are rank-sorted in LDS
 constexpr int kMaxShards = 64;
 constexpr int kMaxRegions = 8192;        // live timing-wheel regions (one per window)
 constexpr int kStreamBlocks = 2048;      // grid of grid-stride streaming kernels
@@ -28,7 +32,7 @@ enum : uint32_t {
   ERR_CAP_A = 1u << 0, ERR_CAP_D = 1u << 1, ERR_CAP_L = 1u << 2, ERR_CAP_X = 1u << 3,
   ERR_ARENA = 1u << 4, ERR_REGIONS = 1u << 5, ERR_CAUSAL = 1u << 6, ERR_SIG_ORDER = 1u << 7,
   ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
-  ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13
+  ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14
 };
 
 // Per-sender egress state derived from network.LinkShape (48 B; gathered by src).
@@ -60,8 +64,10 @@ struct RegionDev {
 enum { Q_A = 0, Q_D = 1, Q_L = 2, Q_X0 = 3 };  // append queues: TB batch, deliveries, wheel, peers
 struct DevScalars {
   int64_t T, t_end;                  // current window
-  // ---- per-window block: zeroed by one memset at window start (kWindowResetBegin..End) ----
-  uint32_t q[Q_X0 + kMaxShards];     // append cursors: A, D, L, exchange per peer
+  // ---- per-window block: zeroed by one memset at window start ----
+  uint32_t q[Q_X0 + kMaxShards];     // exchange cursors per peer (q[Q_X0 + p]); q[0..2] unused
+  uint32_t qpre[3][kNSub + 1];       // A, D, L: prefix over sub-queues (after k_qfinal)
+  uint32_t qn[3];                    // A, D, L: totals (after k_qfinal)
   uint32_t n_extract;                // records extracted from the wheel this window
   uint32_t plan_tail, plan_n;        // region ring range the extraction plan covers
   uint32_t n_large, max_large, n_chunks;
@@ -79,7 +85,12 @@ enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_
        ST_LOCAL, ST_DELIVERED };
 
 struct LargeSeg { uint32_t seg, start, len, pad; };
-struct SigChunk { uint32_t seq_start, len; uint64_t log_pos; };
+struct SigChunk {  // a run of consecutive sequence numbers of one state
+  uint32_t seq_start, len;
+  uint64_t log_pos;          // times in seq order at sig_log[log_pos..] (sorted chunks)
+  int64_t tmin, tmax;
+  uint32_t sorted, pad;
+};
 constexpr int kMaxChunksPerState = 64;
 
 // Sort element of the segmented sorts: order (seg, k1, k2, k3).

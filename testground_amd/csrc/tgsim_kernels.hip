@@ -2,10 +2,10 @@
 //
 //  (1) k_shape        fused route (CIDR LPM over per-sender rule CSR) + netem Philox draws
 //                     (duplicate, loss, corrupt, reorder, jitter) per message -> copy records,
-//                     compacted into per-destination queues with wave64 ballot/prefix appends.
+//                     appended with wave64 ballot/prefix compaction into 64-way sharded queues.
 //  (2) token bucket   copies grouped by sender (stable LSD radix group-by), ordered by
-//                     (netem time, seq, clone-first) with an LDS bitonic sort per sender segment,
-//                     then the HTB GCRA recurrence as a max-plus block scan in LDS.
+//                     (netem time, seq, clone-first) in LDS (rank sort for short segments, bitonic
+//                     otherwise), then the HTB GCRA recurrence as a max-plus block scan in LDS.
 //  (3) deliveries     due copies grouped by receiver, ordered (t, src, seq, clone-first) in LDS,
 //                     written as the inbox SoA; future events go to a timing-wheel region:
 //                     a counting (radix) sort on integer-ns slot, extracted by slot prefix later.
@@ -34,42 +34,62 @@ __device__ __forceinline__ void store_rec(tgsim_record* p, const tgsim_record& r
   q[1] = make_uint4(r.seq, r.size, r.meta, r.corrupt_off);
 }
 
-// Wave64 compaction: every lane with q >= 0 gets a slot in queue q. One atomic per distinct queue
-// per wave (ballot -> leader atomicAdd -> broadcast -> mbcnt rank).
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counters, int q) {
+__device__ __forceinline__ uint32_t wave_uid() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
+
+// Wave64 compaction onto per-lane counters: lanes whose counter pointer is equal share one
+// atomicAdd (ballot -> leader atomic -> broadcast -> mbcnt rank). nullptr = nothing to append.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
   uint32_t pos = 0xFFFFFFFFu;
-  bool pending = q >= 0;
+  bool pending = ctr != nullptr;
+  const uint64_t me = (uint64_t)(uintptr_t)ctr;
   for (;;) {
     const uint64_t m = __ballot(pending);
     if (m == 0) break;
     const int leader = __ffsll((unsigned long long)m) - 1;
-    const int lq = __shfl(q, leader);
-    const bool mine = pending && q == lq;
+    const uint32_t lo = __shfl((uint32_t)me, leader), hi = __shfl((uint32_t)(me >> 32), leader);
+    const uint64_t lp = ((uint64_t)hi << 32) | lo;
+    const bool mine = pending && me == lp;
     const uint64_t mm = __ballot(mine);
     uint32_t base = 0;
-    if ((int)lane_id() == leader) base = atomicAdd(&counters[lq], (uint32_t)__popcll(mm));
+    if ((int)lane_id() == leader) base = atomicAdd(reinterpret_cast<uint32_t*>(lp), (uint32_t)__popcll(mm));
     base = __shfl(base, leader);
     if (mine) { pos = base + mask_rank(mm); pending = false; }
   }
   return pos;
 }
 
+// Batches A (token-bucket input), D (deliveries), L (wheel insert) are split into kNSub
+// sub-queues, each with its own counter on its own 128-B line, so that 10^5-10^6 appends per
+// window do not serialise on one address. X are the per-peer exchange blocks.
 struct Queues {
   DevScalars* sc;
+  uint32_t* qc;
   tgsim_record *A, *D, *L, *X;
-  uint32_t cap, xcap;
-  // Wave-collective: all lanes of the wave must call it (q < 0 = nothing to push).
-  __device__ __forceinline__ void push(int q, const tgsim_record& r) const {
-    const uint32_t pos = wave_append(sc->q, q);
-    if (q < 0) return;
-    tgsim_record* buf;
-    uint32_t c = cap, eb;
-    if (q == Q_A) { buf = A; eb = ERR_CAP_A; }
-    else if (q == Q_D) { buf = D; eb = ERR_CAP_D; }
-    else if (q == Q_L) { buf = L; eb = ERR_CAP_L; }
-    else { buf = X + (size_t)(q - Q_X0) * xcap + 1; c = xcap - 1; eb = ERR_CAP_X; }
-    if (pos < c) store_rec(buf + pos, r);
-    else atomicOr(&sc->err, eb);
+  uint32_t subcap, xcap;
+  // Wave-collective: every lane of the wave calls it; salt must be wave-uniform.
+  __device__ __forceinline__ void push(int q, const tgsim_record& r, uint32_t salt) const {
+    uint32_t* ctr = nullptr;
+    tgsim_record* buf = nullptr;
+    uint32_t cap = 0, eb = 0;
+    if (q >= 0) {
+      if (q < Q_X0) {
+        const uint32_t sub = (salt + wave_uid()) & (kNSub - 1);
+        ctr = qc + (((uint32_t)q * kNSub + sub) << 5);
+        buf = (q == Q_A ? A : (q == Q_D ? D : L)) + (size_t)sub * subcap;
+        cap = subcap;
+        eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
+      } else {
+        ctr = &sc->q[q];
+        buf = X + (size_t)(q - Q_X0) * xcap + 1;
+        cap = xcap - 1;
+        eb = ERR_CAP_X;
+      }
+    }
+    const uint32_t pos = wave_append(ctr);
+    if (q >= 0) {
+      if (pos < cap) store_rec(buf + pos, r);
+      else atomicOr(&sc->err, eb);
+    }
   }
 };
 
@@ -140,6 +160,22 @@ __global__ void k_reset_tb(int64_t* X, const uint32_t* locals, uint32_t n) {
   if (i < n) X[locals[i]] = kNegInf;
 }
 
+// Close a sharded queue for reading: prefix over its sub-queues (one wave).
+__global__ void k_qfinal(DevScalars* sc, const uint32_t* qc, int q, uint32_t subcap) {
+  const uint32_t s = threadIdx.x;  // 64 threads
+  const uint32_t raw = qc[(((uint32_t)q * kNSub) + s) << 5];
+  if (raw > subcap) atomicOr(&sc->err, q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L));
+  const uint32_t c = raw < subcap ? raw : subcap;
+  uint32_t x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)s >= o) x += y;
+  }
+  sc->qpre[q][s] = x - c;
+  if (s == 63) { sc->qpre[q][kNSub] = x; sc->qn[q] = x; }
+}
+
 // ============================================================================================
 // (1) route + netem: one thread per staged message
 // ============================================================================================
@@ -202,12 +238,11 @@ __device__ __forceinline__ int64_t tabledist(int64_t mu, int32_t sigma, uint32_t
   return (int64_t)(rnd % m) + mu - (int64_t)sigma;
 }
 
-// The part of netem_enqueue [EXT] after the duplicate/loss decision, for one copy.
-__device__ __forceinline__ bool netem_copy(const ShapeDev& sh, uint32_t src, uint32_t dst, uint32_t seq,
-                                           uint32_t size, int64_t ts, uint32_t clone, uint32_t k0,
+// The part of netem_enqueue [EXT] after the duplicate/loss decision, for one copy. r0 is the
+// copy's block-0 draw (loss, delay, reorder words).
+__device__ __forceinline__ bool netem_copy(const ShapeDev& sh, const uint32_t r0[4], uint32_t src, uint32_t dst,
+                                           uint32_t seq, uint32_t size, int64_t ts, uint32_t clone, uint32_t k0,
                                            uint32_t k1, tgsim_record& rec) {
-  uint32_t r0[4];
-  philox4x32_10(seq, src, clone, kNetemSalt, k0, k1, r0);
   if (clone && sh.loss_t && sh.loss_t >= r0[1]) return false;
   rec.src = src; rec.dst = dst; rec.seq = seq; rec.size = size;
   rec.meta = clone ? TGSIM_F_CLONE : 0u;
@@ -231,8 +266,8 @@ __device__ __forceinline__ bool netem_copy(const ShapeDev& sh, uint32_t src, uin
   return true;
 }
 
-__device__ __forceinline__ int qid_copy(const ShapeArgs& a, const tgsim_record& r, int64_t t_end) {
-  if (r.meta & TGSIM_F_STAGE_D) return qid_stage_d(a.geo, r.dst, r.t, t_end);
+__device__ __forceinline__ int qid_copy(const Geo& geo, const tgsim_record& r, int64_t t_end) {
+  if (r.meta & TGSIM_F_STAGE_D) return qid_stage_d(geo, r.dst, r.t, t_end);
   return r.t < t_end ? Q_A : Q_L;
 }
 
@@ -241,7 +276,8 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
   const int64_t T = sc->T, t_end = sc->t_end;
   uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+  uint32_t it = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride, ++it) {
     const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
     const int64_t ts = a.t[i];
     tgsim_record r1, r2;
@@ -288,22 +324,24 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
           if (dup && lost) st |= TGSIM_ST_FLAG_DUP_CANCEL;
           if (count == 2) {
             st |= TGSIM_ST_FLAG_DUP;
-            if (netem_copy(sh, src, dst, seq, size, ts, 1u, a.key0, a.key1, r1)) {
-              q1 = qid_copy(a, r1, t_end);
+            uint32_t c0[4];
+            philox4x32_10(seq, src, 1u, kNetemSalt, a.key0, a.key1, c0);
+            if (netem_copy(sh, c0, src, dst, seq, size, ts, 1u, a.key0, a.key1, r1)) {
+              q1 = qid_copy(a.geo, r1, t_end);
               cnt[ST_COPIES]++;
             } else {
               st |= TGSIM_ST_FLAG_CLONE_LOST;
             }
           }
-          netem_copy(sh, src, dst, seq, size, ts, 0u, a.key0, a.key1, r2);
-          q2 = qid_copy(a, r2, t_end);
+          netem_copy(sh, r0, src, dst, seq, size, ts, 0u, a.key0, a.key1, r2);
+          q2 = qid_copy(a.geo, r2, t_end);
           cnt[ST_COPIES]++;
         }
       }
     }
     a.status[i] = st;
-    a.Q.push(q1, r1);
-    a.Q.push(q2, r2);
+    a.Q.push(q1, r1, 2 * it);
+    a.Q.push(q2, r2, 2 * it + 1);
   }
 #pragma unroll
   for (int c = 0; c < 9; ++c) {
@@ -383,7 +421,8 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
   const uint32_t total = sc->n_extract, tail = sc->plan_tail, nl = sc->plan_n;
   const int64_t t_end = sc->t_end;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
+  uint32_t it = 0;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride, ++it) {
     uint32_t lo = 0, hi = nl;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -393,14 +432,13 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
     tgsim_record rec;
     load_rec(arena + r.arena_off + plan_start[lo] + (j - plan_off[lo]), rec);
     const int q = rec.t < t_end ? ((rec.meta & TGSIM_F_STAGE_D) ? Q_D : Q_A) : Q_L;
-    Q.push(q, rec);
+    Q.push(q, rec, it);
   }
 }
 
 // Allocate this window's region in the arena ring (one thread).
-__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, uint32_t cap,
-                               int64_t slot_ns) {
-  const uint32_t n = min(sc->q[Q_L], cap);
+__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, int64_t slot_ns) {
+  const uint32_t n = sc->qn[Q_L];
   if (sc->reg_head - sc->reg_tail >= (uint32_t)kMaxRegions) {
     atomicOr(&sc->err, ERR_REGIONS);
     sc->ins_off = ~0ull;
@@ -435,11 +473,10 @@ __global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_
 
 __global__ __launch_bounds__(kBlock) void k_region_fill(const tgsim_record* L, const uint32_t* keys,
                                                         const uint32_t* vals, tgsim_record* arena,
-                                                        uint32_t* dirs, uint32_t slots, uint32_t cap,
-                                                        const DevScalars* sc) {
+                                                        uint32_t* dirs, uint32_t slots, const DevScalars* sc) {
   const uint64_t off = sc->ins_off;
   if (off == ~0ull) return;
-  const uint32_t n = min(sc->q[Q_L], cap);
+  const uint32_t n = sc->qn[Q_L];
   const uint32_t dir = (sc->reg_head - 1) % kMaxRegions;
   const uint32_t stride = gridDim.x * blockDim.x;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -453,126 +490,163 @@ __global__ __launch_bounds__(kBlock) void k_region_fill(const tgsim_record* L, c
 }
 
 // ============================================================================================
-// stable LSD radix group-by on u32 keys (8-bit digits, wave64 ballot ranking)
+// stable LSD radix group-by on u32 keys: digits of <= 11 bits, per-block histograms, one block
+// per digit to scan its per-block counts, wave64 ballot ranking in the scatter (stable).
 // ============================================================================================
 
 __device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_t& end) {
   uint32_t chunk = (n + kRadixBlocks - 1) / kRadixBlocks;
   chunk = (chunk + kBlock - 1) & ~(uint32_t)(kBlock - 1);
   start = blockIdx.x * chunk;
-  end = min(start + chunk, n);
   if (start > n) start = n;
+  end = min(start + chunk, n);
 }
 
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t* keys, const uint32_t* n_ptr,
-                                                       uint32_t cap, int shift, uint32_t* hist) {
-  __shared__ uint32_t h[256];
+                                                       uint32_t cap, int shift, int db, uint32_t* hist) {
+  __shared__ uint32_t h[kMaxBins];
+  const uint32_t bins = 1u << db, mask = bins - 1;
   const uint32_t n = clamp_n(n_ptr, cap);
   uint32_t start, end;
   radix_range(n, start, end);
-  h[threadIdx.x] = 0;
+  for (uint32_t d = threadIdx.x; d < bins; d += kBlock) h[d] = 0;
   __syncthreads();
-  for (uint32_t i = start + threadIdx.x; i < end; i += kBlock) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+  for (uint32_t i = start + threadIdx.x; i < end; i += kBlock) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
   __syncthreads();
-  hist[threadIdx.x * kRadixBlocks + blockIdx.x] = h[threadIdx.x];
+  for (uint32_t d = threadIdx.x; d < bins; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
 }
 
-// exclusive scan over hist[256 * kRadixBlocks] (digit-major), one block of 1024 threads
-__global__ __launch_bounds__(1024) void k_radix_scan(uint32_t* hist) {
-  constexpr int N = 256 * kRadixBlocks, PER = N / 1024;
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x;
-  uint32_t s = 0;
-  for (int i = 0; i < PER; ++i) s += hist[t * PER + i];
-  part[t] = s;
+// one block per digit: exclusive scan of that digit's per-block counts, digit total to tot[d]
+__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uint32_t* tot) {
+  __shared__ uint32_t ws[kRadixBlocks / 64];
+  const uint32_t d = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t v = hist[d * kRadixBlocks + t];
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
   __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    const uint32_t v = t >= o ? part[t - o] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (int i = 0; i < PER; ++i) {
-    const uint32_t v = hist[t * PER + i];
-    hist[t * PER + i] = run;
-    run += v;
-  }
+  uint32_t pre = 0;
+  for (uint32_t w = 0; w < wave; ++w) pre += ws[w];
+  hist[d * kRadixBlocks + t] = pre + x - v;
+  if (t == kRadixBlocks - 1) tot[d] = pre + x;
 }
 
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* kin, const uint32_t* vin,
                                                           uint32_t* kout, uint32_t* vout,
-                                                          const uint32_t* n_ptr, uint32_t cap, int shift,
-                                                          const uint32_t* hist) {
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t wcnt[4][256];
+                                                          const uint32_t* n_ptr, uint32_t cap, int shift, int db,
+                                                          const uint32_t* hist, const uint32_t* tot) {
+  __shared__ uint32_t base[kMaxBins];
+  __shared__ uint32_t wtag[4][kMaxBins];  // (tile tag << 16) | count of that digit in that wave
+  __shared__ uint32_t part[kBlock];
+  const uint32_t bins = 1u << db, mask = bins - 1;
   const uint32_t n = clamp_n(n_ptr, cap);
   uint32_t start, end;
   radix_range(n, start, end);
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
-  base[tid] = hist[tid * kRadixBlocks + blockIdx.x];
-  for (uint32_t t0 = start; t0 < end; t0 += kBlock) {
+  // digit bases: exclusive scan of the digit totals, plus this block's offset inside the digit
+  const uint32_t per = bins >= kBlock ? bins / kBlock : 1u;
+  const uint32_t d0 = tid * per;
+  uint32_t s = 0;
+  if (d0 < bins)
+    for (uint32_t k = 0; k < per; ++k) s += tot[d0 + k];
+  part[tid] = s;
+  for (uint32_t d = tid; d < bins; d += kBlock) wtag[0][d] = wtag[1][d] = wtag[2][d] = wtag[3][d] = 0;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  if (d0 < bins) {
+    uint32_t run = part[tid] - s;
+    for (uint32_t k = 0; k < per; ++k) {
+      base[d0 + k] = run + hist[(d0 + k) * kRadixBlocks + blockIdx.x];
+      run += tot[d0 + k];
+    }
+  }
+  __syncthreads();
+  uint32_t tag = 1;
+  for (uint32_t t0 = start; t0 < end; t0 += kBlock, ++tag) {
     const uint32_t i = t0 + tid;
     const bool valid = i < end;
     const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
-    const uint32_t d = (k >> shift) & 255u;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
-    __syncthreads();
+    const uint32_t d = (k >> shift) & mask;
     uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < db; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bb = __ballot(valid && bit);
       peers &= bit ? bb : ~bb;
     }
     const uint32_t rank = mask_rank(peers);
-    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+    const uint32_t cnt = (uint32_t)__popcll(peers);
+    if (valid && rank == 0) wtag[wave][d] = (tag << 16) | cnt;
     __syncthreads();
-    const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
-    __syncthreads();
-    wcnt[0][tid] = 0; wcnt[1][tid] = c0; wcnt[2][tid] = c0 + c1; wcnt[3][tid] = c0 + c1 + c2;
-    __syncthreads();
+    bool mylast = false;
+    uint32_t pre = 0;
     if (valid) {
-      const uint32_t pos = base[d] + wcnt[wave][d] + rank;
+      bool later = false;
+#pragma unroll
+      for (uint32_t w = 0; w < 4; ++w) {
+        const uint32_t e = wtag[w][d];
+        const uint32_t c = (e >> 16) == tag ? (e & 0xFFFFu) : 0u;
+        if (w < wave) pre += c;
+        if (w > wave && c) later = true;
+      }
+      const uint32_t pos = base[d] + pre + rank;
       kout[pos] = k;
       vout[pos] = v;
+      mylast = !later && rank + 1 == cnt;
     }
     __syncthreads();
-    base[tid] += c0 + c1 + c2 + c3;
+    if (mylast) base[d] += pre + cnt;
     __syncthreads();
   }
 }
 
-// keys of a record batch: 0 = sender (local), 1 = receiver (local), 2 = wheel slot
-__global__ __launch_bounds__(kBlock) void k_keys_rec(const tgsim_record* batch, const uint32_t* n_ptr,
-                                                     uint32_t cap, int mode, uint32_t lo, int64_t slot_ns,
-                                                     uint32_t slots, const DevScalars* sc, uint32_t* keys,
-                                                     uint32_t* vals) {
-  const uint32_t n = clamp_n(n_ptr, cap);
+// keys of a sharded record batch q (A, D or L); vals = physical index of the record.
+// mode 0 = sender (local id), 1 = receiver (local id), 2 = wheel slot
+__global__ __launch_bounds__(kBlock) void k_keys_rec(const tgsim_record* batch, int q, uint32_t subcap, int mode,
+                                                     uint32_t lo, int64_t slot_ns, uint32_t slots,
+                                                     const DevScalars* sc, uint32_t* keys, uint32_t* vals) {
+  __shared__ uint32_t pre[kNSub + 1];
+  if (threadIdx.x <= kNSub) pre[threadIdx.x] = sc->qpre[q][threadIdx.x];
+  __syncthreads();
+  const uint32_t n = pre[kNSub];
   const int64_t base_slot = sc->t_end / slot_ns;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint4 a = reinterpret_cast<const uint4*>(batch + i)[0];
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    uint32_t a = 0, b = kNSub;
+    while (b - a > 1) {
+      const uint32_t mid = (a + b) >> 1;
+      if (pre[mid] <= j) a = mid; else b = mid;
+    }
+    const uint32_t p = a * subcap + (j - pre[a]);
+    const uint4 r = reinterpret_cast<const uint4*>(batch + p)[0];
     uint32_t k;
-    if (mode == 0) k = a.z - lo;
-    else if (mode == 1) k = a.w - lo;
+    if (mode == 0) k = r.z - lo;
+    else if (mode == 1) k = r.w - lo;
     else {
-      const int64_t t = (int64_t)(((uint64_t)a.y << 32) | a.x);
+      const int64_t t = (int64_t)(((uint64_t)r.y << 32) | r.x);
       int64_t s = t / slot_ns - base_slot;
       s = s < 0 ? 0 : (s > (int64_t)slots - 1 ? (int64_t)slots - 1 : s);
       k = (uint32_t)s;
     }
-    keys[i] = k;
-    vals[i] = i;
+    keys[j] = k;
+    vals[j] = p;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, uint32_t n, uint32_t* keys,
-                                                     uint32_t* vals) {
+__global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, const uint32_t* n_ptr, uint32_t kmin,
+                                                     uint32_t* keys, uint32_t* vals) {
+  const uint32_t n = *n_ptr;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    keys[i] = states[i];
+    keys[i] = states[i] - kmin;
     vals[i] = i;
   }
 }
@@ -602,7 +676,8 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const u
 }
 
 // ============================================================================================
-// segmented sorts: LDS bitonic for small segments, chunk sort + merge path for large ones
+// segmented sorts: LDS rank sort (short segments) / bitonic (up to kTile) per span, and a
+// chunk sort + merge path for segments longer than kTile
 // ============================================================================================
 
 struct SortSmem {
@@ -610,11 +685,17 @@ struct SortSmem {
   uint64_t k2[kSpan];
   uint32_t sg[kSpan];
   uint32_t k3[kSpan];
+  uint32_t perm[kSpan];  // sorted position -> element
   int64_t scA[kBlock];
   int64_t scB[kBlock];
   int64_t carry;
-  uint32_t pad[2];
+  uint32_t maxlen;
+  uint32_t pad;
 };
+
+__device__ __forceinline__ bool el_less(const SortSmem& s, uint32_t a, uint32_t b) {
+  return key_less(s.sg[a], s.k1[a], s.k2[a], s.k3[a], s.sg[b], s.k1[b], s.k2[b], s.k3[b]);
+}
 
 __device__ __forceinline__ void bitonic_lds(SortSmem& s, uint32_t npad) {
   for (uint32_t k = 2; k <= npad; k <<= 1) {
@@ -623,8 +704,7 @@ __device__ __forceinline__ void bitonic_lds(SortSmem& s, uint32_t npad) {
         const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
         const uint32_t l = i + j;
         const bool up = (i & k) == 0;
-        const bool lt = key_less(s.sg[l], s.k1[l], s.k2[l], s.k3[l], s.sg[i], s.k1[i], s.k2[i], s.k3[i]);
-        if (lt == up) {
+        if (el_less(s, l, i) == up) {
           uint32_t ts = s.sg[i]; s.sg[i] = s.sg[l]; s.sg[l] = ts;
           uint64_t t1 = s.k1[i]; s.k1[i] = s.k1[l]; s.k1[l] = t1;
           uint64_t t2 = s.k2[i]; s.k2[i] = s.k2[l]; s.k2[l] = t2;
@@ -638,6 +718,38 @@ __device__ __forceinline__ void bitonic_lds(SortSmem& s, uint32_t npad) {
 
 __device__ __forceinline__ void pad_key(SortSmem& s, uint32_t j) {
   s.sg[j] = 0xFFFFFFFFu; s.k1[j] = ~0ull; s.k2[j] = ~0ull; s.k3[j] = 0xFFFFFFFFu;
+}
+
+// Sort m loaded elements (whole segments, contiguous) and leave perm[] = sorted order.
+// off/s_begin give each element's segment bounds (global positions).
+__device__ __forceinline__ void span_sort(SortSmem& s, uint32_t m, const uint32_t* off, uint32_t s_begin) {
+  if (threadIdx.x == 0) s.maxlen = 0;
+  __syncthreads();
+  uint32_t ml = 0;
+  for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+    const uint32_t g = s.sg[j];
+    const uint32_t len = off[g + 1] - off[g];
+    ml = len > ml ? len : ml;
+  }
+  atomicMax(&s.maxlen, ml);
+  __syncthreads();
+  if (s.maxlen <= (uint32_t)kRankSortMax) {
+    // O(len) rank per element inside its segment; keys are unique (k3 carries the index)
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+      const uint32_t g = s.sg[j];
+      const uint32_t a = off[g] - s_begin, b = off[g + 1] - s_begin;
+      uint32_t r = 0;
+      for (uint32_t i = a; i < b; ++i) r += el_less(s, i, j) ? 1u : 0u;
+      s.perm[a + r] = j;
+    }
+  } else {
+    const uint32_t npad = next_pow2(m);
+    for (uint32_t j = m + threadIdx.x; j < npad; j += kBlock) pad_key(s, j);
+    __syncthreads();
+    bitonic_lds(s, npad);
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) s.perm[j] = j;
+  }
+  __syncthreads();
 }
 
 template <class P>
@@ -656,18 +768,13 @@ __global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys,
     if (off[kl + 1] - off[kl] > (uint32_t)kTile) s_next = off[kl];
     if (s_next <= s_begin) continue;
     const uint32_t m = s_next - s_begin;
-    const uint32_t npad = next_pow2(m);
-    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
-      if (j < m) {
-        const uint32_t i = s_begin + j;
-        p.key(keys[i], vals[i], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-      } else {
-        pad_key(s, j);
-      }
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+      const uint32_t i = s_begin + j;
+      p.key(keys[i], vals[i], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
     }
     __syncthreads();
-    bitonic_lds(s, npad);
-    p.epilogue(s, m, npad, s_begin, off);
+    span_sort(s, m, off, s_begin);
+    p.epilogue(s, m, s_begin, off, w);
     __syncthreads();
   }
 }
@@ -832,33 +939,34 @@ struct TBPolicy {
     const uint4 a = reinterpret_cast<const uint4*>(A + idx)[0];
     const uint4 b = reinterpret_cast<const uint4*>(A + idx)[1];
     sg = seg;
-    k1 = ((uint64_t)a.y << 32) | a.x;                          // netem time_to_send (>= 0)
+    k1 = ((uint64_t)a.y << 32) | a.x;                               // netem time_to_send (>= 0)
     k2 = ((uint64_t)b.x << 1) | ((b.z & TGSIM_F_CLONE) ? 0u : 1u);  // seq, clone first
     k3 = idx;
   }
 
-  // Scan m sorted items in LDS (segments contiguous). has_carry: the first item continues a
-  // segment whose X before it is `carry`. final: the last item ends its segment.
-  __device__ void scan(SortSmem& s, uint32_t m, uint32_t npad, bool has_carry, int64_t carry,
-                       bool final) const {
+  // Scan m sorted items (element perm[j] at sorted position j; segments contiguous).
+  // has_carry: the first item continues a segment whose X before it is `carry`.
+  // final: the last item ends its segment. salt: wave-uniform append salt.
+  __device__ void scan(SortSmem& s, uint32_t m, bool has_carry, int64_t carry, bool final, uint32_t salt) const {
     const int64_t t_end = sc->t_end;
-    const uint32_t IT = npad >= kBlock ? npad / kBlock : 1u;
+    const uint32_t IT = (m + kBlock - 1) / kBlock;
     const uint32_t j0 = threadIdx.x * IT;
     // phase 1: per-thread aggregate
     MP agg = {0, kNegInf};
     for (uint32_t u = 0; u < IT; ++u) {
       const uint32_t j = j0 + u;
       if (j >= m) break;
+      const uint32_t e_ = s.perm[j];
       const uint32_t sl = s.sg[j];
       const ShapeDev& sh = shape[sl];
-      const int64_t e = (int64_t)s.k1[j];
-      const int64_t c = (int64_t)l2t_ns(sh, A[s.k3[j]].size);
+      const int64_t e = (int64_t)s.k1[e_];
+      const int64_t c = (int64_t)l2t_ns(sh, A[s.k3[e_]].size);
       const bool head = (j == 0) ? !has_carry : (s.sg[j - 1] != sl);
       MP f;
       if (head) {
         const int64_t xs = X[sl];
         const int64_t b = xs > e - sh.tau ? xs : e - sh.tau;
-        int64_t v = b + c;
+        const int64_t v = b + c;
         f.A = kNegInf; f.B = v > kTbClamp ? kTbClamp : v;
       } else {
         f.A = c;
@@ -892,10 +1000,11 @@ struct TBPolicy {
       tgsim_record rec;
       int q = -1;
       if (j < m) {
+        const uint32_t e_ = s.perm[j];
         const uint32_t sl = s.sg[j];
         const ShapeDev& sh = shape[sl];
-        const int64_t e = (int64_t)s.k1[j];
-        load_rec(A + s.k3[j], rec);
+        const int64_t e = (int64_t)s.k1[e_];
+        load_rec(A + s.k3[e_], rec);
         const int64_t c = (int64_t)l2t_ns(sh, rec.size);
         const bool head = (j == 0) ? !has_carry : (s.sg[j - 1] != sl);
         int64_t xprev;
@@ -912,26 +1021,26 @@ struct TBPolicy {
           f.B = v > kTbClamp ? kTbClamp : v;
         }
         P = mp_then(P, f);
-        s.k2[j] = (uint64_t)mp_apply(P, kNegInf);  // X after this item (written back below)
+        s.k2[e_] = (uint64_t)mp_apply(P, kNegInf);  // X after this item (written back below)
         if (j + 1 == m) s.carry = mp_apply(P, kNegInf);
         rec.t = e > xprev ? e : xprev;
         rec.meta |= TGSIM_F_STAGE_D;
         q = qid_stage_d(geo, rec.dst, rec.t, t_end);
       }
-      Q.push(q, rec);
+      Q.push(q, rec, salt + u);
     }
     __syncthreads();  // every head has read X before any segment end overwrites it
     for (uint32_t u = 0; u < IT; ++u) {
       const uint32_t j = j0 + u;
       if (j >= m) break;
       const bool last = (j + 1 == m) ? final : (s.sg[j + 1] != s.sg[j]);
-      if (last) X[s.sg[j]] = (int64_t)s.k2[j];
+      if (last) X[s.sg[j]] = (int64_t)s.k2[s.perm[j]];
     }
     __syncthreads();
   }
 
-  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t npad, uint32_t, const uint32_t*) const {
-    scan(s, m, npad, false, 0, true);
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t, const uint32_t*, uint32_t w) const {
+    scan(s, m, false, 0, true, w * 16);
   }
 };
 
@@ -944,14 +1053,14 @@ __global__ __launch_bounds__(kBlock) void k_tb_large(TBPolicy p, const LargeSeg*
     const LargeSeg L = large[li];
     bool has_carry = false;
     int64_t carry = 0;
-    for (uint32_t t0 = 0; t0 < L.len; t0 += kChunk) {
+    uint32_t salt = li * 131;
+    for (uint32_t t0 = 0; t0 < L.len; t0 += kChunk, salt += 16) {
       const uint32_t cnt = min((uint32_t)kChunk, L.len - t0);
-      const uint32_t npad = next_pow2(cnt);
       for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
-        s.sg[j] = L.seg; s.k1[j] = K1[L.start + t0 + j]; s.k3[j] = K3[L.start + t0 + j];
+        s.sg[j] = L.seg; s.k1[j] = K1[L.start + t0 + j]; s.k3[j] = K3[L.start + t0 + j]; s.perm[j] = j;
       }
       __syncthreads();
-      p.scan(s, cnt, npad, has_carry, carry, t0 + cnt == L.len);
+      p.scan(s, cnt, has_carry, carry, t0 + cnt == L.len, salt);
       carry = s.carry;
       has_carry = true;
       __syncthreads();
@@ -984,8 +1093,8 @@ struct EmitPolicy {
     o_t[pos] = r.t; o_src[pos] = r.src; o_dst[pos] = r.dst; o_seq[pos] = r.seq; o_size[pos] = r.size;
     o_flags[pos] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; o_coff[pos] = r.corrupt_off;
   }
-  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t, uint32_t s_begin, const uint32_t*) const {
-    for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s_begin + j, s.k3[j]);
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t s_begin, const uint32_t*, uint32_t) const {
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s_begin + j, s.k3[s.perm[j]]);
   }
 };
 
@@ -1013,6 +1122,7 @@ struct SigPolicy {
   uint32_t* seq_out;
   int64_t* log;
   uint64_t log_base;
+  uint32_t kmin;
 
   __device__ __forceinline__ void key(uint32_t seg, uint32_t idx, uint32_t& sg, uint64_t& k1, uint64_t& k2,
                                       uint32_t& k3) const {
@@ -1021,13 +1131,16 @@ struct SigPolicy {
     k2 = inst[idx];
     k3 = idx;
   }
-  __device__ __forceinline__ void write(uint32_t state, uint32_t gpos, uint32_t seg_start, uint64_t k1,
+  __device__ __forceinline__ void write(uint32_t seg, uint32_t gpos, uint32_t seg_start, uint64_t k1,
                                         uint32_t idx) const {
-    seq_out[idx] = count[state] + (gpos - seg_start) + 1u;
+    seq_out[idx] = count[kmin + seg] + (gpos - seg_start) + 1u;
     log[log_base + gpos] = (int64_t)k1;
   }
-  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t, uint32_t s_begin, const uint32_t* off) const {
-    for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s.sg[j], s_begin + j, off[s.sg[j]], s.k1[j], s.k3[j]);
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t s_begin, const uint32_t* off, uint32_t) const {
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+      const uint32_t e = s.perm[j];
+      write(s.sg[j], s_begin + j, off[s.sg[j]], s.k1[e], s.k3[e]);
+    }
   }
 };
 
@@ -1046,33 +1159,91 @@ __global__ __launch_bounds__(kBlock) void k_sig_large(SigPolicy p, const LargeSe
 }
 
 // Commit a sorted batch: per present state, check time order, append a log chunk, bump the count.
-__global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint32_t K, uint64_t log_base,
-                                                       const int64_t* log, uint32_t* count, int64_t* last,
-                                                       uint32_t* nchunks, SigChunk* chunks, DevScalars* sc) {
+__global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint32_t K, uint32_t kmin,
+                                                       uint64_t log_base, const int64_t* log, uint32_t* count,
+                                                       int64_t* last, uint32_t* nchunks, SigChunk* chunks,
+                                                       DevScalars* sc) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
     const uint32_t a = off[k], b = off[k + 1];
     if (a == b) continue;
+    const uint32_t st = kmin + k;
     const int64_t first = log[log_base + a];
-    if (count[k] > 0 && first < last[k]) atomicOr(&sc->err, ERR_SIG_ORDER);
-    const uint32_t c = nchunks[k];
+    if (count[st] > 0 && first < last[st]) atomicOr(&sc->err, ERR_SIG_ORDER);
+    const uint32_t c = nchunks[st];
     if (c >= (uint32_t)kMaxChunksPerState) {
       atomicOr(&sc->err, ERR_STATE_CHUNKS);
     } else {
       SigChunk ch;
-      ch.seq_start = count[k] + 1u; ch.len = b - a; ch.log_pos = log_base + a;
-      chunks[(size_t)k * kMaxChunksPerState + c] = ch;
-      nchunks[k] = c + 1;
+      ch.seq_start = count[st] + 1u; ch.len = b - a; ch.log_pos = log_base + a;
+      ch.tmin = first; ch.tmax = log[log_base + b - 1]; ch.sorted = 1; ch.pad = 0;
+      chunks[(size_t)st * kMaxChunksPerState + c] = ch;
+      nchunks[st] = c + 1;
     }
-    count[k] += b - a;
-    last[k] = log[log_base + b - 1];
+    count[st] += b - a;
+    last[st] = log[log_base + b - 1];
   }
 }
 
+// Count-only batch (one state, no sequence numbers): min and max time by block reduction.
+__global__ __launch_bounds__(kBlock) void k_sig_reduce(const int64_t* t, const uint32_t* n_ptr, int64_t* red) {
+  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
+  const uint32_t n = *n_ptr;
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t v = t[i];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smin[w] = mn; smax[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
+    if (mn != INT64_MAX) {
+      atomicMin(reinterpret_cast<long long*>(&red[1]), (long long)mn);
+      atomicMax(reinterpret_cast<long long*>(&red[2]), (long long)mx);
+    }
+  }
+}
+
+__global__ void k_sig_commit_count(const uint32_t* n_ptr, uint32_t st, const int64_t* red, uint32_t* count,
+                                   int64_t* last, uint32_t* nchunks, SigChunk* chunks, DevScalars* sc) {
+  const uint32_t n = *n_ptr;
+  if (n == 0) return;
+  if (count[st] > 0 && red[1] < last[st]) atomicOr(&sc->err, ERR_SIG_ORDER);
+  const uint32_t c = nchunks[st];
+  if (c >= (uint32_t)kMaxChunksPerState) {
+    atomicOr(&sc->err, ERR_STATE_CHUNKS);
+  } else {
+    SigChunk ch;
+    ch.seq_start = count[st] + 1u; ch.len = n; ch.log_pos = 0;
+    ch.tmin = red[1]; ch.tmax = red[2]; ch.sorted = 0; ch.pad = 0;
+    chunks[(size_t)st * kMaxChunksPerState + c] = ch;
+    nchunks[st] = c + 1;
+  }
+  count[st] += n;
+  last[st] = red[2];
+}
+
+__global__ void k_add_waiter(uint32_t* w_state, uint32_t* w_target, int64_t* w_twait, int64_t* w_release,
+                             uint32_t i, uint32_t state, uint32_t target, int64_t t_wait) {
+  w_state[i] = state; w_target[i] = target; w_twait[i] = t_wait; w_release[i] = -1;
+}
+
+// A waiter's release time: the time of the target-th signal of its state. For a count-only chunk
+// only its first and last member are known (min / max time); other targets set ERR_UNSORTED_TARGET.
 __global__ __launch_bounds__(kBlock) void k_waiters(uint32_t nw, const uint32_t* w_state, const uint32_t* w_target,
                                                     const int64_t* w_twait, int64_t* w_release,
                                                     const uint32_t* count, const uint32_t* nchunks,
-                                                    const SigChunk* chunks, const int64_t* log) {
+                                                    const SigChunk* chunks, const int64_t* log, DevScalars* sc) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
     if (w_release[w] >= 0) continue;
@@ -1084,7 +1255,11 @@ __global__ __launch_bounds__(kBlock) void k_waiters(uint32_t nw, const uint32_t*
     for (uint32_t c = 0; c < nc; ++c) {
       const SigChunk ch = chunks[(size_t)st * kMaxChunksPerState + c];
       if (tg >= ch.seq_start && tg < ch.seq_start + ch.len) {
-        const int64_t t = log[ch.log_pos + (tg - ch.seq_start)];
+        int64_t t;
+        if (ch.sorted) t = log[ch.log_pos + (tg - ch.seq_start)];
+        else if (tg == ch.seq_start + ch.len - 1) t = ch.tmax;
+        else if (tg == ch.seq_start) t = ch.tmin;
+        else { atomicOr(&sc->err, ERR_UNSORTED_TARGET); break; }
         w_release[w] = t > tw ? t : tw;
         break;
       }
@@ -1110,7 +1285,8 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint
   const int64_t t_end = Q.sc->t_end;
   const uint64_t total = (uint64_t)S * xcap;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint64_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride) {
+  uint32_t it = 0;
+  for (uint64_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride, ++it) {
     const uint32_t p = (uint32_t)(j / xcap), i = (uint32_t)(j % xcap);
     int q = -1;
     tgsim_record rec;
@@ -1123,12 +1299,12 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint
         q = rec.t < t_end ? Q_D : Q_L;
       }
     }
-    Q.push(q, rec);
+    Q.push(q, rec, it);
   }
 }
 
-__global__ void k_finish(DevScalars* sc, uint32_t cap) {
-  const uint32_t n = min(sc->q[Q_D], cap);
+__global__ void k_finish(DevScalars* sc) {
+  const uint32_t n = sc->qn[Q_D];
   sc->n_out = n;
   sc->st[ST_DELIVERED] += n;
 }
@@ -1178,9 +1354,9 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(uint32_t lo, uint32_t nloc
 // host-side pipeline drivers
 // ============================================================================================
 
-#define TG_CHECK(x)                  \
-  do {                               \
-    hipError_t e__ = (x);            \
+#define TG_CHECK(x)                    \
+  do {                                 \
+    hipError_t e__ = (x);              \
     if (e__ != hipSuccess) return e__; \
   } while (0)
 
@@ -1191,19 +1367,23 @@ hipError_t sync_scalars(Dev& d) {
   return hipStreamSynchronize(d.stream);
 }
 
+static hipError_t reset_window(Dev& d) {
+  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
+  TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
+  return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
+}
+
 hipError_t launch_set_window(Dev& d, int64_t T, int64_t t_end) {
   hipLaunchKernelGGL(k_set_window, dim3(1), dim3(1), 0, d.stream, d.sc, T, t_end);
   TG_CHECK(hipGetLastError());
-  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
-  return hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream);
+  return reset_window(d);
 }
 
 hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t offset_ns) {
   hipLaunchKernelGGL(k_set_window_barrier, dim3(1), dim3(1), 0, d.stream, d.sc, d.w_release, waiter, T,
                      offset_ns);
   TG_CHECK(hipGetLastError());
-  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
-  return hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream);
+  return reset_window(d);
 }
 
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n) {
@@ -1221,24 +1401,33 @@ static inline unsigned grid_for(uint64_t n) {
 
 static Queues make_queues(Dev& d) {
   Queues Q;
-  Q.sc = d.sc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.cap = d.cap_rec; Q.xcap = d.xcap;
+  Q.sc = d.sc; Q.qc = d.qc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
   return Q;
+}
+
+static hipError_t qfinal(Dev& d, int q) {
+  hipLaunchKernelGGL(k_qfinal, dim3(1), dim3(64), 0, d.stream, d.sc, d.qc, q, d.subcap);
+  return hipGetLastError();
 }
 
 // Stable group-by of (keys0, vals0)[0..*n_ptr) on keys < K; returns the buffers holding the result.
 static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t** keys, uint32_t** vals) {
   const int bits = bits_for(K);
-  const int passes = (bits + 7) / 8;
   uint32_t *ki = d.keys0, *vi = d.vals0, *ko = d.keys1, *vo = d.vals1;
-  for (int p = 0; p < passes; ++p) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, 8 * p, d.hist);
-    hipLaunchKernelGGL(k_radix_scan, dim3(1), dim3(1024), 0, d.stream, d.hist);
-    hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
-                       d.cap_rec, 8 * p, d.hist);
-    std::swap(ki, ko);
-    std::swap(vi, vo);
+  if (bits > 0) {
+    const int passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
+    const int db = (bits + passes - 1) / passes;
+    for (int p = 0, shift = 0; p < passes; ++p, shift += db) {
+      hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, shift, db,
+                         d.hist);
+      hipLaunchKernelGGL(k_radix_rows, dim3(1u << db), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+      hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
+                         d.cap_rec, shift, db, d.hist, d.tot);
+      std::swap(ki, ko);
+      std::swap(vi, vo);
+    }
+    TG_CHECK(hipGetLastError());
   }
-  TG_CHECK(hipGetLastError());
   *keys = ki;
   *vals = vi;
   return hipSuccess;
@@ -1262,9 +1451,7 @@ static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uin
   const uint32_t max_len = d.h_sc->max_large;
   const uint32_t nl = d.h_sc->n_large;
   hipLaunchKernelGGL(k_large_prep, dim3(1), dim3(kBlock), 0, d.stream, d.large, d.chunk_off, d.sc);
-  uint64_t chunks_ub = 0;
-  (void)nl;
-  chunks_ub = (uint64_t)d.cap_rec / kChunk + nl + 1;
+  const uint64_t chunks_ub = (uint64_t)d.cap_rec / kChunk + nl + 1;
   const unsigned g = (unsigned)std::min<uint64_t>(chunks_ub, (uint64_t)kStreamBlocks);
   hipLaunchKernelGGL((k_large_chunks<P>), dim3(g), dim3(kBlock), 0, d.stream, p, keys, vals, d.large, d.chunk_off,
                      d.sc, d.K1a, d.K2a, d.K3a);
@@ -1281,8 +1468,9 @@ static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uin
 }
 
 static hipError_t run_token_bucket(Dev& d) {
-  uint32_t* nA = &d.sc->q[Q_A];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, nA, d.cap_rec, 0, d.lo,
+  TG_CHECK(qfinal(d, Q_A));
+  uint32_t* nA = &d.sc->qn[Q_A];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, (int)Q_A, d.subcap, 0, d.lo,
                      d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nA, d.nloc, &keys, &vals));
@@ -1329,8 +1517,9 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
 }
 
 static hipError_t run_deliveries(Dev& d) {
-  uint32_t* nD = &d.sc->q[Q_D];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, nD, d.cap_rec, 1, d.lo,
+  TG_CHECK(qfinal(d, Q_D));
+  uint32_t* nD = &d.sc->qn[Q_D];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, (int)Q_D, d.subcap, 1, d.lo,
                      d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nD, d.nloc, &keys, &vals));
@@ -1355,15 +1544,15 @@ static hipError_t run_deliveries(Dev& d) {
 }
 
 static hipError_t run_wheel_insert(Dev& d) {
-  uint32_t* nL = &d.sc->q[Q_L];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, nL, d.cap_rec, 2, d.lo,
+  TG_CHECK(qfinal(d, Q_L));
+  uint32_t* nL = &d.sc->qn[Q_L];
+  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, (int)Q_L, d.subcap, 2, d.lo,
                      d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nL, d.slots, &keys, &vals));
-  hipLaunchKernelGGL(k_region_alloc, dim3(1), dim3(1), 0, d.stream, d.sc, d.regions, d.cap_arena, d.cap_rec,
-                     d.slot_ns);
+  hipLaunchKernelGGL(k_region_alloc, dim3(1), dim3(1), 0, d.stream, d.sc, d.regions, d.cap_arena, d.slot_ns);
   hipLaunchKernelGGL(k_region_fill, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, keys, vals, d.arena, d.dirs,
-                     d.slots, d.cap_rec, d.sc);
+                     d.slots, d.sc);
   return hipGetLastError();
 }
 
@@ -1376,45 +1565,65 @@ hipError_t window_end(Dev& d) {
   }
   TG_CHECK(run_deliveries(d));
   TG_CHECK(run_wheel_insert(d));
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, d.stream, d.sc, d.cap_rec);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, d.stream, d.sc);
   return hipGetLastError();
 }
 
-hipError_t signal_batch(Dev& d, uint32_t n, uint64_t log_base, uint32_t n_waiters) {
+__global__ void k_sig_red_init(int64_t* red) {
+  red[0] = 0; red[1] = INT64_MAX; red[2] = INT64_MIN; red[3] = 0;
+}
+
+hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
+                        bool count_only) {
   if (n) {
-    hipLaunchKernelGGL(k_keys_sig, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_state, n, d.keys0, d.vals0);
-    // the batch count lives in a device word: reuse the Q_A cursor slot of a scratch scalar block
     uint32_t* n_dev = &d.sc->sig_n;
     hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
-    uint32_t *keys, *vals;
-    TG_CHECK(group_by(d, n_dev, d.max_states, &keys, &vals));
-    TG_CHECK(bounds(d, keys, n_dev, d.max_states));
-    SigPolicy p;
-    p.inst = d.s_inst; p.t = d.s_t; p.count = d.st_count; p.seq_out = d.s_seq; p.log = d.sig_log;
-    p.log_base = log_base;
-    hipLaunchKernelGGL(k_seg_small<SigPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
-                       d.seg_off, n_dev, d.cap_rec);
-    TG_CHECK(hipGetLastError());
-    bool any;
-    uint64_t *K1, *K2;
-    uint32_t* K3;
-    TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
-    if (any) {
-      hipLaunchKernelGGL(k_sig_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc,
-                         K1, K3);
+    if (count_only) {
+      hipLaunchKernelGGL(k_sig_red_init, dim3(1), dim3(1), 0, d.stream, d.sig_red);
+      hipLaunchKernelGGL(k_sig_reduce, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_t, n_dev, d.sig_red);
+      hipLaunchKernelGGL(k_sig_commit_count, dim3(1), dim3(1), 0, d.stream, n_dev, kmin, d.sig_red, d.st_count,
+                         d.st_last, d.st_nchunks, d.st_chunks, d.sc);
+      TG_CHECK(hipGetLastError());
+    } else {
+      const uint32_t K = kmax - kmin + 1;
+      hipLaunchKernelGGL(k_keys_sig, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_state, n_dev, kmin, d.keys0,
+                         d.vals0);
+      uint32_t *keys, *vals;
+      TG_CHECK(group_by(d, n_dev, K, &keys, &vals));
+      TG_CHECK(bounds(d, keys, n_dev, K));
+      SigPolicy p;
+      p.inst = d.s_inst; p.t = d.s_t; p.count = d.st_count; p.seq_out = d.s_seq; p.log = d.sig_log;
+      p.log_base = log_base; p.kmin = kmin;
+      hipLaunchKernelGGL(k_seg_small<SigPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                         d.seg_off, n_dev, d.cap_rec);
+      TG_CHECK(hipGetLastError());
+      bool any;
+      uint64_t *K1, *K2;
+      uint32_t* K3;
+      TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
+      if (any) {
+        hipLaunchKernelGGL(k_sig_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc,
+                           K1, K3);
+        TG_CHECK(hipGetLastError());
+      }
+      hipLaunchKernelGGL(k_sig_commit, dim3(grid_for(K)), dim3(kBlock), 0, d.stream, d.seg_off, K, kmin, log_base,
+                         d.sig_log, d.st_count, d.st_last, d.st_nchunks, d.st_chunks, d.sc);
       TG_CHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_sig_commit, dim3(grid_for(d.max_states)), dim3(kBlock), 0, d.stream, d.seg_off,
-                       d.max_states, log_base, d.sig_log, d.st_count, d.st_last, d.st_nchunks, d.st_chunks, d.sc);
-    TG_CHECK(hipGetLastError());
   }
   return resolve_waiters(d, n_waiters);
+}
+
+hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait) {
+  hipLaunchKernelGGL(k_add_waiter, dim3(1), dim3(1), 0, d.stream, d.w_state, d.w_target, d.w_twait, d.w_release, idx,
+                     state, target, t_wait);
+  return hipGetLastError();
 }
 
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters) {
   if (!n_waiters) return hipSuccess;
   hipLaunchKernelGGL(k_waiters, dim3(grid_for(n_waiters)), dim3(kBlock), 0, d.stream, n_waiters, d.w_state,
-                     d.w_target, d.w_twait, d.w_release, d.st_count, d.st_nchunks, d.st_chunks, d.sig_log);
+                     d.w_target, d.w_twait, d.w_release, d.st_count, d.st_nchunks, d.st_chunks, d.sig_log, d.sc);
   return hipGetLastError();
 }
 

@@ -152,10 +152,10 @@ extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
 
 extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (!c) return;
-  if (c->d.stream) hipStreamSynchronize(c->d.stream);
-  for (void* p : c->allocs) hipFree(p);
-  if (c->d.h_sc) hipHostFree(c->d.h_sc);
-  if (c->own_stream && c->d.stream) hipStreamDestroy(c->d.stream);
+  if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->d.h_sc) (void)hipHostFree(c->d.h_sc);
+  if (c->own_stream && c->d.stream) (void)hipStreamDestroy(c->d.stream);
   delete c;
 }
 
@@ -200,6 +200,8 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   }
   d.cap_msgs = (uint32_t)cap_msgs;
   d.cap_rec = (uint32_t)cap_rec;
+  d.subcap = (uint32_t)(cap_rec / kNSub + 4096);  // per sub-queue, with headroom for imbalance
+  const size_t phys_rec = (size_t)kNSub * d.subcap;
   d.cap_arena = 2 * cap_rec;
   d.xcap = c->S > 1 ? (uint32_t)(cfg->exchange_cap ? cfg->exchange_cap : 65536) : 1;
   d.max_states = cfg->max_states ? cfg->max_states : 4096;
@@ -232,9 +234,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.m_size, d.cap_msgs);
   rc |= dalloc(c, &d.m_t, d.cap_msgs);
   rc |= dalloc(c, &d.status, d.cap_msgs);
-  rc |= dalloc(c, &d.A, d.cap_rec);
-  rc |= dalloc(c, &d.D, d.cap_rec);
-  rc |= dalloc(c, &d.L, d.cap_rec);
+  rc |= dalloc(c, &d.A, phys_rec);
+  rc |= dalloc(c, &d.D, phys_rec);
+  rc |= dalloc(c, &d.L, phys_rec);
   rc |= dalloc(c, &d.arena, d.cap_arena);
   rc |= dalloc(c, &d.xsend, (size_t)c->S * d.xcap);
   rc |= dalloc(c, &d.xrecv, (size_t)c->S * d.xcap);
@@ -246,7 +248,10 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.keys1, d.cap_rec);
   rc |= dalloc(c, &d.vals0, d.cap_rec);
   rc |= dalloc(c, &d.vals1, d.cap_rec);
-  rc |= dalloc(c, &d.hist, 256 * kRadixBlocks);
+  rc |= dalloc(c, &d.hist, (size_t)kMaxBins * kRadixBlocks);
+  rc |= dalloc(c, &d.tot, kMaxBins);
+  rc |= dalloc(c, &d.qc, (size_t)3 * kNSub * 32);
+  rc |= dalloc(c, &d.sig_red, 4);
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
   rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
@@ -313,7 +318,7 @@ extern "C" const char* tgsim_last_error(const tgsim_ctx* c) { return c ? c->err.
 extern "C" int tgsim_set_stream(tgsim_ctx* c, void* stream) {
   if (!c) return TGSIM_EINVAL;
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
-  if (c->own_stream) hipStreamDestroy(c->d.stream);
+  if (c->own_stream) (void)hipStreamDestroy(c->d.stream);
   if (stream) {
     c->d.stream = (hipStream_t)stream;
     c->own_stream = false;
@@ -337,6 +342,8 @@ static int check_device_errors(tgsim_ctx* c) {
   if (e & (ERR_CAP_A | ERR_CAP_D | ERR_CAP_L | ERR_CAP_X | ERR_ARENA | ERR_REGIONS | ERR_SIG_CAP | ERR_STATE_CHUNKS))
     return fail(c, TGSIM_ECAPACITY, "device capacity exceeded (err bits 0x%x)", e);
   if (e & (ERR_CAUSAL | ERR_SIG_ORDER)) return fail(c, TGSIM_ECAUSALITY, "causality violation on device (err 0x%x)", e);
+  if (e & ERR_UNSORTED_TARGET)
+    return fail(c, TGSIM_ENOTSUP, "barrier target falls inside a count-only signal batch (only its first/last member is known)");
   if (e & ERR_UNRELEASED) return fail(c, TGSIM_ESTATE, "advance_to_barrier: barrier not released");
   return fail(c, TGSIM_EINVAL, "device error bits 0x%x", e);
 }
@@ -518,7 +525,7 @@ static int upload_tables(tgsim_ctx* c) {
     if (total > c->rules_cap_dev) {
       HIPCK(c, hipStreamSynchronize(d.stream), "sync");
       auto it = std::find(c->allocs.begin(), c->allocs.end(), (void*)d.rules);
-      if (it != c->allocs.end()) { hipFree(d.rules); c->allocs.erase(it); }
+      if (it != c->allocs.end()) { (void)hipFree(d.rules); c->allocs.erase(it); }
       size_t cap = std::max<size_t>(total, 2 * c->rules_cap_dev);
       if (dalloc(c, &d.rules, cap)) return TGSIM_ENOMEM;
       c->rules_cap_dev = cap;
@@ -720,13 +727,15 @@ extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uin
     if (t[i] < 0) return fail(c, TGSIM_ECAUSALITY, "negative signal time");
   }
   Dev& d = c->d;
+  uint32_t kmin = UINT32_MAX, kmax = 0;
+  for (size_t i = 0; i < n; ++i) { kmin = std::min(kmin, states[i]); kmax = std::max(kmax, states[i]); }
   if (n) {
     HIPCK(c, hipMemcpyAsync(d.s_state, states, n * 4, hipMemcpyHostToDevice, d.stream), "signal");
     HIPCK(c, hipMemcpyAsync(d.s_inst, inst, n * 4, hipMemcpyHostToDevice, d.stream), "signal");
     HIPCK(c, hipMemcpyAsync(d.s_t, t, n * 8, hipMemcpyHostToDevice, d.stream), "signal");
   }
   const uint64_t base = c->sig_log_used;
-  HIPCK(c, signal_batch(d, (uint32_t)n, base, c->n_waiters), "signal batch");
+  HIPCK(c, signal_batch(d, (uint32_t)n, n ? kmin : 0, n ? kmax : 0, base, c->n_waiters, false), "signal batch");
   c->sig_log_used += n;
   if (seq_out && n) HIPCK(c, hipMemcpyAsync(seq_out, d.s_seq, n * 4, hipMemcpyDeviceToHost, d.stream), "seq");
   return sync_and_check(c);
@@ -738,11 +747,7 @@ extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target,
   if (c->n_waiters >= c->d.max_waiters) return fail(c, TGSIM_ECAPACITY, "too many barrier waiters");
   Dev& d = c->d;
   const uint32_t i = c->n_waiters;
-  const int64_t minus1 = -1;
-  HIPCK(c, hipMemcpy(d.w_state + i, &state, 4, hipMemcpyHostToDevice), "barrier");
-  HIPCK(c, hipMemcpy(d.w_target + i, &target, 4, hipMemcpyHostToDevice), "barrier");
-  HIPCK(c, hipMemcpy(d.w_twait + i, &t_wait, 8, hipMemcpyHostToDevice), "barrier");
-  HIPCK(c, hipMemcpy(d.w_release + i, &minus1, 8, hipMemcpyHostToDevice), "barrier");
+  HIPCK(c, add_waiter(d, i, state, target, t_wait), "barrier");
   c->n_waiters++;
   *w = i;
   HIPCK(c, resolve_waiters(d, c->n_waiters), "barrier");
@@ -778,11 +783,10 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
-  if (c->sig_log_used + c->nloc > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
   HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state), "gen storm");
   c->n_staged += (uint32_t)n;
-  const uint64_t base = c->sig_log_used;
-  HIPCK(c, signal_batch(c->d, c->nloc, base, c->n_waiters), "storm signals");
-  c->sig_log_used += c->nloc;
+  // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
+  // batch is committed count-only (count, first/last time), DESIGN.md 2.7.
+  HIPCK(c, signal_batch(c->d, c->nloc, state, state, c->sig_log_used, c->n_waiters, true), "storm signals");
   return TGSIM_OK;
 }
