@@ -167,6 +167,9 @@ typedef struct tgsim_delivery_soa {
 typedef struct tgsim_stats {
   uint64_t msgs_in, copies, lost, dropped, rejected, unreachable, external, dest_down, local;
   uint64_t delivered, windows, inflight;
+  uint64_t tb_items;   /* copies that went through the token bucket */
+  uint64_t extracted;  /* records read back from the timing wheel */
+  uint64_t inserted;   /* records written into the timing wheel */
 } tgsim_stats;
 
 typedef struct tgsim_ctx tgsim_ctx;
@@ -196,6 +199,7 @@ int64_t tgsim_now(const tgsim_ctx* ctx); /* current window start (host view) */
 int tgsim_configure_network(tgsim_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg);
 /* Lower-level pieces of the same call. */
 int tgsim_set_shape(tgsim_ctx* ctx, uint32_t instance, const tgsim_link_shape* shape); /* Shape, link.go:155 */
+int tgsim_set_shapes(tgsim_ctx* ctx, const uint32_t* instances, const tgsim_link_shape* shapes, size_t n);
 int tgsim_add_rules(tgsim_ctx* ctx, uint32_t instance, const tgsim_link_rule* rules, size_t n); /* AddRules, link.go:187 */
 int tgsim_set_policy(tgsim_ctx* ctx, uint32_t instance, int32_t policy); /* handleRoutingPolicy, route.go:102 */
 int tgsim_set_enabled(tgsim_ctx* ctx, uint32_t instance, int32_t enabled, int32_t has_ip, uint32_t ip);
@@ -216,6 +220,11 @@ int tgsim_advance_to_barrier(tgsim_ctx* ctx, uint32_t waiter, int64_t offset_ns)
  * header whose .t holds the record count) on the same stream -> end (receiver side). */
 int tgsim_advance_begin(tgsim_ctx* ctx, int64_t t_end);
 int tgsim_exchange_buffers(tgsim_ctx* ctx, void** send_device, void** recv_device, size_t* bytes);
+/* Use caller-owned device buffers (e.g. tensors a collective library reads/writes in place) for the
+ * exchange; each must hold n_shards * exchange_cap records (tgsim_exchange_buffers' size). */
+int tgsim_set_exchange_buffers(tgsim_ctx* ctx, void* send_device, void* recv_device, size_t bytes);
+/* advance_begin with t_end = *t_end_device + offset read on the device (e.g. after an all-reduce). */
+int tgsim_advance_begin_device(tgsim_ctx* ctx, const int64_t* t_end_device, int64_t offset_ns);
 int tgsim_advance_end(tgsim_ctx* ctx);
 /* Results of the last window. Copying forces a stream sync. */
 int tgsim_delivery_count(tgsim_ctx* ctx, size_t* n);
@@ -238,12 +247,24 @@ int tgsim_sync_barrier(tgsim_ctx* ctx, uint32_t state, uint32_t target, int64_t 
 int tgsim_sync_poll(tgsim_ctx* ctx, uint32_t waiter, int64_t* release_out);
 int tgsim_sync_count(tgsim_ctx* ctx, uint32_t state, uint32_t* count_out);
 
+/* ---- profiling: HIP-event timing of kernel classes on the ctx stream ---------------------------- */
+/* mask: bit k enables timing of kernel class k (0..tgsim_kernel_classes()-1); 0 disables. */
+int tgsim_profile_set(tgsim_ctx* ctx, uint32_t mask);
+/* Cumulative milliseconds and launch counts per kernel class (forces a sync). */
+int tgsim_profile_read(tgsim_ctx* ctx, double* ms, uint64_t* launches, size_t cap, size_t* n);
+int tgsim_kernel_classes(void);
+const char* tgsim_kernel_name(int kernel_class);
+
 /* ---- synthetic workloads (device generators) --------------------------------------- */
 /* Gossip storm round (config 4): every instance of this shard sends `fanout` messages of `size`
  * bytes to Philox-chosen distinct peers at t0 + U[0, spread_ns), seq = round*fanout + k, and signals
  * `state` at its last send time. Staged for the next window; the signal batch is kept on the device. */
 int tgsim_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout,
                           uint32_t size, int64_t spread_ns, uint32_t state);
+/* Sharded runs: the storm round's signals are not committed by the generator; this writes the
+ * shard's latest signal time of the last generated round (int64) to device memory, where a MAX
+ * all-reduce across shards yields the release time of SignalAndWait(state, n_instances). */
+int tgsim_storm_release_device(tgsim_ctx* ctx, int64_t* out_device);
 
 #ifdef __cplusplus
 }

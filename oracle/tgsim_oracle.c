@@ -196,6 +196,7 @@ struct tgo_ctx {
   otimes* sig;        /* per state: signal times in seq order */
   size_t n_states;
   owaiter* waiters; size_t n_waiters, waiters_cap;
+  int64_t storm_release;
   char err[512];
 };
 
@@ -330,6 +331,14 @@ int tgo_set_shape(tgo_ctx* c, uint32_t g, const tgsim_link_shape* s) {
   int rc = derive_shape(s, &o, c->err, sizeof(c->err));
   if (rc) return rc;
   if (is_local(c, g)) c->shape[g - c->lo] = o;
+  return TGSIM_OK;
+}
+
+int tgo_set_shapes(tgo_ctx* c, const uint32_t* inst, const tgsim_link_shape* shapes, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    int rc = tgo_set_shape(c, inst[i], &shapes[i]);
+    if (rc) return rc;
+  }
   return TGSIM_OK;
 }
 
@@ -723,7 +732,7 @@ int tgo_copy_status(tgo_ctx* c, uint8_t* out, size_t cap, size_t* n) {
   return 0;
 }
 
-int tgo_get_stats(tgo_ctx* c, tgsim_stats* out) { *out = c->stats; out->inflight = c->heap.n; return 0; }
+int tgo_get_stats(tgo_ctx* c, tgsim_stats* out) { *out = c->stats; out->inflight = c->heap.n; return 0; }  /* tb_items/extracted/inserted stay 0: structure-specific */
 
 /* ============================== sync service ================================================ */
 /* sdk-go sync.Client [EXT]: SignalEntry increments the state's counter and returns the new value
@@ -814,8 +823,7 @@ int tgo_advance_to_barrier(tgo_ctx* c, uint32_t w, int64_t offset) {
  * plans/benchmarks/benchmarks.go:122-141 around a storm round, plans/benchmarks/storm.go:150-197). */
 int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                         int64_t spread_ns, uint32_t state) {
-  if (fanout == 0 || fanout >= c->N || fanout > 64) return fail(c, TGSIM_EINVAL, "bad fanout");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "storm generator signals need a single-shard context");
+  if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
   size_t n = (size_t)c->nloc * fanout;
   uint32_t* src = (uint32_t*)malloc(n * 4); uint32_t* dst = (uint32_t*)malloc(n * 4);
   uint32_t* seq = (uint32_t*)malloc(n * 4); uint32_t* sz = (uint32_t*)malloc(n * 4);
@@ -852,8 +860,19 @@ int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout,
   }
   tgsim_msg_soa m = {src, dst, seq, sz, ts};
   rc = tgo_enqueue(c, &m, n);
-  if (!rc) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
+  if (!rc && c->S == 1) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
+  if (!rc && c->S > 1) { /* sharded: the caller MAX-reduces the local release across shards */
+    int64_t mx = INT64_MIN;
+    for (uint32_t l = 0; l < c->nloc; ++l) mx = stt[l] > mx ? stt[l] : mx;
+    c->storm_release = mx;
+  }
 out:
   free(src); free(dst); free(seq); free(sz); free(ts); free(sst); free(sin); free(stt);
   return rc;
+}
+
+int tgo_storm_release(tgo_ctx* c, int64_t* out) {
+  if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
+  *out = c->storm_release;
+  return TGSIM_OK;
 }

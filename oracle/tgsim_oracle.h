@@ -46,6 +46,7 @@ const char* tgo_last_error(const tgo_ctx* ctx);
 int64_t tgo_now(const tgo_ctx* ctx);
 int tgo_configure_network(tgo_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg);
 int tgo_set_shape(tgo_ctx* ctx, uint32_t instance, const tgsim_link_shape* shape);
+int tgo_set_shapes(tgo_ctx* ctx, const uint32_t* instances, const tgsim_link_shape* shapes, size_t n);
 int tgo_add_rules(tgo_ctx* ctx, uint32_t instance, const tgsim_link_rule* rules, size_t n);
 int tgo_set_policy(tgo_ctx* ctx, uint32_t instance, int32_t policy);
 int tgo_set_enabled(tgo_ctx* ctx, uint32_t instance, int32_t enabled, int32_t has_ip, uint32_t ip);
@@ -72,6 +73,7 @@ int tgo_advance_to_barrier(tgo_ctx* ctx, uint32_t waiter, int64_t offset_ns);
 
 int tgo_gen_storm_round(tgo_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                         int64_t spread_ns, uint32_t state);
+int tgo_storm_release(tgo_ctx* ctx, int64_t* out); /* host-side twin of tgsim_storm_release_device */
 
 #ifdef __cplusplus
 }

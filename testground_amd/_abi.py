@@ -76,7 +76,7 @@ class DeliverySoA(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("msgs_in", "copies", "lost", "dropped", "rejected", "unreachable",
                                           "external", "dest_down", "local", "delivered", "windows",
-                                          "inflight")]
+                                          "inflight", "tb_items", "extracted", "inserted")]
 
 
 RECORD_DTYPE_FIELDS = [("t", "<i8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("size", "<u4"),
@@ -90,6 +90,7 @@ _SIGS = {
     "now": (C.c_int64, [P]),
     "configure_network": (C.c_int, [P, C.c_uint32, C.POINTER(NetworkConfig)]),
     "set_shape": (C.c_int, [P, C.c_uint32, C.POINTER(LinkShape)]),
+    "set_shapes": (C.c_int, [P, C.c_void_p, C.POINTER(LinkShape), C.c_size_t]),
     "add_rules": (C.c_int, [P, C.c_uint32, C.POINTER(LinkRule), C.c_size_t]),
     "set_policy": (C.c_int, [P, C.c_uint32, C.c_int32]),
     "set_enabled": (C.c_int, [P, C.c_uint32, C.c_int32, C.c_int32, C.c_uint32]),
@@ -120,6 +121,13 @@ _SIGS_HIP = {
     "sync": (C.c_int, [P]),
     "enqueue_device": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
     "deliveries_device": (C.c_int, [P, C.POINTER(DeliverySoA)]),
+    "profile_set": (C.c_int, [P, C.c_uint32]),
+    "profile_read": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "kernel_classes": (C.c_int, []),
+    "kernel_name": (C.c_char_p, [C.c_int]),
+    "set_exchange_buffers": (C.c_int, [P, P, P, C.c_size_t]),
+    "advance_begin_device": (C.c_int, [P, P, C.c_int64]),
+    "storm_release_device": (C.c_int, [P, P]),
 }
 
 

@@ -2,11 +2,30 @@
 // implemented in tgsim_kernels.hip. The host runtime (tgsim_runtime.hip) owns allocation, table
 // uploads and the C ABI; everything here is plain pointers.
 #pragma once
+#include <vector>
+
 #include "tgsim_internal.h"
 
 namespace tgsim {
 
+// Kernel classes timed with HIP events on the ctx stream when profiling is on (tgsim_profile_*).
+enum KernelId : int {
+  KID_SHAPE = 0, KID_EXTRACT, KID_TB, KID_EMIT, KID_RADIX_HIST, KID_RADIX_ROWS, KID_RADIX_SCATTER,
+  KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_COUNT
+};
+extern const char* const kKernelNames[KID_COUNT];
+
+struct Prof {
+  uint32_t mask = 0;  // bit per KernelId
+  std::vector<hipEvent_t> pool;
+  struct P { int kid; hipEvent_t a, b; };
+  std::vector<P> pending;
+  double ms[KID_COUNT] = {};
+  unsigned long long n[KID_COUNT] = {};
+};
+
 struct Dev {
+  Prof prof;
   hipStream_t stream = nullptr;
   uint32_t N = 0, S = 1, shard = 0, lo = 0, nloc = 0;
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
@@ -74,13 +93,16 @@ struct Dev {
   int64_t* w_twait = nullptr;
   int64_t* w_release = nullptr;
   int64_t* sig_red = nullptr;     // [4] count-only batch reduction: n, tmin, tmax
+  unsigned long long* stats = nullptr;  // [kNSub][16] sharded k_shape counters (ST_MSGS..ST_LOCAL)
 };
 
 // Every function returns hipSuccess or the first HIP error; device-side capacity/ordering problems
 // are reported through DevScalars::err and surfaced by the host at the next sync.
 hipError_t launch_set_window(Dev& d, int64_t T, int64_t t_end);
 hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t offset_ns);
+hipError_t launch_set_window_dev(Dev& d, int64_t T, const int64_t* t_end_dev, int64_t offset_ns);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
+hipError_t storm_local_release(Dev& d, uint32_t n);  // max signal time of the staged storm batch -> sig_red[2]
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)

@@ -79,10 +79,10 @@ struct DevScalars {
   uint64_t arena_head, arena_tail, arena_used, ins_off;  // arena ring (records)
   uint64_t sig_log_used;             // signal log entries used
   // cumulative statistics (tgsim_stats)
-  unsigned long long st[10];
+  unsigned long long st[13];
 };
 enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_EXTERNAL, ST_DESTDOWN,
-       ST_LOCAL, ST_DELIVERED };
+       ST_LOCAL, ST_DELIVERED, ST_TB_ITEMS, ST_EXTRACTED, ST_INSERTED };
 
 struct LargeSeg { uint32_t seg, start, len, pad; };
 struct SigChunk {  // a run of consecutive sequence numbers of one state

@@ -18,6 +18,52 @@
 
 namespace tgsim {
 
+const char* const kKernelNames[KID_COUNT] = {
+    "k_shape", "k_extract", "token_bucket", "deliveries", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
+    "k_keys", "k_bounds", "k_region_fill", "k_gen_storm", "sync_signal", "large_segments"};
+
+// Times the launches issued while it is alive with a HIP event pair on d.stream (if enabled).
+struct ProfScope {
+  Dev& d;
+  int kid;
+  hipEvent_t a = nullptr;
+  ProfScope(Dev& dd, int k) : d(dd), kid(k) {
+    if (!(d.prof.mask & (1u << kid))) return;
+    a = take();
+    (void)hipEventRecord(a, d.stream);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = take();
+    (void)hipEventRecord(b, d.stream);
+    d.prof.pending.push_back({kid, a, b});
+  }
+  hipEvent_t take() {
+    if (!d.prof.pool.empty()) {
+      hipEvent_t e = d.prof.pool.back();
+      d.prof.pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+    return e;
+  }
+};
+
+// after a stream synchronisation: fold completed event pairs into the per-kernel totals
+static void prof_resolve(Dev& d) {
+  for (auto& p : d.prof.pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      d.prof.ms[p.kid] += ms;
+      d.prof.n[p.kid] += 1;
+    }
+    d.prof.pool.push_back(p.a);
+    d.prof.pool.push_back(p.b);
+  }
+  d.prof.pending.clear();
+}
+
 // ============================================================================================
 // small device helpers
 // ============================================================================================
@@ -51,7 +97,9 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
     const bool mine = pending && me == lp;
     const uint64_t mm = __ballot(mine);
     uint32_t base = 0;
-    if ((int)lane_id() == leader) base = atomicAdd(reinterpret_cast<uint32_t*>(lp), (uint32_t)__popcll(mm));
+    if ((int)lane_id() == leader)
+      base = __hip_atomic_fetch_add(reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(lp),
+                                    (uint32_t)__popcll(mm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = __shfl(base, leader);
     if (mine) { pos = base + mask_rank(mm); pending = false; }
   }
@@ -73,7 +121,9 @@ struct Queues {
     uint32_t cap = 0, eb = 0;
     if (q >= 0) {
       if (q < Q_X0) {
-        const uint32_t sub = (salt + wave_uid()) & (kNSub - 1);
+        // sub-queue: blocks b and b+8 share an XCD under round-robin dispatch, so counters
+        // 8x..8x+7 are only touched from one XCD's L2 (a speed choice; any mapping is correct)
+        const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
         ctr = qc + (((uint32_t)q * kNSub + sub) << 5);
         buf = (q == Q_A ? A : (q == Q_D ? D : L)) + (size_t)sub * subcap;
         cap = subcap;
@@ -153,6 +203,12 @@ __global__ void k_set_window_barrier(DevScalars* sc, const int64_t* w_release, u
   }
 }
 
+__global__ void k_set_window_dev(DevScalars* sc, int64_t T, const int64_t* t_end_dev, int64_t offset) {
+  const int64_t e = *t_end_dev + offset;
+  sc->T = T;
+  sc->t_end = e < T ? T : e;
+}
+
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
 __global__ void k_reset_tb(int64_t* X, const uint32_t* locals, uint32_t n) {
@@ -195,16 +251,14 @@ struct ShapeArgs {
   uint32_t lo, nloc, data_net, data_mask, data_len, key0, key1;
   Geo geo;
   Queues Q;
+  unsigned long long* stats;  // [kNSub][16] sharded counters
 };
 
 // Longest-prefix match over the sender's routing table: rule groups by prefix
 // length (descending), each a sorted run searched by bisection; the data network's connected
 // route and the control network's default route compete at their own prefix lengths.
-__device__ int route_lookup(const ShapeArgs& a, uint32_t sl, uint32_t g, uint32_t dip) {
-  const uint8_t f = a.flags[g];
+__device__ int route_lookup(const ShapeArgs& a, uint8_t f, uint32_t pos, uint32_t end, uint32_t dip) {
   const bool data_ok = (f & 1u) && ((dip & a.data_mask) == a.data_net);
-  uint32_t pos = a.rule_off[sl];
-  const uint32_t end = a.rule_off[sl + 1];
   while (pos < end) {
     const uint32_t plen = a.rules[pos].plen_action & 0xFFu;
     if (data_ok && a.data_len > plen) return R_DATA;
@@ -278,14 +332,28 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
   const uint32_t stride = gridDim.x * blockDim.x;
   uint32_t it = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride, ++it) {
+    // Every load of this message is issued up front with clamped indices, so the wave pays one
+    // round trip for the SoA record and one for the table gathers instead of a branch-serialised chain.
     const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
     const int64_t ts = a.t[i];
+    asm volatile("" ::"v"(src), "v"(dst), "v"(seq), "v"(size), "v"((uint32_t)ts), "v"((uint32_t)((uint64_t)ts >> 32)));  // stage 1: SoA record
+    const uint32_t sl = src - a.lo;
+    const bool src_ok = sl < a.nloc;
+    const uint32_t slc = src_ok ? sl : 0u;
+    const uint32_t dstc = dst < a.geo.N ? dst : 0u;
+    const uint8_t fsrc = a.flags[src_ok ? src : a.lo];
+    const uint8_t fdst = a.flags[dstc];
+    const uint32_t dip = a.ip[dstc];
+    const uint32_t r_lo = a.rule_off[slc], r_hi = a.rule_off[slc + 1];
+    const ShapeDev sh = a.shape[slc];
+    asm volatile("" ::"v"((uint32_t)fsrc), "v"((uint32_t)fdst), "v"(dip), "v"(r_lo), "v"(r_hi),
+                 "v"((uint32_t)sh.mu), "v"((uint32_t)sh.tau), "v"(sh.sigma), "v"(sh.loss_t), "v"(sh.dup_t),
+                 "v"(sh.corrupt_t), "v"(sh.reorder_t), "v"(sh.mult), "v"(sh.limited));  // stage 2: gathers
     tgsim_record r1, r2;
     int q1 = -1, q2 = -1;
     uint8_t st;
     cnt[ST_MSGS]++;
-    const uint32_t sl = src - a.lo;
-    if (sl >= a.nloc || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
+    if (!src_ok || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
       atomicOr(&sc->err, ERR_BAD_MSG);
       st = TGSIM_ST_UNREACHABLE;
       cnt[ST_UNREACH]++;
@@ -301,14 +369,13 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
       cnt[ST_LOCAL]++;
     } else {
       const bool ext = dst == TGSIM_DST_EXTERNAL;
-      const int rt = route_lookup(a, sl, src, ext ? kExternalIp : a.ip[dst]);
+      const int rt = route_lookup(a, fsrc, r_lo, r_hi, ext ? kExternalIp : dip);
       if (rt == R_DROP) { st = TGSIM_ST_DROPPED; cnt[ST_DROPPED]++; }
       else if (rt == R_REJECT) { st = TGSIM_ST_REJECTED; cnt[ST_REJECTED]++; }
       else if (rt == R_DEFAULT && ext) { st = TGSIM_ST_EXTERNAL; cnt[ST_EXTERNAL]++; }
       else if (rt != R_DATA) { st = TGSIM_ST_UNREACHABLE; cnt[ST_UNREACH]++; }
-      else if (!(a.flags[dst] & 1u)) { st = TGSIM_ST_DEST_DOWN; cnt[ST_DESTDOWN]++; }
+      else if (!(fdst & 1u)) { st = TGSIM_ST_DEST_DOWN; cnt[ST_DESTDOWN]++; }
       else {
-        const ShapeDev sh = a.shape[sl];
         uint32_t r0[4];
         philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
         int count = 1;
@@ -343,10 +410,20 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
     a.Q.push(q1, r1, 2 * it);
     a.Q.push(q2, r2, 2 * it + 1);
   }
+  // statistics: wave sums -> LDS -> one add per block into one of kNSub counter rows (128 B each),
+  // so the ~8k waves of a launch do not serialise on one cache line (rows summed on read)
+  __shared__ uint32_t wcnt[kBlock / 64][9];
 #pragma unroll
   for (int c = 0; c < 9; ++c) {
     const uint32_t v = wave_sum(cnt[c]);
-    if (lane_id() == 0 && v) atomicAdd(&sc->st[c], (unsigned long long)v);
+    if (lane_id() == 0) wcnt[threadIdx.x >> 6][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) v += wcnt[w][threadIdx.x];
+    if (v) atomicAdd(&a.stats[(blockIdx.x & (kNSub - 1)) * 16 + threadIdx.x], (unsigned long long)v);
   }
 }
 
@@ -1185,6 +1262,10 @@ __global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint
   }
 }
 
+__global__ void k_sig_red_init(int64_t* red) {
+  red[0] = 0; red[1] = INT64_MAX; red[2] = INT64_MIN; red[3] = 0;
+}
+
 // Count-only batch (one state, no sequence numbers): min and max time by block reduction.
 __global__ __launch_bounds__(kBlock) void k_sig_reduce(const int64_t* t, const uint32_t* n_ptr, int64_t* red) {
   __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
@@ -1307,6 +1388,9 @@ __global__ void k_finish(DevScalars* sc) {
   const uint32_t n = sc->qn[Q_D];
   sc->n_out = n;
   sc->st[ST_DELIVERED] += n;
+  sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
+  sc->st[ST_EXTRACTED] += sc->n_extract;
+  sc->st[ST_INSERTED] += sc->qn[Q_L];
 }
 
 // ============================================================================================
@@ -1360,11 +1444,14 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(uint32_t lo, uint32_t nloc
     if (e__ != hipSuccess) return e__; \
   } while (0)
 
+static inline unsigned grid_for(uint64_t n);
 static inline int bits_for(uint32_t K) { return K <= 1 ? 0 : 32 - __builtin_clz(K - 1); }
 
 hipError_t sync_scalars(Dev& d) {
   TG_CHECK(hipMemcpyAsync(d.h_sc, d.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, d.stream));
-  return hipStreamSynchronize(d.stream);
+  TG_CHECK(hipStreamSynchronize(d.stream));
+  if (!d.prof.pending.empty()) prof_resolve(d);
+  return hipSuccess;
 }
 
 static hipError_t reset_window(Dev& d) {
@@ -1384,6 +1471,20 @@ hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t
                      offset_ns);
   TG_CHECK(hipGetLastError());
   return reset_window(d);
+}
+
+hipError_t launch_set_window_dev(Dev& d, int64_t T, const int64_t* t_end_dev, int64_t offset_ns) {
+  hipLaunchKernelGGL(k_set_window_dev, dim3(1), dim3(1), 0, d.stream, d.sc, T, t_end_dev, offset_ns);
+  TG_CHECK(hipGetLastError());
+  return reset_window(d);
+}
+
+hipError_t storm_local_release(Dev& d, uint32_t n) {
+  uint32_t* n_dev = &d.sc->sig_n;
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
+  hipLaunchKernelGGL(k_sig_red_init, dim3(1), dim3(1), 0, d.stream, d.sig_red);
+  hipLaunchKernelGGL(k_sig_reduce, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_t, n_dev, d.sig_red);
+  return hipGetLastError();
 }
 
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n) {
@@ -1418,11 +1519,20 @@ static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t**
     const int passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
     const int db = (bits + passes - 1) / passes;
     for (int p = 0, shift = 0; p < passes; ++p, shift += db) {
-      hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, shift, db,
-                         d.hist);
-      hipLaunchKernelGGL(k_radix_rows, dim3(1u << db), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
-      hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
-                         d.cap_rec, shift, db, d.hist, d.tot);
+      {
+        ProfScope ps_(d, KID_RADIX_HIST);
+        hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, shift,
+                           db, d.hist);
+      }
+      {
+        ProfScope ps_(d, KID_RADIX_ROWS);
+        hipLaunchKernelGGL(k_radix_rows, dim3(1u << db), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+      }
+      {
+        ProfScope ps_(d, KID_RADIX_SCATTER);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
+                           d.cap_rec, shift, db, d.hist, d.tot);
+      }
       std::swap(ki, ko);
       std::swap(vi, vo);
     }
@@ -1436,8 +1546,11 @@ static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t**
 static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, uint32_t K) {
   const size_t b = offsetof(DevScalars, n_large), e = offsetof(DevScalars, n_recv);
   TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
-  hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)K + 1)), dim3(kBlock), 0, d.stream, keys, n_ptr, d.cap_rec,
-                     K, d.seg_off, d.large, d.sc);
+  {
+    ProfScope ps_(d, KID_BOUNDS);
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)K + 1)), dim3(kBlock), 0, d.stream, keys, n_ptr,
+                       d.cap_rec, K, d.seg_off, d.large, d.sc);
+  }
   return hipGetLastError();
 }
 
@@ -1470,16 +1583,22 @@ static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uin
 static hipError_t run_token_bucket(Dev& d) {
   TG_CHECK(qfinal(d, Q_A));
   uint32_t* nA = &d.sc->qn[Q_A];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, (int)Q_A, d.subcap, 0, d.lo,
-                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  {
+    ProfScope psk_(d, KID_KEYS);
+    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, (int)Q_A, d.subcap, 0, d.lo,
+                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  }
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nA, d.nloc, &keys, &vals));
   TG_CHECK(bounds(d, keys, nA, d.nloc));
   TBPolicy p;
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
-  hipLaunchKernelGGL(k_seg_small<TBPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals, d.seg_off,
-                     nA, d.cap_rec);
+  {
+    ProfScope ps_(d, KID_TB);
+    hipLaunchKernelGGL(k_seg_small<TBPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                       d.seg_off, nA, d.cap_rec);
+  }
   TG_CHECK(hipGetLastError());
   bool any;
   uint64_t *K1, *K2;
@@ -1496,8 +1615,11 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
   Queues Q = make_queues(d);
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(kBlock), 0, d.stream, d.regions, d.dirs, d.slots, d.slot_ns,
                      d.plan_start, d.plan_off, d.sc);
-  hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
-                     d.plan_off, d.arena, Q);
+  {
+    ProfScope ps_(d, KID_EXTRACT);
+    hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
+                       d.plan_off, d.arena, Q);
+  }
   TG_CHECK(hipGetLastError());
   if (n_staged) {
     ShapeArgs a;
@@ -1505,7 +1627,8 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
     a.status = d.status; a.shape = d.shape; a.flags = d.flags; a.ip = d.ip; a.rule_off = d.rule_off;
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
-    hipLaunchKernelGGL(k_shape, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, a);
+    a.stats = d.stats;
+    { ProfScope ps_(d, KID_SHAPE); hipLaunchKernelGGL(k_shape, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, a); }
     TG_CHECK(hipGetLastError());
   }
   TG_CHECK(run_token_bucket(d));
@@ -1519,8 +1642,11 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
 static hipError_t run_deliveries(Dev& d) {
   TG_CHECK(qfinal(d, Q_D));
   uint32_t* nD = &d.sc->qn[Q_D];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, (int)Q_D, d.subcap, 1, d.lo,
-                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  {
+    ProfScope psk_(d, KID_KEYS);
+    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, (int)Q_D, d.subcap, 1, d.lo,
+                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  }
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nD, d.nloc, &keys, &vals));
   TG_CHECK(bounds(d, keys, nD, d.nloc));
@@ -1529,8 +1655,11 @@ static hipError_t run_deliveries(Dev& d) {
   EmitPolicy p;
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
-  hipLaunchKernelGGL(k_seg_small<EmitPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
-                     d.seg_off, nD, d.cap_rec);
+  {
+    ProfScope ps_(d, KID_EMIT);
+    hipLaunchKernelGGL(k_seg_small<EmitPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                       d.seg_off, nD, d.cap_rec);
+  }
   TG_CHECK(hipGetLastError());
   bool any;
   uint64_t *K1, *K2;
@@ -1546,13 +1675,19 @@ static hipError_t run_deliveries(Dev& d) {
 static hipError_t run_wheel_insert(Dev& d) {
   TG_CHECK(qfinal(d, Q_L));
   uint32_t* nL = &d.sc->qn[Q_L];
-  hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, (int)Q_L, d.subcap, 2, d.lo,
-                     d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  {
+    ProfScope psk_(d, KID_KEYS);
+    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, (int)Q_L, d.subcap, 2, d.lo,
+                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+  }
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nL, d.slots, &keys, &vals));
   hipLaunchKernelGGL(k_region_alloc, dim3(1), dim3(1), 0, d.stream, d.sc, d.regions, d.cap_arena, d.slot_ns);
-  hipLaunchKernelGGL(k_region_fill, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, keys, vals, d.arena, d.dirs,
-                     d.slots, d.sc);
+  {
+    ProfScope ps_(d, KID_REGION_FILL);
+    hipLaunchKernelGGL(k_region_fill, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, keys, vals, d.arena,
+                       d.dirs, d.slots, d.sc);
+  }
   return hipGetLastError();
 }
 
@@ -1567,10 +1702,6 @@ hipError_t window_end(Dev& d) {
   TG_CHECK(run_wheel_insert(d));
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, d.stream, d.sc);
   return hipGetLastError();
-}
-
-__global__ void k_sig_red_init(int64_t* red) {
-  red[0] = 0; red[1] = INT64_MAX; red[2] = INT64_MIN; red[3] = 0;
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
@@ -1629,6 +1760,7 @@ hipError_t resolve_waiters(Dev& d, uint32_t n_waiters) {
 
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
                             uint32_t size, int64_t spread_ns, uint32_t state) {
+  ProfScope ps_(d, KID_GEN);
   hipLaunchKernelGGL(k_gen_storm, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.lo, d.nloc, d.N, round, t0,
                      fanout, size, spread_ns, state, d.key0, d.key1, staged_base, d.m_src, d.m_dst, d.m_seq,
                      d.m_size, d.m_t, d.s_state, d.s_inst, d.s_t);

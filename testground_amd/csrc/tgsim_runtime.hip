@@ -252,6 +252,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.tot, kMaxBins);
   rc |= dalloc(c, &d.qc, (size_t)3 * kNSub * 32);
   rc |= dalloc(c, &d.sig_red, 4);
+  rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
   rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
@@ -288,6 +289,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   hipStream_t s = d.stream;
   bool ok = hipMemsetAsync(d.sc, 0, sizeof(DevScalars), s) == hipSuccess &&
             hipMemsetAsync(d.st_count, 0, d.max_states * sizeof(uint32_t), s) == hipSuccess &&
+            hipMemsetAsync(d.stats, 0, (size_t)kNSub * 16 * sizeof(unsigned long long), s) == hipSuccess &&
             hipMemsetAsync(d.st_nchunks, 0, d.max_states * sizeof(uint32_t), s) == hipSuccess &&
             hipMemsetAsync(d.st_last, 0, d.max_states * sizeof(int64_t), s) == hipSuccess &&
             hipMemsetAsync(d.rule_off, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
@@ -366,14 +368,43 @@ extern "C" int tgsim_get_stats(tgsim_ctx* c, tgsim_stats* o) {
   if (!c || !o) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   const DevScalars& h = *c->d.h_sc;
-  o->msgs_in = h.st[ST_MSGS]; o->copies = h.st[ST_COPIES]; o->lost = h.st[ST_LOST];
-  o->dropped = h.st[ST_DROPPED]; o->rejected = h.st[ST_REJECTED]; o->unreachable = h.st[ST_UNREACH];
-  o->external = h.st[ST_EXTERNAL]; o->dest_down = h.st[ST_DESTDOWN]; o->local = h.st[ST_LOCAL];
+  std::vector<unsigned long long> rows((size_t)kNSub * 16);
+  HIPCK(c, hipMemcpy(rows.data(), c->d.stats, rows.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost), "stats");
+  unsigned long long st[16] = {};
+  for (int r = 0; r < kNSub; ++r)
+    for (int k = 0; k < 16; ++k) st[k] += rows[(size_t)r * 16 + k];
+  o->msgs_in = st[ST_MSGS]; o->copies = st[ST_COPIES]; o->lost = st[ST_LOST];
+  o->dropped = st[ST_DROPPED]; o->rejected = st[ST_REJECTED]; o->unreachable = st[ST_UNREACH];
+  o->external = st[ST_EXTERNAL]; o->dest_down = st[ST_DESTDOWN]; o->local = st[ST_LOCAL];
   o->delivered = h.st[ST_DELIVERED];
   o->windows = 0;
   o->inflight = h.arena_used;
+  o->tb_items = h.st[ST_TB_ITEMS];
+  o->extracted = h.st[ST_EXTRACTED];
+  o->inserted = h.st[ST_INSERTED];
   return rc;
 }
+
+extern "C" int tgsim_profile_set(tgsim_ctx* c, uint32_t mask) {
+  if (!c) return TGSIM_EINVAL;
+  c->d.prof.mask = mask;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_profile_read(tgsim_ctx* c, double* ms, uint64_t* launches, size_t cap, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  int rc = sync_and_check(c);
+  *n = KID_COUNT;
+  if (cap < (size_t)KID_COUNT) return fail(c, TGSIM_ECAPACITY, "profile capacity");
+  for (int k = 0; k < KID_COUNT; ++k) {
+    if (ms) ms[k] = c->d.prof.ms[k];
+    if (launches) launches[k] = c->d.prof.n[k];
+  }
+  return rc;
+}
+
+extern "C" int tgsim_kernel_classes(void) { return KID_COUNT; }
+extern "C" const char* tgsim_kernel_name(int k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : "?"; }
 
 extern "C" int64_t tgsim_now(const tgsim_ctx* c) { return c ? c->now : -1; }
 
@@ -390,6 +421,15 @@ extern "C" int tgsim_set_shape(tgsim_ctx* c, uint32_t g, const tgsim_link_shape*
   if (is_local(c, g)) {
     c->shape_h[g - c->lo] = o;
     c->shape_dirty = true;
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_set_shapes(tgsim_ctx* c, const uint32_t* inst, const tgsim_link_shape* shapes, size_t n) {
+  if (!c || (n && (!inst || !shapes))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i) {
+    int rc = tgsim_set_shape(c, inst[i], &shapes[i]);
+    if (rc) return rc;
   }
   return TGSIM_OK;
 }
@@ -630,6 +670,24 @@ extern "C" int tgsim_exchange_buffers(tgsim_ctx* c, void** send, void** recv, si
   return TGSIM_OK;
 }
 
+extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, size_t bytes) {
+  if (!c || !send || !recv) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  const size_t need = (size_t)c->S * c->d.xcap * sizeof(tgsim_record);
+  if (bytes < need) return fail(c, TGSIM_ECAPACITY, "exchange buffers need %zu bytes", need);
+  if ((uintptr_t)send % 16 || (uintptr_t)recv % 16) return fail(c, TGSIM_EINVAL, "exchange buffers must be 16-B aligned");
+  c->d.xsend = static_cast<tgsim_record*>(send);
+  c->d.xrecv = static_cast<tgsim_record*>(recv);
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
+  if (!c || !t_end_dev) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  HIPCK(c, launch_set_window_dev(c->d, c->now, t_end_dev, offset_ns), "set window");
+  return begin_common(c);
+}
+
 extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   if (!c) return TGSIM_EINVAL;
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
@@ -773,20 +831,30 @@ extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
 extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {
   if (!c) return TGSIM_EINVAL;
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "storm generator signals need a single-shard context");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
   if (size >= 0x80000000u || spread_ns < 0) return fail(c, TGSIM_EINVAL, "bad size/spread");
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
-  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t0 < c->now) return fail(c, TGSIM_ECAUSALITY, "t0 before window start");
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
   HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state), "gen storm");
   c->n_staged += (uint32_t)n;
-  // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
-  // batch is committed count-only (count, first/last time), DESIGN.md 2.7.
-  HIPCK(c, signal_batch(c->d, c->nloc, state, state, c->sig_log_used, c->n_waiters, true), "storm signals");
+  if (c->S == 1) {
+    // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
+    // batch is committed count-only (count, first/last time), DESIGN.md 2.7.
+    HIPCK(c, signal_batch(c->d, c->nloc, state, state, c->sig_log_used, c->n_waiters, true), "storm signals");
+  } else {
+    // sharded: the release time is the MAX over shards of the local latest signal
+    HIPCK(c, storm_local_release(c->d, c->nloc), "storm release");
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_storm_release_device(tgsim_ctx* c, int64_t* out) {
+  if (!c || !out) return TGSIM_EINVAL;
+  if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
+  HIPCK(c, hipMemcpyAsync(out, c->d.sig_red + 2, sizeof(int64_t), hipMemcpyDeviceToDevice, c->d.stream), "release");
   return TGSIM_OK;
 }

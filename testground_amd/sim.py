@@ -113,6 +113,11 @@ class Simulator:
     def set_shape(self, instance: int, shape: A.LinkShape) -> None:
         self._check(self.lib.set_shape(self._ctx, instance, C.byref(shape)))
 
+    def set_shapes(self, instances, shapes: list[A.LinkShape]) -> None:
+        inst = np.ascontiguousarray(instances, dtype=np.uint32)
+        arr = (A.LinkShape * max(1, len(shapes)))(*shapes)
+        self._check(self.lib.set_shapes(self._ctx, _ptr(inst), arr, len(shapes)))
+
     def add_rules(self, instance: int, rules: list[A.LinkRule]) -> None:
         arr = (A.LinkRule * max(1, len(rules)))(*rules)
         self._check(self.lib.add_rules(self._ctx, instance, arr, len(rules)))
@@ -150,6 +155,21 @@ class Simulator:
         s, r, b = C.c_void_p(), C.c_void_p(), C.c_size_t()
         self._check(self.lib.exchange_buffers(self._ctx, C.byref(s), C.byref(r), C.byref(b)))
         return s.value, r.value, b.value
+
+    def set_exchange_buffers(self, send_dev: int, recv_dev: int, nbytes: int) -> None:
+        self._check(self.lib.set_exchange_buffers(self._ctx, send_dev, recv_dev, nbytes))
+
+    def advance_begin_device(self, t_end_dev: int, offset_ns: int = 0) -> None:
+        self._check(self.lib.advance_begin_device(self._ctx, t_end_dev, int(offset_ns)))
+
+    def storm_release_device(self, out_dev: int) -> None:
+        self._check(self.lib.storm_release_device(self._ctx, out_dev))
+
+    def set_stream(self, stream: int | None) -> None:
+        self._check(self.lib.set_stream(self._ctx, stream))
+
+    def sync(self) -> None:
+        self._check(self.lib.sync(self._ctx))
 
     def advance_to_barrier(self, waiter: int, offset_ns: int = 0) -> None:
         self._check(self.lib.advance_to_barrier(self._ctx, waiter, int(offset_ns)))
@@ -189,6 +209,24 @@ class Simulator:
         s = A.Stats()
         self._check(self.lib.get_stats(self._ctx, C.byref(s)))
         return {name: getattr(s, name) for name, _ in A.Stats._fields_}
+
+    # ---- profiling (HIP library only) --------------------------------------------------------
+    def profile(self, kernels=None) -> None:
+        """Enable HIP-event timing for the named kernel classes (None = all, [] = off)."""
+        names = self.kernel_names()
+        mask = (1 << len(names)) - 1 if kernels is None else sum(1 << names.index(k) for k in kernels)
+        self._check(self.lib.profile_set(self._ctx, mask))
+
+    def kernel_names(self) -> list[str]:
+        return [self.lib.kernel_name(k).decode() for k in range(self.lib.kernel_classes())]
+
+    def profile_read(self) -> dict[str, tuple[float, int]]:
+        k = self.lib.kernel_classes()
+        ms = np.zeros(k, np.float64)
+        cnt = np.zeros(k, np.uint64)
+        n = C.c_size_t()
+        self._check(self.lib.profile_read(self._ctx, _ptr(ms), _ptr(cnt), k, C.byref(n)))
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(self.kernel_names())}
 
     # ---- sync service -----------------------------------------------------------------------
     def signal(self, states, instances, t, want_seq: bool = True) -> np.ndarray | None:

@@ -11,6 +11,14 @@ from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape, int_
 MS = 1_000_000
 
 
+STRUCTURAL_STATS = ("windows", "inflight", "tb_items", "extracted", "inserted")
+
+
+def parity_stats(sim):
+    """Counters that are part of the semantics (the rest describe implementation structure)."""
+    return {k: v for k, v in sim.stats().items() if k not in STRUCTURAL_STATS}
+
+
 def random_shape(rng, *, allow_bw=True):
     lat = int(rng.choice([0, 1_000, 999_999, 5 * MS, 20 * MS, 100 * MS]))
     jit = int(rng.choice([0, 0, 3 * MS, 10 * MS, 150 * MS]))
@@ -76,10 +84,7 @@ def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_
         t0 += 10 * window_ns
         sim.advance(t0)
         out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
-    st = sim.stats()
-    st.pop("windows", None)
-    st.pop("inflight", None)
-    out.append(dict(stats=st))
+    out.append(dict(stats=parity_stats(sim)))
     sim.close()
     return out
 
@@ -111,7 +116,7 @@ def run_heavy(binding, seed: int):
     t0 += 5_000 * MS
     sim.advance(t0)
     out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
-    out.append(dict(stats={k: v for k, v in sim.stats().items() if k not in ("windows", "inflight")}))
+    out.append(dict(stats=parity_stats(sim)))
     sim.close()
     return out
 
@@ -152,7 +157,7 @@ def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4):
         w = sim.barrier(r, n_inst, t0)
         sim.advance_to_barrier(w, 1 * MS)
         out.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
-    out.append(dict(stats={k: v for k, v in sim.stats().items() if k not in ("windows", "inflight")}))
+    out.append(dict(stats=parity_stats(sim)))
     sim.close()
     return out
 
