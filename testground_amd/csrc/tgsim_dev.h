@@ -67,6 +67,7 @@ struct Dev {
   uint32_t* qc = nullptr;         // [3][kNSub][32] append counters (128 B apart)
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;
+  uint32_t* medium = nullptr;     // [segK] ids of segments kThreadSeg < len <= kTile
   uint32_t* chunk_off = nullptr;
   uint64_t *K1a = nullptr, *K1b = nullptr, *K2a = nullptr, *K2b = nullptr;
   uint32_t *K3a = nullptr, *K3b = nullptr;

@@ -11,8 +11,10 @@ namespace tgsim {
 constexpr int kBlock = 256;              // threads per workgroup (4 wave64)
 constexpr int kTile = 1024;              // small-segment tile: segments <= kTile sorted in LDS
 constexpr int kSpan = 2 * kTile;         // LDS capacity of one small-segment span
+constexpr int kThreadSeg = 16;          // segments up to this long: one thread each (k_seg_thread)
+constexpr int kListBlocks = 1024;       // grid of k_seg_list (device-side count)
 constexpr int kChunk = 2048;             // large-segment chunk (LDS bitonic) and merge tile
-constexpr int kRadixBlocks = 256;        // fixed grid of the radix group-by passes (== kBlock)
+constexpr int kRadixBlocks = 256;        // fixed grid of the radix group-by passes (<= 1024: k_radix_rows block)
 constexpr int kMaxDigitBits = 11;        // radix digit width <= 11 bits (2048 bins)
 constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kNSub = 64;                // append sub-queues per batch (contention sharding)
@@ -71,6 +73,7 @@ struct DevScalars {
   uint32_t n_extract;                // records extracted from the wheel this window
   uint32_t plan_tail, plan_n;        // region ring range the extraction plan covers
   uint32_t n_large, max_large, n_chunks;
+  uint32_t n_medium;                 // segments for the block-per-segment kernel (k_seg_list)
   uint32_t n_recv, n_out;
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits

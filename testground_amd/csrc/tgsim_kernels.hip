@@ -730,9 +730,10 @@ __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, con
 
 // Segment offsets off[k] = first position of key k (k = 0..K), and the list of segments longer
 // than kTile (handled by the merge-path path).
+// thread_max > 0: also list the segments with thread_max < len <= kTile in medium[] (n_medium).
 __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const uint32_t* n_ptr, uint32_t cap,
                                                    uint32_t K, uint32_t* off, LargeSeg* large,
-                                                   DevScalars* sc) {
+                                                   uint32_t thread_max, uint32_t* medium, DevScalars* sc) {
   const uint32_t n = clamp_n(n_ptr, cap);
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= K; k += stride) {
@@ -741,6 +742,9 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const u
     if (k < K) {
       const uint32_t ub = lower_bound_u32(keys, n, k + 1);
       const uint32_t len = ub - lb;
+      const bool med = thread_max && len > thread_max && len <= (uint32_t)kTile;
+      const uint32_t mi = wave_append(med ? &sc->n_medium : nullptr);
+      if (med) medium[mi] = k;
       if (len > (uint32_t)kTile) {
         const uint32_t i = atomicAdd(&sc->n_large, 1u);
         LargeSeg L;
@@ -852,6 +856,84 @@ __global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys,
     __syncthreads();
     span_sort(s, m, off, s_begin);
     p.epilogue(s, m, s_begin, off, w);
+    __syncthreads();
+  }
+}
+
+// Register bitonic network over M (power of two) keys (k1, k2, k3); padding keys are all-ones.
+template <int M>
+__device__ __forceinline__ void net_sort(uint64_t (&k1)[M], uint64_t (&k2)[M], uint32_t (&k3)[M]) {
+#pragma unroll
+  for (int k = 2; k <= M; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const bool sw = key_less(0, k1[l], k2[l], k3[l], 0, k1[i], k2[i], k3[i]) == up;
+          const uint64_t a1 = k1[i], a2 = k2[i];
+          const uint32_t a3 = k3[i];
+          k1[i] = sw ? k1[l] : a1; k2[i] = sw ? k2[l] : a2; k3[i] = sw ? k3[l] : a3;
+          k1[l] = sw ? a1 : k1[l]; k2[l] = sw ? a2 : k2[l]; k3[l] = sw ? a3 : k3[l];
+        }
+      }
+    }
+  }
+}
+
+// Segment bounds of the calling thread for the one-thread-per-segment kernels (0 = not mine) and
+// the block's largest such segment.
+__device__ __forceinline__ uint32_t thread_seg(const uint32_t* off, uint32_t K, uint32_t seg, uint32_t& a,
+                                               uint32_t* s_max) {
+  uint32_t len = 0;
+  a = 0;
+  if (seg < K) {
+    a = off[seg];
+    len = off[seg + 1] - a;
+    if (len > (uint32_t)kThreadSeg) len = 0;
+  }
+  if (threadIdx.x == 0) *s_max = 0;
+  __syncthreads();
+  uint32_t wmax = len;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t v = __shfl_xor(wmax, o);
+    wmax = v > wmax ? v : wmax;
+  }
+  if (lane_id() == 0 && wmax) atomicMax(s_max, wmax);
+  __syncthreads();
+  return len;
+}
+
+template <class P, int M>
+__device__ __forceinline__ void thread_keys(const P& p, const uint32_t* vals, uint32_t seg, uint32_t a, uint32_t len,
+                                            uint64_t (&k1)[M], uint64_t (&k2)[M], uint32_t (&k3)[M]) {
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    k1[u] = ~0ull; k2[u] = ~0ull; k3[u] = 0xFFFFFFFFu;
+    if ((uint32_t)u < len) {
+      uint32_t sg;
+      p.key(seg, vals[a + u], sg, k1[u], k2[u], k3[u]);
+    }
+  }
+  net_sort<M>(k1, k2, k3);
+}
+
+// One block per listed segment (kThreadSeg < len <= kTile): LDS sort + the policy's block epilogue.
+template <class P>
+__global__ __launch_bounds__(kBlock) void k_seg_list(P p, const uint32_t* vals, const uint32_t* off,
+                                                     const uint32_t* list, const DevScalars* sc) {
+  __shared__ SortSmem s;
+  const uint32_t nm = sc->n_medium;
+  for (uint32_t w = blockIdx.x; w < nm; w += gridDim.x) {
+    const uint32_t g = list[w];
+    const uint32_t a = off[g], m = off[g + 1] - a;
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) p.key(g, vals[a + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+    __syncthreads();
+    span_sort(s, m, off, a);
+    p.epilogue(s, m, a, off, w);
     __syncthreads();
   }
 }
@@ -1121,6 +1203,131 @@ struct TBPolicy {
   }
 };
 
+// Exclusive block scan of two per-thread counts; totals returned to every thread. red: [2 * waves].
+__device__ __forceinline__ void block_scan2(uint32_t& v0, uint32_t& v1, uint32_t* red, uint32_t& t0, uint32_t& t1) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x0 = v0, x1 = v1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y0 = __shfl_up(x0, o), y1 = __shfl_up(x1, o);
+    if ((int)lane >= o) { x0 += y0; x1 += y1; }
+  }
+  if (lane == 63) { red[2 * wave] = x0; red[2 * wave + 1] = x1; }
+  __syncthreads();
+  uint32_t p0 = 0, p1 = 0;
+  t0 = 0; t1 = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    const uint32_t a0 = red[2 * w], a1 = red[2 * w + 1];
+    if (w < wave) { p0 += a0; p1 += a1; }
+    t0 += a0; t1 += a1;
+  }
+  v0 = p0 + x0 - v0;
+  v1 = p1 + x1 - v1;
+}
+
+struct TBSmem {
+  uint32_t max_len, any_x;
+  uint32_t red[2 * (kBlock / 64)];
+  uint32_t base[2];
+};
+
+// One sender per thread (<= kThreadSeg items): sort in registers, run the GCRA recurrence
+// sequentially, reserve the block's departed copies with one atomic per queue, then write them.
+template <int M>
+__device__ __forceinline__ void tb_thread_body(const TBPolicy& p, const uint32_t* vals, uint32_t sl, uint32_t a,
+                                               uint32_t len, TBSmem& sm) {
+  uint64_t k1[M], k2[M];
+  uint32_t k3[M];
+  thread_keys<TBPolicy, M>(p, vals, sl, a, len, k1, k2, k3);
+  const int64_t t_end = p.sc->t_end;
+  int64_t dep[M];
+  int code[M];
+  uint32_t nD = 0, nL = 0, nX = 0;
+  int64_t x = 0, tau = 0;
+  uint32_t mult = 0, shift = 0;
+  if (len) {
+    const ShapeDev& sh = p.shape[sl];
+    tau = sh.tau; mult = sh.mult; shift = sh.shift;
+    x = p.X[sl];
+  }
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    dep[u] = 0;
+    code[u] = -1;
+    if ((uint32_t)u < len) {
+      const uint4 r0 = reinterpret_cast<const uint4*>(p.A + k3[u])[0];
+      const uint4 r1 = reinterpret_cast<const uint4*>(p.A + k3[u])[1];
+      const int64_t e = (int64_t)k1[u];
+      uint64_t c = ((uint64_t)r1.y * mult) >> shift;
+      c = c > kCostClamp ? kCostClamp : c;
+      const int64_t xprev = x;
+      const int64_t b = x > e - tau ? x : e - tau;
+      const int64_t v = b + (int64_t)c;
+      x = v > kTbClamp ? kTbClamp : v;
+      dep[u] = e > xprev ? e : xprev;
+      const int q = qid_stage_d(p.geo, r0.w, dep[u], t_end);
+      code[u] = q;
+      nD += q == Q_D; nL += q == Q_L; nX += q >= Q_X0;
+    }
+  }
+  if (len) p.X[sl] = x;
+  if (nX) sm.any_x = 1;
+  uint32_t tD, tL;
+  block_scan2(nD, nL, sm.red, tD, tL);  // nD/nL now this thread's offsets inside the block's runs
+  const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
+  const Queues& Q = p.Q;
+  if (threadIdx.x == 0) {
+    sm.base[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
+    sm.base[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
+  }
+  __syncthreads();
+  uint32_t pD = sm.base[0] + nD, pL = sm.base[1] + nL;
+  tgsim_record* bD = Q.D + (size_t)sub * Q.subcap;
+  tgsim_record* bL = Q.L + (size_t)sub * Q.subcap;
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    if (code[u] == Q_D || code[u] == Q_L) {
+      tgsim_record rec;
+      load_rec(p.A + k3[u], rec);
+      rec.t = dep[u];
+      rec.meta |= TGSIM_F_STAGE_D;
+      const bool isD = code[u] == Q_D;
+      const uint32_t pos = isD ? pD++ : pL++;
+      if (pos < Q.subcap) store_rec((isD ? bD : bL) + pos, rec);
+      else atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
+    }
+  }
+  if (sm.any_x) {  // cross-shard copies (S > 1): per-item wave appends onto the peer blocks
+    const uint32_t salt = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16u;
+#pragma unroll
+    for (int u = 0; u < M; ++u) {
+      tgsim_record rec;
+      const bool mine = code[u] >= Q_X0;
+      if (mine) {
+        load_rec(p.A + k3[u], rec);
+        rec.t = dep[u];
+        rec.meta |= TGSIM_F_STAGE_D;
+      }
+      Q.push(mine ? code[u] : -1, rec, salt + (uint32_t)u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_tb_thread(TBPolicy p, const uint32_t* vals, const uint32_t* off,
+                                                      uint32_t K) {
+  __shared__ TBSmem sm;
+  const uint32_t sl = blockIdx.x * kBlock + threadIdx.x;
+  if (threadIdx.x == 0) sm.any_x = 0;
+  uint32_t a;
+  const uint32_t len = thread_seg(off, K, sl, a, &sm.max_len);
+  const uint32_t M = sm.max_len;
+  if (M == 0) return;  // block-uniform
+  if (M <= 4) tb_thread_body<4>(p, vals, sl, a, len, sm);
+  else if (M <= 8) tb_thread_body<8>(p, vals, sl, a, len, sm);
+  else tb_thread_body<16>(p, vals, sl, a, len, sm);
+}
+
 // One block per large sender segment: sorted keys arrive in tiles of kChunk with a carried X.
 __global__ __launch_bounds__(kBlock) void k_tb_large(TBPolicy p, const LargeSeg* large,
                                                      const uint64_t* K1, const uint32_t* K3) {
@@ -1174,6 +1381,53 @@ struct EmitPolicy {
     for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s_begin + j, s.k3[s.perm[j]]);
   }
 };
+
+constexpr int kStage = 2048;  // LDS staging of one block's output range in k_emit_thread
+
+template <int M>
+__device__ __forceinline__ void emit_thread_body(const EmitPolicy& p, const uint32_t* vals, uint32_t seg, uint32_t a,
+                                                 uint32_t len, uint32_t base, bool staged, uint32_t* stage) {
+  uint64_t k1[M], k2[M];
+  uint32_t k3[M];
+  thread_keys<EmitPolicy, M>(p, vals, seg, a, len, k1, k2, k3);
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    if ((uint32_t)u < len) {
+      if (staged) stage[a - base + u] = k3[u];
+      else p.write(a + u, k3[u]);
+    }
+  }
+}
+
+// One receiver per thread (<= kThreadSeg deliveries): sort in registers; the block's inbox range
+// (contiguous: consecutive receivers) is staged in LDS and written out coalesced.
+__global__ __launch_bounds__(kBlock) void k_emit_thread(EmitPolicy p, const uint32_t* vals, const uint32_t* off,
+                                                        uint32_t K) {
+  __shared__ uint32_t s_max;
+  __shared__ uint32_t stage[kStage];
+  const uint32_t seg = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t a;
+  const uint32_t len = thread_seg(off, K, seg, a, &s_max);
+  const uint32_t M = s_max;
+  if (M == 0) return;  // block-uniform
+  const uint32_t s0 = blockIdx.x * kBlock, s1 = min(s0 + (uint32_t)kBlock, K);
+  const uint32_t base = off[s0], R = off[s1] - base;
+  const bool staged = R <= (uint32_t)kStage;
+  if (staged) {
+    for (uint32_t j = threadIdx.x; j < R; j += kBlock) stage[j] = 0xFFFFFFFFu;
+    __syncthreads();
+  }
+  if (M <= 4) emit_thread_body<4>(p, vals, seg, a, len, base, staged, stage);
+  else if (M <= 8) emit_thread_body<8>(p, vals, seg, a, len, base, staged, stage);
+  else emit_thread_body<16>(p, vals, seg, a, len, base, staged, stage);
+  if (staged) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < R; j += kBlock) {
+      const uint32_t v = stage[j];
+      if (v != 0xFFFFFFFFu) p.write(base + j, v);
+    }
+  }
+}
 
 __global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const LargeSeg* large,
                                                        const uint32_t* chunk_off, const DevScalars* sc,
@@ -1543,13 +1797,13 @@ static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t**
   return hipSuccess;
 }
 
-static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, uint32_t K) {
+static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, uint32_t K, uint32_t thread_max = 0) {
   const size_t b = offsetof(DevScalars, n_large), e = offsetof(DevScalars, n_recv);
   TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
   {
     ProfScope ps_(d, KID_BOUNDS);
     hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)K + 1)), dim3(kBlock), 0, d.stream, keys, n_ptr,
-                       d.cap_rec, K, d.seg_off, d.large, d.sc);
+                       d.cap_rec, K, d.seg_off, d.large, thread_max, d.medium, d.sc);
   }
   return hipGetLastError();
 }
@@ -1590,14 +1844,16 @@ static hipError_t run_token_bucket(Dev& d) {
   }
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nA, d.nloc, &keys, &vals));
-  TG_CHECK(bounds(d, keys, nA, d.nloc));
+  TG_CHECK(bounds(d, keys, nA, d.nloc, kThreadSeg));
   TBPolicy p;
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
   {
     ProfScope ps_(d, KID_TB);
-    hipLaunchKernelGGL(k_seg_small<TBPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
-                       d.seg_off, nA, d.cap_rec);
+    hipLaunchKernelGGL(k_tb_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
+                       d.seg_off, d.nloc);
+    hipLaunchKernelGGL(k_seg_list<TBPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
+                       d.medium, d.sc);
   }
   TG_CHECK(hipGetLastError());
   bool any;
@@ -1649,7 +1905,7 @@ static hipError_t run_deliveries(Dev& d) {
   }
   uint32_t *keys, *vals;
   TG_CHECK(group_by(d, nD, d.nloc, &keys, &vals));
-  TG_CHECK(bounds(d, keys, nD, d.nloc));
+  TG_CHECK(bounds(d, keys, nD, d.nloc, kThreadSeg));
   TG_CHECK(hipMemcpyAsync(d.inbox, d.seg_off, ((size_t)d.nloc + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                           d.stream));
   EmitPolicy p;
@@ -1657,8 +1913,10 @@ static hipError_t run_deliveries(Dev& d) {
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   {
     ProfScope ps_(d, KID_EMIT);
-    hipLaunchKernelGGL(k_seg_small<EmitPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
-                       d.seg_off, nD, d.cap_rec);
+    hipLaunchKernelGGL(k_emit_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
+                       d.seg_off, d.nloc);
+    hipLaunchKernelGGL(k_seg_list<EmitPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
+                       d.medium, d.sc);
   }
   TG_CHECK(hipGetLastError());
   bool any;

@@ -255,6 +255,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
+  rc |= dalloc(c, &d.medium, segK);
   rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
   rc |= dalloc(c, &d.K1a, d.cap_rec);
   rc |= dalloc(c, &d.K1b, d.cap_rec);
