@@ -190,6 +190,12 @@ int tgsim_shard_range(const tgsim_ctx* ctx, uint32_t* lo, uint32_t* hi);
 int tgsim_sync(tgsim_ctx* ctx); /* wait for the stream, surface device-side errors */
 int tgsim_get_stats(tgsim_ctx* ctx, tgsim_stats* out);
 int64_t tgsim_now(const tgsim_ctx* ctx); /* current window start (host view) */
+/* Reaction horizon = start of the last completed window. Messages may be staged with
+ * t_send >= horizon, so an instance can answer a delivery of the last window at its delivery time
+ * (conservative PDES: with window length <= lookahead the answer cannot land in a window that was
+ * already delivered; a record that would is delivered late, in the current window, with its own
+ * time - DESIGN.md 2.8). */
+int64_t tgsim_horizon(const tgsim_ctx* ctx);
 
 /* ---- network configuration (sidecar.Network, pkg/sidecar/instance.go:37-42) -------------------
  * tgsim_configure_network replaces DockerNetwork.ConfigureNetwork (docker_network.go:51-148) for
@@ -206,7 +212,7 @@ int tgsim_set_enabled(tgsim_ctx* ctx, uint32_t instance, int32_t enabled, int32_
 int tgsim_get_ip(const tgsim_ctx* ctx, uint32_t instance, uint32_t* ip);
 
 /* ---- data path (replaces the host kernel's HTB/netem/FIB per packet) ----------------------------- */
-/* Stage messages for the next window (host SoA, copied). t_send must be >= tgsim_now(). */
+/* Stage messages for the next window (host SoA, copied). t_send must be >= tgsim_horizon(). */
 int tgsim_enqueue(tgsim_ctx* ctx, const tgsim_msg_soa* msgs, size_t n);
 /* Stage messages already in device memory (SoA arrays of n elements). */
 int tgsim_enqueue_device(tgsim_ctx* ctx, const tgsim_msg_soa* dev_msgs, size_t n);

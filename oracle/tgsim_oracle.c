@@ -183,6 +183,7 @@ struct tgo_ctx {
   uint32_t* id_of;    /* [2^(32-len)] ip - data_net -> id, or UINT32_MAX */
   size_t id_of_n;
   int64_t now, t_end;
+  int64_t horizon;    /* start of the last completed window: earliest admissible t_send */
   int in_window;
   omsgs staged;
   uint8_t* status; size_t n_status, status_cap;
@@ -319,6 +320,7 @@ void tgo_destroy(tgo_ctx* c) {
 
 const char* tgo_last_error(const tgo_ctx* c) { return c ? c->err : "null context"; }
 int64_t tgo_now(const tgo_ctx* c) { return c->now; }
+int64_t tgo_horizon(const tgo_ctx* c) { return c->horizon; }
 
 static int is_local(const tgo_ctx* c, uint32_t g) { return g >= c->lo && g < c->hi; }
 
@@ -473,7 +475,7 @@ int tgo_enqueue(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
     if (m->src[i] >= c->N || (m->dst[i] >= c->N && m->dst[i] != TGSIM_DST_EXTERNAL))
       return fail(c, TGSIM_EINVAL, "message %zu: bad instance id", i);
     if (!is_local(c, m->src[i])) return fail(c, TGSIM_EINVAL, "message %zu: sender not in this shard", i);
-    if (m->t_send[i] < c->now) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before window start", i);
+    if (m->t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before the reaction horizon", i);
     if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "message %zu: size too large", i);
   }
   memcpy(s->src + s->n, m->src, n * 4); memcpy(s->dst + s->n, m->dst, n * 4);
@@ -694,6 +696,7 @@ int tgo_advance_end(tgo_ctx* c) {
   c->stats.delivered += c->out.n;
   c->stats.windows++;
   c->stats.inflight = c->heap.n;
+  c->horizon = c->now;
   c->now = c->t_end;
   c->in_window = 0;
   return TGSIM_OK;

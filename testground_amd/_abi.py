@@ -88,6 +88,7 @@ _SIGS = {
     "destroy": (None, [P]),
     "last_error": (C.c_char_p, [P]),
     "now": (C.c_int64, [P]),
+    "horizon": (C.c_int64, [P]),
     "configure_network": (C.c_int, [P, C.c_uint32, C.POINTER(NetworkConfig)]),
     "set_shape": (C.c_int, [P, C.c_uint32, C.POINTER(LinkShape)]),
     "set_shapes": (C.c_int, [P, C.c_void_p, C.POINTER(LinkShape), C.c_size_t]),

@@ -66,6 +66,7 @@ struct RegionDev {
 enum { Q_A = 0, Q_D = 1, Q_L = 2, Q_X0 = 3 };  // append queues: TB batch, deliveries, wheel, peers
 struct DevScalars {
   int64_t T, t_end;                  // current window
+  int64_t H;                         // reaction horizon: earliest admissible t_send
   // ---- per-window block: zeroed by one memset at window start ----
   uint32_t q[Q_X0 + kMaxShards];     // exchange cursors per peer (q[Q_X0 + p]); q[0..2] unused
   uint32_t qpre[3][kNSub + 1];       // A, D, L: prefix over sub-queues (after k_qfinal)

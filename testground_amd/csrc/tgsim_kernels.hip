@@ -184,15 +184,17 @@ __device__ __forceinline__ T wave_sum(T v) {
 // window control
 // ============================================================================================
 
-__global__ void k_set_window(DevScalars* sc, int64_t T, int64_t t_end) {
+__global__ void k_set_window(DevScalars* sc, int64_t H, int64_t T, int64_t t_end) {
+  sc->H = H;
   sc->T = T;
   sc->t_end = t_end;
 }
 
 // t_end = release time of a barrier waiter + offset, decided on the device (no host round trip).
 __global__ void k_set_window_barrier(DevScalars* sc, const int64_t* w_release, uint32_t waiter,
-                                     int64_t T, int64_t offset) {
+                                     int64_t H, int64_t T, int64_t offset) {
   const int64_t rel = w_release[waiter];
+  sc->H = H;
   sc->T = T;
   if (rel < 0) {
     atomicOr(&sc->err, ERR_UNRELEASED);
@@ -203,8 +205,9 @@ __global__ void k_set_window_barrier(DevScalars* sc, const int64_t* w_release, u
   }
 }
 
-__global__ void k_set_window_dev(DevScalars* sc, int64_t T, const int64_t* t_end_dev, int64_t offset) {
+__global__ void k_set_window_dev(DevScalars* sc, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset) {
   const int64_t e = *t_end_dev + offset;
+  sc->H = H;
   sc->T = T;
   sc->t_end = e < T ? T : e;
 }
@@ -327,7 +330,7 @@ __device__ __forceinline__ int qid_copy(const Geo& geo, const tgsim_record& r, i
 
 __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
   DevScalars* sc = a.Q.sc;
-  const int64_t T = sc->T, t_end = sc->t_end;
+  const int64_t H = sc->H, t_end = sc->t_end;
   uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t stride = gridDim.x * blockDim.x;
   uint32_t it = 0;
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
       atomicOr(&sc->err, ERR_BAD_MSG);
       st = TGSIM_ST_UNREACHABLE;
       cnt[ST_UNREACH]++;
-    } else if (ts < T || ts >= t_end) {
+    } else if (ts < H || ts >= t_end) {
       atomicOr(&sc->err, ERR_CAUSAL);
       st = TGSIM_ST_UNREACHABLE;
       cnt[ST_UNREACH]++;
@@ -1714,21 +1717,21 @@ static hipError_t reset_window(Dev& d) {
   return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
 }
 
-hipError_t launch_set_window(Dev& d, int64_t T, int64_t t_end) {
-  hipLaunchKernelGGL(k_set_window, dim3(1), dim3(1), 0, d.stream, d.sc, T, t_end);
+hipError_t launch_set_window(Dev& d, int64_t H, int64_t T, int64_t t_end) {
+  hipLaunchKernelGGL(k_set_window, dim3(1), dim3(1), 0, d.stream, d.sc, H, T, t_end);
   TG_CHECK(hipGetLastError());
   return reset_window(d);
 }
 
-hipError_t launch_set_window_barrier(Dev& d, int64_t T, uint32_t waiter, int64_t offset_ns) {
-  hipLaunchKernelGGL(k_set_window_barrier, dim3(1), dim3(1), 0, d.stream, d.sc, d.w_release, waiter, T,
+hipError_t launch_set_window_barrier(Dev& d, int64_t H, int64_t T, uint32_t waiter, int64_t offset_ns) {
+  hipLaunchKernelGGL(k_set_window_barrier, dim3(1), dim3(1), 0, d.stream, d.sc, d.w_release, waiter, H, T,
                      offset_ns);
   TG_CHECK(hipGetLastError());
   return reset_window(d);
 }
 
-hipError_t launch_set_window_dev(Dev& d, int64_t T, const int64_t* t_end_dev, int64_t offset_ns) {
-  hipLaunchKernelGGL(k_set_window_dev, dim3(1), dim3(1), 0, d.stream, d.sc, T, t_end_dev, offset_ns);
+hipError_t launch_set_window_dev(Dev& d, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset_ns) {
+  hipLaunchKernelGGL(k_set_window_dev, dim3(1), dim3(1), 0, d.stream, d.sc, H, T, t_end_dev, offset_ns);
   TG_CHECK(hipGetLastError());
   return reset_window(d);
 }

@@ -37,6 +37,7 @@ struct tgsim_ctx {
   uint32_t* tb_reset_dev = nullptr;
   uint32_t tb_reset_cap = 0;
   int64_t now = 0;
+  int64_t horizon = 0;   // start of the last completed window: earliest admissible t_send
   uint32_t n_staged = 0, n_status_last = 0;
   bool in_window = false;
   bool now_from_device = false;
@@ -354,6 +355,7 @@ static int check_device_errors(tgsim_ctx* c) {
 static int sync_and_check(tgsim_ctx* c) {
   HIPCK(c, sync_scalars(c->d), "sync");
   if (c->now_from_device && !c->in_window) {
+    c->horizon = c->d.h_sc->T;
     c->now = c->d.h_sc->t_end;
     c->now_from_device = false;
   }
@@ -408,6 +410,7 @@ extern "C" int tgsim_kernel_classes(void) { return KID_COUNT; }
 extern "C" const char* tgsim_kernel_name(int k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : "?"; }
 
 extern "C" int64_t tgsim_now(const tgsim_ctx* c) { return c ? c->now : -1; }
+extern "C" int64_t tgsim_horizon(const tgsim_ctx* c) { return c ? c->horizon : -1; }
 
 // ============================== network configuration ========================================
 
@@ -601,7 +604,7 @@ static int validate_msgs(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
     if (m->src[i] >= c->N || (m->dst[i] >= c->N && m->dst[i] != TGSIM_DST_EXTERNAL))
       return fail(c, TGSIM_EINVAL, "message %zu: bad instance id", i);
     if (!is_local(c, m->src[i])) return fail(c, TGSIM_EINVAL, "message %zu: sender not in this shard", i);
-    if (m->t_send[i] < c->now) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before window start", i);
+    if (m->t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "message %zu: t_send before the reaction horizon", i);
     if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "message %zu: size too large", i);
   }
   return TGSIM_OK;
@@ -659,7 +662,7 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
-  HIPCK(c, launch_set_window(c->d, c->now, t_end), "set window");
+  HIPCK(c, launch_set_window(c->d, c->horizon, c->now, t_end), "set window");
   return begin_common(c);
 }
 
@@ -685,7 +688,7 @@ extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, 
 extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
   if (!c || !t_end_dev) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
-  HIPCK(c, launch_set_window_dev(c->d, c->now, t_end_dev, offset_ns), "set window");
+  HIPCK(c, launch_set_window_dev(c->d, c->horizon, c->now, t_end_dev, offset_ns), "set window");
   return begin_common(c);
 }
 
@@ -695,6 +698,7 @@ extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   HIPCK(c, window_end(c->d), "window_end");
   c->in_window = false;
   // window_end synchronised during the delivery sort; h_sc->t_end is this window's end
+  c->horizon = c->d.h_sc->T;
   c->now = c->d.h_sc->t_end;
   c->now_from_device = false;
   return check_device_errors(c);
@@ -714,7 +718,7 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
-  HIPCK(c, launch_set_window_barrier(c->d, c->now, waiter, offset_ns), "set window");
+  HIPCK(c, launch_set_window_barrier(c->d, c->horizon, c->now, waiter, offset_ns), "set window");
   int rc = begin_common(c);
   if (rc) return rc;
   return tgsim_advance_end(c);

@@ -1,0 +1,440 @@
+"""Workload descriptors: the reference's test plans restated as message patterns over simulated
+instances (hard part 6). A plan here is a function ``plan(env) -> ok[]`` that returns
+the per-instance outcome, written against the same client calls the Go plan makes
+(``env.sync``: sync.Client, ``env.net``: network.Client) so it can be read beside the original.
+
+Messages are the units the simulator shapes. A TCP segment is modelled as one message of
+``payload + TCP_OVERHEAD`` bytes; there is no retransmission, so a lost segment fails the exchange
+it belongs to (packet/TCP-level modelling is SURVEY.md 8(f) rank 4).
+
+Registered plans (``PLANS[(plan, case)]``):
+  network/ping-pong           plans/network/pingpong.go:16-201
+  network/traffic-allowed     plans/network/traffic.go:16-72 (AllowAll)
+  network/traffic-blocked     plans/network/traffic.go:16-72 (DenyAll)
+  splitbrain/{drop,reject,accept}   plans/splitbrain/main.go:41-186
+  benchmarks/storm            plans/benchmarks/storm.go:31-197
+  benchmarks/barrier          plans/benchmarks/benchmarks.go:90-145
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _abi as A
+from .network import (MS, SECOND, AllowAll, Config, DenyAll, FilterAction, IPNet, LinkRule, LinkShape,
+                      int_to_ip)
+from .sidecar import NetClient, Sidecar
+from .sim import SimConfig, Simulator
+from .sync import SyncService
+
+TCP_OVERHEAD = 66          # Ethernet 14 + IPv4 20 + TCP 20 + timestamp option 12 bytes per segment
+TCP_CHUNK = 4 * 1024       # storm.go:23 write size
+NEVER = np.iinfo(np.int64).max
+
+
+class PlanEnv:
+    """One simulated run: simulator + sync service + sidecars + network clients, and a message
+    layer that stages sends when their time falls in the next window and records, per message,
+    its status and first arrival time."""
+
+    def __init__(self, n_instances: int, seed: int = 1, test_case: str = "", params: dict | None = None,
+                 binding=None, window_ns: int = 1 * MS, sim_kw: dict | None = None):
+        self.n = int(n_instances)
+        self.test_case = test_case
+        self.params = dict(params or {})
+        self.window_ns = int(window_ns)
+        kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=1024, max_waiters=1 << 16)
+        kw.update(sim_kw or {})
+        self.sim = Simulator(SimConfig(n_instances=self.n, seed=seed, **kw), binding=binding)
+        self.sync = SyncService(self.sim)
+        self.sidecar = Sidecar(self.sim, self.sync, self.n, track_configs=self.n <= 4096)
+        self.net = NetClient(self.sidecar)
+        self._seq = np.zeros(self.n, np.int64)
+        self._pend = []                       # (t, src, dst, seq, size) arrays not yet staged
+        self._st_keys, self._st_vals = [], []  # status log
+        self._ar_keys, self._ar_vals = [], []  # arrival log (first arrival per key after compaction)
+        self.failures: list[str] = []
+        self.sidecar.initialize(0)
+
+    def close(self):
+        self.sim.close()
+
+    # ---- parameters (runtime.RunEnv.IntParam & co.) ---------------------------------------------
+    def int_param(self, name: str, default=None) -> int:
+        v = self.params.get(name, default)
+        if v is None:
+            raise KeyError(f"missing test parameter {name!r}")
+        return int(v)
+
+    # ---- messages ---------------------------------------------------------------------------
+    @staticmethod
+    def key(src, seq):
+        return (np.asarray(src, np.uint64) << np.uint64(32)) | np.asarray(seq, np.uint64)
+
+    def send(self, src, dst, size, t) -> np.ndarray:
+        """Queue messages src[i] -> dst[i] of size[i] bytes at time t[i]; returns their keys."""
+        src = np.atleast_1d(np.asarray(src, np.int64))
+        n = len(src)
+        dst = np.broadcast_to(np.asarray(dst, np.int64), (n,)).copy()
+        size = np.broadcast_to(np.asarray(size, np.int64), (n,)).copy()
+        t = np.broadcast_to(np.asarray(t, np.int64), (n,)).copy()
+        if n == 0:
+            return np.zeros(0, np.uint64)
+        if t.min() < self.sim.horizon:
+            raise A.TgsimError(A.ECAUSALITY, "send before the reaction horizon")
+        order = np.argsort(src, kind="stable")
+        s_sorted = src[order]
+        first = np.r_[0, np.flatnonzero(np.diff(s_sorted)) + 1]
+        run_start = np.repeat(first, np.diff(np.r_[first, n]))
+        rank = np.arange(n) - run_start
+        seq = np.empty(n, np.int64)
+        seq[order] = self._seq[s_sorted] + rank
+        np.add.at(self._seq, src, 1)
+        self._pend.append((t, src, dst, seq, size))
+        return self.key(src, seq)
+
+    def step(self, t_end: int | None = None) -> dict:
+        """Run one window [now, t_end) (default: one window_ns). Returns its deliveries."""
+        t_end = self.sim.now + self.window_ns if t_end is None else int(t_end)
+        if self._pend:
+            t = np.concatenate([p[0] for p in self._pend])
+            cols = [np.concatenate([p[k] for p in self._pend]) for k in range(1, 5)]
+            due = t < t_end
+            keep = ~due
+            self._pend = [(t[keep], *[c[keep] for c in cols])] if keep.any() else []
+            if due.any():
+                src, dst, seq, size = (c[due] for c in cols)
+                self.sim.enqueue(src, dst, seq, size, t[due])
+                staged_keys = self.key(src, seq)
+            else:
+                staged_keys = np.zeros(0, np.uint64)
+        else:
+            staged_keys = np.zeros(0, np.uint64)
+        self.sim.advance(t_end)
+        if len(staged_keys):
+            self._st_keys.append(staged_keys)
+            self._st_vals.append(self.sim.status())
+        d = self.sim.deliveries()
+        if len(d["t_deliver"]):
+            self._ar_keys.append(self.key(d["src"], d["seq"]))
+            self._ar_vals.append(d["t_deliver"])
+        return d
+
+    def _compact(self, keys, vals, first_min: bool):
+        if len(keys) > 1 or (keys and first_min):
+            k = np.concatenate(keys)
+            v = np.concatenate(vals)
+            o = np.lexsort((v, k)) if first_min else np.argsort(k, kind="stable")
+            k, v = k[o], v[o]
+            u = np.r_[True, k[1:] != k[:-1]]
+            keys[:] = [k[u]]
+            vals[:] = [v[u]]
+        return (keys[0], vals[0]) if keys else (np.zeros(0, np.uint64), np.zeros(0, np.int64))
+
+    def status_of(self, keys) -> np.ndarray:
+        """Status byte of each message, or 0xFF if it has not been processed yet."""
+        k, v = self._compact(self._st_keys, self._st_vals, False)
+        return _lookup(k, v, keys, 0xFF).astype(np.int64)
+
+    def arrival_of(self, keys) -> np.ndarray:
+        """First arrival time of each message, or NEVER."""
+        k, v = self._compact(self._ar_keys, self._ar_vals, True)
+        return _lookup(k, v, keys, NEVER)
+
+    def wait(self, keys, timeout_ns: int) -> np.ndarray:
+        """Step windows until every message has arrived or failed (or the timeout). Returns
+        arrival times (NEVER for failures)."""
+        keys = np.asarray(keys, np.uint64)
+        deadline = self.sim.now + int(timeout_ns)
+        while True:
+            arr = self.arrival_of(keys)
+            st = self.status_of(keys)
+            failed = (st != 0xFF) & ((st & 0x0F) != A.ST_QUEUED) & ((st & 0x0F) != A.ST_LOCAL)
+            if np.all((arr != NEVER) | failed) or self.sim.now >= deadline:
+                return arr
+            self.step()
+
+    def advance_to(self, t: int) -> None:
+        """Let simulated time pass until t (time.Sleep), window by window while traffic is in flight."""
+        while self.sim.now < t:
+            idle = not self._pend and self.sim.stats()["inflight"] == 0
+            self.step(t if idle else min(t, self.sim.now + self.window_ns))
+
+    def rpc(self, src, dst, req_size, rep_size, t, timeout_ns) -> tuple[np.ndarray, np.ndarray]:
+        """Request src->dst at t; dst answers at the request's first arrival (in the window right
+        after it, at the arrival time: the reaction horizon allows it). Returns (ok, rtt)."""
+        src = np.atleast_1d(np.asarray(src, np.int64))
+        n = len(src)
+        dst = np.broadcast_to(np.asarray(dst, np.int64), (n,))
+        t = np.broadcast_to(np.asarray(t, np.int64), (n,))
+        req = self.send(src, dst, req_size, t)
+        deadline = int(t.max()) + int(timeout_ns) if n else self.sim.now
+        o_req = np.argsort(req)
+        req_sorted = req[o_req]
+        rep = np.zeros(n, np.uint64)
+        answered = np.zeros(n, bool)
+        while n:
+            d = self.step()
+            if len(d["t_deliver"]):
+                k = self.key(d["src"], d["seq"])
+                i = np.minimum(np.searchsorted(req_sorted, k), n - 1)
+                hit = req_sorted[i] == k
+                idx = o_req[i[hit]]
+                at = d["t_deliver"][hit]
+                idx, first = np.unique(idx, return_index=True)   # duplicates: first copy only
+                at = at[first]
+                new = ~answered[idx]
+                if new.any():
+                    j = idx[new]
+                    rep[j] = self.send(dst[j], src[j], rep_size, at[new])
+                    answered[j] = True
+            st_req = self.status_of(req)
+            req_failed = (st_req != 0xFF) & ~np.isin(st_req & 0x0F, (A.ST_QUEUED, A.ST_LOCAL))
+            arr = np.where(answered, self.arrival_of(rep), NEVER)
+            st_rep = np.where(answered, self.status_of(rep), 0xFF)
+            rep_failed = (st_rep != 0xFF) & ~np.isin(st_rep & 0x0F, (A.ST_QUEUED, A.ST_LOCAL))
+            if np.all((arr != NEVER) | req_failed | rep_failed) or self.sim.now >= deadline:
+                break
+        if not n:
+            return np.zeros(0, bool), np.zeros(0, np.int64)
+        ok = arr != NEVER
+        return ok, np.where(ok, arr - t, -1)
+
+    def fail(self, msg: str) -> None:
+        self.failures.append(msg)
+
+
+def _lookup(k, v, q, missing):
+    q = np.asarray(q, np.uint64)
+    out = np.full(len(q), missing, dtype=v.dtype if len(v) else np.int64)
+    if len(k):
+        i = np.searchsorted(k, q)
+        i = np.minimum(i, len(k) - 1)
+        hit = k[i] == q
+        out[hit] = v[i[hit]]
+    return out
+
+
+# ============================================================================================
+# plans/network
+# ============================================================================================
+
+def pingpong(env: PlanEnv) -> np.ndarray:
+    """plans/network/pingpong.go:16-201: two instances, 100 ms egress latency + 1 Mibit/s each,
+    1-byte ping-pong RTT must be in [200, 215] ms; then 10 ms latency, RTT in [20, 35] ms."""
+    if env.n != 2:
+        raise ValueError("ping-pong needs exactly two instances (pingpong.go:100)")
+    t = env.net.wait_network_initialized(0)
+    # each instance owns its Config (pingpong.go:29-41 runs in two processes)
+    configs = [Config(network="default", enable=True, default=LinkShape(latency=100 * MS, bandwidth=1 << 20),
+                      callback_state="network-configured", routing_policy=DenyAll) for _ in range(2)]
+    rel = [env.net.configure_network(g, configs[g], t) for g in range(2)]
+    t = max(rel)
+    seq, t = env.sync.signal_and_wait("ip-allocation", [0, 1], t, 2)
+    # pingpong.go:57-66: ip = subnet.a.b.(seq>>8 + 1).(seq & 255)
+    base = env.net.get_data_network_ip(0) & 0xFFFF0000
+    rel = []
+    for g in range(2):
+        s = int(seq[g])
+        configs[g].callback_state = "ip-changed"
+        configs[g].ipv4 = IPNet(base | ((((s >> 8) + 1) & 255) << 8) | (s & 255), 15)
+        rel.append(env.net.configure_network(g, configs[g], t))
+    t = max(rel)
+    _, t = env.sync.signal_and_wait("listening", [0, 1], t, 2)
+    env.sync.publish("peers", [0, 1], t, [int_to_ip(env.net.get_data_network_ip(g)) for g in range(2)])
+    _, t = env.sync.signal_and_wait("got-other-addrs", [0, 1], t, 2)
+    env.advance_to(t)
+    # TCP connect from seq 2 to seq 1: SYN / SYN-ACK (+ ACK piggybacked on the first write)
+    dialer = int(np.flatnonzero(seq == 2)[0])
+    ok, _ = env.rpc([dialer], [1 - dialer], TCP_OVERHEAD, TCP_OVERHEAD, env.sim.now, 30 * SECOND)
+    if not ok[0]:
+        env.fail("dial failed")
+        return np.zeros(2, bool)
+    ok = np.ones(2, bool)
+    for test, lo, hi in (("200", 200 * MS, 215 * MS), ("10", 20 * MS, 35 * MS)):
+        if test == "10":
+            for c in configs:
+                c.default.latency = 10 * MS
+                c.callback_state = "latency-reduced"
+            rel = [env.net.configure_network(g, configs[g], env.sim.now) for g in range(2)]
+            env.advance_to(max(rel))
+        rtt = _pingpong_round(env, seq)
+        for g in range(2):
+            if not lo <= rtt[g] <= hi:
+                env.fail(f"instance {g}: expected an RTT between {lo} and {hi}, got {rtt[g]}")
+                ok[g] = False
+        env.rtts = getattr(env, "rtts", []) + [rtt]
+        _, t = env.sync.signal_and_wait("ping-pong-" + test, [0, 1], env.sim.now, 2)
+        env.advance_to(t)
+    return ok
+
+
+def _pingpong_round(env: PlanEnv, seq) -> np.ndarray:
+    """pingpong.go:116-173 over one connection: both write a 0 byte and read the peer's (start);
+    write own id; read the peer's id and echo it; read own id back (end). Returns end - start."""
+    sz = TCP_OVERHEAD + 1
+    now = env.sim.now
+    k = env.send([0, 1], [1, 0], sz, [now, now])
+    arr = env.wait(k, 10 * SECOND)             # arr[0]: 0 -> 1 arrives at 1; arr[1]: at 0
+    start = np.array([arr[1], arr[0]])         # instance g starts after reading the peer's 0
+    kid = env.send([0, 1], [1, 0], sz, start)  # write my id
+    a_id = env.wait(kid, 10 * SECOND)          # a_id[0] = my id (0) at 1, a_id[1] = 1's id at 0
+    got_peer_id = np.array([a_id[1], a_id[0]])
+    echo_t = np.maximum(got_peer_id, start)    # read their id (after my own write), write it back
+    kecho = env.send([0, 1], [1, 0], sz, echo_t)
+    a_echo = env.wait(kecho, 10 * SECOND)      # a_echo[0] = echo of 1's id, arrives at 1
+    back = np.array([a_echo[1], a_echo[0]])
+    end = np.maximum(back, echo_t)             # read my id after echoing theirs
+    if np.any(end == NEVER):
+        env.fail("ping-pong message lost")
+        return np.full(2, -1, np.int64)
+    return end - start
+
+
+def traffic(policy):
+    """plans/network/traffic.go:16-72: an HTTP GET to a host outside the data network must fail
+    under DenyAll and succeed under AllowAll."""
+    def plan(env: PlanEnv) -> np.ndarray:
+        t = env.net.wait_network_initialized(0)
+        cfg = Config(network="default", enable=True, callback_state="network-configured-with-policy",
+                     routing_policy=policy)
+        t = max(env.net.configure_network(g, cfg, t) for g in range(env.n))
+        env.advance_to(t)
+        k = env.send(np.arange(env.n), A.DST_EXTERNAL, TCP_OVERHEAD, env.sim.now)
+        env.step()
+        st = env.status_of(k) & 0x0F
+        reached = st == A.ST_EXTERNAL
+        ok = ~reached if policy == DenyAll else reached
+        for g in np.flatnonzero(~ok):
+            env.fail(f"instance {g}: external request {'succeeded' if reached[g] else 'failed'} under {policy.value}")
+        return ok
+    return plan
+
+
+# ============================================================================================
+# plans/splitbrain
+# ============================================================================================
+
+REGION_A, REGION_B, REGION_C = 0, 1, 2
+
+
+def expect_errors(test_case: str, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """plans/splitbrain/main.go:50-58, vectorised."""
+    if test_case == "accept":
+        return np.zeros(np.broadcast(a, b).shape, bool)
+    return ((a == REGION_A) & (b == REGION_B)) | ((a == REGION_B) & (b == REGION_A))
+
+
+def splitbrain(action: FilterAction):
+    """plans/splitbrain/main.go:60-186: region = SignalEntry("region-select") % 3; region A installs
+    a /32 rule with `action` toward every region-B node; every node then probes every other
+    node (HTTP: request + reply). Failures are expected exactly between A and B."""
+    def plan(env: PlanEnv) -> np.ndarray:
+        n = env.n
+        t = env.net.wait_network_initialized(0)
+        seq = env.sync.signal_entry("region-select", np.arange(n), t)
+        region = (seq.astype(np.int64) % 3)
+        ips = np.array([env.net.get_data_network_ip(g) for g in range(n)], np.int64)
+        env.sync.publish("nodes", np.arange(n), t, list(zip(region.tolist(), ips.tolist())))
+        b_ips = ips[region == REGION_B]
+        for a in np.flatnonzero(region == REGION_A):
+            cfg = Config(network="default", enable=True, callback_state=f"reconfigured{a}", callback_target=1,
+                         rules=[LinkRule(IPNet(int(ip), 32), LinkShape(filter=action)) for ip in b_ips])
+            env.net.configure_network(int(a), cfg, t)
+        _, t = env.sync.signal_and_wait("nodeRoundup", np.arange(n), t, n)
+        env.advance_to(t + 10 * SECOND)   # time.Sleep(10 * time.Second), main.go:145
+        src, dst = np.nonzero(~np.eye(n, dtype=bool))
+        ok_pair, _ = env.rpc(src, dst, TCP_OVERHEAD, TCP_OVERHEAD, env.sim.now, 60 * SECOND)
+        errs = ~ok_pair
+        unexpected = errs & ~expect_errors(env.test_case, region[src], region[dst])
+        env.probe_errors = np.bincount(src[errs], minlength=n)
+        env.region = region
+        ok = np.ones(n, bool)
+        ok[src[unexpected]] = False
+        for g in np.flatnonzero(~ok):
+            env.fail(f"instance {g} (region {region[g]}): unexpected probe failure")
+        _, t = env.sync.signal_and_wait("testcomplete", np.arange(n), env.sim.now, n)
+        return ok
+    return plan
+
+
+# ============================================================================================
+# plans/benchmarks
+# ============================================================================================
+
+def storm(env: PlanEnv) -> np.ndarray:
+    """plans/benchmarks/storm.go:31-197: every instance dials `conn_outgoing` random peers after
+    U[0, conn_delay_ms) ms, SignalAndWait("outgoing-dials-done", N * conn_outgoing), then writes
+    data_size_kb KiB to each connection in 4 KiB writes; SignalAndWait("done writing", N).
+    Dial concurrency limits (concurrent_dials) are not modelled."""
+    n = env.n
+    outgoing = env.int_param("conn_outgoing", 5)
+    delay_ms = env.int_param("conn_delay_ms", 30000)
+    size = env.int_param("data_size_kb", 128) * 1024
+    rng = np.random.default_rng(env.int_param("seed", 0))
+    t = env.net.wait_network_initialized(0)
+    _, t = env.sync.signal_and_wait("listening", np.arange(n), t, n)
+    _, t = env.sync.signal_and_wait("got-other-addrs", np.arange(n), t, n)
+    env.advance_to(t)
+    src = np.repeat(np.arange(n), outgoing)
+    off = rng.integers(1, n, len(src)) if n > 1 else np.zeros(len(src), np.int64)
+    dst = (src + off) % n                                           # rand.Intn over the other nodes
+    t_dial = env.sim.now + rng.integers(0, max(delay_ms, 1), len(src)) * MS
+    ok, rtt = env.rpc(src, dst, TCP_OVERHEAD, TCP_OVERHEAD, t_dial, 30 * SECOND)
+    done = np.where(ok, t_dial + rtt, t_dial)
+    _, t = env.sync.signal_and_wait("outgoing-dials-done", np.flatnonzero(ok) // outgoing, done[ok], n * outgoing)
+    if t < 0:
+        env.fail("outgoing-dials-done never released")
+        return np.zeros(n, bool)
+    env.advance_to(max(t, env.sim.now))
+    chunks = [TCP_CHUNK] * (size // TCP_CHUNK) + ([size % TCP_CHUNK] if size % TCP_CHUNK else [])
+    keys = []
+    now = env.sim.now
+    for c in chunks:
+        keys.append(env.send(src[ok], dst[ok], c + TCP_OVERHEAD, now))
+    env.bytes_sent = int(ok.sum()) * size
+    arr = env.wait(np.concatenate(keys) if keys else np.zeros(0, np.uint64), 3000 * SECOND)
+    _, t = env.sync.signal_and_wait("done writing", np.arange(n), env.sim.now, n)
+    res = np.ones(n, bool)
+    res[src[~ok]] = False
+    if len(arr):
+        lost = np.tile(src[ok], len(chunks))[arr == NEVER]
+        res[lost] = False
+    env.delivered_chunks = int((arr != NEVER).sum())
+    return res
+
+
+def barrier_bench(env: PlanEnv) -> np.ndarray:
+    """plans/benchmarks/benchmarks.go:90-145: for each iteration and percentage p in the Go float
+    loop 0.2, 0.4, ... <= 1.0: SignalAndWait(ready, N), then SignalAndWait(test, max(1, floor(N p)))."""
+    n = env.n
+    iterations = env.int_param("barrier_iterations", 10)
+    t = env.net.wait_network_initialized(0)
+    tests = []
+    p = 0.2
+    while p <= 1.0:        # the same IEEE-754 accumulation as the Go loop
+        tests.append((f"barrier_time_{int(p * 100)}_percent", p))
+        p += 0.2
+    env.barrier_times = {}
+    everyone = np.arange(n)
+    for i in range(1, iterations + 1):
+        for name, p in tests:
+            _, t = env.sync.signal_and_wait(f"ready_{i}_{name}", everyone, t, n)
+            target = int(math.floor(n * p)) or 1
+            _, rel = env.sync.signal_and_wait(f"test_{i}_{name}", everyone, t, target)
+            env.barrier_times.setdefault(name, []).append(rel - t)
+            t = rel
+    return np.ones(n, bool)
+
+
+PLANS = {
+    ("network", "ping-pong"): pingpong,
+    ("network", "traffic-allowed"): traffic(AllowAll),
+    ("network", "traffic-blocked"): traffic(DenyAll),
+    ("splitbrain", "drop"): splitbrain(FilterAction.Drop),
+    ("splitbrain", "reject"): splitbrain(FilterAction.Reject),
+    ("splitbrain", "accept"): splitbrain(FilterAction.Accept),
+    ("benchmarks", "storm"): storm,
+    ("benchmarks", "barrier"): barrier_bench,
+}

@@ -106,9 +106,20 @@ class Simulator:
     def now(self) -> int:
         return int(self.lib.now(self._ctx))
 
+    @property
+    def horizon(self) -> int:
+        """Earliest admissible t_send: the start of the last completed window."""
+        return int(self.lib.horizon(self._ctx))
+
     # ---- network configuration (sidecar.Network) ---------------------------------------------
     def configure_network(self, instance: int, cfg: A.NetworkConfig) -> None:
         self._check(self.lib.configure_network(self._ctx, instance, C.byref(cfg)))
+
+    def configure(self, instance: int, cfg) -> None:
+        """DockerNetwork.ConfigureNetwork for one instance from a testground_amd.network.Config."""
+        c, keep = cfg.to_c()
+        self._check(self.lib.configure_network(self._ctx, int(instance), C.byref(c)))
+        del keep
 
     def set_shape(self, instance: int, shape: A.LinkShape) -> None:
         self._check(self.lib.set_shape(self._ctx, instance, C.byref(shape)))

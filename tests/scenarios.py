@@ -178,3 +178,135 @@ def assert_same(a, b, path="out"):
             raise AssertionError(f"{path}: mismatch at {bad}: {a[bad]} vs {b[bad]}")
     else:
         assert a == b, f"{path}: {a} vs {b}"
+
+
+# ---- sharded runs: contiguous instance ranges per shard, one exchange per window --
+
+def shard_range(n, k, s):
+    return (k * n) // s, ((k + 1) * n) // s
+
+
+def run_random_sharded(make_sim, exchange, world: int, seed: int, n_inst: int = 24, windows: int = 6,
+                       msgs_per_window: int = 300, window_ns: int = 40 * MS, local=None):
+    """run_random's workload split over `world` shards. make_sim(cfg) -> Simulator of one shard;
+    exchange(sims) moves every shard's send blocks to the peers' receive blocks (an all-to-all).
+    local: the shard ids this process runs (default all; one per rank in a multi-process run).
+    Returns (per-shard observables in run_random's structure, per-window global sender arrays)."""
+    rng = np.random.default_rng(seed)
+    local = list(range(world)) if local is None else list(local)
+    sims = [make_sim(SimConfig(n_instances=n_inst, seed=1000 + seed, shard_id=k, n_shards=world,
+                               exchange_cap=4096)) for k in local]
+    outs = [[] for _ in local]
+    srcs = []
+    seqc = np.zeros(n_inst, np.int64)
+    for g in range(n_inst):
+        shp = random_shape(rng)
+        allow = rng.random() < 0.3
+        for s in sims:   # configuration calls go to every shard (replicated tables, owner keeps state)
+            s.set_shape(g, shp)
+            if allow:
+                s.set_policy(g, A.POLICY_ALLOW_ALL)
+    for g in rng.choice(n_inst, size=n_inst // 3, replace=False):
+        rl = []
+        for _ in range(int(rng.integers(1, 6))):
+            tgt = int(rng.integers(0, n_inst))
+            ip = sims[0].get_ip(tgt)
+            plen = int(rng.choice([32, 32, 30, 24, 16, 0]))
+            mask = (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF if plen else 0
+            f = int(rng.choice([A.FILTER_DROP, A.FILTER_REJECT, A.FILTER_ACCEPT]))
+            rl.append(make_rule(f"{int_to_ip(ip & mask)}/{plen}", f))
+        for s in sims:
+            s.add_rules(int(g), rl)
+    t0 = 0
+
+    def window(t_end):
+        for s in sims:
+            s.advance_begin(t_end)
+        exchange(sims)
+        for i, s in enumerate(sims):
+            s.advance_end()
+            outs[i].append(dict(status=s.status(), deliv=s.deliveries(), inbox=s.inbox_offsets()))
+
+    for w in range(windows):
+        if w == windows // 2:
+            for g in rng.choice(n_inst, size=4, replace=False):
+                shp = random_shape(rng)
+                for s in sims:
+                    s.set_shape(int(g), shp)
+            g = int(rng.integers(0, n_inst))
+            ip = sims[0].get_ip(g) + 1000
+            for s in sims:
+                s.set_enabled(g, True, ip=ip)
+                s.set_enabled(int((g + 3) % n_inst), False)
+        n = msgs_per_window
+        src = rng.integers(0, n_inst, n)
+        dst = rng.integers(0, n_inst, n)
+        dst[rng.random(n) < 0.03] = A.DST_EXTERNAL
+        loc = rng.random(n) < 0.02
+        dst[loc] = src[loc]
+        seq = np.zeros(n, np.int64)
+        for i in range(n):
+            seq[i] = seqc[src[i]]
+            seqc[src[i]] += 1
+        size = rng.choice([0, 1, 64, 1024, 4096, 65536], n)
+        t = t0 + np.sort(rng.integers(0, window_ns, n))
+        if rng.random() < 0.5:
+            t[: n // 4] = t0
+        for k, s in zip(local, sims):
+            lo, hi = shard_range(n_inst, k, world)
+            m = (src >= lo) & (src < hi)
+            s.enqueue(src[m], dst[m], seq[m], size[m], t[m])
+        srcs.append(src)
+        t0 += window_ns
+        window(t0)
+    for w in range(3):
+        t0 += 10 * window_ns
+        srcs.append(np.zeros(0, np.int64))
+        window(t0)
+    for i, s in enumerate(sims):
+        outs[i].append(dict(stats=parity_stats(s)))
+        s.close()
+    return outs, srcs
+
+
+def split_single(single, srcs, world: int, n_inst: int = 24):
+    """Single-shard run_random output -> what each shard of a sharded run must report: statuses of
+    its senders (enqueue order), deliveries to its receivers (global inbox order restricted), its
+    local inbox offsets. Statistics are compared as sums over shards."""
+    per = []
+    for k in range(world):
+        lo, hi = shard_range(n_inst, k, world)
+        wins = []
+        for x, src in zip(single[:-1], srcs):
+            m_src = (src >= lo) & (src < hi)
+            d = x["deliv"]
+            m = (d["dst"] >= lo) & (d["dst"] < hi)
+            dk = {f: v[m] for f, v in d.items()}
+            counts = np.bincount(dk["dst"] - lo, minlength=hi - lo) if len(dk["dst"]) else np.zeros(hi - lo, np.int64)
+            inbox = np.r_[0, np.cumsum(counts)].astype(np.uint32)
+            wins.append(dict(status=x["status"][m_src], deliv=dk, inbox=inbox))
+        per.append(wins)
+    return per
+
+
+def assert_sharded_matches(outs, srcs, single, world: int, n_inst: int = 24):
+    want = split_single(single, srcs, world, n_inst)
+    for k in range(world):
+        assert_same(outs[k][:-1], want[k], f"shard{k}")
+    tot = {}
+    for k in range(world):
+        for name, v in outs[k][-1]["stats"].items():
+            tot[name] = tot.get(name, 0) + v
+    assert tot == single[-1]["stats"], (tot, single[-1]["stats"])
+
+
+def memmove_exchange(sims):
+    """In-process all-to-all over host buffers (the oracle's): block p of shard q's send buffer ->
+    block q of shard p's receive buffer."""
+    import ctypes as C
+    S = len(sims)
+    bufs = [s.exchange_buffers() for s in sims]
+    blk = bufs[0][2] // S
+    for q in range(S):
+        for p in range(S):
+            C.memmove(bufs[p][1] + q * blk, bufs[q][0] + p * blk, blk)

@@ -1,0 +1,187 @@
+"""CPU: the reference's own known answers for this path, through the host-side mirrors of its
+interfaces (sidecar.Network, network.Client, sync.Client, api.Runner) over the CPU oracle.
+
+  pkg/sidecar/sidecar_test.go:19-93   initial config, empty-callback error, config pass-through
+  plans/network/pingpong.go:185,195   RTT in [200, 215] ms at 100 ms/side, [20, 35] ms at 10 ms
+  plans/network/traffic.go:46-52      external traffic blocked under DenyAll, allowed under AllowAll
+  plans/splitbrain/main.go:50-58      errors exactly between regions A and B unless "accept"
+  plans/benchmarks/benchmarks.go      barrier ladder (Go float loop 0.2 .. 1.0)
+  plans/benchmarks/storm.go           every dial and write completes without shaping
+"""
+import io
+import tarfile
+
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd import plans as P
+from testground_amd.network import MS, Config, LinkShape
+from testground_amd.runner import LocalMI355XRunner, RunGroup, RunInput
+from testground_amd.sidecar import ERR_NO_CALLBACK, NET_INIT_STATE
+
+
+def env_for(oracle, n, case="", params=None, **kw):
+    return P.PlanEnv(n, seed=1, test_case=case, params=params, binding=oracle, **kw)
+
+
+# ---- pkg/sidecar/sidecar_test.go ---------------------------------------------------------------
+
+def test_network_initialize(oracle):
+    """TestNetworkInitialize: the handler configures the network once at init, and
+    WaitNetworkInitialized returns once every sidecar signalled network-initialized."""
+    env = env_for(oracle, 1)
+    env.net.wait_network_initialized(0)
+    assert len(env.sidecar.network(0).configured) == 1
+    assert env.sync.count(NET_INIT_STATE) == 1
+    assert env.sidecar.network(0).list_active() == ["default"]
+    env.close()
+
+
+def test_network_configured_fails_misconfigured(oracle):
+    """TestNetworkConfiguredFailsMisconfigured: a Config without CallbackState is refused with the
+    SDK's message."""
+    env = env_for(oracle, 1)
+    with pytest.raises(ValueError, match="^" + ERR_NO_CALLBACK + "$"):
+        env.net.configure_network(0, Config(), 0)
+    env.close()
+
+
+def test_network_configured_passes_config_unmodified(oracle):
+    """TestNetworkConfigured: the sidecar passes the config on to the backing network unmodified
+    and the plan's barrier releases once the sidecar signalled the callback state."""
+    env = env_for(oracle, 1)
+    cfg = Config(network="default", enable=True, callback_state="reconfigured",
+                 default=LinkShape(latency=3600 * 10 ** 9))
+    rel = env.net.configure_network(0, cfg, 5)
+    assert rel == 5
+    net = env.sidecar.network(0)
+    assert len(net.configured) == 2
+    assert net.active["default"] == cfg and net.active["default"] is not cfg
+    env.close()
+
+
+def test_unsupported_network(oracle):
+    env = env_for(oracle, 1)
+    with pytest.raises(A.TgsimError) as e:
+        env.net.configure_network(0, Config(network="other", enable=True, callback_state="x"), 0)
+    assert e.value.code == A.EUNSUPPORTED_NETWORK and "unsupported network: other" in str(e.value)
+    env.close()
+
+
+def test_callback_target_defaults_to_all_instances(oracle):
+    env = env_for(oracle, 3)
+    cfg = Config(network="default", enable=True, callback_state="cb")
+    assert env.net.configure_network(0, cfg, 10) == -1        # 1 of 3 sidecars signalled
+    assert env.net.configure_network(1, cfg, 20) == -1
+    assert env.net.configure_network(2, cfg, 30) == 30        # the third releases everyone
+    cfg1 = Config(network="default", enable=True, callback_state="cb1", callback_target=1)
+    assert env.net.configure_network(0, cfg1, 40) == 40
+    env.close()
+
+
+# ---- plans ---------------------------------------------------------------------------------------
+
+def test_pingpong_rtt_windows(oracle):
+    env = env_for(oracle, 2)
+    ok = P.pingpong(env)
+    assert ok.all(), env.failures
+    rtt100, rtt10 = env.rtts
+    assert all(200 * MS <= r <= 215 * MS for r in rtt100)
+    assert all(20 * MS <= r <= 35 * MS for r in rtt10)
+    ips = sorted(env.net.get_data_network_ip(g) & 0xFFFF for g in range(2))
+    assert ips == [0x0101, 0x0102]      # pingpong.go:57-60: x.y.(seq>>8 + 1).seq for seq 1, 2
+    env.close()
+
+
+def test_pingpong_fails_outside_window_with_more_latency(oracle, monkeypatch):
+    """The RTT check is live: 120 ms per side breaks the [200, 215] ms window."""
+    env = env_for(oracle, 2)
+    orig = P.Config
+
+    def patched(**kw):
+        c = orig(**kw)
+        if c.default.latency == 100 * MS:
+            c.default.latency = 120 * MS
+        return c
+    monkeypatch.setattr(P, "Config", patched)
+    ok = P.pingpong(env)
+    assert not ok.all() and any("expected an RTT" in f for f in env.failures)
+    env.close()
+
+
+@pytest.mark.parametrize("case,expect_ok", [("traffic-allowed", True), ("traffic-blocked", True)])
+def test_routing_policy(oracle, case, expect_ok):
+    env = env_for(oracle, 3)
+    ok = P.PLANS[("network", case)](env)
+    assert ok.all() == expect_ok, env.failures
+    env.close()
+
+
+@pytest.mark.parametrize("case", ["drop", "reject", "accept"])
+def test_splitbrain_truth_table(oracle, case):
+    n = 30
+    env = env_for(oracle, n, case)
+    ok = P.PLANS[("splitbrain", case)](env)
+    assert ok.all(), env.failures
+    region = env.region
+    assert list(region) == [(g + 1) % 3 for g in range(n)]   # seq = g + 1 (ties broken by instance)
+    na, nb = (region == 0).sum(), (region == 1).sum()
+    want = np.zeros(n, np.int64)
+    if case != "accept":
+        want[region == 0] = nb
+        want[region == 1] = na
+    assert np.array_equal(env.probe_errors, want)
+    env.close()
+
+
+def test_barrier_bench(oracle):
+    env = env_for(oracle, 50, params={"barrier_iterations": 3})
+    ok = P.barrier_bench(env)
+    assert ok.all()
+    # the Go float loop yields 0.2, 0.4, 0.6000000000000001, 0.8, 1.0
+    assert sorted(env.barrier_times) == sorted(f"barrier_time_{p}_percent" for p in (20, 40, 60, 80, 100))
+    assert all(len(v) == 3 for v in env.barrier_times.values())
+    env.close()
+
+
+def test_storm_completes(oracle):
+    env = env_for(oracle, 20, params={"conn_outgoing": 3, "conn_delay_ms": 1000, "data_size_kb": 10})
+    ok = P.storm(env)
+    assert ok.all(), env.failures
+    assert env.delivered_chunks == 20 * 3 * 3          # 10 KiB in 4 KiB writes = 3 chunks per dial
+    env.close()
+
+
+# ---- api.Runner -----------------------------------------------------------------------------------
+
+def test_runner_contract(oracle):
+    r = LocalMI355XRunner(binding=oracle)
+    assert r.id() == "local:mi355x"
+    assert "exec:go" in r.compatible_builders()
+    assert r.config_type()().window_ns == 1 * MS
+    job = RunInput(run_id="r1", test_plan="splitbrain", test_case="drop", total_instances=12,
+                   groups=[RunGroup("left", 5), RunGroup("right", 7)])
+    out = r.run(job, io.StringIO())
+    assert out.result.outcome == "success"
+    assert {k: (v.total, v.ok) for k, v in out.result.outcomes.items()} == {"left": (5, 5), "right": (7, 7)}
+    buf = io.BytesIO()
+    r.collect_outputs("r1", buf)
+    buf.seek(0)
+    with tarfile.open(fileobj=buf, mode="r:gz") as tar:
+        assert tar.getnames() == ["r1/result.json"]
+
+
+def test_runner_reports_failures(oracle, monkeypatch):
+    r = LocalMI355XRunner(binding=oracle)
+    monkeypatch.setitem(P.PLANS, ("x", "y"), lambda env: np.arange(env.n) % 2 == 0)
+    out = r.run(RunInput("r2", "x", "y", 4, [RunGroup("g", 4)]))
+    assert out.result.outcome == "failure" and out.result.outcomes["g"].ok == 2
+
+
+def test_runner_rejects_unknown_plan(oracle):
+    r = LocalMI355XRunner(binding=oracle)
+    with pytest.raises(ValueError, match="no workload descriptor"):
+        r.run(RunInput("r3", "network", "nope", 2, [RunGroup("g", 2)]))
+    with pytest.raises(ValueError, match="TotalInstances"):
+        r.run(RunInput("r4", "network", "ping-pong", 3, [RunGroup("g", 2)]))
