@@ -30,17 +30,20 @@ MS = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "simulated msgs delivered/sec (100k-inst storm) + % HBM roofline, 1/2/4/8 GPU"
 
-# Algorithmic bytes each kernel class must move per unit of work.
+# Algorithmic bytes each kernel class must move per unit of work; every class
+# below is exactly one kernel, so its HIP-event average agrees with rocprofv3's for that kernel.
 #   k_shape: read the 24 B message + write its 1 B status + write each 32 B copy record
-#   token_bucket: read the 32 B copy + its 8 B (key, index) + write the 32 B departed record
-#   deliveries: read the 32 B record + 8 B (key, index) + write the 32 B delivery (SoA)
-#   k_extract: read + write one 32 B wheel record; k_region_fill: read 32 + 4 B index, write 32 B
+#   k_tb_bucket: per copy, read the 32 B record + its 8 B (key, index), write the 32 B departed record
+#   k_emit_bucket: per delivery, read the 32 B record + 8 B (key, index), write the 32 B SoA delivery
+#   k_extract: read + write one 32 B wheel record; k_region_fill: read 32 + 8 B key/index, write 32 B
+#   k_gen_storm: write the 24 B message
 BYTE_MODELS = {
     "k_shape": lambda d: 25 * d["msgs_in"] + 32 * d["copies"],
-    "token_bucket": lambda d: 72 * d["tb_items"],
-    "deliveries": lambda d: 72 * d["delivered"],
+    "k_tb_bucket": lambda d: 72 * d["tb_items"],
+    "k_emit_bucket": lambda d: 72 * d["delivered"],
     "k_extract": lambda d: 64 * d["extracted"],
-    "k_region_fill": lambda d: 68 * d["inserted"],
+    "k_region_fill": lambda d: 72 * d["inserted"],
+    "k_gen_storm": lambda d: 24 * d["msgs_in"],
 }
 
 
@@ -152,16 +155,24 @@ def main():
             dist.all_to_all_single(recv_t, send_t)
             sim.advance_end()
 
-    # warm-up: also times every kernel class once to find the dominant one
-    sim.profile(None)
+    # warm-up (untimed, unprofiled), then a few probe steps that time every kernel class to find the
+    # dominant one; the timed region carries HIP events around that kernel only
     for r in range(args.warmup):
         step(r)
+    probe = max(3, min(10, args.warmup))
+    sim.profile(None)
+    base_all = sim.profile_read()
+    for r in range(args.warmup, args.warmup + probe):
+        step(r)
     prof = sim.profile_read()
-    warm_kernels = {k: {"avg_us": 1e3 * ms / n, "launches": n} for k, (ms, n) in prof.items() if n}
-    ranked = sorted(((ms, k) for k, (ms, n) in prof.items() if k in BYTE_MODELS and n), reverse=True)
-    dominant = ranked[0][1] if ranked else "deliveries"
+    warm_kernels = {k: {"avg_us": 1e3 * (ms - base_all[k][0]) / (n - base_all[k][1]), "launches": n - base_all[k][1]}
+                    for k, (ms, n) in prof.items() if n > base_all[k][1]}
+    ranked = sorted(((v["avg_us"] * v["launches"], k) for k, v in warm_kernels.items() if k in BYTE_MODELS),
+                    reverse=True)
+    dominant = ranked[0][1] if ranked else "k_emit_bucket"
+    sim.profile([dominant])
     base_prof = sim.profile_read()[dominant]
-    sim.profile([dominant])  # the timed region carries events around the dominant kernel only
+    first = args.warmup + probe
 
     s0 = sim.stats()
     sim_t0 = sim.now
@@ -170,7 +181,7 @@ def main():
     sim.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for r in range(args.warmup, args.warmup + args.steps):
+    for r in range(first, first + args.steps):
         step(r)
     sim.sync()
     torch.cuda.synchronize()
@@ -232,7 +243,7 @@ def main():
                 "bytes_per_launch": bytes_total / max(kern_n, 1),
             },
             "cpu_baseline": cpu,
-            "kernels_warmup": warm_kernels,
+            "kernels_probe": warm_kernels,
         }
         print(json.dumps(line), flush=True)
     sim.close()

@@ -11,7 +11,8 @@ namespace tgsim {
 // Kernel classes timed with HIP events on the ctx stream when profiling is on (tgsim_profile_*).
 enum KernelId : int {
   KID_SHAPE = 0, KID_EXTRACT, KID_TB, KID_EMIT, KID_RADIX_HIST, KID_RADIX_ROWS, KID_RADIX_SCATTER,
-  KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_COUNT
+  KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_BKT_HIST, KID_BKT_SCATTER,
+  KID_BKT_SORT, KID_SEG_REST, KID_COUNT
 };
 extern const char* const kKernelNames[KID_COUNT];
 
@@ -54,6 +55,7 @@ struct Dev {
 
   // record batches and the wheel
   tgsim_record *A = nullptr, *D = nullptr, *L = nullptr, *arena = nullptr;
+  uint32_t *KA = nullptr, *KD = nullptr, *KL = nullptr;  // group-by keys written by the producers
   tgsim_record *xsend = nullptr, *xrecv = nullptr;
   RegionDev* regions = nullptr;
   uint32_t* dirs = nullptr;
@@ -68,6 +70,7 @@ struct Dev {
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;
   uint32_t* medium = nullptr;     // [segK] ids of segments kThreadSeg < len <= kTile
+  uint8_t* deferred = nullptr;    // [kMaxBins] bucket left to the thread/list/large kernels by a fused consumer
   uint32_t* chunk_off = nullptr;
   uint64_t *K1a = nullptr, *K1b = nullptr, *K2a = nullptr, *K2b = nullptr;
   uint32_t *K3a = nullptr, *K3b = nullptr;

@@ -67,6 +67,7 @@ enum { Q_A = 0, Q_D = 1, Q_L = 2, Q_X0 = 3 };  // append queues: TB batch, deliv
 struct DevScalars {
   int64_t T, t_end;                  // current window
   int64_t H;                         // reaction horizon: earliest admissible t_send
+  int64_t base_slot;                 // t_end / slot_ns: timing-wheel slot 0 of this window's insertions
   // ---- per-window block: zeroed by one memset at window start ----
   uint32_t q[Q_X0 + kMaxShards];     // exchange cursors per peer (q[Q_X0 + p]); q[0..2] unused
   uint32_t qpre[3][kNSub + 1];       // A, D, L: prefix over sub-queues (after k_qfinal)

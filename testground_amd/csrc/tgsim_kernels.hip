@@ -19,8 +19,9 @@
 namespace tgsim {
 
 const char* const kKernelNames[KID_COUNT] = {
-    "k_shape", "k_extract", "token_bucket", "deliveries", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
-    "k_keys", "k_bounds", "k_region_fill", "k_gen_storm", "sync_signal", "large_segments"};
+    "k_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
+    "k_keys", "k_bounds", "k_region_fill", "k_gen_storm", "sync_signal", "large_segments",
+    "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest"};
 
 // Times the launches issued while it is alive with a HIP event pair on d.stream (if enabled).
 struct ProfScope {
@@ -113,7 +114,17 @@ struct Queues {
   DevScalars* sc;
   uint32_t* qc;
   tgsim_record *A, *D, *L, *X;
-  uint32_t subcap, xcap;
+  uint32_t* K[3];            // group-by key of each appended record, same physical index (A, D, L)
+  uint32_t subcap, xcap, lo, slots;
+  int64_t slot_ns;
+  // A: local sender; D: local receiver; L: timing-wheel slot relative to this window's end
+  __device__ __forceinline__ uint32_t key_of(int q, const tgsim_record& r) const {
+    if (q == Q_A) return r.src - lo;
+    if (q == Q_D) return r.dst - lo;
+    int64_t s = r.t / slot_ns - sc->base_slot;
+    s = s < 0 ? 0 : (s > (int64_t)slots - 1 ? (int64_t)slots - 1 : s);
+    return (uint32_t)s;
+  }
   // Wave-collective: every lane of the wave calls it; salt must be wave-uniform.
   __device__ __forceinline__ void push(int q, const tgsim_record& r, uint32_t salt) const {
     uint32_t* ctr = nullptr;
@@ -137,8 +148,12 @@ struct Queues {
     }
     const uint32_t pos = wave_append(ctr);
     if (q >= 0) {
-      if (pos < cap) store_rec(buf + pos, r);
-      else atomicOr(&sc->err, eb);
+      if (pos < cap) {
+        store_rec(buf + pos, r);
+        if (q < Q_X0) K[q][(size_t)(buf - (q == Q_A ? A : (q == Q_D ? D : L))) + pos] = key_of(q, r);
+      } else {
+        atomicOr(&sc->err, eb);
+      }
     }
   }
 };
@@ -184,32 +199,44 @@ __device__ __forceinline__ T wave_sum(T v) {
 // window control
 // ============================================================================================
 
-__global__ void k_set_window(DevScalars* sc, int64_t H, int64_t T, int64_t t_end) {
-  sc->H = H;
-  sc->T = T;
-  sc->t_end = t_end;
-}
+__device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t slots, int64_t slot_ns,
+                             uint32_t* plan_start, uint32_t* plan_off, DevScalars* sc, int64_t t_end);
 
-// t_end = release time of a barrier waiter + offset, decided on the device (no host round trip).
-__global__ void k_set_window_barrier(DevScalars* sc, const int64_t* w_release, uint32_t waiter,
-                                     int64_t H, int64_t T, int64_t offset) {
-  const int64_t rel = w_release[waiter];
-  sc->H = H;
-  sc->T = T;
-  if (rel < 0) {
-    atomicOr(&sc->err, ERR_UNRELEASED);
-    sc->t_end = T;
-  } else {
-    const int64_t e = rel + offset;
-    sc->t_end = e < T ? T : e;
+// Window start (one block): the window's end — explicit, a barrier waiter's release + offset
+// (decided on the device, no host round trip), or a device value + offset — then the per-window
+// counters zeroed and the timing-wheel extraction plan of the window.
+enum { WIN_EXPLICIT = 0, WIN_BARRIER = 1, WIN_DEVICE = 2 };
+__global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_t* qc, int mode, int64_t H, int64_t T,
+                                                         int64_t t_end_arg, const int64_t* src, int64_t offset,
+                                                         int64_t slot_ns, RegionDev* regions, const uint32_t* dirs,
+                                                         uint32_t slots, uint32_t* plan_start, uint32_t* plan_off) {
+  __shared__ int64_t s_tend;
+  for (uint32_t i = threadIdx.x; i < 3u * kNSub * 32u; i += kBlock) qc[i] = 0;
+  uint32_t* w = sc->q;  // the per-window block [q, err) of DevScalars
+  const uint32_t nw = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
+  for (uint32_t i = threadIdx.x; i < nw; i += kBlock) w[i] = 0;
+  if (threadIdx.x == 0) {
+    int64_t e = t_end_arg;
+    if (mode == WIN_BARRIER) {
+      const int64_t rel = *src;
+      if (rel < 0) {
+        atomicOr(&sc->err, ERR_UNRELEASED);
+        e = T;
+      } else {
+        e = rel + offset;
+      }
+    } else if (mode == WIN_DEVICE) {
+      e = *src + offset;
+    }
+    e = e < T ? T : e;
+    sc->H = H;
+    sc->T = T;
+    sc->t_end = e;
+    sc->base_slot = e / slot_ns;
+    s_tend = e;
   }
-}
-
-__global__ void k_set_window_dev(DevScalars* sc, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset) {
-  const int64_t e = *t_end_dev + offset;
-  sc->H = H;
-  sc->T = T;
-  sc->t_end = e < T ? T : e;
+  __syncthreads();
+  plan_regions(regions, dirs, slots, slot_ns, plan_start, plan_off, sc, s_tend);
 }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
@@ -220,8 +247,8 @@ __global__ void k_reset_tb(int64_t* X, const uint32_t* locals, uint32_t n) {
 }
 
 // Close a sharded queue for reading: prefix over its sub-queues (one wave).
-__global__ void k_qfinal(DevScalars* sc, const uint32_t* qc, int q, uint32_t subcap) {
-  const uint32_t s = threadIdx.x;  // 64 threads
+__device__ __forceinline__ void queue_final(DevScalars* sc, const uint32_t* qc, int q, uint32_t subcap) {
+  const uint32_t s = threadIdx.x;  // one wave
   const uint32_t raw = qc[(((uint32_t)q * kNSub) + s) << 5];
   if (raw > subcap) atomicOr(&sc->err, q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L));
   const uint32_t c = raw < subcap ? raw : subcap;
@@ -233,6 +260,10 @@ __global__ void k_qfinal(DevScalars* sc, const uint32_t* qc, int q, uint32_t sub
   }
   sc->qpre[q][s] = x - c;
   if (s == 63) { sc->qpre[q][kNSub] = x; sc->qn[q] = x; }
+}
+
+__global__ void k_qfinal(DevScalars* sc, const uint32_t* qc, int q, uint32_t subcap) {
+  queue_final(sc, qc, q, subcap);
 }
 
 // ============================================================================================
@@ -434,14 +465,13 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
 // timing wheel: plan (which slot prefixes of which live regions are due), extract, insert
 // ============================================================================================
 
-__global__ __launch_bounds__(kBlock) void k_plan(RegionDev* regions, const uint32_t* dirs, uint32_t slots,
-                                                 int64_t slot_ns, uint32_t* plan_start,
-                                                 uint32_t* plan_off, DevScalars* sc) {
+// The due slot prefix of every live region (records with time < t_end), and region retirement.
+__device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t slots, int64_t slot_ns,
+                             uint32_t* plan_start, uint32_t* plan_off, DevScalars* sc, int64_t t_end) {
   __shared__ uint32_t part[kBlock];
   __shared__ uint32_t carry;
   const uint32_t tid = threadIdx.x;
   const uint32_t tail = sc->reg_tail, head = sc->reg_head, nlive = head - tail;
-  const int64_t t_end = sc->t_end;
   const int64_t kabs = t_end > 0 ? (t_end - 1) / slot_ns : -1;
   if (tid == 0) carry = 0;
   __syncthreads();
@@ -517,7 +547,7 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
 }
 
 // Allocate this window's region in the arena ring (one thread).
-__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, int64_t slot_ns) {
+__device__ void region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, int64_t slot_ns) {
   const uint32_t n = sc->qn[Q_L];
   if (sc->reg_head - sc->reg_tail >= (uint32_t)kMaxRegions) {
     atomicOr(&sc->err, ERR_REGIONS);
@@ -549,6 +579,10 @@ __global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_
   sc->arena_used += n;
   if (sc->reg_head - sc->reg_tail == 1) sc->arena_tail = off;
   sc->ins_off = off;
+}
+
+__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, int64_t slot_ns) {
+  region_alloc(sc, regions, cap_arena, slot_ns);
 }
 
 __global__ __launch_bounds__(kBlock) void k_region_fill(const tgsim_record* L, const uint32_t* keys,
@@ -760,6 +794,296 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const u
 }
 
 // ============================================================================================
+// bucketed group-by (unstable): the batch is partitioned on the bucket b = key >> bs (<= 2048
+// buckets: per-block LDS histograms, one scan per bucket row, LDS-atomic ranks in the scatter),
+// then one workgroup per bucket counting-sorts its <= 2^bs keys in LDS and writes the key-grouped
+// (keys, vals), the segment offsets and the medium / large segment lists. Four launches and no
+// per-digit ballot loop; order inside a segment is arbitrary, which is safe because every consumer
+// re-sorts a segment by a key that is unique per item.
+// ============================================================================================
+
+constexpr int kBktMaxKeyBits = 13;  // keys per bucket <= 8192 (32 KB of LDS counters)
+
+// Input of a partition pass: a sharded record queue whose keys the producers wrote beside the
+// records (Queues::key_of; block b covers a quarter of sub-queue b / 4, so no index search), or a
+// precomputed (keys, vals) array (mode 3).
+struct BktSrc {
+  const uint32_t* keys;      // physical-index keys of queue q, or mode-3 keys
+  const uint32_t* vals;      // mode 3 only
+  const uint32_t* qc;        // sub-queue counters
+  int q, mode;
+  uint32_t subcap;
+  const uint32_t* n_ptr;     // mode 3: element count
+  uint32_t cap;
+  RegionDev* regions;        // q == Q_L: the window's wheel region is allocated by the first block
+  uint64_t cap_arena;
+  int64_t slot_ns;
+};
+
+static_assert(kRadixBlocks == 4 * kNSub, "partition blocks map onto sub-queue quarters");
+
+// This block's element range [start, end) in the physical index space of the source.
+__device__ __forceinline__ void bkt_block_range(const BktSrc& s, uint32_t& start, uint32_t& end) {
+  if (s.mode == 3) {
+    radix_range(clamp_n(s.n_ptr, s.cap), start, end);
+    return;
+  }
+  const uint32_t sub = blockIdx.x >> 2, part = blockIdx.x & 3;
+  uint32_t c = s.qc[((uint32_t)s.q * kNSub + sub) << 5];
+  c = c < s.subcap ? c : s.subcap;
+  start = sub * s.subcap + (uint32_t)(((uint64_t)c * part) >> 2);
+  end = sub * s.subcap + (uint32_t)(((uint64_t)c * (part + 1)) >> 2);
+}
+
+constexpr int kBktUnroll = 8;
+
+// pass 1: per-block bucket histogram. The first block also closes the queue (prefix over its
+// sub-queues, totals, overflow bit: the former k_qfinal) and, for the wheel batch, allocates the
+// window's region (the former k_region_alloc).
+__global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, int bs, uint32_t B,
+                                                     uint32_t* hist) {
+  __shared__ uint32_t h[kMaxBins];
+  for (uint32_t d = threadIdx.x; d < B; d += kBlock) h[d] = 0;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
+    if (src.mode != 3) {
+      if (threadIdx.x < kNSub) queue_final(sc, src.qc, src.q, src.subcap);
+      if (src.q == Q_L) {
+        __syncthreads();
+        if (threadIdx.x == 0) region_alloc(sc, src.regions, src.cap_arena, src.slot_ns);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t start, end;
+  bkt_block_range(src, start, end);
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
+    uint32_t k[kBktUnroll];
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = j < end ? src.keys[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u)
+      if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[k[u] >> bs], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
+}
+
+// Bucket bases for this block: exclusive scan of the bucket totals + this block's offset in each.
+__device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, const uint32_t* tot, uint32_t* base,
+                                          uint32_t* part) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (B + kBlock - 1) / kBlock;
+  const uint32_t d0 = tid * per;
+  uint32_t s = 0;
+  for (uint32_t k = 0; k < per && d0 + k < B; ++k) s += tot[d0 + k];
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - s;
+  for (uint32_t k = 0; k < per && d0 + k < B; ++k) {
+    base[d0 + k] = run + (hist ? hist[(d0 + k) * kRadixBlocks + blockIdx.x] : 0u);
+    run += tot[d0 + k];
+  }
+  __syncthreads();
+}
+
+// pass 2: scatter (key, physical index) into bucket order (kout, vout); ranks from LDS atomics.
+__global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
+                                                        const uint32_t* hist, const uint32_t* tot) {
+  __shared__ uint32_t base[kMaxBins];
+  __shared__ uint32_t part[kBlock];
+  bkt_bases(B, hist, tot, base, part);
+  uint32_t start, end;
+  bkt_block_range(src, start, end);
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
+    uint32_t k[kBktUnroll], v[kBktUnroll];
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = j < end ? src.keys[j] : 0xFFFFFFFFu;
+      v[u] = src.mode == 3 ? (j < end ? src.vals[j] : 0u) : j;
+    }
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      if (k[u] == 0xFFFFFFFFu) continue;
+      const uint32_t pos = atomicAdd(&base[k[u] >> bs], 1u);
+      kout[pos] = k[u];
+      vout[pos] = v[u];
+    }
+  }
+}
+
+// pass 3 pieces. bkt_count_keys: the bucket's start / size (sum of the totals before it) and the
+// exclusive offsets of its keys in cnt[] (relative to the bucket start); returns the longest segment.
+struct BktHead { uint32_t start, nb, k0, nk; };
+
+__device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, int bs, uint32_t K, const uint32_t* tot,
+                                                   uint32_t* cnt, uint32_t* part, BktHead& h) {
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  h.k0 = b << bs;
+  h.nk = min(K - h.k0, 1u << bs);
+  uint32_t s = 0;
+  for (uint32_t d = tid; d < b; d += kBlock) s += tot[d];
+  part[tid] = s;
+  for (uint32_t i = tid; i < h.nk; i += kBlock) cnt[i] = 0;
+  __syncthreads();
+  for (uint32_t o = kBlock / 2; o > 0; o >>= 1) {
+    if (tid < o) part[tid] += part[tid + o];
+    __syncthreads();
+  }
+  h.start = part[0];
+  h.nb = tot[b];
+  __syncthreads();
+  for (uint32_t j = tid; j < h.nb; j += kBlock) atomicAdd(&cnt[kin[h.start + j] - h.k0], 1u);
+  __syncthreads();
+  const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = tid * per;
+  uint32_t sum = 0, mx = 0;
+  for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
+    sum += cnt[i0 + i];
+    mx = max(mx, cnt[i0 + i]);
+  }
+  part[tid] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - sum;
+  for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
+    const uint32_t len = cnt[i0 + i];
+    cnt[i0 + i] = run;
+    run += len;
+  }
+  __syncthreads();
+  // block max of the segment lengths (part[] is free again)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+  if (lane_id() == 0) part[tid >> 6] = mx;
+  __syncthreads();
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) m = max(m, part[w]);
+  __syncthreads();
+  return m;
+}
+
+// Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
+// medium / large segment lists.
+__device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
+                                                const BktHead& h, uint32_t* off, uint32_t* off2,
+                                                uint32_t thread_max, uint32_t* medium, LargeSeg* large,
+                                                DevScalars* sc) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < h.nk; i += kBlock) {
+    const uint32_t a = cnt[i];
+    const uint32_t len = (i + 1 < h.nk ? cnt[i + 1] : h.nb) - a;
+    const uint32_t k = h.k0 + i, run = h.start + a;
+    off[k] = run;
+    if (off2) off2[k] = run;
+    if (len > (uint32_t)kTile) {
+      const uint32_t li = atomicAdd(&sc->n_large, 1u);
+      LargeSeg L;
+      L.seg = k; L.start = run; L.len = len; L.pad = 0;
+      large[li] = L;
+      atomicMax(&sc->max_large, len);
+    } else if (thread_max && len > thread_max) {
+      medium[atomicAdd(&sc->n_medium, 1u)] = k;
+    }
+  }
+  if (blockIdx.x == B - 1 && tid == 0) {
+    off[K] = h.start + h.nb;
+    if (off2) off2[K] = h.start + h.nb;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < h.nb; j += kBlock) {
+    const uint32_t k = kin[h.start + j];
+    const uint32_t pos = h.start + atomicAdd(&cnt[k - h.k0], 1u);
+    kout[pos] = k;
+    vout[pos] = vin[h.start + j];
+  }
+}
+
+// pass 3: one workgroup per bucket, global form only (signals, and > 2^bs-key fallbacks).
+__global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                     uint32_t* vout, int bs, uint32_t B, uint32_t K,
+                                                     const uint32_t* tot, uint32_t* off, uint32_t* off2,
+                                                     uint32_t thread_max, uint32_t* medium, LargeSeg* large,
+                                                     DevScalars* sc) {
+  __shared__ uint32_t cnt[1u << kBktMaxKeyBits];
+  __shared__ uint32_t part[kBlock];
+  BktHead h;
+  bkt_count_keys(kin, bs, K, tot, cnt, part, h);
+  bkt_emit_global(kin, vin, kout, vout, B, K, cnt, h, off, off2, thread_max, medium, large, sc);
+}
+
+// Wheel insert with buckets = slots (slots <= kMaxBins): records are copied straight from the L
+// batch into this window's arena region in slot order, and the slot directory is the scan. The
+// first block also closes the window's counters (the former k_finish).
+__global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
+                                                          tgsim_record* arena, uint32_t* dirs, uint32_t slots,
+                                                          const uint32_t* hist, const uint32_t* tot) {
+  __shared__ uint32_t base[kMaxBins];
+  __shared__ uint32_t part[kBlock];
+  const uint64_t off = sc->ins_off;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {
+      const uint32_t n = sc->qn[Q_D];
+      sc->n_out = n;
+      sc->st[ST_DELIVERED] += n;
+      sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
+      sc->st[ST_EXTRACTED] += sc->n_extract;
+      sc->st[ST_INSERTED] += sc->qn[Q_L];
+    }
+    if (off != ~0ull) {
+      bkt_bases(slots, nullptr, tot, base, part);
+      const uint32_t dir = (sc->reg_head - 1) % kMaxRegions;
+      for (uint32_t s = threadIdx.x; s < slots; s += kBlock) dirs[(size_t)dir * (slots + 1) + s] = base[s];
+      if (threadIdx.x == 0) dirs[(size_t)dir * (slots + 1) + slots] = sc->qn[Q_L];
+      __syncthreads();
+    }
+  }
+  if (off == ~0ull) return;  // region allocation failed (error bit set)
+  bkt_bases(slots, hist, tot, base, part);
+  uint32_t start, end;
+  bkt_block_range(src, start, end);
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * 4) {
+    uint32_t k[4];
+    uint4 ra[4], rb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = 0xFFFFFFFFu;
+      if (j < end) {
+        k[u] = src.keys[j];
+        const uint4* p = reinterpret_cast<const uint4*>(L + j);
+        ra[u] = p[0];
+        rb[u] = p[1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k[u] == 0xFFFFFFFFu) continue;
+      const uint32_t pos = atomicAdd(&base[k[u]], 1u);
+      uint4* q = reinterpret_cast<uint4*>(arena + off + pos);
+      q[0] = ra[u];
+      q[1] = rb[u];
+    }
+  }
+}
+
+// ============================================================================================
 // segmented sorts: LDS rank sort (short segments) / bitonic (up to kTile) per span, and a
 // chunk sort + merge path for segments longer than kTile
 // ============================================================================================
@@ -889,10 +1213,10 @@ __device__ __forceinline__ void net_sort(uint64_t (&k1)[M], uint64_t (&k2)[M], u
 // Segment bounds of the calling thread for the one-thread-per-segment kernels (0 = not mine) and
 // the block's largest such segment.
 __device__ __forceinline__ uint32_t thread_seg(const uint32_t* off, uint32_t K, uint32_t seg, uint32_t& a,
-                                               uint32_t* s_max) {
+                                               uint32_t* s_max, const uint8_t* deferred = nullptr, int bs = 0) {
   uint32_t len = 0;
   a = 0;
-  if (seg < K) {
+  if (seg < K && (!deferred || deferred[seg >> bs])) {  // keys of fused buckets are already done
     a = off[seg];
     len = off[seg + 1] - a;
     if (len > (uint32_t)kThreadSeg) len = 0;
@@ -1297,8 +1621,12 @@ __device__ __forceinline__ void tb_thread_body(const TBPolicy& p, const uint32_t
       rec.meta |= TGSIM_F_STAGE_D;
       const bool isD = code[u] == Q_D;
       const uint32_t pos = isD ? pD++ : pL++;
-      if (pos < Q.subcap) store_rec((isD ? bD : bL) + pos, rec);
-      else atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
+      if (pos < Q.subcap) {
+        store_rec((isD ? bD : bL) + pos, rec);
+        Q.K[isD ? Q_D : Q_L][(size_t)sub * Q.subcap + pos] = Q.key_of(isD ? Q_D : Q_L, rec);
+      } else {
+        atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
+      }
     }
   }
   if (sm.any_x) {  // cross-shard copies (S > 1): per-item wave appends onto the peer blocks
@@ -1318,12 +1646,12 @@ __device__ __forceinline__ void tb_thread_body(const TBPolicy& p, const uint32_t
 }
 
 __global__ __launch_bounds__(kBlock) void k_tb_thread(TBPolicy p, const uint32_t* vals, const uint32_t* off,
-                                                      uint32_t K) {
+                                                      uint32_t K, const uint8_t* deferred, int bs) {
   __shared__ TBSmem sm;
   const uint32_t sl = blockIdx.x * kBlock + threadIdx.x;
   if (threadIdx.x == 0) sm.any_x = 0;
   uint32_t a;
-  const uint32_t len = thread_seg(off, K, sl, a, &sm.max_len);
+  const uint32_t len = thread_seg(off, K, sl, a, &sm.max_len, deferred, bs);
   const uint32_t M = sm.max_len;
   if (M == 0) return;  // block-uniform
   if (M <= 4) tb_thread_body<4>(p, vals, sl, a, len, sm);
@@ -1405,12 +1733,12 @@ __device__ __forceinline__ void emit_thread_body(const EmitPolicy& p, const uint
 // One receiver per thread (<= kThreadSeg deliveries): sort in registers; the block's inbox range
 // (contiguous: consecutive receivers) is staged in LDS and written out coalesced.
 __global__ __launch_bounds__(kBlock) void k_emit_thread(EmitPolicy p, const uint32_t* vals, const uint32_t* off,
-                                                        uint32_t K) {
+                                                        uint32_t K, const uint8_t* deferred, int bs) {
   __shared__ uint32_t s_max;
   __shared__ uint32_t stage[kStage];
   const uint32_t seg = blockIdx.x * kBlock + threadIdx.x;
   uint32_t a;
-  const uint32_t len = thread_seg(off, K, seg, a, &s_max);
+  const uint32_t len = thread_seg(off, K, seg, a, &s_max, deferred, bs);
   const uint32_t M = s_max;
   if (M == 0) return;  // block-uniform
   const uint32_t s0 = blockIdx.x * kBlock, s1 = min(s0 + (uint32_t)kBlock, K);
@@ -1443,6 +1771,129 @@ __global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const Large
     const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
     for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock) p.write(L.start + j, K3[L.start + j]);
   }
+}
+
+// ============================================================================================
+// fused bucket consumers: one workgroup per bucket of <= 2^9 keys finishes the group-by in LDS
+// (counting sort of the bucket's item list) and runs the token bucket / the delivery emit on it
+// directly, one key per thread. A bucket with more than kBktCap items or a segment longer than
+// kThreadSeg is written out in key order instead (bkt_emit_global) and flagged in deferred[], for
+// the thread / list / large-segment kernels to finish.
+// ============================================================================================
+
+constexpr int kBktCap = 4096;         // items of one bucket held in LDS on the fused path
+constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
+
+template <bool kStage>
+struct BktFusedSmem {
+  uint32_t cnt[1u << kBktFusedKeyBits];
+  uint32_t idx[kBktCap];                  // the bucket's item list, grouped by key
+  uint32_t stage[kStage ? kBktCap : 1];   // emit: sorted item of each output position
+  uint32_t part[kBlock];
+  uint32_t rmax;
+  TBSmem tb;
+};
+
+// Fast-path check + LDS grouping; returns true if the bucket is handled in LDS. The fused
+// consumers are launched only with bs <= kBktFusedKeyBits.
+template <class SM>
+__device__ __forceinline__ bool bkt_fused_prologue(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                   uint32_t* vout, int bs, uint32_t B, uint32_t K,
+                                                   const uint32_t* tot, uint32_t* off, uint32_t* off2,
+                                                   uint32_t* medium, LargeSeg* large, DevScalars* sc,
+                                                   uint8_t* deferred, SM& sm, BktHead& h) {
+  const uint32_t maxlen = bkt_count_keys(kin, bs, K, tot, sm.cnt, sm.part, h);
+  const bool fast = h.nb <= (uint32_t)kBktCap && maxlen <= (uint32_t)kThreadSeg;
+  if (threadIdx.x == 0) deferred[blockIdx.x] = fast ? 0 : 1;
+  if (!fast) {
+    bkt_emit_global(kin, vin, kout, vout, B, K, sm.cnt, h, off, off2, kThreadSeg, medium, large, sc);
+    return false;
+  }
+  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {
+    const uint32_t k = kin[h.start + j];
+    sm.idx[atomicAdd(&sm.cnt[k - h.k0], 1u)] = vin[h.start + j];
+  }
+  __syncthreads();  // cnt[i] is now the END of key i's run: start(i) = i ? cnt[i-1] : 0
+  return true;
+}
+
+// Per round of kBlock keys: the calling thread's key run in sm.idx, and the block's longest run.
+template <class SM>
+__device__ __forceinline__ uint32_t bkt_round(SM& sm, const BktHead& h, uint32_t i, uint32_t& a, uint32_t& M) {
+  uint32_t len = 0;
+  a = 0;
+  if (i < h.nk) {
+    a = i ? sm.cnt[i - 1] : 0u;
+    len = sm.cnt[i] - a;
+  }
+  if (threadIdx.x == 0) { sm.rmax = 0; sm.tb.any_x = 0; }
+  __syncthreads();
+  if (len) atomicMax(&sm.rmax, len);
+  __syncthreads();
+  M = sm.rmax;
+  return len;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, const uint32_t* kin, const uint32_t* vin,
+                                                      uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
+                                                      uint32_t K, const uint32_t* tot, uint32_t* off,
+                                                      uint32_t* medium, LargeSeg* large, DevScalars* sc,
+                                                      uint8_t* deferred) {
+  __shared__ BktFusedSmem<false> sm;
+  BktHead h;
+  if (!bkt_fused_prologue(kin, vin, kout, vout, bs, B, K, tot, off, nullptr, medium, large, sc, deferred, sm, h))
+    return;
+  for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
+    uint32_t a, M;
+    const uint32_t i = r * kBlock + threadIdx.x;
+    const uint32_t len = bkt_round(sm, h, i, a, M);
+    if (M == 0) continue;  // block-uniform
+    const uint32_t sl = h.k0 + i;
+    if (M <= 4) tb_thread_body<4>(p, sm.idx, sl, a, len, sm.tb);
+    else if (M <= 8) tb_thread_body<8>(p, sm.idx, sl, a, len, sm.tb);
+    else tb_thread_body<16>(p, sm.idx, sl, a, len, sm.tb);
+    __syncthreads();
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void emit_stage_body(const EmitPolicy& p, const uint32_t* list, uint32_t seg, uint32_t a,
+                                                uint32_t len, uint32_t* stage) {
+  uint64_t k1[M], k2[M];
+  uint32_t k3[M];
+  thread_keys<EmitPolicy, M>(p, list, seg, a, len, k1, k2, k3);
+#pragma unroll
+  for (int u = 0; u < M; ++u)
+    if ((uint32_t)u < len) stage[a + u] = k3[u];
+}
+
+__global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, const uint32_t* kin, const uint32_t* vin,
+                                                        uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
+                                                        uint32_t K, const uint32_t* tot, uint32_t* off,
+                                                        uint32_t* off2, uint32_t* medium, LargeSeg* large,
+                                                        DevScalars* sc, uint8_t* deferred) {
+  __shared__ BktFusedSmem<true> sm;
+  BktHead h;
+  if (!bkt_fused_prologue(kin, vin, kout, vout, bs, B, K, tot, off, off2, medium, large, sc, deferred, sm, h))
+    return;
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
+    const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
+    off[h.k0 + i] = o;
+    off2[h.k0 + i] = o;
+  }
+  if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
+  for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
+    uint32_t a, M;
+    const uint32_t i = r * kBlock + threadIdx.x;
+    const uint32_t len = bkt_round(sm, h, i, a, M);
+    if (M == 0) continue;
+    const uint32_t seg = h.k0 + i;
+    if (M <= 4) emit_stage_body<4>(p, sm.idx, seg, a, len, sm.stage);
+    else if (M <= 8) emit_stage_body<8>(p, sm.idx, seg, a, len, sm.stage);
+    else emit_stage_body<16>(p, sm.idx, seg, a, len, sm.stage);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) p.write(h.start + j, sm.stage[j]);  // coalesced SoA
 }
 
 // ============================================================================================
@@ -1717,23 +2168,23 @@ static hipError_t reset_window(Dev& d) {
   return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
 }
 
+static hipError_t window_start(Dev& d, int mode, int64_t H, int64_t T, int64_t t_end, const int64_t* src,
+                               int64_t offset) {
+  hipLaunchKernelGGL(k_window_start, dim3(1), dim3(kBlock), 0, d.stream, d.sc, d.qc, mode, H, T, t_end, src, offset,
+                     d.slot_ns, d.regions, d.dirs, d.slots, d.plan_start, d.plan_off);
+  return hipGetLastError();
+}
+
 hipError_t launch_set_window(Dev& d, int64_t H, int64_t T, int64_t t_end) {
-  hipLaunchKernelGGL(k_set_window, dim3(1), dim3(1), 0, d.stream, d.sc, H, T, t_end);
-  TG_CHECK(hipGetLastError());
-  return reset_window(d);
+  return window_start(d, WIN_EXPLICIT, H, T, t_end, nullptr, 0);
 }
 
 hipError_t launch_set_window_barrier(Dev& d, int64_t H, int64_t T, uint32_t waiter, int64_t offset_ns) {
-  hipLaunchKernelGGL(k_set_window_barrier, dim3(1), dim3(1), 0, d.stream, d.sc, d.w_release, waiter, H, T,
-                     offset_ns);
-  TG_CHECK(hipGetLastError());
-  return reset_window(d);
+  return window_start(d, WIN_BARRIER, H, T, 0, d.w_release + waiter, offset_ns);
 }
 
 hipError_t launch_set_window_dev(Dev& d, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset_ns) {
-  hipLaunchKernelGGL(k_set_window_dev, dim3(1), dim3(1), 0, d.stream, d.sc, H, T, t_end_dev, offset_ns);
-  TG_CHECK(hipGetLastError());
-  return reset_window(d);
+  return window_start(d, WIN_DEVICE, H, T, 0, t_end_dev, offset_ns);
 }
 
 hipError_t storm_local_release(Dev& d, uint32_t n) {
@@ -1760,6 +2211,7 @@ static inline unsigned grid_for(uint64_t n) {
 static Queues make_queues(Dev& d) {
   Queues Q;
   Q.sc = d.sc; Q.qc = d.qc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
+  Q.K[0] = d.KA; Q.K[1] = d.KD; Q.K[2] = d.KL; Q.lo = d.lo; Q.slots = d.slots; Q.slot_ns = d.slot_ns;
   return Q;
 }
 
@@ -1811,6 +2263,62 @@ static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, ui
   return hipGetLastError();
 }
 
+// Bucket shift: <= 2048 buckets of <= 2^kBktMaxKeyBits keys, 128 keys per bucket where possible.
+static int bkt_shift(uint32_t K) {
+  const int bits = bits_for(K);
+  return std::max(bits - kMaxDigitBits, std::min(7, bits));
+}
+
+static int bkt_shift_fused(uint32_t K) {  // 256 keys per bucket: one key per thread of the fused consumers
+  const int bits = bits_for(K);
+  return std::max(bits - kMaxDigitBits, std::min(8, bits));
+}
+
+// Passes 1-2 of the bucketed group-by: (keys1, vals1) in bucket order, bucket totals in d.tot.
+static hipError_t bkt_partition(Dev& d, const BktSrc& src, int bs, uint32_t B) {
+  {
+    ProfScope ps_(d, KID_BKT_HIST);
+    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bs, B, d.hist);
+  }
+  {
+    ProfScope ps_(d, KID_RADIX_ROWS);
+    hipLaunchKernelGGL(k_radix_rows, dim3(B), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+  }
+  {
+    ProfScope ps_(d, KID_BKT_SCATTER);
+    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bs, B,
+                       d.hist, d.tot);
+  }
+  return hipGetLastError();
+}
+
+// Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
+// d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
+static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t thread_max, uint32_t* off2,
+                               uint32_t** keys, uint32_t** vals) {
+  const int bs = bkt_shift(K);
+  if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
+  const uint32_t B = (K + (1u << bs) - 1) >> bs;
+  TG_CHECK(bkt_partition(d, src, bs, B));
+  {
+    ProfScope ps_(d, KID_BKT_SORT);
+    hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bs, B, K,
+                       d.tot, d.seg_off, off2, thread_max, d.medium, d.large, d.sc);
+  }
+  TG_CHECK(hipGetLastError());
+  *keys = d.keys0;
+  *vals = d.vals0;
+  return hipSuccess;
+}
+
+static BktSrc bkt_queue(Dev& d, int q) {
+  BktSrc s;
+  s.keys = q == Q_A ? d.KA : (q == Q_D ? d.KD : d.KL);
+  s.vals = nullptr; s.qc = d.qc; s.q = q; s.mode = q; s.subcap = d.subcap; s.n_ptr = nullptr; s.cap = d.cap_rec;
+  s.regions = d.regions; s.cap_arena = d.cap_arena; s.slot_ns = d.slot_ns;
+  return s;
+}
+
 // Sort the large segments (if any) into (K1,K2,K3) scratch; returns which buffer holds the result.
 template <class P>
 static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uint32_t* vals, bool* any,
@@ -1838,23 +2346,30 @@ static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uin
 }
 
 static hipError_t run_token_bucket(Dev& d) {
-  TG_CHECK(qfinal(d, Q_A));
-  uint32_t* nA = &d.sc->qn[Q_A];
-  {
-    ProfScope psk_(d, KID_KEYS);
-    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.A, (int)Q_A, d.subcap, 0, d.lo,
-                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
-  }
-  uint32_t *keys, *vals;
-  TG_CHECK(group_by(d, nA, d.nloc, &keys, &vals));
-  TG_CHECK(bounds(d, keys, nA, d.nloc, kThreadSeg));
   TBPolicy p;
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
+  const BktSrc src = bkt_queue(d, Q_A);
+  const int bs = bkt_shift_fused(d.nloc);
+  const uint8_t* deferred = nullptr;
+  uint32_t *keys = d.keys0, *vals = d.vals0;
+  if (bs <= kBktFusedKeyBits) {
+    // partition by sender bucket, then one workgroup per bucket groups and token-buckets in LDS
+    const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
+    TG_CHECK(bkt_partition(d, src, bs, B));
+    {
+      ProfScope ps_(d, KID_TB);
+      hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs,
+                         B, d.nloc, d.tot, d.seg_off, d.medium, d.large, d.sc, d.deferred);
+    }
+    deferred = d.deferred;
+  } else {
+    TG_CHECK(group_by_bkt(d, src, d.nloc, kThreadSeg, nullptr, &keys, &vals));
+  }
   {
-    ProfScope ps_(d, KID_TB);
+    ProfScope ps_(d, KID_SEG_REST);
     hipLaunchKernelGGL(k_tb_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
-                       d.seg_off, d.nloc);
+                       d.seg_off, d.nloc, deferred, bs);
     hipLaunchKernelGGL(k_seg_list<TBPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
                        d.medium, d.sc);
   }
@@ -1871,9 +2386,7 @@ static hipError_t run_token_bucket(Dev& d) {
 }
 
 hipError_t window_begin(Dev& d, uint32_t n_staged) {
-  Queues Q = make_queues(d);
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(kBlock), 0, d.stream, d.regions, d.dirs, d.slots, d.slot_ns,
-                     d.plan_start, d.plan_off, d.sc);
+  Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
   {
     ProfScope ps_(d, KID_EXTRACT);
     hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
@@ -1899,25 +2412,29 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
 }
 
 static hipError_t run_deliveries(Dev& d) {
-  TG_CHECK(qfinal(d, Q_D));
-  uint32_t* nD = &d.sc->qn[Q_D];
-  {
-    ProfScope psk_(d, KID_KEYS);
-    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.D, (int)Q_D, d.subcap, 1, d.lo,
-                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
-  }
-  uint32_t *keys, *vals;
-  TG_CHECK(group_by(d, nD, d.nloc, &keys, &vals));
-  TG_CHECK(bounds(d, keys, nD, d.nloc, kThreadSeg));
-  TG_CHECK(hipMemcpyAsync(d.inbox, d.seg_off, ((size_t)d.nloc + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                          d.stream));
   EmitPolicy p;
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
+  const BktSrc src = bkt_queue(d, Q_D);
+  const int bs = bkt_shift_fused(d.nloc);
+  const uint8_t* deferred = nullptr;
+  uint32_t *keys = d.keys0, *vals = d.vals0;
+  if (bs <= kBktFusedKeyBits) {
+    const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
+    TG_CHECK(bkt_partition(d, src, bs, B));
+    {
+      ProfScope ps_(d, KID_EMIT);
+      hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0,
+                         bs, B, d.nloc, d.tot, d.seg_off, d.inbox, d.medium, d.large, d.sc, d.deferred);
+    }
+    deferred = d.deferred;
+  } else {
+    TG_CHECK(group_by_bkt(d, src, d.nloc, kThreadSeg, d.inbox, &keys, &vals));
+  }
   {
-    ProfScope ps_(d, KID_EMIT);
+    ProfScope ps_(d, KID_SEG_REST);
     hipLaunchKernelGGL(k_emit_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
-                       d.seg_off, d.nloc);
+                       d.seg_off, d.nloc, deferred, bs);
     hipLaunchKernelGGL(k_seg_list<EmitPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
                        d.medium, d.sc);
   }
@@ -1933,21 +2450,21 @@ static hipError_t run_deliveries(Dev& d) {
   return hipSuccess;
 }
 
+// Wheel insert: one partition pass with buckets = slots; records go straight into the arena.
 static hipError_t run_wheel_insert(Dev& d) {
-  TG_CHECK(qfinal(d, Q_L));
-  uint32_t* nL = &d.sc->qn[Q_L];
+  const BktSrc src = bkt_queue(d, Q_L);
   {
-    ProfScope psk_(d, KID_KEYS);
-    hipLaunchKernelGGL(k_keys_rec, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, (int)Q_L, d.subcap, 2, d.lo,
-                       d.slot_ns, d.slots, d.sc, d.keys0, d.vals0);
+    ProfScope ps_(d, KID_BKT_HIST);
+    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, 0, d.slots, d.hist);
   }
-  uint32_t *keys, *vals;
-  TG_CHECK(group_by(d, nL, d.slots, &keys, &vals));
-  hipLaunchKernelGGL(k_region_alloc, dim3(1), dim3(1), 0, d.stream, d.sc, d.regions, d.cap_arena, d.slot_ns);
+  {
+    ProfScope ps_(d, KID_RADIX_ROWS);
+    hipLaunchKernelGGL(k_radix_rows, dim3(d.slots), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+  }
   {
     ProfScope ps_(d, KID_REGION_FILL);
-    hipLaunchKernelGGL(k_region_fill, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.L, keys, vals, d.arena,
-                       d.dirs, d.slots, d.sc);
+    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, d.L, d.arena,
+                       d.dirs, d.slots, d.hist, d.tot);
   }
   return hipGetLastError();
 }
@@ -1960,9 +2477,7 @@ hipError_t window_end(Dev& d) {
     TG_CHECK(hipGetLastError());
   }
   TG_CHECK(run_deliveries(d));
-  TG_CHECK(run_wheel_insert(d));
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, d.stream, d.sc);
-  return hipGetLastError();
+  return run_wheel_insert(d);  // k_wheel_scatter also closes the window's counters
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
@@ -1981,8 +2496,9 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
       hipLaunchKernelGGL(k_keys_sig, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_state, n_dev, kmin, d.keys0,
                          d.vals0);
       uint32_t *keys, *vals;
-      TG_CHECK(group_by(d, n_dev, K, &keys, &vals));
-      TG_CHECK(bounds(d, keys, n_dev, K));
+      BktSrc src = bkt_queue(d, Q_A);
+      src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
+      TG_CHECK(group_by_bkt(d, src, K, 0, nullptr, &keys, &vals));
       SigPolicy p;
       p.inst = d.s_inst; p.t = d.s_t; p.count = d.st_count; p.seq_out = d.s_seq; p.log = d.sig_log;
       p.log_base = log_base; p.kmin = kmin;

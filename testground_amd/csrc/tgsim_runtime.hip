@@ -195,7 +195,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   d.slots = cfg->wheel_slots ? cfg->wheel_slots : 1024;
   const uint64_t cap_msgs = cfg->max_msgs_per_window ? cfg->max_msgs_per_window : (1u << 20);
   const uint64_t cap_rec = cfg->max_records ? cfg->max_records : (1u << 22);
-  if (cap_msgs > 0x7FFFFFFFull || cap_rec > 0x7FFFFFFFull || d.slots < 2 || d.slots > (1u << 20)) {
+  // group-by limits: <= 2^24 keys (instances per shard, sync states), wheel slots <= 2048 buckets
+  if (cap_msgs > 0x7FFFFFFFull || cap_rec > 0x7FFFFFFFull || d.slots < 2 || d.slots > (uint32_t)kMaxBins ||
+      c->nloc > (1u << 24) || (cfg->max_states && cfg->max_states > (1u << 24))) {
     delete c;
     return TGSIM_EINVAL;
   }
@@ -238,6 +240,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.A, phys_rec);
   rc |= dalloc(c, &d.D, phys_rec);
   rc |= dalloc(c, &d.L, phys_rec);
+  rc |= dalloc(c, &d.KA, phys_rec);
+  rc |= dalloc(c, &d.KD, phys_rec);
+  rc |= dalloc(c, &d.KL, phys_rec);
   rc |= dalloc(c, &d.arena, d.cap_arena);
   rc |= dalloc(c, &d.xsend, (size_t)c->S * d.xcap);
   rc |= dalloc(c, &d.xrecv, (size_t)c->S * d.xcap);
@@ -257,6 +262,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
   rc |= dalloc(c, &d.medium, segK);
+  rc |= dalloc(c, &d.deferred, kMaxBins);
   rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
   rc |= dalloc(c, &d.K1a, d.cap_rec);
   rc |= dalloc(c, &d.K1b, d.cap_rec);
