@@ -122,6 +122,7 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
+    from testground_amd._abi import T_NOW
     from testground_amd.sim import Simulator
 
     torch.cuda.set_device(local)
@@ -144,10 +145,11 @@ def main():
         rel_t = torch.zeros(1, dtype=torch.int64, device="cuda")
 
     def step(r: int):
-        now = sim.now
-        sim.gen_storm_round(r, now, F, args.size, spread, r)
+        # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
+        # step issues its launches without any host round trip
+        sim.gen_storm_round(r, T_NOW, F, args.size, spread, r)
         if world == 1:
-            sim.advance_to_barrier(sim.barrier(r, N, now), rtt)
+            sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
         else:
             sim.storm_release_device(rel_t.data_ptr())
             dist.all_reduce(rel_t, op=dist.ReduceOp.MAX)

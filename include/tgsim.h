@@ -118,6 +118,10 @@ typedef struct tgsim_msg_soa {
 } tgsim_msg_soa;
 
 #define TGSIM_DST_EXTERNAL 0xFFFFFFFFu  /* a host outside the data network (plans/network/traffic.go) */
+/* A time argument equal to TGSIM_T_NOW means "the current window start as the device knows it":
+ * lets a run of device-ended windows (tgsim_advance_to_barrier, tgsim_advance_begin_device) go on
+ * without a host round trip (accepted by tgsim_gen_storm_round's t0 and tgsim_sync_barrier's t_wait). */
+#define TGSIM_T_NOW INT64_MIN
 
 /* Per-message status (1 byte each, in enqueue order). Low nibble = code, high bits = flags. */
 enum {

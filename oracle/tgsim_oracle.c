@@ -787,6 +787,7 @@ int tgo_sync_signal(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, co
 }
 
 int tgo_sync_barrier(tgo_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w) {
+  if (t_wait == TGSIM_T_NOW) t_wait = c->now;
   int rc = ensure_state(c, state);
   if (rc) return rc;
   if (grow((void**)&c->waiters, &c->waiters_cap, c->n_waiters + 1, sizeof(owaiter))) return TGSIM_ENOMEM;
@@ -827,6 +828,7 @@ int tgo_advance_to_barrier(tgo_ctx* c, uint32_t w, int64_t offset) {
 int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                         int64_t spread_ns, uint32_t state) {
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
+  if (t0 == TGSIM_T_NOW) t0 = c->now;
   size_t n = (size_t)c->nloc * fanout;
   uint32_t* src = (uint32_t*)malloc(n * 4); uint32_t* dst = (uint32_t*)malloc(n * 4);
   uint32_t* seq = (uint32_t*)malloc(n * 4); uint32_t* sz = (uint32_t*)malloc(n * 4);

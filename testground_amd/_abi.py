@@ -24,6 +24,7 @@ ERROR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EHIP: "EHIP", ECAPACITY: "ECA
 FILTER_ACCEPT, FILTER_REJECT, FILTER_DROP = 0, 1, 2
 POLICY_DENY_ALL, POLICY_ALLOW_ALL = 0, 1
 DST_EXTERNAL = 0xFFFFFFFF
+T_NOW = -(1 << 63)  # TGSIM_T_NOW: "the current window start as the device knows it"
 
 ST_QUEUED, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACHABLE, ST_EXTERNAL, ST_DEST_DOWN, ST_LOCAL = range(8)
 ST_FLAG_DUP, ST_FLAG_CLONE_LOST, ST_FLAG_DUP_CANCEL = 0x10, 0x20, 0x40

@@ -102,10 +102,11 @@ struct Dev {
 
 // Every function returns hipSuccess or the first HIP error; device-side capacity/ordering problems
 // are reported through DevScalars::err and surfaced by the host at the next sync.
-// H = reaction horizon (earliest admissible t_send), T = window start
-hipError_t launch_set_window(Dev& d, int64_t H, int64_t T, int64_t t_end);
-hipError_t launch_set_window_barrier(Dev& d, int64_t H, int64_t T, uint32_t waiter, int64_t offset_ns);
-hipError_t launch_set_window_dev(Dev& d, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset_ns);
+// Window start: the new window begins at the previous window's end (read on the device); its end is
+// explicit, a barrier waiter's release + offset, or a device value + offset.
+hipError_t launch_set_window(Dev& d, int64_t t_end);
+hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns);
+hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 hipError_t storm_local_release(Dev& d, uint32_t n);  // max signal time of the staged storm batch -> sig_red[2]
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack

@@ -206,7 +206,9 @@ __device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t 
 // (decided on the device, no host round trip), or a device value + offset — then the per-window
 // counters zeroed and the timing-wheel extraction plan of the window.
 enum { WIN_EXPLICIT = 0, WIN_BARRIER = 1, WIN_DEVICE = 2 };
-__global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_t* qc, int mode, int64_t H, int64_t T,
+// The window starts where the previous one ended (H = its start, T = its end), read on the device,
+// so a run of barrier- or device-ended windows needs no host round trip at all.
+__global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_t* qc, int mode,
                                                          int64_t t_end_arg, const int64_t* src, int64_t offset,
                                                          int64_t slot_ns, RegionDev* regions, const uint32_t* dirs,
                                                          uint32_t slots, uint32_t* plan_start, uint32_t* plan_off) {
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_
   const uint32_t nw = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
   for (uint32_t i = threadIdx.x; i < nw; i += kBlock) w[i] = 0;
   if (threadIdx.x == 0) {
+    const int64_t H = sc->T, T = sc->t_end;
     int64_t e = t_end_arg;
     if (mode == WIN_BARRIER) {
       const int64_t rel = *src;
@@ -1774,14 +1777,13 @@ __global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const Large
 }
 
 // ============================================================================================
-// fused bucket consumers: one workgroup per bucket of <= 2^9 keys finishes the group-by in LDS
-// (counting sort of the bucket's item list) and runs the token bucket / the delivery emit on it
-// directly, one key per thread. A bucket with more than kBktCap items or a segment longer than
-// kThreadSeg is written out in key order instead (bkt_emit_global) and flagged in deferred[], for
-// the thread / list / large-segment kernels to finish.
+// fused bucket consumers: one workgroup per bucket of <= 2^9 keys finishes the group-by (counting
+// sort of the bucket's item list, in LDS when it holds <= kBktCap items, else in place in global
+// memory) and runs the token bucket / the delivery emit on it directly, one key per thread for
+// keys with <= kThreadSeg items. Longer keys are copied out in key order and listed for k_rest.
 // ============================================================================================
 
-constexpr int kBktCap = 4096;         // items of one bucket held in LDS on the fused path
+constexpr int kBktCap = 4096;         // items of one bucket held in LDS
 constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
 
 template <bool kStage>
@@ -1794,30 +1796,52 @@ struct BktFusedSmem {
   TBSmem tb;
 };
 
-// Fast-path check + LDS grouping; returns true if the bucket is handled in LDS. The fused
-// consumers are launched only with bs <= kBktFusedKeyBits.
+// Group the bucket by key. On return cnt[i] is the END offset (relative to the bucket start) of key
+// i's run and *list the bucket's item list (LDS, or vout + start in global memory). Keys with more
+// than kThreadSeg items are in (kout, vout) at their global positions, with off[] bounds, in the
+// medium / large lists. Returns whether the list is in LDS.
 template <class SM>
-__device__ __forceinline__ bool bkt_fused_prologue(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                                   uint32_t* vout, int bs, uint32_t B, uint32_t K,
-                                                   const uint32_t* tot, uint32_t* off, uint32_t* off2,
-                                                   uint32_t* medium, LargeSeg* large, DevScalars* sc,
-                                                   uint8_t* deferred, SM& sm, BktHead& h) {
+__device__ __forceinline__ bool bkt_fused_group(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                uint32_t* vout, int bs, uint32_t B, uint32_t K, const uint32_t* tot,
+                                                uint32_t* off, uint32_t* off2, uint32_t* medium, LargeSeg* large,
+                                                DevScalars* sc, SM& sm, BktHead& h, const uint32_t** list) {
   const uint32_t maxlen = bkt_count_keys(kin, bs, K, tot, sm.cnt, sm.part, h);
-  const bool fast = h.nb <= (uint32_t)kBktCap && maxlen <= (uint32_t)kThreadSeg;
-  if (threadIdx.x == 0) deferred[blockIdx.x] = fast ? 0 : 1;
-  if (!fast) {
+  if (h.nb > (uint32_t)kBktCap) {
     bkt_emit_global(kin, vin, kout, vout, B, K, sm.cnt, h, off, off2, kThreadSeg, medium, large, sc);
+    __syncthreads();
+    *list = vout + h.start;
     return false;
   }
   for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {
     const uint32_t k = kin[h.start + j];
     sm.idx[atomicAdd(&sm.cnt[k - h.k0], 1u)] = vin[h.start + j];
   }
-  __syncthreads();  // cnt[i] is now the END of key i's run: start(i) = i ? cnt[i-1] : 0
+  __syncthreads();
+  *list = sm.idx;
+  if (maxlen <= (uint32_t)kThreadSeg) return true;  // block-uniform
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // spill the long keys
+    const uint32_t a = i ? sm.cnt[i - 1] : 0u, len = sm.cnt[i] - a;
+    if (len <= (uint32_t)kThreadSeg) continue;
+    const uint32_t k = h.k0 + i, g = h.start + a;
+    for (uint32_t u = 0; u < len; ++u) { kout[g + u] = k; vout[g + u] = sm.idx[a + u]; }
+    off[k] = g;
+    off[k + 1] = g + len;
+    if (len > (uint32_t)kTile) {
+      const uint32_t li = atomicAdd(&sc->n_large, 1u);
+      LargeSeg L;
+      L.seg = k; L.start = g; L.len = len; L.pad = 0;
+      large[li] = L;
+      atomicMax(&sc->max_large, len);
+    } else {
+      medium[atomicAdd(&sc->n_medium, 1u)] = k;
+    }
+  }
+  __syncthreads();
   return true;
 }
 
-// Per round of kBlock keys: the calling thread's key run in sm.idx, and the block's longest run.
+// Per round of kBlock keys: the calling thread's key run (0 if it is longer than kThreadSeg) and the
+// block's longest such run.
 template <class SM>
 __device__ __forceinline__ uint32_t bkt_round(SM& sm, const BktHead& h, uint32_t i, uint32_t& a, uint32_t& M) {
   uint32_t len = 0;
@@ -1825,6 +1849,7 @@ __device__ __forceinline__ uint32_t bkt_round(SM& sm, const BktHead& h, uint32_t
   if (i < h.nk) {
     a = i ? sm.cnt[i - 1] : 0u;
     len = sm.cnt[i] - a;
+    if (len > (uint32_t)kThreadSeg) len = 0;
   }
   if (threadIdx.x == 0) { sm.rmax = 0; sm.tb.any_x = 0; }
   __syncthreads();
@@ -1837,63 +1862,75 @@ __device__ __forceinline__ uint32_t bkt_round(SM& sm, const BktHead& h, uint32_t
 __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, const uint32_t* kin, const uint32_t* vin,
                                                       uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
                                                       uint32_t K, const uint32_t* tot, uint32_t* off,
-                                                      uint32_t* medium, LargeSeg* large, DevScalars* sc,
-                                                      uint8_t* deferred) {
+                                                      uint32_t* medium, LargeSeg* large, DevScalars* sc) {
   __shared__ BktFusedSmem<false> sm;
   BktHead h;
-  if (!bkt_fused_prologue(kin, vin, kout, vout, bs, B, K, tot, off, nullptr, medium, large, sc, deferred, sm, h))
-    return;
+  const uint32_t* list;
+  bkt_fused_group(kin, vin, kout, vout, bs, B, K, tot, off, nullptr, medium, large, sc, sm, h, &list);
   for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
     uint32_t a, M;
     const uint32_t i = r * kBlock + threadIdx.x;
     const uint32_t len = bkt_round(sm, h, i, a, M);
     if (M == 0) continue;  // block-uniform
     const uint32_t sl = h.k0 + i;
-    if (M <= 4) tb_thread_body<4>(p, sm.idx, sl, a, len, sm.tb);
-    else if (M <= 8) tb_thread_body<8>(p, sm.idx, sl, a, len, sm.tb);
-    else tb_thread_body<16>(p, sm.idx, sl, a, len, sm.tb);
+    if (M <= 4) tb_thread_body<4>(p, list, sl, a, len, sm.tb);
+    else if (M <= 8) tb_thread_body<8>(p, list, sl, a, len, sm.tb);
+    else tb_thread_body<16>(p, list, sl, a, len, sm.tb);
     __syncthreads();
   }
 }
 
 template <int M>
-__device__ __forceinline__ void emit_stage_body(const EmitPolicy& p, const uint32_t* list, uint32_t seg, uint32_t a,
-                                                uint32_t len, uint32_t* stage) {
+__device__ __forceinline__ void emit_seg_body(const EmitPolicy& p, const uint32_t* list, uint32_t seg, uint32_t a,
+                                              uint32_t len, uint32_t* stage, uint32_t gbase) {
   uint64_t k1[M], k2[M];
   uint32_t k3[M];
   thread_keys<EmitPolicy, M>(p, list, seg, a, len, k1, k2, k3);
 #pragma unroll
-  for (int u = 0; u < M; ++u)
-    if ((uint32_t)u < len) stage[a + u] = k3[u];
+  for (int u = 0; u < M; ++u) {
+    if ((uint32_t)u < len) {
+      if (stage) stage[a + u] = k3[u];
+      else p.write(gbase + a + u, k3[u]);
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, const uint32_t* kin, const uint32_t* vin,
                                                         uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
                                                         uint32_t K, const uint32_t* tot, uint32_t* off,
                                                         uint32_t* off2, uint32_t* medium, LargeSeg* large,
-                                                        DevScalars* sc, uint8_t* deferred) {
+                                                        DevScalars* sc) {
   __shared__ BktFusedSmem<true> sm;
   BktHead h;
-  if (!bkt_fused_prologue(kin, vin, kout, vout, bs, B, K, tot, off, off2, medium, large, sc, deferred, sm, h))
-    return;
-  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
-    const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
-    off[h.k0 + i] = o;
-    off2[h.k0 + i] = o;
+  const uint32_t* list;
+  const bool in_lds = bkt_fused_group(kin, vin, kout, vout, bs, B, K, tot, off, off2, medium, large, sc, sm, h, &list);
+  if (in_lds) {
+    for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
+      const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
+      off[h.k0 + i] = o;
+      off2[h.k0 + i] = o;
+    }
+    if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
+    for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) sm.stage[j] = 0xFFFFFFFFu;  // long keys: k_rest writes
   }
-  if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
+  __syncthreads();
+  uint32_t* stage = in_lds ? sm.stage : nullptr;
   for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
     uint32_t a, M;
     const uint32_t i = r * kBlock + threadIdx.x;
     const uint32_t len = bkt_round(sm, h, i, a, M);
     if (M == 0) continue;
     const uint32_t seg = h.k0 + i;
-    if (M <= 4) emit_stage_body<4>(p, sm.idx, seg, a, len, sm.stage);
-    else if (M <= 8) emit_stage_body<8>(p, sm.idx, seg, a, len, sm.stage);
-    else emit_stage_body<16>(p, sm.idx, seg, a, len, sm.stage);
+    if (M <= 4) emit_seg_body<4>(p, list, seg, a, len, stage, h.start);
+    else if (M <= 8) emit_seg_body<8>(p, list, seg, a, len, stage, h.start);
+    else emit_seg_body<16>(p, list, seg, a, len, stage, h.start);
   }
+  if (!in_lds) return;
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) p.write(h.start + j, sm.stage[j]);  // coalesced SoA
+  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {  // coalesced SoA
+    const uint32_t v = sm.stage[j];
+    if (v != 0xFFFFFFFFu) p.write(h.start + j, v);
+  }
 }
 
 // ============================================================================================
@@ -2023,8 +2060,8 @@ __global__ void k_sig_commit_count(const uint32_t* n_ptr, uint32_t st, const int
 }
 
 __global__ void k_add_waiter(uint32_t* w_state, uint32_t* w_target, int64_t* w_twait, int64_t* w_release,
-                             uint32_t i, uint32_t state, uint32_t target, int64_t t_wait) {
-  w_state[i] = state; w_target[i] = target; w_twait[i] = t_wait; w_release[i] = -1;
+                             uint32_t i, uint32_t state, uint32_t target, int64_t t_wait, const DevScalars* sc) {
+  w_state[i] = state; w_target[i] = target; w_twait[i] = t_wait == INT64_MIN ? sc->t_end : t_wait; w_release[i] = -1;
 }
 
 // A waiter's release time: the time of the target-th signal of its state. For a count-only chunk
@@ -2053,6 +2090,125 @@ __global__ __launch_bounds__(kBlock) void k_waiters(uint32_t nw, const uint32_t*
         break;
       }
     }
+  }
+}
+
+// ============================================================================================
+// the rest of a group-by's segments, in one launch and without a host round trip: medium segments
+// (kThreadSeg < len <= kTile) get one block each (LDS sort + the policy's epilogue); a large segment
+// (len > kTile) is owned by one block from start to end - its kChunk chunks are sorted in LDS, merged
+// pairwise through the (K1, K2, K3) scratch inside the block, and handed to the policy's large
+// consumer. Nothing to do costs one launch of early-exiting blocks.
+// ============================================================================================
+
+__device__ void large_consume(const TBPolicy& p, SortSmem& s, const LargeSeg& L, const uint64_t* K1,
+                              const uint32_t* K3, uint32_t salt) {
+  bool has_carry = false;
+  int64_t carry = 0;
+  for (uint32_t t0 = 0; t0 < L.len; t0 += kChunk, salt += 16) {
+    const uint32_t cnt = min((uint32_t)kChunk, L.len - t0);
+    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
+      s.sg[j] = L.seg; s.k1[j] = K1[L.start + t0 + j]; s.k3[j] = K3[L.start + t0 + j]; s.perm[j] = j;
+    }
+    __syncthreads();
+    p.scan(s, cnt, has_carry, carry, t0 + cnt == L.len, salt);
+    carry = s.carry;
+    has_carry = true;
+    __syncthreads();
+  }
+}
+
+__device__ void large_consume(const EmitPolicy& p, SortSmem&, const LargeSeg& L, const uint64_t*, const uint32_t* K3,
+                              uint32_t) {
+  for (uint32_t j = threadIdx.x; j < L.len; j += kBlock) p.write(L.start + j, K3[L.start + j]);
+}
+
+__device__ void large_consume(const SigPolicy& p, SortSmem&, const LargeSeg& L, const uint64_t* K1, const uint32_t* K3,
+                              uint32_t) {
+  for (uint32_t j = threadIdx.x; j < L.len; j += kBlock)
+    p.write(L.seg, L.start + j, L.start, K1[L.start + j], K3[L.start + j]);
+}
+
+// Sort one large segment inside the calling block; returns the buffer set that holds the result.
+template <class P>
+__device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, const uint32_t* keys,
+                                 const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b,
+                                 uint64_t* K2b, uint32_t* K3b) {
+  for (uint32_t c0 = 0; c0 < L.len; c0 += kChunk) {
+    const uint32_t st = L.start + c0;
+    const uint32_t cnt = min((uint32_t)kChunk, L.len - c0);
+    const uint32_t npad = next_pow2(cnt);
+    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
+      if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+      else pad_key(s, j);
+    }
+    __syncthreads();
+    bitonic_lds(s, npad);
+    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
+    __syncthreads();
+  }
+  bool in_a = true;
+  constexpr uint32_t IT = kChunk / kBlock;
+  for (uint32_t W = kChunk; W < L.len; W *= 2) {
+    const uint64_t* sK1 = in_a ? K1a : K1b;
+    const uint64_t* sK2 = in_a ? K2a : K2b;
+    const uint32_t* sK3 = in_a ? K3a : K3b;
+    uint64_t* dK1 = in_a ? K1b : K1a;
+    uint64_t* dK2 = in_a ? K2b : K2a;
+    uint32_t* dK3 = in_a ? K3b : K3a;
+    const uint32_t base = L.start;
+    for (uint32_t o0 = 0; o0 < L.len; o0 += kChunk) {
+      const uint32_t o1 = min(o0 + (uint32_t)kChunk, L.len);
+      const uint32_t As = (o0 / (2 * W)) * 2 * W;
+      const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
+      const uint32_t nA = Ae - As, nB = Be - Ae;
+      const uint32_t dend = o1 - As;
+      const uint32_t d0 = o0 - As + threadIdx.x * IT;
+      if (d0 >= dend) continue;
+      const uint32_t a0 = base + As, b0 = base + Ae;
+      uint32_t lo = d0 > nB ? d0 - nB : 0u, hi = min(d0, nA);
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (!kless(sK1, sK2, sK3, b0 + (d0 - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
+      }
+      uint32_t ia = lo, ib = d0 - lo;
+      for (uint32_t k = 0; k < IT && d0 + k < dend; ++k) {
+        bool takeA;
+        if (ib >= nB) takeA = true;
+        else if (ia >= nA) takeA = false;
+        else takeA = !kless(sK1, sK2, sK3, b0 + ib, a0 + ia);
+        const uint32_t src = takeA ? a0 + ia++ : b0 + ib++;
+        const uint32_t dst = base + As + d0 + k;
+        dK1[dst] = sK1[src]; dK2[dst] = sK2[src]; dK3[dst] = sK3[src];
+      }
+    }
+    __syncthreads();
+    in_a = !in_a;
+  }
+  return in_a;
+}
+
+template <class P>
+__global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
+                                                 const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
+                                                 uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b,
+                                                 uint64_t* K2b, uint32_t* K3b) {
+  __shared__ SortSmem s;
+  const uint32_t nm = sc->n_medium, nl = sc->n_large;
+  for (uint32_t w = blockIdx.x; w < nm + nl; w += gridDim.x) {
+    if (w < nm) {
+      const uint32_t g = medium[w];
+      const uint32_t a = off[g], m = off[g + 1] - a;
+      for (uint32_t j = threadIdx.x; j < m; j += kBlock) p.key(g, vals[a + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+      __syncthreads();
+      span_sort(s, m, off, a);
+      p.epilogue(s, m, a, off, w);
+    } else {
+      const LargeSeg L = large[w - nm];
+      const bool in_a = large_sort_block(p, s, L, keys, vals, K1a, K2a, K3a, K1b, K2b, K3b);
+      large_consume(p, s, L, in_a ? K1a : K1b, in_a ? K3a : K3b, (w - nm) * 131u);
+    }
+    __syncthreads();
   }
 }
 
@@ -2110,7 +2266,9 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(uint32_t lo, uint32_t nloc
                                                       uint32_t state, uint32_t key0, uint32_t key1,
                                                       uint32_t base, uint32_t* m_src, uint32_t* m_dst,
                                                       uint32_t* m_seq, uint32_t* m_size, int64_t* m_t,
-                                                      uint32_t* s_state, uint32_t* s_inst, int64_t* s_t) {
+                                                      uint32_t* s_state, uint32_t* s_inst, int64_t* s_t,
+                                                      const DevScalars* sc) {
+  if (t0 == INT64_MIN) t0 = sc->t_end;  // TGSIM_T_NOW: the device's current window start
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += stride) {
     const uint32_t g = lo + l;
@@ -2168,23 +2326,20 @@ static hipError_t reset_window(Dev& d) {
   return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
 }
 
-static hipError_t window_start(Dev& d, int mode, int64_t H, int64_t T, int64_t t_end, const int64_t* src,
-                               int64_t offset) {
-  hipLaunchKernelGGL(k_window_start, dim3(1), dim3(kBlock), 0, d.stream, d.sc, d.qc, mode, H, T, t_end, src, offset,
+static hipError_t window_start(Dev& d, int mode, int64_t t_end, const int64_t* src, int64_t offset) {
+  hipLaunchKernelGGL(k_window_start, dim3(1), dim3(kBlock), 0, d.stream, d.sc, d.qc, mode, t_end, src, offset,
                      d.slot_ns, d.regions, d.dirs, d.slots, d.plan_start, d.plan_off);
   return hipGetLastError();
 }
 
-hipError_t launch_set_window(Dev& d, int64_t H, int64_t T, int64_t t_end) {
-  return window_start(d, WIN_EXPLICIT, H, T, t_end, nullptr, 0);
+hipError_t launch_set_window(Dev& d, int64_t t_end) { return window_start(d, WIN_EXPLICIT, t_end, nullptr, 0); }
+
+hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns) {
+  return window_start(d, WIN_BARRIER, 0, d.w_release + waiter, offset_ns);
 }
 
-hipError_t launch_set_window_barrier(Dev& d, int64_t H, int64_t T, uint32_t waiter, int64_t offset_ns) {
-  return window_start(d, WIN_BARRIER, H, T, 0, d.w_release + waiter, offset_ns);
-}
-
-hipError_t launch_set_window_dev(Dev& d, int64_t H, int64_t T, const int64_t* t_end_dev, int64_t offset_ns) {
-  return window_start(d, WIN_DEVICE, H, T, 0, t_end_dev, offset_ns);
+hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns) {
+  return window_start(d, WIN_DEVICE, 0, t_end_dev, offset_ns);
 }
 
 hipError_t storm_local_release(Dev& d, uint32_t n) {
@@ -2345,44 +2500,31 @@ static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uin
   return hipSuccess;
 }
 
+template <class P>
+static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const uint32_t* vals) {
+  ProfScope ps_(d, KID_SEG_REST);
+  hipLaunchKernelGGL(k_rest<P>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, keys, vals, d.seg_off, d.medium,
+                     d.large, d.sc, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
+  return hipGetLastError();
+}
+
+// Token bucket: partition the due copies by sender bucket, then one workgroup per bucket groups
+// and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
 static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
-  const BktSrc src = bkt_queue(d, Q_A);
   const int bs = bkt_shift_fused(d.nloc);
-  const uint8_t* deferred = nullptr;
-  uint32_t *keys = d.keys0, *vals = d.vals0;
-  if (bs <= kBktFusedKeyBits) {
-    // partition by sender bucket, then one workgroup per bucket groups and token-buckets in LDS
-    const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
-    TG_CHECK(bkt_partition(d, src, bs, B));
-    {
-      ProfScope ps_(d, KID_TB);
-      hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs,
-                         B, d.nloc, d.tot, d.seg_off, d.medium, d.large, d.sc, d.deferred);
-    }
-    deferred = d.deferred;
-  } else {
-    TG_CHECK(group_by_bkt(d, src, d.nloc, kThreadSeg, nullptr, &keys, &vals));
-  }
+  if (bs > kBktFusedKeyBits) return hipErrorInvalidValue;  // nloc <= 2^20 (checked at create)
+  const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
+  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_A), bs, B));
   {
-    ProfScope ps_(d, KID_SEG_REST);
-    hipLaunchKernelGGL(k_tb_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
-                       d.seg_off, d.nloc, deferred, bs);
-    hipLaunchKernelGGL(k_seg_list<TBPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
-                       d.medium, d.sc);
+    ProfScope ps_(d, KID_TB);
+    hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs, B,
+                       d.nloc, d.tot, d.seg_off, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
-  bool any;
-  uint64_t *K1, *K2;
-  uint32_t* K3;
-  TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
-  if (any) {
-    hipLaunchKernelGGL(k_tb_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, K1, K3);
-    TG_CHECK(hipGetLastError());
-  }
-  return hipSuccess;
+  return launch_rest(d, p, d.keys0, d.vals0);
 }
 
 hipError_t window_begin(Dev& d, uint32_t n_staged) {
@@ -2411,43 +2553,23 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
   return hipSuccess;
 }
 
+// Deliveries: partition the due copies by receiver bucket, then one workgroup per bucket orders
+// each inbox and writes it as SoA (k_emit_bucket); long inboxes finish in k_rest.
 static hipError_t run_deliveries(Dev& d) {
   EmitPolicy p;
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
-  const BktSrc src = bkt_queue(d, Q_D);
   const int bs = bkt_shift_fused(d.nloc);
-  const uint8_t* deferred = nullptr;
-  uint32_t *keys = d.keys0, *vals = d.vals0;
-  if (bs <= kBktFusedKeyBits) {
-    const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
-    TG_CHECK(bkt_partition(d, src, bs, B));
-    {
-      ProfScope ps_(d, KID_EMIT);
-      hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0,
-                         bs, B, d.nloc, d.tot, d.seg_off, d.inbox, d.medium, d.large, d.sc, d.deferred);
-    }
-    deferred = d.deferred;
-  } else {
-    TG_CHECK(group_by_bkt(d, src, d.nloc, kThreadSeg, d.inbox, &keys, &vals));
-  }
+  if (bs > kBktFusedKeyBits) return hipErrorInvalidValue;
+  const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
+  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_D), bs, B));
   {
-    ProfScope ps_(d, KID_SEG_REST);
-    hipLaunchKernelGGL(k_emit_thread, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, p, vals,
-                       d.seg_off, d.nloc, deferred, bs);
-    hipLaunchKernelGGL(k_seg_list<EmitPolicy>, dim3(kListBlocks), dim3(kBlock), 0, d.stream, p, vals, d.seg_off,
-                       d.medium, d.sc);
+    ProfScope ps_(d, KID_EMIT);
+    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs,
+                       B, d.nloc, d.tot, d.seg_off, d.inbox, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
-  bool any;
-  uint64_t *K1, *K2;
-  uint32_t* K3;
-  TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
-  if (any) {
-    hipLaunchKernelGGL(k_emit_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc, K3);
-    TG_CHECK(hipGetLastError());
-  }
-  return hipSuccess;
+  return launch_rest(d, p, d.keys0, d.vals0);
 }
 
 // Wheel insert: one partition pass with buckets = slots; records go straight into the arena.
@@ -2505,15 +2627,7 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
       hipLaunchKernelGGL(k_seg_small<SigPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
                          d.seg_off, n_dev, d.cap_rec);
       TG_CHECK(hipGetLastError());
-      bool any;
-      uint64_t *K1, *K2;
-      uint32_t* K3;
-      TG_CHECK(sort_large(d, p, keys, vals, &any, &K1, &K2, &K3));
-      if (any) {
-        hipLaunchKernelGGL(k_sig_large, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, d.large, d.chunk_off, d.sc,
-                           K1, K3);
-        TG_CHECK(hipGetLastError());
-      }
+      TG_CHECK(launch_rest(d, p, keys, vals));
       hipLaunchKernelGGL(k_sig_commit, dim3(grid_for(K)), dim3(kBlock), 0, d.stream, d.seg_off, K, kmin, log_base,
                          d.sig_log, d.st_count, d.st_last, d.st_nchunks, d.st_chunks, d.sc);
       TG_CHECK(hipGetLastError());
@@ -2524,7 +2638,7 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
 
 hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait) {
   hipLaunchKernelGGL(k_add_waiter, dim3(1), dim3(1), 0, d.stream, d.w_state, d.w_target, d.w_twait, d.w_release, idx,
-                     state, target, t_wait);
+                     state, target, t_wait, d.sc);
   return hipGetLastError();
 }
 
@@ -2540,7 +2654,7 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   ProfScope ps_(d, KID_GEN);
   hipLaunchKernelGGL(k_gen_storm, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.lo, d.nloc, d.N, round, t0,
                      fanout, size, spread_ns, state, d.key0, d.key1, staged_base, d.m_src, d.m_dst, d.m_seq,
-                     d.m_size, d.m_t, d.s_state, d.s_inst, d.s_t);
+                     d.m_size, d.m_t, d.s_state, d.s_inst, d.s_t, d.sc);
   return hipGetLastError();
 }
 

@@ -195,9 +195,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   d.slots = cfg->wheel_slots ? cfg->wheel_slots : 1024;
   const uint64_t cap_msgs = cfg->max_msgs_per_window ? cfg->max_msgs_per_window : (1u << 20);
   const uint64_t cap_rec = cfg->max_records ? cfg->max_records : (1u << 22);
-  // group-by limits: <= 2^24 keys (instances per shard, sync states), wheel slots <= 2048 buckets
+  // group-by limits: <= 2^20 instances per shard, <= 2^24 sync states, <= 2048 wheel slots
   if (cap_msgs > 0x7FFFFFFFull || cap_rec > 0x7FFFFFFFull || d.slots < 2 || d.slots > (uint32_t)kMaxBins ||
-      c->nloc > (1u << 24) || (cfg->max_states && cfg->max_states > (1u << 24))) {
+      c->nloc > (1u << 20) || (cfg->max_states && cfg->max_states > (1u << 24))) {
     delete c;
     return TGSIM_EINVAL;
   }
@@ -415,8 +415,21 @@ extern "C" int tgsim_profile_read(tgsim_ctx* c, double* ms, uint64_t* launches, 
 extern "C" int tgsim_kernel_classes(void) { return KID_COUNT; }
 extern "C" const char* tgsim_kernel_name(int k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : "?"; }
 
-extern "C" int64_t tgsim_now(const tgsim_ctx* c) { return c ? c->now : -1; }
-extern "C" int64_t tgsim_horizon(const tgsim_ctx* c) { return c ? c->horizon : -1; }
+// The host view of the clock lags behind device-ended windows until the next synchronisation.
+static void refresh_clock(const tgsim_ctx* cc) {
+  tgsim_ctx* c = const_cast<tgsim_ctx*>(cc);
+  if (c->now_from_device && !c->in_window) (void)sync_and_check(c);
+}
+extern "C" int64_t tgsim_now(const tgsim_ctx* c) {
+  if (!c) return -1;
+  refresh_clock(c);
+  return c->now;
+}
+extern "C" int64_t tgsim_horizon(const tgsim_ctx* c) {
+  if (!c) return -1;
+  refresh_clock(c);
+  return c->horizon;
+}
 
 // ============================== network configuration ========================================
 
@@ -659,8 +672,7 @@ static int begin_common(tgsim_ctx* c) {
   c->n_status_last = c->n_staged;
   c->n_staged = 0;
   c->in_window = true;
-  // window_begin synchronised once (token-bucket grouping); surface errors seen there
-  return check_device_errors(c);
+  return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
 
 extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
@@ -668,7 +680,7 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
-  HIPCK(c, launch_set_window(c->d, c->horizon, c->now, t_end), "set window");
+  HIPCK(c, launch_set_window(c->d, t_end), "set window");
   return begin_common(c);
 }
 
@@ -694,7 +706,7 @@ extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, 
 extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
   if (!c || !t_end_dev) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
-  HIPCK(c, launch_set_window_dev(c->d, c->horizon, c->now, t_end_dev, offset_ns), "set window");
+  HIPCK(c, launch_set_window_dev(c->d, t_end_dev, offset_ns), "set window");
   return begin_common(c);
 }
 
@@ -703,11 +715,9 @@ extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
   HIPCK(c, window_end(c->d), "window_end");
   c->in_window = false;
-  // window_end synchronised during the delivery sort; h_sc->t_end is this window's end
-  c->horizon = c->d.h_sc->T;
-  c->now = c->d.h_sc->t_end;
-  c->now_from_device = false;
-  return check_device_errors(c);
+  // No host round trip: the window's end (and any device-side error) is read at the next sync.
+  c->now_from_device = true;
+  return TGSIM_OK;
 }
 
 extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
@@ -715,7 +725,9 @@ extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
   if (c->S != 1) return fail(c, TGSIM_ESTATE, "tgsim_advance needs a single-shard context; use begin/end");
   int rc = tgsim_advance_begin(c, t_end);
   if (rc) return rc;
-  return tgsim_advance_end(c);
+  rc = tgsim_advance_end(c);
+  if (rc) return rc;
+  return sync_and_check(c);  // the host-driven API reports the window's errors here
 }
 
 extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
@@ -723,8 +735,7 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   if (c->S != 1) return fail(c, TGSIM_ESTATE, "single-shard context required");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
-  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
-  HIPCK(c, launch_set_window_barrier(c->d, c->horizon, c->now, waiter, offset_ns), "set window");
+  HIPCK(c, launch_set_window_barrier(c->d, waiter, offset_ns), "set window");
   int rc = begin_common(c);
   if (rc) return rc;
   return tgsim_advance_end(c);
@@ -846,7 +857,10 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
   if (size >= 0x80000000u || spread_ns < 0) return fail(c, TGSIM_EINVAL, "bad size/spread");
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
-  if (t0 < c->now) return fail(c, TGSIM_ECAUSALITY, "t0 before window start");
+  if (t0 != TGSIM_T_NOW) {
+    if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+    if (t0 < c->now) return fail(c, TGSIM_ECAUSALITY, "t0 before window start");
+  }
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
