@@ -66,6 +66,8 @@ struct Dev {
   uint32_t *keys0 = nullptr, *keys1 = nullptr, *vals0 = nullptr, *vals1 = nullptr;
   uint32_t* hist = nullptr;       // [kMaxBins * kRadixBlocks]
   uint32_t* tot = nullptr;        // [kMaxBins]
+  int n_cu = 256;                 // compute units of the device (bucket widths)
+  uint32_t* bstart = nullptr;     // [kMaxBins + 1] bucket starts of the last partition pass
   uint32_t* qc = nullptr;         // [3][kNSub][32] append counters (128 B apart)
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;

@@ -807,6 +807,14 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const u
 
 constexpr int kBktMaxKeyBits = 13;  // keys per bucket <= 8192 (32 KB of LDS counters)
 
+// Bucket of a key: b = k / w by a multiply-shift. m = ceil(2^32 / w) is exact when w is a power of
+// two, and for any w while k * w < 2^32 (nloc <= 2^20, w <= 512 on the fused path).
+struct BktDiv {
+  uint32_t w;  // keys per bucket
+  uint64_t m;
+  __device__ __forceinline__ uint32_t of(uint32_t k) const { return (uint32_t)(((uint64_t)k * m) >> 32); }
+};
+
 // Input of a partition pass: a sharded record queue whose keys the producers wrote beside the
 // records (Queues::key_of; block b covers a quarter of sub-queue b / 4, so no index search), or a
 // precomputed (keys, vals) array (mode 3).
@@ -843,7 +851,7 @@ constexpr int kBktUnroll = 8;
 // pass 1: per-block bucket histogram. The first block also closes the queue (prefix over its
 // sub-queues, totals, overflow bit: the former k_qfinal) and, for the wheel batch, allocates the
 // window's region (the former k_region_alloc).
-__global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, int bs, uint32_t B,
+__global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
                                                      uint32_t* hist) {
   __shared__ uint32_t h[kMaxBins];
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) h[d] = 0;
@@ -869,7 +877,7 @@ __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc,
     }
 #pragma unroll
     for (int u = 0; u < kBktUnroll; ++u)
-      if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[k[u] >> bs], 1u);
+      if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[bd.of(k[u])], 1u);
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
@@ -900,11 +908,15 @@ __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, cons
 }
 
 // pass 2: scatter (key, physical index) into bucket order (kout, vout); ranks from LDS atomics.
-__global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
-                                                        const uint32_t* hist, const uint32_t* tot) {
+__global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
+                                                        const uint32_t* hist, const uint32_t* tot, uint32_t* bstart) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   bkt_bases(B, hist, tot, base, part);
+  if (blockIdx.x == 0) {  // block 0's bases are the bucket starts (its per-block offsets are 0)
+    for (uint32_t d = threadIdx.x; d < B; d += kBlock) bstart[d] = base[d];
+    if (threadIdx.x == 0) bstart[B] = base[B - 1] + tot[B - 1];
+  }
   uint32_t start, end;
   bkt_block_range(src, start, end);
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
@@ -918,7 +930,7 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
 #pragma unroll
     for (int u = 0; u < kBktUnroll; ++u) {
       if (k[u] == 0xFFFFFFFFu) continue;
-      const uint32_t pos = atomicAdd(&base[k[u] >> bs], 1u);
+      const uint32_t pos = atomicAdd(&base[bd.of(k[u])], 1u);
       kout[pos] = k[u];
       vout[pos] = v[u];
     }
@@ -929,11 +941,11 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
 // exclusive offsets of its keys in cnt[] (relative to the bucket start); returns the longest segment.
 struct BktHead { uint32_t start, nb, k0, nk; };
 
-__device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, int bs, uint32_t K, const uint32_t* tot,
+__device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv bd, uint32_t K, const uint32_t* tot,
                                                    uint32_t* cnt, uint32_t* part, BktHead& h) {
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
-  h.k0 = b << bs;
-  h.nk = min(K - h.k0, 1u << bs);
+  h.k0 = b * bd.w;
+  h.nk = min(K - h.k0, bd.w);
   uint32_t s = 0;
   for (uint32_t d = tid; d < b; d += kBlock) s += tot[d];
   part[tid] = s;
@@ -982,11 +994,12 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, int bs, 
 }
 
 // Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
-// medium / large segment lists.
+// medium (medium_above < len <= kTile) / large (len > kTile) segment lists.
+constexpr uint32_t kNoMedium = 0xFFFFFFFFu;
 __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                                                 uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
                                                 const BktHead& h, uint32_t* off, uint32_t* off2,
-                                                uint32_t thread_max, uint32_t* medium, LargeSeg* large,
+                                                uint32_t medium_above, uint32_t* medium, LargeSeg* large,
                                                 DevScalars* sc) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < h.nk; i += kBlock) {
@@ -1001,7 +1014,7 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
       L.seg = k; L.start = run; L.len = len; L.pad = 0;
       large[li] = L;
       atomicMax(&sc->max_large, len);
-    } else if (thread_max && len > thread_max) {
+    } else if (len > medium_above) {  // kNoMedium: never
       medium[atomicAdd(&sc->n_medium, 1u)] = k;
     }
   }
@@ -1020,15 +1033,15 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
 
 // pass 3: one workgroup per bucket, global form only (signals, and > 2^bs-key fallbacks).
 __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                                     uint32_t* vout, int bs, uint32_t B, uint32_t K,
+                                                     uint32_t* vout, BktDiv bd, uint32_t B, uint32_t K,
                                                      const uint32_t* tot, uint32_t* off, uint32_t* off2,
-                                                     uint32_t thread_max, uint32_t* medium, LargeSeg* large,
+                                                     uint32_t medium_above, uint32_t* medium, LargeSeg* large,
                                                      DevScalars* sc) {
   __shared__ uint32_t cnt[1u << kBktMaxKeyBits];
   __shared__ uint32_t part[kBlock];
   BktHead h;
-  bkt_count_keys(kin, bs, K, tot, cnt, part, h);
-  bkt_emit_global(kin, vin, kout, vout, B, K, cnt, h, off, off2, thread_max, medium, large, sc);
+  bkt_count_keys(kin, bd, K, tot, cnt, part, h);
+  bkt_emit_global(kin, vin, kout, vout, B, K, cnt, h, off, off2, medium_above, medium, large, sc);
 }
 
 // Wheel insert with buckets = slots (slots <= kMaxBins): records are copied straight from the L
@@ -1777,160 +1790,313 @@ __global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const Large
 }
 
 // ============================================================================================
-// fused bucket consumers: one workgroup per bucket of <= 2^9 keys finishes the group-by (counting
-// sort of the bucket's item list, in LDS when it holds <= kBktCap items, else in place in global
-// memory) and runs the token bucket / the delivery emit on it directly, one key per thread for
-// keys with <= kThreadSeg items. Longer keys are copied out in key order and listed for k_rest.
+// fused bucket consumers: one workgroup per bucket of <= 2^kBktFusedKeyBits keys finishes the
+// group-by in LDS and consumes it there. The bucket's items stay in the registers of the thread
+// that gathered them (kIPT per thread), so a workgroup's critical path is four memory round trips:
+// bucket bounds (+ the senders' shape / token state), item list, one 32-B gather per item, the
+// output reservation. In between, all in LDS: counting sort by key, rank inside each key's run
+// (O(run) compares), and the policy (GCRA along each sender's run / delivery position).
+// A bucket holding more than kBktCap items, and any key longer than kBktRankMax, is written out in
+// key order instead and listed for k_rest (medium / large segments).
 // ============================================================================================
 
-constexpr int kBktCap = 4096;         // items of one bucket held in LDS
+constexpr int kBktCap = 2048;         // items of one bucket held by the workgroup
 constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
+constexpr uint32_t kBktRankMax = 64;  // longest key run ranked in LDS
+constexpr int kIPT = kBktCap / kBlock;  // items per thread
 
-template <bool kStage>
 struct BktFusedSmem {
-  uint32_t cnt[1u << kBktFusedKeyBits];
-  uint32_t idx[kBktCap];                  // the bucket's item list, grouped by key
-  uint32_t stage[kStage ? kBktCap : 1];   // emit: sorted item of each output position
+  uint32_t cnt[1u << kBktFusedKeyBits];  // per key: run start, then run end (relative to the bucket)
+  uint64_t k1[kBktCap];                  // TB: netem time, then departure; emit: delivery time
+  uint64_t k2[kBktCap];                  // TB: seq << 32 | !clone << 31 | size; emit: src << 32 | seq
+  uint32_t k3[kBktCap];                  // batch index (emit: | !clone << 31)
+  uint16_t key[kBktCap];                 // key of each slot, relative to the bucket's first key
+  uint16_t ord[kBktCap];                 // by_pos: sorted position -> slot; else slot -> sorted position
   uint32_t part[kBlock];
-  uint32_t rmax;
-  TBSmem tb;
+  uint32_t maxlen, flag;
+#ifdef TGSIM_PHASE_PROF
+  uint64_t ph[10];
+  uint64_t w0;
+#endif
 };
+#ifdef TGSIM_PHASE_PROF
+#define TG_PH(i) do { if (threadIdx.x == 0) { if ((i) == 0) sm.w0 = wall_clock64(); sm.ph[i] = clock64(); } } while (0)
+__device__ uint64_t g_tg_ph[2][1024][12];
+#define TG_PH_END(kid, nb) do { __syncthreads(); if (threadIdx.x == 0 && blockIdx.x < 1024) { sm.ph[8] = clock64(); \
+  uint64_t* o = g_tg_ph[kid][blockIdx.x]; o[0] = nb; for (int i_ = 0; i_ < 8; ++i_) o[1 + i_] = sm.ph[i_ + 1] - sm.ph[i_]; \
+  o[9] = sm.w0; o[10] = wall_clock64(); o[11] = gridDim.x; } } while (0)
+#else
+#define TG_PH(i) do {} while (0)
+#define TG_PH_END(name, nb) do {} while (0)
+#endif
 
-// Group the bucket by key. On return cnt[i] is the END offset (relative to the bucket start) of key
-// i's run and *list the bucket's item list (LDS, or vout + start in global memory). Keys with more
-// than kThreadSeg items are in (kout, vout) at their global positions, with off[] bounds, in the
-// medium / large lists. Returns whether the list is in LDS.
-template <class SM>
-__device__ __forceinline__ bool bkt_fused_group(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                                uint32_t* vout, int bs, uint32_t B, uint32_t K, const uint32_t* tot,
-                                                uint32_t* off, uint32_t* off2, uint32_t* medium, LargeSeg* large,
-                                                DevScalars* sc, SM& sm, BktHead& h, const uint32_t** list) {
-  const uint32_t maxlen = bkt_count_keys(kin, bs, K, tot, sm.cnt, sm.part, h);
-  if (h.nb > (uint32_t)kBktCap) {
-    bkt_emit_global(kin, vin, kout, vout, B, K, sm.cnt, h, off, off2, kThreadSeg, medium, large, sc);
-    __syncthreads();
-    *list = vout + h.start;
+__device__ __forceinline__ bool k3less(uint64_t a1, uint64_t a2, uint32_t a3, uint64_t b1, uint64_t b2, uint32_t b3) {
+  if (a1 != b1) return a1 < b1;
+  if (a2 != b2) return a2 < b2;
+  return a3 < b3;
+}
+
+// The bucket's items, one gathered record per item in the registers of its thread. On return
+// (true): slot[u] is item u's LDS slot, sm.cnt[k] the END of key k's run, sm.ord the sorted order
+// of every key run of length <= kBktRankMax (by_pos: position -> slot, else slot -> position); longer runs are written out (kout, vout,
+// off) and listed. false: the bucket was too big and went to the global form (k_rest).
+template <bool by_pos, class KeyFn>
+__device__ __forceinline__ bool bkt_fused_load(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                               uint32_t* vout, BktDiv bd, uint32_t B, uint32_t K, const uint32_t* tot,
+                                               const uint32_t* bstart, uint32_t* off, uint32_t* off2,
+                                               uint32_t* medium, LargeSeg* large, DevScalars* sc, BktFusedSmem& sm,
+                                               BktHead& h, const tgsim_record* batch, const KeyFn& keyfn,
+                                               tgsim_record (&rec)[kIPT], uint32_t (&slot)[kIPT]) {
+  const uint32_t b = blockIdx.x;
+  TG_PH(0);
+  h.k0 = b * bd.w;
+  h.nk = min(K - h.k0, bd.w);
+  h.start = bstart[b];
+  h.nb = bstart[b + 1] - h.start;
+  TG_PH(1);
+  if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest
+    bkt_count_keys(kin, bd, K, tot, sm.cnt, sm.part, h);
+    bkt_emit_global(kin, vin, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
     return false;
   }
-  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {
-    const uint32_t k = kin[h.start + j];
-    sm.idx[atomicAdd(&sm.cnt[k - h.k0], 1u)] = vin[h.start + j];
+  uint32_t kk[kIPT], ix[kIPT];
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    const uint32_t j = u * kBlock + threadIdx.x;
+    kk[u] = 0xFFFFFFFFu;
+    ix[u] = 0;
+    if (j < h.nb) { kk[u] = kin[h.start + j] - h.k0; ix[u] = vin[h.start + j]; }
+  }
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) sm.cnt[i] = 0;
+  if (threadIdx.x == 0) sm.maxlen = 0;
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u)
+    if (kk[u] != 0xFFFFFFFFu) load_rec(batch + ix[u], rec[u]);  // issued before the LDS work below
+  __syncthreads();
+  TG_PH(2);
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u)
+    if (kk[u] != 0xFFFFFFFFu) atomicAdd(&sm.cnt[kk[u]], 1u);
+  __syncthreads();
+  TG_PH(3);
+  // exclusive scan of the key counts (each thread a contiguous run of keys) + longest run
+  const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = threadIdx.x * per;
+  uint32_t sum = 0, mx = 0;
+  for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) { sum += sm.cnt[i0 + i]; mx = max(mx, sm.cnt[i0 + i]); }
+  sm.part[threadIdx.x] = sum;
+  if (mx) atomicMax(&sm.maxlen, mx);
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = threadIdx.x >= o ? sm.part[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sm.part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = sm.part[threadIdx.x] - sum;
+  for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
+    const uint32_t len = sm.cnt[i0 + i];
+    sm.cnt[i0 + i] = run;
+    run += len;
   }
   __syncthreads();
-  *list = sm.idx;
-  if (maxlen <= (uint32_t)kThreadSeg) return true;  // block-uniform
-  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // spill the long keys
-    const uint32_t a = i ? sm.cnt[i - 1] : 0u, len = sm.cnt[i] - a;
-    if (len <= (uint32_t)kThreadSeg) continue;
-    const uint32_t k = h.k0 + i, g = h.start + a;
-    for (uint32_t u = 0; u < len; ++u) { kout[g + u] = k; vout[g + u] = sm.idx[a + u]; }
-    off[k] = g;
-    off[k + 1] = g + len;
-    if (len > (uint32_t)kTile) {
-      const uint32_t li = atomicAdd(&sc->n_large, 1u);
-      LargeSeg L;
-      L.seg = k; L.start = g; L.len = len; L.pad = 0;
-      large[li] = L;
-      atomicMax(&sc->max_large, len);
-    } else {
-      medium[atomicAdd(&sc->n_medium, 1u)] = k;
+  TG_PH(4);
+  // slots + sort keys (from the registers: no second gather)
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    slot[u] = 0xFFFFFFFFu;
+    if (kk[u] == 0xFFFFFFFFu) continue;
+    const uint32_t s = atomicAdd(&sm.cnt[kk[u]], 1u);
+    slot[u] = s;
+    keyfn(rec[u], ix[u], sm.k1[s], sm.k2[s], sm.k3[s]);
+    sm.key[s] = (uint16_t)kk[u];
+  }
+  __syncthreads();  // cnt[k] is now the END of key k's run
+  TG_PH(5);
+  // rank inside the run
+  for (uint32_t s = threadIdx.x; s < h.nb; s += kBlock) {
+    const uint32_t k = sm.key[s];
+    const uint32_t a = k ? sm.cnt[k - 1] : 0u, e = sm.cnt[k];
+    if (e - a > kBktRankMax) continue;
+    const uint64_t x1 = sm.k1[s], x2 = sm.k2[s];
+    const uint32_t x3 = sm.k3[s];
+    // k1 alone decides almost every comparison: four k1 loads in flight, the tie-break only on ties
+    uint32_t r = 0, i = a;
+    for (; i + 4 <= e; i += 4) {
+      uint64_t y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = sm.k1[i + j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r += y[j] < x1 ? 1u : 0u;
+        if (y[j] == x1) r += k3less(y[j], sm.k2[i + j], sm.k3[i + j], x1, x2, x3) ? 1u : 0u;
+      }
+    }
+    for (; i < e; ++i) {
+      const uint64_t y = sm.k1[i];
+      r += y < x1 ? 1u : 0u;
+      if (y == x1) r += k3less(y, sm.k2[i], sm.k3[i], x1, x2, x3) ? 1u : 0u;
+    }
+    if (by_pos) sm.ord[a + r] = (uint16_t)s;
+    else sm.ord[s] = (uint16_t)(a + r);
+  }
+  if (sm.maxlen > kBktRankMax) {  // block-uniform: write the long keys out for k_rest
+    for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
+      const uint32_t a = i ? sm.cnt[i - 1] : 0u, len = sm.cnt[i] - a;
+      if (len <= kBktRankMax) continue;
+      const uint32_t k = h.k0 + i, g = h.start + a;
+      for (uint32_t u = 0; u < len; ++u) { kout[g + u] = k; vout[g + u] = sm.k3[a + u] & 0x7FFFFFFFu; }
+      off[k] = g;
+      off[k + 1] = g + len;
+      if (len > (uint32_t)kTile) {
+        const uint32_t li = atomicAdd(&sc->n_large, 1u);
+        LargeSeg L;
+        L.seg = k; L.start = g; L.len = len; L.pad = 0;
+        large[li] = L;
+        atomicMax(&sc->max_large, len);
+      } else {
+        medium[atomicAdd(&sc->n_medium, 1u)] = k;
+      }
     }
   }
   __syncthreads();
+  TG_PH(6);
   return true;
 }
 
-// Per round of kBlock keys: the calling thread's key run (0 if it is longer than kThreadSeg) and the
-// block's longest such run.
-template <class SM>
-__device__ __forceinline__ uint32_t bkt_round(SM& sm, const BktHead& h, uint32_t i, uint32_t& a, uint32_t& M) {
-  uint32_t len = 0;
-  a = 0;
-  if (i < h.nk) {
-    a = i ? sm.cnt[i - 1] : 0u;
-    len = sm.cnt[i] - a;
-    if (len > (uint32_t)kThreadSeg) len = 0;
-  }
-  if (threadIdx.x == 0) { sm.rmax = 0; sm.tb.any_x = 0; }
-  __syncthreads();
-  if (len) atomicMax(&sm.rmax, len);
-  __syncthreads();
-  M = sm.rmax;
-  return len;
+// length of the run of the key owning LDS slot s
+__device__ __forceinline__ uint32_t run_len(const BktFusedSmem& sm, uint32_t s) {
+  const uint32_t k = sm.key[s];
+  return sm.cnt[k] - (k ? sm.cnt[k - 1] : 0u);
 }
+
+struct TBKey {
+  __device__ __forceinline__ void operator()(const tgsim_record& r, uint32_t idx, uint64_t& k1, uint64_t& k2,
+                                             uint32_t& k3) const {
+    k1 = (uint64_t)r.t;                                                                  // netem time_to_send
+    k2 = ((uint64_t)r.seq << 32) | ((r.meta & TGSIM_F_CLONE) ? 0u : 0x80000000u) | r.size;  // seq, clone first, size
+    k3 = idx;
+  }
+};
 
 __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, const uint32_t* kin, const uint32_t* vin,
-                                                      uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
-                                                      uint32_t K, const uint32_t* tot, uint32_t* off,
-                                                      uint32_t* medium, LargeSeg* large, DevScalars* sc) {
-  __shared__ BktFusedSmem<false> sm;
+                                                      uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
+                                                      uint32_t K, const uint32_t* tot, const uint32_t* bstart,
+                                                      uint32_t* off, uint32_t* medium, LargeSeg* large,
+                                                      DevScalars* sc) {
+  __shared__ BktFusedSmem sm;
   BktHead h;
-  const uint32_t* list;
-  bkt_fused_group(kin, vin, kout, vout, bs, B, K, tot, off, nullptr, medium, large, sc, sm, h, &list);
-  for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
-    uint32_t a, M;
-    const uint32_t i = r * kBlock + threadIdx.x;
-    const uint32_t len = bkt_round(sm, h, i, a, M);
-    if (M == 0) continue;  // block-uniform
+  tgsim_record rec[kIPT];
+  uint32_t slot[kIPT];
+  if (!bkt_fused_load<true>(kin, vin, kout, vout, bd, B, K, tot, bstart, off, nullptr, medium, large, sc, sm, h, p.A,
+                      TBKey{}, rec, slot))
+    return;
+  // the GCRA along each sender's run (one thread per sender); departures replace k1
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
+    const uint32_t a = i ? sm.cnt[i - 1] : 0u, e = sm.cnt[i];
+    if (e == a || e - a > kBktRankMax) continue;
     const uint32_t sl = h.k0 + i;
-    if (M <= 4) tb_thread_body<4>(p, list, sl, a, len, sm.tb);
-    else if (M <= 8) tb_thread_body<8>(p, list, sl, a, len, sm.tb);
-    else tb_thread_body<16>(p, list, sl, a, len, sm.tb);
-    __syncthreads();
+    const ShapeDev sh = p.shape[sl];
+    int64_t x = p.X[sl];
+    for (uint32_t r = a; r < e; ++r) {
+      const uint32_t s = sm.ord[r];
+      const int64_t t = (int64_t)sm.k1[s];
+      uint64_t c = ((uint64_t)(sm.k2[s] & 0x7FFFFFFFu) * sh.mult) >> sh.shift;
+      c = c > kCostClamp ? kCostClamp : c;
+      const int64_t d = t > x ? t : x;
+      const int64_t b0 = x > t - sh.tau ? x : t - sh.tau;
+      const int64_t v = b0 + (int64_t)c;
+      x = v > kTbClamp ? kTbClamp : v;
+      sm.k1[s] = (uint64_t)d;
+    }
+    p.X[sl] = x;
   }
-}
-
-template <int M>
-__device__ __forceinline__ void emit_seg_body(const EmitPolicy& p, const uint32_t* list, uint32_t seg, uint32_t a,
-                                              uint32_t len, uint32_t* stage, uint32_t gbase) {
-  uint64_t k1[M], k2[M];
-  uint32_t k3[M];
-  thread_keys<EmitPolicy, M>(p, list, seg, a, len, k1, k2, k3);
+  __syncthreads();
+  TG_PH(7);
+  // route each departed copy from the registers (D now, L later, X another shard); one
+  // reservation per queue for the whole block
+  const int64_t t_end = sc->t_end;
+  int code[kIPT];
+  uint32_t nD = 0, nL = 0, nX = 0;
 #pragma unroll
-  for (int u = 0; u < M; ++u) {
-    if ((uint32_t)u < len) {
-      if (stage) stage[a + u] = k3[u];
-      else p.write(gbase + a + u, k3[u]);
+  for (int u = 0; u < kIPT; ++u) {
+    code[u] = -1;
+    if (slot[u] == 0xFFFFFFFFu || run_len(sm, slot[u]) > kBktRankMax) continue;
+    rec[u].t = (int64_t)sm.k1[slot[u]];
+    rec[u].meta |= TGSIM_F_STAGE_D;
+    code[u] = qid_stage_d(p.geo, rec[u].dst, rec[u].t, t_end);
+    nD += code[u] == Q_D; nL += code[u] == Q_L; nX += code[u] >= Q_X0;
+  }
+  if (threadIdx.x == 0) sm.flag = 0;
+  __syncthreads();
+  if (nX) sm.flag = 1;
+  uint32_t tD, tL;
+  block_scan2(nD, nL, sm.part, tD, tL);  // nD/nL: this thread's offsets inside the block's runs
+  const Queues& Q = p.Q;
+  const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
+  __syncthreads();  // every thread has read the scan partials in sm.part
+  if (threadIdx.x == 0) {
+    sm.part[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
+    sm.part[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
+  }
+  __syncthreads();
+  uint32_t pD = sm.part[0] + nD, pL = sm.part[1] + nL;
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    if (code[u] != Q_D && code[u] != Q_L) continue;
+    const bool isD = code[u] == Q_D;
+    const uint32_t pos = isD ? pD++ : pL++;
+    if (pos < Q.subcap) {
+      store_rec((isD ? Q.D : Q.L) + (size_t)sub * Q.subcap + pos, rec[u]);
+      Q.K[isD ? Q_D : Q_L][(size_t)sub * Q.subcap + pos] = Q.key_of(isD ? Q_D : Q_L, rec[u]);
+    } else {
+      atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
     }
   }
+  if (sm.flag) {  // cross-shard copies (S > 1): wave appends onto the peer blocks
+#pragma unroll
+    for (int u = 0; u < kIPT; ++u) Q.push(code[u] >= Q_X0 ? code[u] : -1, rec[u], (uint32_t)u);
+  }
+  TG_PH_END(0, h.nb);
 }
+
+struct EmitKey {
+  __device__ __forceinline__ void operator()(const tgsim_record& r, uint32_t idx, uint64_t& k1, uint64_t& k2,
+                                             uint32_t& k3) const {
+    k1 = (uint64_t)r.t;                                          // delivery time
+    k2 = ((uint64_t)r.src << 32) | r.seq;                        // src, seq
+    k3 = (((r.meta & TGSIM_F_CLONE) ? 0u : 1u) << 31) | idx;     // clone first
+  }
+};
 
 __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, const uint32_t* kin, const uint32_t* vin,
-                                                        uint32_t* kout, uint32_t* vout, int bs, uint32_t B,
-                                                        uint32_t K, const uint32_t* tot, uint32_t* off,
-                                                        uint32_t* off2, uint32_t* medium, LargeSeg* large,
-                                                        DevScalars* sc) {
-  __shared__ BktFusedSmem<true> sm;
+                                                        uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
+                                                        uint32_t K, const uint32_t* tot, const uint32_t* bstart,
+                                                        uint32_t* off, uint32_t* off2, uint32_t* medium,
+                                                        LargeSeg* large, DevScalars* sc) {
+  __shared__ BktFusedSmem sm;
   BktHead h;
-  const uint32_t* list;
-  const bool in_lds = bkt_fused_group(kin, vin, kout, vout, bs, B, K, tot, off, off2, medium, large, sc, sm, h, &list);
-  if (in_lds) {
-    for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
-      const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
-      off[h.k0 + i] = o;
-      off2[h.k0 + i] = o;
-    }
-    if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
-    for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) sm.stage[j] = 0xFFFFFFFFu;  // long keys: k_rest writes
+  tgsim_record rec[kIPT];
+  uint32_t slot[kIPT];
+  if (!bkt_fused_load<false>(kin, vin, kout, vout, bd, B, K, tot, bstart, off, off2, medium, large, sc, sm, h, p.D,
+                      EmitKey{}, rec, slot))
+    return;
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
+    const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
+    off[h.k0 + i] = o;
+    off2[h.k0 + i] = o;
   }
-  __syncthreads();
-  uint32_t* stage = in_lds ? sm.stage : nullptr;
-  for (uint32_t r = 0; r * kBlock < h.nk; ++r) {
-    uint32_t a, M;
-    const uint32_t i = r * kBlock + threadIdx.x;
-    const uint32_t len = bkt_round(sm, h, i, a, M);
-    if (M == 0) continue;
-    const uint32_t seg = h.k0 + i;
-    if (M <= 4) emit_seg_body<4>(p, list, seg, a, len, stage, h.start);
-    else if (M <= 8) emit_seg_body<8>(p, list, seg, a, len, stage, h.start);
-    else emit_seg_body<16>(p, list, seg, a, len, stage, h.start);
+  if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
+  TG_PH(7);
+  // each thread writes its own items at their inbox positions (long keys: k_rest)
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    if (slot[u] == 0xFFFFFFFFu || run_len(sm, slot[u]) > kBktRankMax) continue;
+    const uint32_t o = h.start + sm.ord[slot[u]];
+    const tgsim_record& r = rec[u];
+    p.o_t[o] = r.t; p.o_src[o] = r.src; p.o_dst[o] = r.dst; p.o_seq[o] = r.seq; p.o_size[o] = r.size;
+    p.o_flags[o] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; p.o_coff[o] = r.corrupt_off;
   }
-  if (!in_lds) return;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {  // coalesced SoA
-    const uint32_t v = sm.stage[j];
-    if (v != 0xFFFFFFFFu) p.write(h.start + j, v);
-  }
+  TG_PH_END(1, h.nb);
 }
 
 // ============================================================================================
@@ -2424,16 +2590,27 @@ static int bkt_shift(uint32_t K) {
   return std::max(bits - kMaxDigitBits, std::min(7, bits));
 }
 
-static int bkt_shift_fused(uint32_t K) {  // 256 keys per bucket: one key per thread of the fused consumers
-  const int bits = bits_for(K);
-  return std::max(bits - kMaxDigitBits, std::min(8, bits));
+static BktDiv bkt_div(uint32_t w) {
+  BktDiv b;
+  b.w = w;
+  b.m = ((1ull << 32) + w - 1) / w;
+  return b;
+}
+
+// Keys per bucket of the fused consumers: >= 128 keys (~1k items of a storm) per workgroup, and
+// few enough buckets that they all run in one wave of workgroups (3 per CU); <= 512 keys.
+static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
+  const uint32_t slots = 3u * (uint32_t)d.n_cu;
+  uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(128u, K));
+  w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
+  return std::max<uint32_t>(w, 1u);
 }
 
 // Passes 1-2 of the bucketed group-by: (keys1, vals1) in bucket order, bucket totals in d.tot.
-static hipError_t bkt_partition(Dev& d, const BktSrc& src, int bs, uint32_t B) {
+static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
   {
     ProfScope ps_(d, KID_BKT_HIST);
-    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bs, B, d.hist);
+    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bd, B, d.hist);
   }
   {
     ProfScope ps_(d, KID_RADIX_ROWS);
@@ -2441,24 +2618,25 @@ static hipError_t bkt_partition(Dev& d, const BktSrc& src, int bs, uint32_t B) {
   }
   {
     ProfScope ps_(d, KID_BKT_SCATTER);
-    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bs, B,
-                       d.hist, d.tot);
+    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bd, B,
+                       d.hist, d.tot, d.bstart);
   }
   return hipGetLastError();
 }
 
 // Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
 // d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
-static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t thread_max, uint32_t* off2,
+static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t medium_above, uint32_t* off2,
                                uint32_t** keys, uint32_t** vals) {
   const int bs = bkt_shift(K);
   if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
   const uint32_t B = (K + (1u << bs) - 1) >> bs;
-  TG_CHECK(bkt_partition(d, src, bs, B));
+  const BktDiv bd = bkt_div(1u << bs);
+  TG_CHECK(bkt_partition(d, src, bd, B));
   {
     ProfScope ps_(d, KID_BKT_SORT);
-    hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bs, B, K,
-                       d.tot, d.seg_off, off2, thread_max, d.medium, d.large, d.sc);
+    hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bd, B, K,
+                       d.tot, d.seg_off, off2, medium_above, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
   *keys = d.keys0;
@@ -2514,14 +2692,13 @@ static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
-  const int bs = bkt_shift_fused(d.nloc);
-  if (bs > kBktFusedKeyBits) return hipErrorInvalidValue;  // nloc <= 2^20 (checked at create)
-  const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
-  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_A), bs, B));
+  const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
+  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= 2048: nloc <= 2^20 (checked at create)
+  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_A), bd, B));
   {
     ProfScope ps_(d, KID_TB);
-    hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs, B,
-                       d.nloc, d.tot, d.seg_off, d.medium, d.large, d.sc);
+    hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bd, B,
+                       d.nloc, d.tot, d.bstart, d.seg_off, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
   return launch_rest(d, p, d.keys0, d.vals0);
@@ -2559,14 +2736,13 @@ static hipError_t run_deliveries(Dev& d) {
   EmitPolicy p;
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
-  const int bs = bkt_shift_fused(d.nloc);
-  if (bs > kBktFusedKeyBits) return hipErrorInvalidValue;
-  const uint32_t B = (d.nloc + (1u << bs) - 1) >> bs;
-  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_D), bs, B));
+  const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
+  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
+  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_D), bd, B));
   {
     ProfScope ps_(d, KID_EMIT);
-    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bs,
-                       B, d.nloc, d.tot, d.seg_off, d.inbox, d.medium, d.large, d.sc);
+    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bd,
+                       B, d.nloc, d.tot, d.bstart, d.seg_off, d.inbox, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
   return launch_rest(d, p, d.keys0, d.vals0);
@@ -2577,7 +2753,7 @@ static hipError_t run_wheel_insert(Dev& d) {
   const BktSrc src = bkt_queue(d, Q_L);
   {
     ProfScope ps_(d, KID_BKT_HIST);
-    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, 0, d.slots, d.hist);
+    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bkt_div(1), d.slots, d.hist);
   }
   {
     ProfScope ps_(d, KID_RADIX_ROWS);
@@ -2620,7 +2796,7 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
       uint32_t *keys, *vals;
       BktSrc src = bkt_queue(d, Q_A);
       src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
-      TG_CHECK(group_by_bkt(d, src, K, 0, nullptr, &keys, &vals));
+      TG_CHECK(group_by_bkt(d, src, K, kNoMedium, nullptr, &keys, &vals));
       SigPolicy p;
       p.inst = d.s_inst; p.t = d.s_t; p.count = d.st_count; p.seq_out = d.s_seq; p.log = d.sig_log;
       p.log_base = log_base; p.kmin = kmin;
@@ -2659,3 +2835,10 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 }
 
 }  // namespace tgsim
+
+#ifdef TGSIM_PHASE_PROF
+// debug builds only: the phase clocks of the last k_tb_bucket / k_emit_bucket launches
+extern "C" int tgsim_debug_phases(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_tg_ph), sizeof(tgsim::g_tg_ph));
+}
+#endif

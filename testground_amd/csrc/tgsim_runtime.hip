@@ -176,6 +176,11 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   c->N = cfg->n_instances;
   c->S = cfg->n_shards;
   c->shard = cfg->shard_id;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, (int)cfg->device) == hipSuccess && ncu > 0)
+      c->d.n_cu = ncu;
+  }
   c->lo = (uint32_t)(((uint64_t)c->shard * c->N) / c->S);
   c->hi = (uint32_t)(((uint64_t)(c->shard + 1) * c->N) / c->S);
   c->nloc = c->hi - c->lo;
@@ -256,6 +261,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.vals1, d.cap_rec);
   rc |= dalloc(c, &d.hist, (size_t)kMaxBins * kRadixBlocks);
   rc |= dalloc(c, &d.tot, kMaxBins);
+  rc |= dalloc(c, &d.bstart, kMaxBins + 1);
   rc |= dalloc(c, &d.qc, (size_t)3 * kNSub * 32);
   rc |= dalloc(c, &d.sig_red, 4);
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
