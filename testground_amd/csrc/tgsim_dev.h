@@ -98,7 +98,8 @@ struct Dev {
   uint32_t* w_target = nullptr;
   int64_t* w_twait = nullptr;
   int64_t* w_release = nullptr;
-  int64_t* sig_red = nullptr;     // [4] count-only batch reduction: n, tmin, tmax
+  int64_t* sig_part = nullptr;    // [2 * 4096] per-block (min, max) of a signal batch
+  int64_t* sig_red = nullptr;     // [4] count-only batch: last tmin, running tmin, running tmax, last tmax
   unsigned long long* stats = nullptr;  // [kNSub][16] sharded k_shape counters (ST_MSGS..ST_LOCAL)
 };
 
@@ -110,7 +111,6 @@ hipError_t launch_set_window(Dev& d, int64_t t_end);
 hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns);
 hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
-hipError_t storm_local_release(Dev& d, uint32_t n);  // max signal time of the staged storm batch -> sig_red[2]
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)
@@ -121,6 +121,6 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
 hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait);
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters);
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
-                            uint32_t size, int64_t spread_ns, uint32_t state);
+                            uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters);
 
 }  // namespace tgsim

@@ -2173,20 +2173,109 @@ __global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint
   }
 }
 
-__global__ void k_sig_red_init(int64_t* red) {
-  red[0] = 0; red[1] = INT64_MAX; red[2] = INT64_MIN; red[3] = 0;
+// Sync-service state a kernel needs to commit a count-only signal batch and resolve waiters.
+struct SigState {
+  uint32_t* count;
+  int64_t* last;
+  uint32_t* nchunks;
+  SigChunk* chunks;
+  const int64_t* log;
+  const uint32_t* w_state;
+  const uint32_t* w_target;
+  const int64_t* w_twait;
+  int64_t* w_release;
+  int64_t* red;   // [4]: the last batch's tmin at [0], tmax at [3]
+  int64_t* part;  // [2 * kSigParts]: per-block (min, max) of a batch
+  DevScalars* sc;
+};
+
+constexpr uint32_t kSigParts = 4096;  // blocks of a batch reduction (grid-stride beyond)
+
+// Commit a count-only batch of n signals of state st with times in [tmin, tmax] (one thread).
+__device__ __forceinline__ void sig_commit_count(const SigState& g, uint32_t n, uint32_t st, int64_t tmin,
+                                                 int64_t tmax) {
+  if (n == 0) return;
+  if (g.count[st] > 0 && tmin < g.last[st]) atomicOr(&g.sc->err, ERR_SIG_ORDER);
+  const uint32_t c = g.nchunks[st];
+  if (c >= (uint32_t)kMaxChunksPerState) {
+    atomicOr(&g.sc->err, ERR_STATE_CHUNKS);
+  } else {
+    SigChunk ch;
+    ch.seq_start = g.count[st] + 1u; ch.len = n; ch.log_pos = 0;
+    ch.tmin = tmin; ch.tmax = tmax; ch.sorted = 0; ch.pad = 0;
+    g.chunks[(size_t)st * kMaxChunksPerState + c] = ch;
+    g.nchunks[st] = c + 1;
+  }
+  g.count[st] += n;
+  g.last[st] = tmax;
 }
 
-// Count-only batch (one state, no sequence numbers): min and max time by block reduction.
-__global__ __launch_bounds__(kBlock) void k_sig_reduce(const int64_t* t, const uint32_t* n_ptr, int64_t* red) {
-  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
-  const uint32_t n = *n_ptr;
-  int64_t mn = INT64_MAX, mx = INT64_MIN;
+// A waiter's release time: the time of the target-th signal of its state. For a count-only chunk
+// only its first and last member are known (min / max time); other targets set ERR_UNSORTED_TARGET.
+__device__ __forceinline__ void resolve_waiter(const SigState& g, uint32_t w) {
+  if (g.w_release[w] >= 0) return;
+  const uint32_t st = g.w_state[w], tg = g.w_target[w];
+  const int64_t tw = g.w_twait[w];
+  if (tg == 0) { g.w_release[w] = tw; return; }
+  if (g.count[st] < tg) return;
+  const uint32_t nc = g.nchunks[st];
+  for (uint32_t c = 0; c < nc; ++c) {
+    const SigChunk ch = g.chunks[(size_t)st * kMaxChunksPerState + c];
+    if (tg >= ch.seq_start && tg < ch.seq_start + ch.len) {
+      int64_t t;
+      if (ch.sorted) t = g.log[ch.log_pos + (tg - ch.seq_start)];
+      else if (tg == ch.seq_start + ch.len - 1) t = ch.tmax;
+      else if (tg == ch.seq_start) t = ch.tmin;
+      else { atomicOr(&g.sc->err, ERR_UNSORTED_TARGET); return; }
+      g.w_release[w] = t > tw ? t : tw;
+      return;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_waiters(SigState g, uint32_t nw) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int64_t v = t[i];
-    mn = v < mn ? v : mn;
-    mx = v > mx ? v : mx;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) resolve_waiter(g, w);
+}
+
+__global__ void k_add_waiter(SigState g, uint32_t* w_state, uint32_t* w_target, int64_t* w_twait, uint32_t i,
+                             uint32_t state, uint32_t target, int64_t t_wait) {
+  w_state[i] = state; w_target[i] = target;
+  w_twait[i] = t_wait == INT64_MIN ? g.sc->t_end : t_wait;
+  g.w_release[i] = -1;
+  resolve_waiter(g, i);  // the other waiters can only move when signals arrive
+}
+
+// Block-reduce (min, max) of a signal batch into this block's partial (no atomics: a batch has
+// thousands of blocks, and same-address device atomics serialise at the memory side).
+__device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn, int64_t mx) {
+  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smin[w] = mn; smax[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
+    g.part[2 * blockIdx.x] = mn;
+    g.part[2 * blockIdx.x + 1] = mx;
+  }
+}
+
+// One block: the batch's (min, max) from the partials -> red[0], red[3]; with commit, the batch is
+// committed count-only to state st and waiters [0, nw) are resolved.
+__global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t nparts, uint32_t commit, uint32_t n,
+                                                       uint32_t st, uint32_t nw) {
+  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) {
+    const int64_t a = g.part[2 * i], b = g.part[2 * i + 1];
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2199,64 +2288,26 @@ __global__ __launch_bounds__(kBlock) void k_sig_reduce(const int64_t* t, const u
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
-    if (mn != INT64_MAX) {
-      atomicMin(reinterpret_cast<long long*>(&red[1]), (long long)mn);
-      atomicMax(reinterpret_cast<long long*>(&red[2]), (long long)mx);
-    }
+    g.red[0] = mn;
+    g.red[3] = mx;
+    if (commit) sig_commit_count(g, n, st, mn, mx);
+  }
+  if (commit && nw) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nw; i += kBlock) resolve_waiter(g, i);
   }
 }
 
-__global__ void k_sig_commit_count(const uint32_t* n_ptr, uint32_t st, const int64_t* red, uint32_t* count,
-                                   int64_t* last, uint32_t* nchunks, SigChunk* chunks, DevScalars* sc) {
-  const uint32_t n = *n_ptr;
-  if (n == 0) return;
-  if (count[st] > 0 && red[1] < last[st]) atomicOr(&sc->err, ERR_SIG_ORDER);
-  const uint32_t c = nchunks[st];
-  if (c >= (uint32_t)kMaxChunksPerState) {
-    atomicOr(&sc->err, ERR_STATE_CHUNKS);
-  } else {
-    SigChunk ch;
-    ch.seq_start = count[st] + 1u; ch.len = n; ch.log_pos = 0;
-    ch.tmin = red[1]; ch.tmax = red[2]; ch.sorted = 0; ch.pad = 0;
-    chunks[(size_t)st * kMaxChunksPerState + c] = ch;
-    nchunks[st] = c + 1;
-  }
-  count[st] += n;
-  last[st] = red[2];
-}
-
-__global__ void k_add_waiter(uint32_t* w_state, uint32_t* w_target, int64_t* w_twait, int64_t* w_release,
-                             uint32_t i, uint32_t state, uint32_t target, int64_t t_wait, const DevScalars* sc) {
-  w_state[i] = state; w_target[i] = target; w_twait[i] = t_wait == INT64_MIN ? sc->t_end : t_wait; w_release[i] = -1;
-}
-
-// A waiter's release time: the time of the target-th signal of its state. For a count-only chunk
-// only its first and last member are known (min / max time); other targets set ERR_UNSORTED_TARGET.
-__global__ __launch_bounds__(kBlock) void k_waiters(uint32_t nw, const uint32_t* w_state, const uint32_t* w_target,
-                                                    const int64_t* w_twait, int64_t* w_release,
-                                                    const uint32_t* count, const uint32_t* nchunks,
-                                                    const SigChunk* chunks, const int64_t* log, DevScalars* sc) {
+// Count-only batch (one state, no sequence numbers): min and max time, then the commit.
+__global__ __launch_bounds__(kBlock) void k_sig_count(SigState g, const int64_t* t, uint32_t n) {
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
-    if (w_release[w] >= 0) continue;
-    const uint32_t st = w_state[w], tg = w_target[w];
-    const int64_t tw = w_twait[w];
-    if (tg == 0) { w_release[w] = tw; continue; }
-    if (count[st] < tg) continue;
-    const uint32_t nc = nchunks[st];
-    for (uint32_t c = 0; c < nc; ++c) {
-      const SigChunk ch = chunks[(size_t)st * kMaxChunksPerState + c];
-      if (tg >= ch.seq_start && tg < ch.seq_start + ch.len) {
-        int64_t t;
-        if (ch.sorted) t = log[ch.log_pos + (tg - ch.seq_start)];
-        else if (tg == ch.seq_start + ch.len - 1) t = ch.tmax;
-        else if (tg == ch.seq_start) t = ch.tmin;
-        else { atomicOr(&sc->err, ERR_UNSORTED_TARGET); break; }
-        w_release[w] = t > tw ? t : tw;
-        break;
-      }
-    }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t v = t[i];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
   }
+  sig_block_partial(g, mn, mx);
 }
 
 // ============================================================================================
@@ -2427,43 +2478,96 @@ __global__ void k_finish(DevScalars* sc) {
 // workload generator: gossip storm round
 // ============================================================================================
 
-__global__ __launch_bounds__(kBlock) void k_gen_storm(uint32_t lo, uint32_t nloc, uint32_t N, uint32_t round,
-                                                      int64_t t0, uint32_t F, uint32_t size, int64_t spread,
-                                                      uint32_t state, uint32_t key0, uint32_t key1,
-                                                      uint32_t base, uint32_t* m_src, uint32_t* m_dst,
-                                                      uint32_t* m_seq, uint32_t* m_size, int64_t* m_t,
-                                                      uint32_t* s_state, uint32_t* s_inst, int64_t* s_t,
-                                                      const DevScalars* sc) {
-  if (t0 == INT64_MIN) t0 = sc->t_end;  // TGSIM_T_NOW: the device's current window start
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += stride) {
-    const uint32_t g = lo + l;
-    uint32_t chosen[32];
-    int64_t tmax = t0;
-    for (uint32_t k = 0; k < F; ++k) {
-      uint32_t out[4];
-      philox4x32_10(g, round, k << 16, kStormSalt, key0, key1, out);
-      const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
-      const int64_t t = t0 + (spread > 0 ? (int64_t)(u % (uint64_t)spread) : 0);
-      uint32_t p;
-      for (uint32_t attempt = 0;; ++attempt) {
-        if (attempt) philox4x32_10(g, round, (k << 16) | attempt, kStormSalt, key0, key1, out);
-        p = out[0] % (N - 1);
-        if (p >= g) ++p;
-        bool dupl = false;
+struct StormArgs {
+  uint32_t lo, nloc, N, round;
+  int64_t t0;
+  uint32_t F, Fp, size, state;
+  int64_t spread;
+  uint32_t key0, key1, base;
+  uint32_t* m_src;
+  uint32_t* m_dst;
+  uint32_t* m_seq;
+  uint32_t* m_size;
+  int64_t* m_t;
+};
+
+// The storm's k-th peer of instance g (drawn without replacement): the first Philox draw of
+// (g, round, k) unless it repeats one of the k earlier peers, then further attempts (ctr word 2 =
+// k << 16 | attempt). Sequential restatement; the kernel below runs it only for a group that drew
+// a repeat.
+__device__ __forceinline__ void storm_peers_serial(const StormArgs& a, uint32_t g, uint32_t l, int64_t t0) {
+  uint32_t chosen[32];
+  for (uint32_t k = 0; k < a.F; ++k) {
+    uint32_t out[4];
+    philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
+    const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
+    const int64_t t = t0 + (a.spread > 0 ? (int64_t)(u % (uint64_t)a.spread) : 0);
+    uint32_t p;
+    for (uint32_t attempt = 0;; ++attempt) {
+      if (attempt) philox4x32_10(g, a.round, (k << 16) | attempt, kStormSalt, a.key0, a.key1, out);
+      p = out[0] % (a.N - 1);
+      if (p >= g) ++p;
+      bool dupl = false;
 #pragma unroll
-        for (uint32_t j = 0; j < 32; ++j) dupl |= (j < k) && chosen[j] == p;
-        if (!dupl) break;
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < 32; ++j)
-        if (j == k) chosen[j] = p;
-      const uint32_t i = base + l * F + k;
-      m_src[i] = g; m_dst[i] = p; m_seq[i] = round * F + k; m_size[i] = size; m_t[i] = t;
-      if (t > tmax) tmax = t;
+      for (uint32_t j = 0; j < 32; ++j) dupl |= (j < k) && chosen[j] == p;
+      if (!dupl) break;
     }
-    s_state[l] = state; s_inst[l] = g; s_t[l] = tmax;
+#pragma unroll
+    for (uint32_t j = 0; j < 32; ++j)
+      if (j == k) chosen[j] = p;
+    const uint32_t i = a.base + l * a.F + k;
+    a.m_dst[i] = p;
   }
+}
+
+// One storm round: every instance sends F messages to F distinct random peers and signals `state`
+// at its latest send time. A group of Fp (power of two >= F) lanes per instance, one message per
+// lane: the first draws of the group are checked for repeats with F shuffles, and only a group
+// that drew a repeat (probability ~F^2/2N) redraws serially, so the output equals the serial
+// restatement (tgo_gen_storm_round). Stores are coalesced (message l*F + k at lane l*Fp + k). The
+// signals are reduced to per-block partials in the same launch (k_sig_commit finishes them).
+__global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) {
+  const int64_t t0 = a.t0 == INT64_MIN ? sg.sc->t_end : a.t0;  // TGSIM_T_NOW: the device's window start
+  const uint32_t total = a.nloc * a.Fp;
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += gridDim.x * kBlock) {  // block-uniform loop
+    const uint32_t tid = b0 + threadIdx.x;
+    const uint32_t l = tid / a.Fp, k = tid % a.Fp;
+    const uint32_t lane = lane_id(), gbase = lane - k;
+    const bool inst = l < a.nloc, msg = inst && k < a.F;
+    const uint32_t g = a.lo + l;
+    uint32_t p = 0xFFFFFFFFu;
+    int64_t t = t0;
+    if (msg) {
+      uint32_t out[4];
+      philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
+      const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
+      t = t0 + (a.spread > 0 ? (int64_t)(u % (uint64_t)a.spread) : 0);
+      p = out[0] % (a.N - 1);
+      if (p >= g) ++p;
+    }
+    bool dup = false;
+    for (uint32_t j = 0; j + 1 < a.F; ++j) {  // lane k compares its draw with lanes j < k of its group
+      const uint32_t q = __shfl(p, (int)(gbase + j));
+      dup |= msg && j < k && q == p;
+    }
+    const uint64_t dmask = __ballot(dup);
+    const uint64_t gmask = (a.Fp >= 64 ? ~0ull : ((1ull << a.Fp) - 1ull)) << gbase;
+    const bool serial = (dmask & gmask) != 0;
+    if (msg) {
+      const uint32_t i = a.base + l * a.F + k;
+      a.m_src[i] = g; a.m_seq[i] = a.round * a.F + k; a.m_size[i] = a.size; a.m_t[i] = t;
+      if (!serial) a.m_dst[i] = p;
+      else if (k == 0) storm_peers_serial(a, g, l, t0);
+    }
+    // the instance's signal time: its latest send
+    for (uint32_t o = a.Fp >> 1; o > 0; o >>= 1) {
+      const int64_t v = __shfl_xor(t, (int)o);
+      t = v > t ? v : t;
+    }
+    if (inst && k == 0) { mn = t < mn ? t : mn; mx = t > mx ? t : mx; }
+  }
+  sig_block_partial(sg, mn, mx);
 }
 
 // ============================================================================================
@@ -2486,6 +2590,14 @@ hipError_t sync_scalars(Dev& d) {
   return hipSuccess;
 }
 
+static SigState sig_state(Dev& d) {
+  SigState g;
+  g.count = d.st_count; g.last = d.st_last; g.nchunks = d.st_nchunks; g.chunks = d.st_chunks; g.log = d.sig_log;
+  g.w_state = d.w_state; g.w_target = d.w_target; g.w_twait = d.w_twait; g.w_release = d.w_release;
+  g.red = d.sig_red; g.part = d.sig_part; g.sc = d.sc;
+  return g;
+}
+
 static hipError_t reset_window(Dev& d) {
   const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
   TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
@@ -2506,14 +2618,6 @@ hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns)
 
 hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns) {
   return window_start(d, WIN_DEVICE, 0, t_end_dev, offset_ns);
-}
-
-hipError_t storm_local_release(Dev& d, uint32_t n) {
-  uint32_t* n_dev = &d.sc->sig_n;
-  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
-  hipLaunchKernelGGL(k_sig_red_init, dim3(1), dim3(1), 0, d.stream, d.sig_red);
-  hipLaunchKernelGGL(k_sig_reduce, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_t, n_dev, d.sig_red);
-  return hipGetLastError();
 }
 
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n) {
@@ -2781,15 +2885,14 @@ hipError_t window_end(Dev& d) {
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
                         bool count_only) {
   if (n) {
-    uint32_t* n_dev = &d.sc->sig_n;
-    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
-    if (count_only) {
-      hipLaunchKernelGGL(k_sig_red_init, dim3(1), dim3(1), 0, d.stream, d.sig_red);
-      hipLaunchKernelGGL(k_sig_reduce, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_t, n_dev, d.sig_red);
-      hipLaunchKernelGGL(k_sig_commit_count, dim3(1), dim3(1), 0, d.stream, n_dev, kmin, d.sig_red, d.st_count,
-                         d.st_last, d.st_nchunks, d.st_chunks, d.sc);
-      TG_CHECK(hipGetLastError());
+    if (count_only) {  // commit and waiters in the same launch
+      const unsigned g = grid_for(n);
+      hipLaunchKernelGGL(k_sig_count, dim3(g), dim3(kBlock), 0, d.stream, sig_state(d), d.s_t, n);
+      hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), g, 1u, n, kmin, n_waiters);
+      return hipGetLastError();
     } else {
+      uint32_t* n_dev = &d.sc->sig_n;
+      hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
       const uint32_t K = kmax - kmin + 1;
       hipLaunchKernelGGL(k_keys_sig, dim3(grid_for(n)), dim3(kBlock), 0, d.stream, d.s_state, n_dev, kmin, d.keys0,
                          d.vals0);
@@ -2813,24 +2916,31 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
 }
 
 hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait) {
-  hipLaunchKernelGGL(k_add_waiter, dim3(1), dim3(1), 0, d.stream, d.w_state, d.w_target, d.w_twait, d.w_release, idx,
-                     state, target, t_wait, d.sc);
+  hipLaunchKernelGGL(k_add_waiter, dim3(1), dim3(1), 0, d.stream, sig_state(d), d.w_state, d.w_target, d.w_twait,
+                     idx, state, target, t_wait);
   return hipGetLastError();
 }
 
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters) {
   if (!n_waiters) return hipSuccess;
-  hipLaunchKernelGGL(k_waiters, dim3(grid_for(n_waiters)), dim3(kBlock), 0, d.stream, n_waiters, d.w_state,
-                     d.w_target, d.w_twait, d.w_release, d.st_count, d.st_nchunks, d.st_chunks, d.sig_log, d.sc);
+  hipLaunchKernelGGL(k_waiters, dim3(grid_for(n_waiters)), dim3(kBlock), 0, d.stream, sig_state(d), n_waiters);
   return hipGetLastError();
 }
 
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
-                            uint32_t size, int64_t spread_ns, uint32_t state) {
+                            uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters) {
   ProfScope ps_(d, KID_GEN);
-  hipLaunchKernelGGL(k_gen_storm, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.lo, d.nloc, d.N, round, t0,
-                     fanout, size, spread_ns, state, d.key0, d.key1, staged_base, d.m_src, d.m_dst, d.m_seq,
-                     d.m_size, d.m_t, d.s_state, d.s_inst, d.s_t, d.sc);
+  StormArgs a;
+  a.lo = d.lo; a.nloc = d.nloc; a.N = d.N; a.round = round; a.t0 = t0; a.F = fanout;
+  a.Fp = 1;
+  while (a.Fp < fanout) a.Fp <<= 1;
+  a.size = size; a.state = state; a.spread = spread_ns; a.key0 = d.key0; a.key1 = d.key1; a.base = staged_base;
+  a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;
+  const uint64_t threads = (uint64_t)d.nloc * a.Fp;
+  const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock, kSigParts);
+  hipLaunchKernelGGL(k_gen_storm, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
+  hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), g, commit ? 1u : 0u, d.nloc,
+                     state, n_waiters);
   return hipGetLastError();
 }
 

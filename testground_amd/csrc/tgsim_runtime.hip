@@ -264,6 +264,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.bstart, kMaxBins + 1);
   rc |= dalloc(c, &d.qc, (size_t)3 * kNSub * 32);
   rc |= dalloc(c, &d.sig_red, 4);
+  rc |= dalloc(c, &d.sig_part, 2 * 4096);
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
@@ -835,8 +836,7 @@ extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target,
   const uint32_t i = c->n_waiters;
   HIPCK(c, add_waiter(d, i, state, target, t_wait), "barrier");
   c->n_waiters++;
-  *w = i;
-  HIPCK(c, resolve_waiters(d, c->n_waiters), "barrier");
+  *w = i;  // k_add_waiter resolves the new waiter; the others can only move when signals arrive
   return TGSIM_OK;
 }
 
@@ -870,22 +870,18 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
-  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state), "gen storm");
+  // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so a
+  // single shard commits the batch count-only (count, first/last time) in the same
+  // launch; sharded, the release time is the MAX over shards of the local latest signal (sig_red[3]).
+  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state, c->S == 1, c->n_waiters),
+        "gen storm");
   c->n_staged += (uint32_t)n;
-  if (c->S == 1) {
-    // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
-    // batch is committed count-only (count, first/last time), DESIGN.md 2.7.
-    HIPCK(c, signal_batch(c->d, c->nloc, state, state, c->sig_log_used, c->n_waiters, true), "storm signals");
-  } else {
-    // sharded: the release time is the MAX over shards of the local latest signal
-    HIPCK(c, storm_local_release(c->d, c->nloc), "storm release");
-  }
   return TGSIM_OK;
 }
 
 extern "C" int tgsim_storm_release_device(tgsim_ctx* c, int64_t* out) {
   if (!c || !out) return TGSIM_EINVAL;
   if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
-  HIPCK(c, hipMemcpyAsync(out, c->d.sig_red + 2, sizeof(int64_t), hipMemcpyDeviceToDevice, c->d.stream), "release");
+  HIPCK(c, hipMemcpyAsync(out, c->d.sig_red + 3, sizeof(int64_t), hipMemcpyDeviceToDevice, c->d.stream), "release");
   return TGSIM_OK;
 }

@@ -34,6 +34,14 @@ def test_storm_rounds(hip, oracle):
     S.assert_same(S.run_storm(hip), S.run_storm(oracle))
 
 
+@pytest.mark.parametrize("n_inst,fanout", [(12, 10), (300, 5), (64, 1), (100, 32), (33, 3)])
+def test_storm_fanouts(hip, oracle, n_inst, fanout):
+    """Lane groups of the next power of two >= fanout; small populations force repeated draws
+    (the serial redraw path) in most groups."""
+    S.assert_same(S.run_storm(hip, n_inst=n_inst, rounds=3, fanout=fanout),
+                  S.run_storm(oracle, n_inst=n_inst, rounds=3, fanout=fanout))
+
+
 @pytest.mark.parametrize("case", SC.CASES, ids=lambda f: f.__name__[5:])
 def test_semantics_hip(hip, case):
     case(hip)
