@@ -113,6 +113,9 @@ def cpu_baseline(args, shapes):
                       f"warm-up rounds"}
 
 
+PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,6 +210,14 @@ def main():
     bytes_total = BYTE_MODELS[dominant](delta)
     avg_ms = kern_ms / max(kern_n, 1)
     achieved = (bytes_total / max(kern_n, 1)) / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
+    # measured HBM bytes per launch of the dominant kernel: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+    # this same command (tools/prof_round.sh -> tools/pmc_traffic.py), committed under profiles/
+    traffic, traffic_src = None, None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_TRAFFIC)
+    if os.path.exists(pmc):
+        k = json.load(open(pmc))["kernels"].get(dominant)
+        if k:
+            traffic, traffic_src = k["traffic_bytes"], PMC_TRAFFIC
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, shapes)
@@ -240,7 +251,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": avg_ms,
                 "bytes_per_launch": bytes_total / max(kern_n, 1),
             },

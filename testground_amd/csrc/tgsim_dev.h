@@ -67,6 +67,8 @@ struct Dev {
   uint32_t* hist = nullptr;       // [kMaxBins * kRadixBlocks]
   uint32_t* tot = nullptr;        // [kMaxBins]
   int n_cu = 256;                 // compute units of the device (bucket widths)
+  int grid_shape = 2048;          // k_shape / k_gen_storm grids (init_launch_geometry)
+  int grid_gen = 2048;
   uint32_t* bstart = nullptr;     // [kMaxBins + 1] bucket starts of the last partition pass
   uint32_t* qc = nullptr;         // [3][kNSub][32] append counters (128 B apart)
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
@@ -120,6 +122,7 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
                         bool count_only);
 hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int64_t t_wait);
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters);
+void init_launch_geometry(Dev& d);
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
                             uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters);
 

@@ -81,6 +81,30 @@ __device__ __forceinline__ void store_rec(tgsim_record* p, const tgsim_record& r
   q[1] = make_uint4(r.seq, r.size, r.meta, r.corrupt_off);
 }
 
+// Block-wide exclusive scan (every thread of the block calls it): a wave scan by shuffles, the
+// four wave totals through red[0..3], two barriers (the second frees red for reuse).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, uint32_t& total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) red[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    const uint32_t a = red[w];
+    pre += w < wave ? a : 0u;
+    total += a;
+  }
+  __syncthreads();
+  return pre + x - v;
+}
+
 __device__ __forceinline__ uint32_t wave_uid() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
 
 // Wave64 compaction onto per-lane counters: lanes whose counter pointer is equal share one
@@ -471,13 +495,11 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
 // The due slot prefix of every live region (records with time < t_end), and region retirement.
 __device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t slots, int64_t slot_ns,
                              uint32_t* plan_start, uint32_t* plan_off, DevScalars* sc, int64_t t_end) {
-  __shared__ uint32_t part[kBlock];
-  __shared__ uint32_t carry;
+  __shared__ uint32_t part[kBlock / 64];
+  uint32_t carry = 0;  // block-uniform
   const uint32_t tid = threadIdx.x;
   const uint32_t tail = sc->reg_tail, head = sc->reg_head, nlive = head - tail;
   const int64_t kabs = t_end > 0 ? (t_end - 1) / slot_ns : -1;
-  if (tid == 0) carry = 0;
-  __syncthreads();
   for (uint32_t base = 0; base < nlive; base += kBlock) {
     const uint32_t k = base + tid;
     uint32_t len = 0;
@@ -495,18 +517,10 @@ __device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t 
       r.consumed = hi;
       plan_start[k] = start;
     }
-    part[tid] = len;
-    __syncthreads();
-    for (uint32_t o = 1; o < kBlock; o <<= 1) {
-      const uint32_t v = tid >= o ? part[tid - o] : 0u;
-      __syncthreads();
-      part[tid] += v;
-      __syncthreads();
-    }
-    if (k < nlive) plan_off[k] = carry + part[tid] - len;
-    __syncthreads();
-    if (tid == kBlock - 1) carry += part[tid];
-    __syncthreads();
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(len, part, total);
+    if (k < nlive) plan_off[k] = carry + ex;
+    carry += total;
   }
   if (tid == 0) {
     plan_off[nlive] = carry;
@@ -891,15 +905,8 @@ __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, cons
   const uint32_t d0 = tid * per;
   uint32_t s = 0;
   for (uint32_t k = 0; k < per && d0 + k < B; ++k) s += tot[d0 + k];
-  part[tid] = s;
-  __syncthreads();
-  for (uint32_t o = 1; o < kBlock; o <<= 1) {
-    const uint32_t v = tid >= o ? part[tid - o] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[tid] - s;
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, part, total);
   for (uint32_t k = 0; k < per && d0 + k < B; ++k) {
     base[d0 + k] = run + (hist ? hist[(d0 + k) * kRadixBlocks + blockIdx.x] : 0u);
     run += tot[d0 + k];
@@ -966,15 +973,8 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv b
     sum += cnt[i0 + i];
     mx = max(mx, cnt[i0 + i]);
   }
-  part[tid] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < kBlock; o <<= 1) {
-    const uint32_t v = tid >= o ? part[tid - o] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[tid] - sum;
+  uint32_t total;
+  uint32_t run = block_excl_scan(sum, part, total);
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
     const uint32_t len = cnt[i0 + i];
     cnt[i0 + i] = run;
@@ -1883,16 +1883,9 @@ __device__ __forceinline__ bool bkt_fused_load(const uint32_t* kin, const uint32
   const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = threadIdx.x * per;
   uint32_t sum = 0, mx = 0;
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) { sum += sm.cnt[i0 + i]; mx = max(mx, sm.cnt[i0 + i]); }
-  sm.part[threadIdx.x] = sum;
   if (mx) atomicMax(&sm.maxlen, mx);
-  __syncthreads();
-  for (uint32_t o = 1; o < kBlock; o <<= 1) {
-    const uint32_t v = threadIdx.x >= o ? sm.part[threadIdx.x - o] : 0u;
-    __syncthreads();
-    sm.part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = sm.part[threadIdx.x] - sum;
+  uint32_t total;
+  uint32_t run = block_excl_scan(sum, sm.part, total);
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
     const uint32_t len = sm.cnt[i0 + i];
     sm.cnt[i0 + i] = run;
@@ -2823,7 +2816,8 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
     a.stats = d.stats;
-    { ProfScope ps_(d, KID_SHAPE); hipLaunchKernelGGL(k_shape, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, a); }
+    const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
+    { ProfScope ps_(d, KID_SHAPE); hipLaunchKernelGGL(k_shape, dim3(g), dim3(kBlock), 0, d.stream, a); }
     TG_CHECK(hipGetLastError());
   }
   TG_CHECK(run_token_bucket(d));
@@ -2927,6 +2921,16 @@ hipError_t resolve_waiters(Dev& d, uint32_t n_waiters) {
   return hipGetLastError();
 }
 
+// Grids of the grid-stride kernels whose register use caps residency below 8 waves per SIMD: one
+// wave of workgroups (resident blocks per CU x CUs), so no tail of late workgroups.
+void init_launch_geometry(Dev& d) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_shape, kBlock, 0) == hipSuccess && b > 0)
+    d.grid_shape = b * d.n_cu;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_gen_storm, kBlock, 0) == hipSuccess && b > 0)
+    d.grid_gen = b * d.n_cu;
+}
+
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
                             uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters) {
   ProfScope ps_(d, KID_GEN);
@@ -2937,7 +2941,8 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   a.size = size; a.state = state; a.spread = spread_ns; a.key0 = d.key0; a.key1 = d.key1; a.base = staged_base;
   a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;
   const uint64_t threads = (uint64_t)d.nloc * a.Fp;
-  const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock, kSigParts);
+  const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock,
+                                                  std::min<uint64_t>(kSigParts, (uint64_t)d.grid_gen));
   hipLaunchKernelGGL(k_gen_storm, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
   hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), g, commit ? 1u : 0u, d.nloc,
                      state, n_waiters);

@@ -300,6 +300,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.w_release, d.max_waiters);
   if (rc) { tgsim_destroy(c); return TGSIM_ENOMEM; }
   c->rules_cap_dev = 1;
+  init_launch_geometry(d);
 
   hipStream_t s = d.stream;
   bool ok = hipMemsetAsync(d.sc, 0, sizeof(DevScalars), s) == hipSuccess &&
