@@ -124,6 +124,11 @@ hipError_t add_waiter(Dev& d, uint32_t idx, uint32_t state, uint32_t target, int
 hipError_t resolve_waiters(Dev& d, uint32_t n_waiters);
 void init_launch_geometry(Dev& d);
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
-                            uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters);
+                            uint32_t size, int64_t spread_ns, uint32_t* nparts);
+// Finish a count-only batch from its per-block partials: (tmin, tmax) -> sig_red[0], [3]; with
+// commit, count it into state st and resolve waiters [0, n_waiters); add: register waiter
+// n_waiters (state, target, t_wait) in the same launch and resolve it.
+hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, uint32_t st, uint32_t n_waiters,
+                             bool add, uint32_t add_state, uint32_t add_target, int64_t add_twait);
 
 }  // namespace tgsim

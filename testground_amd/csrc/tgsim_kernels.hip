@@ -2231,6 +2231,15 @@ __global__ __launch_bounds__(kBlock) void k_waiters(SigState g, uint32_t nw) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) resolve_waiter(g, w);
 }
 
+struct WaiterAdd {
+  uint32_t* w_state;
+  uint32_t* w_target;
+  int64_t* w_twait;
+  uint32_t state, target;
+  int64_t t_wait;
+  uint32_t on;
+};
+
 __global__ void k_add_waiter(SigState g, uint32_t* w_state, uint32_t* w_target, int64_t* w_twait, uint32_t i,
                              uint32_t state, uint32_t target, int64_t t_wait) {
   w_state[i] = state; w_target[i] = target;
@@ -2260,9 +2269,16 @@ __device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn,
 }
 
 // One block: the batch's (min, max) from the partials -> red[0], red[3]; with commit, the batch is
-// committed count-only to state st and waiters [0, nw) are resolved.
+// committed count-only to state st and waiters [0, nw) are resolved. wa.on: a barrier registered
+// right after the batch (waiter nw) is added and resolved in the same launch.
 __global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t nparts, uint32_t commit, uint32_t n,
-                                                       uint32_t st, uint32_t nw) {
+                                                       uint32_t st, uint32_t nw, WaiterAdd wa) {
+  if (wa.on && threadIdx.x == 0) {
+    wa.w_state[nw] = wa.state; wa.w_target[nw] = wa.target;
+    wa.w_twait[nw] = wa.t_wait == INT64_MIN ? g.sc->t_end : wa.t_wait;
+    g.w_release[nw] = -1;
+  }
+  if (wa.on) ++nw;
   __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
   int64_t mn = INT64_MAX, mx = INT64_MIN;
   for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) {
@@ -2285,9 +2301,9 @@ __global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t npar
     g.red[3] = mx;
     if (commit) sig_commit_count(g, n, st, mn, mx);
   }
-  if (commit && nw) {
+  if (nw && (commit || wa.on)) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nw; i += kBlock) resolve_waiter(g, i);
+    for (uint32_t i = commit ? threadIdx.x : nw - 1 + threadIdx.x; i < nw; i += kBlock) resolve_waiter(g, i);
   }
 }
 
@@ -2474,7 +2490,7 @@ __global__ void k_finish(DevScalars* sc) {
 struct StormArgs {
   uint32_t lo, nloc, N, round;
   int64_t t0;
-  uint32_t F, Fp, size, state;
+  uint32_t F, Fp, size;
   int64_t spread;
   uint32_t key0, key1, base;
   uint32_t* m_src;
@@ -2882,8 +2898,7 @@ hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64
     if (count_only) {  // commit and waiters in the same launch
       const unsigned g = grid_for(n);
       hipLaunchKernelGGL(k_sig_count, dim3(g), dim3(kBlock), 0, d.stream, sig_state(d), d.s_t, n);
-      hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), g, 1u, n, kmin, n_waiters);
-      return hipGetLastError();
+      return launch_sig_commit(d, g, true, n, kmin, n_waiters, false, 0, 0, 0);
     } else {
       uint32_t* n_dev = &d.sc->sig_n;
       hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, d.stream, n_dev, n);
@@ -2931,21 +2946,32 @@ void init_launch_geometry(Dev& d) {
     d.grid_gen = b * d.n_cu;
 }
 
+hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, uint32_t st, uint32_t n_waiters,
+                             bool add, uint32_t add_state, uint32_t add_target, int64_t add_twait) {
+  WaiterAdd wa;
+  wa.w_state = d.w_state; wa.w_target = d.w_target; wa.w_twait = d.w_twait;
+  wa.state = add_state; wa.target = add_target; wa.t_wait = add_twait; wa.on = add ? 1u : 0u;
+  hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), nparts, commit ? 1u : 0u, n, st,
+                     n_waiters, wa);
+  return hipGetLastError();
+}
+
+// k_gen_storm only: the batch's per-block partials wait in sig_part for launch_sig_commit (the
+// runtime defers it so that a barrier registered next rides in the same launch). *nparts = grid.
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
-                            uint32_t size, int64_t spread_ns, uint32_t state, bool commit, uint32_t n_waiters) {
+                            uint32_t size, int64_t spread_ns, uint32_t* nparts) {
   ProfScope ps_(d, KID_GEN);
   StormArgs a;
   a.lo = d.lo; a.nloc = d.nloc; a.N = d.N; a.round = round; a.t0 = t0; a.F = fanout;
   a.Fp = 1;
   while (a.Fp < fanout) a.Fp <<= 1;
-  a.size = size; a.state = state; a.spread = spread_ns; a.key0 = d.key0; a.key1 = d.key1; a.base = staged_base;
+  a.size = size; a.spread = spread_ns; a.key0 = d.key0; a.key1 = d.key1; a.base = staged_base;
   a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;
   const uint64_t threads = (uint64_t)d.nloc * a.Fp;
   const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock,
                                                   std::min<uint64_t>(kSigParts, (uint64_t)d.grid_gen));
   hipLaunchKernelGGL(k_gen_storm, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
-  hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), g, commit ? 1u : 0u, d.nloc,
-                     state, n_waiters);
+  *nparts = g;
   return hipGetLastError();
 }
 

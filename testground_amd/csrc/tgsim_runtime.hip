@@ -43,8 +43,19 @@ struct tgsim_ctx {
   bool now_from_device = false;
   uint64_t sig_log_used = 0;
   uint32_t n_waiters = 0;
+  // a storm batch whose count-only commit is deferred to the next sync-service call (a barrier
+  // rides in the same launch): partials in d.sig_part
+  bool storm_pending = false;
+  uint32_t storm_parts = 0, storm_state = 0;
   std::vector<void*> allocs;
 };
+
+// Commit a deferred storm batch before anything reads or reuses the sync state.
+static hipError_t flush_storm(tgsim_ctx* c) {
+  if (!c->storm_pending) return hipSuccess;
+  c->storm_pending = false;
+  return launch_sig_commit(c->d, c->storm_parts, true, c->nloc, c->storm_state, c->n_waiters, false, 0, 0, 0);
+}
 
 static int fail(tgsim_ctx* c, int code, const char* fmt, ...) {
   if (c) {
@@ -367,6 +378,7 @@ static int check_device_errors(tgsim_ctx* c) {
 }
 
 static int sync_and_check(tgsim_ctx* c) {
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, sync_scalars(c->d), "sync");
   if (c->now_from_device && !c->in_window) {
     c->horizon = c->d.h_sc->T;
@@ -688,6 +700,7 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window(c->d, t_end), "set window");
   return begin_common(c);
 }
@@ -714,6 +727,7 @@ extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, 
 extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
   if (!c || !t_end_dev) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window_dev(c->d, t_end_dev, offset_ns), "set window");
   return begin_common(c);
 }
@@ -743,6 +757,7 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   if (c->S != 1) return fail(c, TGSIM_ESTATE, "single-shard context required");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window_barrier(c->d, waiter, offset_ns), "set window");
   int rc = begin_common(c);
   if (rc) return rc;
@@ -815,6 +830,7 @@ extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uin
     if (t[i] < 0) return fail(c, TGSIM_ECAUSALITY, "negative signal time");
   }
   Dev& d = c->d;
+  HIPCK(c, flush_storm(c), "storm commit");
   uint32_t kmin = UINT32_MAX, kmax = 0;
   for (size_t i = 0; i < n; ++i) { kmin = std::min(kmin, states[i]); kmax = std::max(kmax, states[i]); }
   if (n) {
@@ -835,15 +851,22 @@ extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target,
   if (c->n_waiters >= c->d.max_waiters) return fail(c, TGSIM_ECAPACITY, "too many barrier waiters");
   Dev& d = c->d;
   const uint32_t i = c->n_waiters;
-  HIPCK(c, add_waiter(d, i, state, target, t_wait), "barrier");
+  if (c->storm_pending) {  // commit the storm batch, register and resolve the waiter: one launch
+    c->storm_pending = false;
+    HIPCK(c, launch_sig_commit(d, c->storm_parts, true, c->nloc, c->storm_state, i, true, state, target, t_wait),
+          "barrier");
+  } else {
+    HIPCK(c, add_waiter(d, i, state, target, t_wait), "barrier");
+  }
   c->n_waiters++;
-  *w = i;  // k_add_waiter resolves the new waiter; the others can only move when signals arrive
+  *w = i;  // the new waiter is resolved now; the others can only move when signals arrive
   return TGSIM_OK;
 }
 
 extern "C" int tgsim_sync_poll(tgsim_ctx* c, uint32_t w, int64_t* rel) {
   if (!c || !rel) return TGSIM_EINVAL;
   if (w >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, hipMemcpyAsync(rel, c->d.w_release + w, 8, hipMemcpyDeviceToHost, c->d.stream), "poll");
   return sync_and_check(c);
 }
@@ -851,6 +874,7 @@ extern "C" int tgsim_sync_poll(tgsim_ctx* c, uint32_t w, int64_t* rel) {
 extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
   if (!c || !count) return TGSIM_EINVAL;
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
+  HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, hipMemcpyAsync(count, c->d.st_count + state, 4, hipMemcpyDeviceToHost, c->d.stream), "count");
   return sync_and_check(c);
 }
@@ -871,12 +895,21 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
-  // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so a
-  // single shard commits the batch count-only (count, first/last time) in the same
-  // launch; sharded, the release time is the MAX over shards of the local latest signal (sig_red[3]).
-  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, state, c->S == 1, c->n_waiters),
-        "gen storm");
+  HIPCK(c, flush_storm(c), "storm commit");
+  uint32_t parts = 0;
+  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, &parts), "gen storm");
   c->n_staged += (uint32_t)n;
+  if (c->S == 1) {
+    // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
+    // batch is committed count-only (count, first/last time) - deferred to the next
+    // sync-service call, so that the plan's barrier rides in the same launch
+    c->storm_pending = true;
+    c->storm_parts = parts;
+    c->storm_state = state;
+  } else {
+    // sharded: the release time is the MAX over shards of the local latest signal (sig_red[3])
+    HIPCK(c, launch_sig_commit(c->d, parts, false, c->nloc, state, 0, false, 0, 0, 0), "storm release");
+  }
   return TGSIM_OK;
 }
 
