@@ -65,6 +65,10 @@ struct Dev {
   // sort scratch
   uint32_t *keys0 = nullptr, *keys1 = nullptr, *vals0 = nullptr, *vals1 = nullptr;
   uint32_t* hist = nullptr;       // [kMaxBins * kRadixBlocks]
+  uint2* kv1 = nullptr;           // k_bkt_local output: (key, physical index) per item
+  uint32_t* poff = nullptr;       // [kRadixBlocks * (kMaxBins + 1)] per-block bucket offsets (k_bkt_local)
+  uint32_t* keys2 = nullptr;      // oversized fused buckets: contiguous copy for the global path
+  uint32_t* vals2 = nullptr;
   uint32_t* tot = nullptr;        // [kMaxBins]
   int n_cu = 256;                 // compute units of the device (bucket widths)
   int grid_shape = 2048;          // k_shape / k_gen_storm grids (init_launch_geometry)

@@ -897,6 +897,77 @@ __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc,
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
 }
 
+// Element range of partition block p (as bkt_block_range for blockIdx.x == p).
+__device__ __forceinline__ void bkt_range_of(const BktSrc& s, uint32_t p, uint32_t& start, uint32_t& end) {
+  const uint32_t sub = p >> 2, part = p & 3;
+  uint32_t c = s.qc[((uint32_t)s.q * kNSub + sub) << 5];
+  c = c < s.subcap ? c : s.subcap;
+  start = sub * s.subcap + (uint32_t)(((uint64_t)c * part) >> 2);
+  end = sub * s.subcap + (uint32_t)(((uint64_t)c * (part + 1)) >> 2);
+}
+
+// One-kernel partition for the fused consumers (queue sources only): each block counting-sorts
+// its own element range by bucket in place of the physical index space - (key, index) to
+// kv[start + rank] - and writes its exclusive bucket offsets poff[block][0..B]. No global
+// scan and no cross-block scatter: a block's writes stay inside its own ~25 KB range (whole lines,
+// one XCD's L2). The consumer of bucket b finds its items as 256 chunks and its global start as
+// sum_p poff[p][b] (every block's offsets are prefix sums of its own counts). The first block
+// also closes the queue (queue_final) and resets the segment lists.
+__global__ __launch_bounds__(kBlock) void k_bkt_local(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
+                                                      uint2* kv, uint32_t* poff) {
+  __shared__ uint32_t h[kMaxBins + 1];
+  __shared__ uint32_t red[kBlock / 64];
+  for (uint32_t d = threadIdx.x; d <= B; d += kBlock) h[d] = 0;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
+    if (threadIdx.x < kNSub) queue_final(sc, src.qc, src.q, src.subcap);
+  }
+  __syncthreads();
+  uint32_t start, end;
+  bkt_block_range(src, start, end);
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
+    uint32_t k[kBktUnroll];
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = j < end ? src.keys[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u)
+      if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[bd.of(k[u])], 1u);
+  }
+  __syncthreads();
+  // exclusive offsets (each thread a contiguous run of buckets), published to poff
+  const uint32_t per = (B + kBlock - 1) / kBlock, d0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && d0 + i < B; ++i) sum += h[d0 + i];
+  uint32_t total;
+  uint32_t run = block_excl_scan(sum, red, total);
+  uint32_t* row = poff + (size_t)blockIdx.x * (B + 1);
+  for (uint32_t i = 0; i < per && d0 + i < B; ++i) {
+    const uint32_t c = h[d0 + i];
+    h[d0 + i] = run;
+    row[d0 + i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) row[B] = total;
+  __syncthreads();
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
+    uint32_t k[kBktUnroll];
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = j < end ? src.keys[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < kBktUnroll; ++u) {
+      if (k[u] == 0xFFFFFFFFu) continue;
+      const uint32_t pos = start + atomicAdd(&h[bd.of(k[u])], 1u);
+      kv[pos] = make_uint2(k[u], j0 + u * kBlock);
+    }
+  }
+}
+
 // Bucket bases for this block: exclusive scan of the bucket totals + this block's offset in each.
 __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, const uint32_t* tot, uint32_t* base,
                                           uint32_t* part) {
@@ -946,11 +1017,14 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
 
 // pass 3 pieces. bkt_count_keys: the bucket's start / size (sum of the totals before it) and the
 // exclusive offsets of its keys in cnt[] (relative to the bucket start); returns the longest segment.
-struct BktHead { uint32_t start, nb, k0, nk; };
+struct BktHead { uint32_t start, nb, k0, nk, b; };
+__device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t* cnt, uint32_t* part,
+                                                   const BktHead& h);
 
 __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv bd, uint32_t K, const uint32_t* tot,
                                                    uint32_t* cnt, uint32_t* part, BktHead& h) {
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  h.b = b;
   h.k0 = b * bd.w;
   h.nk = min(K - h.k0, bd.w);
   uint32_t s = 0;
@@ -965,6 +1039,14 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv b
   h.start = part[0];
   h.nb = tot[b];
   __syncthreads();
+  return bkt_count_body(kin, cnt, part, h);
+}
+
+// Counting part of bkt_count_keys (h known, cnt[0, h.nk) zeroed and visible): key counts of the
+// bucket's items kin[h.start, +h.nb), exclusive offsets in cnt[], and the longest segment.
+__device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t* cnt, uint32_t* part,
+                                                   const BktHead& h) {
+  const uint32_t tid = threadIdx.x;
   for (uint32_t j = tid; j < h.nb; j += kBlock) atomicAdd(&cnt[kin[h.start + j] - h.k0], 1u);
   __syncthreads();
   const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = tid * per;
@@ -1018,7 +1100,7 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
       medium[atomicAdd(&sc->n_medium, 1u)] = k;
     }
   }
-  if (blockIdx.x == B - 1 && tid == 0) {
+  if (h.b == B - 1 && tid == 0) {
     off[K] = h.start + h.nb;
     if (off2) off2[K] = h.start + h.nb;
   }
@@ -1805,6 +1887,8 @@ constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
 constexpr uint32_t kBktRankMax = 64;  // longest key run ranked in LDS
 constexpr int kIPT = kBktCap / kBlock;  // items per thread
 
+constexpr uint32_t kStageN = 1024;  // records staged per round for the coalesced output (k1 + k2 area)
+
 struct BktFusedSmem {
   uint32_t cnt[1u << kBktFusedKeyBits];  // per key: run start, then run end (relative to the bucket)
   uint64_t k1[kBktCap];                  // TB: netem time, then departure; emit: delivery time
@@ -1840,39 +1924,94 @@ __device__ __forceinline__ bool k3less(uint64_t a1, uint64_t a2, uint32_t a3, ui
 // (true): slot[u] is item u's LDS slot, sm.cnt[k] the END of key k's run, sm.ord the sorted order
 // of every key run of length <= kBktRankMax (by_pos: position -> slot, else slot -> position); longer runs are written out (kout, vout,
 // off) and listed. false: the bucket was too big and went to the global form (k_rest).
+// Bijection of [0, n): block i -> the (i / 8)-th item of XCD i % 8's contiguous share.
+__device__ __forceinline__ uint32_t xcd_major(uint32_t i, uint32_t n) {
+  const uint32_t q = n >> 3, r = n & 7u, x = i & 7u;
+  return x * q + (x < r ? x : r) + (i >> 3);
+}
+
+// chunk of item j: the last chunk p with cexcl[p] <= j (cexcl ascending, cexcl[0] = 0)
+__device__ __forceinline__ uint32_t chunk_of(const uint32_t* cexcl, uint32_t j) {
+  uint32_t lo = 0, hi = kRadixBlocks;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cexcl[mid] <= j) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+static_assert(kRadixBlocks == kBlock, "one consumer thread per partition block");
+
 template <bool by_pos, class KeyFn>
-__device__ __forceinline__ bool bkt_fused_load(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                               uint32_t* vout, BktDiv bd, uint32_t B, uint32_t K, const uint32_t* tot,
-                                               const uint32_t* bstart, uint32_t* off, uint32_t* off2,
-                                               uint32_t* medium, LargeSeg* large, DevScalars* sc, BktFusedSmem& sm,
-                                               BktHead& h, const tgsim_record* batch, const KeyFn& keyfn,
-                                               tgsim_record (&rec)[kIPT], uint32_t (&slot)[kIPT]) {
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t* poff, const uint2* kv,
+                                               uint32_t* kscr, uint32_t* vscr, uint32_t* kout,
+                                               uint32_t* vout, BktDiv bd, uint32_t B, uint32_t K, uint32_t* off,
+                                               uint32_t* off2, uint32_t* medium, LargeSeg* large, DevScalars* sc,
+                                               BktFusedSmem& sm, BktHead& h, const tgsim_record* batch,
+                                               const KeyFn& keyfn, tgsim_record (&rec)[kIPT],
+                                               uint32_t (&slot)[kIPT]) {
+  // XCD-aware bucket order: hardware dispatch puts block i on XCD i % 8, so consecutive buckets -
+  // whose chunks share cache lines in every partition block's range - go to the same XCD's L2
+  const uint32_t b = xcd_major(blockIdx.x, B);
+  h.b = b;
   TG_PH(0);
   h.k0 = b * bd.w;
   h.nk = min(K - h.k0, bd.w);
-  h.start = bstart[b];
-  h.nb = bstart[b + 1] - h.start;
-  TG_PH(1);
-  if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest
-    bkt_count_keys(kin, bd, K, tot, sm.cnt, sm.part, h);
-    bkt_emit_global(kin, vin, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
-    return false;
-  }
-  uint32_t kk[kIPT], ix[kIPT];
-#pragma unroll
-  for (int u = 0; u < kIPT; ++u) {
-    const uint32_t j = u * kBlock + threadIdx.x;
-    kk[u] = 0xFFFFFFFFu;
-    ix[u] = 0;
-    if (j < h.nb) { kk[u] = kin[h.start + j] - h.k0; ix[u] = vin[h.start + j]; }
+  // chunk table (in the k1 area, free until the sort keys are written): partition block p left
+  // this bucket's items at kv[csrc[p] ...), cexcl[p] items of the bucket before them
+  uint32_t* cexcl = reinterpret_cast<uint32_t*>(sm.k1);
+  uint32_t* csrc = cexcl + kRadixBlocks;
+  {
+    const uint32_t p = threadIdx.x;
+    uint32_t ps, pe;
+    bkt_range_of(src, p, ps, pe);
+    const uint32_t* row = poff + (size_t)p * (B + 1);
+    const uint32_t lo = row[b], hi = row[b + 1];
+    uint32_t c = hi - lo, l = lo, tc, tl;
+    block_scan2(c, l, sm.part, tc, tl);  // c: items before chunk p; tc: bucket size; tl: bucket start
+    cexcl[p] = c;
+    csrc[p] = ps + lo;
+    h.nb = tc;
+    h.start = tl;
   }
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) sm.cnt[i] = 0;
   if (threadIdx.x == 0) sm.maxlen = 0;
+  __syncthreads();
+  TG_PH(1);
+  if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest: contiguous copy first
+    for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {
+      const uint32_t p = chunk_of(cexcl, j);
+      const uint2 e = kv[csrc[p] + (j - cexcl[p])];
+      kscr[h.start + j] = e.x;
+      vscr[h.start + j] = e.y;
+    }
+    __syncthreads();
+    bkt_count_body(kscr, sm.cnt, sm.part, h);
+    bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
+    return false;
+  }
+  // this thread's items: kIPT consecutive positions of the bucket (one chunk search, then a walk)
+  uint32_t kk[kIPT], ix[kIPT];
+  {
+    const uint32_t j0 = threadIdx.x * kIPT;
+    uint32_t p = j0 < h.nb ? chunk_of(cexcl, j0) : 0u;
+#pragma unroll
+    for (int u = 0; u < kIPT; ++u) {
+      const uint32_t j = j0 + u;
+      kk[u] = 0xFFFFFFFFu;
+      ix[u] = 0;
+      if (j < h.nb) {
+        while (p + 1 < (uint32_t)kRadixBlocks && cexcl[p + 1] <= j) ++p;
+        const uint2 e = kv[csrc[p] + (j - cexcl[p])];
+        kk[u] = e.x - h.k0;
+        ix[u] = e.y;
+      }
+    }
+  }
 #pragma unroll
   for (int u = 0; u < kIPT; ++u)
     if (kk[u] != 0xFFFFFFFFu) load_rec(batch + ix[u], rec[u]);  // issued before the LDS work below
-  __syncthreads();
+  __syncthreads();  // the chunk table (k1 area) is dead from here
   TG_PH(2);
 #pragma unroll
   for (int u = 0; u < kIPT; ++u)
@@ -1921,13 +2060,14 @@ __device__ __forceinline__ bool bkt_fused_load(const uint32_t* kin, const uint32
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         r += y[j] < x1 ? 1u : 0u;
-        if (y[j] == x1) r += k3less(y[j], sm.k2[i + j], sm.k3[i + j], x1, x2, x3) ? 1u : 0u;
+        // ties only: the slot itself is skipped, or every wave would take this branch each step
+        if (y[j] == x1 && i + j != s) r += k3less(y[j], sm.k2[i + j], sm.k3[i + j], x1, x2, x3) ? 1u : 0u;
       }
     }
     for (; i < e; ++i) {
       const uint64_t y = sm.k1[i];
       r += y < x1 ? 1u : 0u;
-      if (y == x1) r += k3less(y, sm.k2[i], sm.k3[i], x1, x2, x3) ? 1u : 0u;
+      if (y == x1 && i != s) r += k3less(y, sm.k2[i], sm.k3[i], x1, x2, x3) ? 1u : 0u;
     }
     if (by_pos) sm.ord[a + r] = (uint16_t)s;
     else sm.ord[s] = (uint16_t)(a + r);
@@ -1956,6 +2096,9 @@ __device__ __forceinline__ bool bkt_fused_load(const uint32_t* kin, const uint32
   return true;
 }
 
+static_assert(offsetof(BktFusedSmem, k2) == offsetof(BktFusedSmem, k1) + 8 * kBktCap &&
+                  32 * kStageN <= 16 * kBktCap, "output staging uses the k1 + k2 area");
+
 // length of the run of the key owning LDS slot s
 __device__ __forceinline__ uint32_t run_len(const BktFusedSmem& sm, uint32_t s) {
   const uint32_t k = sm.key[s];
@@ -1971,17 +2114,17 @@ struct TBKey {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, const uint32_t* kin, const uint32_t* vin,
-                                                      uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
-                                                      uint32_t K, const uint32_t* tot, const uint32_t* bstart,
-                                                      uint32_t* off, uint32_t* medium, LargeSeg* large,
-                                                      DevScalars* sc) {
+__global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, const uint32_t* poff,
+                                                      const uint2* kv, uint32_t* kscr,
+                                                      uint32_t* vscr, uint32_t* kout, uint32_t* vout, BktDiv bd,
+                                                      uint32_t B, uint32_t K, uint32_t* off, uint32_t* medium,
+                                                      LargeSeg* large, DevScalars* sc) {
   __shared__ BktFusedSmem sm;
   BktHead h;
   tgsim_record rec[kIPT];
   uint32_t slot[kIPT];
-  if (!bkt_fused_load<true>(kin, vin, kout, vout, bd, B, K, tot, bstart, off, nullptr, medium, large, sc, sm, h, p.A,
-                      TBKey{}, rec, slot))
+  if (!bkt_fused_load<true>(src, poff, kv, kscr, vscr, kout, vout, bd, B, K, off, nullptr, medium, large, sc,
+                            sm, h, p.A, TBKey{}, rec, slot))
     return;
   // the GCRA along each sender's run (one thread per sender); departures replace k1
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
@@ -2026,24 +2169,47 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, const uint32_t
   block_scan2(nD, nL, sm.part, tD, tL);  // nD/nL: this thread's offsets inside the block's runs
   const Queues& Q = p.Q;
   const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
-  __syncthreads();  // every thread has read the scan partials in sm.part
+  __syncthreads();  // every thread has read the scan partials in sm.part (and k1 for the last time)
   if (threadIdx.x == 0) {
     sm.part[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
     sm.part[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
   }
-  __syncthreads();
-  uint32_t pD = sm.part[0] + nD, pL = sm.part[1] + nL;
+  // the routed copies pass through LDS in append order (the D run, then the L run), kStageN per
+  // round, so that every wave store covers consecutive records: whole lines, no reliance on L2
+  // merging partial writes
+  uint4* st = reinterpret_cast<uint4*>(sm.k1);
+  const uint32_t nst = tD + tL;
+  for (uint32_t r0 = 0; r0 < nst; r0 += kStageN) {
+    uint32_t cD = nD, cL = tD + nL;
 #pragma unroll
-  for (int u = 0; u < kIPT; ++u) {
-    if (code[u] != Q_D && code[u] != Q_L) continue;
-    const bool isD = code[u] == Q_D;
-    const uint32_t pos = isD ? pD++ : pL++;
-    if (pos < Q.subcap) {
-      store_rec((isD ? Q.D : Q.L) + (size_t)sub * Q.subcap + pos, rec[u]);
-      Q.K[isD ? Q_D : Q_L][(size_t)sub * Q.subcap + pos] = Q.key_of(isD ? Q_D : Q_L, rec[u]);
-    } else {
-      atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
+    for (int u = 0; u < kIPT; ++u) {
+      if (code[u] != Q_D && code[u] != Q_L) continue;
+      const uint32_t q = code[u] == Q_D ? cD++ : cL++;
+      if (q < r0 || q >= r0 + kStageN) continue;
+      const uint32_t i = q - r0;
+      st[2 * i] = make_uint4((uint32_t)rec[u].t, (uint32_t)((uint64_t)rec[u].t >> 32), rec[u].src, rec[u].dst);
+      st[2 * i + 1] = make_uint4(rec[u].seq, rec[u].size, rec[u].meta, rec[u].corrupt_off);
     }
+    __syncthreads();
+    const uint32_t n = min(kStageN, nst - r0);
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+      const uint32_t q = r0 + i;
+      const bool isD = q < tD;
+      const uint32_t pos = isD ? sm.part[0] + q : sm.part[1] + (q - tD);
+      const uint4 a = st[2 * i], b = st[2 * i + 1];
+      if (pos < Q.subcap) {
+        const size_t at = (size_t)sub * Q.subcap + pos;
+        uint4* dst = reinterpret_cast<uint4*>((isD ? Q.D : Q.L) + at);
+        dst[0] = a;
+        dst[1] = b;
+        tgsim_record r;
+        r.t = (int64_t)(((uint64_t)a.y << 32) | a.x); r.src = a.z; r.dst = a.w;
+        Q.K[isD ? Q_D : Q_L][at] = Q.key_of(isD ? Q_D : Q_L, r);
+      } else {
+        atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
+      }
+    }
+    __syncthreads();
   }
   if (sm.flag) {  // cross-shard copies (S > 1): wave appends onto the peer blocks
 #pragma unroll
@@ -2061,33 +2227,50 @@ struct EmitKey {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, const uint32_t* kin, const uint32_t* vin,
-                                                        uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
-                                                        uint32_t K, const uint32_t* tot, const uint32_t* bstart,
-                                                        uint32_t* off, uint32_t* off2, uint32_t* medium,
-                                                        LargeSeg* large, DevScalars* sc) {
+__global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src, const uint32_t* poff,
+                                                        const uint2* kv, uint32_t* kscr,
+                                                        uint32_t* vscr, uint32_t* kout, uint32_t* vout, BktDiv bd,
+                                                        uint32_t B, uint32_t K, uint32_t* off, uint32_t* off2,
+                                                        uint32_t* medium, LargeSeg* large, DevScalars* sc) {
   __shared__ BktFusedSmem sm;
   BktHead h;
   tgsim_record rec[kIPT];
   uint32_t slot[kIPT];
-  if (!bkt_fused_load<false>(kin, vin, kout, vout, bd, B, K, tot, bstart, off, off2, medium, large, sc, sm, h, p.D,
-                      EmitKey{}, rec, slot))
+  if (!bkt_fused_load<false>(src, poff, kv, kscr, vscr, kout, vout, bd, B, K, off, off2, medium, large, sc,
+                             sm, h, p.D, EmitKey{}, rec, slot))
     return;
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
     const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
     off[h.k0 + i] = o;
     off2[h.k0 + i] = o;
   }
-  if (blockIdx.x == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
+  if (h.b == B - 1 && threadIdx.x == 0) { off[K] = h.start + h.nb; off2[K] = h.start + h.nb; }
   TG_PH(7);
-  // each thread writes its own items at their inbox positions (long keys: k_rest)
+  // the deliveries pass through LDS in inbox order (SoA, kStageN per round) and leave with
+  // coalesced stores: every wave store covers 64 consecutive entries of one output array. Entries
+  // of long keys hold stale LDS here; k_rest rewrites them after this kernel.
+  int64_t* st_t = reinterpret_cast<int64_t*>(sm.k1);
+  uint32_t* st_u = reinterpret_cast<uint32_t*>(sm.k1) + 2 * kStageN;
+  for (uint32_t r0 = 0; r0 < h.nb; r0 += kStageN) {
 #pragma unroll
-  for (int u = 0; u < kIPT; ++u) {
-    if (slot[u] == 0xFFFFFFFFu || run_len(sm, slot[u]) > kBktRankMax) continue;
-    const uint32_t o = h.start + sm.ord[slot[u]];
-    const tgsim_record& r = rec[u];
-    p.o_t[o] = r.t; p.o_src[o] = r.src; p.o_dst[o] = r.dst; p.o_seq[o] = r.seq; p.o_size[o] = r.size;
-    p.o_flags[o] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; p.o_coff[o] = r.corrupt_off;
+    for (int u = 0; u < kIPT; ++u) {
+      if (slot[u] == 0xFFFFFFFFu || run_len(sm, slot[u]) > kBktRankMax) continue;
+      const uint32_t o = sm.ord[slot[u]];
+      if (o < r0 || o >= r0 + kStageN) continue;
+      const uint32_t i = o - r0;
+      const tgsim_record& r = rec[u];
+      st_t[i] = r.t;
+      st_u[i] = r.src; st_u[kStageN + i] = r.dst; st_u[2 * kStageN + i] = r.seq; st_u[3 * kStageN + i] = r.size;
+      st_u[4 * kStageN + i] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; st_u[5 * kStageN + i] = r.corrupt_off;
+    }
+    __syncthreads();
+    const uint32_t n = min(kStageN, h.nb - r0);
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+      const uint32_t o = h.start + r0 + i;
+      p.o_t[o] = st_t[i]; p.o_src[o] = st_u[i]; p.o_dst[o] = st_u[kStageN + i]; p.o_seq[o] = st_u[2 * kStageN + i];
+      p.o_size[o] = st_u[3 * kStageN + i]; p.o_flags[o] = st_u[4 * kStageN + i]; p.o_coff[o] = st_u[5 * kStageN + i];
+    }
+    __syncthreads();
   }
   TG_PH_END(1, h.nb);
 }
@@ -2737,6 +2920,13 @@ static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B
   return hipGetLastError();
 }
 
+// Partition for the fused consumers: (keys1, vals1) chunked per partition block, offsets in d.poff.
+static hipError_t bkt_local(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
+  ProfScope ps_(d, KID_BKT_SCATTER);
+  hipLaunchKernelGGL(k_bkt_local, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bd, B, d.kv1, d.poff);
+  return hipGetLastError();
+}
+
 // Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
 // d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
 static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t medium_above, uint32_t* off2,
@@ -2807,11 +2997,12 @@ static hipError_t run_token_bucket(Dev& d) {
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= 2048: nloc <= 2^20 (checked at create)
-  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_A), bd, B));
+  const BktSrc src = bkt_queue(d, Q_A);
+  TG_CHECK(bkt_local(d, src, bd, B));
   {
     ProfScope ps_(d, KID_TB);
-    hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bd, B,
-                       d.nloc, d.tot, d.bstart, d.seg_off, d.medium, d.large, d.sc);
+    hipLaunchKernelGGL(k_tb_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, src, d.poff, d.kv1, d.keys2,
+                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
   return launch_rest(d, p, d.keys0, d.vals0);
@@ -2852,11 +3043,12 @@ static hipError_t run_deliveries(Dev& d) {
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
-  TG_CHECK(bkt_partition(d, bkt_queue(d, Q_D), bd, B));
+  const BktSrc src = bkt_queue(d, Q_D);
+  TG_CHECK(bkt_local(d, src, bd, B));
   {
     ProfScope ps_(d, KID_EMIT);
-    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, d.keys1, d.vals1, d.keys0, d.vals0, bd,
-                       B, d.nloc, d.tot, d.bstart, d.seg_off, d.inbox, d.medium, d.large, d.sc);
+    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, src, d.poff, d.kv1, d.keys2,
+                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
   return launch_rest(d, p, d.keys0, d.vals0);

@@ -266,10 +266,16 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.dirs, (size_t)kMaxRegions * (d.slots + 1));
   rc |= dalloc(c, &d.plan_start, kMaxRegions + 1);
   rc |= dalloc(c, &d.plan_off, kMaxRegions + 1);
-  rc |= dalloc(c, &d.keys0, d.cap_rec);
-  rc |= dalloc(c, &d.keys1, d.cap_rec);
-  rc |= dalloc(c, &d.vals0, d.cap_rec);
-  rc |= dalloc(c, &d.vals1, d.cap_rec);
+  // every per-window item array holds the physical queue space (kNSub sub-queues of subcap): a
+  // window can carry up to kNSub * subcap > cap_rec items before the overflow bits stop it
+  rc |= dalloc(c, &d.keys0, phys_rec);
+  rc |= dalloc(c, &d.keys1, phys_rec);
+  rc |= dalloc(c, &d.keys2, phys_rec);
+  rc |= dalloc(c, &d.kv1, phys_rec);
+  rc |= dalloc(c, &d.vals0, phys_rec);
+  rc |= dalloc(c, &d.vals1, phys_rec);
+  rc |= dalloc(c, &d.vals2, phys_rec);
+  rc |= dalloc(c, &d.poff, (size_t)kRadixBlocks * (kMaxBins + 1));
   rc |= dalloc(c, &d.hist, (size_t)kMaxBins * kRadixBlocks);
   rc |= dalloc(c, &d.tot, kMaxBins);
   rc |= dalloc(c, &d.bstart, kMaxBins + 1);
@@ -278,23 +284,23 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.sig_part, 2 * 4096);
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
   rc |= dalloc(c, &d.seg_off, segK);
-  rc |= dalloc(c, &d.large, d.cap_rec / kTile + 16);
+  rc |= dalloc(c, &d.large, phys_rec / kTile + 16);
   rc |= dalloc(c, &d.medium, segK);
   rc |= dalloc(c, &d.deferred, kMaxBins);
-  rc |= dalloc(c, &d.chunk_off, d.cap_rec / kTile + 17);
-  rc |= dalloc(c, &d.K1a, d.cap_rec);
-  rc |= dalloc(c, &d.K1b, d.cap_rec);
-  rc |= dalloc(c, &d.K2a, d.cap_rec);
-  rc |= dalloc(c, &d.K2b, d.cap_rec);
-  rc |= dalloc(c, &d.K3a, d.cap_rec);
-  rc |= dalloc(c, &d.K3b, d.cap_rec);
-  rc |= dalloc(c, &d.o_t, d.cap_rec);
-  rc |= dalloc(c, &d.o_src, d.cap_rec);
-  rc |= dalloc(c, &d.o_dst, d.cap_rec);
-  rc |= dalloc(c, &d.o_seq, d.cap_rec);
-  rc |= dalloc(c, &d.o_size, d.cap_rec);
-  rc |= dalloc(c, &d.o_flags, d.cap_rec);
-  rc |= dalloc(c, &d.o_coff, d.cap_rec);
+  rc |= dalloc(c, &d.chunk_off, phys_rec / kTile + 17);
+  rc |= dalloc(c, &d.K1a, phys_rec);
+  rc |= dalloc(c, &d.K1b, phys_rec);
+  rc |= dalloc(c, &d.K2a, phys_rec);
+  rc |= dalloc(c, &d.K2b, phys_rec);
+  rc |= dalloc(c, &d.K3a, phys_rec);
+  rc |= dalloc(c, &d.K3b, phys_rec);
+  rc |= dalloc(c, &d.o_t, phys_rec);
+  rc |= dalloc(c, &d.o_src, phys_rec);
+  rc |= dalloc(c, &d.o_dst, phys_rec);
+  rc |= dalloc(c, &d.o_seq, phys_rec);
+  rc |= dalloc(c, &d.o_size, phys_rec);
+  rc |= dalloc(c, &d.o_flags, phys_rec);
+  rc |= dalloc(c, &d.o_coff, phys_rec);
   rc |= dalloc(c, &d.inbox, nl1);
   rc |= dalloc(c, &d.s_state, d.s_cap);
   rc |= dalloc(c, &d.s_inst, d.s_cap);
