@@ -13,7 +13,8 @@ from testground_amd.sim import SimConfig, Simulator, make_shape
 MS = 1_000_000
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-hip = A.hip_library()
+hip = A.bind(os.environ['TGSIM_LIB'], 'tgsim_', 'hip') if os.environ.get('TGSIM_LIB') else A.hip_library()
+print('lib', hip.cdll._name)
 sim = Simulator(SimConfig(n_instances=N, seed=4, data_prefix_len=12, max_msgs_per_window=1 << 20,
                           max_records=1 << 23, max_states=1024), binding=hip)
 rng = np.random.default_rng(4)
