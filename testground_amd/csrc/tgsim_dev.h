@@ -116,6 +116,11 @@ struct Dev {
 hipError_t launch_set_window(Dev& d, int64_t t_end);
 hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns);
 hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns);
+// The storm's deferred count-only commit (+ the barrier registered after it) fused with the window
+// start that waits on waiter `waiter` (launch_sig_commit's arguments).
+hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t offset_ns, uint32_t nparts, uint32_t n,
+                                            uint32_t st, uint32_t nw, bool add, uint32_t add_state,
+                                            uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert

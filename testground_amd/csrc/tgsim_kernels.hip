@@ -232,10 +232,27 @@ __device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t 
 enum { WIN_EXPLICIT = 0, WIN_BARRIER = 1, WIN_DEVICE = 2 };
 // The window starts where the previous one ended (H = its start, T = its end), read on the device,
 // so a run of barrier- or device-ended windows needs no host round trip at all.
-__global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_t* qc, int mode,
-                                                         int64_t t_end_arg, const int64_t* src, int64_t offset,
-                                                         int64_t slot_ns, RegionDev* regions, const uint32_t* dirs,
-                                                         uint32_t slots, uint32_t* plan_start, uint32_t* plan_off) {
+struct WindowArgs {
+  DevScalars* sc;
+  uint32_t* qc;
+  int mode;
+  int64_t t_end_arg;
+  const int64_t* src;
+  int64_t offset;
+  int64_t slot_ns;
+  RegionDev* regions;
+  const uint32_t* dirs;
+  uint32_t slots;
+  uint32_t* plan_start;
+  uint32_t* plan_off;
+};
+
+__device__ __forceinline__ void window_start_block(const WindowArgs& a) {
+  DevScalars* sc = a.sc;
+  uint32_t* qc = a.qc;
+  const int mode = a.mode;
+  const int64_t t_end_arg = a.t_end_arg, offset = a.offset, slot_ns = a.slot_ns;
+  const int64_t* src = a.src;
   __shared__ int64_t s_tend;
   for (uint32_t i = threadIdx.x; i < 3u * kNSub * 32u; i += kBlock) qc[i] = 0;
   uint32_t* w = sc->q;  // the per-window block [q, err) of DevScalars
@@ -263,8 +280,10 @@ __global__ __launch_bounds__(kBlock) void k_window_start(DevScalars* sc, uint32_
     s_tend = e;
   }
   __syncthreads();
-  plan_regions(regions, dirs, slots, slot_ns, plan_start, plan_off, sc, s_tend);
+  plan_regions(a.regions, a.dirs, a.slots, slot_ns, a.plan_start, a.plan_off, sc, s_tend);
 }
+
+__global__ __launch_bounds__(kBlock) void k_window_start(WindowArgs a) { window_start_block(a); }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
@@ -2454,8 +2473,8 @@ __device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn,
 // One block: the batch's (min, max) from the partials -> red[0], red[3]; with commit, the batch is
 // committed count-only to state st and waiters [0, nw) are resolved. wa.on: a barrier registered
 // right after the batch (waiter nw) is added and resolved in the same launch.
-__global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t nparts, uint32_t commit, uint32_t n,
-                                                       uint32_t st, uint32_t nw, WaiterAdd wa) {
+__device__ __forceinline__ void sig_commit_block(const SigState& g, uint32_t nparts, uint32_t commit, uint32_t n,
+                                                 uint32_t st, uint32_t nw, const WaiterAdd& wa) {
   if (wa.on && threadIdx.x == 0) {
     wa.w_state[nw] = wa.state; wa.w_target[nw] = wa.target;
     wa.w_twait[nw] = wa.t_wait == INT64_MIN ? g.sc->t_end : wa.t_wait;
@@ -2488,6 +2507,20 @@ __global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t npar
     __syncthreads();
     for (uint32_t i = commit ? threadIdx.x : nw - 1 + threadIdx.x; i < nw; i += kBlock) resolve_waiter(g, i);
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t nparts, uint32_t commit, uint32_t n,
+                                                       uint32_t st, uint32_t nw, WaiterAdd wa) {
+  sig_commit_block(g, nparts, commit, n, st, nw, wa);
+}
+
+// The storm step's deferred commit + barrier registration and the window start that waits on that
+// barrier, in one single-block launch (the window end is the waiter's release, resolved here).
+__global__ __launch_bounds__(kBlock) void k_window_start_commit(SigState g, uint32_t nparts, uint32_t n, uint32_t st,
+                                                                uint32_t nw, WaiterAdd wa, WindowArgs w) {
+  sig_commit_block(g, nparts, 1u, n, st, nw, wa);
+  __syncthreads();  // the waiter's release (written by some thread of this block) is visible
+  window_start_block(w);
 }
 
 // Count-only batch (one state, no sequence numbers): min and max time, then the commit.
@@ -2782,7 +2815,7 @@ hipError_t sync_scalars(Dev& d) {
   return hipSuccess;
 }
 
-static SigState sig_state(Dev& d) {
+SigState sig_state(Dev& d) {
   SigState g;
   g.count = d.st_count; g.last = d.st_last; g.nchunks = d.st_nchunks; g.chunks = d.st_chunks; g.log = d.sig_log;
   g.w_state = d.w_state; g.w_target = d.w_target; g.w_twait = d.w_twait; g.w_release = d.w_release;
@@ -2796,9 +2829,16 @@ static hipError_t reset_window(Dev& d) {
   return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
 }
 
+static WindowArgs window_args(Dev& d, int mode, int64_t t_end, const int64_t* src, int64_t offset) {
+  WindowArgs a;
+  a.sc = d.sc; a.qc = d.qc; a.mode = mode; a.t_end_arg = t_end; a.src = src; a.offset = offset;
+  a.slot_ns = d.slot_ns; a.regions = d.regions; a.dirs = d.dirs; a.slots = d.slots; a.plan_start = d.plan_start;
+  a.plan_off = d.plan_off;
+  return a;
+}
+
 static hipError_t window_start(Dev& d, int mode, int64_t t_end, const int64_t* src, int64_t offset) {
-  hipLaunchKernelGGL(k_window_start, dim3(1), dim3(kBlock), 0, d.stream, d.sc, d.qc, mode, t_end, src, offset,
-                     d.slot_ns, d.regions, d.dirs, d.slots, d.plan_start, d.plan_off);
+  hipLaunchKernelGGL(k_window_start, dim3(1), dim3(kBlock), 0, d.stream, window_args(d, mode, t_end, src, offset));
   return hipGetLastError();
 }
 
@@ -2806,6 +2846,23 @@ hipError_t launch_set_window(Dev& d, int64_t t_end) { return window_start(d, WIN
 
 hipError_t launch_set_window_barrier(Dev& d, uint32_t waiter, int64_t offset_ns) {
   return window_start(d, WIN_BARRIER, 0, d.w_release + waiter, offset_ns);
+}
+
+SigState sig_state(Dev& d);
+static WaiterAdd waiter_add(Dev& d, bool add, uint32_t state, uint32_t target, int64_t t_wait) {
+  WaiterAdd wa;
+  wa.w_state = d.w_state; wa.w_target = d.w_target; wa.w_twait = d.w_twait;
+  wa.state = state; wa.target = target; wa.t_wait = t_wait; wa.on = add ? 1u : 0u;
+  return wa;
+}
+
+hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t offset_ns, uint32_t nparts, uint32_t n,
+                                            uint32_t st, uint32_t nw, bool add, uint32_t add_state,
+                                            uint32_t add_target, int64_t add_twait) {
+  hipLaunchKernelGGL(k_window_start_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), nparts, n, st, nw,
+                     waiter_add(d, add, add_state, add_target, add_twait),
+                     window_args(d, WIN_BARRIER, 0, d.w_release + waiter, offset_ns));
+  return hipGetLastError();
 }
 
 hipError_t launch_set_window_dev(Dev& d, const int64_t* t_end_dev, int64_t offset_ns) {
@@ -3140,9 +3197,7 @@ void init_launch_geometry(Dev& d) {
 
 hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, uint32_t st, uint32_t n_waiters,
                              bool add, uint32_t add_state, uint32_t add_target, int64_t add_twait) {
-  WaiterAdd wa;
-  wa.w_state = d.w_state; wa.w_target = d.w_target; wa.w_twait = d.w_twait;
-  wa.state = add_state; wa.target = add_target; wa.t_wait = add_twait; wa.on = add ? 1u : 0u;
+  const WaiterAdd wa = waiter_add(d, add, add_state, add_target, add_twait);
   hipLaunchKernelGGL(k_sig_commit, dim3(1), dim3(kBlock), 0, d.stream, sig_state(d), nparts, commit ? 1u : 0u, n, st,
                      n_waiters, wa);
   return hipGetLastError();

@@ -47,6 +47,11 @@ struct tgsim_ctx {
   // rides in the same launch): partials in d.sig_part
   bool storm_pending = false;
   uint32_t storm_parts = 0, storm_state = 0;
+  // ... and a barrier registered after it, not yet launched (waiter storm_nw; the window start that
+  // waits on it carries the commit too)
+  bool storm_add = false;
+  uint32_t storm_nw = 0, add_state = 0, add_target = 0;
+  int64_t add_twait = 0;
   std::vector<void*> allocs;
 };
 
@@ -54,7 +59,10 @@ struct tgsim_ctx {
 static hipError_t flush_storm(tgsim_ctx* c) {
   if (!c->storm_pending) return hipSuccess;
   c->storm_pending = false;
-  return launch_sig_commit(c->d, c->storm_parts, true, c->nloc, c->storm_state, c->n_waiters, false, 0, 0, 0);
+  const bool add = c->storm_add;
+  c->storm_add = false;
+  return launch_sig_commit(c->d, c->storm_parts, true, c->nloc, c->storm_state, add ? c->storm_nw : c->n_waiters,
+                           add, c->add_state, c->add_target, c->add_twait);
 }
 
 static int fail(tgsim_ctx* c, int code, const char* fmt, ...) {
@@ -763,8 +771,16 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   if (c->S != 1) return fail(c, TGSIM_ESTATE, "single-shard context required");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
-  HIPCK(c, flush_storm(c), "storm commit");
-  HIPCK(c, launch_set_window_barrier(c->d, waiter, offset_ns), "set window");
+  if (c->storm_pending) {  // commit + barrier registration + window start: one launch
+    c->storm_pending = false;
+    const bool add = c->storm_add;
+    c->storm_add = false;
+    HIPCK(c, launch_set_window_barrier_commit(c->d, waiter, offset_ns, c->storm_parts, c->nloc, c->storm_state,
+                                              add ? c->storm_nw : c->n_waiters, add, c->add_state, c->add_target,
+                                              c->add_twait), "set window");
+  } else {
+    HIPCK(c, launch_set_window_barrier(c->d, waiter, offset_ns), "set window");
+  }
   int rc = begin_common(c);
   if (rc) return rc;
   return tgsim_advance_end(c);
@@ -857,11 +873,16 @@ extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target,
   if (c->n_waiters >= c->d.max_waiters) return fail(c, TGSIM_ECAPACITY, "too many barrier waiters");
   Dev& d = c->d;
   const uint32_t i = c->n_waiters;
-  if (c->storm_pending) {  // commit the storm batch, register and resolve the waiter: one launch
-    c->storm_pending = false;
-    HIPCK(c, launch_sig_commit(d, c->storm_parts, true, c->nloc, c->storm_state, i, true, state, target, t_wait),
-          "barrier");
+  if (c->storm_pending && !c->storm_add) {
+    // the storm batch's commit and this registration wait for the next launch (normally the window
+    // start that waits on this barrier: tgsim_advance_to_barrier)
+    c->storm_add = true;
+    c->storm_nw = i;
+    c->add_state = state;
+    c->add_target = target;
+    c->add_twait = t_wait;
   } else {
+    HIPCK(c, flush_storm(c), "storm commit");
     HIPCK(c, add_waiter(d, i, state, target, t_wait), "barrier");
   }
   c->n_waiters++;
