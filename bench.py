@@ -76,7 +76,10 @@ def sim_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
     return SimConfig(n_instances=args.instances, seed=args.seed, shard_id=shard, n_shards=n_shards, device=device,
                      data_prefix_len=12, max_msgs_per_window=max(1 << 20, args.instances * args.fanout),
-                     max_records=args.max_records, exchange_cap=1 << 17, max_states=4096)
+                     max_records=args.max_records, max_states=4096,
+                     # a window's cross-shard copies per peer stay below the shard's copies per round:
+                     # 2x headroom; only the used prefix of each block travels (testground_amd/exchange.py)
+                     exchange_cap=max(1 << 17, 2 * args.instances * args.fanout // max(n_shards, 1) + 1))
 
 
 def cpu_baseline(args, shapes):
@@ -141,7 +144,9 @@ def main():
     N, F = args.instances, args.fanout
 
     if world > 1:
+        from testground_amd.exchange import exchange
         _, _, nbytes = sim.exchange_buffers()
+        xcap = nbytes // (world * 32)
         send_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         recv_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         sim.set_exchange_buffers(send_t.data_ptr(), recv_t.data_ptr(), nbytes)
@@ -157,7 +162,7 @@ def main():
             sim.storm_release_device(rel_t.data_ptr())
             dist.all_reduce(rel_t, op=dist.ReduceOp.MAX)
             sim.advance_begin_device(rel_t.data_ptr(), rtt)
-            dist.all_to_all_single(recv_t, send_t)
+            exchange(send_t, recv_t, xcap, dist)
             sim.advance_end()
 
     # warm-up (untimed, unprofiled), then a few probe steps that time every kernel class to find the

@@ -4,8 +4,9 @@ The sharded run must equal the single-shard run bit for bit: per-shard statuses,
 shard's deliveries and inbox offsets, and the summed counters.
 
   * in-process: 2 and 3 oracle shards exchanging through memmove;
-  * multi-process: world_size 2 over torch.distributed gloo (all_to_all_single of the exchange
-    buffers, all_reduce MAX of the storm barrier release), the protocol bench.py runs over RCCL.
+  * multi-process: world_size 2 over torch.distributed gloo (the variable-size exchange of
+    testground_amd/exchange.py, all_reduce MAX of the storm barrier release), the protocol bench.py
+    runs over RCCL.
 """
 import ctypes as C
 import os
@@ -16,6 +17,7 @@ import pytest
 
 from tests import scenarios as S
 from testground_amd.sim import SimConfig, Simulator
+from testground_amd.exchange import exchange as xchg
 
 
 @pytest.mark.parametrize("world,seed", [(2, 1), (2, 5), (3, 2)])
@@ -44,10 +46,10 @@ def _worker(rank, world, port, seed, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         ob = oracle_binding()
 
-        def exchange(sims):
+        def exchange(sims):  # the runner's variable-size exchange (testground_amd/exchange.py)
             s = sims[0]
             send, recv, nbytes = s.exchange_buffers()
-            dist.all_to_all_single(_torch_view(recv, nbytes), _torch_view(send, nbytes))
+            xchg(_torch_view(send, nbytes), _torch_view(recv, nbytes), nbytes // (world * 32), dist)
 
         outs, _ = S.run_random_sharded(lambda c: Simulator(c, binding=ob), exchange, world, seed, local=[rank])
         storm = _storm_rank(ob, rank, world, dist)
@@ -79,7 +81,7 @@ def _storm_rank(binding, rank, world, dist, n=600, rounds=3):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         sim.advance_begin(int(t.item()) + 1 * S.MS)
         send, recv, nbytes = sim.exchange_buffers()
-        dist.all_to_all_single(_torch_view(recv, nbytes), _torch_view(send, nbytes))
+        xchg(_torch_view(send, nbytes), _torch_view(recv, nbytes), nbytes // (world * 32), dist)
         sim.advance_end()
         res.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
     res.append(dict(stats=S.parity_stats(sim)))
@@ -87,9 +89,10 @@ def _storm_rank(binding, rank, world, dist, n=600, rounds=3):
     return res
 
 
-def test_sharded_gloo_world2(oracle):
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gloo(oracle, world):
     import torch.multiprocessing as mp
-    world, seed = 2, 3
+    seed = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
