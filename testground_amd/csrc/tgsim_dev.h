@@ -78,7 +78,6 @@ struct Dev {
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;
   uint32_t* medium = nullptr;     // [segK] ids of segments kThreadSeg < len <= kTile
-  uint8_t* deferred = nullptr;    // [kMaxBins] bucket left to the thread/list/large kernels by a fused consumer
   uint32_t* chunk_off = nullptr;
   uint64_t *K1a = nullptr, *K1b = nullptr, *K2a = nullptr, *K2b = nullptr;
   uint32_t *K3a = nullptr, *K3b = nullptr;

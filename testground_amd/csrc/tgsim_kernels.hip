@@ -105,8 +105,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, u
   return pre + x - v;
 }
 
-__device__ __forceinline__ uint32_t wave_uid() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
-
 // Wave64 compaction onto per-lane counters: lanes whose counter pointer is equal share one
 // atomicAdd (ballot -> leader atomic -> broadcast -> mbcnt rank). nullptr = nothing to append.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
@@ -196,15 +194,6 @@ __device__ __forceinline__ int qid_stage_d(const Geo& g, uint32_t dst, int64_t t
 __device__ __forceinline__ uint32_t clamp_n(const uint32_t* n_ptr, uint32_t cap) {
   const uint32_t n = *n_ptr;
   return n < cap ? n : cap;
-}
-
-__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
 }
 
 __device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
@@ -306,10 +295,6 @@ __device__ __forceinline__ void queue_final(DevScalars* sc, const uint32_t* qc, 
   }
   sc->qpre[q][s] = x - c;
   if (s == 63) { sc->qpre[q][kNSub] = x; sc->qn[q] = x; }
-}
-
-__global__ void k_qfinal(DevScalars* sc, const uint32_t* qc, int q, uint32_t subcap) {
-  queue_final(sc, qc, q, subcap);
 }
 
 // ============================================================================================
@@ -617,28 +602,6 @@ __device__ void region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_ar
   sc->ins_off = off;
 }
 
-__global__ void k_region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_arena, int64_t slot_ns) {
-  region_alloc(sc, regions, cap_arena, slot_ns);
-}
-
-__global__ __launch_bounds__(kBlock) void k_region_fill(const tgsim_record* L, const uint32_t* keys,
-                                                        const uint32_t* vals, tgsim_record* arena,
-                                                        uint32_t* dirs, uint32_t slots, const DevScalars* sc) {
-  const uint64_t off = sc->ins_off;
-  if (off == ~0ull) return;
-  const uint32_t n = sc->qn[Q_L];
-  const uint32_t dir = (sc->reg_head - 1) % kMaxRegions;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint32_t i = tid; i < n; i += stride) {
-    tgsim_record r;
-    load_rec(L + vals[i], r);
-    store_rec(arena + off + i, r);
-  }
-  for (uint32_t s = tid; s <= slots; s += stride)
-    dirs[(size_t)dir * (slots + 1) + s] = lower_bound_u32(keys, n, s);
-}
-
 // ============================================================================================
 // stable LSD radix group-by on u32 keys: digits of <= 11 bits, per-block histograms, one block
 // per digit to scan its per-block counts, wave64 ballot ranking in the scatter (stable).
@@ -650,20 +613,6 @@ __device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_
   start = blockIdx.x * chunk;
   if (start > n) start = n;
   end = min(start + chunk, n);
-}
-
-__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint32_t* keys, const uint32_t* n_ptr,
-                                                       uint32_t cap, int shift, int db, uint32_t* hist) {
-  __shared__ uint32_t h[kMaxBins];
-  const uint32_t bins = 1u << db, mask = bins - 1;
-  const uint32_t n = clamp_n(n_ptr, cap);
-  uint32_t start, end;
-  radix_range(n, start, end);
-  for (uint32_t d = threadIdx.x; d < bins; d += kBlock) h[d] = 0;
-  __syncthreads();
-  for (uint32_t i = start + threadIdx.x; i < end; i += kBlock) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
-  __syncthreads();
-  for (uint32_t d = threadIdx.x; d < bins; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
 }
 
 // one block per digit: exclusive scan of that digit's per-block counts, digit total to tot[d]
@@ -685,112 +634,6 @@ __global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uin
   if (t == kRadixBlocks - 1) tot[d] = pre + x;
 }
 
-__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* kin, const uint32_t* vin,
-                                                          uint32_t* kout, uint32_t* vout,
-                                                          const uint32_t* n_ptr, uint32_t cap, int shift, int db,
-                                                          const uint32_t* hist, const uint32_t* tot) {
-  __shared__ uint32_t base[kMaxBins];
-  __shared__ uint32_t wtag[4][kMaxBins];  // (tile tag << 16) | count of that digit in that wave
-  __shared__ uint32_t part[kBlock];
-  const uint32_t bins = 1u << db, mask = bins - 1;
-  const uint32_t n = clamp_n(n_ptr, cap);
-  uint32_t start, end;
-  radix_range(n, start, end);
-  const uint32_t tid = threadIdx.x, wave = tid >> 6;
-  // digit bases: exclusive scan of the digit totals, plus this block's offset inside the digit
-  const uint32_t per = bins >= kBlock ? bins / kBlock : 1u;
-  const uint32_t d0 = tid * per;
-  uint32_t s = 0;
-  if (d0 < bins)
-    for (uint32_t k = 0; k < per; ++k) s += tot[d0 + k];
-  part[tid] = s;
-  for (uint32_t d = tid; d < bins; d += kBlock) wtag[0][d] = wtag[1][d] = wtag[2][d] = wtag[3][d] = 0;
-  __syncthreads();
-  for (uint32_t o = 1; o < kBlock; o <<= 1) {
-    const uint32_t v = tid >= o ? part[tid - o] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  if (d0 < bins) {
-    uint32_t run = part[tid] - s;
-    for (uint32_t k = 0; k < per; ++k) {
-      base[d0 + k] = run + hist[(d0 + k) * kRadixBlocks + blockIdx.x];
-      run += tot[d0 + k];
-    }
-  }
-  __syncthreads();
-  uint32_t tag = 1;
-  for (uint32_t t0 = start; t0 < end; t0 += kBlock, ++tag) {
-    const uint32_t i = t0 + tid;
-    const bool valid = i < end;
-    const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
-    const uint32_t d = (k >> shift) & mask;
-    uint64_t peers = __ballot(valid);
-    for (int b = 0; b < db; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(valid && bit);
-      peers &= bit ? bb : ~bb;
-    }
-    const uint32_t rank = mask_rank(peers);
-    const uint32_t cnt = (uint32_t)__popcll(peers);
-    if (valid && rank == 0) wtag[wave][d] = (tag << 16) | cnt;
-    __syncthreads();
-    bool mylast = false;
-    uint32_t pre = 0;
-    if (valid) {
-      bool later = false;
-#pragma unroll
-      for (uint32_t w = 0; w < 4; ++w) {
-        const uint32_t e = wtag[w][d];
-        const uint32_t c = (e >> 16) == tag ? (e & 0xFFFFu) : 0u;
-        if (w < wave) pre += c;
-        if (w > wave && c) later = true;
-      }
-      const uint32_t pos = base[d] + pre + rank;
-      kout[pos] = k;
-      vout[pos] = v;
-      mylast = !later && rank + 1 == cnt;
-    }
-    __syncthreads();
-    if (mylast) base[d] += pre + cnt;
-    __syncthreads();
-  }
-}
-
-// keys of a sharded record batch q (A, D or L); vals = physical index of the record.
-// mode 0 = sender (local id), 1 = receiver (local id), 2 = wheel slot
-__global__ __launch_bounds__(kBlock) void k_keys_rec(const tgsim_record* batch, int q, uint32_t subcap, int mode,
-                                                     uint32_t lo, int64_t slot_ns, uint32_t slots,
-                                                     const DevScalars* sc, uint32_t* keys, uint32_t* vals) {
-  __shared__ uint32_t pre[kNSub + 1];
-  if (threadIdx.x <= kNSub) pre[threadIdx.x] = sc->qpre[q][threadIdx.x];
-  __syncthreads();
-  const uint32_t n = pre[kNSub];
-  const int64_t base_slot = sc->t_end / slot_ns;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-    uint32_t a = 0, b = kNSub;
-    while (b - a > 1) {
-      const uint32_t mid = (a + b) >> 1;
-      if (pre[mid] <= j) a = mid; else b = mid;
-    }
-    const uint32_t p = a * subcap + (j - pre[a]);
-    const uint4 r = reinterpret_cast<const uint4*>(batch + p)[0];
-    uint32_t k;
-    if (mode == 0) k = r.z - lo;
-    else if (mode == 1) k = r.w - lo;
-    else {
-      const int64_t t = (int64_t)(((uint64_t)r.y << 32) | r.x);
-      int64_t s = t / slot_ns - base_slot;
-      s = s < 0 ? 0 : (s > (int64_t)slots - 1 ? (int64_t)slots - 1 : s);
-      k = (uint32_t)s;
-    }
-    keys[j] = k;
-    vals[j] = p;
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, const uint32_t* n_ptr, uint32_t kmin,
                                                      uint32_t* keys, uint32_t* vals) {
   const uint32_t n = *n_ptr;
@@ -798,34 +641,6 @@ __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, con
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     keys[i] = states[i] - kmin;
     vals[i] = i;
-  }
-}
-
-// Segment offsets off[k] = first position of key k (k = 0..K), and the list of segments longer
-// than kTile (handled by the merge-path path).
-// thread_max > 0: also list the segments with thread_max < len <= kTile in medium[] (n_medium).
-__global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t* keys, const uint32_t* n_ptr, uint32_t cap,
-                                                   uint32_t K, uint32_t* off, LargeSeg* large,
-                                                   uint32_t thread_max, uint32_t* medium, DevScalars* sc) {
-  const uint32_t n = clamp_n(n_ptr, cap);
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= K; k += stride) {
-    const uint32_t lb = lower_bound_u32(keys, n, k);
-    off[k] = lb;
-    if (k < K) {
-      const uint32_t ub = lower_bound_u32(keys, n, k + 1);
-      const uint32_t len = ub - lb;
-      const bool med = thread_max && len > thread_max && len <= (uint32_t)kTile;
-      const uint32_t mi = wave_append(med ? &sc->n_medium : nullptr);
-      if (med) medium[mi] = k;
-      if (len > (uint32_t)kTile) {
-        const uint32_t i = atomicAdd(&sc->n_large, 1u);
-        LargeSeg L;
-        L.seg = k; L.start = lb; L.len = len; L.pad = 0;
-        large[i] = L;
-        atomicMax(&sc->max_large, len);
-      }
-    }
   }
 }
 
@@ -1304,196 +1119,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys,
   }
 }
 
-// Register bitonic network over M (power of two) keys (k1, k2, k3); padding keys are all-ones.
-template <int M>
-__device__ __forceinline__ void net_sort(uint64_t (&k1)[M], uint64_t (&k2)[M], uint32_t (&k3)[M]) {
-#pragma unroll
-  for (int k = 2; k <= M; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const int l = i ^ j;
-        if (l > i) {
-          const bool up = (i & k) == 0;
-          const bool sw = key_less(0, k1[l], k2[l], k3[l], 0, k1[i], k2[i], k3[i]) == up;
-          const uint64_t a1 = k1[i], a2 = k2[i];
-          const uint32_t a3 = k3[i];
-          k1[i] = sw ? k1[l] : a1; k2[i] = sw ? k2[l] : a2; k3[i] = sw ? k3[l] : a3;
-          k1[l] = sw ? a1 : k1[l]; k2[l] = sw ? a2 : k2[l]; k3[l] = sw ? a3 : k3[l];
-        }
-      }
-    }
-  }
-}
-
-// Segment bounds of the calling thread for the one-thread-per-segment kernels (0 = not mine) and
-// the block's largest such segment.
-__device__ __forceinline__ uint32_t thread_seg(const uint32_t* off, uint32_t K, uint32_t seg, uint32_t& a,
-                                               uint32_t* s_max, const uint8_t* deferred = nullptr, int bs = 0) {
-  uint32_t len = 0;
-  a = 0;
-  if (seg < K && (!deferred || deferred[seg >> bs])) {  // keys of fused buckets are already done
-    a = off[seg];
-    len = off[seg + 1] - a;
-    if (len > (uint32_t)kThreadSeg) len = 0;
-  }
-  if (threadIdx.x == 0) *s_max = 0;
-  __syncthreads();
-  uint32_t wmax = len;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t v = __shfl_xor(wmax, o);
-    wmax = v > wmax ? v : wmax;
-  }
-  if (lane_id() == 0 && wmax) atomicMax(s_max, wmax);
-  __syncthreads();
-  return len;
-}
-
-template <class P, int M>
-__device__ __forceinline__ void thread_keys(const P& p, const uint32_t* vals, uint32_t seg, uint32_t a, uint32_t len,
-                                            uint64_t (&k1)[M], uint64_t (&k2)[M], uint32_t (&k3)[M]) {
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    k1[u] = ~0ull; k2[u] = ~0ull; k3[u] = 0xFFFFFFFFu;
-    if ((uint32_t)u < len) {
-      uint32_t sg;
-      p.key(seg, vals[a + u], sg, k1[u], k2[u], k3[u]);
-    }
-  }
-  net_sort<M>(k1, k2, k3);
-}
-
-// One block per listed segment (kThreadSeg < len <= kTile): LDS sort + the policy's block epilogue.
-template <class P>
-__global__ __launch_bounds__(kBlock) void k_seg_list(P p, const uint32_t* vals, const uint32_t* off,
-                                                     const uint32_t* list, const DevScalars* sc) {
-  __shared__ SortSmem s;
-  const uint32_t nm = sc->n_medium;
-  for (uint32_t w = blockIdx.x; w < nm; w += gridDim.x) {
-    const uint32_t g = list[w];
-    const uint32_t a = off[g], m = off[g + 1] - a;
-    for (uint32_t j = threadIdx.x; j < m; j += kBlock) p.key(g, vals[a + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-    __syncthreads();
-    span_sort(s, m, off, a);
-    p.epilogue(s, m, a, off, w);
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_large_prep(const LargeSeg* large, uint32_t* chunk_off,
-                                                       DevScalars* sc) {
-  __shared__ uint32_t part[kBlock];
-  __shared__ uint32_t carry;
-  const uint32_t nl = sc->n_large, tid = threadIdx.x;
-  if (tid == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < nl; base += kBlock) {
-    const uint32_t i = base + tid;
-    const uint32_t c = i < nl ? (large[i].len + kChunk - 1) / kChunk : 0u;
-    part[tid] = c;
-    __syncthreads();
-    for (uint32_t o = 1; o < kBlock; o <<= 1) {
-      const uint32_t v = tid >= o ? part[tid - o] : 0u;
-      __syncthreads();
-      part[tid] += v;
-      __syncthreads();
-    }
-    if (i < nl) chunk_off[i] = carry + part[tid] - c;
-    __syncthreads();
-    if (tid == kBlock - 1) carry += part[tid];
-    __syncthreads();
-  }
-  if (tid == 0) { chunk_off[nl] = carry; sc->n_chunks = carry; }
-}
-
-__device__ __forceinline__ uint32_t chunk_owner(const uint32_t* chunk_off, uint32_t nl, uint32_t c) {
-  uint32_t lo = 0, hi = nl;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (chunk_off[mid] <= c) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-template <class P>
-__global__ __launch_bounds__(kBlock) void k_large_chunks(P p, const uint32_t* keys, const uint32_t* vals,
-                                                         const LargeSeg* large, const uint32_t* chunk_off,
-                                                         const DevScalars* sc, uint64_t* K1, uint64_t* K2,
-                                                         uint32_t* K3) {
-  __shared__ SortSmem s;
-  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
-  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
-    const uint32_t li = chunk_owner(chunk_off, nl, c);
-    const LargeSeg L = large[li];
-    const uint32_t q = c - chunk_off[li];
-    const uint32_t st = L.start + q * kChunk;
-    const uint32_t cnt = min((uint32_t)kChunk, L.len - q * kChunk);
-    const uint32_t npad = next_pow2(cnt);
-    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
-      if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-      else pad_key(s, j);
-    }
-    __syncthreads();
-    bitonic_lds(s, npad);
-    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
-      K1[st + j] = s.k1[j]; K2[st + j] = s.k2[j]; K3[st + j] = s.k3[j];
-    }
-    __syncthreads();
-  }
-}
-
 __device__ __forceinline__ bool kless(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3,
                                       uint32_t x, uint32_t y) {
   return key_less(0, K1[x], K2[x], K3[x], 0, K1[y], K2[y], K3[y]);
-}
-
-// One merge-path pass: runs of width W inside every large segment are merged pairwise; each work
-// item produces kChunk outputs, 8 per thread from its own diagonal search.
-__global__ __launch_bounds__(kBlock) void k_large_merge(const LargeSeg* large, const uint32_t* chunk_off,
-                                                        const DevScalars* sc, uint32_t W,
-                                                        const uint64_t* sK1, const uint64_t* sK2,
-                                                        const uint32_t* sK3, uint64_t* dK1, uint64_t* dK2,
-                                                        uint32_t* dK3) {
-  constexpr uint32_t IT = kChunk / kBlock;
-  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
-  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
-    const uint32_t li = chunk_owner(chunk_off, nl, c);
-    const LargeSeg L = large[li];
-    const uint32_t q = c - chunk_off[li];
-    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
-    const uint32_t base = L.start;
-    if (L.len <= W) {
-      for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock) {
-        dK1[base + j] = sK1[base + j]; dK2[base + j] = sK2[base + j]; dK3[base + j] = sK3[base + j];
-      }
-      continue;
-    }
-    const uint32_t pair = o0 / (2 * W);
-    const uint32_t As = pair * 2 * W;
-    const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
-    const uint32_t nA = Ae - As, nB = Be - Ae;
-    const uint32_t dend = o1 - As;
-    const uint32_t d0 = o0 - As + threadIdx.x * IT;
-    if (d0 >= dend) continue;
-    const uint32_t a0 = base + As, b0 = base + Ae;
-    uint32_t lo = d0 > nB ? d0 - nB : 0u, hi = min(d0, nA);
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (!kless(sK1, sK2, sK3, b0 + (d0 - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
-    }
-    uint32_t ia = lo, ib = d0 - lo;
-    for (uint32_t k = 0; k < IT && d0 + k < dend; ++k) {
-      bool takeA;
-      if (ib >= nB) takeA = true;
-      else if (ia >= nA) takeA = false;
-      else takeA = !kless(sK1, sK2, sK3, b0 + ib, a0 + ia);
-      const uint32_t src = takeA ? a0 + ia++ : b0 + ib++;
-      const uint32_t dst = base + As + d0 + k;
-      dK1[dst] = sK1[src]; dK2[dst] = sK2[src]; dK3[dst] = sK3[src];
-    }
-  }
 }
 
 // ============================================================================================
@@ -1670,136 +1298,6 @@ __device__ __forceinline__ void block_scan2(uint32_t& v0, uint32_t& v1, uint32_t
   v1 = p1 + x1 - v1;
 }
 
-struct TBSmem {
-  uint32_t max_len, any_x;
-  uint32_t red[2 * (kBlock / 64)];
-  uint32_t base[2];
-};
-
-// One sender per thread (<= kThreadSeg items): sort in registers, run the GCRA recurrence
-// sequentially, reserve the block's departed copies with one atomic per queue, then write them.
-template <int M>
-__device__ __forceinline__ void tb_thread_body(const TBPolicy& p, const uint32_t* vals, uint32_t sl, uint32_t a,
-                                               uint32_t len, TBSmem& sm) {
-  uint64_t k1[M], k2[M];
-  uint32_t k3[M];
-  thread_keys<TBPolicy, M>(p, vals, sl, a, len, k1, k2, k3);
-  const int64_t t_end = p.sc->t_end;
-  int64_t dep[M];
-  int code[M];
-  uint32_t nD = 0, nL = 0, nX = 0;
-  int64_t x = 0, tau = 0;
-  uint32_t mult = 0, shift = 0;
-  if (len) {
-    const ShapeDev& sh = p.shape[sl];
-    tau = sh.tau; mult = sh.mult; shift = sh.shift;
-    x = p.X[sl];
-  }
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    dep[u] = 0;
-    code[u] = -1;
-    if ((uint32_t)u < len) {
-      const uint4 r0 = reinterpret_cast<const uint4*>(p.A + k3[u])[0];
-      const uint4 r1 = reinterpret_cast<const uint4*>(p.A + k3[u])[1];
-      const int64_t e = (int64_t)k1[u];
-      uint64_t c = ((uint64_t)r1.y * mult) >> shift;
-      c = c > kCostClamp ? kCostClamp : c;
-      const int64_t xprev = x;
-      const int64_t b = x > e - tau ? x : e - tau;
-      const int64_t v = b + (int64_t)c;
-      x = v > kTbClamp ? kTbClamp : v;
-      dep[u] = e > xprev ? e : xprev;
-      const int q = qid_stage_d(p.geo, r0.w, dep[u], t_end);
-      code[u] = q;
-      nD += q == Q_D; nL += q == Q_L; nX += q >= Q_X0;
-    }
-  }
-  if (len) p.X[sl] = x;
-  if (nX) sm.any_x = 1;
-  uint32_t tD, tL;
-  block_scan2(nD, nL, sm.red, tD, tL);  // nD/nL now this thread's offsets inside the block's runs
-  const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
-  const Queues& Q = p.Q;
-  if (threadIdx.x == 0) {
-    sm.base[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
-    sm.base[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
-  }
-  __syncthreads();
-  uint32_t pD = sm.base[0] + nD, pL = sm.base[1] + nL;
-  tgsim_record* bD = Q.D + (size_t)sub * Q.subcap;
-  tgsim_record* bL = Q.L + (size_t)sub * Q.subcap;
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    if (code[u] == Q_D || code[u] == Q_L) {
-      tgsim_record rec;
-      load_rec(p.A + k3[u], rec);
-      rec.t = dep[u];
-      rec.meta |= TGSIM_F_STAGE_D;
-      const bool isD = code[u] == Q_D;
-      const uint32_t pos = isD ? pD++ : pL++;
-      if (pos < Q.subcap) {
-        store_rec((isD ? bD : bL) + pos, rec);
-        Q.K[isD ? Q_D : Q_L][(size_t)sub * Q.subcap + pos] = Q.key_of(isD ? Q_D : Q_L, rec);
-      } else {
-        atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
-      }
-    }
-  }
-  if (sm.any_x) {  // cross-shard copies (S > 1): per-item wave appends onto the peer blocks
-    const uint32_t salt = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16u;
-#pragma unroll
-    for (int u = 0; u < M; ++u) {
-      tgsim_record rec;
-      const bool mine = code[u] >= Q_X0;
-      if (mine) {
-        load_rec(p.A + k3[u], rec);
-        rec.t = dep[u];
-        rec.meta |= TGSIM_F_STAGE_D;
-      }
-      Q.push(mine ? code[u] : -1, rec, salt + (uint32_t)u);
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_tb_thread(TBPolicy p, const uint32_t* vals, const uint32_t* off,
-                                                      uint32_t K, const uint8_t* deferred, int bs) {
-  __shared__ TBSmem sm;
-  const uint32_t sl = blockIdx.x * kBlock + threadIdx.x;
-  if (threadIdx.x == 0) sm.any_x = 0;
-  uint32_t a;
-  const uint32_t len = thread_seg(off, K, sl, a, &sm.max_len, deferred, bs);
-  const uint32_t M = sm.max_len;
-  if (M == 0) return;  // block-uniform
-  if (M <= 4) tb_thread_body<4>(p, vals, sl, a, len, sm);
-  else if (M <= 8) tb_thread_body<8>(p, vals, sl, a, len, sm);
-  else tb_thread_body<16>(p, vals, sl, a, len, sm);
-}
-
-// One block per large sender segment: sorted keys arrive in tiles of kChunk with a carried X.
-__global__ __launch_bounds__(kBlock) void k_tb_large(TBPolicy p, const LargeSeg* large,
-                                                     const uint64_t* K1, const uint32_t* K3) {
-  __shared__ SortSmem s;
-  const uint32_t nl = p.sc->n_large;
-  for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
-    const LargeSeg L = large[li];
-    bool has_carry = false;
-    int64_t carry = 0;
-    uint32_t salt = li * 131;
-    for (uint32_t t0 = 0; t0 < L.len; t0 += kChunk, salt += 16) {
-      const uint32_t cnt = min((uint32_t)kChunk, L.len - t0);
-      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
-        s.sg[j] = L.seg; s.k1[j] = K1[L.start + t0 + j]; s.k3[j] = K3[L.start + t0 + j]; s.perm[j] = j;
-      }
-      __syncthreads();
-      p.scan(s, cnt, has_carry, carry, t0 + cnt == L.len, salt);
-      carry = s.carry;
-      has_carry = true;
-      __syncthreads();
-    }
-  }
-}
-
 // ============================================================================================
 // (3) deliveries: inbox order (dst, t, src, seq, clone-first), written as SoA
 // ============================================================================================
@@ -1830,65 +1328,6 @@ struct EmitPolicy {
   }
 };
 
-constexpr int kStage = 2048;  // LDS staging of one block's output range in k_emit_thread
-
-template <int M>
-__device__ __forceinline__ void emit_thread_body(const EmitPolicy& p, const uint32_t* vals, uint32_t seg, uint32_t a,
-                                                 uint32_t len, uint32_t base, bool staged, uint32_t* stage) {
-  uint64_t k1[M], k2[M];
-  uint32_t k3[M];
-  thread_keys<EmitPolicy, M>(p, vals, seg, a, len, k1, k2, k3);
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    if ((uint32_t)u < len) {
-      if (staged) stage[a - base + u] = k3[u];
-      else p.write(a + u, k3[u]);
-    }
-  }
-}
-
-// One receiver per thread (<= kThreadSeg deliveries): sort in registers; the block's inbox range
-// (contiguous: consecutive receivers) is staged in LDS and written out coalesced.
-__global__ __launch_bounds__(kBlock) void k_emit_thread(EmitPolicy p, const uint32_t* vals, const uint32_t* off,
-                                                        uint32_t K, const uint8_t* deferred, int bs) {
-  __shared__ uint32_t s_max;
-  __shared__ uint32_t stage[kStage];
-  const uint32_t seg = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t a;
-  const uint32_t len = thread_seg(off, K, seg, a, &s_max, deferred, bs);
-  const uint32_t M = s_max;
-  if (M == 0) return;  // block-uniform
-  const uint32_t s0 = blockIdx.x * kBlock, s1 = min(s0 + (uint32_t)kBlock, K);
-  const uint32_t base = off[s0], R = off[s1] - base;
-  const bool staged = R <= (uint32_t)kStage;
-  if (staged) {
-    for (uint32_t j = threadIdx.x; j < R; j += kBlock) stage[j] = 0xFFFFFFFFu;
-    __syncthreads();
-  }
-  if (M <= 4) emit_thread_body<4>(p, vals, seg, a, len, base, staged, stage);
-  else if (M <= 8) emit_thread_body<8>(p, vals, seg, a, len, base, staged, stage);
-  else emit_thread_body<16>(p, vals, seg, a, len, base, staged, stage);
-  if (staged) {
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < R; j += kBlock) {
-      const uint32_t v = stage[j];
-      if (v != 0xFFFFFFFFu) p.write(base + j, v);
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_emit_large(EmitPolicy p, const LargeSeg* large,
-                                                       const uint32_t* chunk_off, const DevScalars* sc,
-                                                       const uint32_t* K3) {
-  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
-  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
-    const uint32_t li = chunk_owner(chunk_off, nl, c);
-    const LargeSeg L = large[li];
-    const uint32_t q = c - chunk_off[li];
-    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
-    for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock) p.write(L.start + j, K3[L.start + j]);
-  }
-}
 
 // ============================================================================================
 // fused bucket consumers: one workgroup per bucket of <= 2^kBktFusedKeyBits keys finishes the
@@ -2327,20 +1766,6 @@ struct SigPolicy {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void k_sig_large(SigPolicy p, const LargeSeg* large,
-                                                      const uint32_t* chunk_off, const DevScalars* sc,
-                                                      const uint64_t* K1, const uint32_t* K3) {
-  const uint32_t nc = sc->n_chunks, nl = sc->n_large;
-  for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
-    const uint32_t li = chunk_owner(chunk_off, nl, c);
-    const LargeSeg L = large[li];
-    const uint32_t q = c - chunk_off[li];
-    const uint32_t o0 = q * kChunk, o1 = min(o0 + (uint32_t)kChunk, L.len);
-    for (uint32_t j = o0 + threadIdx.x; j < o1; j += kBlock)
-      p.write(L.seg, L.start + j, L.start, K1[L.start + j], K3[L.start + j]);
-  }
-}
-
 // Commit a sorted batch: per present state, check time order, append a log chunk, bump the count.
 __global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint32_t K, uint32_t kmin,
                                                        uint64_t log_base, const int64_t* log, uint32_t* count,
@@ -2690,15 +2115,6 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint
   }
 }
 
-__global__ void k_finish(DevScalars* sc) {
-  const uint32_t n = sc->qn[Q_D];
-  sc->n_out = n;
-  sc->st[ST_DELIVERED] += n;
-  sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
-  sc->st[ST_EXTRACTED] += sc->n_extract;
-  sc->st[ST_INSERTED] += sc->qn[Q_L];
-}
-
 // ============================================================================================
 // workload generator: gossip storm round
 // ============================================================================================
@@ -2725,8 +2141,6 @@ __device__ __forceinline__ void storm_peers_serial(const StormArgs& a, uint32_t 
   for (uint32_t k = 0; k < a.F; ++k) {
     uint32_t out[4];
     philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
-    const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
-    const int64_t t = t0 + (a.spread > 0 ? (int64_t)(u % (uint64_t)a.spread) : 0);
     uint32_t p;
     for (uint32_t attempt = 0;; ++attempt) {
       if (attempt) philox4x32_10(g, a.round, (k << 16) | attempt, kStormSalt, a.key0, a.key1, out);
@@ -2823,12 +2237,6 @@ SigState sig_state(Dev& d) {
   return g;
 }
 
-static hipError_t reset_window(Dev& d) {
-  const size_t b = offsetof(DevScalars, q), e = offsetof(DevScalars, err);
-  TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
-  return hipMemsetAsync(d.qc, 0, (size_t)3 * kNSub * 32 * sizeof(uint32_t), d.stream);
-}
-
 static WindowArgs window_args(Dev& d, int mode, int64_t t_end, const int64_t* src, int64_t offset) {
   WindowArgs a;
   a.sc = d.sc; a.qc = d.qc; a.mode = mode; a.t_end_arg = t_end; a.src = src; a.offset = offset;
@@ -2887,54 +2295,6 @@ static Queues make_queues(Dev& d) {
   Q.sc = d.sc; Q.qc = d.qc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
   Q.K[0] = d.KA; Q.K[1] = d.KD; Q.K[2] = d.KL; Q.lo = d.lo; Q.slots = d.slots; Q.slot_ns = d.slot_ns;
   return Q;
-}
-
-static hipError_t qfinal(Dev& d, int q) {
-  hipLaunchKernelGGL(k_qfinal, dim3(1), dim3(64), 0, d.stream, d.sc, d.qc, q, d.subcap);
-  return hipGetLastError();
-}
-
-// Stable group-by of (keys0, vals0)[0..*n_ptr) on keys < K; returns the buffers holding the result.
-static hipError_t group_by(Dev& d, const uint32_t* n_ptr, uint32_t K, uint32_t** keys, uint32_t** vals) {
-  const int bits = bits_for(K);
-  uint32_t *ki = d.keys0, *vi = d.vals0, *ko = d.keys1, *vo = d.vals1;
-  if (bits > 0) {
-    const int passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
-    const int db = (bits + passes - 1) / passes;
-    for (int p = 0, shift = 0; p < passes; ++p, shift += db) {
-      {
-        ProfScope ps_(d, KID_RADIX_HIST);
-        hipLaunchKernelGGL(k_radix_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, n_ptr, d.cap_rec, shift,
-                           db, d.hist);
-      }
-      {
-        ProfScope ps_(d, KID_RADIX_ROWS);
-        hipLaunchKernelGGL(k_radix_rows, dim3(1u << db), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
-      }
-      {
-        ProfScope ps_(d, KID_RADIX_SCATTER);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, ki, vi, ko, vo, n_ptr,
-                           d.cap_rec, shift, db, d.hist, d.tot);
-      }
-      std::swap(ki, ko);
-      std::swap(vi, vo);
-    }
-    TG_CHECK(hipGetLastError());
-  }
-  *keys = ki;
-  *vals = vi;
-  return hipSuccess;
-}
-
-static hipError_t bounds(Dev& d, const uint32_t* keys, const uint32_t* n_ptr, uint32_t K, uint32_t thread_max = 0) {
-  const size_t b = offsetof(DevScalars, n_large), e = offsetof(DevScalars, n_recv);
-  TG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(d.sc) + b, 0, e - b, d.stream));
-  {
-    ProfScope ps_(d, KID_BOUNDS);
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for((uint64_t)K + 1)), dim3(kBlock), 0, d.stream, keys, n_ptr,
-                       d.cap_rec, K, d.seg_off, d.large, thread_max, d.medium, d.sc);
-  }
-  return hipGetLastError();
 }
 
 // Bucket shift: <= 2048 buckets of <= 2^kBktMaxKeyBits keys, 128 keys per bucket where possible.
@@ -3010,32 +2370,6 @@ static BktSrc bkt_queue(Dev& d, int q) {
   s.vals = nullptr; s.qc = d.qc; s.q = q; s.mode = q; s.subcap = d.subcap; s.n_ptr = nullptr; s.cap = d.cap_rec;
   s.regions = d.regions; s.cap_arena = d.cap_arena; s.slot_ns = d.slot_ns;
   return s;
-}
-
-// Sort the large segments (if any) into (K1,K2,K3) scratch; returns which buffer holds the result.
-template <class P>
-static hipError_t sort_large(Dev& d, const P& p, const uint32_t* keys, const uint32_t* vals, bool* any,
-                             uint64_t** K1, uint64_t** K2, uint32_t** K3) {
-  TG_CHECK(sync_scalars(d));
-  *any = d.h_sc->n_large > 0;
-  if (!*any) return hipSuccess;
-  const uint32_t max_len = d.h_sc->max_large;
-  const uint32_t nl = d.h_sc->n_large;
-  hipLaunchKernelGGL(k_large_prep, dim3(1), dim3(kBlock), 0, d.stream, d.large, d.chunk_off, d.sc);
-  const uint64_t chunks_ub = (uint64_t)d.cap_rec / kChunk + nl + 1;
-  const unsigned g = (unsigned)std::min<uint64_t>(chunks_ub, (uint64_t)kStreamBlocks);
-  hipLaunchKernelGGL((k_large_chunks<P>), dim3(g), dim3(kBlock), 0, d.stream, p, keys, vals, d.large, d.chunk_off,
-                     d.sc, d.K1a, d.K2a, d.K3a);
-  uint64_t *s1 = d.K1a, *s2 = d.K2a, *d1 = d.K1b, *d2 = d.K2b;
-  uint32_t *s3 = d.K3a, *d3 = d.K3b;
-  for (uint64_t W = kChunk; W < max_len; W *= 2) {
-    hipLaunchKernelGGL(k_large_merge, dim3(g), dim3(kBlock), 0, d.stream, d.large, d.chunk_off, d.sc, (uint32_t)W,
-                       s1, s2, s3, d1, d2, d3);
-    std::swap(s1, d1); std::swap(s2, d2); std::swap(s3, d3);
-  }
-  TG_CHECK(hipGetLastError());
-  *K1 = s1; *K2 = s2; *K3 = s3;
-  return hipSuccess;
 }
 
 template <class P>

@@ -294,7 +294,6 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.seg_off, segK);
   rc |= dalloc(c, &d.large, phys_rec / kTile + 16);
   rc |= dalloc(c, &d.medium, segK);
-  rc |= dalloc(c, &d.deferred, kMaxBins);
   rc |= dalloc(c, &d.chunk_off, phys_rec / kTile + 17);
   rc |= dalloc(c, &d.K1a, phys_rec);
   rc |= dalloc(c, &d.K1b, phys_rec);
