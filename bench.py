@@ -131,9 +131,18 @@ def main():
     from testground_amd._abi import T_NOW
     from testground_amd.sim import Simulator
 
+    # More ranks than visible GPUs (rehearsing the sharded path on a one-GPU box): ranks share the
+    # devices round-robin and the collectives run over gloo on host copies. The driver's multi-GPU
+    # runs (one rank per GPU) always take RCCL.
+    ndev = torch.cuda.device_count()
+    rehearsal = world > ndev
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.Stream()  # one stream shared by the simulator and the collectives
     torch.cuda.set_stream(stream)
     shapes = storm_shapes(args.instances, args.seed)
@@ -151,6 +160,16 @@ def main():
         recv_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         sim.set_exchange_buffers(send_t.data_ptr(), recv_t.data_ptr(), nbytes)
         rel_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+        if rehearsal:
+            send_h, recv_h = torch.empty_like(send_t, device="cpu"), torch.zeros_like(recv_t, device="cpu")
+
+    def all_reduce(t, op):
+        if rehearsal:
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
 
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
@@ -160,9 +179,14 @@ def main():
             sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
         else:
             sim.storm_release_device(rel_t.data_ptr())
-            dist.all_reduce(rel_t, op=dist.ReduceOp.MAX)
+            all_reduce(rel_t, dist.ReduceOp.MAX)
             sim.advance_begin_device(rel_t.data_ptr(), rtt)
-            exchange(send_t, recv_t, xcap, dist)
+            if rehearsal:
+                send_h.copy_(send_t)
+                exchange(send_h, recv_h, xcap, dist)
+                recv_t.copy_(recv_h)
+            else:
+                exchange(send_t, recv_t, xcap, dist)
             sim.advance_end()
 
     # warm-up (untimed, unprofiled), then a few probe steps that time every kernel class to find the
@@ -206,10 +230,10 @@ def main():
     delivered = delta["delivered"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, dist.ReduceOp.MAX)
         elapsed = float(t.item())
         v = torch.tensor([delivered], dtype=torch.int64, device="cuda")
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        all_reduce(v, dist.ReduceOp.SUM)
         delivered = int(v.item())
 
     bytes_total = BYTE_MODELS[dominant](delta)
@@ -245,7 +269,7 @@ def main():
                 "workload": "gossip storm (SURVEY.md 8(d) config 4): 100k instances, fanout 8 Philox peers, "
                             "1 KiB messages within 10 ms, per-sender 10 Mbit/s HTB, latency U[20,100] ms, "
                             "jitter 5 ms, loss 0.5%, SignalAndWait(round, N) + 1 ms sync RTT per round",
-                "instances": N, "fanout": F, "msg_bytes": args.size, "parallelism": f"shard{world}",
+                "instances": N, "fanout": F, "msg_bytes": args.size, "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
                 "delivered_in_timed_steps": delivered,
                 "simulated_ms_per_step": (sim_t1 - sim_t0) / 1e6 / args.steps,
             },
