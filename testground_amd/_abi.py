@@ -158,12 +158,14 @@ _HIP: Binding | None = None
 
 
 def hip_library() -> Binding:
-    """The product library. Raises if it was not built (run __graft_entry__.build())."""
+    """The product library. Raises if it was not built (run __graft_entry__.build()). TGSIM_LIB
+    names an experiment build of the same sources to load instead (tools/ timing probes)."""
     global _HIP
     if _HIP is None:
-        if not os.path.exists(LIB_PATH):
-            raise TgsimError(ENODEV, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-        _HIP = bind(LIB_PATH, "tgsim_", "hip")
+        path = os.environ.get("TGSIM_LIB") or LIB_PATH
+        if not os.path.exists(path):
+            raise TgsimError(ENODEV, f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        _HIP = bind(path, "tgsim_", "hip")
     return _HIP
 
 

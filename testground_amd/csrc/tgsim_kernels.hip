@@ -2124,6 +2124,8 @@ struct StormArgs {
   int64_t t0;
   uint32_t F, Fp, size;
   int64_t spread;
+  uint64_t spread_m;         // u % spread by multiply-shift (Granlund-Montgomery, exact for every u)
+  uint32_t spread_sh1, spread_sh2;
   uint32_t key0, key1, base;
   uint32_t* m_src;
   uint32_t* m_dst;
@@ -2132,39 +2134,23 @@ struct StormArgs {
   int64_t* m_t;
 };
 
-// The storm's k-th peer of instance g (drawn without replacement): the first Philox draw of
-// (g, round, k) unless it repeats one of the k earlier peers, then further attempts (ctr word 2 =
-// k << 16 | attempt). Sequential restatement; the kernel below runs it only for a group that drew
-// a repeat.
-__device__ __forceinline__ void storm_peers_serial(const StormArgs& a, uint32_t g, uint32_t l, int64_t t0) {
-  uint32_t chosen[32];
-  for (uint32_t k = 0; k < a.F; ++k) {
-    uint32_t out[4];
-    philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
-    uint32_t p;
-    for (uint32_t attempt = 0;; ++attempt) {
-      if (attempt) philox4x32_10(g, a.round, (k << 16) | attempt, kStormSalt, a.key0, a.key1, out);
-      p = out[0] % (a.N - 1);
-      if (p >= g) ++p;
-      bool dupl = false;
-#pragma unroll
-      for (uint32_t j = 0; j < 32; ++j) dupl |= (j < k) && chosen[j] == p;
-      if (!dupl) break;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < 32; ++j)
-      if (j == k) chosen[j] = p;
-    const uint32_t i = a.base + l * a.F + k;
-    a.m_dst[i] = p;
-  }
+// u mod d for the launch-invariant divisor d = a.spread > 0: q = (t + ((u - t) >> sh1)) >> sh2 with
+// t = mulhi(m, u) (Granlund & Montgomery 1994, fig. 4.1; m, sh1, sh2 from storm_divisor on the host).
+__device__ __forceinline__ uint64_t spread_mod(const StormArgs& a, uint64_t u) {
+  const uint64_t t = __umul64hi(a.spread_m, u);
+  const uint64_t q = (t + ((u - t) >> a.spread_sh1)) >> a.spread_sh2;
+  return u - q * (uint64_t)a.spread;
 }
 
 // One storm round: every instance sends F messages to F distinct random peers and signals `state`
 // at its latest send time. A group of Fp (power of two >= F) lanes per instance, one message per
-// lane: the first draws of the group are checked for repeats with F shuffles, and only a group
-// that drew a repeat (probability ~F^2/2N) redraws serially, so the output equals the serial
-// restatement (tgo_gen_storm_round). Stores are coalesced (message l*F + k at lane l*Fp + k). The
-// signals are reduced to per-block partials in the same launch (k_sig_commit finishes them).
+// lane. Peer k is the first Philox draw of (g, round, k) unless it repeats one of the k earlier
+// peers, then further attempts (ctr word 2 = k << 16 | attempt) - the serial restatement
+// tgo_gen_storm_round. All first draws are checked with F shuffles; only a wave holding a group that
+// drew a repeat (probability ~F^2/2N per group) walks the group lane by lane, each lane redrawing
+// against the final peers of the lanes before it. Stores are coalesced (message l*F + k at lane
+// l*Fp + k). The signals are reduced to per-block partials in the same launch (k_sig_commit
+// finishes them).
 __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) {
   const int64_t t0 = a.t0 == INT64_MIN ? sg.sc->t_end : a.t0;  // TGSIM_T_NOW: the device's window start
   const uint32_t total = a.nloc * a.Fp;
@@ -2181,7 +2167,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
       uint32_t out[4];
       philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
       const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
-      t = t0 + (a.spread > 0 ? (int64_t)(u % (uint64_t)a.spread) : 0);
+      t = t0 + (a.spread > 0 ? (int64_t)spread_mod(a, u) : 0);
       p = out[0] % (a.N - 1);
       if (p >= g) ++p;
     }
@@ -2190,14 +2176,28 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
       const uint32_t q = __shfl(p, (int)(gbase + j));
       dup |= msg && j < k && q == p;
     }
-    const uint64_t dmask = __ballot(dup);
-    const uint64_t gmask = (a.Fp >= 64 ? ~0ull : ((1ull << a.Fp) - 1ull)) << gbase;
-    const bool serial = (dmask & gmask) != 0;
+    if (__ballot(dup)) {  // wave-uniform, rare: lanes k = 1 .. F-1 in turn settle against lanes j < k
+      uint32_t attempt = 0;
+      for (uint32_t kk = 1; kk < a.F; ++kk) {
+        for (;;) {
+          bool again = false;
+          for (uint32_t j = 0; j < kk; ++j) {
+            const uint32_t q = __shfl(p, (int)(gbase + j));
+            again |= msg && k == kk && q == p;
+          }
+          if (!__ballot(again)) break;
+          if (again) {
+            uint32_t out[4];
+            philox4x32_10(g, a.round, (k << 16) | ++attempt, kStormSalt, a.key0, a.key1, out);
+            p = out[0] % (a.N - 1);
+            if (p >= g) ++p;
+          }
+        }
+      }
+    }
     if (msg) {
       const uint32_t i = a.base + l * a.F + k;
-      a.m_src[i] = g; a.m_seq[i] = a.round * a.F + k; a.m_size[i] = a.size; a.m_t[i] = t;
-      if (!serial) a.m_dst[i] = p;
-      else if (k == 0) storm_peers_serial(a, g, l, t0);
+      a.m_src[i] = g; a.m_dst[i] = p; a.m_seq[i] = a.round * a.F + k; a.m_size[i] = a.size; a.m_t[i] = t;
     }
     // the instance's signal time: its latest send
     for (uint32_t o = a.Fp >> 1; o > 0; o >>= 1) {
@@ -2537,6 +2537,20 @@ hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, u
   return hipGetLastError();
 }
 
+// Multiply-shift constants of u mod d for every 64-bit u (Granlund & Montgomery 1994, fig. 4.1):
+// l = ceil(log2 d), m = floor(2^64 (2^l - d) / d) + 1, sh1 = min(l, 1), sh2 = max(l - 1, 0).
+static void storm_divisor(int64_t d, uint64_t& m, uint32_t& sh1, uint32_t& sh2) {
+  m = 0; sh1 = sh2 = 0;
+  if (d <= 0) return;
+  const uint64_t ud = (uint64_t)d;
+  uint32_t l = 0;
+  while (l < 64 && (1ull << l) < ud) ++l;
+  const unsigned __int128 two_l = (unsigned __int128)1 << l;
+  m = (uint64_t)((((unsigned __int128)1 << 64) * (two_l - ud)) / ud + 1);
+  sh1 = l < 1 ? l : 1;
+  sh2 = l > 1 ? l - 1 : 0;
+}
+
 // k_gen_storm only: the batch's per-block partials wait in sig_part for launch_sig_commit (the
 // runtime defers it so that a barrier registered next rides in the same launch). *nparts = grid.
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
@@ -2546,7 +2560,8 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   a.lo = d.lo; a.nloc = d.nloc; a.N = d.N; a.round = round; a.t0 = t0; a.F = fanout;
   a.Fp = 1;
   while (a.Fp < fanout) a.Fp <<= 1;
-  a.size = size; a.spread = spread_ns; a.key0 = d.key0; a.key1 = d.key1; a.base = staged_base;
+  a.size = size; a.spread = spread_ns; a.key0 = d.key0;
+  storm_divisor(spread_ns, a.spread_m, a.spread_sh1, a.spread_sh2); a.key1 = d.key1; a.base = staged_base;
   a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;
   const uint64_t threads = (uint64_t)d.nloc * a.Fp;
   const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock,

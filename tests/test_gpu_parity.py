@@ -37,7 +37,7 @@ def test_storm_rounds(hip, oracle):
 @pytest.mark.parametrize("n_inst,fanout", [(12, 10), (300, 5), (64, 1), (100, 32), (33, 3)])
 def test_storm_fanouts(hip, oracle, n_inst, fanout):
     """Lane groups of the next power of two >= fanout; small populations force repeated draws
-    (the serial redraw path) in most groups."""
+    (the lane-by-lane redraw of k_gen_storm) in most groups."""
     S.assert_same(S.run_storm(hip, n_inst=n_inst, rounds=3, fanout=fanout),
                   S.run_storm(oracle, n_inst=n_inst, rounds=3, fanout=fanout))
 
