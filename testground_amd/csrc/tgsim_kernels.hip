@@ -963,6 +963,9 @@ __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const 
 // Wheel insert with buckets = slots (slots <= kMaxBins): records are copied straight from the L
 // batch into this window's arena region in slot order, and the slot directory is the scan. The
 // first block also closes the window's counters (the former k_finish).
+constexpr int kWheelUnroll = 8;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                           tgsim_record* arena, uint32_t* dirs, uint32_t slots,
                                                           const uint32_t* hist, const uint32_t* tot) {
@@ -990,27 +993,28 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
   bkt_bases(slots, hist, tot, base, part);
   uint32_t start, end;
   bkt_block_range(src, start, end);
-  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * 4) {
-    uint32_t k[4];
-    uint4 ra[4], rb[4];
+  // kWheelUnroll records in flight per thread; out-of-range lanes load a clamped (valid) record so
+  // the arrays stay in registers (a conditional load, or HIP's uint4 wrapper, left them in scratch)
+  for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kWheelUnroll) {
+    uint32_t k[kWheelUnroll];
+    v4u32 ra[kWheelUnroll], rb[kWheelUnroll];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kWheelUnroll; ++u) {
       const uint32_t j = j0 + u * kBlock;
-      k[u] = 0xFFFFFFFFu;
-      if (j < end) {
-        k[u] = src.keys[j];
-        const uint4* p = reinterpret_cast<const uint4*>(L + j);
-        ra[u] = p[0];
-        rb[u] = p[1];
-      }
+      const bool in = j < end;
+      k[u] = in ? src.keys[j] : 0xFFFFFFFFu;
+      const v4u32* p = reinterpret_cast<const v4u32*>(L + (in ? j : j0));
+      ra[u] = p[0];
+      rb[u] = p[1];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k[u] == 0xFFFFFFFFu) continue;
-      const uint32_t pos = atomicAdd(&base[k[u]], 1u);
-      uint4* q = reinterpret_cast<uint4*>(arena + off + pos);
-      q[0] = ra[u];
-      q[1] = rb[u];
+    for (int u = 0; u < kWheelUnroll; ++u) {
+      if (k[u] != 0xFFFFFFFFu) {
+        const uint32_t pos = atomicAdd(&base[k[u]], 1u);
+        v4u32* q = reinterpret_cast<v4u32*>(arena + off + pos);
+        q[0] = ra[u];
+        q[1] = rb[u];
+      }
     }
   }
 }
