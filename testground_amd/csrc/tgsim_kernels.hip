@@ -28,15 +28,16 @@ struct ProfScope {
   Dev& d;
   int kid;
   hipEvent_t a = nullptr;
-  ProfScope(Dev& dd, int k) : d(dd), kid(k) {
+  hipStream_t st;
+  ProfScope(Dev& dd, int k, hipStream_t s = nullptr) : d(dd), kid(k), st(s ? s : dd.stream) {
     if (!(d.prof.mask & (1u << kid))) return;
     a = take();
-    (void)hipEventRecord(a, d.stream);
+    (void)hipEventRecord(a, st);
   }
   ~ProfScope() {
     if (!a) return;
     hipEvent_t b = take();
-    (void)hipEventRecord(b, d.stream);
+    (void)hipEventRecord(b, st);
     d.prof.pending.push_back({kid, a, b});
   }
   hipEvent_t take() {
@@ -545,25 +546,60 @@ __device__ void plan_regions(RegionDev* regions, const uint32_t* dirs, uint32_t 
   }
 }
 
+constexpr uint32_t kPlanLds = 1024;  // extraction plans up to this many live regions are searched in LDS
+constexpr int kExtractUnroll = 4;     // records in flight per thread
+
+// Copies every due wheel record into A (token bucket now) / D (deliver now) / L (not yet due). The
+// plan (each live region's due prefix and its place in the output) is staged in LDS, so locating
+// a record costs no global round trip; kExtractUnroll records per thread are loaded before the
+// wave appends.
 __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, const uint32_t* plan_start,
                                                     const uint32_t* plan_off, const tgsim_record* arena,
                                                     Queues Q) {
+  __shared__ uint32_t s_off[kPlanLds];
+  __shared__ uint64_t s_src[kPlanLds];
   DevScalars* sc = Q.sc;
   const uint32_t total = sc->n_extract, tail = sc->plan_tail, nl = sc->plan_n;
   const int64_t t_end = sc->t_end;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t it = 0;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride, ++it) {
-    uint32_t lo = 0, hi = nl;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (plan_off[mid] <= j) lo = mid; else hi = mid;
+  const bool lds = nl <= kPlanLds;
+  if (lds) {
+    for (uint32_t k = threadIdx.x; k < nl; k += kBlock) {
+      s_off[k] = plan_off[k];
+      s_src[k] = regions[(tail + k) % kMaxRegions].arena_off + plan_start[k];
     }
-    const RegionDev& r = regions[(tail + lo) % kMaxRegions];
-    tgsim_record rec;
-    load_rec(arena + r.arena_off + plan_start[lo] + (j - plan_off[lo]), rec);
-    const int q = rec.t < t_end ? ((rec.meta & TGSIM_F_STAGE_D) ? Q_D : Q_A) : Q_L;
-    Q.push(q, rec, it);
+    __syncthreads();
+  }
+  const uint32_t step = gridDim.x * kBlock * kExtractUnroll;
+  uint32_t it = 0;
+  for (uint32_t base = blockIdx.x * kBlock * kExtractUnroll; base < total; base += step, ++it) {  // block-uniform
+    tgsim_record rec[kExtractUnroll];
+#pragma unroll
+    for (int u = 0; u < kExtractUnroll; ++u) {
+      uint32_t j = base + u * kBlock + threadIdx.x;
+      j = j < total ? j : total - 1;  // clamped: the load stays valid, the push is skipped
+      uint32_t lo = 0, hi = nl;
+      uint64_t at;
+      if (lds) {
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        at = s_src[lo] + (j - s_off[lo]);
+      } else {
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (plan_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        at = regions[(tail + lo) % kMaxRegions].arena_off + plan_start[lo] + (j - plan_off[lo]);
+      }
+      load_rec(arena + at, rec[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kExtractUnroll; ++u) {
+      const uint32_t j = base + u * kBlock + threadIdx.x;
+      const int q = j >= total ? -1 : (rec[u].t < t_end ? ((rec[u].meta & TGSIM_F_STAGE_D) ? Q_D : Q_A) : Q_L);
+      Q.push(q, rec[u], it * kExtractUnroll + u);
+    }
   }
 }
 
@@ -704,7 +740,9 @@ __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc,
   __shared__ uint32_t h[kMaxBins];
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) h[d] = 0;
   if (blockIdx.x == 0) {
-    if (threadIdx.x == 0) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
+    // the segment lists belong to the group-bys; the wheel insert (Q_L) leaves them alone
+    const bool wheel = src.mode != 3 && src.q == Q_L;
+    if (threadIdx.x == 0 && !wheel) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
     if (src.mode != 3) {
       if (threadIdx.x < kNSub) queue_final(sc, src.qc, src.q, src.subcap);
       if (src.q == Q_L) {
@@ -2432,6 +2470,8 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
 
 // Deliveries: partition the due copies by receiver bucket, then one workgroup per bucket orders
 // each inbox and writes it as SoA (k_emit_bucket); long inboxes finish in k_rest.
+static hipError_t run_wheel_insert(Dev& d, hipStream_t st);
+
 static hipError_t run_deliveries(Dev& d) {
   EmitPolicy p;
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
@@ -2450,19 +2490,19 @@ static hipError_t run_deliveries(Dev& d) {
 }
 
 // Wheel insert: one partition pass with buckets = slots; records go straight into the arena.
-static hipError_t run_wheel_insert(Dev& d) {
+static hipError_t run_wheel_insert(Dev& d, hipStream_t st) {
   const BktSrc src = bkt_queue(d, Q_L);
   {
-    ProfScope ps_(d, KID_BKT_HIST);
-    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bkt_div(1), d.slots, d.hist);
+    ProfScope ps_(d, KID_BKT_HIST, st);
+    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, st, src, d.sc, bkt_div(1), d.slots, d.hist);
   }
   {
-    ProfScope ps_(d, KID_RADIX_ROWS);
-    hipLaunchKernelGGL(k_radix_rows, dim3(d.slots), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+    ProfScope ps_(d, KID_RADIX_ROWS, st);
+    hipLaunchKernelGGL(k_radix_rows, dim3(d.slots), dim3(kRadixBlocks), 0, st, d.hist, d.tot);
   }
   {
-    ProfScope ps_(d, KID_REGION_FILL);
-    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, d.L, d.arena,
+    ProfScope ps_(d, KID_REGION_FILL, st);
+    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, st, src, d.sc, d.L, d.arena,
                        d.dirs, d.slots, d.hist, d.tot);
   }
   return hipGetLastError();
@@ -2476,7 +2516,7 @@ hipError_t window_end(Dev& d) {
     TG_CHECK(hipGetLastError());
   }
   TG_CHECK(run_deliveries(d));
-  return run_wheel_insert(d);  // k_wheel_scatter also closes the window's counters
+  return run_wheel_insert(d, d.stream);  // k_wheel_scatter also closes the window's counters
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
