@@ -144,8 +144,8 @@ def run_sync(binding, seed: int):
     return res
 
 
-def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4):
-    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed), binding=binding)
+def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None):
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **(cfg_kw or {})), binding=binding)
     rng = np.random.default_rng(seed)
     for g in range(n_inst):
         sim.set_shape(g, make_shape(latency_ns=int(rng.integers(20, 101)) * MS, jitter_ns=5 * MS,
