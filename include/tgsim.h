@@ -276,6 +276,24 @@ int tgsim_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t f
  * all-reduce across shards yields the release time of SignalAndWait(state, n_instances). */
 int tgsim_storm_release_device(tgsim_ctx* ctx, int64_t* out_device);
 
+/* ---- flood workload (1M-instance random-regular pubsub) --------------
+ * A publication floods a fixed graph: an instance forwards it, on its first receipt, to every
+ * neighbour except the sender; duplicates are dropped (first-receipt dedup). Replaces the per-peer
+ * re-publish loops of pubsub/gossip test plans (message fan-out as in plans/benchmarks/storm.go:
+ * 98-190; peers from the address exchange of plans/network/pingpong.go:219-245). Messages carry
+ * seq = pub * D + neighbour slot (D = max degree), so (src, seq) stays unique per run.
+ * set_graph: CSR over all N instances (offsets[N+1], degree <= 64, no self loops); resets the
+ *   first-receipt state; max_pubs * D <= 2^32.
+ * publish: instance inst[i] originates pub[i] at t[i] (>= horizon): it is marked as having seen it
+ *   and sends it to all its neighbours (shard-local instances only; others are ignored).
+ * react: for every delivery of the last window, in inbox order, a first receipt forwards at
+ *   max(t_deliver, horizon); *n_forwarded = messages staged. Deliveries whose seq / D >= max_pubs
+ *   are not flood messages: EINVAL. */
+int tgsim_flood_set_graph(tgsim_ctx* ctx, const uint32_t* offsets, const uint32_t* neighbors, uint32_t max_pubs);
+int tgsim_flood_publish(tgsim_ctx* ctx, const uint32_t* instances, const uint32_t* pubs, const int64_t* t,
+                        size_t n, uint32_t size);
+int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
+
 #ifdef __cplusplus
 }
 #endif

@@ -198,6 +198,9 @@ struct tgo_ctx {
   size_t n_states;
   owaiter* waiters; size_t n_waiters, waiters_cap;
   int64_t storm_release;
+  /* flood (config 5): local rows of the graph, first-receipt bits [max_pubs][nloc] */
+  uint32_t* fl_off; uint32_t* fl_nbr; uint32_t* fl_seen;
+  uint32_t fl_D, fl_max_pubs, fl_wpp;
   char err[512];
 };
 
@@ -307,6 +310,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
+  free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
   if (c->rules) for (uint32_t i = 0; i < c->nloc; ++i) free(c->rules[i].v);
   if (c->outbox) for (uint32_t i = 0; i < c->S; ++i) free(c->outbox[i].v);
   if (c->sig) for (size_t i = 0; i < c->n_states; ++i) free(c->sig[i].t);
@@ -880,4 +884,111 @@ int tgo_storm_release(tgo_ctx* c, int64_t* out) {
   if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
   *out = c->storm_release;
   return TGSIM_OK;
+}
+
+/* ============================== flood (config 5) ============================================
+ * Workload of SURVEY.md 8(d) config 5 / BASELINE.json configs[4]: a publication floods a fixed
+ * graph; an instance forwards it on first receipt to every neighbour except the one it came from
+ * (the gossip/flood pattern pubsub plans run over their peers, cf. plans/benchmarks/storm.go:31-197
+ * for the message fan-out and plans/network/pingpong.go:219-245 for the per-instance address
+ * exchange that builds the peer lists). Message seq = pub * D + neighbour slot (D = max degree),
+ * so (src, seq) is unique per run; a forward leaves at max(t_deliver, horizon). */
+
+static int fl_seen_get(const tgo_ctx* c, uint32_t p, uint32_t l) {
+  return (c->fl_seen[(size_t)p * c->fl_wpp + (l >> 5)] >> (l & 31)) & 1u;
+}
+static void fl_seen_set(tgo_ctx* c, uint32_t p, uint32_t l) {
+  c->fl_seen[(size_t)p * c->fl_wpp + (l >> 5)] |= 1u << (l & 31);
+}
+
+int tgo_flood_set_graph(tgo_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
+  if (!off || (off[c->N] && !nbr) || max_pubs == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  uint32_t D = 1;
+  for (uint32_t g = 0; g < c->N; ++g) {
+    if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
+    uint32_t len = off[g + 1] - off[g];
+    if (len > 64) return fail(c, TGSIM_EINVAL, "degree %u > 64", len);
+    if (len > D) D = len;
+    for (uint32_t k = off[g]; k < off[g + 1]; ++k)
+      if (nbr[k] >= c->N || nbr[k] == g) return fail(c, TGSIM_EINVAL, "bad neighbour of %u", g);
+  }
+  if ((uint64_t)max_pubs * D > 0x100000000ull) return fail(c, TGSIM_EINVAL, "max_pubs * degree > 2^32");
+  free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
+  uint32_t base = off[c->lo], m = off[c->hi] - base;
+  c->fl_off = (uint32_t*)malloc((c->nloc + 1) * 4);
+  c->fl_nbr = (uint32_t*)malloc((m ? m : 1) * 4);
+  c->fl_wpp = (c->nloc + 31) / 32;
+  c->fl_seen = (uint32_t*)calloc((size_t)max_pubs * c->fl_wpp + 1, 4);
+  if (!c->fl_off || !c->fl_nbr || !c->fl_seen) return fail(c, TGSIM_ENOMEM, "oom");
+  for (uint32_t l = 0; l <= c->nloc; ++l) c->fl_off[l] = off[c->lo + l] - base;
+  if (m) memcpy(c->fl_nbr, nbr + base, (size_t)m * 4);
+  c->fl_D = D; c->fl_max_pubs = max_pubs;
+  return TGSIM_OK;
+}
+
+/* forwards of local instance l for publication p (excluding neighbour `from`), appended to m */
+static void fl_emit(const tgo_ctx* c, uint32_t l, uint32_t p, uint32_t from, int64_t t, uint32_t size,
+                    uint32_t* src, uint32_t* dst, uint32_t* seq, uint32_t* sz, int64_t* ts, size_t* n) {
+  for (uint32_t k = c->fl_off[l]; k < c->fl_off[l + 1]; ++k) {
+    uint32_t v = c->fl_nbr[k];
+    if (v == from) continue;
+    src[*n] = c->lo + l; dst[*n] = v; seq[*n] = p * c->fl_D + (k - c->fl_off[l]); sz[*n] = size; ts[*n] = t;
+    ++*n;
+  }
+}
+
+static int fl_enqueue(tgo_ctx* c, size_t cap, uint32_t* src, uint32_t* dst, uint32_t* seq, uint32_t* sz,
+                      int64_t* ts, size_t n) {
+  (void)cap;
+  tgsim_msg_soa m = {src, dst, seq, sz, ts};
+  return tgo_enqueue(c, &m, n);
+}
+
+int tgo_flood_publish(tgo_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t, size_t n,
+                      uint32_t size) {
+  if (!c->fl_off) return fail(c, TGSIM_ESTATE, "no flood graph");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (n && (!inst || !pubs || !t)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i)
+    if (inst[i] >= c->N || pubs[i] >= c->fl_max_pubs) return fail(c, TGSIM_EINVAL, "bad publication %zu", i);
+  size_t cap = n * c->fl_D + 1, k = 0;
+  uint32_t* src = malloc(cap * 4); uint32_t* dst = malloc(cap * 4); uint32_t* seq = malloc(cap * 4);
+  uint32_t* sz = malloc(cap * 4); int64_t* ts = malloc(cap * 8);
+  int rc = TGSIM_ENOMEM;
+  if (src && dst && seq && sz && ts) {
+    for (size_t i = 0; i < n; ++i)
+      if (inst[i] >= c->lo && inst[i] < c->hi) fl_emit(c, inst[i] - c->lo, pubs[i], UINT32_MAX, t[i], size, src, dst, seq, sz, ts, &k);
+    rc = fl_enqueue(c, cap, src, dst, seq, sz, ts, k);
+    if (!rc)
+      for (size_t i = 0; i < n; ++i)
+        if (inst[i] >= c->lo && inst[i] < c->hi) fl_seen_set(c, pubs[i], inst[i] - c->lo);
+  }
+  free(src); free(dst); free(seq); free(sz); free(ts);
+  return rc;
+}
+
+int tgo_flood_react(tgo_ctx* c, uint32_t size, size_t* n_fwd) {
+  if (!c->fl_off) return fail(c, TGSIM_ESTATE, "no flood graph");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  const orecs* o = &c->out;
+  size_t cap = o->n * c->fl_D + 1, k = 0;
+  uint32_t* src = malloc(cap * 4); uint32_t* dst = malloc(cap * 4); uint32_t* seq = malloc(cap * 4);
+  uint32_t* sz = malloc(cap * 4); int64_t* ts = malloc(cap * 8);
+  int rc = TGSIM_ENOMEM;
+  if (src && dst && seq && sz && ts) {
+    rc = TGSIM_OK;
+    for (size_t i = 0; i < o->n; ++i) {   /* inbox order: (dst, t, src, seq, clone first) */
+      const tgsim_record* r = &o->v[i];
+      uint32_t p = r->seq / c->fl_D, l = r->dst - c->lo;
+      if (p >= c->fl_max_pubs) { rc = fail(c, TGSIM_EINVAL, "delivery %zu is not a flood message", i); break; }
+      if (fl_seen_get(c, p, l)) continue;
+      fl_seen_set(c, p, l);
+      fl_emit(c, l, p, r->src, r->t > c->horizon ? r->t : c->horizon, size, src, dst, seq, sz, ts, &k);
+    }
+    if (!rc) rc = fl_enqueue(c, cap, src, dst, seq, sz, ts, k);
+  }
+  free(src); free(dst); free(seq); free(sz); free(ts);
+  if (n_fwd) *n_fwd = rc ? 0 : k;
+  return rc;
 }

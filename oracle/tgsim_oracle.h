@@ -76,6 +76,12 @@ int tgo_gen_storm_round(tgo_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanou
                         int64_t spread_ns, uint32_t state);
 int tgo_storm_release(tgo_ctx* ctx, int64_t* out); /* host-side twin of tgsim_storm_release_device */
 
+/* Flood with first-receipt dedup over a fixed graph (tgsim.h). */
+int tgo_flood_set_graph(tgo_ctx* ctx, const uint32_t* offsets, const uint32_t* neighbors, uint32_t max_pubs);
+int tgo_flood_publish(tgo_ctx* ctx, const uint32_t* instances, const uint32_t* pubs, const int64_t* t, size_t n,
+                      uint32_t size);
+int tgo_flood_react(tgo_ctx* ctx, uint32_t size, size_t* n_forwarded);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,6 +113,9 @@ _SIGS = {
     "sync_poll": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_int64)]),
     "sync_count": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
+    "flood_set_graph": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "flood_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]),
+    "flood_react": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_size_t)]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {

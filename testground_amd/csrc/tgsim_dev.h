@@ -25,8 +25,24 @@ struct Prof {
   unsigned long long n[KID_COUNT] = {};
 };
 
+// Flood workload state (config 5, tgsim_flood_*): the local rows of the graph, first-receipt bits
+// [max_pubs][wpp] and per-item scratch of the reaction (count, first flag, exclusive offsets).
+struct Flood {
+  uint32_t* off = nullptr;        // [nloc+1] row offsets (local rows, rebased to 0)
+  uint32_t* nbr = nullptr;        // neighbours (global ids)
+  uint32_t* seen = nullptr;       // [max_pubs * wpp] bit (p, local instance)
+  uint32_t D = 0, max_pubs = 0, wpp = 0;
+  uint32_t* cnt = nullptr;        // [cap+1] forwards per item (0 unless first receipt)
+  uint32_t* pos = nullptr;        // [cap+1] exclusive prefix of cnt; pos[n] = total
+  uint8_t* first = nullptr;       // [cap] first receipt of (pub, receiver)
+  uint32_t* mark = nullptr;       // [mark_cap] (local, pub) pairs of a publish batch
+  void* scan_tmp = nullptr;
+  size_t scan_bytes = 0, cap = 0, mark_cap = 0;
+};
+
 struct Dev {
   Prof prof;
+  Flood fl;
   hipStream_t stream = nullptr;
   uint32_t N = 0, S = 1, shard = 0, lo = 0, nloc = 0;
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
@@ -138,5 +154,16 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 // n_waiters (state, target, t_wait) in the same launch and resolve it.
 hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, uint32_t st, uint32_t n_waiters,
                              bool add, uint32_t add_state, uint32_t add_target, int64_t add_twait);
+
+// Flood reaction over the last window's deliveries (n = n_out, inbox order): count pass (first
+// receipt of (pub, receiver) against the seen bits and the receiver's earlier deliveries), device
+// exclusive scan, then *total is read back (blocking) and the caller launches launch_flood_emit.
+hipError_t launch_flood_count(Dev& d, uint32_t n, uint32_t* total);
+// Forwards of every first receipt: seen bit set, messages staged at staged_base + pos[i] with
+// t_send = max(t_deliver, horizon), seq = pub * D + neighbour slot.
+hipError_t launch_flood_emit(Dev& d, uint32_t n, uint32_t staged_base, uint32_t size, int64_t horizon);
+// A publish batch: set the seen bits of (local, pub) pairs already in d.fl.mark.
+hipError_t launch_flood_mark(Dev& d, uint32_t n);
+size_t flood_scan_bytes(uint32_t n);
 
 }  // namespace tgsim

@@ -53,6 +53,8 @@ struct tgsim_ctx {
   uint32_t storm_nw = 0, add_state = 0, add_target = 0;
   int64_t add_twait = 0;
   std::vector<void*> allocs;
+  // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
+  std::vector<uint32_t> fl_off, fl_nbr;
 };
 
 // Commit a deferred storm batch before anything reads or reuses the sync state.
@@ -86,6 +88,13 @@ static int hipfail(tgsim_ctx* c, hipError_t e, const char* what) {
     hipError_t e__ = (x);                          \
     if (e__ != hipSuccess) return hipfail(c, e__, what); \
   } while (0)
+
+static void dfree(tgsim_ctx* c, void* p) {
+  if (!p) return;
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+  if (it != c->allocs.end()) c->allocs.erase(it);
+  (void)hipFree(p);
+}
 
 template <typename T>
 static int dalloc(tgsim_ctx* c, T** p, size_t n) {
@@ -943,5 +952,110 @@ extern "C" int tgsim_storm_release_device(tgsim_ctx* c, int64_t* out) {
   if (!c || !out) return TGSIM_EINVAL;
   if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
   HIPCK(c, hipMemcpyAsync(out, c->d.sig_red + 3, sizeof(int64_t), hipMemcpyDeviceToDevice, c->d.stream), "release");
+  return TGSIM_OK;
+}
+
+// ============================== flood workload (config 5) ===================================
+// publications flood a fixed graph with first-receipt dedup. The oracle
+// twin is oracle/tgsim_oracle.c tgo_flood_*; kernels in tgsim_flood.hip.
+
+extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
+  if (!c || !off || (off[c->N] && !nbr) || max_pubs == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  uint32_t D = 1;
+  for (uint32_t g = 0; g < c->N; ++g) {
+    if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
+    const uint32_t len = off[g + 1] - off[g];
+    if (len > 64) return fail(c, TGSIM_EINVAL, "degree %u > 64", len);
+    D = std::max(D, len);
+    for (uint32_t k = off[g]; k < off[g + 1]; ++k)
+      if (nbr[k] >= c->N || nbr[k] == g) return fail(c, TGSIM_EINVAL, "bad neighbour of %u", g);
+  }
+  if ((uint64_t)max_pubs * D > 0x100000000ull) return fail(c, TGSIM_EINVAL, "max_pubs * degree > 2^32");
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  Flood& f = c->d.fl;
+  dfree(c, f.off); dfree(c, f.nbr); dfree(c, f.seen);
+  f.off = f.nbr = f.seen = nullptr;
+  const uint32_t base = off[c->lo], m = off[c->hi] - base;
+  c->fl_off.resize(c->nloc + 1);
+  for (uint32_t l = 0; l <= c->nloc; ++l) c->fl_off[l] = off[c->lo + l] - base;
+  c->fl_nbr.assign(nbr + base, nbr + base + m);
+  f.D = D; f.max_pubs = max_pubs; f.wpp = (c->nloc + 31) / 32;
+  const size_t words = (size_t)max_pubs * f.wpp;
+  if (dalloc(c, &f.off, c->nloc + 1) || dalloc(c, &f.nbr, std::max<size_t>(m, 1)) || dalloc(c, &f.seen, words))
+    return TGSIM_ENOMEM;
+  HIPCK(c, hipMemcpy(f.off, c->fl_off.data(), (c->nloc + 1) * 4, hipMemcpyHostToDevice), "graph");
+  if (m) HIPCK(c, hipMemcpy(f.nbr, c->fl_nbr.data(), (size_t)m * 4, hipMemcpyHostToDevice), "graph");
+  HIPCK(c, hipMemset(f.seen, 0, words * 4), "graph");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
+                                   size_t n, uint32_t size) {
+  if (!c) return TGSIM_EINVAL;
+  Flood& f = c->d.fl;
+  if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (n && (!inst || !pubs || !t)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i)
+    if (inst[i] >= c->N || pubs[i] >= f.max_pubs) return fail(c, TGSIM_EINVAL, "bad publication %zu", i);
+  std::vector<uint32_t> src, dst, seq, sz, pairs;
+  std::vector<int64_t> ts;
+  for (size_t i = 0; i < n; ++i) {
+    if (!is_local(c, inst[i])) continue;
+    const uint32_t l = inst[i] - c->lo;
+    for (uint32_t k = c->fl_off[l]; k < c->fl_off[l + 1]; ++k) {
+      src.push_back(inst[i]); dst.push_back(c->fl_nbr[k]); seq.push_back(pubs[i] * f.D + (k - c->fl_off[l]));
+      sz.push_back(size); ts.push_back(t[i]);
+    }
+    pairs.push_back(l); pairs.push_back(pubs[i]);
+  }
+  tgsim_msg_soa m{src.data(), dst.data(), seq.data(), sz.data(), ts.data()};
+  int rc = tgsim_enqueue(c, &m, src.size());
+  if (rc) return rc;
+  const uint32_t np = (uint32_t)(pairs.size() / 2);
+  if (!np) return TGSIM_OK;
+  if (np > f.mark_cap) {
+    dfree(c, f.mark);
+    f.mark = nullptr;
+    if (dalloc(c, &f.mark, 2 * (size_t)np)) return TGSIM_ENOMEM;
+    f.mark_cap = np;
+  }
+  HIPCK(c, hipMemcpyAsync(f.mark, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, c->d.stream), "publish");
+  HIPCK(c, launch_flood_mark(c->d, np), "publish");
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "publish");  // pairs is a pageable host buffer
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
+  if (!c) return TGSIM_EINVAL;
+  if (n_fwd) *n_fwd = 0;
+  Flood& f = c->d.fl;
+  if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  const uint32_t n = c->d.h_sc->n_out;
+  if ((size_t)n + 1 > f.cap) {
+    dfree(c, f.cnt); dfree(c, f.pos); dfree(c, f.first); dfree(c, f.scan_tmp);
+    f.cnt = f.pos = nullptr; f.first = nullptr; f.scan_tmp = nullptr;
+    const size_t cap = std::max<size_t>((size_t)n + 1, 2 * f.cap);
+    f.scan_bytes = flood_scan_bytes((uint32_t)cap);
+    uint8_t* tmp = nullptr;
+    if (dalloc(c, &f.cnt, cap) || dalloc(c, &f.pos, cap) || dalloc(c, &f.first, cap) ||
+        dalloc(c, &tmp, f.scan_bytes))
+      return TGSIM_ENOMEM;
+    f.scan_tmp = tmp;
+    f.cap = cap;
+  }
+  uint32_t total = 0;
+  HIPCK(c, launch_flood_count(c->d, n, &total), "flood count");
+  HIPCK(c, sync_scalars(c->d), "sync");
+  rc = check_device_errors(c);
+  if (rc) return rc;
+  if ((uint64_t)c->n_staged + total > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  HIPCK(c, launch_flood_emit(c->d, n, c->n_staged, size, c->horizon), "flood emit");
+  c->n_staged += total;
+  if (n_fwd) *n_fwd = total;
   return TGSIM_OK;
 }

@@ -270,6 +270,25 @@ class Simulator:
         self._check(self.lib.gen_storm_round(self._ctx, round_, int(t0), fanout, size, int(spread_ns), state))
 
 
+    # ---- flood workload (config 5) -----------------------------------------------------------
+    def flood_set_graph(self, offsets, neighbors, max_pubs: int) -> None:
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        nbr = np.ascontiguousarray(neighbors, dtype=np.uint32)
+        assert len(off) == self.cfg.n_instances + 1
+        self._check(self.lib.flood_set_graph(self._ctx, _ptr(off), _ptr(nbr) if len(nbr) else None, max_pubs))
+
+    def flood_publish(self, instances, pubs, t, size: int) -> None:
+        inst = np.ascontiguousarray(instances, dtype=np.uint32)
+        p = np.ascontiguousarray(pubs, dtype=np.uint32)
+        tt = np.ascontiguousarray(np.broadcast_to(np.asarray(t, dtype=np.int64), inst.shape))
+        self._check(self.lib.flood_publish(self._ctx, _ptr(inst), _ptr(p), _ptr(tt), len(inst), size))
+
+    def flood_react(self, size: int) -> int:
+        n = C.c_size_t()
+        self._check(self.lib.flood_react(self._ctx, size, C.byref(n)))
+        return n.value
+
+
 def make_shape(latency_ns=0, jitter_ns=0, bandwidth_bps=0, loss=0.0, corrupt=0.0, reorder=0.0, duplicate=0.0,
                corrupt_corr=0.0, reorder_corr=0.0, duplicate_corr=0.0, filter=0) -> A.LinkShape:
     return A.LinkShape(int(latency_ns), int(jitter_ns), int(bandwidth_bps), loss, corrupt, corrupt_corr, reorder,

@@ -310,3 +310,43 @@ def memmove_exchange(sims):
     for q in range(S):
         for p in range(S):
             C.memmove(bufs[p][1] + q * blk, bufs[q][0] + p * blk, blk)
+
+
+# ---- config 5: flood with first-receipt dedup over a random-regular graph -----------------------
+
+def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4, window_ns=10 * MS, size=512,
+              seed=5, degree=8, shapes=None, keep=True, on_window=None, cfg_kw=None, max_windows=2000):
+    """Waves of publications flooding the graph; every window: advance, read the deliveries, then
+    tgsim_flood_react stages the first-receipt forwards for the next window. Returns per-window
+    observables (keep=True) and the totals."""
+    from testground_amd import workloads as W
+    kw = dict(max_msgs_per_window=1 << 20, max_records=1 << 22, data_prefix_len=12)
+    kw.update(cfg_kw or {})
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **kw), binding=binding)
+    sim.set_shapes(np.arange(n_inst), shapes if shapes is not None else W.pubsub_shapes(n_inst, seed))
+    off, nbr = W.random_regular_graph(n_inst, degree, seed)
+    sim.flood_set_graph(off, nbr, pubs_per_wave * waves)
+    out, tot = [], dict(delivered=0, forwarded=0, windows=0)
+    t, w, fwd = 0, 0, 0
+    while w < max_windows:
+        if w % wave_gap_windows == 0 and w // wave_gap_windows < waves:
+            wave = w // wave_gap_windows
+            pubs = W.publishers(n_inst, pubs_per_wave, wave, seed)
+            sim.flood_publish(pubs, np.arange(pubs_per_wave) + wave * pubs_per_wave, t, size)
+        elif fwd == 0 and sim.stats()["inflight"] == 0 and w // wave_gap_windows >= waves:
+            break
+        t += window_ns
+        sim.advance(t)
+        d = sim.deliveries()
+        fwd = sim.flood_react(size)
+        tot["delivered"] += len(d["dst"])
+        tot["forwarded"] += fwd
+        if on_window is not None:
+            on_window(w, d, fwd)
+        if keep:
+            out.append(dict(status=sim.status(), deliv=d, inbox=sim.inbox_offsets(), fwd=fwd))
+        w += 1
+    tot["windows"] = w
+    out.append(dict(stats=parity_stats(sim), tot=tot))
+    sim.close()
+    return out

@@ -1,0 +1,141 @@
+"""Flood workload (BASELINE.json configs[4]): publications flood a
+random-regular graph with first-receipt dedup (tgsim_flood_*). The oracle (tgo_flood_*) is checked
+by the flood's invariants on CPU; the HIP path must equal it bit for bit, up to the full 1M-instance
+size."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd import workloads as W
+from testground_amd.sim import SimConfig, Simulator, make_shape
+from tests import scenarios as S
+
+MS = 1_000_000
+
+
+def _lossless(n, lat_ms=(10, 50), jit_ms=5):
+    rng = np.random.default_rng(9)
+    return [make_shape(latency_ns=int(rng.choice(lat_ms)) * MS, jitter_ns=jit_ms * MS) for _ in range(n)]
+
+
+def _check_flood_invariants(run, n, degree=8, seed=5, pubs_per_wave=3, waves=2, full_coverage=True):
+    """Every (instance, pub) is first-received at most once; its forwards go to every neighbour but
+    the sender; with lossless links every publication reaches every instance."""
+    off, nbr = W.random_regular_graph(n, degree, seed)
+    deg = np.diff(off.astype(np.int64))
+    D = int(deg.max())
+    total_pubs = pubs_per_wave * waves
+    seen = np.zeros((total_pubs, n), bool)
+    for wave in range(waves):
+        seen[np.arange(pubs_per_wave) + wave * pubs_per_wave, W.publishers(n, pubs_per_wave, wave, seed)] = True
+    expect_fwd = 0
+    for win in run[:-1]:
+        assert win["fwd"] == _fwd_of_window(win["deliv"], seen, off, nbr, D), "forward count"
+        expect_fwd += win["fwd"]
+    assert run[-1]["tot"]["forwarded"] == expect_fwd
+    if full_coverage:
+        assert seen.all(), f"coverage {seen.sum(axis=1)} of {n}"
+    return seen
+
+
+def _fwd_of_window(d, seen, off, nbr, D):
+    fwd = 0
+    for dst, src, seq in zip(d["dst"].tolist(), d["src"].tolist(), d["seq"].tolist()):
+        p = seq // D
+        if seen[p, dst]:
+            continue
+        seen[p, dst] = True
+        row = nbr[off[dst]:off[dst + 1]]
+        fwd += int(np.count_nonzero(row != src))
+    return fwd
+
+
+def test_graph_is_simple_and_symmetric():
+    n = 2000
+    off, nbr = W.random_regular_graph(n, 8, 5)
+    src = np.repeat(np.arange(n), np.diff(off.astype(np.int64)))
+    assert not np.any(src == nbr)
+    e = set(zip(src.tolist(), nbr.tolist()))
+    assert len(e) == len(src) and all((b, a) in e for a, b in e)
+    assert np.count_nonzero(np.diff(off.astype(np.int64)) == 8) >= n - 60   # O(degree^2) defects
+
+
+def test_flood_oracle_invariants(oracle):
+    n = 1500
+    run = S.run_flood(oracle, n_inst=n, shapes=_lossless(n))
+    _check_flood_invariants(run, n)
+
+
+def test_flood_oracle_heterogeneous(oracle):
+    n = 2000
+    run = S.run_flood(oracle, n_inst=n)
+    seen = _check_flood_invariants(run, n, full_coverage=False)
+    assert seen.sum() >= 0.999 * seen.size
+
+
+def _errors(binding):
+    n = 16
+    sim = Simulator(SimConfig(n_instances=n, seed=1), binding=binding)
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_react(64)
+    assert e.value.code == A.ESTATE
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.uint32)
+    ring = np.stack([(np.arange(n) + 1) % n, (np.arange(n) - 1) % n], axis=1).reshape(-1)
+    bad = ring.copy()
+    bad[0] = 0                                             # self loop
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_set_graph(off, bad, 4)
+    assert e.value.code == A.EINVAL
+    sim.flood_set_graph(off, ring, 4)
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_publish([3], [4], 0, 64)                 # pub >= max_pubs
+    assert e.value.code == A.EINVAL
+    sim.enqueue([1], [2], [1000], [64], [0])               # not a flood message (1000 / 2 >= 4)
+    sim.advance(1)
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_react(64)
+    assert e.value.code == A.EINVAL
+    sim.close()
+
+
+def test_flood_errors_oracle(oracle):
+    _errors(oracle)
+
+
+@pytest.mark.gpu
+def test_flood_errors_hip(hip):
+    _errors(hip)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,kind", [(3000, "pubsub"), (1500, "lossless"), (600, "zero-delay")])
+def test_flood_hip_matches_oracle(hip, oracle, n, kind):
+    """zero-delay: latency 0-2 ms with jitter and duplication, so forwards land inside their own
+    window and inbox runs carry repeats of one publication."""
+    if kind == "pubsub":
+        shapes = None
+    elif kind == "lossless":
+        shapes = _lossless(n)
+    else:
+        rng = np.random.default_rng(4)
+        shapes = [make_shape(latency_ns=int(rng.integers(0, 3)) * MS, jitter_ns=2 * MS, duplicate=20.0)
+                  for _ in range(n)]
+    a = S.run_flood(hip, n_inst=n, shapes=shapes)
+    b = S.run_flood(oracle, n_inst=n, shapes=shapes)
+    S.assert_same(a, b)
+    _check_flood_invariants(a, n, full_coverage=kind == "lossless")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_flood_full_size(hip, oracle):
+    """config 5 at full size: 1M instances, 8-regular, heterogeneous shapes; two publications, the
+    whole flood (~1.4e7 messages) replayed by the oracle bit for bit."""
+    n = 1_000_000
+    shapes = W.pubsub_shapes(n)
+    kw = dict(max_msgs_per_window=1 << 23, max_records=1 << 24)
+    a = S.run_flood(hip, n_inst=n, pubs_per_wave=2, waves=1, shapes=shapes, cfg_kw=kw)
+    print(f"  hip: {a[-1]['tot']}", flush=True)
+    b = S.run_flood(oracle, n_inst=n, pubs_per_wave=2, waves=1, shapes=shapes, cfg_kw=kw)
+    S.assert_same(a, b)
+    assert a[-1]["tot"]["forwarded"] > 0.99 * 2 * 7 * n
