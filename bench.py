@@ -44,6 +44,10 @@ BYTE_MODELS = {
     "k_extract": lambda d: 64 * d["extracted"],
     "k_region_fill": lambda d: 72 * d["inserted"],
     "k_gen_storm": lambda d: 24 * d["msgs_in"],
+    # flood (config 5): count reads (dst, src, seq) and writes count + first flag per delivery;
+    # emit writes the 24 B staged message per forward after re-reading the 17 B per delivery
+    "k_flood_count": lambda d: 21 * d["delivered"],
+    "k_flood_emit": lambda d: 24 * d["msgs_in"] + 17 * d["delivered"],
 }
 
 
@@ -61,7 +65,18 @@ def parse():
     p.add_argument("--max-records", type=int, default=1 << 23)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    return p.parse_args()
+    # config 5 (not the headline): 1M-instance random-regular pubsub flood, one window per step
+    p.add_argument("--workload", choices=("storm", "flood"), default="storm")
+    p.add_argument("--flood-instances", type=int, default=1_000_000)
+    p.add_argument("--flood-size", type=int, default=512)
+    p.add_argument("--pub-every", type=int, default=4, help="windows between publications (flood)")
+    p.add_argument("--window-ms", type=float, default=10.0, help="window length (flood)")
+    a = p.parse_args()
+    if a.workload == "flood":
+        # the flood reaches steady state after a publication's lifetime (~80 windows)
+        a.warmup = a.warmup if "--warmup" in sys.argv else 100
+        a.steps = a.steps if "--steps" in sys.argv else 50
+    return a
 
 
 def storm_shapes(n: int, seed: int):
@@ -121,6 +136,8 @@ PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
 
 def main():
     args = parse()
+    if args.workload == "flood":
+        return main_flood(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -289,6 +306,186 @@ def main():
             "kernels_probe": warm_kernels,
         }
         print(json.dumps(line), flush=True)
+    sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+
+def _dist_setup(args):
+    """One process per GPU; more ranks than GPUs = a gloo rehearsal on shared devices (see main)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    rehearsal = world > ndev
+    local = local % max(ndev, 1)
+    torch.cuda.set_device(local)
+    if world > 1:
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    return torch, dist, world, rank, local, rehearsal, stream
+
+
+def flood_cpu_baseline(args, shapes, graph):
+    """The CPU oracle on the same flood from its first window, for a bounded sample (about
+    args.cpu_seconds): the per-message cost does not depend on the flood's phase."""
+    from oracle.pyoracle import oracle_binding
+    from testground_amd import workloads as W
+    from testground_amd.sim import Simulator
+    N = args.flood_instances
+    sim = Simulator(flood_config(args), binding=oracle_binding())
+    sim.set_shapes(np.arange(N), shapes)
+    sim.flood_set_graph(*graph, flood_max_pubs(args))
+    win = int(args.window_ms * MS)
+    t0 = time.perf_counter()
+    w = 0
+    while True:
+        if w % args.pub_every == 0:
+            sim.flood_publish(W.publishers(N, 1, w // args.pub_every, args.seed), [w // args.pub_every], sim.now,
+                              args.flood_size)
+        sim.advance(sim.now + win)
+        sim.flood_react(args.flood_size)
+        w += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or w >= 400:
+            break
+    delivered = sim.stats()["delivered"]
+    sim.close()
+    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ (single-threaded C restatement), same {N}-instance flood: windows 0..{w - 1} "
+                      f"from the first publication ({el:.1f} s, {delivered} deliveries, incl. the reaction)"}
+
+
+def flood_config(args, shard=0, n_shards=1, device=0):
+    from testground_amd.sim import SimConfig
+    return SimConfig(n_instances=args.flood_instances, seed=args.seed, shard_id=shard, n_shards=n_shards,
+                     device=device, data_prefix_len=11, max_msgs_per_window=1 << 23, max_records=1 << 25,
+                     exchange_cap=max(1 << 17, (1 << 23) // max(n_shards, 1)))
+
+
+def flood_max_pubs(args) -> int:
+    return (args.warmup + args.steps + 20) // args.pub_every + 2
+
+
+def main_flood(args):
+    """Config 5 (BASELINE.json configs[4]): 1M instances on a random 8-regular graph
+    with heterogeneous LinkShapes; one publication every `pub_every` windows floods the graph with
+    first-receipt dedup (tgsim_flood_react after every window). A step is one window; `value` =
+    deliveries of all ranks in the K timed windows / the max-over-ranks wall time."""
+    torch, dist, world, rank, local, rehearsal, stream = _dist_setup(args)
+    from testground_amd import workloads as W
+    from testground_amd.sim import Simulator
+    args.seed = 5 if "--seed" not in sys.argv else args.seed
+    N = args.flood_instances
+    shapes = W.pubsub_shapes(N, args.seed)
+    graph = W.random_regular_graph(N, 8, args.seed)
+    sim = Simulator(flood_config(args, rank, world, local))
+    sim.set_stream(stream.cuda_stream)
+    sim.set_shapes(np.arange(sim.lo, sim.hi), shapes[sim.lo:sim.hi])
+    sim.flood_set_graph(*graph, flood_max_pubs(args))
+    win = int(args.window_ms * MS)
+    if world > 1:
+        from testground_amd.exchange import exchange
+        _, _, nbytes = sim.exchange_buffers()
+        xcap = nbytes // (world * 32)
+        send_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        recv_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        sim.set_exchange_buffers(send_t.data_ptr(), recv_t.data_ptr(), nbytes)
+        if rehearsal:
+            send_h, recv_h = torch.empty_like(send_t, device="cpu"), torch.zeros_like(recv_t, device="cpu")
+
+    def step(w: int):
+        if w % args.pub_every == 0:
+            k = w // args.pub_every
+            sim.flood_publish(W.publishers(N, 1, k, args.seed), [k], sim.now, args.flood_size)
+        t_end = sim.now + win
+        if world == 1:
+            sim.advance(t_end)
+        else:
+            sim.advance_begin(t_end)
+            if rehearsal:
+                send_h.copy_(send_t)
+                exchange(send_h, recv_h, xcap, dist)
+                recv_t.copy_(recv_h)
+            else:
+                exchange(send_t, recv_t, xcap, dist)
+            sim.advance_end()
+        sim.flood_react(args.flood_size)
+
+    for w in range(args.warmup):
+        step(w)
+    probe = 5
+    sim.profile(None)
+    base_all = sim.profile_read()
+    for w in range(args.warmup, args.warmup + probe):
+        step(w)
+    prof = sim.profile_read()
+    warm_kernels = {k: {"avg_us": 1e3 * (ms - base_all[k][0]) / (n - base_all[k][1]), "launches": n - base_all[k][1]}
+                    for k, (ms, n) in prof.items() if n > base_all[k][1]}
+    ranked = sorted(((v["avg_us"] * v["launches"], k) for k, v in warm_kernels.items() if k in BYTE_MODELS),
+                    reverse=True)
+    dominant = ranked[0][1] if ranked else "k_emit_bucket"
+    sim.profile([dominant])
+    base_prof = sim.profile_read()[dominant]
+    first = args.warmup + probe
+    s0 = sim.stats()
+    if world > 1:
+        dist.barrier()
+    sim.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for w in range(first, first + args.steps):
+        step(w)
+    sim.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    s1 = sim.stats()
+    prof = sim.profile_read()[dominant]
+    delta = {k: s1[k] - s0[k] for k in s1}
+    kern_ms, kern_n = prof[0] - base_prof[0], prof[1] - base_prof[1]
+    delivered = delta["delivered"]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        v = torch.tensor([delivered], dtype=torch.int64)
+        if not rehearsal:
+            t, v = t.cuda(), v.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        elapsed, delivered = float(t.item()), int(v.item())
+    bytes_total = BYTE_MODELS[dominant](delta)
+    avg_ms = kern_ms / max(kern_n, 1)
+    achieved = (bytes_total / max(kern_n, 1)) / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = flood_cpu_baseline(args, shapes, graph)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "simulated msgs delivered/sec (1M-inst random-regular pubsub flood) + % HBM roofline",
+            "value": delivered / elapsed, "unit": "msgs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "pubsub flood (SURVEY.md 8(d) config 5): 1M instances, random 8-regular graph, "
+                                   "first-receipt dedup, latency {10,50,100,200} ms, jitter U[0,20] ms, loss "
+                                   "{0,0.1,1}%, bandwidth {1,10,100} Mbit/s; one publication every "
+                                   f"{args.pub_every} windows of {args.window_ms} ms",
+                       "instances": N, "msg_bytes": args.flood_size,
+                       "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
+                       "delivered_in_timed_steps": delivered},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "avg_launch_ms": avg_ms, "bytes_per_launch": bytes_total / max(kern_n, 1)},
+            "cpu_baseline": cpu,
+            "kernels_probe": warm_kernels,
+        }), flush=True)
     sim.close()
     if world > 1:
         dist.destroy_process_group()

@@ -12,7 +12,7 @@ namespace tgsim {
 enum KernelId : int {
   KID_SHAPE = 0, KID_EXTRACT, KID_TB, KID_EMIT, KID_RADIX_HIST, KID_RADIX_ROWS, KID_RADIX_SCATTER,
   KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_BKT_HIST, KID_BKT_SCATTER,
-  KID_BKT_SORT, KID_SEG_REST, KID_COUNT
+  KID_BKT_SORT, KID_SEG_REST, KID_FLOOD_COUNT, KID_FLOOD_EMIT, KID_COUNT
 };
 extern const char* const kKernelNames[KID_COUNT];
 
@@ -122,6 +122,35 @@ struct Dev {
   int64_t* sig_part = nullptr;    // [2 * 4096] per-block (min, max) of a signal batch
   int64_t* sig_red = nullptr;     // [4] count-only batch: last tmin, running tmin, running tmax, last tmax
   unsigned long long* stats = nullptr;  // [kNSub][16] sharded k_shape counters (ST_MSGS..ST_LOCAL)
+};
+
+// Times the launches issued while it is alive with a HIP event pair on d.stream (if enabled).
+struct ProfScope {
+  Dev& d;
+  int kid;
+  hipEvent_t a = nullptr;
+  hipStream_t st;
+  ProfScope(Dev& dd, int k, hipStream_t s = nullptr) : d(dd), kid(k), st(s ? s : dd.stream) {
+    if (!(d.prof.mask & (1u << kid))) return;
+    a = take();
+    (void)hipEventRecord(a, st);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = take();
+    (void)hipEventRecord(b, st);
+    d.prof.pending.push_back({kid, a, b});
+  }
+  hipEvent_t take() {
+    if (!d.prof.pool.empty()) {
+      hipEvent_t e = d.prof.pool.back();
+      d.prof.pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+    return e;
+  }
 };
 
 // Every function returns hipSuccess or the first HIP error; device-side capacity/ordering problems

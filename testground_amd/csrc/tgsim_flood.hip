@@ -80,8 +80,11 @@ inline unsigned blocks(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 
 hipError_t launch_flood_count(Dev& d, uint32_t n, uint32_t* total) {
   Flood& f = d.fl;
-  hipLaunchKernelGGL(k_flood_count, dim3(blocks((uint64_t)n + 1)), dim3(kBlock), 0, d.stream, d.o_dst, d.o_src,
-                     d.o_seq, d.inbox, n, d.lo, f, d.sc);
+  {
+    ProfScope ps_(d, KID_FLOOD_COUNT);
+    hipLaunchKernelGGL(k_flood_count, dim3(blocks((uint64_t)n + 1)), dim3(kBlock), 0, d.stream, d.o_dst, d.o_src,
+                       d.o_seq, d.inbox, n, d.lo, f, d.sc);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t bytes = f.scan_bytes;
@@ -94,6 +97,7 @@ hipError_t launch_flood_count(Dev& d, uint32_t n, uint32_t* total) {
 
 hipError_t launch_flood_emit(Dev& d, uint32_t n, uint32_t staged_base, uint32_t size, int64_t horizon) {
   if (!n) return hipSuccess;
+  ProfScope ps_(d, KID_FLOOD_EMIT);
   hipLaunchKernelGGL(k_flood_emit, dim3(blocks(n)), dim3(kBlock), 0, d.stream, d.o_dst, d.o_src, d.o_seq, d.o_t, n,
                      d.lo, d.fl, staged_base, size, horizon, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();

@@ -21,36 +21,7 @@ namespace tgsim {
 const char* const kKernelNames[KID_COUNT] = {
     "k_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_region_fill", "k_gen_storm", "sync_signal", "large_segments",
-    "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest"};
-
-// Times the launches issued while it is alive with a HIP event pair on d.stream (if enabled).
-struct ProfScope {
-  Dev& d;
-  int kid;
-  hipEvent_t a = nullptr;
-  hipStream_t st;
-  ProfScope(Dev& dd, int k, hipStream_t s = nullptr) : d(dd), kid(k), st(s ? s : dd.stream) {
-    if (!(d.prof.mask & (1u << kid))) return;
-    a = take();
-    (void)hipEventRecord(a, st);
-  }
-  ~ProfScope() {
-    if (!a) return;
-    hipEvent_t b = take();
-    (void)hipEventRecord(b, st);
-    d.prof.pending.push_back({kid, a, b});
-  }
-  hipEvent_t take() {
-    if (!d.prof.pool.empty()) {
-      hipEvent_t e = d.prof.pool.back();
-      d.prof.pool.pop_back();
-      return e;
-    }
-    hipEvent_t e;
-    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
-    return e;
-  }
-};
+    "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
