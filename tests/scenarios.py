@@ -350,3 +350,53 @@ def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4
     out.append(dict(stats=parity_stats(sim), tot=tot))
     sim.close()
     return out
+
+
+def run_flood_sharded(make_sim, exchange, world: int, n_inst=900, pubs_per_wave=3, waves=2, wave_gap_windows=4,
+                      window_ns=10 * MS, size=512, seed=5, degree=8, shapes=None, max_windows=2000):
+    """run_flood over `world` shards of one process (every shard gets the same configuration calls;
+    the owner keeps state). Each window: advance_begin on every shard, exchange, advance_end, react.
+    Returns per window the shards' deliveries concatenated in shard order (= the single run's global
+    inbox order, shards owning contiguous receivers) and the summed forward count, plus the summed
+    statistics."""
+    from testground_amd import workloads as W
+    sims = [make_sim(SimConfig(n_instances=n_inst, seed=seed, shard_id=k, n_shards=world, exchange_cap=1 << 15,
+                               max_msgs_per_window=1 << 20, max_records=1 << 22, data_prefix_len=12))
+            for k in range(world)]
+    shapes = shapes if shapes is not None else W.pubsub_shapes(n_inst, seed)
+    off, nbr = W.random_regular_graph(n_inst, degree, seed)
+    for s in sims:
+        s.set_shapes(np.arange(n_inst), shapes)
+        s.flood_set_graph(off, nbr, pubs_per_wave * waves)
+    out = []
+    t, w, fwd = 0, 0, 0
+    while w < max_windows:
+        if w % wave_gap_windows == 0 and w // wave_gap_windows < waves:
+            wave = w // wave_gap_windows
+            pubs = W.publishers(n_inst, pubs_per_wave, wave, seed)
+            for s in sims:
+                s.flood_publish(pubs, np.arange(pubs_per_wave) + wave * pubs_per_wave, t, size)
+        elif fwd == 0 and sum(s.stats()["inflight"] for s in sims) == 0 and w // wave_gap_windows >= waves:
+            break
+        t += window_ns
+        for s in sims:
+            s.advance_begin(t)
+        exchange(sims)
+        for s in sims:
+            s.advance_end()
+        ds = [s.deliveries() for s in sims]
+        fwd = sum(s.flood_react(size) for s in sims)
+        out.append(dict(deliv={k: np.concatenate([d[k] for d in ds]) for k in ds[0]}, fwd=fwd))
+        w += 1
+    tot = {}
+    for s in sims:
+        for name, v in parity_stats(s).items():
+            tot[name] = tot.get(name, 0) + v
+        s.close()
+    out.append(dict(stats=tot))
+    return out
+
+
+def flood_single_view(single):
+    """run_flood output in run_flood_sharded's structure."""
+    return [dict(deliv=x["deliv"], fwd=x["fwd"]) for x in single[:-1]] + [dict(stats=single[-1]["stats"])]

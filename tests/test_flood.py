@@ -139,3 +139,34 @@ def test_flood_full_size(hip, oracle):
     b = S.run_flood(oracle, n_inst=n, pubs_per_wave=2, waves=1, shapes=shapes, cfg_kw=kw)
     S.assert_same(a, b)
     assert a[-1]["tot"]["forwarded"] > 0.99 * 2 * 7 * n
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_flood_sharded_oracle(oracle, world):
+    """Sharded flood (oracle shards exchanging through memmove) == the single-shard flood."""
+    n = 900
+    got = S.run_flood_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, n_inst=n)
+    S.assert_same(got, S.flood_single_view(S.run_flood(oracle, n_inst=n)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_flood_sharded_hip(hip, oracle, world):
+    """The same with HIP contexts on one device; the exchange is device-to-device copies between
+    their buffers (bench.py moves the same blocks between GPUs over RCCL)."""
+    import ctypes as C
+    hiprt = C.CDLL("libamdhip64.so")
+    hiprt.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+
+    def exchange(sims):
+        bufs = [s.exchange_buffers() for s in sims]
+        blk = bufs[0][2] // len(sims)
+        for s in sims:
+            s.sync()
+        for q in range(len(sims)):
+            for p in range(len(sims)):
+                assert hiprt.hipMemcpy(bufs[p][1] + q * blk, bufs[q][0] + p * blk, blk, 3) == 0
+
+    n = 900
+    got = S.run_flood_sharded(lambda c: Simulator(c), exchange, world, n_inst=n)
+    S.assert_same(got, S.flood_single_view(S.run_flood(oracle, n_inst=n)))
