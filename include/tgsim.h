@@ -256,6 +256,22 @@ int tgsim_sync_barrier(tgsim_ctx* ctx, uint32_t state, uint32_t target, int64_t 
 /* release_out = release time, or -1 while pending. */
 int tgsim_sync_poll(tgsim_ctx* ctx, uint32_t waiter, int64_t* release_out);
 int tgsim_sync_count(tgsim_ctx* ctx, uint32_t state, uint32_t* count_out);
+/* sync.Client Publish / Subscribe [EXT sdk-go; call sites plans/network/pingpong.go:219-245,
+ * plans/benchmarks/storm.go:232-255, plans/splitbrain/main.go:91-103]: ordered topics with full
+ * history replay, kept in device memory. A topic is a sync state id (shared id space): publishing
+ * counts like SignalEntry, so an entry's 1-based position follows (t, instance) order inside a
+ * batch and batches of one topic must not go back in time (ECAUSALITY). Entry i of a batch is
+ * (topics[i], instances[i], t[i], payload[payload_off[i] .. payload_off[i+1])); payload_off has
+ * n+1 entries starting at 0. pos_out (optional) receives the positions. */
+int tgsim_sync_publish(tgsim_ctx* ctx, const uint32_t* topics, const uint32_t* instances, const int64_t* t,
+                       const uint64_t* payload_off, const uint8_t* payload, size_t n, uint32_t* pos_out);
+/* The entries of `topic` from position `from` (1-based) on whose time is <= until_t, in position
+ * order, at most `cap` of them: instances, times, payload offsets (n_out + 1 prefix offsets into
+ * payload_out) and bytes. *n_out / *payload_bytes: entries and bytes returned — or, with
+ * ECAPACITY when the bytes exceed payload_cap, the sizes needed. */
+int tgsim_sync_subscribe(tgsim_ctx* ctx, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                         uint32_t* instances_out, int64_t* t_out, uint64_t* payload_off_out,
+                         uint8_t* payload_out, size_t payload_cap, size_t* n_out, size_t* payload_bytes);
 
 /* ---- profiling: HIP-event timing of kernel classes on the ctx stream ---------------------------- */
 /* mask: bit k enables timing of kernel class k (0..tgsim_kernel_classes()-1); 0 disables. */

@@ -169,6 +169,8 @@ typedef struct { tgsim_record* v; size_t n, cap; } orecs;
 typedef struct { int64_t* t; size_t n, cap; } otimes;
 typedef struct { uint32_t state, target; int64_t t_wait; } owaiter;
 
+typedef struct otopic { uint32_t* inst; int64_t* t; uint64_t* off; uint32_t* len; size_t n, cap; } otopic;
+
 struct tgo_ctx {
   tgsim_config cfg;
   uint32_t N, lo, hi, nloc, S;
@@ -198,6 +200,9 @@ struct tgo_ctx {
   size_t n_states;
   owaiter* waiters; size_t n_waiters, waiters_cap;
   int64_t storm_release;
+  /* topics: per state id, entries in position order; payload bytes in one buffer */
+  struct otopic* topics; size_t n_topics;
+  uint8_t* tp_bytes; size_t tp_nbytes, tp_cap;
   /* flood (config 5): local rows of the graph, first-receipt bits [max_pubs][nloc] */
   uint32_t* fl_off; uint32_t* fl_nbr; uint32_t* fl_seen;
   uint32_t fl_D, fl_max_pubs, fl_wpp;
@@ -311,6 +316,10 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
+  for (size_t i = 0; i < c->n_topics; ++i) {
+    free(c->topics[i].inst); free(c->topics[i].t); free(c->topics[i].off); free(c->topics[i].len);
+  }
+  free(c->topics); free(c->tp_bytes);
   if (c->rules) for (uint32_t i = 0; i < c->nloc; ++i) free(c->rules[i].v);
   if (c->outbox) for (uint32_t i = 0; i < c->S; ++i) free(c->outbox[i].v);
   if (c->sig) for (size_t i = 0; i < c->n_states; ++i) free(c->sig[i].t);
@@ -991,4 +1000,79 @@ int tgo_flood_react(tgo_ctx* c, uint32_t size, size_t* n_fwd) {
   free(src); free(dst); free(seq); free(sz); free(ts);
   if (n_fwd) *n_fwd = rc ? 0 : k;
   return rc;
+}
+
+/* ============================== topics (sync.Client Publish / Subscribe) ===================
+ * [EXT sdk-go]; call sites plans/network/pingpong.go:219-245, plans/benchmarks/storm.go:232-255,
+ * plans/splitbrain/main.go:91-103. A topic is a sync state: tgo_sync_signal assigns the positions
+ * ((t, instance) order inside the batch), then each entry is stored at its position. */
+
+static int topic_put(tgo_ctx* c, uint32_t topic, uint32_t pos, uint32_t inst, int64_t t, uint64_t off, uint32_t len) {
+  if (topic >= c->n_topics) {
+    size_t nn = topic + 1;
+    otopic* q = (otopic*)realloc(c->topics, nn * sizeof(otopic));
+    if (!q) return TGSIM_ENOMEM;
+    memset(q + c->n_topics, 0, (nn - c->n_topics) * sizeof(otopic));
+    c->topics = q; c->n_topics = nn;
+  }
+  otopic* tp = &c->topics[topic];
+  size_t need = pos;  /* 1-based */
+  if (need > tp->cap) {
+    size_t nc = tp->cap ? tp->cap : 16;
+    while (nc < need) nc *= 2;
+    uint32_t* a = realloc(tp->inst, nc * 4); if (!a) return TGSIM_ENOMEM; tp->inst = a;
+    int64_t* b = realloc(tp->t, nc * 8); if (!b) return TGSIM_ENOMEM; tp->t = b;
+    uint64_t* o = realloc(tp->off, nc * 8); if (!o) return TGSIM_ENOMEM; tp->off = o;
+    uint32_t* l = realloc(tp->len, nc * 4); if (!l) return TGSIM_ENOMEM; tp->len = l;
+    tp->cap = nc;
+  }
+  tp->inst[pos - 1] = inst; tp->t[pos - 1] = t; tp->off[pos - 1] = off; tp->len[pos - 1] = len;
+  if (pos > tp->n) tp->n = pos;
+  return TGSIM_OK;
+}
+
+int tgo_sync_publish(tgo_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
+                     const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out) {
+  if (n && (!topics || !inst || !t || !off || (off[n] && !payload))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (n && off[0] != 0) return fail(c, TGSIM_EINVAL, "payload offsets must start at 0");
+  for (size_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFu) return fail(c, TGSIM_EINVAL, "bad payload offsets");
+  if (n == 0) return TGSIM_OK;
+  uint32_t* pos = (uint32_t*)malloc(n * 4);
+  if (!pos) return TGSIM_ENOMEM;
+  int rc = tgo_sync_signal(c, topics, inst, t, n, pos);
+  if (!rc && grow((void**)&c->tp_bytes, &c->tp_cap, c->tp_nbytes + off[n] + 1, 1)) rc = TGSIM_ENOMEM;
+  if (!rc) {
+    if (off[n]) memcpy(c->tp_bytes + c->tp_nbytes, payload, off[n]);
+    for (size_t i = 0; i < n && !rc; ++i)
+      rc = topic_put(c, topics[i], pos[i], inst[i], t[i], c->tp_nbytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+    c->tp_nbytes += off[n];
+  }
+  if (!rc && pos_out) memcpy(pos_out, pos, n * 4);
+  free(pos);
+  return rc;
+}
+
+int tgo_sync_subscribe(tgo_ctx* c, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                       uint32_t* inst_out, int64_t* t_out, uint64_t* off_out, uint8_t* payload_out,
+                       size_t payload_cap, size_t* n_out, size_t* payload_bytes) {
+  if (!n_out || !payload_bytes || from == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
+  *n_out = 0; *payload_bytes = 0;
+  if (topic >= c->cfg.max_states) return fail(c, TGSIM_EINVAL, "bad topic");
+  if (topic >= c->n_topics) return TGSIM_OK;
+  const otopic* tp = &c->topics[topic];
+  size_t k = 0, bytes = 0;
+  for (size_t p = from - 1; p < tp->n && k < cap && tp->t[p] <= until_t; ++p, ++k) bytes += tp->len[p];
+  *n_out = k; *payload_bytes = bytes;
+  if (bytes > payload_cap) return fail(c, TGSIM_ECAPACITY, "payload capacity %zu < %zu", payload_cap, bytes);
+  if (k && (!inst_out || !t_out || !off_out || (bytes && !payload_out))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  size_t b = 0;
+  for (size_t j = 0; j < k; ++j) {
+    size_t p = from - 1 + j;
+    inst_out[j] = tp->inst[p]; t_out[j] = tp->t[p]; off_out[j] = b;
+    if (tp->len[p]) memcpy(payload_out + b, c->tp_bytes + tp->off[p], tp->len[p]);
+    b += tp->len[p];
+  }
+  if (off_out) off_out[k] = b;
+  return TGSIM_OK;
 }

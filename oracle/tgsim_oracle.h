@@ -70,6 +70,11 @@ int tgo_sync_signal(tgo_ctx* ctx, const uint32_t* states, const uint32_t* instan
 int tgo_sync_barrier(tgo_ctx* ctx, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* waiter_out);
 int tgo_sync_poll(tgo_ctx* ctx, uint32_t waiter, int64_t* release_out);
 int tgo_sync_count(tgo_ctx* ctx, uint32_t state, uint32_t* count_out);
+int tgo_sync_publish(tgo_ctx* ctx, const uint32_t* topics, const uint32_t* instances, const int64_t* t,
+                     const uint64_t* payload_off, const uint8_t* payload, size_t n, uint32_t* pos_out);
+int tgo_sync_subscribe(tgo_ctx* ctx, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                       uint32_t* instances_out, int64_t* t_out, uint64_t* payload_off_out,
+                       uint8_t* payload_out, size_t payload_cap, size_t* n_out, size_t* payload_bytes);
 int tgo_advance_to_barrier(tgo_ctx* ctx, uint32_t waiter, int64_t offset_ns);
 
 int tgo_gen_storm_round(tgo_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,

@@ -113,6 +113,11 @@ _SIGS = {
     "sync_poll": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_int64)]),
     "sync_count": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
+    "sync_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                C.c_void_p]),
+    "sync_subscribe": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_int64, C.c_size_t, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                  C.POINTER(C.c_size_t)]),
     "flood_set_graph": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_uint32]),
     "flood_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]),
     "flood_react": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_size_t)]),

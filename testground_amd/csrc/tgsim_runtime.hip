@@ -53,6 +53,19 @@ struct tgsim_ctx {
   uint32_t storm_nw = 0, add_state = 0, add_target = 0;
   int64_t add_twait = 0;
   std::vector<void*> allocs;
+  // topics (tgsim_sync_publish / _subscribe): entries live in device arenas, sorted by (topic,
+  // position) per batch; the host keeps each topic's runs of consecutive positions
+  // latest time of the host-submitted signals per state: a batch that goes back in time is
+  // refused before anything changes (the device check stays for device-generated storm batches)
+  std::vector<int64_t> st_last_h;
+  struct TopicRun { uint32_t pos0, len; uint64_t entry; };
+  std::vector<std::vector<TopicRun>> topic_runs;
+  uint32_t* tp_inst = nullptr;
+  int64_t* tp_t = nullptr;
+  uint64_t* tp_off = nullptr;
+  uint32_t* tp_len = nullptr;
+  uint8_t* tp_bytes = nullptr;
+  uint64_t tp_n = 0, tp_cap = 0, tp_nbytes = 0, tp_bytes_cap = 0;
   // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
   std::vector<uint32_t> fl_off, fl_nbr;
 };
@@ -855,10 +868,13 @@ extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uin
   if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
   if (n > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch larger than %u", c->d.s_cap);
   if (c->sig_log_used + n > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
+  if (c->st_last_h.size() < c->d.max_states) c->st_last_h.resize(c->d.max_states, INT64_MIN);
   for (size_t i = 0; i < n; ++i) {
     if (states[i] >= c->d.max_states) return fail(c, TGSIM_EINVAL, "state id %u >= max_states", states[i]);
     if (t[i] < 0) return fail(c, TGSIM_ECAUSALITY, "negative signal time");
+    if (t[i] < c->st_last_h[states[i]]) return fail(c, TGSIM_ECAUSALITY, "signal %zu goes back in time", i);
   }
+  for (size_t i = 0; i < n; ++i) c->st_last_h[states[i]] = std::max(c->st_last_h[states[i]], t[i]);
   Dev& d = c->d;
   HIPCK(c, flush_storm(c), "storm commit");
   uint32_t kmin = UINT32_MAX, kmax = 0;
@@ -1057,5 +1073,134 @@ extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   HIPCK(c, launch_flood_emit(c->d, n, c->n_staged, size, c->horizon), "flood emit");
   c->n_staged += total;
   if (n_fwd) *n_fwd = total;
+  return TGSIM_OK;
+}
+
+// ============================== topics (sync.Client Publish / Subscribe) ===================
+// [EXT sdk-go]; call sites plans/network/pingpong.go:219-245, plans/benchmarks/storm.go:232-255,
+// plans/splitbrain/main.go:91-103. Positions come from the device signal path (a topic is a sync
+// state); the entries and payload bytes are appended to device arenas in (topic, position) order,
+// so a subscription is a few contiguous copies. Oracle twin: tgo_sync_publish / _subscribe.
+
+template <typename T>
+static int dgrow(tgsim_ctx* c, T** p, uint64_t used, uint64_t need_cap) {
+  T* q = nullptr;
+  if (dalloc(c, &q, need_cap)) return TGSIM_ENOMEM;
+  if (used && *p) HIPCK(c, hipMemcpy(q, *p, used * sizeof(T), hipMemcpyDeviceToDevice), "topic grow");
+  dfree(c, *p);
+  *p = q;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
+                                  const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out) {
+  if (!c) return TGSIM_EINVAL;
+  if (n && (!topics || !inst || !t || !off || (off[n] && !payload))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (n && off[0] != 0) return fail(c, TGSIM_EINVAL, "payload offsets must start at 0");
+  for (size_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) return fail(c, TGSIM_EINVAL, "bad payload offsets");
+  if (n == 0) return TGSIM_OK;
+  std::vector<uint32_t> pos(n);
+  int rc = tgsim_sync_signal(c, topics, inst, t, n, pos.data());
+  if (rc) return rc;
+  std::vector<uint32_t> ord(n);
+  for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+    return topics[a] != topics[b] ? topics[a] < topics[b] : pos[a] < pos[b];
+  });
+  const uint64_t bytes = off[n];
+  if (c->tp_n + n > c->tp_cap) {
+    const uint64_t cap = std::max<uint64_t>(c->tp_n + n, 2 * c->tp_cap);
+    if (dgrow(c, &c->tp_inst, c->tp_n, cap) || dgrow(c, &c->tp_t, c->tp_n, cap) ||
+        dgrow(c, &c->tp_off, c->tp_n, cap) || dgrow(c, &c->tp_len, c->tp_n, cap))
+      return TGSIM_ENOMEM;
+    c->tp_cap = cap;
+  }
+  if (c->tp_nbytes + bytes > c->tp_bytes_cap) {
+    const uint64_t cap = std::max<uint64_t>(c->tp_nbytes + bytes, 2 * c->tp_bytes_cap);
+    if (dgrow(c, &c->tp_bytes, c->tp_nbytes, cap)) return TGSIM_ENOMEM;
+    c->tp_bytes_cap = cap;
+  }
+  std::vector<uint32_t> si(n), sl(n);
+  std::vector<int64_t> st(n);
+  std::vector<uint64_t> so(n);
+  std::vector<uint8_t> sb(bytes);
+  uint64_t b = 0;
+  for (size_t j = 0; j < n; ++j) {
+    const uint32_t i = ord[j];
+    const uint64_t len = off[i + 1] - off[i];
+    si[j] = inst[i]; st[j] = t[i]; so[j] = c->tp_nbytes + b; sl[j] = (uint32_t)len;
+    if (len) memcpy(sb.data() + b, payload + off[i], len);
+    b += len;
+  }
+  const uint64_t e0 = c->tp_n;
+  HIPCK(c, hipMemcpy(c->tp_inst + e0, si.data(), n * 4, hipMemcpyHostToDevice), "publish");
+  HIPCK(c, hipMemcpy(c->tp_t + e0, st.data(), n * 8, hipMemcpyHostToDevice), "publish");
+  HIPCK(c, hipMemcpy(c->tp_off + e0, so.data(), n * 8, hipMemcpyHostToDevice), "publish");
+  HIPCK(c, hipMemcpy(c->tp_len + e0, sl.data(), n * 4, hipMemcpyHostToDevice), "publish");
+  if (bytes) HIPCK(c, hipMemcpy(c->tp_bytes + c->tp_nbytes, sb.data(), bytes, hipMemcpyHostToDevice), "publish");
+  if (c->topic_runs.size() < c->d.max_states) c->topic_runs.resize(c->d.max_states);
+  for (size_t j = 0; j < n;) {
+    size_t k = j;
+    while (k < n && topics[ord[k]] == topics[ord[j]]) ++k;
+    c->topic_runs[topics[ord[j]]].push_back({pos[ord[j]], (uint32_t)(k - j), e0 + j});
+    j = k;
+  }
+  c->tp_n += n;
+  c->tp_nbytes += bytes;
+  if (pos_out) memcpy(pos_out, pos.data(), n * 4);
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_sync_subscribe(tgsim_ctx* c, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                                    uint32_t* inst_out, int64_t* t_out, uint64_t* off_out, uint8_t* payload_out,
+                                    size_t payload_cap, size_t* n_out, size_t* payload_bytes) {
+  if (!c || !n_out || !payload_bytes || from == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
+  *n_out = 0; *payload_bytes = 0;
+  if (topic >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad topic");
+  if (topic >= c->topic_runs.size()) return TGSIM_OK;
+  // the runs of the topic cover positions 1..count contiguously, in order
+  struct Seg { uint64_t entry; uint32_t n; };
+  std::vector<Seg> segs;
+  size_t want = 0;
+  for (const auto& r : c->topic_runs[topic]) {
+    if (want >= cap) break;
+    if (r.pos0 + r.len <= from) continue;
+    const uint32_t skip = from > r.pos0 ? from - r.pos0 : 0u;
+    const uint32_t k = (uint32_t)std::min<size_t>(r.len - skip, cap - want);
+    segs.push_back({r.entry + skip, k});
+    want += k;
+  }
+  std::vector<uint32_t> inst(want), len(want);
+  std::vector<int64_t> tt(want);
+  std::vector<uint64_t> eo(want);
+  size_t at = 0;
+  for (const Seg& s : segs) {
+    HIPCK(c, hipMemcpy(inst.data() + at, c->tp_inst + s.entry, s.n * 4ull, hipMemcpyDeviceToHost), "subscribe");
+    HIPCK(c, hipMemcpy(tt.data() + at, c->tp_t + s.entry, s.n * 8ull, hipMemcpyDeviceToHost), "subscribe");
+    HIPCK(c, hipMemcpy(eo.data() + at, c->tp_off + s.entry, s.n * 8ull, hipMemcpyDeviceToHost), "subscribe");
+    HIPCK(c, hipMemcpy(len.data() + at, c->tp_len + s.entry, s.n * 4ull, hipMemcpyDeviceToHost), "subscribe");
+    at += s.n;
+  }
+  size_t k = 0, bytes = 0;  // times never decrease along the positions: the visible entries are a prefix
+  while (k < want && tt[k] <= until_t) bytes += len[k++];
+  *n_out = k;
+  *payload_bytes = bytes;
+  if (bytes > payload_cap) return fail(c, TGSIM_ECAPACITY, "payload capacity %zu < %zu", payload_cap, bytes);
+  if (k && (!inst_out || !t_out || !off_out || (bytes && !payload_out))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  size_t b = 0, j = 0;
+  for (const Seg& s : segs) {  // a segment's payloads are contiguous in the arena
+    if (j >= k) break;
+    const size_t m = std::min<size_t>(s.n, k - j);
+    size_t nb = 0;
+    for (size_t q = 0; q < m; ++q) nb += len[j + q];
+    if (nb) HIPCK(c, hipMemcpy(payload_out + b, c->tp_bytes + eo[j], nb, hipMemcpyDeviceToHost), "subscribe");
+    for (size_t q = 0; q < m; ++q) {
+      inst_out[j + q] = inst[j + q]; t_out[j + q] = tt[j + q]; off_out[j + q] = b;
+      b += len[j + q];
+    }
+    j += m;
+  }
+  if (off_out) off_out[k] = b;
   return TGSIM_OK;
 }

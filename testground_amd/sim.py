@@ -270,6 +270,41 @@ class Simulator:
         self._check(self.lib.gen_storm_round(self._ctx, round_, int(t0), fanout, size, int(spread_ns), state))
 
 
+    # ---- topics (sync.Client Publish / Subscribe, device-resident logs) ----------------------
+    def publish(self, topics, instances, t, payloads: list[bytes]) -> np.ndarray:
+        inst = np.ascontiguousarray(np.atleast_1d(instances), dtype=np.uint32)
+        tp = np.ascontiguousarray(np.broadcast_to(np.asarray(topics, dtype=np.uint32), inst.shape))
+        tt = np.ascontiguousarray(np.broadcast_to(np.asarray(t, dtype=np.int64), inst.shape))
+        assert len(payloads) == len(inst)
+        off = np.zeros(len(inst) + 1, np.uint64)
+        off[1:] = np.cumsum([len(p) for p in payloads])
+        blob = np.frombuffer(b"".join(payloads) or b"\0", dtype=np.uint8)
+        pos = np.zeros(len(inst), np.uint32)
+        self._check(self.lib.sync_publish(self._ctx, _ptr(tp), _ptr(inst), _ptr(tt), _ptr(off), _ptr(blob),
+                                          len(inst), _ptr(pos)))
+        return pos
+
+    def subscribe(self, topic: int, from_pos: int = 1, until_t: int = (1 << 63) - 1,
+                  cap: int = 1 << 20) -> tuple[np.ndarray, np.ndarray, list[bytes]]:
+        """(instances, times, payloads) of the topic's entries from position from_pos on whose
+        time is <= until_t, in position order."""
+        n, nb = C.c_size_t(), C.c_size_t()
+        inst = np.zeros(cap, np.uint32)
+        tt = np.zeros(cap, np.int64)
+        off = np.zeros(cap + 1, np.uint64)
+        blob = np.zeros(1 << 12, np.uint8)
+        while True:  # ECAPACITY reports the bytes needed
+            rc = self.lib.sync_subscribe(self._ctx, topic, from_pos, until_t, cap, _ptr(inst), _ptr(tt), _ptr(off),
+                                         _ptr(blob), len(blob), C.byref(n), C.byref(nb))
+            if rc == A.ECAPACITY and nb.value > len(blob):
+                blob = np.zeros(nb.value, np.uint8)
+                continue
+            self._check(rc)
+            break
+        k = n.value
+        raw = blob.tobytes()
+        return inst[:k].copy(), tt[:k].copy(), [raw[int(off[j]):int(off[j + 1])] for j in range(k)]
+
     # ---- flood workload (config 5) -----------------------------------------------------------
     def flood_set_graph(self, offsets, neighbors, max_pubs: int) -> None:
         off = np.ascontiguousarray(offsets, dtype=np.uint32)

@@ -11,14 +11,16 @@ Reference: ``github.com/testground/sdk-go`` ``sync.Client`` and ``sync-service v
   deterministic order stands in for the sync service's arrival order, so results do
   not depend on the number of GPUs.
 * ``barrier(state, target, t_wait)`` releases at max(t_wait, time of the target-th signal).
-* ``publish`` / ``subscribe``: ordered topics with full history replay (host-side append logs;
-  the payloads are plan data, not part of the per-message hot path).
+* ``publish`` / ``subscribe``: ordered topics with full history replay, kept as append logs in
+  device memory (``tgsim_sync_publish`` / ``tgsim_sync_subscribe``). A topic counts like a state,
+  so positions follow (t, instance) order within a batch. Payloads travel as JSON (tuples come
+  back as lists).
 
 States are named by strings, as in the SDK; names map to dense device ids in first-use order.
 """
 from __future__ import annotations
 
-from collections import defaultdict
+import json
 
 import numpy as np
 
@@ -29,7 +31,6 @@ class SyncService:
     def __init__(self, sim):
         self.sim = sim
         self._ids: dict[str, int] = {}
-        self._topics: dict[str, list] = defaultdict(list)
 
     def state_id(self, state: str) -> int:
         if state not in self._ids:
@@ -72,19 +73,14 @@ class SyncService:
     # ---- topics -----------------------------------------------------------------------------
     def publish(self, topic: str, instances, t, payloads) -> np.ndarray:
         """Publish one payload per instance; returns the 1-based position of each in the topic.
-        Order within one call: (t, instance), as for signals."""
+        Order within one call: (t, instance), as for signals; a call must not go back in time."""
         inst = np.atleast_1d(np.asarray(instances, dtype=np.int64))
         tt = np.broadcast_to(np.asarray(t, dtype=np.int64), inst.shape)
-        log = self._topics[topic]
-        if log and len(tt) and tt.min() < log[-1][0]:
-            raise A.TgsimError(A.ECAUSALITY, f"publish to {topic!r} goes back in time")
-        order = np.lexsort((inst, tt))
-        pos = np.zeros(len(inst), np.int64)
-        for k in order:
-            log.append((int(tt[k]), int(inst[k]), payloads[k]))
-            pos[k] = len(log)
-        return pos
+        blobs = [json.dumps(p).encode() for p in payloads]
+        return self.sim.publish(self.state_id("topic:" + topic), inst, tt, blobs).astype(np.int64)
 
     def subscribe(self, topic: str, until_t: int | None = None) -> list:
         """All payloads published so far (history replay), in topic order."""
-        return [p for (t, _, p) in self._topics[topic] if until_t is None or t <= until_t]
+        _, _, blobs = self.sim.subscribe(self.state_id("topic:" + topic),
+                                         until_t=(1 << 63) - 1 if until_t is None else until_t)
+        return [json.loads(b) for b in blobs]
