@@ -87,18 +87,14 @@ typedef struct {
   uint32_t mult, shift; /* HTB rate */
   int64_t tau;       /* HTB buffer, ns */
   int limited;       /* Bandwidth != 0 */
+  uint32_t dup_rho, corrupt_rho, reorder_rho; /* netem correlations (Percentage2u32) */
+  int corr;          /* some correlated draw is used: the sender's messages run in (t, seq) order */
 } oshape;
 
 /* LinkShape -> the netem/HTB state the kernel ends up with.
  * link.go:155-181 (Shape), netlink NewHtbClass/NewNetem [EXT], sch_htb/sch_netem change paths [EXT]. */
 static int derive_shape(const tgsim_link_shape* s, oshape* o, char* err, size_t errlen) {
   memset(o, 0, sizeof(*o));
-  /* Correlated loss/dup/corrupt/reorder are a sequential recurrence (netem get_crandom [EXT]);
-   * not in this build. */
-  if (s->corrupt_corr != 0.0f || s->reorder_corr != 0.0f || s->duplicate_corr != 0.0f) {
-    if (err) snprintf(err, errlen, "correlated netem parameters are not supported");
-    return TGSIM_ENOTSUP;
-  }
   /* HTB: link.go:156-167; rate = Bandwidth/8 bytes/s (netlink NewHtbClass); the kernel refuses a
    * zero rate (htb_change_class: !hopt->rate.rate && !rate64 -> EINVAL). */
   uint64_t bw = s->bandwidth_bps == 0 ? UINT64_MAX : s->bandwidth_bps;
@@ -125,6 +121,12 @@ static int derive_shape(const tgsim_link_shape* s, oshape* o, char* err, size_t 
   o->dup_t = tgo_percentage2u32(s->duplicate);
   o->corrupt_t = tgo_percentage2u32(s->corrupt);
   o->reorder_t = tgo_percentage2u32(s->reorder);
+  /* correlations: netlink Percentage2u32 of CorruptCorr / ReorderCorr / DuplicateCorr (link.go:
+   * 173-178); netem draws through get_crandom only when the probability is non-zero [EXT] */
+  o->dup_rho = s->duplicate_corr != 0.0f ? tgo_percentage2u32(s->duplicate_corr) : 0;
+  o->corrupt_rho = s->corrupt_corr != 0.0f ? tgo_percentage2u32(s->corrupt_corr) : 0;
+  o->reorder_rho = s->reorder_corr != 0.0f ? tgo_percentage2u32(s->reorder_corr) : 0;
+  o->corr = (o->dup_rho && o->dup_t) || (o->corrupt_rho && o->corrupt_t) || (o->reorder_rho && o->reorder_t);
   return TGSIM_OK;
 }
 
@@ -200,6 +202,8 @@ struct tgo_ctx {
   size_t n_states;
   owaiter* waiters; size_t n_waiters, waiters_cap;
   int64_t storm_release;
+  uint32_t* cl;       /* [nloc][3] netem crandom state (dup, corrupt, reorder): last answer */
+  uint32_t* epoch;    /* [nloc] Shape calls so far (seeds the state a Shape call re-initialises) */
   /* topics: per state id, entries in position order; payload bytes in one buffer */
   struct otopic* topics; size_t n_topics;
   uint8_t* tp_bytes; size_t tp_nbytes, tp_cap;
@@ -316,6 +320,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
+  free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
     free(c->topics[i].inst); free(c->topics[i].t); free(c->topics[i].off); free(c->topics[i].len);
   }
@@ -345,7 +350,21 @@ int tgo_set_shape(tgo_ctx* c, uint32_t g, const tgsim_link_shape* s) {
   oshape o;
   int rc = derive_shape(s, &o, c->err, sizeof(c->err));
   if (rc) return rc;
-  if (is_local(c, g)) c->shape[g - c->lo] = o;
+  if (is_local(c, g)) {
+    uint32_t l = g - c->lo;
+    c->shape[l] = o;
+    /* netem_change -> get_correlation -> init_crandom: every Shape re-seeds the state [EXT]; the
+     * kernel seeds it from prandom, here from Philox(g, epoch, 0, "CORR") */
+    if (!c->cl) {
+      c->cl = (uint32_t*)calloc((size_t)c->nloc * 3 + 1, 4);
+      c->epoch = (uint32_t*)calloc((size_t)c->nloc + 1, 4);
+      if (!c->cl || !c->epoch) return fail(c, TGSIM_ENOMEM, "oom");
+    }
+    uint32_t ctr[4] = {g, ++c->epoch[l], 0, 0x434F5252u /* "CORR" */}, out[4];
+    uint32_t key[2] = {(uint32_t)c->seed, (uint32_t)(c->seed >> 32)};
+    tgo_philox4x32_10(ctr, key, out);
+    c->cl[3 * l] = out[0]; c->cl[3 * l + 1] = out[1]; c->cl[3 * l + 2] = out[2];
+  }
   return TGSIM_OK;
 }
 
@@ -526,10 +545,19 @@ static void draw(const tgo_ctx* c, uint32_t seq, uint32_t src, uint32_t clone, u
 
 static int route_record(tgo_ctx* c, tgsim_record* r); /* stage-D record -> local newD or outbox */
 
+/* netem get_crandom [EXT sch_netem.c]: the next answer leans on the last one by rho / 2^32. */
+static uint32_t crandom(uint32_t* last, uint32_t rho, uint32_t value) {
+  if (!last || rho == 0) return value;
+  uint64_t r = (uint64_t)rho + 1;
+  uint32_t ans = (uint32_t)(((uint64_t)value * ((1ull << 32) - r) + (uint64_t)*last * r) >> 32);
+  *last = ans;
+  return ans;
+}
+
 /* One copy through the rest of netem_enqueue [EXT] after the duplicate/loss decision:
  * (clone only) loss draw, corruption draw, reorder-or-delay. Returns 1 if a record was produced. */
 static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, uint32_t seq,
-                      uint32_t size, int64_t t_send, uint32_t clone, tgsim_record* rec) {
+                      uint32_t size, int64_t t_send, uint32_t clone, uint32_t* cl, tgsim_record* rec) {
   uint32_t r0[4];
   draw(c, seq, src, clone, 0, r0);
   if (clone && sh->loss_t && sh->loss_t >= r0[1]) return 0;
@@ -538,12 +566,13 @@ static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, 
   if (sh->corrupt_t) {
     uint32_t r1[4];
     draw(c, seq, src, clone, 1, r1);
-    if (sh->corrupt_t >= r1[0] && size > 0) {
+    if (sh->corrupt_t >= crandom(cl ? cl + 1 : NULL, sh->corrupt_rho, r1[0]) && size > 0) {
       rec->meta |= TGSIM_F_CORRUPT | ((r1[2] % 8u) << TGSIM_F_BIT_SHIFT);
       rec->corrupt_off = r1[1] % size;
     }
   }
-  if (sh->reorder_t && !(sh->reorder_t < r0[3])) { /* gap == 1 when reorder > 0 (netlink NewNetem) */
+  if (sh->reorder_t && !(sh->reorder_t < crandom(cl ? cl + 2 : NULL, sh->reorder_rho, r0[3]))) {
+    /* gap == 1 when reorder > 0 (netlink NewNetem) */
     rec->meta |= TGSIM_F_REORDERED;
     rec->t = t_send;
   } else {
@@ -552,6 +581,16 @@ static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, 
   }
   if (!sh->limited) rec->meta |= TGSIM_F_STAGE_D; /* unlimited HTB: departs when netem releases it */
   return 1;
+}
+
+static const omsgs* g_sort_msgs; /* qsort context of cmp_msg_order (single-threaded oracle) */
+static int cmp_msg_order(const void* a, const void* b) {
+  size_t i = *(const size_t*)a, j = *(const size_t*)b;
+  const omsgs* m = g_sort_msgs;
+  if (m->src[i] != m->src[j]) return m->src[i] < m->src[j] ? -1 : 1;
+  if (m->t[i] != m->t[j]) return m->t[i] < m->t[j] ? -1 : 1;
+  if (m->seq[i] != m->seq[j]) return m->seq[i] < m->seq[j] ? -1 : 1;
+  return i < j ? -1 : i > j;
 }
 
 static int cmp_tb(const void* a, const void* b) {
@@ -593,10 +632,22 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     if (r.meta & TGSIM_F_STAGE_D) { if (recs_push(&c->D, &r)) return TGSIM_ENOMEM; }
     else if (recs_push(&c->A, &r)) return TGSIM_ENOMEM;
   }
-  /* 2. route + netem for every staged message, in enqueue order */
+  /* 2. route + netem for every staged message, in enqueue order; a sender with correlated draws
+   *    arrives at its qdisc in (t_send, seq) order, which its crandom state follows */
   if (grow((void**)&c->status, &c->status_cap, s->n + 1, 1)) return fail(c, TGSIM_ENOMEM, "oom");
   c->n_status = s->n;
-  for (size_t i = 0; i < s->n; ++i) {
+  size_t* order = NULL;
+  int any_corr = 0;
+  for (uint32_t l = 0; l < c->nloc && !any_corr; ++l) any_corr = c->shape[l].corr;
+  if (any_corr && s->n) {
+    order = (size_t*)malloc(s->n * sizeof(size_t));
+    if (!order) return fail(c, TGSIM_ENOMEM, "oom");
+    for (size_t i = 0; i < s->n; ++i) order[i] = i;
+    g_sort_msgs = s;
+    qsort(order, s->n, sizeof(size_t), cmp_msg_order);
+  }
+  for (size_t k = 0; k < s->n; ++k) {
+    const size_t i = order ? order[k] : k;
     uint32_t src = s->src[i], dst = s->dst[i], seq = s->seq[i], size = s->size[i];
     int64_t ts = s->t[i];
     c->stats.msgs_in++;
@@ -618,10 +669,11 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     if (rt == R_NONE) { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; continue; }
     if (!c->enabled[dst]) { c->status[i] = TGSIM_ST_DEST_DOWN; c->stats.dest_down++; continue; }
     const oshape* sh = &c->shape[src - c->lo];
+    uint32_t* cl = sh->corr ? c->cl + 3 * (size_t)(src - c->lo) : NULL;
     uint32_t r0[4];
     draw(c, seq, src, 0, 0, r0);
     int count = 1;
-    int dup = sh->dup_t && sh->dup_t >= r0[0];
+    int dup = sh->dup_t && sh->dup_t >= crandom(cl, sh->dup_rho, r0[0]);
     if (dup) ++count;
     int lost = sh->loss_t && sh->loss_t >= r0[1];
     if (lost) --count;
@@ -631,20 +683,21 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     tgsim_record rec;
     if (count == 2) { /* the clone is enqueued first, through the root qdisc, duplicate disabled */
       st |= TGSIM_ST_FLAG_DUP;
-      if (netem_copy(c, sh, src, dst, seq, size, ts, 1, &rec)) {
+      if (netem_copy(c, sh, src, dst, seq, size, ts, 1, cl, &rec)) {
         c->stats.copies++;
         if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
         else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
         else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
       } else st |= TGSIM_ST_FLAG_CLONE_LOST;
     }
-    netem_copy(c, sh, src, dst, seq, size, ts, 0, &rec);
+    netem_copy(c, sh, src, dst, seq, size, ts, 0, cl, &rec);
     c->stats.copies++;
     if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
     else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
     else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
     c->status[i] = st;
   }
+  free(order);
   s->n = 0;
   /* 3. HTB token bucket (GCRA form): copies whose netem time is < t_end, per sender in
    *    (time_to_send, seq, clone-first) order; d = max(e, X); X = min(max(X, e - tau) + cost, 2^61). */

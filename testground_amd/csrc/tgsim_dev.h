@@ -64,6 +64,13 @@ struct Dev {
   uint32_t* rule_off = nullptr;   // [nloc+1]
   RuleDev* rules = nullptr;
 
+  // netem correlations: per local sender (dup, corrupt, reorder, -) rho and crandom state
+  uint32_t* cor_rho = nullptr;    // [4 * nloc]
+  uint32_t* cor_last = nullptr;   // [4 * nloc]
+  uint32_t* corr_idx = nullptr;   // [cap_msgs] deferred message indices (k_shape)
+  uint32_t* corr_sorted = nullptr;  // [cap_msgs] the same, grouped by sender in (t_send, seq) order
+  bool any_corr = false;          // some local shape has kShCorr
+
   // staged messages (SoA) + per-message status
   uint32_t *m_src = nullptr, *m_dst = nullptr, *m_seq = nullptr, *m_size = nullptr;
   int64_t* m_t = nullptr;
@@ -166,6 +173,8 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
                                             uint32_t st, uint32_t nw, bool add, uint32_t add_state,
                                             uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
+// init_crandom on a Shape call: the state of local sender pairs[2i] re-seeded for epoch pairs[2i+1]
+hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n);
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)

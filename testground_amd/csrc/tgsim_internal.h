@@ -43,9 +43,11 @@ struct alignas(16) ShapeDev {
   int64_t tau;       // HTB buffer (ns)
   int32_t sigma;     // netem jitter (ns) as tabledist's s32
   uint32_t loss_t, dup_t, corrupt_t, reorder_t;
-  uint32_t mult, shift, limited;  // HTB rate as multiply-shift; limited = Bandwidth != 0
+  uint32_t mult, shift, flags;    // HTB rate as multiply-shift; flags: kShLimited, kShCorr
 };
 static_assert(sizeof(ShapeDev) == 48, "ShapeDev layout");
+constexpr uint32_t kShLimited = 1u;  // Bandwidth != 0
+constexpr uint32_t kShCorr = 2u;     // a correlated netem draw is used (messages deferred to k_shape_corr)
 
 struct RuleDev {           // per-sender routing rule, CSR, sorted (plen desc, prefix asc)
   uint32_t prefix;
@@ -77,6 +79,7 @@ struct DevScalars {
   uint32_t n_large, max_large, n_chunks;
   uint32_t n_medium;                 // segments for the block-per-segment kernel (k_seg_list)
   uint32_t n_recv, n_out;
+  uint32_t n_corr;                   // messages of correlated senders deferred by k_shape
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits
   uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)

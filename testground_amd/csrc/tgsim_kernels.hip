@@ -289,6 +289,7 @@ struct ShapeArgs {
   Geo geo;
   Queues Q;
   unsigned long long* stats;  // [kNSub][16] sharded counters
+  uint32_t* corr_idx;         // deferred messages of correlated senders (count sc->n_corr)
 };
 
 // Longest-prefix match over the sender's routing table: rule groups by prefix
@@ -353,7 +354,45 @@ __device__ __forceinline__ bool netem_copy(const ShapeDev& sh, const uint32_t r0
     const int64_t delay = tabledist(sh.mu, sh.sigma, r0[2]);
     rec.t = ts + (delay > 0 ? delay : 0);
   }
-  if (!sh.limited) rec.meta |= TGSIM_F_STAGE_D;
+  if (!(sh.flags & kShLimited)) rec.meta |= TGSIM_F_STAGE_D;
+  return true;
+}
+
+// netem get_crandom [EXT sch_netem.c]: the next answer leans on the last one by rho / 2^32 (the
+// u64 sum cannot overflow: (2^32-1)(2^32-r) + (2^32-1) r < 2^64).
+__device__ __forceinline__ uint32_t crandom(uint32_t& last, uint32_t rho, uint32_t value) {
+  if (rho == 0) return value;
+  const uint64_t r = (uint64_t)rho + 1;
+  const uint32_t ans = (uint32_t)(((uint64_t)value * ((1ull << 32) - r) + (uint64_t)last * r) >> 32);
+  last = ans;
+  return ans;
+}
+
+// netem_copy with the sender's correlated corrupt / reorder draws (rho[1], rho[2]; state cl).
+__device__ __forceinline__ bool netem_copy_corr(const ShapeDev& sh, const uint32_t rho[3], uint32_t cl[3],
+                                                const uint32_t r0[4], uint32_t src, uint32_t dst, uint32_t seq,
+                                                uint32_t size, int64_t ts, uint32_t clone, uint32_t k0, uint32_t k1,
+                                                tgsim_record& rec) {
+  if (clone && sh.loss_t && sh.loss_t >= r0[1]) return false;
+  rec.src = src; rec.dst = dst; rec.seq = seq; rec.size = size;
+  rec.meta = clone ? TGSIM_F_CLONE : 0u;
+  rec.corrupt_off = 0;
+  if (sh.corrupt_t) {
+    uint32_t r1[4];
+    philox4x32_10(seq, src, clone | 2u, kNetemSalt, k0, k1, r1);
+    if (sh.corrupt_t >= crandom(cl[1], rho[1], r1[0]) && size > 0) {
+      rec.meta |= TGSIM_F_CORRUPT | ((r1[2] % 8u) << TGSIM_F_BIT_SHIFT);
+      rec.corrupt_off = r1[1] % size;
+    }
+  }
+  if (sh.reorder_t && !(sh.reorder_t < crandom(cl[2], rho[2], r0[3]))) {
+    rec.meta |= TGSIM_F_REORDERED;
+    rec.t = ts;
+  } else {
+    const int64_t delay = tabledist(sh.mu, sh.sigma, r0[2]);
+    rec.t = ts + (delay > 0 ? delay : 0);
+  }
+  if (!(sh.flags & kShLimited)) rec.meta |= TGSIM_F_STAGE_D;
   return true;
 }
 
@@ -385,10 +424,11 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
     const ShapeDev sh = a.shape[slc];
     asm volatile("" ::"v"((uint32_t)fsrc), "v"((uint32_t)fdst), "v"(dip), "v"(r_lo), "v"(r_hi),
                  "v"((uint32_t)sh.mu), "v"((uint32_t)sh.tau), "v"(sh.sigma), "v"(sh.loss_t), "v"(sh.dup_t),
-                 "v"(sh.corrupt_t), "v"(sh.reorder_t), "v"(sh.mult), "v"(sh.limited));  // stage 2: gathers
+                 "v"(sh.corrupt_t), "v"(sh.reorder_t), "v"(sh.mult), "v"(sh.flags));  // stage 2: gathers
     tgsim_record r1, r2;
     int q1 = -1, q2 = -1;
     uint8_t st;
+    bool deferred = false;
     cnt[ST_MSGS]++;
     if (!src_ok || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
       atomicOr(&sc->err, ERR_BAD_MSG);
@@ -412,6 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
       else if (rt == R_DEFAULT && ext) { st = TGSIM_ST_EXTERNAL; cnt[ST_EXTERNAL]++; }
       else if (rt != R_DATA) { st = TGSIM_ST_UNREACHABLE; cnt[ST_UNREACH]++; }
       else if (!(fdst & 1u)) { st = TGSIM_ST_DEST_DOWN; cnt[ST_DESTDOWN]++; }
+      else if (sh.flags & kShCorr) { st = 0; deferred = true; }  // netem in (t_send, seq) order: k_shape_corr
       else {
         uint32_t r0[4];
         philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
@@ -443,7 +484,9 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
         }
       }
     }
-    a.status[i] = st;
+    if (!deferred) a.status[i] = st;
+    const uint32_t cpos = wave_append(deferred ? &sc->n_corr : nullptr);
+    if (deferred) a.corr_idx[cpos] = i;
     a.Q.push(q1, r1, 2 * it);
     a.Q.push(q2, r2, 2 * it + 1);
   }
@@ -1779,6 +1822,116 @@ struct SigPolicy {
   }
 };
 
+// ---- correlated netem (get_crandom [EXT]) --------------------------------------------------
+// A sender whose shape uses a correlated draw has a sequential state per qdisc, advanced in the
+// order its messages reach the qdisc, (t_send, seq). k_shape defers those messages; they are
+// grouped by sender (the bucketed group-by), ordered (t_send, seq) per sender (k_seg_small /
+// k_rest with CorrPolicy) and run through netem by one thread per sender (k_shape_corr). Senders
+// without correlation never take this path (the storm pays nothing for it).
+
+__global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* src, const uint32_t* n_ptr,
+                                                      uint32_t lo, uint32_t* keys, uint32_t* vals) {
+  const uint32_t n = *n_ptr;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const uint32_t i = idx[j];
+    keys[j] = src[i] - lo;
+    vals[j] = i;
+  }
+}
+
+struct CorrPolicy {
+  const int64_t* t;
+  const uint32_t* seq;
+  uint32_t* sorted;
+
+  __device__ __forceinline__ void key(uint32_t seg, uint32_t idx, uint32_t& sg, uint64_t& k1, uint64_t& k2,
+                                      uint32_t& k3) const {
+    sg = seg;
+    k1 = (uint64_t)t[idx] ^ 0x8000000000000000ull;  // signed order (t_send >= 0 anyway)
+    k2 = seq[idx];
+    k3 = idx;
+  }
+  __device__ __forceinline__ void write(uint32_t, uint32_t gpos, uint32_t, uint64_t, uint32_t idx) const {
+    sorted[gpos] = idx;
+  }
+  __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t s_begin, const uint32_t* off, uint32_t) const {
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+      const uint32_t e = s.perm[j];
+      write(s.sg[j], s_begin + j, off[s.sg[j]], s.k1[e], s.k3[e]);
+    }
+  }
+};
+
+// One thread per local sender: its deferred messages in (t_send, seq) order through netem_enqueue
+// with the correlated draws (dup, then the clone's and the original's corrupt / reorder).
+__global__ __launch_bounds__(kBlock) void k_shape_corr(ShapeArgs a, const uint32_t* sorted, const uint32_t* off,
+                                                       const uint32_t* rho4, uint32_t* last4) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= a.nloc) return;
+  const uint32_t j0 = off[l], j1 = off[l + 1];
+  if (j0 == j1) return;
+  const int64_t t_end = a.Q.sc->t_end;
+  const ShapeDev sh = a.shape[l];
+  const uint32_t rho[3] = {rho4[4 * l], rho4[4 * l + 1], rho4[4 * l + 2]};
+  uint32_t cl[3] = {last4[4 * l], last4[4 * l + 1], last4[4 * l + 2]};
+  unsigned long long lost = 0, copies = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t i = sorted[j];
+    const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
+    const int64_t ts = a.t[i];
+    tgsim_record r1, r2;
+    int q1 = -1, q2 = -1;
+    uint32_t r0[4];
+    philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
+    int count = 1;
+    const bool dup = sh.dup_t && sh.dup_t >= crandom(cl[0], rho[0], r0[0]);
+    if (dup) ++count;
+    const bool lst = sh.loss_t && sh.loss_t >= r0[1];
+    if (lst) --count;
+    uint8_t st;
+    if (count == 0) {
+      st = TGSIM_ST_LOST;
+      ++lost;
+    } else {
+      st = TGSIM_ST_QUEUED;
+      if (dup && lst) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+      if (count == 2) {
+        st |= TGSIM_ST_FLAG_DUP;
+        uint32_t c0[4];
+        philox4x32_10(seq, src, 1u, kNetemSalt, a.key0, a.key1, c0);
+        if (netem_copy_corr(sh, rho, cl, c0, src, dst, seq, size, ts, 1u, a.key0, a.key1, r1)) {
+          q1 = qid_copy(a.geo, r1, t_end);
+          ++copies;
+        } else {
+          st |= TGSIM_ST_FLAG_CLONE_LOST;
+        }
+      }
+      netem_copy_corr(sh, rho, cl, r0, src, dst, seq, size, ts, 0u, a.key0, a.key1, r2);
+      q2 = qid_copy(a.geo, r2, t_end);
+      ++copies;
+    }
+    a.status[i] = st;
+    a.Q.push(q1, r1, 2 * j);
+    a.Q.push(q2, r2, 2 * j + 1);
+  }
+  last4[4 * l] = cl[0]; last4[4 * l + 1] = cl[1]; last4[4 * l + 2] = cl[2];
+  unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
+  if (lost) atomicAdd(&row[ST_LOST], lost);
+  if (copies) atomicAdd(&row[ST_COPIES], copies);
+}
+
+// init_crandom at a Shape call: Philox(g, epoch, 0, "CORR") words 0..2 (the kernel uses prandom).
+__global__ void k_reset_corr(const uint32_t* pairs, uint32_t n, uint32_t lo, uint32_t k0, uint32_t k1,
+                             uint32_t* last4) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t l = pairs[2 * i], ep = pairs[2 * i + 1];
+  uint32_t o[4];
+  philox4x32_10(lo + l, ep, 0u, 0x434F5252u /* "CORR" */, k0, k1, o);
+  last4[4 * l] = o[0]; last4[4 * l + 1] = o[1]; last4[4 * l + 2] = o[2]; last4[4 * l + 3] = 0;
+}
+
 // Commit a sorted batch: per present state, check time order, append a log chunk, bump the count.
 __global__ __launch_bounds__(kBlock) void k_sig_commit(const uint32_t* off, uint32_t K, uint32_t kmin,
                                                        uint64_t log_base, const int64_t* log, uint32_t* count,
@@ -2007,6 +2160,11 @@ __device__ void large_consume(const SigPolicy& p, SortSmem&, const LargeSeg& L, 
                               uint32_t) {
   for (uint32_t j = threadIdx.x; j < L.len; j += kBlock)
     p.write(L.seg, L.start + j, L.start, K1[L.start + j], K3[L.start + j]);
+}
+
+__device__ void large_consume(const CorrPolicy& p, SortSmem&, const LargeSeg& L, const uint64_t*, const uint32_t* K3,
+                              uint32_t) {
+  for (uint32_t j = threadIdx.x; j < L.len; j += kBlock) p.sorted[L.start + j] = K3[L.start + j];
 }
 
 // Sort one large segment inside the calling block; returns the buffer set that holds the result.
@@ -2412,6 +2570,35 @@ static hipError_t run_token_bucket(Dev& d) {
   return launch_rest(d, p, d.keys0, d.vals0);
 }
 
+// The deferred messages of correlated senders (k_shape): group by sender, order (t_send, seq),
+// then netem per sender in that order.
+static hipError_t run_shape_corr(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
+  uint32_t* n_dev = &d.sc->n_corr;
+  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.m_src, n_dev,
+                     d.lo, d.keys0, d.vals0);
+  TG_CHECK(hipGetLastError());
+  BktSrc src = bkt_queue(d, Q_A);
+  src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
+  uint32_t *keys, *vals;
+  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, nullptr, &keys, &vals));
+  CorrPolicy p;
+  p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
+  hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                     d.seg_off, n_dev, d.cap_rec);
+  TG_CHECK(hipGetLastError());
+  TG_CHECK(launch_rest(d, p, keys, vals));
+  hipLaunchKernelGGL(k_shape_corr, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, a,
+                     d.corr_sorted, d.seg_off, d.cor_rho, d.cor_last);
+  return hipGetLastError();
+}
+
+hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_reset_corr, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, pairs_dev, n, d.lo,
+                     d.key0, d.key1, d.cor_last);
+  return hipGetLastError();
+}
+
 hipError_t window_begin(Dev& d, uint32_t n_staged) {
   Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
   {
@@ -2427,9 +2614,11 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
     a.stats = d.stats;
+    a.corr_idx = d.corr_idx;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
     { ProfScope ps_(d, KID_SHAPE); hipLaunchKernelGGL(k_shape, dim3(g), dim3(kBlock), 0, d.stream, a); }
     TG_CHECK(hipGetLastError());
+    if (d.any_corr) TG_CHECK(run_shape_corr(d, a, n_staged));
   }
   TG_CHECK(run_token_bucket(d));
   if (d.S > 1) {

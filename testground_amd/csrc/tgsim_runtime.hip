@@ -32,6 +32,11 @@ struct tgsim_ctx {
   std::vector<uint32_t> id_of_h;  // ip - data_net -> instance id
   std::vector<std::vector<RuleDev>> rules_h;
   std::vector<uint32_t> tb_reset;
+  std::vector<uint32_t> rho_h;       // [4 * nloc] netem correlations per local sender
+  std::vector<uint32_t> corr_epoch;  // [nloc] Shape calls so far
+  std::vector<uint32_t> corr_reset;  // (local, epoch) pairs to re-seed at the next upload
+  uint32_t* corr_reset_dev = nullptr;
+  uint32_t corr_reset_cap = 0;
   bool shape_dirty = true, flags_dirty = true, ip_dirty = true, rules_dirty = true;
   size_t rules_cap_dev = 0;
   uint32_t* tb_reset_dev = nullptr;
@@ -140,19 +145,16 @@ static uint32_t to_us(int64_t ns) {  // link.go:143-151
   return (uint32_t)(uint64_t)us;
 }
 
-static int compile_shape(const tgsim_link_shape& s, ShapeDev& o, std::string* err) {
+// rho (optional): netem correlations (dup, corrupt, reorder, 0) via netlink Percentage2u32
+static int compile_shape(const tgsim_link_shape& s, ShapeDev& o, std::string* err, uint32_t* rho = nullptr) {
   memset(&o, 0, sizeof(o));
-  if (s.corrupt_corr != 0.0f || s.reorder_corr != 0.0f || s.duplicate_corr != 0.0f) {
-    if (err) *err = "correlated netem parameters are not supported";
-    return TGSIM_ENOTSUP;
-  }
   const uint64_t bw = s.bandwidth_bps == 0 ? UINT64_MAX : s.bandwidth_bps;  // link.go:156-159
   const uint64_t rate = bw / 8;                                               // netlink NewHtbClass
   if (rate == 0) {
     if (err) *err = "invalid htb rate";
     return TGSIM_EINVAL;
   }
-  o.limited = s.bandwidth_bps != 0;
+  o.flags = s.bandwidth_bps != 0 ? kShLimited : 0u;
   // psched_ratecfg_precompute [EXT]
   uint64_t factor = 1000000000ull;
   uint32_t mult = 1, shift = 0;
@@ -176,6 +178,12 @@ static int compile_shape(const tgsim_link_shape& s, ShapeDev& o, std::string* er
   o.dup_t = pct2u32(s.duplicate);
   o.corrupt_t = pct2u32(s.corrupt);
   o.reorder_t = pct2u32(s.reorder);
+  // correlations (link.go:173-178): get_crandom is only reached when the probability is non-zero
+  const uint32_t dr = s.duplicate_corr != 0.0f ? pct2u32(s.duplicate_corr) : 0u;
+  const uint32_t cr = s.corrupt_corr != 0.0f ? pct2u32(s.corrupt_corr) : 0u;
+  const uint32_t rr = s.reorder_corr != 0.0f ? pct2u32(s.reorder_corr) : 0u;
+  if ((dr && o.dup_t) || (cr && o.corrupt_t) || (rr && o.reorder_t)) o.flags |= kShCorr;
+  if (rho) { rho[0] = dr; rho[1] = cr; rho[2] = rr; rho[3] = 0; }
   return TGSIM_OK;
 }
 
@@ -283,6 +291,10 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.m_size, d.cap_msgs);
   rc |= dalloc(c, &d.m_t, d.cap_msgs);
   rc |= dalloc(c, &d.status, d.cap_msgs);
+  rc |= dalloc(c, &d.corr_idx, d.cap_msgs);
+  rc |= dalloc(c, &d.corr_sorted, d.cap_msgs);
+  rc |= dalloc(c, &d.cor_rho, 4 * (size_t)std::max<uint32_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.cor_last, 4 * (size_t)std::max<uint32_t>(c->nloc, 1));
   rc |= dalloc(c, &d.A, phys_rec);
   rc |= dalloc(c, &d.D, phys_rec);
   rc |= dalloc(c, &d.L, phys_rec);
@@ -360,6 +372,8 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
 
   // initial state = after the sidecar's Config{Network:"default", Enable:true} (sidecar_handler.go:26-29)
   c->shape_h.assign(c->nloc, default_shape());
+  c->rho_h.assign(4 * (size_t)c->nloc, 0u);
+  c->corr_epoch.assign(c->nloc, 0u);
   c->flags_h.assign(c->N, 1u);  // enabled, external routing off (zero RoutingPolicy -> disable)
   c->ip_h.resize(c->N);
   c->id_of_h.assign(space, UINT32_MAX);
@@ -494,11 +508,17 @@ extern "C" int tgsim_set_shape(tgsim_ctx* c, uint32_t g, const tgsim_link_shape*
   if (!c || !s || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
   ShapeDev o;
   std::string e;
-  int rc = compile_shape(*s, o, &e);
+  uint32_t rho[4];
+  int rc = compile_shape(*s, o, &e, rho);
   if (rc) return fail(c, rc, "%s", e.c_str());
   if (is_local(c, g)) {
-    c->shape_h[g - c->lo] = o;
+    const uint32_t l = g - c->lo;
+    c->shape_h[l] = o;
+    memcpy(&c->rho_h[4 * (size_t)l], rho, sizeof(rho));
     c->shape_dirty = true;
+    // netem_change -> init_crandom: every Shape re-seeds the correlation state [EXT]
+    c->corr_reset.push_back(l);
+    c->corr_reset.push_back(++c->corr_epoch[l]);
   }
   return TGSIM_OK;
 }
@@ -620,6 +640,22 @@ static int upload_tables(tgsim_ctx* c) {
   bool copied = false;
   if (c->shape_dirty && c->nloc) {
     HIPCK(c, hipMemcpyAsync(d.shape, c->shape_h.data(), c->nloc * sizeof(ShapeDev), hipMemcpyHostToDevice, d.stream), "upload shapes");
+    HIPCK(c, hipMemcpyAsync(d.cor_rho, c->rho_h.data(), c->rho_h.size() * 4, hipMemcpyHostToDevice, d.stream), "upload shapes");
+    d.any_corr = false;
+    for (const ShapeDev& sh : c->shape_h) d.any_corr |= (sh.flags & kShCorr) != 0;
+    copied = true;
+  }
+  if (!c->corr_reset.empty()) {
+    const uint32_t n = (uint32_t)(c->corr_reset.size() / 2);
+    if (n > c->corr_reset_cap) {
+      HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+      dfree(c, c->corr_reset_dev);
+      c->corr_reset_dev = nullptr;
+      if (dalloc(c, &c->corr_reset_dev, 2 * (size_t)n)) return TGSIM_ENOMEM;
+      c->corr_reset_cap = n;
+    }
+    HIPCK(c, hipMemcpyAsync(c->corr_reset_dev, c->corr_reset.data(), 2 * (size_t)n * 4, hipMemcpyHostToDevice, d.stream), "upload resets");
+    HIPCK(c, launch_reset_corr(d, c->corr_reset_dev, n), "reset corr");
     copied = true;
   }
   if (c->flags_dirty) {
@@ -667,6 +703,7 @@ static int upload_tables(tgsim_ctx* c) {
   // host sources are pageable vectors that later calls may modify: wait for the copies
   if (copied) HIPCK(c, hipStreamSynchronize(d.stream), "sync uploads");
   c->tb_reset.clear();
+  c->corr_reset.clear();
   c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = false;
   return TGSIM_OK;
 }

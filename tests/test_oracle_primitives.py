@@ -106,7 +106,7 @@ def test_derive_shape_known_answers():
 
 def test_derive_shape_rejects():
     assert O.derive_shape(make_shape(bandwidth_bps=7)) == A.EINVAL      # 7 bits/s -> rate 0 B/s
-    assert O.derive_shape(make_shape(duplicate_corr=1.0)) == A.ENOTSUP  # correlated netem
+    assert isinstance(O.derive_shape(make_shape(duplicate_corr=1.0)), list)  # correlated netem: supported
 
 
 # pkg/runner/common_test.go:14-20
