@@ -173,6 +173,12 @@ __device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
   return 1u << (32 - __clz(v - 1));
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -1127,7 +1133,8 @@ __device__ __forceinline__ void span_sort(SortSmem& s, uint32_t m, const uint32_
     const uint32_t len = off[g + 1] - off[g];
     ml = len > ml ? len : ml;
   }
-  atomicMax(&s.maxlen, ml);
+  ml = wave_max(ml);
+  if ((threadIdx.x & 63) == 0) atomicMax(&s.maxlen, ml);
   __syncthreads();
   if (s.maxlen <= (uint32_t)kRankSortMax) {
     // O(len) rank per element inside its segment; keys are unique (k3 carries the index)
@@ -1536,7 +1543,8 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
   const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = threadIdx.x * per;
   uint32_t sum = 0, mx = 0;
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) { sum += sm.cnt[i0 + i]; mx = max(mx, sm.cnt[i0 + i]); }
-  if (mx) atomicMax(&sm.maxlen, mx);
+  mx = wave_max(mx);  // one LDS atomic per wave, not one per key
+  if (mx && (threadIdx.x & 63) == 0) atomicMax(&sm.maxlen, mx);
   uint32_t total;
   uint32_t run = block_excl_scan(sum, sm.part, total);
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
@@ -2482,10 +2490,14 @@ static BktDiv bkt_div(uint32_t w) {
 }
 
 // Keys per bucket of the fused consumers: >= 128 keys (~1k items of a storm) per workgroup, and
-// few enough buckets that they all run in one wave of workgroups (3 per CU); <= 512 keys.
+// few enough buckets that they all run in one wave of workgroups (3 per CU); <= 512 keys; at
+// least TG_BKT_MIN_KEYS (48: measured best for 12.5k-instance shards, neutral at 100k).
 static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
+#ifndef TG_BKT_MIN_KEYS
+#define TG_BKT_MIN_KEYS 48u  // small shards (strong scaling): more, smaller buckets
+#endif
   const uint32_t slots = 3u * (uint32_t)d.n_cu;
-  uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(128u, K));
+  uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(TG_BKT_MIN_KEYS, K));
   w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
   return std::max<uint32_t>(w, 1u);
 }

@@ -2,6 +2,7 @@
 # Times the bench's kernel classes with each experiment build in tools/exp/ (TGSIM_LIB) beside the
 # in-tree library.   tools/exp_libs.sh <outdir>
 set -o pipefail
+shopt -s nullglob
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-exp}
 mkdir -p $OUT
