@@ -992,9 +992,11 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
       medium[atomicAdd(&sc->n_medium, 1u)] = k;
     }
   }
-  if (h.b == B - 1 && tid == 0) {
-    off[K] = h.start + h.nb;
-    if (off2) off2[K] = h.start + h.nb;
+  // the end of this bucket's last segment: a neighbouring bucket on the fused path writes offsets
+  // only for its own long keys, so the boundary must not be left to it (same value if it does)
+  if (tid == 0) {
+    off[h.k0 + h.nk] = h.start + h.nb;
+    if (off2) off2[h.k0 + h.nk] = h.start + h.nb;
   }
   __syncthreads();
   for (uint32_t j = tid; j < h.nb; j += kBlock) {
@@ -1511,24 +1513,23 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
     return false;
   }
-  // this thread's items: kIPT consecutive positions of the bucket (one chunk search, then a walk)
+  // this thread's items (strided: consecutive positions used to leave half the threads idle)
   uint32_t kk[kIPT], ix[kIPT];
-  {
-    const uint32_t j0 = threadIdx.x * kIPT;
-    uint32_t p = j0 < h.nb ? chunk_of(cexcl, j0) : 0u;
+  // item u of this thread is bucket position threadIdx.x + u * kBlock: every thread of the block
+  // issues loads (a bucket of ~1k items fills 4 rounds of 256 threads, not 131 threads x 8)
 #pragma unroll
-    for (int u = 0; u < kIPT; ++u) {
-      const uint32_t j = j0 + u;
-      kk[u] = 0xFFFFFFFFu;
-      ix[u] = 0;
-      if (j < h.nb) {
-        while (p + 1 < (uint32_t)kRadixBlocks && cexcl[p + 1] <= j) ++p;
-        const uint2 e = kv[csrc[p] + (j - cexcl[p])];
-        kk[u] = e.x - h.k0;
-        ix[u] = e.y;
-      }
+  for (int u = 0; u < kIPT; ++u) {
+    const uint32_t j = threadIdx.x + (uint32_t)u * kBlock;
+    kk[u] = 0xFFFFFFFFu;
+    ix[u] = 0;
+    if (j < h.nb) {
+      const uint32_t p = chunk_of(cexcl, j);
+      const uint2 e = kv[csrc[p] + (j - cexcl[p])];
+      kk[u] = e.x - h.k0;
+      ix[u] = e.y;
     }
   }
+
 #pragma unroll
   for (int u = 0; u < kIPT; ++u)
     if (kk[u] != 0xFFFFFFFFu) load_rec(batch + ix[u], rec[u]);  // issued before the LDS work below

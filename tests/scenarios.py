@@ -89,11 +89,12 @@ def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_
     return out
 
 
-def run_heavy(binding, seed: int):
+def run_heavy(binding, seed: int, n_inst: int = 64):
     """One sender with a long backlog (token-bucket segment > LDS tile) and one receiver with a large
-    inbox (delivery segment > LDS tile): exercises the merge-path large-segment paths."""
+    inbox (delivery segment > LDS tile): exercises the merge-path large-segment paths. With more
+    instances than one fused bucket holds, the heavy bucket takes the global form next to normal
+    buckets (the segment boundary between them is written by the oversized one)."""
     rng = np.random.default_rng(seed)
-    n_inst = 64
     sim = Simulator(SimConfig(n_instances=n_inst, seed=seed), binding=binding)
     for g in range(n_inst):
         sim.set_shape(g, make_shape(latency_ns=10 * MS, jitter_ns=int(rng.choice([0, 5 * MS])),

@@ -22,8 +22,9 @@ def test_random_windows_small_wheel(hip, oracle):
     S.assert_same(S.run_random(hip, 11, cfg_kw=kw), S.run_random(oracle, 11, cfg_kw=kw))
 
 
-def test_large_segments(hip, oracle):
-    S.assert_same(S.run_heavy(hip, 7), S.run_heavy(oracle, 7))
+@pytest.mark.parametrize("n_inst", [64, 200, 1000])
+def test_large_segments(hip, oracle, n_inst):
+    S.assert_same(S.run_heavy(hip, 7, n_inst), S.run_heavy(oracle, 7, n_inst))
 
 
 def test_sync_service(hip, oracle):
