@@ -1410,7 +1410,8 @@ constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
 constexpr uint32_t kBktRankMax = 64;  // longest key run ranked in LDS
 constexpr int kIPT = kBktCap / kBlock;  // items per thread
 
-constexpr uint32_t kStageN = 1024;  // records staged per round for the coalesced output (k1 + k2 area)
+constexpr uint32_t kStageN = 1280;  // records staged per round for the coalesced output (k1 + k2 + k3 area:
+                                    // a storm bucket of ~1.1k copies leaves in one round)
 
 struct BktFusedSmem {
   uint32_t cnt[1u << kBktFusedKeyBits];  // per key: run start, then run end (relative to the bucket)
@@ -1620,7 +1621,8 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
 }
 
 static_assert(offsetof(BktFusedSmem, k2) == offsetof(BktFusedSmem, k1) + 8 * kBktCap &&
-                  32 * kStageN <= 16 * kBktCap, "output staging uses the k1 + k2 area");
+                  offsetof(BktFusedSmem, k3) == offsetof(BktFusedSmem, k2) + 8 * kBktCap &&
+                  32 * kStageN <= 20 * kBktCap, "output staging uses the k1 + k2 + k3 area");
 
 // length of the run of the key owning LDS slot s
 __device__ __forceinline__ uint32_t run_len(const BktFusedSmem& sm, uint32_t s) {
