@@ -132,6 +132,7 @@ def cpu_baseline(args, shapes):
 
 
 PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
+PMC_TRAFFIC_FLOOD = "profiles/r01/pmc_traffic_flood.json"
 
 
 def main():
@@ -464,6 +465,12 @@ def main_flood(args):
     bytes_total = BYTE_MODELS[dominant](delta)
     avg_ms = kern_ms / max(kern_n, 1)
     achieved = (bytes_total / max(kern_n, 1)) / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, PMC_TRAFFIC_FLOOD)
+    if os.path.exists(pmc):
+        k = json.load(open(pmc))["kernels"].get(dominant)
+        if k:
+            traffic, traffic_src = k["traffic_bytes"], PMC_TRAFFIC_FLOOD
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = flood_cpu_baseline(args, shapes, graph)
@@ -481,8 +488,8 @@ def main_flood(args):
                        "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
                        "delivered_in_timed_steps": delivered},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "avg_launch_ms": avg_ms, "bytes_per_launch": bytes_total / max(kern_n, 1)},
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src, "avg_launch_ms": avg_ms, "bytes_per_launch": bytes_total / max(kern_n, 1)},
             "cpu_baseline": cpu,
             "kernels_probe": warm_kernels,
         }), flush=True)
