@@ -221,7 +221,7 @@ __device__ __forceinline__ void window_start_block(const WindowArgs& a) {
   const int64_t t_end_arg = a.t_end_arg, offset = a.offset, slot_ns = a.slot_ns;
   const int64_t* src = a.src;
   __shared__ int64_t s_tend;
-  for (uint32_t i = threadIdx.x; i < 3u * kNSub * 32u; i += kBlock) qc[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 3u * kNSub; i += kBlock) qc[i << 5] = 0;  // one counter per 128-B line
   uint32_t* w = sc->q;  // the per-window block [q, err) of DevScalars
   const uint32_t nw = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
   for (uint32_t i = threadIdx.x; i < nw; i += kBlock) w[i] = 0;
