@@ -2304,7 +2304,8 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint
 struct StormArgs {
   uint32_t lo, nloc, N, round;
   int64_t t0;
-  uint32_t F, Fp, size;
+  uint32_t F, Fp, fp_log2, size;
+  uint32_t peer_m, peer_sh1, peer_sh2;  // u % (N - 1) by 32-bit multiply-shift (exact for every u32)
   int64_t spread;
   uint64_t spread_m;         // u % spread by multiply-shift (Granlund-Montgomery, exact for every u)
   uint32_t spread_sh1, spread_sh2;
@@ -2324,6 +2325,13 @@ __device__ __forceinline__ uint64_t spread_mod(const StormArgs& a, uint64_t u) {
   return u - q * (uint64_t)a.spread;
 }
 
+// The peer draw out[0] % (N - 1), the same construction at 32 bits (no emulated integer division).
+__device__ __forceinline__ uint32_t peer_mod(const StormArgs& a, uint32_t u) {
+  const uint32_t t = __umulhi(a.peer_m, u);
+  const uint32_t q = (t + ((u - t) >> a.peer_sh1)) >> a.peer_sh2;
+  return u - q * (a.N - 1);
+}
+
 // One storm round: every instance sends F messages to F distinct random peers and signals `state`
 // at its latest send time. A group of Fp (power of two >= F) lanes per instance, one message per
 // lane. Peer k is the first Philox draw of (g, round, k) unless it repeats one of the k earlier
@@ -2339,7 +2347,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
   int64_t mn = INT64_MAX, mx = INT64_MIN;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += gridDim.x * kBlock) {  // block-uniform loop
     const uint32_t tid = b0 + threadIdx.x;
-    const uint32_t l = tid / a.Fp, k = tid % a.Fp;
+    const uint32_t l = tid >> a.fp_log2, k = tid & (a.Fp - 1u);
     const uint32_t lane = lane_id(), gbase = lane - k;
     const bool inst = l < a.nloc, msg = inst && k < a.F;
     const uint32_t g = a.lo + l;
@@ -2350,7 +2358,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
       philox4x32_10(g, a.round, k << 16, kStormSalt, a.key0, a.key1, out);
       const uint64_t u = ((uint64_t)out[2] << 32) | out[1];
       t = t0 + (a.spread > 0 ? (int64_t)spread_mod(a, u) : 0);
-      p = out[0] % (a.N - 1);
+      p = peer_mod(a, out[0]);
       if (p >= g) ++p;
     }
     bool dup = false;
@@ -2371,7 +2379,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
           if (again) {
             uint32_t out[4];
             philox4x32_10(g, a.round, (k << 16) | ++attempt, kStormSalt, a.key0, a.key1, out);
-            p = out[0] % (a.N - 1);
+            p = peer_mod(a, out[0]);
             if (p >= g) ++p;
           }
         }
@@ -2770,6 +2778,15 @@ static void storm_divisor(int64_t d, uint64_t& m, uint32_t& sh1, uint32_t& sh2) 
   sh2 = l > 1 ? l - 1 : 0;
 }
 
+// The same at 32 bits for the peer draw (d = N - 1 >= 1): m = floor(2^32 (2^l - d) / d) + 1 < 2^32.
+static void peer_divisor(uint32_t d, uint32_t& m, uint32_t& sh1, uint32_t& sh2) {
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;
+  m = (uint32_t)((((unsigned __int128)1 << 32) * ((1ull << l) - d)) / d + 1);
+  sh1 = l < 1 ? l : 1;
+  sh2 = l > 1 ? l - 1 : 0;
+}
+
 // k_gen_storm only: the batch's per-block partials wait in sig_part for launch_sig_commit (the
 // runtime defers it so that a barrier registered next rides in the same launch). *nparts = grid.
 hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
@@ -2777,8 +2794,9 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   ProfScope ps_(d, KID_GEN);
   StormArgs a;
   a.lo = d.lo; a.nloc = d.nloc; a.N = d.N; a.round = round; a.t0 = t0; a.F = fanout;
-  a.Fp = 1;
-  while (a.Fp < fanout) a.Fp <<= 1;
+  a.Fp = 1; a.fp_log2 = 0;
+  while (a.Fp < fanout) { a.Fp <<= 1; ++a.fp_log2; }
+  peer_divisor(d.N > 1 ? d.N - 1 : 1, a.peer_m, a.peer_sh1, a.peer_sh2);
   a.size = size; a.spread = spread_ns; a.key0 = d.key0;
   storm_divisor(spread_ns, a.spread_m, a.spread_sh1, a.spread_sh2); a.key1 = d.key1; a.base = staged_base;
   a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;

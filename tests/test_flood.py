@@ -166,6 +166,9 @@ def test_flood_sharded_hip(hip, oracle, world):
         for q in range(len(sims)):
             for p in range(len(sims)):
                 assert hiprt.hipMemcpy(bufs[p][1] + q * blk, bufs[q][0] + p * blk, blk, 3) == 0
+        # hipMemcpy D2D may return before the copy completes, and the contexts' streams are
+        # non-blocking: finish the copies before any context reads its receive blocks
+        assert hiprt.hipDeviceSynchronize() == 0
 
     n = 900
     got = S.run_flood_sharded(lambda c: Simulator(c), exchange, world, n_inst=n)

@@ -80,6 +80,9 @@ def test_sharded_on_one_device(hip, oracle, world, seed):
         for q in range(n):
             for p in range(n):
                 assert hiprt.hipMemcpy(bufs[p][1] + q * blk, bufs[q][0] + p * blk, blk, D2D) == 0
+        # hipMemcpy D2D may return before the copy completes, and the contexts' streams are
+        # non-blocking: finish the copies before any context reads its receive blocks
+        assert hiprt.hipDeviceSynchronize() == 0
 
     outs, srcs = S.run_random_sharded(make, exchange, world, seed)
     S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
