@@ -2118,11 +2118,176 @@ __global__ __launch_bounds__(kBlock) void k_sig_commit(SigState g, uint32_t npar
 
 // The storm step's deferred commit + barrier registration and the window start that waits on that
 // barrier, in one single-block launch (the window end is the waiter's release, resolved here).
+// The same work as sig_commit_block + window_start_block, with the chain of dependent global round
+// trips cut from ~16 to ~4: every load that nothing in this launch writes first is issued at entry
+// (batch partials, the state's count / last / chunk count, the old waiters' releases, the window
+// and region-ring scalars), each live region's fields one round trip later (overlapping the
+// commit), the registered waiter's release is computed from the new chunk in registers, and the
+// retired prefix of the region ring is found in parallel (thread 0 walked it). More than kBlock
+// live regions or waiters take the general chain.
 __global__ __launch_bounds__(kBlock) void k_window_start_commit(SigState g, uint32_t nparts, uint32_t n, uint32_t st,
                                                                 uint32_t nw, WaiterAdd wa, WindowArgs w) {
-  sig_commit_block(g, nparts, 1u, n, st, nw, wa);
-  __syncthreads();  // the waiter's release (written by some thread of this block) is visible
-  window_start_block(w);
+  DevScalars* sc = w.sc;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tail = sc->reg_tail, head = sc->reg_head, nlive = head - tail;
+  const int64_t H0 = sc->T, T0 = sc->t_end;
+  const uint64_t arena_head0 = sc->arena_head, arena_used0 = sc->arena_used;
+  const uint32_t nw_old = nw;
+  if (nlive > (uint32_t)kBlock || nw_old >= (uint32_t)kBlock) {  // block-uniform: the general chain
+    sig_commit_block(g, nparts, 1u, n, st, nw, wa);
+    __syncthreads();  // the waiter's release (written by some thread of this block) is visible
+    window_start_block(w);
+    return;
+  }
+  uint32_t cnt0 = 0, nch0 = 0;
+  int64_t last0 = 0;
+  if (tid == 0) { cnt0 = g.count[st]; last0 = g.last[st]; nch0 = g.nchunks[st]; }
+  const int64_t rel_old = tid < nw_old ? g.w_release[tid] : 0;
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  for (uint32_t i = tid; i < nparts; i += kBlock) {
+    const int64_t a = g.part[2 * i], b = g.part[2 * i + 1];
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  RegionDev* rp = nullptr;
+  uint32_t r_cons = 0, r_n = 0, r_dir = 0;
+  int64_t r_base = 0;
+  uint64_t r_aoff = 0;
+  if (tid < nlive) {
+    rp = &w.regions[(tail + tid) % kMaxRegions];
+    r_cons = rp->consumed; r_n = rp->n; r_base = rp->base_slot; r_dir = rp->dir; r_aoff = rp->arena_off;
+  }
+  // the per-window counters (nothing below reads them before the barriers)
+  for (uint32_t i = tid; i < 3u * kNSub; i += kBlock) w.qc[i << 5] = 0;
+  {
+    uint32_t* wb = sc->q;
+    const uint32_t nwb = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
+    for (uint32_t i = tid; i < nwb; i += kBlock) wb[i] = 0;
+  }
+  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
+  __shared__ int64_t s_tend;
+  __shared__ uint32_t s_open;
+  __shared__ uint32_t s_part[kBlock / 64];
+  __shared__ unsigned long long s_freed[kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((tid & 63) == 0) { smin[tid >> 6] = mn; smax[tid >> 6] = mx; }
+  __syncthreads();
+  bool fast_rel = false;  // thread 0: the window's waiter is the one registered here, resolved in registers
+  int64_t rel_new = -1;
+  if (tid == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
+    g.red[0] = mn;
+    g.red[3] = mx;
+    bool chunk_ok = false;
+    if (n) {  // sig_commit_count on the preloaded state
+      if (cnt0 > 0 && mn < last0) atomicOr(&sc->err, ERR_SIG_ORDER);
+      if (nch0 >= (uint32_t)kMaxChunksPerState) {
+        atomicOr(&sc->err, ERR_STATE_CHUNKS);
+      } else {
+        SigChunk ch;
+        ch.seq_start = cnt0 + 1u; ch.len = n; ch.log_pos = 0;
+        ch.tmin = mn; ch.tmax = mx; ch.sorted = 0; ch.pad = 0;
+        g.chunks[(size_t)st * kMaxChunksPerState + nch0] = ch;
+        g.nchunks[st] = nch0 + 1;
+        chunk_ok = true;
+      }
+      g.count[st] = cnt0 + n;
+      g.last[st] = mx;
+    }
+    if (wa.on) {
+      const int64_t tw = wa.t_wait == INT64_MIN ? T0 : wa.t_wait;
+      wa.w_state[nw_old] = wa.state; wa.w_target[nw_old] = wa.target; wa.w_twait[nw_old] = tw;
+      // resolve_waiter's answer where it follows from this commit alone; otherwise the general path
+      const uint32_t tg = wa.target, cnt1 = cnt0 + n;
+      bool known = false;
+      if (tg == 0) {
+        rel_new = tw; known = true;
+      } else if (wa.state == st && n) {
+        if (cnt1 < tg) {
+          known = true;
+        } else if (tg > cnt0) {  // inside the new chunk
+          known = true;
+          if (chunk_ok) {
+            if (tg == cnt1) rel_new = mx > tw ? mx : tw;
+            else if (tg == cnt0 + 1u) rel_new = mn > tw ? mn : tw;
+            else atomicOr(&sc->err, ERR_UNSORTED_TARGET);
+          }
+        }
+      }
+      g.w_release[nw_old] = known ? rel_new : -1;
+      if (!known) resolve_waiter(g, nw_old);
+      fast_rel = known && w.mode == WIN_BARRIER && w.src == g.w_release + nw_old;
+    }
+  }
+  __syncthreads();  // the commit is visible to the old waiters' resolution
+  if (tid < nw_old && rel_old < 0) resolve_waiter(g, tid);
+  __syncthreads();  // every release is written
+  if (tid == 0) {
+    int64_t e = w.t_end_arg;
+    if (w.mode == WIN_BARRIER) {
+      const int64_t rel = fast_rel ? rel_new : *w.src;
+      if (rel < 0) {
+        atomicOr(&sc->err, ERR_UNRELEASED);
+        e = T0;
+      } else {
+        e = rel + w.offset;
+      }
+    } else if (w.mode == WIN_DEVICE) {
+      e = *w.src + w.offset;
+    }
+    e = e < T0 ? T0 : e;
+    sc->H = H0;
+    sc->T = T0;
+    sc->t_end = e;
+    sc->base_slot = e / w.slot_ns;
+    s_tend = e;
+    s_open = nlive;
+  }
+  __syncthreads();
+  // the extraction plan (plan_regions with the region fields already in registers)
+  const int64_t t_end = s_tend;
+  const int64_t kabs = t_end > 0 ? (t_end - 1) / w.slot_ns : -1;
+  uint32_t len = 0;
+  if (tid < nlive) {
+    const uint32_t start = r_cons;
+    uint32_t hi = start;
+    if (kabs >= 0) {
+      const int64_t krel = kabs - r_base;
+      if (krel >= (int64_t)w.slots - 1) hi = r_n;
+      else if (krel >= 0) hi = w.dirs[(size_t)r_dir * (w.slots + 1) + (uint32_t)krel + 1];
+    }
+    if (hi < start) hi = start;
+    len = hi - start;
+    rp->consumed = hi;
+    w.plan_start[tid] = start;
+    if (hi != r_n) atomicMin(&s_open, tid);
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan(len, s_part, total);  // its barriers also publish s_open
+  if (tid < nlive) w.plan_off[tid] = ex;
+  const uint32_t open = s_open;  // regions [0, open) of the ring are fully consumed: retired
+  unsigned long long fr = (tid < open) ? (unsigned long long)r_n : 0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) fr += __shfl_xor(fr, o);
+  if ((tid & 63) == 0) s_freed[tid >> 6] = fr;
+  __syncthreads();
+  if (tid == open && open < nlive) sc->arena_tail = r_aoff;
+  if (tid == 0) {
+    unsigned long long freed = 0;
+    for (int k = 0; k < kBlock / 64; ++k) freed += s_freed[k];
+    w.plan_off[nlive] = total;
+    sc->n_extract = total;
+    sc->plan_tail = tail;
+    sc->plan_n = nlive;
+    sc->reg_tail = tail + open;
+    sc->arena_used = arena_used0 - freed;
+    if (open == nlive) sc->arena_tail = arena_head0;
+  }
 }
 
 // Count-only batch (one state, no sequence numbers): min and max time, then the commit.
