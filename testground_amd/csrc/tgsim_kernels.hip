@@ -755,8 +755,8 @@ constexpr int kBktUnroll = 8;
 // pass 1: per-block bucket histogram. The first block also closes the queue (prefix over its
 // sub-queues, totals, overflow bit: the former k_qfinal) and, for the wheel batch, allocates the
 // window's region (the former k_region_alloc).
-__global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
-                                                     uint32_t* hist) {
+__device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc, const BktDiv& bd, uint32_t B,
+                                              uint32_t* hist) {
   __shared__ uint32_t h[kMaxBins];
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) h[d] = 0;
   if (blockIdx.x == 0) {
@@ -787,6 +787,11 @@ __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc,
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
+}
+
+__global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
+                                                     uint32_t* hist) {
+  bkt_hist_body(src, sc, bd, B, hist);
 }
 
 // Element range of partition block p (as bkt_block_range for blockIdx.x == p).
@@ -2403,13 +2408,13 @@ __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, con
 }
 
 template <class P>
-__global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
-                                                 const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
-                                                 uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b,
-                                                 uint64_t* K2b, uint32_t* K3b) {
+__device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
+                                          const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
+                                          uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b, uint64_t* K2b,
+                                          uint32_t* K3b, uint32_t bid, uint32_t nblocks) {
   __shared__ SortSmem s;
   const uint32_t nm = sc->n_medium, nl = sc->n_large;
-  for (uint32_t w = blockIdx.x; w < nm + nl; w += gridDim.x) {
+  for (uint32_t w = bid; w < nm + nl; w += nblocks) {
     if (w < nm) {
       const uint32_t g = medium[w];
       const uint32_t a = off[g], m = off[g + 1] - a;
@@ -2424,6 +2429,31 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
     }
     __syncthreads();
   }
+}
+
+template <class P>
+__global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
+                                                 const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
+                                                 uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b,
+                                                 uint64_t* K2b, uint32_t* K3b) {
+  rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x, gridDim.x);
+}
+
+// Window end: the deliveries' long inboxes (k_rest<Emit>) and the wheel insert's histogram pass are
+// independent (one writes the outputs from D, the other reads L), so they share one launch: blocks
+// [0, kRadixBlocks) are k_bkt_hist's, the rest k_rest's. A launch that finds nothing to do still
+// costs ~4.5 us at a dependent-launch boundary.
+__global__ __launch_bounds__(kBlock) void k_wheel_hist_rest(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
+                                                            uint32_t* hist, EmitPolicy p, const uint32_t* keys,
+                                                            const uint32_t* vals, const uint32_t* off,
+                                                            const uint32_t* medium, const LargeSeg* large,
+                                                            uint64_t* K1a, uint64_t* K2a, uint32_t* K3a,
+                                                            uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
+  if (blockIdx.x < (uint32_t)kRadixBlocks)
+    bkt_hist_body(src, sc, bd, B, hist);
+  else
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - kRadixBlocks,
+              gridDim.x - kRadixBlocks);
 }
 
 // ============================================================================================
@@ -2817,11 +2847,9 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
 }
 
 // Deliveries: partition the due copies by receiver bucket, then one workgroup per bucket orders
-// each inbox and writes it as SoA (k_emit_bucket); long inboxes finish in k_rest.
-static hipError_t run_wheel_insert(Dev& d, hipStream_t st);
-
-static hipError_t run_deliveries(Dev& d) {
-  EmitPolicy p;
+// each inbox and writes it as SoA (k_emit_bucket); long inboxes finish in k_rest<Emit>, which rides
+// in the wheel insert's histogram launch (k_wheel_hist_rest).
+static hipError_t run_deliveries(Dev& d, EmitPolicy& p) {
   p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
@@ -2833,17 +2861,20 @@ static hipError_t run_deliveries(Dev& d) {
     hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, src, d.poff, d.kv1, d.keys2,
                        d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc);
   }
-  TG_CHECK(hipGetLastError());
-  return launch_rest(d, p, d.keys0, d.vals0);
+  return hipGetLastError();
 }
 
-// Wheel insert: one partition pass with buckets = slots; records go straight into the arena.
-static hipError_t run_wheel_insert(Dev& d, hipStream_t st) {
+// Wheel insert: one partition pass with buckets = slots; records go straight into the arena. The
+// histogram launch also finishes the deliveries' long inboxes (p).
+static hipError_t run_wheel_insert(Dev& d, hipStream_t st, const EmitPolicy& p) {
   const BktSrc src = bkt_queue(d, Q_L);
   {
     ProfScope ps_(d, KID_BKT_HIST, st);
-    hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, st, src, d.sc, bkt_div(1), d.slots, d.hist);
+    hipLaunchKernelGGL(k_wheel_hist_rest, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, st, src, d.sc,
+                       bkt_div(1), d.slots, d.hist, p, d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.K1a, d.K2a,
+                       d.K3a, d.K1b, d.K2b, d.K3b);
   }
+  TG_CHECK(hipGetLastError());
   {
     ProfScope ps_(d, KID_RADIX_ROWS, st);
     hipLaunchKernelGGL(k_radix_rows, dim3(d.slots), dim3(kRadixBlocks), 0, st, d.hist, d.tot);
@@ -2863,8 +2894,9 @@ hipError_t window_end(Dev& d) {
     hipLaunchKernelGGL(k_recv, dim3(grid_for(total)), dim3(kBlock), 0, d.stream, d.xrecv, d.S, d.shard, d.xcap, Q);
     TG_CHECK(hipGetLastError());
   }
-  TG_CHECK(run_deliveries(d));
-  return run_wheel_insert(d, d.stream);  // k_wheel_scatter also closes the window's counters
+  EmitPolicy p;
+  TG_CHECK(run_deliveries(d, p));
+  return run_wheel_insert(d, d.stream, p);  // k_wheel_scatter also closes the window's counters
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
