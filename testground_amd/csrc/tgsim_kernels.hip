@@ -407,13 +407,13 @@ __device__ __forceinline__ int qid_copy(const Geo& geo, const tgsim_record& r, i
   return r.t < t_end ? Q_A : Q_L;
 }
 
-__global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
+__device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uint32_t nblocks) {
   DevScalars* sc = a.Q.sc;
   const int64_t H = sc->H, t_end = sc->t_end;
   uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t stride = nblocks * blockDim.x;
   uint32_t it = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride, ++it) {
+  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < a.n; i += stride, ++it) {
     // Every load of this message is issued up front with clamped indices, so the wave pays one
     // round trip for the SoA record and one for the table gathers instead of a branch-serialised chain.
     const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
@@ -513,6 +513,8 @@ __global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) {
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) { shape_body(a, blockIdx.x, gridDim.x); }
+
 // ============================================================================================
 // timing wheel: plan (which slot prefixes of which live regions are due), extract, insert
 // ============================================================================================
@@ -573,9 +575,9 @@ constexpr int kExtractUnroll = 4;     // records in flight per thread
 // plan (each live region's due prefix and its place in the output) is staged in LDS, so locating
 // a record costs no global round trip; kExtractUnroll records per thread are loaded before the
 // wave appends.
-__global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, const uint32_t* plan_start,
-                                                    const uint32_t* plan_off, const tgsim_record* arena,
-                                                    Queues Q) {
+__device__ __forceinline__ void extract_body(const RegionDev* regions, const uint32_t* plan_start,
+                                             const uint32_t* plan_off, const tgsim_record* arena, const Queues& Q,
+                                             uint32_t bid, uint32_t nblocks) {
   __shared__ uint32_t s_off[kPlanLds];
   __shared__ uint64_t s_src[kPlanLds];
   DevScalars* sc = Q.sc;
@@ -589,9 +591,9 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
     }
     __syncthreads();
   }
-  const uint32_t step = gridDim.x * kBlock * kExtractUnroll;
+  const uint32_t step = nblocks * kBlock * kExtractUnroll;
   uint32_t it = 0;
-  for (uint32_t base = blockIdx.x * kBlock * kExtractUnroll; base < total; base += step, ++it) {  // block-uniform
+  for (uint32_t base = bid * kBlock * kExtractUnroll; base < total; base += step, ++it) {  // block-uniform
     tgsim_record rec[kExtractUnroll];
 #pragma unroll
     for (int u = 0; u < kExtractUnroll; ++u) {
@@ -621,6 +623,23 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
       Q.push(q, rec[u], it * kExtractUnroll + u);
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, const uint32_t* plan_start,
+                                                    const uint32_t* plan_off, const tgsim_record* arena,
+                                                    Queues Q) {
+  extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, gridDim.x);
+}
+
+// The wheel extraction and netem of the staged messages are independent (both only append to the
+// A / D / L queues, through reservations), so a window with staged messages runs them as one
+// launch: blocks [0, ne) extract, the rest shape. ne is a multiple of 8, so every block keeps the
+// XCD (blockIdx mod 8) its sub-queue choice assumes.
+__global__ __launch_bounds__(kBlock) void k_extract_shape(const RegionDev* regions, const uint32_t* plan_start,
+                                                          const uint32_t* plan_off, const tgsim_record* arena,
+                                                          Queues Q, ShapeArgs a, uint32_t ne) {
+  if (blockIdx.x < ne) extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, ne);
+  else shape_body(a, blockIdx.x - ne, gridDim.x - ne);
 }
 
 // Allocate this window's region in the arena ring (one thread).
@@ -2819,7 +2838,7 @@ hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
 
 hipError_t window_begin(Dev& d, uint32_t n_staged) {
   Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
-  {
+  if (!n_staged) {
     ProfScope ps_(d, KID_EXTRACT);
     hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
                        d.plan_off, d.arena, Q);
@@ -2834,7 +2853,12 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
-    { ProfScope ps_(d, KID_SHAPE); hipLaunchKernelGGL(k_shape, dim3(g), dim3(kBlock), 0, d.stream, a); }
+    static_assert(kStreamBlocks % 8 == 0, "extract blocks keep their XCD");
+    {
+      ProfScope ps_(d, KID_SHAPE);  // extraction + netem
+      hipLaunchKernelGGL(k_extract_shape, dim3(kStreamBlocks + g), dim3(kBlock), 0, d.stream, d.regions,
+                         d.plan_start, d.plan_off, d.arena, Q, a, (uint32_t)kStreamBlocks);
+    }
     TG_CHECK(hipGetLastError());
     if (d.any_corr) TG_CHECK(run_shape_corr(d, a, n_staged));
   }
