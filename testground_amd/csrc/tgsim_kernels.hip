@@ -691,9 +691,9 @@ __device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_
 }
 
 // one block per digit: exclusive scan of that digit's per-block counts, digit total to tot[d]
-__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uint32_t* tot) {
+__device__ __forceinline__ void radix_rows_body(uint32_t* hist, uint32_t* tot, uint32_t d) {
   __shared__ uint32_t ws[kRadixBlocks / 64];
-  const uint32_t d = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t v = hist[d * kRadixBlocks + t];
   uint32_t x = v;
 #pragma unroll
@@ -707,6 +707,10 @@ __global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uin
   for (uint32_t w = 0; w < wave; ++w) pre += ws[w];
   hist[d * kRadixBlocks + t] = pre + x - v;
   if (t == kRadixBlocks - 1) tot[d] = pre + x;
+}
+
+__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uint32_t* tot) {
+  radix_rows_body(hist, tot, blockIdx.x);
 }
 
 __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, const uint32_t* n_ptr, uint32_t kmin,
@@ -757,12 +761,15 @@ struct BktSrc {
 static_assert(kRadixBlocks == 4 * kNSub, "partition blocks map onto sub-queue quarters");
 
 // This block's element range [start, end) in the physical index space of the source.
-__device__ __forceinline__ void bkt_block_range(const BktSrc& s, uint32_t& start, uint32_t& end) {
+// bid: the partition block (blockIdx.x unless the pass shares its launch; queue mode only then)
+__device__ __forceinline__ void bkt_block_range(const BktSrc& s, uint32_t& start, uint32_t& end,
+                                                uint32_t bid = 0xFFFFFFFFu) {
   if (s.mode == 3) {
     radix_range(clamp_n(s.n_ptr, s.cap), start, end);
     return;
   }
-  const uint32_t sub = blockIdx.x >> 2, part = blockIdx.x & 3;
+  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
+  const uint32_t sub = bid >> 2, part = bid & 3;
   uint32_t c = s.qc[((uint32_t)s.q * kNSub + sub) << 5];
   c = c < s.subcap ? c : s.subcap;
   start = sub * s.subcap + (uint32_t)(((uint64_t)c * part) >> 2);
@@ -775,10 +782,10 @@ constexpr int kBktUnroll = 8;
 // sub-queues, totals, overflow bit: the former k_qfinal) and, for the wheel batch, allocates the
 // window's region (the former k_region_alloc).
 __device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc, const BktDiv& bd, uint32_t B,
-                                              uint32_t* hist) {
+                                              uint32_t* hist, uint32_t bid) {
   __shared__ uint32_t h[kMaxBins];
   for (uint32_t d = threadIdx.x; d < B; d += kBlock) h[d] = 0;
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     // the segment lists belong to the group-bys; the wheel insert (Q_L) leaves them alone
     const bool wheel = src.mode != 3 && src.q == Q_L;
     if (threadIdx.x == 0 && !wheel) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
@@ -792,7 +799,7 @@ __device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc,
   }
   __syncthreads();
   uint32_t start, end;
-  bkt_block_range(src, start, end);
+  bkt_block_range(src, start, end, bid);
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll];
 #pragma unroll
@@ -805,12 +812,12 @@ __device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc,
       if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[bd.of(k[u])], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + blockIdx.x] = h[d];
+  for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + bid] = h[d];
 }
 
 __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
                                                      uint32_t* hist) {
-  bkt_hist_body(src, sc, bd, B, hist);
+  bkt_hist_body(src, sc, bd, B, hist, blockIdx.x);
 }
 
 // Element range of partition block p (as bkt_block_range for blockIdx.x == p).
@@ -829,8 +836,8 @@ __device__ __forceinline__ void bkt_range_of(const BktSrc& s, uint32_t p, uint32
 // one XCD's L2). The consumer of bucket b finds its items as 256 chunks and its global start as
 // sum_p poff[p][b] (every block's offsets are prefix sums of its own counts). The first block
 // also closes the queue (queue_final) and resets the segment lists.
-__global__ __launch_bounds__(kBlock) void k_bkt_local(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
-                                                      uint2* kv, uint32_t* poff) {
+__device__ __forceinline__ void bkt_local_body(const BktSrc& src, DevScalars* sc, const BktDiv& bd, uint32_t B,
+                                               uint2* kv, uint32_t* poff) {
   __shared__ uint32_t h[kMaxBins + 1];
   __shared__ uint32_t red[kBlock / 64];
   for (uint32_t d = threadIdx.x; d <= B; d += kBlock) h[d] = 0;
@@ -882,6 +889,21 @@ __global__ __launch_bounds__(kBlock) void k_bkt_local(BktSrc src, DevScalars* sc
       kv[pos] = make_uint2(k[u], j0 + u * kBlock);
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bkt_local(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
+                                                      uint2* kv, uint32_t* poff) {
+  bkt_local_body(src, sc, bd, B, kv, poff);
+}
+
+// Window end, first pass: the deliveries' partition (blocks [0, kRadixBlocks), k_bkt_local on D)
+// and the wheel insert's histogram (the next kRadixBlocks, k_bkt_hist on L) read different queues
+// and write different buffers, so they share one launch.
+__global__ __launch_bounds__(kBlock) void k_local_hist(BktSrc srcD, DevScalars* sc, BktDiv bdD, uint32_t BD,
+                                                       uint2* kv, uint32_t* poff, BktSrc srcL, BktDiv bdL,
+                                                       uint32_t BL, uint32_t* hist) {
+  if (blockIdx.x < (uint32_t)kRadixBlocks) bkt_local_body(srcD, sc, bdD, BD, kv, poff);
+  else bkt_hist_body(srcL, sc, bdL, BL, hist, blockIdx.x - kRadixBlocks);
 }
 
 // Bucket bases for this block: exclusive scan of the bucket totals + this block's offset in each.
@@ -2458,21 +2480,21 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
   rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x, gridDim.x);
 }
 
-// Window end: the deliveries' long inboxes (k_rest<Emit>) and the wheel insert's histogram pass are
-// independent (one writes the outputs from D, the other reads L), so they share one launch: blocks
-// [0, kRadixBlocks) are k_bkt_hist's, the rest k_rest's. A launch that finds nothing to do still
-// costs ~4.5 us at a dependent-launch boundary.
-__global__ __launch_bounds__(kBlock) void k_wheel_hist_rest(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
-                                                            uint32_t* hist, EmitPolicy p, const uint32_t* keys,
-                                                            const uint32_t* vals, const uint32_t* off,
-                                                            const uint32_t* medium, const LargeSeg* large,
-                                                            uint64_t* K1a, uint64_t* K2a, uint32_t* K3a,
-                                                            uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
-  if (blockIdx.x < (uint32_t)kRadixBlocks)
-    bkt_hist_body(src, sc, bd, B, hist);
+// Window end, third pass: the deliveries' long inboxes (k_rest<Emit>, after k_emit_bucket) and the
+// wheel insert's per-slot scans (k_radix_rows, after the histogram) are independent, so they share
+// one launch: blocks [0, nrows) scan slot rows, the rest are k_rest's. A launch that finds nothing
+// to do still costs ~4.5 us at a dependent-launch boundary.
+__global__ __launch_bounds__(kBlock) void k_rows_rest(uint32_t* hist, uint32_t* tot, uint32_t nrows, EmitPolicy p,
+                                                      const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
+                                                      const uint32_t* medium, const LargeSeg* large,
+                                                      const DevScalars* sc, uint64_t* K1a, uint64_t* K2a,
+                                                      uint32_t* K3a, uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
+  static_assert(kRadixBlocks == kBlock, "slot rows are scanned by one kBlock workgroup each");
+  if (blockIdx.x < nrows)
+    radix_rows_body(hist, tot, blockIdx.x);
   else
-    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - kRadixBlocks,
-              gridDim.x - kRadixBlocks);
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - nrows,
+              gridDim.x - nrows);
 }
 
 // ============================================================================================
@@ -2870,47 +2892,11 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
   return hipSuccess;
 }
 
-// Deliveries: partition the due copies by receiver bucket, then one workgroup per bucket orders
-// each inbox and writes it as SoA (k_emit_bucket); long inboxes finish in k_rest<Emit>, which rides
-// in the wheel insert's histogram launch (k_wheel_hist_rest).
-static hipError_t run_deliveries(Dev& d, EmitPolicy& p) {
-  p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
-  p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
-  const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
-  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
-  const BktSrc src = bkt_queue(d, Q_D);
-  TG_CHECK(bkt_local(d, src, bd, B));
-  {
-    ProfScope ps_(d, KID_EMIT);
-    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, src, d.poff, d.kv1, d.keys2,
-                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc);
-  }
-  return hipGetLastError();
-}
-
-// Wheel insert: one partition pass with buckets = slots; records go straight into the arena. The
-// histogram launch also finishes the deliveries' long inboxes (p).
-static hipError_t run_wheel_insert(Dev& d, hipStream_t st, const EmitPolicy& p) {
-  const BktSrc src = bkt_queue(d, Q_L);
-  {
-    ProfScope ps_(d, KID_BKT_HIST, st);
-    hipLaunchKernelGGL(k_wheel_hist_rest, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, st, src, d.sc,
-                       bkt_div(1), d.slots, d.hist, p, d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.K1a, d.K2a,
-                       d.K3a, d.K1b, d.K2b, d.K3b);
-  }
-  TG_CHECK(hipGetLastError());
-  {
-    ProfScope ps_(d, KID_RADIX_ROWS, st);
-    hipLaunchKernelGGL(k_radix_rows, dim3(d.slots), dim3(kRadixBlocks), 0, st, d.hist, d.tot);
-  }
-  {
-    ProfScope ps_(d, KID_REGION_FILL, st);
-    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, st, src, d.sc, d.L, d.arena,
-                       d.dirs, d.slots, d.hist, d.tot);
-  }
-  return hipGetLastError();
-}
-
+// Window end: deliveries and the wheel insert of L, interleaved in four launches -
+//   k_local_hist   partition D by receiver bucket | histogram of L by wheel slot
+//   k_emit_bucket  one workgroup per receiver bucket: inbox order, SoA deliveries, inbox offsets
+//   k_rows_rest    per-slot scans of the L histogram | long inboxes of the deliveries
+//   k_wheel_scatter L straight into the arena in slot order (also closes the window's counters)
 hipError_t window_end(Dev& d) {
   if (d.S > 1) {
     Queues Q = make_queues(d);
@@ -2919,8 +2905,36 @@ hipError_t window_end(Dev& d) {
     TG_CHECK(hipGetLastError());
   }
   EmitPolicy p;
-  TG_CHECK(run_deliveries(d, p));
-  return run_wheel_insert(d, d.stream, p);  // k_wheel_scatter also closes the window's counters
+  p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
+  const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
+  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
+  const BktSrc srcD = bkt_queue(d, Q_D), srcL = bkt_queue(d, Q_L);
+  {
+    ProfScope ps_(d, KID_BKT_SCATTER);
+    hipLaunchKernelGGL(k_local_hist, dim3(2 * kRadixBlocks), dim3(kBlock), 0, d.stream, srcD, d.sc, bd, B, d.kv1,
+                       d.poff, srcL, bkt_div(1), d.slots, d.hist);
+  }
+  TG_CHECK(hipGetLastError());
+  {
+    ProfScope ps_(d, KID_EMIT);
+    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, srcD, d.poff, d.kv1, d.keys2,
+                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc);
+  }
+  TG_CHECK(hipGetLastError());
+  {
+    ProfScope ps_(d, KID_RADIX_ROWS);
+    hipLaunchKernelGGL(k_rows_rest, dim3(d.slots + kListBlocks), dim3(kBlock), 0, d.stream, d.hist, d.tot, d.slots,
+                       p, d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.sc, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b,
+                       d.K3b);
+  }
+  TG_CHECK(hipGetLastError());
+  {
+    ProfScope ps_(d, KID_REGION_FILL);
+    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L, d.arena,
+                       d.dirs, d.slots, d.hist, d.tot);
+  }
+  return hipGetLastError();
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
