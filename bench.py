@@ -32,17 +32,20 @@ METRIC = "simulated msgs delivered/sec (100k-inst storm) + % HBM roofline, 1/2/4
 
 # Algorithmic bytes each kernel class must move per unit of work; every class
 # below is exactly one kernel, so its HIP-event average agrees with rocprofv3's for that kernel.
-#   k_shape: read the 24 B message + write its 1 B status + write each 32 B copy record
+#   k_extract_shape (one launch, two passes): netem reads the 24 B message + writes its 1 B status
+#      + writes each 32 B copy record; the extraction reads + writes each due 32 B
+#     wheel record (k_extract alone when nothing is staged)
 #   k_tb_bucket: per copy, read the 32 B record + its 8 B (key, index), write the 32 B departed record
 #   k_emit_bucket: per delivery, read the 32 B record + 8 B (key, index), write the 32 B SoA delivery
-#   k_extract: read + write one 32 B wheel record; k_region_fill: read 32 + 8 B key/index, write 32 B
+#   k_extract: read + write one 32 B wheel record; k_wheel_scatter: read 32 + 8 B key/index, write 32 B
 #   k_gen_storm: write the 24 B message
 BYTE_MODELS = {
-    "k_shape": lambda d: 25 * d["msgs_in"] + 32 * d["copies"],
+    # extraction of due wheel records (64 B each) and netem of the staged messages share a launch
+    "k_extract_shape": lambda d: 25 * d["msgs_in"] + 32 * d["copies"] + 64 * d["extracted"],
     "k_tb_bucket": lambda d: 72 * d["tb_items"],
     "k_emit_bucket": lambda d: 72 * d["delivered"],
     "k_extract": lambda d: 64 * d["extracted"],
-    "k_region_fill": lambda d: 72 * d["inserted"],
+    "k_wheel_scatter": lambda d: 72 * d["inserted"],
     "k_gen_storm": lambda d: 24 * d["msgs_in"],
     # flood (config 5): count reads (dst, src, seq) and writes count + first flag per delivery;
     # emit writes the 24 B staged message per forward after re-reading the 17 B per delivery

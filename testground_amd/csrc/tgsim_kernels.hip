@@ -19,8 +19,8 @@
 namespace tgsim {
 
 const char* const kKernelNames[KID_COUNT] = {
-    "k_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
-    "k_keys", "k_bounds", "k_region_fill", "k_gen_storm", "sync_signal", "large_segments",
+    "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_rows_rest", "k_radix_scatter",
+    "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
     "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals

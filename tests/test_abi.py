@@ -47,7 +47,7 @@ def test_binding_covers_header():
     assert hip.version().decode().startswith("tgsim-mi355x")
     assert hip.abi_version() == 1
     names = [hip.kernel_name(k).decode() for k in range(hip.kernel_classes())]
-    assert "k_shape" in names and "k_emit_bucket" in names and "k_tb_bucket" in names
+    assert "k_extract_shape" in names and "k_emit_bucket" in names and "k_tb_bucket" in names
 
 
 def test_struct_layouts_match_header(tmp_path):
