@@ -9,8 +9,8 @@ mkdir -p $OUT
 B="bench.py --workload flood --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv \
   -- python3 -u $B --steps 20 --warmup 100 > $OUT/bench_under_rocprof.log 2>&1 || { echo PROF_FAIL; tail -20 $OUT/bench_under_rocprof.log; exit 1; }
-python3 tools/trace_summary.py $OUT/prof/run_kernel_trace.csv --last 20 > $OUT/trace_summary.txt 2>&1
-KR="k_tb_bucket|k_emit_bucket|k_shape|k_wheel_scatter|k_extract|k_flood|k_bkt"
+python3 tools/trace_summary.py $OUT/prof/run_kernel_trace.csv --last 20 --marker k_window_start > $OUT/trace_summary.txt 2>&1
+KR="k_tb_bucket|k_emit_bucket|k_extract_shape|k_wheel_scatter|k_extract|k_flood|k_bkt|k_local_hist"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_fetch -o run --output-format csv \
   -- python3 -u $B --steps 5 --warmup 100 > $OUT/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_write -o run --output-format csv \

@@ -18,7 +18,8 @@ def main():
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]))
     rows.sort()
     starts = [i for i, r in enumerate(rows) if a.marker in r[2]]
     if len(starts) > a.last:
