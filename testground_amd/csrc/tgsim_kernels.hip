@@ -2577,15 +2577,18 @@ __device__ __forceinline__ uint32_t peer_mod(const StormArgs& a, uint32_t u) {
 // against the final peers of the lanes before it. Stores are coalesced (message l*F + k at lane
 // l*Fp + k). The signals are reduced to per-block partials in the same launch (k_sig_commit
 // finishes them).
+// FIX != 0: fanout FIX = its power of two, known at compile time (the shuffle loops unroll); 0: any.
+template <uint32_t FIX>
 __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) {
+  const uint32_t F = FIX ? FIX : a.F, Fp = FIX ? FIX : a.Fp, fp_log2 = FIX ? (uint32_t)__builtin_ctz(FIX ? FIX : 1u) : a.fp_log2;
   const int64_t t0 = a.t0 == INT64_MIN ? sg.sc->t_end : a.t0;  // TGSIM_T_NOW: the device's window start
-  const uint32_t total = a.nloc * a.Fp;
+  const uint32_t total = a.nloc * Fp;
   int64_t mn = INT64_MAX, mx = INT64_MIN;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += gridDim.x * kBlock) {  // block-uniform loop
     const uint32_t tid = b0 + threadIdx.x;
-    const uint32_t l = tid >> a.fp_log2, k = tid & (a.Fp - 1u);
+    const uint32_t l = tid >> fp_log2, k = tid & (Fp - 1u);
     const uint32_t lane = lane_id(), gbase = lane - k;
-    const bool inst = l < a.nloc, msg = inst && k < a.F;
+    const bool inst = l < a.nloc, msg = inst && k < F;
     const uint32_t g = a.lo + l;
     uint32_t p = 0xFFFFFFFFu;
     int64_t t = t0;
@@ -2598,13 +2601,13 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
       if (p >= g) ++p;
     }
     bool dup = false;
-    for (uint32_t j = 0; j + 1 < a.F; ++j) {  // lane k compares its draw with lanes j < k of its group
+    for (uint32_t j = 0; j + 1 < F; ++j) {  // lane k compares its draw with lanes j < k of its group
       const uint32_t q = __shfl(p, (int)(gbase + j));
       dup |= msg && j < k && q == p;
     }
     if (__ballot(dup)) {  // wave-uniform, rare: lanes k = 1 .. F-1 in turn settle against lanes j < k
       uint32_t attempt = 0;
-      for (uint32_t kk = 1; kk < a.F; ++kk) {
+      for (uint32_t kk = 1; kk < F; ++kk) {
         for (;;) {
           bool again = false;
           for (uint32_t j = 0; j < kk; ++j) {
@@ -2622,11 +2625,11 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
       }
     }
     if (msg) {
-      const uint32_t i = a.base + l * a.F + k;
-      a.m_src[i] = g; a.m_dst[i] = p; a.m_seq[i] = a.round * a.F + k; a.m_size[i] = a.size; a.m_t[i] = t;
+      const uint32_t i = a.base + l * F + k;
+      a.m_src[i] = g; a.m_dst[i] = p; a.m_seq[i] = a.round * F + k; a.m_size[i] = a.size; a.m_t[i] = t;
     }
     // the instance's signal time: its latest send
-    for (uint32_t o = a.Fp >> 1; o > 0; o >>= 1) {
+    for (uint32_t o = Fp >> 1; o > 0; o >>= 1) {
       const int64_t v = __shfl_xor(t, (int)o);
       t = v > t ? v : t;
     }
@@ -2988,7 +2991,7 @@ void init_launch_geometry(Dev& d) {
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_shape, kBlock, 0) == hipSuccess && b > 0)
     d.grid_shape = b * d.n_cu;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_gen_storm, kBlock, 0) == hipSuccess && b > 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_gen_storm<8>, kBlock, 0) == hipSuccess && b > 0)
     d.grid_gen = b * d.n_cu;
 }
 
@@ -3039,7 +3042,8 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   const uint64_t threads = (uint64_t)d.nloc * a.Fp;
   const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock,
                                                   std::min<uint64_t>(kSigParts, (uint64_t)d.grid_gen));
-  hipLaunchKernelGGL(k_gen_storm, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
+  if (fanout == 8) hipLaunchKernelGGL(k_gen_storm<8>, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
+  else hipLaunchKernelGGL(k_gen_storm<0>, dim3(g), dim3(kBlock), 0, d.stream, a, sig_state(d));
   *nparts = g;
   return hipGetLastError();
 }
