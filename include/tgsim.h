@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TGSIM_ABI_VERSION 1
+#define TGSIM_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------------------------- */
 enum {
@@ -133,10 +133,19 @@ enum {
   TGSIM_ST_EXTERNAL = 5,    /* routed out via the control network (AllowAll) - leaves the simulation */
   TGSIM_ST_DEST_DOWN = 6,   /* receiver's data link disabled (Enable=false) at send time */
   TGSIM_ST_LOCAL = 7,       /* src == dst: loopback, unshaped, delivered at t_send */
+  TGSIM_ST_OVERLIMIT = 8,   /* netem queue full: tail-dropped at enqueue (limit TGSIM_NETEM_LIMIT) */
   TGSIM_ST_FLAG_DUP = 0x10,         /* a duplicate clone was created */
   TGSIM_ST_FLAG_CLONE_LOST = 0x20,  /* ... and the clone's own loss draw hit */
-  TGSIM_ST_FLAG_DUP_CANCEL = 0x40   /* duplicate and loss both hit: exactly one copy sent */
+  TGSIM_ST_FLAG_DUP_CANCEL = 0x40,  /* duplicate and loss both hit: exactly one copy sent */
+  TGSIM_ST_FLAG_OVERLIMIT = 0x80    /* the original copy was tail-dropped by the queue limit (a clone
+                                       that did not enter the queue, by loss or limit, is CLONE_LOST) */
 };
+
+/* Netem's queue limit in packets. link.go:169-179 builds the netem qdisc without a Limit, and
+ * vishvananda/netlink v1.1.0 NewNetem then sends its default of 1000 [EXT]. A copy is tail-dropped
+ * at enqueue when this many copies of the same sender, enqueued before it, are still queued (their
+ * departure time is not before its enqueue time): DESIGN.md 2.3a. */
+#define TGSIM_NETEM_LIMIT 1000u
 
 /* Delivery / in-flight record flags (tgsim_record.meta, tgsim_delivery_soa.flags). */
 enum {
@@ -144,7 +153,9 @@ enum {
   TGSIM_F_CORRUPT = 1u << 1,    /* one bit flipped: byte corrupt_off, bit (flags>>4)&7 */
   TGSIM_F_REORDERED = 1u << 2,  /* took the reorder path (sent without delay) */
   TGSIM_F_STAGE_D = 1u << 3,    /* internal: t is the delivery time (else the netem ready time) */
-  TGSIM_F_LOCAL = 1u << 7       /* loopback delivery */
+  TGSIM_F_LOCAL = 1u << 7,      /* loopback delivery */
+  TGSIM_F_WHEEL = 1u << 8       /* internal: the record is counted in its sender's queue occupancy
+                                   (it entered the sender shard's timing wheel) */
 };
 #define TGSIM_F_BIT_SHIFT 4
 
@@ -174,6 +185,7 @@ typedef struct tgsim_stats {
   uint64_t tb_items;   /* copies that went through the token bucket */
   uint64_t extracted;  /* records read back from the timing wheel */
   uint64_t inserted;   /* records written into the timing wheel */
+  uint64_t overlimit;  /* copies tail-dropped by the netem queue limit */
 } tgsim_stats;
 
 typedef struct tgsim_ctx tgsim_ctx;

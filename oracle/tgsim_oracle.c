@@ -192,7 +192,8 @@ struct tgo_ctx {
   omsgs staged;
   uint8_t* status; size_t n_status, status_cap;
   orecs heap;         /* pending records, min-heap on t */
-  orecs A, D, newD;   /* per-window scratch */
+  orecs A, D;         /* per-window scratch */
+  uint32_t* pend;     /* [nloc] copies of local sender l in the pending heap (its queue beyond the window) */
   orecs out;          /* deliveries of the last window (sorted) */
   uint32_t* inbox;    /* [nloc+1] */
   tgsim_record* xsend; tgsim_record* xrecv; size_t xcap;
@@ -288,6 +289,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
   if ((uint64_t)c->N + 2 > c->id_of_n) { free(c); return TGSIM_EINVAL; }
   c->shape = (oshape*)calloc(c->nloc ? c->nloc : 1, sizeof(oshape));
   c->X = (int64_t*)calloc(c->nloc ? c->nloc : 1, sizeof(int64_t));
+  c->pend = (uint32_t*)calloc(c->nloc ? c->nloc : 1, sizeof(uint32_t));
   c->rules = (orules*)calloc(c->nloc ? c->nloc : 1, sizeof(orules));
   c->enabled = (uint8_t*)calloc(c->N, 1);
   c->allow_ext = (uint8_t*)calloc(c->N, 1);
@@ -298,7 +300,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
   c->xcap = cfg->exchange_cap ? cfg->exchange_cap : 1024;
   c->xsend = (tgsim_record*)calloc((size_t)c->S * c->xcap, sizeof(tgsim_record));
   c->xrecv = (tgsim_record*)calloc((size_t)c->S * c->xcap, sizeof(tgsim_record));
-  if (!c->shape || !c->X || !c->rules || !c->enabled || !c->allow_ext || !c->ip || !c->id_of ||
+  if (!c->shape || !c->X || !c->pend || !c->rules || !c->enabled || !c->allow_ext || !c->ip || !c->id_of ||
       !c->inbox || !c->outbox || !c->xsend || !c->xrecv) {
     tgo_destroy(c);
     return TGSIM_ENOMEM;
@@ -332,7 +334,7 @@ void tgo_destroy(tgo_ctx* c) {
   free(c->shape); free(c->X); free(c->rules); free(c->enabled); free(c->allow_ext); free(c->ip);
   free(c->id_of); free(c->inbox); free(c->outbox); free(c->xsend); free(c->xrecv);
   free(c->staged.src); free(c->staged.dst); free(c->staged.seq); free(c->staged.size); free(c->staged.t);
-  free(c->status); free(c->heap.v); free(c->A.v); free(c->D.v); free(c->newD.v); free(c->out.v);
+  free(c->status); free(c->heap.v); free(c->A.v); free(c->D.v); free(c->pend); free(c->out.v);
   free(c);
 }
 
@@ -543,8 +545,6 @@ static void draw(const tgo_ctx* c, uint32_t seq, uint32_t src, uint32_t clone, u
   tgo_philox4x32_10(ctr, key, out);
 }
 
-static int route_record(tgo_ctx* c, tgsim_record* r); /* stage-D record -> local newD or outbox */
-
 /* netem get_crandom [EXT sch_netem.c]: the next answer leans on the last one by rho / 2^32. */
 static uint32_t crandom(uint32_t* last, uint32_t rho, uint32_t value) {
   if (!last || rho == 0) return value;
@@ -554,10 +554,10 @@ static uint32_t crandom(uint32_t* last, uint32_t rho, uint32_t value) {
   return ans;
 }
 
-/* One copy through the rest of netem_enqueue [EXT] after the duplicate/loss decision:
- * (clone only) loss draw, corruption draw, reorder-or-delay. Returns 1 if a record was produced. */
-static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, uint32_t seq,
-                      uint32_t size, int64_t t_send, uint32_t clone, uint32_t* cl, tgsim_record* rec) {
+/* netem_enqueue [EXT sch_netem.c] for one copy, up to the queue-limit check: (clone only) its own
+ * loss draw, then the corruption draw. Returns 0 if the copy is lost. */
+static int netem_pre(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, uint32_t seq, uint32_t size,
+                     uint32_t clone, uint32_t* cl, tgsim_record* rec) {
   uint32_t r0[4];
   draw(c, seq, src, clone, 0, r0);
   if (clone && sh->loss_t && sh->loss_t >= r0[1]) return 0;
@@ -571,6 +571,13 @@ static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, 
       rec->corrupt_off = r1[1] % size;
     }
   }
+  return 1;
+}
+
+/* ... after the queue-limit check (the copy is queued): reorder-or-delay. */
+static void netem_post(tgo_ctx* c, const oshape* sh, int64_t t_send, uint32_t* cl, tgsim_record* rec) {
+  uint32_t r0[4];
+  draw(c, rec->seq, rec->src, (rec->meta & TGSIM_F_CLONE) ? 1u : 0u, 0, r0);
   if (sh->reorder_t && !(sh->reorder_t < crandom(cl ? cl + 2 : NULL, sh->reorder_rho, r0[3]))) {
     /* gap == 1 when reorder > 0 (netlink NewNetem) */
     rec->meta |= TGSIM_F_REORDERED;
@@ -580,7 +587,6 @@ static int netem_copy(tgo_ctx* c, const oshape* sh, uint32_t src, uint32_t dst, 
     rec->t = t_send + (delay > 0 ? delay : 0);
   }
   if (!sh->limited) rec->meta |= TGSIM_F_STAGE_D; /* unlimited HTB: departs when netem releases it */
-  return 1;
 }
 
 static const omsgs* g_sort_msgs; /* qsort context of cmp_msg_order (single-threaded oracle) */
@@ -611,65 +617,134 @@ static int cmp_dl(const void* a, const void* b) {
   return rx < ry ? -1 : rx > ry;
 }
 
-static int route_record(tgo_ctx* c, tgsim_record* r) {
-  uint32_t p = shard_of(c, r->dst);
-  if (p == c->cfg.shard_id) return recs_push(&c->newD, r);
-  return recs_push(&c->outbox[p], r);
+/* The pending set: every copy of a local sender that has not yet departed (reached its delivery
+ * time) waits in the heap; pend[l] counts local sender l's (its netem queue beyond this window). */
+static int pend_push(tgo_ctx* c, const tgsim_record* r) {
+  if (heap_push(&c->heap, r)) return TGSIM_ENOMEM;
+  if (is_local(c, r->src)) c->pend[r->src - c->lo]++;
+  return 0;
+}
+static tgsim_record pend_pop(tgo_ctx* c) {
+  tgsim_record r = heap_pop(&c->heap);
+  if (is_local(c, r.src)) c->pend[r.src - c->lo]--;
+  return r;
 }
 
-int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
-  if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+/* A stage-D record (t = delivery time) of this window's sender side: delivered here if due and
+ * local, exchanged if due and remote (only due records cross shards), pending otherwise. */
+static int route_record(tgo_ctx* c, const tgsim_record* r) {
+  if (r->t >= c->t_end) return pend_push(c, r);
+  uint32_t p = shard_of(c, r->dst);
+  if (p == c->cfg.shard_id) return recs_push(&c->D, r);
+  return recs_push(&c->outbox[p], r);
+}
+/* A copy out of netem: token bucket now (A), pending, or (unlimited) a stage-D record. */
+static int route_copy(tgo_ctx* c, const tgsim_record* r) {
+  if (r->meta & TGSIM_F_STAGE_D) return route_record(c, r);
+  if (r->t < c->t_end) return recs_push(&c->A, r);
+  return pend_push(c, r);
+}
+
+/* ---- the netem queue limit -------------------------------------------------
+ * Per sender, in enqueue order (t_send, seq, clone first), a copy enqueued at t is tail-dropped when
+ * TGSIM_NETEM_LIMIT copies of that sender, enqueued before it, are still queued: departure d >= t.
+ * Counted within a window: the copies pending at the window start (pend + those extracted now) and
+ * those queued in this window. An extracted stage-A copy's departure comes from the HTB GCRA run in
+ * (netem time, seq, clone first) order as the enqueue times pass it - the same recurrence, in the
+ * same order, as the token bucket below. Obvious structures: two binary heaps per sender. */
+typedef struct { int64_t e; uint32_t seq, rank, size; } ou;  /* a queued copy without departure yet */
+typedef struct { ou* v; size_t n, cap; } ouheap;               /* min on (e, seq, clone first) */
+typedef struct { int64_t* v; size_t n, cap; } odheap;          /* min departure time */
+
+static int ou_less(const ou* a, const ou* b) {
+  if (a->e != b->e) return a->e < b->e;
+  if (a->seq != b->seq) return a->seq < b->seq;
+  return a->rank < b->rank;
+}
+static int ou_push(ouheap* h, ou x) {
+  if (grow((void**)&h->v, &h->cap, h->n + 1, sizeof(ou))) return TGSIM_ENOMEM;
+  size_t i = h->n++;
+  h->v[i] = x;
+  while (i) {
+    size_t p = (i - 1) / 2;
+    if (!ou_less(&h->v[i], &h->v[p])) break;
+    ou t = h->v[p]; h->v[p] = h->v[i]; h->v[i] = t; i = p;
+  }
+  return 0;
+}
+static ou ou_pop(ouheap* h) {
+  ou top = h->v[0];
+  h->v[0] = h->v[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    if (l < h->n && ou_less(&h->v[l], &h->v[m])) m = l;
+    if (r < h->n && ou_less(&h->v[r], &h->v[m])) m = r;
+    if (m == i) break;
+    ou t = h->v[m]; h->v[m] = h->v[i]; h->v[i] = t; i = m;
+  }
+  return top;
+}
+static int od_push(odheap* h, int64_t x) {
+  if (grow((void**)&h->v, &h->cap, h->n + 1, sizeof(int64_t))) return TGSIM_ENOMEM;
+  size_t i = h->n++;
+  h->v[i] = x;
+  while (i) {
+    size_t p = (i - 1) / 2;
+    if (h->v[p] <= h->v[i]) break;
+    int64_t t = h->v[p]; h->v[p] = h->v[i]; h->v[i] = t; i = p;
+  }
+  return 0;
+}
+static void od_pop(odheap* h) {
+  h->v[0] = h->v[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    if (l < h->n && h->v[l] < h->v[m]) m = l;
+    if (r < h->n && h->v[r] < h->v[m]) m = r;
+    if (m == i) break;
+    int64_t t = h->v[m]; h->v[m] = h->v[i]; h->v[i] = t; i = m;
+  }
+}
+
+typedef struct { uint32_t src; tgsim_record r; } oext;  /* a copy extracted (due) this window */
+static int cmp_ext(const void* a, const void* b) {
+  const oext* x = (const oext*)a; const oext* y = (const oext*)b;
+  return x->src < y->src ? -1 : x->src > y->src;
+}
+
+/* One sender's staged messages (ord[a..b), enqueue order) through netem_enqueue with the limit. */
+static int sender_window(tgo_ctx* c, const size_t* ord, size_t a, size_t b, const oext* ext, size_t ne,
+                         ouheap* U, odheap* K) {
   omsgs* s = &c->staged;
-  for (size_t i = 0; i < s->n; ++i)
-    if (s->t[i] >= t_end) return fail(c, TGSIM_ECAUSALITY, "staged message %zu sent at/after t_end", i);
-  c->t_end = t_end;
-  c->A.n = c->D.n = c->newD.n = 0;
-  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
-  /* 1. due events from the pending set (netem-ready copies and deliveries before t_end) */
-  while (c->heap.n && c->heap.v[0].t < t_end) {
-    tgsim_record r = heap_pop(&c->heap);
-    if (r.meta & TGSIM_F_STAGE_D) { if (recs_push(&c->D, &r)) return TGSIM_ENOMEM; }
-    else if (recs_push(&c->A, &r)) return TGSIM_ENOMEM;
-  }
-  /* 2. route + netem for every staged message, in enqueue order; a sender with correlated draws
-   *    arrives at its qdisc in (t_send, seq) order, which its crandom state follows */
-  if (grow((void**)&c->status, &c->status_cap, s->n + 1, 1)) return fail(c, TGSIM_ENOMEM, "oom");
-  c->n_status = s->n;
-  size_t* order = NULL;
-  int any_corr = 0;
-  for (uint32_t l = 0; l < c->nloc && !any_corr; ++l) any_corr = c->shape[l].corr;
-  if (any_corr && s->n) {
-    order = (size_t*)malloc(s->n * sizeof(size_t));
-    if (!order) return fail(c, TGSIM_ENOMEM, "oom");
-    for (size_t i = 0; i < s->n; ++i) order[i] = i;
-    g_sort_msgs = s;
-    qsort(order, s->n, sizeof(size_t), cmp_msg_order);
-  }
-  for (size_t k = 0; k < s->n; ++k) {
-    const size_t i = order ? order[k] : k;
-    uint32_t src = s->src[i], dst = s->dst[i], seq = s->seq[i], size = s->size[i];
-    int64_t ts = s->t[i];
-    c->stats.msgs_in++;
-    if (dst == src) {
-      tgsim_record r = {ts, src, dst, seq, size, TGSIM_F_LOCAL | TGSIM_F_STAGE_D, 0};
-      c->status[i] = TGSIM_ST_LOCAL; c->stats.local++;
-      if (route_record(c, &r)) return TGSIM_ENOMEM;
-      continue;
+  const uint32_t src = s->src[ord[a]], l = src - c->lo;
+  const oshape* sh = &c->shape[l];
+  uint32_t* cl = sh->corr ? c->cl + 3 * (size_t)l : NULL;
+  U->n = K->n = 0;
+  for (size_t j = 0; j < ne; ++j) {
+    const tgsim_record* r = &ext[j].r;
+    if (r->meta & TGSIM_F_STAGE_D) { if (od_push(K, r->t)) return TGSIM_ENOMEM; }
+    else {
+      ou u = {r->t, r->seq, (r->meta & TGSIM_F_CLONE) ? 0u : 1u, r->size};
+      if (ou_push(U, u)) return TGSIM_ENOMEM;
     }
-    int ext = dst == TGSIM_DST_EXTERNAL;
-    int rt = route_lookup(c, src, ext ? EXTERNAL_IP : c->ip[dst]);
-    if (rt == R_DROP) { c->status[i] = TGSIM_ST_DROPPED; c->stats.dropped++; continue; }
-    if (rt == R_REJECT) { c->status[i] = TGSIM_ST_REJECTED; c->stats.rejected++; continue; }
-    if (rt == R_DEFAULT) {
-      if (ext) { c->status[i] = TGSIM_ST_EXTERNAL; c->stats.external++; }
-      else { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; }
-      continue;
+  }
+  int64_t X = c->X[l];
+  for (size_t k = a; k < b; ++k) {
+    const size_t i = ord[k];
+    const uint32_t dst = s->dst[i], seq = s->seq[i], size = s->size[i];
+    const int64_t ts = s->t[i];
+    /* departures before ts: the GCRA over the queued copies whose netem time has passed */
+    while (U->n && U->v[0].e < ts) {
+      ou u = ou_pop(U);
+      int64_t d = u.e > X ? u.e : X;
+      int64_t base = X > u.e - sh->tau ? X : u.e - sh->tau;
+      int64_t nx = base + (int64_t)l2t_ns(sh, u.size);
+      X = nx > TB_CLAMP ? TB_CLAMP : nx;
+      if (od_push(K, d)) return TGSIM_ENOMEM;
     }
-    if (rt == R_NONE) { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; continue; }
-    if (!c->enabled[dst]) { c->status[i] = TGSIM_ST_DEST_DOWN; c->stats.dest_down++; continue; }
-    const oshape* sh = &c->shape[src - c->lo];
-    uint32_t* cl = sh->corr ? c->cl + 3 * (size_t)(src - c->lo) : NULL;
+    while (K->n && K->v[0] < ts) od_pop(K);
     uint32_t r0[4];
     draw(c, seq, src, 0, 0, r0);
     int count = 1;
@@ -679,25 +754,106 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     if (lost) --count;
     if (count == 0) { c->status[i] = TGSIM_ST_LOST; c->stats.lost++; continue; }
     uint8_t st = TGSIM_ST_QUEUED;
+    int queued = 0;
     if (dup && lost) st |= TGSIM_ST_FLAG_DUP_CANCEL;
     tgsim_record rec;
-    if (count == 2) { /* the clone is enqueued first, through the root qdisc, duplicate disabled */
-      st |= TGSIM_ST_FLAG_DUP;
-      if (netem_copy(c, sh, src, dst, seq, size, ts, 1, cl, &rec)) {
-        c->stats.copies++;
-        if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
-        else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
-        else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
-      } else st |= TGSIM_ST_FLAG_CLONE_LOST;
+    for (uint32_t clone = (count == 2) ? 1u : 0u;; --clone) {
+      /* the clone is enqueued first, through the root qdisc, duplication off */
+      if (netem_pre(c, sh, src, dst, seq, size, clone, cl, &rec)) {
+        const uint64_t occ = (uint64_t)c->pend[l] + U->n + K->n;
+        if (occ >= TGSIM_NETEM_LIMIT) {  /* sch_netem: sch->q.qlen >= sch->limit -> drop */
+          c->stats.overlimit++;
+          st |= clone ? TGSIM_ST_FLAG_CLONE_LOST : TGSIM_ST_FLAG_OVERLIMIT;
+        } else {
+          netem_post(c, sh, ts, cl, &rec);
+          c->stats.copies++;
+          ++queued;
+          if (rec.meta & TGSIM_F_STAGE_D) {
+            if (rec.t < c->t_end && od_push(K, rec.t)) return TGSIM_ENOMEM;
+          } else if (rec.t < c->t_end) {
+            ou u = {rec.t, rec.seq, clone ? 0u : 1u, rec.size};
+            if (ou_push(U, u)) return TGSIM_ENOMEM;
+          }
+          if (route_copy(c, &rec)) return TGSIM_ENOMEM;
+        }
+      } else {
+        st |= TGSIM_ST_FLAG_CLONE_LOST;
+      }
+      if (clone == 1) st |= TGSIM_ST_FLAG_DUP;
+      if (clone == 0) break;
     }
-    netem_copy(c, sh, src, dst, seq, size, ts, 0, cl, &rec);
-    c->stats.copies++;
-    if (rec.meta & TGSIM_F_STAGE_D) { if (route_record(c, &rec)) return TGSIM_ENOMEM; }
-    else if (rec.t < t_end) { if (recs_push(&c->A, &rec)) return TGSIM_ENOMEM; }
-    else if (heap_push(&c->heap, &rec)) return TGSIM_ENOMEM;
+    if (!queued) { st = (uint8_t)((st & 0xF0u) | TGSIM_ST_OVERLIMIT); }
     c->status[i] = st;
   }
-  free(order);
+  return 0;
+}
+
+int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  omsgs* s = &c->staged;
+  for (size_t i = 0; i < s->n; ++i)
+    if (s->t[i] >= t_end) return fail(c, TGSIM_ECAUSALITY, "staged message %zu sent at/after t_end", i);
+  c->t_end = t_end;
+  c->A.n = c->D.n = 0;
+  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
+  /* 1. due events from the pending set: netem-ready copies (token bucket now) and departures */
+  oext* ext = NULL; size_t n_ext = 0, ext_cap = 0;
+  while (c->heap.n && c->heap.v[0].t < t_end) {
+    tgsim_record r = pend_pop(c);
+    if (grow((void**)&ext, &ext_cap, n_ext + 1, sizeof(oext))) { free(ext); return TGSIM_ENOMEM; }
+    ext[n_ext].src = r.src; ext[n_ext].r = r; ++n_ext;
+    int rc = (r.meta & TGSIM_F_STAGE_D) ? route_record(c, &r) : recs_push(&c->A, &r);
+    if (rc) { free(ext); return TGSIM_ENOMEM; }
+  }
+  if (n_ext) qsort(ext, n_ext, sizeof(oext), cmp_ext);
+  /* 2. route + netem for every staged message; each sender's messages reach its qdisc in
+   *    (t_send, seq) order, which its queue limit and crandom state follow */
+  if (grow((void**)&c->status, &c->status_cap, s->n + 1, 1)) { free(ext); return fail(c, TGSIM_ENOMEM, "oom"); }
+  c->n_status = s->n;
+  size_t* order = (size_t*)malloc((s->n + 1) * sizeof(size_t));
+  if (!order) { free(ext); return fail(c, TGSIM_ENOMEM, "oom"); }
+  size_t nq = 0;  /* messages that reach a qdisc, in order[0..nq) */
+  for (size_t i = 0; i < s->n; ++i) {
+    uint32_t src = s->src[i], dst = s->dst[i], seq = s->seq[i], size = s->size[i];
+    int64_t ts = s->t[i];
+    c->stats.msgs_in++;
+    if (dst == src) {
+      tgsim_record r = {ts, src, dst, seq, size, TGSIM_F_LOCAL | TGSIM_F_STAGE_D, 0};
+      c->status[i] = TGSIM_ST_LOCAL; c->stats.local++;
+      if (route_record(c, &r)) { free(ext); free(order); return TGSIM_ENOMEM; }
+      continue;
+    }
+    int ext_dst = dst == TGSIM_DST_EXTERNAL;
+    int rt = route_lookup(c, src, ext_dst ? EXTERNAL_IP : c->ip[dst]);
+    if (rt == R_DROP) { c->status[i] = TGSIM_ST_DROPPED; c->stats.dropped++; continue; }
+    if (rt == R_REJECT) { c->status[i] = TGSIM_ST_REJECTED; c->stats.rejected++; continue; }
+    if (rt == R_DEFAULT) {
+      if (ext_dst) { c->status[i] = TGSIM_ST_EXTERNAL; c->stats.external++; }
+      else { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; }
+      continue;
+    }
+    if (rt == R_NONE) { c->status[i] = TGSIM_ST_UNREACHABLE; c->stats.unreachable++; continue; }
+    if (!c->enabled[dst]) { c->status[i] = TGSIM_ST_DEST_DOWN; c->stats.dest_down++; continue; }
+    order[nq++] = i;
+  }
+  g_sort_msgs = s;
+  if (nq) qsort(order, nq, sizeof(size_t), cmp_msg_order);
+  ouheap U = {0}; odheap K = {0};
+  int rc = 0;
+  size_t e0 = 0;
+  for (size_t a = 0; a < nq && !rc;) {
+    size_t b = a;
+    const uint32_t src = s->src[order[a]];
+    while (b < nq && s->src[order[b]] == src) ++b;
+    while (e0 < n_ext && ext[e0].src < src) ++e0;
+    size_t e1 = e0;
+    while (e1 < n_ext && ext[e1].src == src) ++e1;
+    rc = sender_window(c, order, a, b, ext + e0, e1 - e0, &U, &K);
+    a = b;
+  }
+  free(U.v); free(K.v); free(order); free(ext);
+  if (rc) return fail(c, rc, "oom");
   s->n = 0;
   /* 3. HTB token bucket (GCRA form): copies whose netem time is < t_end, per sender in
    *    (time_to_send, seq, clone-first) order; d = max(e, X); X = min(max(X, e - tau) + cost, 2^61). */
@@ -735,20 +891,18 @@ int tgo_exchange_buffers(tgo_ctx* c, void** send, void** recv, size_t* bytes) {
 
 int tgo_advance_end(tgo_ctx* c) {
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
-  /* 5. received stage-D records join this shard's own */
+  /* 5. received records (all due this window) join this shard's deliveries */
   if (c->S > 1) {
     for (uint32_t p = 0; p < c->S; ++p) {
       if (p == c->cfg.shard_id) continue;
       const tgsim_record* blk = &c->xrecv[(size_t)p * c->xcap];
       size_t n = (size_t)blk[0].t;
       if (n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "corrupt exchange header");
-      for (size_t i = 0; i < n; ++i) if (recs_push(&c->newD, &blk[1 + i])) return TGSIM_ENOMEM;
+      for (size_t i = 0; i < n; ++i) {
+        if (blk[1 + i].t >= c->t_end) return fail(c, TGSIM_ECAPACITY, "exchanged record not due");
+        if (recs_push(&c->D, &blk[1 + i])) return TGSIM_ENOMEM;
+      }
     }
-  }
-  for (size_t i = 0; i < c->newD.n; ++i) {
-    const tgsim_record* r = &c->newD.v[i];
-    if (r->t < c->t_end) { if (recs_push(&c->D, r)) return TGSIM_ENOMEM; }
-    else if (heap_push(&c->heap, r)) return TGSIM_ENOMEM;
   }
   /* 6. deliveries: inbox order (dst, t, src, seq, clone-first) */
   if (c->D.n) qsort(c->D.v, c->D.n, sizeof(tgsim_record), cmp_dl);

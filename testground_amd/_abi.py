@@ -26,9 +26,11 @@ POLICY_DENY_ALL, POLICY_ALLOW_ALL = 0, 1
 DST_EXTERNAL = 0xFFFFFFFF
 T_NOW = -(1 << 63)  # TGSIM_T_NOW: "the current window start as the device knows it"
 
-ST_QUEUED, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACHABLE, ST_EXTERNAL, ST_DEST_DOWN, ST_LOCAL = range(8)
-ST_FLAG_DUP, ST_FLAG_CLONE_LOST, ST_FLAG_DUP_CANCEL = 0x10, 0x20, 0x40
-F_CLONE, F_CORRUPT, F_REORDERED, F_STAGE_D, F_LOCAL = 1, 2, 4, 8, 128
+(ST_QUEUED, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACHABLE, ST_EXTERNAL, ST_DEST_DOWN, ST_LOCAL,
+ ST_OVERLIMIT) = range(9)
+ST_FLAG_DUP, ST_FLAG_CLONE_LOST, ST_FLAG_DUP_CANCEL, ST_FLAG_OVERLIMIT = 0x10, 0x20, 0x40, 0x80
+F_CLONE, F_CORRUPT, F_REORDERED, F_STAGE_D, F_LOCAL, F_WHEEL = 1, 2, 4, 8, 128, 256
+NETEM_LIMIT = 1000  # TGSIM_NETEM_LIMIT: netlink's default netem limit (link.go:169-179 sets none)
 
 
 class TgsimError(RuntimeError):
@@ -77,7 +79,7 @@ class DeliverySoA(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("msgs_in", "copies", "lost", "dropped", "rejected", "unreachable",
                                           "external", "dest_down", "local", "delivered", "windows",
-                                          "inflight", "tb_items", "extracted", "inserted")]
+                                          "inflight", "tb_items", "extracted", "inserted", "overlimit")]
 
 
 RECORD_DTYPE_FIELDS = [("t", "<i8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("size", "<u4"),

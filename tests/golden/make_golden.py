@@ -34,6 +34,7 @@ SCENARIOS = [
     ("heavy7", "run_heavy", dict(seed=7), False),
     ("sync3", "run_sync", dict(seed=3), True),
     ("storm300", "run_storm", dict(n_inst=300, rounds=4, seed=4), True),
+    ("burst1", "run_burst", dict(seed=1), True),
 ]
 
 PLAN_CASES = [

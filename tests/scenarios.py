@@ -122,6 +122,60 @@ def run_heavy(binding, seed: int, n_inst: int = 64):
     return out
 
 
+def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
+              window_ns: int = 4 * MS):
+    """Senders whose bursts overrun netem's 1000-packet queue under every kind of
+    shape: jitter, a saturated token bucket, duplicates + loss, reorder + corrupt, correlated
+    duplicates, zero delay; late sends (t_send before the window start, at the reaction horizon);
+    queues that stay full across windows and then drain."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=2000 + seed, max_msgs_per_window=1 << 16,
+                              max_records=1 << 18), binding=binding)
+    shapes = [
+        make_shape(latency_ns=10 * MS, jitter_ns=3 * MS),
+        make_shape(latency_ns=2 * MS, bandwidth_bps=100_000_000),
+        make_shape(latency_ns=5 * MS, duplicate=30.0, loss=5.0),
+        make_shape(latency_ns=1 * MS, jitter_ns=1 * MS, reorder=20.0, corrupt=10.0, bandwidth_bps=400_000_000),
+        make_shape(latency_ns=8 * MS, duplicate=20.0, duplicate_corr=50.0, reorder=10.0, reorder_corr=30.0),
+        make_shape(),
+    ]
+    for g, shp in enumerate(shapes):
+        sim.set_shape(g, shp)
+    heavy = np.arange(len(shapes))
+    seqc = np.zeros(n_inst, np.int64)
+    out, t0 = [], 0
+    for w in range(windows + 4):
+        src, ts = [], []
+        if w < windows:
+            for g in heavy:
+                k = per_sender if (w + g) % 3 else per_sender // 4
+                t = t0 + np.sort(rng.integers(0, window_ns // 2, k))
+                t[: k // 4] = t0
+                src.append(np.full(k, g)); ts.append(t)
+            light = rng.integers(len(shapes), n_inst, 50)
+            src.append(light); ts.append(t0 + rng.integers(0, window_ns, 50))
+            if w > 0:   # reactions at the horizon: sent before this window's start
+                late = rng.integers(0, len(shapes), 120)
+                src.append(late); ts.append(t0 - rng.integers(1, window_ns, 120))
+        src = np.concatenate(src) if src else np.zeros(0, np.int64)
+        ts = np.concatenate(ts) if ts else np.zeros(0, np.int64)
+        n = len(src)
+        dst = (src + rng.integers(1, n_inst, n)) % n_inst
+        seq = np.zeros(n, np.int64)
+        for i in range(n):
+            seq[i] = seqc[src[i]]
+            seqc[src[i]] += 1
+        size = rng.choice([64, 1000, 1500], n)
+        if n:
+            sim.enqueue(src, dst, seq, size, ts)
+        t0 += window_ns if w < windows else 60 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_sync(binding, seed: int):
     rng = np.random.default_rng(seed)
     sim = Simulator(SimConfig(n_instances=8, seed=seed, max_states=64), binding=binding)

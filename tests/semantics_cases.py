@@ -81,10 +81,12 @@ def case_duplicate_and_loss_cancel(b):
 
 
 def case_jitter_bounds(b):
-    s = sim(b, seed=11)
-    s.set_shape(0, make_shape(latency_ns=50 * MS, jitter_ns=10 * MS))
+    s = sim(b, n=8, seed=11)
+    senders = [0, 2, 3, 4]    # 1000 each: a full netem queue, nothing tail-dropped (limit 1000)
+    for g in senders:
+        s.set_shape(g, make_shape(latency_ns=50 * MS, jitter_ns=10 * MS))
     n = 4000
-    one_window(s, np.zeros(n, np.int64), 1, 10, 0, 1 * MS)
+    one_window(s, np.repeat(senders, n // 4), 1, 10, 0, 1 * MS)
     s.advance(100 * MS)
     delay = s.deliveries()["t_deliver"]
     assert len(delay) == n
@@ -214,6 +216,68 @@ def case_sync_sequence_and_barrier(b):
     with pytest.raises(A.TgsimError) as e:
         s.signal([0], [1], [65])              # goes back in time for state 0
     assert e.value.code == A.ECAUSALITY
+    s.close()
+
+
+def case_queue_limit_burst(b):
+    """netem limit 1000 [EXT netlink default; link.go:169-179 sets none]: a burst of 1500 at one
+    instant fills the queue with the first 1000 in enqueue order (t_send, seq); 500 tail-drops."""
+    s = sim(b)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    st, d = one_window(s, np.zeros(1500, np.int64), 1, 10, 0, 1 * MS, seq=np.arange(1500)[::-1].copy())
+    # seq runs backwards in enqueue index: the queue takes the 1000 smallest seq (indices 500..1499)
+    assert list(st[500:]) == [A.ST_QUEUED] * 1000 and list(st[:500]) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 500
+    s.advance(20 * MS)
+    d = s.deliveries()
+    assert len(d["seq"]) == 1000 and set(d["seq"]) == set(range(1000))
+    assert s.stats()["overlimit"] == 500
+    s.close()
+
+
+def case_queue_limit_spans_windows(b):
+    """Copies queued in earlier windows count until they depart; a copy departing at exactly t still
+    occupies the queue for an enqueue at t (departure >= t)."""
+    s = sim(b)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    st, _ = one_window(s, np.zeros(1000, np.int64), 1, 10, 0, 5 * MS)
+    assert list(st) == [A.ST_QUEUED] * 1000
+    t = np.array([10 * MS - 1] * 10 + [10 * MS] * 10 + [10 * MS + 1] * 10)
+    st, d = one_window(s, np.zeros(30, np.int64), 1, 10, t, 20 * MS, seq=np.arange(1000, 1030))
+    assert list(st) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 20 + [A.ST_QUEUED] * 10
+    assert len(d["seq"]) == 1000 and s.stats()["overlimit"] == 20
+    s.close()
+
+
+def case_queue_limit_duplicates(b):
+    """The clone is enqueued first (through the root qdisc) and counts for the original's check."""
+    s = sim(b)
+    s.set_shape(0, make_shape(latency_ns=10 * MS, duplicate=100.0))
+    st, _ = one_window(s, np.zeros(600, np.int64), 1, 10, 0, 1 * MS)
+    full = A.ST_OVERLIMIT | A.ST_FLAG_DUP | A.ST_FLAG_CLONE_LOST | A.ST_FLAG_OVERLIMIT
+    assert list(st) == [A.ST_QUEUED | A.ST_FLAG_DUP] * 500 + [full] * 100
+    s.close()
+    s = sim(b)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    one_window(s, np.zeros(999, np.int64), 1, 10, 0, 1 * MS)
+    s.set_shape(0, make_shape(latency_ns=10 * MS, duplicate=100.0))
+    st, _ = one_window(s, [0, 0], 1, 10, 1 * MS, 2 * MS, seq=[999, 1000])
+    # 999 queued: the clone takes the last place, the original is tail-dropped; then both dropped
+    assert list(st) == [A.ST_QUEUED | A.ST_FLAG_DUP | A.ST_FLAG_OVERLIMIT, full]
+    s.close()
+
+
+def case_queue_limit_token_bucket(b):
+    """A limited sender's copies stay queued until the HTB lets them go: the queue admits exactly
+    as many new copies as have departed (departure < t) by the time they arrive."""
+    s = sim(b)
+    s.set_shape(0, make_shape(bandwidth_bps=8_000_000))   # 1000-B copies: 1 ms each
+    st, d0 = one_window(s, np.zeros(1200, np.int64), 1, 1000, 0, 400 * MS)
+    assert list(st) == [A.ST_QUEUED] * 1000 + [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 200
+    st, d1 = one_window(s, np.zeros(700, np.int64), 1, 1000, 500 * MS, 501 * MS, seq=np.arange(1200, 1900))
+    departed = int(np.count_nonzero(d0["t_deliver"] < 500 * MS)) + int(np.count_nonzero(d1["t_deliver"] < 500 * MS))
+    assert 490 < departed < 510
+    assert int(np.count_nonzero(st == A.ST_QUEUED)) == departed
+    assert list(st[departed:]) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * (700 - departed)
     s.close()
 
 

@@ -27,6 +27,14 @@ def test_large_segments(hip, oracle, n_inst):
     S.assert_same(S.run_heavy(hip, 7, n_inst), S.run_heavy(oracle, 7, n_inst))
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_queue_limit_bursts(hip, oracle, seed):
+    """netem's 1000-packet queue under every shape kind, across windows."""
+    a, b = S.run_burst(hip, seed), S.run_burst(oracle, seed)
+    S.assert_same(a, b)
+    assert a[-1]["stats"]["overlimit"] > 1000
+
+
 def test_sync_service(hip, oracle):
     S.assert_same(S.run_sync(hip, 3), S.run_sync(oracle, 3))
 
