@@ -70,6 +70,17 @@ struct Dev {
   uint32_t* corr_idx = nullptr;   // [cap_msgs] deferred message indices (k_shape)
   uint32_t* corr_sorted = nullptr;  // [cap_msgs] the same, grouped by sender in (t_send, seq) order
   bool any_corr = false;          // some local shape has kShCorr
+  uint32_t* moff = nullptr;       // [segK] per local sender: its deferred messages in corr_sorted
+
+  // netem queue limit: pend[l] = local sender l's records in the timing wheel
+  // (maintained by k_wheel_scatter +, k_tb_bucket / k_emit_bucket / k_recv -); heavy = this window's
+  // test (heavy.pend == nullptr: the host proved no sender can reach the limit); H = due wheel
+  // records of heavy senders (copies, grouped by sender for k_shape_seq)
+  uint32_t* pend = nullptr;
+  Heavy heavy{};
+  tgsim_record* H = nullptr;
+  uint32_t *hkeys = nullptr, *hvals = nullptr;
+  uint32_t h_cap = 0;
 
   // staged messages (SoA) + per-message status
   uint32_t *m_src = nullptr, *m_dst = nullptr, *m_seq = nullptr, *m_size = nullptr;

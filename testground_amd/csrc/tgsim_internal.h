@@ -34,7 +34,8 @@ enum : uint32_t {
   ERR_CAP_A = 1u << 0, ERR_CAP_D = 1u << 1, ERR_CAP_L = 1u << 2, ERR_CAP_X = 1u << 3,
   ERR_ARENA = 1u << 4, ERR_REGIONS = 1u << 5, ERR_CAUSAL = 1u << 6, ERR_SIG_ORDER = 1u << 7,
   ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
-  ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14
+  ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14,
+  ERR_QUEUE_CAP = 1u << 15  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
 };
 
 // Per-sender egress state derived from network.LinkShape (48 B; gathered by src).
@@ -79,18 +80,40 @@ struct DevScalars {
   uint32_t n_large, max_large, n_chunks;
   uint32_t n_medium;                 // segments for the block-per-segment kernel (k_seg_list)
   uint32_t n_recv, n_out;
-  uint32_t n_corr;                   // messages of correlated senders deferred by k_shape
+  uint32_t n_corr;                   // messages deferred by k_shape (correlated or queue-heavy senders)
+  uint32_t n_hrec;                   // due wheel records of queue-heavy senders copied to the H list
+  uint32_t max_inbox;                // longest inbox run of the window's deliveries (flood forward bound)
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits
   uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)
   uint32_t sig_n;                    // size of the signal batch being processed
   uint64_t arena_head, arena_tail, arena_used, ins_off;  // arena ring (records)
   uint64_t sig_log_used;             // signal log entries used
+  uint32_t pend_max;                 // max over time of any local sender's queued-copy count (host gate)
+  uint32_t pad_pm;
   // cumulative statistics (tgsim_stats)
   unsigned long long st[13];
 };
 enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_EXTERNAL, ST_DESTDOWN,
        ST_LOCAL, ST_DELIVERED, ST_TB_ITEMS, ST_EXTRACTED, ST_INSERTED };
+constexpr int ST_OVERLIMIT = 13;  // a row counter only ([kNSub][16] rows; ST_DELIVERED.. live in DevScalars::st)
+
+// Netem's queue limit. A local sender is "queue-heavy" in a window when the copies
+// it has queued (pend: its records in the timing wheel at the window start) plus every copy it
+// could add in the window may reach the limit; only then are its messages decided sequentially
+// (k_shape_seq). m_uniform bounds the messages any sender stages in the window, m_inbox * (its last
+// inbox run) the flood forwards; mult = 2 when some shape duplicates.
+struct Heavy {
+  const uint32_t* pend;   // nullptr: the host proved no sender can reach the limit this window
+  const uint32_t* inbox;  // [nloc + 1] the last window's inbox offsets (flood forwards), or nullptr
+  uint32_t m_uniform, m_inbox, mult;
+  __host__ __device__ bool of(uint32_t l) const {
+    if (!pend) return false;
+    uint64_t m = m_uniform;
+    if (m_inbox) m += (uint64_t)m_inbox * (inbox[l + 1] - inbox[l]);
+    return (uint64_t)pend[l] + mult * m > TGSIM_NETEM_LIMIT;
+  }
+};
 
 struct LargeSeg { uint32_t seg, start, len, pad; };
 struct SigChunk {  // a run of consecutive sequence numbers of one state

@@ -154,13 +154,17 @@ struct Queues {
 
 struct Geo { uint32_t N, S, shard; };
 
-// Queue of a stage-D record (its t is the delivery time): the receiver's shard, now or later.
+// Queue of a stage-D record (its t is the delivery time): delivered now (here, or on the receiver's
+// shard through the exchange) or later from this shard's wheel. A record crosses shards only in the
+// window it is due, so every queued copy of a local sender waits on its sender's shard,
+// where its queue occupancy is counted.
 __device__ __forceinline__ int qid_stage_d(const Geo& g, uint32_t dst, int64_t t, int64_t t_end) {
+  if (t >= t_end) return Q_L;
   if (g.S > 1) {
     const uint32_t p = shard_of(dst, g.N, g.S);
     if (p != g.shard) return Q_X0 + (int)p;
   }
-  return t < t_end ? Q_D : Q_L;
+  return Q_D;
 }
 
 __device__ __forceinline__ uint32_t clamp_n(const uint32_t* n_ptr, uint32_t cap) {
@@ -295,7 +299,8 @@ struct ShapeArgs {
   Geo geo;
   Queues Q;
   unsigned long long* stats;  // [kNSub][16] sharded counters
-  uint32_t* corr_idx;         // deferred messages of correlated senders (count sc->n_corr)
+  uint32_t* corr_idx;         // deferred messages of correlated / queue-heavy senders (count sc->n_corr)
+  Heavy heavy;                // the window's queue-limit test
 };
 
 // Longest-prefix match over the sender's routing table: rule groups by prefix
@@ -458,7 +463,7 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
       else if (rt == R_DEFAULT && ext) { st = TGSIM_ST_EXTERNAL; cnt[ST_EXTERNAL]++; }
       else if (rt != R_DATA) { st = TGSIM_ST_UNREACHABLE; cnt[ST_UNREACH]++; }
       else if (!(fdst & 1u)) { st = TGSIM_ST_DEST_DOWN; cnt[ST_DESTDOWN]++; }
-      else if (sh.flags & kShCorr) { st = 0; deferred = true; }  // netem in (t_send, seq) order: k_shape_corr
+      else if ((sh.flags & kShCorr) || a.heavy.of(sl)) { st = 0; deferred = true; }  // (t_send, seq) order: k_shape_seq
       else {
         uint32_t r0[4];
         philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
@@ -575,9 +580,19 @@ constexpr int kExtractUnroll = 4;     // records in flight per thread
 // plan (each live region's due prefix and its place in the output) is staged in LDS, so locating
 // a record costs no global round trip; kExtractUnroll records per thread are loaded before the
 // wave appends.
+// The extraction's share of the queue limit: due records of queue-heavy senders are also copied to
+// the H list (with their sender as the group-by key) for k_shape_seq.
+struct HeavyOut {
+  Heavy hv;
+  Geo geo;
+  tgsim_record* H;
+  uint32_t *hkeys, *hvals;
+  uint32_t hcap, lo;
+};
+
 __device__ __forceinline__ void extract_body(const RegionDev* regions, const uint32_t* plan_start,
                                              const uint32_t* plan_off, const tgsim_record* arena, const Queues& Q,
-                                             uint32_t bid, uint32_t nblocks) {
+                                             uint32_t bid, uint32_t nblocks, const HeavyOut& ho) {
   __shared__ uint32_t s_off[kPlanLds];
   __shared__ uint64_t s_src[kPlanLds];
   DevScalars* sc = Q.sc;
@@ -619,16 +634,32 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
 #pragma unroll
     for (int u = 0; u < kExtractUnroll; ++u) {
       const uint32_t j = base + u * kBlock + threadIdx.x;
-      const int q = j >= total ? -1 : (rec[u].t < t_end ? ((rec[u].meta & TGSIM_F_STAGE_D) ? Q_D : Q_A) : Q_L);
+      const bool due = j < total && rec[u].t < t_end;
+      const int q = j >= total ? -1
+                               : (due ? ((rec[u].meta & TGSIM_F_STAGE_D) ? qid_stage_d(ho.geo, rec[u].dst, rec[u].t, t_end) : Q_A)
+                                      : Q_L);
       Q.push(q, rec[u], it * kExtractUnroll + u);
+      if (ho.hv.pend) {  // launch-uniform
+        const bool h = due && ho.hv.of(rec[u].src - ho.lo);
+        const uint32_t pos = wave_append(h ? &sc->n_hrec : nullptr);
+        if (h) {
+          if (pos < ho.hcap) {
+            store_rec(ho.H + pos, rec[u]);
+            ho.hkeys[pos] = rec[u].src - ho.lo;
+            ho.hvals[pos] = pos;
+          } else {
+            atomicOr(&sc->err, ERR_QUEUE_CAP);
+          }
+        }
+      }
     }
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, const uint32_t* plan_start,
                                                     const uint32_t* plan_off, const tgsim_record* arena,
-                                                    Queues Q) {
-  extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, gridDim.x);
+                                                    Queues Q, HeavyOut ho) {
+  extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, gridDim.x, ho);
 }
 
 // The wheel extraction and netem of the staged messages are independent (both only append to the
@@ -637,8 +668,8 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
 // XCD (blockIdx mod 8) its sub-queue choice assumes.
 __global__ __launch_bounds__(kBlock) void k_extract_shape(const RegionDev* regions, const uint32_t* plan_start,
                                                           const uint32_t* plan_off, const tgsim_record* arena,
-                                                          Queues Q, ShapeArgs a, uint32_t ne) {
-  if (blockIdx.x < ne) extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, ne);
+                                                          Queues Q, ShapeArgs a, uint32_t ne, HeavyOut ho) {
+  if (blockIdx.x < ne) extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, ne, ho);
   else shape_body(a, blockIdx.x - ne, gridDim.x - ne);
 }
 
@@ -1072,9 +1103,34 @@ __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const 
 constexpr int kWheelUnroll = 8;
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
+// Queue occupancy: a record entering the wheel for the first time (no
+// TGSIM_F_WHEEL) is counted in its sender's pend and marked; runs of one sender among a wave's 64
+// consecutive records share one atomic (the token bucket stages its output grouped by sender).
+__device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uint32_t nloc, uint32_t src, bool add,
+                                                uint32_t* pend_max) {
+  const uint32_t lane = lane_id();
+  const uint32_t key = add && src - lo < nloc ? src - lo : 0xFFFFFFFFu;
+  const uint32_t prev = __shfl_up(key, 1);
+  const bool head = key != 0xFFFFFFFFu && (lane == 0 || prev != key);
+  const uint64_t heads = __ballot(head);
+  const uint64_t valid = __ballot(key != 0xFFFFFFFFu);
+  uint32_t post = 0;
+  if (head) {
+    // the run: this lane and the following lanes with the same key (heads end it)
+    const uint64_t after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
+    const uint32_t end = after ? (uint32_t)__ffsll((unsigned long long)after) - 1u : 64u;
+    const uint64_t span = (end >= 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
+    const uint32_t n = (uint32_t)__popcll(valid & span);
+    post = atomicAdd(&pend[key], n) + n;
+  }
+  post = wave_max(post);
+  if (lane == 0 && post) atomicMax(pend_max, post);
+}
+
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                           tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                          const uint32_t* hist, const uint32_t* tot) {
+                                                          const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                          uint32_t lo, uint32_t nloc) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   const uint64_t off = sc->ins_off;
@@ -1115,11 +1171,15 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
     }
 #pragma unroll
     for (int u = 0; u < kWheelUnroll; ++u) {
+      const bool fresh = k[u] != 0xFFFFFFFFu && !(rb[u].z & TGSIM_F_WHEEL);
+      pend_count_wave(pend, lo, nloc, ra[u].z, fresh, &sc->pend_max);
       if (k[u] != 0xFFFFFFFFu) {
         const uint32_t pos = atomicAdd(&base[k[u]], 1u);
         v4u32* q = reinterpret_cast<v4u32*>(arena + off + pos);
         q[0] = ra[u];
-        q[1] = rb[u];
+        v4u32 b = rb[u];
+        b.z |= TGSIM_F_WHEEL;
+        q[1] = b;
       }
     }
   }
@@ -1271,6 +1331,7 @@ struct TBPolicy {
   const tgsim_record* A;
   const ShapeDev* shape;
   int64_t* X;
+  uint32_t* pend;  // queue occupancy: a wheel copy leaving now (D / X) no longer counts
   uint32_t lo;
   Geo geo;
   Queues Q;
@@ -1368,6 +1429,10 @@ struct TBPolicy {
         rec.t = e > xprev ? e : xprev;
         rec.meta |= TGSIM_F_STAGE_D;
         q = qid_stage_d(geo, rec.dst, rec.t, t_end);
+        if ((rec.meta & TGSIM_F_WHEEL) && q != Q_L) {
+          rec.meta &= ~(uint32_t)TGSIM_F_WHEEL;
+          atomicSub(&pend[rec.src - lo], 1u);
+        }
       }
       Q.push(q, rec, salt + u);
     }
@@ -1415,7 +1480,8 @@ __device__ __forceinline__ void block_scan2(uint32_t& v0, uint32_t& v1, uint32_t
 
 struct EmitPolicy {
   const tgsim_record* D;
-  uint32_t lo;
+  uint32_t* pend;  // queue occupancy: a delivered wheel copy of a local sender no longer counts
+  uint32_t lo, nloc;
   int64_t* o_t;
   uint32_t *o_src, *o_dst, *o_seq, *o_size, *o_flags, *o_coff;
 
@@ -1431,8 +1497,9 @@ struct EmitPolicy {
   __device__ __forceinline__ void write(uint32_t pos, uint32_t k3) const {
     tgsim_record r;
     load_rec(D + (k3 & 0x7FFFFFFFu), r);
+    if ((r.meta & TGSIM_F_WHEEL) && r.src - lo < nloc) atomicSub(&pend[r.src - lo], 1u);
     o_t[pos] = r.t; o_src[pos] = r.src; o_dst[pos] = r.dst; o_seq[pos] = r.seq; o_size[pos] = r.size;
-    o_flags[pos] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; o_coff[pos] = r.corrupt_off;
+    o_flags[pos] = r.meta & ~(uint32_t)(TGSIM_F_STAGE_D | TGSIM_F_WHEEL); o_coff[pos] = r.corrupt_off;
   }
   __device__ void epilogue(SortSmem& s, uint32_t m, uint32_t s_begin, const uint32_t*, uint32_t) const {
     for (uint32_t j = threadIdx.x; j < m; j += kBlock) write(s_begin + j, s.k3[s.perm[j]]);
@@ -1466,6 +1533,7 @@ struct BktFusedSmem {
   uint32_t k3[kBktCap];                  // batch index (emit: | !clone << 31)
   uint16_t key[kBktCap];                 // key of each slot, relative to the bucket's first key
   uint16_t ord[kBktCap];                 // by_pos: sorted position -> slot; else slot -> sorted position
+  uint32_t dec[1u << kBktFusedKeyBits];  // TB: per key, wheel copies that leave the sender's queue now
   uint32_t part[kBlock];
   uint32_t maxlen, flag;
 #ifdef TGSIM_PHASE_PROF
@@ -1556,7 +1624,8 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
       vscr[h.start + j] = e.y;
     }
     __syncthreads();
-    bkt_count_body(kscr, sm.cnt, sm.part, h);
+    const uint32_t mx = bkt_count_body(kscr, sm.cnt, sm.part, h);
+    if (!by_pos && threadIdx.x == 0) atomicMax(&sc->max_inbox, mx);  // longest inbox run (flood forwards)
     bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
     return false;
   }
@@ -1601,6 +1670,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     run += len;
   }
   __syncthreads();
+  if (!by_pos && threadIdx.x == 0 && sm.maxlen) atomicMax(&sc->max_inbox, sm.maxlen);
   TG_PH(4);
   // slots + sort keys (from the registers: no second gather)
 #pragma unroll
@@ -1699,6 +1769,7 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     return;
   // the GCRA along each sender's run (one thread per sender); departures replace k1
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
+    sm.dec[i] = 0;
     const uint32_t a = i ? sm.cnt[i - 1] : 0u, e = sm.cnt[i];
     if (e == a || e - a > kBktRankMax) continue;
     const uint32_t sl = h.k0 + i;
@@ -1732,9 +1803,16 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     rec[u].meta |= TGSIM_F_STAGE_D;
     code[u] = qid_stage_d(p.geo, rec[u].dst, rec[u].t, t_end);
     nD += code[u] == Q_D; nL += code[u] == Q_L; nX += code[u] >= Q_X0;
+    if ((rec[u].meta & TGSIM_F_WHEEL) && code[u] != Q_L) {  // leaves its sender's queue now
+      rec[u].meta &= ~(uint32_t)TGSIM_F_WHEEL;
+      atomicAdd(&sm.dec[sm.key[slot[u]]], 1u);
+    }
   }
   if (threadIdx.x == 0) sm.flag = 0;
   __syncthreads();
+  // this workgroup owns its senders' counters for the launch (long runs: k_rest, later)
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock)
+    if (sm.dec[i]) p.pend[h.k0 + i] -= sm.dec[i];
   if (nX) sm.flag = 1;
   uint32_t tD, tL;
   block_scan2(nD, nL, sm.part, tD, tL);  // nD/nL: this thread's offsets inside the block's runs
@@ -1830,9 +1908,10 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
       if (o < r0 || o >= r0 + kStageN) continue;
       const uint32_t i = o - r0;
       const tgsim_record& r = rec[u];
+      if ((r.meta & TGSIM_F_WHEEL) && r.src - p.lo < p.nloc) atomicSub(&p.pend[r.src - p.lo], 1u);
       st_t[i] = r.t;
       st_u[i] = r.src; st_u[kStageN + i] = r.dst; st_u[2 * kStageN + i] = r.seq; st_u[3 * kStageN + i] = r.size;
-      st_u[4 * kStageN + i] = r.meta & ~(uint32_t)TGSIM_F_STAGE_D; st_u[5 * kStageN + i] = r.corrupt_off;
+      st_u[4 * kStageN + i] = r.meta & ~(uint32_t)(TGSIM_F_STAGE_D | TGSIM_F_WHEEL); st_u[5 * kStageN + i] = r.corrupt_off;
     }
     __syncthreads();
     const uint32_t n = min(kStageN, h.nb - r0);
@@ -1879,13 +1958,6 @@ struct SigPolicy {
   }
 };
 
-// ---- correlated netem (get_crandom [EXT]) --------------------------------------------------
-// A sender whose shape uses a correlated draw has a sequential state per qdisc, advanced in the
-// order its messages reach the qdisc, (t_send, seq). k_shape defers those messages; they are
-// grouped by sender (the bucketed group-by), ordered (t_send, seq) per sender (k_seg_small /
-// k_rest with CorrPolicy) and run through netem by one thread per sender (k_shape_corr). Senders
-// without correlation never take this path (the storm pays nothing for it).
-
 __global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* src, const uint32_t* n_ptr,
                                                       uint32_t lo, uint32_t* keys, uint32_t* vals) {
   const uint32_t n = *n_ptr;
@@ -1920,62 +1992,273 @@ struct CorrPolicy {
   }
 };
 
-// One thread per local sender: its deferred messages in (t_send, seq) order through netem_enqueue
-// with the correlated draws (dup, then the clone's and the original's corrupt / reorder).
-__global__ __launch_bounds__(kBlock) void k_shape_corr(ShapeArgs a, const uint32_t* sorted, const uint32_t* off,
-                                                       const uint32_t* rho4, uint32_t* last4) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= a.nloc) return;
-  const uint32_t j0 = off[l], j1 = off[l + 1];
-  if (j0 == j1) return;
-  const int64_t t_end = a.Q.sc->t_end;
-  const ShapeDev sh = a.shape[l];
-  const uint32_t rho[3] = {rho4[4 * l], rho4[4 * l + 1], rho4[4 * l + 2]};
-  uint32_t cl[3] = {last4[4 * l], last4[4 * l + 1], last4[4 * l + 2]};
-  unsigned long long lost = 0, copies = 0;
-  for (uint32_t j = j0; j < j1; ++j) {
-    const uint32_t i = sorted[j];
-    const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
-    const int64_t ts = a.t[i];
-    tgsim_record r1, r2;
-    int q1 = -1, q2 = -1;
-    uint32_t r0[4];
-    philox4x32_10(seq, src, 0u, kNetemSalt, a.key0, a.key1, r0);
-    int count = 1;
-    const bool dup = sh.dup_t && sh.dup_t >= crandom(cl[0], rho[0], r0[0]);
-    if (dup) ++count;
-    const bool lst = sh.loss_t && sh.loss_t >= r0[1];
-    if (lst) --count;
-    uint8_t st;
-    if (count == 0) {
-      st = TGSIM_ST_LOST;
-      ++lost;
-    } else {
-      st = TGSIM_ST_QUEUED;
-      if (dup && lst) st |= TGSIM_ST_FLAG_DUP_CANCEL;
-      if (count == 2) {
-        st |= TGSIM_ST_FLAG_DUP;
-        uint32_t c0[4];
-        philox4x32_10(seq, src, 1u, kNetemSalt, a.key0, a.key1, c0);
-        if (netem_copy_corr(sh, rho, cl, c0, src, dst, seq, size, ts, 1u, a.key0, a.key1, r1)) {
-          q1 = qid_copy(a.geo, r1, t_end);
-          ++copies;
-        } else {
-          st |= TGSIM_ST_FLAG_CLONE_LOST;
+// ---- sequential netem per sender: correlated draws and the queue limit ------------------------
+// A sender whose shape uses a correlated draw (get_crandom [EXT]), or whose queue may reach netem's
+// limit this window (Heavy), is decided in the order its messages reach its qdisc,
+// (t_send, seq). k_shape defers those messages; they are grouped by sender and ordered (k_seg_small
+// / k_rest with CorrPolicy); the extraction copied the heavy senders' due wheel records to H (grouped
+// by the bucketed group-by). One wave per sender (k_shape_seq): the lanes load a chunk of 64
+// messages and their Philox words in parallel, lane 0 walks the chunk in order - correlated state,
+// then the limit - and the lanes write the statuses and append the queued copies. The queue is
+// tracked as in the oracle: copies whose departure is known in this window (min-heap K), queued
+// copies still waiting for the token bucket (min-heap U on (netem time, seq, clone first), run
+// through the HTB GCRA as enqueue times pass them - the recurrence and order of k_tb_bucket), and
+// a count of copies that stay queued past the window. Senders that are not heavy skip the tracking:
+// their queue cannot reach the limit.
+
+constexpr int kSeqCap = 1024;   // copies tracked per heavy sender: >= TGSIM_NETEM_LIMIT (queue never exceeds it)
+constexpr int kSeqChunk = 64;   // messages per chunk, one per lane
+static_assert(kSeqCap >= (int)TGSIM_NETEM_LIMIT, "a heavy sender's queue fits the LDS heaps");
+
+struct SeqSmem {
+  int64_t ue[kSeqCap];      // U: netem time
+  uint64_t uk[kSeqCap];     // U: seq << 1 | !clone (clone first)
+  uint32_t us[kSeqCap];     // U: size
+  int64_t kd[kSeqCap];      // K: departure time
+  int64_t mt[kSeqChunk];
+  uint32_t midx[kSeqChunk], mdst[kSeqChunk], mseq[kSeqChunk], msize[kSeqChunk];
+  uint32_t w0[2][kSeqChunk][4];  // block-0 Philox words: [0] original, [1] clone
+  uint32_t w1[2][kSeqChunk][3];  // block-1 (corrupt) words
+  int64_t ct[2][kSeqChunk];      // queued copy: netem time
+  uint32_t cm[2][kSeqChunk];     // queued copy: meta (flags, corrupt bit)
+  uint32_t co[2][kSeqChunk];     // queued copy: corrupt offset
+  uint8_t st[kSeqChunk], adm[kSeqChunk];  // status, queued copies (bit c = copy c)
+  uint32_t nu, nk;
+};
+
+__device__ __forceinline__ bool u_less(const SeqSmem& m, uint32_t a, uint32_t b) {
+  return m.ue[a] != m.ue[b] ? m.ue[a] < m.ue[b] : m.uk[a] < m.uk[b];
+}
+__device__ __forceinline__ void u_swap(SeqSmem& m, uint32_t a, uint32_t b) {
+  const int64_t e = m.ue[a]; m.ue[a] = m.ue[b]; m.ue[b] = e;
+  const uint64_t k = m.uk[a]; m.uk[a] = m.uk[b]; m.uk[b] = k;
+  const uint32_t s = m.us[a]; m.us[a] = m.us[b]; m.us[b] = s;
+}
+__device__ void u_down(SeqSmem& m, uint32_t i, uint32_t n) {
+  for (;;) {
+    const uint32_t l = 2 * i + 1, r = l + 1;
+    uint32_t s = i;
+    if (l < n && u_less(m, l, s)) s = l;
+    if (r < n && u_less(m, r, s)) s = r;
+    if (s == i) return;
+    u_swap(m, i, s);
+    i = s;
+  }
+}
+__device__ void u_push(SeqSmem& m, int64_t e, uint64_t k, uint32_t size, DevScalars* sc) {
+  if (m.nu >= (uint32_t)kSeqCap) { atomicOr(&sc->err, ERR_QUEUE_CAP); return; }
+  uint32_t i = m.nu++;
+  m.ue[i] = e; m.uk[i] = k; m.us[i] = size;
+  while (i) {
+    const uint32_t p = (i - 1) / 2;
+    if (!u_less(m, i, p)) break;
+    u_swap(m, i, p);
+    i = p;
+  }
+}
+__device__ void k_down(SeqSmem& m, uint32_t i, uint32_t n) {
+  for (;;) {
+    const uint32_t l = 2 * i + 1, r = l + 1;
+    uint32_t s = i;
+    if (l < n && m.kd[l] < m.kd[s]) s = l;
+    if (r < n && m.kd[r] < m.kd[s]) s = r;
+    if (s == i) return;
+    const int64_t t = m.kd[i]; m.kd[i] = m.kd[s]; m.kd[s] = t;
+    i = s;
+  }
+}
+__device__ void k_push(SeqSmem& m, int64_t d, DevScalars* sc) {
+  if (m.nk >= (uint32_t)kSeqCap) { atomicOr(&sc->err, ERR_QUEUE_CAP); return; }
+  uint32_t i = m.nk++;
+  m.kd[i] = d;
+  while (i) {
+    const uint32_t p = (i - 1) / 2;
+    if (m.kd[p] <= m.kd[i]) break;
+    const int64_t t = m.kd[p]; m.kd[p] = m.kd[i]; m.kd[i] = t;
+    i = p;
+  }
+}
+
+__global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint32_t* sorted, const uint32_t* moff,
+                                                         const uint32_t* hoff, const uint32_t* hidx,
+                                                         const tgsim_record* H, const uint32_t* rho4,
+                                                         uint32_t* last4, const int64_t* Xs) {
+  __shared__ SeqSmem m;
+  DevScalars* sc = a.Q.sc;
+  const int64_t t_end = sc->t_end;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
+    const uint32_t j0 = moff[l], j1 = moff[l + 1];
+    if (j0 == j1) continue;
+    const ShapeDev sh = a.shape[l];
+    const bool corr = (sh.flags & kShCorr) != 0;
+    const bool heavy = a.heavy.of(l);
+    const bool limited = (sh.flags & kShLimited) != 0;
+    const uint32_t src = a.lo + l;
+    uint32_t rho[3] = {0, 0, 0}, cl[3] = {0, 0, 0};
+    if (corr) {
+      rho[0] = rho4[4 * l]; rho[1] = rho4[4 * l + 1]; rho[2] = rho4[4 * l + 2];
+      cl[0] = last4[4 * l]; cl[1] = last4[4 * l + 1]; cl[2] = last4[4 * l + 2];
+    }
+    int64_t X = Xs[l];
+    uint64_t far = 0;  // queued copies not leaving in this window
+    if (lane == 0) { m.nu = 0; m.nk = 0; }
+    __syncthreads();
+    if (heavy) {  // the sender's due wheel records: U (token bucket pending) or K (departing now)
+      const uint32_t h0 = hoff[l], h1 = hoff[l + 1];
+      for (uint32_t b = h0; b < h1; b += kSeqChunk) {
+        const uint32_t j = b + lane;
+        tgsim_record r;
+        const bool in = j < h1;
+        if (in) load_rec(H + hidx[j], r);
+        const bool isA = in && !(r.meta & TGSIM_F_STAGE_D), isD = in && !isA;
+        const uint64_t ma = __ballot(isA), md = __ballot(isD);
+        const uint32_t pa = m.nu + mask_rank(ma), pd = m.nk + mask_rank(md);
+        if (isA && pa < (uint32_t)kSeqCap) {
+          m.ue[pa] = r.t; m.uk[pa] = ((uint64_t)r.seq << 1) | ((r.meta & TGSIM_F_CLONE) ? 0u : 1u); m.us[pa] = r.size;
+        }
+        if (isD && pd < (uint32_t)kSeqCap) m.kd[pd] = r.t;
+        __syncthreads();
+        if (lane == 0) {
+          m.nu += (uint32_t)__popcll(ma); m.nk += (uint32_t)__popcll(md);
+          if (m.nu > (uint32_t)kSeqCap || m.nk > (uint32_t)kSeqCap) {
+            atomicOr(&sc->err, ERR_QUEUE_CAP);
+            m.nu = min(m.nu, (uint32_t)kSeqCap); m.nk = min(m.nk, (uint32_t)kSeqCap);
+          }
+        }
+        __syncthreads();
+      }
+      if (lane == 0) {  // Floyd heap construction
+        for (uint32_t i = m.nu / 2; i-- > 0;) u_down(m, i, m.nu);
+        for (uint32_t i = m.nk / 2; i-- > 0;) k_down(m, i, m.nk);
+      }
+      const uint32_t p = a.heavy.pend[l];
+      far = p > h1 - h0 ? p - (h1 - h0) : 0;
+    }
+    const bool need_w0 = sh.dup_t || sh.loss_t || sh.reorder_t || sh.sigma;
+    uint32_t n_lost = 0, n_copies = 0, n_over = 0;
+    for (uint32_t c0 = j0; c0 < j1; c0 += kSeqChunk) {
+      const uint32_t cn = min((uint32_t)kSeqChunk, j1 - c0);
+      // parallel: the chunk's messages and their Philox words
+      if (lane < cn) {
+        const uint32_t i = sorted[c0 + lane];
+        const uint32_t seq = a.seq[i];
+        m.midx[lane] = i; m.mdst[lane] = a.dst[i]; m.mseq[lane] = seq; m.msize[lane] = a.size[i]; m.mt[lane] = a.t[i];
+        for (uint32_t c = 0; c < 2; ++c) {
+          if (c == 1 && !sh.dup_t) break;
+          uint32_t o[4] = {0, 0, 0, 0};
+          if (need_w0) philox4x32_10(seq, src, c, kNetemSalt, a.key0, a.key1, o);
+          m.w0[c][lane][0] = o[0]; m.w0[c][lane][1] = o[1]; m.w0[c][lane][2] = o[2]; m.w0[c][lane][3] = o[3];
+          if (sh.corrupt_t) {
+            philox4x32_10(seq, src, c | 2u, kNetemSalt, a.key0, a.key1, o);
+            m.w1[c][lane][0] = o[0]; m.w1[c][lane][1] = o[1]; m.w1[c][lane][2] = o[2];
+          }
         }
       }
-      netem_copy_corr(sh, rho, cl, r0, src, dst, seq, size, ts, 0u, a.key0, a.key1, r2);
-      q2 = qid_copy(a.geo, r2, t_end);
-      ++copies;
+      __syncthreads();
+      // sequential: netem_enqueue per message in qdisc order
+      if (lane == 0) {
+        for (uint32_t k = 0; k < cn; ++k) {
+          const int64_t ts = m.mt[k];
+          const uint32_t size = m.msize[k];
+          if (heavy) {
+            while (m.nu && m.ue[0] < ts) {  // departures before ts: HTB GCRA in k_tb_bucket's order
+              const int64_t e = m.ue[0];
+              const uint32_t usz = m.us[0];
+              --m.nu;
+              if (m.nu) { m.ue[0] = m.ue[m.nu]; m.uk[0] = m.uk[m.nu]; m.us[0] = m.us[m.nu]; u_down(m, 0, m.nu); }
+              const int64_t dd = e > X ? e : X;
+              const int64_t b0 = X > e - sh.tau ? X : e - sh.tau;
+              const int64_t v = b0 + (int64_t)l2t_ns(sh, usz);
+              X = v > kTbClamp ? kTbClamp : v;
+              k_push(m, dd, sc);
+            }
+            while (m.nk && m.kd[0] < ts) {
+              --m.nk;
+              if (m.nk) { m.kd[0] = m.kd[m.nk]; k_down(m, 0, m.nk); }
+            }
+          }
+          const uint32_t* r0 = m.w0[0][k];
+          const bool dup = sh.dup_t && sh.dup_t >= crandom(cl[0], rho[0], r0[0]);
+          const bool lst = sh.loss_t && sh.loss_t >= r0[1];
+          const int count = 1 + (dup ? 1 : 0) - (lst ? 1 : 0);
+          uint8_t st;
+          uint8_t adm = 0;
+          if (count == 0) {
+            st = TGSIM_ST_LOST;
+            ++n_lost;
+          } else {
+            st = TGSIM_ST_QUEUED;
+            if (dup && lst) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+            for (int c = count == 2 ? 1 : 0; c >= 0; --c) {  // the clone is enqueued first
+              const uint32_t* w = m.w0[c][k];
+              if (c == 1 && sh.loss_t && sh.loss_t >= w[1]) { st |= TGSIM_ST_FLAG_CLONE_LOST; continue; }
+              uint32_t meta = c ? TGSIM_F_CLONE : 0u, coff = 0;
+              if (sh.corrupt_t) {
+                const uint32_t* w1 = m.w1[c][k];
+                if (sh.corrupt_t >= crandom(cl[1], rho[1], w1[0]) && size > 0) {
+                  meta |= TGSIM_F_CORRUPT | ((w1[2] % 8u) << TGSIM_F_BIT_SHIFT);
+                  coff = w1[1] % size;
+                }
+              }
+              if (heavy && far + m.nu + m.nk >= TGSIM_NETEM_LIMIT) {  // sch->q.qlen >= sch->limit
+                ++n_over;
+                st |= c ? TGSIM_ST_FLAG_CLONE_LOST : TGSIM_ST_FLAG_OVERLIMIT;
+                continue;
+              }
+              int64_t e;
+              if (sh.reorder_t && !(sh.reorder_t < crandom(cl[2], rho[2], w[3]))) {
+                meta |= TGSIM_F_REORDERED;
+                e = ts;
+              } else {
+                const int64_t delay = tabledist(sh.mu, sh.sigma, w[2]);
+                e = ts + (delay > 0 ? delay : 0);
+              }
+              if (!limited) meta |= TGSIM_F_STAGE_D;
+              m.ct[c][k] = e; m.cm[c][k] = meta; m.co[c][k] = coff;
+              adm |= (uint8_t)(1u << c);
+              ++n_copies;
+              if (heavy) {
+                if (e >= t_end) ++far;
+                else if (limited) u_push(m, e, ((uint64_t)m.mseq[k] << 1) | (c ? 0u : 1u), size, sc);
+                else k_push(m, e, sc);
+              }
+            }
+            if (count == 2) st |= TGSIM_ST_FLAG_DUP;
+            if (!adm) st = (uint8_t)((st & 0xF0u) | TGSIM_ST_OVERLIMIT);
+          }
+          m.st[k] = st;
+          m.adm[k] = adm;
+        }
+      }
+      __syncthreads();
+      // parallel: statuses and the queued copies
+      tgsim_record r1, r2;
+      int q1 = -1, q2 = -1;
+      if (lane < cn) {
+        a.status[m.midx[lane]] = m.st[lane];
+        const uint8_t adm = m.adm[lane];
+        for (int c = 1; c >= 0; --c) {
+          if (!(adm & (1u << c))) continue;
+          tgsim_record& r = c ? r1 : r2;
+          r.t = m.ct[c][lane]; r.src = src; r.dst = m.mdst[lane]; r.seq = m.mseq[lane]; r.size = m.msize[lane];
+          r.meta = m.cm[c][lane]; r.corrupt_off = m.co[c][lane];
+          (c ? q1 : q2) = qid_copy(a.geo, r, t_end);
+        }
+      }
+      a.Q.push(q1, r1, 2 * c0);
+      a.Q.push(q2, r2, 2 * c0 + 1);
+      __syncthreads();
     }
-    a.status[i] = st;
-    a.Q.push(q1, r1, 2 * j);
-    a.Q.push(q2, r2, 2 * j + 1);
+    if (lane == 0) {
+      if (corr) { last4[4 * l] = cl[0]; last4[4 * l + 1] = cl[1]; last4[4 * l + 2] = cl[2]; }
+      unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
+      if (n_lost) atomicAdd(&row[ST_LOST], (unsigned long long)n_lost);
+      if (n_copies) atomicAdd(&row[ST_COPIES], (unsigned long long)n_copies);
+      if (n_over) atomicAdd(&row[ST_OVERLIMIT], (unsigned long long)n_over);
+    }
+    __syncthreads();
   }
-  last4[4 * l] = cl[0]; last4[4 * l + 1] = cl[1]; last4[4 * l + 2] = cl[2];
-  unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
-  if (lost) atomicAdd(&row[ST_LOST], lost);
-  if (copies) atomicAdd(&row[ST_COPIES], copies);
 }
 
 // init_crandom at a Shape call: Philox(g, epoch, 0, "CORR") words 0..2 (the kernel uses prandom).
@@ -2510,8 +2793,11 @@ __global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const
   store_rec(xsend + (size_t)p * xcap, h);
 }
 
-__global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint32_t S, uint32_t shard,
-                                                 uint32_t xcap, Queues Q) {
+// Receive: every exchanged record is due this window (only due records cross shards) and joins the
+// deliveries. Send side: a wheel copy the extraction sent to a peer leaves its sender's queue.
+__global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, const tgsim_record* xsend, uint32_t S,
+                                                 uint32_t shard, uint32_t xcap, Queues Q, uint32_t* pend,
+                                                 uint32_t lo, uint32_t nloc) {
   const int64_t t_end = Q.sc->t_end;
   const uint64_t total = (uint64_t)S * xcap;
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -2526,7 +2812,17 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, uint
         if (i == 1) atomicOr(&Q.sc->err, ERR_EXCH_HDR);
       } else if ((int64_t)i <= n) {
         load_rec(xrecv + j, rec);
-        q = rec.t < t_end ? Q_D : Q_L;
+        rec.meta &= ~(uint32_t)TGSIM_F_WHEEL;
+        if (rec.t < t_end) q = Q_D;
+        else atomicOr(&Q.sc->err, ERR_EXCH_HDR);
+      }
+      const int64_t ns = xsend[(size_t)p * xcap].t;
+      if (ns > 0 && ns < (int64_t)xcap && (int64_t)i <= ns) {
+        const uint4 b = reinterpret_cast<const uint4*>(xsend + j)[1];
+        if (b.z & TGSIM_F_WHEEL) {
+          const uint32_t src = reinterpret_cast<const uint4*>(xsend + j)[0].z;
+          if (src - lo < nloc) atomicSub(&pend[src - lo], 1u);
+        }
       }
     }
     Q.push(q, rec, it);
@@ -2817,7 +3113,7 @@ static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const ui
 // and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
 static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
-  p.A = d.A; p.shape = d.shape; p.X = d.X; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
+  p.A = d.A; p.shape = d.shape; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= 2048: nloc <= 2^20 (checked at create)
@@ -2832,9 +3128,9 @@ static hipError_t run_token_bucket(Dev& d) {
   return launch_rest(d, p, d.keys0, d.vals0);
 }
 
-// The deferred messages of correlated senders (k_shape): group by sender, order (t_send, seq),
-// then netem per sender in that order.
-static hipError_t run_shape_corr(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
+// The deferred messages (k_shape: correlated or queue-heavy senders): group by sender, order
+// (t_send, seq); the heavy senders' due wheel records (H) grouped by sender; then k_shape_seq.
+static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
   hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.m_src, n_dev,
                      d.lo, d.keys0, d.vals0);
@@ -2842,15 +3138,26 @@ static hipError_t run_shape_corr(Dev& d, const ShapeArgs& a, uint32_t n_staged) 
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
   uint32_t *keys, *vals;
-  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, nullptr, &keys, &vals));
+  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
   hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
                      d.seg_off, n_dev, d.cap_rec);
   TG_CHECK(hipGetLastError());
   TG_CHECK(launch_rest(d, p, keys, vals));
-  hipLaunchKernelGGL(k_shape_corr, dim3((d.nloc + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, a,
-                     d.corr_sorted, d.seg_off, d.cor_rho, d.cor_last);
+  const uint32_t* hoff = nullptr;
+  const uint32_t* hidx = nullptr;
+  if (a.heavy.pend) {
+    BktSrc hs = bkt_queue(d, Q_A);
+    hs.keys = d.hkeys; hs.vals = d.hvals; hs.qc = nullptr; hs.mode = 3; hs.n_ptr = &d.sc->n_hrec; hs.cap = d.h_cap;
+    uint32_t *hk, *hv;
+    TG_CHECK(group_by_bkt(d, hs, d.nloc, kNoMedium, nullptr, &hk, &hv));
+    hoff = d.seg_off;
+    hidx = hv;
+  }
+  const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
+  hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, hoff, hidx,
+                     d.H, d.cor_rho, d.cor_last, d.X);
   return hipGetLastError();
 }
 
@@ -2863,10 +3170,14 @@ hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
 
 hipError_t window_begin(Dev& d, uint32_t n_staged) {
   Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
+  HeavyOut ho;
+  ho.hv = n_staged ? d.heavy : Heavy{};  // H feeds only the staged messages' sequential lane
+  ho.geo = Geo{d.N, d.S, d.shard}; ho.H = d.H; ho.hkeys = d.hkeys; ho.hvals = d.hvals; ho.hcap = d.h_cap;
+  ho.lo = d.lo;
   if (!n_staged) {
     ProfScope ps_(d, KID_EXTRACT);
     hipLaunchKernelGGL(k_extract, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.regions, d.plan_start,
-                       d.plan_off, d.arena, Q);
+                       d.plan_off, d.arena, Q, ho);
   }
   TG_CHECK(hipGetLastError());
   if (n_staged) {
@@ -2877,16 +3188,17 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
+    a.heavy = d.heavy;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
     constexpr uint32_t ne = kStreamBlocks;  // 512 / 1024 / 4096 measured the same
     static_assert(ne % 8 == 0, "extract blocks keep their XCD");
     {
       ProfScope ps_(d, KID_SHAPE);  // extraction + netem
       hipLaunchKernelGGL(k_extract_shape, dim3(ne + g), dim3(kBlock), 0, d.stream, d.regions,
-                         d.plan_start, d.plan_off, d.arena, Q, a, ne);
+                         d.plan_start, d.plan_off, d.arena, Q, a, ne, ho);
     }
     TG_CHECK(hipGetLastError());
-    if (d.any_corr) TG_CHECK(run_shape_corr(d, a, n_staged));
+    if (d.any_corr || d.heavy.pend) TG_CHECK(run_shape_seq(d, a, n_staged));
   }
   TG_CHECK(run_token_bucket(d));
   if (d.S > 1) {
@@ -2905,11 +3217,12 @@ hipError_t window_end(Dev& d) {
   if (d.S > 1) {
     Queues Q = make_queues(d);
     const uint64_t total = (uint64_t)d.S * d.xcap;
-    hipLaunchKernelGGL(k_recv, dim3(grid_for(total)), dim3(kBlock), 0, d.stream, d.xrecv, d.S, d.shard, d.xcap, Q);
+    hipLaunchKernelGGL(k_recv, dim3(grid_for(total)), dim3(kBlock), 0, d.stream, d.xrecv, d.xsend, d.S, d.shard,
+                       d.xcap, Q, d.pend, d.lo, d.nloc);
     TG_CHECK(hipGetLastError());
   }
   EmitPolicy p;
-  p.D = d.D; p.lo = d.lo; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
@@ -2936,7 +3249,7 @@ hipError_t window_end(Dev& d) {
   {
     ProfScope ps_(d, KID_REGION_FILL);
     hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L, d.arena,
-                       d.dirs, d.slots, d.hist, d.tot);
+                       d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc);
   }
   return hipGetLastError();
 }

@@ -10,7 +10,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "tgsim_dev.h"
@@ -29,7 +31,10 @@ struct tgsim_ctx {
   std::vector<ShapeDev> shape_h;
   std::vector<uint8_t> flags_h;
   std::vector<uint32_t> ip_h;
-  std::vector<uint32_t> id_of_h;  // ip - data_net -> instance id
+  uint64_t space = 0;               // addresses in the data subnet
+  // ip - data_net -> instance for addresses that are not their owner's initial one (data_net + 2 + id):
+  // the reverse map stays O(moved instances), whatever the prefix length
+  std::unordered_map<uint32_t, uint32_t> moved;
   std::vector<std::vector<RuleDev>> rules_h;
   std::vector<uint32_t> tb_reset;
   std::vector<uint32_t> rho_h;       // [4 * nloc] netem correlations per local sender
@@ -58,6 +63,19 @@ struct tgsim_ctx {
   uint32_t storm_nw = 0, add_state = 0, add_target = 0;
   int64_t add_twait = 0;
   std::vector<void*> allocs;
+  // netem queue limit: the host's proof that no sender can reach the limit in a
+  // window (then the kernels skip the test). pend_bound >= every local sender's queued copies at the
+  // next window start: the device's pend_max at each synchronisation, plus what one window can add
+  // (mult * the window's per-sender message bound) for each window since.
+  uint64_t pend_bound = 0;
+  std::vector<uint32_t> hcnt;        // host-staged messages per local sender this window
+  std::vector<uint32_t> hcnt_touched;
+  uint32_t win_m_host = 0;           // max of hcnt
+  uint64_t win_m_extra = 0;          // device-staged messages (storm fanout, enqueue_device n): any sender
+  uint32_t win_m_inbox = 0;          // flood forwards staged: (D - 1) per delivery of the sender's last inbox
+  uint32_t inbox_max_h = 0;          // longest inbox run of the last window (read at the flood reaction)
+  bool any_dup = false;
+  int64_t max_tsend_h = INT64_MIN;   // latest host-staged send time (checked against t_end before launch)
   // topics (tgsim_sync_publish / _subscribe): entries live in device arenas, sorted by (topic,
   // position) per batch; the host keeps each topic's runs of consecutive positions
   // latest time of the host-submitted signals per state: a batch that goes back in time is
@@ -209,7 +227,19 @@ extern "C" void tgsim_destroy(tgsim_ctx* c) {
   delete c;
 }
 
+static int create_impl(const tgsim_config* cfg, tgsim_ctx** out);
+
+// Every allocation failure inside the C ABI is an error code, never an exception across extern "C".
 extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
+  try {
+    return create_impl(cfg, out);
+  } catch (const std::bad_alloc&) {
+    if (out) *out = nullptr;
+    return TGSIM_ENOMEM;
+  }
+}
+
+static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   if (!out) return TGSIM_EINVAL;
   *out = nullptr;
   if (!cfg || cfg->n_instances == 0 || cfg->n_shards == 0 || cfg->n_shards > (uint32_t)kMaxShards ||
@@ -221,6 +251,10 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   if (hipSetDevice((int)cfg->device) != hipSuccess) return TGSIM_ENODEV;
 
   tgsim_ctx* c = new tgsim_ctx();
+  struct Guard {  // a bad_alloc below frees the half-built context
+    tgsim_ctx*& c;
+    ~Guard() { if (c) tgsim_destroy(c); }
+  } guard{c};
   c->cfg = *cfg;
   c->N = cfg->n_instances;
   c->S = cfg->n_shards;
@@ -238,7 +272,6 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   c->data_net = cfg->data_subnet & c->data_mask;
   const uint64_t space = 1ull << (32 - c->data_len);
   if ((uint64_t)c->N + 3 > space || (kExternalIp & c->data_mask) == c->data_net) {
-    delete c;
     return TGSIM_EINVAL;
   }
   Dev& d = c->d;
@@ -252,7 +285,6 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   // group-by limits: <= 2^20 instances per shard, <= 2^24 sync states, <= 2048 wheel slots
   if (cap_msgs > 0x7FFFFFFFull || cap_rec > 0x7FFFFFFFull || d.slots < 2 || d.slots > (uint32_t)kMaxBins ||
       c->nloc > (1u << 20) || (cfg->max_states && cfg->max_states > (1u << 24))) {
-    delete c;
     return TGSIM_EINVAL;
   }
   d.cap_msgs = (uint32_t)cap_msgs;
@@ -267,12 +299,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   d.s_cap = std::max<uint32_t>(c->nloc, 1u << 16);
 
   hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
-  if (e != hipSuccess) { delete c; return TGSIM_EHIP; }
+  if (e != hipSuccess) return TGSIM_EHIP;
   c->own_stream = true;
-  if (hipHostMalloc((void**)&d.h_sc, sizeof(DevScalars), hipHostMallocDefault) != hipSuccess) {
-    tgsim_destroy(c);
-    return TGSIM_ENOMEM;
-  }
+  if (hipHostMalloc((void**)&d.h_sc, sizeof(DevScalars), hipHostMallocDefault) != hipSuccess) return TGSIM_ENOMEM;
   memset(d.h_sc, 0, sizeof(DevScalars));
 
   const size_t nl1 = (size_t)c->nloc + 1;
@@ -281,6 +310,8 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.sc, 1);
   rc |= dalloc(c, &d.shape, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.moff, segK);
   rc |= dalloc(c, &d.flags, c->N);
   rc |= dalloc(c, &d.ip, c->N);
   rc |= dalloc(c, &d.rule_off, nl1);
@@ -356,7 +387,7 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.w_target, d.max_waiters);
   rc |= dalloc(c, &d.w_twait, d.max_waiters);
   rc |= dalloc(c, &d.w_release, d.max_waiters);
-  if (rc) { tgsim_destroy(c); return TGSIM_ENOMEM; }
+  if (rc) return TGSIM_ENOMEM;
   c->rules_cap_dev = 1;
   init_launch_geometry(d);
 
@@ -367,8 +398,9 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
             hipMemsetAsync(d.st_nchunks, 0, d.max_states * sizeof(uint32_t), s) == hipSuccess &&
             hipMemsetAsync(d.st_last, 0, d.max_states * sizeof(int64_t), s) == hipSuccess &&
             hipMemsetAsync(d.rule_off, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
-            hipMemsetAsync(d.inbox, 0, nl1 * sizeof(uint32_t), s) == hipSuccess;
-  if (!ok) { tgsim_destroy(c); return TGSIM_EHIP; }
+            hipMemsetAsync(d.inbox, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
+            hipMemsetAsync(d.pend, 0, std::max<size_t>(c->nloc, 1) * sizeof(uint32_t), s) == hipSuccess;
+  if (!ok) return TGSIM_EHIP;
 
   // initial state = after the sidecar's Config{Network:"default", Enable:true} (sidecar_handler.go:26-29)
   c->shape_h.assign(c->nloc, default_shape());
@@ -376,18 +408,16 @@ extern "C" int tgsim_create(const tgsim_config* cfg, tgsim_ctx** out) {
   c->corr_epoch.assign(c->nloc, 0u);
   c->flags_h.assign(c->N, 1u);  // enabled, external routing off (zero RoutingPolicy -> disable)
   c->ip_h.resize(c->N);
-  c->id_of_h.assign(space, UINT32_MAX);
-  for (uint32_t g = 0; g < c->N; ++g) {
-    c->ip_h[g] = c->data_net + 2u + g;
-    c->id_of_h[2u + g] = g;
-  }
+  c->space = space;
+  c->hcnt.assign(c->nloc, 0u);
+  for (uint32_t g = 0; g < c->N; ++g) c->ip_h[g] = c->data_net + 2u + g;
   c->rules_h.assign(c->nloc, {});
   std::vector<int64_t> xs(std::max<uint32_t>(c->nloc, 1), kNegInf);
   if (hipMemcpy(d.X, xs.data(), xs.size() * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
-    tgsim_destroy(c);
     return TGSIM_EHIP;
   }
   *out = c;
+  c = nullptr;  // owned by the caller now
   return TGSIM_OK;
 }
 
@@ -417,7 +447,8 @@ extern "C" int tgsim_shard_range(const tgsim_ctx* c, uint32_t* lo, uint32_t* hi)
 static int check_device_errors(tgsim_ctx* c) {
   const uint32_t e = c->d.h_sc->err;
   if (!e) return TGSIM_OK;
-  if (e & (ERR_CAP_A | ERR_CAP_D | ERR_CAP_L | ERR_CAP_X | ERR_ARENA | ERR_REGIONS | ERR_SIG_CAP | ERR_STATE_CHUNKS))
+  if (e & (ERR_CAP_A | ERR_CAP_D | ERR_CAP_L | ERR_CAP_X | ERR_ARENA | ERR_REGIONS | ERR_SIG_CAP | ERR_STATE_CHUNKS |
+           ERR_QUEUE_CAP))
     return fail(c, TGSIM_ECAPACITY, "device capacity exceeded (err bits 0x%x)", e);
   if (e & (ERR_CAUSAL | ERR_SIG_ORDER)) return fail(c, TGSIM_ECAUSALITY, "causality violation on device (err 0x%x)", e);
   if (e & ERR_UNSORTED_TARGET)
@@ -429,6 +460,7 @@ static int check_device_errors(tgsim_ctx* c) {
 static int sync_and_check(tgsim_ctx* c) {
   HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, sync_scalars(c->d), "sync");
+  if (!c->in_window) c->pend_bound = std::min<uint64_t>(c->pend_bound, c->d.h_sc->pend_max);
   if (c->now_from_device && !c->in_window) {
     c->horizon = c->d.h_sc->T;
     c->now = c->d.h_sc->t_end;
@@ -460,6 +492,7 @@ extern "C" int tgsim_get_stats(tgsim_ctx* c, tgsim_stats* o) {
   o->tb_items = h.st[ST_TB_ITEMS];
   o->extracted = h.st[ST_EXTRACTED];
   o->inserted = h.st[ST_INSERTED];
+  o->overlimit = st[ST_OVERLIMIT];
   return rc;
 }
 
@@ -578,14 +611,23 @@ extern "C" int tgsim_set_policy(tgsim_ctx* c, uint32_t g, int32_t policy) {  // 
   return TGSIM_OK;
 }
 
+// The instance holding data-subnet address offset off, or UINT32_MAX.
+static uint32_t holder_of(const tgsim_ctx* c, uint32_t off) {
+  const auto it = c->moved.find(off);
+  if (it != c->moved.end()) return it->second;
+  if (off >= 2 && off - 2 < c->N && c->ip_h[off - 2] == c->data_net + off) return off - 2;
+  return UINT32_MAX;
+}
+
 static int set_ip(tgsim_ctx* c, uint32_t g, uint32_t ip) {
   if ((ip & c->data_mask) != c->data_net) return fail(c, TGSIM_EINVAL, "ip outside the data subnet");
   const uint32_t off = ip - c->data_net;
-  if (off <= 1 || off == (uint32_t)(c->id_of_h.size() - 1)) return fail(c, TGSIM_EINVAL, "reserved address");
-  if (c->id_of_h[off] != UINT32_MAX && c->id_of_h[off] != g) return fail(c, TGSIM_EINVAL, "address already in use");
-  c->id_of_h[c->ip_h[g] - c->data_net] = UINT32_MAX;
+  if (off <= 1 || off == (uint32_t)(c->space - 1)) return fail(c, TGSIM_EINVAL, "reserved address");
+  const uint32_t h = holder_of(c, off);
+  if (h != UINT32_MAX && h != g) return fail(c, TGSIM_EINVAL, "address already in use");
+  c->moved.erase(c->ip_h[g] - c->data_net);
   c->ip_h[g] = ip;
-  c->id_of_h[off] = g;
+  if (off != g + 2u) c->moved[off] = g;
   c->ip_dirty = true;
   return TGSIM_OK;
 }
@@ -642,7 +684,11 @@ static int upload_tables(tgsim_ctx* c) {
     HIPCK(c, hipMemcpyAsync(d.shape, c->shape_h.data(), c->nloc * sizeof(ShapeDev), hipMemcpyHostToDevice, d.stream), "upload shapes");
     HIPCK(c, hipMemcpyAsync(d.cor_rho, c->rho_h.data(), c->rho_h.size() * 4, hipMemcpyHostToDevice, d.stream), "upload shapes");
     d.any_corr = false;
-    for (const ShapeDev& sh : c->shape_h) d.any_corr |= (sh.flags & kShCorr) != 0;
+    c->any_dup = false;
+    for (const ShapeDev& sh : c->shape_h) {
+      d.any_corr |= (sh.flags & kShCorr) != 0;
+      c->any_dup |= sh.dup_t != 0;
+    }
     copied = true;
   }
   if (!c->corr_reset.empty()) {
@@ -729,6 +775,12 @@ extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   int rc = validate_msgs(c, m, n);
   if (rc) return rc;
   if (!n) return TGSIM_OK;
+  for (size_t i = 0; i < n; ++i) {  // per-sender counts for the queue-limit test, latest send time
+    const uint32_t l = m->src[i] - c->lo;
+    if (c->hcnt[l]++ == 0) c->hcnt_touched.push_back(l);
+    c->win_m_host = std::max(c->win_m_host, c->hcnt[l]);
+    c->max_tsend_h = std::max(c->max_tsend_h, m->t_send[i]);
+  }
   Dev& d = c->d;
   const size_t o = c->n_staged;
   HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
@@ -746,6 +798,7 @@ extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if ((uint64_t)c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (!n) return TGSIM_OK;
+  c->win_m_extra += n;  // any one sender may hold all of them (queue-limit test)
   Dev& d = c->d;
   const size_t o = c->n_staged;
   HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
@@ -757,8 +810,43 @@ extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t
   return TGSIM_OK;
 }
 
+// The window's queue-limit test. The kernels test every sender only when the host
+// cannot prove that none can reach the limit: pend_bound (queued copies of any sender at this
+// window's start) + mult * (the most messages one sender can have staged) <= TGSIM_NETEM_LIMIT.
+static int plan_queue_limit(tgsim_ctx* c) {
+  Dev& d = c->d;
+  const uint64_t mult = c->any_dup ? 2 : 1;
+  const uint64_t m_uniform = std::min<uint64_t>((uint64_t)c->win_m_host + c->win_m_extra, 0x7FFFFFFFull);
+  const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->inbox_max_h;
+  const bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+  d.heavy = Heavy{};
+  if (gate) {
+    if (!d.H) {  // first window that needs the H list: room for every due record of a window
+      HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+      const size_t cap = (size_t)kNSub * d.subcap;
+      if (dalloc(c, &d.H, cap) || dalloc(c, &d.hkeys, cap) || dalloc(c, &d.hvals, cap)) return TGSIM_ENOMEM;
+      d.h_cap = (uint32_t)cap;
+    }
+    d.heavy.pend = d.pend;
+    d.heavy.inbox = c->win_m_inbox ? d.inbox : nullptr;
+    d.heavy.m_uniform = (uint32_t)m_uniform;
+    d.heavy.m_inbox = c->win_m_inbox;
+    d.heavy.mult = (uint32_t)mult;
+  }
+  c->pend_bound = std::min<uint64_t>(c->pend_bound + mult * m_max, 1ull << 62);
+  for (uint32_t l : c->hcnt_touched) c->hcnt[l] = 0;
+  c->hcnt_touched.clear();
+  c->win_m_host = 0;
+  c->win_m_extra = 0;
+  c->win_m_inbox = 0;
+  c->max_tsend_h = INT64_MIN;
+  return TGSIM_OK;
+}
+
 static int begin_common(tgsim_ctx* c) {
   int rc = upload_tables(c);
+  if (rc) return rc;
+  rc = plan_queue_limit(c);
   if (rc) return rc;
   HIPCK(c, window_begin(c->d, c->n_staged), "window_begin");
   c->n_status_last = c->n_staged;
@@ -772,6 +860,9 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  // a host-staged message sent at or after t_end is refused before anything changes (the context
+  // stays usable, as in the oracle); device-staged batches are checked on the device
+  if (c->max_tsend_h >= t_end) return fail(c, TGSIM_ECAUSALITY, "a staged message is sent at/after t_end");
   HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window(c->d, t_end), "set window");
   return begin_common(c);
@@ -987,6 +1078,7 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   uint32_t parts = 0;
   HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, &parts), "gen storm");
   c->n_staged += (uint32_t)n;
+  c->win_m_extra += fanout;
   if (c->S == 1) {
     // SignalAndWait(state, N) by every instance: the return values are unused by the plan, so the
     // batch is committed count-only (count, first/last time) - deferred to the next
@@ -1109,6 +1201,10 @@ extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   if ((uint64_t)c->n_staged + total > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   HIPCK(c, launch_flood_emit(c->d, n, c->n_staged, size, c->horizon), "flood emit");
   c->n_staged += total;
+  // forwards of a sender <= (D - 1) per delivery of its inbox run (queue-limit test; the device
+  // reads each sender's run, the host bound takes the longest)
+  c->win_m_inbox = f.D > 1 ? f.D - 1 : 0;
+  c->inbox_max_h = c->d.h_sc->max_inbox;
   if (n_fwd) *n_fwd = total;
   return TGSIM_OK;
 }

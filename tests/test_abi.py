@@ -45,7 +45,7 @@ def test_binding_covers_header():
     bound = {"tgsim_" + k for k in list(A._SIGS) + list(A._SIGS_HIP)}
     assert set(A.header_symbols()) <= bound, set(A.header_symbols()) - bound
     assert hip.version().decode().startswith("tgsim-mi355x")
-    assert hip.abi_version() == 1
+    assert hip.abi_version() == 2
     names = [hip.kernel_name(k).decode() for k in range(hip.kernel_classes())]
     assert "k_extract_shape" in names and "k_emit_bucket" in names and "k_tb_bucket" in names
 
