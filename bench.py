@@ -30,17 +30,36 @@ MS = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "simulated msgs delivered/sec (100k-inst storm) + % HBM roofline, 1/2/4/8 GPU"
 
-# Algorithmic bytes each kernel class must move per unit of work; every class
-# below is exactly one kernel, so its HIP-event average agrees with rocprofv3's for that kernel.
+# SURVEY.md 8(d)'s algorithmic bytes, attributed to the kernel that does that part of the path:
+#   per input message: read the 24 B record + write its 1 B status (netem + routing: k_extract_shape /
+#   k_shape); per delivered copy: write the 24 B delivery record (k_emit_bucket); per window: read the
+#   48 B shape table entry of every local sender (with the netem pass) and read + write its 16 B
+#   token-bucket state (k_tb_bucket). Kernels that only move the implementation's own structures
+#   (wheel extraction and insertion, partition passes) have none. roofline.frac uses these.
+ALG_MODELS = {
+    "k_extract_shape": lambda d, n, w: 25 * d["msgs_in"] + 48 * n * w,
+    "k_tb_bucket": lambda d, n, w: 16 * n * w,
+    "k_emit_bucket": lambda d, n, w: 24 * d["delivered"],
+    "k_gen_storm": lambda d, n, w: 24 * d["msgs_in"],
+}
+
+
+def alg_bytes_step(d: dict, n_local: int, windows: int) -> int:
+    """SURVEY.md 8(d) B_total of one shard: 25 B per input + 24 B per delivery + 48 B shape + 16 B
+    token state per local sender and window (no rules in these workloads; sync counters ~0)."""
+    return 25 * d["msgs_in"] + 24 * d["delivered"] + (48 + 16) * n_local * windows
+
+
+# The implementation's own bytes per launch (what each kernel reads and writes, DESIGN.md 5):
+# roofline.kernel_bw_eff ("how close does the kernel run to HBM speed") uses these; it is not the
+# algorithmic fraction.
 #   k_extract_shape (one launch, two passes): netem reads the 24 B message + writes its 1 B status
-#      + writes each 32 B copy record; the extraction reads + writes each due 32 B
-#     wheel record (k_extract alone when nothing is staged)
+#     + writes each 32 B copy record; the extraction reads + writes each due 32 B wheel record
 #   k_tb_bucket: per copy, read the 32 B record + its 8 B (key, index), write the 32 B departed record
 #   k_emit_bucket: per delivery, read the 32 B record + 8 B (key, index), write the 32 B SoA delivery
 #   k_extract: read + write one 32 B wheel record; k_wheel_scatter: read 32 + 8 B key/index, write 32 B
 #   k_gen_storm: write the 24 B message
 BYTE_MODELS = {
-    # extraction of due wheel records (64 B each) and netem of the staged messages share a launch
     "k_extract_shape": lambda d: 25 * d["msgs_in"] + 32 * d["copies"] + 64 * d["extracted"],
     "k_tb_bucket": lambda d: 72 * d["tb_items"],
     "k_emit_bucket": lambda d: 72 * d["delivered"],
@@ -52,6 +71,79 @@ BYTE_MODELS = {
     "k_flood_count": lambda d: 21 * d["delivered"],
     "k_flood_emit": lambda d: 24 * d["msgs_in"] + 17 * d["delivered"],
 }
+
+
+def source_hash() -> str:
+    """SHA-256 (16 hex) of the kernel sources and the ABI header: a committed PMC summary is this
+    run's measurement only if it was taken on the same code."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "testground_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "testground_amd", "csrc", "*.h")) +
+                   [os.path.join(ROOT, "include", "tgsim.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel: str, workload: str, n_gpus: int):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary of this same command
+    (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) - only from a
+    summary stamped with this source hash, workload and GPU count; otherwise None."""
+    import glob
+    want = source_hash()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic*.json")), reverse=True):
+        try:
+            j = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if j.get("source_hash") != want or j.get("workload") != workload or j.get("n_gpus") != n_gpus:
+            continue
+        k = j.get("kernels", {}).get(kernel)
+        if k:
+            return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"nproc": avail, "cpu_count": os.cpu_count(), "cpu_model": model}
+
+
+def roofline(dominant: str, delta: dict, kern_ms: float, kern_n: int, n_local: int, windows: int,
+             workload: str, n_gpus: int, b_total: int, elapsed: float) -> dict:
+    """roofline.frac = SURVEY.md 8(d) algorithmic bytes of the dominant kernel per launch / its
+    average launch time / 8 TB/s; frac_step = the whole path's B_total / wall time / (n_gpus x 8 TB/s);
+    kernel_bw_eff = the kernel's own bytes (BYTE_MODELS) at its launch time, as a fraction of peak."""
+    avg_ms = kern_ms / max(kern_n, 1)
+    alg = ALG_MODELS.get(dominant, lambda d, n, w: 0)(delta, n_local, windows) / max(kern_n, 1)
+    impl = BYTE_MODELS.get(dominant, lambda d: 0)(delta) / max(kern_n, 1)
+    achieved = alg / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
+    impl_gbs = impl / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
+    traffic, src = pmc_traffic(dominant, workload, n_gpus)
+    step_gbs = b_total / elapsed / 1e9
+    return {
+        "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+        "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+        "step_achieved": step_gbs, "frac_step": step_gbs / (n_gpus * HBM_PEAK_GBS),
+        "step_alg_bytes": b_total,
+        "kernel_bw_eff": impl_gbs / HBM_PEAK_GBS, "impl_bytes_per_launch": impl,
+        "source_hash": source_hash(),
+    }
 
 
 def parse():
@@ -128,14 +220,12 @@ def cpu_baseline(args, shapes):
             break
     delivered = sim.stats()["delivered"] - d0
     sim.close()
-    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port",
+    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port", **host_cpu(),
             "sample": f"oracle/ (single-threaded C restatement), same {args.instances}-instance storm: "
                       f"rounds {warm}..{r - 1} timed ({el:.1f} s, {delivered} deliveries) after {warm} "
                       f"warm-up rounds"}
 
 
-PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
-PMC_TRAFFIC_FLOOD = "profiles/r01/pmc_traffic_flood.json"
 
 
 def main():
@@ -249,25 +339,16 @@ def main():
     kern_ms = prof[0] - base_prof[0]
     kern_n = prof[1] - base_prof[1]
     delivered = delta["delivered"]
+    b_total = alg_bytes_step(delta, sim.hi - sim.lo, args.steps)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         all_reduce(t, dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        v = torch.tensor([delivered], dtype=torch.int64, device="cuda")
+        v = torch.tensor([delivered, b_total], dtype=torch.int64, device="cuda")
         all_reduce(v, dist.ReduceOp.SUM)
-        delivered = int(v.item())
-
-    bytes_total = BYTE_MODELS[dominant](delta)
-    avg_ms = kern_ms / max(kern_n, 1)
-    achieved = (bytes_total / max(kern_n, 1)) / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
-    # measured HBM bytes per launch of the dominant kernel: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
-    # this same command (tools/prof_round.sh -> tools/pmc_traffic.py), committed under profiles/
-    traffic, traffic_src = None, None
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_TRAFFIC)
-    if os.path.exists(pmc):
-        k = json.load(open(pmc))["kernels"].get(dominant)
-        if k:
-            traffic, traffic_src = k["traffic_bytes"], PMC_TRAFFIC
+        delivered, b_total = int(v[0].item()), int(v[1].item())
+    roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
+                    elapsed)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, shapes)
@@ -294,18 +375,7 @@ def main():
                 "delivered_in_timed_steps": delivered,
                 "simulated_ms_per_step": (sim_t1 - sim_t0) / 1e6 / args.steps,
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dominant,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "avg_launch_ms": avg_ms,
-                "bytes_per_launch": bytes_total / max(kern_n, 1),
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
             "kernels_probe": warm_kernels,
         }
@@ -364,7 +434,7 @@ def flood_cpu_baseline(args, shapes, graph):
             break
     delivered = sim.stats()["delivered"]
     sim.close()
-    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port",
+    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port", **host_cpu(),
             "sample": f"oracle/ (single-threaded C restatement), same {N}-instance flood: windows 0..{w - 1} "
                       f"from the first publication ({el:.1f} s, {delivered} deliveries, incl. the reaction)"}
 
@@ -457,23 +527,17 @@ def main_flood(args):
     delta = {k: s1[k] - s0[k] for k in s1}
     kern_ms, kern_n = prof[0] - base_prof[0], prof[1] - base_prof[1]
     delivered = delta["delivered"]
+    b_total = alg_bytes_step(delta, sim.hi - sim.lo, args.steps)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
-        v = torch.tensor([delivered], dtype=torch.int64)
+        v = torch.tensor([delivered, b_total], dtype=torch.int64)
         if not rehearsal:
             t, v = t.cuda(), v.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        elapsed, delivered = float(t.item()), int(v.item())
-    bytes_total = BYTE_MODELS[dominant](delta)
-    avg_ms = kern_ms / max(kern_n, 1)
-    achieved = (bytes_total / max(kern_n, 1)) / (avg_ms * 1e-3) / 1e9 if kern_n else 0.0
-    traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, PMC_TRAFFIC_FLOOD)
-    if os.path.exists(pmc):
-        k = json.load(open(pmc))["kernels"].get(dominant)
-        if k:
-            traffic, traffic_src = k["traffic_bytes"], PMC_TRAFFIC_FLOOD
+        elapsed, delivered, b_total = float(t.item()), int(v[0].item()), int(v[1].item())
+    roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "flood", world, b_total,
+                    elapsed)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = flood_cpu_baseline(args, shapes, graph)
@@ -490,9 +554,7 @@ def main_flood(args):
                        "instances": N, "msg_bytes": args.flood_size,
                        "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
                        "delivered_in_timed_steps": delivered},
-            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src, "avg_launch_ms": avg_ms, "bytes_per_launch": bytes_total / max(kern_n, 1)},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "kernels_probe": warm_kernels,
         }), flush=True)

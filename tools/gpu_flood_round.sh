@@ -1,6 +1,6 @@
 #!/bin/bash
 # Config 5 evidence in one gpurun call: rocprofv3 trace + stats of the flood bench, FETCH_SIZE /
-# WRITE_SIZE passes (-> profiles/r01/pmc_traffic_flood.json on the box), the bench line with its
+# WRITE_SIZE passes (-> profiles/r02/pmc_traffic_flood.json on the box), the bench line with its
 # CPU baseline.   tools/gpu_flood_round.sh <outdir-under-gpurun_out>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -15,7 +15,7 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $
   -- python3 -u $B --steps 5 --warmup 100 > $OUT/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_write -o run --output-format csv \
   -- python3 -u $B --steps 5 --warmup 100 > $OUT/pmc_write.log 2>&1 || { echo PMC_WRITE_FAIL; exit 1; }
-python3 tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_traffic_flood.json
-mkdir -p profiles/r01 && cp $OUT/pmc_traffic_flood.json profiles/r01/pmc_traffic_flood.json
+python3 tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_traffic_flood.json flood 1
+mkdir -p profiles/r02 && cp $OUT/pmc_traffic_flood.json profiles/r02/pmc_traffic_flood.json
 timeout -k 10 300 python -u bench.py --workload flood > $OUT/bench.log 2>&1 || { echo BENCH_FAIL; tail -30 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log | cut -c1-300
