@@ -184,6 +184,8 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
                                             uint32_t st, uint32_t nw, bool add, uint32_t add_state,
                                             uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
+// sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
+hipError_t launch_pend_max(Dev& d);
 // init_crandom on a Shape call: the state of local sender pairs[2i] re-seeded for epoch pairs[2i+1]
 hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n);
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack

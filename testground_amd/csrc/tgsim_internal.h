@@ -89,7 +89,7 @@ struct DevScalars {
   uint32_t sig_n;                    // size of the signal batch being processed
   uint64_t arena_head, arena_tail, arena_used, ins_off;  // arena ring (records)
   uint64_t sig_log_used;             // signal log entries used
-  uint32_t pend_max;                 // max over time of any local sender's queued-copy count (host gate)
+  uint32_t pend_max;                 // max over local senders of queued copies (k_pend_max, host gate)
   uint32_t pad_pm;
   // cumulative statistics (tgsim_stats)
   unsigned long long st[13];

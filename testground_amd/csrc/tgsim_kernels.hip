@@ -1105,26 +1105,31 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // Queue occupancy: a record entering the wheel for the first time (no
 // TGSIM_F_WHEEL) is counted in its sender's pend and marked; runs of one sender among a wave's 64
-// consecutive records share one atomic (the token bucket stages its output grouped by sender).
-__device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uint32_t nloc, uint32_t src, bool add,
-                                                uint32_t* pend_max) {
+// consecutive records share one atomic (the token bucket stages its output grouped by sender). The
+// atomics return nothing, so no wave waits on them.
+__device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uint32_t nloc, uint32_t src, bool add) {
   const uint32_t lane = lane_id();
   const uint32_t key = add && src - lo < nloc ? src - lo : 0xFFFFFFFFu;
   const uint32_t prev = __shfl_up(key, 1);
   const bool head = key != 0xFFFFFFFFu && (lane == 0 || prev != key);
   const uint64_t heads = __ballot(head);
   const uint64_t valid = __ballot(key != 0xFFFFFFFFu);
-  uint32_t post = 0;
   if (head) {
     // the run: this lane and the following lanes with the same key (heads end it)
     const uint64_t after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
     const uint32_t end = after ? (uint32_t)__ffsll((unsigned long long)after) - 1u : 64u;
     const uint64_t span = (end >= 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
-    const uint32_t n = (uint32_t)__popcll(valid & span);
-    post = atomicAdd(&pend[key], n) + n;
+    __hip_atomic_fetch_add(&pend[key], (uint32_t)__popcll(valid & span), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  post = wave_max(post);
-  if (lane == 0 && post) atomicMax(pend_max, post);
+}
+
+// The host's exact refresh of its occupancy bound: max over local senders of pend -> sc->pend_max
+// (zeroed by the host's memset first).
+__global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, uint32_t nloc, uint32_t* out) {
+  uint32_t mx = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock) mx = max(mx, pend[i]);
+  mx = wave_max(mx);
+  if (lane_id() == 0 && mx) atomicMax(out, mx);
 }
 
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
@@ -1172,7 +1177,9 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
 #pragma unroll
     for (int u = 0; u < kWheelUnroll; ++u) {
       const bool fresh = k[u] != 0xFFFFFFFFu && !(rb[u].z & TGSIM_F_WHEEL);
-      pend_count_wave(pend, lo, nloc, ra[u].z, fresh, &sc->pend_max);
+#ifndef TG_EXP_NO_SCATTER_INC
+      pend_count_wave(pend, lo, nloc, ra[u].z, fresh);
+#endif
       if (k[u] != 0xFFFFFFFFu) {
         const uint32_t pos = atomicAdd(&base[k[u]], 1u);
         v4u32* q = reinterpret_cast<v4u32*>(arena + off + pos);
@@ -1482,6 +1489,7 @@ struct EmitPolicy {
   const tgsim_record* D;
   uint32_t* pend;  // queue occupancy: a delivered wheel copy of a local sender no longer counts
   uint32_t lo, nloc;
+  bool want_max_inbox;  // flood: the longest inbox run -> sc->max_inbox (the host's forward bound)
   int64_t* o_t;
   uint32_t *o_src, *o_dst, *o_seq, *o_size, *o_flags, *o_coff;
 
@@ -1533,7 +1541,7 @@ struct BktFusedSmem {
   uint32_t k3[kBktCap];                  // batch index (emit: | !clone << 31)
   uint16_t key[kBktCap];                 // key of each slot, relative to the bucket's first key
   uint16_t ord[kBktCap];                 // by_pos: sorted position -> slot; else slot -> sorted position
-  uint32_t dec[1u << kBktFusedKeyBits];  // TB: per key, wheel copies that leave the sender's queue now
+                                         // (TB, after the GCRA: per key, wheel copies leaving the queue)
   uint32_t part[kBlock];
   uint32_t maxlen, flag;
 #ifdef TGSIM_PHASE_PROF
@@ -1587,7 +1595,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
                                                uint32_t* off2, uint32_t* medium, LargeSeg* large, DevScalars* sc,
                                                BktFusedSmem& sm, BktHead& h, const tgsim_record* batch,
                                                const KeyFn& keyfn, tgsim_record (&rec)[kIPT],
-                                               uint32_t (&slot)[kIPT]) {
+                                               uint32_t (&slot)[kIPT], bool want_max = false) {
   // XCD-aware bucket order: hardware dispatch puts block i on XCD i % 8, so consecutive buckets -
   // whose chunks share cache lines in every partition block's range - go to the same XCD's L2
   const uint32_t b = xcd_major(blockIdx.x, B);
@@ -1625,7 +1633,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     }
     __syncthreads();
     const uint32_t mx = bkt_count_body(kscr, sm.cnt, sm.part, h);
-    if (!by_pos && threadIdx.x == 0) atomicMax(&sc->max_inbox, mx);  // longest inbox run (flood forwards)
+    if (!by_pos && want_max && threadIdx.x == 0) atomicMax(&sc->max_inbox, mx);  // longest inbox run (flood)
     bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
     return false;
   }
@@ -1670,7 +1678,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     run += len;
   }
   __syncthreads();
-  if (!by_pos && threadIdx.x == 0 && sm.maxlen) atomicMax(&sc->max_inbox, sm.maxlen);
+  if (!by_pos && want_max && threadIdx.x == 0 && sm.maxlen) atomicMax(&sc->max_inbox, sm.maxlen);
   TG_PH(4);
   // slots + sort keys (from the registers: no second gather)
 #pragma unroll
@@ -1769,7 +1777,6 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     return;
   // the GCRA along each sender's run (one thread per sender); departures replace k1
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
-    sm.dec[i] = 0;
     const uint32_t a = i ? sm.cnt[i - 1] : 0u, e = sm.cnt[i];
     if (e == a || e - a > kBktRankMax) continue;
     const uint32_t sl = h.k0 + i;
@@ -1789,6 +1796,11 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     p.X[sl] = x;
   }
   __syncthreads();
+  // the run order is consumed: its LDS counts, per key, the wheel copies that leave the queue now
+  static_assert(sizeof(BktFusedSmem::ord) >= 4u << kBktFusedKeyBits, "dec fits the ord area");
+  uint32_t* dec = reinterpret_cast<uint32_t*>(sm.ord);
+  for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) dec[i] = 0;
+  __syncthreads();
   TG_PH(7);
   // route each departed copy from the registers (D now, L later, X another shard); one
   // reservation per queue for the whole block
@@ -1805,14 +1817,14 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     nD += code[u] == Q_D; nL += code[u] == Q_L; nX += code[u] >= Q_X0;
     if ((rec[u].meta & TGSIM_F_WHEEL) && code[u] != Q_L) {  // leaves its sender's queue now
       rec[u].meta &= ~(uint32_t)TGSIM_F_WHEEL;
-      atomicAdd(&sm.dec[sm.key[slot[u]]], 1u);
+      atomicAdd(&dec[sm.key[slot[u]]], 1u);
     }
   }
   if (threadIdx.x == 0) sm.flag = 0;
   __syncthreads();
   // this workgroup owns its senders' counters for the launch (long runs: k_rest, later)
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock)
-    if (sm.dec[i]) p.pend[h.k0 + i] -= sm.dec[i];
+    if (dec[i]) p.pend[h.k0 + i] -= dec[i];
   if (nX) sm.flag = 1;
   uint32_t tD, tL;
   block_scan2(nD, nL, sm.part, tD, tL);  // nD/nL: this thread's offsets inside the block's runs
@@ -1886,7 +1898,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
   tgsim_record rec[kIPT];
   uint32_t slot[kIPT];
   if (!bkt_fused_load<false>(src, poff, kv, kscr, vscr, kout, vout, bd, B, K, off, off2, medium, large, sc,
-                             sm, h, p.D, EmitKey{}, rec, slot))
+                             sm, h, p.D, EmitKey{}, rec, slot, p.want_max_inbox))
     return;
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
     const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
@@ -1908,7 +1920,9 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
       if (o < r0 || o >= r0 + kStageN) continue;
       const uint32_t i = o - r0;
       const tgsim_record& r = rec[u];
+#ifndef TG_EXP_NO_EMIT_DEC
       if ((r.meta & TGSIM_F_WHEEL) && r.src - p.lo < p.nloc) atomicSub(&p.pend[r.src - p.lo], 1u);
+#endif
       st_t[i] = r.t;
       st_u[i] = r.src; st_u[kStageN + i] = r.dst; st_u[2 * kStageN + i] = r.seq; st_u[3 * kStageN + i] = r.size;
       st_u[4 * kStageN + i] = r.meta & ~(uint32_t)(TGSIM_F_STAGE_D | TGSIM_F_WHEEL); st_u[5 * kStageN + i] = r.corrupt_off;
@@ -3161,6 +3175,12 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   return hipGetLastError();
 }
 
+hipError_t launch_pend_max(Dev& d) {
+  TG_CHECK(hipMemsetAsync(&d.sc->pend_max, 0, sizeof(uint32_t), d.stream));
+  hipLaunchKernelGGL(k_pend_max, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.pend, d.nloc, &d.sc->pend_max);
+  return hipGetLastError();
+}
+
 hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_reset_corr, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, pairs_dev, n, d.lo,
@@ -3222,7 +3242,7 @@ hipError_t window_end(Dev& d) {
     TG_CHECK(hipGetLastError());
   }
   EmitPolicy p;
-  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.want_max_inbox = d.fl.off != nullptr; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;

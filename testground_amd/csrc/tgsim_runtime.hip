@@ -65,9 +65,10 @@ struct tgsim_ctx {
   std::vector<void*> allocs;
   // netem queue limit: the host's proof that no sender can reach the limit in a
   // window (then the kernels skip the test). pend_bound >= every local sender's queued copies at the
-  // next window start: the device's pend_max at each synchronisation, plus what one window can add
-  // (mult * the window's per-sender message bound) for each window since.
+  // next window start: the exact maximum when last refreshed (k_pend_max, only when the bound is
+  // inconclusive), plus what one window can add (mult * its per-sender message bound) for each since.
   uint64_t pend_bound = 0;
+  bool pend_exact = true;
   std::vector<uint32_t> hcnt;        // host-staged messages per local sender this window
   std::vector<uint32_t> hcnt_touched;
   uint32_t win_m_host = 0;           // max of hcnt
@@ -460,7 +461,6 @@ static int check_device_errors(tgsim_ctx* c) {
 static int sync_and_check(tgsim_ctx* c) {
   HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, sync_scalars(c->d), "sync");
-  if (!c->in_window) c->pend_bound = std::min<uint64_t>(c->pend_bound, c->d.h_sc->pend_max);
   if (c->now_from_device && !c->in_window) {
     c->horizon = c->d.h_sc->T;
     c->now = c->d.h_sc->t_end;
@@ -818,7 +818,14 @@ static int plan_queue_limit(tgsim_ctx* c) {
   const uint64_t mult = c->any_dup ? 2 : 1;
   const uint64_t m_uniform = std::min<uint64_t>((uint64_t)c->win_m_host + c->win_m_extra, 0x7FFFFFFFull);
   const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->inbox_max_h;
-  const bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+  bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+  if (gate && !c->pend_exact) {  // inconclusive: refresh the bound with the exact maximum (one sync)
+    HIPCK(c, launch_pend_max(d), "pend max");
+    HIPCK(c, sync_scalars(d), "sync");
+    c->pend_bound = d.h_sc->pend_max;
+    c->pend_exact = true;
+    gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+  }
   d.heavy = Heavy{};
   if (gate) {
     if (!d.H) {  // first window that needs the H list: room for every due record of a window
@@ -834,6 +841,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
     d.heavy.mult = (uint32_t)mult;
   }
   c->pend_bound = std::min<uint64_t>(c->pend_bound + mult * m_max, 1ull << 62);
+  c->pend_exact = m_max == 0;
   for (uint32_t l : c->hcnt_touched) c->hcnt[l] = 0;
   c->hcnt_touched.clear();
   c->win_m_host = 0;

@@ -193,11 +193,19 @@ def case_reaction_horizon(b):
 
 
 def case_staged_after_window_end(b):
+    """A staged message sent at/after the window end is refused before anything changes: the
+    context stays usable and the message goes out with the next window that covers it."""
     s = sim(b)
     s.enqueue([0], [1], [0], [1], [5 * MS])
     with pytest.raises(A.TgsimError) as e:
         s.advance(5 * MS)
     assert e.value.code == A.ECAUSALITY
+    assert s.now == 0
+    s.advance(6 * MS)
+    st, d = s.status(), s.deliveries()
+    assert list(st) == [A.ST_QUEUED] and list(d["t_deliver"]) == [5 * MS]
+    st, _ = one_window(s, [1], [2], 1, 6 * MS, 7 * MS)
+    assert list(st) == [A.ST_QUEUED]
     s.close()
 
 
