@@ -6,8 +6,10 @@ and the single-threaded CPU oracle timed beside it.
 A step is one storm round: every instance sends `fanout` 1 KiB messages to Philox-chosen peers
 within `spread` of the round start and SignalAndWait("round-r", N)s; the round window ends at the
 barrier release + the sync-service RTT, and everything due in it is delivered into inboxes.
-N GPUs = N shards of the same 100k instances (strong scaling); cross-shard copies go through one
-RCCL all-to-all per window, the barrier release through one MAX all-reduce.
+N GPUs = N shards of the same 100k instances (strong scaling), one process per GPU. The library owns
+the cross-shard transport (tgsim_comm_init: an RCCL communicator over xGMI): every shard makes the
+single-shard calls, the window's exchange (the peer blocks, whole - no host read of their counts) and
+the storm batch's MAX all-reduce run inside them on the simulator's stream.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -182,14 +184,20 @@ def storm_shapes(n: int, seed: int):
             for g in range(n)]
 
 
+def exchange_cap(per_window: int, n_shards: int) -> int:
+    """Records per peer block: the copies due in a window between one pair of shards (about
+    per_window / S^2 with uniform peers), 1.25x plus 4096 of headroom. Blocks travel whole, so the
+    bound is also the exchange's volume; an overflow is reported (ECAPACITY), never truncated."""
+    s = max(n_shards, 1)
+    return int(1.25 * per_window / (s * s)) + 4096
+
+
 def sim_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
     return SimConfig(n_instances=args.instances, seed=args.seed, shard_id=shard, n_shards=n_shards, device=device,
                      data_prefix_len=12, max_msgs_per_window=max(1 << 20, args.instances * args.fanout),
-                     max_records=args.max_records, max_states=4096,
-                     # a window's cross-shard copies per peer stay below the shard's copies per round:
-                     # 2x headroom; only the used prefix of each block travels (testground_amd/exchange.py)
-                     exchange_cap=max(1 << 17, 2 * args.instances * args.fanout // max(n_shards, 1) + 1))
+                     max_records=args.max_records // max(1, n_shards // 2), max_states=4096,
+                     exchange_cap=exchange_cap(args.instances * args.fanout, n_shards))
 
 
 def cpu_baseline(args, shapes):
@@ -242,63 +250,23 @@ def main():
     from testground_amd._abi import T_NOW
     from testground_amd.sim import Simulator
 
-    # More ranks than visible GPUs (rehearsing the sharded path on a one-GPU box): ranks share the
-    # devices round-robin and the collectives run over gloo on host copies. The driver's multi-GPU
-    # runs (one rank per GPU) always take RCCL.
-    ndev = torch.cuda.device_count()
-    rehearsal = world > ndev
-    local = local % max(ndev, 1)
-    torch.cuda.set_device(local)
-    if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    stream = torch.cuda.Stream()  # one stream shared by the simulator and the collectives
-    torch.cuda.set_stream(stream)
+    torch, dist, world, rank, local, rehearsal, stream = _dist_setup(args)
+    from testground_amd._abi import T_NOW
+    from testground_amd.sim import Simulator
+
     shapes = storm_shapes(args.instances, args.seed)
     sim = Simulator(sim_config(args, rank, world, local))
     sim.set_stream(stream.cuda_stream)
+    _attach_transport(sim, dist, world, rank, rehearsal)
     sim.set_shapes(np.arange(sim.lo, sim.hi), shapes[sim.lo:sim.hi])
     spread, rtt = int(args.spread_ms * MS), int(args.rtt_ms * MS)
     N, F = args.instances, args.fanout
 
-    if world > 1:
-        from testground_amd.exchange import exchange
-        _, _, nbytes = sim.exchange_buffers()
-        xcap = nbytes // (world * 32)
-        send_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        recv_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        sim.set_exchange_buffers(send_t.data_ptr(), recv_t.data_ptr(), nbytes)
-        rel_t = torch.zeros(1, dtype=torch.int64, device="cuda")
-        if rehearsal:
-            send_h, recv_h = torch.empty_like(send_t, device="cpu"), torch.zeros_like(recv_t, device="cpu")
-
-    def all_reduce(t, op):
-        if rehearsal:
-            h = t.cpu()
-            dist.all_reduce(h, op=op)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, op=op)
-
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
-        # step issues its launches without any host round trip
+        # step issues its launches without any host round trip (sharded: the same calls, collective)
         sim.gen_storm_round(r, T_NOW, F, args.size, spread, r)
-        if world == 1:
-            sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
-        else:
-            sim.storm_release_device(rel_t.data_ptr())
-            all_reduce(rel_t, dist.ReduceOp.MAX)
-            sim.advance_begin_device(rel_t.data_ptr(), rtt)
-            if rehearsal:
-                send_h.copy_(send_t)
-                exchange(send_h, recv_h, xcap, dist)
-                recv_t.copy_(recv_h)
-            else:
-                exchange(send_t, recv_t, xcap, dist)
-            sim.advance_end()
+        sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
 
     # warm-up (untimed, unprofiled), then a few probe steps that time every kernel class to find the
     # dominant one; the timed region carries HIP events around that kernel only
@@ -321,10 +289,10 @@ def main():
 
     s0 = sim.stats()
     sim_t0 = sim.now
-    if world > 1:
-        dist.barrier()
     sim.sync()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for r in range(first, first + args.steps):
         step(r)
@@ -340,12 +308,12 @@ def main():
     kern_n = prof[1] - base_prof[1]
     delivered = delta["delivered"]
     b_total = alg_bytes_step(delta, sim.hi - sim.lo, args.steps)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        all_reduce(t, dist.ReduceOp.MAX)
+    if world > 1:  # the process group is gloo: host tensors
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        v = torch.tensor([delivered, b_total], dtype=torch.int64, device="cuda")
-        all_reduce(v, dist.ReduceOp.SUM)
+        v = torch.tensor([delivered, b_total], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
         delivered, b_total = int(v[0].item()), int(v[1].item())
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
                     elapsed)
@@ -371,7 +339,9 @@ def main():
                 "workload": "gossip storm (SURVEY.md 8(d) config 4): 100k instances, fanout 8 Philox peers, "
                             "1 KiB messages within 10 ms, per-sender 10 Mbit/s HTB, latency U[20,100] ms, "
                             "jitter 5 ms, loss 0.5%, SignalAndWait(round, N) + 1 ms sync RTT per round",
-                "instances": N, "fanout": F, "msg_bytes": args.size, "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
+                "instances": N, "fanout": F, "msg_bytes": args.size,
+                "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else
+                                                  ("-rccl" if world > 1 else "")),
                 "delivered_in_timed_steps": delivered,
                 "simulated_ms_per_step": (sim_t1 - sim_t0) / 1e6 / args.steps,
             },
@@ -387,7 +357,9 @@ def main():
 
 
 def _dist_setup(args):
-    """One process per GPU; more ranks than GPUs = a gloo rehearsal on shared devices (see main)."""
+    """One process per GPU. torch.distributed (gloo, host side) only distributes the RCCL unique id
+    and reduces the timing; the simulator's data path uses its own communicator. More ranks than
+    GPUs = a rehearsal on shared devices over a gloo transport (RCCL refuses two ranks on a GPU)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -400,13 +372,23 @@ def _dist_setup(args):
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    stream = torch.cuda.Stream()
+        dist.init_process_group("gloo")
+    stream = torch.cuda.Stream()  # one stream shared by torch and the simulator
     torch.cuda.set_stream(stream)
     return torch, dist, world, rank, local, rehearsal, stream
+
+
+def _attach_transport(sim, dist, world: int, rank: int, rehearsal: bool) -> None:
+    if world == 1:
+        return
+    if rehearsal:
+        from testground_amd.exchange import GlooTransport
+        sim.set_transport(GlooTransport(dist, device=True))
+        return
+    from testground_amd.sim import Simulator
+    uid = [Simulator.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    sim.comm_init(uid[0], world, rank)
 
 
 def flood_cpu_baseline(args, shapes, graph):
@@ -443,7 +425,7 @@ def flood_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
     return SimConfig(n_instances=args.flood_instances, seed=args.seed, shard_id=shard, n_shards=n_shards,
                      device=device, data_prefix_len=11, max_msgs_per_window=1 << 23, max_records=1 << 25,
-                     exchange_cap=max(1 << 17, (1 << 23) // max(n_shards, 1)))
+                     exchange_cap=exchange_cap(3 << 20, n_shards))
 
 
 def flood_max_pubs(args) -> int:
@@ -464,35 +446,16 @@ def main_flood(args):
     graph = W.random_regular_graph(N, 8, args.seed)
     sim = Simulator(flood_config(args, rank, world, local))
     sim.set_stream(stream.cuda_stream)
+    _attach_transport(sim, dist, world, rank, rehearsal)
     sim.set_shapes(np.arange(sim.lo, sim.hi), shapes[sim.lo:sim.hi])
     sim.flood_set_graph(*graph, flood_max_pubs(args))
     win = int(args.window_ms * MS)
-    if world > 1:
-        from testground_amd.exchange import exchange
-        _, _, nbytes = sim.exchange_buffers()
-        xcap = nbytes // (world * 32)
-        send_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        recv_t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        sim.set_exchange_buffers(send_t.data_ptr(), recv_t.data_ptr(), nbytes)
-        if rehearsal:
-            send_h, recv_h = torch.empty_like(send_t, device="cpu"), torch.zeros_like(recv_t, device="cpu")
 
     def step(w: int):
         if w % args.pub_every == 0:
             k = w // args.pub_every
             sim.flood_publish(W.publishers(N, 1, k, args.seed), [k], sim.now, args.flood_size)
-        t_end = sim.now + win
-        if world == 1:
-            sim.advance(t_end)
-        else:
-            sim.advance_begin(t_end)
-            if rehearsal:
-                send_h.copy_(send_t)
-                exchange(send_h, recv_h, xcap, dist)
-                recv_t.copy_(recv_h)
-            else:
-                exchange(send_t, recv_t, xcap, dist)
-            sim.advance_end()
+        sim.advance(sim.now + win)  # sharded: collective, the exchange inside
         sim.flood_react(args.flood_size)
 
     for w in range(args.warmup):
@@ -512,10 +475,10 @@ def main_flood(args):
     base_prof = sim.profile_read()[dominant]
     first = args.warmup + probe
     s0 = sim.stats()
-    if world > 1:
-        dist.barrier()
     sim.sync()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for w in range(first, first + args.steps):
         step(w)
@@ -528,11 +491,9 @@ def main_flood(args):
     kern_ms, kern_n = prof[0] - base_prof[0], prof[1] - base_prof[1]
     delivered = delta["delivered"]
     b_total = alg_bytes_step(delta, sim.hi - sim.lo, args.steps)
-    if world > 1:
+    if world > 1:  # gloo process group: host tensors
         t = torch.tensor([elapsed], dtype=torch.float64)
         v = torch.tensor([delivered, b_total], dtype=torch.int64)
-        if not rehearsal:
-            t, v = t.cuda(), v.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         elapsed, delivered, b_total = float(t.item()), int(v[0].item()), int(v[1].item())
@@ -552,7 +513,8 @@ def main_flood(args):
                                    "{0,0.1,1}%, bandwidth {1,10,100} Mbit/s; one publication every "
                                    f"{args.pub_every} windows of {args.window_ms} ms",
                        "instances": N, "msg_bytes": args.flood_size,
-                       "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else ""),
+                       "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else
+                                                         ("-rccl" if world > 1 else "")),
                        "delivered_in_timed_steps": delivered},
             "roofline": roof,
             "cpu_baseline": cpu,

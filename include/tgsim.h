@@ -233,11 +233,39 @@ int tgsim_enqueue(tgsim_ctx* ctx, const tgsim_msg_soa* msgs, size_t n);
 /* Stage messages already in device memory (SoA arrays of n elements). */
 int tgsim_enqueue_device(tgsim_ctx* ctx, const tgsim_msg_soa* dev_msgs, size_t n);
 /* Run one window [now, t_end): shape + route staged messages, token-bucket the copies whose netem
- * time is < t_end, deliver everything due before t_end. Single-shard ctx only. */
+ * time is < t_end, deliver everything due before t_end. A sharded ctx needs a transport
+ * (tgsim_comm_init / tgsim_set_transport): the window's exchange runs inside the call, which is
+ * then collective - every shard calls it with the same t_end. A host-staged message sent at or
+ * after t_end is refused with ECAUSALITY before anything changes (the context stays usable). */
 int tgsim_advance(tgsim_ctx* ctx, int64_t t_end);
-/* Same, with t_end = release time of a barrier waiter + offset, read on the device (no host sync). */
+/* Same, with t_end = release time of a barrier waiter + offset, read on the device (no host sync).
+ * Sharded: collective, as tgsim_advance (the barrier's state is replicated on every shard). */
 int tgsim_advance_to_barrier(tgsim_ctx* ctx, uint32_t waiter, int64_t offset_ns);
-/* Sharded window protocol: begin (sender side) -> caller all-to-alls the exchange buffers
+/* ---- cross-shard transport: one exchange per window, inside tgsim_advance* -----
+ * The exchange buffers are peer-major blocks of exchange_cap records; record 0 of a block is a header
+ * whose .t holds the count, and only records due in the window cross shards. Blocks travel whole
+ * (their capacity is the device-known bound), so no count is read back by the host.
+ * Native: RCCL over xGMI, one communicator rank per shard, owned by the ctx. unique_id comes from
+ * tgsim_comm_unique_id on one rank and is distributed by the caller; tgsim_comm_init is collective
+ * (every rank calls it; nranks = n_shards, rank = shard_id). */
+#define TGSIM_COMM_ID_BYTES 128
+int tgsim_comm_unique_id(uint8_t out[TGSIM_COMM_ID_BYTES]);
+int tgsim_comm_init(tgsim_ctx* ctx, const uint8_t unique_id[TGSIM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank);
+/* Caller-supplied transport (MPI, gloo, a Go channel, one process driving several contexts).
+ * Pointers are device pointers and stream the ctx's hipStream_t: an op is enqueued on that stream or
+ * completed before it returns. Each returns 0 on success. */
+typedef struct tgsim_transport {
+  void* user;
+  /* block p (block_bytes) of send -> block <this rank> of rank p's recv, for every p */
+  int (*alltoall)(void* user, const void* send, void* recv, size_t block_bytes, void* stream);
+  /* element-wise MAX over the ranks of n int64 at buf, in place */
+  int (*allreduce_max_i64)(void* user, int64_t* buf, size_t n, void* stream);
+  /* bytes at send of every rank -> recv[rank * bytes] */
+  int (*allgather)(void* user, const void* send, void* recv, size_t bytes, void* stream);
+} tgsim_transport;
+int tgsim_set_transport(tgsim_ctx* ctx, const tgsim_transport* transport);  /* NULL: none */
+
+/* Sharded window protocol without a transport: begin (sender side) -> caller all-to-alls the exchange buffers
  * (n_shards * exchange_cap records each way, peer-major; the first record of each peer block is a
  * header whose .t holds the record count) on the same stream -> end (receiver side). */
 int tgsim_advance_begin(tgsim_ctx* ctx, int64_t t_end);
@@ -258,7 +286,10 @@ int tgsim_deliveries_device(tgsim_ctx* ctx, tgsim_delivery_soa* out_device_ptrs)
 /* ---- sync service (sdk-go sync.Client [EXT]; sync-service v0.1.0) ------------------------------ */
 /* SignalEntry for a batch of (state, instance, t) events. seq_out[i] = 1-based sequence number in
  * (t, instance) order among all signals of that state (NULL = not needed). Batches of one state
- * must not go back in time. In a sharded run every shard receives the same (all-gathered) batch. */
+ * must not go back in time. Sharded with a transport: collective; each shard passes its own
+ * instances' signals, the library all-gathers them (every shard keeps the whole, replicated sync
+ * state, so barriers resolve on every shard). Sharded without one: every shard passes the same
+ * (caller-gathered) batch. */
 int tgsim_sync_signal(tgsim_ctx* ctx, const uint32_t* states, const uint32_t* instances,
                       const int64_t* t, size_t n, uint32_t* seq_out);
 /* Barrier(state, target) registered at time t_wait: releases at max(t_wait, time of the
@@ -296,12 +327,14 @@ const char* tgsim_kernel_name(int kernel_class);
 /* ---- synthetic workloads (device generators) --------------------------------------- */
 /* Gossip storm round (config 4): every instance of this shard sends `fanout` messages of `size`
  * bytes to Philox-chosen distinct peers at t0 + U[0, spread_ns), seq = round*fanout + k, and signals
- * `state` at its last send time. Staged for the next window; the signal batch is kept on the device. */
+ * `state` at its last send time. Staged for the next window; the signal batch is kept on the device
+ * (count-only). Sharded with a transport: collective (the batch's first / last time is
+ * MAX-reduced over the shards and every shard commits the whole batch of n_instances signals). */
 int tgsim_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout,
                           uint32_t size, int64_t spread_ns, uint32_t state);
-/* Sharded runs: the storm round's signals are not committed by the generator; this writes the
- * shard's latest signal time of the last generated round (int64) to device memory, where a MAX
- * all-reduce across shards yields the release time of SignalAndWait(state, n_instances). */
+/* Sharded runs without a transport: the storm round's signals are not committed by the generator;
+ * this writes the shard's latest signal time of the last generated round (int64) to device memory,
+ * where a MAX all-reduce across shards yields the release time of SignalAndWait(state, n_instances). */
 int tgsim_storm_release_device(tgsim_ctx* ctx, int64_t* out_device);
 
 /* ---- flood workload (1M-instance random-regular pubsub) --------------

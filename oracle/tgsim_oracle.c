@@ -211,6 +211,9 @@ struct tgo_ctx {
   /* flood (config 5): local rows of the graph, first-receipt bits [max_pubs][nloc] */
   uint32_t* fl_off; uint32_t* fl_nbr; uint32_t* fl_seen;
   uint32_t fl_D, fl_max_pubs, fl_wpp;
+  /* cross-shard transport (tgsim_set_transport): host buffers, stream NULL */
+  tgsim_transport tr;
+  int has_tr, replicated_batch;
   char err[512];
 };
 
@@ -589,7 +592,7 @@ static void netem_post(tgo_ctx* c, const oshape* sh, int64_t t_send, uint32_t* c
   if (!sh->limited) rec->meta |= TGSIM_F_STAGE_D; /* unlimited HTB: departs when netem releases it */
 }
 
-static const omsgs* g_sort_msgs; /* qsort context of cmp_msg_order (single-threaded oracle) */
+static _Thread_local const omsgs* g_sort_msgs; /* qsort context of cmp_msg_order (one per thread: shards of one run may share a process) */
 static int cmp_msg_order(const void* a, const void* b) {
   size_t i = *(const size_t*)a, j = *(const size_t*)b;
   const omsgs* m = g_sort_msgs;
@@ -922,10 +925,21 @@ int tgo_advance_end(tgo_ctx* c) {
   return TGSIM_OK;
 }
 
+int tgo_set_transport(tgo_ctx* c, const tgsim_transport* t) {
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (t && (!t->alltoall || !t->allreduce_max_i64 || !t->allgather)) return fail(c, TGSIM_EINVAL, "incomplete transport");
+  c->has_tr = t != NULL;
+  if (t) c->tr = *t; else memset(&c->tr, 0, sizeof(c->tr));
+  return TGSIM_OK;
+}
+
+/* One window; sharded: collective, the exchange between the sender and receiver halves. */
 int tgo_advance(tgo_ctx* c, int64_t t_end) {
-  if (c->S != 1) return fail(c, TGSIM_ESTATE, "tgo_advance needs a single-shard context");
+  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "a sharded context needs a transport or begin/end");
   int rc = tgo_advance_begin(c, t_end);
   if (rc) return rc;
+  if (c->S != 1 && c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-to-all failed");
   return tgo_advance_end(c);
 }
 
@@ -983,8 +997,51 @@ static int ensure_state(tgo_ctx* c, uint32_t st) {
   return 0;
 }
 
+static int sync_signal_local(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                             size_t n, uint32_t* seq_out);
+
+/* A sharded batch with a transport: every shard's signals in shard order, processed whole on every
+ * shard (replicated sync state); seq_out = this shard's own sequence numbers. */
 int tgo_sync_signal(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                     size_t n, uint32_t* seq_out) {
+  if (c->S == 1 || !c->has_tr || c->replicated_batch) return sync_signal_local(c, states, inst, t, n, seq_out);
+  typedef struct { uint32_t state, inst; int64_t t; } grec;
+  uint64_t n64 = n;
+  uint64_t* sizes = (uint64_t*)calloc(c->S, 8);
+  if (!sizes) return TGSIM_ENOMEM;
+  if (c->tr.allgather(c->tr.user, &n64, sizes, 8, NULL) != 0) { free(sizes); return fail(c, TGSIM_EHIP, "all-gather failed"); }
+  uint64_t maxn = 0, total = 0, mine = 0;
+  for (uint32_t k = 0; k < c->S; ++k) {
+    if (k == c->cfg.shard_id) mine = total;
+    if (sizes[k] > maxn) maxn = sizes[k];
+    total += sizes[k];
+  }
+  int rc = TGSIM_OK;
+  grec* loc = (grec*)calloc(maxn + 1, sizeof(grec));
+  grec* all = (grec*)calloc(maxn * c->S + 1, sizeof(grec));
+  uint32_t* gs = (uint32_t*)malloc((total + 1) * 4); uint32_t* gi = (uint32_t*)malloc((total + 1) * 4);
+  uint32_t* gq = (uint32_t*)malloc((total + 1) * 4); int64_t* gt = (int64_t*)malloc((total + 1) * 8);
+  if (!loc || !all || !gs || !gi || !gq || !gt) rc = TGSIM_ENOMEM;
+  if (!rc && maxn) {
+    for (size_t i = 0; i < n; ++i) { loc[i].state = states[i]; loc[i].inst = inst[i]; loc[i].t = t[i]; }
+    if (c->tr.allgather(c->tr.user, loc, all, maxn * sizeof(grec), NULL) != 0) rc = fail(c, TGSIM_EHIP, "all-gather failed");
+  }
+  if (!rc) {
+    size_t j = 0;
+    for (uint32_t k = 0; k < c->S; ++k)
+      for (uint64_t i = 0; i < sizes[k]; ++i, ++j) {
+        const grec* r = &all[(size_t)k * maxn + i];
+        gs[j] = r->state; gi[j] = r->inst; gt[j] = r->t;
+      }
+    rc = sync_signal_local(c, gs, gi, gt, total, gq);
+    if (!rc && seq_out && n) memcpy(seq_out, gq + mine, n * 4);
+  }
+  free(sizes); free(loc); free(all); free(gs); free(gi); free(gq); free(gt);
+  return rc;
+}
+
+static int sync_signal_local(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                             size_t n, uint32_t* seq_out) {
   if (n == 0) return 0;
   osig* v = (osig*)malloc(n * sizeof(osig));
   if (!v) return TGSIM_ENOMEM;
@@ -1085,8 +1142,9 @@ int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout,
   }
   tgsim_msg_soa m = {src, dst, seq, sz, ts};
   rc = tgo_enqueue(c, &m, n);
-  if (!rc && c->S == 1) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
-  if (!rc && c->S > 1) { /* sharded: the caller MAX-reduces the local release across shards */
+  /* single shard, or sharded with a transport (the batch is gathered: replicated sync state) */
+  if (!rc && (c->S == 1 || c->has_tr)) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
+  if (!rc && c->S > 1 && !c->has_tr) { /* sharded: the caller MAX-reduces the local release across shards */
     int64_t mx = INT64_MIN;
     for (uint32_t l = 0; l < c->nloc; ++l) mx = stt[l] > mx ? stt[l] : mx;
     c->storm_release = mx;
@@ -1247,7 +1305,9 @@ int tgo_sync_publish(tgo_ctx* c, const uint32_t* topics, const uint32_t* inst, c
   if (n == 0) return TGSIM_OK;
   uint32_t* pos = (uint32_t*)malloc(n * 4);
   if (!pos) return TGSIM_ENOMEM;
+  c->replicated_batch = 1;  /* topics are replicated: every shard publishes the same batch */
   int rc = tgo_sync_signal(c, topics, inst, t, n, pos);
+  c->replicated_batch = 0;
   if (!rc && grow((void**)&c->tp_bytes, &c->tp_cap, c->tp_nbytes + off[n] + 1, 1)) rc = TGSIM_ENOMEM;
   if (!rc) {
     if (off[n]) memcpy(c->tp_bytes + c->tp_nbytes, payload, off[n]);

@@ -82,6 +82,19 @@ class Stats(C.Structure):
                                           "inflight", "tb_items", "extracted", "inserted", "overlimit")]
 
 
+# tgsim_transport (include/tgsim.h): caller-supplied cross-shard operations
+ALLTOALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class Transport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("alltoall", ALLTOALL_FN), ("allreduce_max_i64", ALLREDUCE_FN),
+                ("allgather", ALLGATHER_FN)]
+
+
+COMM_ID_BYTES = 128
+
 RECORD_DTYPE_FIELDS = [("t", "<i8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("size", "<u4"),
                        ("meta", "<u4"), ("corrupt_off", "<u4")]
 
@@ -123,6 +136,7 @@ _SIGS = {
     "flood_set_graph": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_uint32]),
     "flood_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]),
     "flood_react": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_size_t)]),
+    "set_transport": (C.c_int, [P, C.POINTER(Transport)]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {
@@ -140,6 +154,8 @@ _SIGS_HIP = {
     "set_exchange_buffers": (C.c_int, [P, P, P, C.c_size_t]),
     "advance_begin_device": (C.c_int, [P, P, C.c_int64]),
     "storm_release_device": (C.c_int, [P, P]),
+    "comm_unique_id": (C.c_int, [C.c_void_p]),
+    "comm_init": (C.c_int, [P, C.c_void_p, C.c_uint32, C.c_uint32]),
 }
 
 

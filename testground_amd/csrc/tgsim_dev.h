@@ -186,6 +186,10 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
 hipError_t launch_pend_max(Dev& d);
+// sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
+// batch's single partial in sig_part
+hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);
+hipError_t launch_storm_unpack(Dev& d, const int64_t* red2);
 // init_crandom on a Shape call: the state of local sender pairs[2i] re-seeded for epoch pairs[2i+1]
 hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n);
 hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack

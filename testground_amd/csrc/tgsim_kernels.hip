@@ -2633,6 +2633,35 @@ __global__ __launch_bounds__(kBlock) void k_window_start_commit(SigState g, uint
   }
 }
 
+// A sharded storm batch over a transport: the shard's (first, last) time from the generator's
+// partials as {last, -first} for one MAX all-reduce (k_storm_red), and the reduced pair back as the
+// batch's single partial (k_storm_unpack), which the fused commit then takes for the whole batch.
+__global__ __launch_bounds__(kBlock) void k_storm_red(const int64_t* part, uint32_t nparts, int64_t* red2) {
+  __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) {
+    mn = part[2 * i] < mn ? part[2 * i] : mn;
+    mx = part[2 * i + 1] > mx ? part[2 * i + 1] : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0) { smin[threadIdx.x >> 6] = mn; smax[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
+    red2[0] = mx;
+    red2[1] = mn == INT64_MAX ? INT64_MIN : -mn;  // an empty shard contributes nothing
+  }
+}
+__global__ void k_storm_unpack(const int64_t* red2, int64_t* part) {
+  part[0] = -red2[1];
+  part[1] = red2[0];
+}
+
 // Count-only batch (one state, no sequence numbers): min and max time, then the commit.
 __global__ __launch_bounds__(kBlock) void k_sig_count(SigState g, const int64_t* t, uint32_t n) {
   int64_t mn = INT64_MAX, mx = INT64_MIN;
@@ -3172,6 +3201,15 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
   hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, hoff, hidx,
                      d.H, d.cor_rho, d.cor_last, d.X);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2) {
+  hipLaunchKernelGGL(k_storm_red, dim3(1), dim3(kBlock), 0, d.stream, d.sig_part, nparts, red2);
+  return hipGetLastError();
+}
+hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
+  hipLaunchKernelGGL(k_storm_unpack, dim3(1), dim3(1), 0, d.stream, red2, d.sig_part);
   return hipGetLastError();
 }
 

@@ -15,6 +15,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "tgsim_dev.h"
 
 using namespace tgsim;
@@ -57,6 +59,7 @@ struct tgsim_ctx {
   // rides in the same launch): partials in d.sig_part
   bool storm_pending = false;
   uint32_t storm_parts = 0, storm_state = 0;
+  uint32_t storm_n = 0;  // signals in the pending batch (the shard's instances, or all with a transport)
   // ... and a barrier registered after it, not yet launched (waiter storm_nw; the window start that
   // waits on it carries the commit too)
   bool storm_add = false;
@@ -76,6 +79,15 @@ struct tgsim_ctx {
   uint32_t win_m_inbox = 0;          // flood forwards staged: (D - 1) per delivery of the sender's last inbox
   uint32_t inbox_max_h = 0;          // longest inbox run of the last window (read at the flood reaction)
   bool any_dup = false;
+  // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
+  // signal all-gather run inside the library - natively over RCCL (comm), or through caller callbacks
+  bool has_tr = false;
+  tgsim_transport tr{};
+  ncclComm_t comm = nullptr;
+  int64_t* d_red2 = nullptr;   // [2] storm batch: {last time, -first time} for the MAX all-reduce
+  uint64_t* d_gather = nullptr;  // all-gather scratch (signal batch sizes and records)
+  size_t gather_cap = 0;          // in uint64 units
+  bool replicated_batch = false;  // publish: topic batches are replicated, never gathered
   int64_t max_tsend_h = INT64_MIN;   // latest host-staged send time (checked against t_end before launch)
   // topics (tgsim_sync_publish / _subscribe): entries live in device arenas, sorted by (topic,
   // position) per batch; the host keeps each topic's runs of consecutive positions
@@ -100,7 +112,7 @@ static hipError_t flush_storm(tgsim_ctx* c) {
   c->storm_pending = false;
   const bool add = c->storm_add;
   c->storm_add = false;
-  return launch_sig_commit(c->d, c->storm_parts, true, c->nloc, c->storm_state, add ? c->storm_nw : c->n_waiters,
+  return launch_sig_commit(c->d, c->storm_parts, true, c->storm_n, c->storm_state, add ? c->storm_nw : c->n_waiters,
                            add, c->add_state, c->add_target, c->add_twait);
 }
 
@@ -222,6 +234,7 @@ extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
 extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (!c) return;
   if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->d.h_sc) (void)hipHostFree(c->d.h_sc);
   if (c->own_stream && c->d.stream) (void)hipStreamDestroy(c->d.stream);
@@ -312,6 +325,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.shape, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &c->d_red2, 2);
   rc |= dalloc(c, &d.moff, segK);
   rc |= dalloc(c, &d.flags, c->N);
   rc |= dalloc(c, &d.ip, c->N);
@@ -913,11 +927,96 @@ extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   return TGSIM_OK;
 }
 
+// ============================== cross-shard transport =======================================
+// one exchange per window (the peer blocks travel whole: their capacity is the
+// device-known bound, no count goes to the host), one MAX all-reduce per storm batch, an all-gather
+// per host signal batch. RCCL is one implementation of the three operations (ncclSend / ncclRecv
+// grouped, ncclAllReduce, ncclAllGather on the ctx stream); a caller's callbacks are another.
+
+static int rccl_alltoall(void* user, const void* send, void* recv, size_t block, void* stream) {
+  tgsim_ctx* c = static_cast<tgsim_ctx*>(user);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (ncclGroupStart() != ncclSuccess) return -1;
+  for (uint32_t p = 0; p < c->S; ++p) {
+    if (p == c->shard) continue;
+    if (ncclSend(static_cast<const uint8_t*>(send) + p * block, block, ncclUint8, (int)p, c->comm, s) != ncclSuccess ||
+        ncclRecv(static_cast<uint8_t*>(recv) + p * block, block, ncclUint8, (int)p, c->comm, s) != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return -1;
+    }
+  }
+  return ncclGroupEnd() == ncclSuccess ? 0 : -1;
+}
+static int rccl_allreduce_max(void* user, int64_t* buf, size_t n, void* stream) {
+  tgsim_ctx* c = static_cast<tgsim_ctx*>(user);
+  return ncclAllReduce(buf, buf, n, ncclInt64, ncclMax, c->comm, static_cast<hipStream_t>(stream)) == ncclSuccess ? 0 : -1;
+}
+static int rccl_allgather(void* user, const void* send, void* recv, size_t bytes, void* stream) {
+  tgsim_ctx* c = static_cast<tgsim_ctx*>(user);
+  return ncclAllGather(send, recv, bytes, ncclUint8, c->comm, static_cast<hipStream_t>(stream)) == ncclSuccess ? 0 : -1;
+}
+
+extern "C" int tgsim_comm_unique_id(uint8_t out[TGSIM_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == TGSIM_COMM_ID_BYTES, "RCCL unique id size");
+  if (!out) return TGSIM_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return TGSIM_EHIP;
+  memcpy(out, &id, sizeof(id));
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_comm_init(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank) {
+  if (!c || !id) return TGSIM_EINVAL;
+  if (nranks != c->S || rank != c->shard) return fail(c, TGSIM_EINVAL, "communicator rank %u/%u != shard %u/%u", rank, nranks, c->shard, c->S);
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  HIPCK(c, hipSetDevice((int)c->cfg.device), "device");
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+  const ncclResult_t r = ncclCommInitRank(&c->comm, (int)nranks, uid, (int)rank);
+  if (r != ncclSuccess) { c->comm = nullptr; return fail(c, TGSIM_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r)); }
+  c->tr.user = c;
+  c->tr.alltoall = rccl_alltoall;
+  c->tr.allreduce_max_i64 = rccl_allreduce_max;
+  c->tr.allgather = rccl_allgather;
+  c->has_tr = true;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_set_transport(tgsim_ctx* c, const tgsim_transport* t) {
+  if (!c) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (t && (!t->alltoall || !t->allreduce_max_i64 || !t->allgather)) return fail(c, TGSIM_EINVAL, "incomplete transport");
+  if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+  c->has_tr = t != nullptr;
+  c->tr = t ? *t : tgsim_transport{};
+  return TGSIM_OK;
+}
+
+// The window's exchange (between begin and end): the peer blocks, whole.
+static int exchange_window(tgsim_ctx* c) {
+  const size_t block = (size_t)c->d.xcap * sizeof(tgsim_record);
+  if (c->tr.alltoall(c->tr.user, c->d.xsend, c->d.xrecv, block, c->d.stream) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-to-all failed");
+  return TGSIM_OK;
+}
+
+static int need_transport(tgsim_ctx* c) {
+  if (c->S != 1 && !c->has_tr)
+    return fail(c, TGSIM_ESTATE, "a sharded context needs a transport (tgsim_comm_init / tgsim_set_transport) or begin/end");
+  return TGSIM_OK;
+}
+
 extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
-  if (c->S != 1) return fail(c, TGSIM_ESTATE, "tgsim_advance needs a single-shard context; use begin/end");
-  int rc = tgsim_advance_begin(c, t_end);
+  int rc = need_transport(c);
   if (rc) return rc;
+  rc = tgsim_advance_begin(c, t_end);
+  if (rc) return rc;
+  if (c->S != 1) {
+    rc = exchange_window(c);
+    if (rc) return rc;
+  }
   rc = tgsim_advance_end(c);
   if (rc) return rc;
   return sync_and_check(c);  // the host-driven API reports the window's errors here
@@ -925,14 +1024,15 @@ extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
 
 extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
   if (!c) return TGSIM_EINVAL;
-  if (c->S != 1) return fail(c, TGSIM_ESTATE, "single-shard context required");
+  int rc0 = need_transport(c);
+  if (rc0) return rc0;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
   if (c->storm_pending) {  // commit + barrier registration + window start: one launch
     c->storm_pending = false;
     const bool add = c->storm_add;
     c->storm_add = false;
-    HIPCK(c, launch_set_window_barrier_commit(c->d, waiter, offset_ns, c->storm_parts, c->nloc, c->storm_state,
+    HIPCK(c, launch_set_window_barrier_commit(c->d, waiter, offset_ns, c->storm_parts, c->storm_n, c->storm_state,
                                               add ? c->storm_nw : c->n_waiters, add, c->add_state, c->add_target,
                                               c->add_twait), "set window");
   } else {
@@ -940,6 +1040,10 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   }
   int rc = begin_common(c);
   if (rc) return rc;
+  if (c->S != 1) {
+    rc = exchange_window(c);
+    if (rc) return rc;
+  }
   return tgsim_advance_end(c);
 }
 
@@ -998,9 +1102,83 @@ extern "C" int tgsim_deliveries_device(tgsim_ctx* c, tgsim_delivery_soa* o) {
 
 // ============================== sync service =================================================
 
+static int signal_local(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
+                        uint32_t* seq_out);
+
+// A sharded batch over a transport: every shard's signals, gathered in shard order (sizes first,
+// then the records padded to the largest batch), processed whole on every shard; seq_out gets the
+// sequence numbers of this shard's own signals. Every decision below depends on gathered data
+// only, so the shards agree on it (a refusal is collective too).
+static int signal_gathered(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
+                           uint32_t* seq_out) {
+  struct Rec { uint32_t state, inst; int64_t t; };
+  static_assert(sizeof(Rec) == 16, "gather record");
+  Dev& d = c->d;
+  const uint32_t S = c->S;
+  auto room = [&](size_t words) -> int {
+    if (words <= c->gather_cap) return TGSIM_OK;
+    HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+    dfree(c, c->d_gather);
+    c->d_gather = nullptr;
+    const size_t cap = std::max(words, 2 * c->gather_cap);
+    if (dalloc(c, &c->d_gather, cap)) return TGSIM_ENOMEM;
+    c->gather_cap = cap;
+    return TGSIM_OK;
+  };
+  int rc = room(1 + S);
+  if (rc) return rc;
+  const uint64_t n64 = n;
+  HIPCK(c, hipMemcpyAsync(c->d_gather, &n64, 8, hipMemcpyHostToDevice, d.stream), "gather");
+  if (c->tr.allgather(c->tr.user, c->d_gather, c->d_gather + 1, 8, d.stream) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-gather failed");
+  std::vector<uint64_t> sizes(S);
+  HIPCK(c, hipMemcpyAsync(sizes.data(), c->d_gather + 1, 8 * (size_t)S, hipMemcpyDeviceToHost, d.stream), "gather");
+  HIPCK(c, hipStreamSynchronize(d.stream), "gather");
+  uint64_t maxn = 0, total = 0, mine = 0;
+  for (uint32_t k = 0; k < S; ++k) {
+    if (k == c->shard) mine = total;
+    maxn = std::max(maxn, sizes[k]);
+    total += sizes[k];
+  }
+  if (sizes[c->shard] != n64) return fail(c, TGSIM_EHIP, "transport all-gather returned a wrong size");
+  if (total > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "gathered signal batch larger than %u", c->d.s_cap);
+  if (total == 0) return signal_local(c, nullptr, nullptr, nullptr, 0, nullptr);
+  rc = room(2 * maxn * (1 + (size_t)S));
+  if (rc) return rc;
+  std::vector<Rec> loc(maxn, Rec{0, 0, 0});
+  for (size_t i = 0; i < n; ++i) loc[i] = Rec{states[i], inst[i], t[i]};
+  uint64_t* send = c->d_gather;
+  uint64_t* recv = c->d_gather + 2 * maxn;
+  HIPCK(c, hipMemcpyAsync(send, loc.data(), maxn * sizeof(Rec), hipMemcpyHostToDevice, d.stream), "gather");
+  if (c->tr.allgather(c->tr.user, send, recv, maxn * sizeof(Rec), d.stream) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-gather failed");
+  std::vector<Rec> all(maxn * S);
+  HIPCK(c, hipMemcpyAsync(all.data(), recv, all.size() * sizeof(Rec), hipMemcpyDeviceToHost, d.stream), "gather");
+  HIPCK(c, hipStreamSynchronize(d.stream), "gather");
+  std::vector<uint32_t> gs(total), gi(total), gq(total);
+  std::vector<int64_t> gt(total);
+  size_t j = 0;
+  for (uint32_t k = 0; k < S; ++k)
+    for (uint64_t i = 0; i < sizes[k]; ++i, ++j) {
+      const Rec& r = all[(size_t)k * maxn + i];
+      gs[j] = r.state; gi[j] = r.inst; gt[j] = r.t;
+    }
+  rc = signal_local(c, gs.data(), gi.data(), gt.data(), total, gq.data());
+  if (rc) return rc;
+  if (seq_out && n) memcpy(seq_out, gq.data() + mine, n * sizeof(uint32_t));
+  return TGSIM_OK;
+}
+
 extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                                  size_t n, uint32_t* seq_out) {
   if (!c || (n && (!states || !inst || !t))) return TGSIM_EINVAL;
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
+  if (c->S != 1 && c->has_tr && !c->replicated_batch) return signal_gathered(c, states, inst, t, n, seq_out);
+  return signal_local(c, states, inst, t, n, seq_out);
+}
+
+static int signal_local(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
+                        uint32_t* seq_out) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
   if (n > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch larger than %u", c->d.s_cap);
   if (c->sig_log_used + n > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
@@ -1094,6 +1272,18 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
     c->storm_pending = true;
     c->storm_parts = parts;
     c->storm_state = state;
+    c->storm_n = c->nloc;
+  } else if (c->has_tr) {
+    // every shard commits the whole batch: its first / last time MAX-reduced over the shards (the
+    // count is n_instances: every instance signals), replicated sync state
+    HIPCK(c, launch_storm_red(c->d, parts, c->d_red2), "storm reduce");
+    if (c->tr.allreduce_max_i64(c->tr.user, c->d_red2, 2, c->d.stream) != 0)
+      return fail(c, TGSIM_EHIP, "transport all-reduce failed");
+    HIPCK(c, launch_storm_unpack(c->d, c->d_red2), "storm reduce");
+    c->storm_pending = true;
+    c->storm_parts = 1;
+    c->storm_state = state;
+    c->storm_n = c->N;
   } else {
     // sharded: the release time is the MAX over shards of the local latest signal (sig_red[3])
     HIPCK(c, launch_sig_commit(c->d, parts, false, c->nloc, state, 0, false, 0, 0, 0), "storm release");
@@ -1242,7 +1432,9 @@ extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const ui
     if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) return fail(c, TGSIM_EINVAL, "bad payload offsets");
   if (n == 0) return TGSIM_OK;
   std::vector<uint32_t> pos(n);
+  c->replicated_batch = true;  // topics are replicated: every shard publishes the same batch
   int rc = tgsim_sync_signal(c, topics, inst, t, n, pos.data());
+  c->replicated_batch = false;
   if (rc) return rc;
   std::vector<uint32_t> ord(n);
   for (uint32_t i = 0; i < n; ++i) ord[i] = i;

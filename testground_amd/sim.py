@@ -176,6 +176,28 @@ class Simulator:
     def storm_release_device(self, out_dev: int) -> None:
         self._check(self.lib.storm_release_device(self._ctx, out_dev))
 
+    # ---- cross-shard transport ---------------------------------------------
+    def set_transport(self, transport) -> None:
+        """A testground_amd.exchange transport (or None): tgsim_advance* then exchange inside the
+        call, storm batches and signal batches reduce / gather across the shards."""
+        self._transport = transport  # the callbacks must outlive the context's use of them
+        self._check(self.lib.set_transport(self._ctx, C.byref(transport.c) if transport is not None else None))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """An RCCL unique id (one rank creates it, the caller distributes it)."""
+        lib = A.hip_library()
+        buf = (C.c_uint8 * A.COMM_ID_BYTES)()
+        rc = lib.comm_unique_id(buf)
+        if rc != A.OK:
+            raise A.TgsimError(rc, "comm_unique_id failed")
+        return bytes(buf)
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        """The native RCCL communicator (collective over the shards)."""
+        buf = (C.c_uint8 * A.COMM_ID_BYTES).from_buffer_copy(unique_id)
+        self._check(self.lib.comm_init(self._ctx, buf, nranks, rank))
+
     def set_stream(self, stream: int | None) -> None:
         self._check(self.lib.set_stream(self._ctx, stream))
 

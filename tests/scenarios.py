@@ -199,8 +199,13 @@ def run_sync(binding, seed: int):
     return res
 
 
-def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None):
+def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, setup=None):
+    """The storm step of bench.py. Sharded (cfg_kw shard_id / n_shards, setup attaching a
+    transport): the same calls on every shard, each collective; a shard reports its own senders'
+    statuses and its own receivers' deliveries."""
     sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **(cfg_kw or {})), binding=binding)
+    if setup is not None:
+        setup(sim)
     rng = np.random.default_rng(seed)
     for g in range(n_inst):
         sim.set_shape(g, make_shape(latency_ns=int(rng.integers(20, 101)) * MS, jitter_ns=5 * MS,
@@ -244,7 +249,9 @@ def shard_range(n, k, s):
 def run_random_sharded(make_sim, exchange, world: int, seed: int, n_inst: int = 24, windows: int = 6,
                        msgs_per_window: int = 300, window_ns: int = 40 * MS, local=None):
     """run_random's workload split over `world` shards. make_sim(cfg) -> Simulator of one shard;
-    exchange(sims) moves every shard's send blocks to the peers' receive blocks (an all-to-all).
+    exchange(sims) moves every shard's send blocks to the peers' receive blocks (an all-to-all)
+    between advance_begin and advance_end; exchange=None: the shards carry a transport and each
+    calls tgsim_advance (collective: one shard per thread or process, local=[k]).
     local: the shard ids this process runs (default all; one per rank in a multi-process run).
     Returns (per-shard observables in run_random's structure, per-window global sender arrays)."""
     rng = np.random.default_rng(seed)
@@ -275,11 +282,16 @@ def run_random_sharded(make_sim, exchange, world: int, seed: int, n_inst: int = 
     t0 = 0
 
     def window(t_end):
-        for s in sims:
-            s.advance_begin(t_end)
-        exchange(sims)
+        if exchange is None:
+            for s in sims:
+                s.advance(t_end)
+        else:
+            for s in sims:
+                s.advance_begin(t_end)
+            exchange(sims)
+            for s in sims:
+                s.advance_end()
         for i, s in enumerate(sims):
-            s.advance_end()
             outs[i].append(dict(status=s.status(), deliv=s.deliveries(), inbox=s.inbox_offsets()))
 
     for w in range(windows):
@@ -370,25 +382,30 @@ def memmove_exchange(sims):
 # ---- config 5: flood with first-receipt dedup over a random-regular graph -----------------------
 
 def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4, window_ns=10 * MS, size=512,
-              seed=5, degree=8, shapes=None, keep=True, on_window=None, cfg_kw=None, max_windows=2000):
+              seed=5, degree=8, shapes=None, keep=True, on_window=None, cfg_kw=None, max_windows=2000,
+              windows=None, setup=None):
     """Waves of publications flooding the graph; every window: advance, read the deliveries, then
     tgsim_flood_react stages the first-receipt forwards for the next window. Returns per-window
-    observables (keep=True) and the totals."""
+    observables (keep=True) and the totals. windows: run exactly that many windows (a sharded run
+    driven through a transport, whose shards cannot see the global end condition); setup(sim)
+    attaches that transport."""
     from testground_amd import workloads as W
     kw = dict(max_msgs_per_window=1 << 20, max_records=1 << 22, data_prefix_len=12)
     kw.update(cfg_kw or {})
     sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **kw), binding=binding)
+    if setup is not None:
+        setup(sim)
     sim.set_shapes(np.arange(n_inst), shapes if shapes is not None else W.pubsub_shapes(n_inst, seed))
     off, nbr = W.random_regular_graph(n_inst, degree, seed)
     sim.flood_set_graph(off, nbr, pubs_per_wave * waves)
     out, tot = [], dict(delivered=0, forwarded=0, windows=0)
     t, w, fwd = 0, 0, 0
-    while w < max_windows:
+    while w < (windows if windows is not None else max_windows):
         if w % wave_gap_windows == 0 and w // wave_gap_windows < waves:
             wave = w // wave_gap_windows
             pubs = W.publishers(n_inst, pubs_per_wave, wave, seed)
             sim.flood_publish(pubs, np.arange(pubs_per_wave) + wave * pubs_per_wave, t, size)
-        elif fwd == 0 and sim.stats()["inflight"] == 0 and w // wave_gap_windows >= waves:
+        elif windows is None and fwd == 0 and sim.stats()["inflight"] == 0 and w // wave_gap_windows >= waves:
             break
         t += window_ns
         sim.advance(t)
@@ -455,3 +472,56 @@ def run_flood_sharded(make_sim, exchange, world: int, n_inst=900, pubs_per_wave=
 def flood_single_view(single):
     """run_flood output in run_flood_sharded's structure."""
     return [dict(deliv=x["deliv"], fwd=x["fwd"]) for x in single[:-1]] + [dict(stats=single[-1]["stats"])]
+
+
+# ---- sharded runs driven through a transport (tgsim_set_transport): one shard per thread -----------
+
+def sharded_threads(world: int, fn, device: bool = False):
+    """fn(k, member_transport) for every shard k, each on its own thread with a ThreadGroup member
+    (host buffers, or device buffers on one GPU); returns the results in shard order."""
+    from testground_amd.exchange import ThreadGroup, run_threads
+    g = ThreadGroup(world, device=device)
+    return run_threads([lambda k=k: fn(k, g.member(k)) for k in range(world)])
+
+
+def shard_cfg(world: int, k: int, **kw):
+    return dict(shard_id=k, n_shards=world, **kw)
+
+
+def assert_storm_sharded(outs, single, world: int, n: int):
+    """Per-shard storm outputs (run_storm on every shard) against the single-shard run: the shards'
+    statuses (their own senders, generator order) and deliveries (their own receivers, inbox order)
+    concatenate to the single run's, inbox offsets are the single run's slice, clocks agree and the
+    counters sum."""
+    for r in range(len(single) - 1):
+        for f in single[r]["deliv"]:
+            cat = np.concatenate([outs[k][r]["deliv"][f] for k in range(world)])
+            assert_same(cat, single[r]["deliv"][f], f"round {r} deliv.{f}")
+        assert_same(np.concatenate([outs[k][r]["status"] for k in range(world)]), single[r]["status"],
+                    f"round {r} status")
+        for k in range(world):
+            lo, hi = shard_range(n, k, world)
+            inbox = single[r]["inbox"][lo:hi + 1] - single[r]["inbox"][lo]
+            assert_same(outs[k][r]["inbox"], inbox, f"round {r} shard {k} inbox")
+            assert outs[k][r]["now"] == single[r]["now"]
+    tot = {}
+    for k in range(world):
+        for name, v in outs[k][-1]["stats"].items():
+            tot[name] = tot.get(name, 0) + v
+    assert tot == single[-1]["stats"], (tot, single[-1]["stats"])
+
+
+def combine_flood_shards(outs):
+    """Per-shard run_flood outputs -> run_flood_sharded's structure (deliveries concatenated in
+    shard order, forwards and counters summed)."""
+    world = len(outs)
+    res = []
+    for w in range(len(outs[0]) - 1):
+        d = {f: np.concatenate([outs[k][w]["deliv"][f] for k in range(world)]) for f in outs[0][w]["deliv"]}
+        res.append(dict(deliv=d, fwd=sum(outs[k][w]["fwd"] for k in range(world))))
+    tot = {}
+    for k in range(world):
+        for name, v in outs[k][-1]["stats"].items():
+            tot[name] = tot.get(name, 0) + v
+    res.append(dict(stats=tot))
+    return res

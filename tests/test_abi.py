@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_shard_range", "tgsim_sync",
             "tgsim_enqueue_device", "tgsim_deliveries_device", "tgsim_profile_set", "tgsim_profile_read",
             "tgsim_kernel_classes", "tgsim_kernel_name", "tgsim_set_exchange_buffers",
-            "tgsim_advance_begin_device", "tgsim_storm_release_device"}
+            "tgsim_advance_begin_device", "tgsim_storm_release_device", "tgsim_comm_unique_id", "tgsim_comm_init"}
 
 
 def test_header_declares_expected_surface():
@@ -55,7 +55,7 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     structs = {"tgsim_link_shape": A.LinkShape, "tgsim_link_rule": A.LinkRule,
                "tgsim_network_config": A.NetworkConfig, "tgsim_config": A.Config, "tgsim_msg_soa": A.MsgSoA,
-               "tgsim_delivery_soa": A.DeliverySoA, "tgsim_stats": A.Stats}
+               "tgsim_delivery_soa": A.DeliverySoA, "tgsim_stats": A.Stats, "tgsim_transport": A.Transport}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tgsim.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')

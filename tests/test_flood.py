@@ -173,3 +173,24 @@ def test_flood_sharded_hip(hip, oracle, world):
     n = 900
     got = S.run_flood_sharded(lambda c: Simulator(c), exchange, world, n_inst=n)
     S.assert_same(got, S.flood_single_view(S.run_flood(oracle, n_inst=n)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_flood_sharded_full_size(hip):
+    """config 5 at 2, 4 and 8 shards: the 1M flood over HIP contexts on one GPU (one thread each,
+    the exchange through the transport) equals the single-context run window for window (which
+    test_flood_full_size pins to the oracle)."""
+    n = 1_000_000
+    shapes = W.pubsub_shapes(n)
+    kw = dict(max_msgs_per_window=1 << 23, max_records=1 << 24)
+    single = S.run_flood(hip, n_inst=n, pubs_per_wave=2, waves=1, shapes=shapes, cfg_kw=kw)
+    want = S.flood_single_view(single)
+    windows = len(single) - 1
+    for world in (2, 4, 8):
+        skw = dict(max_msgs_per_window=1 << 23, max_records=1 << 23, exchange_cap=1 << 20)
+        outs = S.sharded_threads(world, lambda k, tr: S.run_flood(
+            hip, n_inst=n, pubs_per_wave=2, waves=1, shapes=shapes, windows=windows,
+            cfg_kw=dict(skw, **S.shard_cfg(world, k)), setup=lambda sim: sim.set_transport(tr)), device=True)
+        S.assert_same(S.combine_flood_shards(outs), want)
+        print(f"  flood 1M x {world} shards == single", flush=True)

@@ -235,3 +235,17 @@ def test_cfg4_storm_full(hip, oracle, n=100_000, rounds=8):
     b = S.run_storm(oracle, n_inst=n, rounds=rounds, cfg_kw=kw)
     S.assert_same(a, b)
     assert sum(len(x["deliv"]["dst"]) for x in a[:-1]) > n * 8
+
+
+def test_cfg4_storm_sharded_full(hip, n=100_000, rounds=10, world=8):
+    """config 4 as bench.py shards it: the 100k storm over 8 HIP contexts (one thread each, one GPU,
+    the exchange and the barrier's all-reduce through the transport) equals the single-context run
+    bit for bit (which test_cfg4_storm_full pins to the oracle)."""
+    kw = dict(max_records=1 << 23, data_prefix_len=12)
+    single = S.run_storm(hip, n_inst=n, rounds=rounds, cfg_kw=kw)
+    skw = dict(max_records=1 << 21, data_prefix_len=12, exchange_cap=1 << 15)
+    outs = S.sharded_threads(world, lambda k, tr: S.run_storm(
+        hip, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, **skw),
+        setup=lambda sim: sim.set_transport(tr)), device=True)
+    S.assert_storm_sharded(outs, single, world, n)
+    assert sum(len(x["deliv"]["dst"]) for x in single[:-1]) > n * 8

@@ -94,3 +94,35 @@ def test_sharded_on_one_device(hip, oracle, world, seed):
 
     outs, srcs = S.run_random_sharded(make, exchange, world, seed)
     S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
+
+
+def _hip_with_transport(tr):
+    from testground_amd.sim import Simulator
+
+    def make(c):
+        sim = Simulator(c)
+        sim.set_transport(tr)
+        return sim
+    return make
+
+
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2)])
+def test_transport_on_one_device(hip, oracle, world, seed):
+    """HIP shards on one GPU, one thread each, driven with the single-shard calls: the window's
+    exchange runs inside tgsim_advance through a transport (device-to-device block copies here; the
+    library's RCCL communicator between GPUs), equal to the single-shard oracle run."""
+    outs = S.sharded_threads(world, lambda k, tr: S.run_random_sharded(
+        _hip_with_transport(tr), None, world, seed, local=[k])[0][0], device=True)
+    _, srcs = S.run_random_sharded(lambda c: S.Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
+    S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_storm_transport_on_one_device(hip, oracle, world):
+    """bench.py's storm step on HIP shards: the storm batch's MAX all-reduce and the exchange go
+    through the transport; equal to the single-shard oracle run."""
+    n, rounds = 2000, 6
+    outs = S.sharded_threads(world, lambda k, tr: S.run_storm(
+        hip, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, exchange_cap=1 << 15),
+        setup=lambda sim: sim.set_transport(tr)), device=True)
+    S.assert_storm_sharded(outs, S.run_storm(oracle, n_inst=n, rounds=rounds), world, n)

@@ -3,10 +3,13 @@ sender shard shapes its copies and one all-to-all moves cross-shard records to t
 The sharded run must equal the single-shard run bit for bit: per-shard statuses, the receiver
 shard's deliveries and inbox offsets, and the summed counters.
 
-  * in-process: 2 and 3 oracle shards exchanging through memmove;
-  * multi-process: world_size 2 over torch.distributed gloo (the variable-size exchange of
-    testground_amd/exchange.py, all_reduce MAX of the storm barrier release), the protocol bench.py
-    runs over RCCL.
+  * in-process, caller-driven: 2 and 3 oracle shards exchanging through memmove between
+    advance_begin and advance_end (the transport-less protocol of include/tgsim.h);
+  * in-process, transport-driven: one thread per shard (testground_amd.exchange.ThreadGroup); every
+    shard makes the single-shard calls (tgsim_advance, the storm's gen / barrier / advance_to_barrier)
+    and the library runs the exchange, the storm batch's MAX all-reduce and the signal all-gather;
+  * multi-process: world_size 2 and 3 over torch.distributed gloo (GlooTransport), the same calls -
+    the protocol bench.py runs over the library's RCCL communicator on GPUs.
 """
 import ctypes as C
 import os
@@ -17,13 +20,74 @@ import pytest
 
 from tests import scenarios as S
 from testground_amd.sim import SimConfig, Simulator
-from testground_amd.exchange import exchange as xchg
 
 
 @pytest.mark.parametrize("world,seed", [(2, 1), (2, 5), (3, 2)])
 def test_sharded_equals_single_in_process(oracle, world, seed):
     outs, srcs = S.run_random_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
     S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
+
+
+def _with_transport(binding, tr):
+    def make(c):
+        s = Simulator(c, binding=binding)
+        s.set_transport(tr)
+        return s
+    return make
+
+
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2)])
+def test_sharded_transport_threads(oracle, world, seed):
+    """tgsim_advance on every shard, the exchange inside the call (ThreadGroup transport)."""
+    outs = S.sharded_threads(world, lambda k, tr: S.run_random_sharded(
+        _with_transport(oracle, tr), None, world, seed, local=[k])[0][0])
+    _, srcs = S.run_random_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
+    S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_storm_transport_threads(oracle, world):
+    """bench.py's storm step on every shard with the single-shard calls: the batch's first / last
+    time is MAX-reduced and every shard holds the whole sync state, so the barrier resolves alike."""
+    n, rounds = 600, 4
+    outs = S.sharded_threads(world, lambda k, tr: S.run_storm(
+        oracle, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, exchange_cap=1 << 14),
+        setup=lambda sim: sim.set_transport(tr)))
+    S.assert_storm_sharded(outs, S.run_storm(oracle, n_inst=n, rounds=rounds), world, n)
+
+
+def test_signal_gather_threads(oracle):
+    """tgsim_sync_signal on a sharded run: each shard passes its own signals; sequence numbers and
+    barrier releases equal those of the single-shard call with every signal."""
+    world = 3
+    rng = np.random.default_rng(8)
+    batches = []
+    for b in range(4):
+        n = int(rng.integers(0, 400))
+        batches.append((rng.integers(0, 4, n), rng.integers(0, 300, n), 1000 * b + rng.integers(0, 1000, n)))
+
+    def shard(k, tr):
+        sim = Simulator(SimConfig(n_instances=300, seed=1, shard_id=k, n_shards=world, max_states=16), binding=oracle)
+        sim.set_transport(tr)
+        lo, hi = S.shard_range(300, k, world)
+        res = []
+        for st, ins, t in batches:
+            m = (ins >= lo) & (ins < hi)
+            res.append((m, sim.signal(st[m], ins[m], t[m])))
+            res.append(sim.poll(sim.barrier(1, 50, 0)))
+        sim.close()
+        return res
+
+    outs = S.sharded_threads(world, shard)
+    ref = Simulator(SimConfig(n_instances=300, seed=1, max_states=16), binding=oracle)
+    for i, (st, ins, t) in enumerate(batches):
+        seq = ref.signal(st, ins, t)
+        for k in range(world):
+            m, got = outs[k][2 * i]
+            assert np.array_equal(got, seq[m])
+        rel = ref.poll(ref.barrier(1, 50, 0))
+        assert all(outs[k][2 * i + 1] == rel for k in range(world))
+    ref.close()
 
 
 def _free_port():
@@ -43,50 +107,19 @@ def _worker(rank, world, port, seed, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
         from oracle.pyoracle import oracle_binding
+        from testground_amd.exchange import GlooTransport
         dist.init_process_group("gloo", rank=rank, world_size=world)
         ob = oracle_binding()
-
-        def exchange(sims):  # the runner's variable-size exchange (testground_amd/exchange.py)
-            s = sims[0]
-            send, recv, nbytes = s.exchange_buffers()
-            xchg(_torch_view(send, nbytes), _torch_view(recv, nbytes), nbytes // (world * 32), dist)
-
-        outs, _ = S.run_random_sharded(lambda c: Simulator(c, binding=ob), exchange, world, seed, local=[rank])
-        storm = _storm_rank(ob, rank, world, dist)
+        tr = GlooTransport(dist)
+        outs, _ = S.run_random_sharded(_with_transport(ob, tr), None, world, seed, local=[rank])
+        storm = S.run_storm(ob, n_inst=600, rounds=3, cfg_kw=S.shard_cfg(world, rank, exchange_cap=1 << 14),
+                            setup=lambda sim: sim.set_transport(tr))
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, outs[0], storm))
-    except Exception as e:  # surface the failure in the parent
+    except Exception:  # surface the failure in the parent
         import traceback
         q.put((rank, "ERR", traceback.format_exc()))
-
-
-def _storm_rank(binding, rank, world, dist, n=600, rounds=3):
-    """bench.py's sharded storm step on one rank: generate, MAX-all-reduce the local release time,
-    advance_begin(release + rtt), all-to-all, advance_end."""
-    import torch
-    from testground_amd.sim import make_shape
-    sim = Simulator(SimConfig(n_instances=n, seed=4, shard_id=rank, n_shards=world, exchange_cap=1 << 14),
-                    binding=binding)
-    rng = np.random.default_rng(4)
-    for g in range(n):
-        sim.set_shape(g, make_shape(latency_ns=int(rng.integers(20, 101)) * S.MS, jitter_ns=5 * S.MS,
-                                    bandwidth_bps=10_000_000, loss=0.5))
-    res = []
-    rel = C.c_int64()
-    for r in range(rounds):
-        sim.gen_storm_round(r, sim.now, 8, 1024, 10 * S.MS, r)
-        sim._check(binding.cdll.tgo_storm_release(sim._ctx, C.byref(rel)))
-        t = torch.tensor([rel.value], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        sim.advance_begin(int(t.item()) + 1 * S.MS)
-        send, recv, nbytes = sim.exchange_buffers()
-        xchg(_torch_view(send, nbytes), _torch_view(recv, nbytes), nbytes // (world * 32), dist)
-        sim.advance_end()
-        res.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
-    res.append(dict(stats=S.parity_stats(sim)))
-    sim.close()
-    return res
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -108,14 +141,4 @@ def test_sharded_gloo(oracle, world):
         p.join(timeout=60)
     _, srcs = S.run_random_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
     S.assert_sharded_matches([got[r][0] for r in range(world)], srcs, S.run_random(oracle, seed), world)
-    # storm: shard deliveries concatenate to the single-shard inbox; counters sum
-    single = S.run_storm(oracle, n_inst=600, rounds=3, seed=4)
-    for r in range(3):
-        cat = {f: np.concatenate([got[k][1][r]["deliv"][f] for k in range(world)]) for f in single[r]["deliv"]}
-        S.assert_same(cat, single[r]["deliv"], f"storm round {r}")
-        assert all(got[k][1][r]["now"] == single[r]["now"] for k in range(world))
-    tot = {}
-    for k in range(world):
-        for name, v in got[k][1][-1]["stats"].items():
-            tot[name] = tot.get(name, 0) + v
-    assert tot == single[-1]["stats"]
+    S.assert_storm_sharded([got[r][1] for r in range(world)], S.run_storm(oracle, n_inst=600, rounds=3), world, 600)
