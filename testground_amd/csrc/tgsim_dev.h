@@ -59,8 +59,9 @@ struct Dev {
   // tables
   ShapeDev* shape = nullptr;
   int64_t* X = nullptr;
-  uint8_t* flags = nullptr;       // [N] bit0 link enabled, bit1 external routing allowed
-  uint32_t* ip = nullptr;         // [N]
+  // [N] ip | flags << 32 per instance (flags bit0 link enabled, bit1 external routing allowed): one
+  // 8-B gather gives a destination's address and link state
+  uint64_t* ipf = nullptr;
   uint32_t* rule_off = nullptr;   // [nloc+1]
   RuleDev* rules = nullptr;
 

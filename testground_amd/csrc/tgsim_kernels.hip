@@ -150,6 +150,53 @@ struct Queues {
       }
     }
   }
+
+  // Wave-collective append of U records per lane (q[u] < 0: none). The local queues A / D / L take
+  // one sub-queue per wave for the whole batch: one ballot per (record, queue) gives every slot and
+  // at most three independent atomics (one round trip) reserve them, instead of a dependent atomic
+  // per record and distinct counter. Slots go record-major, lane-minor, so each store instruction
+  // of the wave covers consecutive records. Exchange records (sharded runs) take the per-record path.
+  template <int U>
+  __device__ __forceinline__ void push_batch(const int (&q)[U], const tgsim_record (&r)[U], uint32_t salt) const {
+    const uint32_t lane = lane_id();
+    const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
+    uint64_t mA[U], mD[U], mL[U];
+    bool any_x = false;
+    uint32_t tA = 0, tD = 0, tL = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      mA[u] = __ballot(q[u] == Q_A); mD[u] = __ballot(q[u] == Q_D); mL[u] = __ballot(q[u] == Q_L);
+      tA += (uint32_t)__popcll(mA[u]); tD += (uint32_t)__popcll(mD[u]); tL += (uint32_t)__popcll(mL[u]);
+      any_x |= q[u] >= Q_X0;
+    }
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
+    uint32_t rA = 0, rD = 0, rL = 0;
+    if (lane == leader) {  // three independent atomics: one round trip
+      if (tA) rA = atomicAdd(qc + (((uint32_t)Q_A * kNSub + sub) << 5), tA);
+      if (tD) rD = atomicAdd(qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD);
+      if (tL) rL = atomicAdd(qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL);
+    }
+    uint32_t pA = __shfl(rA, (int)leader), pD = __shfl(rD, (int)leader), pL = __shfl(rL, (int)leader);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // no runtime-indexed private arrays (they would live in scratch)
+      const int k = q[u];
+      if (k >= 0 && k < Q_X0) {
+        const uint32_t pos = k == Q_A ? pA + mask_rank(mA[u]) : (k == Q_D ? pD + mask_rank(mD[u]) : pL + mask_rank(mL[u]));
+        if (pos < subcap) {
+          const size_t at = (size_t)sub * subcap + pos;
+          store_rec((k == Q_A ? A : (k == Q_D ? D : L)) + at, r[u]);
+          (k == Q_A ? K[0] : (k == Q_D ? K[1] : K[2]))[at] = key_of(k, r[u]);
+        } else {
+          atomicOr(&sc->err, k == Q_A ? ERR_CAP_A : (k == Q_D ? ERR_CAP_D : ERR_CAP_L));
+        }
+      }
+      pA += (uint32_t)__popcll(mA[u]); pD += (uint32_t)__popcll(mD[u]); pL += (uint32_t)__popcll(mL[u]);
+    }
+    if (__ballot(any_x)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) push(q[u] >= Q_X0 ? q[u] : -1, r[u], salt + u);
+    }
+  }
 };
 
 struct Geo { uint32_t N, S, shard; };
@@ -291,8 +338,7 @@ struct ShapeArgs {
   uint32_t n;
   uint8_t* status;
   const ShapeDev* shape;
-  const uint8_t* flags;
-  const uint32_t* ip;
+  const uint64_t* ipf;         // [N] ip | flags << 32
   const uint32_t* rule_off;
   const RuleDev* rules;
   uint32_t lo, nloc, data_net, data_mask, data_len, key0, key1;
@@ -428,9 +474,10 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
     const bool src_ok = sl < a.nloc;
     const uint32_t slc = src_ok ? sl : 0u;
     const uint32_t dstc = dst < a.geo.N ? dst : 0u;
-    const uint8_t fsrc = a.flags[src_ok ? src : a.lo];
-    const uint8_t fdst = a.flags[dstc];
-    const uint32_t dip = a.ip[dstc];
+    const uint8_t fsrc = (uint8_t)(a.ipf[src_ok ? src : a.lo] >> 32);
+    const uint64_t vdst = a.ipf[dstc];
+    const uint8_t fdst = (uint8_t)(vdst >> 32);
+    const uint32_t dip = (uint32_t)vdst;
     const uint32_t r_lo = a.rule_off[slc], r_hi = a.rule_off[slc + 1];
     const ShapeDev sh = a.shape[slc];
     asm volatile("" ::"v"((uint32_t)fsrc), "v"((uint32_t)fdst), "v"(dip), "v"(r_lo), "v"(r_hi),
@@ -498,8 +545,9 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
     if (!deferred) a.status[i] = st;
     const uint32_t cpos = wave_append(deferred ? &sc->n_corr : nullptr);
     if (deferred) a.corr_idx[cpos] = i;
-    a.Q.push(q1, r1, 2 * it);
-    a.Q.push(q2, r2, 2 * it + 1);
+    const int qs[2] = {q1, q2};
+    const tgsim_record rs[2] = {r1, r2};
+    a.Q.push_batch<2>(qs, rs, it);
   }
   // statistics: wave sums -> LDS -> one add per block into one of kNSub counter rows (128 B each),
   // so the ~8k waves of a launch do not serialise on one cache line (rows summed on read)
@@ -631,14 +679,20 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
       }
       load_rec(arena + at, rec[u]);
     }
+    int qs[kExtractUnroll];
 #pragma unroll
     for (int u = 0; u < kExtractUnroll; ++u) {
       const uint32_t j = base + u * kBlock + threadIdx.x;
       const bool due = j < total && rec[u].t < t_end;
-      const int q = j >= total ? -1
-                               : (due ? ((rec[u].meta & TGSIM_F_STAGE_D) ? qid_stage_d(ho.geo, rec[u].dst, rec[u].t, t_end) : Q_A)
-                                      : Q_L);
-      Q.push(q, rec[u], it * kExtractUnroll + u);
+      qs[u] = j >= total ? -1
+                         : (due ? ((rec[u].meta & TGSIM_F_STAGE_D) ? qid_stage_d(ho.geo, rec[u].dst, rec[u].t, t_end) : Q_A)
+                                : Q_L);
+    }
+    Q.push_batch<kExtractUnroll>(qs, rec, it);
+#pragma unroll
+    for (int u = 0; u < kExtractUnroll; ++u) {
+      const uint32_t j = base + u * kBlock + threadIdx.x;
+      const bool due = j < total && rec[u].t < t_end;
       if (ho.hv.pend) {  // launch-uniform
         const bool h = due && ho.hv.of(rec[u].src - ho.lo);
         const uint32_t pos = wave_append(h ? &sc->n_hrec : nullptr);
@@ -2260,8 +2314,9 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
           (c ? q1 : q2) = qid_copy(a.geo, r, t_end);
         }
       }
-      a.Q.push(q1, r1, 2 * c0);
-      a.Q.push(q2, r2, 2 * c0 + 1);
+      const int qs[2] = {q1, q2};
+      const tgsim_record rs[2] = {r1, r2};
+      a.Q.push_batch<2>(qs, rs, c0);
       __syncthreads();
     }
     if (lane == 0) {
@@ -3241,7 +3296,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
   if (n_staged) {
     ShapeArgs a;
     a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged;
-    a.status = d.status; a.shape = d.shape; a.flags = d.flags; a.ip = d.ip; a.rule_off = d.rule_off;
+    a.status = d.status; a.shape = d.shape; a.ipf = d.ipf; a.rule_off = d.rule_off;
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
     a.stats = d.stats;

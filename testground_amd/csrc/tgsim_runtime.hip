@@ -327,8 +327,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &c->d_red2, 2);
   rc |= dalloc(c, &d.moff, segK);
-  rc |= dalloc(c, &d.flags, c->N);
-  rc |= dalloc(c, &d.ip, c->N);
+  rc |= dalloc(c, &d.ipf, c->N);
   rc |= dalloc(c, &d.rule_off, nl1);
   rc |= dalloc(c, &d.rules, 1);
   rc |= dalloc(c, &d.m_src, d.cap_msgs);
@@ -718,12 +717,11 @@ static int upload_tables(tgsim_ctx* c) {
     HIPCK(c, launch_reset_corr(d, c->corr_reset_dev, n), "reset corr");
     copied = true;
   }
-  if (c->flags_dirty) {
-    HIPCK(c, hipMemcpyAsync(d.flags, c->flags_h.data(), c->N, hipMemcpyHostToDevice, d.stream), "upload flags");
-    copied = true;
-  }
-  if (c->ip_dirty) {
-    HIPCK(c, hipMemcpyAsync(d.ip, c->ip_h.data(), c->N * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream), "upload ips");
+  std::vector<uint64_t> ipf;
+  if (c->flags_dirty || c->ip_dirty) {
+    ipf.resize(c->N);
+    for (uint32_t g = 0; g < c->N; ++g) ipf[g] = (uint64_t)c->ip_h[g] | ((uint64_t)c->flags_h[g] << 32);
+    HIPCK(c, hipMemcpyAsync(d.ipf, ipf.data(), c->N * sizeof(uint64_t), hipMemcpyHostToDevice, d.stream), "upload ip/flags");
     copied = true;
   }
   std::vector<uint32_t> off;
