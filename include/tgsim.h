@@ -219,6 +219,13 @@ int64_t tgsim_horizon(const tgsim_ctx* ctx);
  * Takes effect for messages sent at or after the current window start. In a sharded run call it on
  * EVERY shard (ip/enable/policy tables are replicated; shape/rules are kept by the owning shard). */
 int tgsim_configure_network(tgsim_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg);
+/* The same call in a named runner's apply order. TGSIM_APPLY_DOCKER is tgsim_configure_network.
+ * TGSIM_APPLY_K8S follows K8sNetwork.ConfigureNetwork (k8s_network.go:43-176): Enable=false only
+ * disconnects and leaves the routing policy as it was; otherwise (re)connect -> Shape -> AddRules ->
+ * policy, so a failing Shape or AddRules leaves the policy unchanged. A reconnect with IPv4 nil keeps
+ * the instance's current address (the CNI IPAM's choice is not modelled). */
+enum { TGSIM_APPLY_DOCKER = 0, TGSIM_APPLY_K8S = 1 };
+int tgsim_configure_network_order(tgsim_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg, int32_t order);
 /* Lower-level pieces of the same call. */
 int tgsim_set_shape(tgsim_ctx* ctx, uint32_t instance, const tgsim_link_shape* shape); /* Shape, link.go:155 */
 int tgsim_set_shapes(tgsim_ctx* ctx, const uint32_t* instances, const tgsim_link_shape* shapes, size_t n);

@@ -487,6 +487,24 @@ int tgo_configure_network(tgo_ctx* c, uint32_t g, const tgsim_network_config* cf
   return tgo_add_rules(c, g, cfg->rules, cfg->n_rules);
 }
 
+/* K8sNetwork.ConfigureNetwork, k8s_network.go:43-176: Enable=false returns after the disconnect
+ * (k8s_network.go:50-61, the policy is not applied); otherwise Shape -> AddRules -> policy
+ * (k8s_network.go:166-174). A reconnect with IPv4 nil keeps the current address (IPAM not modelled). */
+int tgo_configure_network_order(tgo_ctx* c, uint32_t g, const tgsim_network_config* cfg, int32_t order) {
+  if (order == TGSIM_APPLY_DOCKER) return tgo_configure_network(c, g, cfg);
+  if (!cfg || g >= c->N || order != TGSIM_APPLY_K8S) return fail(c, TGSIM_EINVAL, "bad arguments");
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return fail(c, TGSIM_EUNSUPPORTED_NETWORK, "unsupported network: %s", net);
+  if (!cfg->enable) return tgo_set_enabled(c, g, 0, 0, 0);
+  int rc = tgo_set_enabled(c, g, 1, cfg->has_ipv4, cfg->ipv4);
+  if (rc) return rc;
+  rc = tgo_set_shape(c, g, &cfg->default_shape);
+  if (rc) return rc;
+  rc = tgo_add_rules(c, g, cfg->rules, cfg->n_rules);
+  if (rc) return rc;
+  return tgo_set_policy(c, g, cfg->routing_policy);
+}
+
 int tgo_get_ip(const tgo_ctx* c, uint32_t g, uint32_t* ip) {
   if (g >= c->N) return TGSIM_EINVAL;
   *ip = c->ip[g];

@@ -46,6 +46,7 @@ const char* tgo_last_error(const tgo_ctx* ctx);
 int64_t tgo_now(const tgo_ctx* ctx);
 int64_t tgo_horizon(const tgo_ctx* ctx);
 int tgo_configure_network(tgo_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg);
+int tgo_configure_network_order(tgo_ctx* ctx, uint32_t instance, const tgsim_network_config* cfg, int32_t order);
 int tgo_set_shape(tgo_ctx* ctx, uint32_t instance, const tgsim_link_shape* shape);
 int tgo_set_shapes(tgo_ctx* ctx, const uint32_t* instances, const tgsim_link_shape* shapes, size_t n);
 int tgo_add_rules(tgo_ctx* ctx, uint32_t instance, const tgsim_link_rule* rules, size_t n);

@@ -23,6 +23,7 @@ ERROR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EHIP: "EHIP", ECAPACITY: "ECA
 
 FILTER_ACCEPT, FILTER_REJECT, FILTER_DROP = 0, 1, 2
 POLICY_DENY_ALL, POLICY_ALLOW_ALL = 0, 1
+APPLY_DOCKER, APPLY_K8S = 0, 1
 DST_EXTERNAL = 0xFFFFFFFF
 T_NOW = -(1 << 63)  # TGSIM_T_NOW: "the current window start as the device knows it"
 
@@ -106,6 +107,7 @@ _SIGS = {
     "now": (C.c_int64, [P]),
     "horizon": (C.c_int64, [P]),
     "configure_network": (C.c_int, [P, C.c_uint32, C.POINTER(NetworkConfig)]),
+    "configure_network_order": (C.c_int, [P, C.c_uint32, C.POINTER(NetworkConfig), C.c_int32]),
     "set_shape": (C.c_int, [P, C.c_uint32, C.POINTER(LinkShape)]),
     "set_shapes": (C.c_int, [P, C.c_void_p, C.POINTER(LinkShape), C.c_size_t]),
     "add_rules": (C.c_int, [P, C.c_uint32, C.POINTER(LinkRule), C.c_size_t]),

@@ -684,6 +684,22 @@ extern "C" int tgsim_configure_network(tgsim_ctx* c, uint32_t g, const tgsim_net
   return tgsim_add_rules(c, g, cfg->rules, cfg->n_rules);
 }
 
+// K8sNetwork.ConfigureNetwork, k8s_network.go:43-176: policy last, untouched by a disconnect.
+extern "C" int tgsim_configure_network_order(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg, int32_t order) {
+  if (order == TGSIM_APPLY_DOCKER) return tgsim_configure_network(c, g, cfg);
+  if (!c || !cfg || g >= c->N || order != TGSIM_APPLY_K8S) return fail(c, TGSIM_EINVAL, "bad arguments");
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return fail(c, TGSIM_EUNSUPPORTED_NETWORK, "unsupported network: %s", net);
+  if (!cfg->enable) return tgsim_set_enabled(c, g, 0, 0, 0);
+  int rc = tgsim_set_enabled(c, g, 1, cfg->has_ipv4, cfg->ipv4);
+  if (rc) return rc;
+  rc = tgsim_set_shape(c, g, &cfg->default_shape);
+  if (rc) return rc;
+  rc = tgsim_add_rules(c, g, cfg->rules, cfg->n_rules);
+  if (rc) return rc;
+  return tgsim_set_policy(c, g, cfg->routing_policy);
+}
+
 extern "C" int tgsim_get_ip(const tgsim_ctx* c, uint32_t g, uint32_t* ip) {
   if (!c || !ip || g >= c->N) return TGSIM_EINVAL;
   *ip = c->ip_h[g];

@@ -4,8 +4,9 @@ Reference interfaces mirrored here:
 
 * ``sidecar.Network`` (``pkg/sidecar/instance.go:37-42``): ``ConfigureNetwork(ctx, cfg)``,
   ``ListActive()``, ``Close()``. :class:`SimNetwork` implements it for one simulated instance by
-  calling ``tgsim_configure_network`` (the docker apply order of
-  ``pkg/sidecar/docker_network.go:51-148`` is inside the C ABI).
+  calling ``tgsim_configure_network_order`` (the docker apply order of
+  ``pkg/sidecar/docker_network.go:51-148`` or the k8s one of ``pkg/sidecar/k8s_network.go:43-176``
+  is inside the C ABI; the sidecar picks it by runner name like ``sidecar_linux.go:20-58``).
 * The sidecar instance handler (``pkg/sidecar/sidecar_handler.go:15-83``): initial
   ``Config{Network: "default", Enable: true}``, ``SignalAndWait("network-initialized", N)``, then
   every published Config is applied in order and ``SignalEntry(cfg.CallbackState)`` follows when
@@ -36,9 +37,10 @@ ERR_NO_CALLBACK = "failed to configure network; no callback state provided"  # s
 class SimNetwork:
     """sidecar.Network for one simulated instance."""
 
-    def __init__(self, sim, instance: int):
+    def __init__(self, sim, instance: int, order: str = "docker"):
         self.sim = sim
         self.instance = int(instance)
+        self.order = order
         self.active: dict[str, Config] = {}
         self.configured: list[Config] = []   # like MockNetwork.Configured (mock.go:72-76)
         self.closed = False
@@ -46,7 +48,7 @@ class SimNetwork:
     def configure_network(self, cfg: Config) -> None:
         if self.closed:
             raise A.TgsimError(A.ESTATE, "network is closed")
-        self.sim.configure(self.instance, cfg)
+        self.sim.configure(self.instance, cfg, self.order)
         self.configured.append(cfg)
         self.active[cfg.network] = cfg
 
@@ -60,8 +62,12 @@ class SimNetwork:
 class Sidecar:
     """The per-instance sidecar handlers of one run, driven in lock step."""
 
-    def __init__(self, sim, sync: SyncService, n_instances: int, track_configs: bool = False):
+    def __init__(self, sim, sync: SyncService, n_instances: int, track_configs: bool = False,
+                 runner: str = "docker"):
+        if runner not in ("docker", "k8s"):
+            raise ValueError(f"unknown sidecar runner {runner!r}")
         self.sim = sim
+        self.order = runner
         self.sync = sync
         self.n = n_instances
         self.track = track_configs
@@ -70,7 +76,7 @@ class Sidecar:
 
     def network(self, instance: int) -> SimNetwork:
         if instance not in self._nets:
-            self._nets[instance] = SimNetwork(self.sim, instance)
+            self._nets[instance] = SimNetwork(self.sim, instance, self.order)
         return self._nets[instance]
 
     def initialize(self, t: int = 0) -> int:
@@ -92,7 +98,7 @@ class Sidecar:
         if self.track:
             self.network(instance).configure_network(cfg)
         else:
-            self.sim.configure(instance, cfg)
+            self.sim.configure(instance, cfg, self.order)
         if cfg.callback_state:
             self.sync.signal_entry(cfg.callback_state, [instance], t)
 

@@ -115,10 +115,12 @@ class Simulator:
     def configure_network(self, instance: int, cfg: A.NetworkConfig) -> None:
         self._check(self.lib.configure_network(self._ctx, instance, C.byref(cfg)))
 
-    def configure(self, instance: int, cfg) -> None:
-        """DockerNetwork.ConfigureNetwork for one instance from a testground_amd.network.Config."""
+    def configure(self, instance: int, cfg, order: str = "docker") -> None:
+        """ConfigureNetwork for one instance from a testground_amd.network.Config, in the apply order
+        of DockerNetwork (docker_network.go:51-148) or K8sNetwork (k8s_network.go:43-176)."""
         c, keep = cfg.to_c()
-        self._check(self.lib.configure_network(self._ctx, int(instance), C.byref(c)))
+        code = {"docker": A.APPLY_DOCKER, "k8s": A.APPLY_K8S}[order]
+        self._check(self.lib.configure_network_order(self._ctx, int(instance), C.byref(c), code))
         del keep
 
     def set_shape(self, instance: int, shape: A.LinkShape) -> None:

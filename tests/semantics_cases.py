@@ -170,6 +170,40 @@ def case_enable_and_ip_change(b):
     s.close()
 
 
+def case_apply_order_docker_vs_k8s(b):
+    """docker_network.go:51-148 applies the routing policy first, even to a disconnect; K8sNetwork
+    (k8s_network.go:50-61, :166-174) returns after a disconnect and applies the policy last, so a
+    failing AddRules leaves it as it was. External routes leave through the control network and do
+    not need the data link (route.go:68-100)."""
+    from testground_amd.network import Config, IPNet, LinkRule, LinkShape, FilterAction
+    s = sim(b)
+    off = Config(network="default", enable=False, routing_policy="allow_all")
+    s.configure(0, off, "docker")
+    s.configure(1, off, "k8s")
+    st, _ = one_window(s, [0, 1], A.DST_EXTERNAL, 10, 0, 1 * MS)
+    assert list(st) == [A.ST_EXTERNAL, A.ST_UNREACHABLE]
+    bad = Config(network="default", enable=True, routing_policy="allow_all",
+                 rules=[LinkRule(IPNet.parse("16.0.0.5/24"), LinkShape(filter=FilterAction.Drop))])  # host bits
+    for g, order in ((2, "docker"), (3, "k8s")):
+        with pytest.raises(A.TgsimError) as e:
+            s.configure(g, bad, order)
+        assert e.value.code == A.EINVAL
+    st, _ = one_window(s, [2, 3, 0, 1], [A.DST_EXTERNAL, A.DST_EXTERNAL, 3, 3], 10, 1 * MS, 2 * MS, seq=[1, 1, 2, 2])
+    # docker: policy applied before the failing AddRules; k8s: never reached. Disabled senders 0/1
+    # have no data route, whatever their policy says about external traffic.
+    assert list(st) == [A.ST_EXTERNAL, A.ST_UNREACHABLE, A.ST_UNREACHABLE, A.ST_UNREACHABLE]
+    on = Config(network="default", enable=True, routing_policy="allow_all", default=LinkShape(latency=3 * MS))
+    s.configure(1, on, "k8s")
+    st, _ = one_window(s, [1, 1], [2, A.DST_EXTERNAL], 10, 2 * MS, 3 * MS, seq=[3, 4])
+    assert list(st) == [A.ST_QUEUED, A.ST_EXTERNAL]
+    s.advance(10 * MS)
+    assert list(s.deliveries()["t_deliver"]) == [5 * MS]
+    with pytest.raises(A.TgsimError) as e:
+        s.configure(1, Config(network="other", enable=True), "k8s")
+    assert e.value.code == A.EUNSUPPORTED_NETWORK
+    s.close()
+
+
 def case_loopback(b):
     s = sim(b)
     s.set_shape(0, make_shape(latency_ns=10 * MS, loss=100.0))
