@@ -322,6 +322,22 @@ int tgsim_sync_publish(tgsim_ctx* ctx, const uint32_t* topics, const uint32_t* i
 int tgsim_sync_subscribe(tgsim_ctx* ctx, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
                          uint32_t* instances_out, int64_t* t_out, uint64_t* payload_off_out,
                          uint8_t* payload_out, size_t payload_cap, size_t* n_out, size_t* payload_bytes);
+/* Subscribe for a batch of subscribers on the device (the address-exchange fan-out: every instance
+ * reads every entry of one topic, storm.go:232-255), asynchronous on the ctx stream, no host read.
+ * Subscriber i reads topic topics[i] from position from[i] (1-based) on, the entries whose time is
+ * <= until_t[i], at most cap_each of them (a topic >= max_states or from 0 reads none). All arrays are
+ * device memory. offsets_out[0..n] (uint64): exclusive prefix of the per-subscriber counts, so
+ * offsets_out[n] is the total. entries_out (NULL = counts only): subscriber i's inbox is
+ * entries_out[offsets_out[i] .. offsets_out[i+1]), the arena entry ids (tgsim_topic_arena_device) in
+ * position order; ids past entries_cap are not written (compare offsets_out[n] with it). */
+int tgsim_sync_subscribe_device(tgsim_ctx* ctx, size_t n, const uint32_t* topics, const uint32_t* from,
+                                const int64_t* until_t, uint32_t cap_each, uint64_t* offsets_out,
+                                uint32_t* entries_out, size_t entries_cap);
+/* The topic arena in device memory (valid until the next tgsim_sync_publish): per entry id its
+ * publishing instance, time, payload offset into payload and payload length. */
+int tgsim_topic_arena_device(tgsim_ctx* ctx, const uint32_t** instances, const int64_t** t,
+                             const uint64_t** payload_off, const uint32_t** payload_len, const uint8_t** payload,
+                             size_t* n_entries);
 
 /* ---- profiling: HIP-event timing of kernel classes on the ctx stream ---------------------------- */
 /* mask: bit k enables timing of kernel class k (0..tgsim_kernel_classes()-1); 0 disables. */

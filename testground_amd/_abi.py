@@ -158,6 +158,9 @@ _SIGS_HIP = {
     "storm_release_device": (C.c_int, [P, P]),
     "comm_unique_id": (C.c_int, [C.c_void_p]),
     "comm_init": (C.c_int, [P, C.c_void_p, C.c_uint32, C.c_uint32]),
+    "sync_subscribe_device": (C.c_int, [P, C.c_size_t, P, P, P, C.c_uint32, P, P, C.c_size_t]),
+    "topic_arena_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
 }
 
 
@@ -193,6 +196,13 @@ def hip_library() -> Binding:
         path = os.environ.get("TGSIM_LIB") or LIB_PATH
         if not os.path.exists(path):
             raise TgsimError(ENODEV, f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch bundles its own libamdhip64 (soname libamdhip64.so.7). Loaded first, it also serves
+        # libtgsim.so, so the process has one HIP runtime; loaded after /opt/rocm's copy, torch would
+        # bring up a second runtime that finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _HIP = bind(path, "tgsim_", "hip")
     return _HIP
 

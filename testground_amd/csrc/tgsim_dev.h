@@ -40,6 +40,18 @@ struct Flood {
   size_t scan_bytes = 0, cap = 0, mark_cap = 0;
 };
 
+// A topic index for device subscriptions (tgsim_topics.hip): per topic k, runs
+// [run_off[k], run_off[k+1]) in position order; run j holds positions pos0[j] .. pos0[j]+len[j]-1 at
+// arena entries entry[j] ..; t = the arena's entry times.
+struct TopicIndex {
+  const uint32_t* run_off = nullptr;
+  const uint32_t* pos0 = nullptr;
+  const uint32_t* len = nullptr;
+  const uint64_t* entry = nullptr;
+  const int64_t* t = nullptr;
+  uint32_t n_topics = 0;
+};
+
 struct Dev {
   Prof prof;
   Flood fl;
@@ -221,5 +233,12 @@ hipError_t launch_flood_emit(Dev& d, uint32_t n, uint32_t staged_base, uint32_t 
 // A publish batch: set the seen bits of (local, pub) pairs already in d.fl.mark.
 hipError_t launch_flood_mark(Dev& d, uint32_t n);
 size_t flood_scan_bytes(uint32_t n);
+
+// Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),
+// exclusive scan into offsets[0..n], then (entries != nullptr) the entry ids, at most entries_cap.
+hipError_t launch_subscribe(Dev& d, const TopicIndex& ti, uint32_t n, const uint32_t* topics, const uint32_t* from,
+                            const int64_t* until, uint32_t cap_each, uint64_t* cnt, void* scan_tmp, size_t scan_bytes,
+                            uint64_t* offsets, uint32_t* entries, uint64_t entries_cap);
+size_t subscribe_scan_bytes(uint32_t n);
 
 }  // namespace tgsim

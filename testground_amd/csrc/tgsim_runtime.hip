@@ -102,6 +102,14 @@ struct tgsim_ctx {
   uint32_t* tp_len = nullptr;
   uint8_t* tp_bytes = nullptr;
   uint64_t tp_n = 0, tp_cap = 0, tp_nbytes = 0, tp_bytes_cap = 0;
+  // device topic index for tgsim_sync_subscribe_device (CSR of topic_runs; rebuilt after a publish)
+  bool tp_index_dirty = true;
+  uint32_t *ti_off = nullptr, *ti_pos0 = nullptr, *ti_len = nullptr;
+  uint64_t* ti_entry = nullptr;
+  size_t ti_cap = 0;
+  uint64_t* sub_cnt = nullptr;   // [sub_cap + 1] per-subscriber counts (scan input)
+  void* sub_scan = nullptr;
+  size_t sub_cap = 0, sub_scan_bytes = 0;
   // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
   std::vector<uint32_t> fl_off, fl_nbr;
 };
@@ -1445,6 +1453,7 @@ extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const ui
   for (size_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i] || off[i + 1] - off[i] > 0xFFFFFFFFull) return fail(c, TGSIM_EINVAL, "bad payload offsets");
   if (n == 0) return TGSIM_OK;
+  if (c->tp_n + n > 0xFFFFFFFFull) return fail(c, TGSIM_ECAPACITY, "topic arena holds at most 2^32 - 1 entries");
   std::vector<uint32_t> pos(n);
   c->replicated_batch = true;  // topics are replicated: every shard publishes the same batch
   int rc = tgsim_sync_signal(c, topics, inst, t, n, pos.data());
@@ -1456,6 +1465,7 @@ extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const ui
     return topics[a] != topics[b] ? topics[a] < topics[b] : pos[a] < pos[b];
   });
   const uint64_t bytes = off[n];
+  if (c->tp_n + n > 0xFFFFFFFFull) return fail(c, TGSIM_ECAPACITY, "topic arena holds at most 2^32 - 1 entries");
   if (c->tp_n + n > c->tp_cap) {
     const uint64_t cap = std::max<uint64_t>(c->tp_n + n, 2 * c->tp_cap);
     if (dgrow(c, &c->tp_inst, c->tp_n, cap) || dgrow(c, &c->tp_t, c->tp_n, cap) ||
@@ -1495,6 +1505,7 @@ extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const ui
   }
   c->tp_n += n;
   c->tp_nbytes += bytes;
+  c->tp_index_dirty = true;
   if (pos_out) memcpy(pos_out, pos.data(), n * 4);
   return TGSIM_OK;
 }
@@ -1549,5 +1560,80 @@ extern "C" int tgsim_sync_subscribe(tgsim_ctx* c, uint32_t topic, uint32_t from,
     j += m;
   }
   if (off_out) off_out[k] = b;
+  return TGSIM_OK;
+}
+
+// Device fan-out: the topic index (CSR over topics of the host's run lists) is rebuilt after a
+// publish; counts, scan and inbox fill run on the ctx stream (tgsim_topics.hip).
+static int upload_topic_index(tgsim_ctx* c) {
+  const uint32_t K = c->d.max_states;
+  std::vector<uint32_t> off(K + 1, 0), pos0, len;
+  std::vector<uint64_t> entry;
+  for (uint32_t k = 0; k < K; ++k) {
+    if (k < c->topic_runs.size())
+      for (const auto& r : c->topic_runs[k]) { pos0.push_back(r.pos0); len.push_back(r.len); entry.push_back(r.entry); }
+    off[k + 1] = (uint32_t)pos0.size();
+  }
+  const size_t R = pos0.size();
+  if (!c->ti_off && dalloc(c, &c->ti_off, (size_t)K + 1)) return TGSIM_ENOMEM;
+  if (R > c->ti_cap) {
+    const size_t cap = std::max<size_t>(R, 2 * c->ti_cap);
+    HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+    dfree(c, c->ti_pos0); dfree(c, c->ti_len); dfree(c, c->ti_entry);
+    c->ti_pos0 = c->ti_len = nullptr; c->ti_entry = nullptr;
+    if (dalloc(c, &c->ti_pos0, cap) || dalloc(c, &c->ti_len, cap) || dalloc(c, &c->ti_entry, cap)) return TGSIM_ENOMEM;
+    c->ti_cap = cap;
+  }
+  HIPCK(c, hipMemcpyAsync(c->ti_off, off.data(), (K + 1) * 4ull, hipMemcpyHostToDevice, c->d.stream), "topic index");
+  if (R) {
+    HIPCK(c, hipMemcpyAsync(c->ti_pos0, pos0.data(), R * 4, hipMemcpyHostToDevice, c->d.stream), "topic index");
+    HIPCK(c, hipMemcpyAsync(c->ti_len, len.data(), R * 4, hipMemcpyHostToDevice, c->d.stream), "topic index");
+    HIPCK(c, hipMemcpyAsync(c->ti_entry, entry.data(), R * 8, hipMemcpyHostToDevice, c->d.stream), "topic index");
+  }
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "topic index");  // the host vectors go out of scope
+  c->tp_index_dirty = false;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_sync_subscribe_device(tgsim_ctx* c, size_t n, const uint32_t* topics, const uint32_t* from,
+                                           const int64_t* until_t, uint32_t cap_each, uint64_t* offsets_out,
+                                           uint32_t* entries_out, size_t entries_cap) {
+  if (!c || !offsets_out || (n && (!topics || !from || !until_t))) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (n >= 0xFFFFFFFFull) return fail(c, TGSIM_EINVAL, "too many subscribers");
+  if (c->tp_index_dirty) {
+    const int rc = upload_topic_index(c);
+    if (rc) return rc;
+  }
+  if (n > c->sub_cap) {
+    const size_t cap = std::max<size_t>(n, 2 * c->sub_cap);
+    HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+    dfree(c, c->sub_cnt); dfree(c, c->sub_scan);
+    c->sub_cnt = nullptr; c->sub_scan = nullptr;
+    c->sub_scan_bytes = subscribe_scan_bytes((uint32_t)cap);
+    if (dalloc(c, &c->sub_cnt, cap + 1) || dalloc(c, (uint8_t**)&c->sub_scan, c->sub_scan_bytes)) return TGSIM_ENOMEM;
+    c->sub_cap = cap;
+  }
+  if (!c->sub_cnt) {
+    c->sub_scan_bytes = subscribe_scan_bytes(0);
+    if (dalloc(c, &c->sub_cnt, 1) || dalloc(c, (uint8_t**)&c->sub_scan, c->sub_scan_bytes)) return TGSIM_ENOMEM;
+  }
+  TopicIndex ti;
+  ti.run_off = c->ti_off; ti.pos0 = c->ti_pos0; ti.len = c->ti_len; ti.entry = c->ti_entry; ti.t = c->tp_t;
+  ti.n_topics = c->d.max_states;
+  HIPCK(c, launch_subscribe(c->d, ti, (uint32_t)n, topics, from, until_t, cap_each, c->sub_cnt, c->sub_scan,
+                            c->sub_scan_bytes, offsets_out, entries_out, entries_cap),
+        "subscribe");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_topic_arena_device(tgsim_ctx* c, const uint32_t** inst, const int64_t** t, const uint64_t** off,
+                                        const uint32_t** len, const uint8_t** payload, size_t* n) {
+  if (!c) return TGSIM_EINVAL;
+  if (inst) *inst = c->tp_inst;
+  if (t) *t = c->tp_t;
+  if (off) *off = c->tp_off;
+  if (len) *len = c->tp_len;
+  if (payload) *payload = c->tp_bytes;
+  if (n) *n = c->tp_n;
   return TGSIM_OK;
 }

@@ -329,6 +329,58 @@ class Simulator:
         raw = blob.tobytes()
         return inst[:k].copy(), tt[:k].copy(), [raw[int(off[j]):int(off[j + 1])] for j in range(k)]
 
+    def subscribe_device(self, topics, from_pos, until_t, cap_each: int = 0xFFFFFFFF, entries: bool = True,
+                         entries_cap: int | None = None, wait: bool = True):
+        """Subscribe for a batch of subscribers on the device (tgsim_sync_subscribe_device). Inputs
+        are torch tensors on the context's device (uint32 topics / from_pos as int32 or int64
+        tensors, int64 until_t). Returns (offsets [n+1] int64 tensor, entry ids int32 tensor or
+        None); subscriber i's inbox is ids[offsets[i]:offsets[i+1]] (arena entries, topic_arena).
+        The work runs on the context's stream: wait=False returns before it is done (the caller
+        orders its own stream after it, e.g. by sharing the stream through set_stream)."""
+        import torch
+        dev = topics.device
+        tp = topics.to(torch.int32).contiguous()
+        fr = from_pos.to(torch.int32).contiguous()
+        ut = until_t.to(torch.int64).contiguous()
+        n = tp.numel()
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        torch.cuda.current_stream(dev).synchronize()  # the inputs were made on torch's stream
+        ids = None
+        if entries:
+            if entries_cap is None:  # counts first (one host read) to size the inbox arrays exactly
+                self._check(self.lib.sync_subscribe_device(self._ctx, n, tp.data_ptr(), fr.data_ptr(), ut.data_ptr(),
+                                                           cap_each, offs.data_ptr(), None, 0))
+                torch.cuda.synchronize(dev)
+                entries_cap = int(offs[-1].item())
+            ids = torch.empty(max(1, entries_cap), dtype=torch.int32, device=dev)
+        self._check(self.lib.sync_subscribe_device(self._ctx, n, tp.data_ptr(), fr.data_ptr(), ut.data_ptr(), cap_each,
+                                                   offs.data_ptr(), ids.data_ptr() if ids is not None else None,
+                                                   entries_cap or 0))
+        if wait:
+            self.sync()
+        return offs, ids
+
+    def topic_arena(self) -> dict:
+        """The topic arena copied to the host: per entry id instance, t, payload offset / length, and
+        the payload bytes (tgsim_topic_arena_device)."""
+        from .exchange import _D2H, _hip
+        ptrs = [C.c_void_p() for _ in range(5)]
+        n = C.c_size_t()
+        self._check(self.lib.topic_arena_device(self._ctx, *[C.byref(p) for p in ptrs], C.byref(n)))
+        self.sync()
+        hip = _hip()
+        k = n.value
+        out = {"instance": np.zeros(k, np.uint32), "t": np.zeros(k, np.int64), "payload_off": np.zeros(k, np.uint64),
+               "payload_len": np.zeros(k, np.uint32)}
+        for p, key in zip(ptrs[:4], ("instance", "t", "payload_off", "payload_len")):
+            if k:
+                assert hip.hipMemcpy(out[key].ctypes.data, p.value, out[key].nbytes, _D2H) == 0
+        nb = int((out["payload_off"][-1] + out["payload_len"][-1])) if k else 0
+        out["payload"] = np.zeros(nb, np.uint8)
+        if nb:
+            assert hip.hipMemcpy(out["payload"].ctypes.data, ptrs[4].value, nb, _D2H) == 0
+        return out
+
     # ---- flood workload (config 5) -----------------------------------------------------------
     def flood_set_graph(self, offsets, neighbors, max_pubs: int) -> None:
         off = np.ascontiguousarray(offsets, dtype=np.uint32)
