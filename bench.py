@@ -409,7 +409,7 @@ def flood_cpu_baseline(args, shapes, graph):
             sim.flood_publish(W.publishers(N, 1, w // args.pub_every, args.seed), [w // args.pub_every], sim.now,
                               args.flood_size)
         sim.advance(sim.now + win)
-        sim.flood_react(args.flood_size)
+        sim.flood_react(args.flood_size, count=False)
         w += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds or w >= 400:
@@ -455,8 +455,8 @@ def main_flood(args):
         if w % args.pub_every == 0:
             k = w // args.pub_every
             sim.flood_publish(W.publishers(N, 1, k, args.seed), [k], sim.now, args.flood_size)
-        sim.advance(sim.now + win)  # sharded: collective, the exchange inside
-        sim.flood_react(args.flood_size)
+        sim.advance(sim.now + win, wait=False)  # sharded: collective, the exchange inside; no host sync
+        sim.flood_react(args.flood_size, count=False)
 
     for w in range(args.warmup):
         step(w)

@@ -245,6 +245,9 @@ int tgsim_enqueue_device(tgsim_ctx* ctx, const tgsim_msg_soa* dev_msgs, size_t n
  * then collective - every shard calls it with the same t_end. A host-staged message sent at or
  * after t_end is refused with ECAUSALITY before anything changes (the context stays usable). */
 int tgsim_advance(tgsim_ctx* ctx, int64_t t_end);
+/* tgsim_advance without the closing synchronisation: everything stays queued on the ctx stream and
+ * device-side errors surface at the next synchronising call (tgsim_sync, a copy, stats). */
+int tgsim_advance_async(tgsim_ctx* ctx, int64_t t_end);
 /* Same, with t_end = release time of a barrier waiter + offset, read on the device (no host sync).
  * Sharded: collective, as tgsim_advance (the barrier's state is replicated on every shard). */
 int tgsim_advance_to_barrier(tgsim_ctx* ctx, uint32_t waiter, int64_t offset_ns);

@@ -961,6 +961,9 @@ int tgo_advance(tgo_ctx* c, int64_t t_end) {
   return tgo_advance_end(c);
 }
 
+/* The CPU model has no stream: the same call as tgo_advance. */
+int tgo_advance_async(tgo_ctx* c, int64_t t_end) { return tgo_advance(c, t_end); }
+
 int tgo_delivery_count(tgo_ctx* c, size_t* n) { *n = c->out.n; return 0; }
 
 int tgo_copy_deliveries(tgo_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n) {

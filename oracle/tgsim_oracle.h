@@ -56,6 +56,7 @@ int tgo_get_ip(const tgo_ctx* ctx, uint32_t instance, uint32_t* ip);
 
 int tgo_enqueue(tgo_ctx* ctx, const tgsim_msg_soa* msgs, size_t n);
 int tgo_advance(tgo_ctx* ctx, int64_t t_end);
+int tgo_advance_async(tgo_ctx* ctx, int64_t t_end);
 int tgo_advance_begin(tgo_ctx* ctx, int64_t t_end);
 /* host buffers, same layout as tgsim_exchange_buffers (peer-major, header record per peer) */
 int tgo_exchange_buffers(tgo_ctx* ctx, void** send, void** recv, size_t* bytes);

@@ -116,6 +116,7 @@ _SIGS = {
     "get_ip": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "enqueue": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
     "advance": (C.c_int, [P, C.c_int64]),
+    "advance_async": (C.c_int, [P, C.c_int64]),
     "advance_begin": (C.c_int, [P, C.c_int64]),
     "exchange_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_size_t)]),
     "advance_end": (C.c_int, [P]),

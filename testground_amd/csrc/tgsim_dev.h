@@ -32,12 +32,11 @@ struct Flood {
   uint32_t* nbr = nullptr;        // neighbours (global ids)
   uint32_t* seen = nullptr;       // [max_pubs * wpp] bit (p, local instance)
   uint32_t D = 0, max_pubs = 0, wpp = 0;
-  uint32_t* cnt = nullptr;        // [cap+1] forwards per item (0 unless first receipt)
-  uint32_t* pos = nullptr;        // [cap+1] exclusive prefix of cnt; pos[n] = total
+  uint32_t* cnt = nullptr;        // [cap] forwards per delivery (0 unless first receipt)
   uint8_t* first = nullptr;       // [cap] first receipt of (pub, receiver)
+  uint32_t* bsum = nullptr;       // [kFloodBlocks] forwards per chunk -> staged offset of the chunk
   uint32_t* mark = nullptr;       // [mark_cap] (local, pub) pairs of a publish batch
-  void* scan_tmp = nullptr;
-  size_t scan_bytes = 0, cap = 0, mark_cap = 0;
+  size_t cap = 0, mark_cap = 0;
 };
 
 // A topic index for device subscriptions (tgsim_topics.hip): per topic k, runs
@@ -205,7 +204,8 @@ hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);
 hipError_t launch_storm_unpack(Dev& d, const int64_t* red2);
 // init_crandom on a Shape call: the state of local sender pairs[2i] re-seeded for epoch pairs[2i+1]
 hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n);
-hipError_t window_begin(Dev& d, uint32_t n_staged);  // wheel extract, shape, token bucket, pack
+// wheel extract, shape, token bucket, pack; n_dev non-null: the staged count is read on the device
+hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev = nullptr);
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)
 // Signal batch already in d.s_state/s_inst/s_t. States lie in [kmin, kmax]. count_only: the
@@ -223,16 +223,20 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 hipError_t launch_sig_commit(Dev& d, uint32_t nparts, bool commit, uint32_t n, uint32_t st, uint32_t n_waiters,
                              bool add, uint32_t add_state, uint32_t add_target, int64_t add_twait);
 
-// Flood reaction over the last window's deliveries (n = n_out, inbox order): count pass (first
-// receipt of (pub, receiver) against the seen bits and the receiver's earlier deliveries), device
-// exclusive scan, then *total is read back (blocking) and the caller launches launch_flood_emit.
-hipError_t launch_flood_count(Dev& d, uint32_t n, uint32_t* total);
-// Forwards of every first receipt: seen bit set, messages staged at staged_base + pos[i] with
-// t_send = max(t_deliver, horizon), seq = pub * D + neighbour slot.
-hipError_t launch_flood_emit(Dev& d, uint32_t n, uint32_t staged_base, uint32_t size, int64_t horizon);
+// Flood reaction over the last window's deliveries (sc->n_out of them, inbox order), with no host
+// read: count pass (first receipt of (pub, receiver) against the seen bits and the receiver's
+// earlier deliveries) over kFloodBlocks chunks, a one-block scan of the chunk totals, then the
+// forwards of every first receipt (seen bit set, t_send = max(t_deliver, horizon), seq = pub * D +
+// neighbour slot) staged after the staged messages: at base_host, or at sc->n_msgs_dev when
+// base_dev; sc->n_msgs_dev = the new staged count.
+hipError_t launch_flood_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t size, int64_t horizon);
+// Staging behind a device-side count: n messages (SoA at the given device pointers) appended at
+// sc->n_msgs_dev, which then grows by n.
+hipError_t launch_append(Dev& d, const uint32_t* src, const uint32_t* dst, const uint32_t* seq, const uint32_t* size,
+                         const int64_t* t, uint32_t n);
 // A publish batch: set the seen bits of (local, pub) pairs already in d.fl.mark.
 hipError_t launch_flood_mark(Dev& d, uint32_t n);
-size_t flood_scan_bytes(uint32_t n);
+constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),
 // exclusive scan into offsets[0..n], then (entries != nullptr) the entry ids, at most entries_cap.

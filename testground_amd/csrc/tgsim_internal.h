@@ -35,7 +35,8 @@ enum : uint32_t {
   ERR_ARENA = 1u << 4, ERR_REGIONS = 1u << 5, ERR_CAUSAL = 1u << 6, ERR_SIG_ORDER = 1u << 7,
   ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
   ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14,
-  ERR_QUEUE_CAP = 1u << 15  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
+  ERR_QUEUE_CAP = 1u << 15,  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
+  ERR_CAP_M = 1u << 16       // device-counted staging (flood forwards, appends after them) outgrew cap_msgs
 };
 
 // Per-sender egress state derived from network.LinkShape (48 B; gathered by src).
@@ -82,7 +83,6 @@ struct DevScalars {
   uint32_t n_recv, n_out;
   uint32_t n_corr;                   // messages deferred by k_shape (correlated or queue-heavy senders)
   uint32_t n_hrec;                   // due wheel records of queue-heavy senders copied to the H list
-  uint32_t max_inbox;                // longest inbox run of the window's deliveries (flood forward bound)
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits
   uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)
@@ -91,6 +91,11 @@ struct DevScalars {
   uint64_t sig_log_used;             // signal log entries used
   uint32_t pend_max;                 // max over local senders of queued copies (k_pend_max, host gate)
   uint32_t pad_pm;
+  // device-counted staging: once the flood reaction stages its forwards, the staged
+  // count lives here (appends go after it); the window's shape pass reads it, window end moves it
+  // to n_msgs_last (the status count of that window) and clears it
+  uint32_t n_msgs_dev, n_msgs_last;
+  uint32_t fl_total, pad_fl;         // forwards staged by the last flood reaction
   // cumulative statistics (tgsim_stats)
   unsigned long long st[13];
 };
@@ -166,6 +171,30 @@ __host__ __device__ inline uint32_t shard_of(uint32_t g, uint32_t N, uint32_t S)
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ inline uint32_t mask_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Block-wide exclusive scan (every thread of the block calls it): a wave scan by shuffles, the
+// four wave totals through red[0..3], two barriers (the second frees red for reuse).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, uint32_t& total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) red[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    const uint32_t a = red[w];
+    pre += w < wave ? a : 0u;
+    total += a;
+  }
+  __syncthreads();
+  return pre + x - v;
 }
 
 }  // namespace tgsim

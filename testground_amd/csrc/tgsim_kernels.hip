@@ -53,30 +53,6 @@ __device__ __forceinline__ void store_rec(tgsim_record* p, const tgsim_record& r
   q[1] = make_uint4(r.seq, r.size, r.meta, r.corrupt_off);
 }
 
-// Block-wide exclusive scan (every thread of the block calls it): a wave scan by shuffles, the
-// four wave totals through red[0..3], two barriers (the second frees red for reuse).
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, uint32_t& total) {
-  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if ((int)lane >= o) x += y;
-  }
-  if (lane == 63) red[wave] = x;
-  __syncthreads();
-  uint32_t pre = 0;
-  total = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kBlock / 64; ++w) {
-    const uint32_t a = red[w];
-    pre += w < wave ? a : 0u;
-    total += a;
-  }
-  __syncthreads();
-  return pre + x - v;
-}
-
 // Wave64 compaction onto per-lane counters: lanes whose counter pointer is equal share one
 // atomicAdd (ballot -> leader atomic -> broadcast -> mbcnt rank). nullptr = nothing to append.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
@@ -336,6 +312,7 @@ struct ShapeArgs {
   const uint32_t *src, *dst, *seq, *size;
   const int64_t* t;
   uint32_t n;
+  const uint32_t* n_dev;      // non-null: the staged count is device-side (sc->n_msgs_dev), n unused
   uint8_t* status;
   const ShapeDev* shape;
   const uint64_t* ipf;         // [N] ip | flags << 32
@@ -464,7 +441,8 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t stride = nblocks * blockDim.x;
   uint32_t it = 0;
-  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < a.n; i += stride, ++it) {
+  const uint32_t n = a.n_dev ? *a.n_dev : a.n;
+  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += stride, ++it) {
     // Every load of this message is issued up front with clamped indices, so the wave pays one
     // round trip for the SoA record and one for the table gathers instead of a branch-serialised chain.
     const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
@@ -1180,10 +1158,17 @@ __device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uin
 // The host's exact refresh of its occupancy bound: max over local senders of pend -> sc->pend_max
 // (zeroed by the host's memset first).
 __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, uint32_t nloc, uint32_t* out) {
+  __shared__ uint32_t red[kBlock / 64];
   uint32_t mx = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock) mx = max(mx, pend[i]);
   mx = wave_max(mx);
-  if (lane_id() == 0 && mx) atomicMax(out, mx);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  // one atomic per block: same-address atomics from every wave serialise (95 us at 1M senders)
+  if (threadIdx.x == 0) {
+    mx = max(max(red[0], red[1]), max(red[2], red[3]));
+    if (mx) atomicMax(out, mx);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
@@ -1197,6 +1182,8 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
     if (threadIdx.x == 0) {
       const uint32_t n = sc->qn[Q_D];
       sc->n_out = n;
+      sc->n_msgs_last = sc->n_msgs_dev;  // the shape pass of this window has read it
+      sc->n_msgs_dev = 0;
       sc->st[ST_DELIVERED] += n;
       sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
       sc->st[ST_EXTRACTED] += sc->n_extract;
@@ -1543,7 +1530,6 @@ struct EmitPolicy {
   const tgsim_record* D;
   uint32_t* pend;  // queue occupancy: a delivered wheel copy of a local sender no longer counts
   uint32_t lo, nloc;
-  bool want_max_inbox;  // flood: the longest inbox run -> sc->max_inbox (the host's forward bound)
   int64_t* o_t;
   uint32_t *o_src, *o_dst, *o_seq, *o_size, *o_flags, *o_coff;
 
@@ -1649,7 +1635,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
                                                uint32_t* off2, uint32_t* medium, LargeSeg* large, DevScalars* sc,
                                                BktFusedSmem& sm, BktHead& h, const tgsim_record* batch,
                                                const KeyFn& keyfn, tgsim_record (&rec)[kIPT],
-                                               uint32_t (&slot)[kIPT], bool want_max = false) {
+                                               uint32_t (&slot)[kIPT]) {
   // XCD-aware bucket order: hardware dispatch puts block i on XCD i % 8, so consecutive buckets -
   // whose chunks share cache lines in every partition block's range - go to the same XCD's L2
   const uint32_t b = xcd_major(blockIdx.x, B);
@@ -1686,8 +1672,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
       vscr[h.start + j] = e.y;
     }
     __syncthreads();
-    const uint32_t mx = bkt_count_body(kscr, sm.cnt, sm.part, h);
-    if (!by_pos && want_max && threadIdx.x == 0) atomicMax(&sc->max_inbox, mx);  // longest inbox run (flood)
+    (void)bkt_count_body(kscr, sm.cnt, sm.part, h);
     bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
     return false;
   }
@@ -1732,7 +1717,6 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     run += len;
   }
   __syncthreads();
-  if (!by_pos && want_max && threadIdx.x == 0 && sm.maxlen) atomicMax(&sc->max_inbox, sm.maxlen);
   TG_PH(4);
   // slots + sort keys (from the registers: no second gather)
 #pragma unroll
@@ -1952,7 +1936,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
   tgsim_record rec[kIPT];
   uint32_t slot[kIPT];
   if (!bkt_fused_load<false>(src, poff, kv, kscr, vscr, kout, vout, bd, B, K, off, off2, medium, large, sc,
-                             sm, h, p.D, EmitKey{}, rec, slot, p.want_max_inbox))
+                             sm, h, p.D, EmitKey{}, rec, slot))
     return;
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {  // inbox offsets of the bucket's receivers
     const uint32_t o = h.start + (i ? sm.cnt[i - 1] : 0u);
@@ -3270,7 +3254,8 @@ hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
 
 hipError_t launch_pend_max(Dev& d) {
   TG_CHECK(hipMemsetAsync(&d.sc->pend_max, 0, sizeof(uint32_t), d.stream));
-  hipLaunchKernelGGL(k_pend_max, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.pend, d.nloc, &d.sc->pend_max);
+  hipLaunchKernelGGL(k_pend_max, dim3(std::min<unsigned>(grid_for(d.nloc), 1024u)), dim3(kBlock), 0, d.stream, d.pend,
+                     d.nloc, &d.sc->pend_max);
   return hipGetLastError();
 }
 
@@ -3281,8 +3266,9 @@ hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
   return hipGetLastError();
 }
 
-hipError_t window_begin(Dev& d, uint32_t n_staged) {
+hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
   Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
+  if (n_dev) n_staged = d.cap_msgs;  // device-counted: size the launches for the capacity (grid-stride)
   HeavyOut ho;
   ho.hv = n_staged ? d.heavy : Heavy{};  // H feeds only the staged messages' sequential lane
   ho.geo = Geo{d.N, d.S, d.shard}; ho.H = d.H; ho.hkeys = d.hkeys; ho.hvals = d.hvals; ho.hcap = d.h_cap;
@@ -3295,7 +3281,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged) {
   TG_CHECK(hipGetLastError());
   if (n_staged) {
     ShapeArgs a;
-    a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged;
+    a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged; a.n_dev = n_dev;
     a.status = d.status; a.shape = d.shape; a.ipf = d.ipf; a.rule_off = d.rule_off;
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
@@ -3335,7 +3321,7 @@ hipError_t window_end(Dev& d) {
     TG_CHECK(hipGetLastError());
   }
   EmitPolicy p;
-  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.want_max_inbox = d.fl.off != nullptr; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;

@@ -53,6 +53,8 @@ struct tgsim_ctx {
   uint32_t n_staged = 0, n_status_last = 0;
   bool in_window = false;
   bool now_from_device = false;
+  bool end_known = false;             // the open window's end was given by the host (explicit t_end)
+  int64_t end_h = 0;
   uint64_t sig_log_used = 0;
   uint32_t n_waiters = 0;
   // a storm batch whose count-only commit is deferred to the next sync-service call (a barrier
@@ -77,7 +79,19 @@ struct tgsim_ctx {
   uint32_t win_m_host = 0;           // max of hcnt
   uint64_t win_m_extra = 0;          // device-staged messages (storm fanout, enqueue_device n): any sender
   uint32_t win_m_inbox = 0;          // flood forwards staged: (D - 1) per delivery of the sender's last inbox
-  uint32_t inbox_max_h = 0;          // longest inbox run of the last window (read at the flood reaction)
+  // flood: a sender forwards each publication once (first receipt), so (D - 1) * (publications so
+  // far) bounds its forwards in any window without reading the device
+  uint32_t fl_npubs = 0;
+  std::vector<uint8_t> fl_pub_seen;
+  // device-counted staging: after an asynchronous flood reaction the staged count is
+  // sc->n_msgs_dev; host / device enqueues then append behind it on the device
+  bool staged_dev = false;
+  uint8_t* app = nullptr;  // [app_cap * 24] t | src | dst | seq | size, the pinned layout (one copy)
+  size_t app_cap = 0;
+  // pinned staging of host uploads (messages, publish marks): the copies are asynchronous, a buffer
+  // is reused once its event has passed
+  struct Pinned { uint8_t* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool busy = false; };
+  Pinned pin_msgs, pin_marks;
   bool any_dup = false;
   // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
   // signal all-gather run inside the library - natively over RCCL (comm), or through caller callbacks
@@ -145,6 +159,34 @@ static int hipfail(tgsim_ctx* c, hipError_t e, const char* what) {
     hipError_t e__ = (x);                          \
     if (e__ != hipSuccess) return hipfail(c, e__, what); \
   } while (0)
+
+constexpr uint32_t kStatusOnDevice = 0xFFFFFFFFu;  // n_status_last: the count is sc->n_msgs_last
+
+// A pinned upload buffer of at least `bytes` in *out, once the copies that last used it have completed.
+static int pin_acquire(tgsim_ctx* c, tgsim_ctx::Pinned& b, size_t bytes, uint8_t** out) {
+  if (b.busy) {
+    HIPCK(c, hipEventSynchronize(b.ev), "pinned staging event");
+    b.busy = false;
+  }
+  if (!b.ev) HIPCK(c, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming), "event");
+  if (bytes > b.cap) {
+    const size_t cap = std::max<size_t>({bytes, 2 * b.cap, (size_t)1 << 16});
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipHostMalloc((void**)&b.p, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(c, TGSIM_ENOMEM, "pinned staging (%zu bytes)", cap);
+    b.cap = cap;
+  }
+  *out = b.p;
+  return TGSIM_OK;
+}
+// The copies out of b have been issued on the ctx stream.
+static int pin_issued(tgsim_ctx* c, tgsim_ctx::Pinned& b) {
+  HIPCK(c, hipEventRecord(b.ev, c->d.stream), "event");
+  b.busy = true;
+  return TGSIM_OK;
+}
 
 static void dfree(tgsim_ctx* c, void* p) {
   if (!p) return;
@@ -242,6 +284,10 @@ extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
 extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (!c) return;
   if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
+  for (tgsim_ctx::Pinned* b : {&c->pin_msgs, &c->pin_marks}) {
+    if (b->p) (void)hipHostFree(b->p);
+    if (b->ev) (void)hipEventDestroy(b->ev);
+  }
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->d.h_sc) (void)hipHostFree(c->d.h_sc);
@@ -807,7 +853,9 @@ extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
-  if ((uint64_t)c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  if (!c->staged_dev && (uint64_t)c->n_staged + n > c->d.cap_msgs)
+    return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  if (n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   int rc = validate_msgs(c, m, n);
   if (rc) return rc;
   if (!n) return TGSIM_OK;
@@ -818,24 +866,51 @@ extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
     c->max_tsend_h = std::max(c->max_tsend_h, m->t_send[i]);
   }
   Dev& d = c->d;
+  uint8_t* pin = nullptr;  // t | src | dst | seq | size
+  rc = pin_acquire(c, c->pin_msgs, n * 24, &pin);
+  if (rc) return rc;
+  memcpy(pin, m->t_send, n * 8);
+  memcpy(pin + n * 8, m->src, n * 4);
+  memcpy(pin + n * 12, m->dst, n * 4);
+  memcpy(pin + n * 16, m->seq, n * 4);
+  memcpy(pin + n * 20, m->size, n * 4);
+  if (c->staged_dev) {  // behind the device-side count: via scratch, then appended on the device
+    if (n > c->app_cap) {
+      HIPCK(c, hipStreamSynchronize(d.stream), "sync");
+      dfree(c, c->app);
+      c->app = nullptr;
+      const size_t cap = std::max<size_t>(n, 2 * c->app_cap);
+      if (dalloc(c, &c->app, cap * 24)) return TGSIM_ENOMEM;
+      c->app_cap = cap;
+    }
+    HIPCK(c, hipMemcpyAsync(c->app, pin, n * 24, hipMemcpyHostToDevice, d.stream), "enqueue");
+    const uint32_t* a32 = reinterpret_cast<const uint32_t*>(c->app + n * 8);
+    HIPCK(c, launch_append(d, a32, a32 + n, a32 + 2 * n, a32 + 3 * n, reinterpret_cast<const int64_t*>(c->app),
+                           (uint32_t)n), "append");
+    return pin_issued(c, c->pin_msgs);
+  }
   const size_t o = c->n_staged;
-  HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_dst + o, m->dst, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_seq + o, m->seq, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_size + o, m->size, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_t + o, m->t_send, n * 8, hipMemcpyHostToDevice, d.stream), "enqueue");
-  HIPCK(c, hipStreamSynchronize(d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_t + o, pin, n * 8, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_src + o, pin + n * 8, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_dst + o, pin + n * 12, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_seq + o, pin + n * 16, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
+  HIPCK(c, hipMemcpyAsync(d.m_size + o, pin + n * 20, n * 4, hipMemcpyHostToDevice, d.stream), "enqueue");
   c->n_staged += (uint32_t)n;
-  return TGSIM_OK;
+  return pin_issued(c, c->pin_msgs);
 }
 
 extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
-  if ((uint64_t)c->n_staged + n > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
+  if ((c->staged_dev ? 0 : (uint64_t)c->n_staged) + n > c->d.cap_msgs)
+    return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (!n) return TGSIM_OK;
   c->win_m_extra += n;  // any one sender may hold all of them (queue-limit test)
   Dev& d = c->d;
+  if (c->staged_dev) {
+    HIPCK(c, launch_append(d, m->src, m->dst, m->seq, m->size, m->t_send, (uint32_t)n), "append");
+    return TGSIM_OK;
+  }
   const size_t o = c->n_staged;
   HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
   HIPCK(c, hipMemcpyAsync(d.m_dst + o, m->dst, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
@@ -853,7 +928,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
   Dev& d = c->d;
   const uint64_t mult = c->any_dup ? 2 : 1;
   const uint64_t m_uniform = std::min<uint64_t>((uint64_t)c->win_m_host + c->win_m_extra, 0x7FFFFFFFull);
-  const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->inbox_max_h;
+  const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->fl_npubs;
   bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   if (gate && !c->pend_exact) {  // inconclusive: refresh the bound with the exact maximum (one sync)
     HIPCK(c, launch_pend_max(d), "pend max");
@@ -892,9 +967,11 @@ static int begin_common(tgsim_ctx* c) {
   if (rc) return rc;
   rc = plan_queue_limit(c);
   if (rc) return rc;
-  HIPCK(c, window_begin(c->d, c->n_staged), "window_begin");
-  c->n_status_last = c->n_staged;
+  HIPCK(c, window_begin(c->d, c->n_staged, c->staged_dev ? &c->d.sc->n_msgs_dev : nullptr), "window_begin");
+  c->n_status_last = c->staged_dev ? kStatusOnDevice : c->n_staged;
   c->n_staged = 0;
+  c->staged_dev = false;
+  c->end_known = false;  // device-ended windows (barrier / device t_end); explicit ones set it after
   c->in_window = true;
   return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
@@ -909,7 +986,11 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   if (c->max_tsend_h >= t_end) return fail(c, TGSIM_ECAUSALITY, "a staged message is sent at/after t_end");
   HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window(c->d, t_end), "set window");
-  return begin_common(c);
+  const int rc = begin_common(c);
+  if (rc) return rc;
+  c->end_known = true;  // begin_common cleared it
+  c->end_h = t_end;
+  return TGSIM_OK;
 }
 
 extern "C" int tgsim_exchange_buffers(tgsim_ctx* c, void** send, void** recv, size_t* bytes) {
@@ -944,8 +1025,14 @@ extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
   HIPCK(c, window_end(c->d), "window_end");
   c->in_window = false;
-  // No host round trip: the window's end (and any device-side error) is read at the next sync.
-  c->now_from_device = true;
+  // No host round trip: a host-given end is the new clock; a device-ended window's end (and any
+  // device-side error) is read at the next sync.
+  if (c->end_known) {
+    c->horizon = c->now;
+    c->now = c->end_h;
+  } else {
+    c->now_from_device = true;
+  }
   return TGSIM_OK;
 }
 
@@ -1044,6 +1131,19 @@ extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
   return sync_and_check(c);  // the host-driven API reports the window's errors here
 }
 
+extern "C" int tgsim_advance_async(tgsim_ctx* c, int64_t t_end) {
+  if (!c) return TGSIM_EINVAL;
+  int rc = need_transport(c);
+  if (rc) return rc;
+  rc = tgsim_advance_begin(c, t_end);
+  if (rc) return rc;
+  if (c->S != 1) {
+    rc = exchange_window(c);
+    if (rc) return rc;
+  }
+  return tgsim_advance_end(c);
+}
+
 extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
   if (!c) return TGSIM_EINVAL;
   int rc0 = need_transport(c);
@@ -1108,9 +1208,10 @@ extern "C" int tgsim_copy_status(tgsim_ctx* c, uint8_t* out, size_t cap, size_t*
   if (!c || !n) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   if (rc) return rc;
-  *n = c->n_status_last;
-  if (c->n_status_last > cap) return fail(c, TGSIM_ECAPACITY, "status capacity");
-  if (c->n_status_last) HIPCK(c, hipMemcpy(out, c->d.status, c->n_status_last, hipMemcpyDeviceToHost), "copy");
+  const uint32_t k = c->n_status_last == kStatusOnDevice ? c->d.h_sc->n_msgs_last : c->n_status_last;
+  *n = k;
+  if (k > cap) return fail(c, TGSIM_ECAPACITY, "status capacity");
+  if (k) HIPCK(c, hipMemcpy(out, c->d.status, k, hipMemcpyDeviceToHost), "copy");
   return TGSIM_OK;
 }
 
@@ -1275,6 +1376,7 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
   if (size >= 0x80000000u || spread_ns < 0) return fail(c, TGSIM_EINVAL, "bad size/spread");
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
+  if (c->staged_dev) return fail(c, TGSIM_ENOTSUP, "a storm round after a flood reaction in the same window");
   if (t0 != TGSIM_T_NOW) {
     if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
     if (t0 < c->now) return fail(c, TGSIM_ECAUSALITY, "t0 before window start");
@@ -1352,6 +1454,14 @@ extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const ui
   HIPCK(c, hipMemcpy(f.off, c->fl_off.data(), (c->nloc + 1) * 4, hipMemcpyHostToDevice), "graph");
   if (m) HIPCK(c, hipMemcpy(f.nbr, c->fl_nbr.data(), (size_t)m * 4, hipMemcpyHostToDevice), "graph");
   HIPCK(c, hipMemset(f.seen, 0, words * 4), "graph");
+  if (!f.cnt) {  // reaction scratch for every delivery a window can hold
+    const size_t cap = (size_t)kNSub * c->d.subcap;
+    if (dalloc(c, &f.cnt, cap) || dalloc(c, &f.first, cap) || dalloc(c, &f.bsum, (size_t)kFloodBlocks))
+      return TGSIM_ENOMEM;
+    f.cap = cap;
+  }
+  c->fl_pub_seen.assign(max_pubs, 0);
+  c->fl_npubs = 0;
   return TGSIM_OK;
 }
 
@@ -1364,6 +1474,8 @@ extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uin
   if (n && (!inst || !pubs || !t)) return fail(c, TGSIM_EINVAL, "bad arguments");
   for (size_t i = 0; i < n; ++i)
     if (inst[i] >= c->N || pubs[i] >= f.max_pubs) return fail(c, TGSIM_EINVAL, "bad publication %zu", i);
+  for (size_t i = 0; i < n; ++i)  // every shard sees the whole batch: the count is global
+    if (!c->fl_pub_seen[pubs[i]]) { c->fl_pub_seen[pubs[i]] = 1; ++c->fl_npubs; }
   std::vector<uint32_t> src, dst, seq, sz, pairs;
   std::vector<int64_t> ts;
   for (size_t i = 0; i < n; ++i) {
@@ -1386,10 +1498,13 @@ extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uin
     if (dalloc(c, &f.mark, 2 * (size_t)np)) return TGSIM_ENOMEM;
     f.mark_cap = np;
   }
-  HIPCK(c, hipMemcpyAsync(f.mark, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, c->d.stream), "publish");
+  uint8_t* pin = nullptr;
+  rc = pin_acquire(c, c->pin_marks, pairs.size() * 4, &pin);
+  if (rc) return rc;
+  memcpy(pin, pairs.data(), pairs.size() * 4);
+  HIPCK(c, hipMemcpyAsync(f.mark, pin, pairs.size() * 4, hipMemcpyHostToDevice, c->d.stream), "publish");
   HIPCK(c, launch_flood_mark(c->d, np), "publish");
-  HIPCK(c, hipStreamSynchronize(c->d.stream), "publish");  // pairs is a pageable host buffer
-  return TGSIM_OK;
+  return pin_issued(c, c->pin_marks);
 }
 
 extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
@@ -1398,34 +1513,15 @@ extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   Flood& f = c->d.fl;
   if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  int rc = sync_and_check(c);
-  if (rc) return rc;
-  const uint32_t n = c->d.h_sc->n_out;
-  if ((size_t)n + 1 > f.cap) {
-    dfree(c, f.cnt); dfree(c, f.pos); dfree(c, f.first); dfree(c, f.scan_tmp);
-    f.cnt = f.pos = nullptr; f.first = nullptr; f.scan_tmp = nullptr;
-    const size_t cap = std::max<size_t>((size_t)n + 1, 2 * f.cap);
-    f.scan_bytes = flood_scan_bytes((uint32_t)cap);
-    uint8_t* tmp = nullptr;
-    if (dalloc(c, &f.cnt, cap) || dalloc(c, &f.pos, cap) || dalloc(c, &f.first, cap) ||
-        dalloc(c, &tmp, f.scan_bytes))
-      return TGSIM_ENOMEM;
-    f.scan_tmp = tmp;
-    f.cap = cap;
+  // asynchronous: the delivery count, the forwards and the new staged count stay on the device
+  HIPCK(c, launch_flood_react(c->d, c->staged_dev, c->n_staged, size, c->horizon), "flood react");
+  c->staged_dev = true;
+  c->win_m_inbox = f.D > 1 ? f.D - 1 : 0;  // per delivery of the sender's last inbox run
+  if (n_fwd) {  // the caller asked for the count: one synchronisation
+    const int rc = sync_and_check(c);
+    if (rc) return rc;
+    *n_fwd = c->d.h_sc->fl_total;
   }
-  uint32_t total = 0;
-  HIPCK(c, launch_flood_count(c->d, n, &total), "flood count");
-  HIPCK(c, sync_scalars(c->d), "sync");
-  rc = check_device_errors(c);
-  if (rc) return rc;
-  if ((uint64_t)c->n_staged + total > c->d.cap_msgs) return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
-  HIPCK(c, launch_flood_emit(c->d, n, c->n_staged, size, c->horizon), "flood emit");
-  c->n_staged += total;
-  // forwards of a sender <= (D - 1) per delivery of its inbox run (queue-limit test; the device
-  // reads each sender's run, the host bound takes the longest)
-  c->win_m_inbox = f.D > 1 ? f.D - 1 : 0;
-  c->inbox_max_h = c->d.h_sc->max_inbox;
-  if (n_fwd) *n_fwd = total;
   return TGSIM_OK;
 }
 

@@ -155,8 +155,11 @@ class Simulator:
         m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
         self._check(self.lib.enqueue(self._ctx, C.byref(m), n))
 
-    def advance(self, t_end: int) -> None:
-        self._check(self.lib.advance(self._ctx, int(t_end)))
+    def advance(self, t_end: int, wait: bool = True) -> None:
+        """One window [now, t_end). wait=False: tgsim_advance_async (no closing sync; device-side
+        errors surface at the next synchronising call)."""
+        fn = self.lib.advance if wait else self.lib.advance_async
+        self._check(fn(self._ctx, int(t_end)))
 
     def advance_begin(self, t_end: int) -> None:
         self._check(self.lib.advance_begin(self._ctx, int(t_end)))
@@ -394,7 +397,12 @@ class Simulator:
         tt = np.ascontiguousarray(np.broadcast_to(np.asarray(t, dtype=np.int64), inst.shape))
         self._check(self.lib.flood_publish(self._ctx, _ptr(inst), _ptr(p), _ptr(tt), len(inst), size))
 
-    def flood_react(self, size: int) -> int:
+    def flood_react(self, size: int, count: bool = True) -> int | None:
+        """Stage the forwards of the last window's first receipts. count=False keeps it
+        asynchronous (no host read; returns None)."""
+        if not count:
+            self._check(self.lib.flood_react(self._ctx, size, None))
+            return None
         n = C.c_size_t()
         self._check(self.lib.flood_react(self._ctx, size, C.byref(n)))
         return n.value

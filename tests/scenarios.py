@@ -383,13 +383,15 @@ def memmove_exchange(sims):
 
 def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4, window_ns=10 * MS, size=512,
               seed=5, degree=8, shapes=None, keep=True, on_window=None, cfg_kw=None, max_windows=2000,
-              windows=None, setup=None):
+              windows=None, setup=None, count=True):
     """Waves of publications flooding the graph; every window: advance, read the deliveries, then
     tgsim_flood_react stages the first-receipt forwards for the next window. Returns per-window
     observables (keep=True) and the totals. windows: run exactly that many windows (a sharded run
     driven through a transport, whose shards cannot see the global end condition); setup(sim)
-    attaches that transport."""
+    attaches that transport. count=False: the reaction stays asynchronous (no forward counts; give
+    `windows`)."""
     from testground_amd import workloads as W
+    assert count or windows is not None
     kw = dict(max_msgs_per_window=1 << 20, max_records=1 << 22, data_prefix_len=12)
     kw.update(cfg_kw or {})
     sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **kw), binding=binding)
@@ -408,11 +410,11 @@ def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4
         elif windows is None and fwd == 0 and sim.stats()["inflight"] == 0 and w // wave_gap_windows >= waves:
             break
         t += window_ns
-        sim.advance(t)
+        sim.advance(t, wait=count)
         d = sim.deliveries()
-        fwd = sim.flood_react(size)
+        fwd = sim.flood_react(size, count=count)
         tot["delivered"] += len(d["dst"])
-        tot["forwarded"] += fwd
+        tot["forwarded"] += fwd or 0
         if on_window is not None:
             on_window(w, d, fwd)
         if keep:

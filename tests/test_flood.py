@@ -127,6 +127,18 @@ def test_flood_hip_matches_oracle(hip, oracle, n, kind):
 
 
 @pytest.mark.gpu
+def test_flood_async_reaction_matches_oracle(hip, oracle):
+    """tgsim_flood_react without a forward count runs with no host read: the delivery count, the
+    staged count and the forwards stay on the device, and the next wave's publish appends behind
+    them. Deliveries, statuses and inboxes equal the oracle's window by window."""
+    n = 3000
+    a = S.run_flood(hip, n_inst=n, windows=70, count=False)
+    b = S.run_flood(oracle, n_inst=n, windows=70, count=False)
+    S.assert_same(a, b)
+    assert a[-1]["tot"]["delivered"] > 20 * n
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_flood_full_size(hip, oracle):
     """config 5 at full size: 1M instances, 8-regular, heterogeneous shapes; two publications, the
