@@ -1844,7 +1844,7 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
   // reservation per queue for the whole block
   const int64_t t_end = sc->t_end;
   int code[kIPT];
-  uint32_t nD = 0, nL = 0, nX = 0;
+  uint32_t nX = 0;
 #pragma unroll
   for (int u = 0; u < kIPT; ++u) {
     code[u] = -1;
@@ -1852,20 +1852,41 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     rec[u].t = (int64_t)sm.k1[slot[u]];
     rec[u].meta |= TGSIM_F_STAGE_D;
     code[u] = qid_stage_d(p.geo, rec[u].dst, rec[u].t, t_end);
-    nD += code[u] == Q_D; nL += code[u] == Q_L; nX += code[u] >= Q_X0;
+    nX += code[u] >= Q_X0;
     if ((rec[u].meta & TGSIM_F_WHEEL) && code[u] != Q_L) {  // leaves its sender's queue now
       rec[u].meta &= ~(uint32_t)TGSIM_F_WHEEL;
       atomicAdd(&dec[sm.key[slot[u]]], 1u);
     }
   }
+  // staging slots in (wave, item u, lane) order: one ballot per (u, queue), so the lanes of every
+  // staging store hold consecutive records (slots contiguous per thread put the 32-B records of
+  // neighbouring lanes ~128 B apart: 8-way LDS bank conflicts)
+  uint64_t mD[kIPT], mL[kIPT];
+  uint32_t wD = 0, wL = 0;
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    mD[u] = __ballot(code[u] == Q_D);
+    mL[u] = __ballot(code[u] == Q_L);
+    wD += (uint32_t)__popcll(mD[u]);
+    wL += (uint32_t)__popcll(mL[u]);
+  }
+  const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) sm.flag = 0;
+  if ((threadIdx.x & 63) == 0) { sm.part[wave] = wD; sm.part[kBlock / 64 + wave] = wL; }
   __syncthreads();
   // this workgroup owns its senders' counters for the launch (long runs: k_rest, later)
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock)
     if (dec[i]) p.pend[h.k0 + i] -= dec[i];
   if (nX) sm.flag = 1;
-  uint32_t tD, tL;
-  block_scan2(nD, nL, sm.part, tD, tL);  // nD/nL: this thread's offsets inside the block's runs
+  uint32_t tD = 0, tL = 0, bD = 0, bL = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    const uint32_t a = sm.part[w], c = sm.part[kBlock / 64 + w];
+    bD += w < wave ? a : 0u;
+    bL += w < wave ? c : 0u;
+    tD += a;
+    tL += c;
+  }
   const Queues& Q = p.Q;
   const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
   __syncthreads();  // every thread has read the scan partials in sm.part (and k1 for the last time)
@@ -1879,11 +1900,14 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
   uint4* st = reinterpret_cast<uint4*>(sm.k1);
   const uint32_t nst = tD + tL;
   for (uint32_t r0 = 0; r0 < nst; r0 += kStageN) {
-    uint32_t cD = nD, cL = tD + nL;
+    uint32_t cD = bD, cL = tD + bL;
 #pragma unroll
     for (int u = 0; u < kIPT; ++u) {
+      const uint32_t qD = cD + mask_rank(mD[u]), qL = cL + mask_rank(mL[u]);
+      cD += (uint32_t)__popcll(mD[u]);
+      cL += (uint32_t)__popcll(mL[u]);
       if (code[u] != Q_D && code[u] != Q_L) continue;
-      const uint32_t q = code[u] == Q_D ? cD++ : cL++;
+      const uint32_t q = code[u] == Q_D ? qD : qL;
       if (q < r0 || q >= r0 + kStageN) continue;
       const uint32_t i = q - r0;
       st[2 * i] = make_uint4((uint32_t)rec[u].t, (uint32_t)((uint64_t)rec[u].t >> 32), rec[u].src, rec[u].dst);
