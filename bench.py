@@ -166,7 +166,10 @@ def parse():
     p.add_argument("--workload", choices=("storm", "flood"), default="storm")
     p.add_argument("--flood-instances", type=int, default=1_000_000)
     p.add_argument("--flood-size", type=int, default=512)
-    p.add_argument("--pub-every", type=int, default=4, help="windows between publications (flood)")
+    p.add_argument("--pub-every", type=int, default=4, help="windows between publication waves (flood)")
+    p.add_argument("--pubs-per-wave", type=int, default=1,
+                   help="publications per wave (flood; distinct publishers; SURVEY's literal 1%% of 1M "
+                        "instances = 10000 floods per wave does not fit in memory: DESIGN.md 5.4)")
     p.add_argument("--window-ms", type=float, default=10.0, help="window length (flood)")
     a = p.parse_args()
     if a.workload == "flood":
@@ -406,8 +409,8 @@ def flood_cpu_baseline(args, shapes, graph):
     w = 0
     while True:
         if w % args.pub_every == 0:
-            sim.flood_publish(W.publishers(N, 1, w // args.pub_every, args.seed), [w // args.pub_every], sim.now,
-                              args.flood_size)
+            k, P = w // args.pub_every, args.pubs_per_wave
+            sim.flood_publish(W.publishers(N, P, k, args.seed), np.arange(P) + k * P, sim.now, args.flood_size)
         sim.advance(sim.now + win)
         sim.flood_react(args.flood_size, count=False)
         w += 1
@@ -424,12 +427,13 @@ def flood_cpu_baseline(args, shapes, graph):
 def flood_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
     return SimConfig(n_instances=args.flood_instances, seed=args.seed, shard_id=shard, n_shards=n_shards,
-                     device=device, data_prefix_len=11, max_msgs_per_window=1 << 23, max_records=1 << 25,
+                     device=device, data_prefix_len=11, max_msgs_per_window=(1 << 23) * args.pubs_per_wave,
+                     max_records=(1 << 25) * args.pubs_per_wave,
                      exchange_cap=exchange_cap(3 << 20, n_shards))
 
 
 def flood_max_pubs(args) -> int:
-    return (args.warmup + args.steps + 20) // args.pub_every + 2
+    return ((args.warmup + args.steps + 20) // args.pub_every + 2) * args.pubs_per_wave
 
 
 def main_flood(args):
@@ -453,8 +457,8 @@ def main_flood(args):
 
     def step(w: int):
         if w % args.pub_every == 0:
-            k = w // args.pub_every
-            sim.flood_publish(W.publishers(N, 1, k, args.seed), [k], sim.now, args.flood_size)
+            k, P = w // args.pub_every, args.pubs_per_wave
+            sim.flood_publish(W.publishers(N, P, k, args.seed), np.arange(P) + k * P, sim.now, args.flood_size)
         sim.advance(sim.now + win, wait=False)  # sharded: collective, the exchange inside; no host sync
         sim.flood_react(args.flood_size, count=False)
 
@@ -510,8 +514,10 @@ def main_flood(args):
             "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": "pubsub flood (SURVEY.md 8(d) config 5): 1M instances, random 8-regular graph, "
                                    "first-receipt dedup, latency {10,50,100,200} ms, jitter U[0,20] ms, loss "
-                                   "{0,0.1,1}%, bandwidth {1,10,100} Mbit/s; one publication every "
-                                   f"{args.pub_every} windows of {args.window_ms} ms",
+                                   "{0,0.1,1}%, bandwidth {1,10,100} Mbit/s; "
+                                   f"{args.pubs_per_wave} publication(s) every {args.pub_every} windows of "
+                                   f"{args.window_ms} ms",
+                       "pubs_per_wave": args.pubs_per_wave,
                        "instances": N, "msg_bytes": args.flood_size,
                        "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else
                                                          ("-rccl" if world > 1 else "")),
