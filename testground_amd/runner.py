@@ -10,9 +10,16 @@ restatement drives the identical C ABI through ctypes and is what the tests exer
 Instances are simulated: the group's artifact is not executed; the (plan, case) pair selects a
 workload descriptor from :data:`testground_amd.plans.PLANS`. Instance ids are assigned group by
 group in composition order (the order ``local_exec.go:108-160`` starts them in).
+
+Outcomes travel as the instances' runtime events (sdk-go ``runtime.Event`` [EXT]: StartEvent,
+SuccessEvent{TestGroupID}, FailureEvent{TestGroupID, Error}, stamped with the simulated time), and
+the result is counted from them exactly as ``LocalDockerRunner.collectOutcomes`` does
+(``local_docker.go:216-255``). :class:`PrettyPrinter` renders the same stream the way
+``pkg/runner/pretty.go:113-232`` renders an instance's stdout.
 """
 from __future__ import annotations
 
+import enum
 import io
 import json
 import os
@@ -39,6 +46,97 @@ def next_data_network(n_networks: int):
     return net, net.ip | 1
 
 
+class EventType(enum.IntEnum):
+    """pretty.go:21-33, in its order (the printer's classes index by it)."""
+    Error = 0
+    Start = 1
+    Ok = 2
+    Fail = 3
+    Crash = 4
+    Incomplete = 5
+    Message = 6
+    Metric = 7
+    Other = 8
+    InternalErr = 9
+
+
+_CLASS = ["ERROR", "START", "OK", "FAIL", "CRASH", "INCOMPLETE", "MESSAGE", "METRIC", "OTHER", "INTERNAL_ERR"]
+
+
+def start_event(group: str, runenv: dict) -> dict:
+    return {"StartEvent": {"Runenv": {**runenv, "TestGroupID": group}}}
+
+
+def success_event(group: str) -> dict:
+    return {"SuccessEvent": {"TestGroupID": group}}
+
+
+def failure_event(group: str, error: str) -> dict:
+    return {"FailureEvent": {"TestGroupID": group, "Error": error}}
+
+
+def collect_outcomes(events, result: "Result") -> None:
+    """local_docker.go:216-255: count SuccessEvent per group; FailureEvent and CrashEvent count as
+    reported but not ok; stop once every instance has reported; then update the outcome."""
+    expecting = sum(g.total for g in result.outcomes.values())
+    for e in events:
+        if expecting <= 0:
+            break
+        ev = e["event"]
+        if "SuccessEvent" in ev:
+            result.outcomes[ev["SuccessEvent"]["TestGroupID"]].ok += 1
+            expecting -= 1
+        elif "FailureEvent" in ev or "CrashEvent" in ev:
+            expecting -= 1
+    result.update_outcome()
+
+
+class PrettyPrinter:
+    """pretty.go:39-232 for simulated instances: one line per event, ``%5.4fs %10s << id >> msg``
+    with the elapsed time measured from the run's start (here: simulated time); an instance that
+    ends without a success or failure event is INCOMPLETE; wait() reports "N nodes failed"."""
+
+    def __init__(self, ow):
+        self.ow = ow
+        self.failed = 0
+        self.count = 0
+
+    def manage(self, instance_id: str, events) -> None:
+        """processStdout for one instance (pretty.go:113-182)."""
+        self.count += 1
+        ok = failed = False
+        for e in events:
+            ev, ts = e["event"], e["ts"]
+            if "SuccessEvent" in ev:
+                ok = True
+                self._print(instance_id, ts, EventType.Ok, "")
+            elif "FailureEvent" in ev:
+                failed = True
+                self._print(instance_id, ts, EventType.Fail, ev["FailureEvent"]["Error"])
+            elif "CrashEvent" in ev:
+                failed = True
+                self._print(instance_id, ts, EventType.Crash, ev["CrashEvent"]["Error"])
+            elif "MessageEvent" in ev:
+                self._print(instance_id, ts, EventType.Message, ev["MessageEvent"]["Message"])
+            elif "StartEvent" in ev:
+                self._print(instance_id, ts, EventType.Start, json.dumps(ev["StartEvent"]["Runenv"], sort_keys=True))
+            else:
+                self._print(instance_id, ts, EventType.InternalErr, f"unknown event: {ev}")
+                return
+        if not ok and not failed:
+            self._print(instance_id, None, EventType.Incomplete, "")
+        if not ok or failed:
+            self.failed += 1
+
+    def wait(self):
+        """pretty.go:82-94: an error message if any instance failed, else None."""
+        return f"{self.failed} nodes failed" if self.failed else None
+
+    def _print(self, instance_id: str, ts_ns, et: EventType, msg: str) -> None:
+        elapsed = max(0, ts_ns or 0) / 1e9
+        self.ow.write(f"{elapsed:5.4f}s {_CLASS[et]:>10s} << {instance_id} >> {msg}\n")
+
+
 @dataclass
 class LocalMI355XRunnerConfig:
     """Coalesced from .env.toml [runners."local:mi355x"] and the composition's [global.run_config]
@@ -49,6 +147,7 @@ class LocalMI355XRunnerConfig:
     max_msgs_per_window: int = 1 << 18
     max_records: int = 1 << 20
     outputs_dir: str = ""
+    pretty: bool = True          # print every instance's events (pretty.go) when an output writer is given
 
 
 @dataclass
@@ -150,18 +249,38 @@ class LocalMI355XRunner:
         finally:
             env.close()
             self._active -= 1
-        base = 0
-        for g in job.groups:
-            result.outcomes[g.id].ok = int(ok[base:base + g.instances].sum())
-            base += g.instances
-        result.update_outcome()
+        events = self._events(job, ok, sim_now, failures)
+        collect_outcomes((e for per in events for e in per[1]), result)
         result.journal["failures"] = failures
         result.journal["events"] = {"simulated_ns": str(sim_now), "wall_s": f"{time.perf_counter() - t0:.3f}"}
         self._outputs[job.run_id] = {"run_id": job.run_id, "plan": job.test_plan, "case": job.test_case,
                                      "result": _jsonable(asdict(result)), "stats": stats}
         if ow is not None:
+            if cfg.pretty:
+                pp = PrettyPrinter(ow)
+                for iid, evs in events:
+                    pp.manage(iid, evs)
+                err = pp.wait()
+                if err:
+                    ow.write(f"{err}\n")
             ow.write(f"local:mi355x run {job.run_id}: {result.outcome}\n")
         return RunOutput(run_id=job.run_id, result=result)
+
+    @staticmethod
+    def _events(job: RunInput, ok, t_end: int, failures: list) -> list:
+        """Each simulated instance's runtime events: StartEvent at time 0, then SuccessEvent or
+        FailureEvent at the plan's end (the instance's id is <group>[<index in group>])."""
+        out, base = [], 0
+        err = failures[0] if failures else "the instance did not complete the test case"
+        for g in job.groups:
+            runenv = {"TestPlan": job.test_plan, "TestCase": job.test_case, "TestRun": job.run_id,
+                      "TestInstanceCount": job.total_instances, "TestGroupInstanceCount": g.instances}
+            for i in range(g.instances):
+                done = success_event(g.id) if ok[base + i] else failure_event(g.id, err)
+                out.append((f"{g.id}[{i}]", [{"ts": 0, "event": start_event(g.id, runenv)},
+                                             {"ts": int(t_end), "event": done}]))
+            base += g.instances
+        return out
 
     def collect_outputs(self, run_id: str, w) -> None:
         """Writes a tar.gz with the run's result and counters (CollectOutputs, runner.go:31-33)."""

@@ -175,8 +175,35 @@ def test_runner_contract(oracle):
 def test_runner_reports_failures(oracle, monkeypatch):
     r = LocalMI355XRunner(binding=oracle)
     monkeypatch.setitem(P.PLANS, ("x", "y"), lambda env: np.arange(env.n) % 2 == 0)
-    out = r.run(RunInput("r2", "x", "y", 4, [RunGroup("g", 4)]))
+    ow = io.StringIO()
+    out = r.run(RunInput("r2", "x", "y", 4, [RunGroup("g", 4)]), ow)
     assert out.result.outcome == "failure" and out.result.outcomes["g"].ok == 2
+    lines = ow.getvalue().splitlines()
+    # pretty.go: START and an outcome per instance, then the printer's "N nodes failed"
+    assert sum(" START " in x for x in lines) == 4 and sum("     OK << g[" in x for x in lines) == 2
+    assert [x.split("<< ")[1].split(" >>")[0] for x in lines if "  FAIL << " in x] == ["g[1]", "g[3]"]
+    assert "2 nodes failed" in lines and lines[-1] == "local:mi355x run r2: failure"
+
+
+def test_runner_event_stream_and_printer():
+    """collectOutcomes counts SuccessEvents per group and stops after every instance reported
+    (local_docker.go:216-255); an instance with no outcome event is INCOMPLETE (pretty.go:127-135)."""
+    from testground_amd.runner import (GroupOutcome, PrettyPrinter, Result, collect_outcomes, failure_event,
+                                       start_event, success_event)
+    res = Result(outcomes={"a": GroupOutcome(total=2), "b": GroupOutcome(total=1)})
+    evs = [{"ts": 0, "event": start_event("a", {})}, {"ts": 5, "event": success_event("a")},
+           {"ts": 6, "event": failure_event("b", "boom")}, {"ts": 7, "event": success_event("a")},
+           {"ts": 8, "event": success_event("b")}]   # after every instance reported: not counted
+    collect_outcomes(evs, res)
+    assert (res.outcomes["a"].ok, res.outcomes["b"].ok, res.outcome) == (2, 0, "failure")
+    ow = io.StringIO()
+    pp = PrettyPrinter(ow)
+    pp.manage("x[0]", [{"ts": 1_500_000_000, "event": start_event("x", {"TestPlan": "p"})}])
+    pp.manage("x[1]", [{"ts": 2_000_000_000, "event": success_event("x")}])
+    out = ow.getvalue().splitlines()
+    assert out[0] == '1.5000s      START << x[0] >> {"TestGroupID": "x", "TestPlan": "p"}'
+    assert out[1] == "0.0000s INCOMPLETE << x[0] >> " and out[2] == "2.0000s         OK << x[1] >> "
+    assert pp.wait() == "1 nodes failed"
 
 
 def test_runner_rejects_unknown_plan(oracle):
