@@ -381,6 +381,48 @@ int tgsim_flood_publish(tgsim_ctx* ctx, const uint32_t* instances, const uint32_
                         size_t n, uint32_t size);
 int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
 
+/* ---- TCP-level mode ----------------------------------
+ * The reference plans move application data over TCP (plans/benchmarks/storm.go:127-180 dials and
+ * writes in chunks, plans/network/pingpong.go:73-104 times round trips over a connection); with loss
+ * the message-level model undercounts what the receiver sees. In TCP mode an application write
+ * (tgsim_tcp_send) becomes ceil(size / mss) segments, each a packet of payload + header_bytes on
+ * the wire through the unchanged netem / HTB / FIB path. A segment's attempt fails when none of its
+ * copies enters the egress queue, or every copy that does arrives corrupted (the TCP checksum drops
+ * it); attempt a + 1 is then sent at max(t_a + rto * 2^a, the time the failure is known), up to
+ * max_attempts attempts (then the write fails). A route that refuses the packet (prohibit / no
+ * route) fails the write at once. A segment arrives with its first intact copy; a write completes
+ * when its last segment arrives. Not modelled: ACK packets on the reverse path, congestion window,
+ * fast retransmit, spurious timeouts (a copy slower than the RTO is waited for). Single-shard
+ * contexts; while TCP mode is on, all traffic is TCP (tgsim_enqueue is refused). Packet seq =
+ * segment id * 16 + attempt (segment ids count from 0 in send order, < 2^28). */
+typedef struct tgsim_tcp_config {
+  uint32_t mss;           /* payload bytes per segment; 0 = 1448 */
+  uint32_t header_bytes;  /* wire overhead per segment (IPv4 + TCP with timestamps); 0 = 52 */
+  int64_t rto_ns;         /* first retransmission timeout; 0 = 200 ms (Linux TCP_RTO_MIN) */
+  uint32_t max_attempts;  /* attempts per segment, 1..16; 0 = 16 */
+  uint32_t reserved;
+  uint64_t max_writes;    /* write-table capacity over the run; 0 = 2^22 */
+  uint64_t max_segments;  /* segment-table capacity over the run; 0 = 2^24 */
+} tgsim_tcp_config;
+
+enum { TGSIM_TCP_PENDING = 0, TGSIM_TCP_DELIVERED = 1, TGSIM_TCP_TIMEOUT = 2, TGSIM_TCP_REFUSED = 3 };
+
+typedef struct tgsim_tcp_stats {
+  uint64_t writes, segments, packets, retransmissions, delivered, failed, pending_retx;
+} tgsim_tcp_stats;
+
+int tgsim_tcp_enable(tgsim_ctx* ctx, const tgsim_tcp_config* cfg);
+/* Application writes (src, dst, seq = the write's order key on its connection, size, t_send), staged
+ * like tgsim_enqueue (t_send >= tgsim_horizon). Write ids count from 0 in send order. */
+int tgsim_tcp_send(tgsim_ctx* ctx, const tgsim_msg_soa* writes, size_t n);
+/* After every window, before staging for the next: account the window's packets (queued copies) and
+ * deliveries (arrivals, corrupt copies), schedule retransmissions (staged by the window that covers
+ * their time), complete writes. *n_completed = writes delivered or failed in this call (may be NULL). */
+int tgsim_tcp_react(tgsim_ctx* ctx, size_t* n_completed);
+/* Per write id: state TGSIM_TCP_* and time (arrival of its last segment, or the failure time). */
+int tgsim_tcp_writes(tgsim_ctx* ctx, uint8_t* state_out, int64_t* t_out, size_t cap, size_t* n);
+int tgsim_tcp_get_stats(tgsim_ctx* ctx, tgsim_tcp_stats* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -214,8 +214,21 @@ struct tgo_ctx {
   /* cross-shard transport (tgsim_set_transport): host buffers, stream NULL */
   tgsim_transport tr;
   int has_tr, replicated_batch;
+  /* TCP mode: writes, segments, segments with a retransmission scheduled */
+  int tcp_on, tcp_need_react;
+  tgsim_tcp_config tcp;
+  struct otcpw* tw; size_t tw_n, tw_cap;
+  struct otcps* tsg; size_t tsg_n, tsg_cap;
+  uint32_t* tpend; size_t tpend_n, tpend_cap;
+  tgsim_tcp_stats tstats;
   char err[512];
 };
+
+typedef struct otcpw { uint32_t src, dst, remaining, state; int64_t t; } otcpw;
+typedef struct otcps {
+  uint32_t w, wire, attempt, outstanding, arrived, touched;
+  int64_t t_att, arrival, t_last;
+} otcps;
 
 static int fail(tgo_ctx* c, int code, const char* fmt, ...) {
   if (c) { va_list ap; va_start(ap, fmt); vsnprintf(c->err, sizeof(c->err), fmt, ap); va_end(ap); }
@@ -325,6 +338,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
+  free(c->tw); free(c->tsg); free(c->tpend);
   free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
     free(c->topics[i].inst); free(c->topics[i].t); free(c->topics[i].off); free(c->topics[i].len);
@@ -513,7 +527,12 @@ int tgo_get_ip(const tgo_ctx* c, uint32_t g, uint32_t* ip) {
 
 /* ============================== data path =================================================== */
 
+static int enqueue_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n);
 int tgo_enqueue(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tcp_send");
+  return enqueue_impl(c, m, n);
+}
+static int enqueue_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   omsgs* s = &c->staged;
   size_t need = s->n + n;
@@ -809,9 +828,15 @@ static int sender_window(tgo_ctx* c, const size_t* ord, size_t a, size_t b, cons
   return 0;
 }
 
+static int tcp_release(tgo_ctx* c, int64_t t_end);
 int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  if (c->tcp_on) {
+    if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
+    int rc = tcp_release(c, t_end);
+    if (rc) return rc;
+  }
   omsgs* s = &c->staged;
   for (size_t i = 0; i < s->n; ++i)
     if (s->t[i] >= t_end) return fail(c, TGSIM_ECAUSALITY, "staged message %zu sent at/after t_end", i);
@@ -901,6 +926,7 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
   }
   c->in_window = 1;
+  c->tcp_need_react = c->tcp_on;
   return TGSIM_OK;
 }
 
@@ -1362,5 +1388,232 @@ int tgo_sync_subscribe(tgo_ctx* c, uint32_t topic, uint32_t from, int64_t until_
     b += tp->len[p];
   }
   if (off_out) off_out[k] = b;
+  return TGSIM_OK;
+}
+
+/* ============================== TCP mode ==================================== */
+/* Segmentation and loss recovery over the per-packet path: plans/benchmarks/storm.go:127-180 writes
+ * `size` bytes over a dialled connection, plans/network/pingpong.go:73-104 times round trips on one.
+ * A segment's attempt fails when no copy enters the egress queue (the status of its packet) or when
+ * every queued copy arrives corrupted; the next attempt leaves at max(t_a + rto * 2^a, the time the
+ * failure is known) [EXT Linux tcp_retransmit_timer: exponential backoff from TCP_RTO_MIN]. */
+
+int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
+  if (!cfg) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
+  if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
+  if (c->staged.n) return fail(c, TGSIM_ESTATE, "messages already staged");
+  tgsim_tcp_config t = *cfg;
+  if (!t.mss) t.mss = 1448;
+  if (!t.header_bytes) t.header_bytes = 52;
+  if (!t.rto_ns) t.rto_ns = 200000000;
+  if (!t.max_attempts) t.max_attempts = 16;
+  if (!t.max_writes) t.max_writes = 1u << 22;
+  if (!t.max_segments) t.max_segments = 1u << 24;
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28))
+    return fail(c, TGSIM_EINVAL, "bad TCP configuration");
+  c->tcp = t;
+  c->tcp_on = 1;
+  return TGSIM_OK;
+}
+
+int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  size_t nseg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (m->src[i] >= c->N || m->dst[i] >= c->N) return fail(c, TGSIM_EINVAL, "write %zu: bad instance id", i);
+    if (m->t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
+    if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
+    nseg += m->size[i] ? (m->size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
+  }
+  if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + nseg > c->tcp.max_segments)
+    return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  if (grow((void**)&c->tw, &c->tw_cap, c->tw_n + n + 1, sizeof(otcpw)) ||
+      grow((void**)&c->tsg, &c->tsg_cap, c->tsg_n + nseg + 1, sizeof(otcps)))
+    return fail(c, TGSIM_ENOMEM, "oom");
+  uint32_t* src = malloc((nseg + 1) * 4); uint32_t* dst = malloc((nseg + 1) * 4);
+  uint32_t* seq = malloc((nseg + 1) * 4); uint32_t* sz = malloc((nseg + 1) * 4);
+  int64_t* ts = malloc((nseg + 1) * 8);
+  if (!src || !dst || !seq || !sz || !ts) { free(src); free(dst); free(seq); free(sz); free(ts); return TGSIM_ENOMEM; }
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t size = m->size[i], ns = size ? (size + c->tcp.mss - 1) / c->tcp.mss : 1;
+    otcpw w = {m->src[i], m->dst[i], ns, TGSIM_TCP_PENDING, INT64_MIN};
+    const uint32_t wi = (uint32_t)c->tw_n++;
+    c->tw[wi] = w;
+    for (uint32_t j = 0; j < ns; ++j, ++k) {
+      const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
+      const uint32_t sid = (uint32_t)c->tsg_n++;
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN};
+      c->tsg[sid] = g;
+      src[k] = w.src; dst[k] = w.dst; seq[k] = sid << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
+    }
+  }
+  tgsim_msg_soa p = {src, dst, seq, sz, ts};
+  int rc = enqueue_impl(c, &p, k);
+  free(src); free(dst); free(seq); free(sz); free(ts);
+  if (rc) return rc;
+  c->tstats.writes += n;
+  c->tstats.segments += k;
+  c->tstats.packets += k;
+  return TGSIM_OK;
+}
+
+/* A write ends once: delivered (its last segment arrived) or failed. A failed write keeps its
+ * earliest failure, refusal before timeout at equal times (key t * 2 + (timeout ? 1 : 0)), so the
+ * outcome does not depend on the order the failures are found in. */
+static void tcp_finish(tgo_ctx* c, uint32_t wi, uint32_t state, int64_t t, size_t* done) {
+  otcpw* w = &c->tw[wi];
+  if (w->state == TGSIM_TCP_DELIVERED) return;
+  if (w->state != TGSIM_TCP_PENDING) {  /* already failed: keep the earlier failure */
+    const int64_t k_old = w->t * 2 + (w->state == TGSIM_TCP_TIMEOUT), k_new = t * 2 + (state == TGSIM_TCP_TIMEOUT);
+    if (state != TGSIM_TCP_DELIVERED && k_new < k_old) { w->state = state; w->t = t; }
+    return;
+  }
+  w->state = state;
+  w->t = t;
+  ++*done;
+  if (state == TGSIM_TCP_DELIVERED) c->tstats.delivered++; else c->tstats.failed++;
+}
+
+/* attempt g->attempt failed; the failure is known at t_known. A segment of a write that has
+ * already failed is still scheduled (and dropped at release), so scheduling is order-independent. */
+static int tcp_schedule(tgo_ctx* c, uint32_t sid, int64_t t_known, size_t* done) {
+  otcps* g = &c->tsg[sid];
+  int64_t t = g->t_att + (c->tcp.rto_ns << g->attempt);
+  if (t < t_known) t = t_known;
+  if (g->attempt + 1 >= c->tcp.max_attempts) { tcp_finish(c, g->w, TGSIM_TCP_TIMEOUT, t, done); return TGSIM_OK; }
+  g->attempt++;
+  g->t_att = t;
+  g->t_last = INT64_MIN;
+  if (grow((void**)&c->tpend, &c->tpend_cap, c->tpend_n + 1, 4)) return TGSIM_ENOMEM;
+  c->tpend[c->tpend_n++] = sid;
+  c->tstats.retransmissions++;
+  return TGSIM_OK;
+}
+
+/* copies of a packet that entered its egress queue, from its status (tgsim.h status flags) */
+static uint32_t tcp_copies(uint8_t st) {
+  const uint8_t code = st & 0x0Fu;
+  if (code == TGSIM_ST_LOCAL) return 1;
+  if (code != TGSIM_ST_QUEUED) return 0;
+  uint32_t q = (st & TGSIM_ST_FLAG_OVERLIMIT) ? 0u : 1u;
+  if ((st & TGSIM_ST_FLAG_DUP) && !(st & TGSIM_ST_FLAG_CLONE_LOST)) ++q;
+  return q;
+}
+
+int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
+  size_t done = 0;
+  if (n_done) *n_done = 0;
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->tcp_need_react) return TGSIM_OK;
+  /* 1. the window's packets (staged arrays are intact until the next staging) */
+  const omsgs* s = &c->staged;
+  for (size_t i = 0; i < c->n_status; ++i) {
+    const uint32_t sid = s->seq[i] >> 4;
+    otcps* g = &c->tsg[sid];
+    const uint32_t q = tcp_copies(c->status[i]);
+    if (q) { g->outstanding += q; continue; }
+    const uint8_t code = c->status[i] & 0x0Fu;
+    if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, &done);
+    else if (tcp_schedule(c, sid, g->t_att, &done)) return fail(c, TGSIM_ENOMEM, "oom");
+  }
+  /* 2. the window's deliveries: first intact arrival, copies accounted */
+  uint32_t* touched = (uint32_t*)malloc((c->out.n + 1) * 4);
+  if (!touched) return fail(c, TGSIM_ENOMEM, "oom");
+  size_t nt = 0;
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    const uint32_t sid = r->seq >> 4;
+    otcps* g = &c->tsg[sid];
+    if (!(r->meta & TGSIM_F_CORRUPT) && r->t < g->arrival) g->arrival = r->t;
+    if (r->t > g->t_last) g->t_last = r->t;
+    g->outstanding--;
+    if (!g->touched) { g->touched = 1; touched[nt++] = sid; }
+  }
+  int rc = 0;
+  for (size_t k = 0; k < nt && !rc; ++k) {
+    otcps* g = &c->tsg[touched[k]];
+    g->touched = 0;
+    if (g->arrived) continue;
+    if (g->arrival != INT64_MAX) {
+      g->arrived = 1;
+      otcpw* w = &c->tw[g->w];
+      if (g->arrival > w->t && w->state == TGSIM_TCP_PENDING) w->t = g->arrival;
+      if (--w->remaining == 0) tcp_finish(c, g->w, TGSIM_TCP_DELIVERED, w->t, &done);
+    } else if (g->outstanding == 0) {
+      rc = tcp_schedule(c, touched[k], g->t_last, &done);
+    }
+  }
+  free(touched);
+  if (rc) return fail(c, TGSIM_ENOMEM, "oom");
+  c->tcp_need_react = 0;
+  c->tstats.pending_retx = c->tpend_n;
+  if (n_done) *n_done = done;
+  return TGSIM_OK;
+}
+
+typedef struct { int64_t t; uint32_t sid; } otx;
+static int cmp_otx(const void* a, const void* b) {
+  const otx* x = (const otx*)a; const otx* y = (const otx*)b;
+  if (x->t != y->t) return x->t < y->t ? -1 : 1;
+  return x->sid < y->sid ? -1 : (x->sid > y->sid);
+}
+
+/* Stage the retransmissions whose time falls before t_end, in (time, segment) order; those of a
+ * failed write are dropped. */
+static int tcp_release(tgo_ctx* c, int64_t t_end) {
+  if (!c->tpend_n) return TGSIM_OK;
+  otx* due = (otx*)malloc(c->tpend_n * sizeof(otx));
+  if (!due) return fail(c, TGSIM_ENOMEM, "oom");
+  size_t nd = 0, keep = 0;
+  for (size_t i = 0; i < c->tpend_n; ++i) {
+    const uint32_t sid = c->tpend[i];
+    const otcps* g = &c->tsg[sid];
+    if (c->tw[g->w].state != TGSIM_TCP_PENDING) continue;
+    if (g->t_att < t_end) { due[nd].t = g->t_att; due[nd].sid = sid; ++nd; }
+    else c->tpend[keep++] = sid;
+  }
+  c->tpend_n = keep;
+  c->tstats.pending_retx = keep;
+  int rc = TGSIM_OK;
+  if (nd) {
+    qsort(due, nd, sizeof(otx), cmp_otx);
+    uint32_t* src = malloc(nd * 4); uint32_t* dst = malloc(nd * 4); uint32_t* seq = malloc(nd * 4);
+    uint32_t* sz = malloc(nd * 4); int64_t* ts = malloc(nd * 8);
+    if (!src || !dst || !seq || !sz || !ts) rc = TGSIM_ENOMEM;
+    for (size_t i = 0; i < nd && !rc; ++i) {
+      const otcps* g = &c->tsg[due[i].sid];
+      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (due[i].sid << 4) | g->attempt;
+      sz[i] = g->wire; ts[i] = g->t_att;
+    }
+    if (!rc) {
+      tgsim_msg_soa p = {src, dst, seq, sz, ts};
+      rc = enqueue_impl(c, &p, nd);
+      c->tstats.packets += nd;
+    }
+    free(src); free(dst); free(seq); free(sz); free(ts);
+  }
+  free(due);
+  return rc;
+}
+
+int tgo_tcp_writes(tgo_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n) {
+  if (!n) return TGSIM_EINVAL;
+  *n = c->tw_n;
+  if (c->tw_n > cap) return fail(c, TGSIM_ECAPACITY, "write capacity");
+  for (size_t i = 0; i < c->tw_n; ++i) {
+    if (state) state[i] = (uint8_t)c->tw[i].state;
+    if (t) t[i] = c->tw[i].state == TGSIM_TCP_PENDING ? INT64_MIN : c->tw[i].t;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_tcp_get_stats(tgo_ctx* c, tgsim_tcp_stats* out) {
+  if (!out) return TGSIM_EINVAL;
+  *out = c->tstats;
   return TGSIM_OK;
 }

@@ -83,6 +83,20 @@ class Stats(C.Structure):
                                           "inflight", "tb_items", "extracted", "inserted", "overlimit")]
 
 
+class TcpConfig(C.Structure):
+    _fields_ = [("mss", C.c_uint32), ("header_bytes", C.c_uint32), ("rto_ns", C.c_int64),
+                ("max_attempts", C.c_uint32), ("reserved", C.c_uint32), ("max_writes", C.c_uint64),
+                ("max_segments", C.c_uint64)]
+
+
+class TcpStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("writes", "segments", "packets", "retransmissions", "delivered",
+                                          "failed", "pending_retx")]
+
+
+TCP_PENDING, TCP_DELIVERED, TCP_TIMEOUT, TCP_REFUSED = 0, 1, 2, 3
+
+
 # tgsim_transport (include/tgsim.h): caller-supplied cross-shard operations
 ALLTOALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
@@ -140,6 +154,11 @@ _SIGS = {
     "flood_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]),
     "flood_react": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_size_t)]),
     "set_transport": (C.c_int, [P, C.POINTER(Transport)]),
+    "tcp_enable": (C.c_int, [P, C.POINTER(TcpConfig)]),
+    "tcp_send": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
+    "tcp_react": (C.c_int, [P, C.POINTER(C.c_size_t)]),
+    "tcp_writes": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "tcp_get_stats": (C.c_int, [P, C.POINTER(TcpStats)]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {

@@ -51,6 +51,29 @@ struct TopicIndex {
   uint32_t n_topics = 0;
 };
 
+// TCP mode (tgsim_tcp_*): write and segment tables, two lists of segments with a
+// retransmission scheduled (the current one is released at the next window start, survivors move
+// to the other), and counters.
+struct TcpScalars {
+  uint32_t pend_n[2];             // entries of the two pending lists
+  uint32_t done;                  // writes finished by the running reaction
+  uint32_t pad;
+  unsigned long long retx, delivered, failed, released;
+};
+struct TcpDev {
+  uint32_t *w_src = nullptr, *w_dst = nullptr, *w_rem = nullptr, *w_state = nullptr;
+  int64_t* w_tarr = nullptr;      // latest segment arrival (atomicMax)
+  int64_t* w_fail = nullptr;      // earliest failure key t * 2 + (timeout ? 1 : 0) (atomicMin)
+  uint32_t *s_w = nullptr, *s_wire = nullptr, *s_att = nullptr, *s_out = nullptr, *s_flags = nullptr,
+           *s_mark = nullptr;
+  int64_t *s_tatt = nullptr, *s_arr = nullptr, *s_tlast = nullptr;
+  uint32_t* pend[2] = {nullptr, nullptr};
+  TcpScalars* sc = nullptr;
+  uint32_t mss = 0, hdr = 0, max_att = 0;
+  int64_t rto = 0;
+  uint64_t cap_w = 0, cap_s = 0;
+};
+
 struct Dev {
   Prof prof;
   Flood fl;
@@ -236,6 +259,12 @@ hipError_t launch_append(Dev& d, const uint32_t* src, const uint32_t* dst, const
                          const int64_t* t, uint32_t n);
 // A publish batch: set the seen bits of (local, pub) pairs already in d.fl.mark.
 hipError_t launch_flood_mark(Dev& d, uint32_t n);
+// TCP mode: the last window's packets (status, seq; count n_host or *n_dev) and deliveries ->
+// queued copies, first intact arrivals, finished writes, retransmissions onto pend[cur]
+hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch);
+// window start: pend[cur] entries due before the window's end staged behind sc->n_msgs_dev (which
+// the caller has set), the others moved to pend[cur ^ 1]
+hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_pending, bool base_dev, uint32_t base_host);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),

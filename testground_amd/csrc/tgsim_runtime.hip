@@ -91,7 +91,15 @@ struct tgsim_ctx {
   // pinned staging of host uploads (messages, publish marks): the copies are asynchronous, a buffer
   // is reused once its event has passed
   struct Pinned { uint8_t* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool busy = false; };
-  Pinned pin_msgs, pin_marks;
+  Pinned pin_msgs, pin_marks, pin_tcp;
+  // TCP mode (tgsim_tcp_*)
+  bool tcp_on = false, tcp_need_react = false;
+  tgsim_tcp_config tcp{};
+  TcpDev td;
+  uint64_t tw_n = 0, tsg_n = 0;       // writes / segments so far
+  uint32_t tcp_cur = 0, tcp_epoch = 0;
+  uint32_t tcp_pend_h = 0;            // retransmissions pending after the last reaction
+  tgsim_tcp_stats tstats{};
   bool any_dup = false;
   // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
   // signal all-gather run inside the library - natively over RCCL (comm), or through caller callbacks
@@ -284,7 +292,7 @@ extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
 extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (!c) return;
   if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
-  for (tgsim_ctx::Pinned* b : {&c->pin_msgs, &c->pin_marks}) {
+  for (tgsim_ctx::Pinned* b : {&c->pin_msgs, &c->pin_marks, &c->pin_tcp}) {
     if (b->p) (void)hipHostFree(b->p);
     if (b->ev) (void)hipEventDestroy(b->ev);
   }
@@ -849,7 +857,12 @@ static int validate_msgs(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   return TGSIM_OK;
 }
 
+static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n);
 extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (c && c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
+  return enqueue_host(c, m, n);
+}
+static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
@@ -901,6 +914,7 @@ extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
 
 extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if ((c->staged_dev ? 0 : (uint64_t)c->n_staged) + n > c->d.cap_msgs)
     return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
@@ -965,6 +979,15 @@ static int plan_queue_limit(tgsim_ctx* c) {
 static int begin_common(tgsim_ctx* c) {
   int rc = upload_tables(c);
   if (rc) return rc;
+  if (c->tcp_on) {
+    if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
+    if (c->tcp_pend_h) {  // due retransmissions join the staged packets behind a device-side count
+      HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->tcp_pend_h, c->staged_dev, c->n_staged), "tcp release");
+      c->win_m_extra += c->tcp_pend_h;  // queue-limit test: any sender may hold all of them
+      c->staged_dev = true;
+      c->tcp_cur ^= 1u;
+    }
+  }
   rc = plan_queue_limit(c);
   if (rc) return rc;
   HIPCK(c, window_begin(c->d, c->n_staged, c->staged_dev ? &c->d.sc->n_msgs_dev : nullptr), "window_begin");
@@ -973,6 +996,7 @@ static int begin_common(tgsim_ctx* c) {
   c->staged_dev = false;
   c->end_known = false;  // device-ended windows (barrier / device t_end); explicit ones set it after
   c->in_window = true;
+  c->tcp_need_react = c->tcp_on;
   return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
 
@@ -1731,5 +1755,179 @@ extern "C" int tgsim_topic_arena_device(tgsim_ctx* c, const uint32_t** inst, con
   if (len) *len = c->tp_len;
   if (payload) *payload = c->tp_bytes;
   if (n) *n = c->tp_n;
+  return TGSIM_OK;
+}
+
+// ============================== TCP mode ===================================
+// Host side of tgsim_tcp_*: segmentation (tgsim_tcp_send stages the packets), the reaction after
+// every window (tgsim_tcp.hip; one synchronisation reads the retransmissions pending), the write
+// table. Oracle twin: tgo_tcp_*.
+
+namespace {
+__global__ void k_fill_i64(int64_t* p, size_t n, int64_t v) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+}  // namespace
+
+extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
+  if (!c || !cfg) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
+  if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
+  if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "messages already staged");
+  tgsim_tcp_config t = *cfg;
+  if (!t.mss) t.mss = 1448;
+  if (!t.header_bytes) t.header_bytes = 52;
+  if (!t.rto_ns) t.rto_ns = 200000000;
+  if (!t.max_attempts) t.max_attempts = 16;
+  if (!t.max_writes) t.max_writes = 1u << 22;
+  if (!t.max_segments) t.max_segments = 1u << 24;
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > 0xFFFFFFFFull)
+    return fail(c, TGSIM_EINVAL, "bad TCP configuration");
+  TcpDev& d = c->td;
+  const size_t W = t.max_writes, S = t.max_segments;
+  if (dalloc(c, &d.w_src, W) || dalloc(c, &d.w_dst, W) || dalloc(c, &d.w_rem, W) || dalloc(c, &d.w_state, W) ||
+      dalloc(c, &d.w_tarr, W) || dalloc(c, &d.w_fail, W) || dalloc(c, &d.s_w, S) || dalloc(c, &d.s_wire, S) ||
+      dalloc(c, &d.s_att, S) || dalloc(c, &d.s_out, S) || dalloc(c, &d.s_flags, S) || dalloc(c, &d.s_mark, S) ||
+      dalloc(c, &d.s_tatt, S) || dalloc(c, &d.s_arr, S) || dalloc(c, &d.s_tlast, S) || dalloc(c, &d.pend[0], S) ||
+      dalloc(c, &d.pend[1], S) || dalloc(c, &d.sc, (size_t)1))
+    return TGSIM_ENOMEM;
+  hipStream_t st = c->d.stream;
+  HIPCK(c, hipMemsetAsync(d.w_state, 0, W * 4, st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.s_att, 0, S * 4, st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.s_out, 0, S * 4, st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.s_flags, 0, S * 4, st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.s_mark, 0, S * 4, st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.sc, 0, sizeof(TcpScalars), st), "tcp init");
+  hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.w_tarr, W, INT64_MIN);
+  hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.w_fail, W, INT64_MAX);
+  hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.s_arr, S, INT64_MAX);
+  hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.s_tlast, S, INT64_MIN);
+  HIPCK(c, hipGetLastError(), "tcp init");
+  HIPCK(c, hipStreamSynchronize(st), "tcp init");
+  d.mss = t.mss; d.hdr = t.header_bytes; d.max_att = t.max_attempts; d.rto = t.rto_ns; d.cap_w = W; d.cap_s = S;
+  c->tcp = t;
+  c->tcp_on = true;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (!c || !m) return TGSIM_EINVAL;
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  if (!n) return TGSIM_OK;
+  size_t nseg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (m->src[i] >= c->N || m->dst[i] >= c->N) return fail(c, TGSIM_EINVAL, "write %zu: bad instance id", i);
+    if (m->t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
+    if (m->size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
+    nseg += m->size[i] ? (m->size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
+  }
+  if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + nseg > c->tcp.max_segments)
+    return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  // write table (src, dst, segments left), segment table (write, wire size, attempt-0 time) and the
+  // packets, built on the host: the segment count of every write is known here
+  std::vector<uint32_t> w3(3 * n), s2(2 * nseg), p_src(nseg), p_dst(nseg), p_seq(nseg), p_size(nseg);
+  std::vector<int64_t> s_t(nseg);
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t size = m->size[i], ns = size ? (size + c->tcp.mss - 1) / c->tcp.mss : 1;
+    w3[i] = m->src[i]; w3[n + i] = m->dst[i]; w3[2 * n + i] = ns;
+    for (uint32_t j = 0; j < ns; ++j, ++k) {
+      const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
+      const uint32_t sid = (uint32_t)(c->tsg_n + k);
+      s2[k] = (uint32_t)(c->tw_n + i); s2[nseg + k] = pay + c->tcp.header_bytes; s_t[k] = m->t_send[i];
+      p_src[k] = m->src[i]; p_dst[k] = m->dst[i]; p_seq[k] = sid << 4; p_size[k] = pay + c->tcp.header_bytes;
+    }
+  }
+  uint8_t* pin = nullptr;
+  int rc = pin_acquire(c, c->pin_tcp, 12 * n + 16 * nseg, &pin);
+  if (rc) return rc;
+  memcpy(pin, s_t.data(), 8 * nseg);
+  memcpy(pin + 8 * nseg, w3.data(), 12 * n);
+  memcpy(pin + 8 * nseg + 12 * n, s2.data(), 8 * nseg);
+  TcpDev& d = c->td;
+  hipStream_t st = c->d.stream;
+  const uint8_t* pw = pin + 8 * nseg;
+  const uint8_t* ps = pw + 12 * n;
+  HIPCK(c, hipMemcpyAsync(d.s_tatt + c->tsg_n, pin, 8 * nseg, hipMemcpyHostToDevice, st), "tcp send");
+  HIPCK(c, hipMemcpyAsync(d.w_src + c->tw_n, pw, 4 * n, hipMemcpyHostToDevice, st), "tcp send");
+  HIPCK(c, hipMemcpyAsync(d.w_dst + c->tw_n, pw + 4 * n, 4 * n, hipMemcpyHostToDevice, st), "tcp send");
+  HIPCK(c, hipMemcpyAsync(d.w_rem + c->tw_n, pw + 8 * n, 4 * n, hipMemcpyHostToDevice, st), "tcp send");
+  HIPCK(c, hipMemcpyAsync(d.s_w + c->tsg_n, ps, 4 * nseg, hipMemcpyHostToDevice, st), "tcp send");
+  HIPCK(c, hipMemcpyAsync(d.s_wire + c->tsg_n, ps + 4 * nseg, 4 * nseg, hipMemcpyHostToDevice, st), "tcp send");
+  rc = pin_issued(c, c->pin_tcp);
+  if (rc) return rc;
+  tgsim_msg_soa p{p_src.data(), p_dst.data(), p_seq.data(), p_size.data(), s_t.data()};
+  rc = enqueue_host(c, &p, nseg);
+  if (rc) return rc;
+  c->tw_n += n;
+  c->tsg_n += nseg;
+  c->tstats.writes += n;
+  c->tstats.segments += nseg;
+  c->tstats.packets += nseg;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
+  if (n_done) *n_done = 0;
+  if (!c) return TGSIM_EINVAL;
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->tcp_need_react) return TGSIM_OK;
+  const bool on_dev = c->n_status_last == kStatusOnDevice;
+  HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
+                            on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch), "tcp react");
+  // one synchronisation: the pending count sizes the next window's release (and its queue-limit bound)
+  TcpScalars ts;
+  HIPCK(c, hipMemcpyAsync(&ts, c->td.sc, sizeof(ts), hipMemcpyDeviceToHost, c->d.stream), "tcp react");
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  c->tcp_pend_h = ts.pend_n[c->tcp_cur];
+  c->tcp_need_react = false;
+  c->tstats.retransmissions = ts.retx;
+  c->tstats.delivered = ts.delivered;
+  c->tstats.failed = ts.failed;
+  c->tstats.pending_retx = c->tcp_pend_h;
+  c->tstats.packets = c->tstats.segments + ts.released;
+  if (n_done) *n_done = ts.done;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  *n = c->tw_n;
+  if (!c->tcp_on) return TGSIM_OK;
+  if (c->tw_n > cap) return fail(c, TGSIM_ECAPACITY, "write capacity");
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  const size_t W = c->tw_n;
+  std::vector<uint32_t> st(W);
+  std::vector<int64_t> ta(W), tf(W);
+  if (W) {
+    HIPCK(c, hipMemcpy(st.data(), c->td.w_state, W * 4, hipMemcpyDeviceToHost), "tcp writes");
+    HIPCK(c, hipMemcpy(ta.data(), c->td.w_tarr, W * 8, hipMemcpyDeviceToHost), "tcp writes");
+    HIPCK(c, hipMemcpy(tf.data(), c->td.w_fail, W * 8, hipMemcpyDeviceToHost), "tcp writes");
+  }
+  for (size_t i = 0; i < W; ++i) {
+    // a failed write reports its earliest failure (key t * 2 + timeout), whatever failed first
+    uint32_t s_i = st[i];
+    int64_t t_i = ta[i];
+    if (s_i != TGSIM_TCP_PENDING && s_i != TGSIM_TCP_DELIVERED) {
+      t_i = tf[i] >> 1;
+      s_i = (tf[i] & 1) ? TGSIM_TCP_TIMEOUT : TGSIM_TCP_REFUSED;
+    } else if (s_i == TGSIM_TCP_PENDING) {
+      t_i = INT64_MIN;
+    }
+    if (state) state[i] = (uint8_t)s_i;
+    if (t) t[i] = t_i;
+  }
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_tcp_get_stats(tgsim_ctx* c, tgsim_tcp_stats* out) {
+  if (!c || !out) return TGSIM_EINVAL;
+  *out = c->tstats;
   return TGSIM_OK;
 }

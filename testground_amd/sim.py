@@ -155,6 +155,37 @@ class Simulator:
         m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
         self._check(self.lib.enqueue(self._ctx, C.byref(m), n))
 
+    # ---- TCP mode (tgsim_tcp_*) ------------------------------------------------
+    def tcp_enable(self, mss: int = 0, header_bytes: int = 0, rto_ns: int = 0, max_attempts: int = 0,
+                   max_writes: int = 0, max_segments: int = 0) -> None:
+        cfg = A.TcpConfig(mss, header_bytes, rto_ns, max_attempts, 0, max_writes, max_segments)
+        self._check(self.lib.tcp_enable(self._ctx, C.byref(cfg)))
+
+    def tcp_send(self, src, dst, seq, size, t_send) -> None:
+        arrs = [np.ascontiguousarray(np.broadcast_to(x, np.shape(t_send)), dtype=np.uint32) for x in (src, dst, seq, size)]
+        t = np.ascontiguousarray(t_send, dtype=np.int64)
+        m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
+        self._check(self.lib.tcp_send(self._ctx, C.byref(m), len(t)))
+
+    def tcp_react(self) -> int:
+        n = C.c_size_t()
+        self._check(self.lib.tcp_react(self._ctx, C.byref(n)))
+        return n.value
+
+    def tcp_writes(self) -> tuple[np.ndarray, np.ndarray]:
+        """(state TCP_*, time) per write id: last segment's arrival, or the failure time."""
+        n = C.c_size_t()
+        self.lib.tcp_writes(self._ctx, None, None, 0, C.byref(n))  # size query (ECAPACITY when n > 0)
+        st = np.zeros(n.value, np.uint8)
+        t = np.zeros(n.value, np.int64)
+        self._check(self.lib.tcp_writes(self._ctx, _ptr(st), _ptr(t), n.value, C.byref(n)))
+        return st, t
+
+    def tcp_stats(self) -> dict:
+        s = A.TcpStats()
+        self._check(self.lib.tcp_get_stats(self._ctx, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in A.TcpStats._fields_}
+
     def advance(self, t_end: int, wait: bool = True) -> None:
         """One window [now, t_end). wait=False: tgsim_advance_async (no closing sync; device-side
         errors surface at the next synchronising call)."""

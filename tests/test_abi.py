@@ -56,6 +56,7 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     structs = {"tgsim_link_shape": A.LinkShape, "tgsim_link_rule": A.LinkRule,
                "tgsim_network_config": A.NetworkConfig, "tgsim_config": A.Config, "tgsim_msg_soa": A.MsgSoA,
+               "tgsim_tcp_config": A.TcpConfig, "tgsim_tcp_stats": A.TcpStats,
                "tgsim_delivery_soa": A.DeliverySoA, "tgsim_stats": A.Stats, "tgsim_transport": A.Transport}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tgsim.h"', "int main(void) {"]
     for cname, py in structs.items():

@@ -1,0 +1,193 @@
+"""TCP mode (tgsim_tcp_*): writes segmented into MSS
+packets over the per-packet path, lost / corrupted segments retransmitted with exponential backoff
+from the RTO, refused routes failing the write, in-order delivery per connection. Hand-computed
+answers run on the oracle (CPU) and the HIP library (GPU); randomised runs compare the two bit for
+bit (deliveries, per-packet statuses as a multiset — the device releases retransmissions in
+arbitrary order —, write outcomes, counters). Parity unpinned against real TCP: there is no packet
+capture of the reference's plans to compare with."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd import tcp as T
+from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape
+
+MS = 1_000_000
+
+
+def sim(b, n=4, **kw):
+    kw.setdefault("max_msgs_per_window", 1 << 14)
+    kw.setdefault("max_records", 1 << 16)
+    s = Simulator(SimConfig(n_instances=n, seed=kw.pop("seed", 3), **kw), binding=b)
+    return s
+
+
+def window(s, t_end):
+    s.advance(t_end)
+    d = s.deliveries()
+    s.tcp_react()
+    return d
+
+
+def case_segmentation(b):
+    s = sim(b)
+    s.tcp_enable()
+    s.tcp_send([0, 1], [1, 2], [0, 0], [4096, 0], [5, 6])
+    d = window(s, 1 * MS)
+    # 4096 B = 1448 + 1448 + 1200, each + 52 B of headers; a 0-byte write is one bare segment
+    assert sorted(zip(d["seq"].tolist(), d["size"].tolist())) == [(0, 1500), (16, 1500), (32, 1252), (48, 52)]
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED] * 2 and list(t) == [5, 6]
+    assert s.tcp_stats()["segments"] == 4 and s.tcp_stats()["retransmissions"] == 0
+    with pytest.raises(A.TgsimError) as e:
+        s.enqueue([0], [1], [9], [1], [2 * MS])   # TCP mode: all traffic is TCP
+    assert e.value.code == A.ESTATE
+    s.close()
+
+
+def case_loss_backoff_and_timeout(b):
+    s = sim(b)
+    s.tcp_enable(max_attempts=3)
+    s.set_shape(0, make_shape(loss=100.0))
+    s.tcp_send([0, 2], [1, 1], [0, 0], [100, 100], [1 * MS, 1 * MS])
+    for k in range(1, 1500, 50):                 # 50 ms windows up to 1.5 s
+        window(s, k * MS + 50 * MS)
+        if k == 151:                              # sender 2 loses everything from 0.2 s on
+            s.set_shape(2, make_shape(loss=100.0))
+    st, t = s.tcp_writes()
+    # sender 0: attempts at 1, 201, 601 ms all lost; the third failure times out at 601 + 800 ms
+    assert st[0] == A.TCP_TIMEOUT and t[0] == 1401 * MS
+    assert st[1] == A.TCP_DELIVERED and t[1] == 1 * MS
+    stats = s.tcp_stats()
+    assert stats["retransmissions"] == 2 and stats["failed"] == 1 and stats["delivered"] == 1
+    assert stats["packets"] == 2 + 2
+    s.close()
+
+
+def case_retransmission_recovers(b):
+    s = sim(b)
+    s.tcp_enable()
+    s.set_shape(0, make_shape(loss=100.0))
+    s.tcp_send([0], [1], [0], [10], [3 * MS])
+    window(s, 10 * MS)
+    s.set_shape(0, make_shape(latency_ns=7 * MS))  # the link heals before the 200 ms timer fires
+    for k in range(1, 30):
+        window(s, 10 * MS + k * 10 * MS)
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_DELIVERED and t[0] == 3 * MS + 200 * MS + 7 * MS
+    s.close()
+
+
+def case_corruption_waits_for_the_copy(b):
+    """Every copy corrupted: the retransmission leaves at max(t + RTO, the corrupted copy's
+    arrival) - a 300 ms path is slower than the 200 ms RTO."""
+    s = sim(b)
+    s.tcp_enable(max_attempts=2)
+    s.set_shape(0, make_shape(latency_ns=300 * MS, corrupt=100.0))
+    s.tcp_send([0], [1], [0], [64], [0])
+    for k in range(1, 120):
+        window(s, k * 10 * MS)
+    st, t = s.tcp_writes()
+    # attempt 0 at 0 arrives corrupted at 300 ms -> attempt 1 at 300 ms, corrupted at 600 ms;
+    # attempt 1 was the last: timeout at max(300 + 400, 600) = 700 ms
+    assert st[0] == A.TCP_TIMEOUT and t[0] == 700 * MS
+    s.close()
+
+
+def case_duplicates_and_refusal(b):
+    s = sim(b, n=8)
+    s.tcp_enable()
+    s.set_shape(0, make_shape(duplicate=100.0, latency_ns=2 * MS))
+    from testground_amd.network import int_to_ip
+    s.add_rules(3, [make_rule(int_to_ip(s.get_ip(4)) + "/32", A.FILTER_REJECT)])
+    s.tcp_send([0, 3, 3], [1, 4, 5], [0, 0, 0], [3000, 10, 10], [0, 1, 2])
+    window(s, 10 * MS)
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED, A.TCP_REFUSED, A.TCP_DELIVERED] and list(t) == [2 * MS, 1, 2]
+    assert s.tcp_stats()["retransmissions"] == 0
+    s.close()
+
+
+CASES = [case_segmentation, case_loss_backoff_and_timeout, case_retransmission_recovers,
+         case_corruption_waits_for_the_copy, case_duplicates_and_refusal]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c.__name__[5:] for c in CASES])
+def test_tcp_oracle(oracle, case):
+    case(oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c.__name__[5:] for c in CASES])
+def test_tcp_hip(hip, case):
+    case(hip)
+
+
+def test_in_order_view():
+    # connection 0->1: write b (seq 1) arrives before write a (seq 0) is retransmitted
+    src, dst, seq, ts = [0, 0, 0, 2], [1, 1, 1, 1], [0, 1, 2, 0], [0, 0, 0, 0]
+    st = [T.DELIVERED, T.DELIVERED, T.PENDING, T.TIMEOUT]
+    td = [205, 10, 0, 900]
+    s2, t2 = T.in_order(src, dst, seq, ts, st, td)
+    assert list(s2) == [T.DELIVERED, T.DELIVERED, T.PENDING, T.TIMEOUT]
+    assert list(t2) == [205, 205, T.NEVER, 900]
+    s3, t3 = T.in_order([0, 0], [1, 1], [0, 1], [0, 0], [T.REFUSED, T.DELIVERED], [3, 50])
+    assert list(s3) == [T.REFUSED, T.REFUSED] and list(t3) == [3, 3]   # the reset fails what follows
+
+
+def run_random(b, seed, n=300, windows=60, window_ns=10 * MS):
+    """Lossy, corrupting, duplicating, reordering links with jitter and rate limits; writes of 0 to
+    9000 B over the first 30 windows. Per window: deliveries and the statuses as a sorted multiset;
+    at the end the write outcomes and counters."""
+    rng = np.random.default_rng(seed)
+    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18),
+                  binding=b)
+    s.tcp_enable(max_attempts=int(rng.integers(3, 8)), rto_ns=int(rng.integers(20, 80)) * MS)
+    for g in range(n):
+        s.set_shape(g, make_shape(latency_ns=int(rng.integers(1, 60)) * MS, jitter_ns=int(rng.integers(0, 5)) * MS,
+                                  bandwidth_bps=int(rng.choice([0, 2_000_000, 20_000_000])),
+                                  loss=float(rng.choice([0, 2, 10])), corrupt=float(rng.choice([0, 3])),
+                                  duplicate=float(rng.choice([0, 5])), reorder=float(rng.choice([0, 10]))))
+    out, t = [], 0
+    for w in range(windows):
+        if w < 30:
+            k = int(rng.integers(0, 80))
+            src = rng.integers(0, n, k)
+            s.tcp_send(src, (src + rng.integers(1, n, k)) % n, rng.integers(0, 1 << 20, k),
+                       rng.integers(0, 9000, k), t + rng.integers(0, window_ns, k))
+        t += window_ns
+        s.advance(t)
+        st = s.status()
+        d = s.deliveries()
+        s.tcp_react()
+        out.append(dict(deliv=d, status=np.sort(st)))
+    ws, wt = s.tcp_writes()
+    out.append(dict(writes=(ws, wt), stats=s.tcp_stats()))
+    s.close()
+    return out
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a[:-1], b[:-1]):
+        for k in x["deliv"]:
+            assert np.array_equal(x["deliv"][k], y["deliv"][k]), k
+        assert np.array_equal(x["status"], y["status"])
+    assert np.array_equal(a[-1]["writes"][0], b[-1]["writes"][0])
+    assert np.array_equal(a[-1]["writes"][1], b[-1]["writes"][1])
+    assert a[-1]["stats"] == b[-1]["stats"]
+
+
+def test_tcp_random_oracle_properties(oracle):
+    out = run_random(oracle, 1)
+    ws, wt = out[-1]["writes"]
+    st = out[-1]["stats"]
+    assert st["retransmissions"] > 0 and st["delivered"] > 0.8 * st["writes"]
+    assert np.all(wt[ws != A.TCP_PENDING] >= 0)
+    assert st["packets"] == st["segments"] + sum(np.count_nonzero(x["status"] >= 0) for x in out[:-1]) - st["segments"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_tcp_random_hip_matches_oracle(hip, oracle, seed):
+    _same(run_random(hip, seed), run_random(oracle, seed))
