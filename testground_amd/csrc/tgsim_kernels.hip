@@ -87,6 +87,16 @@ struct Queues {
   uint32_t* K[3];            // group-by key of each appended record, same physical index (A, D, L)
   uint32_t subcap, xcap, lo, slots;
   int64_t slot_ns;
+  // consumer groups of A / D keys: the fused consumers give XCD x a contiguous run of buckets
+  // (xcd_major), i.e. keys [gb[x-1], gb[x]); producers order each wave's A / D slots by group, so a
+  // line of records is read by one XCD (whose L2 then serves its other records)
+  uint32_t gb[7];
+  __device__ __forceinline__ uint32_t group_of(uint32_t key) const {
+    uint32_t g = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) g += key >= gb[j] ? 1u : 0u;
+    return g;
+  }
   // A: local sender; D: local receiver; L: timing-wheel slot relative to this window's end
   __device__ __forceinline__ uint32_t key_of(int q, const tgsim_record& r) const {
     if (q == Q_A) return r.src - lo;
@@ -128,36 +138,59 @@ struct Queues {
   }
 
   // Wave-collective append of U records per lane (q[u] < 0: none). The local queues A / D / L take
-  // one sub-queue per wave for the whole batch: one ballot per (record, queue) gives every slot and
-  // at most three independent atomics (one round trip) reserve them, instead of a dependent atomic
-  // per record and distinct counter. Slots go record-major, lane-minor, so each store instruction
-  // of the wave covers consecutive records. Exchange records (sharded runs) take the per-record path.
+  // one sub-queue per wave for the whole batch and at most three independent atomics (one round
+  // trip) reserve it, instead of a dependent atomic per record and distinct counter. L slots go
+  // record-major, lane-minor (one ballot per record), so each store instruction covers consecutive
+  // records; A and D slots go by consumer group (a per-wave counting sort in LDS), so each line is
+  // read by one XCD. Exchange records (sharded runs) take the per-record path.
   template <int U>
   __device__ __forceinline__ void push_batch(const int (&q)[U], const tgsim_record (&r)[U], uint32_t salt) const {
+    __shared__ uint32_t gcnt[kBlock / 64][16];  // per wave: [A groups 0..7 | D groups 0..7]
     const uint32_t lane = lane_id();
+    uint32_t* cnt = gcnt[threadIdx.x >> 6];
     const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
-    uint64_t mA[U], mD[U], mL[U];
+    // any lanes may be active (grid-stride tails): the first active one keeps the 16 counters
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
+    if (lane == leader)
+      for (int i = 0; i < 16; ++i) cnt[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint64_t mL[U];
+    uint32_t rk[U];
     bool any_x = false;
-    uint32_t tA = 0, tD = 0, tL = 0;
+    uint32_t tL = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      mA[u] = __ballot(q[u] == Q_A); mD[u] = __ballot(q[u] == Q_D); mL[u] = __ballot(q[u] == Q_L);
-      tA += (uint32_t)__popcll(mA[u]); tD += (uint32_t)__popcll(mD[u]); tL += (uint32_t)__popcll(mL[u]);
+      mL[u] = __ballot(q[u] == Q_L);
+      tL += (uint32_t)__popcll(mL[u]);
       any_x |= q[u] >= Q_X0;
+      rk[u] = 0;
+      if (q[u] == Q_A || q[u] == Q_D)
+        rk[u] = ((q[u] == Q_D ? 8u : 0u) + group_of(key_of(q[u], r[u]))) << 24 |
+                atomicAdd(&cnt[(q[u] == Q_D ? 8u : 0u) + group_of(key_of(q[u], r[u]))], 1u);
     }
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
+    __builtin_amdgcn_wave_barrier();
+    // group counts -> exclusive offsets inside each queue's reservation
+    uint32_t sA = 0, sD = 0;
+    if (lane == leader) {
+      for (int i = 0; i < 8; ++i) { const uint32_t v = cnt[i]; cnt[i] = sA; sA += v; }
+      for (int i = 8; i < 16; ++i) { const uint32_t v = cnt[i]; cnt[i] = sD; sD += v; }
+    }
+    const uint32_t tA = __shfl(sA, (int)leader), tD = __shfl(sD, (int)leader);
+    __builtin_amdgcn_wave_barrier();
     uint32_t rA = 0, rD = 0, rL = 0;
     if (lane == leader) {  // three independent atomics: one round trip
       if (tA) rA = atomicAdd(qc + (((uint32_t)Q_A * kNSub + sub) << 5), tA);
       if (tD) rD = atomicAdd(qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD);
       if (tL) rL = atomicAdd(qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL);
     }
-    uint32_t pA = __shfl(rA, (int)leader), pD = __shfl(rD, (int)leader), pL = __shfl(rL, (int)leader);
+    const uint32_t pA = __shfl(rA, (int)leader), pD = __shfl(rD, (int)leader);
+    uint32_t pL = __shfl(rL, (int)leader);
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // no runtime-indexed private arrays (they would live in scratch)
       const int k = q[u];
       if (k >= 0 && k < Q_X0) {
-        const uint32_t pos = k == Q_A ? pA + mask_rank(mA[u]) : (k == Q_D ? pD + mask_rank(mD[u]) : pL + mask_rank(mL[u]));
+        const uint32_t pos = k == Q_L ? pL + mask_rank(mL[u])
+                                      : (k == Q_A ? pA : pD) + cnt[rk[u] >> 24] + (rk[u] & 0xFFFFFFu);
         if (pos < subcap) {
           const size_t at = (size_t)sub * subcap + pos;
           store_rec((k == Q_A ? A : (k == Q_D ? D : L)) + at, r[u]);
@@ -166,7 +199,7 @@ struct Queues {
           atomicOr(&sc->err, k == Q_A ? ERR_CAP_A : (k == Q_D ? ERR_CAP_D : ERR_CAP_L));
         }
       }
-      pA += (uint32_t)__popcll(mA[u]); pD += (uint32_t)__popcll(mD[u]); pL += (uint32_t)__popcll(mL[u]);
+      pL += (uint32_t)__popcll(mL[u]);
     }
     if (__ballot(any_x)) {
 #pragma unroll
@@ -1858,36 +1891,52 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
       atomicAdd(&dec[sm.key[slot[u]]], 1u);
     }
   }
-  // staging slots in (wave, item u, lane) order: one ballot per (u, queue), so the lanes of every
-  // staging store hold consecutive records (slots contiguous per thread put the 32-B records of
-  // neighbouring lanes ~128 B apart: 8-way LDS bank conflicts)
-  uint64_t mD[kIPT], mL[kIPT];
-  uint32_t wD = 0, wL = 0;
+  // staging slots, so that the lanes of a staging store hold neighbouring records (slots contiguous
+  // per thread put neighbouring lanes' 32-B records ~128 B apart: 8-way LDS bank conflicts). D by
+  // consumer group (an LDS counting sort: lanes of one group get consecutive slots) - each output
+  // line then holds records that one XCD's emit workgroups read (Queues::group_of) -, L in
+  // (wave, item, lane) order from ballots.
+  const Queues& Q = p.Q;
+  uint32_t* gcnt = sm.part + 2 * (kBlock / 64);  // [8] D records per consumer group, then offsets
+  uint32_t rkD[kIPT];
+  uint64_t mL[kIPT];
+  uint32_t wL = 0;
 #pragma unroll
   for (int u = 0; u < kIPT; ++u) {
-    mD[u] = __ballot(code[u] == Q_D);
     mL[u] = __ballot(code[u] == Q_L);
-    wD += (uint32_t)__popcll(mD[u]);
     wL += (uint32_t)__popcll(mL[u]);
   }
   const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) sm.flag = 0;
-  if ((threadIdx.x & 63) == 0) { sm.part[wave] = wD; sm.part[kBlock / 64 + wave] = wL; }
+  if (threadIdx.x < 8) gcnt[threadIdx.x] = 0;
+  if ((threadIdx.x & 63) == 0) sm.part[kBlock / 64 + wave] = wL;
   __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kIPT; ++u) {
+    rkD[u] = 0;
+    if (code[u] == Q_D) {
+      const uint32_t g = Q.group_of(rec[u].dst - p.lo);
+      rkD[u] = (g << 24) | atomicAdd(&gcnt[g], 1u);
+    }
+  }
   // this workgroup owns its senders' counters for the launch (long runs: k_rest, later)
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock)
     if (dec[i]) p.pend[h.k0 + i] -= dec[i];
   if (nX) sm.flag = 1;
-  uint32_t tD = 0, tL = 0, bD = 0, bL = 0;
+  __syncthreads();  // group counts complete
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int g = 0; g < 8; ++g) { const uint32_t v = gcnt[g]; gcnt[8 + g] = run; run += v; }
+    gcnt[16] = run;
+  }
+  __syncthreads();
+  uint32_t tD = gcnt[16], tL = 0, bL = 0;
 #pragma unroll
   for (uint32_t w = 0; w < kBlock / 64; ++w) {
-    const uint32_t a = sm.part[w], c = sm.part[kBlock / 64 + w];
-    bD += w < wave ? a : 0u;
+    const uint32_t c = sm.part[kBlock / 64 + w];
     bL += w < wave ? c : 0u;
-    tD += a;
     tL += c;
   }
-  const Queues& Q = p.Q;
   const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u);
   __syncthreads();  // every thread has read the scan partials in sm.part (and k1 for the last time)
   if (threadIdx.x == 0) {
@@ -1900,11 +1949,11 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
   uint4* st = reinterpret_cast<uint4*>(sm.k1);
   const uint32_t nst = tD + tL;
   for (uint32_t r0 = 0; r0 < nst; r0 += kStageN) {
-    uint32_t cD = bD, cL = tD + bL;
+    uint32_t cL = tD + bL;
 #pragma unroll
     for (int u = 0; u < kIPT; ++u) {
-      const uint32_t qD = cD + mask_rank(mD[u]), qL = cL + mask_rank(mL[u]);
-      cD += (uint32_t)__popcll(mD[u]);
+      const uint32_t qD = gcnt[8 + (rkD[u] >> 24)] + (rkD[u] & 0xFFFFFFu);
+      const uint32_t qL = cL + mask_rank(mL[u]);
       cL += (uint32_t)__popcll(mL[u]);
       if (code[u] != Q_D && code[u] != Q_L) continue;
       const uint32_t q = code[u] == Q_D ? qD : qL;
@@ -3121,10 +3170,15 @@ static inline unsigned grid_for(uint64_t n) {
   return (unsigned)g;
 }
 
+static uint32_t bkt_width_fused(const Dev& d, uint32_t K);
 static Queues make_queues(Dev& d) {
   Queues Q;
   Q.sc = d.sc; Q.qc = d.qc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
   Q.K[0] = d.KA; Q.K[1] = d.KD; Q.K[2] = d.KL; Q.lo = d.lo; Q.slots = d.slots; Q.slot_ns = d.slot_ns;
+  // the fused consumers' buckets (bkt_width_fused over the local keys) in xcd_major order: XCD x
+  // runs buckets [x q + min(x, r), (x+1) q + min(x+1, r)) with q = B / 8, r = B % 8
+  const uint32_t w = bkt_width_fused(d, d.nloc), B = (d.nloc + w - 1) / w, q8 = B >> 3, r8 = B & 7u;
+  for (uint32_t j = 1; j < 8; ++j) Q.gb[j - 1] = (j * q8 + std::min(j, r8)) * w;
   return Q;
 }
 
