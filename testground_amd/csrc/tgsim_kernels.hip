@@ -475,12 +475,22 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   const uint32_t stride = nblocks * blockDim.x;
   uint32_t it = 0;
   const uint32_t n = a.n_dev ? *a.n_dev : a.n;
-  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += stride, ++it) {
-    // Every load of this message is issued up front with clamped indices, so the wave pays one
-    // round trip for the SoA record and one for the table gathers instead of a branch-serialised chain.
-    const uint32_t src = a.src[i], dst = a.dst[i], seq = a.seq[i], size = a.size[i];
-    const int64_t ts = a.t[i];
+  // Every load of a message is issued up front with clamped indices: one round trip for the SoA
+  // record and one for the table gathers instead of a branch-serialised chain. The next message's
+  // SoA record is loaded beside this one's gathers (software pipelining across the grid stride), so
+  // an iteration pays one load round trip, not two.
+  uint32_t i = bid * blockDim.x + threadIdx.x;
+  uint32_t n_src = 0, n_dst = 0, n_seq = 0, n_size = 0;
+  int64_t n_ts = 0;
+  if (i < n) { n_src = a.src[i]; n_dst = a.dst[i]; n_seq = a.seq[i]; n_size = a.size[i]; n_ts = a.t[i]; }
+  for (; i < n; i += stride, ++it) {
+    const uint32_t src = n_src, dst = n_dst, seq = n_seq, size = n_size;
+    const int64_t ts = n_ts;
     asm volatile("" ::"v"(src), "v"(dst), "v"(seq), "v"(size), "v"((uint32_t)ts), "v"((uint32_t)((uint64_t)ts >> 32)));  // stage 1: SoA record
+    {
+      const uint32_t i2 = i + stride < n ? i + stride : i;  // clamped: the last iteration reloads itself
+      n_src = a.src[i2]; n_dst = a.dst[i2]; n_seq = a.seq[i2]; n_size = a.size[i2]; n_ts = a.t[i2];
+    }
     const uint32_t sl = src - a.lo;
     const bool src_ok = sl < a.nloc;
     const uint32_t slc = src_ok ? sl : 0u;
