@@ -96,6 +96,7 @@ struct Dev {
   // [N] ip | flags << 32 per instance (flags bit0 link enabled, bit1 external routing allowed): one
   // 8-B gather gives a destination's address and link state
   uint64_t* ipf = nullptr;
+  uint32_t* en_bits = nullptr;    // [N / 32 + 1] link enabled (flags bit 0), the destination test
   uint32_t* rule_off = nullptr;   // [nloc+1]
   RuleDev* rules = nullptr;
 

@@ -349,6 +349,7 @@ struct ShapeArgs {
   uint8_t* status;
   const ShapeDev* shape;
   const uint64_t* ipf;         // [N] ip | flags << 32
+  const uint32_t* en_bits;     // [N / 32] link enabled per instance (the destination test, L2-resident)
   const uint32_t* rule_off;
   const RuleDev* rules;
   uint32_t lo, nloc, data_net, data_mask, data_len, key0, key1;
@@ -496,12 +497,13 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
     const uint32_t slc = src_ok ? sl : 0u;
     const uint32_t dstc = dst < a.geo.N ? dst : 0u;
     const uint8_t fsrc = (uint8_t)(a.ipf[src_ok ? src : a.lo] >> 32);
-    const uint64_t vdst = a.ipf[dstc];
-    const uint8_t fdst = (uint8_t)(vdst >> 32);
-    const uint32_t dip = (uint32_t)vdst;
+    // the destination's link bit from a bitmap (N bits: L2-resident even at 1M instances); its
+    // address only when the sender has rules to match it against (every instance address lies in
+    // the data network, so without rules any of them routes the same)
+    const uint32_t fdst = (a.en_bits[dstc >> 5] >> (dstc & 31u)) & 1u;
     const uint32_t r_lo = a.rule_off[slc], r_hi = a.rule_off[slc + 1];
     const ShapeDev sh = a.shape[slc];
-    asm volatile("" ::"v"((uint32_t)fsrc), "v"((uint32_t)fdst), "v"(dip), "v"(r_lo), "v"(r_hi),
+    asm volatile("" ::"v"((uint32_t)fsrc), "v"(fdst), "v"(r_lo), "v"(r_hi),
                  "v"((uint32_t)sh.mu), "v"((uint32_t)sh.tau), "v"(sh.sigma), "v"(sh.loss_t), "v"(sh.dup_t),
                  "v"(sh.corrupt_t), "v"(sh.reorder_t), "v"(sh.mult), "v"(sh.flags));  // stage 2: gathers
     tgsim_record r1, r2;
@@ -525,7 +527,8 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
       cnt[ST_LOCAL]++;
     } else {
       const bool ext = dst == TGSIM_DST_EXTERNAL;
-      const int rt = route_lookup(a, fsrc, r_lo, r_hi, ext ? kExternalIp : dip);
+      const uint32_t dip = ext ? kExternalIp : (r_hi > r_lo ? (uint32_t)a.ipf[dstc] : a.data_net);
+      const int rt = route_lookup(a, fsrc, r_lo, r_hi, dip);
       if (rt == R_DROP) { st = TGSIM_ST_DROPPED; cnt[ST_DROPPED]++; }
       else if (rt == R_REJECT) { st = TGSIM_ST_REJECTED; cnt[ST_REJECTED]++; }
       else if (rt == R_DEFAULT && ext) { st = TGSIM_ST_EXTERNAL; cnt[ST_EXTERNAL]++; }
@@ -3370,7 +3373,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
   if (n_staged) {
     ShapeArgs a;
     a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged; a.n_dev = n_dev;
-    a.status = d.status; a.shape = d.shape; a.ipf = d.ipf; a.rule_off = d.rule_off;
+    a.status = d.status; a.shape = d.shape; a.ipf = d.ipf; a.en_bits = d.en_bits; a.rule_off = d.rule_off;
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
     a.stats = d.stats;

@@ -390,6 +390,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &c->d_red2, 2);
   rc |= dalloc(c, &d.moff, segK);
   rc |= dalloc(c, &d.ipf, c->N);
+  rc |= dalloc(c, &d.en_bits, (size_t)c->N / 32 + 1);
   rc |= dalloc(c, &d.rule_off, nl1);
   rc |= dalloc(c, &d.rules, 1);
   rc |= dalloc(c, &d.m_src, d.cap_msgs);
@@ -796,10 +797,16 @@ static int upload_tables(tgsim_ctx* c) {
     copied = true;
   }
   std::vector<uint64_t> ipf;
+  std::vector<uint32_t> en;
   if (c->flags_dirty || c->ip_dirty) {
     ipf.resize(c->N);
-    for (uint32_t g = 0; g < c->N; ++g) ipf[g] = (uint64_t)c->ip_h[g] | ((uint64_t)c->flags_h[g] << 32);
+    en.assign((size_t)c->N / 32 + 1, 0u);
+    for (uint32_t g = 0; g < c->N; ++g) {
+      ipf[g] = (uint64_t)c->ip_h[g] | ((uint64_t)c->flags_h[g] << 32);
+      en[g >> 5] |= (uint32_t)(c->flags_h[g] & 1u) << (g & 31u);
+    }
     HIPCK(c, hipMemcpyAsync(d.ipf, ipf.data(), c->N * sizeof(uint64_t), hipMemcpyHostToDevice, d.stream), "upload ip/flags");
+    HIPCK(c, hipMemcpyAsync(d.en_bits, en.data(), en.size() * 4, hipMemcpyHostToDevice, d.stream), "upload ip/flags");
     copied = true;
   }
   std::vector<uint32_t> off;
