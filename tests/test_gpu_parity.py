@@ -126,3 +126,60 @@ def test_storm_transport_on_one_device(hip, oracle, world):
         hip, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, exchange_cap=1 << 15),
         setup=lambda sim: sim.set_transport(tr)), device=True)
     S.assert_storm_sharded(outs, S.run_storm(oracle, n_inst=n, rounds=rounds), world, n)
+
+
+@pytest.mark.gpu
+def test_shared_torch_stream_ordering(hip, oracle):
+    """bench.py runs the library on torch's stream (tgsim_set_stream): torch kernels that produce the
+    messages, the library's window and torch kernels that consume the deliveries are then ordered by
+    the stream alone. Here the messages are computed by torch on a side stream, staged with
+    tgsim_enqueue_device and advanced with tgsim_advance_async, and the deliveries are read back
+    by torch from the device arrays (tgsim_deliveries_device) - with no synchronisation in between.
+    Equal to the oracle fed the same messages."""
+    import ctypes as C
+    import torch
+    from testground_amd import _abi as A
+    from testground_amd.sim import SimConfig, Simulator, make_shape
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    n_inst, n = 64, 4096
+    sims = [Simulator(SimConfig(n_instances=n_inst, seed=9, max_msgs_per_window=1 << 14, max_records=1 << 16),
+                      binding=b) for b in (hip, oracle)]
+    for sm in sims:
+        for g in range(n_inst):
+            sm.set_shape(g, make_shape(latency_ns=(g % 5) * 100_000, jitter_ns=50_000, loss=1.0))
+    hs = sims[0]
+    hs.set_stream(s.cuda_stream)
+    with torch.cuda.stream(s):
+        i = torch.arange(n, device=dev, dtype=torch.int64)
+        src = (i * 7 % n_inst).to(torch.int32)
+        dst = ((i * 13 + 5) % n_inst).to(torch.int32)
+        seq = i.to(torch.int32)
+        size = (64 + i % 512).to(torch.int32)
+        t = (i * 97) % 1_000_000
+        big = torch.empty(1 << 24, device=dev).normal_()   # a long torch kernel ahead of the staging
+        soa = A.MsgSoA(src.data_ptr(), dst.data_ptr(), seq.data_ptr(), size.data_ptr(), t.data_ptr())
+        assert hip.enqueue_device(hs._ctx, C.byref(soa), n) == 0
+        assert hip.advance_async(hs._ctx, 3_000_000) == 0
+        out = A.DeliverySoA()
+        assert hip.deliveries_device(hs._ctx, C.byref(out)) == 0
+        del big
+    s.synchronize()
+    src_h, dst_h, seq_h, size_h, t_h = (x.cpu().numpy() for x in (src, dst, seq, size, t))
+    k = hs.delivery_count()
+    # torch reads the device delivery arrays (stream-ordered after the window)
+    with torch.cuda.stream(s):
+        dt = torch.empty(k, dtype=torch.int64, device=dev)
+        hip_memcpy = C.CDLL("libamdhip64.so").hipMemcpyAsync
+        hip_memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        assert hip_memcpy(dt.data_ptr(), out.t_deliver, 8 * k, 3, C.c_void_p(s.cuda_stream)) == 0
+        dt2 = dt + 0                                       # a torch kernel on the copied data
+    s.synchronize()
+    got_t = dt2.cpu().numpy()
+    sims[1].enqueue(src_h, dst_h, seq_h, size_h, t_h)
+    sims[1].advance(3_000_000)
+    want = sims[1].deliveries()
+    assert np.array_equal(got_t, want["t_deliver"])
+    assert np.array_equal(hs.deliveries()["seq"], want["seq"])
+    for sm in sims:
+        sm.close()
