@@ -55,6 +55,13 @@ class PlanEnv:
         self._st_keys, self._st_vals = [], []  # status log
         self._ar_keys, self._ar_vals = [], []  # arrival log (first arrival per key after compaction)
         self.failures: list[str] = []
+        # transport "tcp" (a test parameter): application data goes through TCP mode (DESIGN.md
+        # 2.11); a step then reports the writes that completed, at their last segment's arrival
+        self.tcp = self.params.get("transport", "message") == "tcp"
+        if self.tcp:
+            self.sim.tcp_enable()
+            self._tw_keys = []                     # write id -> key, in send order
+            self._tw_seen = np.zeros(0, bool)      # writes already reported
         self.sidecar.initialize(0)
 
     def close(self):
@@ -105,12 +112,18 @@ class PlanEnv:
             self._pend = [(t[keep], *[c[keep] for c in cols])] if keep.any() else []
             if due.any():
                 src, dst, seq, size = (c[due] for c in cols)
-                self.sim.enqueue(src, dst, seq, size, t[due])
+                if self.tcp:
+                    self.sim.tcp_send(src, dst, seq, size, t[due])
+                    self._tw_keys.append(self.key(src, seq))
+                else:
+                    self.sim.enqueue(src, dst, seq, size, t[due])
                 staged_keys = self.key(src, seq)
             else:
                 staged_keys = np.zeros(0, np.uint64)
         else:
             staged_keys = np.zeros(0, np.uint64)
+        if self.tcp:
+            return self._step_tcp(t_end)
         self.sim.advance(t_end)
         if len(staged_keys):
             self._st_keys.append(staged_keys)
@@ -120,6 +133,32 @@ class PlanEnv:
             self._ar_keys.append(self.key(d["src"], d["seq"]))
             self._ar_vals.append(d["t_deliver"])
         return d
+
+    def _step_tcp(self, t_end: int) -> dict:
+        """One window in TCP mode: the writes that completed in it as deliveries (src, dst, seq =
+        the write's key, t_deliver = its last segment's arrival); failed writes enter the status
+        log (TIMEOUT as LOST, REFUSED as REJECTED)."""
+        self.sim.advance(t_end)
+        self.sim.tcp_react()
+        st, t = self.sim.tcp_writes()
+        keys = np.concatenate(self._tw_keys) if self._tw_keys else np.zeros(0, np.uint64)
+        self._tw_keys = [keys] if len(keys) else []
+        seen = np.zeros(len(st), bool)
+        seen[:len(self._tw_seen)] = self._tw_seen
+        new = (st != A.TCP_PENDING) & ~seen
+        self._tw_seen = seen | new
+        ok = new & (st == A.TCP_DELIVERED)
+        bad = new & (st != A.TCP_DELIVERED)
+        if bad.any():
+            self._st_keys.append(keys[bad])
+            self._st_vals.append(np.where(st[bad] == A.TCP_TIMEOUT, A.ST_LOST, A.ST_REJECTED).astype(np.uint8))
+        if ok.any():
+            self._ar_keys.append(keys[ok])
+            self._ar_vals.append(t[ok])
+        order = np.argsort(t[ok], kind="stable")
+        k = keys[ok][order]
+        return {"src": (k >> np.uint64(32)).astype(np.uint32), "seq": (k & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                "t_deliver": t[ok][order]}
 
     def _compact(self, keys, vals, first_min: bool):
         if len(keys) > 1 or (keys and first_min):

@@ -191,3 +191,56 @@ def test_tcp_random_oracle_properties(oracle):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_tcp_random_hip_matches_oracle(hip, oracle, seed):
     _same(run_random(hip, seed), run_random(oracle, seed))
+
+
+def _pingpong_tcp(binding):
+    """plans/network/pingpong.go over TCP mode: the reference's RTT windows hold ([200, 215] ms at
+    100 ms egress latency, [20, 35] ms at 10 ms) - the plan's data is 1-byte writes on one
+    connection, so segmentation adds only the 52 header bytes."""
+    from testground_amd import plans as P
+    env = P.PlanEnv(2, seed=1, params={"transport": "tcp"}, binding=binding)
+    ok = P.pingpong(env)
+    rtts = getattr(env, "rtts", [])
+    stats = env.sim.tcp_stats()
+    env.close()
+    return ok, rtts, stats
+
+
+def test_pingpong_over_tcp_oracle(oracle):
+    ok, rtts, stats = _pingpong_tcp(oracle)
+    assert ok.all() and len(rtts) == 2 and stats["writes"] > 0 and stats["retransmissions"] == 0
+
+
+@pytest.mark.gpu
+def test_pingpong_over_tcp_hip(hip, oracle):
+    a, b = _pingpong_tcp(hip), _pingpong_tcp(oracle)
+    assert a[0].all() and [list(x) for x in a[1]] == [list(x) for x in b[1]] and a[2] == b[2]
+
+
+def _lossy_rpc(binding):
+    """Request / reply over a 30 %-loss link in TCP mode: every exchange completes (the lost
+    segments are retransmitted after 200 ms, 400 ms, ...), and the RTTs fall on the retransmission
+    grid - base RTT + k * 200 ms - instead of being lost as in the message-level model."""
+    from testground_amd import plans as P
+    from testground_amd.network import MS as NMS
+    env = P.PlanEnv(8, seed=2, params={"transport": "tcp"}, binding=binding)
+    for g in range(8):
+        env.sim.set_shape(g, make_shape(latency_ns=5 * MS, loss=30.0))
+    src = np.arange(8)
+    ok, rtt = env.rpc(src, (src + 1) % 8, 100, 100, env.sim.now, 10_000 * NMS)
+    env.close()
+    return ok, rtt
+
+
+def test_lossy_rpc_over_tcp_oracle(oracle):
+    ok, rtt = _lossy_rpc(oracle)
+    assert ok.all()
+    extra = (rtt - 10 * MS) % (200 * MS)
+    assert np.all(rtt >= 10 * MS) and np.all((extra <= 1 * MS) | (extra >= 199 * MS))
+    assert rtt.max() >= 210 * MS   # some exchange needed a retransmission
+
+
+@pytest.mark.gpu
+def test_lossy_rpc_over_tcp_hip(hip, oracle):
+    a, b = _lossy_rpc(hip), _lossy_rpc(oracle)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
