@@ -164,6 +164,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     # config 5 (not the headline): 1M-instance random-regular pubsub flood, one window per step
     p.add_argument("--workload", choices=("storm", "flood"), default="storm")
+    p.add_argument("--tcp", action="store_true",
+                   help="storm over TCP mode (DESIGN.md 2.11): writes, retransmissions, one reaction per window")
     p.add_argument("--flood-instances", type=int, default=1_000_000)
     p.add_argument("--flood-size", type=int, default=512)
     p.add_argument("--pub-every", type=int, default=4, help="windows between publication waves (flood)")
@@ -265,9 +267,20 @@ def main():
     spread, rtt = int(args.spread_ms * MS), int(args.rtt_ms * MS)
     N, F = args.instances, args.fanout
 
+    if args.tcp:
+        if world > 1:
+            raise SystemExit("--tcp: TCP mode needs a single-shard context")
+        rounds = args.warmup + max(3, min(10, args.warmup)) + args.steps + 1
+        sim.tcp_enable(max_writes=rounds * N * F, max_segments=rounds * N * F)
+
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
         # step issues its launches without any host round trip (sharded: the same calls, collective)
+        if args.tcp:  # the same round as TCP writes; the reaction reads one counter back per window
+            sim.tcp_gen_storm_round(r, T_NOW, F, args.size, spread, r)
+            sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
+            sim.tcp_react()
+            return
         sim.gen_storm_round(r, T_NOW, F, args.size, spread, r)
         sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
 
@@ -291,6 +304,7 @@ def main():
     first = args.warmup + probe
 
     s0 = sim.stats()
+    tcp0 = sim.tcp_stats() if args.tcp else None
     sim_t0 = sim.now
     sim.sync()
     torch.cuda.synchronize()
@@ -303,6 +317,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     s1 = sim.stats()
+    tcp1 = sim.tcp_stats() if args.tcp else None
     sim_t1 = sim.now
     prof = sim.profile_read()[dominant]
     delta = {k: s1[k] - s0[k] for k in s1}
@@ -321,9 +336,19 @@ def main():
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
                     elapsed)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.tcp:
         cpu = cpu_baseline(args, shapes)
 
+    if rank == 0 and args.tcp:
+        dt = {k: tcp1[k] - tcp0[k] for k in tcp1}
+        print(json.dumps({
+            "metric": "TCP writes delivered/sec (100k-inst storm over TCP mode, DESIGN.md 2.11)",
+            "value": dt["delivered"] / elapsed, "unit": "writes/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "packets_delivered_per_s": delivered / elapsed, "tcp_in_timed_steps": dt,
+            "dtype": "int64", "data": "synthetic", "kernels_probe": warm_kernels}), flush=True)
+        sim.close()
+        return
     if rank == 0:
         line = {
             "metric": METRIC,

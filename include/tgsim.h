@@ -401,7 +401,7 @@ typedef struct tgsim_tcp_config {
   int64_t rto_ns;         /* first retransmission timeout; 0 = 200 ms (Linux TCP_RTO_MIN) */
   uint32_t max_attempts;  /* attempts per segment, 1..16; 0 = 16 */
   uint32_t reserved;
-  uint64_t max_writes;    /* write-table capacity over the run; 0 = 2^22 */
+  uint64_t max_writes;    /* write-table capacity over the run; 0 = 2^22, at most 2^28 */
   uint64_t max_segments;  /* segment-table capacity over the run; 0 = 2^24 */
 } tgsim_tcp_config;
 
@@ -422,6 +422,10 @@ int tgsim_tcp_react(tgsim_ctx* ctx, size_t* n_completed);
 /* Per write id: state TGSIM_TCP_* and time (arrival of its last segment, or the failure time). */
 int tgsim_tcp_writes(tgsim_ctx* ctx, uint8_t* state_out, int64_t* t_out, size_t cap, size_t* n);
 int tgsim_tcp_get_stats(tgsim_ctx* ctx, tgsim_tcp_stats* out);
+/* tgsim_gen_storm_round as TCP writes (TCP mode; size <= mss: one segment per write), generated on
+ * the device: the round's messages become writes with ids in generation order (instance-major). */
+int tgsim_tcp_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                              int64_t spread_ns, uint32_t state);
 
 #ifdef __cplusplus
 }

@@ -1149,8 +1149,24 @@ int tgo_advance_to_barrier(tgo_ctx* c, uint32_t w, int64_t offset) {
 /* Instance g picks `fanout` distinct peers != g by Philox (rejection on repeats), sends `size` bytes
  * to each at t0 + U[0, spread), and signals `state` at its last send (the SignalAndWait pattern of
  * plans/benchmarks/benchmarks.go:122-141 around a storm round, plans/benchmarks/storm.go:150-197). */
+static int gen_storm_impl(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                          int64_t spread_ns, uint32_t state, int tcp);
 int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                         int64_t spread_ns, uint32_t state) {
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_gen_storm_round");
+  return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state, 0);
+}
+
+/* The storm round as TCP writes (one segment each: size <= mss), staged like tgo_tcp_send. */
+int tgo_tcp_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                            int64_t spread_ns, uint32_t state) {
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (size > c->tcp.mss) return fail(c, TGSIM_EINVAL, "a storm write must fit one segment");
+  return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state, 1);
+}
+
+static int gen_storm_impl(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                          int64_t spread_ns, uint32_t state, int tcp) {
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
   if (t0 == TGSIM_T_NOW) t0 = c->now;
   size_t n = (size_t)c->nloc * fanout;
@@ -1188,7 +1204,7 @@ int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout,
     sst[l] = state; sin[l] = g; stt[l] = tmax;
   }
   tgsim_msg_soa m = {src, dst, seq, sz, ts};
-  rc = tgo_enqueue(c, &m, n);
+  rc = tcp ? tgo_tcp_send(c, &m, n) : enqueue_impl(c, &m, n);
   /* single shard, or sharded with a transport (the batch is gathered: replicated sync state) */
   if (!rc && (c->S == 1 || c->has_tr)) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
   if (!rc && c->S > 1 && !c->has_tr) { /* sharded: the caller MAX-reduces the local release across shards */
@@ -1410,7 +1426,7 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   if (!t.max_attempts) t.max_attempts = 16;
   if (!t.max_writes) t.max_writes = 1u << 22;
   if (!t.max_segments) t.max_segments = 1u << 24;
-  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28))
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28))
     return fail(c, TGSIM_EINVAL, "bad TCP configuration");
   c->tcp = t;
   c->tcp_on = 1;

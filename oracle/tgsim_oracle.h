@@ -62,6 +62,8 @@ int tgo_tcp_send(tgo_ctx* ctx, const tgsim_msg_soa* writes, size_t n);
 int tgo_tcp_react(tgo_ctx* ctx, size_t* n_completed);
 int tgo_tcp_writes(tgo_ctx* ctx, uint8_t* state_out, int64_t* t_out, size_t cap, size_t* n);
 int tgo_tcp_get_stats(tgo_ctx* ctx, tgsim_tcp_stats* out);
+int tgo_tcp_gen_storm_round(tgo_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                            int64_t spread_ns, uint32_t state);
 int tgo_advance_begin(tgo_ctx* ctx, int64_t t_end);
 /* host buffers, same layout as tgsim_exchange_buffers (peer-major, header record per peer) */
 int tgo_exchange_buffers(tgo_ctx* ctx, void** send, void** recv, size_t* bytes);

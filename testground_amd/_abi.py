@@ -159,6 +159,7 @@ _SIGS = {
     "tcp_react": (C.c_int, [P, C.POINTER(C.c_size_t)]),
     "tcp_writes": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "tcp_get_stats": (C.c_int, [P, C.POINTER(TcpStats)]),
+    "tcp_gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {

@@ -54,20 +54,27 @@ struct TopicIndex {
 // TCP mode (tgsim_tcp_*): write and segment tables, two lists of segments with a
 // retransmission scheduled (the current one is released at the next window start, survivors move
 // to the other), and counters.
+constexpr int kTcpArriveBlocks = 2048;  // k_tcp_arrive's grid (= TcpDev::part entries)
 struct TcpScalars {
   uint32_t pend_n[2];             // entries of the two pending lists
   uint32_t done;                  // writes finished by the running reaction
-  uint32_t pad;
+  uint32_t pend_max;              // most retransmissions pending for one sender (queue-limit bound)
   unsigned long long retx, delivered, failed, released;
 };
 struct TcpDev {
   uint32_t *w_src = nullptr, *w_dst = nullptr, *w_rem = nullptr, *w_state = nullptr;
-  int64_t* w_tarr = nullptr;      // latest segment arrival (atomicMax)
+  int64_t* w_tarr = nullptr;      // delivery time (the latest segment's arrival); INT64_MIN until delivered
+  int64_t* w_tmax = nullptr;      // latest arrival so far of a multi-segment write (atomicMax)
   int64_t* w_fail = nullptr;      // earliest failure key t * 2 + (timeout ? 1 : 0) (atomicMin)
-  uint32_t *s_w = nullptr, *s_wire = nullptr, *s_att = nullptr, *s_out = nullptr, *s_flags = nullptr,
-           *s_mark = nullptr;
+  uint32_t* s_w = nullptr;        // write (bits 0-27) | copies of the current attempt << 28 | kSoleSeg
+  uint32_t *s_wire = nullptr, *s_att = nullptr, *s_out = nullptr, *s_mark = nullptr;
   int64_t *s_tatt = nullptr, *s_arr = nullptr, *s_tlast = nullptr;
+  // per-window decision bits: retransmissions over the packets (bm_s) and the deliveries (bm_r),
+  // duplicated deliveries (bm_d); per-block partial counts of k_tcp_arrive
+  uint64_t *bm_s = nullptr, *bm_r = nullptr, *bm_d = nullptr;
+  uint32_t* part = nullptr;
   uint32_t* pend[2] = {nullptr, nullptr};
+  uint32_t* pend_by = nullptr;    // [N] retransmissions pending per sender
   TcpScalars* sc = nullptr;
   uint32_t mss = 0, hdr = 0, max_att = 0;
   int64_t rto = 0;
@@ -266,6 +273,8 @@ hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, co
 // window start: pend[cur] entries due before the window's end staged behind sc->n_msgs_dev (which
 // the caller has set), the others moved to pend[cur ^ 1]
 hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_pending, bool base_dev, uint32_t base_host);
+// TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
+hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),

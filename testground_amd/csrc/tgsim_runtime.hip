@@ -99,6 +99,7 @@ struct tgsim_ctx {
   uint64_t tw_n = 0, tsg_n = 0;       // writes / segments so far
   uint32_t tcp_cur = 0, tcp_epoch = 0;
   uint32_t tcp_pend_h = 0;            // retransmissions pending after the last reaction
+  uint32_t tcp_pend_max_h = 0;        // ... of the sender with the most
   tgsim_tcp_stats tstats{};
   bool any_dup = false;
   // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
@@ -990,7 +991,7 @@ static int begin_common(tgsim_ctx* c) {
     if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
     if (c->tcp_pend_h) {  // due retransmissions join the staged packets behind a device-side count
       HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->tcp_pend_h, c->staged_dev, c->n_staged), "tcp release");
-      c->win_m_extra += c->tcp_pend_h;  // queue-limit test: any sender may hold all of them
+      c->win_m_extra += c->tcp_pend_max_h;  // queue-limit test: the most any one sender releases
       c->staged_dev = true;
       c->tcp_cur ^= 1u;
     }
@@ -1400,8 +1401,16 @@ extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
 
 // ============================== workloads ====================================================
 
+static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size, int64_t spread_ns,
+                          uint32_t state);
 extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {
+  if (c && c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_gen_storm_round");
+  return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state);
+}
+
+static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size, int64_t spread_ns,
+                          uint32_t state) {
   if (!c) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
@@ -1788,24 +1797,28 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (!t.max_attempts) t.max_attempts = 16;
   if (!t.max_writes) t.max_writes = 1u << 22;
   if (!t.max_segments) t.max_segments = 1u << 24;
-  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > 0xFFFFFFFFull)
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28))
     return fail(c, TGSIM_EINVAL, "bad TCP configuration");
   TcpDev& d = c->td;
   const size_t W = t.max_writes, S = t.max_segments;
   if (dalloc(c, &d.w_src, W) || dalloc(c, &d.w_dst, W) || dalloc(c, &d.w_rem, W) || dalloc(c, &d.w_state, W) ||
-      dalloc(c, &d.w_tarr, W) || dalloc(c, &d.w_fail, W) || dalloc(c, &d.s_w, S) || dalloc(c, &d.s_wire, S) ||
-      dalloc(c, &d.s_att, S) || dalloc(c, &d.s_out, S) || dalloc(c, &d.s_flags, S) || dalloc(c, &d.s_mark, S) ||
+      dalloc(c, &d.w_tarr, W) || dalloc(c, &d.w_tmax, W) || dalloc(c, &d.w_fail, W) || dalloc(c, &d.s_w, S) || dalloc(c, &d.s_wire, S) ||
+      dalloc(c, &d.s_att, S) || dalloc(c, &d.s_out, S) || dalloc(c, &d.s_mark, S) ||
       dalloc(c, &d.s_tatt, S) || dalloc(c, &d.s_arr, S) || dalloc(c, &d.s_tlast, S) || dalloc(c, &d.pend[0], S) ||
-      dalloc(c, &d.pend[1], S) || dalloc(c, &d.sc, (size_t)1))
+      dalloc(c, &d.pend[1], S) || dalloc(c, &d.pend_by, (size_t)c->N) || 
+      dalloc(c, &d.bm_s, (size_t)c->d.cap_msgs / 64 + 1) || dalloc(c, &d.bm_r, (size_t)kNSub * c->d.subcap / 64 + 1) ||
+      dalloc(c, &d.bm_d, (size_t)kNSub * c->d.subcap / 64 + 1) || dalloc(c, &d.part, (size_t)kTcpArriveBlocks) ||
+      dalloc(c, &d.sc, (size_t)1))
     return TGSIM_ENOMEM;
   hipStream_t st = c->d.stream;
   HIPCK(c, hipMemsetAsync(d.w_state, 0, W * 4, st), "tcp init");
   HIPCK(c, hipMemsetAsync(d.s_att, 0, S * 4, st), "tcp init");
   HIPCK(c, hipMemsetAsync(d.s_out, 0, S * 4, st), "tcp init");
-  HIPCK(c, hipMemsetAsync(d.s_flags, 0, S * 4, st), "tcp init");
   HIPCK(c, hipMemsetAsync(d.s_mark, 0, S * 4, st), "tcp init");
   HIPCK(c, hipMemsetAsync(d.sc, 0, sizeof(TcpScalars), st), "tcp init");
+  HIPCK(c, hipMemsetAsync(d.pend_by, 0, (size_t)c->N * 4, st), "tcp init");
   hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.w_tarr, W, INT64_MIN);
+  hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.w_tmax, W, INT64_MIN);
   hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.w_fail, W, INT64_MAX);
   hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.s_arr, S, INT64_MAX);
   hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.s_tlast, S, INT64_MIN);
@@ -1844,7 +1857,9 @@ extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
     for (uint32_t j = 0; j < ns; ++j, ++k) {
       const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
       const uint32_t sid = (uint32_t)(c->tsg_n + k);
-      s2[k] = (uint32_t)(c->tw_n + i); s2[nseg + k] = pay + c->tcp.header_bytes; s_t[k] = m->t_send[i];
+      // the write, and whether this is its only segment (tgsim_tcp.hip kSoleSeg)
+      s2[k] = (uint32_t)(c->tw_n + i) | (ns == 1 ? 0x80000000u : 0u);
+      s2[nseg + k] = pay + c->tcp.header_bytes; s_t[k] = m->t_send[i];
       p_src[k] = m->src[i]; p_dst[k] = m->dst[i]; p_seq[k] = sid << 4; p_size[k] = pay + c->tcp.header_bytes;
     }
   }
@@ -1892,6 +1907,7 @@ extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
   int rc = sync_and_check(c);
   if (rc) return rc;
   c->tcp_pend_h = ts.pend_n[c->tcp_cur];
+  c->tcp_pend_max_h = ts.pend_max;
   c->tcp_need_react = false;
   c->tstats.retransmissions = ts.retx;
   c->tstats.delivered = ts.delivered;
@@ -1919,7 +1935,8 @@ extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t
   }
   for (size_t i = 0; i < W; ++i) {
     // a failed write reports its earliest failure (key t * 2 + timeout), whatever failed first
-    uint32_t s_i = st[i];
+    // a delivered write is marked by its time alone (tgsim_tcp.hip tcp_arrived)
+    uint32_t s_i = ta[i] != INT64_MIN ? (uint32_t)TGSIM_TCP_DELIVERED : st[i];
     int64_t t_i = ta[i];
     if (s_i != TGSIM_TCP_PENDING && s_i != TGSIM_TCP_DELIVERED) {
       t_i = tf[i] >> 1;
@@ -1936,5 +1953,27 @@ extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t
 extern "C" int tgsim_tcp_get_stats(tgsim_ctx* c, tgsim_tcp_stats* out) {
   if (!c || !out) return TGSIM_EINVAL;
   *out = c->tstats;
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_tcp_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                         int64_t spread_ns, uint32_t state) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
+  if (size > c->tcp.mss) return fail(c, TGSIM_EINVAL, "a storm write must fit one segment");
+  if (fanout == 0 || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
+  const uint64_t n = (uint64_t)c->nloc * fanout;
+  if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + n > c->tcp.max_segments)
+    return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  const uint32_t base = c->n_staged;
+  int rc = gen_storm_impl(c, round, t0, fanout, size, spread_ns, state);
+  if (rc) return rc;
+  HIPCK(c, launch_tcp_adopt(c->d, c->td, base, (uint32_t)n, (uint32_t)c->tw_n, (uint32_t)c->tsg_n), "tcp adopt");
+  c->tw_n += n;
+  c->tsg_n += n;
+  c->tstats.writes += n;
+  c->tstats.segments += n;
+  c->tstats.packets += n;
   return TGSIM_OK;
 }

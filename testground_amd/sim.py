@@ -181,6 +181,9 @@ class Simulator:
         self._check(self.lib.tcp_writes(self._ctx, _ptr(st), _ptr(t), n.value, C.byref(n)))
         return st, t
 
+    def tcp_gen_storm_round(self, round_: int, t0: int, fanout: int, size: int, spread_ns: int, state: int) -> None:
+        self._check(self.lib.tcp_gen_storm_round(self._ctx, round_, t0, fanout, size, spread_ns, state))
+
     def tcp_stats(self) -> dict:
         s = A.TcpStats()
         self._check(self.lib.tcp_get_stats(self._ctx, C.byref(s)))

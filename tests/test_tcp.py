@@ -244,3 +244,40 @@ def test_lossy_rpc_over_tcp_oracle(oracle):
 def test_lossy_rpc_over_tcp_hip(hip, oracle):
     a, b = _lossy_rpc(hip), _lossy_rpc(oracle)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def run_tcp_storm(b, seed=4, n=400, rounds=6):
+    """The storm plan over TCP mode (plans/benchmarks/storm.go dials and writes 1 KiB per peer):
+    tgsim_tcp_gen_storm_round generates each round as writes on the device, SignalAndWait ends
+    the window, and the reaction recovers the 10 % lost segments. Drained afterwards."""
+    rng = np.random.default_rng(seed)
+    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18,
+                            max_states=64), binding=b)
+    s.tcp_enable(max_attempts=5, rto_ns=30 * MS)
+    for g in range(n):
+        s.set_shape(g, make_shape(latency_ns=int(rng.integers(5, 21)) * MS, jitter_ns=2 * MS, loss=10.0,
+                                  bandwidth_bps=10_000_000))
+    for r in range(rounds):
+        s.tcp_gen_storm_round(r, A.T_NOW, 8, 1024, 5 * MS, r)
+        w = s.barrier(r, n, A.T_NOW)
+        s.advance_to_barrier(w, 1 * MS)
+        s.tcp_react()
+    for _ in range(40):
+        s.advance(s.now + 20 * MS)
+        s.tcp_react()
+    st, t = s.tcp_writes()
+    out = (st, t, s.tcp_stats(), s.stats()["delivered"])
+    s.close()
+    return out
+
+
+def test_tcp_storm_oracle(oracle):
+    st, t, stats, _ = run_tcp_storm(oracle)
+    assert stats["writes"] == 6 * 400 * 8 and stats["retransmissions"] > 0.05 * stats["writes"]
+    assert np.all(st != A.TCP_PENDING) and (st == A.TCP_DELIVERED).mean() > 0.99
+
+
+@pytest.mark.gpu
+def test_tcp_storm_hip_matches_oracle(hip, oracle):
+    a, b = run_tcp_storm(hip), run_tcp_storm(oracle)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]

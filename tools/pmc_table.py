@@ -10,8 +10,8 @@ import numpy as np
 v = defaultdict(lambda: defaultdict(list))
 for path in sys.argv[1:]:
     for row in csv.DictReader(open(path)):
-        name = re.sub(r"\(.*", "", row["Kernel_Name"]).replace("tgsim::", "").replace("void ", "")
-        name = name.replace("(anonymous namespace)::", "")
+        name = row["Kernel_Name"].replace("(anonymous namespace)::", "")
+        name = re.sub(r"\(.*", "", name).replace("tgsim::", "").replace("void ", "")
         v[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
         v[name]["_vgpr"] = [float(row["VGPR_Count"])]
         v[name]["_lds"] = [float(row["LDS_Block_Size"])]
