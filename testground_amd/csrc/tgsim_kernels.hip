@@ -19,7 +19,7 @@
 namespace tgsim {
 
 const char* const kKernelNames[KID_COUNT] = {
-    "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_rows_rest", "k_radix_scatter",
+    "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
     "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit"};
 
@@ -1217,10 +1217,10 @@ __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, uint3
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
-                                                          tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                          const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
-                                                          uint32_t lo, uint32_t nloc) {
+__device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars* sc, const tgsim_record* L,
+                                                   tgsim_record* arena, uint32_t* dirs, uint32_t slots,
+                                                   const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                   uint32_t lo, uint32_t nloc) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   const uint64_t off = sc->ins_off;
@@ -2016,7 +2016,14 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
                                                         const uint2* kv, uint32_t* kscr,
                                                         uint32_t* vscr, uint32_t* kout, uint32_t* vout, BktDiv bd,
                                                         uint32_t B, uint32_t K, uint32_t* off, uint32_t* off2,
-                                                        uint32_t* medium, LargeSeg* large, DevScalars* sc) {
+                                                        uint32_t* medium, LargeSeg* large, DevScalars* sc,
+                                                        uint32_t* hist, uint32_t* tot) {
+  // blocks [B, B + slots): the wheel insert's per-slot scans of the L histogram (k_local_hist made it;
+  // nothing here reads it), one slot row each - they share this launch instead of a dependent one
+  if (blockIdx.x >= B) {
+    radix_rows_body(hist, tot, blockIdx.x - B);
+    return;
+  }
   __shared__ BktFusedSmem sm;
   BktHead h;
   tgsim_record rec[kIPT];
@@ -2931,21 +2938,24 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
   rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x, gridDim.x);
 }
 
-// Window end, third pass: the deliveries' long inboxes (k_rest<Emit>, after k_emit_bucket) and the
-// wheel insert's per-slot scans (k_radix_rows, after the histogram) are independent, so they share
-// one launch: blocks [0, nrows) scan slot rows, the rest are k_rest's. A launch that finds nothing
-// to do still costs ~4.5 us at a dependent-launch boundary.
-__global__ __launch_bounds__(kBlock) void k_rows_rest(uint32_t* hist, uint32_t* tot, uint32_t nrows, EmitPolicy p,
-                                                      const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
-                                                      const uint32_t* medium, const LargeSeg* large,
-                                                      const DevScalars* sc, uint64_t* K1a, uint64_t* K2a,
-                                                      uint32_t* K3a, uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
+// Window end, last pass: the wheel insert (blocks [0, kRadixBlocks)) and the deliveries' long
+// inboxes (k_rest<Emit>, the other blocks) are independent after k_emit_bucket, so they share one
+// launch: a launch that finds nothing to do still costs ~4.5 us at a dependent-launch boundary
+// (DESIGN.md 5). The scatter runs one workgroup per CU, so rest_body's LDS costs it no occupancy.
+__global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
+                                                          tgsim_record* arena, uint32_t* dirs, uint32_t slots,
+                                                          const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                          uint32_t lo, uint32_t nloc, EmitPolicy p,
+                                                          const uint32_t* keys, const uint32_t* vals,
+                                                          const uint32_t* off, const uint32_t* medium,
+                                                          const LargeSeg* large, uint64_t* K1a, uint64_t* K2a,
+                                                          uint32_t* K3a, uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
   static_assert(kRadixBlocks == kBlock, "slot rows are scanned by one kBlock workgroup each");
-  if (blockIdx.x < nrows)
-    radix_rows_body(hist, tot, blockIdx.x);
+  if (blockIdx.x < (uint32_t)kRadixBlocks)
+    wheel_scatter_body(src, sc, L, arena, dirs, slots, hist, tot, pend, lo, nloc);
   else
-    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - nrows,
-              gridDim.x - nrows);
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - kRadixBlocks,
+              gridDim.x - kRadixBlocks);
 }
 
 // ============================================================================================
@@ -3398,11 +3408,12 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
   return hipSuccess;
 }
 
-// Window end: deliveries and the wheel insert of L, interleaved in four launches -
+// Window end: deliveries and the wheel insert of L, interleaved in three launches -
 //   k_local_hist   partition D by receiver bucket | histogram of L by wheel slot
-//   k_emit_bucket  one workgroup per receiver bucket: inbox order, SoA deliveries, inbox offsets
-//   k_rows_rest    per-slot scans of the L histogram | long inboxes of the deliveries
-//   k_wheel_scatter L straight into the arena in slot order (also closes the window's counters)
+//   k_emit_bucket  one workgroup per receiver bucket: inbox order, SoA deliveries, inbox offsets |
+//                  per-slot scans of the L histogram
+//   k_wheel_scatter L straight into the arena in slot order (also closes the window's counters) |
+//                  long inboxes of the deliveries
 hipError_t window_end(Dev& d) {
   if (d.S > 1) {
     Queues Q = make_queues(d);
@@ -3425,21 +3436,16 @@ hipError_t window_end(Dev& d) {
   TG_CHECK(hipGetLastError());
   {
     ProfScope ps_(d, KID_EMIT);
-    hipLaunchKernelGGL(k_emit_bucket, dim3(B), dim3(kBlock), 0, d.stream, p, srcD, d.poff, d.kv1, d.keys2,
-                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc);
-  }
-  TG_CHECK(hipGetLastError());
-  {
-    ProfScope ps_(d, KID_RADIX_ROWS);
-    hipLaunchKernelGGL(k_rows_rest, dim3(d.slots + kListBlocks), dim3(kBlock), 0, d.stream, d.hist, d.tot, d.slots,
-                       p, d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.sc, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b,
-                       d.K3b);
+    hipLaunchKernelGGL(k_emit_bucket, dim3(B + d.slots), dim3(kBlock), 0, d.stream, p, srcD, d.poff, d.kv1, d.keys2,
+                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc, d.hist,
+                       d.tot);
   }
   TG_CHECK(hipGetLastError());
   {
     ProfScope ps_(d, KID_REGION_FILL);
-    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L, d.arena,
-                       d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc);
+    hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L,
+                       d.arena, d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
+                       d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   }
   return hipGetLastError();
 }
