@@ -276,10 +276,10 @@ def main():
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
         # step issues its launches without any host round trip (sharded: the same calls, collective)
-        if args.tcp:  # the same round as TCP writes; the reaction reads one counter back per window
+        if args.tcp:  # the same round as TCP writes; the reaction is queued without a read-back
             sim.tcp_gen_storm_round(r, T_NOW, F, args.size, spread, r)
             sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
-            sim.tcp_react()
+            sim.tcp_react(wait=False)
             return
         sim.gen_storm_round(r, T_NOW, F, args.size, spread, r)
         sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)

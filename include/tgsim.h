@@ -417,7 +417,10 @@ int tgsim_tcp_enable(tgsim_ctx* ctx, const tgsim_tcp_config* cfg);
 int tgsim_tcp_send(tgsim_ctx* ctx, const tgsim_msg_soa* writes, size_t n);
 /* After every window, before staging for the next: account the window's packets (queued copies) and
  * deliveries (arrivals, corrupt copies), schedule retransmissions (staged by the window that covers
- * their time), complete writes. *n_completed = writes delivered or failed in this call (may be NULL). */
+ * their time), complete writes. *n_completed = writes delivered or failed in this call. NULL: the
+ * reaction is only queued on the context stream (no synchronisation; its counters reach
+ * tgsim_tcp_get_stats / tgsim_tcp_writes, which synchronise, and device errors the next synchronising
+ * call). */
 int tgsim_tcp_react(tgsim_ctx* ctx, size_t* n_completed);
 /* Per write id: state TGSIM_TCP_* and time (arrival of its last segment, or the failure time). */
 int tgsim_tcp_writes(tgsim_ctx* ctx, uint8_t* state_out, int64_t* t_out, size_t cap, size_t* n);

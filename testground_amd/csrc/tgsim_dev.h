@@ -58,7 +58,7 @@ constexpr int kTcpArriveBlocks = 2048;  // k_tcp_arrive's grid (= TcpDev::part e
 struct TcpScalars {
   uint32_t pend_n[2];             // entries of the two pending lists
   uint32_t done;                  // writes finished by the running reaction
-  uint32_t pend_max;              // most retransmissions pending for one sender (queue-limit bound)
+  uint32_t pad;
   unsigned long long retx, delivered, failed, released;
 };
 struct TcpDev {
@@ -74,7 +74,7 @@ struct TcpDev {
   uint64_t *bm_s = nullptr, *bm_r = nullptr, *bm_d = nullptr;
   uint32_t* part = nullptr;
   uint32_t* pend[2] = {nullptr, nullptr};
-  uint32_t* pend_by = nullptr;    // [N] retransmissions pending per sender
+  uint32_t* pend_by = nullptr;    // [N] retransmissions pending (or released into the open window) per sender
   TcpScalars* sc = nullptr;
   uint32_t mss = 0, hdr = 0, max_att = 0;
   int64_t rto = 0;
@@ -228,7 +228,7 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
                                             uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
-hipError_t launch_pend_max(Dev& d);
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t mult);  // retx: TCP pending per sender
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part
 hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);
@@ -272,7 +272,7 @@ hipError_t launch_flood_mark(Dev& d, uint32_t n);
 hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch);
 // window start: pend[cur] entries due before the window's end staged behind sc->n_msgs_dev (which
 // the caller has set), the others moved to pend[cur ^ 1]
-hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_pending, bool base_dev, uint32_t base_host);
+hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, uint32_t base_host);
 // TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)

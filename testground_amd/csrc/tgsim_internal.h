@@ -111,11 +111,13 @@ constexpr int ST_OVERLIMIT = 13;  // a row counter only ([kNSub][16] rows; ST_DE
 struct Heavy {
   const uint32_t* pend;   // nullptr: the host proved no sender can reach the limit this window
   const uint32_t* inbox;  // [nloc + 1] the last window's inbox offsets (flood forwards), or nullptr
+  const uint32_t* retx;   // TCP mode: [nloc] retransmissions pending or released into this window
   uint32_t m_uniform, m_inbox, mult;
   __host__ __device__ bool of(uint32_t l) const {
     if (!pend) return false;
     uint64_t m = m_uniform;
     if (m_inbox) m += (uint64_t)m_inbox * (inbox[l + 1] - inbox[l]);
+    if (retx) m += retx[l];
     return (uint64_t)pend[l] + mult * m > TGSIM_NETEM_LIMIT;
   }
 };

@@ -98,8 +98,14 @@ struct tgsim_ctx {
   TcpDev td;
   uint64_t tw_n = 0, tsg_n = 0;       // writes / segments so far
   uint32_t tcp_cur = 0, tcp_epoch = 0;
-  uint32_t tcp_pend_h = 0;            // retransmissions pending after the last reaction
-  uint32_t tcp_pend_max_h = 0;        // ... of the sender with the most
+  // the reactions' counters land in two pinned snapshots (read once their event has completed);
+  // nothing on the window path reads them (the queue-limit bound folds the pending retransmissions
+  // into the occupancy: tgsim_tcp.hip)
+  TcpScalars* tcp_snap = nullptr;
+  hipEvent_t tcp_ev[2] = {nullptr, nullptr};
+  uint32_t tcp_snap_cur[2] = {0, 0};
+  bool tcp_snap_live[2] = {false, false};
+  uint32_t tcp_snap_slot = 0;         // the next snapshot's slot (the other one holds the latest)
   tgsim_tcp_stats tstats{};
   bool any_dup = false;
   // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
@@ -300,6 +306,9 @@ extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->d.h_sc) (void)hipHostFree(c->d.h_sc);
+  if (c->tcp_snap) (void)hipHostFree(c->tcp_snap);
+  for (hipEvent_t e : c->tcp_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->own_stream && c->d.stream) (void)hipStreamDestroy(c->d.stream);
   delete c;
 }
@@ -953,7 +962,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
   const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->fl_npubs;
   bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   if (gate && !c->pend_exact) {  // inconclusive: refresh the bound with the exact maximum (one sync)
-    HIPCK(c, launch_pend_max(d), "pend max");
+    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, (uint32_t)mult), "pend max");
     HIPCK(c, sync_scalars(d), "sync");
     c->pend_bound = d.h_sc->pend_max;
     c->pend_exact = true;
@@ -969,6 +978,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
     }
     d.heavy.pend = d.pend;
     d.heavy.inbox = c->win_m_inbox ? d.inbox : nullptr;
+    d.heavy.retx = c->tcp_on ? c->td.pend_by : nullptr;  // single shard: local = global ids
     d.heavy.m_uniform = (uint32_t)m_uniform;
     d.heavy.m_inbox = c->win_m_inbox;
     d.heavy.mult = (uint32_t)mult;
@@ -989,12 +999,11 @@ static int begin_common(tgsim_ctx* c) {
   if (rc) return rc;
   if (c->tcp_on) {
     if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
-    if (c->tcp_pend_h) {  // due retransmissions join the staged packets behind a device-side count
-      HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->tcp_pend_h, c->staged_dev, c->n_staged), "tcp release");
-      c->win_m_extra += c->tcp_pend_max_h;  // queue-limit test: the most any one sender releases
-      c->staged_dev = true;
-      c->tcp_cur ^= 1u;
-    }
+    // due retransmissions join the staged packets behind the device-side count (the pending count
+    // is device-side too, and the queue-limit test reads the per-sender counts on the device)
+    HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
+    c->staged_dev = true;
+    c->tcp_cur ^= 1u;
   }
   rc = plan_queue_limit(c);
   if (rc) return rc;
@@ -1824,6 +1833,9 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   hipLaunchKernelGGL(k_fill_i64, dim3(1024), dim3(256), 0, st, d.s_tlast, S, INT64_MIN);
   HIPCK(c, hipGetLastError(), "tcp init");
   HIPCK(c, hipStreamSynchronize(st), "tcp init");
+  if (hipHostMalloc((void**)&c->tcp_snap, 2 * sizeof(TcpScalars), hipHostMallocDefault) != hipSuccess)
+    return fail(c, TGSIM_ENOMEM, "pinned TCP snapshots");
+  for (hipEvent_t& e : c->tcp_ev) HIPCK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "tcp init");
   d.mss = t.mss; d.hdr = t.header_bytes; d.max_att = t.max_attempts; d.rto = t.rto_ns; d.cap_w = W; d.cap_s = S;
   c->tcp = t;
   c->tcp_on = true;
@@ -1892,6 +1904,8 @@ extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   return TGSIM_OK;
 }
 
+static int tcp_refresh(tgsim_ctx* c);
+
 extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
   if (n_done) *n_done = 0;
   if (!c) return TGSIM_EINVAL;
@@ -1901,20 +1915,43 @@ extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
   const bool on_dev = c->n_status_last == kStatusOnDevice;
   HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
                             on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch), "tcp react");
-  // one synchronisation: the pending count sizes the next window's release (and its queue-limit bound)
-  TcpScalars ts;
-  HIPCK(c, hipMemcpyAsync(&ts, c->td.sc, sizeof(ts), hipMemcpyDeviceToHost, c->d.stream), "tcp react");
+  c->tcp_need_react = false;
+  // the counters into the next pinned snapshot, behind the reaction on the stream
+  const uint32_t k = c->tcp_snap_slot;
+  HIPCK(c, hipMemcpyAsync(&c->tcp_snap[k], c->td.sc, sizeof(TcpScalars), hipMemcpyDeviceToHost, c->d.stream),
+        "tcp react");
+  HIPCK(c, hipEventRecord(c->tcp_ev[k], c->d.stream), "tcp react");
+  c->tcp_snap_cur[k] = c->tcp_cur;
+  c->tcp_snap_live[k] = true;
+  c->tcp_snap_slot = k ^ 1u;
+  if (!n_done) return TGSIM_OK;  // asynchronous: the counters arrive with a later synchronising call
   int rc = sync_and_check(c);
   if (rc) return rc;
-  c->tcp_pend_h = ts.pend_n[c->tcp_cur];
-  c->tcp_pend_max_h = ts.pend_max;
-  c->tcp_need_react = false;
-  c->tstats.retransmissions = ts.retx;
-  c->tstats.delivered = ts.delivered;
-  c->tstats.failed = ts.failed;
-  c->tstats.pending_retx = c->tcp_pend_h;
-  c->tstats.packets = c->tstats.segments + ts.released;
-  if (n_done) *n_done = ts.done;
+  const uint32_t done = c->tcp_snap[k].done;
+  rc = tcp_refresh(c);
+  if (rc) return rc;
+  *n_done = done;
+  return TGSIM_OK;
+}
+
+// The TCP counters from the newest completed snapshot.
+static int tcp_refresh(tgsim_ctx* c) {
+  const uint32_t latest = c->tcp_snap_slot ^ 1u, older = c->tcp_snap_slot;
+  for (uint32_t k : {latest, older}) {
+    if (!c->tcp_snap_live[k]) continue;
+    const hipError_t q = hipEventQuery(c->tcp_ev[k]);
+    if (q == hipErrorNotReady) continue;
+    HIPCK(c, q, "tcp snapshot");
+    const TcpScalars& ts = c->tcp_snap[k];
+    c->tstats.retransmissions = ts.retx;
+    c->tstats.delivered = ts.delivered;
+    c->tstats.failed = ts.failed;
+    c->tstats.pending_retx = ts.pend_n[c->tcp_snap_cur[k]];
+    c->tstats.packets = c->tstats.segments + ts.released;
+    c->tcp_snap_live[k] = false;
+    if (k == latest) c->tcp_snap_live[older] = false;  // superseded (an older one leaves the latest in flight)
+    break;
+  }
   return TGSIM_OK;
 }
 
@@ -1952,6 +1989,12 @@ extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t
 
 extern "C" int tgsim_tcp_get_stats(tgsim_ctx* c, tgsim_tcp_stats* out) {
   if (!c || !out) return TGSIM_EINVAL;
+  if (c->tcp_on && (c->tcp_snap_live[0] || c->tcp_snap_live[1])) {  // an asynchronous reaction: its counters
+    int rc = sync_and_check(c);
+    if (rc) return rc;
+    rc = tcp_refresh(c);
+    if (rc) return rc;
+  }
   *out = c->tstats;
   return TGSIM_OK;
 }

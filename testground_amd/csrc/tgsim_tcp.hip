@@ -19,6 +19,11 @@
 //                  once the window's copies are counted
 //   k_tcp_release  at the next window start: due retransmissions appended to the staged messages
 //                  (device-side count), the rest kept for a later window
+// Queue limit: a sender's pending retransmissions (pend_by, including those released into the open
+// window until their packet is accounted) join its queue occupancy in the per-window test
+// (Heavy::retx) and in the host's exact refresh, mult * (occupancy + pending): that bounds mult *
+// (the sender's unsettled segments), which only new segments raise, so the host bound needs no
+// read-back of the TCP state.
 // Device-scope atomics execute at the memory side, one request per lane, so the common case uses
 // none: a delivery reads one segment word (write, copies, one-segment flag) and stores the write's
 // time; a write is delivered once its time is set. Every decision is order-independent: the result equals the oracle's
@@ -93,10 +98,12 @@ __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict
                                                        const uint32_t* n_dev, TcpDev t) {
   const uint32_t n = n_dev ? *n_dev : n_host;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t sid = seq[i] >> 4;
+    const uint32_t sq = seq[i], sid = sq >> 4;
     const uint8_t st = status[i];
     const uint32_t q = tcp_copies(st), code = st & 0x0Fu;
     bool retx = false;
+    // a released retransmission leaves its sender's pending count once its packet is accounted
+    if (sq & 15u) atomicSub(&t.pend_by[t.w_src[t.s_w[sid] & kWMask]], 1u);
     if (q) {
       t.s_out[sid] = q;
       t.s_w[sid] = (t.s_w[sid] & ~(3u << kQShift)) | (q << kQShift);
@@ -230,22 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_collect(const uint32_t* __restri
 }
 
 __global__ __launch_bounds__(kBlock) void k_tcp_reset(TcpDev t, uint32_t cur) {
-  if (threadIdx.x == 0) { t.sc->done = 0; t.sc->pend_n[cur ^ 1u] = 0; t.sc->pend_max = 0; }
-}
-
-// the largest per-sender pending count (one atomic per block)
-__global__ __launch_bounds__(kBlock) void k_tcp_pend_max(TcpDev t, uint32_t n) {
-  __shared__ uint32_t red[kBlock / 64];
-  uint32_t mx = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) mx = max(mx, t.pend_by[i]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    mx = max(max(red[0], red[1]), max(red[2], red[3]));
-    if (mx) atomicMax(&t.sc->pend_max, mx);
-  }
+  if (threadIdx.x == 0) { t.sc->done = 0; t.sc->pend_n[cur ^ 1u] = 0; }
 }
 
 __global__ __launch_bounds__(kBlock) void k_tcp_base(DevScalars* sc, uint32_t base_host) {
@@ -265,8 +257,10 @@ __global__ __launch_bounds__(kBlock) void k_tcp_release(TcpDev t, uint32_t cur, 
       t.pend[nxt][atomicAdd(&t.sc->pend_n[nxt], 1u)] = sid;
       continue;
     }
-    atomicSub(&t.pend_by[t.w_src[w]], 1u);
-    if (t.w_state[w] != TGSIM_TCP_PENDING) continue;  // the write has failed: nothing more is sent
+    if (t.w_state[w] != TGSIM_TCP_PENDING) {  // the write has failed: nothing more is sent
+      atomicSub(&t.pend_by[t.w_src[w]], 1u);
+      continue;
+    }
     const uint32_t p = atomicAdd(&sc->n_msgs_dev, 1u);
     if (p >= cap) {
       atomicOr(&sc->err, ERR_CAP_M);
@@ -309,15 +303,13 @@ hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, co
   hipLaunchKernelGGL(k_tcp_settle, dim3(64), dim3(kBlock), 0, d.stream, d.o_seq, d.sc, t, epoch, cur);
   hipLaunchKernelGGL(k_tcp_collect, dim3(64), dim3(kBlock), 0, d.stream, d.m_seq, n_host, n_dev, d.o_seq, d.sc, t, cur,
                      (uint32_t)kTcpArriveBlocks);
-  hipLaunchKernelGGL(k_tcp_pend_max, dim3(std::min<unsigned>((d.N + kBlock - 1) / kBlock, 1024u)), dim3(kBlock), 0,
-                     d.stream, t, d.N);
   return hipGetLastError();
 }
 
-hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_pending, bool base_dev, uint32_t base_host) {
+hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, uint32_t base_host) {
   if (!base_dev) hipLaunchKernelGGL(k_tcp_base, dim3(1), dim3(kBlock), 0, d.stream, d.sc, base_host);
-  const unsigned g = std::min<unsigned>((n_pending + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
-  hipLaunchKernelGGL(k_tcp_release, dim3(g ? g : 1), dim3(kBlock), 0, d.stream, t, cur, d.sc, d.cap_msgs, d.m_src,
+  // the pending count is device-side: a fixed grid, grid-stride
+  hipLaunchKernelGGL(k_tcp_release, dim3(256), dim3(kBlock), 0, d.stream, t, cur, d.sc, d.cap_msgs, d.m_src,
                      d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }

@@ -167,7 +167,12 @@ class Simulator:
         m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
         self._check(self.lib.tcp_send(self._ctx, C.byref(m), len(t)))
 
-    def tcp_react(self) -> int:
+    def tcp_react(self, wait: bool = True) -> int:
+        """The window's TCP reaction. wait=False: asynchronous (no count returned, no read-back; the
+        counters arrive with a later synchronising call)."""
+        if not wait:
+            self._check(self.lib.tcp_react(self._ctx, None))
+            return -1
         n = C.c_size_t()
         self._check(self.lib.tcp_react(self._ctx, C.byref(n)))
         return n.value

@@ -135,7 +135,7 @@ def test_in_order_view():
     assert list(s3) == [T.REFUSED, T.REFUSED] and list(t3) == [3, 3]   # the reset fails what follows
 
 
-def run_random(b, seed, n=300, windows=60, window_ns=10 * MS):
+def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True):
     """Lossy, corrupting, duplicating, reordering links with jitter and rate limits; writes of 0 to
     9000 B over the first 30 windows. Per window: deliveries and the statuses as a sorted multiset;
     at the end the write outcomes and counters."""
@@ -159,7 +159,7 @@ def run_random(b, seed, n=300, windows=60, window_ns=10 * MS):
         s.advance(t)
         st = s.status()
         d = s.deliveries()
-        s.tcp_react()
+        s.tcp_react(wait=wait)
         out.append(dict(deliv=d, status=np.sort(st)))
     ws, wt = s.tcp_writes()
     out.append(dict(writes=(ws, wt), stats=s.tcp_stats()))
@@ -191,6 +191,13 @@ def test_tcp_random_oracle_properties(oracle):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_tcp_random_hip_matches_oracle(hip, oracle, seed):
     _same(run_random(hip, seed), run_random(oracle, seed))
+
+
+@pytest.mark.gpu
+def test_tcp_random_async_reaction_matches_oracle(hip, oracle):
+    """Reactions queued without a read-back (the host's pending bounds grow until a snapshot is
+    read): the same windows, statuses and outcomes as the oracle's synchronous reactions."""
+    _same(run_random(hip, 2, wait=False), run_random(oracle, 2))
 
 
 def _pingpong_tcp(binding):
@@ -246,7 +253,7 @@ def test_lossy_rpc_over_tcp_hip(hip, oracle):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def run_tcp_storm(b, seed=4, n=400, rounds=6):
+def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True):
     """The storm plan over TCP mode (plans/benchmarks/storm.go dials and writes 1 KiB per peer):
     tgsim_tcp_gen_storm_round generates each round as writes on the device, SignalAndWait ends
     the window, and the reaction recovers the 10 % lost segments. Drained afterwards."""
@@ -261,10 +268,10 @@ def run_tcp_storm(b, seed=4, n=400, rounds=6):
         s.tcp_gen_storm_round(r, A.T_NOW, 8, 1024, 5 * MS, r)
         w = s.barrier(r, n, A.T_NOW)
         s.advance_to_barrier(w, 1 * MS)
-        s.tcp_react()
+        s.tcp_react(wait=wait)
     for _ in range(40):
-        s.advance(s.now + 20 * MS)
-        s.tcp_react()
+        s.advance(s.now + 20 * MS, wait=wait)
+        s.tcp_react(wait=wait)
     st, t = s.tcp_writes()
     out = (st, t, s.tcp_stats(), s.stats()["delivered"])
     s.close()
@@ -278,6 +285,8 @@ def test_tcp_storm_oracle(oracle):
 
 
 @pytest.mark.gpu
-def test_tcp_storm_hip_matches_oracle(hip, oracle):
-    a, b = run_tcp_storm(hip), run_tcp_storm(oracle)
+@pytest.mark.parametrize("wait", [True, False], ids=["sync", "async"])
+def test_tcp_storm_hip_matches_oracle(hip, oracle, wait):
+    """async: every window and reaction queued without a host read-back (bench.py --tcp's loop)."""
+    a, b = run_tcp_storm(hip, wait=wait), run_tcp_storm(oracle)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
