@@ -391,16 +391,27 @@ int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
  * it); attempt a + 1 is then sent at max(t_a + rto * 2^a, the time the failure is known), up to
  * max_attempts attempts (then the write fails). A route that refuses the packet (prohibit / no
  * route) fails the write at once. A segment arrives with its first intact copy; a write completes
- * when its last segment arrives. Not modelled: ACK packets on the reverse path, congestion window,
- * fast retransmit, spurious timeouts (a copy slower than the RTO is waited for). Single-shard
- * contexts; while TCP mode is on, all traffic is TCP (tgsim_enqueue is refused). Packet seq =
- * segment id * 16 + attempt (segment ids count from 0 in send order, < 2^28). */
+ * when its last segment arrives. Single-shard contexts; while TCP mode is on, all traffic is TCP
+ * (tgsim_enqueue is refused). Packet seq = segment id * 16 + attempt (segment ids count from 0 in
+ * send order, < 2^28).
+ *
+ * acks = 1 adds the reverse path: every intact data copy the receiver gets is answered by an ACK
+ * packet (header_bytes, seq = TGSIM_TCP_ACK_BIT | the data packet's seq) sent at max(arrival, the
+ * next window's start) through the receiver's egress. Attempt a of a segment arms a timer at
+ * t_a + rto * 2^a; at the start of each window, every timer of an attempt sent in an earlier window
+ * that falls before the window's end fires unless an intact ACK of the segment arrived in an
+ * earlier window: attempt a + 1 leaves at max(timer, window start) (spurious retransmissions
+ * included), and after max_attempts attempts the segment gives up (the write fails, TIMEOUT at the
+ * timer, if it has not completed). A write's outcome is its first event in window order: a write
+ * that failed stays failed. Segment ids < 2^27. Not modelled: congestion window (IW10 never binds
+ * for writes below 14.5 KB), delayed ACKs, fast retransmit. */
+#define TGSIM_TCP_ACK_BIT 0x80000000u
 typedef struct tgsim_tcp_config {
   uint32_t mss;           /* payload bytes per segment; 0 = 1448 */
   uint32_t header_bytes;  /* wire overhead per segment (IPv4 + TCP with timestamps); 0 = 52 */
   int64_t rto_ns;         /* first retransmission timeout; 0 = 200 ms (Linux TCP_RTO_MIN) */
   uint32_t max_attempts;  /* attempts per segment, 1..16; 0 = 16 */
-  uint32_t reserved;
+  uint32_t acks;          /* 1: ACK packets on the reverse path and retransmission timers (above) */
   uint64_t max_writes;    /* write-table capacity over the run; 0 = 2^22, at most 2^28 */
   uint64_t max_segments;  /* segment-table capacity over the run; 0 = 2^24 */
 } tgsim_tcp_config;

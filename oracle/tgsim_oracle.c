@@ -220,6 +220,7 @@ struct tgo_ctx {
   struct otcpw* tw; size_t tw_n, tw_cap;
   struct otcps* tsg; size_t tsg_n, tsg_cap;
   uint32_t* tpend; size_t tpend_n, tpend_cap;
+  struct otack* tack; size_t tack_n, tack_cap;  /* acks = 1: ACK packets for the next window */
   tgsim_tcp_stats tstats;
   char err[512];
 };
@@ -228,7 +229,9 @@ typedef struct otcpw { uint32_t src, dst, remaining, state; int64_t t; } otcpw;
 typedef struct otcps {
   uint32_t w, wire, attempt, outstanding, arrived, touched;
   int64_t t_att, arrival, t_last;
+  uint32_t acked, gave_up;  /* acks = 1 */
 } otcps;
+typedef struct otack { uint32_t src, dst, seq; int64_t t; } otack;
 
 static int fail(tgo_ctx* c, int code, const char* fmt, ...) {
   if (c) { va_list ap; va_start(ap, fmt); vsnprintf(c->err, sizeof(c->err), fmt, ap); va_end(ap); }
@@ -338,7 +341,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
-  free(c->tw); free(c->tsg); free(c->tpend);
+  free(c->tw); free(c->tsg); free(c->tpend); free(c->tack);
   free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
     free(c->topics[i].inst); free(c->topics[i].t); free(c->topics[i].off); free(c->topics[i].len);
@@ -1426,7 +1429,8 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   if (!t.max_attempts) t.max_attempts = 16;
   if (!t.max_writes) t.max_writes = 1u << 22;
   if (!t.max_segments) t.max_segments = 1u << 24;
-  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28))
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28) || t.acks > 1 ||
+      (t.acks && t.max_segments > (1u << 27)))
     return fail(c, TGSIM_EINVAL, "bad TCP configuration");
   c->tcp = t;
   c->tcp_on = 1;
@@ -1462,7 +1466,7 @@ int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
     for (uint32_t j = 0; j < ns; ++j, ++k) {
       const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
       const uint32_t sid = (uint32_t)c->tsg_n++;
-      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN};
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0};
       c->tsg[sid] = g;
       src[k] = w.src; dst[k] = w.dst; seq[k] = sid << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
     }
@@ -1520,12 +1524,21 @@ static uint32_t tcp_copies(uint8_t st) {
   return q;
 }
 
+static int tcp_react_acks(tgo_ctx* c, size_t* done);
+
 int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
   size_t done = 0;
   if (n_done) *n_done = 0;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->tcp_need_react) return TGSIM_OK;
+  if (c->tcp.acks) {
+    int rc = tcp_react_acks(c, &done);
+    if (rc) return rc;
+    c->tcp_need_react = 0;
+    if (n_done) *n_done = done;
+    return TGSIM_OK;
+  }
   /* 1. the window's packets (staged arrays are intact until the next staging) */
   const omsgs* s = &c->staged;
   for (size_t i = 0; i < c->n_status; ++i) {
@@ -1572,6 +1585,51 @@ int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
   return TGSIM_OK;
 }
 
+/* acks = 1: the window's packets only refuse (a timer handles every other failure); its deliveries
+ * are data (first intact arrival, and an ACK back for every intact copy at max(arrival, the next
+ * window's start)) or ACKs (an intact one acknowledges its segment). */
+static int tcp_react_acks(tgo_ctx* c, size_t* done) {
+  const omsgs* s = &c->staged;
+  for (size_t i = 0; i < c->n_status; ++i) {
+    if (s->seq[i] & TGSIM_TCP_ACK_BIT) continue;
+    const uint8_t code = c->status[i] & 0x0Fu;
+    otcps* g = &c->tsg[s->seq[i] >> 4];
+    if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, done);
+  }
+  uint32_t* touched = (uint32_t*)malloc((c->out.n + 1) * 4);
+  if (!touched || grow((void**)&c->tack, &c->tack_cap, c->tack_n + c->out.n + 1, sizeof(otack))) {
+    free(touched);
+    return fail(c, TGSIM_ENOMEM, "oom");
+  }
+  size_t nt = 0;
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    const int intact = !(r->meta & TGSIM_F_CORRUPT);
+    otcps* g = &c->tsg[(r->seq & ~TGSIM_TCP_ACK_BIT) >> 4];
+    if (r->seq & TGSIM_TCP_ACK_BIT) {
+      if (intact) g->acked = 1;
+      continue;
+    }
+    if (!intact) continue;
+    if (r->t < g->arrival) g->arrival = r->t;
+    if (!g->touched) { g->touched = 1; touched[nt++] = (r->seq >> 4); }
+    otack a = {r->dst, r->src, TGSIM_TCP_ACK_BIT | r->seq, r->t > c->t_end ? r->t : c->t_end};
+    c->tack[c->tack_n++] = a;
+  }
+  for (size_t k = 0; k < nt; ++k) {
+    otcps* g = &c->tsg[touched[k]];
+    g->touched = 0;
+    if (g->arrived) continue;
+    g->arrived = 1;
+    otcpw* w = &c->tw[g->w];
+    if (w->state != TGSIM_TCP_PENDING) continue;  /* failed first: stays failed */
+    if (g->arrival > w->t) w->t = g->arrival;
+    if (--w->remaining == 0) tcp_finish(c, g->w, TGSIM_TCP_DELIVERED, w->t, done);
+  }
+  free(touched);
+  return TGSIM_OK;
+}
+
 typedef struct { int64_t t; uint32_t sid; } otx;
 static int cmp_otx(const void* a, const void* b) {
   const otx* x = (const otx*)a; const otx* y = (const otx*)b;
@@ -1581,7 +1639,9 @@ static int cmp_otx(const void* a, const void* b) {
 
 /* Stage the retransmissions whose time falls before t_end, in (time, segment) order; those of a
  * failed write are dropped. */
+static int tcp_release_acks(tgo_ctx* c, int64_t t_end);
 static int tcp_release(tgo_ctx* c, int64_t t_end) {
+  if (c->tcp.acks) return tcp_release_acks(c, t_end);
   if (!c->tpend_n) return TGSIM_OK;
   otx* due = (otx*)malloc(c->tpend_n * sizeof(otx));
   if (!due) return fail(c, TGSIM_ENOMEM, "oom");
@@ -1614,6 +1674,72 @@ static int tcp_release(tgo_ctx* c, int64_t t_end) {
     free(src); free(dst); free(seq); free(sz); free(ts);
   }
   free(due);
+  return rc;
+}
+
+/* acks = 1, at the start of window [now, t_end): the ACKs of the last reaction, then every timer of
+ * an attempt sent in an earlier window that falls before t_end and whose segment no ACK has reached:
+ * the next attempt at max(timer, now), or the segment gives up (TIMEOUT at the timer for a write
+ * that has not completed). Packets are staged in (time, segment) order, the ACKs first. */
+static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
+  const int64_t H = c->now;
+  int rc = TGSIM_OK;
+  if (c->tack_n) {
+    const size_t na = c->tack_n;
+    uint32_t* src = malloc(na * 4); uint32_t* dst = malloc(na * 4); uint32_t* seq = malloc(na * 4);
+    uint32_t* sz = malloc(na * 4); int64_t* ts = malloc(na * 8);
+    if (!src || !dst || !seq || !sz || !ts) rc = TGSIM_ENOMEM;
+    for (size_t i = 0; i < na && !rc; ++i) {
+      src[i] = c->tack[i].src; dst[i] = c->tack[i].dst; seq[i] = c->tack[i].seq; sz[i] = c->tcp.header_bytes;
+      ts[i] = c->tack[i].t;
+    }
+    if (!rc) {
+      tgsim_msg_soa p = {src, dst, seq, sz, ts};
+      rc = enqueue_impl(c, &p, na);
+    }
+    free(src); free(dst); free(seq); free(sz); free(ts);
+    c->tack_n = 0;
+    if (rc) return rc;
+  }
+  otx* due = (otx*)malloc((c->tsg_n + 1) * sizeof(otx));
+  if (!due) return fail(c, TGSIM_ENOMEM, "oom");
+  size_t nd = 0, done = 0;
+  for (size_t sid = 0; sid < c->tsg_n; ++sid) {
+    otcps* g = &c->tsg[sid];
+    if (g->acked || g->gave_up || g->t_att >= H) continue;  /* settled, or its attempt not yet sent */
+    const uint32_t st = c->tw[g->w].state;
+    if (st == TGSIM_TCP_TIMEOUT || st == TGSIM_TCP_REFUSED) continue;
+    const int64_t T = g->t_att + (c->tcp.rto_ns << g->attempt);
+    if (T >= t_end) continue;
+    if (g->attempt + 1 >= c->tcp.max_attempts) {
+      g->gave_up = 1;
+      tcp_finish(c, g->w, TGSIM_TCP_TIMEOUT, T, &done);
+      continue;
+    }
+    g->attempt++;
+    g->t_att = T > H ? T : H;
+    c->tstats.retransmissions++;
+    due[nd].t = g->t_att; due[nd].sid = (uint32_t)sid; ++nd;
+  }
+  if (nd) {
+    qsort(due, nd, sizeof(otx), cmp_otx);
+    uint32_t* src = malloc(nd * 4); uint32_t* dst = malloc(nd * 4); uint32_t* seq = malloc(nd * 4);
+    uint32_t* sz = malloc(nd * 4); int64_t* ts = malloc(nd * 8);
+    if (!src || !dst || !seq || !sz || !ts) rc = TGSIM_ENOMEM;
+    for (size_t i = 0; i < nd && !rc; ++i) {
+      const otcps* g = &c->tsg[due[i].sid];
+      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (due[i].sid << 4) | g->attempt;
+      sz[i] = g->wire; ts[i] = g->t_att;
+    }
+    if (!rc) {
+      tgsim_msg_soa p = {src, dst, seq, sz, ts};
+      rc = enqueue_impl(c, &p, nd);
+      c->tstats.packets += nd;
+    }
+    free(src); free(dst); free(seq); free(sz); free(ts);
+  }
+  free(due);
+  c->tstats.pending_retx = 0;
   return rc;
 }
 

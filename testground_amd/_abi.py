@@ -85,7 +85,7 @@ class Stats(C.Structure):
 
 class TcpConfig(C.Structure):
     _fields_ = [("mss", C.c_uint32), ("header_bytes", C.c_uint32), ("rto_ns", C.c_int64),
-                ("max_attempts", C.c_uint32), ("reserved", C.c_uint32), ("max_writes", C.c_uint64),
+                ("max_attempts", C.c_uint32), ("acks", C.c_uint32), ("max_writes", C.c_uint64),
                 ("max_segments", C.c_uint64)]
 
 
@@ -95,6 +95,7 @@ class TcpStats(C.Structure):
 
 
 TCP_PENDING, TCP_DELIVERED, TCP_TIMEOUT, TCP_REFUSED = 0, 1, 2, 3
+TCP_ACK_BIT = 0x80000000
 
 
 # tgsim_transport (include/tgsim.h): caller-supplied cross-shard operations

@@ -55,10 +55,20 @@ struct TopicIndex {
 // retransmission scheduled (the current one is released at the next window start, survivors move
 // to the other), and counters.
 constexpr int kTcpArriveBlocks = 2048;  // k_tcp_arrive's grid (= TcpDev::part entries)
+constexpr uint32_t kTcpBatches = 1u << 14;  // acks mode: ring of attempt-0 timer batches (one per window)
+// acks mode: the segments first sent in one window, [lo, hi), their timers in [t_lo, t_hi)
+struct TcpBatch {
+  uint32_t lo, hi;
+  int64_t t_lo, t_hi;
+  uint32_t done, pad;
+};
 struct TcpScalars {
-  uint32_t pend_n[2];             // entries of the two pending lists
+  uint32_t pend_n[2];             // entries of the two pending lists (acks mode: retransmitted attempts' timers)
   uint32_t done;                  // writes finished by the running reaction
-  uint32_t pad;
+  uint32_t ack_n;                 // acks mode: ACKs of the last reaction (delivery indices in ack_idx)
+  uint32_t ack_base;              // ... their first staged slot at the release
+  uint32_t tb_tail;               // ... oldest live timer batch
+  uint32_t plan_n, plan_total;    // ... batches due at this release and their segments
   unsigned long long retx, delivered, failed, released;
 };
 struct TcpDev {
@@ -73,6 +83,15 @@ struct TcpDev {
   // duplicated deliveries (bm_d); per-block partial counts of k_tcp_arrive
   uint64_t *bm_s = nullptr, *bm_r = nullptr, *bm_d = nullptr;
   uint32_t* part = nullptr;
+  // acks mode (tgsim_tcp_config.acks): ACK bits over the deliveries (intact data), the reaction's ACK
+  // list, a segment's settled byte (1 an ACK arrived, 2 gave up), the timer-batch ring and the
+  // release's plan over it
+  uint32_t acks = 0;
+  uint64_t* bm_a = nullptr;
+  uint32_t* ack_idx = nullptr;
+  uint8_t* s_done = nullptr;
+  TcpBatch* tb = nullptr;
+  uint32_t *plan_lo = nullptr, *plan_off = nullptr;
   uint32_t* pend[2] = {nullptr, nullptr};
   uint32_t* pend_by = nullptr;    // [N] retransmissions pending (or released into the open window) per sender
   TcpScalars* sc = nullptr;
@@ -228,7 +247,7 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
                                             uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t mult);  // retx: TCP pending per sender
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, bool acks, uint32_t mult);  // retx: TCP pending per sender
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part
 hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);
@@ -269,10 +288,16 @@ hipError_t launch_append(Dev& d, const uint32_t* src, const uint32_t* dst, const
 hipError_t launch_flood_mark(Dev& d, uint32_t n);
 // TCP mode: the last window's packets (status, seq; count n_host or *n_dev) and deliveries ->
 // queued copies, first intact arrivals, finished writes, retransmissions onto pend[cur]
-hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch);
+hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch,
+                            uint32_t fill);  // fill: acks mode, the batch registered for this window (or ~0u)
 // window start: pend[cur] entries due before the window's end staged behind sc->n_msgs_dev (which
 // the caller has set), the others moved to pend[cur ^ 1]
 hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, uint32_t base_host);
+// acks mode, at the window start: the last reaction's ACKs staged, due timers fired (attempt-0 batches
+// [tail, head) and the retransmitted attempts on pend[cur]), survivors to pend[cur ^ 1]; batch `head`
+// registered for the segments [lo, hi) this window sends (reg)
+hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, uint32_t base_host, uint32_t head,
+                                   bool reg, uint32_t lo, uint32_t hi);
 // TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)

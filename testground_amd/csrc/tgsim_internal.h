@@ -36,7 +36,8 @@ enum : uint32_t {
   ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
   ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14,
   ERR_QUEUE_CAP = 1u << 15,  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
-  ERR_CAP_M = 1u << 16       // device-counted staging (flood forwards, appends after them) outgrew cap_msgs
+  ERR_CAP_M = 1u << 16,      // device-counted staging (flood forwards, appends after them) outgrew cap_msgs
+  ERR_TCP_TIMERS = 1u << 17  // TCP acks mode: more live timer batches than the ring holds
 };
 
 // Per-sender egress state derived from network.LinkShape (48 B; gathered by src).

@@ -1203,13 +1203,19 @@ __device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uin
 
 // The host's exact refresh of its occupancy bound: max over local senders of pend -> sc->pend_max
 // (zeroed by the host's memset first). TCP mode: mult * (pend + pending retransmissions), which
-// bounds mult * the sender's unsettled segments (tgsim_tcp.hip).
-__global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const uint32_t* retx, uint32_t mult,
-                                                     uint32_t nloc, uint32_t* out) {
+// bounds mult * the sender's unsettled segments (tgsim_tcp.hip). TCP acks mode (refreshed every
+// window): pend + mult * (retransmissions released into the window + the deliveries the sender got
+// last window, each answered by at most one ACK).
+__global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const uint32_t* retx, const uint32_t* inbox,
+                                                     uint32_t mult, uint32_t nloc, uint32_t* out) {
   __shared__ uint32_t red[kBlock / 64];
   uint32_t mx = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock)
-    mx = max(mx, retx ? (uint32_t)min<uint64_t>((uint64_t)mult * (pend[i] + retx[i]), 0xFFFFFFFFull) : pend[i]);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock) {
+    uint64_t v = pend[i];
+    if (inbox) v += (uint64_t)mult * ((uint64_t)retx[i] + (inbox[i + 1] - inbox[i]));
+    else if (retx) v = (uint64_t)mult * (v + retx[i]);
+    mx = max(mx, (uint32_t)min<uint64_t>(v, 0xFFFFFFFFull));
+  }
   mx = wave_max(mx);
   if (lane_id() == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
@@ -3356,10 +3362,10 @@ hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
   return hipGetLastError();
 }
 
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t mult) {
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, bool acks, uint32_t mult) {
   TG_CHECK(hipMemsetAsync(&d.sc->pend_max, 0, sizeof(uint32_t), d.stream));
   hipLaunchKernelGGL(k_pend_max, dim3(std::min<unsigned>(grid_for(d.nloc), 1024u)), dim3(kBlock), 0, d.stream, d.pend,
-                     retx, mult, d.nloc, &d.sc->pend_max);
+                     retx, acks ? d.inbox : nullptr, mult, d.nloc, &d.sc->pend_max);
   return hipGetLastError();
 }
 

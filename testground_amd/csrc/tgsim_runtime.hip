@@ -98,6 +98,10 @@ struct tgsim_ctx {
   TcpDev td;
   uint64_t tw_n = 0, tsg_n = 0;       // writes / segments so far
   uint32_t tcp_cur = 0, tcp_epoch = 0;
+  // acks mode: timer batches registered (one per window with new segments), the first segment not
+  // yet in one, and the batch the open window registered (its timer range is filled at the reaction)
+  uint32_t tcp_nb = 0, tcp_fill = ~0u;
+  uint64_t tcp_seg_batched = 0;
   // the reactions' counters land in two pinned snapshots (read once their event has completed);
   // nothing on the window path reads them (the queue-limit bound folds the pending retransmissions
   // into the occupancy: tgsim_tcp.hip)
@@ -535,7 +539,7 @@ static int check_device_errors(tgsim_ctx* c) {
   const uint32_t e = c->d.h_sc->err;
   if (!e) return TGSIM_OK;
   if (e & (ERR_CAP_A | ERR_CAP_D | ERR_CAP_L | ERR_CAP_X | ERR_ARENA | ERR_REGIONS | ERR_SIG_CAP | ERR_STATE_CHUNKS |
-           ERR_QUEUE_CAP))
+           ERR_QUEUE_CAP | ERR_CAP_M | ERR_TCP_TIMERS))
     return fail(c, TGSIM_ECAPACITY, "device capacity exceeded (err bits 0x%x)", e);
   if (e & (ERR_CAUSAL | ERR_SIG_ORDER)) return fail(c, TGSIM_ECAUSALITY, "causality violation on device (err 0x%x)", e);
   if (e & ERR_UNSORTED_TARGET)
@@ -962,7 +966,8 @@ static int plan_queue_limit(tgsim_ctx* c) {
   const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->fl_npubs;
   bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   if (gate && !c->pend_exact) {  // inconclusive: refresh the bound with the exact maximum (one sync)
-    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, (uint32_t)mult), "pend max");
+    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks, (uint32_t)mult),
+          "pend max");
     HIPCK(c, sync_scalars(d), "sync");
     c->pend_bound = d.h_sc->pend_max;
     c->pend_exact = true;
@@ -981,6 +986,10 @@ static int plan_queue_limit(tgsim_ctx* c) {
     d.heavy.retx = c->tcp_on ? c->td.pend_by : nullptr;  // single shard: local = global ids
     d.heavy.m_uniform = (uint32_t)m_uniform;
     d.heavy.m_inbox = c->win_m_inbox;
+    if (c->tcp_on && c->tcp.acks) {  // ACKs: at most one per delivery the sender got last window
+      d.heavy.inbox = d.inbox;
+      d.heavy.m_inbox = 1;
+    }
     d.heavy.mult = (uint32_t)mult;
   }
   c->pend_bound = std::min<uint64_t>(c->pend_bound + mult * m_max, 1ull << 62);
@@ -999,9 +1008,24 @@ static int begin_common(tgsim_ctx* c) {
   if (rc) return rc;
   if (c->tcp_on) {
     if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
-    // due retransmissions join the staged packets behind the device-side count (the pending count
-    // is device-side too, and the queue-limit test reads the per-sender counts on the device)
-    HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
+    if (c->tcp.acks) {
+      // the last reaction's ACKs and the due timers join the staged packets behind the device-side
+      // count; the window's new segments (all staged now) register one timer batch
+      const bool reg = c->tsg_n > c->tcp_seg_batched;
+      HIPCK(c, launch_tcp_release_acks(c->d, c->td, c->tcp_cur, c->staged_dev, c->n_staged, c->tcp_nb, reg,
+                                       (uint32_t)c->tcp_seg_batched, (uint32_t)c->tsg_n), "tcp release");
+      c->tcp_fill = reg ? c->tcp_nb : ~0u;
+      if (reg) c->tcp_nb++;
+      c->tcp_seg_batched = c->tsg_n;
+      // a timer can re-queue a segment that sits in no count (delivered, ACK outstanding): the
+      // queue-limit bound is refreshed exactly every window
+      c->pend_bound = 1ull << 62;
+      c->pend_exact = false;
+    } else {
+      // due retransmissions join the staged packets behind the device-side count (the pending count
+      // is device-side too, and the queue-limit test reads the per-sender counts on the device)
+      HIPCK(c, launch_tcp_release(c->d, c->td, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
+    }
     c->staged_dev = true;
     c->tcp_cur ^= 1u;
   }
@@ -1806,9 +1830,19 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (!t.max_attempts) t.max_attempts = 16;
   if (!t.max_writes) t.max_writes = 1u << 22;
   if (!t.max_segments) t.max_segments = 1u << 24;
-  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28))
+  if (t.max_attempts > 16 || t.rto_ns < 0 || t.max_segments > (1u << 28) || t.max_writes > (1u << 28) || t.acks > 1 ||
+      (t.acks && t.max_segments > (1u << 27)))
     return fail(c, TGSIM_EINVAL, "bad TCP configuration");
   TcpDev& d = c->td;
+  if (t.acks) {
+    const size_t S = t.max_segments, R = (size_t)kNSub * c->d.subcap;  // per-window deliveries
+    if (dalloc(c, &d.s_done, S) || dalloc(c, &d.bm_a, R / 64 + 1) || dalloc(c, &d.ack_idx, R) ||
+        dalloc(c, &d.tb, (size_t)kTcpBatches) || dalloc(c, &d.plan_lo, (size_t)kTcpBatches + 1) ||
+        dalloc(c, &d.plan_off, (size_t)kTcpBatches + 1))
+      return TGSIM_ENOMEM;
+    HIPCK(c, hipMemsetAsync(d.s_done, 0, S, c->d.stream), "tcp init");
+    d.acks = 1;
+  }
   const size_t W = t.max_writes, S = t.max_segments;
   if (dalloc(c, &d.w_src, W) || dalloc(c, &d.w_dst, W) || dalloc(c, &d.w_rem, W) || dalloc(c, &d.w_state, W) ||
       dalloc(c, &d.w_tarr, W) || dalloc(c, &d.w_tmax, W) || dalloc(c, &d.w_fail, W) || dalloc(c, &d.s_w, S) || dalloc(c, &d.s_wire, S) ||
@@ -1914,7 +1948,8 @@ extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
   if (!c->tcp_need_react) return TGSIM_OK;
   const bool on_dev = c->n_status_last == kStatusOnDevice;
   HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
-                            on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch), "tcp react");
+                            on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch, c->tcp_fill), "tcp react");
+  c->tcp_fill = ~0u;
   c->tcp_need_react = false;
   // the counters into the next pinned snapshot, behind the reaction on the stream
   const uint32_t k = c->tcp_snap_slot;
@@ -1946,7 +1981,7 @@ static int tcp_refresh(tgsim_ctx* c) {
     c->tstats.retransmissions = ts.retx;
     c->tstats.delivered = ts.delivered;
     c->tstats.failed = ts.failed;
-    c->tstats.pending_retx = ts.pend_n[c->tcp_snap_cur[k]];
+    c->tstats.pending_retx = c->tcp.acks ? 0 : ts.pend_n[c->tcp_snap_cur[k]];  // acks: timers, not a pending list
     c->tstats.packets = c->tstats.segments + ts.released;
     c->tcp_snap_live[k] = false;
     if (k == latest) c->tcp_snap_live[older] = false;  // superseded (an older one leaves the latest in flight)

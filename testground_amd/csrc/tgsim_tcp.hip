@@ -99,18 +99,20 @@ __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict
   const uint32_t n = n_dev ? *n_dev : n_host;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t sq = seq[i], sid = sq >> 4;
-    const uint8_t st = status[i];
-    const uint32_t q = tcp_copies(st), code = st & 0x0Fu;
     bool retx = false;
-    // a released retransmission leaves its sender's pending count once its packet is accounted
-    if (sq & 15u) atomicSub(&t.pend_by[t.w_src[t.s_w[sid] & kWMask]], 1u);
-    if (q) {
-      t.s_out[sid] = q;
-      t.s_w[sid] = (t.s_w[sid] & ~(3u << kQShift)) | (q << kQShift);
-    } else if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) {
-      tcp_fail(t, t.s_w[sid] & kWMask, t.s_tatt[sid], TGSIM_TCP_REFUSED);
-    } else {
-      retx = tcp_next(t, sid, t.s_tatt[sid]);
+    if (!(t.acks && (sq & TGSIM_TCP_ACK_BIT))) {  // acks mode: an ACK packet's fate concerns nobody
+      const uint8_t st = status[i];
+      const uint32_t q = tcp_copies(st), code = st & 0x0Fu;
+      // a released retransmission leaves its sender's pending count once its packet is accounted
+      if (sq & 15u) atomicSub(&t.pend_by[t.w_src[t.s_w[sid] & kWMask]], 1u);
+      if (q) {
+        t.s_out[sid] = q;
+        t.s_w[sid] = (t.s_w[sid] & ~(3u << kQShift)) | (q << kQShift);
+      } else if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) {
+        tcp_fail(t, t.s_w[sid] & kWMask, t.s_tatt[sid], TGSIM_TCP_REFUSED);
+      } else if (!t.acks) {  // acks mode: the attempt's timer decides
+        retx = tcp_next(t, sid, t.s_tatt[sid]);
+      }
     }
     put_bits(t.bm_s, i, retx);
   }
@@ -120,6 +122,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict
 // whose every segment arrived cannot fail, so its time alone marks it delivered
 __device__ __forceinline__ uint32_t tcp_arrived(TcpDev& t, uint32_t sw, int64_t arr) {
   const uint32_t w = sw & kWMask;
+  // acks mode: a write can fail (give up) while its data is still on the way; failed stays failed
+  if (t.acks && t.w_state[w] != TGSIM_TCP_PENDING) return 0u;
   if (sw & kSoleSeg) {  // no other segment: nothing else writes the write's entries
     t.w_tarr[w] = arr;
     return 1u;
@@ -142,9 +146,32 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
   const uint32_t n = sc->n_out;
   uint32_t ndel = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t sid = o_seq[i] >> 4;
+    const uint32_t sq = o_seq[i];
     const int64_t ti = o_t[i];
     const bool corrupt = o_flags[i] & TGSIM_F_CORRUPT;
+    if (t.acks) {  // acks mode: ACKs settle segments, intact data is answered; timers decide the rest
+      bool ack = false, dup = false;
+      if (sq & TGSIM_TCP_ACK_BIT) {
+        if (!corrupt) t.s_done[(sq & ~TGSIM_TCP_ACK_BIT) >> 4] = 1;
+      } else if (!corrupt) {
+        ack = true;
+        const uint32_t sid = sq >> 4, sw = t.s_w[sid];
+        // the first attempt's only copy is the segment's only delivery (a later attempt - and with
+        // it another copy - would have raised s_att): this thread settles it
+        if (((sw >> kQShift) & 3u) == 1u && t.s_att[sid] == 0) {
+          t.s_mark[sid] = kArrived;
+          ndel += tcp_arrived(t, sw, ti);
+        } else {
+          atomicMin(reinterpret_cast<long long*>(&t.s_arr[sid]), (long long)ti);
+          dup = true;
+        }
+      }
+      put_bits(t.bm_r, i, false);
+      put_bits(t.bm_d, i, dup);
+      put_bits(t.bm_a, i, ack);
+      continue;
+    }
+    const uint32_t sid = sq >> 4;
     const uint32_t sw = t.s_w[sid];
     const bool sole = ((sw >> kQShift) & 3u) == 1u;
     bool retx = false;
@@ -178,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_settle(const uint32_t* __restric
       if (arr != INT64_MAX) {
         t.s_mark[sid] = kArrived;
         ndel += tcp_arrived(t, t.s_w[sid], arr);
-      } else if (t.s_out[sid] == 0 && tcp_next(t, sid, t.s_tlast[sid])) {
+      } else if (!t.acks && t.s_out[sid] == 0 && tcp_next(t, sid, t.s_tlast[sid])) {
         t.pend[cur][atomicAdd(&t.sc->pend_n[cur], 1u)] = sid;
         atomicAdd(&t.sc->retx, 1ull);
       }
@@ -224,6 +251,19 @@ __global__ __launch_bounds__(kBlock) void k_tcp_collect(const uint32_t* __restri
     nretx += tot;
     __syncthreads();  // sbase is rewritten by the next round
   }
+  if (t.acks) {  // the ACK list (delivery indices), one reservation per block and round
+    for (uint32_t b0 = blockIdx.x * kBlock; b0 < wr; b0 += gridDim.x * kBlock) {  // uniform per block
+      const uint32_t wi = b0 + threadIdx.x;
+      uint64_t m = wi < wr ? t.bm_a[wi] : 0ull;
+      uint32_t tot;
+      uint32_t p = block_excl_scan((uint32_t)__popcll(m), red, tot);
+      if (threadIdx.x == 0 && tot) sbase = atomicAdd(&t.sc->ack_n, tot);
+      __syncthreads();
+      p += sbase;
+      for (; m; m &= m - 1) t.ack_idx[p++] = wi * 64u + (uint32_t)__builtin_ctzll(m);
+      __syncthreads();
+    }
+  }
   uint32_t nd = 0;
   if (blockIdx.x == 0)
     for (uint32_t k = threadIdx.x; k < nparts; k += kBlock) nd += t.part[k];
@@ -236,8 +276,17 @@ __global__ __launch_bounds__(kBlock) void k_tcp_collect(const uint32_t* __restri
   if (threadIdx.x == 0 && nretx) atomicAdd(&t.sc->retx, (unsigned long long)nretx);
 }
 
-__global__ __launch_bounds__(kBlock) void k_tcp_reset(TcpDev t, uint32_t cur) {
-  if (threadIdx.x == 0) { t.sc->done = 0; t.sc->pend_n[cur ^ 1u] = 0; }
+__global__ __launch_bounds__(kBlock) void k_tcp_reset(TcpDev t, uint32_t cur, const DevScalars* sc, uint32_t fill) {
+  if (threadIdx.x == 0) {
+    t.sc->done = 0;
+    t.sc->pend_n[cur ^ 1u] = 0;
+    t.sc->ack_n = 0;
+    if (fill != ~0u) {  // acks mode: the window's new segments sent in [T, t_end): timers in [T, t_end) + rto
+      TcpBatch& b = t.tb[fill % kTcpBatches];
+      b.t_lo = sc->T + t.rto;
+      b.t_hi = sc->t_end + t.rto;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_tcp_base(DevScalars* sc, uint32_t base_host) {
@@ -272,6 +321,150 @@ __global__ __launch_bounds__(kBlock) void k_tcp_release(TcpDev t, uint32_t cur, 
   }
 }
 
+// acks mode, window start (one block): the last reaction's ACKs get their staged slots; the live
+// timer batches whose earliest timer falls before the window's end form the plan (per batch its
+// first segment and its offset in the plan's item space; a batch whose every timer falls before the
+// end is scanned for the last time and retires); the window's new segments register a batch.
+__global__ __launch_bounds__(kBlock) void k_tcp_tplan(TcpDev t, DevScalars* sc, uint32_t head, uint32_t reg,
+                                                      uint32_t lo, uint32_t hi, uint32_t cap) {
+  __shared__ uint32_t red[kBlock / 64];
+  const int64_t t_end = sc->t_end;
+  const uint32_t tail = t.sc->tb_tail;
+  if (threadIdx.x == 0) {
+    const uint32_t base = sc->n_msgs_dev, na = t.sc->ack_n;
+    t.sc->ack_base = base;
+    sc->n_msgs_dev = base + na;
+    if (base + na > cap) atomicOr(&sc->err, ERR_CAP_M);
+  }
+  uint32_t carry = 0;
+  for (uint32_t b0 = tail; b0 < head; b0 += kBlock) {  // block-uniform
+    const uint32_t k = b0 + threadIdx.x;
+    uint32_t len = 0, first = 0;
+    if (k < head) {
+      TcpBatch& b = t.tb[k % kTcpBatches];
+      first = b.lo;
+      if (!b.done && b.t_lo < t_end) {
+        len = b.hi - b.lo;
+        if (b.t_hi <= t_end) b.done = 1u;
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(len, red, tot);
+    if (k < head) {
+      t.plan_lo[k - tail] = first;
+      t.plan_off[k - tail] = carry + ex;
+    }
+    carry += tot;
+  }
+  __syncthreads();  // the done flags above
+  if (threadIdx.x == 0) {
+    t.plan_off[head - tail] = carry;
+    t.sc->plan_n = head - tail;
+    t.sc->plan_total = carry;
+    uint32_t tl = tail;
+    while (tl < head && t.tb[tl % kTcpBatches].done) ++tl;
+    t.sc->tb_tail = tl;
+    if (reg) {
+      if (head + 1u - tl > kTcpBatches) atomicOr(&sc->err, ERR_TCP_TIMERS);
+      TcpBatch& b = t.tb[head % kTcpBatches];
+      b.lo = lo; b.hi = hi; b.t_lo = INT64_MAX; b.t_hi = INT64_MAX; b.done = 0u; b.pad = 0u;
+    }
+  }
+}
+
+// acks mode, window start: the ACKs staged (at max(arrival, window start)); every planned
+// attempt-0 timer and every retransmitted attempt's timer (pend[cur]) checked - settled (ACKed,
+// gave up) or of a failed write: dropped; before the window's end: the next attempt at max(timer,
+// window start), or the segment gives up; else kept (pend[cur ^ 1]). One reservation per block and
+// round for the fired packets and one for the kept timers.
+__global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, uint32_t cur, uint32_t cap,
+                                                     const uint32_t* __restrict__ o_src,
+                                                     const uint32_t* __restrict__ o_dst,
+                                                     const uint32_t* __restrict__ o_seq,
+                                                     const int64_t* __restrict__ o_t, uint32_t* __restrict__ m_src,
+                                                     uint32_t* __restrict__ m_dst, uint32_t* __restrict__ m_seq,
+                                                     uint32_t* __restrict__ m_size, int64_t* __restrict__ m_t) {
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t sb_f, sb_k;
+  const int64_t H = sc->T, t_end = sc->t_end;  // the window [T, t_end) (k_window_start: H is the one before)
+  const uint32_t nxt = cur ^ 1u, stride = gridDim.x * kBlock;
+  const uint32_t na = t.sc->ack_n, ab = t.sc->ack_base;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < na; i += stride) {
+    const uint32_t d = t.ack_idx[i], p = ab + i;
+    if (p < cap) {
+      m_src[p] = o_dst[d]; m_dst[p] = o_src[d]; m_seq[p] = TGSIM_TCP_ACK_BIT | o_seq[d]; m_size[p] = t.hdr;
+      m_t[p] = o_t[d] > H ? o_t[d] : H;
+    }
+  }
+  const uint32_t np = t.sc->plan_n, nb = t.sc->plan_total, total = nb + t.sc->pend_n[cur];
+  uint32_t nfire = 0;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += stride) {  // block-uniform
+    const uint32_t j = b0 + threadIdx.x;
+    bool fire = false, keep = false;
+    uint32_t sid = 0, w = 0, att = 0;
+    int64_t tf = 0;
+    if (j < total) {
+      const bool batch = j < nb;
+      if (batch) {  // the last plan entry starting at or before j (empty entries share offsets)
+        uint32_t l = 0, h = np;
+        while (h - l > 1) {
+          const uint32_t mid = (l + h) >> 1;
+          if (t.plan_off[mid] <= j) l = mid; else h = mid;
+        }
+        sid = t.plan_lo[l] + (j - t.plan_off[l]);
+      } else {
+        sid = t.pend[cur][j - nb];
+      }
+      const uint32_t a = t.s_att[sid];
+      // a batch entry whose segment was retransmitted already has its timer on the list
+      if (!(batch && a != 0) && t.s_done[sid] == 0) {
+        w = t.s_w[sid] & kWMask;
+        const uint32_t wst = t.w_state[w];
+        if (wst != TGSIM_TCP_TIMEOUT && wst != TGSIM_TCP_REFUSED) {
+          const int64_t T = t.s_tatt[sid] + (t.rto << a);
+          if (T >= t_end) {
+            keep = !batch;
+          } else if (a + 1u >= t.max_att) {
+            t.s_done[sid] = 2;
+            if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, T, TGSIM_TCP_TIMEOUT);
+          } else {
+            att = a + 1u;
+            tf = T > H ? T : H;
+            t.s_att[sid] = att;
+            t.s_tatt[sid] = tf;
+            fire = keep = true;
+          }
+        }
+      }
+    }
+    uint32_t totf, totk;
+    const uint32_t pf = block_excl_scan(fire ? 1u : 0u, red, totf);
+    const uint32_t pk = block_excl_scan(keep ? 1u : 0u, red, totk);
+    if (threadIdx.x == 0) {
+      sb_f = totf ? atomicAdd(&sc->n_msgs_dev, totf) : 0u;
+      sb_k = totk ? atomicAdd(&t.sc->pend_n[nxt], totk) : 0u;
+    }
+    __syncthreads();
+    if (fire) {
+      const uint32_t p = sb_f + pf;
+      if (p < cap) {
+        m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | att; m_size[p] = t.s_wire[sid];
+        m_t[p] = tf;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_M);
+      }
+      atomicAdd(&t.pend_by[t.w_src[w]], 1u);  // released into this window until its status is read
+    }
+    if (keep) t.pend[nxt][sb_k + pk] = sid;
+    nfire += totf;
+    __syncthreads();  // sb_f / sb_k are rewritten by the next round
+  }
+  if (threadIdx.x == 0 && nfire) {
+    atomicAdd(&t.sc->retx, (unsigned long long)nfire);
+    atomicAdd(&t.sc->released, (unsigned long long)nfire);
+  }
+}
+
 // A generated storm round (staged [base, base + n)) becomes TCP writes: one segment each.
 __global__ __launch_bounds__(kBlock) void k_tcp_adopt(TcpDev t, uint32_t base, uint32_t n, uint32_t wbase,
                                                       uint32_t sbase, uint32_t* __restrict__ m_src,
@@ -296,8 +489,9 @@ hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32
   return hipGetLastError();
 }
 
-hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch) {
-  hipLaunchKernelGGL(k_tcp_reset, dim3(1), dim3(kBlock), 0, d.stream, t, cur);
+hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch,
+                            uint32_t fill) {
+  hipLaunchKernelGGL(k_tcp_reset, dim3(1), dim3(kBlock), 0, d.stream, t, cur, d.sc, fill);
   hipLaunchKernelGGL(k_tcp_status, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.status, d.m_seq, n_host, n_dev, t);
   hipLaunchKernelGGL(k_tcp_arrive, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_seq, d.o_t, d.o_flags, d.sc, t);
   hipLaunchKernelGGL(k_tcp_settle, dim3(64), dim3(kBlock), 0, d.stream, d.o_seq, d.sc, t, epoch, cur);
@@ -311,6 +505,15 @@ hipError_t launch_tcp_release(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, ui
   // the pending count is device-side: a fixed grid, grid-stride
   hipLaunchKernelGGL(k_tcp_release, dim3(256), dim3(kBlock), 0, d.stream, t, cur, d.sc, d.cap_msgs, d.m_src,
                      d.m_dst, d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_dev, uint32_t base_host, uint32_t head,
+                                   bool reg, uint32_t lo, uint32_t hi) {
+  if (!base_dev) hipLaunchKernelGGL(k_tcp_base, dim3(1), dim3(kBlock), 0, d.stream, d.sc, base_host);
+  hipLaunchKernelGGL(k_tcp_tplan, dim3(1), dim3(kBlock), 0, d.stream, t, d.sc, head, reg ? 1u : 0u, lo, hi, d.cap_msgs);
+  hipLaunchKernelGGL(k_tcp_fire, dim3(512), dim3(kBlock), 0, d.stream, t, d.sc, cur, d.cap_msgs, d.o_src, d.o_dst,
+                     d.o_seq, d.o_t, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 

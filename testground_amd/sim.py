@@ -157,8 +157,9 @@ class Simulator:
 
     # ---- TCP mode (tgsim_tcp_*) ------------------------------------------------
     def tcp_enable(self, mss: int = 0, header_bytes: int = 0, rto_ns: int = 0, max_attempts: int = 0,
-                   max_writes: int = 0, max_segments: int = 0) -> None:
-        cfg = A.TcpConfig(mss, header_bytes, rto_ns, max_attempts, 0, max_writes, max_segments)
+                   max_writes: int = 0, max_segments: int = 0, acks: bool = False) -> None:
+        """acks=True: ACK packets on the reverse path and retransmission timers (tgsim.h)."""
+        cfg = A.TcpConfig(mss, header_bytes, rto_ns, max_attempts, int(acks), max_writes, max_segments)
         self._check(self.lib.tcp_enable(self._ctx, C.byref(cfg)))
 
     def tcp_send(self, src, dst, seq, size, t_send) -> None:

@@ -112,6 +112,106 @@ CASES = [case_segmentation, case_loss_backoff_and_timeout, case_retransmission_r
          case_corruption_waits_for_the_copy, case_duplicates_and_refusal]
 
 
+# ---- acks = 1: ACK packets on the reverse path, retransmission timers (tgsim.h) ------------------
+
+def _run_windows(s, until_ms, step_ms=10):
+    """10 ms windows up to until_ms; every window's deliveries, concatenated."""
+    out = []
+    for k in range(step_ms, until_ms + 1, step_ms):
+        d = window(s, k * MS)
+        out.append(d)
+    return {key: np.concatenate([d[key] for d in out]) for key in out[0]}
+
+
+def case_ack_clean(b):
+    """The data arrives at 10 ms; its ACK leaves at the next window start (20 ms) and arrives at
+    30 ms, before the 200 ms timer: nothing is retransmitted."""
+    s = sim(b)
+    s.tcp_enable(acks=True)
+    for g in range(4):
+        s.set_shape(g, make_shape(latency_ns=10 * MS))
+    s.tcp_send([0], [1], [0], [100], [0])
+    d = _run_windows(s, 400)
+    acks = (d["seq"] & A.TCP_ACK_BIT) != 0
+    assert d["t_deliver"][~acks].tolist() == [10 * MS] and d["t_deliver"][acks].tolist() == [30 * MS]
+    assert d["src"][acks].tolist() == [1] and d["dst"][acks].tolist() == [0]
+    assert d["size"][acks].tolist() == [52]
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_DELIVERED and t[0] == 10 * MS
+    assert s.tcp_stats()["retransmissions"] == 0 and s.tcp_stats()["packets"] == 1
+    s.close()
+
+
+def case_ack_lost_spurious(b):
+    """Every ACK is lost (the receiver's link drops everything): the sender retransmits at 200 and
+    600 ms although the data arrived at 10 ms, then gives up at 1400 ms; the write stays delivered."""
+    s = sim(b)
+    s.tcp_enable(acks=True, max_attempts=3)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    s.set_shape(1, make_shape(loss=100.0))
+    s.tcp_send([0], [1], [0], [100], [0])
+    d = _run_windows(s, 1600)
+    data = (d["seq"] & A.TCP_ACK_BIT) == 0
+    assert d["t_deliver"][data].tolist() == [10 * MS, 210 * MS, 610 * MS]
+    assert (d["seq"][data] & 15).tolist() == [0, 1, 2]
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_DELIVERED and t[0] == 10 * MS
+    stats = s.tcp_stats()
+    assert stats["retransmissions"] == 2 and stats["failed"] == 0 and stats["packets"] == 3
+    s.close()
+
+
+def case_ack_data_lost(b):
+    """The first attempt is lost; the timer resends it at 200 ms once the link has healed."""
+    s = sim(b)
+    s.tcp_enable(acks=True)
+    s.set_shape(0, make_shape(loss=100.0))
+    s.set_shape(1, make_shape(latency_ns=10 * MS))
+    s.tcp_send([0], [1], [0], [100], [0])
+    window(s, 10 * MS)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    _run_windows(s, 400)
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_DELIVERED and t[0] == 210 * MS
+    assert s.tcp_stats()["retransmissions"] == 1
+    s.close()
+
+
+def case_ack_slow_path(b):
+    """A 300 ms data path is slower than the 200 ms timer: a spurious retransmission leaves at 200 ms
+    (arriving at 500 ms); the original's ACK (sent at 310, arriving at 315 ms) stops the next timer."""
+    s = sim(b)
+    s.tcp_enable(acks=True)
+    s.set_shape(0, make_shape(latency_ns=300 * MS))
+    s.set_shape(1, make_shape(latency_ns=5 * MS))
+    s.tcp_send([0], [1], [0], [100], [0])
+    d = _run_windows(s, 1000)
+    data = (d["seq"] & A.TCP_ACK_BIT) == 0
+    assert d["t_deliver"][data].tolist() == [300 * MS, 500 * MS]
+    assert sorted(d["t_deliver"][~data].tolist()) == [315 * MS, 515 * MS]
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_DELIVERED and t[0] == 300 * MS
+    assert s.tcp_stats()["retransmissions"] == 1
+    s.close()
+
+
+def case_ack_timeout_before_data(b):
+    """max_attempts = 1 and a 300 ms path: the only timer fires at 200 ms, before the data arrives -
+    the write fails (TIMEOUT at 200 ms) and the later arrival does not revive it."""
+    s = sim(b)
+    s.tcp_enable(acks=True, max_attempts=1)
+    s.set_shape(0, make_shape(latency_ns=300 * MS))
+    s.tcp_send([0], [1], [0], [100], [0])
+    _run_windows(s, 500)
+    st, t = s.tcp_writes()
+    assert st[0] == A.TCP_TIMEOUT and t[0] == 200 * MS
+    s.close()
+
+
+ACK_CASES = [case_ack_clean, case_ack_lost_spurious, case_ack_data_lost, case_ack_slow_path,
+             case_ack_timeout_before_data]
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c.__name__[5:] for c in CASES])
 def test_tcp_oracle(oracle, case):
     case(oracle)
@@ -120,6 +220,17 @@ def test_tcp_oracle(oracle, case):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=[c.__name__[5:] for c in CASES])
 def test_tcp_hip(hip, case):
+    case(hip)
+
+
+@pytest.mark.parametrize("case", ACK_CASES, ids=[c.__name__[5:] for c in ACK_CASES])
+def test_tcp_ack_oracle(oracle, case):
+    case(oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ACK_CASES, ids=[c.__name__[5:] for c in ACK_CASES])
+def test_tcp_ack_hip(hip, case):
     case(hip)
 
 
@@ -135,14 +246,14 @@ def test_in_order_view():
     assert list(s3) == [T.REFUSED, T.REFUSED] and list(t3) == [3, 3]   # the reset fails what follows
 
 
-def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True):
+def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True, acks=False):
     """Lossy, corrupting, duplicating, reordering links with jitter and rate limits; writes of 0 to
     9000 B over the first 30 windows. Per window: deliveries and the statuses as a sorted multiset;
     at the end the write outcomes and counters."""
     rng = np.random.default_rng(seed)
     s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18),
                   binding=b)
-    s.tcp_enable(max_attempts=int(rng.integers(3, 8)), rto_ns=int(rng.integers(20, 80)) * MS)
+    s.tcp_enable(max_attempts=int(rng.integers(3, 8)), rto_ns=int(rng.integers(20, 80)) * MS, acks=acks)
     for g in range(n):
         s.set_shape(g, make_shape(latency_ns=int(rng.integers(1, 60)) * MS, jitter_ns=int(rng.integers(0, 5)) * MS,
                                   bandwidth_bps=int(rng.choice([0, 2_000_000, 20_000_000])),
@@ -191,6 +302,25 @@ def test_tcp_random_oracle_properties(oracle):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_tcp_random_hip_matches_oracle(hip, oracle, seed):
     _same(run_random(hip, seed), run_random(oracle, seed))
+
+
+def test_tcp_random_acks_oracle_properties(oracle):
+    """acks mode on the lossy links: every write ends (delivered or timed out), ACKs travel the
+    reverse path (deliveries with the ACK bit, header-sized), and retransmissions happen."""
+    out = run_random(oracle, 1, acks=True, windows=120)
+    ws, wt = out[-1]["writes"]
+    st = out[-1]["stats"]
+    acks = np.concatenate([(x["deliv"]["seq"] & A.TCP_ACK_BIT) != 0 for x in out[:-1]])
+    sizes = np.concatenate([x["deliv"]["size"] for x in out[:-1]])
+    assert acks.any() and np.all(sizes[acks] == 52)
+    assert st["retransmissions"] > 0 and st["delivered"] > 0.8 * st["writes"]
+    assert np.all(ws != A.TCP_PENDING) and np.all(wt[ws != A.TCP_PENDING] >= 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_tcp_random_acks_hip_matches_oracle(hip, oracle, seed):
+    _same(run_random(hip, seed, acks=True, windows=120), run_random(oracle, seed, acks=True, windows=120))
 
 
 @pytest.mark.gpu
@@ -253,14 +383,14 @@ def test_lossy_rpc_over_tcp_hip(hip, oracle):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True):
+def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False):
     """The storm plan over TCP mode (plans/benchmarks/storm.go dials and writes 1 KiB per peer):
     tgsim_tcp_gen_storm_round generates each round as writes on the device, SignalAndWait ends
     the window, and the reaction recovers the 10 % lost segments. Drained afterwards."""
     rng = np.random.default_rng(seed)
     s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18,
                             max_states=64), binding=b)
-    s.tcp_enable(max_attempts=5, rto_ns=30 * MS)
+    s.tcp_enable(max_attempts=5, rto_ns=30 * MS, acks=acks)
     for g in range(n):
         s.set_shape(g, make_shape(latency_ns=int(rng.integers(5, 21)) * MS, jitter_ns=2 * MS, loss=10.0,
                                   bandwidth_bps=10_000_000))
@@ -282,6 +412,19 @@ def test_tcp_storm_oracle(oracle):
     st, t, stats, _ = run_tcp_storm(oracle)
     assert stats["writes"] == 6 * 400 * 8 and stats["retransmissions"] > 0.05 * stats["writes"]
     assert np.all(st != A.TCP_PENDING) and (st == A.TCP_DELIVERED).mean() > 0.99
+
+
+def test_tcp_storm_acks_oracle(oracle):
+    st, t, stats, _ = run_tcp_storm(oracle, acks=True)
+    assert stats["writes"] == 6 * 400 * 8 and stats["retransmissions"] > 0.05 * stats["writes"]
+    assert np.all(st != A.TCP_PENDING) and (st == A.TCP_DELIVERED).mean() > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wait", [True, False], ids=["sync", "async"])
+def test_tcp_storm_acks_hip_matches_oracle(hip, oracle, wait):
+    a, b = run_tcp_storm(hip, wait=wait, acks=True), run_tcp_storm(oracle, acks=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
 
 
 @pytest.mark.gpu
