@@ -166,6 +166,8 @@ def parse():
     p.add_argument("--workload", choices=("storm", "flood"), default="storm")
     p.add_argument("--tcp", action="store_true",
                    help="storm over TCP mode (DESIGN.md 2.11): writes, retransmissions, one reaction per window")
+    p.add_argument("--tcp-acks", action="store_true",
+                   help="with --tcp: ACK packets on the reverse path and retransmission timers (tgsim.h acks = 1)")
     p.add_argument("--flood-instances", type=int, default=1_000_000)
     p.add_argument("--flood-size", type=int, default=512)
     p.add_argument("--pub-every", type=int, default=4, help="windows between publication waves (flood)")
@@ -199,9 +201,13 @@ def exchange_cap(per_window: int, n_shards: int) -> int:
 
 def sim_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
+    # TCP with ACKs: a window stages the round's writes plus the last window's ACKs (one per
+    # delivered data packet) plus the fired timers, and keeps about twice the records in flight
+    acks = getattr(args, "tcp", False) and getattr(args, "tcp_acks", False)
+    per_window = args.instances * args.fanout * (2 if acks else 1) + (1 << 16 if acks else 0)
     return SimConfig(n_instances=args.instances, seed=args.seed, shard_id=shard, n_shards=n_shards, device=device,
-                     data_prefix_len=12, max_msgs_per_window=max(1 << 20, args.instances * args.fanout),
-                     max_records=args.max_records // max(1, n_shards // 2), max_states=4096,
+                     data_prefix_len=12, max_msgs_per_window=max(1 << 20, per_window),
+                     max_records=args.max_records * (2 if acks else 1) // max(1, n_shards // 2), max_states=4096,
                      exchange_cap=exchange_cap(args.instances * args.fanout, n_shards))
 
 
@@ -271,7 +277,7 @@ def main():
         if world > 1:
             raise SystemExit("--tcp: TCP mode needs a single-shard context")
         rounds = args.warmup + max(3, min(10, args.warmup)) + args.steps + 1
-        sim.tcp_enable(max_writes=rounds * N * F, max_segments=rounds * N * F)
+        sim.tcp_enable(max_writes=rounds * N * F, max_segments=rounds * N * F, acks=args.tcp_acks)
 
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
@@ -342,7 +348,8 @@ def main():
     if rank == 0 and args.tcp:
         dt = {k: tcp1[k] - tcp0[k] for k in tcp1}
         print(json.dumps({
-            "metric": "TCP writes delivered/sec (100k-inst storm over TCP mode, DESIGN.md 2.11)",
+            "metric": "TCP writes delivered/sec (100k-inst storm over TCP mode, DESIGN.md 2.11)"
+                      + (", ACKs on the reverse path" if args.tcp_acks else ""),
             "value": dt["delivered"] / elapsed, "unit": "writes/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "packets_delivered_per_s": delivered / elapsed, "tcp_in_timed_steps": dt,

@@ -475,7 +475,8 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t stride = nblocks * blockDim.x;
   uint32_t it = 0;
-  const uint32_t n = a.n_dev ? *a.n_dev : a.n;
+  // device-counted: a.n is the staged capacity, and the count never exceeds it (appenders clamp)
+  const uint32_t n = a.n_dev ? min(*a.n_dev, a.n) : a.n;
   // Every load of a message is issued up front with clamped indices: one round trip for the SoA
   // record and one for the table gathers instead of a branch-serialised chain. The next message's
   // SoA record is loaded beside this one's gathers (software pipelining across the grid stride), so
@@ -3234,7 +3235,9 @@ static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
 #ifndef TG_BKT_MIN_KEYS
 #define TG_BKT_MIN_KEYS 48u  // small shards (strong scaling): more, smaller buckets
 #endif
-  const uint32_t slots = 3u * (uint32_t)d.n_cu;
+  // a context whose windows carry bkt_load times the packets per key (TCP acks: an ACK per data
+  // packet) splits its keys over as many more buckets, so a bucket still fits kBktCap items
+  const uint32_t slots = 3u * (uint32_t)d.n_cu * d.bkt_load;
   uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(TG_BKT_MIN_KEYS, K));
   w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
   return std::max<uint32_t>(w, 1u);

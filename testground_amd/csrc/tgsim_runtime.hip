@@ -1842,6 +1842,7 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
       return TGSIM_ENOMEM;
     HIPCK(c, hipMemsetAsync(d.s_done, 0, S, c->d.stream), "tcp init");
     d.acks = 1;
+    c->d.bkt_load = 2;  // every data packet is answered by an ACK: twice the copies per key
   }
   const size_t W = t.max_writes, S = t.max_segments;
   if (dalloc(c, &d.w_src, W) || dalloc(c, &d.w_dst, W) || dalloc(c, &d.w_rem, W) || dalloc(c, &d.w_state, W) ||

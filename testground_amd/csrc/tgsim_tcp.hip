@@ -93,6 +93,16 @@ __device__ __forceinline__ void block_partial(uint32_t v, uint32_t* part) {
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// A reservation of n staged slots behind the device-side count that never leaves the count above
+// the capacity: an adder that overshoots pulls it back to cap after its add, so once every adder
+// is done the count is <= cap, and every slot below it was reserved by exactly one adder (which
+// writes it when p < cap and reports ERR_CAP_M otherwise). The shape pass reads this count.
+__device__ __forceinline__ uint32_t reserve_staged(uint32_t* cnt, uint32_t n, uint32_t cap) {
+  const uint32_t old = atomicAdd(cnt, n);
+  if ((uint64_t)old + n > cap) atomicMin(cnt, cap);
+  return old;
+}
+
 __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict__ status,
                                                        const uint32_t* __restrict__ seq, uint32_t n_host,
                                                        const uint32_t* n_dev, TcpDev t) {
@@ -310,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_release(TcpDev t, uint32_t cur, 
       atomicSub(&t.pend_by[t.w_src[w]], 1u);
       continue;
     }
-    const uint32_t p = atomicAdd(&sc->n_msgs_dev, 1u);
+    const uint32_t p = reserve_staged(&sc->n_msgs_dev, 1u, cap);
     if (p >= cap) {
       atomicOr(&sc->err, ERR_CAP_M);
       continue;
@@ -333,8 +343,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_tplan(TcpDev t, DevScalars* sc, 
   if (threadIdx.x == 0) {
     const uint32_t base = sc->n_msgs_dev, na = t.sc->ack_n;
     t.sc->ack_base = base;
-    sc->n_msgs_dev = base + na;
-    if (base + na > cap) atomicOr(&sc->err, ERR_CAP_M);
+    // ACK slots beyond the capacity are not written (k_tcp_fire) and not counted
+    sc->n_msgs_dev = (uint64_t)base + na > cap ? cap : base + na;
+    if ((uint64_t)base + na > cap) atomicOr(&sc->err, ERR_CAP_M);
   }
   uint32_t carry = 0;
   for (uint32_t b0 = tail; b0 < head; b0 += kBlock) {  // block-uniform
@@ -441,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
     const uint32_t pf = block_excl_scan(fire ? 1u : 0u, red, totf);
     const uint32_t pk = block_excl_scan(keep ? 1u : 0u, red, totk);
     if (threadIdx.x == 0) {
-      sb_f = totf ? atomicAdd(&sc->n_msgs_dev, totf) : 0u;
+      sb_f = totf ? reserve_staged(&sc->n_msgs_dev, totf, cap) : 0u;
       sb_k = totk ? atomicAdd(&t.sc->pend_n[nxt], totk) : 0u;
     }
     __syncthreads();

@@ -433,3 +433,24 @@ def test_tcp_storm_hip_matches_oracle(hip, oracle, wait):
     """async: every window and reaction queued without a host read-back (bench.py --tcp's loop)."""
     a, b = run_tcp_storm(hip, wait=wait), run_tcp_storm(oracle)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
+
+
+@pytest.mark.gpu
+def test_tcp_acks_staged_overflow_reports_capacity(hip):
+    """acks mode stages the last reaction's ACKs and the fired timers behind the device-side staged
+    count, which the host cannot see: a window whose data + ACKs exceed max_msgs_per_window must end
+    in ECAPACITY with the count held at the capacity (the netem pass reads it), not read past the
+    staged arrays. 400 instances x fanout 8 = 3200 writes per round plus ~3200 ACKs > 4096."""
+    s = Simulator(SimConfig(n_instances=400, seed=4, max_msgs_per_window=4096, max_records=1 << 18,
+                            max_states=64), binding=hip)
+    s.tcp_enable(max_attempts=5, rto_ns=30 * MS, acks=True)
+    for g in range(400):
+        s.set_shape(g, make_shape(latency_ns=5 * MS, bandwidth_bps=10_000_000))
+    with pytest.raises(A.TgsimError) as e:
+        for r in range(4):
+            s.tcp_gen_storm_round(r, A.T_NOW, 8, 1024, 5 * MS, r)
+            s.advance_to_barrier(s.barrier(r, 400, A.T_NOW), 1 * MS)
+            s.tcp_react()
+        s.sync()
+    assert e.value.code == A.ECAPACITY
+    s.close()
