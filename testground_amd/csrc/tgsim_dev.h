@@ -76,7 +76,7 @@ struct TcpDev {
   int64_t* w_tarr = nullptr;      // delivery time (the latest segment's arrival); INT64_MIN until delivered
   int64_t* w_tmax = nullptr;      // latest arrival so far of a multi-segment write (atomicMax)
   int64_t* w_fail = nullptr;      // earliest failure key t * 2 + (timeout ? 1 : 0) (atomicMin)
-  uint32_t* s_w = nullptr;        // write (bits 0-27) | copies of the current attempt << 28 | kSoleSeg
+  uint32_t* s_w = nullptr;        // write (bits 0-27) | copies of the current attempt << 28 | kRetxBit (acks) | kSoleSeg
   uint32_t *s_wire = nullptr, *s_att = nullptr, *s_out = nullptr, *s_mark = nullptr;
   int64_t *s_tatt = nullptr, *s_arr = nullptr, *s_tlast = nullptr;
   // per-window decision bits: retransmissions over the packets (bm_s) and the deliveries (bm_r),

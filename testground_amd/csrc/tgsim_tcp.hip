@@ -38,6 +38,10 @@ constexpr uint32_t kArrived = 0xFFFFFFFFu;  // s_mark of a duplicated segment th
 constexpr uint32_t kSoleSeg = 0x80000000u;  // s_w: the segment is its write's only one
 constexpr uint32_t kWMask = 0x0FFFFFFFu;    // s_w: the write
 constexpr uint32_t kQShift = 28;            // s_w: copies of the current attempt (2 bits)
+constexpr uint32_t kRetxBit = 0x40000000u;  // s_w, acks mode: the segment was retransmitted (s_att > 0)
+constexpr uint32_t kPlanLds = 1024;         // k_tcp_fire: timer plans up to this many batches are searched in LDS
+constexpr uint32_t kFireRounds = 8;         // k_tcp_fire: rounds of entries per block reservation (mask bits)
+constexpr uint32_t kFireUnroll = 4;         // k_tcp_fire: entries whose loads are in flight together
 
 __device__ __forceinline__ uint32_t tcp_copies(uint8_t st) {
   const uint32_t code = st & 0x0Fu;
@@ -167,8 +171,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
         ack = true;
         const uint32_t sid = sq >> 4, sw = t.s_w[sid];
         // the first attempt's only copy is the segment's only delivery (a later attempt - and with
-        // it another copy - would have raised s_att): this thread settles it
-        if (((sw >> kQShift) & 3u) == 1u && t.s_att[sid] == 0) {
+        // it another copy - would have set kRetxBit): this thread settles it
+        if (((sw >> kQShift) & 3u) == 1u && !(sw & kRetxBit)) {
           t.s_mark[sid] = kArrived;
           ndel += tcp_arrived(t, sw, ti);
         } else {
@@ -408,65 +412,113 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
     }
   }
   const uint32_t np = t.sc->plan_n, nb = t.sc->plan_total, total = nb + t.sc->pend_n[cur];
-  uint32_t nfire = 0;
-  for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += stride) {  // block-uniform
-    const uint32_t j = b0 + threadIdx.x;
-    bool fire = false, keep = false;
-    uint32_t sid = 0, w = 0, att = 0;
-    int64_t tf = 0;
-    if (j < total) {
-      const bool batch = j < nb;
-      if (batch) {  // the last plan entry starting at or before j (empty entries share offsets)
-        uint32_t l = 0, h = np;
-        while (h - l > 1) {
-          const uint32_t mid = (l + h) >> 1;
-          if (t.plan_off[mid] <= j) l = mid; else h = mid;
-        }
-        sid = t.plan_lo[l] + (j - t.plan_off[l]);
-      } else {
-        sid = t.pend[cur][j - nb];
+  // the plan (a few dozen live batches) in LDS: locating an entry costs no global round trip
+  __shared__ uint32_t s_off[kPlanLds], s_lo[kPlanLds];
+  const bool lds = np <= kPlanLds;
+  if (lds) {
+    for (uint32_t k = threadIdx.x; k < np; k += kBlock) {
+      s_off[k] = t.plan_off[k];
+      s_lo[k] = t.plan_lo[k];
+    }
+    __syncthreads();
+  }
+  // entry j -> its segment: a batch entry (the last plan entry starting at or before j; empty
+  // entries share offsets) or a retransmitted attempt's timer
+  auto locate = [&](uint32_t j) -> uint32_t {
+    if (j >= nb) return t.pend[cur][j - nb];
+    uint32_t l = 0, h = np;
+    if (lds) {
+      while (h - l > 1) {
+        const uint32_t mid = (l + h) >> 1;
+        if (s_off[mid] <= j) l = mid; else h = mid;
       }
-      const uint32_t a = t.s_att[sid];
-      // a batch entry whose segment was retransmitted already has its timer on the list
-      if (!(batch && a != 0) && t.s_done[sid] == 0) {
-        w = t.s_w[sid] & kWMask;
-        const uint32_t wst = t.w_state[w];
-        if (wst != TGSIM_TCP_TIMEOUT && wst != TGSIM_TCP_REFUSED) {
-          const int64_t T = t.s_tatt[sid] + (t.rto << a);
-          if (T >= t_end) {
-            keep = !batch;
-          } else if (a + 1u >= t.max_att) {
-            t.s_done[sid] = 2;
-            if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, T, TGSIM_TCP_TIMEOUT);
-          } else {
-            att = a + 1u;
-            tf = T > H ? T : H;
-            t.s_att[sid] = att;
-            t.s_tatt[sid] = tf;
-            fire = keep = true;
-          }
+      return s_lo[l] + (j - s_off[l]);
+    }
+    while (h - l > 1) {
+      const uint32_t mid = (l + h) >> 1;
+      if (t.plan_off[mid] <= j) l = mid; else h = mid;
+    }
+    return t.plan_lo[l] + (j - t.plan_off[l]);
+  };
+  // A block takes kFireRounds rounds of entries at a time: the decisions (and their effects on the
+  // segment) first, recorded as one bit per round in two masks per thread, then one reservation per
+  // block for the fired packets and one for the kept timers, then the writes. A reservation per
+  // round would put total / 256 updates on each of the two counters, which the memory side
+  // serialises.
+  const uint32_t span = kBlock * kFireRounds;
+  uint32_t nfire = 0;
+  for (uint32_t c0 = blockIdx.x * span; c0 < total; c0 += gridDim.x * span) {  // block-uniform
+    uint32_t fmask = 0, kmask = 0;
+    // kFireUnroll entries at a time, each level of their dependent loads issued together
+    for (uint32_t r0 = 0; r0 < kFireRounds; r0 += kFireUnroll) {
+      uint32_t sid[kFireUnroll], a[kFireUnroll], sw[kFireUnroll], wst[kFireUnroll];
+      uint8_t dn[kFireUnroll];
+      int64_t ta[kFireUnroll];
+      bool batch[kFireUnroll], live[kFireUnroll];
+#pragma unroll
+      for (uint32_t u = 0; u < kFireUnroll; ++u) {
+        const uint32_t j = c0 + (r0 + u) * kBlock + threadIdx.x;
+        live[u] = j < total;
+        batch[u] = j < nb;
+        sid[u] = live[u] ? locate(j) : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kFireUnroll; ++u) {
+        a[u] = live[u] ? t.s_att[sid[u]] : 0u;
+        dn[u] = live[u] ? t.s_done[sid[u]] : (uint8_t)1;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kFireUnroll; ++u) {
+        // a batch entry whose segment was retransmitted already has its timer on the list
+        live[u] = live[u] && !(batch[u] && a[u] != 0) && dn[u] == 0;
+        sw[u] = live[u] ? t.s_w[sid[u]] : 0u;
+        ta[u] = live[u] ? t.s_tatt[sid[u]] : 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kFireUnroll; ++u) wst[u] = live[u] ? t.w_state[sw[u] & kWMask] : 0u;
+#pragma unroll
+      for (uint32_t u = 0; u < kFireUnroll; ++u) {
+        if (!live[u] || wst[u] == TGSIM_TCP_TIMEOUT || wst[u] == TGSIM_TCP_REFUSED) continue;
+        const uint32_t r = r0 + u, w = sw[u] & kWMask;
+        const int64_t T = ta[u] + (t.rto << a[u]);
+        if (T >= t_end) {
+          if (!batch[u]) kmask |= 1u << r;
+        } else if (a[u] + 1u >= t.max_att) {
+          t.s_done[sid[u]] = 2;
+          if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, T, TGSIM_TCP_TIMEOUT);
+        } else {
+          t.s_att[sid[u]] = a[u] + 1u;
+          t.s_tatt[sid[u]] = T > H ? T : H;
+          if (!(sw[u] & kRetxBit)) t.s_w[sid[u]] = sw[u] | kRetxBit;
+          fmask |= 1u << r;
+          kmask |= 1u << r;
         }
       }
     }
     uint32_t totf, totk;
-    const uint32_t pf = block_excl_scan(fire ? 1u : 0u, red, totf);
-    const uint32_t pk = block_excl_scan(keep ? 1u : 0u, red, totk);
+    const uint32_t pf = block_excl_scan((uint32_t)__popc(fmask), red, totf);
+    const uint32_t pk = block_excl_scan((uint32_t)__popc(kmask), red, totk);
     if (threadIdx.x == 0) {
       sb_f = totf ? reserve_staged(&sc->n_msgs_dev, totf, cap) : 0u;
       sb_k = totk ? atomicAdd(&t.sc->pend_n[nxt], totk) : 0u;
     }
     __syncthreads();
-    if (fire) {
-      const uint32_t p = sb_f + pf;
+    uint32_t qf = sb_f + pf, qk = sb_k + pk;
+    for (uint32_t m = kmask; m; m &= m - 1) {  // every fired entry is also kept
+      const uint32_t r = (uint32_t)__builtin_ctz(m);
+      const uint32_t sid = locate(c0 + r * kBlock + threadIdx.x);
+      t.pend[nxt][qk++] = sid;
+      if (!((fmask >> r) & 1u)) continue;
+      const uint32_t w = t.s_w[sid] & kWMask, src = t.w_src[w];
+      const uint32_t p = qf++;
       if (p < cap) {
-        m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | att; m_size[p] = t.s_wire[sid];
-        m_t[p] = tf;
+        m_src[p] = src; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | t.s_att[sid]; m_size[p] = t.s_wire[sid];
+        m_t[p] = t.s_tatt[sid];
       } else {
         atomicOr(&sc->err, ERR_CAP_M);
       }
-      atomicAdd(&t.pend_by[t.w_src[w]], 1u);  // released into this window until its status is read
+      atomicAdd(&t.pend_by[src], 1u);  // released into this window until its status is read
     }
-    if (keep) t.pend[nxt][sb_k + pk] = sid;
     nfire += totf;
     __syncthreads();  // sb_f / sb_k are rewritten by the next round
   }
@@ -523,7 +575,7 @@ hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_de
                                    bool reg, uint32_t lo, uint32_t hi) {
   if (!base_dev) hipLaunchKernelGGL(k_tcp_base, dim3(1), dim3(kBlock), 0, d.stream, d.sc, base_host);
   hipLaunchKernelGGL(k_tcp_tplan, dim3(1), dim3(kBlock), 0, d.stream, t, d.sc, head, reg ? 1u : 0u, lo, hi, d.cap_msgs);
-  hipLaunchKernelGGL(k_tcp_fire, dim3(512), dim3(kBlock), 0, d.stream, t, d.sc, cur, d.cap_msgs, d.o_src, d.o_dst,
+  hipLaunchKernelGGL(k_tcp_fire, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, t, d.sc, cur, d.cap_msgs, d.o_src, d.o_dst,
                      d.o_seq, d.o_t, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
