@@ -311,28 +311,52 @@ __global__ __launch_bounds__(kBlock) void k_tcp_release(TcpDev t, uint32_t cur, 
                                                         uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
                                                         uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
                                                         int64_t* __restrict__ m_t) {
+  // one reservation per block and round for the released packets and one for the kept entries
+  // (per-item reservations serialise on the two counters at the memory side)
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t sb_r, sb_k;
   const uint32_t n = t.sc->pend_n[cur], nxt = cur ^ 1u;
   const int64_t t_end = sc->t_end;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t sid = t.pend[cur][i], w = t.s_w[sid] & kWMask;
-    const int64_t ta = t.s_tatt[sid];
-    if (t.w_state[w] == TGSIM_TCP_PENDING && ta >= t_end) {
-      t.pend[nxt][atomicAdd(&t.sc->pend_n[nxt], 1u)] = sid;
-      continue;
+  uint32_t nrel = 0;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
+    const uint32_t i = b0 + threadIdx.x;
+    bool rel = false, keep = false;
+    uint32_t sid = 0, w = 0;
+    int64_t ta = 0;
+    if (i < n) {
+      sid = t.pend[cur][i];
+      w = t.s_w[sid] & kWMask;
+      ta = t.s_tatt[sid];
+      if (t.w_state[w] != TGSIM_TCP_PENDING) {  // the write has failed: nothing more is sent
+        atomicSub(&t.pend_by[t.w_src[w]], 1u);
+      } else if (ta >= t_end) {
+        keep = true;
+      } else {
+        rel = true;
+      }
     }
-    if (t.w_state[w] != TGSIM_TCP_PENDING) {  // the write has failed: nothing more is sent
-      atomicSub(&t.pend_by[t.w_src[w]], 1u);
-      continue;
+    uint32_t totr, totk;
+    const uint32_t pr = block_excl_scan(rel ? 1u : 0u, red, totr);
+    const uint32_t pk = block_excl_scan(keep ? 1u : 0u, red, totk);
+    if (threadIdx.x == 0) {
+      sb_r = totr ? reserve_staged(&sc->n_msgs_dev, totr, cap) : 0u;
+      sb_k = totk ? atomicAdd(&t.sc->pend_n[nxt], totk) : 0u;
     }
-    const uint32_t p = reserve_staged(&sc->n_msgs_dev, 1u, cap);
-    if (p >= cap) {
-      atomicOr(&sc->err, ERR_CAP_M);
-      continue;
+    __syncthreads();
+    if (keep) t.pend[nxt][sb_k + pk] = sid;
+    if (rel) {
+      const uint32_t p = sb_r + pr;
+      if (p < cap) {
+        m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | t.s_att[sid]; m_size[p] = t.s_wire[sid];
+        m_t[p] = ta;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_M);
+      }
     }
-    m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | t.s_att[sid]; m_size[p] = t.s_wire[sid];
-    m_t[p] = ta;
-    atomicAdd(&t.sc->released, 1ull);
+    nrel += totr;
+    __syncthreads();  // sb_r / sb_k are rewritten by the next round
   }
+  if (threadIdx.x == 0 && nrel) atomicAdd(&t.sc->released, (unsigned long long)nrel);
 }
 
 // acks mode, window start (one block): the last reaction's ACKs get their staged slots; the live
