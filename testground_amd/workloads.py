@@ -13,31 +13,60 @@ MS = 1_000_000
 
 
 def random_regular_graph(n: int, degree: int = 8, seed: int = 5) -> tuple[np.ndarray, np.ndarray]:
-    """Random `degree`-regular graph by the permutation model: degree/2 uniform permutations s_i,
-    v adjacent to s_i(v) and s_i^-1(v). Self loops and repeated neighbours (O(degree^2) vertices, about 28 at degree 8, in
-    expectation) are dropped, so the graph is simple and symmetric and all but a handful of vertices
-    have exactly `degree` neighbours. Returns CSR (offsets[n+1] u32, neighbours u32); neighbours keep
-    the generation order (the flood's seq slot)."""
-    assert degree % 2 == 0 and n > degree
+    """Random `degree`-regular simple graph by the configuration model:
+    n * degree stubs paired uniformly at random, then every self loop and every repeated edge (about
+    (d-1)/2 + (d-1)^2/4, ~16 at degree 8, in expectation) removed by a random switching with another
+    edge: (a, b) + (c, d) -> (a, c) + (b, d), taken only when neither new edge is a loop or already
+    present. Every vertex ends with exactly `degree` neighbours. Returns CSR (offsets[n+1] u32,
+    neighbours u32); a vertex's neighbours are in edge order (the flood's seq slot)."""
+    assert (n * degree) % 2 == 0 and n > degree
     rng = np.random.default_rng(seed)
-    cols = []
-    for _ in range(degree // 2):
-        s = rng.permutation(n).astype(np.int64)
-        inv = np.empty_like(s)
-        inv[s] = np.arange(n)
-        cols += [s, inv]
-    nb = np.stack(cols, axis=1)                                   # [n, degree]
-    keep = nb != np.arange(n)[:, None]
-    order = np.argsort(nb, axis=1, kind="stable")
-    srt = np.take_along_axis(nb, order, axis=1)
-    dup_sorted = np.zeros_like(keep)
-    dup_sorted[:, 1:] = srt[:, 1:] == srt[:, :-1]                  # later copies of a repeated neighbour
-    dup = np.zeros_like(keep)
-    np.put_along_axis(dup, order, dup_sorted, axis=1)
-    keep &= ~dup
+    stubs = np.repeat(np.arange(n, dtype=np.int64), degree)
+    rng.shuffle(stubs)
+    u, v = stubs[0::2].copy(), stubs[1::2].copy()                 # edge e = (u[e], v[e])
+    m = len(u)
+    keys = np.minimum(u, v) * n + np.maximum(u, v)
+    order = np.argsort(keys, kind="stable")
+    sk = keys[order]
+    bad = u == v
+    rep = np.zeros(m, bool)
+    rep[order[1:][sk[1:] == sk[:-1]]] = True                      # later copies of a repeated edge
+    bad |= rep
+    delta: dict[int, int] = {}                                    # edge multiset = sk + delta
+
+    def key(a: int, b: int) -> int:
+        return min(a, b) * n + max(a, b)
+
+    def present(k: int) -> bool:
+        base = int(np.searchsorted(sk, k, "right") - np.searchsorted(sk, k, "left"))
+        return base + delta.get(k, 0) > 0
+
+    for e1 in np.flatnonzero(bad).tolist():
+        a, b = int(u[e1]), int(v[e1])
+        while True:
+            e2 = int(rng.integers(m))
+            if e2 == e1 or bad[e2]:
+                continue
+            c, d = int(u[e2]), int(v[e2])
+            if rng.integers(2):
+                c, d = d, c
+            if a == c or b == d:
+                continue
+            k1, k2 = key(a, c), key(b, d)
+            if k1 == k2 or present(k1) or present(k2):
+                continue
+            break
+        for k, dv in ((key(a, b), -1), (key(c, d), -1), (k1, 1), (k2, 1)):
+            delta[k] = delta.get(k, 0) + dv
+        u[e1], v[e1], u[e2], v[e2] = a, c, b, d
+        bad[e1] = False
+    src = np.concatenate([u, v])
+    dst = np.concatenate([v, u])
+    slot = np.concatenate([2 * np.arange(m), 2 * np.arange(m) + 1])
+    o = np.lexsort((slot, src))
     off = np.zeros(n + 1, np.uint32)
-    off[1:] = np.cumsum(keep.sum(axis=1))
-    return off, nb[keep].astype(np.uint32)
+    off[1:] = np.cumsum(np.bincount(src, minlength=n))
+    return off, dst[o].astype(np.uint32)
 
 
 def pubsub_shapes(n: int, seed: int = 5) -> list:

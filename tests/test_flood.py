@@ -57,7 +57,17 @@ def test_graph_is_simple_and_symmetric():
     assert not np.any(src == nbr)
     e = set(zip(src.tolist(), nbr.tolist()))
     assert len(e) == len(src) and all((b, a) in e for a, b in e)
-    assert np.count_nonzero(np.diff(off.astype(np.int64)) == 8) >= n - 60   # O(degree^2) defects
+    assert np.all(np.diff(off.astype(np.int64)) == 8)                        # exactly regular
+
+
+def test_configuration_model_repairs_loops_and_repeats():
+    """Small n forces many loops / repeated pairs in the raw pairing; every one is switched away."""
+    for n, d, seed in ((12, 6, 1), (30, 8, 2), (101, 4, 3), (1000, 8, 4)):
+        off, nbr = W.random_regular_graph(n, d, seed)
+        src = np.repeat(np.arange(n), np.diff(off.astype(np.int64)))
+        assert np.all(np.diff(off.astype(np.int64)) == d) and not np.any(src == nbr)
+        e = set(zip(src.tolist(), nbr.tolist()))
+        assert len(e) == n * d and all((b, a) in e for a, b in e)
 
 
 def test_flood_oracle_invariants(oracle):
