@@ -167,7 +167,10 @@ struct Dev {
   uint32_t* vals2 = nullptr;
   uint32_t* tot = nullptr;        // [kMaxBins]
   int n_cu = 256;                 // compute units of the device (bucket widths)
-  uint32_t bkt_load = 1;          // copies per key relative to one packet per message (TCP acks: 2)
+#ifndef TG_BKT_LOAD
+#define TG_BKT_LOAD 1u
+#endif
+  uint32_t bkt_load = TG_BKT_LOAD;  // copies per key relative to one packet per message (TCP acks: 2)
   int grid_shape = 2048;          // k_shape / k_gen_storm grids (init_launch_geometry)
   int grid_gen = 2048;
   uint32_t* bstart = nullptr;     // [kMaxBins + 1] bucket starts of the last partition pass
