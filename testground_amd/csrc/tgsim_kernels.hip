@@ -3240,6 +3240,8 @@ static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
   const uint32_t slots = 3u * (uint32_t)d.n_cu * d.bkt_load;
   uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(TG_BKT_MIN_KEYS, K));
   w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
+  // never more than kMaxBins buckets (the partition's LDS histograms and d.poff rows are that wide)
+  w = std::max<uint32_t>(w, (K + kMaxBins - 1) / kMaxBins);
   return std::max<uint32_t>(w, 1u);
 }
 
@@ -3311,7 +3313,8 @@ static hipError_t run_token_bucket(Dev& d) {
   p.A = d.A; p.shape = d.shape; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
-  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= 2048: nloc <= 2^20 (checked at create)
+  const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= kMaxBins (bkt_width_fused)
+  if (B > (uint32_t)kMaxBins) return hipErrorInvalidValue;
   const BktSrc src = bkt_queue(d, Q_A);
   TG_CHECK(bkt_local(d, src, bd, B));
   {
@@ -3439,6 +3442,7 @@ hipError_t window_end(Dev& d) {
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
+  if (B > (uint32_t)kMaxBins) return hipErrorInvalidValue;
   const BktSrc srcD = bkt_queue(d, Q_D), srcL = bkt_queue(d, Q_L);
   {
     ProfScope ps_(d, KID_BKT_SCATTER);
