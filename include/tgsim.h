@@ -381,6 +381,20 @@ int tgsim_flood_publish(tgsim_ctx* ctx, const uint32_t* instances, const uint32_
                         size_t n, uint32_t size);
 int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
 
+/* ---- window-boundary snapshot (SURVEY.md 5 checkpoint/resume) ---------------------------------
+ * The whole message-path state between windows as an opaque image: in-flight records (the timing
+ * wheel), token buckets, queue occupancy, netem correlation states, every configuration table
+ * (shapes, rules, routing policy, link enable, addresses), the sync service (counts, signal log,
+ * barrier waiters), the clock and the last window's deliveries. Philox draws are counter-based, so
+ * a run restored into a fresh context continues bit for bit as the uninterrupted run would.
+ * tgsim_snapshot(ctx, NULL, 0, &n) returns the size; it synchronises the context. The image is
+ * restored into a context created with the same configuration: per shard, a sharded run snapshots
+ * every shard and sets the transport of the restored contexts again. Both calls need a window
+ * boundary with nothing staged (ESTATE) and are ENOTSUP once TCP mode, topics or a flood graph are in
+ * use. A malformed or foreign image is EINVAL and leaves the context unchanged. */
+int tgsim_snapshot(tgsim_ctx* ctx, void* buf, size_t cap, size_t* n);
+int tgsim_restore(tgsim_ctx* ctx, const void* buf, size_t n);
+
 /* ---- TCP-level mode ----------------------------------
  * The reference plans move application data over TCP (plans/benchmarks/storm.go:127-180 dials and
  * writes in chunks, plans/network/pingpong.go:73-104 times round trips over a connection); with loss

@@ -183,6 +183,8 @@ _SIGS_HIP = {
     "sync_subscribe_device": (C.c_int, [P, C.c_size_t, P, P, P, C.c_uint32, P, P, C.c_size_t]),
     "topic_arena_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "snapshot": (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "restore": (C.c_int, [P, C.c_void_p, C.c_size_t]),
 }
 
 

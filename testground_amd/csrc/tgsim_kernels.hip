@@ -1179,7 +1179,10 @@ __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const 
 // Wheel insert with buckets = slots (slots <= kMaxBins): records are copied straight from the L
 // batch into this window's arena region in slot order, and the slot directory is the scan. The
 // first block also closes the window's counters (the former k_finish).
-constexpr int kWheelUnroll = 8;
+#ifndef TG_WHEEL_UNROLL
+#define TG_WHEEL_UNROLL 8
+#endif
+constexpr int kWheelUnroll = TG_WHEEL_UNROLL;
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // Queue occupancy: a record entering the wheel for the first time (no

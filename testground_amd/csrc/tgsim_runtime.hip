@@ -2056,3 +2056,205 @@ extern "C" int tgsim_tcp_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t
   c->tstats.packets += n;
   return TGSIM_OK;
 }
+
+// ============================== window-boundary snapshot ===================================
+// SURVEY.md 5 (checkpoint/resume, optional): the message path's whole state between windows as one
+// opaque image - device: scalars (clock, wheel ring, counters), token buckets, queue occupancy,
+// correlation states, the timing-wheel arena with its regions and slot directories, the last
+// window's deliveries, the sync service (counts, times, chunks, the used part of the signal log and
+// of the waiter table); host: the configuration mirrors (shapes, correlations, flags, addresses,
+// rules, pending resets), the clock, the queue-limit bound. Device tables compiled from the host
+// mirrors are re-uploaded at the next window. Randomness needs no state (Philox is counter-based).
+namespace {
+
+constexpr uint64_t kSnapMagic = 0x3130504E53475454ull;  // "TTGSNP01"
+
+struct SnapHeader {
+  uint64_t magic, bytes;
+  uint32_t dev_scalars, N, S, shard, nloc, slots, cap_rec, cap_msgs, max_states, max_waiters;
+  uint64_t max_signals, seed, cap_arena;
+};
+
+struct SnapWriter {  // sizing pass when p == nullptr
+  uint8_t* p;
+  size_t n = 0;
+  void raw(const void* src, size_t k) {
+    if (p) memcpy(p + n, src, k);
+    n += k;
+  }
+  template <class T> void val(const T& v) { raw(&v, sizeof(T)); }
+  template <class T> void vec(const std::vector<T>& v) {
+    val<uint64_t>(v.size());
+    raw(v.data(), v.size() * sizeof(T));
+  }
+};
+
+struct SnapReader {
+  const uint8_t* p;
+  size_t n, at = 0;
+  bool ok = true;
+  const uint8_t* take(size_t k) {
+    if (!ok || k > n - at) { ok = false; return nullptr; }
+    const uint8_t* q = p + at;
+    at += k;
+    return q;
+  }
+  template <class T> T val() {
+    T v{};
+    if (const uint8_t* q = take(sizeof(T))) memcpy(&v, q, sizeof(T));
+    return v;
+  }
+  template <class T> bool vec(std::vector<T>& v, size_t expect = SIZE_MAX) {
+    const uint64_t k = val<uint64_t>();
+    if (!ok || (expect != SIZE_MAX && k != expect) || k > (n - at) / sizeof(T)) return ok = false;
+    v.resize(k);
+    if (const uint8_t* q = take(k * sizeof(T))) memcpy(v.data(), q, k * sizeof(T));
+    return ok;
+  }
+};
+
+// the device state regions (pointer, bytes), in image order
+std::vector<std::pair<void*, size_t>> snap_regions(tgsim_ctx* c) {
+  Dev& d = c->d;
+  const size_t nl = std::max<size_t>(c->nloc, 1), phys = (size_t)kNSub * d.subcap;
+  return {
+      {d.sc, sizeof(DevScalars)},
+      {d.X, 8 * nl},
+      {d.pend, 4 * nl},
+      {d.cor_last, 16 * nl},
+      {d.arena, sizeof(tgsim_record) * d.cap_arena},
+      {d.regions, sizeof(RegionDev) * kMaxRegions},
+      {d.dirs, 4ull * kMaxRegions * (d.slots + 1)},
+      {d.o_t, 8 * phys}, {d.o_src, 4 * phys}, {d.o_dst, 4 * phys}, {d.o_seq, 4 * phys},
+      {d.o_size, 4 * phys}, {d.o_flags, 4 * phys}, {d.o_coff, 4 * phys},
+      {d.inbox, 4 * ((size_t)c->nloc + 1)},
+      {d.stats, 8ull * kNSub * 16},
+      {d.sig_red, 8 * 4},
+      {d.st_count, 4ull * d.max_states},
+      {d.st_last, 8ull * d.max_states},
+      {d.st_nchunks, 4ull * d.max_states},
+      {d.st_chunks, sizeof(SigChunk) * d.max_states * kMaxChunksPerState},
+      {d.sig_log, 8 * c->sig_log_used},
+      {d.w_state, 4ull * c->n_waiters}, {d.w_target, 4ull * c->n_waiters},
+      {d.w_twait, 8ull * c->n_waiters}, {d.w_release, 8ull * c->n_waiters},
+  };
+}
+
+SnapHeader snap_header(tgsim_ctx* c) {
+  SnapHeader h{};
+  h.magic = kSnapMagic;
+  h.dev_scalars = sizeof(DevScalars);
+  h.N = c->N; h.S = c->S; h.shard = c->shard; h.nloc = c->nloc; h.slots = c->d.slots;
+  h.cap_rec = c->d.cap_rec; h.cap_msgs = c->d.cap_msgs; h.max_states = c->d.max_states;
+  h.max_waiters = c->d.max_waiters; h.max_signals = c->d.max_signals; h.seed = c->cfg.seed;
+  h.cap_arena = c->d.cap_arena;
+  return h;
+}
+
+// the host half; the same function writes (w.p set), sizes (w.p null)
+void snap_host(tgsim_ctx* c, SnapWriter& w) {
+  w.vec(c->shape_h); w.vec(c->flags_h); w.vec(c->ip_h); w.vec(c->rho_h); w.vec(c->corr_epoch);
+  w.vec(c->corr_reset); w.vec(c->tb_reset); w.vec(c->st_last_h);
+  w.val<uint64_t>(c->moved.size());
+  for (const auto& kv : c->moved) { w.val(kv.first); w.val(kv.second); }
+  w.val<uint64_t>(c->rules_h.size());
+  for (const auto& r : c->rules_h) w.vec(r);
+  w.val(c->now); w.val(c->horizon); w.val(c->n_status_last); w.val(c->sig_log_used); w.val(c->n_waiters);
+  w.val(c->pend_bound); w.val(c->pend_exact);
+}
+
+int snap_refusal(tgsim_ctx* c) {
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "snapshot/restore: inside a window");
+  if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "snapshot/restore: messages are staged");
+  if (c->tcp_on || c->tp_n || !c->fl_off.empty())
+    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics and flood graphs are not captured");
+  return TGSIM_OK;
+}
+
+}  // namespace
+
+extern "C" int tgsim_snapshot(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  int rc = snap_refusal(c);
+  if (rc) return rc;
+  rc = sync_and_check(c);  // commits a deferred storm batch, settles the device clock
+  if (rc) return rc;
+  const auto regs = snap_regions(c);
+  SnapWriter sz{nullptr};
+  sz.val(SnapHeader{});
+  snap_host(c, sz);
+  for (const auto& r : regs) sz.n += r.second;
+  *n = sz.n;
+  if (!buf) return TGSIM_OK;
+  if (cap < sz.n) return fail(c, TGSIM_ECAPACITY, "snapshot needs %zu bytes", sz.n);
+  SnapHeader h = snap_header(c);
+  h.bytes = sz.n;
+  SnapWriter w{static_cast<uint8_t*>(buf)};
+  w.val(h);
+  snap_host(c, w);
+  for (const auto& r : regs) {
+    if (r.second) HIPCK(c, hipMemcpyAsync(w.p + w.n, r.first, r.second, hipMemcpyDeviceToHost, c->d.stream), "snapshot");
+    w.n += r.second;
+  }
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "snapshot");
+  return TGSIM_OK;
+}
+
+extern "C" int tgsim_restore(tgsim_ctx* c, const void* buf, size_t n) {
+  if (!c || !buf) return TGSIM_EINVAL;
+  int rc = snap_refusal(c);
+  if (rc) return rc;
+  if (c->storm_pending) return fail(c, TGSIM_ESTATE, "restore: a storm round is pending");
+  SnapReader r{static_cast<const uint8_t*>(buf), n};
+  const SnapHeader h = r.val<SnapHeader>(), want = snap_header(c);
+  if (!r.ok || h.magic != kSnapMagic || h.bytes != n) return fail(c, TGSIM_EINVAL, "restore: not a snapshot image");
+  SnapHeader hc = h;
+  hc.bytes = 0;
+  if (memcmp(&hc, &want, sizeof(SnapHeader)) != 0)
+    return fail(c, TGSIM_EINVAL, "restore: the image was taken from a context with another configuration");
+  // host half into temporaries first: a malformed image leaves the context untouched
+  std::vector<ShapeDev> shape; std::vector<uint8_t> flags; std::vector<uint32_t> ip, rho, epoch, creset, treset;
+  std::vector<int64_t> stlast;
+  r.vec(shape, c->nloc); r.vec(flags, c->N); r.vec(ip, c->N); r.vec(rho, 4 * (size_t)c->nloc);
+  r.vec(epoch, c->nloc); r.vec(creset); r.vec(treset); r.vec(stlast);
+  std::unordered_map<uint32_t, uint32_t> moved;
+  const uint64_t nm = r.val<uint64_t>();
+  for (uint64_t i = 0; r.ok && i < nm; ++i) {
+    const uint32_t k = r.val<uint32_t>();
+    moved[k] = r.val<uint32_t>();
+  }
+  std::vector<std::vector<RuleDev>> rules(r.val<uint64_t>() == c->nloc ? c->nloc : 0);
+  if (rules.size() != c->nloc) r.ok = false;
+  for (auto& v : rules) r.vec(v);
+  const int64_t now = r.val<int64_t>(), horizon = r.val<int64_t>();
+  const uint32_t n_status_last = r.val<uint32_t>();
+  const uint64_t sig_used = r.val<uint64_t>();
+  const uint32_t n_waiters = r.val<uint32_t>();
+  const uint64_t pend_bound = r.val<uint64_t>();
+  const bool pend_exact = r.val<bool>();
+  if (!r.ok || sig_used > c->d.max_signals || n_waiters > c->d.max_waiters)
+    return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
+  c->sig_log_used = sig_used;  // sizes the log / waiter regions below
+  c->n_waiters = n_waiters;
+  const auto regs = snap_regions(c);
+  size_t need = r.at;
+  for (const auto& g : regs) need += g.second;
+  if (need != n) return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
+  size_t at = r.at;
+  for (const auto& g : regs) {
+    if (g.second) HIPCK(c, hipMemcpyAsync(g.first, r.p + at, g.second, hipMemcpyHostToDevice, c->d.stream), "restore");
+    at += g.second;
+  }
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
+  c->shape_h.swap(shape); c->flags_h.swap(flags); c->ip_h.swap(ip); c->rho_h.swap(rho); c->corr_epoch.swap(epoch);
+  c->corr_reset.swap(creset); c->tb_reset.swap(treset); c->st_last_h.swap(stlast); c->moved.swap(moved);
+  c->rules_h.swap(rules);
+  c->now = now; c->horizon = horizon; c->n_status_last = n_status_last;
+  c->pend_bound = pend_bound; c->pend_exact = pend_exact;
+  c->now_from_device = false;
+  c->max_tsend_h = INT64_MIN;
+  c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = true;  // re-uploaded at the next window
+  memcpy(c->d.h_sc, r.p + r.at, sizeof(DevScalars));
+  return check_device_errors(c);
+}

@@ -288,6 +288,18 @@ class Simulator:
         self._check(self.lib.get_stats(self._ctx, C.byref(s)))
         return {name: getattr(s, name) for name, _ in A.Stats._fields_}
 
+    # ---- checkpoint / resume (HIP library only; tgsim.h tgsim_snapshot) ----------------------
+    def snapshot(self) -> bytes:
+        """The context's state at this window boundary as an opaque image (tgsim_restore)."""
+        n = C.c_size_t()
+        self._check(self.lib.snapshot(self._ctx, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        self._check(self.lib.snapshot(self._ctx, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, image: bytes) -> None:
+        self._check(self.lib.restore(self._ctx, image, len(image)))
+
     # ---- profiling (HIP library only) --------------------------------------------------------
     def profile(self, kernels=None) -> None:
         """Enable HIP-event timing for the named kernel classes (None = all, [] = off)."""

@@ -32,7 +32,8 @@ def random_shape(rng, *, allow_bw=True):
 
 
 def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_window: int = 300,
-               window_ns: int = 40 * MS, rules: bool = True, cfg_kw=None):
+               window_ns: int = 40 * MS, rules: bool = True, cfg_kw=None, restart=None):
+    """restart(w, sim) -> sim, after window w (checkpoint / resume tests)."""
     rng = np.random.default_rng(seed)
     cfg = SimConfig(n_instances=n_inst, seed=1000 + seed, **(cfg_kw or {}))
     sim = Simulator(cfg, binding=binding)
@@ -79,6 +80,8 @@ def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_
         t0 += window_ns
         sim.advance(t0)
         out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if restart is not None:
+            sim = restart(w, sim)
     # drain
     for w in range(3):
         t0 += 10 * window_ns
@@ -123,7 +126,7 @@ def run_heavy(binding, seed: int, n_inst: int = 64):
 
 
 def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
-              window_ns: int = 4 * MS):
+              window_ns: int = 4 * MS, restart=None):
     """Senders whose bursts overrun netem's 1000-packet queue under every kind of
     shape: jitter, a saturated token bucket, duplicates + loss, reorder + corrupt, correlated
     duplicates, zero delay; late sends (t_send before the window start, at the reaction horizon);
@@ -171,12 +174,14 @@ def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender
         t0 += window_ns if w < windows else 60 * MS
         sim.advance(t0)
         out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if restart is not None:
+            sim = restart(w, sim)
     out.append(dict(stats=parity_stats(sim)))
     sim.close()
     return out
 
 
-def run_sync(binding, seed: int):
+def run_sync(binding, seed: int, restart=None):
     rng = np.random.default_rng(seed)
     sim = Simulator(SimConfig(n_instances=8, seed=seed, max_states=64), binding=binding)
     res = []
@@ -195,11 +200,13 @@ def run_sync(binding, seed: int):
         res.append(("rel", [sim.poll(w) for w in waiters]))
         res.append(("cnt", [sim.count(s) for s in range(6)]))
         t += 1000
+        if restart is not None:
+            sim = restart(b, sim)
     sim.close()
     return res
 
 
-def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, setup=None):
+def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, setup=None, restart=None):
     """The storm step of bench.py. Sharded (cfg_kw shard_id / n_shards, setup attaching a
     transport): the same calls on every shard, each collective; a shard reports its own senders'
     statuses and its own receivers' deliveries."""
@@ -217,6 +224,8 @@ def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, se
         w = sim.barrier(r, n_inst, t0)
         sim.advance_to_barrier(w, 1 * MS)
         out.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if restart is not None:
+            sim = restart(r, sim)
     out.append(dict(stats=parity_stats(sim)))
     sim.close()
     return out

@@ -16,7 +16,10 @@ HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_sha
             "tgsim_enqueue_device", "tgsim_deliveries_device", "tgsim_profile_set", "tgsim_profile_read",
             "tgsim_kernel_classes", "tgsim_kernel_name", "tgsim_set_exchange_buffers",
             "tgsim_advance_begin_device", "tgsim_storm_release_device", "tgsim_comm_unique_id", "tgsim_comm_init",
-            "tgsim_sync_subscribe_device", "tgsim_topic_arena_device"}
+            "tgsim_sync_subscribe_device", "tgsim_topic_arena_device",
+            # checkpoint / resume is a runtime facility of the product library; the oracle's run is the
+            # uninterrupted reference a restored run is compared with (tests/test_snapshot.py)
+            "tgsim_snapshot", "tgsim_restore"}
 
 
 def test_header_declares_expected_surface():

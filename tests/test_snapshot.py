@@ -1,0 +1,95 @@
+"""Checkpoint / resume (tgsim_snapshot / tgsim_restore): a run that is snapshotted at a
+window boundary, destroyed and restored into a fresh context continues exactly as the uninterrupted
+run - which the oracle's uninterrupted run pins (every window's statuses, deliveries and inbox
+offsets, the counters, sync sequence numbers and barrier releases). The checkpoints fall before
+mid-run reconfigurations, inside queue-limit bursts with late sends, between storm rounds with
+wheel records in flight, and between signal batches with open barriers."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd.sim import SimConfig, Simulator, make_shape
+
+from . import scenarios as S
+
+MS = 1_000_000
+
+
+def restarter(binding, at):
+    """restart hook: after window `at`, snapshot, destroy, restore into a new context."""
+    def f(w, sim):
+        if w not in at:
+            return sim
+        image = sim.snapshot()
+        cfg = sim.cfg
+        sim.close()
+        fresh = Simulator(cfg, binding=binding)
+        fresh.restore(image)
+        return fresh
+    return f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_resumed_matches_oracle(hip, oracle, seed):
+    a = S.run_random(hip, seed, windows=8, restart=restarter(hip, {1, 3}))
+    b = S.run_random(oracle, seed, windows=8)
+    S.assert_same(a, b)
+
+
+@pytest.mark.gpu
+def test_burst_resumed_matches_oracle(hip, oracle):
+    """queue-limit bursts and late sends at the reaction horizon across the checkpoint"""
+    a = S.run_burst(hip, 1, restart=restarter(hip, {1, 5}))
+    b = S.run_burst(oracle, 1)
+    S.assert_same(a, b)
+
+
+@pytest.mark.gpu
+def test_storm_resumed_matches_oracle(hip, oracle):
+    a = S.run_storm(hip, n_inst=2000, rounds=10, restart=restarter(hip, {3, 6}))
+    b = S.run_storm(oracle, n_inst=2000, rounds=10)
+    S.assert_same(a, b)
+
+
+@pytest.mark.gpu
+def test_sync_resumed_matches_oracle(hip, oracle):
+    a = S.run_sync(hip, 5, restart=restarter(hip, {1, 3}))
+    b = S.run_sync(oracle, 5)
+    assert len(a) == len(b)
+    for (ka, va), (kb, vb) in zip(a, b):
+        assert ka == kb and np.array_equal(np.asarray(va), np.asarray(vb)), ka
+
+
+@pytest.mark.gpu
+def test_snapshot_refusals(hip):
+    s = Simulator(SimConfig(n_instances=8, seed=1), binding=hip)
+    s.set_shape(0, make_shape(latency_ns=5 * MS))
+    s.enqueue([0], [1], [0], [100], [0])
+    with pytest.raises(A.TgsimError) as e:     # staged messages: not a window boundary
+        s.snapshot()
+    assert e.value.code == A.ESTATE
+    s.advance(1 * MS)
+    image = s.snapshot()
+    other = Simulator(SimConfig(n_instances=9, seed=1), binding=hip)
+    with pytest.raises(A.TgsimError) as e:     # another configuration
+        other.restore(image)
+    assert e.value.code == A.EINVAL
+    same = Simulator(SimConfig(n_instances=8, seed=1), binding=hip)
+    with pytest.raises(A.TgsimError) as e:     # truncated image: refused, the context unchanged
+        same.restore(image[:-8])
+    assert e.value.code == A.EINVAL
+    same.enqueue([2], [3], [0], [10], [0])
+    same.advance(1 * MS)
+    assert same.deliveries()["dst"].tolist() == [3]
+    same.restore(image)                        # the in-flight copy of 0 -> 1 arrives at 5 ms
+    assert same.now == 1 * MS
+    same.advance(10 * MS)
+    d = same.deliveries()
+    assert d["src"].tolist() == [0] and d["t_deliver"].tolist() == [5 * MS]
+    s.tcp_enable()
+    with pytest.raises(A.TgsimError) as e:
+        s.snapshot()
+    assert e.value.code == A.ENOTSUP
+    for x in (s, other, same):
+        x.close()
