@@ -261,6 +261,9 @@ hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n);
 // wheel extract, shape, token bucket, pack; n_dev non-null: the staged count is read on the device
 hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev = nullptr);
 hipError_t window_end(Dev& d);                       // receive, deliveries, wheel insert
+// window_end with the storm round `round` (fanout 8, t0 = this window's end, staged at 0, spread,
+// size) generated inside the wheel-insert launch; *nparts = its signal partials
+hipError_t window_end_storm(Dev& d, uint32_t round, uint32_t size, int64_t spread_ns, uint32_t* nparts);
 hipError_t sync_scalars(Dev& d);                     // copy DevScalars to d.h_sc (blocking)
 // Signal batch already in d.s_state/s_inst/s_t. States lie in [kmin, kmax]. count_only: the
 // batch has one state and no sequence numbers are materialised.

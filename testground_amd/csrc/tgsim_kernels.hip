@@ -2475,6 +2475,7 @@ struct SigState {
 };
 
 constexpr uint32_t kSigParts = 4096;  // blocks of a batch reduction (grid-stride beyond)
+constexpr uint32_t kSpecGenBlocks = 512;  // generator blocks inside the wheel-insert launch (k_wheel_scatter_gen)
 
 // Commit a count-only batch of n signals of state st with times in [tmin, tmax] (one thread).
 __device__ __forceinline__ void sig_commit_count(const SigState& g, uint32_t n, uint32_t st, int64_t tmin,
@@ -2542,7 +2543,9 @@ __global__ void k_add_waiter(SigState g, uint32_t* w_state, uint32_t* w_target, 
 
 // Block-reduce (min, max) of a signal batch into this block's partial (no atomics: a batch has
 // thousands of blocks, and same-address device atomics serialise at the memory side).
-__device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn, int64_t mx) {
+__device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn, int64_t mx,
+                                                  uint32_t bid = 0xFFFFFFFFu) {
+  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
   __shared__ int64_t smin[kBlock / 64], smax[kBlock / 64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2555,8 +2558,8 @@ __device__ __forceinline__ void sig_block_partial(const SigState& g, int64_t mn,
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int k = 1; k < kBlock / 64; ++k) { mn = smin[k] < mn ? smin[k] : mn; mx = smax[k] > mx ? smax[k] : mx; }
-    g.part[2 * blockIdx.x] = mn;
-    g.part[2 * blockIdx.x + 1] = mx;
+    g.part[2 * bid] = mn;
+    g.part[2 * bid + 1] = mx;
   }
 }
 
@@ -3066,12 +3069,12 @@ __device__ __forceinline__ uint32_t peer_mod(const StormArgs& a, uint32_t u) {
 // finishes them).
 // FIX != 0: fanout FIX = its power of two, known at compile time (the shuffle loops unroll); 0: any.
 template <uint32_t FIX>
-__global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) {
+__device__ __forceinline__ void gen_storm_body(const StormArgs& a, const SigState& sg, uint32_t bid, uint32_t nb) {
   const uint32_t F = FIX ? FIX : a.F, Fp = FIX ? FIX : a.Fp, fp_log2 = FIX ? (uint32_t)__builtin_ctz(FIX ? FIX : 1u) : a.fp_log2;
   const int64_t t0 = a.t0 == INT64_MIN ? sg.sc->t_end : a.t0;  // TGSIM_T_NOW: the device's window start
   const uint32_t total = a.nloc * Fp;
   int64_t mn = INT64_MAX, mx = INT64_MIN;
-  for (uint32_t b0 = blockIdx.x * kBlock; b0 < total; b0 += gridDim.x * kBlock) {  // block-uniform loop
+  for (uint32_t b0 = bid * kBlock; b0 < total; b0 += nb * kBlock) {  // block-uniform loop
     const uint32_t tid = b0 + threadIdx.x;
     const uint32_t l = tid >> fp_log2, k = tid & (Fp - 1u);
     const uint32_t lane = lane_id(), gbase = lane - k;
@@ -3122,7 +3125,35 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
     }
     if (inst && k == 0) { mn = t < mn ? t : mn; mx = t > mx ? t : mx; }
   }
-  sig_block_partial(sg, mn, mx);
+  sig_block_partial(sg, mn, mx, bid);
+}
+
+template <uint32_t FIX>
+__global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) {
+  gen_storm_body<FIX>(a, sg, blockIdx.x, gridDim.x);
+}
+
+// The wheel insert of window r with the storm round r + 1 generated speculatively beside it
+// (DESIGN.md 5): blocks [0, kRadixBlocks) scatter, then g generator blocks, then the long inboxes.
+// The scatter streams records while the generator is bound by integer multiplies, so they overlap
+// on the same CUs; the generator writes only the staged arrays (consumed by this window's netem
+// pass) and the signal partials (consumed by this window's start).
+__global__ __launch_bounds__(kBlock) void k_wheel_scatter_gen(BktSrc src, DevScalars* sc, const tgsim_record* L,
+                                                              tgsim_record* arena, uint32_t* dirs, uint32_t slots,
+                                                              const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                              uint32_t lo, uint32_t nloc, EmitPolicy p,
+                                                              const uint32_t* keys, const uint32_t* vals,
+                                                              const uint32_t* off, const uint32_t* medium,
+                                                              const LargeSeg* large, uint64_t* K1a, uint64_t* K2a,
+                                                              uint32_t* K3a, uint64_t* K1b, uint64_t* K2b, uint32_t* K3b,
+                                                              StormArgs ga, SigState sg, uint32_t g) {
+  if (blockIdx.x < (uint32_t)kRadixBlocks)
+    wheel_scatter_body(src, sc, L, arena, dirs, slots, hist, tot, pend, lo, nloc);
+  else if (blockIdx.x < (uint32_t)kRadixBlocks + g)
+    gen_storm_body<8>(ga, sg, blockIdx.x - kRadixBlocks, g);
+  else
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x - kRadixBlocks - g,
+              gridDim.x - kRadixBlocks - g);
 }
 
 // ============================================================================================
@@ -3432,7 +3463,13 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
 //                  per-slot scans of the L histogram
 //   k_wheel_scatter L straight into the arena in slot order (also closes the window's counters) |
 //                  long inboxes of the deliveries
-hipError_t window_end(Dev& d) {
+static StormArgs storm_args(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                            int64_t spread_ns);
+
+// spec_round != nullptr: the storm round *spec_round (fanout 8, t0 = the window's end, staged at 0)
+// is generated inside the wheel-insert launch; *spec_parts = its signal partials
+static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t size, int64_t spread_ns,
+                                  uint32_t* spec_parts) {
   if (d.S > 1) {
     Queues Q = make_queues(d);
     const uint64_t total = (uint64_t)d.S * d.xcap;
@@ -3460,13 +3497,28 @@ hipError_t window_end(Dev& d) {
                        d.tot);
   }
   TG_CHECK(hipGetLastError());
-  {
+  if (spec_round) {
+    ProfScope ps_(d, KID_REGION_FILL);
+    const StormArgs ga = storm_args(d, 0, *spec_round, INT64_MIN, 8, size, spread_ns);
+    const uint64_t threads = (uint64_t)d.nloc * 8;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((threads + kBlock - 1) / kBlock, kSpecGenBlocks);
+    hipLaunchKernelGGL(k_wheel_scatter_gen, dim3(kRadixBlocks + g + kListBlocks), dim3(kBlock), 0, d.stream, srcL,
+                       d.sc, d.L, d.arena, d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0,
+                       d.seg_off, d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b, ga, sig_state(d), g);
+    *spec_parts = g;
+  } else {
     ProfScope ps_(d, KID_REGION_FILL);
     hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L,
                        d.arena, d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
                        d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   }
   return hipGetLastError();
+}
+
+hipError_t window_end(Dev& d) { return window_end_impl(d, nullptr, 0, 0, nullptr); }
+
+hipError_t window_end_storm(Dev& d, uint32_t round, uint32_t size, int64_t spread_ns, uint32_t* nparts) {
+  return window_end_impl(d, &round, size, spread_ns, nparts);
 }
 
 hipError_t signal_batch(Dev& d, uint32_t n, uint32_t kmin, uint32_t kmax, uint64_t log_base, uint32_t n_waiters,
@@ -3556,9 +3608,8 @@ static void peer_divisor(uint32_t d, uint32_t& m, uint32_t& sh1, uint32_t& sh2) 
 
 // k_gen_storm only: the batch's per-block partials wait in sig_part for launch_sig_commit (the
 // runtime defers it so that a barrier registered next rides in the same launch). *nparts = grid.
-hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
-                            uint32_t size, int64_t spread_ns, uint32_t* nparts) {
-  ProfScope ps_(d, KID_GEN);
+static StormArgs storm_args(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                            int64_t spread_ns) {
   StormArgs a;
   a.lo = d.lo; a.nloc = d.nloc; a.N = d.N; a.round = round; a.t0 = t0; a.F = fanout;
   a.Fp = 1; a.fp_log2 = 0;
@@ -3567,6 +3618,13 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
   a.size = size; a.spread = spread_ns; a.key0 = d.key0;
   storm_divisor(spread_ns, a.spread_m, a.spread_sh1, a.spread_sh2); a.key1 = d.key1; a.base = staged_base;
   a.m_src = d.m_src; a.m_dst = d.m_dst; a.m_seq = d.m_seq; a.m_size = d.m_size; a.m_t = d.m_t;
+  return a;
+}
+
+hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_t t0, uint32_t fanout,
+                            uint32_t size, int64_t spread_ns, uint32_t* nparts) {
+  ProfScope ps_(d, KID_GEN);
+  const StormArgs a = storm_args(d, staged_base, round, t0, fanout, size, spread_ns);
   const uint64_t threads = (uint64_t)d.nloc * a.Fp;
   const unsigned g = (unsigned)std::min<uint64_t>((threads + kBlock - 1) / kBlock,
                                                   std::min<uint64_t>(kSigParts, (uint64_t)d.grid_gen));

@@ -68,6 +68,12 @@ struct tgsim_ctx {
   uint32_t storm_nw = 0, add_state = 0, add_target = 0;
   int64_t add_twait = 0;
   std::vector<void*> allocs;
+  // speculative storm generation: after a storm round staged at the device clock, the
+  // window's last launch also generates the next round (round + 1, state + 1, same shape); the
+  // next tgsim_gen_storm_round that asks for exactly it only does the host bookkeeping. Any call that
+  // writes the staged arrays or the signal partials first drops it.
+  struct StormSpec { bool hint = false, valid = false; uint32_t round = 0, size = 0, state = 0, parts = 0; int64_t spread = 0; };
+  StormSpec spec;
   // netem queue limit: the host's proof that no sender can reach the limit in a
   // window (then the kernels skip the test). pend_bound >= every local sender's queued copies at the
   // next window start: the exact maximum when last refreshed (k_pend_max, only when the bound is
@@ -885,6 +891,7 @@ extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
 }
 static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
+  c->spec.valid = false;  // staged arrays change: no speculative storm round
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (!c->staged_dev && (uint64_t)c->n_staged + n > c->d.cap_msgs)
@@ -935,6 +942,7 @@ static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
 
 extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
+  c->spec.valid = false;  // staged arrays change: no speculative storm round
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
   if ((c->staged_dev ? 0 : (uint64_t)c->n_staged) + n > c->d.cap_msgs)
@@ -1004,6 +1012,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
 }
 
 static int begin_common(tgsim_ctx* c) {
+  c->spec.valid = false;  // a window runs before any storm round: the speculative one is stale
   int rc = upload_tables(c);
   if (rc) return rc;
   if (c->tcp_on) {
@@ -1088,7 +1097,22 @@ extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev
 extern "C" int tgsim_advance_end(tgsim_ctx* c) {
   if (!c) return TGSIM_EINVAL;
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
-  HIPCK(c, window_end(c->d), "window_end");
+  {
+    tgsim_ctx::StormSpec& sp = c->spec;
+    sp.valid = false;
+    // the next round is generated here only when nothing can read the staged arrays or the
+    // signal partials in between: no deferred storm commit, no TCP / flood staging
+    const bool spec = sp.hint && !c->storm_pending && !c->tcp_on && !c->staged_dev && c->n_staged == 0 &&
+                      (uint64_t)c->nloc * 8 <= c->d.cap_msgs && c->nloc <= c->d.s_cap && sp.state < c->d.max_states &&
+                      c->fl_off.empty();
+    sp.hint = false;
+    if (spec) {
+      HIPCK(c, window_end_storm(c->d, sp.round, sp.size, sp.spread, &sp.parts), "window_end");
+      sp.valid = true;
+    } else {
+      HIPCK(c, window_end(c->d), "window_end");
+    }
+  }
   c->in_window = false;
   // No host round trip: a host-given end is the new clock; a device-ended window's end (and any
   // device-side error) is read at the next sync.
@@ -1360,6 +1384,7 @@ static int signal_gathered(tgsim_ctx* c, const uint32_t* states, const uint32_t*
 extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                                  size_t n, uint32_t* seq_out) {
   if (!c || (n && (!states || !inst || !t))) return TGSIM_EINVAL;
+  c->spec.valid = false;  // signal partials change: no speculative storm round
   if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
   if (c->S != 1 && c->has_tr && !c->replicated_batch) return signal_gathered(c, states, inst, t, n, seq_out);
   return signal_local(c, states, inst, t, n, seq_out);
@@ -1459,7 +1484,18 @@ static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fan
   if (c->nloc > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch capacity");
   HIPCK(c, flush_storm(c), "storm commit");
   uint32_t parts = 0;
-  HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, &parts), "gen storm");
+  tgsim_ctx::StormSpec& sp = c->spec;
+  if (sp.valid && c->n_staged == 0 && t0 == TGSIM_T_NOW && fanout == 8 && round == sp.round && size == sp.size &&
+      spread_ns == sp.spread && state == sp.state) {
+    parts = sp.parts;  // generated by the last window's final launch
+  } else {
+    HIPCK(c, launch_gen_storm(c->d, c->n_staged, round, t0, fanout, size, spread_ns, &parts), "gen storm");
+  }
+  sp.valid = false;
+  // arm the next round's speculation (plain storm rounds at the device clock only; the TCP variant
+  // rewrites the staged records after generation)
+  sp.hint = !c->tcp_on && t0 == TGSIM_T_NOW && fanout == 8 && c->n_staged == 0 && round + 1u != 0u;
+  sp.round = round + 1u; sp.size = size; sp.spread = spread_ns; sp.state = state + 1u;
   c->n_staged += (uint32_t)n;
   c->win_m_extra += fanout;
   if (c->S == 1) {
@@ -1541,6 +1577,7 @@ extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const ui
 extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
                                    size_t n, uint32_t size) {
   if (!c) return TGSIM_EINVAL;
+  c->spec.valid = false;
   Flood& f = c->d.fl;
   if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
@@ -1582,6 +1619,7 @@ extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uin
 
 extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   if (!c) return TGSIM_EINVAL;
+  c->spec.valid = false;
   if (n_fwd) *n_fwd = 0;
   Flood& f = c->d.fl;
   if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
@@ -1617,6 +1655,7 @@ static int dgrow(tgsim_ctx* c, T** p, uint64_t used, uint64_t need_cap) {
 extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
                                   const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out) {
   if (!c) return TGSIM_EINVAL;
+  c->spec.valid = false;  // signal partials change: no speculative storm round
   if (n && (!topics || !inst || !t || !off || (off[n] && !payload))) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (n && off[0] != 0) return fail(c, TGSIM_EINVAL, "payload offsets must start at 0");
   for (size_t i = 0; i < n; ++i)
@@ -1879,6 +1918,7 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
 
 extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
+  c->spec.valid = false;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
@@ -2202,6 +2242,7 @@ extern "C" int tgsim_snapshot(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
 
 extern "C" int tgsim_restore(tgsim_ctx* c, const void* buf, size_t n) {
   if (!c || !buf) return TGSIM_EINVAL;
+  c->spec = tgsim_ctx::StormSpec{};
   int rc = snap_refusal(c);
   if (rc) return rc;
   if (c->storm_pending) return fail(c, TGSIM_ESTATE, "restore: a storm round is pending");

@@ -206,10 +206,13 @@ def run_sync(binding, seed: int, restart=None):
     return res
 
 
-def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, setup=None, restart=None):
+def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, setup=None, restart=None,
+              t_now=False, size_of=None, between=None):
     """The storm step of bench.py. Sharded (cfg_kw shard_id / n_shards, setup attaching a
     transport): the same calls on every shard, each collective; a shard reports its own senders'
-    statuses and its own receivers' deliveries."""
+    statuses and its own receivers' deliveries. t_now: rounds start at the device clock
+    (TGSIM_T_NOW, bench.py's loop: the library may generate the next round speculatively);
+    size_of(r): the round's message size; between(r, sim): calls made before round r's generation."""
     sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, **(cfg_kw or {})), binding=binding)
     if setup is not None:
         setup(sim)
@@ -219,8 +222,10 @@ def run_storm(binding, n_inst=2000, rounds=12, fanout=8, seed=4, cfg_kw=None, se
                                     bandwidth_bps=10_000_000, loss=0.5))
     out = []
     for r in range(rounds):
-        t0 = sim.now
-        sim.gen_storm_round(r, t0, fanout, 1024, 10 * MS, r)
+        if between is not None:
+            between(r, sim)
+        t0 = A.T_NOW if t_now else sim.now
+        sim.gen_storm_round(r, t0, fanout, size_of(r) if size_of else 1024, 10 * MS, r)
         w = sim.barrier(r, n_inst, t0)
         sim.advance_to_barrier(w, 1 * MS)
         out.append(dict(now=sim.now, status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))

@@ -120,12 +120,34 @@ def test_transport_on_one_device(hip, oracle, world, seed):
 @pytest.mark.parametrize("world", [2, 4])
 def test_storm_transport_on_one_device(hip, oracle, world):
     """bench.py's storm step on HIP shards: the storm batch's MAX all-reduce and the exchange go
-    through the transport; equal to the single-shard oracle run."""
+    through the transport, rounds at the device clock (speculative generation); equal to the
+    single-shard oracle run."""
     n, rounds = 2000, 6
     outs = S.sharded_threads(world, lambda k, tr: S.run_storm(
         hip, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, exchange_cap=1 << 15),
-        setup=lambda sim: sim.set_transport(tr)), device=True)
+        setup=lambda sim: sim.set_transport(tr), t_now=True), device=True)
     S.assert_storm_sharded(outs, S.run_storm(oracle, n_inst=n, rounds=rounds), world, n)
+
+
+@pytest.mark.gpu
+def test_storm_device_clock_speculation(hip, oracle):
+    """bench.py's loop (rounds at TGSIM_T_NOW): each window's last launch generates the next round,
+    which the next tgsim_gen_storm_round adopts. Calls that touch the staged arrays or the signal
+    partials in between (an enqueue, a signal batch), a round of another size and a round staged
+    at a host time each make the library generate the round itself; equal to the oracle throughout."""
+    from testground_amd import _abi as A
+
+    def between(r, sim):
+        if r == 3:
+            sim.enqueue([1, 2], [5, 6], [900000, 900000], [64, 64], [sim.now, sim.now])
+        if r == 5:
+            sim.signal([40, 40], [0, 1], [sim.now, sim.now])
+
+    def size_of(r):
+        return 512 if r == 7 else 1024
+
+    kw = dict(n_inst=3000, rounds=11, t_now=True, size_of=size_of, between=between)
+    S.assert_same(S.run_storm(hip, **kw), S.run_storm(oracle, **kw))
 
 
 @pytest.mark.gpu

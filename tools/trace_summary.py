@@ -13,7 +13,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=30)
-    ap.add_argument("--marker", default="k_gen_storm")
+    ap.add_argument("--marker", default="k_window_start")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
