@@ -12,7 +12,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv \
   -- python3 -u bench.py --no-cpu-baseline --steps 20 --warmup 15 > $OUT/bench_under_rocprof.log 2>&1 || { echo PROF_FAIL; tail -20 $OUT/bench_under_rocprof.log; exit 1; }
-python3 tools/trace_summary.py $OUT/prof/run_kernel_trace.csv --last 20 > $OUT/trace_summary.txt 2>&1
+python3 tools/trace_summary.py $OUT/prof/run_kernel_trace.csv --last 20 --marker k_window_start > $OUT/trace_summary.txt 2>&1
 KR="k_tb_bucket|k_emit_bucket|k_shape|k_wheel_scatter|k_wheel_hist_rest|k_extract|k_gen_storm|k_bkt"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_fetch -o run --output-format csv \
   -- python3 -u bench.py --no-cpu-baseline --steps 5 --warmup 5 > $OUT/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; exit 1; }
