@@ -2275,12 +2275,18 @@ extern "C" int tgsim_restore(tgsim_ctx* c, const void* buf, size_t n) {
   const bool pend_exact = r.val<bool>();
   if (!r.ok || sig_used > c->d.max_signals || n_waiters > c->d.max_waiters)
     return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
+  const uint64_t sig_used0 = c->sig_log_used;
+  const uint32_t n_waiters0 = c->n_waiters;
   c->sig_log_used = sig_used;  // sizes the log / waiter regions below
   c->n_waiters = n_waiters;
   const auto regs = snap_regions(c);
   size_t need = r.at;
   for (const auto& g : regs) need += g.second;
-  if (need != n) return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
+  if (need != n) {
+    c->sig_log_used = sig_used0;
+    c->n_waiters = n_waiters0;
+    return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
+  }
   HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
   size_t at = r.at;
   for (const auto& g : regs) {
