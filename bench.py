@@ -268,7 +268,7 @@ def main():
     shapes = storm_shapes(args.instances, args.seed)
     sim = Simulator(sim_config(args, rank, world, local))
     sim.set_stream(stream.cuda_stream)
-    _attach_transport(sim, dist, world, rank, rehearsal)
+    transport = _attach_transport(sim, dist, world, rank, rehearsal)
     sim.set_shapes(np.arange(sim.lo, sim.hi), shapes[sim.lo:sim.hi])
     spread, rtt = int(args.spread_ms * MS), int(args.rtt_ms * MS)
     N, F = args.instances, args.fanout
@@ -375,8 +375,7 @@ def main():
                             "1 KiB messages within 10 ms, per-sender 10 Mbit/s HTB, latency U[20,100] ms, "
                             "jitter 5 ms, loss 0.5%, SignalAndWait(round, N) + 1 ms sync RTT per round",
                 "instances": N, "fanout": F, "msg_bytes": args.size,
-                "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else
-                                                  ("-rccl" if world > 1 else "")),
+                "parallelism": f"shard{world}{transport}",
                 "delivered_in_timed_steps": delivered,
                 "simulated_ms_per_step": (sim_t1 - sim_t0) / 1e6 / args.steps,
             },
@@ -403,7 +402,9 @@ def _dist_setup(args):
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     ndev = torch.cuda.device_count()
-    rehearsal = world > ndev
+    # TGSIM_BENCH_TRY_RCCL=1: ranks sharing a GPU still try the RCCL communicator (which refuses a
+    # duplicate GPU), exercising the agreed gloo fallback of _attach_transport on a one-GPU box
+    rehearsal = world > ndev and os.environ.get("TGSIM_BENCH_TRY_RCCL") != "1"
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
@@ -413,17 +414,33 @@ def _dist_setup(args):
     return torch, dist, world, rank, local, rehearsal, stream
 
 
-def _attach_transport(sim, dist, world: int, rank: int, rehearsal: bool) -> None:
+def _attach_transport(sim, dist, world: int, rank: int, rehearsal: bool) -> str:
+    """The shards' transport: the library's RCCL communicator, or (rehearsal, or when any rank's
+    communicator fails to come up) the gloo transport - agreed over all ranks, and named in the
+    JSON line's parallelism so a fallback is never mistaken for the RCCL path."""
     if world == 1:
-        return
+        return ""
+    from testground_amd.exchange import GlooTransport
     if rehearsal:
-        from testground_amd.exchange import GlooTransport
         sim.set_transport(GlooTransport(dist, device=True))
-        return
+        return "-gloo-rehearsal"
+    import torch
     from testground_amd.sim import Simulator
     uid = [Simulator.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
-    sim.comm_init(uid[0], world, rank)
+    ok = 1
+    try:
+        sim.comm_init(uid[0], world, rank)
+    except Exception as e:  # noqa: BLE001 - reported, then every rank takes the same path
+        print(f"rank {rank}: RCCL communicator failed ({e}); falling back to the gloo transport",
+              file=sys.stderr, flush=True)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return "-rccl"
+    sim.set_transport(GlooTransport(dist, device=True))
+    return "-gloo-fallback"
 
 
 def flood_cpu_baseline(args, shapes, graph):
@@ -482,7 +499,7 @@ def main_flood(args):
     graph = W.random_regular_graph(N, 8, args.seed)
     sim = Simulator(flood_config(args, rank, world, local))
     sim.set_stream(stream.cuda_stream)
-    _attach_transport(sim, dist, world, rank, rehearsal)
+    transport = _attach_transport(sim, dist, world, rank, rehearsal)
     sim.set_shapes(np.arange(sim.lo, sim.hi), shapes[sim.lo:sim.hi])
     sim.flood_set_graph(*graph, flood_max_pubs(args))
     win = int(args.window_ms * MS)
@@ -551,8 +568,7 @@ def main_flood(args):
                                    f"{args.window_ms} ms",
                        "pubs_per_wave": args.pubs_per_wave,
                        "instances": N, "msg_bytes": args.flood_size,
-                       "parallelism": f"shard{world}" + ("-gloo-rehearsal" if world > 1 and rehearsal else
-                                                         ("-rccl" if world > 1 else "")),
+                       "parallelism": f"shard{world}{transport}",
                        "delivered_in_timed_steps": delivered},
             "roofline": roof,
             "cpu_baseline": cpu,
