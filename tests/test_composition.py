@@ -198,3 +198,12 @@ def test_composition_runs_on_the_runner(oracle):
     assert res.result.outcome == OUTCOME_SUCCESS
     assert {k: (v.total, v.ok) for k, v in res.result.outcomes.items()} == {"dialers": (30, 30), "listeners": (10, 10)}
     assert "local:mi355x run storm-run: success" in out.getvalue()
+
+
+@pytest.mark.gpu
+def test_composition_runs_on_the_hip_runner(hip):
+    c = CP.parse_composition(STORM)
+    CP.validate_for_run(c)
+    job = CP.to_run_input(CP.prepare_for_run(c, CP.parse_manifest(MANIFEST)), "storm-run-hip")
+    res = LocalMI355XRunner(binding=hip).run(job, io.StringIO())
+    assert res.result.outcome == OUTCOME_SUCCESS
