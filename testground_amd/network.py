@@ -8,12 +8,22 @@ The reference consumes these types but does not vendor them: ``github.com/testgr
 restated here reads like the Go plan (compare ``plans/network/pingpong.go:29-41``).
 
 ``Config.to_c()`` lowers a config to the C ABI struct ``tgsim_network_config`` (include/tgsim.h).
+``Config.to_wire()`` / ``Config.from_wire()`` are the JSON form a config travels in on the sync
+topic ``network:<hostname>`` that the sidecar subscribes to (``pkg/sidecar/sidecar_handler.go:49-
+80``): Go ``encoding/json`` of sdk-go's types [EXT]: ``network``, ``enable``, ``default``, ``rules``,
+``callback_state``, ``routing_policy`` tags, ``IPv4`` / ``IPv6`` as ``net.IPNet`` objects
+(``{"IP": "a.b.c.d", "Mask": <base64 bytes>}``), untagged ``LinkShape`` fields by Go name, durations
+in integer nanoseconds, ``LinkRule`` = the embedded ``LinkShape`` fields + ``Subnet``.
+``CallbackTarget`` is ``json:"-"``: it never travels. Decoding matches keys case-insensitively, as
+Go does, and also takes the JS SDK's spellings (``callbackState``, ``routingPolicy``, ``IPv4`` as
+``"a.b.c.d/n"``: ``plans/example-js/pingpong.js:25-33``).
 The callback fields (``callback_state``, ``callback_target``) never reach the C ABI: the sidecar
 handler consumes them (``pkg/sidecar/sidecar_handler.go:75-79``), which lives in
 :mod:`testground_amd.sidecar`.
 """
 from __future__ import annotations
 
+import base64
 import ctypes as C
 import enum
 from dataclasses import dataclass, field
@@ -107,6 +117,53 @@ class LinkShape:
                            self.corrupt_corr, self.reorder, self.reorder_corr, self.duplicate,
                            self.duplicate_corr, int(self.filter))
 
+    def to_wire(self) -> dict:
+        return {go: (int(getattr(self, py)) if py in _INT_FIELDS else float(getattr(self, py)))
+                for go, py in _SHAPE_FIELDS}
+
+    @staticmethod
+    def from_wire(d: dict) -> "LinkShape":
+        sh = LinkShape()
+        for go, py in _SHAPE_FIELDS:
+            v = _get(d, go)
+            if v is not None:
+                setattr(sh, py, FilterAction(int(v)) if py == "filter" else (int(v) if py in _INT_FIELDS else float(v)))
+        return sh
+
+
+# Go field name -> Python attribute of network.LinkShape (untagged fields: encoding/json uses the names)
+_SHAPE_FIELDS = (("Latency", "latency"), ("Jitter", "jitter"), ("Bandwidth", "bandwidth"), ("Filter", "filter"),
+                 ("Loss", "loss"), ("Corrupt", "corrupt"), ("CorruptCorr", "corrupt_corr"), ("Reorder", "reorder"),
+                 ("ReorderCorr", "reorder_corr"), ("Duplicate", "duplicate"), ("DuplicateCorr", "duplicate_corr"))
+_INT_FIELDS = {"latency", "jitter", "bandwidth", "filter"}
+
+
+def _get(d: dict, *names):
+    """encoding/json's key match: exact first, then case-insensitive."""
+    for n in names:
+        if n in d:
+            return d[n]
+    low = {k.lower(): v for k, v in d.items()}
+    for n in names:
+        if n.lower() in low:
+            return low[n.lower()]
+    return None
+
+
+def ipnet_to_wire(n: IPNet) -> dict:
+    """net.IPNet's JSON: IP as text, Mask ([]byte) as base64."""
+    return {"IP": int_to_ip(n.ip), "Mask": base64.b64encode(n.mask.to_bytes(4, "big")).decode()}
+
+
+def ipnet_from_wire(v) -> IPNet:
+    if isinstance(v, str):
+        return IPNet.parse(v)
+    mask = int.from_bytes(base64.b64decode(_get(v, "Mask")), "big")
+    plen = bin(mask).count("1")
+    if mask != ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF if plen else 0):
+        raise ValueError(f"non-canonical netmask {mask:#010x}")
+    return IPNet(ip_to_int(_get(v, "IP")), plen)
+
 
 @dataclass
 class LinkRule:
@@ -116,6 +173,13 @@ class LinkRule:
 
     def to_c(self) -> A.LinkRule:
         return A.LinkRule(self.subnet.ip, self.subnet.prefix_len, self.shape.to_c())
+
+    def to_wire(self) -> dict:
+        return {**self.shape.to_wire(), "Subnet": ipnet_to_wire(self.subnet)}
+
+    @staticmethod
+    def from_wire(d: dict) -> "LinkRule":
+        return LinkRule(ipnet_from_wire(_get(d, "Subnet")), LinkShape.from_wire(d))
 
 
 @dataclass
@@ -130,6 +194,23 @@ class Config:
     routing_policy: str = ""
     ipv4: Optional[IPNet] = None
     ipv6: Optional[str] = None
+
+    def to_wire(self) -> dict:
+        """The JSON object published on network:<hostname> (callback_target does not travel)."""
+        return {"network": self.network, "IPv4": ipnet_to_wire(self.ipv4) if self.ipv4 is not None else None,
+                "IPv6": self.ipv6, "enable": bool(self.enable), "default": self.default.to_wire(),
+                "rules": [r.to_wire() for r in self.rules], "callback_state": self.callback_state,
+                "routing_policy": str(getattr(self.routing_policy, "value", self.routing_policy))}
+
+    @staticmethod
+    def from_wire(d: dict) -> "Config":
+        ip4 = _get(d, "IPv4")
+        return Config(network=_get(d, "network") or "", enable=bool(_get(d, "enable")),
+                      default=LinkShape.from_wire(_get(d, "default") or {}),
+                      rules=[LinkRule.from_wire(r) for r in (_get(d, "rules") or [])],
+                      callback_state=_get(d, "callback_state", "callbackState") or "",
+                      routing_policy=_get(d, "routing_policy", "routingPolicy") or "",
+                      ipv4=ipnet_from_wire(ip4) if ip4 else None, ipv6=_get(d, "IPv6") or None)
 
     def to_c(self):
         """Returns (tgsim_network_config, keepalive) - keep the second alive during the call."""

@@ -48,7 +48,9 @@ class PlanEnv:
         kw.update(sim_kw or {})
         self.sim = Simulator(SimConfig(n_instances=self.n, seed=seed, **kw), binding=binding)
         self.sync = SyncService(self.sim)
-        self.sidecar = Sidecar(self.sim, self.sync, self.n, track_configs=self.n <= 4096)
+        # sidecar_wire (a test parameter): configs travel as JSON on the network:<hostname> topics
+        wire = self.params.get("sidecar_wire", "false") == "true"
+        self.sidecar = Sidecar(self.sim, self.sync, self.n, track_configs=self.n <= 4096, wire=wire)
         self.net = NetClient(self.sidecar)
         self._seq = np.zeros(self.n, np.int64)
         self._pend = []                       # (t, src, dst, seq, size) arrays not yet staged

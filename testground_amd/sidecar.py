@@ -18,6 +18,11 @@ Reference interfaces mirrored here:
 
 Configuration takes effect from the next simulated window for every message that window
 processes.
+
+``wire=True`` routes every config the way the reference does: ``NetClient`` publishes its JSON form
+(``Config.to_wire``) on the sync topic ``network:<hostname>`` (device-resident topics)
+and the instance's sidecar replays the topic from its last position, decodes each entry
+(``Config.from_wire``) and applies it (``sidecar_handler.go:49-80``).
 """
 from __future__ import annotations
 
@@ -63,9 +68,11 @@ class Sidecar:
     """The per-instance sidecar handlers of one run, driven in lock step."""
 
     def __init__(self, sim, sync: SyncService, n_instances: int, track_configs: bool = False,
-                 runner: str = "docker"):
+                 runner: str = "docker", wire: bool = False):
         if runner not in ("docker", "k8s"):
             raise ValueError(f"unknown sidecar runner {runner!r}")
+        self.wire = wire
+        self._consumed: dict[int, int] = {}   # wire mode: topic entries each sidecar has applied
         self.sim = sim
         self.order = runner
         self.sync = sync
@@ -92,6 +99,21 @@ class Sidecar:
         _, rel = self.sync.signal_and_wait(NET_INIT_STATE, np.arange(self.n), t, self.n)
         self.t_initialized = rel
         return rel
+
+    @staticmethod
+    def topic(instance: int) -> str:
+        """The instance's config topic, "network:" + its hostname (sidecar_handler.go:49)."""
+        return f"network:instance-{instance}"
+
+    def poll(self, instance: int, t: int) -> int:
+        """Wire mode: the instance's sidecar receives the configs published on its topic since its
+        last poll, in topic order, and applies each one. Returns how many it applied."""
+        entries = self.sync.subscribe(self.topic(instance), until_t=t)
+        start = self._consumed.get(instance, 0)
+        for d in entries[start:]:
+            self.apply(instance, Config.from_wire(d), t)
+        self._consumed[instance] = len(entries)
+        return len(entries) - start
 
     def apply(self, instance: int, cfg: Config, t: int) -> None:
         """One iteration of the handler loop (sidecar_handler.go:64-80)."""
@@ -120,7 +142,11 @@ class NetClient:
         Returns the barrier release time (-1 while fewer than target sidecars have signalled)."""
         if not cfg.callback_state:
             raise ValueError(ERR_NO_CALLBACK)
-        self.sidecar.apply(instance, copy.deepcopy(cfg), t)
+        if self.sidecar.wire:   # publish on network:<hostname>; the sidecar's subscription applies it
+            self.sidecar.sync.publish(Sidecar.topic(instance), [instance], t, [cfg.to_wire()])
+            self.sidecar.poll(instance, t)
+        else:
+            self.sidecar.apply(instance, copy.deepcopy(cfg), t)
         target = cfg.callback_target or self.sidecar.n
         return self.sidecar.sync.barrier(cfg.callback_state, target, t)
 
