@@ -33,6 +33,24 @@ TCP_CHUNK = 4 * 1024       # storm.go:23 write size
 NEVER = np.iinfo(np.int64).max
 
 
+class RunParams(dict):
+    """A run's test parameters; names whose value differs between groups raise when read (the
+    descriptors are written for one value per run; runtime.RunEnv in the reference is per instance)."""
+
+    def __init__(self, values: dict, ambiguous=()):
+        super().__init__(values)
+        self.ambiguous = frozenset(ambiguous)
+
+    def get(self, name, default=None):
+        if name in self.ambiguous:
+            raise ValueError(f"test parameter {name!r} differs between groups; the workload descriptor "
+                             f"takes one value per run")
+        return super().get(name, default)
+
+    def __getitem__(self, name):
+        return self.get(name) if name in self else super().__getitem__(name)
+
+
 class PlanEnv:
     """One simulated run: simulator + sync service + sidecars + network clients, and a message
     layer that stages sends when their time falls in the next window and records, per message,
@@ -42,7 +60,7 @@ class PlanEnv:
                  binding=None, window_ns: int = 1 * MS, sim_kw: dict | None = None):
         self.n = int(n_instances)
         self.test_case = test_case
-        self.params = dict(params or {})
+        self.params = params if isinstance(params, RunParams) else RunParams(params or {})
         self.window_ns = int(window_ns)
         kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=1024, max_waiters=1 << 16)
         kw.update(sim_kw or {})

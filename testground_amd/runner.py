@@ -225,9 +225,15 @@ class LocalMI355XRunner:
         if total != job.total_instances:
             raise ValueError(f"groups hold {total} instances, TotalInstances is {job.total_instances}")
         cfg = job.runner_config
-        params = {}
+        # the workload descriptors take one value per parameter for the whole run: a parameter the
+        # groups set differently is ambiguous and fails the run if the descriptor reads it
+        params, ambiguous = {}, set()
         for g in job.groups:
-            params.update(g.parameters)
+            for k, v in g.parameters.items():
+                if k in params and params[k] != v:
+                    ambiguous.add(k)
+                params.setdefault(k, v)
+        params = P.RunParams(params, ambiguous)
         result = Result(outcomes={g.id: GroupOutcome(total=g.instances) for g in job.groups})
         t0 = time.perf_counter()
         subnet, _ = next_data_network(self._active)

@@ -56,13 +56,14 @@ seed = 7
 [global.run.test_params]
 conn_outgoing = "3"
 conn_delay_ms = "200"
+data_size_kb = "8"
 
 [[groups]]
 id = "dialers"
 instances = { percentage = 0.75 }
 
   [groups.run.test_params]
-  data_size_kb = "8"
+  role = "dialer"
 
 [[groups]]
 id = "listeners"
@@ -182,7 +183,8 @@ def test_run_input_from_composition():
     assert job.runner_config.seed == 7 and job.runner_config.window_ns == 2_000_000
     assert job.runner_config.max_records == 1 << 18
     d, l = (g.parameters for g in job.groups)
-    assert d["data_size_kb"] == "8" and l["data_size_kb"] == "128"       # group value, manifest default
+    assert d["role"] == "dialer" and "role" not in l                    # group-only value
+    assert d["data_size_kb"] == l["data_size_kb"] == "8" and d["conn_count"] == "5"   # manifest default
     assert d["conn_outgoing"] == l["conn_outgoing"] == "3"              # [global.run] trickled down
     assert d["verbose"] == "false" and d["region"] == "eu"
 
@@ -198,6 +200,14 @@ def test_composition_runs_on_the_runner(oracle):
     assert res.result.outcome == OUTCOME_SUCCESS
     assert {k: (v.total, v.ok) for k, v in res.result.outcomes.items()} == {"dialers": (30, 30), "listeners": (10, 10)}
     assert "local:mi355x run storm-run: success" in out.getvalue()
+
+
+def test_groups_disagreeing_on_a_read_parameter_fail_the_run(oracle):
+    c = CP.parse_composition(STORM.replace('role = "dialer"', 'role = "dialer"\n  conn_outgoing = "4"'))
+    CP.validate_for_run(c)
+    job = CP.to_run_input(CP.prepare_for_run(c, CP.parse_manifest(MANIFEST)), "ambiguous")
+    with pytest.raises(ValueError, match="'conn_outgoing' differs between groups"):
+        LocalMI355XRunner(binding=oracle).run(job)
 
 
 @pytest.mark.gpu
