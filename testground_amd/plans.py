@@ -14,6 +14,7 @@ Registered plans (``PLANS[(plan, case)]``):
   splitbrain/{drop,reject,accept}   plans/splitbrain/main.go:41-186
   benchmarks/storm            plans/benchmarks/storm.go:31-197
   benchmarks/barrier          plans/benchmarks/benchmarks.go:90-145
+  benchmarks/{startup,netinit,netlinkshape,subtree}   plans/benchmarks/benchmarks.go:20-86, 148-270
 """
 from __future__ import annotations
 
@@ -487,6 +488,77 @@ def barrier_bench(env: PlanEnv) -> np.ndarray:
     return np.ones(n, bool)
 
 
+def startup(env: PlanEnv) -> np.ndarray:
+    """plans/benchmarks/benchmarks.go:20-24 (StartTimeBench): records the time since the run
+    started; simulated instances start at time 0."""
+    env.time_to_start = np.zeros(env.n, np.int64)
+    return np.ones(env.n, bool)
+
+
+def netinit(env: PlanEnv) -> np.ndarray:
+    """benchmarks.go:29-48 (NetworkInitBench): the time until the sidecars' network-initialized
+    barrier releases."""
+    t = env.net.wait_network_initialized(0)
+    env.time_to_network_init = np.full(env.n, t, np.int64)
+    return np.ones(env.n, bool)
+
+
+def netlinkshape(env: PlanEnv) -> np.ndarray:
+    """benchmarks.go:51-86 (NetworkLinkShapeBench): every instance sends its sidecar
+    Config{Network: "default", Default: {Latency: 250 ms}, CallbackState: callback-<random>,
+    CallbackTarget: 1} and waits for its own callback. Enable is left at its zero value, so the
+    sidecar disconnects the data link (docker_network.go:65-88) - as the reference plan does."""
+    n = env.n
+    t = env.net.wait_network_initialized(0)
+    rng = np.random.default_rng(env.int_param("seed", 0))
+    rel = np.empty(n, np.int64)
+    for g in range(n):
+        cfg = Config(network="default", default=LinkShape(latency=250 * MS),
+                     callback_state=f"callback-{int(rng.integers(0, 1 << 62))}", callback_target=1)
+        rel[g] = env.net.configure_network(g, cfg, t)
+    env.time_to_shape_network = rel - t
+    return rel >= 0
+
+
+def subtree(env: PlanEnv) -> np.ndarray:
+    """benchmarks.go:148-270 (SubtreeBench): every instance publishes its run id on "instances";
+    the one with sequence number 1 publishes `subtree_iterations` items on each of the topics
+    subtree_time_<size>_bytes (size 64 .. 4096, doubling), signals "handoff" and waits on "end"
+    for the whole group; the others wait for "handoff", read `subtree_iterations` items of every
+    topic, compare each with the published value and signal "end". The published value is the
+    reference's `string(make([]byte, 0, size))` after rand.Read: zero bytes are read into a
+    zero-length slice, so every item is the empty string."""
+    n = env.n
+    iterations = env.int_param("subtree_iterations", 2000)
+    t = env.net.wait_network_initialized(0)
+    seq = env.sync.publish("instances", np.arange(n), t, ["run"] * n)
+    pub = int(np.flatnonzero(seq == 1)[0])
+    sizes = []
+    s = 64
+    while s <= 4 * 1024:
+        sizes.append(s)
+        s <<= 1
+    data = ""
+    for size in sizes:
+        env.sync.publish(f"subtree_time_{size}_bytes", np.full(iterations, pub), t, [data] * iterations)
+    env.sync.signal_entry("handoff", [pub], t)
+    ok = np.ones(n, bool)
+    receivers = np.flatnonzero(np.arange(n) != pub)
+    if len(receivers):
+        t_h = env.sync.barrier("handoff", 1, t)
+        for size in sizes:
+            items = env.sync.subscribe(f"subtree_time_{size}_bytes", until_t=t_h)
+            if len(items) < iterations or any(x != data for x in items[:iterations]):
+                ok[receivers] = False
+                env.fail(f"subtree_time_{size}_bytes: received unexpected value")
+        env.sync.signal_entry("end", receivers, t_h)
+    _, t_end = env.sync.signal_and_wait("end", [pub], t, n)
+    if t_end < 0:
+        ok[pub] = False
+        env.fail("end never released")
+    return ok
+
+
 PLANS = {
     ("network", "ping-pong"): pingpong,
     ("network", "traffic-allowed"): traffic(AllowAll),
@@ -496,4 +568,8 @@ PLANS = {
     ("splitbrain", "accept"): splitbrain(FilterAction.Accept),
     ("benchmarks", "storm"): storm,
     ("benchmarks", "barrier"): barrier_bench,
+    ("benchmarks", "startup"): startup,
+    ("benchmarks", "netinit"): netinit,
+    ("benchmarks", "netlinkshape"): netlinkshape,
+    ("benchmarks", "subtree"): subtree,
 }

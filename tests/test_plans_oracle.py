@@ -145,6 +145,26 @@ def test_barrier_bench(oracle):
     env.close()
 
 
+def test_benchmark_small_cases(oracle):
+    """benchmarks.go:20-86 / 148-270: startup, netinit, netlinkshape, subtree"""
+    env = env_for(oracle, 6, "startup")
+    assert P.startup(env).all() and env.time_to_start.max() == 0
+    env.close()
+    env = env_for(oracle, 6, "netinit")
+    assert P.netinit(env).all()
+    env.close()
+    env = env_for(oracle, 6, "netlinkshape", params={"seed": "3"})
+    assert P.netlinkshape(env).all() and np.all(env.time_to_shape_network >= 0)
+    # Enable stays false in the plan's config: the sidecar disconnects every data link
+    assert not any(env.sidecar.network(g).list_active() for g in range(6))
+    env.close()
+    env = env_for(oracle, 5, "subtree", params={"subtree_iterations": "50"})
+    assert P.subtree(env).all() and not env.failures
+    assert env.sync.count("end") == 5 and env.sync.count("handoff") == 1
+    assert len(env.sync.subscribe("subtree_time_4096_bytes")) == 50
+    env.close()
+
+
 def test_storm_completes(oracle):
     env = env_for(oracle, 20, params={"conn_outgoing": 3, "conn_delay_ms": 1000, "data_size_kb": 10})
     ok = P.storm(env)
@@ -212,3 +232,16 @@ def test_runner_rejects_unknown_plan(oracle):
         r.run(RunInput("r3", "network", "nope", 2, [RunGroup("g", 2)]))
     with pytest.raises(ValueError, match="TotalInstances"):
         r.run(RunInput("r4", "network", "ping-pong", 3, [RunGroup("g", 2)]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,params", [("netlinkshape", {"seed": "3"}), ("subtree", {"subtree_iterations": "50"})])
+def test_benchmark_small_cases_hip(hip, oracle, case, params):
+    out = []
+    for b in (hip, oracle):
+        env = P.PlanEnv(6, seed=1, test_case=case, params=params, binding=b)
+        ok = P.PLANS[("benchmarks", case)](env)
+        out.append((ok.tolist(), env.sim.now, env.sync.count("end") if case == "subtree" else 0,
+                    getattr(env, "time_to_shape_network", np.zeros(0)).tolist()))
+        env.close()
+    assert out[0] == out[1]

@@ -22,6 +22,10 @@ CASES = [
     (("splitbrain", "accept"), 12, {}),
     (("benchmarks", "barrier"), 50, {"barrier_iterations": 2}),
     (("benchmarks", "storm"), 20, {"conn_outgoing": 3, "conn_delay_ms": 1000, "data_size_kb": 16}),
+    (("benchmarks", "startup"), 10, {}),
+    (("benchmarks", "netinit"), 10, {}),
+    (("benchmarks", "netlinkshape"), 10, {}),
+    (("benchmarks", "subtree"), 10, {"subtree_iterations": 100}),
 ]
 
 
