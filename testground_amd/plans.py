@@ -15,6 +15,7 @@ Registered plans (``PLANS[(plan, case)]``):
   benchmarks/storm            plans/benchmarks/storm.go:31-197
   benchmarks/barrier          plans/benchmarks/benchmarks.go:90-145
   benchmarks/{startup,netinit,netlinkshape,subtree}   plans/benchmarks/benchmarks.go:20-86, 148-270
+  verify/uses-data-network    plans/verify/main.go:43-130
 """
 from __future__ import annotations
 
@@ -559,6 +560,59 @@ def subtree(env: PlanEnv) -> np.ndarray:
     return ok
 
 
+# ============================================================================================
+# plans/verify
+# ============================================================================================
+
+def _is_control_net(addr: str) -> bool:
+    """verify/main.go:33-35: the local:docker and cluster:k8s control networks"""
+    return addr.startswith("192.18.") or addr.startswith("100.96.")
+
+
+def verify_uses_data_network(env: PlanEnv) -> np.ndarray:
+    """plans/verify/main.go:43-130 (UsesDataNetwork): SignalAndWait("ready", N); the instance with
+    sequence number 1 (targetmode) publishes the addresses of its control interface (eth0, on
+    192.18.0.0/16) and its data interface (eth1) and "endOfNetworks" on topic "addrs", then signals
+    "target-ready"; every other instance waits for it and pings each address 10 times, 500 ms
+    apart with a 1 s timeout: the control address must lose 100 % of the pings, the data address
+    0 % (:103-106). SignalAndWait("finished", N). A simulated instance routes only its data
+    network (and, under AllowAll, the default route out of it), so a control address is outside
+    everything it can reach."""
+    n = env.n
+    t = env.net.wait_network_initialized(0)
+    seq, t = env.sync.signal_and_wait("ready", np.arange(n), t, n)
+    target = int(np.flatnonzero(seq == 1)[0])
+    data_ip = env.net.get_data_network_ip(target)
+    addrs = [f"192.18.{(target >> 8) & 255}.{(target & 255) or 1}/16",
+             f"{int_to_ip(data_ip)}/{env.sim.cfg.data_prefix_len}", "endOfNetworks"]
+    env.sync.publish("addrs", [target] * len(addrs), t, addrs)
+    env.sync.signal_entry("target-ready", [target], t)
+    ok = np.ones(n, bool)
+    pingers = np.flatnonzero(np.arange(n) != target)
+    env.packet_loss = {}
+    t_ready = env.sync.barrier("target-ready", 1, t)
+    if len(pingers):
+        env.advance_to(t_ready)
+        for a in env.sync.subscribe("addrs", until_t=t_ready):
+            if a == "endOfNetworks":
+                break
+            ip = a.split("/")[0]
+            dst = target if ip == int_to_ip(data_ip) else A.DST_EXTERNAL
+            t0 = env.sim.now
+            src = np.repeat(pingers, 10)
+            t_ping = t0 + np.tile(np.arange(10) * 500 * MS, len(pingers))
+            got, _ = env.rpc(src, dst, 84, 84, t_ping, 1 * SECOND)     # ICMP echo: 56 B + 8 + 20
+            loss = 100.0 * (1.0 - got.reshape(len(pingers), 10).mean(axis=1))
+            env.packet_loss[a] = loss
+            bad = loss != 100.0 if _is_control_net(ip) else loss > 0.0
+            for g in pingers[bad]:
+                env.fail(f"instance {g}: " + ("control network is accessible; it should not be" if _is_control_net(ip)
+                                              else "data network is not accessible; it should be"))
+            ok[pingers[bad]] = False
+    _, t_fin = env.sync.signal_and_wait("finished", np.arange(n), max(env.sim.now, t_ready), n)
+    return ok & (t_fin >= 0)
+
+
 PLANS = {
     ("network", "ping-pong"): pingpong,
     ("network", "traffic-allowed"): traffic(AllowAll),
@@ -572,4 +626,5 @@ PLANS = {
     ("benchmarks", "netinit"): netinit,
     ("benchmarks", "netlinkshape"): netlinkshape,
     ("benchmarks", "subtree"): subtree,
+    ("verify", "uses-data-network"): verify_uses_data_network,
 }

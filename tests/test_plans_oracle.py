@@ -165,6 +165,18 @@ def test_benchmark_small_cases(oracle):
     env.close()
 
 
+def test_verify_uses_data_network(oracle):
+    """plans/verify/main.go:103-106: pings to the target's control address lose 100 %, to its data
+    address 0 %"""
+    env = env_for(oracle, 4, "uses-data-network")
+    ok = P.verify_uses_data_network(env)
+    assert ok.all() and not env.failures
+    (ctl, c_loss), (dat, d_loss) = env.packet_loss.items()
+    assert ctl.startswith("192.18.") and np.all(c_loss == 100.0)
+    assert dat.startswith("16.0.") and np.all(d_loss == 0.0)
+    env.close()
+
+
 def test_storm_completes(oracle):
     env = env_for(oracle, 20, params={"conn_outgoing": 3, "conn_delay_ms": 1000, "data_size_kb": 10})
     ok = P.storm(env)
@@ -235,13 +247,16 @@ def test_runner_rejects_unknown_plan(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,params", [("netlinkshape", {"seed": "3"}), ("subtree", {"subtree_iterations": "50"})])
-def test_benchmark_small_cases_hip(hip, oracle, case, params):
+@pytest.mark.parametrize("plan,case,params", [("benchmarks", "netlinkshape", {"seed": "3"}),
+                                              ("benchmarks", "subtree", {"subtree_iterations": "50"}),
+                                              ("verify", "uses-data-network", {})])
+def test_small_plan_cases_hip(hip, oracle, plan, case, params):
     out = []
     for b in (hip, oracle):
         env = P.PlanEnv(6, seed=1, test_case=case, params=params, binding=b)
-        ok = P.PLANS[("benchmarks", case)](env)
+        ok = P.PLANS[(plan, case)](env)
         out.append((ok.tolist(), env.sim.now, env.sync.count("end") if case == "subtree" else 0,
-                    getattr(env, "time_to_shape_network", np.zeros(0)).tolist()))
+                    getattr(env, "time_to_shape_network", np.zeros(0)).tolist(),
+                    {k: v.tolist() for k, v in getattr(env, "packet_loss", {}).items()}))
         env.close()
-    assert out[0] == out[1]
+    assert out[0] == out[1] and all(out[0][0])

@@ -26,6 +26,7 @@ CASES = [
     (("benchmarks", "netinit"), 10, {}),
     (("benchmarks", "netlinkshape"), 10, {}),
     (("benchmarks", "subtree"), 10, {"subtree_iterations": 100}),
+    (("verify", "uses-data-network"), 4, {}),
 ]
 
 
