@@ -16,6 +16,7 @@ Registered plans (``PLANS[(plan, case)]``):
   benchmarks/barrier          plans/benchmarks/benchmarks.go:90-145
   benchmarks/{startup,netinit,netlinkshape,subtree}   plans/benchmarks/benchmarks.go:20-86, 148-270
   verify/uses-data-network    plans/verify/main.go:43-130
+  placebo/{ok,panic,stall}    plans/placebo/main.go:17-40
 """
 from __future__ import annotations
 
@@ -561,6 +562,32 @@ def subtree(env: PlanEnv) -> np.ndarray:
 
 
 # ============================================================================================
+# plans/placebo (the engine's own integration plan: outcome reporting)
+# ============================================================================================
+
+class PlanPanic(Exception):
+    """A test case that panics: every instance of the run reports a CrashEvent (sdk-go runtime)."""
+
+
+def placebo_ok(env: PlanEnv) -> np.ndarray:
+    """plans/placebo/main.go:23-27: bind a sync client and return."""
+    return np.ones(env.n, bool)
+
+
+def placebo_panic(env: PlanEnv) -> np.ndarray:
+    """plans/placebo/main.go:29-33: panic(errors.New("this is an intentional panic"))."""
+    raise PlanPanic("this is an intentional panic")
+
+
+def placebo_stall(env: PlanEnv) -> np.ndarray:
+    """plans/placebo/main.go:35-40: sleep 24 hours, then return. Simulated time costs nothing while
+    nothing is in flight: the run ends 24 simulated hours later (a wall-clock run timeout, the
+    reference runners' way out of it, never fires)."""
+    env.advance_to(24 * 3600 * SECOND)
+    return np.ones(env.n, bool)
+
+
+# ============================================================================================
 # plans/verify
 # ============================================================================================
 
@@ -627,4 +654,7 @@ PLANS = {
     ("benchmarks", "netlinkshape"): netlinkshape,
     ("benchmarks", "subtree"): subtree,
     ("verify", "uses-data-network"): verify_uses_data_network,
+    ("placebo", "ok"): placebo_ok,
+    ("placebo", "panic"): placebo_panic,
+    ("placebo", "stall"): placebo_stall,
 }

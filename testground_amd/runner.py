@@ -75,6 +75,10 @@ def failure_event(group: str, error: str) -> dict:
     return {"FailureEvent": {"TestGroupID": group, "Error": error}}
 
 
+def crash_event(group: str, error: str) -> dict:
+    return {"CrashEvent": {"TestGroupID": group, "Error": error, "Stacktrace": ""}}
+
+
 def collect_outcomes(events, result: "Result") -> None:
     """local_docker.go:216-255: count SuccessEvent per group; FailureEvent and CrashEvent count as
     reported but not ok; stop once every instance has reported; then update the outcome."""
@@ -247,15 +251,20 @@ class LocalMI355XRunner:
         except Exception:
             self._active -= 1
             raise
+        crash = None
         try:
-            ok = np.asarray(P.PLANS[key](env), bool)
+            try:
+                ok = np.asarray(P.PLANS[key](env), bool)
+            except P.PlanPanic as e:   # the test case panicked: every instance crashes
+                crash = str(e)
+                ok = np.zeros(total, bool)
             stats = env.sim.stats()
             sim_now = env.sim.now
             failures = list(env.failures)
         finally:
             env.close()
             self._active -= 1
-        events = self._events(job, ok, sim_now, failures)
+        events = self._events(job, ok, sim_now, failures, crash)
         collect_outcomes((e for per in events for e in per[1]), result)
         result.journal["failures"] = failures
         result.journal["events"] = {"simulated_ns": str(sim_now), "wall_s": f"{time.perf_counter() - t0:.3f}"}
@@ -273,16 +282,18 @@ class LocalMI355XRunner:
         return RunOutput(run_id=job.run_id, result=result)
 
     @staticmethod
-    def _events(job: RunInput, ok, t_end: int, failures: list) -> list:
-        """Each simulated instance's runtime events: StartEvent at time 0, then SuccessEvent or
-        FailureEvent at the plan's end (the instance's id is <group>[<index in group>])."""
+    def _events(job: RunInput, ok, t_end: int, failures: list, crash: str | None = None) -> list:
+        """Each simulated instance's runtime events: StartEvent at time 0, then SuccessEvent,
+        FailureEvent or (the case panicked) CrashEvent at the plan's end (the instance's id is
+        <group>[<index in group>])."""
         out, base = [], 0
         err = failures[0] if failures else "the instance did not complete the test case"
         for g in job.groups:
             runenv = {"TestPlan": job.test_plan, "TestCase": job.test_case, "TestRun": job.run_id,
                       "TestInstanceCount": job.total_instances, "TestGroupInstanceCount": g.instances}
             for i in range(g.instances):
-                done = success_event(g.id) if ok[base + i] else failure_event(g.id, err)
+                done = (crash_event(g.id, crash) if crash is not None else
+                        success_event(g.id) if ok[base + i] else failure_event(g.id, err))
                 out.append((f"{g.id}[{i}]", [{"ts": 0, "event": start_event(g.id, runenv)},
                                              {"ts": int(t_end), "event": done}]))
             base += g.instances

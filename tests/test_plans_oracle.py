@@ -260,3 +260,19 @@ def test_small_plan_cases_hip(hip, oracle, plan, case, params):
                     {k: v.tolist() for k, v in getattr(env, "packet_loss", {}).items()}))
         env.close()
     assert out[0] == out[1] and all(out[0][0])
+
+
+def test_placebo_outcomes(oracle):
+    """plans/placebo through the runner: ok succeeds, panic crashes every instance (CrashEvent,
+    counted not-ok as collectOutcomes does), stall ends 24 simulated hours later"""
+    r = LocalMI355XRunner(binding=oracle)
+    outs = {}
+    for case in ("ok", "panic", "stall"):
+        job = RunInput(run_id=f"placebo-{case}", test_plan="placebo", test_case=case, total_instances=3,
+                       groups=[RunGroup(id="single", instances=3)])
+        w = io.StringIO()
+        outs[case] = (r.run(job, w).result, w.getvalue())
+    assert outs["ok"][0].outcome == "success" and outs["stall"][0].outcome == "success"
+    res, text = outs["panic"]
+    assert res.outcome == "failure" and res.outcomes["single"].ok == 0
+    assert text.count("CRASH") == 3 and "this is an intentional panic" in text

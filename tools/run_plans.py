@@ -27,6 +27,8 @@ CASES = [
     (("benchmarks", "netlinkshape"), 10, {}),
     (("benchmarks", "subtree"), 10, {"subtree_iterations": 100}),
     (("verify", "uses-data-network"), 4, {}),
+    (("placebo", "ok"), 3, {}),
+    (("placebo", "stall"), 3, {}),
 ]
 
 
