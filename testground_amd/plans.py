@@ -17,6 +17,7 @@ Registered plans (``PLANS[(plan, case)]``):
   benchmarks/{startup,netinit,netlinkshape,subtree}   plans/benchmarks/benchmarks.go:20-86, 148-270
   verify/uses-data-network    plans/verify/main.go:43-130
   placebo/{ok,panic,stall}    plans/placebo/main.go:17-40
+  example/{sync,failure,panic} plans/example/{sync,failure,panic}.go
 """
 from __future__ import annotations
 
@@ -588,6 +589,45 @@ def placebo_stall(env: PlanEnv) -> np.ndarray:
 
 
 # ============================================================================================
+# plans/example (the SDK's demonstration plan)
+# ============================================================================================
+
+def example_sync(env: PlanEnv) -> np.ndarray:
+    """plans/example/sync.go:20-80 (ExampleSync): every instance signals "enrolled" at start; the
+    one with sequence number 1 leads: it waits on Barrier("ready", N - 1), sleeps 1 + 5 s and
+    signals "released"; each follower sleeps U{0..4} s, signals "ready" and waits on
+    Barrier("released", 1). env.released = each follower's release time."""
+    n = env.n
+    rng = np.random.default_rng(env.int_param("seed", 0))
+    seq = env.sync.signal_entry("enrolled", np.arange(n), 0)
+    leader = int(np.flatnonzero(seq == 1)[0])
+    followers = np.flatnonzero(np.arange(n) != leader)
+    t_ready = rng.integers(0, 5, len(followers)) * SECOND
+    if len(followers):
+        env.sync.signal_entry("ready", followers, t_ready)
+    t_all = env.sync.barrier("ready", len(followers), 0)
+    ok = np.ones(n, bool)
+    if t_all < 0:
+        env.fail("the followers never became ready")
+        return np.zeros(n, bool)
+    env.sync.signal_entry("released", [leader], t_all + 6 * SECOND)
+    env.released = np.array([env.sync.barrier("released", 1, int(t)) for t in t_ready], np.int64)
+    ok[followers] = env.released >= 0
+    return ok
+
+
+def example_failure(env: PlanEnv) -> np.ndarray:
+    """plans/example/failure.go:11-14: returns errors.New("intentional oops")."""
+    env.fail("intentional oops")
+    return np.zeros(env.n, bool)
+
+
+def example_panic(env: PlanEnv) -> np.ndarray:
+    """plans/example/panic.go:12: panic("intentional panic")."""
+    raise PlanPanic("intentional panic")
+
+
+# ============================================================================================
 # plans/verify
 # ============================================================================================
 
@@ -657,4 +697,7 @@ PLANS = {
     ("placebo", "ok"): placebo_ok,
     ("placebo", "panic"): placebo_panic,
     ("placebo", "stall"): placebo_stall,
+    ("example", "sync"): example_sync,
+    ("example", "failure"): example_failure,
+    ("example", "panic"): example_panic,
 }

@@ -276,3 +276,23 @@ def test_placebo_outcomes(oracle):
     res, text = outs["panic"]
     assert res.outcome == "failure" and res.outcomes["single"].ok == 0
     assert text.count("CRASH") == 3 and "this is an intentional panic" in text
+
+
+def test_example_sync_leader_releases_followers(oracle):
+    """plans/example/sync.go: the leader (sequence 1 of "enrolled") releases every follower 6 s
+    after the last one is ready"""
+    env = env_for(oracle, 7, "sync", params={"seed": "4"})
+    ok = P.example_sync(env)
+    assert ok.all()
+    rng = np.random.default_rng(4)
+    t_ready = rng.integers(0, 5, 6) * 1_000_000_000
+    assert np.all(env.released == t_ready.max() + 6_000_000_000)
+    env.close()
+
+
+def test_example_failure_through_the_runner(oracle):
+    job = RunInput(run_id="ex-fail", test_plan="example", test_case="failure", total_instances=2,
+                   groups=[RunGroup(id="g", instances=2)])
+    w = io.StringIO()
+    res = LocalMI355XRunner(binding=oracle).run(job, w).result
+    assert res.outcome == "failure" and w.getvalue().count("FAIL") >= 2 and "intentional oops" in w.getvalue()

@@ -29,6 +29,7 @@ CASES = [
     (("verify", "uses-data-network"), 4, {}),
     (("placebo", "ok"), 3, {}),
     (("placebo", "stall"), 3, {}),
+    (("example", "sync"), 6, {}),
 ]
 
 
