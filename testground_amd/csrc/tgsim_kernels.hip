@@ -1625,12 +1625,25 @@ struct EmitPolicy {
 // key order instead and listed for k_rest (medium / large segments).
 // ============================================================================================
 
-constexpr int kBktCap = 2048;         // items of one bucket held by the workgroup
+// 1536 items per bucket keep a workgroup at 40 KB of LDS and 112-118 VGPRs, so four buckets share a
+// CU (2048 items: 52.7 KB, three per CU); the fourth workgroup's memory phases overlap the others'
+// LDS-bound ranking: storm step -8.7 %, flood -5.5 %. 1024 items / five per CU made
+// the consumers faster still but overflowed the flood's buckets (1M senders: ~900 items each).
+#ifndef TG_BKT_CAP
+#define TG_BKT_CAP 1536
+#endif
+#ifndef TG_STAGE_N
+#define TG_STAGE_N 960
+#endif
+#ifndef TG_BKT_WGS_PER_CU
+#define TG_BKT_WGS_PER_CU 4
+#endif
+constexpr int kBktCap = TG_BKT_CAP;   // items of one bucket held by the workgroup
 constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
 constexpr uint32_t kBktRankMax = 64;  // longest key run ranked in LDS
 constexpr int kIPT = kBktCap / kBlock;  // items per thread
 
-constexpr uint32_t kStageN = 1280;  // records staged per round for the coalesced output (k1 + k2 + k3 area:
+constexpr uint32_t kStageN = TG_STAGE_N;  // records staged per round for the coalesced output (k1 + k2 + k3 area:
                                     // a storm bucket of ~1.1k copies leaves in one round)
 
 struct BktFusedSmem {
@@ -3262,16 +3275,16 @@ static BktDiv bkt_div(uint32_t w) {
   return b;
 }
 
-// Keys per bucket of the fused consumers: >= 128 keys (~1k items of a storm) per workgroup, and
-// few enough buckets that they all run in one wave of workgroups (3 per CU); <= 512 keys; at
-// least TG_BKT_MIN_KEYS (48: measured best for 12.5k-instance shards, neutral at 100k).
+// Keys per bucket of the fused consumers: few enough buckets that they all run in one wave of
+// workgroups (TG_BKT_WGS_PER_CU per CU: ~98 keys, ~780 items of a storm per workgroup); <= 512
+// keys; at least TG_BKT_MIN_KEYS (48: measured best for 12.5k-instance shards, neutral at 100k).
 static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
 #ifndef TG_BKT_MIN_KEYS
 #define TG_BKT_MIN_KEYS 48u  // small shards (strong scaling): more, smaller buckets
 #endif
   // a context whose windows carry bkt_load times the packets per key (TCP acks: an ACK per data
   // packet) splits its keys over as many more buckets, so a bucket still fits kBktCap items
-  const uint32_t slots = 3u * (uint32_t)d.n_cu * d.bkt_load;
+  const uint32_t slots = (uint32_t)TG_BKT_WGS_PER_CU * (uint32_t)d.n_cu * d.bkt_load;
   uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(TG_BKT_MIN_KEYS, K));
   w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
   // never more than kMaxBins buckets (the partition's LDS histograms and d.poff rows are that wide)
