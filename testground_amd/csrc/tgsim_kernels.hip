@@ -3277,10 +3277,11 @@ static BktDiv bkt_div(uint32_t w) {
 
 // Keys per bucket of the fused consumers: few enough buckets that they all run in one wave of
 // workgroups (TG_BKT_WGS_PER_CU per CU: ~98 keys, ~780 items of a storm per workgroup); <= 512
-// keys; at least TG_BKT_MIN_KEYS (48: measured best for 12.5k-instance shards, neutral at 100k).
+// keys; at least TG_BKT_MIN_KEYS (24 with four workgroups per CU: 12.5k-instance shards -6 %, 25k -3 %,
+// 50k and 100k unchanged; 48 was best with three per CU).
 static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
 #ifndef TG_BKT_MIN_KEYS
-#define TG_BKT_MIN_KEYS 48u  // small shards (strong scaling): more, smaller buckets
+#define TG_BKT_MIN_KEYS 24u  // small shards (strong scaling): more, smaller buckets
 #endif
   // a context whose windows carry bkt_load times the packets per key (TCP acks: an ACK per data
   // packet) splits its keys over as many more buckets, so a bucket still fits kBktCap items
