@@ -426,10 +426,18 @@ def _attach_transport(sim, dist, world: int, rank: int, rehearsal: bool) -> str:
         return "-gloo-rehearsal"
     import torch
     from testground_amd.sim import Simulator
-    uid = [Simulator.comm_unique_id() if rank == 0 else None]
+    uid = [None]
+    if rank == 0:
+        try:
+            uid[0] = Simulator.comm_unique_id()
+        except Exception as e:  # noqa: BLE001 - every rank sees None and takes the fallback
+            print(f"rank 0: RCCL unique id failed ({e}); falling back to the gloo transport",
+                  file=sys.stderr, flush=True)
     dist.broadcast_object_list(uid, src=0)
     ok = 1
     try:
+        if uid[0] is None:
+            raise RuntimeError("no RCCL unique id")
         sim.comm_init(uid[0], world, rank)
     except Exception as e:  # noqa: BLE001 - reported, then every rank takes the same path
         print(f"rank {rank}: RCCL communicator failed ({e}); falling back to the gloo transport",

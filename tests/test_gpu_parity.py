@@ -130,6 +130,17 @@ def test_storm_transport_on_one_device(hip, oracle, world):
 
 
 @pytest.mark.gpu
+def test_rccl_communicator_one_rank(hip, oracle):
+    """The native communicator comes up on the box (unique id, bootstrap, ncclCommInitRank - what
+    bench.py --gpus N does on every rank) and a one-shard storm with it attached equals the oracle.
+    RCCL refuses two ranks on one GPU, so the collectives themselves run only between GPUs."""
+    from testground_amd.sim import Simulator
+    uid = Simulator.comm_unique_id()
+    kw = dict(n_inst=1500, rounds=4, t_now=True)
+    S.assert_same(S.run_storm(hip, setup=lambda sim: sim.comm_init(uid, 1, 0), **kw), S.run_storm(oracle, **kw))
+
+
+@pytest.mark.gpu
 def test_storm_device_clock_speculation(hip, oracle):
     """bench.py's loop (rounds at TGSIM_T_NOW): each window's last launch generates the next round,
     which the next tgsim_gen_storm_round adopts. Calls that touch the staged arrays or the signal
