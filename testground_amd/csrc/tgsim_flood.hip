@@ -92,6 +92,10 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
                                                        uint32_t* __restrict__ m_dst, uint32_t* __restrict__ m_seq,
                                                        uint32_t* __restrict__ m_size, int64_t* __restrict__ m_t) {
   __shared__ uint32_t red[kBlock / 64];
+  // the tile's first receipts in LDS; their forwards are then written one output slot per thread
+  // (consecutive lanes, consecutive slots) instead of one delivery per thread (lanes ≈deg slots apart)
+  __shared__ uint32_t s_off[kBlock], s_g[kBlock], s_s[kBlock], s_p[kBlock], s_k0[kBlock], s_k1[kBlock];
+  __shared__ int64_t s_t[kBlock];
   uint32_t i0, i1;
   chunk_range(sc->n_out, i0, i1);
   uint32_t run = f.bsum[blockIdx.x];
@@ -100,19 +104,38 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
     const bool in = i < i1;
     const bool first = in && f.first[i];
     uint32_t tile;
-    uint32_t w = run + block_excl_scan(first ? f.cnt[i] : 0u, red, tile);
-    run += tile;
-    if (!first) continue;
-    const uint32_t g = o_dst[i], v = g - lo, s = o_src[i], p = o_seq[i] / f.D;
-    atomicOr(&f.seen[(size_t)p * f.wpp + (v >> 5)], 1u << (v & 31));
-    const int64_t t = o_t[i] > horizon ? o_t[i] : horizon;
-    const uint32_t k0 = f.off[v], k1 = f.off[v + 1];
-    for (uint32_t k = k0; k < k1; ++k) {
-      const uint32_t u = f.nbr[k];
-      if (u == s) continue;
-      if (w < cap) { m_src[w] = g; m_dst[w] = u; m_seq[w] = p * f.D + (k - k0); m_size[w] = size; m_t[w] = t; }
-      ++w;
+    s_off[threadIdx.x] = block_excl_scan(first ? f.cnt[i] : 0u, red, tile);
+    if (first) {
+      const uint32_t g = o_dst[i], v = g - lo, p = o_seq[i] / f.D;
+      atomicOr(&f.seen[(size_t)p * f.wpp + (v >> 5)], 1u << (v & 31));
+      s_g[threadIdx.x] = g; s_s[threadIdx.x] = o_src[i]; s_p[threadIdx.x] = p;
+      s_k0[threadIdx.x] = f.off[v]; s_k1[threadIdx.x] = f.off[v + 1];
+      s_t[threadIdx.x] = o_t[i] > horizon ? o_t[i] : horizon;
     }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < tile; j += kBlock) {
+      // the delivery d whose forwards cover j: the last offset <= j (a delivery with forwards has a
+      // larger offset than every one before it)
+      uint32_t lo_d = 0, hi_d = kBlock;
+      while (hi_d - lo_d > 1) {
+        const uint32_t mid = (lo_d + hi_d) >> 1;
+        if (s_off[mid] <= j) lo_d = mid; else hi_d = mid;
+      }
+      const uint32_t d = lo_d, s = s_s[d], k0 = s_k0[d], k1 = s_k1[d];
+      uint32_t r = j - s_off[d], k = k0;
+      for (; k < k1; ++k) {  // the r-th neighbour other than the sender (row order)
+        if (f.nbr[k] == s) continue;
+        if (r == 0) break;
+        --r;
+      }
+      const uint32_t w = run + j;
+      if (w < cap) {
+        m_src[w] = s_g[d]; m_dst[w] = f.nbr[k]; m_seq[w] = s_p[d] * f.D + (k - k0); m_size[w] = size;
+        m_t[w] = s_t[d];
+      }
+    }
+    run += tile;
+    __syncthreads();  // the next tile rewrites the LDS arrays
   }
 }
 
