@@ -24,6 +24,8 @@ namespace tgsim {
 
 namespace {
 
+constexpr uint32_t kWalkMax = 32;  // k_flood_emit: rows up to this long are written one slot per thread
+
 // Chunk c of the n deliveries: [c * per, min(n, (c + 1) * per)).
 __device__ __forceinline__ void chunk_range(uint32_t n, uint32_t& i0, uint32_t& i1) {
   const uint32_t per = (n + kFloodBlocks - 1) / kFloodBlocks;
@@ -111,6 +113,17 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
       s_g[threadIdx.x] = g; s_s[threadIdx.x] = o_src[i]; s_p[threadIdx.x] = p;
       s_k0[threadIdx.x] = f.off[v]; s_k1[threadIdx.x] = f.off[v + 1];
       s_t[threadIdx.x] = o_t[i] > horizon ? o_t[i] : horizon;
+      const uint32_t k0 = s_k0[threadIdx.x], k1 = s_k1[threadIdx.x];
+      if (k1 - k0 > kWalkMax) {  // a long row: its own thread writes it (the walk below is O(row) per slot)
+        const uint32_t s = s_s[threadIdx.x];
+        uint32_t w = run + s_off[threadIdx.x];
+        for (uint32_t k = k0; k < k1; ++k) {
+          const uint32_t u = f.nbr[k];
+          if (u == s) continue;
+          if (w < cap) { m_src[w] = g; m_dst[w] = u; m_seq[w] = p * f.D + (k - k0); m_size[w] = size; m_t[w] = s_t[threadIdx.x]; }
+          ++w;
+        }
+      }
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < tile; j += kBlock) {
@@ -122,6 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
         if (s_off[mid] <= j) lo_d = mid; else hi_d = mid;
       }
       const uint32_t d = lo_d, s = s_s[d], k0 = s_k0[d], k1 = s_k1[d];
+      if (k1 - k0 > kWalkMax) continue;
       uint32_t r = j - s_off[d], k = k0;
       for (; k < k1; ++k) {  // the r-th neighbour other than the sender (row order)
         if (f.nbr[k] == s) continue;

@@ -137,6 +137,17 @@ def test_flood_hip_matches_oracle(hip, oracle, n, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("degree", [32, 40])
+def test_flood_row_lengths_hip(hip, oracle, degree):
+    """k_flood_emit writes rows of up to 32 neighbours one output slot per thread and longer rows
+    one delivery per thread: both sides of the switch equal the oracle."""
+    n = 400
+    a = S.run_flood(hip, n_inst=n, degree=degree, shapes=_lossless(n))
+    S.assert_same(a, S.run_flood(oracle, n_inst=n, degree=degree, shapes=_lossless(n)))
+    _check_flood_invariants(a, n, degree=degree)
+
+
+@pytest.mark.gpu
 def test_flood_async_reaction_matches_oracle(hip, oracle):
     """tgsim_flood_react without a forward count runs with no host read: the delivery count, the
     staged count and the forwards stay on the device, and the next wave's publish appends behind
