@@ -25,6 +25,7 @@ namespace tgsim {
 namespace {
 
 constexpr uint32_t kWalkMax = 32;  // k_flood_emit: rows up to this long are written one slot per thread
+constexpr uint32_t kMultiSender = 0xFFFFFFFFu;  // k_flood_emit: the sender occurs more than once in the row
 
 // Chunk c of the n deliveries: [c * per, min(n, (c + 1) * per)).
 __device__ __forceinline__ void chunk_range(uint32_t n, uint32_t& i0, uint32_t& i1) {
@@ -97,6 +98,7 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
   // the tile's first receipts in LDS; their forwards are then written one output slot per thread
   // (consecutive lanes, consecutive slots) instead of one delivery per thread (lanes ≈deg slots apart)
   __shared__ uint32_t s_off[kBlock], s_g[kBlock], s_s[kBlock], s_p[kBlock], s_k0[kBlock], s_k1[kBlock];
+  __shared__ uint32_t s_pos[kBlock];  // the sender's place in a short row (kMultiSender: more than one)
   __shared__ int64_t s_t[kBlock];
   uint32_t i0, i1;
   chunk_range(sc->n_out, i0, i1);
@@ -123,6 +125,15 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
           if (w < cap) { m_src[w] = g; m_dst[w] = u; m_seq[w] = p * f.D + (k - k0); m_size[w] = size; m_t[w] = s_t[threadIdx.x]; }
           ++w;
         }
+      } else {  // one pass over the short row: where the sender sits, so a slot needs one row load
+        const uint32_t s = s_s[threadIdx.x];
+        uint32_t pos = k1 - k0, mult = 0;
+        for (uint32_t k = k0; k < k1; ++k) {
+          const bool hit = f.nbr[k] == s;
+          pos = hit && !mult ? k - k0 : pos;
+          mult += hit;
+        }
+        s_pos[threadIdx.x] = mult > 1 ? kMultiSender : pos;
       }
     }
     __syncthreads();
@@ -137,10 +148,15 @@ __global__ __launch_bounds__(kBlock) void k_flood_emit(const uint32_t* __restric
       const uint32_t d = lo_d, s = s_s[d], k0 = s_k0[d], k1 = s_k1[d];
       if (k1 - k0 > kWalkMax) continue;
       uint32_t r = j - s_off[d], k = k0;
-      for (; k < k1; ++k) {  // the r-th neighbour other than the sender (row order)
-        if (f.nbr[k] == s) continue;
-        if (r == 0) break;
-        --r;
+      const uint32_t pos = s_pos[d];
+      if (pos != kMultiSender) {  // the r-th neighbour other than the sender (row order)
+        k = k0 + r + (r >= pos ? 1u : 0u);
+      } else {
+        for (; k < k1; ++k) {
+          if (f.nbr[k] == s) continue;
+          if (r == 0) break;
+          --r;
+        }
       }
       const uint32_t w = run + j;
       if (w < cap) {
