@@ -690,8 +690,10 @@ static int route_copy(tgo_ctx* c, const tgsim_record* r) {
 
 /* ---- the netem queue limit -------------------------------------------------
  * Per sender, in enqueue order (t_send, seq, clone first), a copy enqueued at t is tail-dropped when
- * TGSIM_NETEM_LIMIT copies of that sender, enqueued before it, are still queued: departure d >= t.
- * Counted within a window: the copies pending at the window start (pend + those extracted now) and
+ * TGSIM_NETEM_LIMIT copies of that sender, enqueued before it, are still queued: departure d > t (a
+ * copy occupies the queue over [enqueue, departure): one leaving at t has left - a zero-delay packet
+ * is dequeued in the same dev_queue_xmit that enqueued it [EXT]). A copy still waiting for its HTB
+ * turn (netem time >= t, departure not yet known) counts as queued. Counted within a window: the copies pending at the window start (pend + those extracted now) and
  * those queued in this window. An extracted stage-A copy's departure comes from the HTB GCRA run in
  * (netem time, seq, clone first) order as the enqueue times pass it - the same recurrence, in the
  * same order, as the token bucket below. Obvious structures: two binary heaps per sender. */
@@ -778,7 +780,7 @@ static int sender_window(tgo_ctx* c, const size_t* ord, size_t a, size_t b, cons
     const size_t i = ord[k];
     const uint32_t dst = s->dst[i], seq = s->seq[i], size = s->size[i];
     const int64_t ts = s->t[i];
-    /* departures before ts: the GCRA over the queued copies whose netem time has passed */
+    /* departures up to ts: the GCRA over the queued copies whose netem time has passed */
     while (U->n && U->v[0].e < ts) {
       ou u = ou_pop(U);
       int64_t d = u.e > X ? u.e : X;
@@ -787,7 +789,7 @@ static int sender_window(tgo_ctx* c, const size_t* ord, size_t a, size_t b, cons
       X = nx > TB_CLAMP ? TB_CLAMP : nx;
       if (od_push(K, d)) return TGSIM_ENOMEM;
     }
-    while (K->n && K->v[0] < ts) od_pop(K);
+    while (K->n && K->v[0] <= ts) od_pop(K);
     uint32_t r0[4];
     draw(c, seq, src, 0, 0, r0);
     int count = 1;

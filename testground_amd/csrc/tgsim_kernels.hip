@@ -2333,7 +2333,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
           const int64_t ts = m.mt[k];
           const uint32_t size = m.msize[k];
           if (heavy) {
-            while (m.nu && m.ue[0] < ts) {  // departures before ts: HTB GCRA in k_tb_bucket's order
+            while (m.nu && m.ue[0] < ts) {  // departures up to ts: HTB GCRA in k_tb_bucket's order
               const int64_t e = m.ue[0];
               const uint32_t usz = m.us[0];
               --m.nu;
@@ -2344,7 +2344,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
               X = v > kTbClamp ? kTbClamp : v;
               k_push(m, dd, sc);
             }
-            while (m.nk && m.kd[0] < ts) {
+            while (m.nk && m.kd[0] <= ts) {  // a copy leaving at ts has left (occupancy [enqueue, d))
               --m.nk;
               if (m.nk) { m.kd[0] = m.kd[m.nk]; k_down(m, 0, m.nk); }
             }

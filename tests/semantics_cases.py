@@ -277,16 +277,16 @@ def case_queue_limit_burst(b):
 
 
 def case_queue_limit_spans_windows(b):
-    """Copies queued in earlier windows count until they depart; a copy departing at exactly t still
-    occupies the queue for an enqueue at t (departure >= t)."""
+    """Copies queued in earlier windows count until they depart; a copy departing at exactly t has
+    left the queue for an enqueue at t (occupancy over [enqueue, departure))."""
     s = sim(b)
     s.set_shape(0, make_shape(latency_ns=10 * MS))
     st, _ = one_window(s, np.zeros(1000, np.int64), 1, 10, 0, 5 * MS)
     assert list(st) == [A.ST_QUEUED] * 1000
     t = np.array([10 * MS - 1] * 10 + [10 * MS] * 10 + [10 * MS + 1] * 10)
     st, d = one_window(s, np.zeros(30, np.int64), 1, 10, t, 20 * MS, seq=np.arange(1000, 1030))
-    assert list(st) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 20 + [A.ST_QUEUED] * 10
-    assert len(d["seq"]) == 1000 and s.stats()["overlimit"] == 20
+    assert list(st) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 10 + [A.ST_QUEUED] * 20
+    assert len(d["seq"]) == 1000 and s.stats()["overlimit"] == 10
     s.close()
 
 
@@ -310,13 +310,13 @@ def case_queue_limit_duplicates(b):
 
 def case_queue_limit_token_bucket(b):
     """A limited sender's copies stay queued until the HTB lets them go: the queue admits exactly
-    as many new copies as have departed (departure < t) by the time they arrive."""
+    as many new copies as have departed (departure <= t) by the time they arrive."""
     s = sim(b)
     s.set_shape(0, make_shape(bandwidth_bps=8_000_000))   # 1000-B copies: 1 ms each
     st, d0 = one_window(s, np.zeros(1200, np.int64), 1, 1000, 0, 400 * MS)
     assert list(st) == [A.ST_QUEUED] * 1000 + [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * 200
     st, d1 = one_window(s, np.zeros(700, np.int64), 1, 1000, 500 * MS, 501 * MS, seq=np.arange(1200, 1900))
-    departed = int(np.count_nonzero(d0["t_deliver"] < 500 * MS)) + int(np.count_nonzero(d1["t_deliver"] < 500 * MS))
+    departed = int(np.count_nonzero(d0["t_deliver"] <= 500 * MS)) + int(np.count_nonzero(d1["t_deliver"] <= 500 * MS))
     assert 490 < departed < 510
     assert int(np.count_nonzero(st == A.ST_QUEUED)) == departed
     assert list(st[departed:]) == [A.ST_OVERLIMIT | A.ST_FLAG_OVERLIMIT] * (700 - departed)
