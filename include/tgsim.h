@@ -349,6 +349,10 @@ int tgsim_profile_set(tgsim_ctx* ctx, uint32_t mask);
 int tgsim_profile_read(tgsim_ctx* ctx, double* ms, uint64_t* launches, size_t cap, size_t* n);
 int tgsim_kernel_classes(void);
 const char* tgsim_kernel_name(int kernel_class);
+/* Test hook: the nth host allocation point from now (tgsim_add_rules, tgsim_flood_set_graph) throws
+ * std::bad_alloc inside the library; the entry point returns TGSIM_ENOMEM and the context stays
+ * usable (no C++ exception ever crosses this ABI). 0 disarms. */
+int tgsim_debug_fail_alloc(tgsim_ctx* ctx, uint32_t nth);
 
 /* ---- synthetic workloads (device generators) --------------------------------------- */
 /* Gossip storm round (config 4): every instance of this shard sends `fanout` messages of `size`

@@ -1246,6 +1246,7 @@ static void fl_seen_set(tgo_ctx* c, uint32_t p, uint32_t l) {
 int tgo_flood_set_graph(tgo_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
   if (!off || (off[c->N] && !nbr) || max_pubs == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   uint32_t D = 1;
   for (uint32_t g = 0; g < c->N; ++g) {
     if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
@@ -1313,6 +1314,7 @@ int tgo_flood_publish(tgo_ctx* c, const uint32_t* inst, const uint32_t* pubs, co
 int tgo_flood_react(tgo_ctx* c, uint32_t size, size_t* n_fwd) {
   if (!c->fl_off) return fail(c, TGSIM_ESTATE, "no flood graph");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   const orecs* o = &c->out;
   size_t cap = o->n * c->fl_D + 1, k = 0;
   uint32_t* src = malloc(cap * 4); uint32_t* dst = malloc(cap * 4); uint32_t* seq = malloc(cap * 4);
@@ -1424,6 +1426,7 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->staged.n) return fail(c, TGSIM_ESTATE, "messages already staged");
+  if (c->fl_off) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
   tgsim_tcp_config t = *cfg;
   if (!t.mss) t.mss = 1448;
   if (!t.header_bytes) t.header_bytes = 52;

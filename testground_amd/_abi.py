@@ -185,6 +185,7 @@ _SIGS_HIP = {
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "snapshot": (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "restore": (C.c_int, [P, C.c_void_p, C.c_size_t]),
+    "debug_fail_alloc": (C.c_int, [P, C.c_uint32]),
 }
 
 

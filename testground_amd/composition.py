@@ -24,11 +24,13 @@ Errors are ``ValueError`` with the reference's messages. A plan runs on ``local:
 manifest enables that runner (``[runners."local:mi355x"] enabled = true``)."""
 from __future__ import annotations
 
+import bisect
 import copy
 import json
 import math
 from dataclasses import dataclass, field, fields
 
+import numpy as np
 import tomli
 
 from .runner import LocalMI355XRunnerConfig, RunGroup, RunInput
@@ -112,7 +114,48 @@ def _run(d: dict | None) -> Run:
 
 
 def _strs(m):
-    return None if m is None else {str(k): str(v) for k, v in m.items()}
+    """A TOML table decoded into Go's map[string]string: a non-string value is a decoding error
+    there (BurntSushi/toml refuses to store an integer, float, boolean or table in a string)."""
+    if m is None:
+        return None
+    out = {}
+    for k, v in m.items():
+        if not isinstance(v, str):
+            raise ValueError(f"toml: cannot load TOML value of type {type(v).__name__} into a Go string "
+                             f"(key {k!r}); quote the value")
+        out[str(k)] = v
+    return out
+
+
+def _go_float(x: float) -> str:
+    """encoding/json's float64 text: the shortest round-trip digits, 'f' form for magnitudes in
+    [1e-6, 1e21) (so 1.0 is "1"), else 'e' form with at least two exponent digits ("1e+21")."""
+    if x != x or x in (float("inf"), float("-inf")):
+        raise ValueError(f"json: unsupported value: {x}")
+    if x == 0 or 1e-6 <= abs(x) < 1e21:
+        return np.format_float_positional(x, trim="-")
+    return np.format_float_scientific(x, trim="-", exp_digits=2)
+
+
+def _go_json(v) -> str:
+    """json.Marshal of a TOML-decoded interface{} value: map keys sorted, floats as Go prints them."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return _go_float(v)
+    if isinstance(v, str):
+        return json.dumps(v, ensure_ascii=False).replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+    if v is None:
+        return "null"
+    if isinstance(v, dict):
+        return "{" + ",".join(f"{_go_json(str(k))}:{_go_json(v[k])}" for k in sorted(v)) + "}"
+    if isinstance(v, (list, tuple)):
+        return "[" + ",".join(_go_json(x) for x in v) + "]"
+    if hasattr(v, "isoformat"):   # TOML datetimes: time.Time marshals as RFC 3339
+        return json.dumps(v.isoformat())
+    raise ValueError(f"json: unsupported type {type(v).__name__}")
 
 
 def parse_composition(text: str) -> Composition:
@@ -195,8 +238,10 @@ def prepare_for_run(c: Composition, manifest: Manifest) -> Composition:
     if not manifest.runners:
         raise ValueError("plan supports no runners; review the manifest")
     runners = sorted(manifest.runners)
-    if g.runner not in runners:
-        raise ValueError(f"plan does not support runner {g.runner}; supported: {runners}")
+    # sort.SearchStrings(runners, runner) == len(runners) (composition.go:444): the insertion index,
+    # so an unlisted runner that sorts before the last listed one passes this check, as it does there
+    if bisect.bisect_left(runners, g.runner) == len(runners):
+        raise ValueError(f"plan does not support runner {g.runner}; supported: [{' '.join(runners)}]")
     rcfg = manifest.runners.get(g.runner)
     if rcfg:
         g.run_config = dict(g.run_config or {})
@@ -220,7 +265,7 @@ def prepare_for_run(c: Composition, manifest: Manifest) -> Composition:
                 gr.run.artifact = g.run.artifact
             gr.run.test_params = trickle(g.run.test_params, gr.run.test_params)
             gr.run.profiles = trickle(g.run.profiles, gr.run.profiles)
-    defaults = {n: (p.default if isinstance(p.default, str) else json.dumps(p.default, separators=(",", ":")))
+    defaults = {n: (p.default if isinstance(p.default, str) else _go_json(p.default))
                 for n, p in tc.parameters.items()}
     for gr in c.groups:
         if gr.run.test_params is None:

@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -151,7 +152,14 @@ struct tgsim_ctx {
   size_t sub_cap = 0, sub_scan_bytes = 0;
   // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
   std::vector<uint32_t> fl_off, fl_nbr;
+  uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
 };
+
+// An allocation point of a host-side table (tgsim_debug_fail_alloc makes the chosen one throw, so
+// the tests can drive the ABI's bad_alloc path without exhausting memory).
+static void alloc_point(tgsim_ctx* c) {
+  if (c && c->fail_alloc && --c->fail_alloc == 0) throw std::bad_alloc();
+}
 
 // Commit a deferred storm batch before anything reads or reuses the sync state.
 static hipError_t flush_storm(tgsim_ctx* c) {
@@ -170,9 +178,30 @@ static int fail(tgsim_ctx* c, int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
-    c->err = buf;
+    try {
+      c->err = buf;
+    } catch (...) {  // no memory for the message: the code still reports the error
+      c->err.clear();
+    }
   }
   return code;
+}
+
+// Every int-returning entry point runs its body through this guard: nothing thrown by the host
+// side (std::vector / std::string growth, std::unordered_map) crosses extern "C" into a Go or
+// Python caller. An allocation failure is TGSIM_ENOMEM and leaves the context usable: the tables
+// are rebuilt into temporaries and swapped in only once complete.
+template <class F>
+static int abi_guard(tgsim_ctx* c, F&& body) noexcept {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    return fail(c, TGSIM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(c, TGSIM_EINVAL, "internal error: %s", e.what());
+  } catch (...) {
+    return fail(c, TGSIM_EINVAL, "internal error");
+  }
 }
 
 static int hipfail(tgsim_ctx* c, hipError_t e, const char* what) {
@@ -520,7 +549,11 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
 
 extern "C" const char* tgsim_last_error(const tgsim_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+static int tgsim_set_stream_body(tgsim_ctx* c, void* stream);
 extern "C" int tgsim_set_stream(tgsim_ctx* c, void* stream) {
+  return abi_guard(c, [&] { return tgsim_set_stream_body(c, stream); });
+}
+static int tgsim_set_stream_body(tgsim_ctx* c, void* stream) {
   if (!c) return TGSIM_EINVAL;
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   if (c->own_stream) (void)hipStreamDestroy(c->d.stream);
@@ -534,7 +567,11 @@ extern "C" int tgsim_set_stream(tgsim_ctx* c, void* stream) {
   return TGSIM_OK;
 }
 
+static int tgsim_shard_range_body(const tgsim_ctx* c, uint32_t* lo, uint32_t* hi);
 extern "C" int tgsim_shard_range(const tgsim_ctx* c, uint32_t* lo, uint32_t* hi) {
+  return abi_guard(const_cast<tgsim_ctx*>(c), [&] { return tgsim_shard_range_body(c, lo, hi); });
+}
+static int tgsim_shard_range_body(const tgsim_ctx* c, uint32_t* lo, uint32_t* hi) {
   if (!c) return TGSIM_EINVAL;
   *lo = c->lo;
   *hi = c->hi;
@@ -565,12 +602,20 @@ static int sync_and_check(tgsim_ctx* c) {
   return check_device_errors(c);
 }
 
+static int tgsim_sync_body(tgsim_ctx* c);
 extern "C" int tgsim_sync(tgsim_ctx* c) {
+  return abi_guard(c, [&] { return tgsim_sync_body(c); });
+}
+static int tgsim_sync_body(tgsim_ctx* c) {
   if (!c) return TGSIM_EINVAL;
   return sync_and_check(c);
 }
 
+static int tgsim_get_stats_body(tgsim_ctx* c, tgsim_stats* o);
 extern "C" int tgsim_get_stats(tgsim_ctx* c, tgsim_stats* o) {
+  return abi_guard(c, [&] { return tgsim_get_stats_body(c, o); });
+}
+static int tgsim_get_stats_body(tgsim_ctx* c, tgsim_stats* o) {
   if (!c || !o) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   const DevScalars& h = *c->d.h_sc;
@@ -592,13 +637,33 @@ extern "C" int tgsim_get_stats(tgsim_ctx* c, tgsim_stats* o) {
   return rc;
 }
 
+static int tgsim_profile_set_body(tgsim_ctx* c, uint32_t mask);
 extern "C" int tgsim_profile_set(tgsim_ctx* c, uint32_t mask) {
+  return abi_guard(c, [&] { return tgsim_profile_set_body(c, mask); });
+}
+static int tgsim_profile_set_body(tgsim_ctx* c, uint32_t mask) {
   if (!c) return TGSIM_EINVAL;
   c->d.prof.mask = mask;
   return TGSIM_OK;
 }
 
+// Test hook: the n-th host allocation point from now (add_rules, flood_set_graph) throws
+// std::bad_alloc, which the entry point must turn into TGSIM_ENOMEM with the context usable.
+static int tgsim_debug_fail_alloc_body(tgsim_ctx* c, uint32_t nth);
+extern "C" int tgsim_debug_fail_alloc(tgsim_ctx* c, uint32_t nth) {
+  return abi_guard(c, [&] { return tgsim_debug_fail_alloc_body(c, nth); });
+}
+static int tgsim_debug_fail_alloc_body(tgsim_ctx* c, uint32_t nth) {
+  if (!c) return TGSIM_EINVAL;
+  c->fail_alloc = nth;
+  return TGSIM_OK;
+}
+
+static int tgsim_profile_read_body(tgsim_ctx* c, double* ms, uint64_t* launches, size_t cap, size_t* n);
 extern "C" int tgsim_profile_read(tgsim_ctx* c, double* ms, uint64_t* launches, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_profile_read_body(c, ms, launches, cap, n); });
+}
+static int tgsim_profile_read_body(tgsim_ctx* c, double* ms, uint64_t* launches, size_t cap, size_t* n) {
   if (!c || !n) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   *n = KID_COUNT;
@@ -633,7 +698,11 @@ extern "C" int64_t tgsim_horizon(const tgsim_ctx* c) {
 
 static bool is_local(const tgsim_ctx* c, uint32_t g) { return g >= c->lo && g < c->hi; }
 
+static int tgsim_set_shape_body(tgsim_ctx* c, uint32_t g, const tgsim_link_shape* s);
 extern "C" int tgsim_set_shape(tgsim_ctx* c, uint32_t g, const tgsim_link_shape* s) {
+  return abi_guard(c, [&] { return tgsim_set_shape_body(c, g, s); });
+}
+static int tgsim_set_shape_body(tgsim_ctx* c, uint32_t g, const tgsim_link_shape* s) {
   if (!c || !s || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
   ShapeDev o;
   std::string e;
@@ -652,7 +721,11 @@ extern "C" int tgsim_set_shape(tgsim_ctx* c, uint32_t g, const tgsim_link_shape*
   return TGSIM_OK;
 }
 
+static int tgsim_set_shapes_body(tgsim_ctx* c, const uint32_t* inst, const tgsim_link_shape* shapes, size_t n);
 extern "C" int tgsim_set_shapes(tgsim_ctx* c, const uint32_t* inst, const tgsim_link_shape* shapes, size_t n) {
+  return abi_guard(c, [&] { return tgsim_set_shapes_body(c, inst, shapes, n); });
+}
+static int tgsim_set_shapes_body(tgsim_ctx* c, const uint32_t* inst, const tgsim_link_shape* shapes, size_t n) {
   if (!c || (n && (!inst || !shapes))) return fail(c, TGSIM_EINVAL, "bad arguments");
   for (size_t i = 0; i < n; ++i) {
     int rc = tgsim_set_shape(c, inst[i], &shapes[i]);
@@ -667,40 +740,81 @@ static bool rule_before(const RuleDev& a, uint32_t prefix, uint32_t plen) {
   return a.prefix < prefix;
 }
 
-// NetlinkLink.AddRules (link.go:187-217)
+// NetlinkLink.AddRules (link.go:187-217): the rules in order, each a RouteReplace (Drop, Reject) or
+// a RouteDel of both routes for exactly that prefix (Accept, errors ignored); the first invalid rule
+// returns its error with the earlier ones applied, as the reference's loop does. A batch is applied
+// as one sort + merge (the last rule per prefix wins): O(R log R + table), not O(R) per rule.
+static int tgsim_add_rules_body(tgsim_ctx* c, uint32_t g, const tgsim_link_rule* rules, size_t n);
 extern "C" int tgsim_add_rules(tgsim_ctx* c, uint32_t g, const tgsim_link_rule* rules, size_t n) {
+  return abi_guard(c, [&] { return tgsim_add_rules_body(c, g, rules, n); });
+}
+static int tgsim_add_rules_body(tgsim_ctx* c, uint32_t g, const tgsim_link_rule* rules, size_t n) {
   if (!c || g >= c->N || (n && !rules)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  struct Op { uint32_t prefix, plen, action, idx; };
+  std::vector<Op> ops;
+  int rc = TGSIM_OK;
+  const bool local = is_local(c, g);
+  if (local) ops.reserve(n);
   for (size_t i = 0; i < n; ++i) {
     const uint32_t plen = rules[i].prefix_len;
-    if (plen > 32) return fail(c, TGSIM_EINVAL, "invalid prefix length %u", plen);
+    if (plen > 32) { rc = fail(c, TGSIM_EINVAL, "invalid prefix length %u", plen); break; }
     const uint32_t mask = plen ? 0xFFFFFFFFu << (32 - plen) : 0u;
     const uint32_t prefix = rules[i].subnet_ip;
     const int action = rules[i].shape.filter;
-    if (action != TGSIM_FILTER_ACCEPT && action != TGSIM_FILTER_REJECT && action != TGSIM_FILTER_DROP)
-      return fail(c, TGSIM_EINVAL, "unknown filter action %d", action);
-    if (action != TGSIM_FILTER_ACCEPT && (prefix & ~mask))
-      return fail(c, TGSIM_EINVAL, "invalid prefix for given prefix length");
-    if (!is_local(c, g)) continue;
-    auto& v = c->rules_h[g - c->lo];
-    if (action == TGSIM_FILTER_ACCEPT) {  // RouteDel blackhole + prohibit, errors ignored
-      if (prefix & ~mask) continue;
-      auto it = std::lower_bound(v.begin(), v.end(), 0, [&](const RuleDev& r, int) { return rule_before(r, prefix, plen); });
-      if (it != v.end() && it->prefix == prefix && (it->plen_action & 0xFFu) == plen) {
-        v.erase(it);
-        c->rules_dirty = true;
-      }
-      continue;
+    if (action != TGSIM_FILTER_ACCEPT && action != TGSIM_FILTER_REJECT && action != TGSIM_FILTER_DROP) {
+      rc = fail(c, TGSIM_EINVAL, "unknown filter action %d", action);
+      break;
     }
-    auto it = std::lower_bound(v.begin(), v.end(), 0, [&](const RuleDev& r, int) { return rule_before(r, prefix, plen); });
-    const uint32_t pa = plen | ((uint32_t)action << 8);
-    if (it != v.end() && it->prefix == prefix && (it->plen_action & 0xFFu) == plen) it->plen_action = pa;  // RouteReplace
-    else v.insert(it, RuleDev{prefix, pa});
+    if (action != TGSIM_FILTER_ACCEPT && (prefix & ~mask)) {
+      rc = fail(c, TGSIM_EINVAL, "invalid prefix for given prefix length");
+      break;
+    }
+    if (!local) continue;
+    if (action == TGSIM_FILTER_ACCEPT && (prefix & ~mask)) continue;  // RouteDel finds nothing
+    ops.push_back(Op{prefix, plen, (uint32_t)action, (uint32_t)i});
+  }
+  if (ops.empty()) return rc;
+  alloc_point(c);
+  // table order (plen desc, prefix asc); within a key the batch order, so the last op is the one kept
+  std::sort(ops.begin(), ops.end(), [](const Op& a, const Op& b) {
+    if (a.plen != b.plen) return a.plen > b.plen;
+    if (a.prefix != b.prefix) return a.prefix < b.prefix;
+    return a.idx < b.idx;
+  });
+  auto& v = c->rules_h[g - c->lo];
+  std::vector<RuleDev> out;
+  out.reserve(v.size() + ops.size());
+  size_t j = 0;
+  bool changed = false;
+  for (size_t i = 0; i < ops.size();) {
+    size_t k = i;
+    while (k + 1 < ops.size() && ops[k + 1].plen == ops[i].plen && ops[k + 1].prefix == ops[i].prefix) ++k;
+    const Op& o = ops[k];  // the last rule for this prefix
+    while (j < v.size() && rule_before(v[j], o.prefix, o.plen)) out.push_back(v[j++]);
+    const bool present = j < v.size() && v[j].prefix == o.prefix && (v[j].plen_action & 0xFFu) == o.plen;
+    if (o.action == TGSIM_FILTER_ACCEPT) {
+      if (present) { ++j; changed = true; }
+    } else {
+      const uint32_t pa = o.plen | (o.action << 8);
+      if (present) ++j;
+      out.push_back(RuleDev{o.prefix, pa});
+      changed = true;
+    }
+    i = k + 1;
+  }
+  while (j < v.size()) out.push_back(v[j++]);
+  if (changed) {
+    v.swap(out);
     c->rules_dirty = true;
   }
-  return TGSIM_OK;
+  return rc;
 }
 
-extern "C" int tgsim_set_policy(tgsim_ctx* c, uint32_t g, int32_t policy) {  // route.go:102-117
+static int tgsim_set_policy_body(tgsim_ctx* c, uint32_t g, int32_t policy);
+extern "C" int tgsim_set_policy(tgsim_ctx* c, uint32_t g, int32_t policy) {
+  return abi_guard(c, [&] { return tgsim_set_policy_body(c, g, policy); });
+}
+static int tgsim_set_policy_body(tgsim_ctx* c, uint32_t g, int32_t policy) {  // route.go:102-117
   if (!c || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
   const uint8_t f = (uint8_t)((c->flags_h[g] & 1u) | (policy == TGSIM_POLICY_ALLOW_ALL ? 2u : 0u));
   if (f != c->flags_h[g]) { c->flags_h[g] = f; c->flags_dirty = true; }
@@ -729,7 +843,11 @@ static int set_ip(tgsim_ctx* c, uint32_t g, uint32_t ip) {
 }
 
 // docker_network.go:65-133: disconnect / (re)connect; a new link is a fresh HTB class + netem qdisc.
+static int tgsim_set_enabled_body(tgsim_ctx* c, uint32_t g, int32_t enabled, int32_t has_ip, uint32_t ip);
 extern "C" int tgsim_set_enabled(tgsim_ctx* c, uint32_t g, int32_t enabled, int32_t has_ip, uint32_t ip) {
+  return abi_guard(c, [&] { return tgsim_set_enabled_body(c, g, enabled, has_ip, ip); });
+}
+static int tgsim_set_enabled_body(tgsim_ctx* c, uint32_t g, int32_t enabled, int32_t has_ip, uint32_t ip) {
   if (!c || g >= c->N) return fail(c, TGSIM_EINVAL, "bad instance");
   uint8_t& f = c->flags_h[g];
   if (!enabled) {
@@ -753,7 +871,11 @@ extern "C" int tgsim_set_enabled(tgsim_ctx* c, uint32_t g, int32_t enabled, int3
   return TGSIM_OK;
 }
 
+static int tgsim_configure_network_body(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg);
 extern "C" int tgsim_configure_network(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg) {
+  return abi_guard(c, [&] { return tgsim_configure_network_body(c, g, cfg); });
+}
+static int tgsim_configure_network_body(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg) {
   if (!c || !cfg || g >= c->N) return fail(c, TGSIM_EINVAL, "bad arguments");
   const char* net = cfg->network ? cfg->network : "";
   if (strcmp(net, "default") != 0) return fail(c, TGSIM_EUNSUPPORTED_NETWORK, "unsupported network: %s", net);
@@ -768,7 +890,11 @@ extern "C" int tgsim_configure_network(tgsim_ctx* c, uint32_t g, const tgsim_net
 }
 
 // K8sNetwork.ConfigureNetwork, k8s_network.go:43-176: policy last, untouched by a disconnect.
+static int tgsim_configure_network_order_body(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg, int32_t order);
 extern "C" int tgsim_configure_network_order(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg, int32_t order) {
+  return abi_guard(c, [&] { return tgsim_configure_network_order_body(c, g, cfg, order); });
+}
+static int tgsim_configure_network_order_body(tgsim_ctx* c, uint32_t g, const tgsim_network_config* cfg, int32_t order) {
   if (order == TGSIM_APPLY_DOCKER) return tgsim_configure_network(c, g, cfg);
   if (!c || !cfg || g >= c->N || order != TGSIM_APPLY_K8S) return fail(c, TGSIM_EINVAL, "bad arguments");
   const char* net = cfg->network ? cfg->network : "";
@@ -783,7 +909,11 @@ extern "C" int tgsim_configure_network_order(tgsim_ctx* c, uint32_t g, const tgs
   return tgsim_set_policy(c, g, cfg->routing_policy);
 }
 
+static int tgsim_get_ip_body(const tgsim_ctx* c, uint32_t g, uint32_t* ip);
 extern "C" int tgsim_get_ip(const tgsim_ctx* c, uint32_t g, uint32_t* ip) {
+  return abi_guard(const_cast<tgsim_ctx*>(c), [&] { return tgsim_get_ip_body(c, g, ip); });
+}
+static int tgsim_get_ip_body(const tgsim_ctx* c, uint32_t g, uint32_t* ip) {
   if (!c || !ip || g >= c->N) return TGSIM_EINVAL;
   *ip = c->ip_h[g];
   return TGSIM_OK;
@@ -885,7 +1015,11 @@ static int validate_msgs(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
 }
 
 static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n);
+static int tgsim_enqueue_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n);
 extern "C" int tgsim_enqueue(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  return abi_guard(c, [&] { return tgsim_enqueue_body(c, m, n); });
+}
+static int tgsim_enqueue_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (c && c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
   return enqueue_host(c, m, n);
 }
@@ -940,7 +1074,11 @@ static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   return pin_issued(c, c->pin_msgs);
 }
 
+static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n);
 extern "C" int tgsim_enqueue_device(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  return abi_guard(c, [&] { return tgsim_enqueue_device_body(c, m, n); });
+}
+static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   c->spec.valid = false;  // staged arrays change: no speculative storm round
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
@@ -1050,7 +1188,11 @@ static int begin_common(tgsim_ctx* c) {
   return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
 
+static int tgsim_advance_begin_body(tgsim_ctx* c, int64_t t_end);
 extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
+  return abi_guard(c, [&] { return tgsim_advance_begin_body(c, t_end); });
+}
+static int tgsim_advance_begin_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
@@ -1067,7 +1209,11 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
   return TGSIM_OK;
 }
 
+static int tgsim_exchange_buffers_body(tgsim_ctx* c, void** send, void** recv, size_t* bytes);
 extern "C" int tgsim_exchange_buffers(tgsim_ctx* c, void** send, void** recv, size_t* bytes) {
+  return abi_guard(c, [&] { return tgsim_exchange_buffers_body(c, send, recv, bytes); });
+}
+static int tgsim_exchange_buffers_body(tgsim_ctx* c, void** send, void** recv, size_t* bytes) {
   if (!c || !send || !recv || !bytes) return TGSIM_EINVAL;
   *send = c->d.xsend;
   *recv = c->d.xrecv;
@@ -1075,7 +1221,11 @@ extern "C" int tgsim_exchange_buffers(tgsim_ctx* c, void** send, void** recv, si
   return TGSIM_OK;
 }
 
+static int tgsim_set_exchange_buffers_body(tgsim_ctx* c, void* send, void* recv, size_t bytes);
 extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, size_t bytes) {
+  return abi_guard(c, [&] { return tgsim_set_exchange_buffers_body(c, send, recv, bytes); });
+}
+static int tgsim_set_exchange_buffers_body(tgsim_ctx* c, void* send, void* recv, size_t bytes) {
   if (!c || !send || !recv) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   const size_t need = (size_t)c->S * c->d.xcap * sizeof(tgsim_record);
@@ -1086,7 +1236,11 @@ extern "C" int tgsim_set_exchange_buffers(tgsim_ctx* c, void* send, void* recv, 
   return TGSIM_OK;
 }
 
+static int tgsim_advance_begin_device_body(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns);
 extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
+  return abi_guard(c, [&] { return tgsim_advance_begin_device_body(c, t_end_dev, offset_ns); });
+}
+static int tgsim_advance_begin_device_body(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
   if (!c || !t_end_dev) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   HIPCK(c, flush_storm(c), "storm commit");
@@ -1094,7 +1248,11 @@ extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev
   return begin_common(c);
 }
 
+static int tgsim_advance_end_body(tgsim_ctx* c);
 extern "C" int tgsim_advance_end(tgsim_ctx* c) {
+  return abi_guard(c, [&] { return tgsim_advance_end_body(c); });
+}
+static int tgsim_advance_end_body(tgsim_ctx* c) {
   if (!c) return TGSIM_EINVAL;
   if (!c->in_window) return fail(c, TGSIM_ESTATE, "no open window");
   {
@@ -1154,7 +1312,11 @@ static int rccl_allgather(void* user, const void* send, void* recv, size_t bytes
   return ncclAllGather(send, recv, bytes, ncclUint8, c->comm, static_cast<hipStream_t>(stream)) == ncclSuccess ? 0 : -1;
 }
 
+static int tgsim_comm_unique_id_body(uint8_t out[TGSIM_COMM_ID_BYTES]);
 extern "C" int tgsim_comm_unique_id(uint8_t out[TGSIM_COMM_ID_BYTES]) {
+  return abi_guard(nullptr, [&] { return tgsim_comm_unique_id_body(out); });
+}
+static int tgsim_comm_unique_id_body(uint8_t out[TGSIM_COMM_ID_BYTES]) {
   static_assert(sizeof(ncclUniqueId) == TGSIM_COMM_ID_BYTES, "RCCL unique id size");
   if (!out) return TGSIM_EINVAL;
   ncclUniqueId id;
@@ -1163,7 +1325,11 @@ extern "C" int tgsim_comm_unique_id(uint8_t out[TGSIM_COMM_ID_BYTES]) {
   return TGSIM_OK;
 }
 
+static int tgsim_comm_init_body(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank);
 extern "C" int tgsim_comm_init(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank) {
+  return abi_guard(c, [&] { return tgsim_comm_init_body(c, id, nranks, rank); });
+}
+static int tgsim_comm_init_body(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYTES], uint32_t nranks, uint32_t rank) {
   if (!c || !id) return TGSIM_EINVAL;
   if (nranks != c->S || rank != c->shard) return fail(c, TGSIM_EINVAL, "communicator rank %u/%u != shard %u/%u", rank, nranks, c->shard, c->S);
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
@@ -1181,7 +1347,11 @@ extern "C" int tgsim_comm_init(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYTE
   return TGSIM_OK;
 }
 
+static int tgsim_set_transport_body(tgsim_ctx* c, const tgsim_transport* t);
 extern "C" int tgsim_set_transport(tgsim_ctx* c, const tgsim_transport* t) {
+  return abi_guard(c, [&] { return tgsim_set_transport_body(c, t); });
+}
+static int tgsim_set_transport_body(tgsim_ctx* c, const tgsim_transport* t) {
   if (!c) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (t && (!t->alltoall || !t->allreduce_max_i64 || !t->allgather)) return fail(c, TGSIM_EINVAL, "incomplete transport");
@@ -1205,7 +1375,11 @@ static int need_transport(tgsim_ctx* c) {
   return TGSIM_OK;
 }
 
+static int tgsim_advance_body(tgsim_ctx* c, int64_t t_end);
 extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
+  return abi_guard(c, [&] { return tgsim_advance_body(c, t_end); });
+}
+static int tgsim_advance_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
   int rc = need_transport(c);
   if (rc) return rc;
@@ -1220,7 +1394,11 @@ extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
   return sync_and_check(c);  // the host-driven API reports the window's errors here
 }
 
+static int tgsim_advance_async_body(tgsim_ctx* c, int64_t t_end);
 extern "C" int tgsim_advance_async(tgsim_ctx* c, int64_t t_end) {
+  return abi_guard(c, [&] { return tgsim_advance_async_body(c, t_end); });
+}
+static int tgsim_advance_async_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
   int rc = need_transport(c);
   if (rc) return rc;
@@ -1233,7 +1411,11 @@ extern "C" int tgsim_advance_async(tgsim_ctx* c, int64_t t_end) {
   return tgsim_advance_end(c);
 }
 
+static int tgsim_advance_to_barrier_body(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns);
 extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
+  return abi_guard(c, [&] { return tgsim_advance_to_barrier_body(c, waiter, offset_ns); });
+}
+static int tgsim_advance_to_barrier_body(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
   if (!c) return TGSIM_EINVAL;
   int rc0 = need_transport(c);
   if (rc0) return rc0;
@@ -1258,14 +1440,22 @@ extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t o
   return tgsim_advance_end(c);
 }
 
+static int tgsim_delivery_count_body(tgsim_ctx* c, size_t* n);
 extern "C" int tgsim_delivery_count(tgsim_ctx* c, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_delivery_count_body(c, n); });
+}
+static int tgsim_delivery_count_body(tgsim_ctx* c, size_t* n) {
   if (!c || !n) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   *n = c->d.h_sc->n_out;
   return rc;
 }
 
+static int tgsim_copy_deliveries_body(tgsim_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n);
 extern "C" int tgsim_copy_deliveries(tgsim_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_copy_deliveries_body(c, o, cap, n); });
+}
+static int tgsim_copy_deliveries_body(tgsim_ctx* c, tgsim_delivery_soa* o, size_t cap, size_t* n) {
   if (!c || !o || !n) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   if (rc) return rc;
@@ -1284,7 +1474,11 @@ extern "C" int tgsim_copy_deliveries(tgsim_ctx* c, tgsim_delivery_soa* o, size_t
   return TGSIM_OK;
 }
 
+static int tgsim_copy_inbox_offsets_body(tgsim_ctx* c, uint32_t* out, size_t cap);
 extern "C" int tgsim_copy_inbox_offsets(tgsim_ctx* c, uint32_t* out, size_t cap) {
+  return abi_guard(c, [&] { return tgsim_copy_inbox_offsets_body(c, out, cap); });
+}
+static int tgsim_copy_inbox_offsets_body(tgsim_ctx* c, uint32_t* out, size_t cap) {
   if (!c || !out) return TGSIM_EINVAL;
   if (cap < (size_t)c->nloc + 1) return fail(c, TGSIM_ECAPACITY, "inbox capacity");
   int rc = sync_and_check(c);
@@ -1293,7 +1487,11 @@ extern "C" int tgsim_copy_inbox_offsets(tgsim_ctx* c, uint32_t* out, size_t cap)
   return TGSIM_OK;
 }
 
+static int tgsim_copy_status_body(tgsim_ctx* c, uint8_t* out, size_t cap, size_t* n);
 extern "C" int tgsim_copy_status(tgsim_ctx* c, uint8_t* out, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_copy_status_body(c, out, cap, n); });
+}
+static int tgsim_copy_status_body(tgsim_ctx* c, uint8_t* out, size_t cap, size_t* n) {
   if (!c || !n) return TGSIM_EINVAL;
   int rc = sync_and_check(c);
   if (rc) return rc;
@@ -1304,7 +1502,11 @@ extern "C" int tgsim_copy_status(tgsim_ctx* c, uint8_t* out, size_t cap, size_t*
   return TGSIM_OK;
 }
 
+static int tgsim_deliveries_device_body(tgsim_ctx* c, tgsim_delivery_soa* o);
 extern "C" int tgsim_deliveries_device(tgsim_ctx* c, tgsim_delivery_soa* o) {
+  return abi_guard(c, [&] { return tgsim_deliveries_device_body(c, o); });
+}
+static int tgsim_deliveries_device_body(tgsim_ctx* c, tgsim_delivery_soa* o) {
   if (!c || !o) return TGSIM_EINVAL;
   Dev& d = c->d;
   o->t_deliver = d.o_t; o->src = d.o_src; o->dst = d.o_dst; o->seq = d.o_seq; o->size = d.o_size;
@@ -1381,7 +1583,13 @@ static int signal_gathered(tgsim_ctx* c, const uint32_t* states, const uint32_t*
   return TGSIM_OK;
 }
 
+static int tgsim_sync_signal_body(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                                 size_t n, uint32_t* seq_out);
 extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                                 size_t n, uint32_t* seq_out) {
+  return abi_guard(c, [&] { return tgsim_sync_signal_body(c, states, inst, t, n, seq_out); });
+}
+static int tgsim_sync_signal_body(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                                  size_t n, uint32_t* seq_out) {
   if (!c || (n && (!states || !inst || !t))) return TGSIM_EINVAL;
   c->spec.valid = false;  // signal partials change: no speculative storm round
@@ -1418,7 +1626,11 @@ static int signal_local(tgsim_ctx* c, const uint32_t* states, const uint32_t* in
   return sync_and_check(c);
 }
 
+static int tgsim_sync_barrier_body(tgsim_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w);
 extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w) {
+  return abi_guard(c, [&] { return tgsim_sync_barrier_body(c, state, target, t_wait, w); });
+}
+static int tgsim_sync_barrier_body(tgsim_ctx* c, uint32_t state, uint32_t target, int64_t t_wait, uint32_t* w) {
   if (!c || !w) return TGSIM_EINVAL;
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "state id %u >= max_states", state);
   if (c->n_waiters >= c->d.max_waiters) return fail(c, TGSIM_ECAPACITY, "too many barrier waiters");
@@ -1441,7 +1653,11 @@ extern "C" int tgsim_sync_barrier(tgsim_ctx* c, uint32_t state, uint32_t target,
   return TGSIM_OK;
 }
 
+static int tgsim_sync_poll_body(tgsim_ctx* c, uint32_t w, int64_t* rel);
 extern "C" int tgsim_sync_poll(tgsim_ctx* c, uint32_t w, int64_t* rel) {
+  return abi_guard(c, [&] { return tgsim_sync_poll_body(c, w, rel); });
+}
+static int tgsim_sync_poll_body(tgsim_ctx* c, uint32_t w, int64_t* rel) {
   if (!c || !rel) return TGSIM_EINVAL;
   if (w >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
   HIPCK(c, flush_storm(c), "storm commit");
@@ -1449,7 +1665,11 @@ extern "C" int tgsim_sync_poll(tgsim_ctx* c, uint32_t w, int64_t* rel) {
   return sync_and_check(c);
 }
 
+static int tgsim_sync_count_body(tgsim_ctx* c, uint32_t state, uint32_t* count);
 extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
+  return abi_guard(c, [&] { return tgsim_sync_count_body(c, state, count); });
+}
+static int tgsim_sync_count_body(tgsim_ctx* c, uint32_t state, uint32_t* count) {
   if (!c || !count) return TGSIM_EINVAL;
   if (state >= c->d.max_states) return fail(c, TGSIM_EINVAL, "bad state");
   HIPCK(c, flush_storm(c), "storm commit");
@@ -1461,7 +1681,13 @@ extern "C" int tgsim_sync_count(tgsim_ctx* c, uint32_t state, uint32_t* count) {
 
 static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size, int64_t spread_ns,
                           uint32_t state);
+static int tgsim_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                     int64_t spread_ns, uint32_t state);
 extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                     int64_t spread_ns, uint32_t state) {
+  return abi_guard(c, [&] { return tgsim_gen_storm_round_body(c, round, t0, fanout, size, spread_ns, state); });
+}
+static int tgsim_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {
   if (c && c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_gen_storm_round");
   return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state);
@@ -1524,7 +1750,11 @@ static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fan
   return TGSIM_OK;
 }
 
+static int tgsim_storm_release_device_body(tgsim_ctx* c, int64_t* out);
 extern "C" int tgsim_storm_release_device(tgsim_ctx* c, int64_t* out) {
+  return abi_guard(c, [&] { return tgsim_storm_release_device_body(c, out); });
+}
+static int tgsim_storm_release_device_body(tgsim_ctx* c, int64_t* out) {
   if (!c || !out) return TGSIM_EINVAL;
   if (c->S == 1) return fail(c, TGSIM_ESTATE, "single-shard storms commit their signals: use a barrier");
   HIPCK(c, hipMemcpyAsync(out, c->d.sig_red + 3, sizeof(int64_t), hipMemcpyDeviceToDevice, c->d.stream), "release");
@@ -1535,9 +1765,16 @@ extern "C" int tgsim_storm_release_device(tgsim_ctx* c, int64_t* out) {
 // publications flood a fixed graph with first-receipt dedup. The oracle
 // twin is oracle/tgsim_oracle.c tgo_flood_*; kernels in tgsim_flood.hip.
 
+static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs);
 extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
+  return abi_guard(c, [&] { return tgsim_flood_set_graph_body(c, off, nbr, max_pubs); });
+}
+static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
   if (!c || !off || (off[c->N] && !nbr) || max_pubs == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  // a flood reaction reads deliveries as publications (seq / D): TCP packets (seq = segment << 4 |
+  // attempt) would be forwarded as floods and corrupt the TCP state
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   uint32_t D = 1;
   for (uint32_t g = 0; g < c->N; ++g) {
     if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
@@ -1548,14 +1785,18 @@ extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const ui
       if (nbr[k] >= c->N || nbr[k] == g) return fail(c, TGSIM_EINVAL, "bad neighbour of %u", g);
   }
   if ((uint64_t)max_pubs * D > 0x100000000ull) return fail(c, TGSIM_EINVAL, "max_pubs * degree > 2^32");
+  // host rows first (the only host allocations): a failure here leaves the previous graph intact
+  const uint32_t base = off[c->lo], m = off[c->hi] - base;
+  alloc_point(c);
+  std::vector<uint32_t> rows_off(c->nloc + 1), rows_nbr(nbr + base, nbr + base + m);
+  for (uint32_t l = 0; l <= c->nloc; ++l) rows_off[l] = off[c->lo + l] - base;
+  std::vector<uint8_t> pub_seen(max_pubs, 0);
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   Flood& f = c->d.fl;
   dfree(c, f.off); dfree(c, f.nbr); dfree(c, f.seen);
   f.off = f.nbr = f.seen = nullptr;
-  const uint32_t base = off[c->lo], m = off[c->hi] - base;
-  c->fl_off.resize(c->nloc + 1);
-  for (uint32_t l = 0; l <= c->nloc; ++l) c->fl_off[l] = off[c->lo + l] - base;
-  c->fl_nbr.assign(nbr + base, nbr + base + m);
+  c->fl_off.swap(rows_off);
+  c->fl_nbr.swap(rows_nbr);
   f.D = D; f.max_pubs = max_pubs; f.wpp = (c->nloc + 31) / 32;
   const size_t words = (size_t)max_pubs * f.wpp;
   if (dalloc(c, &f.off, c->nloc + 1) || dalloc(c, &f.nbr, std::max<size_t>(m, 1)) || dalloc(c, &f.seen, words))
@@ -1569,12 +1810,18 @@ extern "C" int tgsim_flood_set_graph(tgsim_ctx* c, const uint32_t* off, const ui
       return TGSIM_ENOMEM;
     f.cap = cap;
   }
-  c->fl_pub_seen.assign(max_pubs, 0);
+  c->fl_pub_seen.swap(pub_seen);
   c->fl_npubs = 0;
   return TGSIM_OK;
 }
 
+static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
+                                   size_t n, uint32_t size);
 extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
+                                   size_t n, uint32_t size) {
+  return abi_guard(c, [&] { return tgsim_flood_publish_body(c, inst, pubs, t, n, size); });
+}
+static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
                                    size_t n, uint32_t size) {
   if (!c) return TGSIM_EINVAL;
   c->spec.valid = false;
@@ -1617,13 +1864,18 @@ extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uin
   return pin_issued(c, c->pin_marks);
 }
 
+static int tgsim_flood_react_body(tgsim_ctx* c, uint32_t size, size_t* n_fwd);
 extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
+  return abi_guard(c, [&] { return tgsim_flood_react_body(c, size, n_fwd); });
+}
+static int tgsim_flood_react_body(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   if (!c) return TGSIM_EINVAL;
   c->spec.valid = false;
   if (n_fwd) *n_fwd = 0;
   Flood& f = c->d.fl;
   if (!f.off) return fail(c, TGSIM_ESTATE, "no flood graph");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   // asynchronous: the delivery count, the forwards and the new staged count stay on the device
   HIPCK(c, launch_flood_react(c->d, c->staged_dev, c->n_staged, size, c->horizon), "flood react");
   c->staged_dev = true;
@@ -1652,7 +1904,13 @@ static int dgrow(tgsim_ctx* c, T** p, uint64_t used, uint64_t need_cap) {
   return TGSIM_OK;
 }
 
+static int tgsim_sync_publish_body(tgsim_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
+                                  const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out);
 extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
+                                  const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out) {
+  return abi_guard(c, [&] { return tgsim_sync_publish_body(c, topics, inst, t, off, payload, n, pos_out); });
+}
+static int tgsim_sync_publish_body(tgsim_ctx* c, const uint32_t* topics, const uint32_t* inst, const int64_t* t,
                                   const uint64_t* off, const uint8_t* payload, size_t n, uint32_t* pos_out) {
   if (!c) return TGSIM_EINVAL;
   c->spec.valid = false;  // signal partials change: no speculative storm round
@@ -1718,7 +1976,15 @@ extern "C" int tgsim_sync_publish(tgsim_ctx* c, const uint32_t* topics, const ui
   return TGSIM_OK;
 }
 
+static int tgsim_sync_subscribe_body(tgsim_ctx* c, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                                    uint32_t* inst_out, int64_t* t_out, uint64_t* off_out, uint8_t* payload_out,
+                                    size_t payload_cap, size_t* n_out, size_t* payload_bytes);
 extern "C" int tgsim_sync_subscribe(tgsim_ctx* c, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
+                                    uint32_t* inst_out, int64_t* t_out, uint64_t* off_out, uint8_t* payload_out,
+                                    size_t payload_cap, size_t* n_out, size_t* payload_bytes) {
+  return abi_guard(c, [&] { return tgsim_sync_subscribe_body(c, topic, from, until_t, cap, inst_out, t_out, off_out, payload_out, payload_cap, n_out, payload_bytes); });
+}
+static int tgsim_sync_subscribe_body(tgsim_ctx* c, uint32_t topic, uint32_t from, int64_t until_t, size_t cap,
                                     uint32_t* inst_out, int64_t* t_out, uint64_t* off_out, uint8_t* payload_out,
                                     size_t payload_cap, size_t* n_out, size_t* payload_bytes) {
   if (!c || !n_out || !payload_bytes || from == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
@@ -1803,7 +2069,15 @@ static int upload_topic_index(tgsim_ctx* c) {
   return TGSIM_OK;
 }
 
+static int tgsim_sync_subscribe_device_body(tgsim_ctx* c, size_t n, const uint32_t* topics, const uint32_t* from,
+                                           const int64_t* until_t, uint32_t cap_each, uint64_t* offsets_out,
+                                           uint32_t* entries_out, size_t entries_cap);
 extern "C" int tgsim_sync_subscribe_device(tgsim_ctx* c, size_t n, const uint32_t* topics, const uint32_t* from,
+                                           const int64_t* until_t, uint32_t cap_each, uint64_t* offsets_out,
+                                           uint32_t* entries_out, size_t entries_cap) {
+  return abi_guard(c, [&] { return tgsim_sync_subscribe_device_body(c, n, topics, from, until_t, cap_each, offsets_out, entries_out, entries_cap); });
+}
+static int tgsim_sync_subscribe_device_body(tgsim_ctx* c, size_t n, const uint32_t* topics, const uint32_t* from,
                                            const int64_t* until_t, uint32_t cap_each, uint64_t* offsets_out,
                                            uint32_t* entries_out, size_t entries_cap) {
   if (!c || !offsets_out || (n && (!topics || !from || !until_t))) return fail(c, TGSIM_EINVAL, "bad arguments");
@@ -1834,7 +2108,13 @@ extern "C" int tgsim_sync_subscribe_device(tgsim_ctx* c, size_t n, const uint32_
   return TGSIM_OK;
 }
 
+static int tgsim_topic_arena_device_body(tgsim_ctx* c, const uint32_t** inst, const int64_t** t, const uint64_t** off,
+                                        const uint32_t** len, const uint8_t** payload, size_t* n);
 extern "C" int tgsim_topic_arena_device(tgsim_ctx* c, const uint32_t** inst, const int64_t** t, const uint64_t** off,
+                                        const uint32_t** len, const uint8_t** payload, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_topic_arena_device_body(c, inst, t, off, len, payload, n); });
+}
+static int tgsim_topic_arena_device_body(tgsim_ctx* c, const uint32_t** inst, const int64_t** t, const uint64_t** off,
                                         const uint32_t** len, const uint8_t** payload, size_t* n) {
   if (!c) return TGSIM_EINVAL;
   if (inst) *inst = c->tp_inst;
@@ -1857,11 +2137,16 @@ __global__ void k_fill_i64(int64_t* p, size_t n, int64_t v) {
 }
 }  // namespace
 
+static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg);
 extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
+  return abi_guard(c, [&] { return tgsim_tcp_enable_body(c, cfg); });
+}
+static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (!c || !cfg) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "messages already staged");
+  if (!c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
   tgsim_tcp_config t = *cfg;
   if (!t.mss) t.mss = 1448;
   if (!t.header_bytes) t.header_bytes = 52;
@@ -1916,7 +2201,11 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   return TGSIM_OK;
 }
 
+static int tgsim_tcp_send_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n);
 extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  return abi_guard(c, [&] { return tgsim_tcp_send_body(c, m, n); });
+}
+static int tgsim_tcp_send_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   c->spec.valid = false;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
@@ -1950,8 +2239,13 @@ extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
       p_src[k] = m->src[i]; p_dst[k] = m->dst[i]; p_seq[k] = sid << 4; p_size[k] = pay + c->tcp.header_bytes;
     }
   }
+  // the packets first: enqueue_host's capacity and validation checks decide whether the writes
+  // exist, so the tables below are uploaded only for writes the host counts
+  tgsim_msg_soa p{p_src.data(), p_dst.data(), p_seq.data(), p_size.data(), s_t.data()};
+  int rc = enqueue_host(c, &p, nseg);
+  if (rc) return rc;
   uint8_t* pin = nullptr;
-  int rc = pin_acquire(c, c->pin_tcp, 12 * n + 16 * nseg, &pin);
+  rc = pin_acquire(c, c->pin_tcp, 12 * n + 16 * nseg, &pin);
   if (rc) return rc;
   memcpy(pin, s_t.data(), 8 * nseg);
   memcpy(pin + 8 * nseg, w3.data(), 12 * n);
@@ -1968,9 +2262,6 @@ extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   HIPCK(c, hipMemcpyAsync(d.s_wire + c->tsg_n, ps + 4 * nseg, 4 * nseg, hipMemcpyHostToDevice, st), "tcp send");
   rc = pin_issued(c, c->pin_tcp);
   if (rc) return rc;
-  tgsim_msg_soa p{p_src.data(), p_dst.data(), p_seq.data(), p_size.data(), s_t.data()};
-  rc = enqueue_host(c, &p, nseg);
-  if (rc) return rc;
   c->tw_n += n;
   c->tsg_n += nseg;
   c->tstats.writes += n;
@@ -1981,7 +2272,11 @@ extern "C" int tgsim_tcp_send(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
 
 static int tcp_refresh(tgsim_ctx* c);
 
+static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done);
 extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
+  return abi_guard(c, [&] { return tgsim_tcp_react_body(c, n_done); });
+}
+static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   if (n_done) *n_done = 0;
   if (!c) return TGSIM_EINVAL;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
@@ -2031,7 +2326,11 @@ static int tcp_refresh(tgsim_ctx* c) {
   return TGSIM_OK;
 }
 
+static int tgsim_tcp_writes_body(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n);
 extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_tcp_writes_body(c, state, t, cap, n); });
+}
+static int tgsim_tcp_writes_body(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n) {
   if (!c || !n) return TGSIM_EINVAL;
   *n = c->tw_n;
   if (!c->tcp_on) return TGSIM_OK;
@@ -2063,7 +2362,11 @@ extern "C" int tgsim_tcp_writes(tgsim_ctx* c, uint8_t* state, int64_t* t, size_t
   return TGSIM_OK;
 }
 
+static int tgsim_tcp_get_stats_body(tgsim_ctx* c, tgsim_tcp_stats* out);
 extern "C" int tgsim_tcp_get_stats(tgsim_ctx* c, tgsim_tcp_stats* out) {
+  return abi_guard(c, [&] { return tgsim_tcp_get_stats_body(c, out); });
+}
+static int tgsim_tcp_get_stats_body(tgsim_ctx* c, tgsim_tcp_stats* out) {
   if (!c || !out) return TGSIM_EINVAL;
   if (c->tcp_on && (c->tcp_snap_live[0] || c->tcp_snap_live[1])) {  // an asynchronous reaction: its counters
     int rc = sync_and_check(c);
@@ -2075,7 +2378,13 @@ extern "C" int tgsim_tcp_get_stats(tgsim_ctx* c, tgsim_tcp_stats* out) {
   return TGSIM_OK;
 }
 
+static int tgsim_tcp_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                         int64_t spread_ns, uint32_t state);
 extern "C" int tgsim_tcp_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
+                                         int64_t spread_ns, uint32_t state) {
+  return abi_guard(c, [&] { return tgsim_tcp_gen_storm_round_body(c, round, t0, fanout, size, spread_ns, state); });
+}
+static int tgsim_tcp_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                          int64_t spread_ns, uint32_t state) {
   if (!c) return TGSIM_EINVAL;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
@@ -2213,7 +2522,11 @@ int snap_refusal(tgsim_ctx* c) {
 
 }  // namespace
 
+static int tgsim_snapshot_body(tgsim_ctx* c, void* buf, size_t cap, size_t* n);
 extern "C" int tgsim_snapshot(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_snapshot_body(c, buf, cap, n); });
+}
+static int tgsim_snapshot_body(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
   if (!c || !n) return TGSIM_EINVAL;
   int rc = snap_refusal(c);
   if (rc) return rc;
@@ -2240,7 +2553,11 @@ extern "C" int tgsim_snapshot(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
   return TGSIM_OK;
 }
 
+static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n);
 extern "C" int tgsim_restore(tgsim_ctx* c, const void* buf, size_t n) {
+  return abi_guard(c, [&] { return tgsim_restore_body(c, buf, n); });
+}
+static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   if (!c || !buf) return TGSIM_EINVAL;
   c->spec = tgsim_ctx::StormSpec{};
   int rc = snap_refusal(c);

@@ -143,6 +143,25 @@ def case_rules_longest_prefix(b):
     s.close()
 
 
+def case_rules_batch_order(b):
+    """AddRules applies a batch in order (link.go:187-217): the last rule for a prefix wins within
+    the batch (Drop then Accept deletes, Accept then Reject installs), and the first invalid rule
+    stops the batch with the earlier rules applied."""
+    s = sim(b, n=8)
+    from testground_amd.network import int_to_ip
+    ip = [int_to_ip(s.get_ip(g)) + "/32" for g in range(8)]
+    s.add_rules(0, [make_rule(ip[1], A.FILTER_DROP), make_rule(ip[2], A.FILTER_ACCEPT), make_rule(ip[1], A.FILTER_ACCEPT),
+                    make_rule(ip[2], A.FILTER_REJECT), make_rule(ip[3], A.FILTER_REJECT), make_rule(ip[3], A.FILTER_DROP)])
+    st, _ = one_window(s, [0, 0, 0, 0], [1, 2, 3, 4], 10, 0, 1 * MS)
+    assert list(st) == [A.ST_QUEUED, A.ST_REJECTED, A.ST_DROPPED, A.ST_QUEUED]
+    with pytest.raises(A.TgsimError) as e:
+        s.add_rules(0, [make_rule(ip[4], A.FILTER_DROP), make_rule(ip[5], 7), make_rule(ip[6], A.FILTER_DROP)])
+    assert e.value.code == A.EINVAL
+    st, _ = one_window(s, [0, 0, 0], [4, 5, 6], 10, 1 * MS, 2 * MS, seq=[4, 5, 6])
+    assert list(st) == [A.ST_DROPPED, A.ST_QUEUED, A.ST_QUEUED]
+    s.close()
+
+
 def case_policy_and_external(b):
     s = sim(b)
     s.set_policy(1, A.POLICY_ALLOW_ALL)

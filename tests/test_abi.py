@@ -19,7 +19,9 @@ HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_sha
             "tgsim_sync_subscribe_device", "tgsim_topic_arena_device",
             # checkpoint / resume is a runtime facility of the product library; the oracle's run is the
             # uninterrupted reference a restored run is compared with (tests/test_snapshot.py)
-            "tgsim_snapshot", "tgsim_restore"}
+            "tgsim_snapshot", "tgsim_restore",
+            # allocation-failure injection into the library's C++ host tables (no C++ in the oracle)
+            "tgsim_debug_fail_alloc"}
 
 
 def test_header_declares_expected_surface():

@@ -155,10 +155,16 @@ param6 = { type = "bool", default = true }
 
 def test_prepare_refusals():
     m = CP.parse_manifest(MANIFEST)
-    c = CP.parse_composition(STORM.replace('runner = "local:mi355x"', 'runner = "cluster:k8s"'))
+    c = CP.parse_composition(STORM.replace('runner = "local:mi355x"', 'runner = "local:zzz"'))
     CP.validate_for_run(c)
-    with pytest.raises(ValueError, match=r"plan does not support runner cluster:k8s; supported: \['local:docker', 'local:mi355x'\]"):
+    with pytest.raises(ValueError, match=r"plan does not support runner local:zzz; supported: \[local:docker local:mi355x\]"):
         CP.prepare_for_run(c, m)
+    # sort.SearchStrings returns the insertion index (composition.go:444): an unlisted runner that
+    # sorts before the last listed one passes the check, exactly as in the reference
+    for runner in ("cluster:k8s", "local:exec"):
+        c = CP.parse_composition(STORM.replace('runner = "local:mi355x"', f'runner = "{runner}"'))
+        CP.validate_for_run(c)
+        assert CP.prepare_for_run(c, m).global_.runner == runner
     c = CP.parse_composition(STORM.replace('case = "storm"', 'case = "nope"'))
     CP.validate_for_run(c)
     with pytest.raises(ValueError, match="test case nope not found in plan benchmarks"):
@@ -217,3 +223,23 @@ def test_composition_runs_on_the_hip_runner(hip):
     job = CP.to_run_input(CP.prepare_for_run(c, CP.parse_manifest(MANIFEST)), "storm-run-hip")
     res = LocalMI355XRunner(binding=hip).run(job, io.StringIO())
     assert res.result.outcome == OUTCOME_SUCCESS
+
+
+def test_test_params_are_strings_as_in_go():
+    """[groups.run.test_params] decodes into map[string]string: an unquoted value is an error."""
+    with pytest.raises(ValueError, match="cannot load TOML value"):
+        CP.parse_composition(STORM.replace('role = "dialer"', 'role = "dialer"\n  verbose = true'))
+
+
+@pytest.mark.parametrize("value,text", [(10, "10"), (1.0, "1"), (1.5, "1.5"), (True, "true"), (0.1, "0.1"),
+                                        (1e21, "1e+21"), (1e-7, "1e-07"), (123456789.0, "123456789"),
+                                        ({"b": 1, "a": [1, 2.0]}, '{"a":[1,2],"b":1}'), ("x", "x")])
+def test_manifest_defaults_marshal_like_go(value, text):
+    """PrepareForRun JSON-encodes non-string defaults with encoding/json (composition.go:508-517):
+    integral floats without a fraction, exponents in Go's form, map keys sorted."""
+    m = CP.parse_manifest(MANIFEST)
+    tc = m.test_case("storm")
+    tc.parameters = {"p": CP.Parameter(type="x", default=value)}
+    c = CP.parse_composition(STORM)
+    CP.validate_for_run(c)
+    assert CP.prepare_for_run(c, m).groups[0].run.test_params["p"] == text

@@ -105,6 +105,19 @@ def _errors(binding):
     with pytest.raises(A.TgsimError) as e:
         sim.flood_react(64)
     assert e.value.code == A.EINVAL
+    with pytest.raises(A.TgsimError) as e:                 # floods and TCP mode exclude each other
+        sim.tcp_enable()
+    assert e.value.code == A.ESTATE
+    sim.close()
+    # ... in the other order too: a TCP context refuses a graph and a reaction
+    sim = Simulator(SimConfig(n_instances=n, seed=1), binding=binding)
+    sim.tcp_enable()
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_set_graph(off, ring, 4)
+    assert e.value.code == A.ESTATE
+    with pytest.raises(A.TgsimError) as e:
+        sim.flood_react(64)
+    assert e.value.code == A.ESTATE
     sim.close()
 
 
