@@ -399,6 +399,44 @@ int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
 int tgsim_snapshot(tgsim_ctx* ctx, void* buf, size_t cap, size_t* n);
 int tgsim_restore(tgsim_ctx* ctx, const void* buf, size_t n);
 
+/* ---- sequential probes: request / reply, one at a time per instance ----------
+ * plans/splitbrain/main.go:153-175: every node GETs each peer in turn with http.Client{Timeout: 1
+ * minute}; the next GET starts when the previous one returned. Here every local instance probes
+ * order[0..n_order) except itself, in that order: a request (request_bytes, seq = TGSIM_PROBE_REQ |
+ * its position in order) whose first arrival at the peer is answered by one reply (reply_bytes,
+ * seq = TGSIM_PROBE_REP | the prober) at max(arrival, horizon). A probe ends
+ *   TGSIM_PROBE_REFUSED at its send time when the prober's route refuses the request (blackhole,
+ *     prohibit, no route: connect() fails at once - a local route error is immediate [EXT]);
+ *   TGSIM_PROBE_OK at the reply's first arrival, if that is before the deadline (send + timeout);
+ *   TGSIM_PROBE_TIMEOUT at the deadline otherwise (lost request or reply, a peer whose reply its
+ *     own routes drop, a disabled peer);
+ * and the next probe leaves at max(end, horizon). Call tgsim_probe_react after every window. It
+ * also proposes the next window's end: one window_ns later while anything is staged or in flight,
+ * else the earliest pending deadline + 1 (idle stretches cost one window). Single-shard contexts;
+ * message mode (not with TCP mode or a flood graph). */
+#define TGSIM_PROBE_REQ 0x40000000u
+#define TGSIM_PROBE_REP 0xC0000000u
+typedef struct tgsim_probe_config {
+  uint32_t request_bytes, reply_bytes;  /* wire bytes of a request / a reply */
+  int64_t timeout_ns;                   /* per probe (> 0) */
+  int64_t window_ns;                    /* window length while messages are staged or in flight (> 0) */
+} tgsim_probe_config;
+enum { TGSIM_PROBE_NONE = 0, TGSIM_PROBE_OK = 1, TGSIM_PROBE_REFUSED = 2, TGSIM_PROBE_TIMEOUT = 3 };
+
+int tgsim_probe_setup(tgsim_ctx* ctx, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg);
+/* Every local instance sends its first probe at t0 (>= horizon). */
+int tgsim_probe_start(tgsim_ctx* ctx, int64_t t0);
+/* After a window: resolve probes, stage replies and next requests (device-side staging). next_end /
+ * n_active non-NULL: synchronise and return the proposed window end and the instances still probing;
+ * both NULL: asynchronous (see tgsim_probe_next_end_device). */
+int tgsim_probe_react(tgsim_ctx* ctx, int64_t* next_end, uint32_t* n_active);
+/* Device address of the proposed window end (for tgsim_advance_begin_device: no host round trip)
+ * and of the count of instances still probing. */
+int tgsim_probe_state_device(tgsim_ctx* ctx, const int64_t** next_end_device, const uint32_t** n_active_device);
+/* outcome[l * n_order + j] = TGSIM_PROBE_* of local instance l's probe of order[j] (NONE for itself
+ * and probes not yet ended); t_done[l] = when its last probe ended (INT64_MIN while probing). */
+int tgsim_probe_results(tgsim_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap_outcome);
+
 /* ---- TCP-level mode ----------------------------------
  * The reference plans move application data over TCP (plans/benchmarks/storm.go:127-180 dials and
  * writes in chunks, plans/network/pingpong.go:73-104 times round trips over a connection); with loss

@@ -222,6 +222,8 @@ struct tgo_ctx {
   uint32_t* tpend; size_t tpend_n, tpend_cap;
   struct otack* tack; size_t tack_n, tack_cap;  /* acks = 1: ACK packets for the next window */
   tgsim_tcp_stats tstats;
+  /* sequential probes (tgsim_probe_*) */
+  struct oprobe* pr; uint32_t* pr_order; uint8_t* pr_out; uint32_t pr_n; tgsim_probe_config pr_cfg;
   char err[512];
 };
 
@@ -342,6 +344,7 @@ void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
   free(c->tw); free(c->tsg); free(c->tpend); free(c->tack);
+  free(c->pr); free(c->pr_order); free(c->pr_out);
   free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
     free(c->topics[i].inst); free(c->topics[i].t); free(c->topics[i].off); free(c->topics[i].len);
@@ -1246,6 +1249,7 @@ static void fl_seen_set(tgo_ctx* c, uint32_t p, uint32_t l) {
 int tgo_flood_set_graph(tgo_ctx* c, const uint32_t* off, const uint32_t* nbr, uint32_t max_pubs) {
   if (!off || (off[c->N] && !nbr) || max_pubs == 0) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->pr) return fail(c, TGSIM_ESTATE, "probes are set up: floods need the deliveries to themselves");
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   uint32_t D = 1;
   for (uint32_t g = 0; g < c->N; ++g) {
@@ -1335,6 +1339,168 @@ int tgo_flood_react(tgo_ctx* c, uint32_t size, size_t* n_fwd) {
   free(src); free(dst); free(seq); free(sz); free(ts);
   if (n_fwd) *n_fwd = rc ? 0 : k;
   return rc;
+}
+
+/* ============================== sequential probes ===========================
+ * plans/splitbrain/main.go:153-175: each node GETs its peers one at a time (http.Client{Timeout:
+ * time.Minute}); the next GET starts when the previous one returned. A probe is a request and its
+ * reply; it ends OK at the reply's first arrival before the deadline, REFUSED at once when the
+ * prober's own route refuses the request (a local route error fails connect() immediately [EXT]),
+ * TIMEOUT at the deadline otherwise. */
+
+enum { PR_IDLE = 0, PR_WAIT = 1, PR_DONE = 2 };
+#define PR_NONE INT64_MAX
+#define PR_MASK 0x3FFFFFFFu
+typedef struct oprobe {
+  uint32_t pos, state, refused, replied;
+  int64_t t_req, t_reqarr, t_reparr, t_done;
+} oprobe;
+
+int tgo_probe_setup(tgo_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg) {
+  if (!order || !cfg || n_order == 0 || n_order > PR_MASK) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (cfg->timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->request_bytes >= 0x80000000u || cfg->reply_bytes >= 0x80000000u)
+    return fail(c, TGSIM_EINVAL, "bad probe configuration");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "probes need a single-shard context");
+  if (c->N > PR_MASK) return fail(c, TGSIM_ENOTSUP, "too many instances for probe tags");
+  if (c->tcp_on || c->fl_off) return fail(c, TGSIM_ESTATE, "probes run in message mode, without a flood graph");
+  for (uint32_t j = 0; j < n_order; ++j)
+    if (order[j] >= c->N) return fail(c, TGSIM_EINVAL, "order[%u] is not an instance", j);
+  oprobe* pr = (oprobe*)calloc(c->nloc ? c->nloc : 1, sizeof(oprobe));
+  uint32_t* ord = (uint32_t*)malloc((size_t)n_order * 4);
+  uint8_t* out = (uint8_t*)calloc((size_t)(c->nloc ? c->nloc : 1) * n_order, 1);
+  if (!pr || !ord || !out) { free(pr); free(ord); free(out); return fail(c, TGSIM_ENOMEM, "oom"); }
+  memcpy(ord, order, (size_t)n_order * 4);
+  for (uint32_t l = 0; l < c->nloc; ++l) pr[l].t_done = INT64_MIN;
+  free(c->pr); free(c->pr_order); free(c->pr_out);
+  c->pr = pr; c->pr_order = ord; c->pr_out = out; c->pr_n = n_order; c->pr_cfg = *cfg;
+  return TGSIM_OK;
+}
+
+/* The next position after pos (or the first, pos = UINT32_MAX) that is not the prober itself. */
+static uint32_t pr_next(const tgo_ctx* c, const oprobe* p, uint32_t pos) {
+  uint32_t j = pos == UINT32_MAX ? 0 : pos + 1;
+  while (j < c->pr_n && c->pr_order[j] == c->lo + (uint32_t)(p - c->pr)) ++j;
+  return j;
+}
+
+typedef struct { uint32_t* src; uint32_t* dst; uint32_t* seq; uint32_t* size; int64_t* t; size_t n; } pbuf;
+static void pr_stage(pbuf* b, uint32_t src, uint32_t dst, uint32_t seq, uint32_t size, int64_t t) {
+  b->src[b->n] = src; b->dst[b->n] = dst; b->seq[b->n] = seq; b->size[b->n] = size; b->t[b->n] = t; ++b->n;
+}
+/* the previous probe of local l ended at te: probe pos leaves at max(te, H), or l is done at te */
+static void pr_begin(tgo_ctx* c, uint32_t l, uint32_t pos, int64_t te, int64_t H, pbuf* b) {
+  oprobe* p = &c->pr[l];
+  if (pos >= c->pr_n) { p->state = PR_DONE; p->t_done = te; p->pos = c->pr_n; return; }
+  const int64_t t = te > H ? te : H;
+  p->state = PR_WAIT; p->pos = pos; p->t_req = t;
+  p->refused = p->replied = 0; p->t_reqarr = p->t_reparr = PR_NONE;
+  pr_stage(b, c->lo + l, c->pr_order[pos], TGSIM_PROBE_REQ | pos, c->pr_cfg.request_bytes, t);
+}
+static int pr_alloc(pbuf* b, size_t cap) {
+  b->n = 0;
+  b->src = malloc(cap * 4); b->dst = malloc(cap * 4); b->seq = malloc(cap * 4); b->size = malloc(cap * 4);
+  b->t = malloc(cap * 8);
+  return b->src && b->dst && b->seq && b->size && b->t ? 0 : TGSIM_ENOMEM;
+}
+static void pr_free(pbuf* b) { free(b->src); free(b->dst); free(b->seq); free(b->size); free(b->t); }
+static int pr_flush(tgo_ctx* c, pbuf* b) {
+  tgsim_msg_soa m = {b->src, b->dst, b->seq, b->size, b->t};
+  int rc = b->n ? tgo_enqueue(c, &m, b->n) : TGSIM_OK;
+  pr_free(b);
+  return rc;
+}
+
+int tgo_probe_start(tgo_ctx* c, int64_t t0) {
+  if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
+  pbuf b;
+  if (pr_alloc(&b, (size_t)c->nloc + 1)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  for (uint32_t l = 0; l < c->nloc; ++l)
+    if (c->pr[l].state == PR_IDLE) pr_begin(c, l, pr_next(c, &c->pr[l], UINT32_MAX), t0, t0, &b);
+  return pr_flush(c, &b);
+}
+
+int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  const omsgs* s = &c->staged;
+  const int64_t H = c->horizon, t_end = c->now, timeout = c->pr_cfg.timeout_ns;
+  /* 1. the window's requests: a route that refused one ends the probe at once */
+  for (size_t i = 0; i < c->n_status; ++i) {
+    const uint32_t sq = s->seq[i];
+    if ((sq >> 30) != 1u) continue;
+    const uint32_t code = c->status[i] & 0x0Fu, l = s->src[i] - c->lo;
+    oprobe* p = &c->pr[l];
+    if ((code == TGSIM_ST_DROPPED || code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) && p->state == PR_WAIT &&
+        p->pos == (sq & PR_MASK) && c->pr_order[p->pos] == s->dst[i])
+      p->refused = 1;
+  }
+  /* 2. the window's deliveries: first arrivals of the current request at its peer and of its reply */
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    const uint32_t tag = r->seq >> 30;
+    if (tag == 1u) {
+      oprobe* p = &c->pr[r->src - c->lo];
+      if (p->state == PR_WAIT && p->pos == (r->seq & PR_MASK) && c->pr_order[p->pos] == r->dst && r->t < p->t_reqarr)
+        p->t_reqarr = r->t;
+    } else if (tag == 3u && (r->seq & PR_MASK) == r->dst) {
+      oprobe* p = &c->pr[r->dst - c->lo];
+      if (p->state == PR_WAIT && p->replied && c->pr_order[p->pos] == r->src && r->t < p->t_reparr) p->t_reparr = r->t;
+    }
+  }
+  /* 3. per prober: the peer's reply, then the probe's end and the next request */
+  pbuf b;
+  if (pr_alloc(&b, 2 * (size_t)c->nloc + 1)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  int64_t min_dl = INT64_MAX;
+  uint32_t active = 0;
+  for (uint32_t l = 0; l < c->nloc; ++l) {
+    oprobe* p = &c->pr[l];
+    if (p->state != PR_WAIT) continue;
+    if (p->t_reqarr != PR_NONE && !p->replied) {
+      pr_stage(&b, c->pr_order[p->pos], c->lo + l, TGSIM_PROBE_REP | (c->lo + l), c->pr_cfg.reply_bytes,
+               p->t_reqarr > H ? p->t_reqarr : H);
+      p->replied = 1;
+    }
+    p->t_reqarr = PR_NONE;
+    const int64_t dl = p->t_req + timeout;
+    uint8_t outc = TGSIM_PROBE_NONE;
+    int64_t te = 0;
+    if (p->refused) { outc = TGSIM_PROBE_REFUSED; te = p->t_req; }
+    else if (p->t_reparr != PR_NONE && p->t_reparr < dl) { outc = TGSIM_PROBE_OK; te = p->t_reparr; }
+    else if (dl < t_end) { outc = TGSIM_PROBE_TIMEOUT; te = dl; }
+    if (outc != TGSIM_PROBE_NONE) {
+      c->pr_out[(size_t)l * c->pr_n + p->pos] = outc;
+      pr_begin(c, l, pr_next(c, p, p->pos), te, H, &b);
+    }
+    if (p->state == PR_WAIT) {
+      ++active;
+      const int64_t d = p->t_req + timeout;
+      if (d < min_dl) min_dl = d;
+    }
+  }
+  int rc = pr_flush(c, &b);
+  if (rc) return rc;
+  /* 4. the next window: one window_ns while anything is staged or in flight, else up to the
+   *    earliest deadline */
+  int64_t ne = t_end + c->pr_cfg.window_ns;
+  if (!c->staged.n && !c->heap.n && active && min_dl != INT64_MAX && min_dl + 1 > ne) ne = min_dl + 1;
+  if (next_end) *next_end = ne;
+  if (n_active) *n_active = active;
+  return TGSIM_OK;
+}
+
+int tgo_probe_results(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
+  const size_t n = (size_t)c->nloc * c->pr_n;
+  if (outcome) {
+    if (cap < n) return fail(c, TGSIM_ECAPACITY, "outcome capacity %zu < %zu", cap, n);
+    memcpy(outcome, c->pr_out, n);
+  }
+  if (t_done)
+    for (uint32_t l = 0; l < c->nloc; ++l) t_done[l] = c->pr[l].t_done;
+  return TGSIM_OK;
 }
 
 /* ============================== topics (sync.Client Publish / Subscribe) ===================
@@ -1427,6 +1593,7 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->staged.n) return fail(c, TGSIM_ESTATE, "messages already staged");
   if (c->fl_off) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
+  if (c->pr) return fail(c, TGSIM_ESTATE, "probes are set up: probes run in message mode");
   tgsim_tcp_config t = *cfg;
   if (!t.mss) t.mss = 1448;
   if (!t.header_bytes) t.header_bytes = 52;

@@ -96,6 +96,10 @@ int tgo_flood_set_graph(tgo_ctx* ctx, const uint32_t* offsets, const uint32_t* n
 int tgo_flood_publish(tgo_ctx* ctx, const uint32_t* instances, const uint32_t* pubs, const int64_t* t, size_t n,
                       uint32_t size);
 int tgo_flood_react(tgo_ctx* ctx, uint32_t size, size_t* n_forwarded);
+int tgo_probe_setup(tgo_ctx* ctx, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg);
+int tgo_probe_start(tgo_ctx* ctx, int64_t t0);
+int tgo_probe_react(tgo_ctx* ctx, int64_t* next_end, uint32_t* n_active);
+int tgo_probe_results(tgo_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap_outcome);
 
 #ifdef __cplusplus
 }

@@ -95,6 +95,15 @@ class TcpStats(C.Structure):
 
 
 TCP_PENDING, TCP_DELIVERED, TCP_TIMEOUT, TCP_REFUSED = 0, 1, 2, 3
+
+
+class ProbeConfig(C.Structure):
+    _fields_ = [("request_bytes", C.c_uint32), ("reply_bytes", C.c_uint32), ("timeout_ns", C.c_int64),
+                ("window_ns", C.c_int64)]
+
+
+PROBE_NONE, PROBE_OK, PROBE_REFUSED, PROBE_TIMEOUT = 0, 1, 2, 3
+PROBE_REQ, PROBE_REP = 0x40000000, 0xC0000000
 TCP_ACK_BIT = 0x80000000
 
 
@@ -161,6 +170,10 @@ _SIGS = {
     "tcp_writes": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "tcp_get_stats": (C.c_int, [P, C.POINTER(TcpStats)]),
     "tcp_gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
+    "probe_setup": (C.c_int, [P, C.c_void_p, C.c_uint32, C.POINTER(ProbeConfig)]),
+    "probe_start": (C.c_int, [P, C.c_int64]),
+    "probe_react": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_uint32)]),
+    "probe_results": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {
@@ -186,6 +199,7 @@ _SIGS_HIP = {
     "snapshot": (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "restore": (C.c_int, [P, C.c_void_p, C.c_size_t]),
     "debug_fail_alloc": (C.c_int, [P, C.c_uint32]),
+    "probe_state_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
 }
 
 

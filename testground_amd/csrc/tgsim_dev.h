@@ -100,9 +100,31 @@ struct TcpDev {
   uint64_t cap_w = 0, cap_s = 0;
 };
 
+// Sequential probes (tgsim_probe_*): per local prober its position in order,
+// state, flags and times; outcome bytes [nloc][n_order]; per-reaction scalars.
+struct ProbeScalars {
+  int64_t next_end;               // the proposed end of the next window
+  int64_t min_dl;                 // running min over waiting probers of their deadline (k_probe_step)
+  uint32_t active;                // probers still waiting (k_probe_step -> snapshot n_active)
+  uint32_t n_active;
+};
+struct ProbeDev {
+  uint32_t* order = nullptr;      // [n_order]
+  uint32_t* pos = nullptr;        // [nloc] the current probe's position
+  uint8_t* state = nullptr;       // [nloc] idle / waiting / done
+  uint8_t* refused = nullptr;     // [nloc] the current request was refused by the prober's route
+  uint8_t* replied = nullptr;     // [nloc] the peer has answered the current request
+  int64_t *t_req = nullptr, *t_reqarr = nullptr, *t_reparr = nullptr, *t_done = nullptr;  // [nloc]
+  uint8_t* out = nullptr;         // [nloc * n_order] TGSIM_PROBE_*
+  ProbeScalars* sc = nullptr;
+  uint32_t n_order = 0, req_bytes = 0, rep_bytes = 0;
+  int64_t timeout = 0, window = 0;
+};
+
 struct Dev {
   Prof prof;
   Flood fl;
+  ProbeDev pr;
   hipStream_t stream = nullptr;
   uint32_t N = 0, S = 1, shard = 0, lo = 0, nloc = 0;
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
@@ -308,6 +330,16 @@ hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_de
 // TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
+
+// Sequential probes: every local prober without a probe sends its first at t0 (device staging
+// behind sc->n_msgs_dev, set from base_host unless base_dev).
+hipError_t launch_probe_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t0);
+// After a window: the window's refused requests (status over the staged packets, n_host or
+// *n_dev), first arrivals of requests and replies (deliveries), then per prober the reply it owes,
+// the end of its probe and the next request (staged behind sc->n_msgs_dev), and the next window's
+// proposed end (ProbeScalars::next_end)
+hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                              const uint32_t* n_status_dev);
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),
 // exclusive scan into offsets[0..n], then (entries != nullptr) the entry ids, at most entries_cap.

@@ -86,6 +86,7 @@ struct tgsim_ctx {
   uint32_t win_m_host = 0;           // max of hcnt
   uint64_t win_m_extra = 0;          // device-staged messages (storm fanout, enqueue_device n): any sender
   uint32_t win_m_inbox = 0;          // flood forwards staged: (D - 1) per delivery of the sender's last inbox
+  uint64_t win_inbox_max = 0;        // a bound on any sender's last inbox run (probes: N; floods use fl_npubs)
   // flood: a sender forwards each publication once (first receipt), so (D - 1) * (publications so
   // far) bounds its forwards in any window without reading the device
   uint32_t fl_npubs = 0;
@@ -153,6 +154,7 @@ struct tgsim_ctx {
   // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
   std::vector<uint32_t> fl_off, fl_nbr;
   uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
+  bool probes = false;      // tgsim_probe_setup done
 };
 
 // An allocation point of a host-side table (tgsim_debug_fail_alloc makes the chosen one throw, so
@@ -1109,9 +1111,11 @@ static int plan_queue_limit(tgsim_ctx* c) {
   Dev& d = c->d;
   const uint64_t mult = c->any_dup ? 2 : 1;
   const uint64_t m_uniform = std::min<uint64_t>((uint64_t)c->win_m_host + c->win_m_extra, 0x7FFFFFFFull);
-  const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * c->fl_npubs;
+  const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * std::max<uint64_t>(c->fl_npubs, c->win_inbox_max);
   bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
-  if (gate && !c->pend_exact) {  // inconclusive: refresh the bound with the exact maximum (one sync)
+  // inconclusive: refresh the bound with the exact maximum (one sync) - unless the window's own
+  // staging bound already reaches the limit, when no refresh can close the gate
+  if (gate && !c->pend_exact && mult * m_max <= TGSIM_NETEM_LIMIT) {
     HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks, (uint32_t)mult),
           "pend max");
     HIPCK(c, sync_scalars(d), "sync");
@@ -1145,6 +1149,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
   c->win_m_host = 0;
   c->win_m_extra = 0;
   c->win_m_inbox = 0;
+  c->win_inbox_max = 0;
   c->max_tsend_h = INT64_MIN;
   return TGSIM_OK;
 }
@@ -1775,6 +1780,7 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
   // a flood reaction reads deliveries as publications (seq / D): TCP packets (seq = segment << 4 |
   // attempt) would be forwarded as floods and corrupt the TCP state
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
+  if (c->probes) return fail(c, TGSIM_ESTATE, "probes are set up: floods need the deliveries to themselves");
   uint32_t D = 1;
   for (uint32_t g = 0; g < c->N; ++g) {
     if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
@@ -1885,6 +1891,130 @@ static int tgsim_flood_react_body(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
     if (rc) return rc;
     *n_fwd = c->d.h_sc->fl_total;
   }
+  return TGSIM_OK;
+}
+
+// ============================== sequential probes ===========================
+// plans/splitbrain/main.go:153-175 (one httpclient.Get after another, Timeout: 1 minute). Kernels in
+// tgsim_probe.hip, oracle twin tgo_probe_*.
+
+static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg);
+extern "C" int tgsim_probe_setup(tgsim_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg) {
+  return abi_guard(c, [&] { return tgsim_probe_setup_body(c, order, n_order, cfg); });
+}
+static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg) {
+  if (!c || !order || !cfg || n_order == 0 || n_order > 0x3FFFFFFFu) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (cfg->timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->request_bytes >= 0x80000000u || cfg->reply_bytes >= 0x80000000u)
+    return fail(c, TGSIM_EINVAL, "bad probe configuration");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "probes need a single-shard context");
+  if (c->N > 0x3FFFFFFFu) return fail(c, TGSIM_ENOTSUP, "too many instances for probe tags");
+  if (c->tcp_on || !c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "probes run in message mode, without a flood graph");
+  for (uint32_t j = 0; j < n_order; ++j)
+    if (order[j] >= c->N) return fail(c, TGSIM_EINVAL, "order[%u] is not an instance", j);
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  ProbeDev& p = c->d.pr;
+  for (void* q : {(void*)p.order, (void*)p.pos, (void*)p.state, (void*)p.refused, (void*)p.replied,
+                  (void*)p.t_req, (void*)p.t_reqarr, (void*)p.t_reparr, (void*)p.t_done, (void*)p.out, (void*)p.sc})
+    dfree(c, q);
+  p = ProbeDev{};
+  c->probes = false;
+  const size_t nl = std::max<uint32_t>(c->nloc, 1);
+  if (dalloc(c, &p.order, n_order) || dalloc(c, &p.pos, nl) || dalloc(c, &p.state, nl) || dalloc(c, &p.refused, nl) ||
+      dalloc(c, &p.replied, nl) || dalloc(c, &p.t_req, nl) || dalloc(c, &p.t_reqarr, nl) || dalloc(c, &p.t_reparr, nl) ||
+      dalloc(c, &p.t_done, nl) || dalloc(c, &p.out, nl * n_order) || dalloc(c, &p.sc, 1))
+    return TGSIM_ENOMEM;
+  hipStream_t st = c->d.stream;
+  HIPCK(c, hipMemcpyAsync(p.order, order, (size_t)n_order * 4, hipMemcpyHostToDevice, st), "probe setup");
+  HIPCK(c, hipMemsetAsync(p.state, 0, nl, st), "probe setup");
+  HIPCK(c, hipMemsetAsync(p.out, 0, nl * n_order, st), "probe setup");
+  HIPCK(c, hipMemsetAsync(p.sc, 0, sizeof(ProbeScalars), st), "probe setup");
+  std::vector<int64_t> tmin(nl, INT64_MIN);
+  HIPCK(c, hipMemcpyAsync(p.t_done, tmin.data(), nl * 8, hipMemcpyHostToDevice, st), "probe setup");
+  HIPCK(c, hipStreamSynchronize(st), "probe setup");  // tmin goes out of scope
+  p.n_order = n_order;
+  p.req_bytes = cfg->request_bytes;
+  p.rep_bytes = cfg->reply_bytes;
+  p.timeout = cfg->timeout_ns;
+  p.window = cfg->window_ns;
+  c->probes = true;
+  return TGSIM_OK;
+}
+
+// Probes stage on the device: behind the device-side count, which starts at the host's count.
+static void probes_staged(tgsim_ctx* c) {
+  c->spec.valid = false;
+  c->staged_dev = true;
+  c->win_m_extra += 1;                                        // one request per prober
+  c->win_m_inbox = std::max<uint32_t>(c->win_m_inbox, 1u);    // one reply per request delivered last window
+  c->win_inbox_max = std::max<uint64_t>(c->win_inbox_max, c->N);
+}
+
+static int tgsim_probe_start_body(tgsim_ctx* c, int64_t t0);
+extern "C" int tgsim_probe_start(tgsim_ctx* c, int64_t t0) {
+  return abi_guard(c, [&] { return tgsim_probe_start_body(c, t0); });
+}
+static int tgsim_probe_start_body(tgsim_ctx* c, int64_t t0) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
+  HIPCK(c, launch_probe_start(c->d, c->staged_dev, c->n_staged, t0), "probe start");
+  probes_staged(c);
+  c->max_tsend_h = std::max(c->max_tsend_h, t0);
+  return TGSIM_OK;
+}
+
+static int tgsim_probe_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active);
+extern "C" int tgsim_probe_react(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  return abi_guard(c, [&] { return tgsim_probe_react_body(c, next_end, n_active); });
+}
+static int tgsim_probe_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  const bool on_dev = c->n_status_last == kStatusOnDevice;
+  HIPCK(c, launch_probe_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                              on_dev ? &c->d.sc->n_msgs_last : nullptr), "probe react");
+  probes_staged(c);
+  if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
+  ProbeScalars ps;
+  HIPCK(c, hipMemcpyAsync(&ps, c->d.pr.sc, sizeof(ps), hipMemcpyDeviceToHost, c->d.stream), "probe react");
+  const int rc = sync_and_check(c);
+  if (rc) return rc;
+  if (next_end) *next_end = ps.next_end;
+  if (n_active) *n_active = ps.n_active;
+  return TGSIM_OK;
+}
+
+static int tgsim_probe_state_device_body(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active);
+extern "C" int tgsim_probe_state_device(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active) {
+  return abi_guard(c, [&] { return tgsim_probe_state_device_body(c, next_end, n_active); });
+}
+static int tgsim_probe_state_device_body(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
+  if (next_end) *next_end = &c->d.pr.sc->next_end;
+  if (n_active) *n_active = &c->d.pr.sc->n_active;
+  return TGSIM_OK;
+}
+
+static int tgsim_probe_results_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap);
+extern "C" int tgsim_probe_results(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  return abi_guard(c, [&] { return tgsim_probe_results_body(c, outcome, t_done, cap); });
+}
+static int tgsim_probe_results_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  const size_t n = (size_t)c->nloc * c->d.pr.n_order;
+  if (outcome) {
+    if (cap < n) return fail(c, TGSIM_ECAPACITY, "outcome capacity %zu < %zu", cap, n);
+    if (n) HIPCK(c, hipMemcpy(outcome, c->d.pr.out, n, hipMemcpyDeviceToHost), "probe results");
+  }
+  if (t_done && c->nloc) HIPCK(c, hipMemcpy(t_done, c->d.pr.t_done, (size_t)c->nloc * 8, hipMemcpyDeviceToHost), "probe results");
   return TGSIM_OK;
 }
 
@@ -2147,6 +2277,7 @@ static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "messages already staged");
   if (!c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
+  if (c->probes) return fail(c, TGSIM_ESTATE, "probes are set up: probes run in message mode");
   tgsim_tcp_config t = *cfg;
   if (!t.mss) t.mss = 1448;
   if (!t.header_bytes) t.header_bytes = 52;
@@ -2515,8 +2646,8 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
 int snap_refusal(tgsim_ctx* c) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "snapshot/restore: inside a window");
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "snapshot/restore: messages are staged");
-  if (c->tcp_on || c->tp_n || !c->fl_off.empty())
-    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics and flood graphs are not captured");
+  if (c->tcp_on || c->tp_n || !c->fl_off.empty() || c->probes)
+    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics, flood graphs and probes are not captured");
   return TGSIM_OK;
 }
 

@@ -97,16 +97,6 @@ __device__ __forceinline__ void block_partial(uint32_t v, uint32_t* part) {
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// A reservation of n staged slots behind the device-side count that never leaves the count above
-// the capacity: an adder that overshoots pulls it back to cap after its add, so once every adder
-// is done the count is <= cap, and every slot below it was reserved by exactly one adder (which
-// writes it when p < cap and reports ERR_CAP_M otherwise). The shape pass reads this count.
-__device__ __forceinline__ uint32_t reserve_staged(uint32_t* cnt, uint32_t n, uint32_t cap) {
-  const uint32_t old = atomicAdd(cnt, n);
-  if ((uint64_t)old + n > cap) atomicMin(cnt, cap);
-  return old;
-}
-
 __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict__ status,
                                                        const uint32_t* __restrict__ seq, uint32_t n_host,
                                                        const uint32_t* n_dev, TcpDev t) {

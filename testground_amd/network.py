@@ -182,6 +182,13 @@ class LinkRule:
         return LinkRule(ipnet_from_wire(_get(d, "Subnet")), LinkShape.from_wire(d))
 
 
+class RuleList(list):
+    """A rule list that many Configs share (splitbrain: every region-A node installs the same
+    /32 block): its C array is built once and reused while the list's length is unchanged."""
+    c_array = None
+    c_len = -1
+
+
 @dataclass
 class Config:
     """network.Config. ``callback_target == 0`` means "all instances" (network.Client [EXT])."""
@@ -216,7 +223,11 @@ class Config:
         """Returns (tgsim_network_config, keepalive) - keep the second alive during the call."""
         if self.ipv6:
             raise A.TgsimError(A.ENOTSUP, "IPv6 data networks are not simulated")
-        rules = (A.LinkRule * max(1, len(self.rules)))(*[r.to_c() for r in self.rules])
+        rules = getattr(self.rules, "c_array", None)
+        if rules is None or self.rules.c_len != len(self.rules):
+            rules = (A.LinkRule * max(1, len(self.rules)))(*[r.to_c() for r in self.rules])
+            if isinstance(self.rules, RuleList):
+                self.rules.c_array, self.rules.c_len = rules, len(self.rules)
         name = self.network.encode()
         cfg = A.NetworkConfig(name, int(bool(self.enable)), policy_code(self.routing_policy), self.default.to_c(),
                               C.cast(rules, C.POINTER(A.LinkRule)), len(self.rules),

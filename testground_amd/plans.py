@@ -26,7 +26,7 @@ import math
 import numpy as np
 
 from . import _abi as A
-from .network import (MS, SECOND, AllowAll, Config, DenyAll, FilterAction, IPNet, LinkRule, LinkShape,
+from .network import (MS, SECOND, AllowAll, Config, DenyAll, FilterAction, IPNet, LinkRule, LinkShape, RuleList,
                       int_to_ip)
 from .sidecar import NetClient, Sidecar
 from .sim import SimConfig, Simulator
@@ -66,6 +66,9 @@ class PlanEnv:
         self.test_case = test_case
         self.params = params if isinstance(params, RunParams) else RunParams(params or {})
         self.window_ns = int(window_ns)
+        # reaction latency of a request/reply hop on an unshaped link (a local HTTP round trip over a
+        # bridge is ~100 us): the window of the sequential probes while messages are in flight
+        self.probe_window_ns = int(self.params.get("probe_window_ns", 100_000))
         kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=1024, max_waiters=1 << 16)
         kw.update(sim_kw or {})
         self.sim = Simulator(SimConfig(n_instances=self.n, seed=seed, **kw), binding=binding)
@@ -264,6 +267,26 @@ class PlanEnv:
         ok = arr != NEVER
         return ok, np.where(ok, arr - t, -1)
 
+    def probe(self, order, req_size: int, rep_size: int, timeout_ns: int, t0: int, window_ns: int | None = None):
+        """Every instance probes order[...] (itself excluded) one request/reply at a time, the next
+        probe leaving when the previous one ended (tgsim_probe_*): the sequential
+        httpclient.Get loop of plans/splitbrain/main.go:159-175. Windows follow the device's
+        proposal (window_ns while traffic is in flight, a jump to the next deadline when idle).
+        Returns (outcome[instance, position in order], t_done[instance])."""
+        window = int(window_ns or self.probe_window_ns)
+        self.advance_to(t0)
+        self.sim.probe_setup(order, req_size, rep_size, timeout_ns, window)
+        self.sim.probe_start(t0)
+        ne = max(int(t0), self.sim.now) + window
+        self.probe_windows = 0
+        while True:
+            self.sim.advance(ne)
+            self.probe_windows += 1
+            ne, active = self.sim.probe_react()
+            if active == 0:
+                break
+        return self.sim.probe_results()
+
     def fail(self, msg: str) -> None:
         self.failures.append(msg)
 
@@ -389,35 +412,62 @@ def expect_errors(test_case: str, a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return ((a == REGION_A) & (b == REGION_B)) | ((a == REGION_B) & (b == REGION_A))
 
 
+SPLITBRAIN_CTX_NS = 300 * SECOND     # context.WithTimeout(..., 300*time.Second), main.go:64
+PROBE_TIMEOUT_NS = 60 * SECOND       # http.Client{Timeout: time.Minute}, main.go:153-155
+
+
 def splitbrain(action: FilterAction):
-    """plans/splitbrain/main.go:60-186: region = SignalEntry("region-select") % 3; region A installs
-    a /32 rule with `action` toward every region-B node; every node then probes every other
-    node (HTTP: request + reply). Failures are expected exactly between A and B."""
+    """plans/splitbrain/main.go:60-186: region = SignalEntry("region-select") % 3; every node
+    publishes itself on "nodes" and lists the others in topic order; region A installs a /32 rule
+    with `action` toward every region-B node; SignalAndWait("nodeRoundup"); time.Sleep(10 s); then
+    each node GETs every other node ONE AT A TIME in that order (main.go:159-175), each GET with a
+    one-minute timeout; SignalAndWait("testcomplete") under the plan's 300 s context (main.go:64).
+
+    A probe is a request and its reply (device sequential probes): it fails at once
+    when the prober's own route refuses it (A -> B: blackhole / prohibit make connect() fail
+    immediately) and at the one-minute deadline when the peer's reply is dropped by the peer's
+    routes (B -> A: the SYN-ACK meets A's rule). Failures are expected exactly between A and B
+    (expectErrors, main.go:50-58); an unexpected one fails the prober. The "testcomplete" barrier
+    releases when the slowest prober is done; a release past the 300 s context is an error for every
+    instance - which is what the reference does once region B waits out enough one-minute timeouts
+    (>= 5 region-A nodes). env.probe_unexpected / env.probe_errors keep the probe truth table."""
     def plan(env: PlanEnv) -> np.ndarray:
         n = env.n
         t = env.net.wait_network_initialized(0)
         seq = env.sync.signal_entry("region-select", np.arange(n), t)
         region = (seq.astype(np.int64) % 3)
         ips = np.array([env.net.get_data_network_ip(g) for g in range(n)], np.int64)
-        env.sync.publish("nodes", np.arange(n), t, list(zip(region.tolist(), ips.tolist())))
-        b_ips = ips[region == REGION_B]
+        pos = env.sync.publish("nodes", np.arange(n), t, list(zip(region.tolist(), ips.tolist())))
+        order = np.argsort(pos, kind="stable")                 # instances in topic order
+        b_ips = ips[order][region[order] == REGION_B]          # main.go:118: nodes in topic order
+        rules = RuleList(LinkRule(IPNet(int(ip), 32), LinkShape(filter=action)) for ip in b_ips)
         for a in np.flatnonzero(region == REGION_A):
             cfg = Config(network="default", enable=True, callback_state=f"reconfigured{a}", callback_target=1,
-                         rules=[LinkRule(IPNet(int(ip), 32), LinkShape(filter=action)) for ip in b_ips])
+                         rules=rules)
             env.net.configure_network(int(a), cfg, t)
         _, t = env.sync.signal_and_wait("nodeRoundup", np.arange(n), t, n)
-        env.advance_to(t + 10 * SECOND)   # time.Sleep(10 * time.Second), main.go:145
-        src, dst = np.nonzero(~np.eye(n, dtype=bool))
-        ok_pair, _ = env.rpc(src, dst, TCP_OVERHEAD, TCP_OVERHEAD, env.sim.now, 60 * SECOND)
-        errs = ~ok_pair
-        unexpected = errs & ~expect_errors(env.test_case, region[src], region[dst])
-        env.probe_errors = np.bincount(src[errs], minlength=n)
+        t_probe = t + 10 * SECOND                               # time.Sleep(10 * time.Second), main.go:145
+        outcome, t_done = env.probe(order, TCP_OVERHEAD, TCP_OVERHEAD, PROBE_TIMEOUT_NS, t_probe)
+        peer = np.broadcast_to(order, outcome.shape)
+        me = np.broadcast_to(np.arange(n)[:, None], outcome.shape)
+        probed = peer != me
+        errs = probed & (outcome != A.PROBE_OK)
+        unexpected = errs & ~expect_errors(env.test_case, region[me], region[peer])
+        env.probe_outcome = outcome
+        env.probe_errors = errs.sum(axis=1)
+        env.probe_unexpected = unexpected.sum(axis=1)
+        env.probe_done = t_done
         env.region = region
-        ok = np.ones(n, bool)
-        ok[src[unexpected]] = False
+        ok = env.probe_unexpected == 0
         for g in np.flatnonzero(~ok):
-            env.fail(f"instance {g} (region {region[g]}): unexpected probe failure")
-        _, t = env.sync.signal_and_wait("testcomplete", np.arange(n), env.sim.now, n)
+            env.fail(f"instance {g} (region {region[g]}): {env.probe_unexpected[g]} unexpected probe failures")
+        _, t_all = env.sync.signal_and_wait("testcomplete", np.arange(n), t_done, n)
+        env.testcomplete = t_all
+        if t_all > SPLITBRAIN_CTX_NS:
+            env.fail(f"testcomplete released at {t_all / SECOND:.1f} s, after the plan's 300 s context "
+                     f"(main.go:64): context deadline exceeded")
+            ok[:] = False
+        env.advance_to(max(env.sim.now, t_all))
         return ok
     return plan
 

@@ -146,7 +146,12 @@ class NetClient:
             self.sidecar.sync.publish(Sidecar.topic(instance), [instance], t, [cfg.to_wire()])
             self.sidecar.poll(instance, t)
         else:
-            self.sidecar.apply(instance, copy.deepcopy(cfg), t)
+            # the plan may change its Config after the call (pingpong.go mutates latency and IP):
+            # the sidecar keeps a copy; rule lists are shared, not copied (plans never edit one in
+            # place, and a shared RuleList keeps its C array)
+            c = copy.copy(cfg)
+            c.default = copy.copy(cfg.default)
+            self.sidecar.apply(instance, c, t)
         target = cfg.callback_target or self.sidecar.n
         return self.sidecar.sync.barrier(cfg.callback_state, target, t)
 

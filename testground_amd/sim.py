@@ -436,6 +436,33 @@ class Simulator:
             assert hip.hipMemcpy(out["payload"].ctypes.data, ptrs[4].value, nb, _D2H) == 0
         return out
 
+    # ---- sequential probes (tgsim_probe_*) ------------------------------------
+    def probe_setup(self, order, request_bytes: int, reply_bytes: int, timeout_ns: int, window_ns: int) -> None:
+        o = np.ascontiguousarray(order, dtype=np.uint32)
+        self._probe_n = len(o)
+        cfg = A.ProbeConfig(request_bytes, reply_bytes, timeout_ns, window_ns)
+        self._check(self.lib.probe_setup(self._ctx, _ptr(o), len(o), C.byref(cfg)))
+
+    def probe_start(self, t0: int) -> None:
+        self._check(self.lib.probe_start(self._ctx, int(t0)))
+
+    def probe_react(self, wait: bool = True):
+        """After a window. wait: (proposed next window end, instances still probing); else None."""
+        if not wait:
+            self._check(self.lib.probe_react(self._ctx, None, None))
+            return None
+        ne, act = C.c_int64(), C.c_uint32()
+        self._check(self.lib.probe_react(self._ctx, C.byref(ne), C.byref(act)))
+        return ne.value, act.value
+
+    def probe_results(self) -> tuple[np.ndarray, np.ndarray]:
+        """(outcome[local, position in order] of TGSIM_PROBE_*, t_done[local])."""
+        nloc = self.hi - self.lo
+        out = np.zeros((nloc, self._probe_n), np.uint8)
+        t = np.zeros(nloc, np.int64)
+        self._check(self.lib.probe_results(self._ctx, _ptr(out), _ptr(t), out.size))
+        return out, t
+
     # ---- flood workload (config 5) -----------------------------------------------------------
     def flood_set_graph(self, offsets, neighbors, max_pubs: int) -> None:
         off = np.ascontiguousarray(offsets, dtype=np.uint32)

@@ -21,7 +21,9 @@ HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_sha
             # uninterrupted reference a restored run is compared with (tests/test_snapshot.py)
             "tgsim_snapshot", "tgsim_restore",
             # allocation-failure injection into the library's C++ host tables (no C++ in the oracle)
-            "tgsim_debug_fail_alloc"}
+            "tgsim_debug_fail_alloc",
+            # device address of the proposed window end (tgsim_advance_begin_device has no oracle twin)
+            "tgsim_probe_state_device"}
 
 
 def test_header_declares_expected_surface():

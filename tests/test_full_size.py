@@ -198,7 +198,76 @@ def _splitbrain_want(n, phase, policy, src, dst):
     return want
 
 
-def test_cfg3_splitbrain_full(hip, oracle, n=10_000, chunk=1000):
+def _splitbrain_descriptor(binding, n, case):
+    """plans/splitbrain as the reference runs it (testground_amd.plans.splitbrain): sequential
+    probes, one-minute timeouts, the 300 s plan context."""
+    from testground_amd import plans as P
+    env = P.PlanEnv(n, seed=3, test_case=case, binding=binding,
+                    sim_kw=dict(max_msgs_per_window=1 << 16, max_records=1 << 18, max_waiters=1 << 16))
+    ok = P.PLANS[("splitbrain", case)](env)
+    res = dict(ok=ok, outcome=env.probe_outcome, done=env.probe_done, region=env.region,
+               windows=env.probe_windows, unexpected=env.probe_unexpected, errors=env.probe_errors,
+               stats={k: v for k, v in env.sim.stats().items() if k not in ("windows", "inflight")},
+               testcomplete=env.testcomplete)
+    env.close()
+    return res
+
+
+def _check_splitbrain_truth(r, n, case):
+    from testground_amd import plans as P
+    region = r["region"]
+    assert list(region) == [(g + 1) % 3 for g in range(n)]
+    assert not r["unexpected"].any() and r["stats"]["overlimit"] == 0
+    out = r["outcome"]
+    a, b = np.flatnonzero(region == 0), np.flatnonzero(region == 1)
+    probed = ~np.eye(n, dtype=bool)               # topic order = instance order (seq = g + 1)
+    if case == "accept":
+        assert np.all(out[probed] == A.PROBE_OK)
+        # zero latency, lock step: n - 1 probes of two one-window hops each, from t0 on
+        assert len(np.unique(r["done"])) == 1 and r["ok"].all()
+    else:
+        assert np.all(out[np.ix_(a, b)] == A.PROBE_REFUSED) and np.all(out[np.ix_(b, a)] == A.PROBE_TIMEOUT)
+        other = probed.copy()
+        other[np.ix_(a, b)] = other[np.ix_(b, a)] = False
+        assert np.all(out[other] == A.PROBE_OK)
+        # region B waits out one minute per region-A peer: far past the plan's 300 s context
+        assert r["done"][b].min() > len(a) * P.PROBE_TIMEOUT_NS and not r["ok"].any()
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_splitbrain_full(hip, oracle, n=10_000):
+    """BASELINE config 3 as the reference plan generates it: 10k instances,
+    region = seq % 3, every node GETs every other node one at a time (plans/splitbrain/main.go:
+    153-175) - 1e8 probes, 2e8 messages over 2e4 windows. HIP and the oracle agree on every probe's
+    outcome, every node's end time, the window count and the counters."""
+    gpu = _splitbrain_descriptor(hip, n, "accept")
+    _check_splitbrain_truth(gpu, n, "accept")
+    ref = _splitbrain_descriptor(oracle, n, "accept")
+    assert gpu["windows"] == ref["windows"]
+    assert np.array_equal(gpu["outcome"], ref["outcome"]) and np.array_equal(gpu["done"], ref["done"])
+    assert gpu["stats"] == ref["stats"] and gpu["testcomplete"] == ref["testcomplete"]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("case", ["drop", "reject"])
+def test_cfg3_splitbrain_blocked_full(hip, oracle, case, n=10_000):
+    """drop / reject at 10k on HIP (3.3k /32 rules on each of 3.3k region-A nodes; region B's
+    probes of region A wait out one-minute timeouts, so the run covers ~56 simulated hours in
+    ~5e4 windows): the truth table of main.go:50-58 probe by probe; at 2k, bit-exact vs the oracle."""
+    gpu = _splitbrain_descriptor(hip, n, case)
+    _check_splitbrain_truth(gpu, n, case)
+    m = 2000
+    g2, o2 = _splitbrain_descriptor(hip, m, case), _splitbrain_descriptor(oracle, m, case)
+    _check_splitbrain_truth(g2, m, case)
+    assert g2["windows"] == o2["windows"] and g2["stats"] == o2["stats"]
+    assert np.array_equal(g2["outcome"], o2["outcome"]) and np.array_equal(g2["done"], o2["done"])
+
+
+def test_cfg3_all_at_once_stress(hip, oracle, n=10_000, chunk=1000):
+    """STRESS TEST, not the reference's traffic: SURVEY.md 8(d)'s synthetic config 3 - every node
+    fires all its probes at one instant (the reference plan sends one GET at a time: see
+    test_cfg3_splitbrain_full) through 1.1e7 /32 rules, policy flips and 10 ms links, so the netem
+    queue limit tail-drops all but 1000 per sender."""
     subset = np.unique(np.array([0, 1, 2, 3, 4, 5, n // 3, 2 * n // 3, n - 3, n - 2, n - 1, 1500, 4001], np.uint32))
     in_subset = np.zeros(n, bool)
     in_subset[subset] = True

@@ -118,12 +118,15 @@ def test_routing_policy(oracle, case, expect_ok):
     env.close()
 
 
+@pytest.mark.parametrize("n", [12, 30])
 @pytest.mark.parametrize("case", ["drop", "reject", "accept"])
-def test_splitbrain_truth_table(oracle, case):
-    n = 30
+def test_splitbrain_truth_table(oracle, case, n):
+    """main.go:50-58 over sequential probes: errors exactly between regions A and B. B -> A probes
+    wait out the one-minute timeout (A's rule drops the reply), so with 10 region-A nodes (n = 30)
+    region B is still probing when the plan's 300 s context expires (main.go:64) and every
+    SignalAndWait("testcomplete") fails, as in the reference; with 4 (n = 12) it finishes."""
     env = env_for(oracle, n, case)
     ok = P.PLANS[("splitbrain", case)](env)
-    assert ok.all(), env.failures
     region = env.region
     assert list(region) == [(g + 1) % 3 for g in range(n)]   # seq = g + 1 (ties broken by instance)
     na, nb = (region == 0).sum(), (region == 1).sum()
@@ -132,6 +135,31 @@ def test_splitbrain_truth_table(oracle, case):
         want[region == 0] = nb
         want[region == 1] = na
     assert np.array_equal(env.probe_errors, want)
+    assert not env.probe_unexpected.any()
+    out, order = env.probe_outcome, np.argsort(np.arange(n))   # topic order = instance order here
+    if case != "accept":
+        a, b = np.flatnonzero(region == 0), np.flatnonzero(region == 1)
+        assert np.all(out[np.ix_(a, b)] == A.PROBE_REFUSED)      # A's own route refuses: immediate
+        assert np.all(out[np.ix_(b, a)] == A.PROBE_TIMEOUT)      # A drops the reply: one minute
+    slow = 10 * 60 * P.SECOND if case != "accept" else 0
+    if case == "accept" or n == 12:
+        assert ok.all(), env.failures
+        assert env.testcomplete < P.SPLITBRAIN_CTX_NS
+    else:
+        assert not ok.any() and any("context deadline exceeded" in f for f in env.failures)
+        assert env.testcomplete > slow
+    env.close()
+
+
+def test_splitbrain_accept_1200(oracle):
+    """splitbrain accept at 1,200 instances passes (sequential probes; the all-at-once
+    descriptor of round 2 tail-dropped 437,800 probes at this size)."""
+    n = 1200
+    env = env_for(oracle, n, "accept")
+    ok = P.PLANS[("splitbrain", "accept")](env)
+    assert ok.all(), env.failures[:3]
+    assert np.all(env.probe_outcome.sum(axis=1) == n - 1)       # n - 1 probes OK per node
+    assert env.sim.stats()["overlimit"] == 0
     env.close()
 
 

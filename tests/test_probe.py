@@ -1,0 +1,123 @@
+"""Sequential probes (tgsim_probe_*): plans/splitbrain/main.go:153-175 probes its
+peers one httpclient.Get at a time, each with a one-minute timeout. Hand-computed answers on the
+oracle and the HIP library, randomised HIP-vs-oracle parity (every window's statuses, deliveries,
+outcomes and end times)."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd.network import int_to_ip
+from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape
+from tests import scenarios as S
+
+MS = 1_000_000
+SEC = 1000 * MS
+W = 100_000          # 100 us reaction windows
+
+
+def drive(sim, order, t0=0, req=66, rep=66, timeout=60 * SEC, window=W, max_windows=200_000, keep=True):
+    """probe_setup + start, then window after window at the proposed end until no instance probes."""
+    sim.probe_setup(order, req, rep, timeout, window)
+    sim.probe_start(t0)
+    out, ne, w = [], t0 + window, 0
+    while w < max_windows:
+        sim.advance(ne)
+        st, d = sim.status(), sim.deliveries()
+        ne, act = sim.probe_react()
+        if keep:
+            out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+        w += 1
+        if act == 0:
+            break
+    res, t_done = sim.probe_results()
+    return out, res, t_done, w
+
+
+def _hand_case(b):
+    """0 drops its route to 1 (blackhole), 2 rejects 3 (prohibit): 0 -> 1 and 2 -> 3 end REFUSED at
+    once; 1 -> 0 and 3 -> 2 reach the peer, whose reply its own route discards, so they end at the
+    one-minute deadline; every other probe takes a request and a reply, one window each."""
+    n = 5
+    s = Simulator(SimConfig(n_instances=n, seed=3), binding=b)
+    ip = [int_to_ip(s.get_ip(g)) + "/32" for g in range(n)]
+    s.add_rules(0, [make_rule(ip[1], A.FILTER_DROP)])
+    s.add_rules(2, [make_rule(ip[3], A.FILTER_REJECT)])
+    _, res, t_done, w = drive(s, np.arange(n))
+    OK, RF, TO = A.PROBE_OK, A.PROBE_REFUSED, A.PROBE_TIMEOUT
+    assert res.tolist() == [[0, RF, OK, OK, OK],
+                            [TO, 0, OK, OK, OK],
+                            [OK, OK, 0, RF, OK],
+                            [OK, OK, TO, 0, OK],
+                            [OK, OK, OK, OK, 0]]
+    # a reply leaves at max(request arrival, horizon) and the next request at max(reply arrival,
+    # horizon): with zero latency every hop after the first costs one window W. Instance 4: four
+    # probes end at 0, 2W, 4W, 6W; instance 0's refusal ends at once, then three probes: 5W
+    assert t_done[4] == 6 * W and t_done[0] == 5 * W and t_done[2] == 5 * W
+    # 1's first probe waits out the deadline (60 s after t = 0; the window jumps to it: end + 1 ns),
+    # then three probes end at +1, +1 + 2W, +1 + 4W
+    assert t_done[1] == 60 * SEC + 1 + 4 * W
+    assert w < 40
+    s.close()
+
+
+def test_probe_hand_oracle(oracle):
+    _hand_case(oracle)
+
+
+@pytest.mark.gpu
+def test_probe_hand_hip(hip):
+    _hand_case(hip)
+
+
+def _random_run(b, seed, n=40, keep=True):
+    rng = np.random.default_rng(seed)
+    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 14, max_records=1 << 16), binding=b)
+    shapes = [make_shape(latency_ns=int(rng.integers(0, 3)) * MS, jitter_ns=int(rng.integers(0, 2)) * MS // 2,
+                         loss=float(rng.choice([0.0, 0.0, 5.0])), duplicate=float(rng.choice([0.0, 10.0])))
+              for _ in range(n)]
+    s.set_shapes(np.arange(n), shapes)
+    ip = [int_to_ip(s.get_ip(g)) + "/32" for g in range(n)]
+    for g in rng.choice(n, n // 4, replace=False):
+        tgt = rng.choice(n, 5, replace=False)
+        s.add_rules(int(g), [make_rule(ip[int(t)], int(rng.choice([A.FILTER_DROP, A.FILTER_REJECT]))) for t in tgt if t != g])
+    s.set_enabled(int(rng.integers(n)), False)
+    order = rng.permutation(n)
+    out, res, t_done, w = drive(s, order, t0=3 * MS, timeout=int(rng.integers(20, 200)) * MS, window=W, keep=keep)
+    stats = S.parity_stats(s)
+    s.close()
+    return out, res, t_done, w, stats, order
+
+
+def test_probe_random_oracle_properties(oracle):
+    out, res, t_done, w, _, order = _random_run(oracle, 1)
+    assert out[-1]["act"] == 0 and np.all(t_done >= 3 * MS)
+    n = len(res)
+    assert np.all(res[order, np.arange(n)] == A.PROBE_NONE)     # nobody probes itself
+    assert np.count_nonzero(res) == n * (n - 1)                # every other probe ended
+    assert set(np.unique(res)) <= {0, A.PROBE_OK, A.PROBE_REFUSED, A.PROBE_TIMEOUT}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_probe_random_hip_matches_oracle(hip, oracle, seed):
+    a = _random_run(hip, seed)
+    b = _random_run(oracle, seed)
+    assert a[3] == b[3], "window count"
+    S.assert_same(a[0], b[0])
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[4] == b[4]
+
+
+def test_probe_errors(oracle):
+    s = Simulator(SimConfig(n_instances=4, seed=1), binding=oracle)
+    with pytest.raises(A.TgsimError) as e:
+        s.probe_react()
+    assert e.value.code == A.ESTATE
+    with pytest.raises(A.TgsimError) as e:
+        s.probe_setup([0, 9], 66, 66, SEC, W)
+    assert e.value.code == A.EINVAL
+    s.probe_setup(np.arange(4), 66, 66, SEC, W)
+    with pytest.raises(A.TgsimError) as e:
+        s.tcp_enable()
+    assert e.value.code == A.ESTATE
+    s.close()
