@@ -496,6 +496,32 @@ int tgsim_tcp_get_stats(tgsim_ctx* ctx, tgsim_tcp_stats* out);
  * the device: the round's messages become writes with ids in generation order (instance-major). */
 int tgsim_tcp_gen_storm_round(tgsim_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                               int64_t spread_ns, uint32_t state);
+/* Writes ids [first, first + n): state and time as tgsim_tcp_writes (a range, so a caller polling
+ * the unsettled tail of a long run reads O(range), not O(writes so far)). */
+int tgsim_tcp_writes_range(tgsim_ctx* ctx, uint64_t first, size_t n, uint8_t* state_out, int64_t* t_out);
+
+/* ---- TCP connections: congestion window and ACK clocking (acks = 1 only) -------
+ * plans/benchmarks/storm.go:141-183 dials a connection and writes 4 KiB chunks into it; the socket
+ * sends while its congestion window allows. A connection (src -> dst) queues the segments of its
+ * writes in write order and keeps a window [EXT Linux tcp_cong.c Reno, RFC 5681]: cwnd starts at
+ * 10 segments (IW10), ssthresh unbounded; segments leave while the flight (sent, neither ACKed nor
+ * given up) is below cwnd - a write's segments at its t_send if the window has room then, the rest
+ * at the end of the window in which ACKs opened room (ACKs are processed window by window, as they
+ * are sent: tgsim_tcp_config.acks). Each first ACK of a segment: flight - 1 and, below ssthresh,
+ * cwnd + 1 (slow start), else one more segment per cwnd ACKs (congestion avoidance); cwnd <= 65535.
+ * The first retransmission timeout of a connection in a window sets cwnd = 1 and, unless cwnd was
+ * already 1 (the same loss episode), ssthresh = max(cwnd / 2, 2); the retransmitted segments
+ * themselves are not held back. A refused segment (local
+ * route error) breaks the connection: its queued writes fail (REFUSED). A context uses either
+ * connections or tgsim_tcp_send / tgsim_tcp_gen_storm_round, not both. Connection ids count from 0. */
+int tgsim_tcp_connect(tgsim_ctx* ctx, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* conn_out);
+/* Writes (conn[i], size[i], t_send[i] >= horizon) appended to their connections' send queues in
+ * call order; write ids continue tgsim_tcp_writes' numbering. */
+int tgsim_tcp_write(tgsim_ctx* ctx, const uint32_t* conn, const uint32_t* size, const int64_t* t_send, size_t n);
+/* Per connection [first, first + n): segments ACKed so far (cumulative), cwnd, flight, queued
+ * (written, not yet sent) - any output may be NULL. Synchronises. */
+int tgsim_tcp_conns(tgsim_ctx* ctx, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd, uint32_t* flight,
+                    uint32_t* queued);
 
 #ifdef __cplusplus
 }

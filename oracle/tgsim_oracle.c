@@ -221,18 +221,29 @@ struct tgo_ctx {
   struct otcps* tsg; size_t tsg_n, tsg_cap;
   uint32_t* tpend; size_t tpend_n, tpend_cap;
   struct otack* tack; size_t tack_n, tack_cap;  /* acks = 1: ACK packets for the next window */
+  struct otcpc* tc; size_t tc_n, tc_cap;        /* connections (tgsim_tcp_connect) */
   tgsim_tcp_stats tstats;
   /* sequential probes (tgsim_probe_*) */
   struct oprobe* pr; uint32_t* pr_order; uint8_t* pr_out; uint32_t pr_n; tgsim_probe_config pr_cfg;
   char err[512];
 };
 
-typedef struct otcpw { uint32_t src, dst, remaining, state; int64_t t; } otcpw;
+typedef struct otcpw { uint32_t src, dst, remaining, state; int64_t t; uint32_t conn; } otcpw;
 typedef struct otcps {
   uint32_t w, wire, attempt, outstanding, arrived, touched;
   int64_t t_att, arrival, t_last;
   uint32_t acked, gave_up;  /* acks = 1 */
+  uint32_t next, unsent;    /* connections: the connection's next segment; queued, not yet sent */
 } otcps;
+/* a TCP connection: congestion window and the queue of its unsent segments */
+typedef struct otcpc {
+  uint32_t src, dst, cwnd, ssthresh, cnt, flight, queued, head, tail, acks, broken;
+  uint64_t acked;
+  int64_t rto_win;          /* start of the window of its last cwnd collapse */
+} otcpc;
+#define TCP_NOSEG 0xFFFFFFFFu
+#define TCP_IW 10u
+#define TCP_CWND_CLAMP 65535u
 typedef struct otack { uint32_t src, dst, seq; int64_t t; } otack;
 
 static int fail(tgo_ctx* c, int code, const char* fmt, ...) {
@@ -343,7 +354,7 @@ int tgo_create(const tgsim_config* cfg, tgo_ctx** out) {
 void tgo_destroy(tgo_ctx* c) {
   if (!c) return;
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
-  free(c->tw); free(c->tsg); free(c->tpend); free(c->tack);
+  free(c->tw); free(c->tsg); free(c->tpend); free(c->tack); free(c->tc);
   free(c->pr); free(c->pr_order); free(c->pr_out);
   free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
@@ -1611,6 +1622,7 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
 
 int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tc_n) return fail(c, TGSIM_ESTATE, "a context with connections writes through tcp_write");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   size_t nseg = 0;
@@ -1632,13 +1644,13 @@ int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   size_t k = 0;
   for (size_t i = 0; i < n; ++i) {
     const uint32_t size = m->size[i], ns = size ? (size + c->tcp.mss - 1) / c->tcp.mss : 1;
-    otcpw w = {m->src[i], m->dst[i], ns, TGSIM_TCP_PENDING, INT64_MIN};
+    otcpw w = {m->src[i], m->dst[i], ns, TGSIM_TCP_PENDING, INT64_MIN, TCP_NOSEG};
     const uint32_t wi = (uint32_t)c->tw_n++;
     c->tw[wi] = w;
     for (uint32_t j = 0; j < ns; ++j, ++k) {
       const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
       const uint32_t sid = (uint32_t)c->tsg_n++;
-      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0};
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 0};
       c->tsg[sid] = g;
       src[k] = w.src; dst[k] = w.dst; seq[k] = sid << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
     }
@@ -1650,6 +1662,127 @@ int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   c->tstats.writes += n;
   c->tstats.segments += k;
   c->tstats.packets += k;
+  return TGSIM_OK;
+}
+
+/* ---- connections: congestion window and ACK clocking (acks = 1) ------------
+ * Reno [EXT Linux tcp_cong.c, RFC 5681]: IW10, slow start below ssthresh, one segment per cwnd ACKs
+ * above, ssthresh = max(cwnd / 2, 2) and cwnd = 1 at a window's first retransmission timeout. */
+
+typedef struct { uint32_t* src; uint32_t* dst; uint32_t* seq; uint32_t* size; int64_t* t; size_t n, cap; } ostage;
+static int ostage_push(ostage* b, uint32_t src, uint32_t dst, uint32_t seq, uint32_t size, int64_t t) {
+  if (b->n == b->cap) {
+    size_t nc = b->cap ? 2 * b->cap : 256;
+    uint32_t* a = realloc(b->src, nc * 4); if (!a) return TGSIM_ENOMEM; b->src = a;
+    a = realloc(b->dst, nc * 4); if (!a) return TGSIM_ENOMEM; b->dst = a;
+    a = realloc(b->seq, nc * 4); if (!a) return TGSIM_ENOMEM; b->seq = a;
+    a = realloc(b->size, nc * 4); if (!a) return TGSIM_ENOMEM; b->size = a;
+    int64_t* q = realloc(b->t, nc * 8); if (!q) return TGSIM_ENOMEM; b->t = q;
+    b->cap = nc;
+  }
+  b->src[b->n] = src; b->dst[b->n] = dst; b->seq[b->n] = seq; b->size[b->n] = size; b->t[b->n] = t; ++b->n;
+  return TGSIM_OK;
+}
+static int ostage_flush(tgo_ctx* c, ostage* b) {
+  int rc = TGSIM_OK;
+  if (b->n) {
+    tgsim_msg_soa m = {b->src, b->dst, b->seq, b->size, b->t};
+    rc = enqueue_impl(c, &m, b->n);
+    c->tstats.packets += b->n;
+  }
+  free(b->src); free(b->dst); free(b->seq); free(b->size); free(b->t);
+  return rc;
+}
+
+/* connection k sends queued segments while its flight is below cwnd, each at max(written, t0) */
+static int conn_release(tgo_ctx* c, uint32_t k, int64_t t0, ostage* b) {
+  otcpc* q = &c->tc[k];
+  while (q->flight < q->cwnd && q->head != TCP_NOSEG) {
+    const uint32_t sid = q->head;
+    otcps* g = &c->tsg[sid];
+    const int64_t t = g->t_att > t0 ? g->t_att : t0;
+    g->t_att = t;
+    g->unsent = 0;
+    q->head = g->next;
+    q->queued--;
+    q->flight++;
+    if (ostage_push(b, q->src, q->dst, sid << 4, g->wire, t)) return TGSIM_ENOMEM;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* conn_out) {
+  if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->tw_n && !c->tc_n) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
+  if (n && (!src || !dst)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i)
+    if (src[i] >= c->N || dst[i] >= c->N) return fail(c, TGSIM_EINVAL, "connection %zu: bad instance id", i);
+  if (c->tc_n + n > c->tcp.max_writes) return fail(c, TGSIM_ECAPACITY, "connection capacity");
+  if (grow((void**)&c->tc, &c->tc_cap, c->tc_n + n + 1, sizeof(otcpc))) return fail(c, TGSIM_ENOMEM, "oom");
+  for (size_t i = 0; i < n; ++i) {
+    otcpc q = {src[i], dst[i], TCP_IW, 0x7FFFFFFFu, 0, 0, 0, TCP_NOSEG, TCP_NOSEG, 0, 0, 0, INT64_MIN};
+    if (conn_out) conn_out[i] = (uint32_t)c->tc_n;
+    c->tc[c->tc_n++] = q;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_tcp_write(tgo_ctx* c, const uint32_t* conn, const uint32_t* size, const int64_t* t, size_t n) {
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (n && (!conn || !size || !t)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  size_t nseg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (conn[i] >= c->tc_n) return fail(c, TGSIM_EINVAL, "write %zu: no connection %u", i, conn[i]);
+    if (t[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
+    if (size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
+    nseg += size[i] ? (size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
+  }
+  if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + nseg > c->tcp.max_segments)
+    return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  if (grow((void**)&c->tw, &c->tw_cap, c->tw_n + n + 1, sizeof(otcpw)) ||
+      grow((void**)&c->tsg, &c->tsg_cap, c->tsg_n + nseg + 1, sizeof(otcps)))
+    return fail(c, TGSIM_ENOMEM, "oom");
+  for (size_t i = 0; i < n; ++i) {
+    otcpc* q = &c->tc[conn[i]];
+    const uint32_t sz = size[i], ns = sz ? (sz + c->tcp.mss - 1) / c->tcp.mss : 1;
+    const uint32_t wi = (uint32_t)c->tw_n++;
+    otcpw w = {q->src, q->dst, ns, TGSIM_TCP_PENDING, INT64_MIN, conn[i]};
+    c->tw[wi] = w;
+    for (uint32_t j = 0; j < ns; ++j) {
+      const uint32_t pay = sz ? (j + 1 < ns ? c->tcp.mss : sz - j * c->tcp.mss) : 0;
+      const uint32_t sid = (uint32_t)c->tsg_n++;
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, t[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 1};
+      c->tsg[sid] = g;
+      if (q->tail != TCP_NOSEG) c->tsg[q->tail].next = sid;
+      if (q->head == TCP_NOSEG) q->head = sid;
+      q->tail = sid;
+      q->queued++;
+    }
+  }
+  c->tstats.writes += n;
+  c->tstats.segments += nseg;
+  /* what the windows have room for leaves now, at its write time */
+  ostage b = {0};
+  int rc = TGSIM_OK;
+  for (uint32_t k = 0; k < c->tc_n && !rc; ++k)
+    if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &b);
+  const int rc2 = ostage_flush(c, &b);
+  return rc ? fail(c, rc, "oom") : rc2;
+}
+
+int tgo_tcp_conns(tgo_ctx* c, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd, uint32_t* flight,
+                  uint32_t* queued) {
+  if ((uint64_t)first + n > c->tc_n) return fail(c, TGSIM_EINVAL, "connections [%u, +%zu) out of range", first, n);
+  for (size_t i = 0; i < n; ++i) {
+    const otcpc* q = &c->tc[first + i];
+    if (acked) acked[i] = q->acked;
+    if (cwnd) cwnd[i] = q->cwnd;
+    if (flight) flight[i] = q->flight;
+    if (queued) queued[i] = q->queued;
+  }
   return TGSIM_OK;
 }
 
@@ -1766,7 +1899,10 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     if (s->seq[i] & TGSIM_TCP_ACK_BIT) continue;
     const uint8_t code = c->status[i] & 0x0Fu;
     otcps* g = &c->tsg[s->seq[i] >> 4];
-    if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, done);
+    if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) {
+      tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, done);
+      if (c->tw[g->w].conn != TCP_NOSEG) c->tc[c->tw[g->w].conn].broken = 1;  /* the connection is reset */
+    }
   }
   uint32_t* touched = (uint32_t*)malloc((c->out.n + 1) * 4);
   if (!touched || grow((void**)&c->tack, &c->tack_cap, c->tack_n + c->out.n + 1, sizeof(otack))) {
@@ -1779,7 +1915,12 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     const int intact = !(r->meta & TGSIM_F_CORRUPT);
     otcps* g = &c->tsg[(r->seq & ~TGSIM_TCP_ACK_BIT) >> 4];
     if (r->seq & TGSIM_TCP_ACK_BIT) {
-      if (intact) g->acked = 1;
+      /* the first intact ACK of a segment that has not given up settles it (its flight slot) */
+      if (intact && !g->acked && !g->gave_up) {
+        g->acked = 1;
+        const uint32_t k = c->tw[g->w].conn;
+        if (k != TCP_NOSEG) c->tc[k].acks++;
+      }
       continue;
     }
     if (!intact) continue;
@@ -1799,7 +1940,35 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     if (--w->remaining == 0) tcp_finish(c, g->w, TGSIM_TCP_DELIVERED, w->t, done);
   }
   free(touched);
-  return TGSIM_OK;
+  /* connections: the window's first ACKs free flight and open cwnd; the window's end releases what
+   * now fits; a reset connection fails its queued writes */
+  ostage b = {0};
+  int rc = TGSIM_OK;
+  for (uint32_t k = 0; k < c->tc_n && !rc; ++k) {
+    otcpc* q = &c->tc[k];
+    q->flight -= q->acks;
+    q->acked += q->acks;
+    for (uint32_t a = 0; a < q->acks; ++a) {
+      if (q->cwnd < q->ssthresh) ++q->cwnd;
+      else if (++q->cnt >= q->cwnd) { ++q->cwnd; q->cnt = 0; }
+      if (q->cwnd > TCP_CWND_CLAMP) q->cwnd = TCP_CWND_CLAMP;
+    }
+    q->acks = 0;
+    if (q->broken) {
+      while (q->head != TCP_NOSEG) {
+        otcps* g = &c->tsg[q->head];
+        tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att > c->t_end ? g->t_att : c->t_end, done);
+        g->unsent = 0;
+        g->gave_up = 1;
+        q->head = g->next;
+      }
+      q->queued = 0;
+      continue;
+    }
+    rc = conn_release(c, k, c->t_end, &b);
+  }
+  const int rc2 = ostage_flush(c, &b);
+  return rc ? fail(c, rc, "oom") : rc2;
 }
 
 typedef struct { int64_t t; uint32_t sid; } otx;
@@ -1878,15 +2047,26 @@ static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
   size_t nd = 0, done = 0;
   for (size_t sid = 0; sid < c->tsg_n; ++sid) {
     otcps* g = &c->tsg[sid];
-    if (g->acked || g->gave_up || g->t_att >= H) continue;  /* settled, or its attempt not yet sent */
+    if (g->acked || g->gave_up || g->unsent || g->t_att >= H) continue;  /* settled, or its attempt not yet sent */
     const uint32_t st = c->tw[g->w].state;
     if (st == TGSIM_TCP_TIMEOUT || st == TGSIM_TCP_REFUSED) continue;
     const int64_t T = g->t_att + (c->tcp.rto_ns << g->attempt);
     if (T >= t_end) continue;
+    const uint32_t k = c->tw[g->w].conn;
     if (g->attempt + 1 >= c->tcp.max_attempts) {
       g->gave_up = 1;
+      if (k != TCP_NOSEG) c->tc[k].flight--;
       tcp_finish(c, g->w, TGSIM_TCP_TIMEOUT, T, &done);
       continue;
+    }
+    if (k != TCP_NOSEG && c->tc[k].rto_win != H) {  /* the connection's first timeout in this window */
+      otcpc* q = &c->tc[k];
+      q->rto_win = H;
+      /* a new loss episode halves ssthresh; cwnd = 1 with no ACK since means the same episode
+       * (tcp_enter_loss recomputes ssthresh once per episode [EXT]) */
+      if (q->cwnd > 1) q->ssthresh = q->cwnd / 2 > 2 ? q->cwnd / 2 : 2;
+      q->cwnd = 1;
+      q->cnt = 0;
     }
     g->attempt++;
     g->t_att = T > H ? T : H;
@@ -1922,6 +2102,16 @@ int tgo_tcp_writes(tgo_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n
   for (size_t i = 0; i < c->tw_n; ++i) {
     if (state) state[i] = (uint8_t)c->tw[i].state;
     if (t) t[i] = c->tw[i].state == TGSIM_TCP_PENDING ? INT64_MIN : c->tw[i].t;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_tcp_writes_range(tgo_ctx* c, uint64_t first, size_t n, uint8_t* state, int64_t* t) {
+  if (first + n > c->tw_n) return fail(c, TGSIM_EINVAL, "writes [%llu, +%zu) out of range", (unsigned long long)first, n);
+  for (size_t i = 0; i < n; ++i) {
+    const otcpw* w = &c->tw[first + i];
+    if (state) state[i] = (uint8_t)w->state;
+    if (t) t[i] = w->state == TGSIM_TCP_PENDING ? INT64_MIN : w->t;
   }
   return TGSIM_OK;
 }

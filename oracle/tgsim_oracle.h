@@ -62,6 +62,11 @@ int tgo_tcp_send(tgo_ctx* ctx, const tgsim_msg_soa* writes, size_t n);
 int tgo_tcp_react(tgo_ctx* ctx, size_t* n_completed);
 int tgo_tcp_writes(tgo_ctx* ctx, uint8_t* state_out, int64_t* t_out, size_t cap, size_t* n);
 int tgo_tcp_get_stats(tgo_ctx* ctx, tgsim_tcp_stats* out);
+int tgo_tcp_writes_range(tgo_ctx* ctx, uint64_t first, size_t n, uint8_t* state_out, int64_t* t_out);
+int tgo_tcp_connect(tgo_ctx* ctx, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* conn_out);
+int tgo_tcp_write(tgo_ctx* ctx, const uint32_t* conn, const uint32_t* size, const int64_t* t_send, size_t n);
+int tgo_tcp_conns(tgo_ctx* ctx, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd, uint32_t* flight,
+                  uint32_t* queued);
 int tgo_tcp_gen_storm_round(tgo_ctx* ctx, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                             int64_t spread_ns, uint32_t state);
 int tgo_advance_begin(tgo_ctx* ctx, int64_t t_end);

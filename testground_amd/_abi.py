@@ -170,6 +170,10 @@ _SIGS = {
     "tcp_writes": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "tcp_get_stats": (C.c_int, [P, C.POINTER(TcpStats)]),
     "tcp_gen_storm_round": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32]),
+    "tcp_writes_range": (C.c_int, [P, C.c_uint64, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "tcp_connect": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "tcp_write": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tcp_conns": (C.c_int, [P, C.c_uint32, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "probe_setup": (C.c_int, [P, C.c_void_p, C.c_uint32, C.POINTER(ProbeConfig)]),
     "probe_start": (C.c_int, [P, C.c_int64]),
     "probe_react": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_uint32)]),

@@ -95,6 +95,16 @@ struct TcpDev {
   uint32_t* pend[2] = {nullptr, nullptr};
   uint32_t* pend_by = nullptr;    // [N] retransmissions pending (or released into the open window) per sender
   TcpScalars* sc = nullptr;
+  // connections (tgsim_tcp_connect): Reno window and the queue of unsent segments
+  // (a chain through s_next from c_head); w_conn / s_ack1 exist in acks mode
+  uint32_t n_conn = 0;
+  uint32_t *c_src = nullptr, *c_dst = nullptr, *c_cwnd = nullptr, *c_ssth = nullptr, *c_cnt = nullptr;
+  uint32_t *c_flight = nullptr, *c_queued = nullptr, *c_head = nullptr, *c_acks = nullptr, *c_broken = nullptr;
+  unsigned long long* c_acked = nullptr;  // cumulative first ACKs
+  int64_t* c_rto = nullptr;       // start of the window of the connection's last cwnd collapse
+  uint32_t* w_conn = nullptr;     // [W] the write's connection (kNoSeg: tgsim_tcp_send writes)
+  uint32_t* s_next = nullptr;     // [S] the connection's next segment
+  uint32_t* s_ack1 = nullptr;     // [S] first-ACK claim (a segment frees one flight slot once)
   uint32_t mss = 0, hdr = 0, max_att = 0;
   int64_t rto = 0;
   uint64_t cap_w = 0, cap_s = 0;
@@ -273,7 +283,8 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
                                             uint32_t add_target, int64_t add_twait);
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, bool acks, uint32_t mult);  // retx: TCP pending per sender
+// retx: TCP pending per sender; inbox_mult: acks mode, packets per delivery of the sender's last inbox
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult);
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part
 hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);
@@ -329,6 +340,13 @@ hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_de
                                    bool reg, uint32_t lo, uint32_t hi);
 // TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
+// connections: new segments linked to their queues (links: n quads conn, old tail, first, count),
+// then every connection sends what its window has room for, at max(written, t0) (t0 = INT64_MIN:
+// at the write times; after_window: first apply the window's ACKs and resets, t0 = the window's
+// end), staged behind sc->n_msgs_dev (set from base_host unless base_dev), timers on pend[cur]
+hipError_t launch_tcp_link(Dev& d, TcpDev& t, const uint32_t* links, uint32_t n);
+hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, bool after_window, uint32_t cur, bool base_dev,
+                                   uint32_t base_host);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
 
 // Sequential probes: every local prober without a probe sends its first at t0 (device staging

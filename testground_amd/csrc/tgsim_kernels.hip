@@ -1211,12 +1211,12 @@ __device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uin
 // window): pend + mult * (retransmissions released into the window + the deliveries the sender got
 // last window, each answered by at most one ACK).
 __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const uint32_t* retx, const uint32_t* inbox,
-                                                     uint32_t mult, uint32_t nloc, uint32_t* out) {
+                                                     uint32_t inbox_mult, uint32_t mult, uint32_t nloc, uint32_t* out) {
   __shared__ uint32_t red[kBlock / 64];
   uint32_t mx = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock) {
     uint64_t v = pend[i];
-    if (inbox) v += (uint64_t)mult * ((uint64_t)retx[i] + (inbox[i + 1] - inbox[i]));
+    if (inbox) v += (uint64_t)mult * ((uint64_t)retx[i] + (uint64_t)inbox_mult * (inbox[i + 1] - inbox[i]));
     else if (retx) v = (uint64_t)mult * (v + retx[i]);
     mx = max(mx, (uint32_t)min<uint64_t>(v, 0xFFFFFFFFull));
   }
@@ -3416,10 +3416,10 @@ hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
   return hipGetLastError();
 }
 
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, bool acks, uint32_t mult) {
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult) {
   TG_CHECK(hipMemsetAsync(&d.sc->pend_max, 0, sizeof(uint32_t), d.stream));
   hipLaunchKernelGGL(k_pend_max, dim3(std::min<unsigned>(grid_for(d.nloc), 1024u)), dim3(kBlock), 0, d.stream, d.pend,
-                     retx, acks ? d.inbox : nullptr, mult, d.nloc, &d.sc->pend_max);
+                     retx, inbox_mult ? d.inbox : nullptr, inbox_mult, mult, d.nloc, &d.sc->pend_max);
   return hipGetLastError();
 }
 

@@ -110,6 +110,11 @@ struct tgsim_ctx {
   // yet in one, and the batch the open window registered (its timer range is filled at the reaction)
   uint32_t tcp_nb = 0, tcp_fill = ~0u;
   uint64_t tcp_seg_batched = 0;
+  // connections: host copies of their ends and queue tails; link scratch
+  std::vector<uint32_t> conn_src, conn_dst, conn_tail;
+  uint32_t conn_cap = 0;
+  uint32_t* link_dev = nullptr;
+  size_t link_cap = 0;
   // the reactions' counters land in two pinned snapshots (read once their event has completed);
   // nothing on the window path reads them (the queue-limit bound folds the pending retransmissions
   // into the occupancy: tgsim_tcp.hip)
@@ -1104,6 +1109,10 @@ static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_
   return TGSIM_OK;
 }
 
+// acks mode: packets a sender can stage per delivery it got last window - one ACK per data copy,
+// and with connections up to two segments more per ACK (slow start: a flight slot and a cwnd step)
+static uint32_t tcp_inbox_mult(const tgsim_ctx* c) { return c->td.n_conn ? 3u : 1u; }
+
 // The window's queue-limit test. The kernels test every sender only when the host
 // cannot prove that none can reach the limit: pend_bound (queued copies of any sender at this
 // window's start) + mult * (the most messages one sender can have staged) <= TGSIM_NETEM_LIMIT.
@@ -1116,8 +1125,8 @@ static int plan_queue_limit(tgsim_ctx* c) {
   // inconclusive: refresh the bound with the exact maximum (one sync) - unless the window's own
   // staging bound already reaches the limit, when no refresh can close the gate
   if (gate && !c->pend_exact && mult * m_max <= TGSIM_NETEM_LIMIT) {
-    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks, (uint32_t)mult),
-          "pend max");
+    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks ? tcp_inbox_mult(c) : 0u,
+                             (uint32_t)mult), "pend max");
     HIPCK(c, sync_scalars(d), "sync");
     c->pend_bound = d.h_sc->pend_max;
     c->pend_exact = true;
@@ -1138,7 +1147,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
     d.heavy.m_inbox = c->win_m_inbox;
     if (c->tcp_on && c->tcp.acks) {  // ACKs: at most one per delivery the sender got last window
       d.heavy.inbox = d.inbox;
-      d.heavy.m_inbox = 1;
+      d.heavy.m_inbox = tcp_inbox_mult(c);
     }
     d.heavy.mult = (uint32_t)mult;
   }
@@ -1163,6 +1172,7 @@ static int begin_common(tgsim_ctx* c) {
     if (c->tcp.acks) {
       // the last reaction's ACKs and the due timers join the staged packets behind the device-side
       // count; the window's new segments (all staged now) register one timer batch
+      if (c->td.n_conn) c->tcp_seg_batched = c->tsg_n;  // connection segments' timers ride the pend lists
       const bool reg = c->tsg_n > c->tcp_seg_batched;
       HIPCK(c, launch_tcp_release_acks(c->d, c->td, c->tcp_cur, c->staged_dev, c->n_staged, c->tcp_nb, reg,
                                        (uint32_t)c->tcp_seg_batched, (uint32_t)c->tsg_n), "tcp release");
@@ -2340,6 +2350,7 @@ static int tgsim_tcp_send_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   c->spec.valid = false;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->td.n_conn) return fail(c, TGSIM_ESTATE, "a context with connections writes through tgsim_tcp_write");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
@@ -2416,6 +2427,10 @@ static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   const bool on_dev = c->n_status_last == kStatusOnDevice;
   HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
                             on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch, c->tcp_fill), "tcp react");
+  if (c->td.n_conn) {  // the window's ACKs open the connections' windows: send what fits, at its end
+    HIPCK(c, launch_tcp_conn_release(c->d, c->td, true, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
+    c->staged_dev = true;
+  }
   c->tcp_fill = ~0u;
   c->tcp_need_react = false;
   // the counters into the next pinned snapshot, behind the reaction on the stream
@@ -2519,6 +2534,7 @@ static int tgsim_tcp_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t 
                                          int64_t spread_ns, uint32_t state) {
   if (!c) return TGSIM_EINVAL;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->td.n_conn) return fail(c, TGSIM_ESTATE, "a context with connections writes through tgsim_tcp_write");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
   if (size > c->tcp.mss) return fail(c, TGSIM_EINVAL, "a storm write must fit one segment");
   if (fanout == 0 || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
@@ -2534,6 +2550,230 @@ static int tgsim_tcp_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t 
   c->tstats.writes += n;
   c->tstats.segments += n;
   c->tstats.packets += n;
+  return TGSIM_OK;
+}
+
+// ---- TCP connections: congestion window and ACK clocking -------------------
+
+static int tgsim_tcp_writes_range_body(tgsim_ctx* c, uint64_t first, size_t n, uint8_t* state, int64_t* t);
+extern "C" int tgsim_tcp_writes_range(tgsim_ctx* c, uint64_t first, size_t n, uint8_t* state, int64_t* t) {
+  return abi_guard(c, [&] { return tgsim_tcp_writes_range_body(c, first, n, state, t); });
+}
+static int tgsim_tcp_writes_range_body(tgsim_ctx* c, uint64_t first, size_t n, uint8_t* state, int64_t* t) {
+  if (!c) return TGSIM_EINVAL;
+  if (first + n > c->tw_n) return fail(c, TGSIM_EINVAL, "writes [%llu, +%zu) out of range", (unsigned long long)first, n);
+  if (!n || !c->tcp_on) return TGSIM_OK;
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  std::vector<uint32_t> st(n);
+  std::vector<int64_t> ta(n), tf(n);
+  HIPCK(c, hipMemcpy(st.data(), c->td.w_state + first, n * 4, hipMemcpyDeviceToHost), "tcp writes");
+  HIPCK(c, hipMemcpy(ta.data(), c->td.w_tarr + first, n * 8, hipMemcpyDeviceToHost), "tcp writes");
+  HIPCK(c, hipMemcpy(tf.data(), c->td.w_fail + first, n * 8, hipMemcpyDeviceToHost), "tcp writes");
+  for (size_t i = 0; i < n; ++i) {  // the decoding of tgsim_tcp_writes
+    uint32_t s_i = ta[i] != INT64_MIN ? (uint32_t)TGSIM_TCP_DELIVERED : st[i];
+    int64_t t_i = ta[i];
+    if (s_i != TGSIM_TCP_PENDING && s_i != TGSIM_TCP_DELIVERED) {
+      t_i = tf[i] >> 1;
+      s_i = (tf[i] & 1) ? TGSIM_TCP_TIMEOUT : TGSIM_TCP_REFUSED;
+    } else if (s_i == TGSIM_TCP_PENDING) {
+      t_i = INT64_MIN;
+    }
+    if (state) state[i] = (uint8_t)s_i;
+    if (t) t[i] = t_i;
+  }
+  return TGSIM_OK;
+}
+
+// grow the device connection arrays to hold `need` connections (copying the live ones)
+static int conn_grow(tgsim_ctx* c, uint32_t need) {
+  TcpDev& t = c->td;
+  if (need <= c->conn_cap) return TGSIM_OK;
+  const uint32_t cap = std::max<uint32_t>({need, 2 * c->conn_cap, 1024u});
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  uint32_t** u32[] = {&t.c_src, &t.c_dst, &t.c_cwnd, &t.c_ssth, &t.c_cnt, &t.c_flight, &t.c_queued, &t.c_head,
+                      &t.c_acks, &t.c_broken};
+  for (uint32_t** a : u32)
+    if (dgrow(c, a, t.n_conn, cap)) return TGSIM_ENOMEM;
+  if (dgrow(c, &t.c_acked, t.n_conn, cap) || dgrow(c, &t.c_rto, t.n_conn, cap)) return TGSIM_ENOMEM;
+  c->conn_cap = cap;
+  return TGSIM_OK;
+}
+
+static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* out);
+extern "C" int tgsim_tcp_connect(tgsim_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* out) {
+  return abi_guard(c, [&] { return tgsim_tcp_connect_body(c, src, dst, n, out); });
+}
+static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* out) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->tw_n && !c->td.n_conn) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
+  if (n && (!src || !dst)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (size_t i = 0; i < n; ++i)
+    if (src[i] >= c->N || dst[i] >= c->N) return fail(c, TGSIM_EINVAL, "connection %zu: bad instance id", i);
+  TcpDev& t = c->td;
+  if ((uint64_t)t.n_conn + n > c->tcp.max_writes) return fail(c, TGSIM_ECAPACITY, "connection capacity");
+  if (!n) return TGSIM_OK;
+  alloc_point(c);
+  if (!t.w_conn) {  // first connection: the per-write / per-segment connection tables
+    const size_t W = c->tcp.max_writes, S = c->tcp.max_segments;
+    if (dalloc(c, &t.w_conn, W) || dalloc(c, &t.s_next, S) || dalloc(c, &t.s_ack1, S)) return TGSIM_ENOMEM;
+    HIPCK(c, hipMemsetAsync(t.s_ack1, 0, S * 4, c->d.stream), "tcp connect");
+  }
+  const uint32_t n0 = t.n_conn, n1 = (uint32_t)(n0 + n);
+  int rc = conn_grow(c, n1);
+  if (rc) return rc;
+  std::vector<uint32_t> a(src, src + n), b(dst, dst + n), iw(n, 10u), ss(n, 0x7FFFFFFFu), none(n, 0xFFFFFFFFu);
+  std::vector<int64_t> never(n, INT64_MIN);
+  hipStream_t st = c->d.stream;
+  HIPCK(c, hipMemcpyAsync(t.c_src + n0, a.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_dst + n0, b.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_cwnd + n0, iw.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_ssth + n0, ss.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_head + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_rto + n0, never.data(), n * 8, hipMemcpyHostToDevice, st), "tcp connect");
+  for (uint32_t* z : {t.c_cnt, t.c_flight, t.c_queued, t.c_acks, t.c_broken})
+    HIPCK(c, hipMemsetAsync(z + n0, 0, n * 4, st), "tcp connect");
+  HIPCK(c, hipMemsetAsync(t.c_acked + n0, 0, n * 8, st), "tcp connect");
+  HIPCK(c, hipStreamSynchronize(st), "tcp connect");  // the host vectors go out of scope
+  c->conn_src.insert(c->conn_src.end(), src, src + n);
+  c->conn_dst.insert(c->conn_dst.end(), dst, dst + n);
+  c->conn_tail.resize(n1, 0xFFFFFFFFu);
+  for (size_t i = 0; i < n; ++i)
+    if (out) out[i] = n0 + (uint32_t)i;
+  t.n_conn = n1;
+  return TGSIM_OK;
+}
+
+static int tgsim_tcp_write_body(tgsim_ctx* c, const uint32_t* conn, const uint32_t* size, const int64_t* t_send, size_t n);
+extern "C" int tgsim_tcp_write(tgsim_ctx* c, const uint32_t* conn, const uint32_t* size, const int64_t* t_send, size_t n) {
+  return abi_guard(c, [&] { return tgsim_tcp_write_body(c, conn, size, t_send, n); });
+}
+static int tgsim_tcp_write_body(tgsim_ctx* c, const uint32_t* conn, const uint32_t* size, const int64_t* t_send,
+                                size_t n) {
+  if (!c) return TGSIM_EINVAL;
+  c->spec.valid = false;
+  if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (n && (!conn || !size || !t_send)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  TcpDev& td = c->td;
+  size_t nseg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (conn[i] >= td.n_conn) return fail(c, TGSIM_EINVAL, "write %zu: no connection %u", i, conn[i]);
+    if (t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
+    if (size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
+    nseg += size[i] ? (size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
+  }
+  if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + nseg > c->tcp.max_segments)
+    return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  if (!n) return TGSIM_OK;
+  alloc_point(c);
+  // write table (src, dst, segments, connection), segment table (write | sole, wire size, written
+  // at, next on the connection) and one link per touched connection
+  std::vector<uint32_t> w4(4 * n), s3(3 * nseg);
+  std::vector<int64_t> s_t(nseg);
+  std::vector<uint32_t> tail = c->conn_tail;  // updated copy: committed once the uploads are issued
+  std::unordered_map<uint32_t, uint32_t> link_of;  // connection -> its quad
+  std::vector<uint32_t> quads;
+  size_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t cn = conn[i], sz = size[i], ns = sz ? (sz + c->tcp.mss - 1) / c->tcp.mss : 1;
+    const uint32_t wi = (uint32_t)(c->tw_n + i);
+    w4[i] = c->conn_src[cn]; w4[n + i] = c->conn_dst[cn]; w4[2 * n + i] = ns; w4[3 * n + i] = cn;
+    for (uint32_t j = 0; j < ns; ++j, ++k) {
+      const uint32_t pay = sz ? (j + 1 < ns ? c->tcp.mss : sz - j * c->tcp.mss) : 0;
+      const uint32_t sid = (uint32_t)(c->tsg_n + k);
+      s3[k] = wi | (ns == 1 ? 0x80000000u : 0u);
+      s3[nseg + k] = pay + c->tcp.header_bytes;
+      s3[2 * nseg + k] = 0xFFFFFFFFu;
+      s_t[k] = t_send[i];
+      auto it = link_of.find(cn);
+      if (it == link_of.end()) {  // the batch's first segment on cn: linked to the device queue
+        link_of.emplace(cn, (uint32_t)(quads.size() / 4));
+        quads.insert(quads.end(), {cn, tail[cn], sid, 0u});
+      } else {                    // chained to the batch's previous segment on cn, here
+        s3[2 * nseg + (tail[cn] - (uint32_t)c->tsg_n)] = sid;
+      }
+      quads[4 * link_of[cn] + 3] += 1;
+      tail[cn] = sid;
+    }
+  }
+  uint8_t* pin = nullptr;
+  int rc = pin_acquire(c, c->pin_tcp, 16 * n + 20 * nseg + 4 * quads.size(), &pin);
+  if (rc) return rc;
+  uint8_t* pt = pin;
+  uint8_t* pw = pt + 8 * nseg;
+  uint8_t* ps = pw + 16 * n;
+  uint8_t* pq = ps + 12 * nseg;
+  memcpy(pt, s_t.data(), 8 * nseg);
+  memcpy(pw, w4.data(), 16 * n);
+  memcpy(ps, s3.data(), 12 * nseg);
+  memcpy(pq, quads.data(), 4 * quads.size());
+  const uint32_t nq = (uint32_t)(quads.size() / 4);
+  if (quads.size() > c->link_cap) {
+    HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+    dfree(c, c->link_dev);
+    c->link_dev = nullptr;
+    const size_t cap = std::max<size_t>(quads.size(), 2 * c->link_cap);
+    if (dalloc(c, &c->link_dev, cap)) return TGSIM_ENOMEM;
+    c->link_cap = cap;
+  }
+  hipStream_t st = c->d.stream;
+  const uint64_t w0 = c->tw_n, s0 = c->tsg_n;
+  HIPCK(c, hipMemcpyAsync(td.s_tatt + s0, pt, 8 * nseg, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.w_src + w0, pw, 4 * n, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.w_dst + w0, pw + 4 * n, 4 * n, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.w_rem + w0, pw + 8 * n, 4 * n, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.w_conn + w0, pw + 12 * n, 4 * n, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.s_w + s0, ps, 4 * nseg, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.s_wire + s0, ps + 4 * nseg, 4 * nseg, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(td.s_next + s0, ps + 8 * nseg, 4 * nseg, hipMemcpyHostToDevice, st), "tcp write");
+  HIPCK(c, hipMemcpyAsync(c->link_dev, pq, 4 * quads.size(), hipMemcpyHostToDevice, st), "tcp write");
+  rc = pin_issued(c, c->pin_tcp);
+  if (rc) return rc;
+  HIPCK(c, launch_tcp_link(c->d, td, c->link_dev, nq), "tcp write");
+  // the windows' room goes now, at the write times
+  HIPCK(c, launch_tcp_conn_release(c->d, td, false, c->tcp_cur, c->staged_dev, c->n_staged), "tcp write");
+  c->staged_dev = true;
+  c->conn_tail.swap(tail);
+  for (size_t i = 0; i < n; ++i) {  // the queue-limit bound: a sender's new segments (any may leave now)
+    const uint32_t src = c->conn_src[conn[i]];
+    if (!is_local(c, src)) continue;
+    const uint32_t l = src - c->lo, ns = size[i] ? (size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
+    if (c->hcnt[l] == 0) c->hcnt_touched.push_back(l);
+    c->hcnt[l] += ns;
+    c->win_m_host = std::max(c->win_m_host, c->hcnt[l]);
+    c->max_tsend_h = std::max(c->max_tsend_h, t_send[i]);
+  }
+  c->tw_n += n;
+  c->tsg_n += nseg;
+  c->tcp_seg_batched = c->tsg_n;  // no timer batches: released segments' timers ride the pend lists
+  c->tstats.writes += n;
+  c->tstats.segments += nseg;
+  return TGSIM_OK;
+}
+
+static int tgsim_tcp_conns_body(tgsim_ctx* c, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd,
+                                uint32_t* flight, uint32_t* queued);
+extern "C" int tgsim_tcp_conns(tgsim_ctx* c, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd,
+                               uint32_t* flight, uint32_t* queued) {
+  return abi_guard(c, [&] { return tgsim_tcp_conns_body(c, first, n, acked, cwnd, flight, queued); });
+}
+static int tgsim_tcp_conns_body(tgsim_ctx* c, uint32_t first, size_t n, uint64_t* acked, uint32_t* cwnd,
+                                uint32_t* flight, uint32_t* queued) {
+  if (!c) return TGSIM_EINVAL;
+  const TcpDev& t = c->td;
+  if ((uint64_t)first + n > t.n_conn) return fail(c, TGSIM_EINVAL, "connections [%u, +%zu) out of range", first, n);
+  if (!n) return TGSIM_OK;
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  if (acked) HIPCK(c, hipMemcpy(acked, t.c_acked + first, n * 8, hipMemcpyDeviceToHost), "tcp conns");
+  if (cwnd) HIPCK(c, hipMemcpy(cwnd, t.c_cwnd + first, n * 4, hipMemcpyDeviceToHost), "tcp conns");
+  if (flight) HIPCK(c, hipMemcpy(flight, t.c_flight + first, n * 4, hipMemcpyDeviceToHost), "tcp conns");
+  if (queued) HIPCK(c, hipMemcpy(queued, t.c_queued + first, n * 4, hipMemcpyDeviceToHost), "tcp conns");
   return TGSIM_OK;
 }
 

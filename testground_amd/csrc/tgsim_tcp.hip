@@ -42,6 +42,8 @@ constexpr uint32_t kRetxBit = 0x40000000u;  // s_w, acks mode: the segment was r
 constexpr uint32_t kPlanLds = 1024;         // k_tcp_fire: timer plans up to this many batches are searched in LDS
 constexpr uint32_t kFireRounds = 8;         // k_tcp_fire: rounds of entries per block reservation (mask bits)
 constexpr uint32_t kFireUnroll = 4;         // k_tcp_fire: entries whose loads are in flight together
+constexpr uint32_t kNoSeg = 0xFFFFFFFFu;    // connections: end of a segment chain / no connection
+constexpr uint32_t kCwndClamp = 65535u;    // Linux snd_cwnd_clamp (Reno window in segments)
 
 __device__ __forceinline__ uint32_t tcp_copies(uint8_t st) {
   const uint32_t code = st & 0x0Fu;
@@ -113,7 +115,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict
         t.s_out[sid] = q;
         t.s_w[sid] = (t.s_w[sid] & ~(3u << kQShift)) | (q << kQShift);
       } else if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) {
-        tcp_fail(t, t.s_w[sid] & kWMask, t.s_tatt[sid], TGSIM_TCP_REFUSED);
+        const uint32_t w = t.s_w[sid] & kWMask;
+        tcp_fail(t, w, t.s_tatt[sid], TGSIM_TCP_REFUSED);
+        if (t.n_conn && t.w_conn[w] != kNoSeg) t.c_broken[t.w_conn[w]] = 1u;  // the connection is reset
       } else if (!t.acks) {  // acks mode: the attempt's timer decides
         retx = tcp_next(t, sid, t.s_tatt[sid]);
       }
@@ -156,7 +160,15 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
     if (t.acks) {  // acks mode: ACKs settle segments, intact data is answered; timers decide the rest
       bool ack = false, dup = false;
       if (sq & TGSIM_TCP_ACK_BIT) {
-        if (!corrupt) t.s_done[(sq & ~TGSIM_TCP_ACK_BIT) >> 4] = 1;
+        const uint32_t sid = (sq & ~TGSIM_TCP_ACK_BIT) >> 4;
+        // the first intact ACK of a segment that has not given up frees its connection a flight slot
+        if (!corrupt && t.s_done[sid] != 2) {
+          t.s_done[sid] = 1;
+          if (t.n_conn && atomicExch(&t.s_ack1[sid], 1u) == 0u) {
+            const uint32_t k = t.w_conn[t.s_w[sid] & kWMask];
+            if (k != kNoSeg) atomicAdd(&t.c_acks[k], 1u);
+          }
+        }
       } else if (!corrupt) {
         ack = true;
         const uint32_t sid = sq >> 4, sw = t.s_w[sid];
@@ -495,12 +507,21 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
         if (!live[u] || wst[u] == TGSIM_TCP_TIMEOUT || wst[u] == TGSIM_TCP_REFUSED) continue;
         const uint32_t r = r0 + u, w = sw[u] & kWMask;
         const int64_t T = ta[u] + (t.rto << a[u]);
-        if (T >= t_end) {
+        const uint32_t k = t.n_conn ? t.w_conn[w] : kNoSeg;
+        if (T >= t_end || (!batch[u] && ta[u] >= H)) {  // not due, or sent in this window
           if (!batch[u]) kmask |= 1u << r;
         } else if (a[u] + 1u >= t.max_att) {
           t.s_done[sid[u]] = 2;
+          if (k != kNoSeg) atomicSub(&t.c_flight[k], 1u);
           if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, T, TGSIM_TCP_TIMEOUT);
         } else {
+          // the connection's first timeout in this window: ssthresh = max(cwnd / 2, 2), cwnd = 1
+          if (k != kNoSeg && atomicMax(reinterpret_cast<long long*>(&t.c_rto[k]), (long long)H) < (long long)H) {
+            const uint32_t cw = t.c_cwnd[k];
+            if (cw > 1u) t.c_ssth[k] = cw / 2u > 2u ? cw / 2u : 2u;  // once per loss episode
+            t.c_cwnd[k] = 1u;
+            t.c_cnt[k] = 0u;
+          }
           t.s_att[sid[u]] = a[u] + 1u;
           t.s_tatt[sid[u]] = T > H ? T : H;
           if (!(sw[u] & kRetxBit)) t.s_w[sid[u]] = sw[u] | kRetxBit;
@@ -542,6 +563,96 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
   }
 }
 
+// Connections: a batch's new segments join their queues. One quad per touched connection (conn,
+// its tail before the batch, the batch's first segment on it, count); the host chained the
+// batch's own segments of a connection already.
+__global__ __launch_bounds__(kBlock) void k_tcp_link(TcpDev t, const uint32_t* __restrict__ q, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = q[4 * i], tail = q[4 * i + 1], first = q[4 * i + 2], cnt = q[4 * i + 3];
+  if (tail != kNoSeg) t.s_next[tail] = first;
+  if (t.c_head[k] == kNoSeg) t.c_head[k] = first;
+  t.c_queued[k] += cnt;
+}
+
+// Every connection sends its queued segments while the flight is below cwnd, at max(written, t0).
+// after_window: first the window's ACKs (flight, slow start / congestion avoidance) and resets (a
+// reset connection fails its queued writes), t0 = the window's end. One thread per connection;
+// staged slots and timer-list slots reserved once per block.
+__global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalars* sc, uint32_t after_window,
+                                                             uint32_t cur, uint32_t cap, uint32_t* __restrict__ m_src,
+                                                             uint32_t* __restrict__ m_dst,
+                                                             uint32_t* __restrict__ m_seq,
+                                                             uint32_t* __restrict__ m_size,
+                                                             int64_t* __restrict__ m_t) {
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t sb_m, sb_p;
+  const int64_t t0 = after_window ? sc->t_end : INT64_MIN;
+  const uint32_t n = t.n_conn;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
+    const uint32_t k = b0 + threadIdx.x;
+    uint32_t go = 0, head = kNoSeg;
+    if (k < n) {
+      uint32_t cw = t.c_cwnd[k], fl = t.c_flight[k];
+      if (after_window) {
+        const uint32_t acks = t.c_acks[k];
+        if (acks) {
+          t.c_acks[k] = 0u;
+          fl -= acks;
+          t.c_acked[k] += acks;
+          uint32_t ss = t.c_ssth[k], cnt = t.c_cnt[k];
+          for (uint32_t a = 0; a < acks; ++a) {
+            if (cw < ss) ++cw;
+            else if (++cnt >= cw) { ++cw; cnt = 0u; }
+            cw = cw > kCwndClamp ? kCwndClamp : cw;
+          }
+          t.c_cwnd[k] = cw;
+          t.c_cnt[k] = cnt;
+          t.c_flight[k] = fl;
+        }
+        if (t.c_broken[k]) {  // a reset connection: its queued writes fail
+          for (uint32_t sid = t.c_head[k]; sid != kNoSeg; sid = t.s_next[sid]) {
+            const int64_t tw = t.s_tatt[sid];
+            t.s_done[sid] = 2;
+            tcp_fail(t, t.s_w[sid] & kWMask, tw > t0 ? tw : t0, TGSIM_TCP_REFUSED);
+          }
+          t.c_head[k] = kNoSeg;
+          t.c_queued[k] = 0u;
+        }
+      }
+      head = t.c_head[k];
+      const uint32_t qd = t.c_queued[k];
+      go = fl < cw ? min(cw - fl, qd) : 0u;
+      if (go) {
+        t.c_flight[k] = fl + go;
+        t.c_queued[k] = qd - go;
+      }
+    }
+    uint32_t tot;
+    const uint32_t pm = block_excl_scan(go, red, tot);
+    if (threadIdx.x == 0) {
+      sb_m = tot ? reserve_staged(&sc->n_msgs_dev, tot, cap) : 0u;
+      sb_p = tot ? atomicAdd(&t.sc->pend_n[cur], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t sid = head;
+    for (uint32_t j = 0; j < go; ++j) {
+      const int64_t tw = t.s_tatt[sid], ts = tw > t0 ? tw : t0;
+      t.s_tatt[sid] = ts;
+      const uint32_t p = sb_m + pm + j;
+      if (p < cap) {
+        m_src[p] = t.c_src[k]; m_dst[p] = t.c_dst[k]; m_seq[p] = sid << 4; m_size[p] = t.s_wire[sid]; m_t[p] = ts;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_M);
+      }
+      t.pend[cur][sb_p + pm + j] = sid;  // its timer
+      sid = t.s_next[sid];
+    }
+    if (go) t.c_head[k] = sid;
+    __syncthreads();  // sb_m / sb_p are rewritten by the next round
+  }
+}
+
 // A generated storm round (staged [base, base + n)) becomes TCP writes: one segment each.
 __global__ __launch_bounds__(kBlock) void k_tcp_adopt(TcpDev t, uint32_t base, uint32_t n, uint32_t wbase,
                                                       uint32_t sbase, uint32_t* __restrict__ m_src,
@@ -563,6 +674,22 @@ hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32
   const unsigned g = std::min<unsigned>((n + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
   hipLaunchKernelGGL(k_tcp_adopt, dim3(g), dim3(kBlock), 0, d.stream, t, base, n, wbase, sbase, d.m_src, d.m_dst,
                      d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_link(Dev& d, TcpDev& t, const uint32_t* links, uint32_t n) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_tcp_link, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, d.stream, t, links, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, bool after_window, uint32_t cur, bool base_dev,
+                                   uint32_t base_host) {
+  if (!t.n_conn) return hipSuccess;
+  if (!base_dev) hipLaunchKernelGGL(k_tcp_base, dim3(1), dim3(kBlock), 0, d.stream, d.sc, base_host);
+  const unsigned g = std::min<unsigned>((t.n_conn + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
+  hipLaunchKernelGGL(k_tcp_conn_release, dim3(g), dim3(kBlock), 0, d.stream, t, d.sc, after_window ? 1u : 0u, cur,
+                     d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 

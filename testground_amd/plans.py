@@ -69,7 +69,9 @@ class PlanEnv:
         # reaction latency of a request/reply hop on an unshaped link (a local HTTP round trip over a
         # bridge is ~100 us): the window of the sequential probes while messages are in flight
         self.probe_window_ns = int(self.params.get("probe_window_ns", 100_000))
-        kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=1024, max_waiters=1 << 16)
+        # plans give instances their own sync states (splitbrain's "reconfigured<host>" callbacks)
+        kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=max(1024, 2 * self.n + 256),
+                  max_waiters=max(1 << 16, 4 * self.n))
         kw.update(sim_kw or {})
         self.sim = Simulator(SimConfig(n_instances=self.n, seed=seed, **kw), binding=binding)
         self.sync = SyncService(self.sim)

@@ -187,6 +187,51 @@ class Simulator:
         self._check(self.lib.tcp_writes(self._ctx, _ptr(st), _ptr(t), n.value, C.byref(n)))
         return st, t
 
+    def tcp_writes_range(self, first: int, n: int) -> tuple[np.ndarray, np.ndarray]:
+        """(state, time) of writes [first, first + n)."""
+        st = np.zeros(n, np.uint8)
+        t = np.zeros(n, np.int64)
+        if n:
+            self._check(self.lib.tcp_writes_range(self._ctx, int(first), n, _ptr(st), _ptr(t)))
+        return st, t
+
+    def tcp_connect(self, src, dst) -> np.ndarray:
+        """Connections src[i] -> dst[i]; returns their ids."""
+        s = np.ascontiguousarray(np.atleast_1d(src), dtype=np.uint32)
+        d = np.ascontiguousarray(np.broadcast_to(dst, s.shape), dtype=np.uint32)
+        out = np.zeros(len(s), np.uint32)
+        self._check(self.lib.tcp_connect(self._ctx, _ptr(s), _ptr(d), len(s), _ptr(out)))
+        return out
+
+    def tcp_write(self, conn, size, t_send) -> None:
+        c = np.ascontiguousarray(np.atleast_1d(conn), dtype=np.uint32)
+        z = np.ascontiguousarray(np.broadcast_to(size, c.shape), dtype=np.uint32)
+        t = np.ascontiguousarray(np.broadcast_to(t_send, c.shape), dtype=np.int64)
+        self._check(self.lib.tcp_write(self._ctx, _ptr(c), _ptr(z), _ptr(t), len(c)))
+
+    def tcp_conns(self, first: int = 0, n: int | None = None) -> dict:
+        """Per connection: segments ACKed so far, cwnd, flight, queued (unsent)."""
+        if n is None:
+            n = self._n_conn() - first
+        out = dict(acked=np.zeros(n, np.uint64), cwnd=np.zeros(n, np.uint32), flight=np.zeros(n, np.uint32),
+                   queued=np.zeros(n, np.uint32))
+        if n:
+            self._check(self.lib.tcp_conns(self._ctx, first, n, *(_ptr(out[k]) for k in ("acked", "cwnd", "flight",
+                                                                                        "queued"))))
+        return out
+
+    def _n_conn(self) -> int:
+        lo, hi = 0, 1
+        while self.lib.tcp_conns(self._ctx, 0, hi, None, None, None, None) == A.OK:
+            lo, hi = hi, hi * 2
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if self.lib.tcp_conns(self._ctx, 0, mid, None, None, None, None) == A.OK:
+                lo = mid
+            else:
+                hi = mid
+        return lo
+
     def tcp_gen_storm_round(self, round_: int, t0: int, fanout: int, size: int, spread_ns: int, state: int) -> None:
         self._check(self.lib.tcp_gen_storm_round(self._ctx, round_, t0, fanout, size, spread_ns, state))
 

@@ -203,7 +203,7 @@ def _splitbrain_descriptor(binding, n, case):
     probes, one-minute timeouts, the 300 s plan context."""
     from testground_amd import plans as P
     env = P.PlanEnv(n, seed=3, test_case=case, binding=binding,
-                    sim_kw=dict(max_msgs_per_window=1 << 16, max_records=1 << 18, max_waiters=1 << 16))
+                    sim_kw=dict(max_msgs_per_window=1 << 16, max_records=1 << 18))
     ok = P.PLANS[("splitbrain", case)](env)
     res = dict(ok=ok, outcome=env.probe_outcome, done=env.probe_done, region=env.region,
                windows=env.probe_windows, unexpected=env.probe_unexpected, errors=env.probe_errors,

@@ -1,0 +1,180 @@
+"""TCP connections (tgsim_tcp_connect / _write): a per-connection Reno window over
+the acks = 1 path, so a connection's writes are ACK-clocked (plans/benchmarks/
+storm.go:158-183 writes 4 KiB chunks into one connection). Hand-computed slow start, congestion
+avoidance after a timeout, reset connections; randomised HIP-vs-oracle parity."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape
+from testground_amd.network import int_to_ip
+from tests import scenarios as S
+
+MS = 1_000_000
+MSS = 1448
+
+
+def sim(b, n=4, **kw):
+    kw.setdefault("max_msgs_per_window", 1 << 14)
+    kw.setdefault("max_records", 1 << 16)
+    s = Simulator(SimConfig(n_instances=n, seed=kw.pop("seed", 3), **kw), binding=b)
+    s.tcp_enable(acks=True)
+    return s
+
+
+def run(s, t_end, step=1 * MS, writes=None):
+    """1 ms windows up to t_end; returns per-window deliveries; writes: {t: [(conn, size)]}."""
+    out, t = [], s.now
+    while t < t_end:
+        for (tw, items) in sorted((writes or {}).items()):
+            if t <= tw < t + step:
+                s.tcp_write([c for c, _ in items], [z for _, z in items], [tw] * len(items))
+        s.advance(t + step)
+        d = s.deliveries()
+        s.tcp_react()
+        out.append((t, d))
+        t += step
+    return out
+
+
+def data_arrivals(out, src):
+    """times at which data segments of sender src arrived, with counts"""
+    got = {}
+    for _, d in out:
+        m = (d["src"] == src) & ((d["seq"] & A.TCP_ACK_BIT) == 0)
+        for t in d["t_deliver"][m].tolist():
+            got[t] = got.get(t, 0) + 1
+    return sorted(got.items())
+
+
+def case_slow_start(b):
+    """100 segments on one connection, 10 ms each way: IW10 at 0; every ACK round (a data
+    arrival at 10 ms + k*22 ms, its ACK leaving at the next window start, 11 ms back) doubles the
+    window: 10, 20, 40, then the last 30."""
+    s = sim(b)
+    s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS)] * 2)
+    c = s.tcp_connect([0], [1])
+    assert list(c) == [0]
+    out = run(s, 100 * MS, writes={0: [(0, 100 * MSS)]})
+    assert data_arrivals(out, 0) == [(10 * MS, 10), (32 * MS, 20), (54 * MS, 40), (76 * MS, 30)]
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [76 * MS]
+    cs = s.tcp_conns()
+    assert cs["acked"].tolist() == [100] and cs["cwnd"].tolist() == [110]
+    assert cs["flight"].tolist() == [0] and cs["queued"].tolist() == [0]
+    s.close()
+
+
+def case_timeout_then_congestion_avoidance(b):
+    """The first 10 segments are lost twice (the link drops everything until 300 ms): the 200 ms
+    timeout halves ssthresh to 5 and resets cwnd to 1; at 600 ms the third attempt gets through;
+    its 10 ACKs (621 ms) grow cwnd 1 -> 5 in slow start, then one step in congestion avoidance:
+    6 segments leave at 622 ms, their 6 ACKs make it 7, the last 4 leave at 644 ms."""
+    s = sim(b)
+    s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS, loss=100.0), make_shape(latency_ns=10 * MS)])
+    s.tcp_connect([0], [1])
+    out = run(s, 300 * MS, writes={0: [(0, 20 * MSS)]})
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    out += run(s, 700 * MS)
+    assert data_arrivals(out, 0) == [(610 * MS, 10), (632 * MS, 6), (654 * MS, 4)]
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [654 * MS]
+    cs = s.tcp_conns()
+    assert cs["cwnd"].tolist() == [7] and cs["acked"].tolist() == [20]
+    assert s.tcp_stats()["retransmissions"] == 20
+    s.close()
+
+
+def case_queued_writes_and_reset(b):
+    """Two connections from one sender; the second meets a prohibit route: its first segment is
+    refused and the connection resets, failing its queued writes; the first is unaffected and its
+    writes complete in order."""
+    s = sim(b)
+    ip = int_to_ip(s.get_ip(2)) + "/32"
+    s.add_rules(0, [make_rule(ip, A.FILTER_REJECT)])
+    c = s.tcp_connect([0, 0], [1, 2])
+    out = run(s, 20 * MS, writes={0: [(c[0], 30 * MSS), (c[1], 30 * MSS), (c[0], 1000), (c[1], 1000)]})
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED, A.TCP_REFUSED, A.TCP_DELIVERED, A.TCP_REFUSED]
+    assert t[1] == 0 and t[3] == 1 * MS                 # refused at once / at the reset's window end
+    cs = s.tcp_conns()
+    assert cs["acked"].tolist() == [31, 0] and cs["queued"].tolist() == [0, 0]
+    s.close()
+
+
+def case_errors(b):
+    s = Simulator(SimConfig(n_instances=4, seed=1), binding=b)
+    s.tcp_enable()                                       # acks = 0: no ACK clock
+    with pytest.raises(A.TgsimError) as e:
+        s.tcp_connect([0], [1])
+    assert e.value.code == A.ESTATE
+    s.close()
+    s = sim(b)
+    s.tcp_connect([0], [1])
+    with pytest.raises(A.TgsimError) as e:
+        s.tcp_send([0], [1], [0], [10], [0])             # one interface per context
+    assert e.value.code == A.ESTATE
+    with pytest.raises(A.TgsimError) as e:
+        s.tcp_write([5], [10], [0])
+    assert e.value.code == A.EINVAL
+    s.close()
+
+
+CASES = [case_slow_start, case_timeout_then_congestion_avoidance, case_queued_writes_and_reset, case_errors]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda f: f.__name__)
+def test_conn_oracle(oracle, case):
+    case(oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda f: f.__name__)
+def test_conn_hip(hip, case):
+    case(hip)
+
+
+def random_conn_run(b, seed, n=16, windows=160):
+    """Connections between random pairs (some twice), lossy / duplicating / corrupting links of a
+    few ms, writes of 1 B .. 40 segments arriving over the first 60 windows, a prohibit route."""
+    rng = np.random.default_rng(seed)
+    s = sim(b, n=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17)
+    s.set_shapes(np.arange(n), [make_shape(latency_ns=int(rng.integers(1, 6)) * MS, jitter_ns=int(rng.integers(0, 2)) * MS,
+                                           loss=float(rng.choice([0.0, 2.0, 10.0])), duplicate=float(rng.choice([0.0, 5.0])),
+                                           corrupt=float(rng.choice([0.0, 3.0]))) for _ in range(n)])
+    s.add_rules(3, [make_rule(int_to_ip(s.get_ip(7)) + "/32", A.FILTER_REJECT)])
+    src = rng.integers(0, n, 24)
+    dst = (src + rng.integers(1, n, 24)) % n
+    src[0], dst[0] = 3, 7
+    conns = s.tcp_connect(src, dst)
+    writes = {}
+    for w in range(60):
+        k = int(rng.integers(0, 4))
+        if k:
+            t = w * MS + int(rng.integers(0, MS))
+            writes[t] = [(int(rng.choice(conns)), int(rng.integers(1, 40 * MSS))) for _ in range(k)]
+    out = run(s, windows * MS, writes=writes)
+    st, t = s.tcp_writes()
+    res = dict(deliv=[d for _, d in out], status=None, writes=(st, t), conns=s.tcp_conns(), stats=S.parity_stats(s),
+               tcp=s.tcp_stats())
+    s.close()
+    return res
+
+
+def test_conn_random_oracle_properties(oracle):
+    r = random_conn_run(oracle, 1)
+    st, _ = r["writes"]
+    assert np.count_nonzero(st == A.TCP_DELIVERED) > 0.6 * len(st)
+    cs = r["conns"]
+    assert np.all(cs["cwnd"] >= 1) and cs["acked"].sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_conn_random_hip_matches_oracle(hip, oracle, seed):
+    a, b = random_conn_run(hip, seed), random_conn_run(oracle, seed)
+    S.assert_same(a["deliv"], b["deliv"])
+    assert np.array_equal(a["writes"][0], b["writes"][0]) and np.array_equal(a["writes"][1], b["writes"][1])
+    for k in a["conns"]:
+        assert np.array_equal(a["conns"][k], b["conns"][k]), k
+    assert a["stats"] == b["stats"]
