@@ -34,6 +34,7 @@ from .sync import SyncService
 
 TCP_OVERHEAD = 66          # Ethernet 14 + IPv4 20 + TCP 20 + timestamp option 12 bytes per segment
 TCP_CHUNK = 4 * 1024       # storm.go:23 write size
+T_MSS = 1448               # tgsim_tcp_config.mss default
 NEVER = np.iinfo(np.int64).max
 
 
@@ -88,9 +89,13 @@ class PlanEnv:
         # 2.11); a step then reports the writes that completed, at their last segment's arrival
         self.tcp = self.params.get("transport", "message") == "tcp"
         if self.tcp:
-            self.sim.tcp_enable()
+            # tcp_acks (default true): ACK packets, timers and the connections' Reno windows
+            # (DESIGN.md 2.11b); "false" keeps the per-write model without a reverse path
+            self.tcp_acks = self.params.get("tcp_acks", "true") == "true"
+            self.sim.tcp_enable(acks=self.tcp_acks)
             self._tw_keys = []                     # write id -> key, in send order
-            self._tw_seen = np.zeros(0, bool)      # writes already reported
+            self._tw_first = 0                     # writes before it have all been reported
+            self._tw_seen = np.zeros(0, bool)      # writes [_tw_first, ...) already reported
         self.sidecar.initialize(0)
 
     def close(self):
@@ -166,16 +171,21 @@ class PlanEnv:
     def _step_tcp(self, t_end: int) -> dict:
         """One window in TCP mode: the writes that completed in it as deliveries (src, dst, seq =
         the write's key, t_deliver = its last segment's arrival); failed writes enter the status
-        log (TIMEOUT as LOST, REFUSED as REJECTED)."""
+        log (TIMEOUT as LOST, REFUSED as REJECTED). Only writes from the first unsettled one on are
+        read back (not the whole table every window)."""
         self.sim.advance(t_end)
         self.sim.tcp_react()
-        st, t = self.sim.tcp_writes()
+        # _tw_keys holds the keys of writes _tw_first, _tw_first + 1, ... (the settled prefix is dropped)
         keys = np.concatenate(self._tw_keys) if self._tw_keys else np.zeros(0, np.uint64)
-        self._tw_keys = [keys] if len(keys) else []
-        seen = np.zeros(len(st), bool)
-        seen[:len(self._tw_seen)] = self._tw_seen
+        st, t = self.sim.tcp_writes_range(self._tw_first, len(keys))
+        seen = np.r_[self._tw_seen, np.zeros(len(st) - len(self._tw_seen), bool)]
         new = (st != A.TCP_PENDING) & ~seen
-        self._tw_seen = seen | new
+        seen |= new
+        settled = int(np.argmin(seen)) if not seen.all() else len(seen)
+        self._tw_keys = [keys[settled:]] if settled < len(keys) else []
+        self._tw_first += settled
+        self._tw_seen = seen[settled:]
+        self.tcp_settled_keys = keys[new]
         ok = new & (st == A.TCP_DELIVERED)
         bad = new & (st != A.TCP_DELIVERED)
         if bad.any():
@@ -268,6 +278,92 @@ class PlanEnv:
             return np.zeros(0, bool), np.zeros(0, np.int64)
         ok = arr != NEVER
         return ok, np.where(ok, arr - t, -1)
+
+    def tcp_write(self, conn, sizes, t, src, dst) -> np.ndarray:
+        """Writes on TCP connections (transport=tcp) at t; returns their keys
+        (src, seq) - tracked like sent messages: arrival = the write's delivery, a failure enters
+        the status log."""
+        src = np.atleast_1d(np.asarray(src, np.int64))
+        n = len(src)
+        order = np.argsort(src, kind="stable")
+        s_sorted = src[order]
+        first = np.r_[0, np.flatnonzero(np.diff(s_sorted)) + 1] if n else np.zeros(0, np.int64)
+        rank = np.arange(n) - np.repeat(first, np.diff(np.r_[first, n])) if n else np.zeros(0, np.int64)
+        seq = np.empty(n, np.int64)
+        seq[order] = self._seq[s_sorted] + rank
+        np.add.at(self._seq, src, 1)
+        keys = self.key(src, seq)
+        self.sim.tcp_write(conn, sizes, t)
+        self._tw_keys.append(keys)
+        return keys
+
+    def dial(self, src, dst, t_ready, limit: int, timeout_ns: int, syn_size: int = TCP_OVERHEAD):
+        """net.DialTimeout under a per-instance semaphore of `limit` (plans/benchmarks/storm.go:
+        141-152: `sem <- struct{}{}` before the dial, `<-sem` after it): dial i waits from t_ready[i]
+        for a free slot of its instance (FIFO, as a Go channel queues blocked senders), then sends a
+        SYN that its peer answers at first arrival; it ends at the SYN-ACK's first arrival (ok), at
+        once when its own route refuses it, or at the timeout. Returns (ok, t_end) per dial."""
+        src = np.asarray(src, np.int64)
+        dst = np.asarray(dst, np.int64)
+        t_ready = np.asarray(t_ready, np.int64)
+        m = len(src)
+        ok = np.zeros(m, bool)
+        t_done = np.full(m, NEVER, np.int64)
+        t_start = np.full(m, NEVER, np.int64)
+        req = np.zeros(m, np.uint64)
+        rep = np.zeros(m, np.uint64)
+        answered = np.zeros(m, bool)
+        active = np.zeros(m, bool)
+        # per instance: dials in FIFO order (t_ready, index) and the times its slots fall free
+        waiting = {}
+        for i in np.lexsort((np.arange(m), t_ready)):
+            waiting.setdefault(int(src[i]), []).append(int(i))
+        free = {g: [-(1 << 62)] * limit for g in waiting}
+        key_to = {}
+        while True:
+            for g, q in waiting.items():   # start what the free slots allow
+                fr = free[g]
+                while q and fr:
+                    i = q.pop(0)
+                    fr.sort()
+                    t0 = max(int(t_ready[i]), fr.pop(0))
+                    t_start[i] = t0
+                    req[i] = self.send([src[i]], [dst[i]], syn_size, [t0])[0]
+                    key_to[int(req[i])] = i
+                    active[i] = True
+            if not active.any() and not any(waiting.values()):
+                break
+            idle = not self._pend and self.sim.stats()["inflight"] == 0
+            if idle and active.any() and answered[active].all() is not None:
+                # only timeouts can end the active dials: jump to the first one
+                t_next = int((t_start[active] + timeout_ns).min()) + 1
+                d = self.step(max(t_next, self.sim.now + self.window_ns))
+            else:
+                d = self.step()
+            if len(d["t_deliver"]):
+                k = self.key(d["src"], d["seq"])
+                for kk, tt in zip(k.tolist(), d["t_deliver"].tolist()):
+                    i = key_to.get(kk)
+                    if i is None:
+                        continue
+                    if kk == int(req[i]) and not answered[i]:          # SYN at the listener: SYN-ACK
+                        rep[i] = self.send([dst[i]], [src[i]], syn_size, [tt])[0]
+                        key_to[int(rep[i])] = i
+                        answered[i] = True
+                    elif answered[i] and kk == int(rep[i]) and active[i] and tt < t_start[i] + timeout_ns:
+                        ok[i], t_done[i], active[i] = True, tt, False
+                        free[int(src[i])].append(tt)
+            idx = np.flatnonzero(active)
+            if len(idx):
+                st = self.status_of(req[idx]) & 0x0F
+                refused = np.isin(st, (A.ST_DROPPED, A.ST_REJECTED, A.ST_UNREACHABLE))
+                late = self.sim.now >= t_start[idx] + timeout_ns
+                for i, rf, lt in zip(idx.tolist(), refused.tolist(), late.tolist()):
+                    if rf or lt:
+                        t_done[i] = int(t_start[i]) + (0 if rf else timeout_ns)
+                        active[i] = False
+                        free[int(src[i])].append(int(t_done[i]))
+        return ok, t_done
 
     def probe(self, order, req_size: int, rep_size: int, timeout_ns: int, t0: int, window_ns: int | None = None):
         """Every instance probes order[...] (itself excluded) one request/reply at a time, the next
@@ -478,14 +574,66 @@ def splitbrain(action: FilterAction):
 # plans/benchmarks
 # ============================================================================================
 
+STORM_DIAL_TIMEOUT_NS = 30 * SECOND   # net.DialTimeout("tcp", addr, 30*time.Second), storm.go:144
+STORM_CTX_NS = 3000 * SECOND          # context.WithTimeout(..., 3000*time.Second), storm.go:32
+STORM_MSG_WINDOW = 10                 # message mode: writes a connection keeps in flight (IW10's segments)
+
+
+def _writesem_round(g_queue, holders, room, remaining, limit, emit):
+    """One instant of storm.go:158-183 for one instance: goroutines take the write semaphore in
+    FIFO order (`writesem <- struct{}{}`); conn.Write returns once the connection's buffer has
+    room, else the goroutine blocks holding its slot. emit(conn) sends one chunk. Runs until no
+    goroutine can progress; returns the chunks written."""
+    wrote, progress = 0, True
+    while progress:
+        progress = False
+        for h in list(holders):                       # blocked writers whose buffer drained
+            if room[h] > 0:
+                holders.remove(h)
+                room[h] -= 1
+                remaining[h] -= 1
+                emit(h)
+                wrote += 1
+                progress = True
+                if remaining[h]:
+                    g_queue.append(h)
+        while len(holders) < limit and g_queue:
+            h = g_queue.popleft()
+            if room[h] > 0:
+                room[h] -= 1
+                remaining[h] -= 1
+                emit(h)
+                wrote += 1
+                progress = True
+                if remaining[h]:
+                    g_queue.append(h)
+            else:
+                holders.append(h)
+    return wrote
+
+
 def storm(env: PlanEnv) -> np.ndarray:
-    """plans/benchmarks/storm.go:31-197: every instance dials `conn_outgoing` random peers after
-    U[0, conn_delay_ms) ms, SignalAndWait("outgoing-dials-done", N * conn_outgoing), then writes
-    data_size_kb KiB to each connection in 4 KiB writes; SignalAndWait("done writing", N).
-    Dial concurrency limits (concurrent_dials) are not modelled."""
+    """plans/benchmarks/storm.go:31-197: every instance dials `conn_outgoing` random peers, each
+    after U[0, conn_delay_ms) ms and under a semaphore of `concurrent_dials` (storm.go:141-152:
+    DialTimeout 30 s); every dialler signals "outgoing-dials-done" (target N * conn_outgoing) and,
+    once it releases, writes data_size_kb KiB into its connection in 4 KiB chunks, each conn.Write
+    under a second semaphore of `concurrent_dials` (writesem, storm.go:158-183); conn.Write returns
+    when the chunk fits the socket's buffer, so a full buffer blocks its writer - holding its
+    writesem slot. Then SignalAndWait("done writing", N).
+
+    transport=message: a chunk is one message; a connection keeps at most STORM_MSG_WINDOW in
+    flight (a chunk leaves the buffer at its arrival: message mode has no ACKs), and a lost chunk
+    fails its instance. transport=tcp: connections with the Reno window (tgsim_tcp_connect,
+    DESIGN.md 2.11b), the SYN a bare segment whose ACK completes the dial; the buffer holds
+    2 * cwnd segments (Linux autotunes sk_sndbuf to about twice the window, tcp_sndbuf_expand
+    [EXT]) and drains as ACKs arrive; a write fails on a timeout or a reset. A failed dial never
+    signals, so "outgoing-dials-done" cannot release and the run fails at its 3000 s context, as
+    in the reference."""
+    from collections import deque
     n = env.n
     outgoing = env.int_param("conn_outgoing", 5)
     delay_ms = env.int_param("conn_delay_ms", 30000)
+    limit = max(1, env.int_param("concurrent_dials", 10))
     size = env.int_param("data_size_kb", 128) * 1024
     rng = np.random.default_rng(env.int_param("seed", 0))
     t = env.net.wait_network_initialized(0)
@@ -495,29 +643,141 @@ def storm(env: PlanEnv) -> np.ndarray:
     src = np.repeat(np.arange(n), outgoing)
     off = rng.integers(1, n, len(src)) if n > 1 else np.zeros(len(src), np.int64)
     dst = (src + off) % n                                           # rand.Intn over the other nodes
-    t_dial = env.sim.now + rng.integers(0, max(delay_ms, 1), len(src)) * MS
-    ok, rtt = env.rpc(src, dst, TCP_OVERHEAD, TCP_OVERHEAD, t_dial, 30 * SECOND)
-    done = np.where(ok, t_dial + rtt, t_dial)
-    _, t = env.sync.signal_and_wait("outgoing-dials-done", np.flatnonzero(ok) // outgoing, done[ok], n * outgoing)
-    if t < 0:
-        env.fail("outgoing-dials-done never released")
-        return np.zeros(n, bool)
-    env.advance_to(max(t, env.sim.now))
+    t_ready = env.sim.now + rng.integers(0, max(delay_ms, 1), len(src)) * MS
     chunks = [TCP_CHUNK] * (size // TCP_CHUNK) + ([size % TCP_CHUNK] if size % TCP_CHUNK else [])
-    keys = []
-    now = env.sim.now
-    for c in chunks:
-        keys.append(env.send(src[ok], dst[ok], c + TCP_OVERHEAD, now))
-    env.bytes_sent = int(ok.sum()) * size
-    arr = env.wait(np.concatenate(keys) if keys else np.zeros(0, np.uint64), 3000 * SECOND)
-    _, t = env.sync.signal_and_wait("done writing", np.arange(n), env.sim.now, n)
+    m = len(src)
+    env.bytes_sent = 0
+    if env.tcp and not env.tcp_acks:
+        raise ValueError("storm over TCP writes into connections: it needs tcp_acks = true (the ACK clock)")
+    if env.tcp:
+        conn = env.sim.tcp_connect(src, dst)
+        ok, t_dial = _tcp_dials(env, conn, src, dst, t_ready, limit)
+    else:
+        ok, t_dial = env.dial(src, dst, t_ready, limit, STORM_DIAL_TIMEOUT_NS)
+    env.dials_ok = int(ok.sum())
     res = np.ones(n, bool)
-    res[src[~ok]] = False
-    if len(arr):
-        lost = np.tile(src[ok], len(chunks))[arr == NEVER]
-        res[lost] = False
+    if not ok.all():
+        for i in np.flatnonzero(~ok)[:5]:
+            env.fail(f"instance {src[i]}: couldnt dial {dst[i]}")
+        env.fail("outgoing-dials-done never released (a failed dial does not signal): context deadline exceeded")
+        res[:] = False
+        return res
+    _, t_b = env.sync.signal_and_wait("outgoing-dials-done", src, t_dial, n * outgoing)
+    env.advance_to(max(t_b, env.sim.now))
+    # the write phase: per instance its goroutines (one per connection) in dial order
+    remaining = np.full(m, len(chunks), np.int64)
+    queues = {g: deque(np.flatnonzero(src == g).tolist()) for g in range(n)}
+    holders = {g: [] for g in range(n)}
+    keys, wrote_at = [], []
+    seg_per_chunk = np.array([max(1, -(-c // T_MSS)) for c in chunks], np.int64)
+    written_segs = np.zeros(m, np.int64)
+    last_return = np.full(n, int(t_b), np.int64)
+    while True:
+        now = env.sim.now
+        if env.tcp:
+            cs = env.sim.tcp_conns(int(conn[0]), m)
+            buffered = written_segs - cs["acked"].astype(np.int64)
+            room_segs = 2 * cs["cwnd"].astype(np.int64) - buffered
+            nxt = np.array([seg_per_chunk[len(chunks) - r] if r else 1 for r in remaining])
+            room = np.where(room_segs >= nxt, 1, 0)      # conn.Write blocks until the chunk fits
+        else:
+            inflight = np.zeros(m, np.int64)
+            if keys:
+                k = np.concatenate(keys)
+                who = np.concatenate(wrote_at)
+                arr = env.arrival_of(k)
+                st = env.status_of(k) & 0x0F
+                gone = (arr != NEVER) | ((st != 0x0F) & (st != A.ST_QUEUED) & (st != A.ST_LOCAL))
+                np.add.at(inflight, who[~gone], 1)
+            room = STORM_MSG_WINDOW - inflight
+        room = room.tolist()
+        batch_c, batch_z = [], []
+
+        def emit(h):
+            c = chunks[len(chunks) - remaining[h] - 1]
+            batch_c.append(h)
+            batch_z.append(c)
+        for g in range(n):
+            if _writesem_round(queues[g], holders[g], room, remaining, limit, emit):
+                last_return[g] = now
+        if batch_c:
+            bc = np.array(batch_c, np.int64)
+            if env.tcp:
+                written_segs_add = np.array([max(1, -(-z // T_MSS)) for z in batch_z], np.int64)
+                np.add.at(written_segs, bc, written_segs_add)
+                keys.append(env.tcp_write(conn[bc], batch_z, now, src[bc], dst[bc]))
+            else:
+                keys.append(env.send(src[bc], dst[bc], np.array(batch_z) + TCP_OVERHEAD, now))
+                wrote_at.append(bc)
+            env.bytes_sent += int(sum(batch_z))
+        if not remaining.any():
+            break
+        if env.sim.now > STORM_CTX_NS:
+            env.fail("writes still blocked at the 3000 s context")
+            return np.zeros(n, bool)
+        env.step()
+    # wg.Wait(): the last conn.Write of each instance returned; then SignalAndWait("done writing", N)
+    _, t = env.sync.signal_and_wait("done writing", np.arange(n), last_return, n)
+    # the written data drains (the plan's time.Sleep(10 s) after the barrier); a lost chunk (message
+    # mode) or a failed write (TCP) fails its writer
+    allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
+    arr = env.wait(allk, 10 * SECOND + max(0, t - env.sim.now))
+    lost = (allk[arr == NEVER] >> np.uint64(32)).astype(np.int64)
+    res[lost] = False
     env.delivered_chunks = int((arr != NEVER).sum())
+    env.overlimit = int(env.sim.stats()["overlimit"])
     return res
+
+
+def _tcp_dials(env: PlanEnv, conn, src, dst, t_ready, limit: int):
+    """TCP mode dials: the SYN is a bare segment on the connection, written when the dial gets its
+    semaphore slot; its ACK, seen at the end of the window it arrives in, completes the dial; a
+    refused or timed-out SYN fails it."""
+    m = len(conn)
+    ok = np.zeros(m, bool)
+    t_done = np.full(m, NEVER, np.int64)
+    started = np.zeros(m, bool)
+    syn = np.zeros(m, np.uint64)
+    waiting = {}
+    for i in np.lexsort((np.arange(m), t_ready)):
+        waiting.setdefault(int(src[i]), []).append(int(i))
+    free = {g: [-(1 << 62)] * limit for g in waiting}
+    t_start = np.full(m, NEVER, np.int64)
+    while True:
+        now = env.sim.now
+        for g, q in waiting.items():
+            fr = free[g]
+            while q and fr:
+                fr.sort()
+                t0 = max(int(t_ready[q[0]]), fr[0], now)
+                if t0 >= now + env.window_ns:     # not in the next window: the writer still sleeps
+                    break
+                i = q.pop(0)
+                fr.pop(0)
+                t_start[i] = t0
+                started[i] = True
+                syn[i] = env.tcp_write(conn[[i]], [0], t0, src[[i]], dst[[i]])[0]
+        act = started & (t_done == NEVER)
+        if not act.any() and not any(waiting.values()):
+            break
+        if not act.any() and not env._pend and env.sim.stats()["inflight"] == 0:
+            # every dialler still sleeps (conn_delay_ms): jump to the first wake-up
+            nxt = min(max(int(t_ready[q[0]]), min(free[g])) for g, q in waiting.items() if q and free[g])
+            if nxt > now + env.window_ns:
+                env.advance_to(nxt)
+                continue
+        env.step()
+        cs = env.sim.tcp_conns(int(conn[0]), m)
+        got = act & (cs["acked"] >= 1)
+        st = env.status_of(syn) & 0x0F
+        failed = act & ~got & started & (st != 0x0F)
+        for i in np.flatnonzero(got):
+            ok[i], t_done[i] = True, env.sim.now
+            free[int(src[i])].append(int(env.sim.now))
+        for i in np.flatnonzero(failed):
+            t_done[i] = env.sim.now
+            free[int(src[i])].append(int(env.sim.now))
+    return ok, t_done
 
 
 def barrier_bench(env: PlanEnv) -> np.ndarray:

@@ -205,6 +205,35 @@ def test_verify_uses_data_network(oracle):
     env.close()
 
 
+STORM_TOML = {"conn_count": "10", "conn_outgoing": "10", "conn_delay_ms": "30000", "concurrent_dials": "2",
+              "data_size_kb": "1024"}   # plans/benchmarks/compositions/storm.toml:18-23 (50 instances)
+
+
+def storm_toml_run(binding, transport, n=50):
+    env = env_for(binding, n, "storm", params=dict(STORM_TOML, transport=transport))
+    ok = P.storm(env)
+    res = dict(ok=ok, failures=list(env.failures), stats=env.sim.stats(), now=env.sim.now, chunks=env.delivered_chunks,
+               dials=env.dials_ok, bytes=env.bytes_sent)
+    if transport == "tcp":
+        res["tcp"] = env.sim.tcp_stats()
+    env.close()
+    return res
+
+
+@pytest.mark.parametrize("transport", ["message", "tcp"])
+def test_storm_toml_passes(oracle, transport):
+    """the reference's own storm composition (50 x 10 dials x 1024 KiB in 4 KiB
+    writes, concurrent_dials 2, unshaped) passes - 50/50 with no tail drops - once dials and writes
+    are paced as storm.go paces them (dial / write semaphores, writes blocking on the send buffer;
+    TCP: the Reno window). Round 2's all-at-once descriptor gave 0/50 with 78,000 tail drops."""
+    r = storm_toml_run(oracle, transport)
+    assert r["ok"].all(), r["failures"][:3]
+    assert r["stats"]["overlimit"] == 0 and r["dials"] == 500 and r["bytes"] == 500 * 1024 * 1024
+    assert r["chunks"] == 500 * 256
+    if transport == "tcp":
+        assert r["tcp"]["retransmissions"] == 0 and r["tcp"]["failed"] == 0 and r["tcp"]["delivered"] == 500 * 257
+
+
 def test_storm_completes(oracle):
     env = env_for(oracle, 20, params={"conn_outgoing": 3, "conn_delay_ms": 1000, "data_size_kb": 10})
     ok = P.storm(env)
@@ -324,3 +353,12 @@ def test_example_failure_through_the_runner(oracle):
     w = io.StringIO()
     res = LocalMI355XRunner(binding=oracle).run(job, w).result
     assert res.outcome == "failure" and w.getvalue().count("FAIL") >= 2 and "intentional oops" in w.getvalue()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["message", "tcp"])
+def test_storm_toml_hip_matches_oracle(hip, oracle, transport):
+    a, b = storm_toml_run(hip, transport), storm_toml_run(oracle, transport)
+    assert a["ok"].all() and np.array_equal(a["ok"], b["ok"])
+    for k in ("stats", "now", "chunks", "dials", "bytes") + (("tcp",) if transport == "tcp" else ()):
+        assert a[k] == b[k], k

@@ -335,7 +335,7 @@ def _pingpong_tcp(binding):
     100 ms egress latency, [20, 35] ms at 10 ms) - the plan's data is 1-byte writes on one
     connection, so segmentation adds only the 52 header bytes."""
     from testground_amd import plans as P
-    env = P.PlanEnv(2, seed=1, params={"transport": "tcp"}, binding=binding)
+    env = P.PlanEnv(2, seed=1, params={"transport": "tcp", "tcp_acks": "false"}, binding=binding)
     ok = P.pingpong(env)
     rtts = getattr(env, "rtts", [])
     stats = env.sim.tcp_stats()
@@ -360,7 +360,7 @@ def _lossy_rpc(binding):
     grid - base RTT + k * 200 ms - instead of being lost as in the message-level model."""
     from testground_amd import plans as P
     from testground_amd.network import MS as NMS
-    env = P.PlanEnv(8, seed=2, params={"transport": "tcp"}, binding=binding)
+    env = P.PlanEnv(8, seed=2, params={"transport": "tcp", "tcp_acks": "false"}, binding=binding)
     for g in range(8):
         env.sim.set_shape(g, make_shape(latency_ns=5 * MS, loss=30.0))
     src = np.arange(8)
