@@ -148,6 +148,42 @@ def roofline(dominant: str, delta: dict, kern_ms: float, kern_n: int, n_local: i
     }
 
 
+def probe_steps(args) -> int:
+    """Probe steps before the timed region: as many as it has (at least 10), so the dominant kernel
+    is chosen over as many launches as the timed region makes (a 5-step probe flipped
+    between two kernels within 2 %)."""
+    return max(10, args.steps)
+
+
+def probe_kernels(sim, step, first: int, probe: int):
+    """Every kernel class timed (HIP events on the context stream) over `probe` steps; returns
+    ({kernel: avg_us, launches, total_ms}, the kernel with the largest total time among those
+    with a byte model)."""
+    sim.profile(None)
+    base = sim.profile_read()
+    for r in range(first, first + probe):
+        step(r)
+    prof = sim.profile_read()
+    ks = {k: {"avg_us": 1e3 * (ms - base[k][0]) / (n - base[k][1]), "launches": n - base[k][1],
+              "total_ms": ms - base[k][0]} for k, (ms, n) in prof.items() if n > base[k][1]}
+    ranked = sorted(((v["total_ms"], k) for k, v in ks.items() if k in BYTE_MODELS or k in ALG_MODELS), reverse=True)
+    return ks, (ranked[0][1] if ranked else "k_emit_bucket")
+
+
+def kernel_fracs(kernels: dict, delta: dict, n_local: int, windows: int, probe: int) -> dict:
+    """SURVEY.md 8(d) bytes per launch / the probe's average launch time, for every kernel with an
+    algorithmic byte model (delta: the timed region's counters over `windows` steps, scaled to one
+    launch of the probe's cadence)."""
+    out = {}
+    for k, v in kernels.items():
+        if k not in ALG_MODELS or not v["launches"]:
+            continue
+        per_launch = ALG_MODELS[k](delta, n_local, windows) / max(1, windows) * probe / v["launches"]
+        out[k] = {"alg_bytes_per_launch": per_launch, "avg_us": v["avg_us"],
+                  "frac": per_launch / (v["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
+    return out
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -163,7 +199,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     # config 5 (not the headline): 1M-instance random-regular pubsub flood, one window per step
-    p.add_argument("--workload", choices=("storm", "flood"), default="storm")
+    p.add_argument("--workload", choices=("storm", "flood", "a2a", "splitbrain"), default="storm")
+    p.add_argument("--a2a-instances", type=int, default=1000)
+    p.add_argument("--sb-instances", type=int, default=10_000)
+    p.add_argument("--sb-case", choices=("accept", "drop", "reject"), default="accept")
     p.add_argument("--tcp", action="store_true",
                    help="storm over TCP mode (DESIGN.md 2.11): writes, retransmissions, one reaction per window")
     p.add_argument("--tcp-acks", action="store_true",
@@ -176,6 +215,9 @@ def parse():
                         "instances = 10000 floods per wave does not fit in memory: DESIGN.md 5.4)")
     p.add_argument("--window-ms", type=float, default=10.0, help="window length (flood)")
     a = p.parse_args()
+    if a.workload == "splitbrain":
+        a.warmup = a.warmup if "--warmup" in sys.argv else 200
+        a.steps = a.steps if "--steps" in sys.argv else 500
     if a.workload == "flood":
         # the flood reaches steady state after a publication's lifetime (~80 windows)
         a.warmup = a.warmup if "--warmup" in sys.argv else 100
@@ -251,6 +293,10 @@ def main():
     args = parse()
     if args.workload == "flood":
         return main_flood(args)
+    if args.workload == "a2a":
+        return main_a2a(args)
+    if args.workload == "splitbrain":
+        return main_splitbrain(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -276,7 +322,7 @@ def main():
     if args.tcp:
         if world > 1:
             raise SystemExit("--tcp: TCP mode needs a single-shard context")
-        rounds = args.warmup + max(3, min(10, args.warmup)) + args.steps + 1
+        rounds = args.warmup + probe_steps(args) + args.steps + 1
         sim.tcp_enable(max_writes=rounds * N * F, max_segments=rounds * N * F, acks=args.tcp_acks)
 
     def step(r: int):
@@ -290,21 +336,13 @@ def main():
         sim.gen_storm_round(r, T_NOW, F, args.size, spread, r)
         sim.advance_to_barrier(sim.barrier(r, N, T_NOW), rtt)
 
-    # warm-up (untimed, unprofiled), then a few probe steps that time every kernel class to find the
-    # dominant one; the timed region carries HIP events around that kernel only
+    # warm-up (untimed, unprofiled), then probe steps (as many as the timed region) that time every
+    # kernel class: the dominant one is the largest total time; the timed region carries HIP events
+    # around that kernel only
     for r in range(args.warmup):
         step(r)
-    probe = max(3, min(10, args.warmup))
-    sim.profile(None)
-    base_all = sim.profile_read()
-    for r in range(args.warmup, args.warmup + probe):
-        step(r)
-    prof = sim.profile_read()
-    warm_kernels = {k: {"avg_us": 1e3 * (ms - base_all[k][0]) / (n - base_all[k][1]), "launches": n - base_all[k][1]}
-                    for k, (ms, n) in prof.items() if n > base_all[k][1]}
-    ranked = sorted(((v["avg_us"] * v["launches"], k) for k, v in warm_kernels.items() if k in BYTE_MODELS),
-                    reverse=True)
-    dominant = ranked[0][1] if ranked else "k_emit_bucket"
+    probe = probe_steps(args)
+    warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
     sim.profile([dominant])
     base_prof = sim.profile_read()[dominant]
     first = args.warmup + probe
@@ -341,6 +379,7 @@ def main():
         delivered, b_total = int(v[0].item()), int(v[1].item())
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
                     elapsed)
+    roof["kernels"] = kernel_fracs(warm_kernels, delta, sim.hi - sim.lo, args.steps, probe)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.tcp:
         cpu = cpu_baseline(args, shapes)
@@ -521,17 +560,8 @@ def main_flood(args):
 
     for w in range(args.warmup):
         step(w)
-    probe = 5
-    sim.profile(None)
-    base_all = sim.profile_read()
-    for w in range(args.warmup, args.warmup + probe):
-        step(w)
-    prof = sim.profile_read()
-    warm_kernels = {k: {"avg_us": 1e3 * (ms - base_all[k][0]) / (n - base_all[k][1]), "launches": n - base_all[k][1]}
-                    for k, (ms, n) in prof.items() if n > base_all[k][1]}
-    ranked = sorted(((v["avg_us"] * v["launches"], k) for k, v in warm_kernels.items() if k in BYTE_MODELS),
-                    reverse=True)
-    dominant = ranked[0][1] if ranked else "k_emit_bucket"
+    probe = probe_steps(args)
+    warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
     sim.profile([dominant])
     base_prof = sim.profile_read()[dominant]
     first = args.warmup + probe
@@ -560,6 +590,7 @@ def main_flood(args):
         elapsed, delivered, b_total = float(t.item()), int(v[0].item()), int(v[1].item())
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "flood", world, b_total,
                     elapsed)
+    roof["kernels"] = kernel_fracs(warm_kernels, delta, sim.hi - sim.lo, args.steps, probe)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = flood_cpu_baseline(args, shapes, graph)
@@ -585,6 +616,240 @@ def main_flood(args):
     sim.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+# ---- config 2: 1k instances all-to-all (BASELINE.json configs[1]) -------------
+
+A2A_ROUND_NS = 10 * MS
+
+
+def a2a_round(n: int, r: int, senders=None):
+    """Round r of config 2: every sender to every other instance, 4 KiB, t_send = r * 10 ms +
+    U[0, 1 ms) as a pure function of (src, seq), seq = r * n + dst (tests/test_full_size.py)."""
+    snd = np.arange(n, dtype=np.uint32) if senders is None else np.asarray(senders, np.uint32)
+    src = np.repeat(snd, n - 1)
+    dst = (src + np.tile(np.arange(1, n, dtype=np.uint32), len(snd))) % np.uint32(n)
+    seq = np.uint32(r * n) + dst
+    h = (src.astype(np.uint64) * np.uint64(2654435761) + seq.astype(np.uint64) * np.uint64(40503)) & np.uint64(0xFFFFFFFF)
+    t = r * A2A_ROUND_NS + (h % np.uint64(MS)).astype(np.int64)
+    return src, dst, seq, np.full(len(src), 4096, np.uint32), t
+
+
+def a2a_shapes(n: int):
+    from testground_amd.sim import make_shape
+    return [make_shape(latency_ns=50 * MS, jitter_ns=10 * MS, loss=1.0)] * n
+
+
+def a2a_config(n: int):
+    from testground_amd.sim import SimConfig
+    return SimConfig(n_instances=n, seed=2, max_msgs_per_window=1 << 20, max_records=1 << 23)
+
+
+def main_a2a(args):
+    """Config 2: 1k instances all-to-all, 4 KiB, latency 50 ms, jitter 10 ms, loss 1 %, one round of
+    999k messages per 10 ms window (the synthetic all-at-once pattern SURVEY.md 8(d) states: every
+    sender's queue holds ~5 rounds, so netem's 1000-packet limit tail-drops ~80 % and every sender
+    takes the sequential queue-limit lane, k_shape_seq). A step = one round. The rounds' messages
+    are generated into HBM before the timed region; a step stages one (tgsim_enqueue_device)."""
+    import torch
+    from testground_amd.sim import Simulator
+    n = args.a2a_instances
+    rounds = args.warmup + probe_steps(args) + args.steps
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    cols = []
+    for r in range(rounds):
+        src, dst, seq, size, t = a2a_round(n, r)
+        cols.append(tuple(torch.from_numpy(x.view(np.int32) if x.dtype == np.uint32 else x).to(dev)
+                          for x in (src, dst, seq, size, t)))
+    torch.cuda.synchronize()
+    sim = Simulator(a2a_config(n))
+    sim.set_stream(stream.cuda_stream)
+    sim.set_shapes(np.arange(n), a2a_shapes(n))
+    m = n * (n - 1)
+
+    def step(r: int):
+        c = cols[r]
+        sim.enqueue_device(c[0].data_ptr(), c[1].data_ptr(), c[2].data_ptr(), c[3].data_ptr(), c[4].data_ptr(), m)
+        sim.advance((r + 1) * A2A_ROUND_NS, wait=False)
+
+    for r in range(args.warmup):
+        step(r)
+    probe = probe_steps(args)
+    warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
+    sim.profile([dominant])
+    base_prof = sim.profile_read()[dominant]
+    first = args.warmup + probe
+    s0 = sim.stats()
+    sim.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(first, first + args.steps):
+        step(r)
+    sim.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    s1 = sim.stats()
+    prof = sim.profile_read()[dominant]
+    delta = {k: s1[k] - s0[k] for k in s1}
+    b_total = alg_bytes_step(delta, n, args.steps)
+    roof = roofline(dominant, delta, prof[0] - base_prof[0], prof[1] - base_prof[1], n, args.steps, "a2a", 1,
+                    b_total, elapsed)
+    roof["kernels"] = kernel_fracs(warm_kernels, delta, n, args.steps, probe)
+    cpu = None if args.no_cpu_baseline else a2a_cpu_baseline(args, n)
+    print(json.dumps({
+        "metric": "simulated msgs delivered/sec (1k-inst all-to-all storm, config 2) + % HBM roofline",
+        "value": delta["delivered"] / elapsed, "unit": "msgs/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "config": {"workload": "all-to-all (SURVEY.md 8(d) config 2): 1000 instances, 4 KiB, t_send U[0,1 ms) per "
+                               "10 ms round, latency 50 ms, jitter 10 ms, loss 1%; synthetic all-at-once rounds "
+                               "(a stress pattern: the reference's storm paces its writes - tests/test_plans_oracle.py)",
+                   "instances": n, "msgs_per_round": m, "parallelism": "shard1",
+                   "msgs_in_timed_steps": delta["msgs_in"], "overlimit_in_timed_steps": delta["overlimit"],
+                   "delivered_in_timed_steps": delta["delivered"]},
+        "roofline": roof, "cpu_baseline": cpu, "kernels_probe": warm_kernels}), flush=True)
+    sim.close()
+
+
+def a2a_cpu_baseline(args, n):
+    from oracle.pyoracle import oracle_binding
+    from testground_amd.sim import Simulator
+    sim = Simulator(a2a_config(n), binding=oracle_binding())
+    sim.set_shapes(np.arange(n), a2a_shapes(n))
+    warm = 8
+    for r in range(warm):
+        sim.enqueue(*a2a_round(n, r))
+        sim.advance((r + 1) * A2A_ROUND_NS)
+    d0 = sim.stats()["delivered"]
+    t0 = time.perf_counter()
+    r = warm
+    while True:
+        src, dst, seq, size, t = a2a_round(n, r)
+        sim.enqueue(src, dst, seq, size, t)
+        sim.advance((r + 1) * A2A_ROUND_NS)
+        r += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or r - warm >= 40:
+            break
+    delivered = sim.stats()["delivered"] - d0
+    sim.close()
+    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port", **host_cpu(),
+            "sample": f"oracle/ (single-threaded C restatement), same {n}-instance all-to-all: rounds {warm}..{r - 1} "
+                      f"timed ({el:.1f} s, {delivered} deliveries) after {warm} warm-up rounds"}
+
+
+# ---- config 3: 10k-instance splitbrain with sequential probes (BASELINE.json configs[2]) --------------
+
+SB_WINDOW_NS = 100_000
+SB_TIMEOUT_NS = 60_000 * MS
+
+
+def sb_setup(sim, n: int, case: str):
+    """plans/splitbrain at config 3: region = seq % 3 with seq = g + 1; region A holds a /32 rule
+    (Drop / Reject) toward every region-B address (accept: none); probes in instance order."""
+    from testground_amd import _abi as A
+    region = (np.arange(n) + 1) % 3
+    if case != "accept":
+        action = A.FILTER_DROP if case == "drop" else A.FILTER_REJECT
+        b = np.flatnonzero(region == 1)
+        rules = (A.LinkRule * len(b))()
+        for i, g in enumerate(b):
+            rules[i].subnet_ip = sim.get_ip(int(g))
+            rules[i].prefix_len = 32
+            rules[i].shape.filter = action
+        for g in np.flatnonzero(region == 0):
+            sim._check(sim.lib.add_rules(sim._ctx, int(g), rules, len(b)))
+    sim.probe_setup(np.arange(n), 66, 66, SB_TIMEOUT_NS, SB_WINDOW_NS)
+    sim.probe_start(0)
+
+
+def sb_config(n: int):
+    from testground_amd.sim import SimConfig
+    return SimConfig(n_instances=n, seed=3, max_msgs_per_window=1 << 16, max_records=1 << 18)
+
+
+def main_splitbrain(args):
+    """Config 3 as the reference plan generates it: every node probes every other node one request /
+    reply at a time (tgsim_probe_*). A step is one window; the window's end is the
+    device's proposal (tgsim_probe_state_device -> tgsim_advance_begin_device), so the loop never
+    reads the device. value = deliveries / wall time."""
+    import torch
+    from testground_amd.sim import Simulator
+    n = args.sb_instances
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sim = Simulator(sb_config(n))
+    sim.set_stream(stream.cuda_stream)
+    sb_setup(sim, n, args.sb_case)
+    sim.advance(SB_WINDOW_NS)
+    sim.probe_react(wait=False)
+    ne_ptr, act_ptr = sim.probe_state_device()
+
+    def step(_w: int):
+        sim.advance_begin_device(ne_ptr, 0)
+        sim.advance_end()
+        sim.probe_react(wait=False)
+
+    for w in range(args.warmup):
+        step(w)
+    probe = probe_steps(args)
+    warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
+    sim.profile([dominant])
+    base_prof = sim.profile_read()[dominant]
+    s0 = sim.stats()
+    sim.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for w in range(args.steps):
+        step(w)
+    sim.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    s1 = sim.stats()
+    prof = sim.profile_read()[dominant]
+    ne, act = sim.probe_react()  # one more reaction, synchronised: the state after the timed region
+    delta = {k: s1[k] - s0[k] for k in s1}
+    b_total = alg_bytes_step(delta, n, args.steps)
+    roof = roofline(dominant, delta, prof[0] - base_prof[0], prof[1] - base_prof[1], n, args.steps, "splitbrain", 1,
+                    b_total, elapsed)
+    roof["kernels"] = kernel_fracs(warm_kernels, delta, n, args.steps, probe)
+    cpu = None if args.no_cpu_baseline else sb_cpu_baseline(args, n)
+    print(json.dumps({
+        "metric": "simulated msgs delivered/sec (10k-inst splitbrain, sequential probes, config 3) + % HBM roofline",
+        "value": delta["delivered"] / elapsed, "unit": "msgs/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "config": {"workload": f"splitbrain {args.sb_case} (SURVEY.md 8(d) config 3, plans/splitbrain/main.go:153-175): "
+                               f"{n} instances, region = seq % 3, each GETs every other one at a time "
+                               f"(request + reply, 60 s timeout), {SB_WINDOW_NS // 1000} us reaction windows",
+                   "instances": n, "case": args.sb_case, "parallelism": "shard1", "step": "one window",
+                   "delivered_in_timed_steps": delta["delivered"], "active_probers_after": act},
+        "roofline": roof, "cpu_baseline": cpu, "kernels_probe": warm_kernels}), flush=True)
+    sim.close()
+
+
+def sb_cpu_baseline(args, n):
+    from oracle.pyoracle import oracle_binding
+    from testground_amd.sim import Simulator
+    sim = Simulator(sb_config(n), binding=oracle_binding())
+    sb_setup(sim, n, args.sb_case)
+    ne = SB_WINDOW_NS
+    d0, w = sim.stats()["delivered"], 0
+    t0 = time.perf_counter()
+    while True:
+        sim.advance(ne)
+        ne, act = sim.probe_react()
+        w += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or act == 0 or w >= 20_000:
+            break
+    delivered = sim.stats()["delivered"] - d0
+    sim.close()
+    return {"value": delivered / el, "unit": "msgs/s", "cores": 1, "kind": "port", **host_cpu(),
+            "sample": f"oracle/ (single-threaded C restatement), same {n}-instance splitbrain {args.sb_case}: "
+                      f"windows 0..{w - 1} ({el:.1f} s, {delivered} deliveries, incl. the probe reaction)"}
 
 
 if __name__ == "__main__":

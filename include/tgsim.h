@@ -272,8 +272,17 @@ typedef struct tgsim_transport {
   int (*allreduce_max_i64)(void* user, int64_t* buf, size_t n, void* stream);
   /* bytes at send of every rank -> recv[rank * bytes] */
   int (*allgather)(void* user, const void* send, void* recv, size_t bytes, void* stream);
+  /* optional (NULL: none): a shard whose sharded call fails calls it, so the other ranks' pending
+   * and later collectives return an error instead of waiting for this one; the context then refuses
+   * sharded calls (TGSIM_ESTATE). The native communicator (tgsim_comm_init) is aborted the same way
+   * (ncclCommAbort). */
+  void (*abort)(void* user);
 } tgsim_transport;
 int tgsim_set_transport(tgsim_ctx* ctx, const tgsim_transport* transport);  /* NULL: none */
+/* A shard that stops early (its run was cancelled, or the caller gave up on it) aborts its side of
+ * the shard group: the transport's abort callback / ncclCommAbort, so no peer waits for it; the
+ * context then refuses sharded calls. A failing sharded call does this by itself. */
+int tgsim_comm_abort(tgsim_ctx* ctx);
 
 /* Sharded window protocol without a transport: begin (sender side) -> caller all-to-alls the exchange buffers
  * (n_shards * exchange_cap records each way, peer-major; the first record of each peer block is a

@@ -213,7 +213,7 @@ struct tgo_ctx {
   uint32_t fl_D, fl_max_pubs, fl_wpp;
   /* cross-shard transport (tgsim_set_transport): host buffers, stream NULL */
   tgsim_transport tr;
-  int has_tr, replicated_batch;
+  int has_tr, replicated_batch, tr_aborted;
   /* TCP mode: writes, segments, segments with a retransmission scheduled */
   int tcp_on, tcp_need_react;
   tgsim_tcp_config tcp;
@@ -988,23 +988,45 @@ int tgo_advance_end(tgo_ctx* c) {
   return TGSIM_OK;
 }
 
+/* A shard whose sharded call fails tells the others (tgsim_transport.abort): their pending and later
+ * collectives fail instead of waiting for it; this context refuses sharded calls from then on. */
+static int shard_failed(tgo_ctx* c, int rc) {
+  if (rc && c->S > 1 && c->has_tr) {
+    if (c->tr.abort) c->tr.abort(c->tr.user);
+    c->has_tr = 0;
+    c->tr_aborted = 1;
+  }
+  return rc;
+}
+
+int tgo_comm_abort(tgo_ctx* c) {
+  (void)shard_failed(c, TGSIM_ESTATE);
+  return TGSIM_OK;
+}
+
 int tgo_set_transport(tgo_ctx* c, const tgsim_transport* t) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (t && (!t->alltoall || !t->allreduce_max_i64 || !t->allgather)) return fail(c, TGSIM_EINVAL, "incomplete transport");
   c->has_tr = t != NULL;
+  c->tr_aborted = 0;
   if (t) c->tr = *t; else memset(&c->tr, 0, sizeof(c->tr));
   return TGSIM_OK;
 }
 
 /* One window; sharded: collective, the exchange between the sender and receiver halves. */
-int tgo_advance(tgo_ctx* c, int64_t t_end) {
-  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "a sharded context needs a transport or begin/end");
+static int advance_impl(tgo_ctx* c, int64_t t_end) {
+  if (c->S != 1 && !c->has_tr)
+    return fail(c, TGSIM_ESTATE, c->tr_aborted ? "the transport was aborted (a shard failed)"
+                                               : "a sharded context needs a transport or begin/end");
   int rc = tgo_advance_begin(c, t_end);
   if (rc) return rc;
-  if (c->S != 1 && c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0)
+  if (c->S != 1 && c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0) {
+    c->in_window = 0;
     return fail(c, TGSIM_EHIP, "transport all-to-all failed");
+  }
   return tgo_advance_end(c);
 }
+int tgo_advance(tgo_ctx* c, int64_t t_end) { return shard_failed(c, advance_impl(c, t_end)); }
 
 /* The CPU model has no stream: the same call as tgo_advance. */
 int tgo_advance_async(tgo_ctx* c, int64_t t_end) { return tgo_advance(c, t_end); }
@@ -1068,9 +1090,15 @@ static int sync_signal_local(tgo_ctx* c, const uint32_t* states, const uint32_t*
 
 /* A sharded batch with a transport: every shard's signals in shard order, processed whole on every
  * shard (replicated sync state); seq_out = this shard's own sequence numbers. */
+static int sync_signal_gathered(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                                size_t n, uint32_t* seq_out);
 int tgo_sync_signal(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                     size_t n, uint32_t* seq_out) {
   if (c->S == 1 || !c->has_tr || c->replicated_batch) return sync_signal_local(c, states, inst, t, n, seq_out);
+  return shard_failed(c, sync_signal_gathered(c, states, inst, t, n, seq_out));
+}
+static int sync_signal_gathered(tgo_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
+                                size_t n, uint32_t* seq_out) {
   typedef struct { uint32_t state, inst; int64_t t; } grec;
   uint64_t n64 = n;
   uint64_t* sizes = (uint64_t*)calloc(c->S, 8);
@@ -1159,8 +1187,8 @@ int tgo_sync_count(tgo_ctx* c, uint32_t state, uint32_t* count) {
 int tgo_advance_to_barrier(tgo_ctx* c, uint32_t w, int64_t offset) {
   int64_t rel;
   int rc = tgo_sync_poll(c, w, &rel);
-  if (rc) return rc;
-  if (rel < 0) return fail(c, TGSIM_ESTATE, "barrier not released");
+  if (rc) return shard_failed(c, rc);
+  if (rel < 0) return shard_failed(c, fail(c, TGSIM_ESTATE, "barrier not released"));
   return tgo_advance(c, rel + offset);
 }
 

@@ -74,6 +74,7 @@ int tgo_advance_begin(tgo_ctx* ctx, int64_t t_end);
 int tgo_exchange_buffers(tgo_ctx* ctx, void** send, void** recv, size_t* bytes);
 int tgo_advance_end(tgo_ctx* ctx);
 int tgo_set_transport(tgo_ctx* ctx, const tgsim_transport* transport); /* host buffers, stream NULL */
+int tgo_comm_abort(tgo_ctx* ctx);
 int tgo_delivery_count(tgo_ctx* ctx, size_t* n);
 int tgo_copy_deliveries(tgo_ctx* ctx, tgsim_delivery_soa* out, size_t cap, size_t* n);
 int tgo_copy_inbox_offsets(tgo_ctx* ctx, uint32_t* out, size_t cap);

@@ -111,11 +111,12 @@ TCP_ACK_BIT = 0x80000000
 ALLTOALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ABORT_FN = C.CFUNCTYPE(None, C.c_void_p)
 
 
 class Transport(C.Structure):
     _fields_ = [("user", C.c_void_p), ("alltoall", ALLTOALL_FN), ("allreduce_max_i64", ALLREDUCE_FN),
-                ("allgather", ALLGATHER_FN)]
+                ("allgather", ALLGATHER_FN), ("abort", ABORT_FN)]
 
 
 COMM_ID_BYTES = 128
@@ -164,6 +165,7 @@ _SIGS = {
     "flood_publish": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]),
     "flood_react": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_size_t)]),
     "set_transport": (C.c_int, [P, C.POINTER(Transport)]),
+    "comm_abort": (C.c_int, [P]),
     "tcp_enable": (C.c_int, [P, C.POINTER(TcpConfig)]),
     "tcp_send": (C.c_int, [P, C.POINTER(MsgSoA), C.c_size_t]),
     "tcp_react": (C.c_int, [P, C.POINTER(C.c_size_t)]),

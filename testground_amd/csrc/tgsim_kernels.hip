@@ -21,7 +21,8 @@ namespace tgsim {
 const char* const kKernelNames[KID_COUNT] = {
     "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
-    "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit"};
+    "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit",
+    "k_shape_seq", "k_probe"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
@@ -2195,6 +2196,9 @@ struct SeqSmem {
   uint32_t co[2][kSeqChunk];     // queued copy: corrupt offset
   uint8_t st[kSeqChunk], adm[kSeqChunk];  // status, queued copies (bit c = copy c)
   uint32_t nu, nk;
+  // parallel form: the chunk's candidate copies in enqueue order (INT64_MIN: none) and the admitted
+  // ones that outlive the chunk, sorted; K lives in ue / kd (two ascending buffers)
+  int64_t ce[2 * kSeqChunk], cb[2 * kSeqChunk];
 };
 
 __device__ __forceinline__ bool u_less(const SeqSmem& m, uint32_t a, uint32_t b) {
@@ -2250,6 +2254,62 @@ __device__ void k_push(SeqSmem& m, int64_t d, DevScalars* sc) {
   }
 }
 
+// ---- the parallel form for queue-heavy senders without HTB or correlation ----------------------
+// Without a token bucket a copy departs at its netem time, and without correlation every draw is a
+// pure function of the message: only the limit couples a sender's copies. Copy q enqueued at t_q is
+// admitted iff far + #{queued departures > t_q} < limit, the queued departures being the sorted
+// array K (due wheel records, earlier chunks' copies) plus this chunk's admitted copies before q.
+// Per chunk (64 messages, up to 128 copies, clone first) every lane computes its copies and their
+// base = far + |K > t| by bisection; if the count with every earlier copy admitted stays below the
+// limit nothing is dropped; otherwise one wave-uniform pass decides the copies in order, counting
+// the earlier admitted ones with ballots. The chunk's admitted copies that outlive its last enqueue
+// are then merged into K (bitonic sort + merge path). Same decisions as the heaps below, in
+// parallel (the all-to-all and splitbrain senders took lane 0's serial walk).
+
+// first index in [lo, hi) of the ascending k whose value is > t
+__device__ __forceinline__ uint32_t upper_idx(const int64_t* k, uint32_t lo, uint32_t hi, int64_t t) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (k[mid] <= t) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// ascending bitonic sort of v[0..n) (n a power of two) by the block's one wave
+__device__ void wave_bitonic(int64_t* v, uint32_t n) {
+  for (uint32_t k = 2; k <= n; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += kSeqChunk) {
+        const uint32_t p = i ^ j;
+        if (p > i) {
+          const int64_t x = v[i], y = v[p];
+          if ((x > y) == ((i & k) == 0)) { v[i] = y; v[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// out[0..a+b) = merge of the ascending A[0..a) and B[0..b), merge path split per lane
+__device__ void wave_merge(const int64_t* A, uint32_t a, const int64_t* B, uint32_t b, int64_t* out) {
+  const uint32_t T = a + b, per = (T + kSeqChunk - 1) / kSeqChunk;
+  const uint32_t d = min(T, threadIdx.x * per), e = min(T, d + per);
+  uint32_t lo = d > b ? d - b : 0u, hi = min(d, a);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (A[mid] <= B[d - mid - 1]) lo = mid + 1; else hi = mid;
+  }
+  uint32_t i = lo, j = d - lo;
+  for (uint32_t o = d; o < e; ++o) out[o] = (j >= b || (i < a && A[i] <= B[j])) ? A[i++] : B[j++];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor(v, o);
+  return v;
+}
+
 __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint32_t* sorted, const uint32_t* moff,
                                                          const uint32_t* hoff, const uint32_t* hidx,
                                                          const tgsim_record* H, const uint32_t* rho4,
@@ -2275,7 +2335,30 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
     uint64_t far = 0;  // queued copies not leaving in this window
     if (lane == 0) { m.nu = 0; m.nk = 0; }
     __syncthreads();
-    if (heavy) {  // the sender's due wheel records: U (token bucket pending) or K (departing now)
+    // the parallel form: heavy, no HTB, no correlation, and every due record's departure known
+    bool fast = heavy && !corr && !limited;
+    uint32_t kcur = 0, kh = 0, ksz = 0;  // K: ascending in m.ue (kcur 0) or m.kd (kcur 1), [kh, ksz) live
+    if (fast) {
+      const uint32_t h0 = hoff[l], h1 = hoff[l + 1];
+      bool anyA = false;
+      for (uint32_t b = h0 + lane; b < h1; b += kSeqChunk) anyA |= !(H[hidx[b]].meta & TGSIM_F_STAGE_D);
+      fast = __ballot(anyA) == 0;  // a stage-A record (queued under an earlier, limited shape): heaps
+      if (fast) {
+        uint32_t n0 = h1 - h0;
+        if (n0 > (uint32_t)kSeqCap) {
+          if (lane == 0) atomicOr(&sc->err, ERR_QUEUE_CAP);
+          n0 = kSeqCap;
+        }
+        const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
+        for (uint32_t j = lane; j < np2; j += kSeqChunk) m.ue[j] = j < n0 ? H[hidx[h0 + j]].t : INT64_MAX;
+        __syncthreads();
+        if (np2 > 1) wave_bitonic(m.ue, np2);
+        ksz = n0;
+        const uint32_t p = a.heavy.pend[l];
+        far = p > h1 - h0 ? p - (h1 - h0) : 0;
+      }
+    }
+    if (heavy && !fast) {  // the sender's due wheel records: U (token bucket pending) or K (departing now)
       const uint32_t h0 = hoff[l], h1 = hoff[l + 1];
       for (uint32_t b = h0; b < h1; b += kSeqChunk) {
         const uint32_t j = b + lane;
@@ -2327,8 +2410,125 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
         }
       }
       __syncthreads();
+      if (fast) {
+        // every lane: its message's copies (clone first) with their netem times, as k_shape_seq's walk
+        uint8_t st = 0, adm = 0, valid = 0;
+        int64_t e2[2] = {INT64_MIN, INT64_MIN};
+        uint32_t meta2[2] = {0, 0}, coff2[2] = {0, 0};
+        int64_t ts = INT64_MAX, base = 0;
+        if (lane < cn) {
+          ts = m.mt[lane];
+          const uint32_t size = m.msize[lane];
+          const uint32_t* r0 = m.w0[0][lane];
+          const bool dup = sh.dup_t && sh.dup_t >= r0[0];
+          const bool lst = sh.loss_t && sh.loss_t >= r0[1];
+          const int count = 1 + (dup ? 1 : 0) - (lst ? 1 : 0);
+          if (count == 0) {
+            st = TGSIM_ST_LOST;
+          } else {
+            st = TGSIM_ST_QUEUED;
+            if (dup && lst) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+            if (count == 2) st |= TGSIM_ST_FLAG_DUP;
+            for (int c = count == 2 ? 1 : 0; c >= 0; --c) {
+              const uint32_t* w = m.w0[c][lane];
+              if (c == 1 && sh.loss_t && sh.loss_t >= w[1]) { st |= TGSIM_ST_FLAG_CLONE_LOST; continue; }
+              uint32_t meta = c ? TGSIM_F_CLONE : 0u, coff = 0;
+              if (sh.corrupt_t) {
+                const uint32_t* w1 = m.w1[c][lane];
+                if (sh.corrupt_t >= w1[0] && size > 0) {
+                  meta |= TGSIM_F_CORRUPT | ((w1[2] % 8u) << TGSIM_F_BIT_SHIFT);
+                  coff = w1[1] % size;
+                }
+              }
+              int64_t e;
+              if (sh.reorder_t && !(sh.reorder_t < w[3])) {
+                meta |= TGSIM_F_REORDERED;
+                e = ts;
+              } else {
+                const int64_t delay = tabledist(sh.mu, sh.sigma, w[2]);
+                e = ts + (delay > 0 ? delay : 0);
+              }
+              meta |= TGSIM_F_STAGE_D;  // unlimited: the netem time is the departure
+              e2[c] = e; meta2[c] = meta; coff2[c] = coff;
+              valid |= (uint8_t)(1u << c);
+            }
+          }
+          base = (int64_t)far + (int64_t)(ksz - upper_idx(kcur ? m.kd : m.ue, kh, ksz, ts));
+        }
+        // enqueue order: message by message, clone (c = 1) before original (c = 0)
+        m.ce[2 * lane] = (valid & 2u) ? e2[1] : INT64_MIN;
+        m.ce[2 * lane + 1] = (valid & 1u) ? e2[0] : INT64_MIN;
+        __syncthreads();
+        // every earlier copy admitted: the largest count any copy could see
+        bool over = false;
+        for (int c = 1; c >= 0; --c) {
+          if (!(valid & (1u << c))) continue;
+          const uint32_t q = 2 * lane + (c ? 0u : 1u);
+          int64_t cnt = 0;
+          for (uint32_t pq = 0; pq < q; ++pq) cnt += m.ce[pq] > ts ? 1 : 0;  // INT64_MIN: no copy
+          over |= base + cnt >= (int64_t)TGSIM_NETEM_LIMIT;
+        }
+        if (__ballot(over) == 0) {
+          adm = valid;
+        } else {  // decide copy by copy, in enqueue order, counting the earlier admitted ones
+          for (uint32_t q = 0; q < 2 * cn; ++q) {
+            const int owner = (int)(q >> 1), c = (q & 1u) ? 0 : 1;
+            const int64_t tq = __shfl(ts, owner), bq = __shfl(base, owner);
+            const uint32_t vq = __shfl((uint32_t)valid, owner);
+            const uint64_t b1 = __ballot((adm & 2u) && 2 * lane < q && e2[1] > tq);
+            const uint64_t b0 = __ballot((adm & 1u) && 2 * lane + 1 < q && e2[0] > tq);
+            const bool in = ((vq >> c) & 1u) && bq + (int64_t)(__popcll(b1) + __popcll(b0)) < (int64_t)TGSIM_NETEM_LIMIT;
+            if ((int)lane == owner && in) adm |= (uint8_t)(1u << c);
+          }
+        }
+        if (lane < cn) {
+          if (st != TGSIM_ST_LOST) {
+            const uint8_t dropped = valid & ~adm;
+            if (dropped & 2u) st |= TGSIM_ST_FLAG_CLONE_LOST;
+            if (dropped & 1u) st |= TGSIM_ST_FLAG_OVERLIMIT;
+            if (!adm) st = (uint8_t)((st & 0xF0u) | TGSIM_ST_OVERLIMIT);
+            n_over += (uint32_t)__popc(dropped);
+            n_copies += (uint32_t)__popc(adm);
+          } else {
+            ++n_lost;
+          }
+          m.st[lane] = st;
+          m.adm[lane] = adm;
+          for (int c = 0; c < 2; ++c) { m.ct[c][lane] = e2[c]; m.cm[c][lane] = meta2[c]; m.co[c][lane] = coff2[c]; }
+        }
+        // the queue after the chunk: departures up to its last enqueue have left; copies going past
+        // the window stay counted in far; the rest join K
+        const int64_t t_last = __shfl(ts, (int)cn - 1);
+        uint32_t nfar = 0, nk = 0;
+        for (int c = 0; c < 2; ++c) {
+          const bool in = (adm >> c) & 1u;
+          nfar += in && e2[c] >= t_end ? 1u : 0u;
+          const bool keep = in && e2[c] < t_end && e2[c] > t_last;
+          const uint64_t bk = __ballot(keep);
+          if (keep) m.cb[nk + mask_rank(bk)] = e2[c];  // slots per round, filled below
+          nk += (uint32_t)__popcll(bk);
+        }
+        far += wave_sum(nfar);
+        kh = upper_idx(kcur ? m.kd : m.ue, kh, ksz, t_last);
+        if (nk) {
+          const uint32_t np2 = nk > 1 ? next_pow2(nk) : 1u;
+          for (uint32_t j = nk + lane; j < np2; j += kSeqChunk) m.cb[j] = INT64_MAX;
+          __syncthreads();
+          if (np2 > 1) wave_bitonic(m.cb, np2);
+          uint32_t na = ksz - kh;
+          if (na + nk > (uint32_t)kSeqCap) {  // cannot happen: the queue never holds more than the limit
+            if (lane == 0) atomicOr(&sc->err, ERR_QUEUE_CAP);
+            na = (uint32_t)kSeqCap - nk;
+          }
+          wave_merge((kcur ? m.kd : m.ue) + kh, na, m.cb, nk, kcur ? m.ue : m.kd);
+          kcur ^= 1u;
+          kh = 0;
+          ksz = na + nk;
+        }
+        __syncthreads();
+      }
       // sequential: netem_enqueue per message in qdisc order
-      if (lane == 0) {
+      if (!fast && lane == 0) {
         for (uint32_t k = 0; k < cn; ++k) {
           const int64_t ts = m.mt[k];
           const uint32_t size = m.msize[k];
@@ -2422,6 +2622,9 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
       a.Q.push_batch<2>(qs, rs, c0);
       __syncthreads();
     }
+    n_lost = wave_sum(n_lost);  // the walk counts in lane 0, the parallel form in every lane
+    n_copies = wave_sum(n_copies);
+    n_over = wave_sum(n_over);
     if (lane == 0) {
       if (corr) { last4[4 * l] = cl[0]; last4[4 * l + 1] = cl[1]; last4[4 * l + 2] = cl[2]; }
       unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
@@ -3461,7 +3664,10 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
                          d.plan_start, d.plan_off, d.arena, Q, a, ne, ho);
     }
     TG_CHECK(hipGetLastError());
-    if (d.any_corr || d.heavy.pend) TG_CHECK(run_shape_seq(d, a, n_staged));
+    if (d.any_corr || d.heavy.pend) {
+      ProfScope ps_(d, KID_SHAPE_SEQ);  // deferred messages grouped + the sequential lane
+      TG_CHECK(run_shape_seq(d, a, n_staged));
+    }
   }
   TG_CHECK(run_token_bucket(d));
   if (d.S > 1) {

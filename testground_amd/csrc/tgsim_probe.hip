@@ -227,6 +227,7 @@ hipError_t launch_probe_start(Dev& d, bool base_dev, uint32_t base_host, int64_t
 hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev) {
   ProbeDev& p = d.pr;
+  ProfScope ps_(d, KID_PROBE);
   hipLaunchKernelGGL(k_probe_reset, dim3(1), dim3(1), 0, d.stream, p);
   hipLaunchKernelGGL(k_probe_status, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst,
                      d.m_seq, n_status_host, n_status_dev, p, d.lo);

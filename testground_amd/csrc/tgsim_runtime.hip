@@ -127,7 +127,7 @@ struct tgsim_ctx {
   bool any_dup = false;
   // cross-shard transport: the exchange, the storm batch's MAX all-reduce and the
   // signal all-gather run inside the library - natively over RCCL (comm), or through caller callbacks
-  bool has_tr = false;
+  bool has_tr = false, tr_aborted = false;
   tgsim_transport tr{};
   ncclComm_t comm = nullptr;
   int64_t* d_red2 = nullptr;   // [2] storm batch: {last time, -first time} for the MAX all-reduce
@@ -1358,7 +1358,9 @@ static int tgsim_comm_init_body(tgsim_ctx* c, const uint8_t id[TGSIM_COMM_ID_BYT
   c->tr.alltoall = rccl_alltoall;
   c->tr.allreduce_max_i64 = rccl_allreduce_max;
   c->tr.allgather = rccl_allgather;
+  c->tr.abort = nullptr;  // shard_failed aborts the communicator itself
   c->has_tr = true;
+  c->tr_aborted = false;
   return TGSIM_OK;
 }
 
@@ -1373,6 +1375,7 @@ static int tgsim_set_transport_body(tgsim_ctx* c, const tgsim_transport* t) {
   if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
   c->has_tr = t != nullptr;
   c->tr = t ? *t : tgsim_transport{};
+  c->tr_aborted = false;
   return TGSIM_OK;
 }
 
@@ -1386,13 +1389,43 @@ static int exchange_window(tgsim_ctx* c) {
 
 static int need_transport(tgsim_ctx* c) {
   if (c->S != 1 && !c->has_tr)
-    return fail(c, TGSIM_ESTATE, "a sharded context needs a transport (tgsim_comm_init / tgsim_set_transport) or begin/end");
+    return fail(c, TGSIM_ESTATE, c->tr_aborted ? "the transport was aborted (a shard failed)"
+                                               : "a sharded context needs a transport (tgsim_comm_init / tgsim_set_transport) or begin/end");
   return TGSIM_OK;
 }
 
+// A shard whose sharded call fails must not leave the others waiting in a collective it will never
+// join: the caller's transport is told (tgsim_transport.abort) and the native
+// communicator aborted, so the peers' pending and later collectives fail; sharded calls are then
+// refused here.
+static int shard_failed(tgsim_ctx* c, int rc) {
+  if (rc == TGSIM_OK || c == nullptr || c->S == 1 || !c->has_tr) return rc;
+  if (c->comm) {
+    (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+  } else if (c->tr.abort) {
+    c->tr.abort(c->tr.user);
+  }
+  c->has_tr = false;
+  c->tr_aborted = true;
+  c->in_window = false;
+  return rc;
+}
+
+static int tgsim_comm_abort_body(tgsim_ctx* c);
+extern "C" int tgsim_comm_abort(tgsim_ctx* c) {
+  return abi_guard(c, [&] { return tgsim_comm_abort_body(c); });
+}
+static int tgsim_comm_abort_body(tgsim_ctx* c) {
+  if (!c) return TGSIM_EINVAL;
+  (void)shard_failed(c, TGSIM_ESTATE);
+  return TGSIM_OK;
+}
+
+
 static int tgsim_advance_body(tgsim_ctx* c, int64_t t_end);
 extern "C" int tgsim_advance(tgsim_ctx* c, int64_t t_end) {
-  return abi_guard(c, [&] { return tgsim_advance_body(c, t_end); });
+  return abi_guard(c, [&] { return shard_failed(c, tgsim_advance_body(c, t_end)); });
 }
 static int tgsim_advance_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
@@ -1411,7 +1444,7 @@ static int tgsim_advance_body(tgsim_ctx* c, int64_t t_end) {
 
 static int tgsim_advance_async_body(tgsim_ctx* c, int64_t t_end);
 extern "C" int tgsim_advance_async(tgsim_ctx* c, int64_t t_end) {
-  return abi_guard(c, [&] { return tgsim_advance_async_body(c, t_end); });
+  return abi_guard(c, [&] { return shard_failed(c, tgsim_advance_async_body(c, t_end)); });
 }
 static int tgsim_advance_async_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
@@ -1428,7 +1461,7 @@ static int tgsim_advance_async_body(tgsim_ctx* c, int64_t t_end) {
 
 static int tgsim_advance_to_barrier_body(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns);
 extern "C" int tgsim_advance_to_barrier(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
-  return abi_guard(c, [&] { return tgsim_advance_to_barrier_body(c, waiter, offset_ns); });
+  return abi_guard(c, [&] { return shard_failed(c, tgsim_advance_to_barrier_body(c, waiter, offset_ns)); });
 }
 static int tgsim_advance_to_barrier_body(tgsim_ctx* c, uint32_t waiter, int64_t offset_ns) {
   if (!c) return TGSIM_EINVAL;
@@ -1602,7 +1635,7 @@ static int tgsim_sync_signal_body(tgsim_ctx* c, const uint32_t* states, const ui
                                  size_t n, uint32_t* seq_out);
 extern "C" int tgsim_sync_signal(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                                  size_t n, uint32_t* seq_out) {
-  return abi_guard(c, [&] { return tgsim_sync_signal_body(c, states, inst, t, n, seq_out); });
+  return abi_guard(c, [&] { return shard_failed(c, tgsim_sync_signal_body(c, states, inst, t, n, seq_out)); });
 }
 static int tgsim_sync_signal_body(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t,
                                  size_t n, uint32_t* seq_out) {
@@ -1700,7 +1733,7 @@ static int tgsim_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, 
                                      int64_t spread_ns, uint32_t state);
 extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {
-  return abi_guard(c, [&] { return tgsim_gen_storm_round_body(c, round, t0, fanout, size, spread_ns, state); });
+  return abi_guard(c, [&] { return shard_failed(c, tgsim_gen_storm_round_body(c, round, t0, fanout, size, spread_ns, state)); });
 }
 static int tgsim_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {

@@ -56,9 +56,18 @@ class Transport:
                     traceback.print_exc()
                     return -1
             return cb
+        def abort_cb(_user):
+            try:
+                self.abort()
+            except Exception:  # noqa: BLE001 - an abort must not raise into the library
+                traceback.print_exc()
         self._cbs = (A.ALLTOALL_FN(wrap(self.alltoall)), A.ALLREDUCE_FN(wrap(self.allreduce_max)),
-                     A.ALLGATHER_FN(wrap(self.allgather)))
+                     A.ALLGATHER_FN(wrap(self.allgather)), A.ABORT_FN(abort_cb))
         self.c = A.Transport(None, *self._cbs)
+
+    def abort(self):
+        """tgsim_transport.abort: this shard failed; the peers' pending and later collectives must
+        fail instead of waiting for it."""
 
     def alltoall(self, send, recv, block, stream):
         raise NotImplementedError
@@ -96,6 +105,10 @@ class GlooTransport(Transport):
             return
         if len(arr):
             assert self.hip.hipMemcpy(addr, arr.ctypes.data, len(arr), _H2D) == 0
+
+    def abort(self):
+        # the peers' gloo collectives fail once this rank's connections close
+        self.dist.destroy_process_group()
 
     def alltoall(self, send, recv, block, stream):
         import torch
@@ -144,6 +157,9 @@ class _ThreadMember(Transport):
     def __init__(self, g: ThreadGroup, k: int):
         super().__init__()
         self.g, self.k = g, k
+
+    def abort(self):
+        self.g.bar.abort()   # every pending and later wait raises BrokenBarrierError -> -1
 
     def _sync(self, stream):
         if self.g.device:

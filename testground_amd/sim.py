@@ -155,6 +155,11 @@ class Simulator:
         m = A.MsgSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), _ptr(t))
         self._check(self.lib.enqueue(self._ctx, C.byref(m), n))
 
+    def enqueue_device(self, src_ptr: int, dst_ptr: int, seq_ptr: int, size_ptr: int, t_ptr: int, n: int) -> None:
+        """tgsim_enqueue_device: n messages already in device memory (SoA at the given addresses)."""
+        m = A.MsgSoA(src_ptr, dst_ptr, seq_ptr, size_ptr, t_ptr)
+        self._check(self.lib.enqueue_device(self._ctx, C.byref(m), n))
+
     # ---- TCP mode (tgsim_tcp_*, DESIGN.md 2.11) ------------------------------------------------
     def tcp_enable(self, mss: int = 0, header_bytes: int = 0, rto_ns: int = 0, max_attempts: int = 0,
                    max_writes: int = 0, max_segments: int = 0, acks: bool = False) -> None:
@@ -267,6 +272,10 @@ class Simulator:
         self._check(self.lib.storm_release_device(self._ctx, out_dev))
 
     # ---- cross-shard transport ---------------------------------------------
+    def comm_abort(self) -> None:
+        """tgsim_comm_abort: this shard stops; no peer waits for it in a collective."""
+        self._check(self.lib.comm_abort(self._ctx))
+
     def set_transport(self, transport) -> None:
         """A testground_amd.exchange transport (or None): tgsim_advance* then exchange inside the
         call, storm batches and signal batches reduce / gather across the shards."""
@@ -499,6 +508,12 @@ class Simulator:
         ne, act = C.c_int64(), C.c_uint32()
         self._check(self.lib.probe_react(self._ctx, C.byref(ne), C.byref(act)))
         return ne.value, act.value
+
+    def probe_state_device(self) -> tuple[int, int]:
+        """Device addresses of the proposed next window end (int64) and the probers still active."""
+        a, b = C.c_void_p(), C.c_void_p()
+        self._check(self.lib.probe_state_device(self._ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def probe_results(self) -> tuple[np.ndarray, np.ndarray]:
         """(outcome[local, position in order] of TGSIM_PROBE_*, t_done[local])."""

@@ -103,3 +103,18 @@ def test_create_rejects_bad_config(oracle):
         with pytest.raises(A.TgsimError) as e:
             Simulator(SimConfig(**kw), binding=oracle)
         assert e.value.code == A.EINVAL
+
+
+def test_one_rccl_per_process():
+    """libtgsim.so needs librccl.so.1 (soname); torch's bundled RCCL has the same soname, so in a
+    process that imported torch first (bench.py, the tests) the dynamic loader satisfies libtgsim's
+    dependency with torch's copy: exactly one RCCL build is mapped. Without torch
+    (a Go runner) /opt/rocm's is the one."""
+    import subprocess
+    import sys
+    code = ("import torch, ctypes, sys; ctypes.CDLL(sys.argv[1]); "
+            "print(sorted({l.split()[-1] for l in open('/proc/self/maps') if 'librccl' in l}))")
+    out = subprocess.run([sys.executable, "-c", code, A.LIB_PATH], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    paths = eval(out.stdout.strip().splitlines()[-1])
+    assert len(paths) == 1, paths

@@ -142,3 +142,62 @@ def test_sharded_gloo(oracle, world):
     _, srcs = S.run_random_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
     S.assert_sharded_matches([got[r][0] for r in range(world)], srcs, S.run_random(oracle, seed), world)
     S.assert_storm_sharded([got[r][1] for r in range(world)], S.run_storm(oracle, n_inst=600, rounds=3), world, 600)
+
+
+def _failing_shard_run(binding, device=False, world=3):
+    """World 3 over a thread group; two windows run normally, then shard 1 asks for a window that ends
+    before its clock (ECAUSALITY) while the others enter the window's exchange. Every shard must
+    return an error, within seconds, instead of waiting for shard 1."""
+    import threading
+    import time
+
+    from testground_amd import _abi as A
+    from testground_amd.exchange import ThreadGroup, run_threads
+    MS = 1_000_000
+    g = ThreadGroup(world, device=device, timeout=120.0)
+    codes, elapsed = [None] * world, [None] * world
+    start = threading.Barrier(world)
+
+    def shard(k):
+        sim = Simulator(SimConfig(n_instances=24, seed=1, shard_id=k, n_shards=world, exchange_cap=1 << 10,
+                                  max_msgs_per_window=1 << 12, max_records=1 << 14), binding=binding)
+        sim.set_transport(g.member(k))
+        for w in range(2):
+            src = np.arange(sim.lo, sim.hi, dtype=np.uint32)
+            sim.enqueue(src, (src + 5) % 24, np.full(len(src), w), np.full(len(src), 100), np.full(len(src), w * MS))
+            sim.advance((w + 1) * MS)
+        start.wait()
+        t0 = time.perf_counter()
+        try:
+            sim.advance(1 * MS if k == 1 else 3 * MS)   # shard 1: t_end before its clock
+            codes[k] = A.OK
+        except A.TgsimError as e:
+            codes[k] = e.code
+        elapsed[k] = time.perf_counter() - t0
+        try:                                             # the context refuses sharded calls now
+            sim.advance(4 * MS)
+            after = A.OK
+        except A.TgsimError as e:
+            after = e.code
+        sim.close()
+        return after
+
+    after = run_threads([lambda k=k: shard(k) for k in range(world)])
+    return codes, elapsed, after
+
+
+def test_shard_failure_aborts_peers(oracle):
+    from testground_amd import _abi as A
+    codes, elapsed, after = _failing_shard_run(oracle)
+    assert codes[1] == A.ECAUSALITY
+    assert codes[0] == A.EHIP and codes[2] == A.EHIP          # their exchange failed instead of waiting
+    assert max(elapsed) < 10.0
+    assert all(a == A.ESTATE for a in after)
+
+
+@pytest.mark.gpu
+def test_shard_failure_aborts_peers_hip(hip):
+    from testground_amd import _abi as A
+    codes, elapsed, after = _failing_shard_run(hip, device=True)
+    assert codes[1] == A.ECAUSALITY and codes[0] == A.EHIP and codes[2] == A.EHIP
+    assert max(elapsed) < 10.0 and all(a == A.ESTATE for a in after)
