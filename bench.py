@@ -473,10 +473,31 @@ def _attach_transport(sim, dist, world: int, rank: int, rehearsal: bool) -> str:
             print(f"rank 0: RCCL unique id failed ({e}); falling back to the gloo transport",
                   file=sys.stderr, flush=True)
     dist.broadcast_object_list(uid, src=0)
-    ok = 1
+    # ncclCommInitRank blocks until every rank joins: agree over gloo first that every rank can
+    # (a unique id, a working device of its own), so that one rank failing fast cannot leave the
+    # others waiting in RCCL's bootstrap
+    import socket
+    pre = 1
+    dev = None
     try:
         if uid[0] is None:
             raise RuntimeError("no RCCL unique id")
+        dev = torch.cuda.current_device()
+        torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001 - reported, then every rank takes the same path
+        print(f"rank {rank}: RCCL preconditions failed ({e})", file=sys.stderr, flush=True)
+        pre = 0
+    where = [None] * world
+    dist.all_gather_object(where, (socket.gethostname(), dev))
+    if pre and len(set(where)) != world:
+        print(f"rank {rank}: ranks share a device ({where}); no RCCL communicator", file=sys.stderr, flush=True)
+        pre = 0
+    flag = torch.tensor([pre], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    ok = 1
+    try:
+        if int(flag.item()) != 1:
+            raise RuntimeError("a rank failed the RCCL preconditions")
         sim.comm_init(uid[0], world, rank)
     except Exception as e:  # noqa: BLE001 - reported, then every rank takes the same path
         print(f"rank {rank}: RCCL communicator failed ({e}); falling back to the gloo transport",

@@ -49,6 +49,14 @@ struct alignas(16) ShapeDev {
   uint32_t mult, shift, flags;    // HTB rate as multiply-shift; flags: kShLimited, kShCorr
 };
 static_assert(sizeof(ShapeDev) == 48, "ShapeDev layout");
+
+// The token bucket's share of ShapeDev (16 B; gathered by sender in k_tb_bucket / k_rest<TB>, where
+// the 48 B entry cost a third of the flood's token-bucket traffic).
+struct alignas(16) TbShape {
+  int64_t tau;
+  uint32_t mult, shift;
+};
+static_assert(sizeof(TbShape) == 16, "TbShape layout");
 constexpr uint32_t kShLimited = 1u;  // Bandwidth != 0
 constexpr uint32_t kShCorr = 2u;     // a correlated netem draw is used (messages deferred to k_shape_corr)
 

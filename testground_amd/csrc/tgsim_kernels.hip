@@ -1430,14 +1430,15 @@ __device__ __forceinline__ int64_t mp_apply(MP f, int64_t x) {
   return v > f.B ? v : f.B;
 }
 
-__device__ __forceinline__ uint64_t l2t_ns(const ShapeDev& sh, uint32_t len) {
+template <class Sh>
+__device__ __forceinline__ uint64_t l2t_ns(const Sh& sh, uint32_t len) {
   const uint64_t c = ((uint64_t)len * sh.mult) >> sh.shift;
   return c > kCostClamp ? kCostClamp : c;
 }
 
 struct TBPolicy {
   const tgsim_record* A;
-  const ShapeDev* shape;
+  const TbShape* shape;
   int64_t* X;
   uint32_t* pend;  // queue occupancy: a wheel copy leaving now (D / X) no longer counts
   uint32_t lo;
@@ -1469,7 +1470,7 @@ struct TBPolicy {
       if (j >= m) break;
       const uint32_t e_ = s.perm[j];
       const uint32_t sl = s.sg[j];
-      const ShapeDev& sh = shape[sl];
+      const TbShape& sh = shape[sl];
       const int64_t e = (int64_t)s.k1[e_];
       const int64_t c = (int64_t)l2t_ns(sh, A[s.k3[e_]].size);
       const bool head = (j == 0) ? !has_carry : (s.sg[j - 1] != sl);
@@ -1513,7 +1514,7 @@ struct TBPolicy {
       if (j < m) {
         const uint32_t e_ = s.perm[j];
         const uint32_t sl = s.sg[j];
-        const ShapeDev& sh = shape[sl];
+        const TbShape& sh = shape[sl];
         const int64_t e = (int64_t)s.k1[e_];
         load_rec(A + s.k3[e_], rec);
         const int64_t c = (int64_t)l2t_ns(sh, rec.size);
@@ -1891,7 +1892,7 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     const uint32_t a = i ? sm.cnt[i - 1] : 0u, e = sm.cnt[i];
     if (e == a || e - a > kBktRankMax) continue;
     const uint32_t sl = h.k0 + i;
-    const ShapeDev sh = p.shape[sl];
+    const TbShape sh = p.shape[sl];
     int64_t x = p.X[sl];
     for (uint32_t r = a; r < e; ++r) {
       const uint32_t s = sm.ord[r];
@@ -3561,7 +3562,7 @@ static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const ui
 // and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
 static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
-  p.A = d.A; p.shape = d.shape; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
+  p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= kMaxBins (bkt_width_fused)

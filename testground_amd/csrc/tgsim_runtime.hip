@@ -32,6 +32,7 @@ struct tgsim_ctx {
   uint32_t N = 0, S = 1, shard = 0, lo = 0, hi = 0, nloc = 0;
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
   std::vector<ShapeDev> shape_h;
+  std::vector<TbShape> tbs_h;       // source of the last d.tbs upload (kept alive for the async copy)
   std::vector<uint8_t> flags_h;
   std::vector<uint32_t> ip_h;
   uint64_t space = 0;               // addresses in the data subnet
@@ -441,6 +442,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   int rc = 0;
   rc |= dalloc(c, &d.sc, 1);
   rc |= dalloc(c, &d.shape, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.tbs, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &c->d_red2, 2);
@@ -934,10 +936,14 @@ static int upload_tables(tgsim_ctx* c) {
     HIPCK(c, hipMemcpyAsync(d.cor_rho, c->rho_h.data(), c->rho_h.size() * 4, hipMemcpyHostToDevice, d.stream), "upload shapes");
     d.any_corr = false;
     c->any_dup = false;
-    for (const ShapeDev& sh : c->shape_h) {
+    c->tbs_h.resize(c->nloc);
+    for (uint32_t l = 0; l < c->nloc; ++l) {
+      const ShapeDev& sh = c->shape_h[l];
       d.any_corr |= (sh.flags & kShCorr) != 0;
       c->any_dup |= sh.dup_t != 0;
+      c->tbs_h[l] = TbShape{sh.tau, sh.mult, sh.shift};
     }
+    HIPCK(c, hipMemcpyAsync(d.tbs, c->tbs_h.data(), c->nloc * sizeof(TbShape), hipMemcpyHostToDevice, d.stream), "upload shapes");
     copied = true;
   }
   if (!c->corr_reset.empty()) {
