@@ -144,12 +144,17 @@ struct Queues {
   // record-major, lane-minor (one ballot per record), so each store instruction covers consecutive
   // records; A and D slots go by consumer group (a per-wave counting sort in LDS), so each line is
   // read by one XCD. Exchange records (sharded runs) take the per-record path.
+  // spread: the salt alone picks the sub-queue (any of the 64), for a producer whose one workgroup
+  // may append far more than a sub-queue's share (k_shape_seq: one sender per workgroup, every one
+  // of its chunks in turn; with the XCD-pinned choice a 10k-reply sender filled one sub-queue)
   template <int U>
-  __device__ __forceinline__ void push_batch(const int (&q)[U], const tgsim_record (&r)[U], uint32_t salt) const {
+  __device__ __forceinline__ void push_batch(const int (&q)[U], const tgsim_record (&r)[U], uint32_t salt,
+                                             bool spread = false) const {
     __shared__ uint32_t gcnt[kBlock / 64][16];  // per wave: [A groups 0..7 | D groups 0..7]
     const uint32_t lane = lane_id();
     uint32_t* cnt = gcnt[threadIdx.x >> 6];
-    const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
+    const uint32_t sub = spread ? (salt & (kNSub - 1u))
+                                : ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
     // any lanes may be active (grid-stride tails): the first active one keeps the 16 counters
     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
     if (lane == leader)
@@ -2620,7 +2625,8 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
       }
       const int qs[2] = {q1, q2};
       const tgsim_record rs[2] = {r1, r2};
-      a.Q.push_batch<2>(qs, rs, c0);
+      // chunk k of sender l: sub-queue (l + k) % 64, so one sender's appends spread over all of them
+      a.Q.push_batch<2>(qs, rs, l + (c0 - j0) / kSeqChunk, true);
       __syncthreads();
     }
     n_lost = wave_sum(n_lost);  // the walk counts in lane 0, the parallel form in every lane

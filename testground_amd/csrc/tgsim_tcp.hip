@@ -622,7 +622,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
       }
       head = t.c_head[k];
       const uint32_t qd = t.c_queued[k];
-      go = fl < cw ? min(cw - fl, qd) : 0u;
+      // a write onto a reset connection stays queued until the next reaction fails it at that
+      // window's end (tgo_tcp_write releases only connections that are not broken)
+      go = fl < cw && !t.c_broken[k] ? min(cw - fl, qd) : 0u;
       if (go) {
         t.c_flight[k] = fl + go;
         t.c_queued[k] = qd - go;
