@@ -151,6 +151,7 @@ struct Dev {
   // tables
   ShapeDev* shape = nullptr;
   TbShape* tbs = nullptr;  // [nloc] the token bucket's fields of shape (uploaded with it)
+  uint32_t* zd = nullptr;  // [nloc / 32 + 1] zero-delay unshaped senders (Heavy::zd, uploaded with shape)
   int64_t* X = nullptr;
   // [N] ip | flags << 32 per instance (flags bit0 link enabled, bit1 external routing allowed): one
   // 8-B gather gives a destination's address and link state

@@ -117,13 +117,20 @@ constexpr int ST_OVERLIMIT = 13;  // a row counter only ([kNSub][16] rows; ST_DE
 // could add in the window may reach the limit; only then are its messages decided sequentially
 // (k_shape_seq). m_uniform bounds the messages any sender stages in the window, m_inbox * (its last
 // inbox run) the flood forwards; mult = 2 when some shape duplicates.
+// A sender with a zero-delay, unshaped link (latency 0, jitter 0, no HTB: every copy departs at its
+// enqueue instant, so the next enqueue finds it gone) adds nothing to its own queue: only the copies
+// queued at the window start (pend) can count, and it is heavy only when they alone reach the limit
+// (zd: bit per local sender, from the shape table). The splitbrain target that receives 10k requests
+// in a window then answers them in the parallel netem pass instead of one wave's chunk walk.
 struct Heavy {
   const uint32_t* pend;   // nullptr: the host proved no sender can reach the limit this window
   const uint32_t* inbox;  // [nloc + 1] the last window's inbox offsets (flood forwards), or nullptr
   const uint32_t* retx;   // TCP mode: [nloc] retransmissions pending or released into this window
+  const uint32_t* zd;     // [nloc / 32 + 1] zero-delay unshaped senders
   uint32_t m_uniform, m_inbox, mult;
   __host__ __device__ bool of(uint32_t l) const {
     if (!pend) return false;
+    if (zd && ((zd[l >> 5] >> (l & 31u)) & 1u)) return pend[l] >= TGSIM_NETEM_LIMIT;
     uint64_t m = m_uniform;
     if (m_inbox) m += (uint64_t)m_inbox * (inbox[l + 1] - inbox[l]);
     if (retx) m += retx[l];

@@ -674,6 +674,8 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
                                              uint32_t bid, uint32_t nblocks, const HeavyOut& ho) {
   __shared__ uint32_t s_off[kPlanLds];
   __shared__ uint64_t s_src[kPlanLds];
+  __shared__ uint32_t s_hred[kBlock / 64];
+  __shared__ uint32_t s_hbase;
   DevScalars* sc = Q.sc;
   const uint32_t total = sc->n_extract, tail = sc->plan_tail, nl = sc->plan_n;
   const int64_t t_end = sc->t_end;
@@ -720,14 +722,27 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
                                 : Q_L);
     }
     Q.push_batch<kExtractUnroll>(qs, rec, it);
+    if (ho.hv.pend) {  // launch-uniform
+      // one reservation on the H counter per block and round: every due record of an all-to-all
+      // round is a heavy sender's, and a reservation per wave serialised ~16k atomics on one
+      // address (~170 us of the extraction)
+      bool h[kExtractUnroll];
+      uint32_t nh = 0;
 #pragma unroll
-    for (int u = 0; u < kExtractUnroll; ++u) {
-      const uint32_t j = base + u * kBlock + threadIdx.x;
-      const bool due = j < total && rec[u].t < t_end;
-      if (ho.hv.pend) {  // launch-uniform
-        const bool h = due && ho.hv.of(rec[u].src - ho.lo);
-        const uint32_t pos = wave_append(h ? &sc->n_hrec : nullptr);
-        if (h) {
+      for (int u = 0; u < kExtractUnroll; ++u) {
+        const uint32_t j = base + u * kBlock + threadIdx.x;
+        h[u] = j < total && rec[u].t < t_end && ho.hv.of(rec[u].src - ho.lo);
+        nh += h[u] ? 1u : 0u;
+      }
+      uint32_t tot_h;
+      uint32_t pos = block_excl_scan(nh, s_hred, tot_h);
+      if (tot_h) {  // block-uniform
+        if (threadIdx.x == 0) s_hbase = atomicAdd(&sc->n_hrec, tot_h);
+        __syncthreads();
+        pos += s_hbase;
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+          if (!h[u]) continue;
           if (pos < ho.hcap) {
             store_rec(ho.H + pos, rec[u]);
             ho.hkeys[pos] = rec[u].src - ho.lo;
@@ -735,7 +750,9 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
           } else {
             atomicOr(&sc->err, ERR_QUEUE_CAP);
           }
+          ++pos;
         }
+        __syncthreads();  // s_hbase is rewritten by the next round
       }
     }
   }
@@ -2202,9 +2219,9 @@ struct SeqSmem {
   uint32_t co[2][kSeqChunk];     // queued copy: corrupt offset
   uint8_t st[kSeqChunk], adm[kSeqChunk];  // status, queued copies (bit c = copy c)
   uint32_t nu, nk;
-  // parallel form: the chunk's candidate copies in enqueue order (INT64_MIN: none) and the admitted
-  // ones that outlive the chunk, sorted; K lives in ue / kd (two ascending buffers)
-  int64_t ce[2 * kSeqChunk], cb[2 * kSeqChunk];
+  // parallel form: the chunk's admitted copies that outlive it, sorted; K lives in ue / kd (two
+  // ascending buffers)
+  int64_t cb[2 * kSeqChunk];
 };
 
 __device__ __forceinline__ bool u_less(const SeqSmem& m, uint32_t a, uint32_t b) {
@@ -2345,19 +2362,47 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
     bool fast = heavy && !corr && !limited;
     uint32_t kcur = 0, kh = 0, ksz = 0;  // K: ascending in m.ue (kcur 0) or m.kd (kcur 1), [kh, ksz) live
     if (fast) {
+      // one pass over the due records: their departures into K (padded to a power of two) and whether
+      // any is a stage-A record (queued under an earlier, limited shape: heaps). Four records per lane
+      // in flight: a dependent index -> record chain per 64 records took ~2 us each.
       const uint32_t h0 = hoff[l], h1 = hoff[l + 1];
+      uint32_t n0 = h1 - h0;
+      if (n0 > (uint32_t)kSeqCap) {
+        if (lane == 0) atomicOr(&sc->err, ERR_QUEUE_CAP);
+        n0 = kSeqCap;
+      }
+      const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
       bool anyA = false;
-      for (uint32_t b = h0 + lane; b < h1; b += kSeqChunk) anyA |= !(H[hidx[b]].meta & TGSIM_F_STAGE_D);
-      fast = __ballot(anyA) == 0;  // a stage-A record (queued under an earlier, limited shape): heaps
-      if (fast) {
-        uint32_t n0 = h1 - h0;
-        if (n0 > (uint32_t)kSeqCap) {
-          if (lane == 0) atomicOr(&sc->err, ERR_QUEUE_CAP);
-          n0 = kSeqCap;
+      for (uint32_t j0 = 0; j0 < np2; j0 += 4 * kSeqChunk) {
+        uint32_t ix[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t j = j0 + u * kSeqChunk + lane;
+          ix[u] = j < n0 ? hidx[h0 + j] : 0u;
         }
-        const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
-        for (uint32_t j = lane; j < np2; j += kSeqChunk) m.ue[j] = j < n0 ? H[hidx[h0 + j]].t : INT64_MAX;
-        __syncthreads();
+        uint4 ra[4], rb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t j = j0 + u * kSeqChunk + lane;
+          if (j < n0) {
+            ra[u] = reinterpret_cast<const uint4*>(H + ix[u])[0];
+            rb[u] = reinterpret_cast<const uint4*>(H + ix[u])[1];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t j = j0 + u * kSeqChunk + lane;
+          if (j < n0) {
+            m.ue[j] = (int64_t)(((uint64_t)ra[u].y << 32) | ra[u].x);
+            anyA |= !(rb[u].z & TGSIM_F_STAGE_D);
+          } else if (j < np2) {
+            m.ue[j] = INT64_MAX;
+          }
+        }
+      }
+      fast = __ballot(anyA) == 0;
+      __syncthreads();
+      if (fast) {
         if (np2 > 1) wave_bitonic(m.ue, np2);
         ksz = n0;
         const uint32_t p = a.heavy.pend[l];
@@ -2461,26 +2506,25 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
           }
           base = (int64_t)far + (int64_t)(ksz - upper_idx(kcur ? m.kd : m.ue, kh, ksz, ts));
         }
-        // enqueue order: message by message, clone (c = 1) before original (c = 0)
-        m.ce[2 * lane] = (valid & 2u) ? e2[1] : INT64_MIN;
-        m.ce[2 * lane + 1] = (valid & 1u) ? e2[0] : INT64_MIN;
-        __syncthreads();
-        // every earlier copy admitted: the largest count any copy could see
+        // every earlier copy admitted and still queued: at most q of them before copy q (enqueue order:
+        // message by message, clone first), so base + q below the limit admits every copy of the chunk
         bool over = false;
-        for (int c = 1; c >= 0; --c) {
-          if (!(valid & (1u << c))) continue;
-          const uint32_t q = 2 * lane + (c ? 0u : 1u);
-          int64_t cnt = 0;
-          for (uint32_t pq = 0; pq < q; ++pq) cnt += m.ce[pq] > ts ? 1 : 0;  // INT64_MIN: no copy
-          over |= base + cnt >= (int64_t)TGSIM_NETEM_LIMIT;
-        }
+        for (int c = 1; c >= 0; --c)
+          if (valid & (1u << c)) over |= base + (int64_t)(2 * lane + (c ? 0u : 1u)) >= (int64_t)TGSIM_NETEM_LIMIT;
         if (__ballot(over) == 0) {
           adm = valid;
         } else {  // decide copy by copy, in enqueue order, counting the earlier admitted ones
+          // the owner's fields come through readlane (q is wave-uniform): scalar registers, no LDS
+          // round trip per copy as a shuffle would take
+          const uint32_t ts_lo = (uint32_t)(uint64_t)ts, ts_hi = (uint32_t)((uint64_t)ts >> 32);
+          const uint32_t b_lo = (uint32_t)(uint64_t)base, b_hi = (uint32_t)((uint64_t)base >> 32);
           for (uint32_t q = 0; q < 2 * cn; ++q) {
             const int owner = (int)(q >> 1), c = (q & 1u) ? 0 : 1;
-            const int64_t tq = __shfl(ts, owner), bq = __shfl(base, owner);
-            const uint32_t vq = __shfl((uint32_t)valid, owner);
+            const int64_t tq = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ts_hi, owner) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((int)ts_lo, owner));
+            const int64_t bq = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)b_hi, owner) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((int)b_lo, owner));
+            const uint32_t vq = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)valid, owner);
             const uint64_t b1 = __ballot((adm & 2u) && 2 * lane < q && e2[1] > tq);
             const uint64_t b0 = __ballot((adm & 1u) && 2 * lane + 1 < q && e2[0] > tq);
             const bool in = ((vq >> c) & 1u) && bq + (int64_t)(__popcll(b1) + __popcll(b0)) < (int64_t)TGSIM_NETEM_LIMIT;
@@ -3473,9 +3517,12 @@ static Queues make_queues(Dev& d) {
 }
 
 // Bucket shift: <= 2048 buckets of <= 2^kBktMaxKeyBits keys, 128 keys per bucket where possible.
-static int bkt_shift(uint32_t K) {
+// fine: as few keys per bucket as 2048 buckets allow (one per key when K <= 2048) - for batches with
+// many items per key (the deferred messages of queue-heavy senders: 1000 senders x 999 messages in
+// eight 128-key buckets took 221 us per group-by in one workgroup per bucket).
+static int bkt_shift(uint32_t K, bool fine = false) {
   const int bits = bits_for(K);
-  return std::max(bits - kMaxDigitBits, std::min(7, bits));
+  return std::max(bits - kMaxDigitBits, fine ? 0 : std::min(7, bits));
 }
 
 static BktDiv bkt_div(uint32_t w) {
@@ -3531,8 +3578,8 @@ static hipError_t bkt_local(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
 // Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
 // d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
 static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t medium_above, uint32_t* off2,
-                               uint32_t** keys, uint32_t** vals) {
-  const int bs = bkt_shift(K);
+                               uint32_t** keys, uint32_t** vals, bool fine = false) {
+  const int bs = bkt_shift(K, fine);
   if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
   const uint32_t B = (K + (1u << bs) - 1) >> bs;
   const BktDiv bd = bkt_div(1u << bs);
@@ -3594,7 +3641,7 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
   uint32_t *keys, *vals;
-  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals));
+  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
   hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
@@ -3607,7 +3654,7 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     BktSrc hs = bkt_queue(d, Q_A);
     hs.keys = d.hkeys; hs.vals = d.hvals; hs.qc = nullptr; hs.mode = 3; hs.n_ptr = &d.sc->n_hrec; hs.cap = d.h_cap;
     uint32_t *hk, *hv;
-    TG_CHECK(group_by_bkt(d, hs, d.nloc, kNoMedium, nullptr, &hk, &hv));
+    TG_CHECK(group_by_bkt(d, hs, d.nloc, kNoMedium, nullptr, &hk, &hv, true));
     hoff = d.seg_off;
     hidx = hv;
   }

@@ -33,6 +33,8 @@ struct tgsim_ctx {
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
   std::vector<ShapeDev> shape_h;
   std::vector<TbShape> tbs_h;       // source of the last d.tbs upload (kept alive for the async copy)
+  std::vector<uint32_t> zd_h;       // source of the last d.zd upload
+  bool all_zd = false;              // every local sender is zero-delay and unshaped (Heavy::zd)
   std::vector<uint8_t> flags_h;
   std::vector<uint32_t> ip_h;
   uint64_t space = 0;               // addresses in the data subnet
@@ -443,6 +445,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.sc, 1);
   rc |= dalloc(c, &d.shape, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.tbs, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.zd, (size_t)c->nloc / 32 + 1);
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &c->d_red2, 2);
@@ -937,13 +940,18 @@ static int upload_tables(tgsim_ctx* c) {
     d.any_corr = false;
     c->any_dup = false;
     c->tbs_h.resize(c->nloc);
+    c->zd_h.assign((size_t)c->nloc / 32 + 1, 0u);
+    c->all_zd = true;
     for (uint32_t l = 0; l < c->nloc; ++l) {
       const ShapeDev& sh = c->shape_h[l];
       d.any_corr |= (sh.flags & kShCorr) != 0;
       c->any_dup |= sh.dup_t != 0;
       c->tbs_h[l] = TbShape{sh.tau, sh.mult, sh.shift};
+      if (sh.mu == 0 && sh.sigma == 0 && !(sh.flags & kShLimited)) c->zd_h[l >> 5] |= 1u << (l & 31u);
+      else c->all_zd = false;
     }
     HIPCK(c, hipMemcpyAsync(d.tbs, c->tbs_h.data(), c->nloc * sizeof(TbShape), hipMemcpyHostToDevice, d.stream), "upload shapes");
+    HIPCK(c, hipMemcpyAsync(d.zd, c->zd_h.data(), c->zd_h.size() * 4, hipMemcpyHostToDevice, d.stream), "upload shapes");
     copied = true;
   }
   if (!c->corr_reset.empty()) {
@@ -1127,16 +1135,19 @@ static int plan_queue_limit(tgsim_ctx* c) {
   const uint64_t mult = c->any_dup ? 2 : 1;
   const uint64_t m_uniform = std::min<uint64_t>((uint64_t)c->win_m_host + c->win_m_extra, 0x7FFFFFFFull);
   const uint64_t m_max = m_uniform + (uint64_t)c->win_m_inbox * std::max<uint64_t>(c->fl_npubs, c->win_inbox_max);
-  bool gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+  // zero-delay unshaped senders only: the window's own copies never count, and none of them stays
+  // queued past its enqueue instant, so the bound does not grow either (Heavy::zd)
+  const bool zd_only = c->all_zd && !c->tcp_on;
+  bool gate = zd_only ? c->pend_bound >= TGSIM_NETEM_LIMIT : c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   // inconclusive: refresh the bound with the exact maximum (one sync) - unless the window's own
   // staging bound already reaches the limit, when no refresh can close the gate
-  if (gate && !c->pend_exact && mult * m_max <= TGSIM_NETEM_LIMIT) {
+  if (gate && !c->pend_exact && (zd_only || mult * m_max <= TGSIM_NETEM_LIMIT)) {
     HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks ? tcp_inbox_mult(c) : 0u,
                              (uint32_t)mult), "pend max");
     HIPCK(c, sync_scalars(d), "sync");
     c->pend_bound = d.h_sc->pend_max;
     c->pend_exact = true;
-    gate = c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
+    gate = zd_only ? c->pend_bound >= TGSIM_NETEM_LIMIT : c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   }
   d.heavy = Heavy{};
   if (gate) {
@@ -1147,6 +1158,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
       d.h_cap = (uint32_t)cap;
     }
     d.heavy.pend = d.pend;
+    d.heavy.zd = d.zd;
     d.heavy.inbox = c->win_m_inbox ? d.inbox : nullptr;
     d.heavy.retx = c->tcp_on ? c->td.pend_by : nullptr;  // single shard: local = global ids
     d.heavy.m_uniform = (uint32_t)m_uniform;
@@ -1157,8 +1169,10 @@ static int plan_queue_limit(tgsim_ctx* c) {
     }
     d.heavy.mult = (uint32_t)mult;
   }
-  c->pend_bound = std::min<uint64_t>(c->pend_bound + mult * m_max, 1ull << 62);
-  c->pend_exact = m_max == 0;
+  if (!zd_only) {
+    c->pend_bound = std::min<uint64_t>(c->pend_bound + mult * m_max, 1ull << 62);
+    c->pend_exact = m_max == 0;
+  }
   for (uint32_t l : c->hcnt_touched) c->hcnt[l] = 0;
   c->hcnt_touched.clear();
   c->win_m_host = 0;
