@@ -364,6 +364,7 @@ struct ShapeArgs {
   unsigned long long* stats;  // [kNSub][16] sharded counters
   uint32_t* corr_idx;         // deferred messages of correlated / queue-heavy senders (count sc->n_corr)
   Heavy heavy;                // the window's queue-limit test
+  uint32_t may_defer;         // some shape is correlated or the queue-limit test is on
 };
 
 // Longest-prefix match over the sender's routing table: rule groups by prefix
@@ -487,16 +488,24 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   // record and one for the table gathers instead of a branch-serialised chain. The next message's
   // SoA record is loaded beside this one's gathers (software pipelining across the grid stride), so
   // an iteration pays one load round trip, not two.
+  // Deferred messages (correlated / queue-heavy senders) are listed with one reservation per block
+  // and round: an all-to-all round defers every message, and a reservation per wave serialised ~16k
+  // atomics on sc->n_corr (~160 us). The loop is block-uniform for it; lanes past n idle.
+  __shared__ uint32_t s_cred[kBlock / 64];
+  __shared__ uint32_t s_cbase;
   uint32_t i = bid * blockDim.x + threadIdx.x;
   uint32_t n_src = 0, n_dst = 0, n_seq = 0, n_size = 0;
   int64_t n_ts = 0;
   if (i < n) { n_src = a.src[i]; n_dst = a.dst[i]; n_seq = a.seq[i]; n_size = a.size[i]; n_ts = a.t[i]; }
-  for (; i < n; i += stride, ++it) {
+  for (uint32_t b0 = bid * blockDim.x; b0 < n; b0 += stride, ++it) {  // block-uniform
+    i = b0 + threadIdx.x;
+    const bool act = i < n;
     const uint32_t src = n_src, dst = n_dst, seq = n_seq, size = n_size;
     const int64_t ts = n_ts;
     asm volatile("" ::"v"(src), "v"(dst), "v"(seq), "v"(size), "v"((uint32_t)ts), "v"((uint32_t)((uint64_t)ts >> 32)));  // stage 1: SoA record
     {
-      const uint32_t i2 = i + stride < n ? i + stride : i;  // clamped: the last iteration reloads itself
+      // clamped: the last iteration reloads itself, an idle lane message 0 (n >= 1 here)
+      const uint32_t i2 = act ? (i + stride < n ? i + stride : i) : 0u;
       n_src = a.src[i2]; n_dst = a.dst[i2]; n_seq = a.seq[i2]; n_size = a.size[i2]; n_ts = a.t[i2];
     }
     const uint32_t sl = src - a.lo;
@@ -515,10 +524,12 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
                  "v"(sh.corrupt_t), "v"(sh.reorder_t), "v"(sh.mult), "v"(sh.flags));  // stage 2: gathers
     tgsim_record r1, r2;
     int q1 = -1, q2 = -1;
-    uint8_t st;
+    uint8_t st = 0;
     bool deferred = false;
-    cnt[ST_MSGS]++;
-    if (!src_ok || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
+    cnt[ST_MSGS] += act ? 1u : 0u;
+    if (!act) {
+      // past the staged count: nothing to decide, nothing to append
+    } else if (!src_ok || (dst >= a.geo.N && dst != TGSIM_DST_EXTERNAL) || size >= 0x80000000u) {
       atomicOr(&sc->err, ERR_BAD_MSG);
       st = TGSIM_ST_UNREACHABLE;
       cnt[ST_UNREACH]++;
@@ -573,9 +584,17 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
         }
       }
     }
-    if (!deferred) a.status[i] = st;
-    const uint32_t cpos = wave_append(deferred ? &sc->n_corr : nullptr);
-    if (deferred) a.corr_idx[cpos] = i;
+    if (act && !deferred) a.status[i] = st;
+    if (a.may_defer) {  // launch-uniform
+      uint32_t tot;
+      const uint32_t pos = block_excl_scan(deferred ? 1u : 0u, s_cred, tot);
+      if (tot) {  // block-uniform
+        if (threadIdx.x == 0) s_cbase = atomicAdd(&sc->n_corr, tot);
+        __syncthreads();
+        if (deferred) a.corr_idx[s_cbase + pos] = i;
+        __syncthreads();  // s_cbase is rewritten by the next round
+      }
+    }
     const int qs[2] = {q1, q2};
     const tgsim_record rs[2] = {r1, r2};
     a.Q.push_batch<2>(qs, rs, it);
@@ -2333,6 +2352,19 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+#ifdef TGSIM_PHASE_PROF
+// debug builds: per sender (first 1024 blocks' last sender) the cycles of k_shape_seq's phases:
+// [0] K setup, [1] chunk loads + Philox, [2] decisions, [3] queue after the chunk, [4] appends, [5] chunks
+__device__ uint64_t g_seq_ph[1024][8];
+#define SQ_T0() uint64_t sq_t = clock64(); uint64_t sq_acc[6] = {0, 0, 0, 0, 0, 0}
+#define SQ_PH(k) do { const uint64_t n_ = clock64(); sq_acc[k] += n_ - sq_t; sq_t = n_; } while (0)
+#define SQ_END() do { if (lane == 0 && blockIdx.x < 1024) for (int k_ = 0; k_ < 6; ++k_) g_seq_ph[blockIdx.x][k_] = sq_acc[k_]; } while (0)
+#else
+#define SQ_T0() do {} while (0)
+#define SQ_PH(k) do {} while (0)
+#define SQ_END() do {} while (0)
+#endif
+
 __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint32_t* sorted, const uint32_t* moff,
                                                          const uint32_t* hoff, const uint32_t* hidx,
                                                          const tgsim_record* H, const uint32_t* rho4,
@@ -2356,6 +2388,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
     }
     int64_t X = Xs[l];
     uint64_t far = 0;  // queued copies not leaving in this window
+    SQ_T0();
     if (lane == 0) { m.nu = 0; m.nk = 0; }
     __syncthreads();
     // the parallel form: heavy, no HTB, no correlation, and every due record's departure known
@@ -2442,6 +2475,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
     }
     const bool need_w0 = sh.dup_t || sh.loss_t || sh.reorder_t || sh.sigma;
     uint32_t n_lost = 0, n_copies = 0, n_over = 0;
+    SQ_PH(0);
     for (uint32_t c0 = j0; c0 < j1; c0 += kSeqChunk) {
       const uint32_t cn = min((uint32_t)kSeqChunk, j1 - c0);
       // parallel: the chunk's messages and their Philox words
@@ -2461,6 +2495,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
         }
       }
       __syncthreads();
+      SQ_PH(1);
       if (fast) {
         // every lane: its message's copies (clone first) with their netem times, as k_shape_seq's walk
         uint8_t st = 0, adm = 0, valid = 0;
@@ -2511,26 +2546,113 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
         bool over = false;
         for (int c = 1; c >= 0; --c)
           if (valid & (1u << c)) over |= base + (int64_t)(2 * lane + (c ? 0u : 1u)) >= (int64_t)TGSIM_NETEM_LIMIT;
+        // Closed form when every copy of the chunk outlives the chunk's last enqueue (an all-to-all
+        // round: 50 ms of latency against a 1 ms send spread): then every earlier admitted copy is
+        // still queued at each enqueue, so copy k (k-th valid copy in enqueue order) is admitted iff
+        // A_k < lim_k = limit - base_k, A_k = copies admitted before it. base_k never grows along the
+        // chunk (its enqueue times do not decrease), so with L_k = max(lim_k, 0) the recurrence is
+        // A_{k+1} = min(A_k + 1, L_k), i.e. A_{k+1} = (k + 1) + min(0, min_{i <= k} (L_i - i - 1)):
+        // a prefix minimum over the wave instead of a step per copy.
+        int64_t emin = INT64_MAX, tmax = INT64_MIN;
+        if (valid & 2u) emin = e2[1] < emin ? e2[1] : emin;
+        if (valid & 1u) emin = e2[0] < emin ? e2[0] : emin;
+        if (valid) tmax = ts;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const int64_t a = __shfl_xor(emin, o), b = __shfl_xor(tmax, o);
+          emin = a < emin ? a : emin;
+          tmax = b > tmax ? b : tmax;
+        }
+        const bool closed = emin > tmax;  // wave-uniform
         if (__ballot(over) == 0) {
           adm = valid;
-        } else {  // decide copy by copy, in enqueue order, counting the earlier admitted ones
-          // the owner's fields come through readlane (q is wave-uniform): scalar registers, no LDS
-          // round trip per copy as a shuffle would take
-          const uint32_t ts_lo = (uint32_t)(uint64_t)ts, ts_hi = (uint32_t)((uint64_t)ts >> 32);
-          const uint32_t b_lo = (uint32_t)(uint64_t)base, b_hi = (uint32_t)((uint64_t)base >> 32);
-          for (uint32_t q = 0; q < 2 * cn; ++q) {
-            const int owner = (int)(q >> 1), c = (q & 1u) ? 0 : 1;
-            const int64_t tq = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ts_hi, owner) << 32) |
-                                         (uint32_t)__builtin_amdgcn_readlane((int)ts_lo, owner));
-            const int64_t bq = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)b_hi, owner) << 32) |
-                                         (uint32_t)__builtin_amdgcn_readlane((int)b_lo, owner));
-            const uint32_t vq = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)valid, owner);
-            const uint64_t b1 = __ballot((adm & 2u) && 2 * lane < q && e2[1] > tq);
-            const uint64_t b0 = __ballot((adm & 1u) && 2 * lane + 1 < q && e2[0] > tq);
-            const bool in = ((vq >> c) & 1u) && bq + (int64_t)(__popcll(b1) + __popcll(b0)) < (int64_t)TGSIM_NETEM_LIMIT;
-            if ((int)lane == owner && in) adm |= (uint8_t)(1u << c);
+        } else if (closed) {
+          const uint32_t nv = (uint32_t)__popc((uint32_t)valid);
+          uint32_t k0 = nv;  // exclusive prefix of valid copies over the lanes
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(k0, o);
+            if ((int)lane >= o) k0 += y;
           }
+          k0 -= nv;
+          const int64_t lim = (int64_t)TGSIM_NETEM_LIMIT - base;
+          const int64_t Lp = lim > 0 ? lim : 0;
+          // this lane's copies in enqueue order: clone (if valid), then the original
+          const int64_t x0 = Lp - (int64_t)k0 - 1, x1 = Lp - (int64_t)k0 - 2;
+          int64_t lmin = nv == 0 ? INT64_MAX : (nv == 1 ? x0 : (x0 < x1 ? x0 : x1));
+          int64_t incl = lmin;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(incl, o);
+            if ((int)lane >= o) incl = y < incl ? y : incl;
+          }
+          int64_t prev = __shfl_up(incl, 1);  // prefix minimum before this lane's first copy
+          if (lane == 0) prev = INT64_MAX;
+          adm = 0;
+          uint32_t k = k0;
+          for (int c = 1; c >= 0; --c) {  // clone first
+            if (!(valid & (1u << c))) continue;
+            const int64_t x = Lp - (int64_t)k - 1;
+            const int64_t cur = prev < x ? prev : x;
+            const int64_t before = (int64_t)k + (prev < 0 ? prev : 0);
+            const int64_t after = (int64_t)k + 1 + (cur < 0 ? cur : 0);
+            if (after == before + 1) adm |= (uint8_t)(1u << c);
+            prev = cur;
+            ++k;
+          }
+        } else {  // decide copy by copy, in enqueue order, counting the earlier admitted ones
+          // Copy q (= 2 * message + (original ? 1 : 0): clone first) is admitted iff it is valid and
+          // base_q + #{admitted p < q with e_p > t_q} < limit. Every lane first builds, for its
+          // message's enqueue time, the 128-bit set G of the chunk's copies with e > t (one pass over
+          // the candidates in LDS); the walk is then scalar: the admitted set A in two 64-bit words,
+          // per copy one AND + popcount against the owner's G (readlane) and its limit. Ballots over
+          // the admitted bits cost ~230 cycles per copy (VALU -> SALU -> VALU per step).
+          int64_t* ce = m.cb;  // candidates in enqueue order (the kept copies reuse it afterwards)
+          ce[2 * lane] = (valid & 2u) ? e2[1] : INT64_MIN;
+          ce[2 * lane + 1] = (valid & 1u) ? e2[0] : INT64_MIN;
+          __syncthreads();
+          uint64_t g0 = 0, g1 = 0;
+#pragma unroll 8
+          for (uint32_t p = 0; p < 64; ++p) {
+            g0 |= (uint64_t)(ce[p] > ts ? 1u : 0u) << p;
+            g1 |= (uint64_t)(ce[64 + p] > ts ? 1u : 0u) << p;
+          }
+          __syncthreads();  // ce is rewritten by the kept copies below
+          // admission limit of the lane's copies: count < limit - base (invalid: never)
+          const int64_t lim = (int64_t)TGSIM_NETEM_LIMIT - base;
+          const int32_t lim32 = lim < INT32_MIN ? INT32_MIN : (lim > INT32_MAX ? INT32_MAX : (int32_t)lim);
+          const int32_t lim1 = (valid & 2u) ? lim32 : INT32_MIN, lim0 = (valid & 1u) ? lim32 : INT32_MIN;
+          const uint32_t g0l = (uint32_t)g0, g0h = (uint32_t)(g0 >> 32), g1l = (uint32_t)g1, g1h = (uint32_t)(g1 >> 32);
+          uint64_t A0 = 0, A1 = 0;
+          // only lanes with a copy the limit can still admit take a step (an all-to-all sender's queue
+          // is full: ~20 % of its copies get in), in lane order, clone before original
+          uint64_t cand = __ballot(lim1 > 0 || lim0 > 0);
+          while (cand) {
+            const int owner = __ffsll((unsigned long long)cand) - 1;
+            cand &= cand - 1ull;
+            const uint64_t G0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g0h, owner) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)g0l, owner);
+            const uint64_t G1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g1h, owner) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)g1l, owner);
+            const int32_t l1 = __builtin_amdgcn_readlane(lim1, owner), l0 = __builtin_amdgcn_readlane(lim0, owner);
+#pragma unroll
+            for (uint32_t o = 0; o < 2; ++o) {
+              const uint32_t q = 2u * (uint32_t)owner + o;
+              const int32_t lq = o ? l0 : l1;
+              const uint64_t m0 = q < 64 ? ((1ull << q) - 1ull) : ~0ull;
+              const uint64_t m1 = q < 64 ? 0ull : ((1ull << (q - 64)) - 1ull);
+              const int32_t cnt = __popcll(A0 & G0 & m0) + __popcll(A1 & G1 & m1);
+              if (cnt < lq) {
+                if (q < 64) A0 |= 1ull << q; else A1 |= 1ull << (q - 64);
+              }
+            }
+          }
+          const uint32_t qc = 2 * lane, qo = 2 * lane + 1;  // this lane's clone / original
+          const uint64_t Ac = qc < 64 ? A0 >> qc : A1 >> (qc - 64);
+          const uint64_t Ao = qo < 64 ? A0 >> qo : A1 >> (qo - 64);
+          adm = (uint8_t)(((Ac & 1u) << 1) | (Ao & 1u));
         }
+        SQ_PH(2);
         if (lane < cn) {
           if (st != TGSIM_ST_LOST) {
             const uint8_t dropped = valid & ~adm;
@@ -2576,6 +2698,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
           ksz = na + nk;
         }
         __syncthreads();
+        SQ_PH(3);
       }
       // sequential: netem_enqueue per message in qdisc order
       if (!fast && lane == 0) {
@@ -2672,7 +2795,12 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
       // chunk k of sender l: sub-queue (l + k) % 64, so one sender's appends spread over all of them
       a.Q.push_batch<2>(qs, rs, l + (c0 - j0) / kSeqChunk, true);
       __syncthreads();
+      SQ_PH(4);
+#ifdef TGSIM_PHASE_PROF
+      sq_acc[5]++;
+#endif
     }
+    SQ_END();
     n_lost = wave_sum(n_lost);  // the walk counts in lane 0, the parallel form in every lane
     n_copies = wave_sum(n_copies);
     n_over = wave_sum(n_over);
@@ -3158,30 +3286,53 @@ __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, con
     uint64_t* dK2 = in_a ? K2b : K2a;
     uint32_t* dK3 = in_a ? K3b : K3a;
     const uint32_t base = L.start;
+    // Output tile [o0, o1) of the pair [As, Be): its A and B slices come from two merge-path
+    // splits, are staged in LDS with coalesced loads, and merged there - each thread its IT outputs
+    // after a merge-path search in LDS (the per-thread searches and merges over global memory were
+    // chains of dependent loads: a 10k-delivery inbox took ~300 us in one block).
+    __shared__ uint32_t spl[2];
     for (uint32_t o0 = 0; o0 < L.len; o0 += kChunk) {
       const uint32_t o1 = min(o0 + (uint32_t)kChunk, L.len);
       const uint32_t As = (o0 / (2 * W)) * 2 * W;
       const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
       const uint32_t nA = Ae - As, nB = Be - Ae;
-      const uint32_t dend = o1 - As;
-      const uint32_t d0 = o0 - As + threadIdx.x * IT;
-      if (d0 >= dend) continue;
       const uint32_t a0 = base + As, b0 = base + Ae;
-      uint32_t lo = d0 > nB ? d0 - nB : 0u, hi = min(d0, nA);
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (!kless(sK1, sK2, sK3, b0 + (d0 - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
+      if (threadIdx.x < 2) {
+        const uint32_t d = (threadIdx.x ? o1 : o0) - As;
+        uint32_t lo = d > nB ? d - nB : 0u, hi = min(d, nA);
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (!kless(sK1, sK2, sK3, b0 + (d - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
+        }
+        spl[threadIdx.x] = lo;
       }
-      uint32_t ia = lo, ib = d0 - lo;
-      for (uint32_t k = 0; k < IT && d0 + k < dend; ++k) {
-        bool takeA;
-        if (ib >= nB) takeA = true;
-        else if (ia >= nA) takeA = false;
-        else takeA = !kless(sK1, sK2, sK3, b0 + ib, a0 + ia);
-        const uint32_t src = takeA ? a0 + ia++ : b0 + ib++;
-        const uint32_t dst = base + As + d0 + k;
-        dK1[dst] = sK1[src]; dK2[dst] = sK2[src]; dK3[dst] = sK3[src];
+      __syncthreads();
+      const uint32_t ia0 = spl[0], ib0 = (o0 - As) - ia0;
+      const uint32_t na = spl[1] - ia0, nt = o1 - o0, nb = nt - na;
+      for (uint32_t j = threadIdx.x; j < nt; j += kBlock) {
+        const uint32_t src = j < na ? a0 + ia0 + j : b0 + ib0 + (j - na);
+        s.k1[j] = sK1[src]; s.k2[j] = sK2[src]; s.k3[j] = sK3[src];
       }
+      __syncthreads();
+      const uint32_t d0 = threadIdx.x * IT;
+      if (d0 < nt) {
+        uint32_t lo = d0 > nb ? d0 - nb : 0u, hi = min(d0, na);
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (!kless(s.k1, s.k2, s.k3, na + (d0 - 1 - mid), mid)) lo = mid + 1; else hi = mid;
+        }
+        uint32_t ia = lo, ib = d0 - lo;
+        for (uint32_t k = 0; k < IT && d0 + k < nt; ++k) {
+          bool takeA;
+          if (ib >= nb) takeA = true;
+          else if (ia >= na) takeA = false;
+          else takeA = !kless(s.k1, s.k2, s.k3, na + ib, ia);
+          const uint32_t src = takeA ? ia++ : na + ib++;
+          const uint32_t dst = base + o0 + d0 + k;
+          dK1[dst] = s.k1[src]; dK2[dst] = s.k2[src]; dK3[dst] = s.k3[src];
+        }
+      }
+      __syncthreads();  // the staged slices and spl are rewritten by the next tile
     }
     __syncthreads();
     in_a = !in_a;
@@ -3709,6 +3860,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
     a.heavy = d.heavy;
+    a.may_defer = (d.any_corr || d.heavy.pend) ? 1u : 0u;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
     constexpr uint32_t ne = kStreamBlocks;  // 512 / 1024 / 4096 measured the same
     static_assert(ne % 8 == 0, "extract blocks keep their XCD");
@@ -3914,5 +4066,9 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 // debug builds only: the phase clocks of the last k_tb_bucket / k_emit_bucket launches
 extern "C" int tgsim_debug_phases(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_tg_ph), sizeof(tgsim::g_tg_ph));
+}
+// ... and of the last k_shape_seq launch (per block: its last sender)
+extern "C" int tgsim_debug_seq_phases(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_seq_ph), sizeof(tgsim::g_seq_ph));
 }
 #endif
