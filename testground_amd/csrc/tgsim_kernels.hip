@@ -1379,6 +1379,98 @@ __device__ __forceinline__ void pad_key(SortSmem& s, uint32_t j) {
   s.sg[j] = 0xFFFFFFFFu; s.k1[j] = ~0ull; s.k2[j] = ~0ull; s.k3[j] = 0xFFFFFFFFu;
 }
 
+// Sort the m loaded elements of s (whole segments, contiguous in sg order) into perm[] (sorted
+// position -> element), the arrays staying in place; npad = next_pow2(m). Returns false, touching
+// nothing, when k1 spreads too far over the elements to pack.
+__device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
+    // k1's spread over the span: below 2^52 the sort runs on (segment rank << 53 | k1 - min,
+    // element) pairs - one u64 compare per step, two arrays swapped instead of four; equal packed
+    // keys (same segment and k1) are ordered by (k2, k3) through the elements. The packed keys
+    // live in k1's array (it has no spare LDS: every kernel that reaches rest_body allocates this
+    // struct) and k1 is restored by element afterwards.
+    uint64_t mn = ~0ull, mx = 0;
+    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
+      mn = s.k1[j] < mn ? s.k1[j] : mn;
+      mx = s.k1[j] > mx ? s.k1[j] : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) { s.scA[threadIdx.x >> 6] = (int64_t)mn; s.scB[threadIdx.x >> 6] = (int64_t)mx; }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      const uint64_t a = (uint64_t)s.scA[w], b = (uint64_t)s.scB[w];
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    __syncthreads();  // scA / scB are free again
+    if (!(mx - mn < (1ull << 52))) return false;
+    {
+      uint64_t* kw = s.k1;
+      // segment rank of each position: segment starts up to it, minus one (m <= kSpan = 2^11)
+      constexpr uint32_t PER = kSpan / kBlock;
+      const uint32_t p0 = threadIdx.x * PER;
+      uint32_t c = 0;
+      for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t j = p0 + u;
+        c += (j < m && j > 0 && s.sg[j] != s.sg[j - 1]) ? 1u : 0u;
+      }
+      uint32_t tot;
+      uint32_t r = block_excl_scan(c, s.perm, tot);  // perm is scratch until it is filled below
+      uint64_t nk[PER];
+      for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t j = p0 + u;
+        nk[u] = ~0ull;  // padding: above every real key (rank <= 2^11 - 1, spread < 2^52)
+        if (j < m) {
+          r += (j > 0 && s.sg[j] != s.sg[j - 1]) ? 1u : 0u;
+          nk[u] = ((uint64_t)r << 53) | (s.k1[j] - mn);
+        }
+      }
+      __syncthreads();  // every k1 read before the packed keys replace them
+      for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t j = p0 + u;
+        if (j < npad) { kw[j] = nk[u]; s.perm[j] = j < m ? j : 0xFFFFFFFFu; }
+      }
+      __syncthreads();
+      for (uint32_t k = 2; k <= npad; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+          for (uint32_t q = threadIdx.x; q < (npad >> 1); q += kBlock) {
+            const uint32_t i = ((q & ~(jj - 1)) << 1) | (q & (jj - 1));
+            const uint32_t l = i + jj;
+            const bool up = (i & k) == 0;
+            const uint64_t ki = kw[i], kl = kw[l];
+            const uint32_t ei = s.perm[i], el = s.perm[l];
+            bool lt;  // element at l sorts before the one at i
+            if (kl != ki) lt = kl < ki;
+            else if (el == 0xFFFFFFFFu || ei == 0xFFFFFFFFu) lt = el < ei;  // padding (never ties a real key)
+            else lt = s.k2[el] != s.k2[ei] ? s.k2[el] < s.k2[ei] : s.k3[el] < s.k3[ei];
+            if (lt == up) {
+              kw[i] = kl; kw[l] = ki;
+              s.perm[i] = el; s.perm[l] = ei;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // restore k1 by element: sorted position i holds element perm[i]'s key
+      uint32_t ee[PER];
+      for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t i = p0 + u;
+        ee[u] = 0xFFFFFFFFu;
+        if (i < m) { ee[u] = s.perm[i]; nk[u] = (kw[i] & ((1ull << 53) - 1)) + mn; }
+      }
+      __syncthreads();
+      for (uint32_t u = 0; u < PER; ++u)
+        if (ee[u] != 0xFFFFFFFFu) s.k1[ee[u]] = nk[u];
+    }
+    __syncthreads();
+    return true;
+}
+
 // Sort m loaded elements (whole segments, contiguous) and leave perm[] = sorted order.
 // off/s_begin give each element's segment bounds (global positions).
 __device__ __forceinline__ void span_sort(SortSmem& s, uint32_t m, const uint32_t* off, uint32_t s_begin) {
@@ -1404,10 +1496,12 @@ __device__ __forceinline__ void span_sort(SortSmem& s, uint32_t m, const uint32_
     }
   } else {
     const uint32_t npad = next_pow2(m);
-    for (uint32_t j = m + threadIdx.x; j < npad; j += kBlock) pad_key(s, j);
-    __syncthreads();
-    bitonic_lds(s, npad);
-    for (uint32_t j = threadIdx.x; j < m; j += kBlock) s.perm[j] = j;
+    if (!packed_bitonic(s, m, npad)) {
+      for (uint32_t j = m + threadIdx.x; j < npad; j += kBlock) pad_key(s, j);
+      __syncthreads();
+      bitonic_lds(s, npad);
+      for (uint32_t j = threadIdx.x; j < m; j += kBlock) s.perm[j] = j;
+    }
   }
   __syncthreads();
 }
@@ -3272,8 +3366,15 @@ __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, con
       else pad_key(s, j);
     }
     __syncthreads();
-    bitonic_lds(s, npad);
-    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
+    if (packed_bitonic(s, cnt, npad)) {  // sorted through perm, the arrays in place
+      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
+        const uint32_t e = s.perm[j];
+        K1a[st + j] = s.k1[e]; K2a[st + j] = s.k2[e]; K3a[st + j] = s.k3[e];
+      }
+    } else {
+      bitonic_lds(s, npad);
+      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
+    }
     __syncthreads();
   }
   bool in_a = true;
@@ -3289,15 +3390,50 @@ __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, con
     // Output tile [o0, o1) of the pair [As, Be): its A and B slices come from two merge-path
     // splits, are staged in LDS with coalesced loads, and merged there - each thread its IT outputs
     // after a merge-path search in LDS (the per-thread searches and merges over global memory were
-    // chains of dependent loads: a 10k-delivery inbox took ~300 us in one block).
+    // chains of dependent loads). The splits of every tile boundary of the pass are searched at
+    // once, one thread each (tile t starts at t * kChunk; a tile never spans two pairs), so a pass
+    // pays one search latency, not one per tile: a 10k-delivery inbox took ~300 us in one block.
+    // Boundaries beyond sg's capacity are searched per tile.
     __shared__ uint32_t spl[2];
+    const uint32_t ntiles = (L.len + kChunk - 1) / kChunk;
+    const bool pre = ntiles < (uint32_t)kSpan;  // block-uniform
+    if (pre) {
+      for (uint32_t t = threadIdx.x; t <= ntiles; t += kBlock) {
+        // boundary o = t * kChunk (the segment end for t = ntiles), as the end of tile t - 1 (the
+        // pair of tile t - 1) -> sg[t]; as the start of tile t -> perm[t]
+        const uint32_t o = min(t * (uint32_t)kChunk, L.len);
+        for (int side = 0; side < 2; ++side) {
+          if (side == 0 && t == 0) continue;
+          if (side == 1 && t == ntiles) continue;
+          const uint32_t ot = side ? o : o - 1;  // an output inside the tile whose pair is wanted
+          const uint32_t As = (ot / (2 * W)) * 2 * W;
+          const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
+          const uint32_t nA = Ae - As, nB = Be - Ae;
+          const uint32_t a0 = base + As, b0 = base + Ae;
+          const uint32_t d = o - As;
+          uint32_t lo = d > nB ? d - nB : 0u, hi = min(d, nA);
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (!kless(sK1, sK2, sK3, b0 + (d - 1 - mid), a0 + mid)) lo = mid + 1; else hi = mid;
+          }
+          (side ? s.perm : s.sg)[t] = lo;
+        }
+      }
+      __syncthreads();
+    }
     for (uint32_t o0 = 0; o0 < L.len; o0 += kChunk) {
       const uint32_t o1 = min(o0 + (uint32_t)kChunk, L.len);
       const uint32_t As = (o0 / (2 * W)) * 2 * W;
       const uint32_t Ae = min(As + W, L.len), Be = min(As + 2 * W, L.len);
       const uint32_t nA = Ae - As, nB = Be - Ae;
       const uint32_t a0 = base + As, b0 = base + Ae;
-      if (threadIdx.x < 2) {
+      if (pre) {
+        if (threadIdx.x == 0) {
+          const uint32_t t = o0 / kChunk;
+          spl[0] = s.perm[t];
+          spl[1] = s.sg[t + 1];
+        }
+      } else if (threadIdx.x < 2) {
         const uint32_t d = (threadIdx.x ? o1 : o0) - As;
         uint32_t lo = d > nB ? d - nB : 0u, hi = min(d, nA);
         while (lo < hi) {
