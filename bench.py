@@ -550,7 +550,8 @@ def flood_config(args, shard=0, n_shards=1, device=0):
 
 
 def flood_max_pubs(args) -> int:
-    return ((args.warmup + args.steps + 20) // args.pub_every + 2) * args.pubs_per_wave
+    # every window of the run publishes on schedule: warm-up, the kernel probe and the timed steps
+    return ((args.warmup + probe_steps(args) + args.steps + 20) // args.pub_every + 2) * args.pubs_per_wave
 
 
 def main_flood(args):

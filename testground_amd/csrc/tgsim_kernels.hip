@@ -42,6 +42,28 @@ static void prof_resolve(Dev& d) {
 // small device helpers
 // ============================================================================================
 
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
+// Stores of the records and arrays one launch writes and the next reads. TG_NT_STORES (experiment
+// builds) makes them non-temporal, so fewer dirty L2 lines are left for the write-back at the
+// launch boundary (MI355X_MICROARCH.md: + B / 6 TB/s behind a predecessor that leaves B dirty).
+__device__ __forceinline__ void st4(void* p, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  const v4u32 v = {x, y, z, w};
+#ifdef TG_NT_STORES
+  __builtin_nontemporal_store(v, reinterpret_cast<v4u32*>(p));
+#else
+  *reinterpret_cast<v4u32*>(p) = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void stn(T* p, T v) {
+#ifdef TG_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ void load_rec(const tgsim_record* p, tgsim_record& r) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   const uint4 a = q[0], b = q[1];
@@ -50,8 +72,8 @@ __device__ __forceinline__ void load_rec(const tgsim_record* p, tgsim_record& r)
 }
 __device__ __forceinline__ void store_rec(tgsim_record* p, const tgsim_record& r) {
   uint4* q = reinterpret_cast<uint4*>(p);
-  q[0] = make_uint4((uint32_t)(uint64_t)r.t, (uint32_t)((uint64_t)r.t >> 32), r.src, r.dst);
-  q[1] = make_uint4(r.seq, r.size, r.meta, r.corrupt_off);
+  st4(q, (uint32_t)(uint64_t)r.t, (uint32_t)((uint64_t)r.t >> 32), r.src, r.dst);
+  st4(q + 1, r.seq, r.size, r.meta, r.corrupt_off);
 }
 
 // Wave64 compaction onto per-lane counters: lanes whose counter pointer is equal share one
@@ -200,7 +222,7 @@ struct Queues {
         if (pos < subcap) {
           const size_t at = (size_t)sub * subcap + pos;
           store_rec((k == Q_A ? A : (k == Q_D ? D : L)) + at, r[u]);
-          (k == Q_A ? K[0] : (k == Q_D ? K[1] : K[2]))[at] = key_of(k, r[u]);
+          stn((k == Q_A ? K[0] : (k == Q_D ? K[1] : K[2])) + at, key_of(k, r[u]));
         } else {
           atomicOr(&sc->err, k == Q_A ? ERR_CAP_A : (k == Q_D ? ERR_CAP_D : ERR_CAP_L));
         }
@@ -1225,7 +1247,6 @@ __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const 
 #define TG_WHEEL_UNROLL 8
 #endif
 constexpr int kWheelUnroll = TG_WHEEL_UNROLL;
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // Queue occupancy: a record entering the wheel for the first time (no
 // TGSIM_F_WHEEL) is counted in its sender's pend and marked; runs of one sender among a wave's 64
@@ -1325,10 +1346,10 @@ __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars
       if (k[u] != 0xFFFFFFFFu) {
         const uint32_t pos = atomicAdd(&base[k[u]], 1u);
         v4u32* q = reinterpret_cast<v4u32*>(arena + off + pos);
-        q[0] = ra[u];
         v4u32 b = rb[u];
         b.z |= TGSIM_F_WHEEL;
-        q[1] = b;
+        st4(q, ra[u].x, ra[u].y, ra[u].z, ra[u].w);
+        st4(q + 1, b.x, b.y, b.z, b.w);
       }
     }
   }
@@ -2148,11 +2169,11 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
       if (pos < Q.subcap) {
         const size_t at = (size_t)sub * Q.subcap + pos;
         uint4* dst = reinterpret_cast<uint4*>((isD ? Q.D : Q.L) + at);
-        dst[0] = a;
-        dst[1] = b;
+        st4(dst, a.x, a.y, a.z, a.w);
+        st4(dst + 1, b.x, b.y, b.z, b.w);
         tgsim_record r;
         r.t = (int64_t)(((uint64_t)a.y << 32) | a.x); r.src = a.z; r.dst = a.w;
-        Q.K[isD ? Q_D : Q_L][at] = Q.key_of(isD ? Q_D : Q_L, r);
+        stn(Q.K[isD ? Q_D : Q_L] + at, Q.key_of(isD ? Q_D : Q_L, r));
       } else {
         atomicOr(&Q.sc->err, isD ? ERR_CAP_D : ERR_CAP_L);
       }
@@ -2225,8 +2246,9 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
     const uint32_t n = min(kStageN, h.nb - r0);
     for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
       const uint32_t o = h.start + r0 + i;
-      p.o_t[o] = st_t[i]; p.o_src[o] = st_u[i]; p.o_dst[o] = st_u[kStageN + i]; p.o_seq[o] = st_u[2 * kStageN + i];
-      p.o_size[o] = st_u[3 * kStageN + i]; p.o_flags[o] = st_u[4 * kStageN + i]; p.o_coff[o] = st_u[5 * kStageN + i];
+      stn(p.o_t + o, st_t[i]); stn(p.o_src + o, st_u[i]); stn(p.o_dst + o, st_u[kStageN + i]);
+      stn(p.o_seq + o, st_u[2 * kStageN + i]); stn(p.o_size + o, st_u[3 * kStageN + i]);
+      stn(p.o_flags + o, st_u[4 * kStageN + i]); stn(p.o_coff + o, st_u[5 * kStageN + i]);
     }
     __syncthreads();
   }
@@ -3670,7 +3692,8 @@ __device__ __forceinline__ void gen_storm_body(const StormArgs& a, const SigStat
     }
     if (msg) {
       const uint32_t i = a.base + l * F + k;
-      a.m_src[i] = g; a.m_dst[i] = p; a.m_seq[i] = a.round * F + k; a.m_size[i] = a.size; a.m_t[i] = t;
+      stn(a.m_src + i, g); stn(a.m_dst + i, p); stn(a.m_seq + i, a.round * F + k); stn(a.m_size + i, a.size);
+      stn(a.m_t + i, t);
     }
     // the instance's signal time: its latest send
     for (uint32_t o = Fp >> 1; o > 0; o >>= 1) {
