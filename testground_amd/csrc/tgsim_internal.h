@@ -33,11 +33,12 @@ constexpr uint32_t kStormSalt = 0x53544F52u;  // "STOR": storm generator draws
 enum : uint32_t {
   ERR_CAP_A = 1u << 0, ERR_CAP_D = 1u << 1, ERR_CAP_L = 1u << 2, ERR_CAP_X = 1u << 3,
   ERR_ARENA = 1u << 4, ERR_REGIONS = 1u << 5, ERR_CAUSAL = 1u << 6, ERR_SIG_ORDER = 1u << 7,
-  ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_CHUNKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
+  ERR_UNRELEASED = 1u << 8, ERR_SIG_CAP = 1u << 9, ERR_TASKS = 1u << 10, ERR_EXCH_HDR = 1u << 11,
   ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14,
   ERR_QUEUE_CAP = 1u << 15,  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
   ERR_CAP_M = 1u << 16,      // device-counted staging (flood forwards, appends after them) outgrew cap_msgs
   ERR_TCP_TIMERS = 1u << 17  // TCP acks mode: more live timer batches than the ring holds
+  // ERR_TASKS: a large-segment rank task waited past its bound for its chunks (k_rest; never expected)
 };
 
 // Per-sender egress state derived from network.LinkShape (48 B; gathered by src).

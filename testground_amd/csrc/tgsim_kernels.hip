@@ -3374,31 +3374,36 @@ __device__ void large_consume(const CorrPolicy& p, SortSmem&, const LargeSeg& L,
   for (uint32_t j = threadIdx.x; j < L.len; j += kBlock) p.sorted[L.start + j] = K3[L.start + j];
 }
 
+// Sort chunk [c0, c0 + kChunk) of a large segment in LDS into (K1a, K2a, K3a) at the same positions.
+template <class P>
+__device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uint32_t c0, const uint32_t* keys,
+                                 const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a) {
+  const uint32_t st = L.start + c0;
+  const uint32_t cnt = min((uint32_t)kChunk, L.len - c0);
+  const uint32_t npad = next_pow2(cnt);
+  for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
+    if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+    else pad_key(s, j);
+  }
+  __syncthreads();
+  if (packed_bitonic(s, cnt, npad)) {  // sorted through perm, the arrays in place
+    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
+      const uint32_t e = s.perm[j];
+      K1a[st + j] = s.k1[e]; K2a[st + j] = s.k2[e]; K3a[st + j] = s.k3[e];
+    }
+  } else {
+    bitonic_lds(s, npad);
+    for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
+  }
+  __syncthreads();
+}
+
 // Sort one large segment inside the calling block; returns the buffer set that holds the result.
 template <class P>
 __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, const uint32_t* keys,
                                  const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b,
                                  uint64_t* K2b, uint32_t* K3b) {
-  for (uint32_t c0 = 0; c0 < L.len; c0 += kChunk) {
-    const uint32_t st = L.start + c0;
-    const uint32_t cnt = min((uint32_t)kChunk, L.len - c0);
-    const uint32_t npad = next_pow2(cnt);
-    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
-      if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-      else pad_key(s, j);
-    }
-    __syncthreads();
-    if (packed_bitonic(s, cnt, npad)) {  // sorted through perm, the arrays in place
-      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
-        const uint32_t e = s.perm[j];
-        K1a[st + j] = s.k1[e]; K2a[st + j] = s.k2[e]; K3a[st + j] = s.k3[e];
-      }
-    } else {
-      bitonic_lds(s, npad);
-      for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
-    }
-    __syncthreads();
-  }
+  for (uint32_t c0 = 0; c0 < L.len; c0 += kChunk) large_chunk_sort(p, s, L, c0, keys, vals, K1a, K2a, K3a);
   bool in_a = true;
   constexpr uint32_t IT = kChunk / kBlock;
   for (uint32_t W = kChunk; W < L.len; W *= 2) {
@@ -3498,14 +3503,73 @@ __device__ bool large_sort_block(const P& p, SortSmem& s, const LargeSeg& L, con
   return in_a;
 }
 
+// Where a ranked element of a large segment goes (the tasks of rest_body): the deliveries, signal
+// sequence numbers and deferred-message order are written at their sorted position at once; the
+// token bucket's GCRA runs along the whole segment in order, so its elements are placed in
+// (K1b, K2b, K3b) and the segment's last rank task scans them (large_consume).
+__device__ __forceinline__ void large_place(const EmitPolicy& p, const LargeSeg& L, uint32_t r, uint64_t, uint64_t,
+                                            uint32_t k3, uint64_t*, uint64_t*, uint32_t*) {
+  p.write(L.start + r, k3);
+}
+__device__ __forceinline__ void large_place(const SigPolicy& p, const LargeSeg& L, uint32_t r, uint64_t k1, uint64_t,
+                                            uint32_t k3, uint64_t*, uint64_t*, uint32_t*) {
+  p.write(L.seg, L.start + r, L.start, k1, k3);
+}
+__device__ __forceinline__ void large_place(const CorrPolicy& p, const LargeSeg& L, uint32_t r, uint64_t, uint64_t,
+                                            uint32_t k3, uint64_t*, uint64_t*, uint32_t*) {
+  p.sorted[L.start + r] = k3;
+}
+__device__ __forceinline__ void large_place(const TBPolicy&, const LargeSeg& L, uint32_t r, uint64_t k1, uint64_t k2,
+                                            uint32_t k3, uint64_t* K1b, uint64_t* K2b, uint32_t* K3b) {
+  K1b[L.start + r] = k1; K2b[L.start + r] = k2; K3b[L.start + r] = k3;
+}
+template <class P> struct LargeScan { static constexpr bool v = false; };
+template <> struct LargeScan<TBPolicy> { static constexpr bool v = true; };
+
+// elements of the sorted chunk (K1, K2, K3)[b, b + n) below the key (k1, k2, k3): four chunks' binary
+// searches advance together, so their loads are in flight at once
+__device__ __forceinline__ void below4(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3, const uint32_t (&b)[4],
+                                       const uint32_t (&n)[4], uint64_t k1, uint64_t k2, uint32_t k3, uint32_t (&lo)[4]) {
+  uint32_t hi[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { lo[q] = 0; hi[q] = n[q]; }
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (lo[q] >= hi[q]) continue;
+      any = true;
+      const uint32_t mid = (lo[q] + hi[q]) >> 1, x = b[q] + mid;
+      const uint64_t y1 = K1[x];
+      const bool lt = y1 != k1 ? y1 < k1 : key_less(0, y1, K2[x], K3[x], 0, k1, k2, k3);
+      if (lt) lo[q] = mid + 1; else hi[q] = mid;
+    }
+    if (!any) break;
+  }
+}
+
+constexpr uint32_t kRankTile = kBlock;   // elements of a large segment ranked per task (one per thread)
+constexpr uint32_t kLargeTab = 256;      // large segments whose task table fits LDS (else one block each)
+
+// The rest of a group-by's segments. Medium segments: one block each. Large segments (len > kTile)
+// are sorted by many blocks at once through a task counter: first every kChunk chunk
+// of every large segment is sorted in LDS by its own task, then every element is ranked by its own
+// task thread - its place in its chunk plus, in every other sorted chunk, the number of elements below
+// it (binary searches) - and placed. A rank task waits until its segment's chunks are sorted
+// (LargeSeg::pad counts them); tasks are claimed in that order, so a waiting block only waits on
+// tasks that running blocks hold. One block sorting a 10k-delivery inbox through merge passes took
+// ~280 us; the tasks take the time of one chunk sort and one rank search.
 template <class P>
 __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
                                           const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
                                           uint64_t* K1a, uint64_t* K2a, uint32_t* K3a, uint64_t* K1b, uint64_t* K2b,
                                           uint32_t* K3b, uint32_t bid, uint32_t nblocks) {
   __shared__ SortSmem s;
+  __shared__ uint32_t s_c1[kLargeTab + 1], s_c2[kLargeTab + 1];
+  __shared__ uint32_t s_task, s_last;
   const uint32_t nm = sc->n_medium, nl = sc->n_large;
-  for (uint32_t w = bid; w < nm + nl; w += nblocks) {
+  const bool par = nl > 0 && nl <= kLargeTab && sc->max_large < (1u << 24);  // launch-uniform
+  for (uint32_t w = bid; w < nm + (par ? 0u : nl); w += nblocks) {
     if (w < nm) {
       const uint32_t g = medium[w];
       const uint32_t a = off[g], m = off[g + 1] - a;
@@ -3519,6 +3583,94 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
       large_consume(p, s, L, in_a ? K1a : K1b, in_a ? K3a : K3b, (w - nm) * 131u);
     }
     __syncthreads();
+  }
+  if (!par) return;
+  // task table: chunk tasks of segment i at [c1[i], c1[i + 1]), its rank tasks at T1 + [c2[i], c2[i + 1])
+  {
+    const uint32_t i = threadIdx.x;  // nl <= kLargeTab = kBlock
+    uint32_t a = 0, b = 0, ta, tb;
+    if (i < nl) {
+      const uint32_t len = large[i].len;
+      a = (len + kChunk - 1) / kChunk;
+      b = (len + kRankTile - 1) / kRankTile;
+    }
+    block_scan2(a, b, s.perm, ta, tb);
+    if (i < nl) { s_c1[i] = a; s_c2[i] = b; }
+    if (i == 0) { s_c1[nl] = ta; s_c2[nl] = tb; }
+    __syncthreads();
+  }
+  const uint32_t T1 = s_c1[nl], T = T1 + s_c2[nl];
+  LargeSeg* lg = const_cast<LargeSeg*>(large);
+  uint32_t* ctr = const_cast<uint32_t*>(&sc->n_chunks);  // the launch's task counter (zeroed with the lists)
+  for (;;) {
+    __syncthreads();  // the previous task is done with LDS and s_task
+    if (threadIdx.x == 0) s_task = atomicAdd(ctr, 1u);
+    __syncthreads();
+    // readfirstlane: the task is provably wave-uniform to the compiler, so every branch on it below
+    // (and the barriers inside) stays uniform control flow
+    const uint32_t task = __builtin_amdgcn_readfirstlane(s_task);
+    if (task >= T) break;
+    const bool chunk = task < T1;
+    const uint32_t* tab = chunk ? s_c1 : s_c2;
+    const uint32_t r = chunk ? task : task - T1;
+    uint32_t i = 0, hi = nl;  // the segment: last i with tab[i] <= r
+    while (hi - i > 1) {
+      const uint32_t mid = (i + hi) >> 1;
+      if (tab[mid] <= r) i = mid; else hi = mid;
+    }
+    const LargeSeg L = large[i];
+    const uint32_t nch = s_c1[i + 1] - s_c1[i], nrk = s_c2[i + 1] - s_c2[i];
+    if (chunk) {
+      large_chunk_sort(p, s, L, (r - s_c1[i]) * kChunk, keys, vals, K1a, K2a, K3a);
+      __threadfence();  // the sorted chunk is visible device-wide before it is counted
+      __syncthreads();
+      if (threadIdx.x == 0) atomicAdd(&lg[i].pad, 1u);
+      continue;
+    }
+    if (threadIdx.x == 0) {
+      // the count is read with an atomic read-modify-write: a plain (even atomic) load of coarse-
+      // grained memory can keep hitting this XCD's L2 copy of the line while another XCD counts
+      uint32_t spins = 0;
+      while ((__hip_atomic_fetch_add(&lg[i].pad, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & 0xFFFFu) < nch) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == (1u << 24)) {  // a bound, never expected: report instead of hanging the device
+          atomicOr(const_cast<uint32_t*>(&sc->err), ERR_TASKS);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __threadfence();
+    const uint32_t e = (r - s_c2[i]) * kRankTile + threadIdx.x;
+    if (e < L.len) {
+      const uint32_t x = L.start + e, c = e / kChunk;
+      const uint64_t k1 = K1a[x], k2 = K2a[x];
+      const uint32_t k3 = K3a[x];
+      uint32_t rank = e - c * kChunk;
+      for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+        uint32_t b[4], n[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t cc = c0 + q;
+          b[q] = L.start + cc * kChunk;
+          n[q] = (cc < nch && cc != c) ? min((uint32_t)kChunk, L.len - cc * kChunk) : 0u;
+        }
+        below4(K1a, K2a, K3a, b, n, k1, k2, k3, lo);
+        rank += lo[0] + lo[1] + lo[2] + lo[3];
+      }
+      large_place(p, L, rank, k1, k2, k3, K1b, K2b, K3b);
+    }
+    if (LargeScan<P>::v) {  // compile-time: the segment's last rank task runs the scan
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) s_last = (atomicAdd(&lg[i].pad, 1u << 16) >> 16) == nrk - 1;
+      __syncthreads();
+      if (__builtin_amdgcn_readfirstlane(s_last)) {
+        __threadfence();
+        large_consume(p, s, L, K1b, K3b, i * 131u);
+      }
+      __syncthreads();
+    }
   }
 }
 

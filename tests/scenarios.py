@@ -125,6 +125,37 @@ def run_heavy(binding, seed: int, n_inst: int = 64):
     return out
 
 
+def run_many_large(binding, seed: int, n_inst: int = 64, n: int = 40_000):
+    """Several long backlogs and large inboxes in the same window (k_rest's task-parallel path: every
+    chunk of every large segment sorted by its own task, every element ranked by its own thread):
+    four heavy senders (~8k copies each: four chunks) and two heavy receivers (~16k deliveries:
+    eight chunks, so the rank search covers more than one group of four chunks)."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed), binding=binding)
+    for g in range(n_inst):
+        sim.set_shape(g, make_shape(latency_ns=int(rng.choice([0, 2 * MS])), jitter_ns=int(rng.choice([0, 3 * MS])),
+                                    bandwidth_bps=int(rng.choice([0, 0, 0, 1_000_000_000])), duplicate=1.0))
+    out = []
+    t0 = 0
+    for w in range(3):
+        src = np.where(rng.random(n) < 0.8, rng.integers(0, 4, n), rng.integers(4, n_inst, n))
+        dst = np.where(rng.random(n) < 0.8, rng.integers(5, 7, n), rng.integers(0, n_inst, n))
+        dst[dst == src] = (dst[dst == src] + 9) % n_inst
+        seq = np.arange(n) + w * n
+        t = t0 + rng.integers(0, 20 * MS, n)
+        t[: n // 10] = t0 + 7 * MS  # ties on the primary key, broken by (src, seq, clone)
+        sim.enqueue(src, dst, seq, rng.choice([64, 1500], n), t)
+        t0 += 20 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    t0 += 200 * MS
+    sim.advance(t0)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
               window_ns: int = 4 * MS, restart=None):
     """Senders whose bursts overrun netem's 1000-packet queue under every kind of

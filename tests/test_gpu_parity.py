@@ -27,6 +27,13 @@ def test_large_segments(hip, oracle, n_inst):
     S.assert_same(S.run_heavy(hip, 7, n_inst), S.run_heavy(oracle, 7, n_inst))
 
 
+def test_many_large_segments(hip, oracle):
+    """k_rest's task-parallel sort of several large segments at once."""
+    a = S.run_many_large(hip, 11)
+    S.assert_same(a, S.run_many_large(oracle, 11))
+    assert max(np.diff(x["inbox"]).max() for x in a[:3]) > 8192
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_queue_limit_bursts(hip, oracle, seed):
     """netem's 1000-packet queue under every shape kind, across windows."""
