@@ -3377,9 +3377,10 @@ __device__ void large_consume(const CorrPolicy& p, SortSmem&, const LargeSeg& L,
 // Sort chunk [c0, c0 + kChunk) of a large segment in LDS into (K1a, K2a, K3a) at the same positions.
 template <class P>
 __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uint32_t c0, const uint32_t* keys,
-                                 const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a) {
+                                 const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a,
+                                 uint32_t chunk = kChunk) {
   const uint32_t st = L.start + c0;
-  const uint32_t cnt = min((uint32_t)kChunk, L.len - c0);
+  const uint32_t cnt = min(chunk, L.len - c0);
   const uint32_t npad = next_pow2(cnt);
   for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
     if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
@@ -3526,17 +3527,18 @@ __device__ __forceinline__ void large_place(const TBPolicy&, const LargeSeg& L, 
 template <class P> struct LargeScan { static constexpr bool v = false; };
 template <> struct LargeScan<TBPolicy> { static constexpr bool v = true; };
 
-// elements of the sorted chunk (K1, K2, K3)[b, b + n) below the key (k1, k2, k3): four chunks' binary
-// searches advance together, so their loads are in flight at once
-__device__ __forceinline__ void below4(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3, const uint32_t (&b)[4],
-                                       const uint32_t (&n)[4], uint64_t k1, uint64_t k2, uint32_t k3, uint32_t (&lo)[4]) {
-  uint32_t hi[4];
+// elements of the sorted chunk (K1, K2, K3)[b, b + n) below the key (k1, k2, k3): kRankPar chunks'
+// binary searches advance together, so their loads are in flight at once
+constexpr int kRankPar = 8;  // chunks whose binary searches a rank thread runs together
+__device__ __forceinline__ void below_n(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3, const uint32_t (&b)[kRankPar],
+                                       const uint32_t (&n)[kRankPar], uint64_t k1, uint64_t k2, uint32_t k3, uint32_t (&lo)[kRankPar]) {
+  uint32_t hi[kRankPar];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) { lo[q] = 0; hi[q] = n[q]; }
+  for (int q = 0; q < kRankPar; ++q) { lo[q] = 0; hi[q] = n[q]; }
   for (;;) {
     bool any = false;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kRankPar; ++q) {
       if (lo[q] >= hi[q]) continue;
       any = true;
       const uint32_t mid = (lo[q] + hi[q]) >> 1, x = b[q] + mid;
@@ -3549,6 +3551,7 @@ __device__ __forceinline__ void below4(const uint64_t* K1, const uint64_t* K2, c
 }
 
 constexpr uint32_t kRankTile = kBlock;   // elements of a large segment ranked per task (one per thread)
+constexpr uint32_t kParChunk = 1024;    // chunk of the task-parallel path: half the LDS sort, twice the searches
 constexpr uint32_t kLargeTab = 256;      // large segments whose task table fits LDS (else one block each)
 
 // The rest of a group-by's segments. Medium segments: one block each. Large segments (len > kTile)
@@ -3591,7 +3594,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     uint32_t a = 0, b = 0, ta, tb;
     if (i < nl) {
       const uint32_t len = large[i].len;
-      a = (len + kChunk - 1) / kChunk;
+      a = (len + kParChunk - 1) / kParChunk;
       b = (len + kRankTile - 1) / kRankTile;
     }
     block_scan2(a, b, s.perm, ta, tb);
@@ -3621,7 +3624,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     const LargeSeg L = large[i];
     const uint32_t nch = s_c1[i + 1] - s_c1[i], nrk = s_c2[i + 1] - s_c2[i];
     if (chunk) {
-      large_chunk_sort(p, s, L, (r - s_c1[i]) * kChunk, keys, vals, K1a, K2a, K3a);
+      large_chunk_sort(p, s, L, (r - s_c1[i]) * kParChunk, keys, vals, K1a, K2a, K3a, kParChunk);
       __threadfence();  // the sorted chunk is visible device-wide before it is counted
       __syncthreads();
       if (threadIdx.x == 0) atomicAdd(&lg[i].pad, 1u);
@@ -3643,20 +3646,21 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     __threadfence();
     const uint32_t e = (r - s_c2[i]) * kRankTile + threadIdx.x;
     if (e < L.len) {
-      const uint32_t x = L.start + e, c = e / kChunk;
+      const uint32_t x = L.start + e, c = e / kParChunk;
       const uint64_t k1 = K1a[x], k2 = K2a[x];
       const uint32_t k3 = K3a[x];
-      uint32_t rank = e - c * kChunk;
-      for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
-        uint32_t b[4], n[4], lo[4];
+      uint32_t rank = e - c * kParChunk;
+      for (uint32_t c0 = 0; c0 < nch; c0 += kRankPar) {
+        uint32_t b[kRankPar], n[kRankPar], lo[kRankPar];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kRankPar; ++q) {
           const uint32_t cc = c0 + q;
-          b[q] = L.start + cc * kChunk;
-          n[q] = (cc < nch && cc != c) ? min((uint32_t)kChunk, L.len - cc * kChunk) : 0u;
+          b[q] = L.start + cc * kParChunk;
+          n[q] = (cc < nch && cc != c) ? min(kParChunk, L.len - cc * kParChunk) : 0u;
         }
-        below4(K1a, K2a, K3a, b, n, k1, k2, k3, lo);
-        rank += lo[0] + lo[1] + lo[2] + lo[3];
+        below_n(K1a, K2a, K3a, b, n, k1, k2, k3, lo);
+#pragma unroll
+        for (int q = 0; q < kRankPar; ++q) rank += lo[q];
       }
       large_place(p, L, rank, k1, k2, k3, K1b, K2b, K3b);
     }
