@@ -326,6 +326,9 @@ hipError_t launch_flood_react(Dev& d, bool base_dev, uint32_t base_host, uint32_
 // sc->n_msgs_dev, which then grows by n.
 hipError_t launch_append(Dev& d, const uint32_t* src, const uint32_t* dst, const uint32_t* seq, const uint32_t* size,
                          const int64_t* t, uint32_t n);
+// The same copy at a host-known staged offset `base` (tgsim_enqueue_device): one launch, five arrays.
+hipError_t launch_stage(Dev& d, const uint32_t* src, const uint32_t* dst, const uint32_t* seq, const uint32_t* size,
+                        const int64_t* t, uint32_t n, uint32_t base);
 // A publish batch: set the seen bits of (local, pub) pairs already in d.fl.mark.
 hipError_t launch_flood_mark(Dev& d, uint32_t n);
 // TCP mode: the last window's packets (status, seq; count n_host or *n_dev) and deliveries ->

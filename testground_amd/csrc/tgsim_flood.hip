@@ -176,17 +176,18 @@ __global__ __launch_bounds__(kBlock) void k_flood_mark(const uint32_t* __restric
   atomicOr(&f.seen[(size_t)p * f.wpp + (v >> 5)], 1u << (v & 31));
 }
 
-// Appends behind the device-side staged count: every thread reads the same base (nothing in this
-// launch writes it); k_append_commit moves the count afterwards.
+// Appends behind the device-side staged count (sc non-null: every thread reads the same base, nothing
+// in this launch writes it; k_append_commit moves the count afterwards), or at the host-known base
+// (sc null: tgsim_enqueue_device, one launch for the five arrays instead of five copies).
 __global__ __launch_bounds__(kBlock) void k_append(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                                    const uint32_t* __restrict__ seq,
                                                    const uint32_t* __restrict__ size, const int64_t* __restrict__ t,
-                                                   uint32_t n, uint32_t cap, const DevScalars* sc,
+                                                   uint32_t n, uint32_t cap, const DevScalars* sc, uint32_t base_host,
                                                    uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
                                                    uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
                                                    int64_t* __restrict__ m_t) {
-  const uint32_t base = sc->n_msgs_dev;
-  if ((uint64_t)base + n > cap) return;  // k_append_commit reports it
+  const uint32_t base = sc ? sc->n_msgs_dev : base_host;
+  if ((uint64_t)base + n > cap) return;  // k_append_commit reports it (the host checked its own base)
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     m_src[base + i] = src[i]; m_dst[base + i] = dst[i]; m_seq[base + i] = seq[i]; m_size[base + i] = size[i];
     m_t[base + i] = t[i];
@@ -222,9 +223,18 @@ hipError_t launch_append(Dev& d, const uint32_t* src, const uint32_t* dst, const
                          const int64_t* t, uint32_t n) {
   if (!n) return hipSuccess;
   const unsigned g = std::min<unsigned>((n + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
-  hipLaunchKernelGGL(k_append, dim3(g), dim3(kBlock), 0, d.stream, src, dst, seq, size, t, n, d.cap_msgs, d.sc,
+  hipLaunchKernelGGL(k_append, dim3(g), dim3(kBlock), 0, d.stream, src, dst, seq, size, t, n, d.cap_msgs, d.sc, 0u,
                      d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   hipLaunchKernelGGL(k_append_commit, dim3(1), dim3(1), 0, d.stream, n, d.cap_msgs, d.sc);
+  return hipGetLastError();
+}
+
+hipError_t launch_stage(Dev& d, const uint32_t* src, const uint32_t* dst, const uint32_t* seq, const uint32_t* size,
+                        const int64_t* t, uint32_t n, uint32_t base) {
+  if (!n) return hipSuccess;
+  const unsigned g = std::min<unsigned>((n + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
+  hipLaunchKernelGGL(k_append, dim3(g), dim3(kBlock), 0, d.stream, src, dst, seq, size, t, n, d.cap_msgs,
+                     (const DevScalars*)nullptr, base, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 

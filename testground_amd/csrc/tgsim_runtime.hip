@@ -1113,12 +1113,9 @@ static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_
     HIPCK(c, launch_append(d, m->src, m->dst, m->seq, m->size, m->t_send, (uint32_t)n), "append");
     return TGSIM_OK;
   }
-  const size_t o = c->n_staged;
-  HIPCK(c, hipMemcpyAsync(d.m_src + o, m->src, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_dst + o, m->dst, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_seq + o, m->seq, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_size + o, m->size, n * 4, hipMemcpyDeviceToDevice, d.stream), "enqueue");
-  HIPCK(c, hipMemcpyAsync(d.m_t + o, m->t_send, n * 8, hipMemcpyDeviceToDevice, d.stream), "enqueue");
+  // one copy kernel for the five arrays (five hipMemcpyAsync cost ~5 us of launch each: config 2's
+  // million-message rounds spent 28 us per round staging)
+  HIPCK(c, launch_stage(d, m->src, m->dst, m->seq, m->size, m->t_send, (uint32_t)n, c->n_staged), "enqueue");
   c->n_staged += (uint32_t)n;
   return TGSIM_OK;
 }
