@@ -117,6 +117,7 @@ struct ProbeScalars {
   int64_t min_dl;                 // running min over waiting probers of their deadline (k_probe_step)
   uint32_t active;                // probers still waiting (k_probe_step -> snapshot n_active)
   uint32_t n_active;
+  uint32_t done, pad;             // k_probe_step workgroups finished (the last one proposes the window end)
 };
 struct ProbeDev {
   uint32_t* order = nullptr;      // [n_order]

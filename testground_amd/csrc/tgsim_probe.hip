@@ -35,10 +35,6 @@ __device__ __forceinline__ uint32_t next_pos(const ProbeDev& p, uint32_t g, uint
 
 __global__ void k_probe_base(DevScalars* sc, uint32_t base_host) { sc->n_msgs_dev = base_host; }
 
-__global__ void k_probe_reset(ProbeDev p) {
-  p.sc->min_dl = kNone;
-  p.sc->active = 0;
-}
 
 // Stage up to two messages per thread (a reply, then a request) with one reservation per block.
 struct Staged {
@@ -125,13 +121,12 @@ __global__ __launch_bounds__(kBlock) void k_probe_start(ProbeDev p, DevScalars* 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_probe_status(const uint8_t* __restrict__ status,
-                                                         const uint32_t* __restrict__ m_src,
-                                                         const uint32_t* __restrict__ m_dst,
-                                                         const uint32_t* __restrict__ m_seq, uint32_t n_host,
-                                                         const uint32_t* n_dev, ProbeDev p, uint32_t lo) {
+__device__ __forceinline__ void probe_status(const uint8_t* __restrict__ status, const uint32_t* __restrict__ m_src,
+                                             const uint32_t* __restrict__ m_dst, const uint32_t* __restrict__ m_seq,
+                                             uint32_t n_host, const uint32_t* n_dev, ProbeDev& p, uint32_t lo,
+                                             uint32_t bid, uint32_t nb) {
   const uint32_t n = n_dev ? *n_dev : n_host;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+  for (uint32_t i = bid * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
     const uint32_t sq = m_seq[i];
     if ((sq >> 30) != 1u) continue;
     const uint32_t code = status[i] & 0x0Fu;
@@ -141,13 +136,12 @@ __global__ __launch_bounds__(kBlock) void k_probe_status(const uint8_t* __restri
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_probe_arrive(const uint32_t* __restrict__ o_src,
-                                                         const uint32_t* __restrict__ o_dst,
-                                                         const uint32_t* __restrict__ o_seq,
-                                                         const int64_t* __restrict__ o_t, const DevScalars* sc,
-                                                         ProbeDev p, uint32_t lo) {
+__device__ __forceinline__ void probe_arrive(const uint32_t* __restrict__ o_src, const uint32_t* __restrict__ o_dst,
+                                             const uint32_t* __restrict__ o_seq, const int64_t* __restrict__ o_t,
+                                             const DevScalars* sc, ProbeDev& p, uint32_t lo, uint32_t bid,
+                                             uint32_t nb) {
   const uint32_t n = sc->n_out;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+  for (uint32_t i = bid * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
     const uint32_t sq = o_seq[i], tag = sq >> 30;
     if (tag == 1u) {  // a request at its peer
       const uint32_t l = o_src[i] - lo, j = sq & kTagMask;
@@ -160,6 +154,30 @@ __global__ __launch_bounds__(kBlock) void k_probe_arrive(const uint32_t* __restr
     }
   }
 }
+
+// The reaction's first launch: the window's refused requests (blocks [0, nb)) and first arrivals
+// (blocks [nb, 2 nb)) are independent of each other; block 0 also resets the step's reductions and
+// (host-counted staging) sets the staged base - four launches of ~5 us each became one.
+__global__ __launch_bounds__(kBlock) void k_probe_pre(const uint8_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ m_src,
+                                                      const uint32_t* __restrict__ m_dst,
+                                                      const uint32_t* __restrict__ m_seq, uint32_t n_host,
+                                                      const uint32_t* n_dev, const uint32_t* __restrict__ o_src,
+                                                      const uint32_t* __restrict__ o_dst,
+                                                      const uint32_t* __restrict__ o_seq,
+                                                      const int64_t* __restrict__ o_t, DevScalars* sc, ProbeDev p,
+                                                      uint32_t lo, uint32_t nb, uint32_t set_base, uint32_t base_host) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    p.sc->min_dl = kNone;
+    p.sc->active = 0;
+    p.sc->done = 0;
+    if (set_base) sc->n_msgs_dev = base_host;  // nothing in this launch reads it
+  }
+  if (blockIdx.x < nb) probe_status(status, m_src, m_dst, m_seq, n_host, n_dev, p, lo, blockIdx.x, nb);
+  else probe_arrive(o_src, o_dst, o_seq, o_t, sc, p, lo, blockIdx.x - nb, nb);
+}
+
+__device__ __forceinline__ void probe_end(ProbeDev& p, const DevScalars* sc);
 
 __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* sc, uint32_t lo, uint32_t nloc,
                                                        uint32_t cap, uint32_t* __restrict__ m_src,
@@ -199,14 +217,28 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
     flush_block(st, red, &sbase, sc, cap, m_src, m_dst, m_seq, m_size, m_t);
     block_waiting(p, dl_wait, waiting);
   }
+  // the last workgroup to finish proposes the next window's end (the former k_probe_end launch)
+  __shared__ uint32_t s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&p.sc->done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
+    __threadfence();
+    probe_end(p, sc);
+  }
 }
 
-__global__ void k_probe_end(ProbeDev p, const DevScalars* sc) {
+// every k_probe_step workgroup's reductions and reservations are done: the counters are read with
+// device-scope atomic loads (another XCD's L2 may hold the lines)
+__device__ __forceinline__ void probe_end(ProbeDev& p, const DevScalars* sc) {
   const int64_t t_end = sc->t_end;
   int64_t ne = t_end + p.window;
-  const uint32_t act = p.sc->active;
-  const int64_t m = p.sc->min_dl;
-  if (sc->n_msgs_dev == 0 && sc->arena_used == 0 && act && m != kNone && m + 1 > ne) ne = m + 1;
+  const uint32_t act = __hip_atomic_load(&p.sc->active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t m = __hip_atomic_load(&p.sc->min_dl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t staged = __hip_atomic_load(const_cast<uint32_t*>(&sc->n_msgs_dev), __ATOMIC_ACQUIRE,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  if (staged == 0 && sc->arena_used == 0 && act && m != kNone && m + 1 > ne) ne = m + 1;
   p.sc->next_end = ne;
   p.sc->n_active = act;
 }
@@ -228,15 +260,12 @@ hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_
                               const uint32_t* n_status_dev) {
   ProbeDev& p = d.pr;
   ProfScope ps_(d, KID_PROBE);
-  hipLaunchKernelGGL(k_probe_reset, dim3(1), dim3(1), 0, d.stream, p);
-  hipLaunchKernelGGL(k_probe_status, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst,
-                     d.m_seq, n_status_host, n_status_dev, p, d.lo);
-  hipLaunchKernelGGL(k_probe_arrive, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.o_src, d.o_dst, d.o_seq, d.o_t,
-                     d.sc, p, d.lo);
-  if (!base_dev) hipLaunchKernelGGL(k_probe_base, dim3(1), dim3(1), 0, d.stream, d.sc, base_host);
+  constexpr uint32_t nb = kStreamBlocks / 2;
+  hipLaunchKernelGGL(k_probe_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
+                     n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, p, d.lo, nb,
+                     base_dev ? 0u : 1u, base_host);
   hipLaunchKernelGGL(k_probe_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, p, d.sc, d.lo, d.nloc,
                      d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
-  hipLaunchKernelGGL(k_probe_end, dim3(1), dim3(1), 0, d.stream, p, d.sc);
   return hipGetLastError();
 }
 
