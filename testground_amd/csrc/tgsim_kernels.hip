@@ -907,6 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, con
 // ============================================================================================
 
 constexpr int kBktMaxKeyBits = 13;  // keys per bucket <= 8192 (32 KB of LDS counters)
+constexpr int kGlobUnroll = 8;      // items in flight per thread where one workgroup walks a whole bucket
 
 // Bucket of a key: b = k / w by a multiply-shift. m = ceil(2^32 / w) is exact when w is a power of
 // two, and for any w while k * w < 2^32 (nloc <= 2^20, w <= 512 on the fused path).
@@ -1159,7 +1160,19 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv b
 __device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t* cnt, uint32_t* part,
                                                    const BktHead& h) {
   const uint32_t tid = threadIdx.x;
-  for (uint32_t j = tid; j < h.nb; j += kBlock) atomicAdd(&cnt[kin[h.start + j] - h.k0], 1u);
+  // kGlobUnroll keys in flight per thread: one workgroup walks an oversized bucket alone (a probed
+  // target's 10k-request inbox), and a load per iteration made that a chain of ~40 latencies
+  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
+    uint32_t k[kGlobUnroll];
+#pragma unroll
+    for (int u = 0; u < kGlobUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      k[u] = j < h.nb ? kin[h.start + j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < kGlobUnroll; ++u)
+      if (k[u] != 0xFFFFFFFFu) atomicAdd(&cnt[k[u] - h.k0], 1u);
+  }
   __syncthreads();
   const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = tid * per;
   uint32_t sum = 0, mx = 0;
@@ -1219,11 +1232,22 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
     if (off2) off2[h.k0 + h.nk] = h.start + h.nb;
   }
   __syncthreads();
-  for (uint32_t j = tid; j < h.nb; j += kBlock) {
-    const uint32_t k = kin[h.start + j];
-    const uint32_t pos = h.start + atomicAdd(&cnt[k - h.k0], 1u);
-    kout[pos] = k;
-    vout[pos] = vin[h.start + j];
+  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
+    uint32_t k[kGlobUnroll], v[kGlobUnroll];
+#pragma unroll
+    for (int u = 0; u < kGlobUnroll; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      const bool in = j < h.nb;
+      k[u] = in ? kin[h.start + j] : 0xFFFFFFFFu;
+      v[u] = in ? vin[h.start + j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kGlobUnroll; ++u) {
+      if (k[u] == 0xFFFFFFFFu) continue;
+      const uint32_t pos = h.start + atomicAdd(&cnt[k[u] - h.k0], 1u);
+      kout[pos] = k[u];
+      vout[pos] = v[u];
+    }
   }
 }
 
@@ -1895,11 +1919,19 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
   __syncthreads();
   TG_PH(1);
   if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest: contiguous copy first
-    for (uint32_t j = threadIdx.x; j < h.nb; j += kBlock) {
-      const uint32_t p = chunk_of(cexcl, j);
-      const uint2 e = kv[csrc[p] + (j - cexcl[p])];
-      kscr[h.start + j] = e.x;
-      vscr[h.start + j] = e.y;
+    for (uint32_t j0 = threadIdx.x; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
+      uint2 e[kGlobUnroll];
+#pragma unroll
+      for (int u = 0; u < kGlobUnroll; ++u) {
+        const uint32_t j = min(j0 + u * kBlock, h.nb - 1);  // clamped: the load stays valid
+        const uint32_t p = chunk_of(cexcl, j);
+        e[u] = kv[csrc[p] + (j - cexcl[p])];
+      }
+#pragma unroll
+      for (int u = 0; u < kGlobUnroll; ++u) {
+        const uint32_t j = j0 + u * kBlock;
+        if (j < h.nb) { kscr[h.start + j] = e[u].x; vscr[h.start + j] = e[u].y; }
+      }
     }
     __syncthreads();
     (void)bkt_count_body(kscr, sm.cnt, sm.part, h);
