@@ -225,6 +225,7 @@ struct tgo_ctx {
   tgsim_tcp_stats tstats;
   /* sequential probes (tgsim_probe_*) */
   struct oprobe* pr; uint32_t* pr_order; uint8_t* pr_out; uint32_t pr_n; tgsim_probe_config pr_cfg;
+  int pr_need_react;  /* a window ended with probes set up: tgo_probe_react before staging or the next window */
   char err[512];
 };
 
@@ -545,8 +546,12 @@ int tgo_get_ip(const tgo_ctx* c, uint32_t g, uint32_t* ip) {
 /* ============================== data path =================================================== */
 
 static int enqueue_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n);
+static int react_owed(tgo_ctx* c) {
+  return c->pr_need_react ? fail(c, TGSIM_ESTATE, "probes: probe_react after every window") : TGSIM_OK;
+}
 int tgo_enqueue(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tcp_send");
+  if (react_owed(c)) return TGSIM_ESTATE;
   return enqueue_impl(c, m, n);
 }
 static int enqueue_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
@@ -851,6 +856,7 @@ static int tcp_release(tgo_ctx* c, int64_t t_end);
 int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
+  if (react_owed(c)) return TGSIM_ESTATE;
   if (c->tcp_on) {
     if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
     int rc = tcp_release(c, t_end);
@@ -946,6 +952,7 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
   }
   c->in_window = 1;
   c->tcp_need_react = c->tcp_on;
+  c->pr_need_react = c->pr != NULL;
   return TGSIM_OK;
 }
 
@@ -1201,6 +1208,7 @@ static int gen_storm_impl(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanou
 int tgo_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                         int64_t spread_ns, uint32_t state) {
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_gen_storm_round");
+  if (react_owed(c)) return TGSIM_ESTATE;
   return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state, 0);
 }
 
@@ -1413,6 +1421,7 @@ int tgo_probe_setup(tgo_ctx* c, const uint32_t* order, uint32_t n_order, const t
   for (uint32_t l = 0; l < c->nloc; ++l) pr[l].t_done = INT64_MIN;
   free(c->pr); free(c->pr_order); free(c->pr_out);
   c->pr = pr; c->pr_order = ord; c->pr_out = out; c->pr_n = n_order; c->pr_cfg = *cfg;
+  c->pr_need_react = 0;
   return TGSIM_OK;
 }
 
@@ -1453,6 +1462,7 @@ static int pr_flush(tgo_ctx* c, pbuf* b) {
 int tgo_probe_start(tgo_ctx* c, int64_t t0) {
   if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (react_owed(c)) return TGSIM_ESTATE;
   if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
   pbuf b;
   if (pr_alloc(&b, (size_t)c->nloc + 1)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
@@ -1464,6 +1474,8 @@ int tgo_probe_start(tgo_ctx* c, int64_t t0) {
 int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->pr_need_react) return fail(c, TGSIM_ESTATE, "probes: no window since the last reaction");
+  c->pr_need_react = 0;  /* the window's staged rows are read exactly once */
   const omsgs* s = &c->staged;
   const int64_t H = c->horizon, t_end = c->now, timeout = c->pr_cfg.timeout_ns;
   /* 1. the window's requests: a route that refused one ends the probe at once */
@@ -1497,18 +1509,20 @@ int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   for (uint32_t l = 0; l < c->nloc; ++l) {
     oprobe* p = &c->pr[l];
     if (p->state != PR_WAIT) continue;
+    const int64_t dl = p->t_req + timeout;
+    int reply_pending = 0;  /* a reply staged now before the deadline can still beat it */
     if (p->t_reqarr != PR_NONE && !p->replied) {
-      pr_stage(&b, c->pr_order[p->pos], c->lo + l, TGSIM_PROBE_REP | (c->lo + l), c->pr_cfg.reply_bytes,
-               p->t_reqarr > H ? p->t_reqarr : H);
+      const int64_t trep = p->t_reqarr > H ? p->t_reqarr : H;
+      pr_stage(&b, c->pr_order[p->pos], c->lo + l, TGSIM_PROBE_REP | (c->lo + l), c->pr_cfg.reply_bytes, trep);
       p->replied = 1;
+      reply_pending = trep < dl;
     }
     p->t_reqarr = PR_NONE;
-    const int64_t dl = p->t_req + timeout;
     uint8_t outc = TGSIM_PROBE_NONE;
     int64_t te = 0;
     if (p->refused) { outc = TGSIM_PROBE_REFUSED; te = p->t_req; }
     else if (p->t_reparr != PR_NONE && p->t_reparr < dl) { outc = TGSIM_PROBE_OK; te = p->t_reparr; }
-    else if (dl < t_end) { outc = TGSIM_PROBE_TIMEOUT; te = dl; }
+    else if (dl < t_end && !reply_pending) { outc = TGSIM_PROBE_TIMEOUT; te = dl; }
     if (outc != TGSIM_PROBE_NONE) {
       c->pr_out[(size_t)l * c->pr_n + p->pos] = outc;
       pr_begin(c, l, pr_next(c, p, p->pos), te, H, &b);

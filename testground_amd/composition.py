@@ -129,12 +129,18 @@ def _strs(m):
 
 def _go_float(x: float) -> str:
     """encoding/json's float64 text: the shortest round-trip digits, 'f' form for magnitudes in
-    [1e-6, 1e21) (so 1.0 is "1"), else 'e' form with at least two exponent digits ("1e+21")."""
+    [1e-6, 1e21) (so 1.0 is "1"), else 'e' form: "1e+21", and "1e-7" (a negative exponent's leading
+    zero is dropped, encoding/json's "e-09 to e-9" clean-up)."""
     if x != x or x in (float("inf"), float("-inf")):
         raise ValueError(f"json: unsupported value: {x}")
     if x == 0 or 1e-6 <= abs(x) < 1e21:
         return np.format_float_positional(x, trim="-")
-    return np.format_float_scientific(x, trim="-", exp_digits=2)
+    s = np.format_float_scientific(x, trim="-", exp_digits=2)
+    # encoding/json "clean up e-09 to e-9": a negative exponent loses its leading zero (1e-7);
+    # positive ones keep two digits (1e+21)
+    if len(s) >= 4 and s[-4:-2] == "e-" and s[-2] == "0":
+        s = s[:-2] + s[-1]
+    return s
 
 
 def _go_json(v) -> str:

@@ -194,17 +194,22 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
     if (l < nloc && p.state[l] == kWait) {
       const uint32_t g = lo + l, pos = p.pos[l];
       const int64_t rq = p.t_reqarr[l];
+      const int64_t tr = p.t_req[l], dl = tr + p.timeout, ra = p.t_reparr[l];
+      // a reply staged now, before the deadline, may still beat it: its arrival decides next window
+      // (a request arriving within one window of the deadline is not a timeout)
+      bool reply_pending = false;
       if (rq != kNone && !p.replied[l]) {  // the peer answers the request's first arrival
-        st.add(p.order[pos], g, TGSIM_PROBE_REP | g, p.rep_bytes, rq > H ? rq : H);
+        const int64_t trep = rq > H ? rq : H;
+        st.add(p.order[pos], g, TGSIM_PROBE_REP | g, p.rep_bytes, trep);
         p.replied[l] = 1;
+        reply_pending = trep < dl;
       }
       p.t_reqarr[l] = kNone;
-      const int64_t tr = p.t_req[l], dl = tr + p.timeout, ra = p.t_reparr[l];
       uint8_t out = TGSIM_PROBE_NONE;
       int64_t te = 0;
       if (p.refused[l]) { out = TGSIM_PROBE_REFUSED; te = tr; }
       else if (ra != kNone && ra < dl) { out = TGSIM_PROBE_OK; te = ra; }
-      else if (dl < t_end) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
+      else if (dl < t_end && !reply_pending) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
       if (out != TGSIM_PROBE_NONE) {
         p.out[(size_t)l * p.n_order + pos] = out;
         begin_probe(p, l, g, next_pos(p, g, pos), te, H, st);

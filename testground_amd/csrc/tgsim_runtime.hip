@@ -163,7 +163,17 @@ struct tgsim_ctx {
   std::vector<uint32_t> fl_off, fl_nbr;
   uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
   bool probes = false;      // tgsim_probe_setup done
+  // a window ended with probes set up: tgsim_probe_react must run before anything stages messages or
+  // opens the next window (it reads the window's staged rows and deliveries)
+  bool probe_need_react = false;
 };
+
+// Calls that stage messages or open a window refuse while a reaction is owed for the last one.
+static int fail(tgsim_ctx* c, int code, const char* fmt, ...);
+static int react_owed(tgsim_ctx* c) {
+  if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "probes: tgsim_probe_react after every window");
+  return 0;
+}
 
 // An allocation point of a host-side table (tgsim_debug_fail_alloc makes the chosen one throw, so
 // the tests can drive the ABI's bad_alloc path without exhausting memory).
@@ -1048,6 +1058,7 @@ static int enqueue_host(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   c->spec.valid = false;  // staged arrays change: no speculative storm round
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
+  if (int rc = react_owed(c)) return rc;
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (!c->staged_dev && (uint64_t)c->n_staged + n > c->d.cap_msgs)
     return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
@@ -1104,6 +1115,7 @@ static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_
   c->spec.valid = false;  // staged arrays change: no speculative storm round
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: traffic goes through tgsim_tcp_send");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "enqueue inside a window");
+  if (int rc = react_owed(c)) return rc;
   if ((c->staged_dev ? 0 : (uint64_t)c->n_staged) + n > c->d.cap_msgs)
     return fail(c, TGSIM_ECAPACITY, "staged-message capacity");
   if (!n) return TGSIM_OK;
@@ -1217,6 +1229,7 @@ static int begin_common(tgsim_ctx* c) {
   c->end_known = false;  // device-ended windows (barrier / device t_end); explicit ones set it after
   c->in_window = true;
   c->tcp_need_react = c->tcp_on;
+  c->probe_need_react = c->probes;
   return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
 
@@ -1227,6 +1240,7 @@ extern "C" int tgsim_advance_begin(tgsim_ctx* c, int64_t t_end) {
 static int tgsim_advance_begin_body(tgsim_ctx* c, int64_t t_end) {
   if (!c) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (int rc = react_owed(c)) return rc;
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t_end < c->now) return fail(c, TGSIM_ECAUSALITY, "t_end before window start");
   // a host-staged message sent at or after t_end is refused before anything changes (the context
@@ -1275,6 +1289,7 @@ extern "C" int tgsim_advance_begin_device(tgsim_ctx* c, const int64_t* t_end_dev
 static int tgsim_advance_begin_device_body(tgsim_ctx* c, const int64_t* t_end_dev, int64_t offset_ns) {
   if (!c || !t_end_dev) return TGSIM_EINVAL;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
+  if (int rc = react_owed(c)) return rc;
   HIPCK(c, flush_storm(c), "storm commit");
   HIPCK(c, launch_set_window_dev(c->d, t_end_dev, offset_ns), "set window");
   return begin_common(c);
@@ -1486,6 +1501,7 @@ static int tgsim_advance_to_barrier_body(tgsim_ctx* c, uint32_t waiter, int64_t 
   if (rc0) return rc0;
   if (c->in_window) return fail(c, TGSIM_ESTATE, "window already open");
   if (waiter >= c->n_waiters) return fail(c, TGSIM_EINVAL, "bad waiter");
+  if (int rc = react_owed(c)) return rc;
   if (c->storm_pending) {  // commit + barrier registration + window start: one launch
     c->storm_pending = false;
     const bool add = c->storm_add;
@@ -1755,6 +1771,7 @@ extern "C" int tgsim_gen_storm_round(tgsim_ctx* c, uint32_t round, int64_t t0, u
 static int tgsim_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                                      int64_t spread_ns, uint32_t state) {
   if (c && c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_gen_storm_round");
+  if (c) if (int rc = react_owed(c)) return rc;
   return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state);
 }
 
@@ -1979,6 +1996,7 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
     dfree(c, q);
   p = ProbeDev{};
   c->probes = false;
+  c->probe_need_react = false;
   const size_t nl = std::max<uint32_t>(c->nloc, 1);
   if (dalloc(c, &p.order, n_order) || dalloc(c, &p.pos, nl) || dalloc(c, &p.state, nl) || dalloc(c, &p.refused, nl) ||
       dalloc(c, &p.replied, nl) || dalloc(c, &p.t_req, nl) || dalloc(c, &p.t_reqarr, nl) || dalloc(c, &p.t_reparr, nl) ||
@@ -2018,6 +2036,7 @@ static int tgsim_probe_start_body(tgsim_ctx* c, int64_t t0) {
   if (!c) return TGSIM_EINVAL;
   if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (int rc = react_owed(c)) return rc;
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
   HIPCK(c, launch_probe_start(c->d, c->staged_dev, c->n_staged, t0), "probe start");
@@ -2034,10 +2053,12 @@ static int tgsim_probe_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_a
   if (!c) return TGSIM_EINVAL;
   if (!c->probes) return fail(c, TGSIM_ESTATE, "no probes set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->probe_need_react) return fail(c, TGSIM_ESTATE, "probes: no window since the last reaction");
   const bool on_dev = c->n_status_last == kStatusOnDevice;
   HIPCK(c, launch_probe_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
                               on_dev ? &c->d.sc->n_msgs_last : nullptr), "probe react");
   probes_staged(c);
+  c->probe_need_react = false;
   if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
   ProbeScalars ps;
   HIPCK(c, hipMemcpyAsync(&ps, c->d.pr.sc, sizeof(ps), hipMemcpyDeviceToHost, c->d.stream), "probe react");

@@ -182,11 +182,16 @@ class LinkRule:
         return LinkRule(ipnet_from_wire(_get(d, "Subnet")), LinkShape.from_wire(d))
 
 
-class RuleList(list):
+class RuleList(tuple):
     """A rule list that many Configs share (splitbrain: every region-A node installs the same
-    /32 block): its C array is built once and reused while the list's length is unchanged."""
-    c_array = None
-    c_len = -1
+    /32 block). It is immutable and snapshots its rules' C form when it is built, so every Config
+    that carries it passes the same array without rebuilding it (a mutable list whose
+    cache was keyed on its length could hand out a stale array after an in-place edit)."""
+
+    def __new__(cls, rules=()):
+        self = super().__new__(cls, rules)
+        self.c_array = (A.LinkRule * max(1, len(self)))(*[r.to_c() for r in self])
+        return self
 
 
 @dataclass
@@ -223,11 +228,10 @@ class Config:
         """Returns (tgsim_network_config, keepalive) - keep the second alive during the call."""
         if self.ipv6:
             raise A.TgsimError(A.ENOTSUP, "IPv6 data networks are not simulated")
-        rules = getattr(self.rules, "c_array", None)
-        if rules is None or self.rules.c_len != len(self.rules):
+        if isinstance(self.rules, RuleList):
+            rules = self.rules.c_array
+        else:
             rules = (A.LinkRule * max(1, len(self.rules)))(*[r.to_c() for r in self.rules])
-            if isinstance(self.rules, RuleList):
-                self.rules.c_array, self.rules.c_len = rules, len(self.rules)
         name = self.network.encode()
         cfg = A.NetworkConfig(name, int(bool(self.enable)), policy_code(self.routing_policy), self.default.to_c(),
                               C.cast(rules, C.POINTER(A.LinkRule)), len(self.rules),

@@ -334,7 +334,7 @@ class PlanEnv:
             if not active.any() and not any(waiting.values()):
                 break
             idle = not self._pend and self.sim.stats()["inflight"] == 0
-            if idle and active.any() and answered[active].all() is not None:
+            if idle and active.any():
                 # only timeouts can end the active dials: jump to the first one
                 t_next = int((t_start[active] + timeout_ns).min()) + 1
                 d = self.step(max(t_next, self.sim.now + self.window_ns))

@@ -232,7 +232,7 @@ def test_test_params_are_strings_as_in_go():
 
 
 @pytest.mark.parametrize("value,text", [(10, "10"), (1.0, "1"), (1.5, "1.5"), (True, "true"), (0.1, "0.1"),
-                                        (1e21, "1e+21"), (1e-7, "1e-07"), (123456789.0, "123456789"),
+                                        (1e21, "1e+21"), (1e-7, "1e-7"), (2.5e-10, "2.5e-10"), (-3e-8, "-3e-8"), (123456789.0, "123456789"),
                                         ({"b": 1, "a": [1, 2.0]}, '{"a":[1,2],"b":1}'), ("x", "x")])
 def test_manifest_defaults_marshal_like_go(value, text):
     """PrepareForRun JSON-encodes non-string defaults with encoding/json (composition.go:508-517):

@@ -121,3 +121,60 @@ def test_probe_errors(oracle):
         s.tcp_enable()
     assert e.value.code == A.ESTATE
     s.close()
+
+
+def _deadline_case(b):
+    """a request that arrives within one window of its deadline. 0 -> 1 has 1 ms of
+    latency and the probes a 1.05 ms timeout: 0's request arrives at 1.0 ms, in the window
+    [1.0, 1.1) ms, and 1 answers it at 1.0 ms over its zero-latency link. The reaction after that
+    window sees the deadline (1.05 ms) already behind the window end, but the reply it just staged
+    can still beat it: the decision waits a window, and the reply's arrival at 1.0 ms makes the probe
+    OK. 1's probe of 0 crosses the slow link on the way back and ends OK at 1.0 ms as well."""
+    s = Simulator(SimConfig(n_instances=2, seed=5), binding=b)
+    s.set_shapes([0], [make_shape(latency_ns=1 * MS)])
+    _, res, t_done, _ = drive(s, np.arange(2), timeout=1 * MS + 50_000)
+    assert res.tolist() == [[0, A.PROBE_OK], [A.PROBE_OK, 0]]
+    assert t_done.tolist() == [1 * MS, 1 * MS]
+    s.close()
+
+
+def test_probe_deadline_within_a_window_oracle(oracle):
+    _deadline_case(oracle)
+
+
+@pytest.mark.gpu
+def test_probe_deadline_within_a_window_hip(hip):
+    _deadline_case(hip)
+
+
+def _react_owed_case(b):
+    """after a window, the probe reaction owns the window's staged rows and deliveries.
+    Staging, a probe start or the next window before tgsim_probe_react is refused (ESTATE), and so
+    is a second reaction without a window in between."""
+    s = Simulator(SimConfig(n_instances=4, seed=1), binding=b)
+    s.probe_setup(np.arange(4), 66, 66, SEC, W)
+    s.probe_start(0)
+    s.advance(W)
+    for call in (lambda: s.enqueue([0], [1], [77], [64], [W]), lambda: s.probe_start(W),
+                 lambda: s.advance(2 * W), lambda: s.gen_storm_round(0, W, 2, 64, 0, 1)):
+        with pytest.raises(A.TgsimError) as e:
+            call()
+        assert e.value.code == A.ESTATE
+    ne, act = s.probe_react()
+    assert act > 0 and ne == 2 * W
+    with pytest.raises(A.TgsimError) as e:
+        s.probe_react()
+    assert e.value.code == A.ESTATE
+    s.enqueue([0], [1], [77], [64], [W])   # now allowed
+    s.advance(ne)
+    s.probe_react()
+    s.close()
+
+
+def test_probe_react_owed_oracle(oracle):
+    _react_owed_case(oracle)
+
+
+@pytest.mark.gpu
+def test_probe_react_owed_hip(hip):
+    _react_owed_case(hip)
