@@ -446,6 +446,68 @@ int tgsim_probe_state_device(tgsim_ctx* ctx, const int64_t** next_end_device, co
  * and probes not yet ended); t_done[l] = when its last probe ended (INT64_MIN while probing). */
 int tgsim_probe_results(tgsim_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap_outcome);
 
+/* ---- storm plan reactor: dials and paced writes on the device -----------------
+ * plans/benchmarks/storm.go:117-190, per instance: `outgoing` goroutines, each sleeping until its
+ * t_ready (conn_delay_ms), then dialling its peer under the dial semaphore `sem` (concurrent slots,
+ * FIFO in (t_ready, connection) order; net.DialTimeout, storm.go:141-152), and - once every dial is
+ * done and "outgoing-dials-done" released - writing data_bytes in chunk_bytes writes, each under the
+ * write semaphore `writesem` (storm.go:158-183), where conn.Write returns once the chunk fits the
+ * connection's send buffer and blocks its goroutine, holding its slot, while the buffer is full.
+ * Connection h = instance * outgoing + k (k < outgoing) goes to dst[h]. Message mode:
+ *  - a dial is a SYN (syn_bytes, seq = TGSIM_STORM_SYN | k) that the peer answers at its first
+ *    arrival with a SYN-ACK (seq = TGSIM_STORM_SYNACK | h) at max(arrival, horizon); the dial ends
+ *    TGSIM_PROBE_OK at the SYN-ACK's first arrival before the deadline (start + dial_timeout_ns),
+ *    TGSIM_PROBE_REFUSED at its start when the dialler's route refuses the SYN, TGSIM_PROBE_TIMEOUT
+ *    at the deadline otherwise; its semaphore slot is free from its end on;
+ *  - a write is one message of payload + header_bytes (seq = TGSIM_STORM_DATA | k * n_chunks + j,
+ *    n_chunks = ceil(data_bytes / chunk_bytes)); a connection's buffer holds msg_window chunks that
+ *    have neither arrived (first copy) nor failed (a status other than QUEUED).
+ * After every window, tgsim_storm_react resolves dials, answers SYNs, starts the dials the semaphore
+ * admits (those due before the next window's end), and in the write phase runs each instance's
+ * writesem round at the window's end over the room the window's arrivals and failures freed, all
+ * staged on the device behind the device-side staged count. It proposes the next window's end
+ * (window_ns later while anything is staged or in flight, else the next deadline + 1 or the next
+ * dial's start). Single-shard contexts, message mode (not with probes, a flood graph or TCP mode).
+ * Like probes, it owns each window's statuses and deliveries: staging or the next window before the
+ * reaction is ESTATE. */
+#define TGSIM_STORM_SYN 0x40000000u
+#define TGSIM_STORM_DATA 0x80000000u
+#define TGSIM_STORM_SYNACK 0xC0000000u
+typedef struct tgsim_storm_config {
+  uint32_t outgoing;          /* connections per instance (conn_outgoing), >= 1 */
+  uint32_t concurrent;        /* width of the dial and write semaphores (concurrent_dials), >= 1 */
+  uint32_t chunk_bytes;       /* bytes per conn.Write (storm.go:23 buffersize: 4096), >= 1 */
+  uint32_t header_bytes;      /* wire overhead added to every chunk */
+  uint64_t data_bytes;        /* bytes each connection writes (data_size_kb * 1024) */
+  uint32_t syn_bytes;         /* wire bytes of a SYN and of a SYN-ACK */
+  uint32_t msg_window;        /* chunks a connection's send buffer holds (>= 1) */
+  int64_t dial_timeout_ns;    /* net.DialTimeout (storm.go:144: 30 s), > 0 */
+  int64_t window_ns;          /* window length while traffic is staged or in flight, > 0 */
+} tgsim_storm_config;
+typedef struct tgsim_storm_totals {
+  uint64_t chunks_written, chunks_delivered, chunks_failed, bytes_written;
+  uint32_t dials_ok, dials_failed, dials_pending, conns_writing;  /* conns_writing: chunks left or in flight */
+} tgsim_storm_totals;
+/* dst[h], t_ready[h] (>= tgsim_now) for every connection h < n_instances * outgoing; resets the reactor. */
+int tgsim_storm_setup(tgsim_ctx* ctx, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg);
+/* Stage the dials the semaphores admit before tgsim_now + window_ns (the first reaction). */
+int tgsim_storm_start(tgsim_ctx* ctx);
+/* After every window (see above). next_end / n_active non-NULL: synchronise and return the proposed
+ * window end and the connections still dialling (dial phase) or writing / in flight (write phase);
+ * both NULL: asynchronous (tgsim_storm_state_device). */
+int tgsim_storm_react(tgsim_ctx* ctx, int64_t* next_end, uint32_t* n_active);
+int tgsim_storm_state_device(tgsim_ctx* ctx, const int64_t** next_end_device, const uint32_t** n_active_device);
+/* Per connection: dial outcome TGSIM_PROBE_* (NONE while pending) and its end time. */
+int tgsim_storm_dials(tgsim_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap);
+/* The write phase: every connection's goroutine takes writesem at t0 (>= horizon; the release of
+ * "outgoing-dials-done", storm.go:156), in connection order. */
+int tgsim_storm_write_start(tgsim_ctx* ctx, int64_t t0);
+/* Per instance: failed = a chunk of it failed (lost, tail-dropped, refused) or is still in flight;
+ * t_last = when its last conn.Write returned (INT64_MIN: none); totals. Any output may be NULL. */
+int tgsim_storm_results(tgsim_ctx* ctx, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* totals);
+/* Detach the reactor: windows no longer need tgsim_storm_react. */
+int tgsim_storm_end(tgsim_ctx* ctx);
+
 /* ---- TCP-level mode ----------------------------------
  * The reference plans move application data over TCP (plans/benchmarks/storm.go:127-180 dials and
  * writes in chunks, plans/network/pingpong.go:73-104 times round trips over a connection); with loss

@@ -106,6 +106,13 @@ int tgo_probe_setup(tgo_ctx* ctx, const uint32_t* order, uint32_t n_order, const
 int tgo_probe_start(tgo_ctx* ctx, int64_t t0);
 int tgo_probe_react(tgo_ctx* ctx, int64_t* next_end, uint32_t* n_active);
 int tgo_probe_results(tgo_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap_outcome);
+int tgo_storm_setup(tgo_ctx* ctx, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg);
+int tgo_storm_start(tgo_ctx* ctx);
+int tgo_storm_react(tgo_ctx* ctx, int64_t* next_end, uint32_t* n_active);
+int tgo_storm_dials(tgo_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_t cap);
+int tgo_storm_write_start(tgo_ctx* ctx, int64_t t0);
+int tgo_storm_results(tgo_ctx* ctx, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* totals);
+int tgo_storm_end(tgo_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -102,6 +102,19 @@ class ProbeConfig(C.Structure):
                 ("window_ns", C.c_int64)]
 
 
+class StormConfig(C.Structure):
+    _fields_ = [("outgoing", C.c_uint32), ("concurrent", C.c_uint32), ("chunk_bytes", C.c_uint32),
+                ("header_bytes", C.c_uint32), ("data_bytes", C.c_uint64), ("syn_bytes", C.c_uint32),
+                ("msg_window", C.c_uint32), ("dial_timeout_ns", C.c_int64), ("window_ns", C.c_int64)]
+
+
+class StormTotals(C.Structure):
+    _fields_ = [("chunks_written", C.c_uint64), ("chunks_delivered", C.c_uint64), ("chunks_failed", C.c_uint64),
+                ("bytes_written", C.c_uint64), ("dials_ok", C.c_uint32), ("dials_failed", C.c_uint32),
+                ("dials_pending", C.c_uint32), ("conns_writing", C.c_uint32)]
+
+
+STORM_SYN, STORM_DATA, STORM_SYNACK = 0x40000000, 0x80000000, 0xC0000000
 PROBE_NONE, PROBE_OK, PROBE_REFUSED, PROBE_TIMEOUT = 0, 1, 2, 3
 PROBE_REQ, PROBE_REP = 0x40000000, 0xC0000000
 TCP_ACK_BIT = 0x80000000
@@ -180,6 +193,13 @@ _SIGS = {
     "probe_start": (C.c_int, [P, C.c_int64]),
     "probe_react": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_uint32)]),
     "probe_results": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "storm_setup": (C.c_int, [P, C.c_void_p, C.c_void_p, C.POINTER(StormConfig)]),
+    "storm_start": (C.c_int, [P]),
+    "storm_react": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_uint32)]),
+    "storm_dials": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "storm_write_start": (C.c_int, [P, C.c_int64]),
+    "storm_results": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(StormTotals)]),
+    "storm_end": (C.c_int, [P]),
 }
 # entry points only the HIP library has
 _SIGS_HIP = {
@@ -206,6 +226,7 @@ _SIGS_HIP = {
     "restore": (C.c_int, [P, C.c_void_p, C.c_size_t]),
     "debug_fail_alloc": (C.c_int, [P, C.c_uint32]),
     "probe_state_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "storm_state_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
 }
 
 

@@ -132,10 +132,50 @@ struct ProbeDev {
   int64_t timeout = 0, window = 0;
 };
 
+// Storm plan reactor (tgsim_storm_*): per connection h (instance * O + k) its dial
+// and write state, per local instance its dial FIFO position, semaphore slots and writesem queue.
+struct StormScalars {
+  int64_t next_end;               // the proposed end of the next window
+  int64_t min_dl;                 // running min of waiting dials' deadlines (k_storm_step)
+  int64_t next_start;             // running min of the start times of admitted dials not yet due
+  uint32_t active, n_active;      // connections dialling / writing (k_storm_step -> snapshot)
+  uint32_t done, pad;             // k_storm_step workgroups finished (the last proposes the window end)
+  unsigned long long written, delivered, failed, bytes;  // chunks (cumulative)
+};
+struct StormDev {
+  uint32_t O = 0, C = 0, Hc = 0;  // connections per instance, semaphore width, holder capacity min(C, O)
+  uint32_t nchunks = 0, chunk = 0, hdr = 0, syn = 0, win = 0;
+  uint64_t data = 0;
+  int64_t timeout = 0, window = 0;
+  uint32_t n_conn = 0, phase = 0;  // phase 0: dials, 1: writes
+  // [n_conn]
+  uint32_t* dst = nullptr;
+  int64_t* t_ready = nullptr;
+  uint8_t* state = nullptr;       // sleeping / waiting / done (dial) - kept through the write phase
+  uint8_t* flags = nullptr;       // bit 0 refused, bit 1 the peer answered the SYN
+  uint8_t* res = nullptr;         // TGSIM_PROBE_* dial outcome
+  uint32_t* slot = nullptr;       // the dial semaphore slot a waiting dial holds
+  int64_t *t_start = nullptr, *t_synarr = nullptr, *t_ackarr = nullptr, *t_done = nullptr, *t_rep = nullptr;
+  uint32_t* emit = nullptr;       // this reaction's staging per connection (dial: bits; writes: chunks)
+  uint32_t* rem = nullptr;        // chunks not yet written
+  uint32_t* infl = nullptr;       // chunks in the send buffer (neither arrived nor failed)
+  uint32_t* order = nullptr;      // per instance its connections k in dial FIFO order (t_ready, k)
+  uint32_t* ring = nullptr;       // per instance the writesem FIFO (O entries, a ring)
+  uint32_t* claim = nullptr;      // bit per chunk (h * nchunks + j): first arrival seen
+  // [nloc]
+  uint32_t *dq = nullptr, *qh = nullptr, *ql = nullptr, *nh = nullptr;
+  int64_t* slot_t = nullptr;      // [nloc * C] time each semaphore slot fell free (kBusy: held)
+  uint32_t* hold = nullptr;       // [nloc * Hc] goroutines holding writesem, blocked in conn.Write
+  uint8_t* failed = nullptr;      // an instance's chunk failed
+  int64_t* t_last = nullptr;      // its last conn.Write return
+  StormScalars* sc = nullptr;
+};
+
 struct Dev {
   Prof prof;
   Flood fl;
   ProbeDev pr;
+  StormDev sm;
   hipStream_t stream = nullptr;
   uint32_t N = 0, S = 1, shard = 0, lo = 0, nloc = 0;
   uint32_t data_net = 0, data_mask = 0, data_len = 0;
@@ -364,6 +404,15 @@ hipError_t launch_probe_start(Dev& d, bool base_dev, uint32_t base_host, int64_t
 // proposed end (ProbeScalars::next_end)
 hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev);
+
+// Storm plan reactor. start: the first dials (frame H = t_end = t_now); react: the window's statuses
+// and deliveries, then per instance its dials / writes (staged behind sc->n_msgs_dev, set from
+// base_host unless base_dev) and the next window's proposed end (StormScalars::next_end).
+hipError_t launch_storm_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t_now);
+hipError_t launch_storm_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                              const uint32_t* n_status_dev);
+// the write phase: every connection queued on its instance's writesem, first round at t0
+hipError_t launch_storm_write_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t0);
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),
 // exclusive scan into offsets[0..n], then (entries != nullptr) the entry ids, at most entries_cap.

@@ -166,12 +166,15 @@ struct tgsim_ctx {
   // a window ended with probes set up: tgsim_probe_react must run before anything stages messages or
   // opens the next window (it reads the window's staged rows and deliveries)
   bool probe_need_react = false;
+  bool storm_on = false;    // tgsim_storm_setup done, not ended
+  bool storm_need_react = false;
 };
 
 // Calls that stage messages or open a window refuse while a reaction is owed for the last one.
 static int fail(tgsim_ctx* c, int code, const char* fmt, ...);
 static int react_owed(tgsim_ctx* c) {
   if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "probes: tgsim_probe_react after every window");
+  if (c->storm_need_react) return fail(c, TGSIM_ESTATE, "storm: tgsim_storm_react after every window");
   return 0;
 }
 
@@ -1230,6 +1233,7 @@ static int begin_common(tgsim_ctx* c) {
   c->in_window = true;
   c->tcp_need_react = c->tcp_on;
   c->probe_need_react = c->probes;
+  c->storm_need_react = c->storm_on;
   return TGSIM_OK;  // device-side errors surface at the next synchronisation
 }
 
@@ -1858,6 +1862,7 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
   // attempt) would be forwarded as floods and corrupt the TCP state
   if (c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is on: flood workloads need message mode");
   if (c->probes) return fail(c, TGSIM_ESTATE, "probes are set up: floods need the deliveries to themselves");
+  if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor is set up: floods need the deliveries to themselves");
   uint32_t D = 1;
   for (uint32_t g = 0; g < c->N; ++g) {
     if (off[g + 1] < off[g]) return fail(c, TGSIM_EINVAL, "offsets not monotonic");
@@ -1987,6 +1992,7 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "probes need a single-shard context");
   if (c->N > 0x3FFFFFFFu) return fail(c, TGSIM_ENOTSUP, "too many instances for probe tags");
   if (c->tcp_on || !c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "probes run in message mode, without a flood graph");
+  if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor is set up: it owns the deliveries");
   for (uint32_t j = 0; j < n_order; ++j)
     if (order[j] >= c->N) return fail(c, TGSIM_EINVAL, "order[%u] is not an instance", j);
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
@@ -2096,6 +2102,275 @@ static int tgsim_probe_results_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_d
     if (n) HIPCK(c, hipMemcpy(outcome, c->d.pr.out, n, hipMemcpyDeviceToHost), "probe results");
   }
   if (t_done && c->nloc) HIPCK(c, hipMemcpy(t_done, c->d.pr.t_done, (size_t)c->nloc * 8, hipMemcpyDeviceToHost), "probe results");
+  return TGSIM_OK;
+}
+
+// ============================== storm plan reactor ==========================
+// plans/benchmarks/storm.go:117-190: the dial semaphore, DialTimeout, writesem and conn.Write
+// blocking on the send buffer, for every instance on the device. Kernels in tgsim_storm.hip, oracle
+// twin tgo_storm_*.
+
+static void storm_free(tgsim_ctx* c) {
+  StormDev& s = c->d.sm;
+  for (void* q : {(void*)s.dst, (void*)s.t_ready, (void*)s.state, (void*)s.flags, (void*)s.res, (void*)s.slot,
+                  (void*)s.t_start, (void*)s.t_synarr, (void*)s.t_ackarr, (void*)s.t_done, (void*)s.t_rep,
+                  (void*)s.emit, (void*)s.rem, (void*)s.infl, (void*)s.order, (void*)s.ring, (void*)s.claim,
+                  (void*)s.dq, (void*)s.qh, (void*)s.ql, (void*)s.nh, (void*)s.slot_t, (void*)s.hold,
+                  (void*)s.failed, (void*)s.t_last, (void*)s.sc})
+    dfree(c, q);
+  s = StormDev{};
+  c->storm_on = false;
+  c->storm_need_react = false;
+}
+
+static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg);
+extern "C" int tgsim_storm_setup(tgsim_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg) {
+  return abi_guard(c, [&] { return tgsim_storm_setup_body(c, dst, t_ready, cfg); });
+}
+static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg) {
+  if (!c || !cfg) return TGSIM_EINVAL;
+  if (cfg->outgoing == 0 || cfg->concurrent == 0 || cfg->chunk_bytes == 0 || cfg->msg_window == 0 ||
+      cfg->dial_timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->syn_bytes >= 0x80000000u ||
+      (uint64_t)cfg->chunk_bytes + cfg->header_bytes >= 0x80000000ull)
+    return fail(c, TGSIM_EINVAL, "bad storm configuration");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
+  if (c->tcp_on || !c->fl_off.empty() || c->probes)
+    return fail(c, TGSIM_ESTATE, "the storm reactor runs in message mode, without a flood graph or probes");
+  const uint64_t n_conn = (uint64_t)c->N * cfg->outgoing;
+  const uint64_t nchunks = (cfg->data_bytes + cfg->chunk_bytes - 1) / cfg->chunk_bytes;
+  if (n_conn > 0x3FFFFFFFull || nchunks * cfg->outgoing > 0x3FFFFFFFull)
+    return fail(c, TGSIM_ENOTSUP, "too many connections or chunks for the storm's packet tags");
+  if (n_conn && (!dst || !t_ready)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  for (uint64_t h = 0; h < n_conn; ++h) {
+    if (dst[h] >= c->N) return fail(c, TGSIM_EINVAL, "connection %llu: bad peer", (unsigned long long)h);
+    if (t_ready[h] < c->now) return fail(c, TGSIM_ECAUSALITY, "connection %llu: t_ready before now", (unsigned long long)h);
+  }
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  storm_free(c);
+  alloc_point(c);
+  const uint32_t O = cfg->outgoing, C = cfg->concurrent, Hc = std::min(C, O);
+  // per instance, its connections in dial FIFO order (t_ready, k): a Go channel queues blocked
+  // senders in arrival order, and a goroutine arrives when its sleep ends
+  std::vector<uint32_t> order(n_conn);
+  for (uint32_t g = 0; g < c->N; ++g) {
+    uint32_t* o = order.data() + (size_t)g * O;
+    const int64_t* tr = t_ready + (size_t)g * O;
+    for (uint32_t k = 0; k < O; ++k) o[k] = k;
+    std::stable_sort(o, o + O, [&](uint32_t a, uint32_t b) { return tr[a] < tr[b]; });
+  }
+  StormDev& s = c->d.sm;
+  const size_t nc = std::max<uint64_t>(n_conn, 1), nl = std::max<uint32_t>(c->nloc, 1);
+  const size_t claim_words = std::max<uint64_t>((n_conn * nchunks + 31) / 32, 1);
+  if (dalloc(c, &s.dst, nc) || dalloc(c, &s.t_ready, nc) || dalloc(c, &s.state, nc) || dalloc(c, &s.flags, nc) ||
+      dalloc(c, &s.res, nc) || dalloc(c, &s.slot, nc) || dalloc(c, &s.t_start, nc) || dalloc(c, &s.t_synarr, nc) ||
+      dalloc(c, &s.t_ackarr, nc) || dalloc(c, &s.t_done, nc) || dalloc(c, &s.t_rep, nc) || dalloc(c, &s.emit, nc) ||
+      dalloc(c, &s.rem, nc) || dalloc(c, &s.infl, nc) || dalloc(c, &s.order, nc) || dalloc(c, &s.ring, nc) ||
+      dalloc(c, &s.claim, claim_words) || dalloc(c, &s.dq, nl) || dalloc(c, &s.qh, nl) || dalloc(c, &s.ql, nl) ||
+      dalloc(c, &s.nh, nl) || dalloc(c, &s.slot_t, nl * C) || dalloc(c, &s.hold, nl * Hc) ||
+      dalloc(c, &s.failed, nl) || dalloc(c, &s.t_last, nl) || dalloc(c, &s.sc, 1)) {
+    storm_free(c);
+    return TGSIM_ENOMEM;
+  }
+  hipStream_t st = c->d.stream;
+  std::vector<int64_t> tmin(std::max(nl * C, nc), INT64_MIN);
+  HIPCK(c, hipMemcpyAsync(s.dst, dst, n_conn * 4, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.t_ready, t_ready, n_conn * 8, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.order, order.data(), n_conn * 4, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.slot_t, tmin.data(), nl * C * 8, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.t_last, tmin.data(), nl * 8, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.t_done, tmin.data(), nc * 8, hipMemcpyHostToDevice, st), "storm setup");
+  for (void* z : {(void*)s.state, (void*)s.flags, (void*)s.res}) HIPCK(c, hipMemsetAsync(z, 0, nc, st), "storm setup");
+  for (void* z : {(void*)s.rem, (void*)s.infl, (void*)s.emit}) HIPCK(c, hipMemsetAsync(z, 0, nc * 4, st), "storm setup");
+  HIPCK(c, hipMemsetAsync(s.claim, 0, claim_words * 4, st), "storm setup");
+  for (void* z : {(void*)s.dq, (void*)s.qh, (void*)s.ql, (void*)s.nh}) HIPCK(c, hipMemsetAsync(z, 0, nl * 4, st), "storm setup");
+  HIPCK(c, hipMemsetAsync(s.failed, 0, nl, st), "storm setup");
+  HIPCK(c, hipMemsetAsync(s.sc, 0, sizeof(StormScalars), st), "storm setup");
+  HIPCK(c, hipStreamSynchronize(st), "storm setup");  // the host vectors go out of scope
+  s.O = O;
+  s.C = C;
+  s.Hc = Hc;
+  s.nchunks = (uint32_t)nchunks;
+  s.chunk = cfg->chunk_bytes;
+  s.hdr = cfg->header_bytes;
+  s.syn = cfg->syn_bytes;
+  s.win = cfg->msg_window;
+  s.data = cfg->data_bytes;
+  s.timeout = cfg->dial_timeout_ns;
+  s.window = cfg->window_ns;
+  s.n_conn = (uint32_t)n_conn;
+  s.phase = 0;
+  c->storm_on = true;
+  c->storm_need_react = false;
+  return TGSIM_OK;
+}
+
+// The reactor stages on the device, behind the device-side count. The queue-limit bound per sender:
+// dial phase - its SYNs (one per connection) and a SYN-ACK per delivery of its last inbox; write
+// phase - at most msg_window chunks per connection (a connection's buffer).
+static void storm_staged(tgsim_ctx* c) {
+  const StormDev& s = c->d.sm;
+  c->spec.valid = false;
+  c->staged_dev = true;
+  if (s.phase == 0) {
+    c->win_m_extra += s.O;
+    c->win_m_inbox = std::max<uint32_t>(c->win_m_inbox, 1u);
+    c->win_inbox_max = std::max<uint64_t>(c->win_inbox_max, s.n_conn);
+  } else {
+    c->win_m_extra += (uint64_t)s.win * s.O;
+  }
+}
+
+static int tgsim_storm_start_body(tgsim_ctx* c);
+extern "C" int tgsim_storm_start(tgsim_ctx* c) {
+  return abi_guard(c, [&] { return tgsim_storm_start_body(c); });
+}
+static int tgsim_storm_start_body(tgsim_ctx* c) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->d.sm.phase != 0) return fail(c, TGSIM_ESTATE, "the storm's dials have started");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (int rc = react_owed(c)) return rc;
+  if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
+  HIPCK(c, launch_storm_start(c->d, c->staged_dev, c->n_staged, c->now), "storm start");
+  storm_staged(c);
+  return TGSIM_OK;
+}
+
+static int storm_read_scalars(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  StormScalars ss;
+  HIPCK(c, hipMemcpyAsync(&ss, c->d.sm.sc, sizeof(ss), hipMemcpyDeviceToHost, c->d.stream), "storm react");
+  const int rc = sync_and_check(c);
+  if (rc) return rc;
+  if (next_end) *next_end = ss.next_end;
+  if (n_active) *n_active = ss.n_active;
+  return TGSIM_OK;
+}
+
+static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active);
+extern "C" int tgsim_storm_react(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  return abi_guard(c, [&] { return tgsim_storm_react_body(c, next_end, n_active); });
+}
+static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->storm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
+  const bool on_dev = c->n_status_last == kStatusOnDevice;
+  HIPCK(c, launch_storm_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                              on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
+  storm_staged(c);
+  c->storm_need_react = false;
+  if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
+  return storm_read_scalars(c, next_end, n_active);
+}
+
+static int tgsim_storm_state_device_body(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active);
+extern "C" int tgsim_storm_state_device(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active) {
+  return abi_guard(c, [&] { return tgsim_storm_state_device_body(c, next_end, n_active); });
+}
+static int tgsim_storm_state_device_body(tgsim_ctx* c, const int64_t** next_end, const uint32_t** n_active) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (next_end) *next_end = &c->d.sm.sc->next_end;
+  if (n_active) *n_active = &c->d.sm.sc->n_active;
+  return TGSIM_OK;
+}
+
+static int tgsim_storm_dials_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap);
+extern "C" int tgsim_storm_dials(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  return abi_guard(c, [&] { return tgsim_storm_dials_body(c, outcome, t_done, cap); });
+}
+static int tgsim_storm_dials_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  const size_t n = c->d.sm.n_conn;
+  if ((outcome || t_done) && cap < n) return fail(c, TGSIM_ECAPACITY, "dial capacity %zu < %zu", cap, n);
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  if (outcome && n) HIPCK(c, hipMemcpy(outcome, c->d.sm.res, n, hipMemcpyDeviceToHost), "storm dials");
+  if (t_done && n) HIPCK(c, hipMemcpy(t_done, c->d.sm.t_done, n * 8, hipMemcpyDeviceToHost), "storm dials");
+  return TGSIM_OK;
+}
+
+static int tgsim_storm_write_start_body(tgsim_ctx* c, int64_t t0);
+extern "C" int tgsim_storm_write_start(tgsim_ctx* c, int64_t t0) {
+  return abi_guard(c, [&] { return tgsim_storm_write_start_body(c, t0); });
+}
+static int tgsim_storm_write_start_body(tgsim_ctx* c, int64_t t0) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->d.sm.phase != 0) return fail(c, TGSIM_ESTATE, "the write phase has started");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (int rc = react_owed(c)) return rc;
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
+  // a goroutine writes only after its dial succeeded and "outgoing-dials-done" released, which needs
+  // every dial (storm.go:156): the write phase starts once all of them are OK
+  std::vector<uint8_t> res(c->d.sm.n_conn);
+  if (!res.empty()) HIPCK(c, hipMemcpy(res.data(), c->d.sm.res, res.size(), hipMemcpyDeviceToHost), "storm write start");
+  for (size_t h = 0; h < res.size(); ++h)
+    if (res[h] != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %zu has not dialled successfully", h);
+  c->d.sm.phase = 1;
+  HIPCK(c, launch_storm_write_start(c->d, c->staged_dev, c->n_staged, t0), "storm write start");
+  storm_staged(c);
+  return TGSIM_OK;
+}
+
+static int tgsim_storm_results_body(tgsim_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot);
+extern "C" int tgsim_storm_results(tgsim_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot) {
+  return abi_guard(c, [&] { return tgsim_storm_results_body(c, failed, t_last, cap, tot); });
+}
+static int tgsim_storm_results_body(tgsim_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if ((failed || t_last) && cap < c->nloc) return fail(c, TGSIM_ECAPACITY, "result capacity %zu < %u", cap, c->nloc);
+  int rc = sync_and_check(c);
+  if (rc) return rc;
+  const StormDev& s = c->d.sm;
+  const size_t n = s.n_conn;
+  std::vector<uint32_t> infl(n), rem(n);
+  std::vector<uint8_t> res(n), fl(c->nloc);
+  if (n) {
+    HIPCK(c, hipMemcpy(infl.data(), s.infl, n * 4, hipMemcpyDeviceToHost), "storm results");
+    HIPCK(c, hipMemcpy(rem.data(), s.rem, n * 4, hipMemcpyDeviceToHost), "storm results");
+    HIPCK(c, hipMemcpy(res.data(), s.res, n, hipMemcpyDeviceToHost), "storm results");
+  }
+  if (c->nloc) HIPCK(c, hipMemcpy(fl.data(), s.failed, c->nloc, hipMemcpyDeviceToHost), "storm results");
+  for (size_t h = 0; h < n; ++h)
+    if (infl[h]) fl[h / s.O] = 1;  // still in flight: it never arrived
+  if (failed) memcpy(failed, fl.data(), c->nloc);
+  if (t_last && c->nloc) HIPCK(c, hipMemcpy(t_last, s.t_last, (size_t)c->nloc * 8, hipMemcpyDeviceToHost), "storm results");
+  if (tot) {
+    StormScalars ss;
+    HIPCK(c, hipMemcpy(&ss, s.sc, sizeof(ss), hipMemcpyDeviceToHost), "storm results");
+    *tot = tgsim_storm_totals{};
+    tot->chunks_written = ss.written;
+    tot->chunks_delivered = ss.delivered;
+    tot->chunks_failed = ss.failed;
+    tot->bytes_written = ss.bytes;
+    for (size_t h = 0; h < n; ++h) {
+      tot->dials_ok += res[h] == TGSIM_PROBE_OK;
+      tot->dials_failed += res[h] == TGSIM_PROBE_REFUSED || res[h] == TGSIM_PROBE_TIMEOUT;
+      tot->dials_pending += res[h] == TGSIM_PROBE_NONE;
+      tot->conns_writing += s.phase == 1 && (rem[h] || infl[h]);
+    }
+  }
+  return TGSIM_OK;
+}
+
+static int tgsim_storm_end_body(tgsim_ctx* c);
+extern "C" int tgsim_storm_end(tgsim_ctx* c) {
+  return abi_guard(c, [&] { return tgsim_storm_end_body(c); });
+}
+static int tgsim_storm_end_body(tgsim_ctx* c) {
+  if (!c) return TGSIM_EINVAL;
+  if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
+  storm_free(c);
   return TGSIM_OK;
 }
 
@@ -2359,6 +2634,7 @@ static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "messages already staged");
   if (!c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
   if (c->probes) return fail(c, TGSIM_ESTATE, "probes are set up: probes run in message mode");
+  if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor is set up: it runs in message mode");
   tgsim_tcp_config t = *cfg;
   if (!t.mss) t.mss = 1448;
   if (!t.header_bytes) t.header_bytes = 52;
@@ -2957,7 +3233,7 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
 int snap_refusal(tgsim_ctx* c) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "snapshot/restore: inside a window");
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "snapshot/restore: messages are staged");
-  if (c->tcp_on || c->tp_n || !c->fl_off.empty() || c->probes)
+  if (c->tcp_on || c->tp_n || !c->fl_off.empty() || c->probes || c->storm_on)
     return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics, flood graphs and probes are not captured");
   return TGSIM_OK;
 }

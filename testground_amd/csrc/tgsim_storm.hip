@@ -1,0 +1,451 @@
+// tgsim_storm.hip — device side of the storm plan reactor (tgsim_storm_*): the dial
+// and write pacing of plans/benchmarks/storm.go:117-190 for every instance at once, so a storm plan
+// run costs the host O(1) per window whatever its instance count. Oracle twin: tgo_storm_*.
+//
+// After each window, with no host round trip:
+//   k_storm_pre   blocks [0, nb): the window's staged packets - a SYN its dialler's route refused,
+//                 a chunk that failed (no copy queued: its buffer slot frees, its instance failed);
+//                 blocks [nb, 2 nb): the window's deliveries - first arrivals of SYNs (at the
+//                 listener) and SYN-ACKs (at the dialler) by atomicMin, the first copy of each chunk
+//                 by a claim bit (its buffer slot frees); block 0 also resets the step's reductions
+//   k_storm_step  one thread per instance: dial phase - the SYN-ACKs its peers owe, each waiting
+//                 dial's end (refused / SYN-ACK before the deadline / deadline passed), then the
+//                 dial semaphore's FIFO admits dials into the free slots (those due before the next
+//                 window's end); write phase - the writesem round (storm.go:158-183) over the room
+//                 the buffers have; the staged slots reserved once per block behind sc->n_msgs_dev;
+//                 the last workgroup proposes the next window's end
+// A connection's state lives in its own slots, written by its instance's thread; the only shared
+// updates are the arrival minima, the claim bits, the buffer counts and the per-block reductions.
+#include <algorithm>
+
+#include "tgsim_dev.h"
+
+namespace tgsim {
+
+namespace {
+
+constexpr uint32_t kTagMask = 0x3FFFFFFFu;
+constexpr int64_t kNone = INT64_MAX;
+constexpr int64_t kBusy = INT64_MAX;  // a held semaphore slot
+enum : uint8_t { kSleep = 0, kWait = 1, kDone = 2 };
+enum : uint32_t { kEmitSynAck = 1u, kEmitSyn = 2u };
+enum : uint32_t { kModeStart = 0, kModeReact = 1, kModeWrites = 2 };
+
+__device__ __forceinline__ bool failed_code(uint32_t st) {
+  const uint32_t code = st & 0x0Fu;
+  return code != TGSIM_ST_QUEUED && code != TGSIM_ST_LOCAL;
+}
+__device__ __forceinline__ bool refused_code(uint32_t st) {
+  const uint32_t code = st & 0x0Fu;
+  return code == TGSIM_ST_DROPPED || code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE;
+}
+
+// per block: the sum of v into *dst with one atomic
+__device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long long v, unsigned long long* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += red[w];
+    if (t) atomicAdd(dst, t);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ m_src,
+                                                      const uint32_t* __restrict__ m_dst,
+                                                      const uint32_t* __restrict__ m_seq, uint32_t n_host,
+                                                      const uint32_t* n_dev, const uint32_t* __restrict__ o_src,
+                                                      const uint32_t* __restrict__ o_dst,
+                                                      const uint32_t* __restrict__ o_seq,
+                                                      const int64_t* __restrict__ o_t, DevScalars* sc, StormDev s,
+                                                      uint32_t nb, uint32_t set_base, uint32_t base_host) {
+  __shared__ unsigned long long red[kBlock / 64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    s.sc->min_dl = kNone;
+    s.sc->next_start = kNone;
+    s.sc->active = 0;
+    s.sc->done = 0;
+    if (set_base) sc->n_msgs_dev = base_host;  // nothing in this launch reads it
+  }
+  const uint32_t O = s.O;
+  unsigned long long cnt = 0;
+  if (blockIdx.x < nb) {  // the window's packets
+    const uint32_t n = n_dev ? *n_dev : n_host;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
+      const uint32_t sq = m_seq[i], tag = sq >> 30;
+      if (tag == 1u) {  // a SYN: refused by the dialler's route
+        if (!refused_code(status[i])) continue;
+        const size_t h = (size_t)m_src[i] * O + (sq & kTagMask);
+        if (s.state[h] == kWait && s.dst[h] == m_dst[i]) s.flags[h] |= 1u;
+      } else if (tag == 2u) {  // a chunk that no copy of entered the egress queue
+        if (!failed_code(status[i])) continue;
+        const uint32_t g = m_src[i], k = (sq & kTagMask) / s.nchunks;
+        atomicSub(&s.infl[(size_t)g * O + k], 1u);
+        s.failed[g] = 1;
+        ++cnt;
+      }
+    }
+    block_add(&s.sc->failed, cnt, red);
+  } else {  // the window's deliveries
+    const uint32_t n = sc->n_out;
+    for (uint32_t i = (blockIdx.x - nb) * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
+      const uint32_t sq = o_seq[i], tag = sq >> 30;
+      if (tag == 1u) {  // a SYN at its listener
+        const size_t h = (size_t)o_src[i] * O + (sq & kTagMask);
+        if (s.state[h] == kWait && s.dst[h] == o_dst[i])
+          atomicMin(reinterpret_cast<long long*>(&s.t_synarr[h]), (long long)o_t[i]);
+      } else if (tag == 3u) {  // a SYN-ACK at its dialler
+        const size_t h = sq & kTagMask;
+        if (h < s.n_conn && h / O == o_dst[i] && s.dst[h] == o_src[i] && s.state[h] == kWait && (s.flags[h] & 2u))
+          atomicMin(reinterpret_cast<long long*>(&s.t_ackarr[h]), (long long)o_t[i]);
+      } else if (tag == 2u) {  // a chunk: its first copy frees a buffer slot
+        const uint32_t c = sq & kTagMask, k = c / s.nchunks;
+        const size_t h = (size_t)o_src[i] * O + k;
+        const uint64_t bit = (uint64_t)h * s.nchunks + (c - k * s.nchunks);
+        const uint32_t m = 1u << (bit & 31u);
+        if (!(atomicOr(&s.claim[bit >> 5], m) & m)) {
+          atomicSub(&s.infl[h], 1u);
+          ++cnt;
+        }
+      }
+    }
+    block_add(&s.sc->delivered, cnt, red);
+  }
+}
+
+// per block: the minimum deadline / start time of its instances and the active count
+__device__ __forceinline__ void block_reduce(StormDev& s, int64_t dl, int64_t ns, uint32_t act) {
+  __shared__ int64_t s_dl[kBlock / 64], s_ns[kBlock / 64];
+  __shared__ uint32_t s_n[kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t y = __shfl_xor(dl, o), z = __shfl_xor(ns, o);
+    dl = y < dl ? y : dl;
+    ns = z < ns ? z : ns;
+    act += (uint32_t)__shfl_xor(act, o);
+  }
+  if (lane_id() == 0) { s_dl[threadIdx.x >> 6] = dl; s_ns[threadIdx.x >> 6] = ns; s_n[threadIdx.x >> 6] = act; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t m = s_dl[0], q = s_ns[0];
+    uint32_t n = s_n[0];
+    for (int w = 1; w < kBlock / 64; ++w) {
+      m = s_dl[w] < m ? s_dl[w] : m;
+      q = s_ns[w] < q ? s_ns[w] : q;
+      n += s_n[w];
+    }
+    if (m != kNone) atomicMin(reinterpret_cast<long long*>(&s.sc->min_dl), (long long)m);
+    if (q != kNone) atomicMin(reinterpret_cast<long long*>(&s.sc->next_start), (long long)q);
+    if (n) atomicAdd(&s.sc->active, n);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t chunk_payload(const StormDev& s, uint32_t j) {
+  return j + 1 < s.nchunks ? s.chunk : (uint32_t)(s.data - (uint64_t)j * s.chunk);
+}
+
+__device__ __forceinline__ void storm_end(StormDev& s, const DevScalars* sc, int64_t t_end);
+
+// Dial phase of instance l: resolve its waiting dials (react), then admit dials. Returns the messages
+// to stage (emit[h] bits); dl / ns / act: its reductions.
+__device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t g, bool resolve, int64_t H,
+                                              int64_t t_end, int64_t& dl_min, int64_t& ns_min, uint32_t& act) {
+  const uint32_t O = s.O, C = s.C;
+  const size_t base = (size_t)g * O;
+  uint32_t cnt = 0;
+  for (uint32_t k = 0; k < O; ++k) {
+    const size_t h = base + k;
+    s.emit[h] = 0;
+    if (!resolve || s.state[h] != kWait) continue;
+    const int64_t dl = s.t_start[h] + s.timeout;
+    bool reply_pending = false;
+    const int64_t sa = s.t_synarr[h];
+    if (sa != kNone && !(s.flags[h] & 2u)) {  // the listener answers the SYN's first arrival
+      const int64_t trep = sa > H ? sa : H;
+      s.t_rep[h] = trep;
+      s.emit[h] = kEmitSynAck;
+      s.flags[h] |= 2u;
+      reply_pending = trep < dl;
+      ++cnt;
+    }
+    s.t_synarr[h] = kNone;
+    const int64_t aa = s.t_ackarr[h];
+    uint8_t out = TGSIM_PROBE_NONE;
+    int64_t te = 0;
+    if (s.flags[h] & 1u) { out = TGSIM_PROBE_REFUSED; te = s.t_start[h]; }
+    else if (aa != kNone && aa < dl) { out = TGSIM_PROBE_OK; te = aa; }
+    else if (dl < t_end && !reply_pending) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
+    if (out != TGSIM_PROBE_NONE) {
+      s.state[h] = kDone;
+      s.res[h] = out;
+      s.t_done[h] = te;
+      s.slot_t[(size_t)l * C + s.slot[h]] = te;  // `<-sem`: the slot is free from the dial's end
+    } else {
+      ++act;
+      dl_min = dl < dl_min ? dl : dl_min;
+    }
+  }
+  // the semaphore admits dials in FIFO order while a slot is free: dial at max(t_ready, slot free, H)
+  uint32_t q = s.dq[l];
+  while (q < O) {
+    uint32_t best = C;
+    int64_t bt = kBusy;
+    for (uint32_t c = 0; c < C; ++c) {
+      const int64_t t = s.slot_t[(size_t)l * C + c];
+      if (t < bt) { bt = t; best = c; }
+    }
+    if (best == C) break;  // every slot held by a waiting dial
+    const uint32_t k = s.order[base + q];
+    const size_t h = base + k;
+    int64_t t0 = s.t_ready[h];
+    t0 = bt > t0 ? bt : t0;
+    t0 = H > t0 ? H : t0;
+    if (t0 >= t_end + s.window) {  // still asleep (or queued) past the next window
+      ns_min = t0 < ns_min ? t0 : ns_min;
+      break;
+    }
+    s.slot_t[(size_t)l * C + best] = kBusy;
+    s.slot[h] = best;
+    s.state[h] = kWait;
+    s.t_start[h] = t0;
+    s.flags[h] = 0;
+    s.t_synarr[h] = kNone;
+    s.t_ackarr[h] = kNone;
+    s.emit[h] |= kEmitSyn;
+    ++cnt;
+    ++act;
+    const int64_t dl = t0 + s.timeout;
+    dl_min = dl < dl_min ? dl : dl_min;
+    ++q;
+  }
+  s.dq[l] = q;
+  act += O - q;  // asleep, not yet admitted
+  return cnt;
+}
+
+// Write phase of instance l at time t: one writesem round (storm.go:158-183). Goroutines take the
+// semaphore in FIFO order; a conn.Write whose chunk fits the buffer returns and its goroutine queues
+// again for the next chunk, one that does not fit blocks holding its slot (the holders retry first,
+// in order). Returns the chunks written (emit[h] per connection).
+__device__ __forceinline__ uint32_t write_step(StormDev& s, uint32_t l, uint32_t g, uint32_t& act) {
+  const uint32_t O = s.O, C = s.C, win = s.win;
+  const size_t base = (size_t)g * O;
+  uint32_t* ring = s.ring + base;
+  uint32_t* hold = s.hold + (size_t)l * s.Hc;
+  uint32_t qh = s.qh[l], ql = s.ql[l], nh = s.nh[l];
+  for (uint32_t k = 0; k < O; ++k) s.emit[base + k] = 0;
+  uint32_t cnt = 0;
+  bool progress = true;
+  while (progress) {
+    progress = false;
+    uint32_t keep = 0;
+    for (uint32_t i = 0; i < nh; ++i) {  // blocked writers whose buffer drained
+      const uint32_t k = hold[i];
+      const size_t h = base + k;
+      if (s.infl[h] + s.emit[h] < win) {
+        s.emit[h] += 1;
+        const uint32_t r = --s.rem[h];
+        ++cnt;
+        progress = true;
+        if (r) { ring[(qh + ql) % O] = k; ++ql; }
+      } else {
+        hold[keep++] = k;
+      }
+    }
+    nh = keep;
+    while (nh < C && ql > 0) {  // free slots go to the queue's head
+      const uint32_t k = ring[qh];
+      qh = (qh + 1) % O;
+      --ql;
+      const size_t h = base + k;
+      if (s.infl[h] + s.emit[h] < win) {
+        s.emit[h] += 1;
+        const uint32_t r = --s.rem[h];
+        ++cnt;
+        progress = true;
+        if (r) { ring[(qh + ql) % O] = k; ++ql; }
+      } else {
+        hold[nh++] = k;
+      }
+    }
+  }
+  s.qh[l] = qh;
+  s.ql[l] = ql;
+  s.nh[l] = nh;
+  for (uint32_t k = 0; k < O; ++k) {
+    const size_t h = base + k;
+    const uint32_t f = s.infl[h] + s.emit[h];
+    s.infl[h] = f;
+    act += (s.rem[h] || f) ? 1u : 0u;
+  }
+  return cnt;
+}
+
+__global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* sc, uint32_t lo, uint32_t nloc,
+                                                       uint32_t mode, int64_t H_host, int64_t tend_host, uint32_t cap,
+                                                       uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
+                                                       uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
+                                                       int64_t* __restrict__ m_t) {
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ unsigned long long red64[kBlock / 64];
+  __shared__ uint32_t sbase;
+  const bool react = mode == kModeReact;
+  const int64_t H = react ? sc->T : H_host, t_end = react ? sc->t_end : tend_host;
+  const bool writes = s.phase == 1;
+  const uint32_t O = s.O;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < nloc; b0 += gridDim.x * kBlock) {  // block-uniform
+    const uint32_t l = b0 + threadIdx.x;
+    int64_t dl = kNone, ns = kNone;
+    uint32_t act = 0, cnt = 0;
+    const uint32_t g = lo + l;
+    if (l < nloc) cnt = writes ? write_step(s, l, g, act) : dial_step(s, l, g, react, H, t_end, dl, ns, act);
+    if (writes && cnt && l < nloc) s.t_last[l] = t_end;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(cnt, red, tot);
+    if (threadIdx.x == 0) sbase = tot ? reserve_staged(&sc->n_msgs_dev, tot, cap) : 0u;
+    __syncthreads();
+    unsigned long long bytes = 0;
+    if (cnt) {
+      uint32_t w = sbase + ex;
+      const size_t base = (size_t)g * O;
+      for (uint32_t k = 0; k < O; ++k) {
+        const size_t h = base + k;
+        const uint32_t e = s.emit[h];
+        if (!e) continue;
+        if (writes) {  // chunks j0 .. j0 + e - 1 at t_end
+          const uint32_t j0 = s.nchunks - s.rem[h] - e;
+          for (uint32_t j = j0; j < j0 + e; ++j, ++w) {
+            const uint32_t pay = chunk_payload(s, j);
+            bytes += pay;
+            if (w < cap) {
+              m_src[w] = g; m_dst[w] = s.dst[h]; m_seq[w] = TGSIM_STORM_DATA | (k * s.nchunks + j);
+              m_size[w] = pay + s.hdr; m_t[w] = t_end;
+            } else {
+              atomicOr(&sc->err, ERR_CAP_M);
+            }
+          }
+        } else {
+          if (e & kEmitSynAck) {  // from the listener, on the dialler's connection id
+            if (w < cap) {
+              m_src[w] = s.dst[h]; m_dst[w] = g; m_seq[w] = TGSIM_STORM_SYNACK | (uint32_t)h; m_size[w] = s.syn;
+              m_t[w] = s.t_rep[h];
+            } else {
+              atomicOr(&sc->err, ERR_CAP_M);
+            }
+            ++w;
+          }
+          if (e & kEmitSyn) {
+            if (w < cap) {
+              m_src[w] = g; m_dst[w] = s.dst[h]; m_seq[w] = TGSIM_STORM_SYN | k; m_size[w] = s.syn;
+              m_t[w] = s.t_start[h];
+            } else {
+              atomicOr(&sc->err, ERR_CAP_M);
+            }
+            ++w;
+          }
+        }
+      }
+    }
+    __syncthreads();  // sbase is rewritten by the next round
+    if (writes) {
+      block_add(&s.sc->written, cnt, red64);
+      block_add(&s.sc->bytes, bytes, red64);
+    }
+    block_reduce(s, dl, ns, act);
+  }
+  // the last workgroup to finish proposes the next window's end
+  __shared__ uint32_t s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&s.sc->done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
+    __threadfence();
+    storm_end(s, sc, t_end);
+  }
+}
+
+// every k_storm_step workgroup's reductions and reservations are done: read with device-scope atomic
+// loads (another XCD's L2 may hold the lines)
+__device__ __forceinline__ void storm_end(StormDev& s, const DevScalars* sc, int64_t t_end) {
+  int64_t ne = t_end + s.window;
+  const uint32_t act = __hip_atomic_load(&s.sc->active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t m = __hip_atomic_load(&s.sc->min_dl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t q = __hip_atomic_load(&s.sc->next_start, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t staged = __hip_atomic_load(const_cast<uint32_t*>(&sc->n_msgs_dev), __ATOMIC_ACQUIRE,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  if (staged == 0 && sc->arena_used == 0 && act) {  // idle: jump to the next deadline or dial
+    int64_t cand = m != kNone ? m + 1 : kNone;
+    cand = q < cand ? q : cand;
+    if (cand != kNone && cand > ne) ne = cand;
+  }
+  s.sc->next_end = ne;
+  s.sc->n_active = act;
+}
+
+__global__ void k_storm_reset(StormDev s, DevScalars* sc, uint32_t set_base, uint32_t base_host) {
+  if (threadIdx.x == 0) {
+    s.sc->min_dl = kNone;
+    s.sc->next_start = kNone;
+    s.sc->active = 0;
+    s.sc->done = 0;
+    if (set_base) sc->n_msgs_dev = base_host;
+  }
+}
+
+// the write phase's start: every connection's goroutine queued on writesem in connection order
+__global__ __launch_bounds__(kBlock) void k_storm_write_init(StormDev s, uint32_t lo, uint32_t nloc) {
+  for (uint32_t l = blockIdx.x * kBlock + threadIdx.x; l < nloc; l += gridDim.x * kBlock) {
+    const size_t base = (size_t)(lo + l) * s.O;
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < s.O; ++k) {
+      s.rem[base + k] = s.nchunks;
+      s.infl[base + k] = 0;
+      if (s.nchunks) s.ring[base + n++] = k;
+    }
+    s.qh[l] = 0;
+    s.ql[l] = n;
+    s.nh[l] = 0;
+  }
+}
+
+unsigned grid_for(uint32_t n) {
+  return std::max(1u, std::min<unsigned>((n + kBlock - 1) / kBlock, (unsigned)kStreamBlocks));
+}
+
+}  // namespace
+
+hipError_t launch_storm_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t_now) {
+  hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
+                     (uint32_t)kModeStart, t_now, t_now, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_write_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t0) {
+  hipLaunchKernelGGL(k_storm_write_init, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.lo, d.nloc);
+  hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
+                     (uint32_t)kModeWrites, t0, t0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                              const uint32_t* n_status_dev) {
+  ProfScope ps_(d, KID_PROBE);
+  constexpr uint32_t nb = kStreamBlocks / 2;
+  hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
+                     n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, d.sm, nb,
+                     base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
+                     (uint32_t)kModeReact, (int64_t)0, (int64_t)0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size,
+                     d.m_t);
+  return hipGetLastError();
+}
+
+}  // namespace tgsim

@@ -297,74 +297,6 @@ class PlanEnv:
         self._tw_keys.append(keys)
         return keys
 
-    def dial(self, src, dst, t_ready, limit: int, timeout_ns: int, syn_size: int = TCP_OVERHEAD):
-        """net.DialTimeout under a per-instance semaphore of `limit` (plans/benchmarks/storm.go:
-        141-152: `sem <- struct{}{}` before the dial, `<-sem` after it): dial i waits from t_ready[i]
-        for a free slot of its instance (FIFO, as a Go channel queues blocked senders), then sends a
-        SYN that its peer answers at first arrival; it ends at the SYN-ACK's first arrival (ok), at
-        once when its own route refuses it, or at the timeout. Returns (ok, t_end) per dial."""
-        src = np.asarray(src, np.int64)
-        dst = np.asarray(dst, np.int64)
-        t_ready = np.asarray(t_ready, np.int64)
-        m = len(src)
-        ok = np.zeros(m, bool)
-        t_done = np.full(m, NEVER, np.int64)
-        t_start = np.full(m, NEVER, np.int64)
-        req = np.zeros(m, np.uint64)
-        rep = np.zeros(m, np.uint64)
-        answered = np.zeros(m, bool)
-        active = np.zeros(m, bool)
-        # per instance: dials in FIFO order (t_ready, index) and the times its slots fall free
-        waiting = {}
-        for i in np.lexsort((np.arange(m), t_ready)):
-            waiting.setdefault(int(src[i]), []).append(int(i))
-        free = {g: [-(1 << 62)] * limit for g in waiting}
-        key_to = {}
-        while True:
-            for g, q in waiting.items():   # start what the free slots allow
-                fr = free[g]
-                while q and fr:
-                    i = q.pop(0)
-                    fr.sort()
-                    t0 = max(int(t_ready[i]), fr.pop(0))
-                    t_start[i] = t0
-                    req[i] = self.send([src[i]], [dst[i]], syn_size, [t0])[0]
-                    key_to[int(req[i])] = i
-                    active[i] = True
-            if not active.any() and not any(waiting.values()):
-                break
-            idle = not self._pend and self.sim.stats()["inflight"] == 0
-            if idle and active.any():
-                # only timeouts can end the active dials: jump to the first one
-                t_next = int((t_start[active] + timeout_ns).min()) + 1
-                d = self.step(max(t_next, self.sim.now + self.window_ns))
-            else:
-                d = self.step()
-            if len(d["t_deliver"]):
-                k = self.key(d["src"], d["seq"])
-                for kk, tt in zip(k.tolist(), d["t_deliver"].tolist()):
-                    i = key_to.get(kk)
-                    if i is None:
-                        continue
-                    if kk == int(req[i]) and not answered[i]:          # SYN at the listener: SYN-ACK
-                        rep[i] = self.send([dst[i]], [src[i]], syn_size, [tt])[0]
-                        key_to[int(rep[i])] = i
-                        answered[i] = True
-                    elif answered[i] and kk == int(rep[i]) and active[i] and tt < t_start[i] + timeout_ns:
-                        ok[i], t_done[i], active[i] = True, tt, False
-                        free[int(src[i])].append(tt)
-            idx = np.flatnonzero(active)
-            if len(idx):
-                st = self.status_of(req[idx]) & 0x0F
-                refused = np.isin(st, (A.ST_DROPPED, A.ST_REJECTED, A.ST_UNREACHABLE))
-                late = self.sim.now >= t_start[idx] + timeout_ns
-                for i, rf, lt in zip(idx.tolist(), refused.tolist(), late.tolist()):
-                    if rf or lt:
-                        t_done[i] = int(t_start[i]) + (0 if rf else timeout_ns)
-                        active[i] = False
-                        free[int(src[i])].append(int(t_done[i]))
-        return ok, t_done
-
     def probe(self, order, req_size: int, rep_size: int, timeout_ns: int, t0: int, window_ns: int | None = None):
         """Every instance probes order[...] (itself excluded) one request/reply at a time, the next
         probe leaving when the previous one ended (tgsim_probe_*): the sequential
@@ -649,11 +581,10 @@ def storm(env: PlanEnv) -> np.ndarray:
     env.bytes_sent = 0
     if env.tcp and not env.tcp_acks:
         raise ValueError("storm over TCP writes into connections: it needs tcp_acks = true (the ACK clock)")
-    if env.tcp:
-        conn = env.sim.tcp_connect(src, dst)
-        ok, t_dial = _tcp_dials(env, conn, src, dst, t_ready, limit)
-    else:
-        ok, t_dial = env.dial(src, dst, t_ready, limit, STORM_DIAL_TIMEOUT_NS)
+    if not env.tcp:
+        return _storm_device(env, dst, t_ready, outgoing, limit, size)
+    conn = env.sim.tcp_connect(src, dst)
+    ok, t_dial = _tcp_dials(env, conn, src, dst, t_ready, limit)
     env.dials_ok = int(ok.sum())
     res = np.ones(n, bool)
     if not ok.all():
@@ -727,6 +658,64 @@ def storm(env: PlanEnv) -> np.ndarray:
     env.delivered_chunks = int((arr != NEVER).sum())
     env.overlimit = int(env.sim.stats()["overlimit"])
     return res
+
+
+def _storm_windows(env: PlanEnv, t_first: int, deadline: int) -> bool:
+    """Windows at the storm reactor's proposed ends until no connection is active; False if
+    simulated time passed the deadline first. Host work per window is O(1): one window and one
+    reaction, whose proposal and active count are the only values read back."""
+    ne = t_first + env.window_ns
+    while True:
+        env.sim.advance(ne)
+        env.storm_windows += 1
+        ne, act = env.sim.storm_react()
+        if act == 0:
+            return True
+        if env.sim.now > deadline:
+            return False
+
+
+def _storm_device(env: PlanEnv, dst, t_ready, outgoing: int, limit: int, size: int) -> np.ndarray:
+    """The message-mode storm on the device reactor (tgsim_storm_*): dials under
+    `sem` with DialTimeout (storm.go:141-152), SignalAndWait("outgoing-dials-done", N * outgoing)
+    (:156), then 4 KiB conn.Writes under `writesem` (:158-183), each connection's send buffer holding
+    STORM_MSG_WINDOW chunks; SignalAndWait("done writing", N) at each instance's last write (:190)."""
+    n, sim = env.n, env.sim
+    env.storm_windows = 0
+    sim.storm_setup(dst, t_ready, outgoing=outgoing, concurrent=limit, data_bytes=size, chunk_bytes=TCP_CHUNK,
+                    header_bytes=TCP_OVERHEAD, syn_bytes=TCP_OVERHEAD, msg_window=STORM_MSG_WINDOW,
+                    dial_timeout_ns=STORM_DIAL_TIMEOUT_NS, window_ns=env.window_ns)
+    try:
+        sim.storm_start()
+        _storm_windows(env, sim.now, STORM_CTX_NS)
+        res, t_dial = sim.storm_dials()
+        ok = res == A.PROBE_OK
+        env.dials_ok = int(ok.sum())
+        env.bytes_sent = 0
+        if not ok.all():
+            src = np.repeat(np.arange(n), outgoing)
+            for i in np.flatnonzero(~ok)[:5]:
+                env.fail(f"instance {src[i]}: couldnt dial {dst[i]}")
+            env.fail("outgoing-dials-done never released (a failed dial does not signal): context deadline exceeded")
+            return np.zeros(n, bool)
+        _, t_b = env.sync.signal_and_wait("outgoing-dials-done", np.repeat(np.arange(n), outgoing), t_dial,
+                                          n * outgoing)
+        t_w = max(int(t_b), sim.now)
+        sim.storm_write_start(t_w)
+        if not _storm_windows(env, t_w, STORM_CTX_NS):
+            env.fail("writes still blocked at the 3000 s context")
+            return np.zeros(n, bool)
+        failed, t_last, tot = sim.storm_results()
+    finally:
+        sim.storm_end()
+    env.bytes_sent = int(tot["bytes_written"])
+    env.delivered_chunks = int(tot["chunks_delivered"])
+    env.storm_totals = tot
+    # wg.Wait(): the last conn.Write of each instance returned; then SignalAndWait("done writing", N)
+    t_last = np.where(t_last == np.iinfo(np.int64).min, int(t_b), t_last)
+    env.sync.signal_and_wait("done writing", np.arange(n), t_last, n)
+    env.overlimit = int(sim.stats()["overlimit"])
+    return ~failed
 
 
 def _tcp_dials(env: PlanEnv, conn, src, dst, t_ready, limit: int):

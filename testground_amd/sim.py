@@ -523,6 +523,57 @@ class Simulator:
         self._check(self.lib.probe_results(self._ctx, _ptr(out), _ptr(t), out.size))
         return out, t
 
+    # ---- storm plan reactor (tgsim_storm_*) ----------------------------------
+    def storm_setup(self, dst, t_ready, *, outgoing: int, concurrent: int, data_bytes: int, chunk_bytes: int = 4096,
+                    header_bytes: int = 66, syn_bytes: int = 66, msg_window: int = 10,
+                    dial_timeout_ns: int = 30 * 10**9, window_ns: int = 10**6) -> None:
+        d = np.ascontiguousarray(dst, dtype=np.uint32)
+        t = np.ascontiguousarray(t_ready, dtype=np.int64)
+        assert len(d) == len(t) == self.cfg.n_instances * outgoing
+        self._storm_n = len(d)
+        cfg = A.StormConfig(outgoing, concurrent, chunk_bytes, header_bytes, data_bytes, syn_bytes, msg_window,
+                            dial_timeout_ns, window_ns)
+        self._check(self.lib.storm_setup(self._ctx, _ptr(d), _ptr(t), C.byref(cfg)))
+
+    def storm_start(self) -> None:
+        self._check(self.lib.storm_start(self._ctx))
+
+    def storm_react(self, wait: bool = True):
+        """After a window. wait: (proposed next window end, connections still active); else None."""
+        if not wait:
+            self._check(self.lib.storm_react(self._ctx, None, None))
+            return None
+        ne, act = C.c_int64(), C.c_uint32()
+        self._check(self.lib.storm_react(self._ctx, C.byref(ne), C.byref(act)))
+        return ne.value, act.value
+
+    def storm_state_device(self) -> tuple[int, int]:
+        a, b = C.c_void_p(), C.c_void_p()
+        self._check(self.lib.storm_state_device(self._ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def storm_dials(self) -> tuple[np.ndarray, np.ndarray]:
+        """(outcome TGSIM_PROBE_* per connection, its end time)."""
+        out = np.zeros(self._storm_n, np.uint8)
+        t = np.zeros(self._storm_n, np.int64)
+        self._check(self.lib.storm_dials(self._ctx, _ptr(out), _ptr(t), self._storm_n))
+        return out, t
+
+    def storm_write_start(self, t0: int) -> None:
+        self._check(self.lib.storm_write_start(self._ctx, int(t0)))
+
+    def storm_results(self) -> tuple[np.ndarray, np.ndarray, dict]:
+        """(failed[local], t_last[local], totals)."""
+        nloc = self.hi - self.lo
+        f = np.zeros(nloc, np.uint8)
+        t = np.zeros(nloc, np.int64)
+        tot = A.StormTotals()
+        self._check(self.lib.storm_results(self._ctx, _ptr(f), _ptr(t), nloc, C.byref(tot)))
+        return f.astype(bool), t, {k: getattr(tot, k) for k, _ in A.StormTotals._fields_}
+
+    def storm_end(self) -> None:
+        self._check(self.lib.storm_end(self._ctx))
+
     # ---- flood workload (config 5) -----------------------------------------------------------
     def flood_set_graph(self, offsets, neighbors, max_pubs: int) -> None:
         off = np.ascontiguousarray(offsets, dtype=np.uint32)

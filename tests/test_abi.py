@@ -23,7 +23,7 @@ HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_sha
             # allocation-failure injection into the library's C++ host tables (no C++ in the oracle)
             "tgsim_debug_fail_alloc",
             # device address of the proposed window end (tgsim_advance_begin_device has no oracle twin)
-            "tgsim_probe_state_device"}
+            "tgsim_probe_state_device", "tgsim_storm_state_device"}
 
 
 def test_header_declares_expected_surface():
@@ -64,7 +64,9 @@ def test_struct_layouts_match_header(tmp_path):
     structs = {"tgsim_link_shape": A.LinkShape, "tgsim_link_rule": A.LinkRule,
                "tgsim_network_config": A.NetworkConfig, "tgsim_config": A.Config, "tgsim_msg_soa": A.MsgSoA,
                "tgsim_tcp_config": A.TcpConfig, "tgsim_tcp_stats": A.TcpStats,
-               "tgsim_delivery_soa": A.DeliverySoA, "tgsim_stats": A.Stats, "tgsim_transport": A.Transport}
+               "tgsim_delivery_soa": A.DeliverySoA, "tgsim_stats": A.Stats, "tgsim_transport": A.Transport,
+               "tgsim_probe_config": A.ProbeConfig, "tgsim_storm_config": A.StormConfig,
+               "tgsim_storm_totals": A.StormTotals}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tgsim.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')

@@ -1,0 +1,278 @@
+"""The storm plan reactor (tgsim_storm_*): plans/benchmarks/storm.go:117-190's dial
+semaphore, DialTimeout, writesem and conn.Write blocking on a full send buffer, for every instance
+on the device. Hand-computed answers on the oracle and the HIP library, the protocol (a reaction
+after every window), randomised HIP-vs-oracle parity window by window, and the plan at 20k
+instances on HIP against the oracle."""
+import numpy as np
+import pytest
+
+from testground_amd import _abi as A
+from testground_amd import plans as P
+from testground_amd.network import int_to_ip
+from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape
+from tests import scenarios as S
+
+MS = 1_000_000
+SEC = 1000 * MS
+W = MS
+NONE = np.iinfo(np.int64).min
+
+
+def drive(sim, keep=True, max_windows=100_000):
+    """Reactions after every window at the proposed ends until nothing is active. Returns the
+    windows' observations (sorted statuses, deliveries, proposal, active count)."""
+    out, ne, w = [], sim.now + W, 0
+    while w < max_windows:
+        sim.advance(ne)
+        st, d = sim.status(), sim.deliveries()
+        ne, act = sim.storm_react()
+        if keep:
+            out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+        w += 1
+        if act == 0:
+            return out, w
+    raise AssertionError("the storm reactor did not finish")
+
+
+def _hand_case(b):
+    """2 instances x 2 connections, one semaphore slot, 2 chunks each, a one-chunk send buffer,
+    zero-latency links, 1 ms windows. Dials: 0.0 (t_ready 0) and 1.1 (t_ready 0) SYN at 0; their
+    peers answer at the SYN's arrival (0), the SYN-ACKs arrive at 0 in the window [1, 2) ms: OK at 0.
+    The slots are free from 0: 0.1 (t_ready 0.5 ms) dials at max(0.5, 0, horizon 1) = 1 ms, 1.0
+    (t_ready 2.3 ms) at 2.3 ms; their SYN-ACKs leave at max(arrival, horizon) = 2 and 2.3 ms and
+    arrive in [3, 4) ms: OK at 2 and 2.3 ms. Writes from 4 ms: each instance's round writes chunk 0
+    of both connections (the second taker blocks on nothing: the first released the slot), then the
+    first connection, queued again, finds its buffer full and holds the slot; at 5 ms both buffers
+    have drained and both write their last chunk."""
+    s = Simulator(SimConfig(n_instances=2, seed=7), binding=b)
+    dst = [1, 1, 0, 0]
+    t_ready = [0, 500_000, 2_300_000, 0]
+    s.storm_setup(dst, t_ready, outgoing=2, concurrent=1, data_bytes=8192, msg_window=1, window_ns=W)
+    s.storm_start()
+    dial_obs, _ = drive(s)
+    res, t_done = s.storm_dials()
+    assert res.tolist() == [A.PROBE_OK] * 4
+    assert t_done.tolist() == [0, 2 * MS, 2_300_000, 0]
+    assert s.now == 4 * MS
+    s.storm_write_start(s.now)
+    obs, w = drive(s)
+    arr = [(int(a), int(b_), int(q) & 0x3FFFFFFF, int(t)) for o in obs
+           for a, b_, q, t in zip(o["deliv"]["src"], o["deliv"]["dst"], o["deliv"]["seq"], o["deliv"]["t_deliver"])]
+    # (src, dst, k * n_chunks + j, t): chunk 0 of both connections at 4 ms, chunk 1 at 5 ms
+    assert sorted(arr) == sorted([(0, 1, 0, 4 * MS), (0, 1, 2, 4 * MS), (1, 0, 0, 4 * MS), (1, 0, 2, 4 * MS),
+                                  (0, 1, 1, 5 * MS), (0, 1, 3, 5 * MS), (1, 0, 1, 5 * MS), (1, 0, 3, 5 * MS)])
+    failed, t_last, tot = s.storm_results()
+    assert not failed.any() and t_last.tolist() == [5 * MS, 5 * MS]
+    assert tot["chunks_written"] == tot["chunks_delivered"] == 8 and tot["bytes_written"] == 4 * 8192
+    assert tot["dials_ok"] == 4 and tot["conns_writing"] == 0 and w == 2
+    s.storm_end()
+    s.close()
+
+
+def test_storm_hand_oracle(oracle):
+    _hand_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_hand_hip(hip):
+    _hand_case(hip)
+
+
+def _blocking_case(b):
+    """writesem blocks: one instance, three connections, one slot, a one-chunk buffer, 2 ms latency
+    (windows of 1 ms), 2 chunks each. At the write start connection 0 writes and queues again, 1
+    writes, 2 writes, then 0 takes the slot and blocks holding it (buffer full): no one else can
+    write until 0's chunk arrives at +2 ms; then 0 writes its last chunk and leaves, 1 takes the
+    slot and writes (its chunk arrived too), 2 writes. So chunk 0 of all three leaves at the start
+    t_w and chunk 1 of all three at the reaction after the window the first chunks arrive in."""
+    s = Simulator(SimConfig(n_instances=2, seed=3), binding=b)
+    s.set_shapes([0, 1], [make_shape(latency_ns=2 * MS)] * 2)
+    s.storm_setup([1, 1, 1, 0, 0, 0], [0] * 6, outgoing=3, concurrent=1, data_bytes=2 * 4096, msg_window=1,
+                  window_ns=W)
+    s.storm_start()
+    drive(s, keep=False)
+    res, t_done = s.storm_dials()
+    assert (res == A.PROBE_OK).all()
+    t_w = s.now
+    s.storm_write_start(t_w)
+    obs, _ = drive(s)
+    sent = sorted((int(t) - 2 * MS, int(q) & 0x3FFFFFFF) for o in obs
+                  for q, t, src in zip(o["deliv"]["seq"], o["deliv"]["t_deliver"], o["deliv"]["src"]) if src == 0)
+    # first chunks (j = 0: k * 2) at t_w; the arrivals at t_w + 2 ms fall in the window ending at
+    # t_w + 3 ms, whose reaction writes the second chunks
+    assert sent == [(t_w, 0), (t_w, 2), (t_w, 4), (t_w + 3 * MS, 1), (t_w + 3 * MS, 3), (t_w + 3 * MS, 5)]
+    s.storm_end()
+    s.close()
+
+
+def test_storm_blocking_oracle(oracle):
+    _blocking_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_blocking_hip(hip):
+    _blocking_case(hip)
+
+
+def _failure_case(b):
+    """A dial refused by the dialler's own route ends at its start (REFUSED), and so does every dial
+    of a disabled instance (no route: UNREACHABLE); one to a disabled peer waits out the 30 s
+    DialTimeout (the reactor jumps to the deadline + 1 ns). On the one-slot semaphore a dial queued
+    behind a refused one starts at once, one behind a finished dial at max(its t_ready, the slot's
+    release, the horizon)."""
+    s = Simulator(SimConfig(n_instances=4, seed=1), binding=b)
+    s.add_rules(0, [make_rule(int_to_ip(s.get_ip(1)) + "/32", A.FILTER_DROP)])
+    s.set_enabled(2, False)
+    s.storm_setup([1, 2, 2, 3, 0, 1, 1, 0], [0, 0, 1 * MS, 0, 0, 0, 0, 0], outgoing=2, concurrent=1,
+                  data_bytes=4096, window_ns=W)
+    s.storm_start()
+    _, w = drive(s, keep=False)
+    res, t_done = s.storm_dials()
+    OK, RF, TO = A.PROBE_OK, A.PROBE_REFUSED, A.PROBE_TIMEOUT
+    # instance 0: 0 -> 1 refused at 0 (its blackhole), then 0 -> 2 (peer down) from 0 to 30 s
+    # instance 1: 1 -> 3 (t_ready 0) OK at 0, then 1 -> 2 at max(1 ms, 0, horizon 1 ms) to 30.001 s
+    # instance 2 (disabled, no route): both dials refused at 0
+    # instance 3: 3 -> 1 OK at 0; 3 -> 0 at max(0, 0, horizon 1 ms), answered at max(1 ms, 2 ms): OK at 2 ms
+    assert res.tolist() == [RF, TO, TO, OK, RF, RF, OK, OK]
+    assert t_done.tolist() == [0, 30 * SEC, 30 * SEC + 1 * MS, 0, 0, 0, 0, 2 * MS]
+    assert w < 20
+    with pytest.raises(A.TgsimError) as e:
+        s.storm_write_start(s.now)       # a dial failed: "outgoing-dials-done" never releases
+    assert e.value.code == A.ESTATE
+    s.storm_end()
+    s.close()
+
+
+def test_storm_failures_oracle(oracle):
+    _failure_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_failures_hip(hip):
+    _failure_case(hip)
+
+
+def _protocol_case(b):
+    s = Simulator(SimConfig(n_instances=4, seed=1), binding=b)
+    with pytest.raises(A.TgsimError) as e:
+        s.storm_react()
+    assert e.value.code == A.ESTATE
+    s.storm_setup([1, 2, 3, 0], [0, 0, 0, 0], outgoing=1, concurrent=1, data_bytes=4096, window_ns=W)
+    s.storm_start()
+    s.advance(W)
+    for call in (lambda: s.enqueue([0], [1], [5], [64], [W]), lambda: s.advance(2 * W),
+                 lambda: s.storm_write_start(W), lambda: s.probe_setup([0, 1], 66, 66, SEC, W)):
+        with pytest.raises(A.TgsimError) as e:
+            call()
+        assert e.value.code == A.ESTATE
+    s.storm_react()
+    with pytest.raises(A.TgsimError) as e:
+        s.storm_react()
+    assert e.value.code == A.ESTATE
+    s.storm_end()
+    s.advance(2 * W)          # detached: windows no longer need a reaction
+    s.close()
+
+
+def test_storm_protocol_oracle(oracle):
+    _protocol_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_protocol_hip(hip):
+    _protocol_case(hip)
+
+
+def random_run(b, seed, n=60, keep=True):
+    """Shaped, lossy, duplicating links, a few blackhole / prohibit rules and a disabled instance:
+    dials refused, timed out and OK; then (on a second context, lossless while it dials) the write
+    phase with blocking writers and lost chunks."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for phase in ("dials", "writes"):
+        s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17),
+                      binding=b)
+        kw = [dict(latency_ns=int(rng.integers(0, 4)) * MS, jitter_ns=int(rng.integers(0, 3)) * MS // 2,
+                   loss=float(rng.choice([0.0, 0.0, 3.0])), duplicate=float(rng.choice([0.0, 5.0])),
+                   bandwidth_bps=int(rng.choice([0, 0, 50_000_000]))) for _ in range(n)]
+        lossless = [make_shape(**{**k, "loss": 0.0}) for k in kw]
+        s.set_shapes(np.arange(n), [make_shape(**k) for k in kw] if phase == "dials" else lossless)
+        O = int(rng.integers(1, 5))
+        src = np.repeat(np.arange(n), O)
+        dst = (src + rng.integers(1, n, len(src))) % n
+        t_ready = rng.integers(0, 40, len(src)) * MS // 3
+        if phase == "dials":
+            ip = [int_to_ip(s.get_ip(g)) + "/32" for g in range(n)]
+            for g in rng.choice(n, n // 6, replace=False):
+                tgt = rng.choice(n, 4, replace=False)
+                s.add_rules(int(g), [make_rule(ip[int(t)], int(rng.choice([A.FILTER_DROP, A.FILTER_REJECT])))
+                                     for t in tgt if t != g])
+            s.set_enabled(int(rng.integers(n)), False)
+        s.storm_setup(dst, t_ready, outgoing=O, concurrent=int(rng.integers(1, 4)),
+                      data_bytes=int(rng.integers(0, 9)) * 1500 + int(rng.integers(0, 3)) * 4096,
+                      msg_window=int(rng.integers(1, 4)), dial_timeout_ns=int(rng.integers(30, 90)) * MS,
+                      window_ns=W)
+        s.storm_start()
+        obs, w = drive(s, keep=keep)
+        res, t_done = s.storm_dials()
+        out[phase] = dict(obs=obs, w=w, res=res, t_done=t_done)
+        if phase == "writes":
+            assert (res == A.PROBE_OK).all()
+            s.set_shapes(np.arange(n), [make_shape(**k) for k in kw])
+            s.storm_write_start(s.now)
+            obs, w = drive(s, keep=keep)
+            failed, t_last, tot = s.storm_results()
+            out["write_obs"], out["write_w"] = obs, w
+            out["failed"], out["t_last"], out["totals"] = failed, t_last, tot
+        out[phase + "_stats"] = S.parity_stats(s)
+        s.storm_end()
+        s.close()
+    return out
+
+
+def test_storm_random_oracle_properties(oracle):
+    r = random_run(oracle, 1)
+    res = r["dials"]["res"]
+    assert {A.PROBE_OK, A.PROBE_REFUSED, A.PROBE_TIMEOUT} <= set(np.unique(res).tolist())
+    tot = r["totals"]
+    assert tot["chunks_written"] == tot["chunks_delivered"] + tot["chunks_failed"]
+    assert tot["conns_writing"] == 0 and tot["dials_pending"] == 0
+    assert tot["chunks_failed"] > 0 and r["failed"].any() and not r["failed"].all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_storm_random_hip_matches_oracle(hip, oracle, seed):
+    a, b = random_run(hip, seed), random_run(oracle, seed)
+    for k in ("dials", "writes"):
+        assert a[k]["w"] == b[k]["w"], f"{k}: window count"
+        S.assert_same(a[k]["obs"], b[k]["obs"])
+        assert np.array_equal(a[k]["res"], b[k]["res"]) and np.array_equal(a[k]["t_done"], b[k]["t_done"])
+        assert a[k + "_stats"] == b[k + "_stats"]
+    assert a["write_w"] == b["write_w"]
+    S.assert_same(a["write_obs"], b["write_obs"])
+    assert np.array_equal(a["failed"], b["failed"]) and np.array_equal(a["t_last"], b["t_last"])
+    assert a["totals"] == b["totals"]
+
+
+def storm_plan_run(b, n, params, seed=1):
+    env = P.PlanEnv(n, seed=seed, test_case="storm", params=params, binding=b,
+                    sim_kw=dict(max_msgs_per_window=max(1 << 18, 64 * n), max_records=max(1 << 20, 128 * n)))
+    ok = P.storm(env)
+    r = dict(ok=ok, failures=list(env.failures), now=env.sim.now, totals=getattr(env, "storm_totals", None),
+             windows=env.storm_windows, stats={k: v for k, v in env.sim.stats().items() if k != "windows"})
+    env.close()
+    return r
+
+
+@pytest.mark.gpu
+def test_storm_plan_20k_hip_matches_oracle(hip, oracle):
+    """the storm plan at 20k instances (5 dials each, 8 KiB per connection, dials
+    spread over 2 s) on the device reactor, equal to the oracle."""
+    params = {"conn_outgoing": "5", "conn_delay_ms": "2000", "concurrent_dials": "3", "data_size_kb": "8"}
+    a = storm_plan_run(hip, 20_000, params)
+    b = storm_plan_run(oracle, 20_000, params)
+    assert a["ok"].all() and np.array_equal(a["ok"], b["ok"])
+    for k in ("now", "totals", "windows", "stats"):
+        assert a[k] == b[k], k
+    assert a["totals"]["chunks_delivered"] == 20_000 * 5 * 2
