@@ -358,6 +358,11 @@ int tgsim_profile_set(tgsim_ctx* ctx, uint32_t mask);
 int tgsim_profile_read(tgsim_ctx* ctx, double* ms, uint64_t* launches, size_t cap, size_t* n);
 int tgsim_kernel_classes(void);
 const char* tgsim_kernel_name(int kernel_class);
+/* Cumulative implementation counters (forces a sync), for attributing SURVEY.md 8(d) bytes to the
+ * kernels that move them: [0] messages decided in the sequential queue-limit / correlation lane
+ * (k_shape_seq), [1] token-bucket copies of senders with long runs (k_rest), [2] deliveries of long
+ * inboxes (written by the wheel-insert launch's k_rest part), [3] reserved. *n = the count (4). */
+int tgsim_kernel_counters(tgsim_ctx* ctx, uint64_t* out, size_t cap, size_t* n);
 /* Test hook: the nth host allocation point from now (tgsim_add_rules, tgsim_flood_set_graph) throws
  * std::bad_alloc inside the library; the entry point returns TGSIM_ENOMEM and the context stays
  * usable (no C++ exception ever crosses this ABI). 0 disarms. */

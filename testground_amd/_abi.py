@@ -227,6 +227,7 @@ _SIGS_HIP = {
     "debug_fail_alloc": (C.c_int, [P, C.c_uint32]),
     "probe_state_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "storm_state_device": (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "kernel_counters": (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
 

@@ -22,7 +22,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
     "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit",
-    "k_shape_seq", "k_probe"};
+    "k_shape_seq", "k_probe", "k_seg_small", "k_storm"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
@@ -2321,8 +2321,10 @@ struct SigPolicy {
 };
 
 __global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* src, const uint32_t* n_ptr,
-                                                      uint32_t lo, uint32_t* keys, uint32_t* vals) {
+                                                      uint32_t lo, uint32_t* keys, uint32_t* vals,
+                                                      unsigned long long* kc_deferred) {
   const uint32_t n = *n_ptr;
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(kc_deferred, (unsigned long long)n);
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
     const uint32_t i = idx[j];
@@ -3594,6 +3596,16 @@ constexpr uint32_t kLargeTab = 256;      // large segments whose task table fits
 // (LargeSeg::pad counts them); tasks are claimed in that order, so a waiting block only waits on
 // tasks that running blocks hold. One block sorting a 10k-delivery inbox through merge passes took
 // ~280 us; the tasks take the time of one chunk sort and one rank search.
+// which implementation counter (DevScalars::kc) counts a policy's long-segment items
+template <class P> struct KcLong { static constexpr int v = -1; };
+template <> struct KcLong<TBPolicy> { static constexpr int v = KC_LONG_TB; };
+template <> struct KcLong<EmitPolicy> { static constexpr int v = KC_LONG_EMIT; };
+template <class P>
+__device__ __forceinline__ void count_long(const DevScalars* sc, uint32_t len) {
+  if (KcLong<P>::v >= 0 && threadIdx.x == 0)
+    atomicAdd(const_cast<unsigned long long*>(&sc->kc[KcLong<P>::v]), (unsigned long long)len);
+}
+
 template <class P>
 __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
                                           const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
@@ -3612,8 +3624,10 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
       __syncthreads();
       span_sort(s, m, off, a);
       p.epilogue(s, m, a, off, w);
+      count_long<P>(sc, m);
     } else {
       const LargeSeg L = large[w - nm];
+      count_long<P>(sc, L.len);
       const bool in_a = large_sort_block(p, s, L, keys, vals, K1a, K2a, K3a, K1b, K2b, K3b);
       large_consume(p, s, L, in_a ? K1a : K1b, in_a ? K3a : K3b, (w - nm) * 131u);
     }
@@ -3656,6 +3670,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     const LargeSeg L = large[i];
     const uint32_t nch = s_c1[i + 1] - s_c1[i], nrk = s_c2[i + 1] - s_c2[i];
     if (chunk) {
+      if (r == s_c1[i]) count_long<P>(sc, L.len);  // the segment's first chunk task counts it
       large_chunk_sort(p, s, L, (r - s_c1[i]) * kParChunk, keys, vals, K1a, K2a, K3a, kParChunk);
       __threadfence();  // the sorted chunk is visible device-wide before it is counted
       __syncthreads();
@@ -4134,7 +4149,7 @@ static hipError_t run_token_bucket(Dev& d) {
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
   hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.m_src, n_dev,
-                     d.lo, d.keys0, d.vals0);
+                     d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED]);
   TG_CHECK(hipGetLastError());
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
@@ -4142,8 +4157,11 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
-  hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
-                     d.seg_off, n_dev, d.cap_rec);
+  {
+    ProfScope ps_(d, KID_SEG_SMALL);  // each sender's deferred messages in (t_send, seq) order
+    hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
+                       d.seg_off, n_dev, d.cap_rec);
+  }
   TG_CHECK(hipGetLastError());
   TG_CHECK(launch_rest(d, p, keys, vals));
   const uint32_t* hoff = nullptr;
@@ -4157,6 +4175,7 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     hidx = hv;
   }
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
+  ProfScope ps_(d, KID_SHAPE_SEQ);  // the sequential lane itself
   hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, hoff, hidx,
                      d.H, d.cor_rho, d.cor_last, d.X);
   return hipGetLastError();
@@ -4217,10 +4236,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
                          d.plan_start, d.plan_off, d.arena, Q, a, ne, ho);
     }
     TG_CHECK(hipGetLastError());
-    if (d.any_corr || d.heavy.pend) {
-      ProfScope ps_(d, KID_SHAPE_SEQ);  // deferred messages grouped + the sequential lane
-      TG_CHECK(run_shape_seq(d, a, n_staged));
-    }
+    if (d.any_corr || d.heavy.pend) TG_CHECK(run_shape_seq(d, a, n_staged));
   }
   TG_CHECK(run_token_bucket(d));
   if (d.S > 1) {

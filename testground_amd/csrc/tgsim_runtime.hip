@@ -700,6 +700,21 @@ static int tgsim_profile_read_body(tgsim_ctx* c, double* ms, uint64_t* launches,
   return rc;
 }
 
+static int tgsim_kernel_counters_body(tgsim_ctx* c, uint64_t* out, size_t cap, size_t* n);
+extern "C" int tgsim_kernel_counters(tgsim_ctx* c, uint64_t* out, size_t cap, size_t* n) {
+  return abi_guard(c, [&] { return tgsim_kernel_counters_body(c, out, cap, n); });
+}
+static int tgsim_kernel_counters_body(tgsim_ctx* c, uint64_t* out, size_t cap, size_t* n) {
+  if (!c || !n) return TGSIM_EINVAL;
+  *n = KC_COUNT;
+  if (!out) return TGSIM_OK;
+  if (cap < (size_t)KC_COUNT) return fail(c, TGSIM_ECAPACITY, "counter capacity");
+  const int rc = sync_and_check(c);
+  if (rc) return rc;
+  for (int k = 0; k < KC_COUNT; ++k) out[k] = c->d.h_sc->kc[k];
+  return TGSIM_OK;
+}
+
 extern "C" int tgsim_kernel_classes(void) { return KID_COUNT; }
 extern "C" const char* tgsim_kernel_name(int k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : "?"; }
 

@@ -437,7 +437,7 @@ hipError_t launch_storm_write_start(Dev& d, bool base_dev, uint32_t base_host, i
 
 hipError_t launch_storm_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev) {
-  ProfScope ps_(d, KID_PROBE);
+  ProfScope ps_(d, KID_STORM);
   constexpr uint32_t nb = kStreamBlocks / 2;
   hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
                      n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, d.sm, nb,

@@ -372,6 +372,15 @@ class Simulator:
         self._check(self.lib.profile_read(self._ctx, _ptr(ms), _ptr(cnt), k, C.byref(n)))
         return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(self.kernel_names())}
 
+    KERNEL_COUNTERS = ("deferred", "long_tb", "long_emit", "reserved")
+
+    def kernel_counters(self) -> dict[str, int]:
+        """Cumulative implementation counters (tgsim_kernel_counters; HIP library only)."""
+        out = np.zeros(len(self.KERNEL_COUNTERS), np.uint64)
+        n = C.c_size_t()
+        self._check(self.lib.kernel_counters(self._ctx, _ptr(out), len(out), C.byref(n)))
+        return {k: int(out[i]) for i, k in enumerate(self.KERNEL_COUNTERS)}
+
     # ---- sync service -----------------------------------------------------------------------
     def signal(self, states, instances, t, want_seq: bool = True) -> np.ndarray | None:
         st = np.ascontiguousarray(states, dtype=np.uint32)

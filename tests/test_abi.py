@@ -23,7 +23,9 @@ HIP_ONLY = {"tgsim_version", "tgsim_abi_version", "tgsim_set_stream", "tgsim_sha
             # allocation-failure injection into the library's C++ host tables (no C++ in the oracle)
             "tgsim_debug_fail_alloc",
             # device address of the proposed window end (tgsim_advance_begin_device has no oracle twin)
-            "tgsim_probe_state_device", "tgsim_storm_state_device"}
+            "tgsim_probe_state_device", "tgsim_storm_state_device",
+            # implementation counters of the device pipeline (bench.py's per-kernel byte attribution)
+            "tgsim_kernel_counters"}
 
 
 def test_header_declares_expected_surface():

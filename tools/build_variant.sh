@@ -1,10 +1,9 @@
 #!/bin/bash
 # Experiment build of the product sources with extra defines, beside the product library:
 #   tools/build_variant.sh <name> -DFOO [-DBAR=1 ...]  ->  testground_amd/libtgsim_<name>.so
-# (load it with TGSIM_LIB=...; tools/gpu_ab.sh times it against the product build)
+# (load it with TGSIM_LIB=...; `tools/gpu.sh ab` times it against the product build;
+#  tools/build_variant.sh phase -DTGSIM_PHASE_PROF is the phase-clock build of tools/phase_probe.py)
 set -e
 name=$1; shift
-cd "$(dirname "$0")/../testground_amd/csrc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -shared \
-  -o ../libtgsim_$name.so tgsim_kernels.hip tgsim_runtime.hip tgsim_flood.hip tgsim_topics.hip tgsim_tcp.hip tgsim_probe.hip \
-  -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+make -s -B -C "$(dirname "$0")/../testground_amd/csrc" ARCH=gfx950 OUT=../libtgsim_$name.so \
+  CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result $*"
