@@ -1566,361 +1566,6 @@ int tgo_probe_results(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap)
   return TGSIM_OK;
 }
 
-/* ============================== storm plan reactor (DESIGN.md 2.13) ==========================
- * plans/benchmarks/storm.go:117-190 per instance: `outgoing` goroutines sleep until t_ready, take
- * the dial semaphore `sem` (FIFO, concurrent slots), DialTimeout 30 s (:141-152); after
- * "outgoing-dials-done" each writes data_size in 4 KiB chunks, every conn.Write under `writesem`
- * (:158-183) and blocking its goroutine (holding the slot) while the send buffer is full. A dial is a
- * SYN answered by a SYN-ACK, a probe of DESIGN.md 2.12; a chunk stays in its connection's buffer until
- * its first copy arrives or it fails. Straight loops over instances and connections. */
-
-enum { SM_SLEEP = 0, SM_WAIT = 1, SM_DONE = 2 };
-#define SM_NONE INT64_MAX
-#define SM_BUSY INT64_MAX
-typedef struct ostorm_conn {
-  uint32_t dst, slot, emit, rem, infl;
-  uint8_t state, flags, res, pad;
-  int64_t t_ready, t_start, t_synarr, t_ackarr, t_done, t_rep;
-} ostorm_conn;
-typedef struct ostorm ostorm;
-struct ostorm {
-  tgsim_storm_config cfg;
-  uint32_t O, C, nchunks, phase;
-  uint64_t n_conn;
-  ostorm_conn* conn;
-  uint32_t* order;  /* per instance its connections in (t_ready, k) order */
-  uint8_t* claim;   /* per chunk: first arrival seen */
-  uint32_t *dq, *qh, *ql, *nh, *ring, *hold;
-  int64_t* slot_t;
-  uint8_t* failed;
-  int64_t* t_last;
-  uint64_t written, delivered, failed_chunks, bytes;
-};
-
-static void sm_free(tgo_ctx* c) {
-  ostorm* s = c->sm;
-  if (!s) return;
-  free(s->conn); free(s->order); free(s->claim); free(s->dq); free(s->qh); free(s->ql); free(s->nh);
-  free(s->ring); free(s->hold); free(s->slot_t); free(s->failed); free(s->t_last); free(s);
-  c->sm = NULL;
-  c->sm_need_react = 0;
-}
-
-static const int64_t* g_sm_tr;
-static int cmp_sm_order(const void* a, const void* b) {
-  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
-  if (g_sm_tr[x] != g_sm_tr[y]) return g_sm_tr[x] < g_sm_tr[y] ? -1 : 1;
-  return x < y ? -1 : x > y;
-}
-
-int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg) {
-  if (!cfg) return TGSIM_EINVAL;
-  if (cfg->outgoing == 0 || cfg->concurrent == 0 || cfg->chunk_bytes == 0 || cfg->msg_window == 0 ||
-      cfg->dial_timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->syn_bytes >= 0x80000000u ||
-      (uint64_t)cfg->chunk_bytes + cfg->header_bytes >= 0x80000000ull)
-    return fail(c, TGSIM_EINVAL, "bad storm configuration");
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
-  if (c->tcp_on || c->fl_off || c->pr)
-    return fail(c, TGSIM_ESTATE, "the storm reactor runs in message mode, without a flood graph or probes");
-  const uint64_t n_conn = (uint64_t)c->N * cfg->outgoing;
-  const uint64_t nchunks = (cfg->data_bytes + cfg->chunk_bytes - 1) / cfg->chunk_bytes;
-  if (n_conn > 0x3FFFFFFFull || nchunks * cfg->outgoing > 0x3FFFFFFFull)
-    return fail(c, TGSIM_ENOTSUP, "too many connections or chunks for the storm's packet tags");
-  if (n_conn && (!dst || !t_ready)) return fail(c, TGSIM_EINVAL, "bad arguments");
-  for (uint64_t h = 0; h < n_conn; ++h) {
-    if (dst[h] >= c->N) return fail(c, TGSIM_EINVAL, "connection %llu: bad peer", (unsigned long long)h);
-    if (t_ready[h] < c->now) return fail(c, TGSIM_ECAUSALITY, "connection %llu: t_ready before now", (unsigned long long)h);
-  }
-  sm_free(c);
-  const uint32_t O = cfg->outgoing, C = cfg->concurrent, Hc = C < O ? C : O;
-  const size_t nl = c->nloc ? c->nloc : 1, nc = n_conn ? n_conn : 1;
-  ostorm* s = (ostorm*)calloc(1, sizeof(ostorm));
-  if (!s) return fail(c, TGSIM_ENOMEM, "oom");
-  c->sm = s;
-  s->conn = (ostorm_conn*)calloc(nc, sizeof(ostorm_conn));
-  s->order = (uint32_t*)malloc(nc * 4);
-  s->claim = (uint8_t*)calloc(n_conn * nchunks + 1, 1);
-  s->dq = (uint32_t*)calloc(nl, 4); s->qh = (uint32_t*)calloc(nl, 4); s->ql = (uint32_t*)calloc(nl, 4);
-  s->nh = (uint32_t*)calloc(nl, 4); s->ring = (uint32_t*)calloc(nc, 4); s->hold = (uint32_t*)calloc(nl * Hc, 4);
-  s->slot_t = (int64_t*)malloc(nl * C * 8); s->failed = (uint8_t*)calloc(nl, 1); s->t_last = (int64_t*)malloc(nl * 8);
-  if (!s->conn || !s->order || !s->claim || !s->dq || !s->qh || !s->ql || !s->nh || !s->ring || !s->hold ||
-      !s->slot_t || !s->failed || !s->t_last) { sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
-  for (size_t i = 0; i < nl * C; ++i) s->slot_t[i] = INT64_MIN;
-  for (size_t i = 0; i < nl; ++i) s->t_last[i] = INT64_MIN;
-  for (uint64_t h = 0; h < n_conn; ++h) {
-    s->conn[h].dst = dst[h];
-    s->conn[h].t_ready = t_ready[h];
-    s->conn[h].t_done = INT64_MIN;
-  }
-  for (uint32_t g = 0; g < c->N; ++g) {
-    uint32_t* o = s->order + (size_t)g * O;
-    for (uint32_t k = 0; k < O; ++k) o[k] = k;
-    g_sm_tr = t_ready + (size_t)g * O;
-    qsort(o, O, 4, cmp_sm_order);
-  }
-  s->cfg = *cfg; s->O = O; s->C = C; s->nchunks = (uint32_t)nchunks; s->n_conn = n_conn; s->phase = 0;
-  return TGSIM_OK;
-}
-
-static int sm_failed_code(uint8_t st) {
-  const uint32_t code = st & 0x0Fu;
-  return code != TGSIM_ST_QUEUED && code != TGSIM_ST_LOCAL;
-}
-
-/* Dial phase of instance g (frame: horizon H, window end t_end): resolve its waiting dials, then the
- * semaphore admits dials in FIFO order into free slots, each at max(t_ready, slot free, H), while
- * that is before the next window's end. */
-static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_end, pbuf* b, int64_t* dl_min,
-                     int64_t* ns_min, uint32_t* act) {
-  ostorm* s = c->sm;
-  const uint32_t O = s->O, C = s->C;
-  const int64_t timeout = s->cfg.dial_timeout_ns;
-  ostorm_conn* cn = s->conn + (size_t)g * O;
-  for (uint32_t k = 0; k < O && resolve; ++k) {
-    ostorm_conn* x = &cn[k];
-    if (x->state != SM_WAIT) continue;
-    const int64_t dl = x->t_start + timeout;
-    int reply_pending = 0;
-    if (x->t_synarr != SM_NONE && !(x->flags & 2u)) {  /* the listener answers the SYN's first arrival */
-      const int64_t trep = x->t_synarr > H ? x->t_synarr : H;
-      pr_stage(b, x->dst, g, TGSIM_STORM_SYNACK | (uint32_t)((size_t)g * O + k), s->cfg.syn_bytes, trep);
-      x->flags |= 2u;
-      reply_pending = trep < dl;
-    }
-    x->t_synarr = SM_NONE;
-    uint8_t out = TGSIM_PROBE_NONE;
-    int64_t te = 0;
-    if (x->flags & 1u) { out = TGSIM_PROBE_REFUSED; te = x->t_start; }
-    else if (x->t_ackarr != SM_NONE && x->t_ackarr < dl) { out = TGSIM_PROBE_OK; te = x->t_ackarr; }
-    else if (dl < t_end && !reply_pending) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
-    if (out != TGSIM_PROBE_NONE) {
-      x->state = SM_DONE; x->res = out; x->t_done = te;
-      s->slot_t[(size_t)g * C + x->slot] = te;
-    } else {
-      ++*act;
-      if (dl < *dl_min) *dl_min = dl;
-    }
-  }
-  uint32_t q = s->dq[g];
-  while (q < O) {
-    uint32_t best = C;
-    int64_t bt = SM_BUSY;
-    for (uint32_t j = 0; j < C; ++j)
-      if (s->slot_t[(size_t)g * C + j] < bt) { bt = s->slot_t[(size_t)g * C + j]; best = j; }
-    if (best == C) break;
-    const uint32_t k = s->order[(size_t)g * O + q];
-    ostorm_conn* x = &cn[k];
-    int64_t t0 = x->t_ready;
-    if (bt > t0) t0 = bt;
-    if (H > t0) t0 = H;
-    if (t0 >= t_end + s->cfg.window_ns) { if (t0 < *ns_min) *ns_min = t0; break; }
-    s->slot_t[(size_t)g * C + best] = SM_BUSY;
-    x->slot = best; x->state = SM_WAIT; x->t_start = t0; x->flags = 0;
-    x->t_synarr = x->t_ackarr = SM_NONE;
-    pr_stage(b, g, x->dst, TGSIM_STORM_SYN | k, s->cfg.syn_bytes, t0);
-    ++*act;
-    if (t0 + timeout < *dl_min) *dl_min = t0 + timeout;
-    ++q;
-  }
-  s->dq[g] = q;
-  *act += O - q;
-}
-
-static uint32_t sm_payload(const ostorm* s, uint32_t j) {
-  return j + 1 < s->nchunks ? s->cfg.chunk_bytes : (uint32_t)(s->cfg.data_bytes - (uint64_t)j * s->cfg.chunk_bytes);
-}
-/* conn.Write of the connection's next chunk at t (the buffer had room) */
-static void sm_write(tgo_ctx* c, uint32_t g, uint32_t k, int64_t t, pbuf* b) {
-  ostorm* s = c->sm;
-  ostorm_conn* x = &s->conn[(size_t)g * s->O + k];
-  const uint32_t j = s->nchunks - x->rem;
-  pr_stage(b, g, x->dst, TGSIM_STORM_DATA | (k * s->nchunks + j), sm_payload(s, j) + s->cfg.header_bytes, t);
-  x->rem--; x->infl++;
-  s->written++; s->bytes += sm_payload(s, j);
-}
-/* Write phase of instance g at t: one writesem round (storm.go:158-183). */
-static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act) {
-  ostorm* s = c->sm;
-  const uint32_t O = s->O, C = s->C, Hc = C < O ? C : O, win = s->cfg.msg_window;
-  ostorm_conn* cn = s->conn + (size_t)g * O;
-  uint32_t* ring = s->ring + (size_t)g * O;
-  uint32_t* hold = s->hold + (size_t)g * Hc;
-  uint32_t qh = s->qh[g], ql = s->ql[g], nh = s->nh[g], wrote = 0;
-  int progress = 1;
-  while (progress) {
-    progress = 0;
-    uint32_t keep = 0;
-    for (uint32_t i = 0; i < nh; ++i) {  /* blocked writers whose buffer drained */
-      const uint32_t k = hold[i];
-      if (cn[k].infl < win) {
-        sm_write(c, g, k, t, b); ++wrote; progress = 1;
-        if (cn[k].rem) { ring[(qh + ql) % O] = k; ++ql; }
-      } else {
-        hold[keep++] = k;
-      }
-    }
-    nh = keep;
-    while (nh < C && ql > 0) {  /* free slots go to the queue's head */
-      const uint32_t k = ring[qh];
-      qh = (qh + 1) % O; --ql;
-      if (cn[k].infl < win) {
-        sm_write(c, g, k, t, b); ++wrote; progress = 1;
-        if (cn[k].rem) { ring[(qh + ql) % O] = k; ++ql; }
-      } else {
-        hold[nh++] = k;
-      }
-    }
-  }
-  s->qh[g] = qh; s->ql[g] = ql; s->nh[g] = nh;
-  if (wrote) s->t_last[g] = t;
-  for (uint32_t k = 0; k < O; ++k) *act += (cn[k].rem || cn[k].infl) ? 1u : 0u;
-}
-
-/* one reaction frame (H, t_end): every instance's step, then the proposal of the next window's end */
-static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* next_end, uint32_t* n_active) {
-  ostorm* s = c->sm;
-  pbuf b;
-  const size_t cap = s->phase ? (size_t)s->n_conn * s->cfg.msg_window + 1 : 2 * (size_t)s->n_conn + 1;
-  if (pr_alloc(&b, cap)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
-  int64_t dl = SM_NONE, ns = SM_NONE;
-  uint32_t act = 0;
-  for (uint32_t g = 0; g < c->N; ++g) {
-    if (s->phase) sm_writes(c, g, t_end, &b, &act);
-    else sm_dials(c, g, resolve, H, t_end, &b, &dl, &ns, &act);
-  }
-  int rc = pr_flush(c, &b);
-  if (rc) return rc;
-  int64_t ne = t_end + s->cfg.window_ns;
-  if (!c->staged.n && !c->heap.n && act) {  /* idle: jump to the next deadline or dial */
-    int64_t cand = dl != SM_NONE ? dl + 1 : SM_NONE;
-    if (ns < cand) cand = ns;
-    if (cand != SM_NONE && cand > ne) ne = cand;
-  }
-  if (next_end) *next_end = ne;
-  if (n_active) *n_active = act;
-  return TGSIM_OK;
-}
-
-int tgo_storm_start(tgo_ctx* c) {
-  if (!c->sm) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if (c->sm->phase != 0) return fail(c, TGSIM_ESTATE, "the storm's dials have started");
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (react_owed(c)) return TGSIM_ESTATE;
-  return sm_step(c, 0, c->now, c->now, NULL, NULL);
-}
-
-int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
-  ostorm* s = c->sm;
-  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (!c->sm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
-  c->sm_need_react = 0;
-  const omsgs* st = &c->staged;
-  const uint32_t O = s->O;
-  /* 1. the window's packets: refused SYNs, chunks no copy of entered the egress queue */
-  for (size_t i = 0; i < c->n_status; ++i) {
-    const uint32_t sq = st->seq[i], tag = sq >> 30, code = c->status[i] & 0x0Fu;
-    if (tag == 1u) {
-      ostorm_conn* x = &s->conn[(size_t)st->src[i] * O + (sq & PR_MASK)];
-      if ((code == TGSIM_ST_DROPPED || code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) &&
-          x->state == SM_WAIT && x->dst == st->dst[i])
-        x->flags |= 1u;
-    } else if (tag == 2u && sm_failed_code(c->status[i])) {
-      s->conn[(size_t)st->src[i] * O + (sq & PR_MASK) / s->nchunks].infl--;
-      s->failed[st->src[i]] = 1;
-      s->failed_chunks++;
-    }
-  }
-  /* 2. the window's deliveries: first arrivals of SYNs and SYN-ACKs, the first copy of each chunk */
-  for (size_t i = 0; i < c->out.n; ++i) {
-    const tgsim_record* r = &c->out.v[i];
-    const uint32_t tag = r->seq >> 30;
-    if (tag == 1u) {
-      ostorm_conn* x = &s->conn[(size_t)r->src * O + (r->seq & PR_MASK)];
-      if (x->state == SM_WAIT && x->dst == r->dst && r->t < x->t_synarr) x->t_synarr = r->t;
-    } else if (tag == 3u) {
-      const size_t h = r->seq & PR_MASK;
-      if (h < s->n_conn && h / O == r->dst) {
-        ostorm_conn* x = &s->conn[h];
-        if (x->dst == r->src && x->state == SM_WAIT && (x->flags & 2u) && r->t < x->t_ackarr) x->t_ackarr = r->t;
-      }
-    } else if (tag == 2u) {
-      const uint32_t cj = r->seq & PR_MASK, k = cj / s->nchunks;
-      const size_t h = (size_t)r->src * O + k;
-      const uint64_t bit = (uint64_t)h * s->nchunks + (cj - k * s->nchunks);
-      if (!s->claim[bit]) { s->claim[bit] = 1; s->conn[h].infl--; s->delivered++; }
-    }
-  }
-  /* 3. per instance: dials or writes, then the proposal */
-  return sm_step(c, 1, c->horizon, c->now, next_end, n_active);
-}
-
-int tgo_storm_dials(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
-  ostorm* s = c->sm;
-  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if ((outcome || t_done) && cap < s->n_conn) return fail(c, TGSIM_ECAPACITY, "dial capacity");
-  for (uint64_t h = 0; h < s->n_conn; ++h) {
-    if (outcome) outcome[h] = s->conn[h].res;
-    if (t_done) t_done[h] = s->conn[h].t_done;
-  }
-  return TGSIM_OK;
-}
-
-int tgo_storm_write_start(tgo_ctx* c, int64_t t0) {
-  ostorm* s = c->sm;
-  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if (s->phase != 0) return fail(c, TGSIM_ESTATE, "the write phase has started");
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (react_owed(c)) return TGSIM_ESTATE;
-  if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
-  for (uint64_t h = 0; h < s->n_conn; ++h)
-    if (s->conn[h].res != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %llu has not dialled successfully", (unsigned long long)h);
-  s->phase = 1;
-  for (uint32_t g = 0; g < c->N; ++g) {
-    uint32_t n = 0;
-    for (uint32_t k = 0; k < s->O; ++k) {
-      ostorm_conn* x = &s->conn[(size_t)g * s->O + k];
-      x->rem = s->nchunks; x->infl = 0;
-      if (s->nchunks) s->ring[(size_t)g * s->O + n++] = k;
-    }
-    s->qh[g] = 0; s->ql[g] = n; s->nh[g] = 0;
-  }
-  return sm_step(c, 0, t0, t0, NULL, NULL);
-}
-
-int tgo_storm_results(tgo_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot) {
-  ostorm* s = c->sm;
-  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if ((failed || t_last) && cap < c->nloc) return fail(c, TGSIM_ECAPACITY, "result capacity");
-  for (uint32_t g = 0; g < c->nloc; ++g) {
-    uint8_t f = s->failed[g];
-    for (uint32_t k = 0; k < s->O; ++k) f |= s->conn[(size_t)g * s->O + k].infl ? 1 : 0;
-    if (failed) failed[g] = f;
-    if (t_last) t_last[g] = s->t_last[g];
-  }
-  if (tot) {
-    memset(tot, 0, sizeof(*tot));
-    tot->chunks_written = s->written; tot->chunks_delivered = s->delivered;
-    tot->chunks_failed = s->failed_chunks; tot->bytes_written = s->bytes;
-    for (uint64_t h = 0; h < s->n_conn; ++h) {
-      const ostorm_conn* x = &s->conn[h];
-      tot->dials_ok += x->res == TGSIM_PROBE_OK;
-      tot->dials_failed += x->res == TGSIM_PROBE_REFUSED || x->res == TGSIM_PROBE_TIMEOUT;
-      tot->dials_pending += x->res == TGSIM_PROBE_NONE;
-      tot->conns_writing += s->phase == 1 && (x->rem || x->infl);
-    }
-  }
-  return TGSIM_OK;
-}
-
-int tgo_storm_end(tgo_ctx* c) {
-  if (!c->sm) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  sm_free(c);
-  return TGSIM_OK;
-}
-
 /* ============================== topics (sync.Client Publish / Subscribe) ===================
  * [EXT sdk-go]; call sites plans/network/pingpong.go:219-245, plans/benchmarks/storm.go:232-255,
  * plans/splitbrain/main.go:91-103. A topic is a sync state: tgo_sync_signal assigns the positions
@@ -2121,6 +1766,7 @@ static int conn_release(tgo_ctx* c, uint32_t k, int64_t t0, ostage* b) {
 
 int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* conn_out) {
   if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
+  if (c->sm) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->tw_n && !c->tc_n) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
   if (n && (!src || !dst)) return fail(c, TGSIM_EINVAL, "bad arguments");
@@ -2138,6 +1784,7 @@ int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t
 
 int tgo_tcp_write(tgo_ctx* c, const uint32_t* conn, const uint32_t* size, const int64_t* t, size_t n) {
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->sm) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (n && (!conn || !size || !t)) return fail(c, TGSIM_EINVAL, "bad arguments");
@@ -2529,3 +2176,504 @@ int tgo_tcp_get_stats(tgo_ctx* c, tgsim_tcp_stats* out) {
   *out = c->tstats;
   return TGSIM_OK;
 }
+
+/* ============================== storm plan reactor (DESIGN.md 2.13) ==========================
+ * plans/benchmarks/storm.go:117-190 per instance: `outgoing` goroutines sleep until t_ready, take
+ * the dial semaphore `sem` (FIFO, concurrent slots), DialTimeout 30 s (:141-152); after
+ * "outgoing-dials-done" each writes data_size in 4 KiB chunks, every conn.Write under `writesem`
+ * (:158-183) and blocking its goroutine (holding the slot) while the send buffer is full. A dial is a
+ * SYN answered by a SYN-ACK, a probe of DESIGN.md 2.12; a chunk stays in its connection's buffer until
+ * its first copy arrives or it fails. Straight loops over instances and connections. */
+
+enum { SM_SLEEP = 0, SM_WAIT = 1, SM_DONE = 2 };
+#define SM_NONE INT64_MAX
+#define SM_BUSY INT64_MAX
+typedef struct ostorm_conn {
+  uint32_t dst, slot, emit, rem, infl;
+  uint8_t state, flags, res, pad;
+  int64_t t_ready, t_start, t_synarr, t_ackarr, t_done, t_rep;
+} ostorm_conn;
+typedef struct ostorm ostorm;
+struct ostorm {
+  tgsim_storm_config cfg;
+  uint32_t O, C, nchunks, phase;
+  uint64_t n_conn;
+  ostorm_conn* conn;
+  uint32_t* order;  /* per instance its connections in (t_ready, k) order */
+  uint8_t* claim;   /* per chunk: first arrival seen */
+  uint32_t *dq, *qh, *ql, *nh, *ring, *hold;
+  int64_t* slot_t;
+  uint8_t* failed;
+  int64_t* t_last;
+  uint64_t written, delivered, failed_chunks, bytes;
+  /* TCP mode: connection h is TCP connection h; write W0 + h * (nchunks + 1) + j
+   * (j = 0 the SYN) and segments from S0 + h * spcon (the SYN's, then spc per full chunk) are
+   * reserved at setup and linked onto the connection's queue when written */
+  int tcp;
+  uint32_t W0, S0, spc, spcon;
+  uint32_t *settled, *wsegs;
+};
+
+static void sm_free(tgo_ctx* c) {
+  ostorm* s = c->sm;
+  if (!s) return;
+  free(s->conn); free(s->order); free(s->claim); free(s->dq); free(s->qh); free(s->ql); free(s->nh);
+  free(s->ring); free(s->hold); free(s->slot_t); free(s->failed); free(s->t_last); free(s->settled); free(s->wsegs);
+  free(s);
+  c->sm = NULL;
+  c->sm_need_react = 0;
+}
+
+static const int64_t* g_sm_tr;
+static int cmp_sm_order(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  if (g_sm_tr[x] != g_sm_tr[y]) return g_sm_tr[x] < g_sm_tr[y] ? -1 : 1;
+  return x < y ? -1 : x > y;
+}
+
+int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg) {
+  if (!cfg) return TGSIM_EINVAL;
+  if (cfg->outgoing == 0 || cfg->concurrent == 0 || cfg->chunk_bytes == 0 || cfg->msg_window == 0 ||
+      cfg->dial_timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->syn_bytes >= 0x80000000u ||
+      (uint64_t)cfg->chunk_bytes + cfg->header_bytes >= 0x80000000ull)
+    return fail(c, TGSIM_EINVAL, "bad storm configuration");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
+  if (c->fl_off || c->pr) return fail(c, TGSIM_ESTATE, "the storm reactor runs without a flood graph or probes");
+  if (c->tcp_on && (!c->tcp.acks || c->tc_n || c->tw_n))
+    return fail(c, TGSIM_ESTATE, "a TCP storm needs acks = 1 and a context without connections or writes yet");
+  const uint64_t n_conn = (uint64_t)c->N * cfg->outgoing;
+  const uint64_t nchunks = (cfg->data_bytes + cfg->chunk_bytes - 1) / cfg->chunk_bytes;
+  if (n_conn > 0x3FFFFFFFull || nchunks * cfg->outgoing > 0x3FFFFFFFull)
+    return fail(c, TGSIM_ENOTSUP, "too many connections or chunks for the storm's packet tags");
+  if (n_conn && (!dst || !t_ready)) return fail(c, TGSIM_EINVAL, "bad arguments");
+  for (uint64_t h = 0; h < n_conn; ++h) {
+    if (dst[h] >= c->N) return fail(c, TGSIM_EINVAL, "connection %llu: bad peer", (unsigned long long)h);
+    if (t_ready[h] < c->now) return fail(c, TGSIM_ECAUSALITY, "connection %llu: t_ready before now", (unsigned long long)h);
+  }
+  uint64_t spc = 0, spcon = 0, tot_w = 0, tot_s = 0;
+  if (c->tcp_on) {
+    const uint64_t mss = c->tcp.mss, last = nchunks ? cfg->data_bytes - (nchunks - 1) * cfg->chunk_bytes : 0;
+    spc = (cfg->chunk_bytes + mss - 1) / mss;
+    spcon = 1 + (nchunks ? (nchunks - 1) * spc + (last + mss - 1) / mss : 0);
+    tot_w = n_conn * (nchunks + 1);
+    tot_s = n_conn * spcon;
+    if (n_conn > c->tcp.max_writes || tot_w > c->tcp.max_writes || tot_s > c->tcp.max_segments)
+      return fail(c, TGSIM_ECAPACITY, "TCP storm: writes / segments exceed the TCP capacities");
+  }
+  sm_free(c);
+  const uint32_t O = cfg->outgoing, C = cfg->concurrent, Hc = C < O ? C : O;
+  const size_t nl = c->nloc ? c->nloc : 1, nc = n_conn ? n_conn : 1;
+  ostorm* s = (ostorm*)calloc(1, sizeof(ostorm));
+  if (!s) return fail(c, TGSIM_ENOMEM, "oom");
+  c->sm = s;
+  s->conn = (ostorm_conn*)calloc(nc, sizeof(ostorm_conn));
+  s->order = (uint32_t*)malloc(nc * 4);
+  s->claim = (uint8_t*)calloc(n_conn * nchunks + 1, 1);
+  s->dq = (uint32_t*)calloc(nl, 4); s->qh = (uint32_t*)calloc(nl, 4); s->ql = (uint32_t*)calloc(nl, 4);
+  s->nh = (uint32_t*)calloc(nl, 4); s->ring = (uint32_t*)calloc(nc, 4); s->hold = (uint32_t*)calloc(nl * Hc, 4);
+  s->slot_t = (int64_t*)malloc(nl * C * 8); s->failed = (uint8_t*)calloc(nl, 1); s->t_last = (int64_t*)malloc(nl * 8);
+  if (!s->conn || !s->order || !s->claim || !s->dq || !s->qh || !s->ql || !s->nh || !s->ring || !s->hold ||
+      !s->slot_t || !s->failed || !s->t_last) { sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
+  for (size_t i = 0; i < nl * C; ++i) s->slot_t[i] = INT64_MIN;
+  for (size_t i = 0; i < nl; ++i) s->t_last[i] = INT64_MIN;
+  for (uint64_t h = 0; h < n_conn; ++h) {
+    s->conn[h].dst = dst[h];
+    s->conn[h].t_ready = t_ready[h];
+    s->conn[h].t_done = INT64_MIN;
+  }
+  for (uint32_t g = 0; g < c->N; ++g) {
+    uint32_t* o = s->order + (size_t)g * O;
+    for (uint32_t k = 0; k < O; ++k) o[k] = k;
+    g_sm_tr = t_ready + (size_t)g * O;
+    qsort(o, O, 4, cmp_sm_order);
+  }
+  s->cfg = *cfg; s->O = O; s->C = C; s->nchunks = (uint32_t)nchunks; s->n_conn = n_conn; s->phase = 0;
+  if (c->tcp_on) {  /* the connections, then the reserved writes and segments as tgo_tcp_write builds them */
+    uint32_t* src = (uint32_t*)malloc(nc * 4);
+    s->settled = (uint32_t*)calloc(nc, 4);
+    s->wsegs = (uint32_t*)calloc(nc, 4);
+    if (!src || !s->settled || !s->wsegs) { free(src); sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
+    for (uint64_t h = 0; h < n_conn; ++h) src[h] = (uint32_t)(h / O);
+    ostorm* keep = c->sm;
+    c->sm = NULL;  /* tgo_tcp_connect refuses while a reactor owns the connections */
+    int rc = tgo_tcp_connect(c, src, dst, n_conn, NULL);
+    c->sm = keep;
+    free(src);
+    if (rc) { sm_free(c); return rc; }
+    if (grow((void**)&c->tw, &c->tw_cap, c->tw_n + tot_w + 1, sizeof(otcpw)) ||
+        grow((void**)&c->tsg, &c->tsg_cap, c->tsg_n + tot_s + 1, sizeof(otcps))) { sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
+    s->tcp = 1; s->spc = (uint32_t)spc; s->spcon = (uint32_t)spcon;
+    s->W0 = (uint32_t)c->tw_n; s->S0 = (uint32_t)c->tsg_n;
+    const uint32_t mss = c->tcp.mss, hdr = c->tcp.header_bytes;
+    for (uint64_t h = 0; h < n_conn; ++h) {
+      for (uint32_t j = 0; j <= s->nchunks; ++j) {
+        const uint32_t pay = j ? (j < s->nchunks ? cfg->chunk_bytes
+                                                 : (uint32_t)(cfg->data_bytes - (uint64_t)(j - 1) * cfg->chunk_bytes)) : 0;
+        const uint32_t ns = pay ? (pay + mss - 1) / mss : 1;
+        const uint32_t wi = s->W0 + (uint32_t)h * (s->nchunks + 1) + j;
+        const uint32_t first = s->S0 + (uint32_t)h * s->spcon + (j ? 1 + (j - 1) * s->spc : 0);
+        otcpw w = {(uint32_t)(h / O), dst[h], ns, TGSIM_TCP_PENDING, INT64_MIN, (uint32_t)h};
+        c->tw[wi] = w;
+        for (uint32_t i = 0; i < ns; ++i) {
+          otcps g = {wi, (pay ? (i + 1 < ns ? mss : pay - i * mss) : 0) + hdr, 0, 0, 0, 0, 0, INT64_MAX, INT64_MIN, 0, 0,
+                     TCP_NOSEG, 1};
+          c->tsg[first + i] = g;
+        }
+      }
+    }
+    c->tw_n += tot_w; c->tsg_n += tot_s;
+    c->tstats.writes += tot_w; c->tstats.segments += tot_s;
+  }
+  return TGSIM_OK;
+}
+
+/* TCP mode: a write's segments join connection h's send queue at time t (tgo_tcp_write's loop) */
+static void sm_link(tgo_ctx* c, uint64_t h, uint32_t first, uint32_t n, int64_t t) {
+  otcpc* q = &c->tc[h];
+  for (uint32_t sid = first; sid < first + n; ++sid) {
+    c->tsg[sid].t_att = t;
+    if (q->tail != TCP_NOSEG) c->tsg[q->tail].next = sid;
+    if (q->head == TCP_NOSEG) q->head = sid;
+    q->tail = sid;
+    q->queued++;
+  }
+}
+static uint32_t sm_wid(const ostorm* s, uint64_t h, uint32_t j) { return s->W0 + (uint32_t)h * (s->nchunks + 1) + j; }
+
+static int sm_failed_code(uint8_t st) {
+  const uint32_t code = st & 0x0Fu;
+  return code != TGSIM_ST_QUEUED && code != TGSIM_ST_LOCAL;
+}
+
+/* Dial phase of instance g (frame: horizon H, window end t_end): resolve its waiting dials, then the
+ * semaphore admits dials in FIFO order into free slots, each at max(t_ready, slot free, H), while
+ * that is before the next window's end. */
+static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_end, pbuf* b, int64_t* dl_min,
+                     int64_t* ns_min, uint32_t* act, uint32_t* waiting) {
+  ostorm* s = c->sm;
+  const uint32_t O = s->O, C = s->C;
+  const int64_t timeout = s->cfg.dial_timeout_ns;
+  ostorm_conn* cn = s->conn + (size_t)g * O;
+  for (uint32_t k = 0; k < O && resolve; ++k) {
+    ostorm_conn* x = &cn[k];
+    if (x->state != SM_WAIT) continue;
+    if (s->tcp) {  /* the SYN write: ACKed (connect() returned, seen at the window's end) or failed */
+      const uint64_t h = (uint64_t)g * O + k;
+      const uint32_t ws = c->tw[sm_wid(s, h, 0)].state;
+      uint8_t out = c->tc[h].acked >= 1 ? TGSIM_PROBE_OK
+                  : ws == TGSIM_TCP_TIMEOUT ? TGSIM_PROBE_TIMEOUT : ws == TGSIM_TCP_REFUSED ? TGSIM_PROBE_REFUSED : TGSIM_PROBE_NONE;
+      if (out != TGSIM_PROBE_NONE) {
+        x->state = SM_DONE; x->res = out; x->t_done = t_end;
+        s->slot_t[(size_t)g * C + x->slot] = t_end;
+      } else {
+        ++*act; ++*waiting;
+      }
+      continue;
+    }
+    const int64_t dl = x->t_start + timeout;
+    int reply_pending = 0;
+    if (x->t_synarr != SM_NONE && !(x->flags & 2u)) {  /* the listener answers the SYN's first arrival */
+      const int64_t trep = x->t_synarr > H ? x->t_synarr : H;
+      pr_stage(b, x->dst, g, TGSIM_STORM_SYNACK | (uint32_t)((size_t)g * O + k), s->cfg.syn_bytes, trep);
+      x->flags |= 2u;
+      reply_pending = trep < dl;
+    }
+    x->t_synarr = SM_NONE;
+    uint8_t out = TGSIM_PROBE_NONE;
+    int64_t te = 0;
+    if (x->flags & 1u) { out = TGSIM_PROBE_REFUSED; te = x->t_start; }
+    else if (x->t_ackarr != SM_NONE && x->t_ackarr < dl) { out = TGSIM_PROBE_OK; te = x->t_ackarr; }
+    else if (dl < t_end && !reply_pending) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
+    if (out != TGSIM_PROBE_NONE) {
+      x->state = SM_DONE; x->res = out; x->t_done = te;
+      s->slot_t[(size_t)g * C + x->slot] = te;
+    } else {
+      ++*act; ++*waiting;
+      if (dl < *dl_min) *dl_min = dl;
+    }
+  }
+  if (s->tcp && t_end > H) H = t_end;  /* TCP: the reaction saw the previous dial end at the window's end */
+  uint32_t q = s->dq[g];
+  while (q < O) {
+    uint32_t best = C;
+    int64_t bt = SM_BUSY;
+    for (uint32_t j = 0; j < C; ++j)
+      if (s->slot_t[(size_t)g * C + j] < bt) { bt = s->slot_t[(size_t)g * C + j]; best = j; }
+    if (best == C) break;
+    const uint32_t k = s->order[(size_t)g * O + q];
+    ostorm_conn* x = &cn[k];
+    int64_t t0 = x->t_ready;
+    if (bt > t0) t0 = bt;
+    if (H > t0) t0 = H;
+    if (t0 >= t_end + s->cfg.window_ns) { if (t0 < *ns_min) *ns_min = t0; break; }
+    s->slot_t[(size_t)g * C + best] = SM_BUSY;
+    x->slot = best; x->state = SM_WAIT; x->t_start = t0; x->flags = 0;
+    ++*act; ++*waiting;
+    ++q;
+    if (s->tcp) {  /* the SYN: a bare segment written on the connection */
+      const uint64_t h = (uint64_t)g * O + k;
+      sm_link(c, h, s->S0 + (uint32_t)h * s->spcon, 1, t0);
+      s->wsegs[h] = 1;
+      continue;
+    }
+    x->t_synarr = x->t_ackarr = SM_NONE;
+    pr_stage(b, g, x->dst, TGSIM_STORM_SYN | k, s->cfg.syn_bytes, t0);
+    if (t0 + timeout < *dl_min) *dl_min = t0 + timeout;
+  }
+  s->dq[g] = q;
+  *act += O - q;
+}
+
+static uint32_t sm_payload(const ostorm* s, uint32_t j) {
+  return j + 1 < s->nchunks ? s->cfg.chunk_bytes : (uint32_t)(s->cfg.data_bytes - (uint64_t)j * s->cfg.chunk_bytes);
+}
+/* conn.Write of the connection's next chunk at t (the buffer had room) */
+static uint32_t sm_nseg(const tgo_ctx* c, const ostorm* s, uint32_t j) {
+  return (sm_payload(s, j) + c->tcp.mss - 1) / c->tcp.mss;
+}
+static void sm_write(tgo_ctx* c, uint32_t g, uint32_t k, int64_t t, pbuf* b) {
+  ostorm* s = c->sm;
+  const uint64_t h = (uint64_t)g * s->O + k;
+  ostorm_conn* x = &s->conn[h];
+  const uint32_t j = s->nchunks - x->rem;
+  if (s->tcp) {  /* its segments after the previous write's last one */
+    const uint32_t first = s->S0 + (uint32_t)h * s->spcon + 1 + j * s->spc, n = sm_nseg(c, s, j);
+    sm_link(c, h, first, n, t);
+    s->wsegs[h] += n;
+  } else {
+    pr_stage(b, g, x->dst, TGSIM_STORM_DATA | (k * s->nchunks + j), sm_payload(s, j) + s->cfg.header_bytes, t);
+    x->infl++;
+  }
+  x->rem--;
+  s->written++; s->bytes += sm_payload(s, j);
+}
+/* conn.Write of connection (g, k)'s next chunk fits: message mode, the buffer's `msg_window` chunks;
+ * TCP, 2 x cwnd segments minus those written and not ACKed, one chunk per reaction */
+static int sm_room(tgo_ctx* c, const ostorm* s, uint64_t h, uint32_t wrote_now) {
+  const ostorm_conn* x = &s->conn[h];
+  if (!s->tcp) return x->infl < s->cfg.msg_window;
+  if (wrote_now) return 0;
+  const int64_t buffered = (int64_t)s->wsegs[h] - (int64_t)c->tc[h].acked;
+  return 2 * (int64_t)c->tc[h].cwnd - buffered >= (int64_t)sm_nseg(c, s, s->nchunks - x->rem);
+}
+/* Write phase of instance g at t: one writesem round (storm.go:158-183). */
+static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act) {
+  ostorm* s = c->sm;
+  const uint32_t O = s->O, C = s->C, Hc = C < O ? C : O, win = s->cfg.msg_window;
+  ostorm_conn* cn = s->conn + (size_t)g * O;
+  uint32_t* ring = s->ring + (size_t)g * O;
+  uint32_t* hold = s->hold + (size_t)g * Hc;
+  uint32_t qh = s->qh[g], ql = s->ql[g], nh = s->nh[g], wrote = 0;
+  uint8_t now_[1024];  /* TCP: connections written in this round (one chunk per reaction) */
+  uint8_t* now = O <= sizeof(now_) ? now_ : (uint8_t*)malloc(O);
+  memset(now, 0, O);
+  (void)win;
+  if (s->tcp) {  /* settle the written chunks in order from their write states */
+    for (uint32_t k = 0; k < O; ++k) {
+      const uint64_t h = (uint64_t)g * O + k;
+      const uint32_t written = s->nchunks - cn[k].rem;
+      while (s->settled[h] < written) {
+        const uint32_t st = c->tw[sm_wid(s, h, 1 + s->settled[h])].state;
+        if (st == TGSIM_TCP_PENDING) break;
+        if (st == TGSIM_TCP_DELIVERED) s->delivered++;
+        else { s->failed_chunks++; s->failed[g] = 1; }
+        s->settled[h]++;
+      }
+    }
+  }
+  int progress = 1;
+  while (progress) {
+    progress = 0;
+    uint32_t keep = 0;
+    for (uint32_t i = 0; i < nh; ++i) {  /* blocked writers whose buffer drained */
+      const uint32_t k = hold[i];
+      if (sm_room(c, s, (uint64_t)g * O + k, now[k])) {
+        sm_write(c, g, k, t, b); now[k] = 1; ++wrote; progress = 1;
+        if (cn[k].rem) { ring[(qh + ql) % O] = k; ++ql; }
+      } else {
+        hold[keep++] = k;
+      }
+    }
+    nh = keep;
+    while (nh < C && ql > 0) {  /* free slots go to the queue's head */
+      const uint32_t k = ring[qh];
+      qh = (qh + 1) % O; --ql;
+      if (sm_room(c, s, (uint64_t)g * O + k, now[k])) {
+        sm_write(c, g, k, t, b); now[k] = 1; ++wrote; progress = 1;
+        if (cn[k].rem) { ring[(qh + ql) % O] = k; ++ql; }
+      } else {
+        hold[nh++] = k;
+      }
+    }
+  }
+  s->qh[g] = qh; s->ql[g] = ql; s->nh[g] = nh;
+  if (wrote) s->t_last[g] = t;
+  for (uint32_t k = 0; k < O; ++k) {
+    const uint64_t h = (uint64_t)g * O + k;
+    *act += (cn[k].rem || (s->tcp ? s->settled[h] < s->nchunks - cn[k].rem : cn[k].infl != 0)) ? 1u : 0u;
+  }
+  if (now != now_) free(now);
+}
+
+/* one reaction frame (H, t_end): every instance's step, then the proposal of the next window's end */
+static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* next_end, uint32_t* n_active) {
+  ostorm* s = c->sm;
+  pbuf b;
+  const size_t cap = s->phase ? (size_t)s->n_conn * s->cfg.msg_window + 1 : 2 * (size_t)s->n_conn + 1;
+  if (pr_alloc(&b, cap)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  int64_t dl = SM_NONE, ns = SM_NONE;
+  uint32_t act = 0, waiting = 0;
+  for (uint32_t g = 0; g < c->N; ++g) {
+    if (s->phase) sm_writes(c, g, t_end, &b, &act);
+    else sm_dials(c, g, resolve, H, t_end, &b, &dl, &ns, &act, &waiting);
+  }
+  int rc = pr_flush(c, &b);
+  if (rc) return rc;
+  /* TCP: the windows' room goes at the write times (tgo_tcp_write's release); the proposal looks
+   * at the staged packets before it, as the device does (its release runs after the reaction) */
+  const int staged_before = c->staged.n != 0;
+  if (s->tcp) {
+    ostage q = {0};
+    for (uint32_t k = 0; k < c->tc_n && !rc; ++k)
+      if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &q);
+    const int rc2 = ostage_flush(c, &q);
+    if (rc || rc2) return rc ? fail(c, rc, "oom") : rc2;
+  }
+  int64_t ne = t_end + s->cfg.window_ns;
+  if (!staged_before && !c->heap.n && act && (!s->tcp || !waiting)) {  /* idle: jump to the next deadline or dial */
+    int64_t cand = dl != SM_NONE ? dl + 1 : SM_NONE;
+    if (ns < cand) cand = ns;
+    if (cand != SM_NONE && cand > ne) ne = cand;
+  }
+  if (next_end) *next_end = ne;
+  if (n_active) *n_active = act;
+  return TGSIM_OK;
+}
+
+int tgo_storm_start(tgo_ctx* c) {
+  if (!c->sm) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->sm->phase != 0) return fail(c, TGSIM_ESTATE, "the storm's dials have started");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (react_owed(c)) return TGSIM_ESTATE;
+  return sm_step(c, 0, c->now, c->now, NULL, NULL);
+}
+
+int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  ostorm* s = c->sm;
+  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (!c->sm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react before storm_react");
+  c->sm_need_react = 0;
+  if (s->tcp) return sm_step(c, 1, c->horizon, c->now, next_end, n_active);  /* the TCP reaction settled the window */
+  const omsgs* st = &c->staged;
+  const uint32_t O = s->O;
+  /* 1. the window's packets: refused SYNs, chunks no copy of entered the egress queue */
+  for (size_t i = 0; i < c->n_status; ++i) {
+    const uint32_t sq = st->seq[i], tag = sq >> 30, code = c->status[i] & 0x0Fu;
+    if (tag == 1u) {
+      ostorm_conn* x = &s->conn[(size_t)st->src[i] * O + (sq & PR_MASK)];
+      if ((code == TGSIM_ST_DROPPED || code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) &&
+          x->state == SM_WAIT && x->dst == st->dst[i])
+        x->flags |= 1u;
+    } else if (tag == 2u && sm_failed_code(c->status[i])) {
+      s->conn[(size_t)st->src[i] * O + (sq & PR_MASK) / s->nchunks].infl--;
+      s->failed[st->src[i]] = 1;
+      s->failed_chunks++;
+    }
+  }
+  /* 2. the window's deliveries: first arrivals of SYNs and SYN-ACKs, the first copy of each chunk */
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    const uint32_t tag = r->seq >> 30;
+    if (tag == 1u) {
+      ostorm_conn* x = &s->conn[(size_t)r->src * O + (r->seq & PR_MASK)];
+      if (x->state == SM_WAIT && x->dst == r->dst && r->t < x->t_synarr) x->t_synarr = r->t;
+    } else if (tag == 3u) {
+      const size_t h = r->seq & PR_MASK;
+      if (h < s->n_conn && h / O == r->dst) {
+        ostorm_conn* x = &s->conn[h];
+        if (x->dst == r->src && x->state == SM_WAIT && (x->flags & 2u) && r->t < x->t_ackarr) x->t_ackarr = r->t;
+      }
+    } else if (tag == 2u) {
+      const uint32_t cj = r->seq & PR_MASK, k = cj / s->nchunks;
+      const size_t h = (size_t)r->src * O + k;
+      const uint64_t bit = (uint64_t)h * s->nchunks + (cj - k * s->nchunks);
+      if (!s->claim[bit]) { s->claim[bit] = 1; s->conn[h].infl--; s->delivered++; }
+    }
+  }
+  /* 3. per instance: dials or writes, then the proposal */
+  return sm_step(c, 1, c->horizon, c->now, next_end, n_active);
+}
+
+int tgo_storm_dials(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
+  ostorm* s = c->sm;
+  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if ((outcome || t_done) && cap < s->n_conn) return fail(c, TGSIM_ECAPACITY, "dial capacity");
+  for (uint64_t h = 0; h < s->n_conn; ++h) {
+    if (outcome) outcome[h] = s->conn[h].res;
+    if (t_done) t_done[h] = s->conn[h].t_done;
+  }
+  return TGSIM_OK;
+}
+
+int tgo_storm_write_start(tgo_ctx* c, int64_t t0) {
+  ostorm* s = c->sm;
+  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (s->phase != 0) return fail(c, TGSIM_ESTATE, "the write phase has started");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (react_owed(c)) return TGSIM_ESTATE;
+  if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
+  for (uint64_t h = 0; h < s->n_conn; ++h)
+    if (s->conn[h].res != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %llu has not dialled successfully", (unsigned long long)h);
+  s->phase = 1;
+  for (uint32_t g = 0; g < c->N; ++g) {
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < s->O; ++k) {
+      ostorm_conn* x = &s->conn[(size_t)g * s->O + k];
+      x->rem = s->nchunks; x->infl = 0;
+      if (s->nchunks) s->ring[(size_t)g * s->O + n++] = k;
+    }
+    s->qh[g] = 0; s->ql[g] = n; s->nh[g] = 0;
+  }
+  return sm_step(c, 0, t0, t0, NULL, NULL);
+}
+
+int tgo_storm_results(tgo_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot) {
+  ostorm* s = c->sm;
+  if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if ((failed || t_last) && cap < c->nloc) return fail(c, TGSIM_ECAPACITY, "result capacity");
+  for (uint32_t g = 0; g < c->nloc; ++g) {
+    uint8_t f = s->failed[g];
+    for (uint32_t k = 0; k < s->O; ++k) {
+      const uint64_t h = (uint64_t)g * s->O + k;
+      const ostorm_conn* x = &s->conn[h];
+      f |= (s->phase == 1 && x->rem) ? 1 : 0;
+      f |= (s->tcp ? (s->phase == 1 && s->settled[h] < s->nchunks - x->rem) : x->infl != 0) ? 1 : 0;
+    }
+    if (failed) failed[g] = f;
+    if (t_last) t_last[g] = s->t_last[g];
+  }
+  if (tot) {
+    memset(tot, 0, sizeof(*tot));
+    tot->chunks_written = s->written; tot->chunks_delivered = s->delivered;
+    tot->chunks_failed = s->failed_chunks; tot->bytes_written = s->bytes;
+    for (uint64_t h = 0; h < s->n_conn; ++h) {
+      const ostorm_conn* x = &s->conn[h];
+      tot->dials_ok += x->res == TGSIM_PROBE_OK;
+      tot->dials_failed += x->res == TGSIM_PROBE_REFUSED || x->res == TGSIM_PROBE_TIMEOUT;
+      tot->dials_pending += x->res == TGSIM_PROBE_NONE;
+      tot->conns_writing += s->phase == 1 && (x->rem || (s->tcp ? s->settled[h] < s->nchunks - x->rem : x->infl != 0));
+    }
+  }
+  return TGSIM_OK;
+}
+
+int tgo_storm_end(tgo_ctx* c) {
+  if (!c->sm) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
+  if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  sm_free(c);
+  return TGSIM_OK;
+}
+

@@ -56,6 +56,10 @@ struct TopicIndex {
 // retransmission scheduled (the current one is released at the next window start, survivors move
 // to the other), and counters.
 constexpr int kTcpArriveBlocks = 2048;  // k_tcp_arrive's grid (= TcpDev::part entries)
+// the segment word and chains, shared with the storm reactor's writes on connections
+constexpr uint32_t kTcpSoleSeg = 0x80000000u;  // s_w: the segment is its write's only one
+constexpr uint32_t kTcpWMask = 0x0FFFFFFFu;    // s_w: the write
+constexpr uint32_t kTcpNoSeg = 0xFFFFFFFFu;    // end of a connection's segment chain
 constexpr uint32_t kTcpBatches = 1u << 14;  // acks mode: ring of attempt-0 timer batches (one per window)
 // acks mode: the segments first sent in one window, [lo, hi), their timers in [t_lo, t_hi)
 struct TcpBatch {
@@ -140,7 +144,8 @@ struct StormScalars {
   int64_t min_dl;                 // running min of waiting dials' deadlines (k_storm_step)
   int64_t next_start;             // running min of the start times of admitted dials not yet due
   uint32_t active, n_active;      // connections dialling / writing (k_storm_step -> snapshot)
-  uint32_t done, pad;             // k_storm_step workgroups finished (the last proposes the window end)
+  uint32_t done, waiting;         // k_storm_step workgroups finished (the last proposes the window end);
+                                  // dials holding a semaphore slot
   unsigned long long written, delivered, failed, bytes;  // chunks (cumulative)
 };
 struct StormDev {
@@ -149,6 +154,12 @@ struct StormDev {
   uint64_t data = 0;
   int64_t timeout = 0, window = 0;
   uint32_t n_conn = 0, phase = 0;  // phase 0: dials, 1: writes
+  // TCP mode: connection h is TCP connection h; its SYN write and chunk writes have
+  // ids reserved at setup - write W0 + h * (nchunks + 1) + j (j = 0 the SYN), segments from
+  // S0 + h * spcon (the SYN's, then spc per full chunk)
+  uint32_t tcp = 0, W0 = 0, S0 = 0, spcon = 0, spc = 0, mss = 0;
+  uint32_t* settled = nullptr;    // [n_conn] chunk writes settled (delivered or failed), in order
+  uint32_t* wsegs = nullptr;      // [n_conn] segments written (the SYN's included)
   // [n_conn]
   uint32_t* dst = nullptr;
   int64_t* t_ready = nullptr;
@@ -409,11 +420,13 @@ hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_
 // Storm plan reactor. start: the first dials (frame H = t_end = t_now); react: the window's statuses
 // and deliveries, then per instance its dials / writes (staged behind sc->n_msgs_dev, set from
 // base_host unless base_dev) and the next window's proposed end (StormScalars::next_end).
-hipError_t launch_storm_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t_now);
-hipError_t launch_storm_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+hipError_t launch_storm_start(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, int64_t t_now);
+hipError_t launch_storm_react(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev);
 // the write phase: every connection queued on its instance's writesem, first round at t0
-hipError_t launch_storm_write_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t0);
+hipError_t launch_storm_write_start(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, int64_t t0);
+// TCP mode: the reserved writes' and segments' static fields (sources, sizes, chains inside a write)
+hipError_t launch_storm_tcp_init(Dev& d, const TcpDev& td);
 
 // Batched Subscribe (tgsim_sync_subscribe_device): per-subscriber counts into cnt[0..n] (u64 scratch),
 // exclusive scan into offsets[0..n], then (entries != nullptr) the entry ids, at most entries_cap.

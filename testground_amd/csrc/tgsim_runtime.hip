@@ -1698,10 +1698,11 @@ static int tgsim_sync_signal_body(tgsim_ctx* c, const uint32_t* states, const ui
   return signal_local(c, states, inst, t, n, seq_out);
 }
 
+static int signal_submit(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
+                         uint32_t* seq_out);
 static int signal_local(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
                         uint32_t* seq_out) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "signal inside a window");
-  if (n > c->d.s_cap) return fail(c, TGSIM_ECAPACITY, "signal batch larger than %u", c->d.s_cap);
   if (c->sig_log_used + n > c->d.max_signals) return fail(c, TGSIM_ECAPACITY, "signal log full");
   if (c->st_last_h.size() < c->d.max_states) c->st_last_h.resize(c->d.max_states, INT64_MIN);
   for (size_t i = 0; i < n; ++i) {
@@ -1710,6 +1711,36 @@ static int signal_local(tgsim_ctx* c, const uint32_t* states, const uint32_t* in
     if (t[i] < c->st_last_h[states[i]]) return fail(c, TGSIM_ECAUSALITY, "signal %zu goes back in time", i);
   }
   for (size_t i = 0; i < n; ++i) c->st_last_h[states[i]] = std::max(c->st_last_h[states[i]], t[i]);
+  if (n <= c->d.s_cap) return signal_submit(c, states, inst, t, n, seq_out);
+  // A batch larger than the device batch (the storm's N * outgoing dial signals): in (t, instance)
+  // order - the order sequence numbers follow inside a batch - cut into consecutive device batches,
+  // so every state's signals get the numbers one batch would give them, and no cut goes back in time.
+  alloc_point(c);
+  std::vector<uint32_t> ord(n);
+  for (size_t i = 0; i < n; ++i) ord[i] = (uint32_t)i;
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+    return t[a] != t[b] ? t[a] < t[b] : inst[a] < inst[b];
+  });
+  const size_t cap = c->d.s_cap;
+  std::vector<uint32_t> bs(cap), bi(cap), bq(cap);
+  std::vector<int64_t> bt(cap);
+  for (size_t a = 0; a < n; a += cap) {
+    const size_t m = std::min(cap, n - a);
+    for (size_t j = 0; j < m; ++j) {
+      const uint32_t i = ord[a + j];
+      bs[j] = states[i]; bi[j] = inst[i]; bt[j] = t[i];
+    }
+    const int rc = signal_submit(c, bs.data(), bi.data(), bt.data(), m, bq.data());
+    if (rc) return rc;
+    if (seq_out)
+      for (size_t j = 0; j < m; ++j) seq_out[ord[a + j]] = bq[j];
+  }
+  return TGSIM_OK;
+}
+
+// One device batch (n <= s_cap), validated by signal_local.
+static int signal_submit(tgsim_ctx* c, const uint32_t* states, const uint32_t* inst, const int64_t* t, size_t n,
+                         uint32_t* seq_out) {
   Dev& d = c->d;
   HIPCK(c, flush_storm(c), "storm commit");
   uint32_t kmin = UINT32_MAX, kmax = 0;
@@ -2125,13 +2156,14 @@ static int tgsim_probe_results_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_d
 // blocking on the send buffer, for every instance on the device. Kernels in tgsim_storm.hip, oracle
 // twin tgo_storm_*.
 
+static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* out);
 static void storm_free(tgsim_ctx* c) {
   StormDev& s = c->d.sm;
   for (void* q : {(void*)s.dst, (void*)s.t_ready, (void*)s.state, (void*)s.flags, (void*)s.res, (void*)s.slot,
                   (void*)s.t_start, (void*)s.t_synarr, (void*)s.t_ackarr, (void*)s.t_done, (void*)s.t_rep,
                   (void*)s.emit, (void*)s.rem, (void*)s.infl, (void*)s.order, (void*)s.ring, (void*)s.claim,
                   (void*)s.dq, (void*)s.qh, (void*)s.ql, (void*)s.nh, (void*)s.slot_t, (void*)s.hold,
-                  (void*)s.failed, (void*)s.t_last, (void*)s.sc})
+                  (void*)s.failed, (void*)s.t_last, (void*)s.sc, (void*)s.settled, (void*)s.wsegs})
     dfree(c, q);
   s = StormDev{};
   c->storm_on = false;
@@ -2150,8 +2182,10 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
     return fail(c, TGSIM_EINVAL, "bad storm configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
-  if (c->tcp_on || !c->fl_off.empty() || c->probes)
-    return fail(c, TGSIM_ESTATE, "the storm reactor runs in message mode, without a flood graph or probes");
+  if (!c->fl_off.empty() || c->probes)
+    return fail(c, TGSIM_ESTATE, "the storm reactor runs without a flood graph or probes");
+  if (c->tcp_on && (!c->tcp.acks || c->td.n_conn || c->tw_n))
+    return fail(c, TGSIM_ESTATE, "a TCP storm needs acks = 1 and a context without connections or writes yet");
   const uint64_t n_conn = (uint64_t)c->N * cfg->outgoing;
   const uint64_t nchunks = (cfg->data_bytes + cfg->chunk_bytes - 1) / cfg->chunk_bytes;
   if (n_conn > 0x3FFFFFFFull || nchunks * cfg->outgoing > 0x3FFFFFFFull)
@@ -2161,6 +2195,19 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
   for (uint64_t h = 0; h < n_conn; ++h) {
     if (dst[h] >= c->N) return fail(c, TGSIM_EINVAL, "connection %llu: bad peer", (unsigned long long)h);
     if (t_ready[h] < c->now) return fail(c, TGSIM_ECAUSALITY, "connection %llu: t_ready before now", (unsigned long long)h);
+  }
+  // TCP mode: connection h = instance * outgoing + k; its SYN write and its chunks' writes get ids
+  // reserved now, so the device writes them with no host bookkeeping
+  uint64_t spc = 0, spcon = 0, tot_w = 0, tot_s = 0;
+  if (c->tcp_on) {
+    const uint64_t mss = c->td.mss, last = nchunks ? cfg->data_bytes - (nchunks - 1) * cfg->chunk_bytes : 0;
+    spc = (cfg->chunk_bytes + mss - 1) / mss;
+    spcon = 1 + (nchunks ? (nchunks - 1) * spc + (last + mss - 1) / mss : 0);
+    tot_w = n_conn * (nchunks + 1);
+    tot_s = n_conn * spcon;
+    if (n_conn > c->tcp.max_writes || tot_w > c->tcp.max_writes || tot_s > c->tcp.max_segments)
+      return fail(c, TGSIM_ECAPACITY, "TCP storm: %llu writes / %llu segments exceed the TCP capacities",
+                  (unsigned long long)tot_w, (unsigned long long)tot_s);
   }
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   storm_free(c);
@@ -2184,7 +2231,8 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
       dalloc(c, &s.rem, nc) || dalloc(c, &s.infl, nc) || dalloc(c, &s.order, nc) || dalloc(c, &s.ring, nc) ||
       dalloc(c, &s.claim, claim_words) || dalloc(c, &s.dq, nl) || dalloc(c, &s.qh, nl) || dalloc(c, &s.ql, nl) ||
       dalloc(c, &s.nh, nl) || dalloc(c, &s.slot_t, nl * C) || dalloc(c, &s.hold, nl * Hc) ||
-      dalloc(c, &s.failed, nl) || dalloc(c, &s.t_last, nl) || dalloc(c, &s.sc, 1)) {
+      dalloc(c, &s.failed, nl) || dalloc(c, &s.t_last, nl) || dalloc(c, &s.sc, 1) ||
+      (c->tcp_on && (dalloc(c, &s.settled, nc) || dalloc(c, &s.wsegs, nc)))) {
     storm_free(c);
     return TGSIM_ENOMEM;
   }
@@ -2216,8 +2264,37 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
   s.window = cfg->window_ns;
   s.n_conn = (uint32_t)n_conn;
   s.phase = 0;
+  if (c->tcp_on) {
+    std::vector<uint32_t> src(n_conn);
+    for (uint64_t h = 0; h < n_conn; ++h) src[h] = (uint32_t)(h / O);
+    int rc = tgsim_tcp_connect_body(c, src.data(), dst, n_conn, nullptr);  // connection ids 0 .. n_conn - 1
+    if (rc) { storm_free(c); return rc; }
+    s.tcp = 1;
+    s.mss = c->td.mss;
+    s.spc = (uint32_t)spc;
+    s.spcon = (uint32_t)spcon;
+    s.W0 = (uint32_t)c->tw_n;
+    s.S0 = (uint32_t)c->tsg_n;
+    HIPCK(c, hipMemsetAsync(s.settled, 0, nc * 4, st), "storm setup");
+    HIPCK(c, hipMemsetAsync(s.wsegs, 0, nc * 4, st), "storm setup");
+    HIPCK(c, launch_storm_tcp_init(c->d, c->td), "storm setup");
+    for (uint64_t h = 0; h < n_conn; ++h) c->conn_tail[h] = (uint32_t)(s.S0 + (h + 1) * spcon - 1);
+    c->tw_n += tot_w;
+    c->tsg_n += tot_s;
+    c->tcp_seg_batched = c->tsg_n;
+    c->tstats.writes += tot_w;
+    c->tstats.segments += tot_s;
+  }
   c->storm_on = true;
   c->storm_need_react = false;
+  return TGSIM_OK;
+}
+
+// TCP mode: what the connections' windows have room for leaves at the write times (the reactor's
+// writes were linked onto the queues; tgsim_tcp_write does the same after a host write)
+static int storm_tcp_release(tgsim_ctx* c) {
+  if (!c->d.sm.tcp) return TGSIM_OK;
+  HIPCK(c, launch_tcp_conn_release(c->d, c->td, false, c->tcp_cur, true, 0), "storm tcp release");
   return TGSIM_OK;
 }
 
@@ -2228,7 +2305,9 @@ static void storm_staged(tgsim_ctx* c) {
   const StormDev& s = c->d.sm;
   c->spec.valid = false;
   c->staged_dev = true;
-  if (s.phase == 0) {
+  if (s.tcp) {  // SYNs, then one chunk's segments per connection per reaction
+    c->win_m_extra += (uint64_t)s.O * (s.phase == 0 ? 1u : s.spc);
+  } else if (s.phase == 0) {
     c->win_m_extra += s.O;
     c->win_m_inbox = std::max<uint32_t>(c->win_m_inbox, 1u);
     c->win_inbox_max = std::max<uint64_t>(c->win_inbox_max, s.n_conn);
@@ -2248,9 +2327,9 @@ static int tgsim_storm_start_body(tgsim_ctx* c) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (int rc = react_owed(c)) return rc;
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
-  HIPCK(c, launch_storm_start(c->d, c->staged_dev, c->n_staged, c->now), "storm start");
+  HIPCK(c, launch_storm_start(c->d, c->td, c->staged_dev, c->n_staged, c->now), "storm start");
   storm_staged(c);
-  return TGSIM_OK;
+  return storm_tcp_release(c);
 }
 
 static int storm_read_scalars(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
@@ -2272,11 +2351,13 @@ static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_a
   if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->storm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react before tgsim_storm_react");
   const bool on_dev = c->n_status_last == kStatusOnDevice;
-  HIPCK(c, launch_storm_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+  HIPCK(c, launch_storm_react(c->d, c->td, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
                               on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
   storm_staged(c);
   c->storm_need_react = false;
+  if (int rc = storm_tcp_release(c)) return rc;
   if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
   return storm_read_scalars(c, next_end, n_active);
 }
@@ -2329,9 +2410,9 @@ static int tgsim_storm_write_start_body(tgsim_ctx* c, int64_t t0) {
   for (size_t h = 0; h < res.size(); ++h)
     if (res[h] != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %zu has not dialled successfully", h);
   c->d.sm.phase = 1;
-  HIPCK(c, launch_storm_write_start(c->d, c->staged_dev, c->n_staged, t0), "storm write start");
+  HIPCK(c, launch_storm_write_start(c->d, c->td, c->staged_dev, c->n_staged, t0), "storm write start");
   storm_staged(c);
-  return TGSIM_OK;
+  return storm_tcp_release(c);
 }
 
 static int tgsim_storm_results_body(tgsim_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot);
@@ -2349,13 +2430,20 @@ static int tgsim_storm_results_body(tgsim_ctx* c, uint8_t* failed, int64_t* t_la
   std::vector<uint32_t> infl(n), rem(n);
   std::vector<uint8_t> res(n), fl(c->nloc);
   if (n) {
-    HIPCK(c, hipMemcpy(infl.data(), s.infl, n * 4, hipMemcpyDeviceToHost), "storm results");
+    // "in flight": message mode, chunks in the buffer; TCP, written chunks not yet settled
+    if (s.tcp) {
+      HIPCK(c, hipMemcpy(infl.data(), s.settled, n * 4, hipMemcpyDeviceToHost), "storm results");
+      HIPCK(c, hipMemcpy(rem.data(), s.rem, n * 4, hipMemcpyDeviceToHost), "storm results");
+      for (size_t h = 0; h < n; ++h) infl[h] = s.phase == 1 ? (s.nchunks - rem[h]) - infl[h] : 0u;
+    } else {
+      HIPCK(c, hipMemcpy(infl.data(), s.infl, n * 4, hipMemcpyDeviceToHost), "storm results");
+    }
     HIPCK(c, hipMemcpy(rem.data(), s.rem, n * 4, hipMemcpyDeviceToHost), "storm results");
     HIPCK(c, hipMemcpy(res.data(), s.res, n, hipMemcpyDeviceToHost), "storm results");
   }
   if (c->nloc) HIPCK(c, hipMemcpy(fl.data(), s.failed, c->nloc, hipMemcpyDeviceToHost), "storm results");
   for (size_t h = 0; h < n; ++h)
-    if (infl[h]) fl[h / s.O] = 1;  // still in flight: it never arrived
+    if (infl[h] || (s.phase == 1 && rem[h])) fl[h / s.O] = 1;  // still in flight or unwritten
   if (failed) memcpy(failed, fl.data(), c->nloc);
   if (t_last && c->nloc) HIPCK(c, hipMemcpy(t_last, s.t_last, (size_t)c->nloc * 8, hipMemcpyDeviceToHost), "storm results");
   if (tot) {
@@ -2968,6 +3056,7 @@ extern "C" int tgsim_tcp_connect(tgsim_ctx* c, const uint32_t* src, const uint32
 }
 static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* out) {
   if (!c) return TGSIM_EINVAL;
+  if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->tw_n && !c->td.n_conn) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
@@ -3019,6 +3108,7 @@ static int tgsim_tcp_write_body(tgsim_ctx* c, const uint32_t* conn, const uint32
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
+  if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (n && (!conn || !size || !t_send)) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (c->now_from_device) { int rc = sync_and_check(c); if (rc) return rc; }
   TcpDev& td = c->td;

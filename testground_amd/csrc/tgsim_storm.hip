@@ -68,6 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
     s.sc->min_dl = kNone;
     s.sc->next_start = kNone;
     s.sc->active = 0;
+    s.sc->waiting = 0;
     s.sc->done = 0;
     if (set_base) sc->n_msgs_dev = base_host;  // nothing in this launch reads it
   }
@@ -118,26 +119,31 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
 }
 
 // per block: the minimum deadline / start time of its instances and the active count
-__device__ __forceinline__ void block_reduce(StormDev& s, int64_t dl, int64_t ns, uint32_t act) {
+__device__ __forceinline__ void block_reduce(StormDev& s, int64_t dl, int64_t ns, uint32_t act, uint32_t waiting) {
   __shared__ int64_t s_dl[kBlock / 64], s_ns[kBlock / 64];
-  __shared__ uint32_t s_n[kBlock / 64];
+  __shared__ uint32_t s_n[kBlock / 64], s_w[kBlock / 64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const int64_t y = __shfl_xor(dl, o), z = __shfl_xor(ns, o);
     dl = y < dl ? y : dl;
     ns = z < ns ? z : ns;
     act += (uint32_t)__shfl_xor(act, o);
+    waiting += (uint32_t)__shfl_xor(waiting, o);
   }
-  if (lane_id() == 0) { s_dl[threadIdx.x >> 6] = dl; s_ns[threadIdx.x >> 6] = ns; s_n[threadIdx.x >> 6] = act; }
+  if (lane_id() == 0) {
+    s_dl[threadIdx.x >> 6] = dl; s_ns[threadIdx.x >> 6] = ns; s_n[threadIdx.x >> 6] = act; s_w[threadIdx.x >> 6] = waiting;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t m = s_dl[0], q = s_ns[0];
-    uint32_t n = s_n[0];
+    uint32_t n = s_n[0], wt = s_w[0];
     for (int w = 1; w < kBlock / 64; ++w) {
       m = s_dl[w] < m ? s_dl[w] : m;
       q = s_ns[w] < q ? s_ns[w] : q;
       n += s_n[w];
+      wt += s_w[w];
     }
+    if (wt) atomicAdd(&s.sc->waiting, wt);
     if (m != kNone) atomicMin(reinterpret_cast<long long*>(&s.sc->min_dl), (long long)m);
     if (q != kNone) atomicMin(reinterpret_cast<long long*>(&s.sc->next_start), (long long)q);
     if (n) atomicAdd(&s.sc->active, n);
@@ -149,12 +155,33 @@ __device__ __forceinline__ uint32_t chunk_payload(const StormDev& s, uint32_t j)
   return j + 1 < s.nchunks ? s.chunk : (uint32_t)(s.data - (uint64_t)j * s.chunk);
 }
 
-__device__ __forceinline__ void storm_end(StormDev& s, const DevScalars* sc, int64_t t_end);
+// TCP mode: the ids reserved at setup for connection h's SYN write and chunk c's
+// write, and the link of a write's segments onto the connection's send queue (what tgsim_tcp_write
+// and k_tcp_link do for a host write; one instance's thread owns its connections' queues)
+__device__ __forceinline__ uint32_t tcp_wid(const StormDev& s, size_t h, uint32_t j) {  // j = 0: the SYN
+  return s.W0 + (uint32_t)h * (s.nchunks + 1) + j;
+}
+__device__ __forceinline__ uint32_t tcp_syn_seg(const StormDev& s, size_t h) { return s.S0 + (uint32_t)h * s.spcon; }
+__device__ __forceinline__ uint32_t tcp_chunk_seg(const StormDev& s, size_t h, uint32_t c) {
+  return tcp_syn_seg(s, h) + 1 + c * s.spc;
+}
+__device__ __forceinline__ uint32_t tcp_nseg(const StormDev& s, uint32_t c) {
+  return (chunk_payload(s, c) + s.mss - 1) / s.mss;
+}
+__device__ __forceinline__ void tcp_link(TcpDev& t, size_t h, uint32_t prev, uint32_t first, uint32_t n, int64_t tw) {
+  for (uint32_t x = first; x < first + n; ++x) t.s_tatt[x] = tw;
+  if (prev != kTcpNoSeg) t.s_next[prev] = first;
+  if (t.c_head[h] == kTcpNoSeg) t.c_head[h] = first;
+  t.c_queued[h] += n;
+}
+
+__device__ __forceinline__ void storm_end(StormDev& s, const TcpDev& t, const DevScalars* sc, int64_t t_end);
 
 // Dial phase of instance l: resolve its waiting dials (react), then admit dials. Returns the messages
 // to stage (emit[h] bits); dl / ns / act: its reductions.
-__device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t g, bool resolve, int64_t H,
-                                              int64_t t_end, int64_t& dl_min, int64_t& ns_min, uint32_t& act) {
+__device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l, uint32_t g, bool resolve,
+                                              int64_t H, int64_t t_end, int64_t& dl_min, int64_t& ns_min,
+                                              uint32_t& act, uint32_t& waiting) {
   const uint32_t O = s.O, C = s.C;
   const size_t base = (size_t)g * O;
   uint32_t cnt = 0;
@@ -162,6 +189,25 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t 
     const size_t h = base + k;
     s.emit[h] = 0;
     if (!resolve || s.state[h] != kWait) continue;
+    if (s.tcp) {  // the SYN write: ACKed (connect() returned, seen at the window's end) or failed
+      uint8_t out = TGSIM_PROBE_NONE;
+      if (t.c_acked[h] >= 1) {
+        out = TGSIM_PROBE_OK;
+      } else {
+        const uint32_t ws = t.w_state[tcp_wid(s, h, 0)];
+        out = ws == TGSIM_TCP_TIMEOUT ? TGSIM_PROBE_TIMEOUT : ws == TGSIM_TCP_REFUSED ? TGSIM_PROBE_REFUSED : out;
+      }
+      if (out != TGSIM_PROBE_NONE) {
+        s.state[h] = kDone;
+        s.res[h] = out;
+        s.t_done[h] = t_end;
+        s.slot_t[(size_t)l * C + s.slot[h]] = t_end;
+      } else {
+        ++act;
+        ++waiting;
+      }
+      continue;
+    }
     const int64_t dl = s.t_start[h] + s.timeout;
     bool reply_pending = false;
     const int64_t sa = s.t_synarr[h];
@@ -187,10 +233,13 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t 
       s.slot_t[(size_t)l * C + s.slot[h]] = te;  // `<-sem`: the slot is free from the dial's end
     } else {
       ++act;
+      ++waiting;
       dl_min = dl < dl_min ? dl : dl_min;
     }
   }
   // the semaphore admits dials in FIFO order while a slot is free: dial at max(t_ready, slot free, H)
+  // (TCP: the window's end, when the reaction saw the previous dial's end)
+  if (s.tcp) H = t_end > H ? t_end : H;
   uint32_t q = s.dq[l];
   while (q < O) {
     uint32_t best = C;
@@ -213,15 +262,21 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t 
     s.slot[h] = best;
     s.state[h] = kWait;
     s.t_start[h] = t0;
+    ++act;
+    ++waiting;
+    ++q;
+    if (s.tcp) {  // the SYN: a bare segment written on the connection (the first on its queue)
+      tcp_link(t, h, kTcpNoSeg, tcp_syn_seg(s, h), 1, t0);
+      s.wsegs[h] = 1;
+      continue;
+    }
     s.flags[h] = 0;
     s.t_synarr[h] = kNone;
     s.t_ackarr[h] = kNone;
     s.emit[h] |= kEmitSyn;
     ++cnt;
-    ++act;
     const int64_t dl = t0 + s.timeout;
     dl_min = dl < dl_min ? dl : dl_min;
-    ++q;
   }
   s.dq[l] = q;
   act += O - q;  // asleep, not yet admitted
@@ -232,13 +287,45 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, uint32_t l, uint32_t 
 // semaphore in FIFO order; a conn.Write whose chunk fits the buffer returns and its goroutine queues
 // again for the next chunk, one that does not fit blocks holding its slot (the holders retry first,
 // in order). Returns the chunks written (emit[h] per connection).
-__device__ __forceinline__ uint32_t write_step(StormDev& s, uint32_t l, uint32_t g, uint32_t& act) {
+//   message mode: a connection's buffer holds `win` chunks that have neither arrived nor failed;
+//   TCP mode: conn.Write returns once the chunk's segments fit the socket buffer, 2 x cwnd segments
+//   (Linux autotunes sk_sndbuf to about twice the window [EXT]) minus those written and not yet
+//   ACKed - at most one chunk per connection per reaction, as the ACKs drain it window by window.
+// TCP mode also settles the connection's written chunks in order (delivered / failed, from the write
+// states) and links each new chunk's segments onto its send queue.
+__device__ __forceinline__ uint32_t write_step(StormDev& s, TcpDev& t, uint32_t l, uint32_t g, int64_t t_end,
+                                               uint32_t& act, unsigned long long& bytes, unsigned long long& dcnt,
+                                               unsigned long long& fcnt) {
   const uint32_t O = s.O, C = s.C, win = s.win;
   const size_t base = (size_t)g * O;
   uint32_t* ring = s.ring + base;
   uint32_t* hold = s.hold + (size_t)l * s.Hc;
   uint32_t qh = s.qh[l], ql = s.ql[l], nh = s.nh[l];
-  for (uint32_t k = 0; k < O; ++k) s.emit[base + k] = 0;
+  for (uint32_t k = 0; k < O; ++k) {
+    const size_t h = base + k;
+    s.emit[h] = 0;
+    if (!s.tcp) continue;
+    const uint32_t written = s.nchunks - s.rem[h];
+    uint32_t st = s.settled[h];
+    while (st < written) {
+      const uint32_t ws = t.w_state[tcp_wid(s, h, 1 + st)];
+      if (ws == TGSIM_TCP_PENDING) break;
+      if (ws == TGSIM_TCP_DELIVERED) {
+        ++dcnt;
+      } else {
+        ++fcnt;
+        s.failed[l] = 1;
+      }
+      ++st;
+    }
+    s.settled[h] = st;
+  }
+  auto room = [&](size_t h) -> bool {
+    if (!s.tcp) return s.infl[h] + s.emit[h] < win;
+    if (s.emit[h]) return false;
+    const int64_t buffered = (int64_t)s.wsegs[h] - (int64_t)t.c_acked[h];
+    return 2 * (int64_t)t.c_cwnd[h] - buffered >= (int64_t)tcp_nseg(s, s.nchunks - s.rem[h]);
+  };
   uint32_t cnt = 0;
   bool progress = true;
   while (progress) {
@@ -247,7 +334,7 @@ __device__ __forceinline__ uint32_t write_step(StormDev& s, uint32_t l, uint32_t
     for (uint32_t i = 0; i < nh; ++i) {  // blocked writers whose buffer drained
       const uint32_t k = hold[i];
       const size_t h = base + k;
-      if (s.infl[h] + s.emit[h] < win) {
+      if (room(h)) {
         s.emit[h] += 1;
         const uint32_t r = --s.rem[h];
         ++cnt;
@@ -263,7 +350,7 @@ __device__ __forceinline__ uint32_t write_step(StormDev& s, uint32_t l, uint32_t
       qh = (qh + 1) % O;
       --ql;
       const size_t h = base + k;
-      if (s.infl[h] + s.emit[h] < win) {
+      if (room(h)) {
         s.emit[h] += 1;
         const uint32_t r = --s.rem[h];
         ++cnt;
@@ -279,14 +366,26 @@ __device__ __forceinline__ uint32_t write_step(StormDev& s, uint32_t l, uint32_t
   s.nh[l] = nh;
   for (uint32_t k = 0; k < O; ++k) {
     const size_t h = base + k;
-    const uint32_t f = s.infl[h] + s.emit[h];
-    s.infl[h] = f;
-    act += (s.rem[h] || f) ? 1u : 0u;
+    const uint32_t e = s.emit[h];
+    const uint32_t j0 = s.nchunks - s.rem[h] - e;
+    for (uint32_t j = j0; j < j0 + e; ++j) bytes += chunk_payload(s, j);
+    if (s.tcp) {
+      if (e) {  // chunk j0 (one per reaction): its segments after the previous write's last one
+        const uint32_t first = tcp_chunk_seg(s, h, j0), n = tcp_nseg(s, j0);
+        tcp_link(t, h, j0 ? first - 1 : tcp_syn_seg(s, h), first, n, t_end);
+        s.wsegs[h] += n;
+      }
+      act += (s.rem[h] || s.settled[h] < s.nchunks - s.rem[h]) ? 1u : 0u;
+    } else {
+      const uint32_t f = s.infl[h] + e;
+      s.infl[h] = f;
+      act += (s.rem[h] || f) ? 1u : 0u;
+    }
   }
   return cnt;
 }
 
-__global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* sc, uint32_t lo, uint32_t nloc,
+__global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, TcpDev t, DevScalars* sc, uint32_t lo, uint32_t nloc,
                                                        uint32_t mode, int64_t H_host, int64_t tend_host, uint32_t cap,
                                                        uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
                                                        uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
@@ -301,15 +400,19 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* s
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < nloc; b0 += gridDim.x * kBlock) {  // block-uniform
     const uint32_t l = b0 + threadIdx.x;
     int64_t dl = kNone, ns = kNone;
-    uint32_t act = 0, cnt = 0;
+    uint32_t act = 0, waiting = 0, wrote = 0, cnt = 0;
+    unsigned long long bytes = 0, dcnt = 0, fcnt = 0;
     const uint32_t g = lo + l;
-    if (l < nloc) cnt = writes ? write_step(s, l, g, act) : dial_step(s, l, g, react, H, t_end, dl, ns, act);
-    if (writes && cnt && l < nloc) s.t_last[l] = t_end;
+    if (l < nloc) {
+      if (writes) wrote = write_step(s, t, l, g, t_end, act, bytes, dcnt, fcnt);
+      else cnt = dial_step(s, t, l, g, react, H, t_end, dl, ns, act, waiting);
+    }
+    if (wrote) s.t_last[l] = t_end;
+    if (!s.tcp) cnt += wrote;  // TCP: the connections' queues send them (k_tcp_conn_release)
     uint32_t tot;
     const uint32_t ex = block_excl_scan(cnt, red, tot);
     if (threadIdx.x == 0) sbase = tot ? reserve_staged(&sc->n_msgs_dev, tot, cap) : 0u;
     __syncthreads();
-    unsigned long long bytes = 0;
     if (cnt) {
       uint32_t w = sbase + ex;
       const size_t base = (size_t)g * O;
@@ -321,7 +424,6 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* s
           const uint32_t j0 = s.nchunks - s.rem[h] - e;
           for (uint32_t j = j0; j < j0 + e; ++j, ++w) {
             const uint32_t pay = chunk_payload(s, j);
-            bytes += pay;
             if (w < cap) {
               m_src[w] = g; m_dst[w] = s.dst[h]; m_seq[w] = TGSIM_STORM_DATA | (k * s.nchunks + j);
               m_size[w] = pay + s.hdr; m_t[w] = t_end;
@@ -353,10 +455,14 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* s
     }
     __syncthreads();  // sbase is rewritten by the next round
     if (writes) {
-      block_add(&s.sc->written, cnt, red64);
+      block_add(&s.sc->written, wrote, red64);
       block_add(&s.sc->bytes, bytes, red64);
+      if (s.tcp) {
+        block_add(&s.sc->delivered, dcnt, red64);
+        block_add(&s.sc->failed, fcnt, red64);
+      }
     }
-    block_reduce(s, dl, ns, act);
+    block_reduce(s, dl, ns, act, waiting);
   }
   // the last workgroup to finish proposes the next window's end
   __shared__ uint32_t s_last;
@@ -366,20 +472,24 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, DevScalars* s
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
     __threadfence();
-    storm_end(s, sc, t_end);
+    storm_end(s, t, sc, t_end);
   }
 }
 
 // every k_storm_step workgroup's reductions and reservations are done: read with device-scope atomic
 // loads (another XCD's L2 may hold the lines)
-__device__ __forceinline__ void storm_end(StormDev& s, const DevScalars* sc, int64_t t_end) {
+__device__ __forceinline__ void storm_end(StormDev& s, const TcpDev& t, const DevScalars* sc, int64_t t_end) {
   int64_t ne = t_end + s.window;
   const uint32_t act = __hip_atomic_load(&s.sc->active, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  // TCP: no jump while a dial waits for its ACK (its SYN may be waiting out a retransmission timer;
+  // with no dial waiting no timer is armed in the dial phase, and the write phase never jumps: it has
+  // no deadlines or starts)
+  const bool tcp_idle = !s.tcp || __hip_atomic_load(&s.sc->waiting, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0;
   const int64_t m = __hip_atomic_load(&s.sc->min_dl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t q = __hip_atomic_load(&s.sc->next_start, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t staged = __hip_atomic_load(const_cast<uint32_t*>(&sc->n_msgs_dev), __ATOMIC_ACQUIRE,
                                             __HIP_MEMORY_SCOPE_AGENT);
-  if (staged == 0 && sc->arena_used == 0 && act) {  // idle: jump to the next deadline or dial
+  if (staged == 0 && sc->arena_used == 0 && act && tcp_idle) {  // idle: jump to the next deadline or dial
     int64_t cand = m != kNone ? m + 1 : kNone;
     cand = q < cand ? q : cand;
     if (cand != kNone && cand > ne) ne = cand;
@@ -393,6 +503,7 @@ __global__ void k_storm_reset(StormDev s, DevScalars* sc, uint32_t set_base, uin
     s.sc->min_dl = kNone;
     s.sc->next_start = kNone;
     s.sc->active = 0;
+    s.sc->waiting = 0;
     s.sc->done = 0;
     if (set_base) sc->n_msgs_dev = base_host;
   }
@@ -406,11 +517,32 @@ __global__ __launch_bounds__(kBlock) void k_storm_write_init(StormDev s, uint32_
     for (uint32_t k = 0; k < s.O; ++k) {
       s.rem[base + k] = s.nchunks;
       s.infl[base + k] = 0;
+      if (s.tcp) s.settled[base + k] = 0;
       if (s.nchunks) s.ring[base + n++] = k;
     }
     s.qh[l] = 0;
     s.ql[l] = n;
     s.nh[l] = 0;
+  }
+}
+
+// TCP mode: the reserved writes (the SYN, then every chunk) and their segments, as tgsim_tcp_write
+// would build them; their times and links are set when they are written
+__global__ __launch_bounds__(kBlock) void k_storm_tcp_init(StormDev s, TcpDev t) {
+  for (uint32_t h = blockIdx.x * kBlock + threadIdx.x; h < s.n_conn; h += gridDim.x * kBlock) {
+    const uint32_t g = h / s.O, d = s.dst[h];
+    for (uint32_t j = 0; j <= s.nchunks; ++j) {
+      const uint32_t w = tcp_wid(s, h, j);
+      const uint32_t pay = j ? chunk_payload(s, j - 1) : 0u, n = j ? tcp_nseg(s, j - 1) : 1u;
+      const uint32_t first = j ? tcp_chunk_seg(s, h, j - 1) : tcp_syn_seg(s, h);
+      t.w_src[w] = g; t.w_dst[w] = d; t.w_rem[w] = n; t.w_conn[w] = h;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t x = first + i;
+        t.s_w[x] = w | (n == 1 ? kTcpSoleSeg : 0u);
+        t.s_wire[x] = (i + 1 < n ? s.mss : pay - i * s.mss) + t.hdr;
+        t.s_next[x] = i + 1 < n ? x + 1 : kTcpNoSeg;
+      }
+    }
   }
 }
 
@@ -420,31 +552,39 @@ unsigned grid_for(uint32_t n) {
 
 }  // namespace
 
-hipError_t launch_storm_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t_now) {
+hipError_t launch_storm_start(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, int64_t t_now) {
   hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
-  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
-                     (uint32_t)kModeStart, t_now, t_now, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, td, d.sc, d.lo,
+                     d.nloc, (uint32_t)kModeStart, t_now, t_now, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 
-hipError_t launch_storm_write_start(Dev& d, bool base_dev, uint32_t base_host, int64_t t0) {
+hipError_t launch_storm_write_start(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, int64_t t0) {
   hipLaunchKernelGGL(k_storm_write_init, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.lo, d.nloc);
   hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
-  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
-                     (uint32_t)kModeWrites, t0, t0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, td, d.sc, d.lo,
+                     d.nloc, (uint32_t)kModeWrites, t0, t0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 
-hipError_t launch_storm_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+hipError_t launch_storm_react(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev) {
   ProfScope ps_(d, KID_STORM);
   constexpr uint32_t nb = kStreamBlocks / 2;
-  hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
-                     n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, d.sm, nb,
-                     base_dev ? 0u : 1u, base_host);
-  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, d.sc, d.lo, d.nloc,
-                     (uint32_t)kModeReact, (int64_t)0, (int64_t)0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size,
-                     d.m_t);
+  if (d.sm.tcp)  // the TCP reaction has settled the window's packets and deliveries
+    hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
+  else
+    hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
+                       n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, d.sm, nb,
+                       base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, td, d.sc, d.lo,
+                     d.nloc, (uint32_t)kModeReact, (int64_t)0, (int64_t)0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq,
+                     d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_tcp_init(Dev& d, const TcpDev& td) {
+  hipLaunchKernelGGL(k_storm_tcp_init, dim3(grid_for(d.sm.n_conn)), dim3(kBlock), 0, d.stream, d.sm, td);
   return hipGetLastError();
 }
 

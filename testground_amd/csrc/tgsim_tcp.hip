@@ -35,14 +35,14 @@ namespace tgsim {
 namespace {
 
 constexpr uint32_t kArrived = 0xFFFFFFFFu;  // s_mark of a duplicated segment that has arrived (above every epoch)
-constexpr uint32_t kSoleSeg = 0x80000000u;  // s_w: the segment is its write's only one
-constexpr uint32_t kWMask = 0x0FFFFFFFu;    // s_w: the write
+constexpr uint32_t kSoleSeg = kTcpSoleSeg;  // s_w: the segment is its write's only one
+constexpr uint32_t kWMask = kTcpWMask;      // s_w: the write
 constexpr uint32_t kQShift = 28;            // s_w: copies of the current attempt (2 bits)
 constexpr uint32_t kRetxBit = 0x40000000u;  // s_w, acks mode: the segment was retransmitted (s_att > 0)
 constexpr uint32_t kPlanLds = 1024;         // k_tcp_fire: timer plans up to this many batches are searched in LDS
 constexpr uint32_t kFireRounds = 8;         // k_tcp_fire: rounds of entries per block reservation (mask bits)
 constexpr uint32_t kFireUnroll = 4;         // k_tcp_fire: entries whose loads are in flight together
-constexpr uint32_t kNoSeg = 0xFFFFFFFFu;    // connections: end of a segment chain / no connection
+constexpr uint32_t kNoSeg = kTcpNoSeg;      // connections: end of a segment chain / no connection
 constexpr uint32_t kCwndClamp = 65535u;    // Linux snd_cwnd_clamp (Reno window in segments)
 
 __device__ __forceinline__ uint32_t tcp_copies(uint8_t st) {

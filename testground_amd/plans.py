@@ -34,7 +34,6 @@ from .sync import SyncService
 
 TCP_OVERHEAD = 66          # Ethernet 14 + IPv4 20 + TCP 20 + timestamp option 12 bytes per segment
 TCP_CHUNK = 4 * 1024       # storm.go:23 write size
-T_MSS = 1448               # tgsim_tcp_config.mss default
 NEVER = np.iinfo(np.int64).max
 
 
@@ -511,39 +510,6 @@ STORM_CTX_NS = 3000 * SECOND          # context.WithTimeout(..., 3000*time.Secon
 STORM_MSG_WINDOW = 10                 # message mode: writes a connection keeps in flight (IW10's segments)
 
 
-def _writesem_round(g_queue, holders, room, remaining, limit, emit):
-    """One instant of storm.go:158-183 for one instance: goroutines take the write semaphore in
-    FIFO order (`writesem <- struct{}{}`); conn.Write returns once the connection's buffer has
-    room, else the goroutine blocks holding its slot. emit(conn) sends one chunk. Runs until no
-    goroutine can progress; returns the chunks written."""
-    wrote, progress = 0, True
-    while progress:
-        progress = False
-        for h in list(holders):                       # blocked writers whose buffer drained
-            if room[h] > 0:
-                holders.remove(h)
-                room[h] -= 1
-                remaining[h] -= 1
-                emit(h)
-                wrote += 1
-                progress = True
-                if remaining[h]:
-                    g_queue.append(h)
-        while len(holders) < limit and g_queue:
-            h = g_queue.popleft()
-            if room[h] > 0:
-                room[h] -= 1
-                remaining[h] -= 1
-                emit(h)
-                wrote += 1
-                progress = True
-                if remaining[h]:
-                    g_queue.append(h)
-            else:
-                holders.append(h)
-    return wrote
-
-
 def storm(env: PlanEnv) -> np.ndarray:
     """plans/benchmarks/storm.go:31-197: every instance dials `conn_outgoing` random peers, each
     after U[0, conn_delay_ms) ms and under a semaphore of `concurrent_dials` (storm.go:141-152:
@@ -561,7 +527,6 @@ def storm(env: PlanEnv) -> np.ndarray:
     [EXT]) and drains as ACKs arrive; a write fails on a timeout or a reset. A failed dial never
     signals, so "outgoing-dials-done" cannot release and the run fails at its 3000 s context, as
     in the reference."""
-    from collections import deque
     n = env.n
     outgoing = env.int_param("conn_outgoing", 5)
     delay_ms = env.int_param("conn_delay_ms", 30000)
@@ -576,88 +541,10 @@ def storm(env: PlanEnv) -> np.ndarray:
     off = rng.integers(1, n, len(src)) if n > 1 else np.zeros(len(src), np.int64)
     dst = (src + off) % n                                           # rand.Intn over the other nodes
     t_ready = env.sim.now + rng.integers(0, max(delay_ms, 1), len(src)) * MS
-    chunks = [TCP_CHUNK] * (size // TCP_CHUNK) + ([size % TCP_CHUNK] if size % TCP_CHUNK else [])
-    m = len(src)
     env.bytes_sent = 0
     if env.tcp and not env.tcp_acks:
         raise ValueError("storm over TCP writes into connections: it needs tcp_acks = true (the ACK clock)")
-    if not env.tcp:
-        return _storm_device(env, dst, t_ready, outgoing, limit, size)
-    conn = env.sim.tcp_connect(src, dst)
-    ok, t_dial = _tcp_dials(env, conn, src, dst, t_ready, limit)
-    env.dials_ok = int(ok.sum())
-    res = np.ones(n, bool)
-    if not ok.all():
-        for i in np.flatnonzero(~ok)[:5]:
-            env.fail(f"instance {src[i]}: couldnt dial {dst[i]}")
-        env.fail("outgoing-dials-done never released (a failed dial does not signal): context deadline exceeded")
-        res[:] = False
-        return res
-    _, t_b = env.sync.signal_and_wait("outgoing-dials-done", src, t_dial, n * outgoing)
-    env.advance_to(max(t_b, env.sim.now))
-    # the write phase: per instance its goroutines (one per connection) in dial order
-    remaining = np.full(m, len(chunks), np.int64)
-    queues = {g: deque(np.flatnonzero(src == g).tolist()) for g in range(n)}
-    holders = {g: [] for g in range(n)}
-    keys, wrote_at = [], []
-    seg_per_chunk = np.array([max(1, -(-c // T_MSS)) for c in chunks], np.int64)
-    written_segs = np.zeros(m, np.int64)
-    last_return = np.full(n, int(t_b), np.int64)
-    while True:
-        now = env.sim.now
-        if env.tcp:
-            cs = env.sim.tcp_conns(int(conn[0]), m)
-            buffered = written_segs - cs["acked"].astype(np.int64)
-            room_segs = 2 * cs["cwnd"].astype(np.int64) - buffered
-            nxt = np.array([seg_per_chunk[len(chunks) - r] if r else 1 for r in remaining])
-            room = np.where(room_segs >= nxt, 1, 0)      # conn.Write blocks until the chunk fits
-        else:
-            inflight = np.zeros(m, np.int64)
-            if keys:
-                k = np.concatenate(keys)
-                who = np.concatenate(wrote_at)
-                arr = env.arrival_of(k)
-                st = env.status_of(k) & 0x0F
-                gone = (arr != NEVER) | ((st != 0x0F) & (st != A.ST_QUEUED) & (st != A.ST_LOCAL))
-                np.add.at(inflight, who[~gone], 1)
-            room = STORM_MSG_WINDOW - inflight
-        room = room.tolist()
-        batch_c, batch_z = [], []
-
-        def emit(h):
-            c = chunks[len(chunks) - remaining[h] - 1]
-            batch_c.append(h)
-            batch_z.append(c)
-        for g in range(n):
-            if _writesem_round(queues[g], holders[g], room, remaining, limit, emit):
-                last_return[g] = now
-        if batch_c:
-            bc = np.array(batch_c, np.int64)
-            if env.tcp:
-                written_segs_add = np.array([max(1, -(-z // T_MSS)) for z in batch_z], np.int64)
-                np.add.at(written_segs, bc, written_segs_add)
-                keys.append(env.tcp_write(conn[bc], batch_z, now, src[bc], dst[bc]))
-            else:
-                keys.append(env.send(src[bc], dst[bc], np.array(batch_z) + TCP_OVERHEAD, now))
-                wrote_at.append(bc)
-            env.bytes_sent += int(sum(batch_z))
-        if not remaining.any():
-            break
-        if env.sim.now > STORM_CTX_NS:
-            env.fail("writes still blocked at the 3000 s context")
-            return np.zeros(n, bool)
-        env.step()
-    # wg.Wait(): the last conn.Write of each instance returned; then SignalAndWait("done writing", N)
-    _, t = env.sync.signal_and_wait("done writing", np.arange(n), last_return, n)
-    # the written data drains (the plan's time.Sleep(10 s) after the barrier); a lost chunk (message
-    # mode) or a failed write (TCP) fails its writer
-    allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
-    arr = env.wait(allk, 10 * SECOND + max(0, t - env.sim.now))
-    lost = (allk[arr == NEVER] >> np.uint64(32)).astype(np.int64)
-    res[lost] = False
-    env.delivered_chunks = int((arr != NEVER).sum())
-    env.overlimit = int(env.sim.stats()["overlimit"])
-    return res
+    return _storm_device(env, dst, t_ready, outgoing, limit, size)
 
 
 def _storm_windows(env: PlanEnv, t_first: int, deadline: int) -> bool:
@@ -668,6 +555,8 @@ def _storm_windows(env: PlanEnv, t_first: int, deadline: int) -> bool:
     while True:
         env.sim.advance(ne)
         env.storm_windows += 1
+        if env.tcp:
+            env.sim.tcp_react(wait=False)   # segments, ACKs, timers and the windows' ACK clock
         ne, act = env.sim.storm_react()
         if act == 0:
             return True
@@ -676,10 +565,12 @@ def _storm_windows(env: PlanEnv, t_first: int, deadline: int) -> bool:
 
 
 def _storm_device(env: PlanEnv, dst, t_ready, outgoing: int, limit: int, size: int) -> np.ndarray:
-    """The message-mode storm on the device reactor (tgsim_storm_*): dials under
-    `sem` with DialTimeout (storm.go:141-152), SignalAndWait("outgoing-dials-done", N * outgoing)
-    (:156), then 4 KiB conn.Writes under `writesem` (:158-183), each connection's send buffer holding
-    STORM_MSG_WINDOW chunks; SignalAndWait("done writing", N) at each instance's last write (:190)."""
+    """The storm on the device reactor (tgsim_storm_*): dials under `sem` with
+    DialTimeout (storm.go:141-152), SignalAndWait("outgoing-dials-done", N * outgoing) (:156), then
+    4 KiB conn.Writes under `writesem` (:158-183), each connection's send buffer holding
+    STORM_MSG_WINDOW chunks (message mode) or 2 x cwnd segments (TCP mode: connections, the SYN a
+    bare segment whose ACK completes the dial); SignalAndWait("done writing", N) at each instance's
+    last write (:190)."""
     n, sim = env.n, env.sim
     env.storm_windows = 0
     sim.storm_setup(dst, t_ready, outgoing=outgoing, concurrent=limit, data_bytes=size, chunk_bytes=TCP_CHUNK,
@@ -716,57 +607,6 @@ def _storm_device(env: PlanEnv, dst, t_ready, outgoing: int, limit: int, size: i
     env.sync.signal_and_wait("done writing", np.arange(n), t_last, n)
     env.overlimit = int(sim.stats()["overlimit"])
     return ~failed
-
-
-def _tcp_dials(env: PlanEnv, conn, src, dst, t_ready, limit: int):
-    """TCP mode dials: the SYN is a bare segment on the connection, written when the dial gets its
-    semaphore slot; its ACK, seen at the end of the window it arrives in, completes the dial; a
-    refused or timed-out SYN fails it."""
-    m = len(conn)
-    ok = np.zeros(m, bool)
-    t_done = np.full(m, NEVER, np.int64)
-    started = np.zeros(m, bool)
-    syn = np.zeros(m, np.uint64)
-    waiting = {}
-    for i in np.lexsort((np.arange(m), t_ready)):
-        waiting.setdefault(int(src[i]), []).append(int(i))
-    free = {g: [-(1 << 62)] * limit for g in waiting}
-    t_start = np.full(m, NEVER, np.int64)
-    while True:
-        now = env.sim.now
-        for g, q in waiting.items():
-            fr = free[g]
-            while q and fr:
-                fr.sort()
-                t0 = max(int(t_ready[q[0]]), fr[0], now)
-                if t0 >= now + env.window_ns:     # not in the next window: the writer still sleeps
-                    break
-                i = q.pop(0)
-                fr.pop(0)
-                t_start[i] = t0
-                started[i] = True
-                syn[i] = env.tcp_write(conn[[i]], [0], t0, src[[i]], dst[[i]])[0]
-        act = started & (t_done == NEVER)
-        if not act.any() and not any(waiting.values()):
-            break
-        if not act.any() and not env._pend and env.sim.stats()["inflight"] == 0:
-            # every dialler still sleeps (conn_delay_ms): jump to the first wake-up
-            nxt = min(max(int(t_ready[q[0]]), min(free[g])) for g, q in waiting.items() if q and free[g])
-            if nxt > now + env.window_ns:
-                env.advance_to(nxt)
-                continue
-        env.step()
-        cs = env.sim.tcp_conns(int(conn[0]), m)
-        got = act & (cs["acked"] >= 1)
-        st = env.status_of(syn) & 0x0F
-        failed = act & ~got & started & (st != 0x0F)
-        for i in np.flatnonzero(got):
-            ok[i], t_done[i] = True, env.sim.now
-            free[int(src[i])].append(int(env.sim.now))
-        for i in np.flatnonzero(failed):
-            t_done[i] = env.sim.now
-            free[int(src[i])].append(int(env.sim.now))
-    return ok, t_done
 
 
 def barrier_bench(env: PlanEnv) -> np.ndarray:

@@ -276,3 +276,141 @@ def test_storm_plan_20k_hip_matches_oracle(hip, oracle):
     for k in ("now", "totals", "windows", "stats"):
         assert a[k] == b[k], k
     assert a["totals"]["chunks_delivered"] == 20_000 * 5 * 2
+
+
+def _big_signal_batch(b, n=150_000):
+    """A signal batch larger than the device's batch (the storm's N * outgoing "outgoing-dials-done"
+    signals): cut in (t, instance) order into device batches, every state's sequence numbers are those
+    one batch gives, and a barrier on the last one releases at the last signal."""
+    rng = np.random.default_rng(9)
+    s = Simulator(SimConfig(n_instances=40_000, seed=1, max_states=8), binding=b)
+    inst = rng.integers(0, 40_000, n).astype(np.uint32)
+    t = rng.integers(0, 5_000, n) * 1000
+    st = rng.integers(0, 3, n).astype(np.uint32)
+    seq = s.signal(st, inst, t)
+    w = s.barrier(2, int((st == 2).sum()), 0)
+    rel = s.poll(w)
+    s.close()
+    return seq, rel
+
+
+def test_big_signal_batch_oracle(oracle):
+    seq, rel = _big_signal_batch(oracle)
+    assert rel >= 0 and len(np.unique(seq)) < len(seq)
+
+
+@pytest.mark.gpu
+def test_big_signal_batch_hip_matches_oracle(hip, oracle):
+    a, b = _big_signal_batch(hip), _big_signal_batch(oracle)
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1]
+
+
+# ---- TCP mode: connections, the SYN a bare segment, the socket buffer 2 x cwnd ----------------------
+
+def drive_tcp(sim, keep=True, max_windows=100_000):
+    """As drive, with the TCP reaction (ACK clock, timers) before the storm's."""
+    out, ne, w = [], sim.now + W, 0
+    while w < max_windows:
+        sim.advance(ne)
+        st, d = sim.status(), sim.deliveries()
+        sim.tcp_react()
+        ne, act = sim.storm_react()
+        if keep:
+            out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+        w += 1
+        if act == 0:
+            return out, w
+    raise AssertionError("the storm reactor did not finish")
+
+
+def _tcp_hand_case(b):
+    """2 instances x 1 connection, zero latency, 1 ms windows, 3 chunks of 4 KiB (3 segments each).
+    The SYN leaves at 0 and arrives at 0; its ACK leaves at the next window's start (1 ms) and
+    arrives in [1, 2) ms, so both dials end at that window's end, 2 ms. From the write start at 2 ms
+    a connection writes one chunk per reaction while 2 x cwnd (IW10) covers the unACKed segments:
+    chunk 0 at 2 ms, 1 at 3 ms, 2 at 4 ms, each delivered in the window it is sent in; every write
+    settles DELIVERED and the last conn.Write returned at 4 ms."""
+    s = Simulator(SimConfig(n_instances=2, seed=11), binding=b)
+    s.tcp_enable(acks=True, rto_ns=200 * MS)
+    s.storm_setup([1, 0], [0, 0], outgoing=1, concurrent=1, data_bytes=3 * 4096, window_ns=W)
+    s.storm_start()
+    drive_tcp(s, keep=False)
+    res, t_done = s.storm_dials()
+    assert res.tolist() == [A.PROBE_OK] * 2 and t_done.tolist() == [2 * MS, 2 * MS]
+    assert s.now == 2 * MS
+    s.storm_write_start(s.now)
+    obs, w = drive_tcp(s)
+    data = sorted((int(sq) >> 4, int(t)) for o in obs
+                  for sq, t, src in zip(o["deliv"]["seq"], o["deliv"]["t_deliver"], o["deliv"]["src"])
+                  if not (int(sq) & A.TCP_ACK_BIT) and src == 0)
+    # instance 0's segments: SYN = its first reserved segment, then 3 per chunk
+    assert [t for _, t in data] == [2 * MS] * 3 + [3 * MS] * 3 + [4 * MS] * 3
+    failed, t_last, tot = s.storm_results()
+    assert not failed.any() and t_last.tolist() == [4 * MS, 4 * MS]
+    assert tot["chunks_written"] == tot["chunks_delivered"] == 6 and tot["chunks_failed"] == 0 and w == 3
+    st = s.tcp_stats()
+    assert st["writes"] == 8 and st["delivered"] == 8 and st["retransmissions"] == 0
+    s.storm_end()
+    s.close()
+
+
+def test_storm_tcp_hand_oracle(oracle):
+    _tcp_hand_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_tcp_hand_hip(hip):
+    _tcp_hand_case(hip)
+
+
+def random_tcp_run(b, seed, n=40, keep=True):
+    """TCP storm on shaped, lossy, duplicating, corrupting links: SYN and data retransmissions, the
+    Reno window's collapses, writes blocked on the socket buffer; window by window."""
+    rng = np.random.default_rng(seed)
+    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17), binding=b)
+    s.tcp_enable(acks=True, rto_ns=30 * MS, max_attempts=6, max_writes=1 << 16, max_segments=1 << 18)
+    s.set_shapes(np.arange(n), [make_shape(latency_ns=int(rng.integers(1, 4)) * MS, jitter_ns=int(rng.integers(0, 2)) * MS // 2,
+                                           loss=float(rng.choice([0.0, 2.0])), duplicate=float(rng.choice([0.0, 5.0])),
+                                           corrupt=float(rng.choice([0.0, 1.0])),
+                                           bandwidth_bps=int(rng.choice([0, 100_000_000]))) for _ in range(n)])
+    O = int(rng.integers(1, 4))
+    src = np.repeat(np.arange(n), O)
+    dst = (src + rng.integers(1, n, len(src))) % n
+    s.storm_setup(dst, rng.integers(0, 30, len(src)) * MS // 2, outgoing=O, concurrent=int(rng.integers(1, 3)),
+                  data_bytes=int(rng.integers(1, 6)) * 4096 + int(rng.integers(0, 2)) * 1000, window_ns=W)
+    s.storm_start()
+    dial_obs, dial_w = drive_tcp(s, keep=keep)
+    res, t_done = s.storm_dials()
+    out = dict(dial_obs=dial_obs, dial_w=dial_w, res=res, t_done=t_done)
+    if (res == A.PROBE_OK).all():
+        s.storm_write_start(s.now)
+        out["write_obs"], out["write_w"] = drive_tcp(s, keep=keep)
+        out["failed"], out["t_last"], out["totals"] = s.storm_results()
+    out["tcp"] = s.tcp_stats()
+    out["stats"] = S.parity_stats(s)
+    s.storm_end()
+    s.close()
+    return out
+
+
+def test_storm_tcp_random_oracle(oracle):
+    r = random_tcp_run(oracle, 1)
+    assert "totals" in r and r["tcp"]["retransmissions"] > 0
+    tot = r["totals"]
+    assert tot["chunks_written"] == tot["chunks_delivered"] + tot["chunks_failed"] and tot["conns_writing"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_storm_tcp_random_hip_matches_oracle(hip, oracle, seed):
+    a, b = random_tcp_run(hip, seed), random_tcp_run(oracle, seed)
+    assert a["dial_w"] == b["dial_w"]
+    S.assert_same(a["dial_obs"], b["dial_obs"])
+    assert np.array_equal(a["res"], b["res"]) and np.array_equal(a["t_done"], b["t_done"])
+    assert ("totals" in a) == ("totals" in b)
+    if "totals" in a:
+        assert a["write_w"] == b["write_w"]
+        S.assert_same(a["write_obs"], b["write_obs"])
+        assert np.array_equal(a["failed"], b["failed"]) and np.array_equal(a["t_last"], b["t_last"])
+        assert a["totals"] == b["totals"]
+    assert a["tcp"] == b["tcp"] and a["stats"] == b["stats"]
