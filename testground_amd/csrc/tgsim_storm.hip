@@ -168,6 +168,13 @@ __device__ __forceinline__ uint32_t tcp_chunk_seg(const StormDev& s, size_t h, u
 __device__ __forceinline__ uint32_t tcp_nseg(const StormDev& s, uint32_t c) {
   return (chunk_payload(s, c) + s.mss - 1) / s.mss;
 }
+// a write's outcome as tgsim_tcp_writes decodes it: delivered once its arrival time is set, else
+// failed (the earliest failure's kind in w_fail) once its state left PENDING
+__device__ __forceinline__ uint32_t tcp_write_state(const TcpDev& t, uint32_t w) {
+  if (t.w_tarr[w] != INT64_MIN) return TGSIM_TCP_DELIVERED;
+  if (t.w_state[w] == TGSIM_TCP_PENDING) return TGSIM_TCP_PENDING;
+  return (t.w_fail[w] & 1) ? TGSIM_TCP_TIMEOUT : TGSIM_TCP_REFUSED;
+}
 __device__ __forceinline__ void tcp_link(TcpDev& t, size_t h, uint32_t prev, uint32_t first, uint32_t n, int64_t tw) {
   for (uint32_t x = first; x < first + n; ++x) t.s_tatt[x] = tw;
   if (prev != kTcpNoSeg) t.s_next[prev] = first;
@@ -194,7 +201,7 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l
       if (t.c_acked[h] >= 1) {
         out = TGSIM_PROBE_OK;
       } else {
-        const uint32_t ws = t.w_state[tcp_wid(s, h, 0)];
+        const uint32_t ws = tcp_write_state(t, tcp_wid(s, h, 0));
         out = ws == TGSIM_TCP_TIMEOUT ? TGSIM_PROBE_TIMEOUT : ws == TGSIM_TCP_REFUSED ? TGSIM_PROBE_REFUSED : out;
       }
       if (out != TGSIM_PROBE_NONE) {
@@ -308,7 +315,7 @@ __device__ __forceinline__ uint32_t write_step(StormDev& s, TcpDev& t, uint32_t 
     const uint32_t written = s.nchunks - s.rem[h];
     uint32_t st = s.settled[h];
     while (st < written) {
-      const uint32_t ws = t.w_state[tcp_wid(s, h, 1 + st)];
+      const uint32_t ws = tcp_write_state(t, tcp_wid(s, h, 1 + st));
       if (ws == TGSIM_TCP_PENDING) break;
       if (ws == TGSIM_TCP_DELIVERED) {
         ++dcnt;
