@@ -853,7 +853,9 @@ def main_splitbrain(args):
     elapsed = time.perf_counter() - t0
     s1 = counters(sim)
     prof = sim.profile_read()[dominant]
-    ne, act = sim.probe_react()  # one more reaction, synchronised: the state after the timed region
+    sim.advance_begin_device(ne_ptr, 0)  # one more window and reaction, synchronised: the state after
+    sim.advance_end()                    # the timed region
+    ne, act = sim.probe_react()
     delta = {k: s1[k] - s0[k] for k in s1}
     b_total = alg_bytes_step(delta, n, args.steps)
     roof = roofline(dominant, delta, prof[0] - base_prof[0], prof[1] - base_prof[1], n, args.steps, "splitbrain", 1,

@@ -70,8 +70,10 @@ class PlanEnv:
         # bridge is ~100 us): the window of the sequential probes while messages are in flight
         self.probe_window_ns = int(self.params.get("probe_window_ns", 100_000))
         # plans give instances their own sync states (splitbrain's "reconfigured<host>" callbacks)
+        # a /16 data network holds 65,534 instances (pkg/runner/common.go:28-40); larger runs get a
+        # wider simulated prefix with the same CIDR semantics (hard part 7)
         kw = dict(max_msgs_per_window=1 << 18, max_records=1 << 20, max_states=max(1024, 2 * self.n + 256),
-                  max_waiters=max(1 << 16, 4 * self.n))
+                  max_waiters=max(1 << 16, 4 * self.n), data_prefix_len=16 if self.n <= 65534 else 8)
         kw.update(sim_kw or {})
         self.sim = Simulator(SimConfig(n_instances=self.n, seed=seed, **kw), binding=binding)
         self.sync = SyncService(self.sim)
