@@ -181,7 +181,7 @@ def probe_kernels(sim, step, first: int, probe: int):
               "total_ms": ms - base[k][0]} for k, (ms, n) in prof.items() if n > base[k][1]}
     # the dominant kernel is the one with the most time, whether or not SURVEY.md
     # 8(d) assigns it bytes (its roofline then says so with frac 0)
-    ranked = sorted(((v["total_ms"], k) for k, v in ks.items()), reverse=True)
+    ranked = sorted(((v["total_ms"], k) for k, v in ks.items() if k not in COLLECTIVES), reverse=True)
     return ks, (ranked[0][1] if ranked else "k_emit_bucket")
 
 
@@ -204,6 +204,37 @@ def kernel_fracs(kernels: dict, delta: dict, n_local: int, windows: int, probe: 
         out[k] = {"alg_bytes_per_launch": per_launch, "avg_us": v["avg_us"],
                   "frac": per_launch / (v["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
     return out
+
+
+COLLECTIVES = ("exchange", "allreduce")
+
+
+def collective_stats(sim, dist, world: int, base: dict, steps: int, transport: str) -> dict | None:
+    """Per-rank time of the window's exchange (the peer blocks, tgsim_advance*) and of the storm
+    batch's MAX all-reduce over the timed steps (HIP events around the transport calls on the
+    context stream), max / mean over the ranks, and the bytes each rank sends per step (whole padded
+    peer blocks of exchange_cap 32-B records): what a SCALE curve needs to be attributed."""
+    if world == 1:
+        return None
+    import torch
+    prof = sim.profile_read()
+    mine = []
+    for k in COLLECTIVES:
+        ms, n = prof[k][0] - base[k][0], prof[k][1] - base[k][1]
+        mine += [ms / max(steps, 1), n / max(steps, 1)]
+    t = torch.tensor(mine, dtype=torch.float64)
+    tmax, tsum = t.clone(), t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    xbytes = (world - 1) * sim.cfg.exchange_cap * 32
+    ex_ms = float(tmax[0].item())
+    return {"transport": transport.lstrip("-"), "rehearsal": "rehearsal" in transport or "fallback" in transport,
+            "exchange_ms_per_step": {"max": ex_ms, "mean": float(tsum[0].item()) / world},
+            "exchange_calls_per_step": float(tmax[1].item()),
+            "allreduce_ms_per_step": {"max": float(tmax[2].item()), "mean": float(tsum[2].item()) / world},
+            "allreduce_calls_per_step": float(tmax[3].item()),
+            "exchange_bytes_per_step_per_rank": xbytes * float(tmax[1].item()),
+            "exchange_gbs_per_rank": xbytes * float(tmax[1].item()) / (ex_ms * 1e-3) / 1e9 if ex_ms > 0 else None}
 
 
 def parse():
@@ -236,6 +267,8 @@ def parse():
                    help="publications per wave (flood; distinct publishers; SURVEY's literal 1%% of 1M "
                         "instances = 10000 floods per wave does not fit in memory: DESIGN.md 5.4)")
     p.add_argument("--window-ms", type=float, default=10.0, help="window length (flood)")
+    p.add_argument("--no-beside", action="store_true",
+                   help="storm: skip config 5 (the 1M flood, same GPU count) reported beside the headline")
     a = p.parse_args()
     if a.workload == "splitbrain":
         a.warmup = a.warmup if "--warmup" in sys.argv else 200
@@ -365,8 +398,9 @@ def main():
         step(r)
     probe = probe_steps(args)
     warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
-    sim.profile([dominant])
-    base_prof = sim.profile_read()[dominant]
+    sim.profile([dominant] + (list(COLLECTIVES) if world > 1 else []))
+    base_all = sim.profile_read()
+    base_prof = base_all[dominant]
     first = args.warmup + probe
 
     s0 = counters(sim)
@@ -402,6 +436,9 @@ def main():
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
                     elapsed)
     roof["kernels"] = kernel_fracs(warm_kernels, delta, sim.hi - sim.lo, args.steps, probe)
+    coll = collective_stats(sim, dist, world, base_all, args.steps, transport)
+    if coll:
+        roof["collectives"] = coll
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.tcp:
         cpu = cpu_baseline(args, shapes)
@@ -444,8 +481,18 @@ def main():
             "cpu_baseline": cpu,
             "kernels_probe": warm_kernels,
         }
-        print(json.dumps(line), flush=True)
     sim.close()
+    if not args.no_beside:
+        # config 5 at the same GPU count (the weak-scaling-friendly config beside
+        # the headline, so a SCALE run carries both curves); its own defaults, no CPU baseline
+        fa = argparse.Namespace(**vars(args))
+        fa.warmup, fa.steps, fa.no_cpu_baseline, fa.seed = 100, 50, True, 5
+        fl = main_flood(fa, ctx=(torch, dist, world, rank, local, rehearsal, stream), emit=False)
+        if rank == 0:
+            line["beside"] = {"flood": {k: fl[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
+                                                            "config", "roofline")}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -576,12 +623,13 @@ def flood_max_pubs(args) -> int:
     return ((args.warmup + probe_steps(args) + args.steps + 20) // args.pub_every + 2) * args.pubs_per_wave
 
 
-def main_flood(args):
+def main_flood(args, ctx=None, emit=True):
     """Config 5 (BASELINE.json configs[4]): 1M instances on a random 8-regular graph
     with heterogeneous LinkShapes; one publication every `pub_every` windows floods the graph with
     first-receipt dedup (tgsim_flood_react after every window). A step is one window; `value` =
-    deliveries of all ranks in the K timed windows / the max-over-ranks wall time."""
-    torch, dist, world, rank, local, rehearsal, stream = _dist_setup(args)
+    deliveries of all ranks in the K timed windows / the max-over-ranks wall time. ctx: the process
+    group and stream of a storm run that reports this line beside its own (emit=False: returned)."""
+    torch, dist, world, rank, local, rehearsal, stream = ctx or _dist_setup(args)
     from testground_amd import workloads as W
     from testground_amd.sim import Simulator
     args.seed = 5 if "--seed" not in sys.argv else args.seed
@@ -606,8 +654,9 @@ def main_flood(args):
         step(w)
     probe = probe_steps(args)
     warm_kernels, dominant = probe_kernels(sim, step, args.warmup, probe)
-    sim.profile([dominant])
-    base_prof = sim.profile_read()[dominant]
+    sim.profile([dominant] + (list(COLLECTIVES) if world > 1 else []))
+    base_all = sim.profile_read()
+    base_prof = base_all[dominant]
     first = args.warmup + probe
     s0 = counters(sim)
     sim.sync()
@@ -635,11 +684,15 @@ def main_flood(args):
     roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "flood", world, b_total,
                     elapsed)
     roof["kernels"] = kernel_fracs(warm_kernels, delta, sim.hi - sim.lo, args.steps, probe)
+    coll = collective_stats(sim, dist, world, base_all, args.steps, transport)
+    if coll:
+        roof["collectives"] = coll
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = flood_cpu_baseline(args, shapes, graph)
+    out = None
     if rank == 0:
-        print(json.dumps({
+        out = {
             "metric": "simulated msgs delivered/sec (1M-inst random-regular pubsub flood) + % HBM roofline",
             "value": delivered / elapsed, "unit": "msgs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -656,10 +709,13 @@ def main_flood(args):
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels_probe": warm_kernels,
-        }), flush=True)
+        }
+        if emit:
+            print(json.dumps(out), flush=True)
     sim.close()
-    if world > 1:
+    if world > 1 and ctx is None:
         dist.destroy_process_group()
+    return out
 
 
 # ---- config 2: 1k instances all-to-all (BASELINE.json configs[1]) -------------

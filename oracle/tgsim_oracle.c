@@ -238,12 +238,15 @@ typedef struct otcps {
   int64_t t_att, arrival, t_last;
   uint32_t acked, gave_up;  /* acks = 1 */
   uint32_t next, unsent;    /* connections: the connection's next segment; queued, not yet sent */
+  uint32_t lost;            /* connections: marked lost at a timeout, waiting to be resent under cwnd */
 } otcps;
 /* a TCP connection: congestion window and the queue of its unsent segments */
 typedef struct otcpc {
   uint32_t src, dst, cwnd, ssthresh, cnt, flight, queued, head, tail, acks, broken;
   uint64_t acked;
-  int64_t rto_win;          /* start of the window of its last cwnd collapse */
+  int64_t tloss;            /* the window's earliest expired timer (INT64_MAX: none): a loss episode */
+  uint32_t una;             /* no segment before it is outstanding (advanced lazily at a timeout) */
+  uint32_t facks;           /* the window's first ACKs of segments in flight (not marked lost) */
 } otcpc;
 #define TCP_NOSEG 0xFFFFFFFFu
 #define TCP_IW 10u
@@ -1703,7 +1706,7 @@ int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
     for (uint32_t j = 0; j < ns; ++j, ++k) {
       const uint32_t pay = size ? (j + 1 < ns ? c->tcp.mss : size - j * c->tcp.mss) : 0;
       const uint32_t sid = (uint32_t)c->tsg_n++;
-      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 0};
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 0, 0};
       c->tsg[sid] = g;
       src[k] = w.src; dst[k] = w.dst; seq[k] = sid << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
     }
@@ -1747,19 +1750,38 @@ static int ostage_flush(tgo_ctx* c, ostage* b) {
   return rc;
 }
 
-/* connection k sends queued segments while its flight is below cwnd, each at max(written, t0) */
-static int conn_release(tgo_ctx* c, uint32_t k, int64_t t0, ostage* b) {
+static void tcp_finish(tgo_ctx* c, uint32_t wi, uint32_t state, int64_t t, size_t* done);
+
+/* Connection k sends while its flight is below cwnd, each segment at max(written, t0): first the
+ * segments a timeout marked lost (in order, the next attempt; settled ones are passed over, and one
+ * of a failed write or out of attempts gives up), then new ones. */
+static int conn_release(tgo_ctx* c, uint32_t k, int64_t t0, ostage* b, size_t* done) {
   otcpc* q = &c->tc[k];
   while (q->flight < q->cwnd && q->head != TCP_NOSEG) {
     const uint32_t sid = q->head;
     otcps* g = &c->tsg[sid];
-    const int64_t t = g->t_att > t0 ? g->t_att : t0;
-    g->t_att = t;
-    g->unsent = 0;
     q->head = g->next;
-    q->queued--;
+    if (g->acked || g->gave_up) continue;
+    const int64_t t = g->t_att > t0 ? g->t_att : t0;
+    uint32_t seq = sid << 4;
+    if (g->lost) {
+      const uint32_t st = c->tw[g->w].state;
+      g->lost = 0;
+      if (st == TGSIM_TCP_TIMEOUT || st == TGSIM_TCP_REFUSED || g->attempt + 1 >= c->tcp.max_attempts) {
+        g->gave_up = 1;
+        tcp_finish(c, g->w, TGSIM_TCP_TIMEOUT, t, done);
+        continue;
+      }
+      g->attempt++;
+      seq |= g->attempt;
+      c->tstats.retransmissions++;
+    } else {
+      g->unsent = 0;
+      q->queued--;
+    }
+    g->t_att = t;
     q->flight++;
-    if (ostage_push(b, q->src, q->dst, sid << 4, g->wire, t)) return TGSIM_ENOMEM;
+    if (ostage_push(b, q->src, q->dst, seq, g->wire, t)) return TGSIM_ENOMEM;
   }
   return TGSIM_OK;
 }
@@ -1775,7 +1797,7 @@ int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t
   if (c->tc_n + n > c->tcp.max_writes) return fail(c, TGSIM_ECAPACITY, "connection capacity");
   if (grow((void**)&c->tc, &c->tc_cap, c->tc_n + n + 1, sizeof(otcpc))) return fail(c, TGSIM_ENOMEM, "oom");
   for (size_t i = 0; i < n; ++i) {
-    otcpc q = {src[i], dst[i], TCP_IW, 0x7FFFFFFFu, 0, 0, 0, TCP_NOSEG, TCP_NOSEG, 0, 0, 0, INT64_MIN};
+    otcpc q = {src[i], dst[i], TCP_IW, 0x7FFFFFFFu, 0, 0, 0, TCP_NOSEG, TCP_NOSEG, 0, 0, 0, INT64_MAX, TCP_NOSEG, 0};
     if (conn_out) conn_out[i] = (uint32_t)c->tc_n;
     c->tc[c->tc_n++] = q;
   }
@@ -1809,10 +1831,11 @@ int tgo_tcp_write(tgo_ctx* c, const uint32_t* conn, const uint32_t* size, const 
     for (uint32_t j = 0; j < ns; ++j) {
       const uint32_t pay = sz ? (j + 1 < ns ? c->tcp.mss : sz - j * c->tcp.mss) : 0;
       const uint32_t sid = (uint32_t)c->tsg_n++;
-      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, t[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 1};
+      otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, t[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 1, 0};
       c->tsg[sid] = g;
       if (q->tail != TCP_NOSEG) c->tsg[q->tail].next = sid;
       if (q->head == TCP_NOSEG) q->head = sid;
+      if (q->una == TCP_NOSEG) q->una = sid;
       q->tail = sid;
       q->queued++;
     }
@@ -1822,8 +1845,9 @@ int tgo_tcp_write(tgo_ctx* c, const uint32_t* conn, const uint32_t* size, const 
   /* what the windows have room for leaves now, at its write time */
   ostage b = {0};
   int rc = TGSIM_OK;
+  size_t done = 0;
   for (uint32_t k = 0; k < c->tc_n && !rc; ++k)
-    if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &b);
+    if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &b, &done);
   const int rc2 = ostage_flush(c, &b);
   return rc ? fail(c, rc, "oom") : rc2;
 }
@@ -1974,7 +1998,10 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
       if (intact && !g->acked && !g->gave_up) {
         g->acked = 1;
         const uint32_t k = c->tw[g->w].conn;
-        if (k != TCP_NOSEG) c->tc[k].acks++;
+        if (k != TCP_NOSEG) {
+          c->tc[k].acks++;
+          if (!g->lost) c->tc[k].facks++;  /* a segment marked lost holds no flight slot */
+        }
       }
       continue;
     }
@@ -2001,7 +2028,8 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
   int rc = TGSIM_OK;
   for (uint32_t k = 0; k < c->tc_n && !rc; ++k) {
     otcpc* q = &c->tc[k];
-    q->flight -= q->acks;
+    q->flight -= q->facks;
+    q->facks = 0;
     q->acked += q->acks;
     for (uint32_t a = 0; a < q->acks; ++a) {
       if (q->cwnd < q->ssthresh) ++q->cwnd;
@@ -2020,7 +2048,7 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
       q->queued = 0;
       continue;
     }
-    rc = conn_release(c, k, c->t_end, &b);
+    rc = conn_release(c, k, c->t_end, &b, done);
   }
   const int rc2 = ostage_flush(c, &b);
   return rc ? fail(c, rc, "oom") : rc2;
@@ -2102,7 +2130,8 @@ static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
   size_t nd = 0, done = 0;
   for (size_t sid = 0; sid < c->tsg_n; ++sid) {
     otcps* g = &c->tsg[sid];
-    if (g->acked || g->gave_up || g->unsent || g->t_att >= H) continue;  /* settled, or its attempt not yet sent */
+    /* settled, marked lost (no timer until resent), or its attempt not yet sent */
+    if (g->acked || g->gave_up || g->unsent || g->lost || g->t_att >= H) continue;
     const uint32_t st = c->tw[g->w].state;
     if (st == TGSIM_TCP_TIMEOUT || st == TGSIM_TCP_REFUSED) continue;
     const int64_t T = g->t_att + (c->tcp.rto_ns << g->attempt);
@@ -2114,14 +2143,9 @@ static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
       tcp_finish(c, g->w, TGSIM_TCP_TIMEOUT, T, &done);
       continue;
     }
-    if (k != TCP_NOSEG && c->tc[k].rto_win != H) {  /* the connection's first timeout in this window */
-      otcpc* q = &c->tc[k];
-      q->rto_win = H;
-      /* a new loss episode halves ssthresh; cwnd = 1 with no ACK since means the same episode
-       * (tcp_enter_loss recomputes ssthresh once per episode [EXT]) */
-      if (q->cwnd > 1) q->ssthresh = q->cwnd / 2 > 2 ? q->cwnd / 2 : 2;
-      q->cwnd = 1;
-      q->cnt = 0;
+    if (k != TCP_NOSEG) {  /* a connection's timeout: its loss episode below resends under cwnd */
+      if (T < c->tc[k].tloss) c->tc[k].tloss = T;
+      continue;
     }
     g->attempt++;
     g->t_att = T > H ? T : H;
@@ -2146,8 +2170,31 @@ static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
     free(src); free(dst); free(seq); free(sz); free(ts);
   }
   free(due);
+  /* loss episodes [EXT Linux tcp_enter_loss, RFC 5681 3.1 / RFC 6298 5.4]: a connection whose timer
+   * expired in this window, at its earliest expiry T: ssthresh = max(cwnd / 2, 2) unless cwnd is
+   * already 1 (the same episode), cwnd = 1; every outstanding segment is marked lost and the send
+   * queue restarts at the oldest, which leaves at max(T, H); the rest follow as ACKs open cwnd. */
+  ostage b = {0};
+  for (uint32_t k = 0; k < c->tc_n && !rc; ++k) {
+    otcpc* q = &c->tc[k];
+    if (q->tloss == INT64_MAX) continue;
+    const int64_t tl = q->tloss;
+    q->tloss = INT64_MAX;
+    if (q->cwnd > 1) q->ssthresh = q->cwnd / 2 > 2 ? q->cwnd / 2 : 2;
+    q->cwnd = 1;
+    q->cnt = 0;
+    uint32_t u = q->una;
+    while (u != q->head && (c->tsg[u].acked || c->tsg[u].gave_up)) u = c->tsg[u].next;
+    q->una = u;
+    for (uint32_t x = u; x != q->head; x = c->tsg[x].next)
+      if (!c->tsg[x].acked && !c->tsg[x].gave_up) c->tsg[x].lost = 1;
+    q->head = u;
+    q->flight = 0;
+    if (!q->broken) rc = conn_release(c, k, tl > H ? tl : H, &b, &done);
+  }
+  const int rc2 = ostage_flush(c, &b);
   c->tstats.pending_retx = 0;
-  return rc;
+  return rc ? rc : rc2;
 }
 
 int tgo_tcp_writes(tgo_ctx* c, uint8_t* state, int64_t* t, size_t cap, size_t* n) {
@@ -2317,7 +2364,7 @@ int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, con
         c->tw[wi] = w;
         for (uint32_t i = 0; i < ns; ++i) {
           otcps g = {wi, (pay ? (i + 1 < ns ? mss : pay - i * mss) : 0) + hdr, 0, 0, 0, 0, 0, INT64_MAX, INT64_MIN, 0, 0,
-                     TCP_NOSEG, 1};
+                     TCP_NOSEG, 1, 0};
           c->tsg[first + i] = g;
         }
       }
@@ -2335,6 +2382,7 @@ static void sm_link(tgo_ctx* c, uint64_t h, uint32_t first, uint32_t n, int64_t 
     c->tsg[sid].t_att = t;
     if (q->tail != TCP_NOSEG) c->tsg[q->tail].next = sid;
     if (q->head == TCP_NOSEG) q->head = sid;
+    if (q->una == TCP_NOSEG) q->una = sid;
     q->tail = sid;
     q->queued++;
   }
@@ -2535,8 +2583,9 @@ static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* n
   const int staged_before = c->staged.n != 0;
   if (s->tcp) {
     ostage q = {0};
+    size_t done = 0;
     for (uint32_t k = 0; k < c->tc_n && !rc; ++k)
-      if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &q);
+      if (!c->tc[k].broken) rc = conn_release(c, k, INT64_MIN, &q, &done);
     const int rc2 = ostage_flush(c, &q);
     if (rc || rc2) return rc ? fail(c, rc, "oom") : rc2;
   }

@@ -13,7 +13,7 @@ enum KernelId : int {
   KID_SHAPE = 0, KID_EXTRACT, KID_TB, KID_EMIT, KID_RADIX_HIST, KID_RADIX_ROWS, KID_RADIX_SCATTER,
   KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_BKT_HIST, KID_BKT_SCATTER,
   KID_BKT_SORT, KID_SEG_REST, KID_FLOOD_COUNT, KID_FLOOD_EMIT, KID_SHAPE_SEQ, KID_PROBE, KID_SEG_SMALL, KID_STORM,
-  KID_COUNT
+  KID_EXCHANGE, KID_ALLREDUCE, KID_SHAPE_WIDE, KID_COUNT
 };
 extern const char* const kKernelNames[KID_COUNT];
 
@@ -60,6 +60,9 @@ constexpr int kTcpArriveBlocks = 2048;  // k_tcp_arrive's grid (= TcpDev::part e
 constexpr uint32_t kTcpSoleSeg = 0x80000000u;  // s_w: the segment is its write's only one
 constexpr uint32_t kTcpWMask = 0x0FFFFFFFu;    // s_w: the write
 constexpr uint32_t kTcpNoSeg = 0xFFFFFFFFu;    // end of a connection's segment chain
+// k_tcp_conn_release modes: at a write (t0 = the write times), after a window (its ACKs first, t0 =
+// the window's end), at a window start for the connections whose timer expired (loss episodes)
+constexpr uint32_t kRelAtWrite = 0, kRelAfterWindow = 1, kRelLoss = 2;
 constexpr uint32_t kTcpBatches = 1u << 14;  // acks mode: ring of attempt-0 timer batches (one per window)
 // acks mode: the segments first sent in one window, [lo, hi), their timers in [t_lo, t_hi)
 struct TcpBatch {
@@ -106,10 +109,14 @@ struct TcpDev {
   uint32_t *c_src = nullptr, *c_dst = nullptr, *c_cwnd = nullptr, *c_ssth = nullptr, *c_cnt = nullptr;
   uint32_t *c_flight = nullptr, *c_queued = nullptr, *c_head = nullptr, *c_acks = nullptr, *c_broken = nullptr;
   unsigned long long* c_acked = nullptr;  // cumulative first ACKs
-  int64_t* c_rto = nullptr;       // start of the window of the connection's last cwnd collapse
+  int64_t* c_tloss = nullptr;     // the window's earliest expired timer (INT64_MAX: none): a loss episode
+  uint32_t* c_una = nullptr;      // no segment before it is outstanding (advanced at a loss episode)
+  uint32_t* c_fack = nullptr;     // the window's first ACKs of segments in flight (not marked lost)
   uint32_t* w_conn = nullptr;     // [W] the write's connection (kNoSeg: tgsim_tcp_send writes)
   uint32_t* s_next = nullptr;     // [S] the connection's next segment
   uint32_t* s_ack1 = nullptr;     // [S] first-ACK claim (a segment frees one flight slot once)
+  uint8_t* s_lost = nullptr;      // [S] marked lost by a loss episode: resent under cwnd, no timer meanwhile
+  uint8_t* s_tq = nullptr;        // [S] the segment has an entry on the timer lists (pend)
   uint32_t mss = 0, hdr = 0, max_att = 0;
   int64_t rto = 0;
   uint64_t cap_w = 0, cap_s = 0;
@@ -230,6 +237,7 @@ struct Dev {
   tgsim_record* H = nullptr;
   uint32_t *hkeys = nullptr, *hvals = nullptr;
   uint32_t h_cap = 0;
+  uint8_t* seq_done = nullptr;     // [nloc] k_shape_seq_wide decided the sender's deferred messages
 
   // staged messages (SoA) + per-message status
   uint32_t *m_src = nullptr, *m_dst = nullptr, *m_seq = nullptr, *m_size = nullptr;
@@ -403,7 +411,7 @@ hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32
 // at the write times; after_window: first apply the window's ACKs and resets, t0 = the window's
 // end), staged behind sc->n_msgs_dev (set from base_host unless base_dev), timers on pend[cur]
 hipError_t launch_tcp_link(Dev& d, TcpDev& t, const uint32_t* links, uint32_t n);
-hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, bool after_window, uint32_t cur, bool base_dev,
+hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, uint32_t mode, uint32_t cur, bool base_dev,
                                    uint32_t base_host);
 constexpr uint32_t kFloodBlocks = 4096;  // chunks of the flood reaction (>= 16 waves per CU)
 

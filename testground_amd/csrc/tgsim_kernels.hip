@@ -22,7 +22,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
     "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit",
-    "k_shape_seq", "k_probe", "k_seg_small", "k_storm"};
+    "k_shape_seq", "k_probe", "k_seg_small", "k_storm", "exchange", "allreduce", "k_shape_seq_wide"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
@@ -169,10 +169,10 @@ struct Queues {
   // spread: the salt alone picks the sub-queue (any of the 64), for a producer whose one workgroup
   // may append far more than a sub-queue's share (k_shape_seq: one sender per workgroup, every one
   // of its chunks in turn; with the XCD-pinned choice a 10k-reply sender filled one sub-queue)
-  template <int U>
+  template <int U, int Waves = kBlock / 64>
   __device__ __forceinline__ void push_batch(const int (&q)[U], const tgsim_record (&r)[U], uint32_t salt,
                                              bool spread = false) const {
-    __shared__ uint32_t gcnt[kBlock / 64][16];  // per wave: [A groups 0..7 | D groups 0..7]
+    __shared__ uint32_t gcnt[Waves][16];  // per wave: [A groups 0..7 | D groups 0..7]
     const uint32_t lane = lane_id();
     uint32_t* cnt = gcnt[threadIdx.x >> 6];
     const uint32_t sub = spread ? (salt & (kNSub - 1u))
@@ -2518,14 +2518,14 @@ __device__ uint64_t g_seq_ph[1024][8];
 __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint32_t* sorted, const uint32_t* moff,
                                                          const uint32_t* hoff, const uint32_t* hidx,
                                                          const tgsim_record* H, const uint32_t* rho4,
-                                                         uint32_t* last4, const int64_t* Xs) {
+                                                         uint32_t* last4, const int64_t* Xs, const uint8_t* done) {
   __shared__ SeqSmem m;
   DevScalars* sc = a.Q.sc;
   const int64_t t_end = sc->t_end;
   const uint32_t lane = threadIdx.x;
   for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
     const uint32_t j0 = moff[l], j1 = moff[l + 1];
-    if (j0 == j1) continue;
+    if (j0 == j1 || done[l]) continue;  // k_shape_seq_wide decided the sender's window
     const ShapeDev sh = a.shape[l];
     const bool corr = (sh.flags & kShCorr) != 0;
     const bool heavy = a.heavy.of(l);
@@ -2960,6 +2960,292 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
       if (n_lost) atomicAdd(&row[ST_LOST], (unsigned long long)n_lost);
       if (n_copies) atomicAdd(&row[ST_COPIES], (unsigned long long)n_copies);
       if (n_over) atomicAdd(&row[ST_OVERLIMIT], (unsigned long long)n_over);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- the whole-sender closed form -----------------------------------------
+// The parallel form above walks a sender's window chunk by chunk in one wave: the admission test of
+// chunk c needs the queue the earlier chunks left. When every copy the sender enqueues in the window
+// outlives its last enqueue (min netem time > max send time: an all-to-all round's 50 ms of latency
+// against a 1 ms send spread), every earlier admitted copy is still queued at each enqueue, so copy
+// k is admitted iff A_k < L_k with A_k the copies admitted before it and L_k = limit - far -
+// |K > t_k| (K: the due wheel records' departures), and A_{k+1} = min(A_k + 1, max(L_k, 0)) has the
+// closed form A_k = k + min(0, min_{i<k} (L_i - i - 1)) (L never decreases along the window). One
+// 1024-thread workgroup per sender evaluates it for the whole window at once: one message per
+// thread, two block scans. A sender it cannot take (correlated, shaped, a due stage-A record, more
+// than 1024 messages or due records, or the condition fails) is left to k_shape_seq (done[l] = 0).
+constexpr int kWide = 1024;
+constexpr int kWideWaves = kWide / 64;
+
+__device__ __forceinline__ uint32_t wide_excl_scan(uint32_t v, uint32_t* red, uint32_t& total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) red[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kWideWaves; ++w) {
+    const uint32_t a = red[w];
+    pre += w < (int)wave ? a : 0u;
+    total += a;
+  }
+  __syncthreads();
+  return pre + x - v;
+}
+// exclusive prefix minimum over the block's threads (INT64_MAX for thread 0)
+__device__ __forceinline__ int64_t wide_excl_min(int64_t v, int64_t* red) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x = y < x ? y : x;
+  }
+  if (lane == 63) red[wave] = x;
+  __syncthreads();
+  int64_t pre = INT64_MAX;
+#pragma unroll
+  for (int w = 0; w < kWideWaves; ++w) {
+    const int64_t a = red[w];
+    if (w < (int)wave) pre = a < pre ? a : pre;
+  }
+  __syncthreads();
+  int64_t ex = __shfl_up(x, 1);
+  if (lane == 0) ex = INT64_MAX;
+  return ex < pre ? ex : pre;
+}
+
+__global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,
+                                                          const uint32_t* moff, const uint32_t* hoff,
+                                                          const uint32_t* hidx, const tgsim_record* H,
+                                                          uint8_t* done) {
+  __shared__ int64_t K[kWide];
+  __shared__ uint64_t S1[kWide];
+  __shared__ uint32_t S2[kWide], S3[kWide];
+  __shared__ uint32_t red[kWideWaves];
+  __shared__ int64_t red64[kWideWaves], rmin[kWideWaves], rmax[kWideWaves];
+  __shared__ uint32_t s_flag;
+  DevScalars* sc = a.Q.sc;
+  const int64_t t_end = sc->t_end;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
+    const uint32_t j0 = moff[l], j1 = moff[l + 1], n = j1 - j0;
+    if (n == 0) continue;
+    if (n > (uint32_t)kWide) {  // k_rest ordered it; k_shape_seq walks it
+      if (tid == 0) done[l] = 0;
+      continue;
+    }
+    // the sender's deferred messages in (t_send, seq) order (k_seg_small<CorrPolicy>'s order, which
+    // this kernel replaces for every sender of at most kWide = kTile of them): one bitonic sort in LDS
+    // over (t_send, seq, index), unique keys
+    {
+      const uint32_t np2m = n > 1 ? next_pow2(n) : 1u;
+      if (tid < n) {
+        const uint32_t i = gvals[j0 + tid];
+        S1[tid] = (uint64_t)a.t[i] ^ 0x8000000000000000ull;
+        S2[tid] = a.seq[i];
+        S3[tid] = i;
+      } else if (tid < np2m) {
+        S1[tid] = ~0ull; S2[tid] = ~0u; S3[tid] = ~0u;
+      }
+      __syncthreads();
+      for (uint32_t k = 2; k <= np2m; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          if (tid < np2m) {
+            const uint32_t p = tid ^ j;
+            if (p > tid) {
+              const uint64_t x1 = S1[tid], y1 = S1[p];
+              const uint32_t x2 = S2[tid], y2 = S2[p], x3 = S3[tid], y3 = S3[p];
+              const bool gt = x1 != y1 ? x1 > y1 : (x2 != y2 ? x2 > y2 : x3 > y3);
+              if (gt == ((tid & k) == 0)) {
+                S1[tid] = y1; S1[p] = x1; S2[tid] = y2; S2[p] = x2; S3[tid] = y3; S3[p] = x3;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      if (tid < n) sorted[j0 + tid] = S3[tid];
+    }
+    const ShapeDev sh = a.shape[l];
+    const uint32_t h0 = hoff ? hoff[l] : 0u, h1 = hoff ? hoff[l + 1] : 0u, n0 = h1 - h0;
+    if (!a.heavy.of(l) || (sh.flags & (kShCorr | kShLimited)) || n0 > (uint32_t)kWide || !hoff) {
+      if (tid == 0) done[l] = 0;
+      continue;
+    }
+    // K: the due records' departures, ascending; a stage-A record (queued under an earlier, shaped
+    // Shape) needs the heaps of k_shape_seq
+    if (tid == 0) s_flag = 0;
+    __syncthreads();
+    const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
+    if (tid < n0) {
+      tgsim_record r;
+      load_rec(H + hidx[h0 + tid], r);
+      K[tid] = r.t;
+      if (!(r.meta & TGSIM_F_STAGE_D)) atomicOr(&s_flag, 1u);
+    } else if (tid < np2) {
+      K[tid] = INT64_MAX;
+    }
+    __syncthreads();
+    if (s_flag) {
+      if (tid == 0) done[l] = 0;
+      __syncthreads();
+      continue;
+    }
+    for (uint32_t k = 2; k <= np2; k <<= 1)  // bitonic, one element per thread
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        if (tid < np2) {
+          const uint32_t p = tid ^ j;
+          if (p > tid) {
+            const int64_t x = K[tid], y = K[p];
+            if ((x > y) == ((tid & k) == 0)) { K[tid] = y; K[p] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    const uint32_t pnd = a.heavy.pend[l];
+    const int64_t far = pnd > n0 ? (int64_t)(pnd - n0) : 0;
+    // this thread's message: its copies (clone first) and netem times, as k_shape_seq's parallel form
+    const uint32_t src = a.lo + l;
+    uint8_t st = 0, valid = 0;
+    int64_t e2[2] = {INT64_MIN, INT64_MIN};
+    uint32_t meta2[2] = {0, 0}, coff2[2] = {0, 0};
+    int64_t ts = INT64_MIN, base = 0;
+    uint32_t idx = 0, dst = 0, seq = 0, size = 0;
+    if (tid < n) {
+      idx = S3[tid];
+      seq = a.seq[idx]; dst = a.dst[idx]; size = a.size[idx]; ts = a.t[idx];
+      uint32_t w0[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, w1[2][3] = {{0, 0, 0}, {0, 0, 0}};
+      const bool need_w0 = sh.dup_t || sh.loss_t || sh.reorder_t || sh.sigma;
+#pragma unroll
+      for (uint32_t c = 0; c < 2; ++c) {
+        if (c == 1 && !sh.dup_t) break;
+        if (need_w0) philox4x32_10(seq, src, c, kNetemSalt, a.key0, a.key1, w0[c]);
+        if (sh.corrupt_t) {
+          uint32_t o[4];
+          philox4x32_10(seq, src, c | 2u, kNetemSalt, a.key0, a.key1, o);
+          w1[c][0] = o[0]; w1[c][1] = o[1]; w1[c][2] = o[2];
+        }
+      }
+      const bool dup = sh.dup_t && sh.dup_t >= w0[0][0];
+      const bool lst = sh.loss_t && sh.loss_t >= w0[0][1];
+      const int count = 1 + (dup ? 1 : 0) - (lst ? 1 : 0);
+      if (count == 0) {
+        st = TGSIM_ST_LOST;
+      } else {
+        st = TGSIM_ST_QUEUED;
+        if (dup && lst) st |= TGSIM_ST_FLAG_DUP_CANCEL;
+        if (count == 2) st |= TGSIM_ST_FLAG_DUP;
+#pragma unroll
+        for (int c = 1; c >= 0; --c) {
+          if (c == 1 && count != 2) continue;
+          const uint32_t* w = w0[c];
+          if (c == 1 && sh.loss_t && sh.loss_t >= w[1]) { st |= TGSIM_ST_FLAG_CLONE_LOST; continue; }
+          uint32_t meta = c ? TGSIM_F_CLONE : 0u, coff = 0;
+          if (sh.corrupt_t && sh.corrupt_t >= w1[c][0] && size > 0) {
+            meta |= TGSIM_F_CORRUPT | ((w1[c][2] % 8u) << TGSIM_F_BIT_SHIFT);
+            coff = w1[c][1] % size;
+          }
+          int64_t e;
+          if (sh.reorder_t && !(sh.reorder_t < w[3])) {
+            meta |= TGSIM_F_REORDERED;
+            e = ts;
+          } else {
+            const int64_t delay = tabledist(sh.mu, sh.sigma, w[2]);
+            e = ts + (delay > 0 ? delay : 0);
+          }
+          meta |= TGSIM_F_STAGE_D;  // unlimited: the netem time is the departure
+          e2[c] = e; meta2[c] = meta; coff2[c] = coff;
+          valid |= (uint8_t)(1u << c);
+        }
+      }
+      base = far + (int64_t)(n0 - upper_idx(K, 0, n0, ts));
+    }
+    // the closed form holds when every copy outlives the window's last enqueue
+    int64_t emin = INT64_MAX, tmax = INT64_MIN;
+    if (valid & 2u) emin = e2[1] < emin ? e2[1] : emin;
+    if (valid & 1u) emin = e2[0] < emin ? e2[0] : emin;
+    if (valid) tmax = ts;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t x = __shfl_xor(emin, o), y = __shfl_xor(tmax, o);
+      emin = x < emin ? x : emin;
+      tmax = y > tmax ? y : tmax;
+    }
+    if (lane_id() == 0) { rmin[tid >> 6] = emin; rmax[tid >> 6] = tmax; }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kWideWaves; ++w) {
+      emin = rmin[w] < emin ? rmin[w] : emin;
+      tmax = rmax[w] > tmax ? rmax[w] : tmax;
+    }
+    if (!(emin > tmax)) {  // block-uniform: k_shape_seq walks it
+      if (tid == 0) done[l] = 0;
+      __syncthreads();
+      continue;
+    }
+    // copy k (enqueue order: message, clone first) admitted iff A_{k+1} = A_k + 1
+    const uint32_t nv = (uint32_t)__popc((uint32_t)valid);
+    uint32_t tot;
+    const uint32_t k0 = wide_excl_scan(nv, red, tot);
+    const int64_t lim = (int64_t)TGSIM_NETEM_LIMIT - base;
+    const int64_t Lp = lim > 0 ? lim : 0;
+    const int64_t x0 = Lp - (int64_t)k0 - 1, x1 = Lp - (int64_t)k0 - 2;
+    const int64_t lmin = nv == 0 ? INT64_MAX : (nv == 1 ? x0 : (x0 < x1 ? x0 : x1));
+    int64_t prev = wide_excl_min(lmin, red64);
+    uint8_t adm = 0;
+    uint32_t k = k0;
+#pragma unroll
+    for (int c = 1; c >= 0; --c) {
+      if (!(valid & (1u << c))) continue;
+      const int64_t x = Lp - (int64_t)k - 1;
+      const int64_t cur = prev < x ? prev : x;
+      const int64_t before = (int64_t)k + (prev < 0 ? prev : 0);
+      const int64_t after = (int64_t)k + 1 + (cur < 0 ? cur : 0);
+      if (after == before + 1) adm |= (uint8_t)(1u << c);
+      prev = cur;
+      ++k;
+    }
+    uint32_t n_lost = 0, n_copies = 0, n_over = 0;
+    tgsim_record r1, r2;
+    int q1 = -1, q2 = -1;
+    if (tid < n) {
+      if (st != TGSIM_ST_LOST) {
+        const uint8_t dropped = valid & ~adm;
+        if (dropped & 2u) st |= TGSIM_ST_FLAG_CLONE_LOST;
+        if (dropped & 1u) st |= TGSIM_ST_FLAG_OVERLIMIT;
+        if (!adm) st = (uint8_t)((st & 0xF0u) | TGSIM_ST_OVERLIMIT);
+        n_over = (uint32_t)__popc(dropped);
+        n_copies = (uint32_t)__popc(adm);
+      } else {
+        n_lost = 1;
+      }
+      a.status[idx] = st;
+      r1.t = e2[1]; r1.src = src; r1.dst = dst; r1.seq = seq; r1.size = size; r1.meta = meta2[1]; r1.corrupt_off = coff2[1];
+      r2.t = e2[0]; r2.src = src; r2.dst = dst; r2.seq = seq; r2.size = size; r2.meta = meta2[0]; r2.corrupt_off = coff2[0];
+      if (adm & 2u) q1 = qid_copy(a.geo, r1, t_end);
+      if (adm & 1u) q2 = qid_copy(a.geo, r2, t_end);
+    }
+    const int qs[2] = {q1, q2};
+    const tgsim_record rs[2] = {r1, r2};
+    a.Q.push_batch<2, kWideWaves>(qs, rs, l + (tid >> 6), true);
+    uint32_t tl, tc, to;
+    (void)wide_excl_scan(n_lost, red, tl);
+    (void)wide_excl_scan(n_copies, red, tc);
+    (void)wide_excl_scan(n_over, red, to);
+    if (tid == 0) {
+      unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
+      if (tl) atomicAdd(&row[ST_LOST], (unsigned long long)tl);
+      if (tc) atomicAdd(&row[ST_COPIES], (unsigned long long)tc);
+      if (to) atomicAdd(&row[ST_OVERLIMIT], (unsigned long long)to);
+      done[l] = 1;
     }
     __syncthreads();
   }
@@ -4157,7 +4443,7 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
-  {
+  if (!a.heavy.pend) {  // with queue tracking k_shape_seq_wide orders the senders of <= kTile messages
     ProfScope ps_(d, KID_SEG_SMALL);  // each sender's deferred messages in (t_send, seq) order
     hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
                        d.seg_off, n_dev, d.cap_rec);
@@ -4175,9 +4461,16 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     hidx = hv;
   }
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
+  if (a.heavy.pend) {  // the whole-sender closed form first (heavy senders without HTB / correlation)
+    ProfScope ps_(d, KID_SHAPE_WIDE);
+    hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, vals, d.corr_sorted, d.moff, hoff, hidx,
+                       d.H, d.seq_done);
+  } else {
+    TG_CHECK(hipMemsetAsync(d.seq_done, 0, std::max<uint32_t>(d.nloc, 1u), d.stream));
+  }
   ProfScope ps_(d, KID_SHAPE_SEQ);  // the sequential lane itself
   hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, hoff, hidx,
-                     d.H, d.cor_rho, d.cor_last, d.X);
+                     d.H, d.cor_rho, d.cor_last, d.X, d.seq_done);
   return hipGetLastError();
 }
 

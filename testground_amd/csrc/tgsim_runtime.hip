@@ -461,6 +461,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.zd, (size_t)c->nloc / 32 + 1);
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.seq_done, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &c->d_red2, 2);
   rc |= dalloc(c, &d.moff, segK);
   rc |= dalloc(c, &d.ipf, c->N);
@@ -1433,6 +1434,7 @@ static int tgsim_set_transport_body(tgsim_ctx* c, const tgsim_transport* t) {
 // The window's exchange (between begin and end): the peer blocks, whole.
 static int exchange_window(tgsim_ctx* c) {
   const size_t block = (size_t)c->d.xcap * sizeof(tgsim_record);
+  ProfScope ps_(c->d, KID_EXCHANGE);  // the window's peer blocks (HIP events on the ctx stream)
   if (c->tr.alltoall(c->tr.user, c->d.xsend, c->d.xrecv, block, c->d.stream) != 0)
     return fail(c, TGSIM_EHIP, "transport all-to-all failed");
   return TGSIM_OK;
@@ -1868,8 +1870,11 @@ static int gen_storm_impl(tgsim_ctx* c, uint32_t round, int64_t t0, uint32_t fan
     // every shard commits the whole batch: its first / last time MAX-reduced over the shards (the
     // count is n_instances: every instance signals), replicated sync state
     HIPCK(c, launch_storm_red(c->d, parts, c->d_red2), "storm reduce");
-    if (c->tr.allreduce_max_i64(c->tr.user, c->d_red2, 2, c->d.stream) != 0)
-      return fail(c, TGSIM_EHIP, "transport all-reduce failed");
+    {
+      ProfScope ps_(c->d, KID_ALLREDUCE);  // the storm batch's SignalAndWait: one MAX all-reduce
+      if (c->tr.allreduce_max_i64(c->tr.user, c->d_red2, 2, c->d.stream) != 0)
+        return fail(c, TGSIM_EHIP, "transport all-reduce failed");
+    }
     HIPCK(c, launch_storm_unpack(c->d, c->d_red2), "storm reduce");
     c->storm_pending = true;
     c->storm_parts = 1;
@@ -2294,7 +2299,7 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
 // writes were linked onto the queues; tgsim_tcp_write does the same after a host write)
 static int storm_tcp_release(tgsim_ctx* c) {
   if (!c->d.sm.tcp) return TGSIM_OK;
-  HIPCK(c, launch_tcp_conn_release(c->d, c->td, false, c->tcp_cur, true, 0), "storm tcp release");
+  HIPCK(c, launch_tcp_conn_release(c->d, c->td, kRelAtWrite, c->tcp_cur, true, 0), "storm tcp release");
   return TGSIM_OK;
 }
 
@@ -2878,7 +2883,7 @@ static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
                             on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch, c->tcp_fill), "tcp react");
   if (c->td.n_conn) {  // the window's ACKs open the connections' windows: send what fits, at its end
-    HIPCK(c, launch_tcp_conn_release(c->d, c->td, true, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
+    HIPCK(c, launch_tcp_conn_release(c->d, c->td, kRelAfterWindow, c->tcp_cur, c->staged_dev, c->n_staged), "tcp release");
     c->staged_dev = true;
   }
   c->tcp_fill = ~0u;
@@ -3042,10 +3047,10 @@ static int conn_grow(tgsim_ctx* c, uint32_t need) {
   const uint32_t cap = std::max<uint32_t>({need, 2 * c->conn_cap, 1024u});
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   uint32_t** u32[] = {&t.c_src, &t.c_dst, &t.c_cwnd, &t.c_ssth, &t.c_cnt, &t.c_flight, &t.c_queued, &t.c_head,
-                      &t.c_acks, &t.c_broken};
+                      &t.c_acks, &t.c_broken, &t.c_una, &t.c_fack};
   for (uint32_t** a : u32)
     if (dgrow(c, a, t.n_conn, cap)) return TGSIM_ENOMEM;
-  if (dgrow(c, &t.c_acked, t.n_conn, cap) || dgrow(c, &t.c_rto, t.n_conn, cap)) return TGSIM_ENOMEM;
+  if (dgrow(c, &t.c_acked, t.n_conn, cap) || dgrow(c, &t.c_tloss, t.n_conn, cap)) return TGSIM_ENOMEM;
   c->conn_cap = cap;
   return TGSIM_OK;
 }
@@ -3069,22 +3074,27 @@ static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint3
   alloc_point(c);
   if (!t.w_conn) {  // first connection: the per-write / per-segment connection tables
     const size_t W = c->tcp.max_writes, S = c->tcp.max_segments;
-    if (dalloc(c, &t.w_conn, W) || dalloc(c, &t.s_next, S) || dalloc(c, &t.s_ack1, S)) return TGSIM_ENOMEM;
+    if (dalloc(c, &t.w_conn, W) || dalloc(c, &t.s_next, S) || dalloc(c, &t.s_ack1, S) || dalloc(c, &t.s_lost, S) ||
+        dalloc(c, &t.s_tq, S))
+      return TGSIM_ENOMEM;
     HIPCK(c, hipMemsetAsync(t.s_ack1, 0, S * 4, c->d.stream), "tcp connect");
+    HIPCK(c, hipMemsetAsync(t.s_lost, 0, S, c->d.stream), "tcp connect");
+    HIPCK(c, hipMemsetAsync(t.s_tq, 0, S, c->d.stream), "tcp connect");
   }
   const uint32_t n0 = t.n_conn, n1 = (uint32_t)(n0 + n);
   int rc = conn_grow(c, n1);
   if (rc) return rc;
   std::vector<uint32_t> a(src, src + n), b(dst, dst + n), iw(n, 10u), ss(n, 0x7FFFFFFFu), none(n, 0xFFFFFFFFu);
-  std::vector<int64_t> never(n, INT64_MIN);
+  std::vector<int64_t> never(n, INT64_MAX);
   hipStream_t st = c->d.stream;
   HIPCK(c, hipMemcpyAsync(t.c_src + n0, a.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_dst + n0, b.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_cwnd + n0, iw.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_ssth + n0, ss.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_head + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
-  HIPCK(c, hipMemcpyAsync(t.c_rto + n0, never.data(), n * 8, hipMemcpyHostToDevice, st), "tcp connect");
-  for (uint32_t* z : {t.c_cnt, t.c_flight, t.c_queued, t.c_acks, t.c_broken})
+  HIPCK(c, hipMemcpyAsync(t.c_una + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_tloss + n0, never.data(), n * 8, hipMemcpyHostToDevice, st), "tcp connect");
+  for (uint32_t* z : {t.c_cnt, t.c_flight, t.c_queued, t.c_acks, t.c_broken, t.c_fack})
     HIPCK(c, hipMemsetAsync(z + n0, 0, n * 4, st), "tcp connect");
   HIPCK(c, hipMemsetAsync(t.c_acked + n0, 0, n * 8, st), "tcp connect");
   HIPCK(c, hipStreamSynchronize(st), "tcp connect");  // the host vectors go out of scope
@@ -3188,7 +3198,7 @@ static int tgsim_tcp_write_body(tgsim_ctx* c, const uint32_t* conn, const uint32
   if (rc) return rc;
   HIPCK(c, launch_tcp_link(c->d, td, c->link_dev, nq), "tcp write");
   // the windows' room goes now, at the write times
-  HIPCK(c, launch_tcp_conn_release(c->d, td, false, c->tcp_cur, c->staged_dev, c->n_staged), "tcp write");
+  HIPCK(c, launch_tcp_conn_release(c->d, td, kRelAtWrite, c->tcp_cur, c->staged_dev, c->n_staged), "tcp write");
   c->staged_dev = true;
   c->conn_tail.swap(tail);
   for (size_t i = 0; i < n; ++i) {  // the queue-limit bound: a sender's new segments (any may leave now)

@@ -179,6 +179,7 @@ __device__ __forceinline__ void tcp_link(TcpDev& t, size_t h, uint32_t prev, uin
   for (uint32_t x = first; x < first + n; ++x) t.s_tatt[x] = tw;
   if (prev != kTcpNoSeg) t.s_next[prev] = first;
   if (t.c_head[h] == kTcpNoSeg) t.c_head[h] = first;
+  if (t.c_una[h] == kTcpNoSeg) t.c_una[h] = first;
   t.c_queued[h] += n;
 }
 

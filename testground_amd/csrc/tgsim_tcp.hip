@@ -166,7 +166,10 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
           t.s_done[sid] = 1;
           if (t.n_conn && atomicExch(&t.s_ack1[sid], 1u) == 0u) {
             const uint32_t k = t.w_conn[t.s_w[sid] & kWMask];
-            if (k != kNoSeg) atomicAdd(&t.c_acks[k], 1u);
+            if (k != kNoSeg) {
+              atomicAdd(&t.c_acks[k], 1u);
+              if (!t.s_lost[sid]) atomicAdd(&t.c_fack[k], 1u);  // a segment marked lost holds no slot
+            }
           }
         }
       } else if (!corrupt) {
@@ -504,24 +507,24 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
       for (uint32_t u = 0; u < kFireUnroll; ++u) wst[u] = live[u] ? t.w_state[sw[u] & kWMask] : 0u;
 #pragma unroll
       for (uint32_t u = 0; u < kFireUnroll; ++u) {
-        if (!live[u] || wst[u] == TGSIM_TCP_TIMEOUT || wst[u] == TGSIM_TCP_REFUSED) continue;
+        if (!live[u]) continue;
         const uint32_t r = r0 + u, w = sw[u] & kWMask;
-        const int64_t T = ta[u] + (t.rto << a[u]);
         const uint32_t k = t.n_conn ? t.w_conn[w] : kNoSeg;
+        // a connection segment marked lost has no timer until it is resent (which enters it again)
+        if (k != kNoSeg && t.s_lost[sid[u]]) { t.s_tq[sid[u]] = 0; continue; }
+        if (wst[u] == TGSIM_TCP_TIMEOUT || wst[u] == TGSIM_TCP_REFUSED) continue;
+        const int64_t T = ta[u] + (t.rto << a[u]);
         if (T >= t_end || (!batch[u] && ta[u] >= H)) {  // not due, or sent in this window
           if (!batch[u]) kmask |= 1u << r;
         } else if (a[u] + 1u >= t.max_att) {
           t.s_done[sid[u]] = 2;
           if (k != kNoSeg) atomicSub(&t.c_flight[k], 1u);
           if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, T, TGSIM_TCP_TIMEOUT);
+        } else if (k != kNoSeg) {
+          // a connection's timeout: the loss episode (k_tcp_conn_release, kRelLoss) resends under cwnd
+          atomicMin(reinterpret_cast<long long*>(&t.c_tloss[k]), (long long)T);
+          t.s_tq[sid[u]] = 0;
         } else {
-          // the connection's first timeout in this window: ssthresh = max(cwnd / 2, 2), cwnd = 1
-          if (k != kNoSeg && atomicMax(reinterpret_cast<long long*>(&t.c_rto[k]), (long long)H) < (long long)H) {
-            const uint32_t cw = t.c_cwnd[k];
-            if (cw > 1u) t.c_ssth[k] = cw / 2u > 2u ? cw / 2u : 2u;  // once per loss episode
-            t.c_cwnd[k] = 1u;
-            t.c_cnt[k] = 0u;
-          }
           t.s_att[sid[u]] = a[u] + 1u;
           t.s_tatt[sid[u]] = T > H ? T : H;
           if (!(sw[u] & kRetxBit)) t.s_w[sid[u]] = sw[u] | kRetxBit;
@@ -572,33 +575,68 @@ __global__ __launch_bounds__(kBlock) void k_tcp_link(TcpDev t, const uint32_t* _
   const uint32_t k = q[4 * i], tail = q[4 * i + 1], first = q[4 * i + 2], cnt = q[4 * i + 3];
   if (tail != kNoSeg) t.s_next[tail] = first;
   if (t.c_head[k] == kNoSeg) t.c_head[k] = first;
+  if (t.c_una[k] == kNoSeg) t.c_una[k] = first;
   t.c_queued[k] += cnt;
 }
 
-// Every connection sends its queued segments while the flight is below cwnd, at max(written, t0).
-// after_window: first the window's ACKs (flight, slow start / congestion avoidance) and resets (a
-// reset connection fails its queued writes), t0 = the window's end. One thread per connection;
-// staged slots and timer-list slots reserved once per block.
-__global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalars* sc, uint32_t after_window,
-                                                             uint32_t cur, uint32_t cap, uint32_t* __restrict__ m_src,
+// Every connection sends while its flight is below cwnd, each segment at max(written, t0): first the
+// segments a loss episode marked lost (in order, the next attempt; settled ones are passed over, one
+// of a failed write or out of attempts gives up), then new ones. Modes (kRel*):
+//   at a write: t0 = the write times;
+//   after a window: first the window's ACKs (flight, slow start / congestion avoidance) and resets (a
+//     reset connection fails its queued writes), t0 = the window's end;
+//   loss: at a window start, the connections whose timer expired in the window just begun (k_tcp_fire:
+//     c_tloss) [EXT Linux tcp_enter_loss, RFC 5681 3.1]: ssthresh = max(cwnd / 2, 2) unless cwnd is
+//     already 1 (the same episode), cwnd = 1, every outstanding segment marked lost and the queue
+//     restarted at the oldest, t0 = max(expiry, window start).
+// One thread per connection; staged slots and timer-list slots reserved once per block. A resent
+// segment that still has an entry on the timer lists keeps it (the entry reads its new attempt).
+__global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalars* sc, uint32_t mode, uint32_t list,
+                                                             uint32_t cap, uint32_t* __restrict__ m_src,
                                                              uint32_t* __restrict__ m_dst,
                                                              uint32_t* __restrict__ m_seq,
                                                              uint32_t* __restrict__ m_size,
                                                              int64_t* __restrict__ m_t) {
   __shared__ uint32_t red[kBlock / 64];
   __shared__ uint32_t sb_m, sb_p;
-  const int64_t t0 = after_window ? sc->t_end : INT64_MIN;
+  const int64_t H = sc->T;
   const uint32_t n = t.n_conn;
+  unsigned long long nretx = 0;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
     const uint32_t k = b0 + threadIdx.x;
-    uint32_t go = 0, head = kNoSeg;
-    if (k < n) {
+    uint32_t go = 0, nent = 0, head = kNoSeg, end = kNoSeg;
+    bool slow = false;
+    int64_t t0 = mode == kRelAfterWindow ? sc->t_end : INT64_MIN;
+    bool act = k < n;
+    if (act && mode == kRelLoss) {
+      const int64_t tl = t.c_tloss[k];
+      act = tl != INT64_MAX;
+      if (act) {
+        t.c_tloss[k] = INT64_MAX;
+        t0 = tl > H ? tl : H;
+        const uint32_t cw = t.c_cwnd[k];
+        if (cw > 1u) t.c_ssth[k] = cw / 2u > 2u ? cw / 2u : 2u;
+        t.c_cwnd[k] = 1u;
+        t.c_cnt[k] = 0u;
+        const uint32_t h0 = t.c_head[k];
+        uint32_t u = t.c_una[k];
+        while (u != h0 && t.s_done[u]) u = t.s_next[u];
+        t.c_una[k] = u;
+        for (uint32_t x = u; x != h0; x = t.s_next[x])
+          if (!t.s_done[x]) t.s_lost[x] = 1;
+        t.c_head[k] = u;
+        t.c_flight[k] = 0u;
+      }
+    }
+    if (act) {
       uint32_t cw = t.c_cwnd[k], fl = t.c_flight[k];
-      if (after_window) {
+      if (mode == kRelAfterWindow) {
         const uint32_t acks = t.c_acks[k];
         if (acks) {
+          const uint32_t fa = t.c_fack[k];
           t.c_acks[k] = 0u;
-          fl -= acks;
+          t.c_fack[k] = 0u;
+          fl -= fa;
           t.c_acked[k] += acks;
           uint32_t ss = t.c_ssth[k], cnt = t.c_cnt[k];
           for (uint32_t a = 0; a < acks; ++a) {
@@ -610,48 +648,101 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
           t.c_cnt[k] = cnt;
           t.c_flight[k] = fl;
         }
-        if (t.c_broken[k]) {  // a reset connection: its queued writes fail
+        if (t.c_broken[k]) {  // a reset connection: its queued (and lost) segments' writes fail
           for (uint32_t sid = t.c_head[k]; sid != kNoSeg; sid = t.s_next[sid]) {
             const int64_t tw = t.s_tatt[sid];
+            const uint32_t w = t.s_w[sid] & kWMask;
             t.s_done[sid] = 2;
-            tcp_fail(t, t.s_w[sid] & kWMask, tw > t0 ? tw : t0, TGSIM_TCP_REFUSED);
+            if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, tw > t0 ? tw : t0, TGSIM_TCP_REFUSED);
           }
           t.c_head[k] = kNoSeg;
           t.c_queued[k] = 0u;
         }
       }
       head = t.c_head[k];
-      const uint32_t qd = t.c_queued[k];
       // a write onto a reset connection stays queued until the next reaction fails it at that
       // window's end (tgo_tcp_write releases only connections that are not broken)
-      go = fl < cw && !t.c_broken[k] ? min(cw - fl, qd) : 0u;
-      if (go) {
-        t.c_flight[k] = fl + go;
-        t.c_queued[k] = qd - go;
+      const uint32_t room = fl < cw && !t.c_broken[k] ? cw - fl : 0u;
+      if (room && head != kNoSeg && !t.s_lost[head] && !t.s_done[head]) {  // only new segments from here
+        go = min(room, t.c_queued[k]);
+        nent = go;
+      } else if (room) {  // segments marked lost first: count the sends, give up the hopeless ones
+        slow = true;
+        uint32_t sid = head;
+        while (sid != kNoSeg && go < room) {
+          const uint32_t nx = t.s_next[sid];
+          if (!t.s_done[sid]) {
+            const uint32_t w = t.s_w[sid] & kWMask;
+            const uint32_t ws = t.w_state[w];
+            if (t.s_lost[sid] && (ws == TGSIM_TCP_TIMEOUT || ws == TGSIM_TCP_REFUSED || t.s_att[sid] + 1u >= t.max_att)) {
+              const int64_t tw = t.s_tatt[sid];
+              t.s_lost[sid] = 0;
+              t.s_done[sid] = 2;
+              if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, tw > t0 ? tw : t0, TGSIM_TCP_TIMEOUT);
+            } else {
+              ++go;
+              nent += t.s_tq[sid] ? 0u : 1u;
+            }
+          }
+          sid = nx;
+        }
+        end = sid;  // past the last send and any segment given up behind it
+        if (go == 0) t.c_head[k] = end;
       }
     }
-    uint32_t tot;
-    const uint32_t pm = block_excl_scan(go, red, tot);
+    uint32_t tm, tp;
+    const uint32_t pm = block_excl_scan(go, red, tm);
+    const uint32_t pp = block_excl_scan(nent, red, tp);
     if (threadIdx.x == 0) {
-      sb_m = tot ? reserve_staged(&sc->n_msgs_dev, tot, cap) : 0u;
-      sb_p = tot ? atomicAdd(&t.sc->pend_n[cur], tot) : 0u;
+      sb_m = tm ? reserve_staged(&sc->n_msgs_dev, tm, cap) : 0u;
+      sb_p = tp ? atomicAdd(&t.sc->pend_n[list], tp) : 0u;
     }
     __syncthreads();
-    uint32_t sid = head;
-    for (uint32_t j = 0; j < go; ++j) {
-      const int64_t tw = t.s_tatt[sid], ts = tw > t0 ? tw : t0;
-      t.s_tatt[sid] = ts;
-      const uint32_t p = sb_m + pm + j;
-      if (p < cap) {
-        m_src[p] = t.c_src[k]; m_dst[p] = t.c_dst[k]; m_seq[p] = sid << 4; m_size[p] = t.s_wire[sid]; m_t[p] = ts;
-      } else {
-        atomicOr(&sc->err, ERR_CAP_M);
+    if (go) {
+      uint32_t sid = head, sent = 0, qd = 0, e = 0;
+      const uint32_t src = t.c_src[k], dst = t.c_dst[k];
+      while (sent < go) {
+        const uint32_t nx = t.s_next[sid];
+        if (!t.s_done[sid]) {
+          const int64_t tw = t.s_tatt[sid], ts = tw > t0 ? tw : t0;
+          uint32_t seq = sid << 4;
+          if (t.s_lost[sid]) {  // the next attempt of a segment marked lost
+            const uint32_t a = t.s_att[sid] + 1u;
+            t.s_att[sid] = a;
+            t.s_lost[sid] = 0;
+            t.s_w[sid] |= kRetxBit;
+            seq |= a;
+            atomicAdd(&t.pend_by[src], 1u);  // released into the window until its status is read
+            ++nretx;
+          } else {
+            ++qd;
+          }
+          t.s_tatt[sid] = ts;
+          const uint32_t p = sb_m + pm + sent;
+          if (p < cap) {
+            m_src[p] = src; m_dst[p] = dst; m_seq[p] = seq; m_size[p] = t.s_wire[sid]; m_t[p] = ts;
+          } else {
+            atomicOr(&sc->err, ERR_CAP_M);
+          }
+          if (!t.s_tq[sid]) {  // its timer
+            t.s_tq[sid] = 1;
+            t.pend[list][sb_p + pp + e++] = sid;
+          }
+          ++sent;
+        }
+        sid = nx;
       }
-      t.pend[cur][sb_p + pm + j] = sid;  // its timer
-      sid = t.s_next[sid];
+      t.c_head[k] = slow ? end : sid;
+      t.c_flight[k] += go;
+      t.c_queued[k] -= qd;
     }
-    if (go) t.c_head[k] = sid;
     __syncthreads();  // sb_m / sb_p are rewritten by the next round
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nretx += __shfl_xor(nretx, o);
+  if (lane_id() == 0 && nretx) {
+    atomicAdd(&t.sc->retx, nretx);
+    atomicAdd(&t.sc->released, nretx);
   }
 }
 
@@ -685,13 +776,13 @@ hipError_t launch_tcp_link(Dev& d, TcpDev& t, const uint32_t* links, uint32_t n)
   return hipGetLastError();
 }
 
-hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, bool after_window, uint32_t cur, bool base_dev,
+hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, uint32_t mode, uint32_t cur, bool base_dev,
                                    uint32_t base_host) {
   if (!t.n_conn) return hipSuccess;
   if (!base_dev) hipLaunchKernelGGL(k_tcp_base, dim3(1), dim3(kBlock), 0, d.stream, d.sc, base_host);
   const unsigned g = std::min<unsigned>((t.n_conn + kBlock - 1) / kBlock, (unsigned)kStreamBlocks);
-  hipLaunchKernelGGL(k_tcp_conn_release, dim3(g), dim3(kBlock), 0, d.stream, t, d.sc, after_window ? 1u : 0u, cur,
-                     d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  hipLaunchKernelGGL(k_tcp_conn_release, dim3(g), dim3(kBlock), 0, d.stream, t, d.sc, mode, cur, d.cap_msgs, d.m_src,
+                     d.m_dst, d.m_seq, d.m_size, d.m_t);
   return hipGetLastError();
 }
 
@@ -720,7 +811,10 @@ hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_de
   hipLaunchKernelGGL(k_tcp_tplan, dim3(1), dim3(kBlock), 0, d.stream, t, d.sc, head, reg ? 1u : 0u, lo, hi, d.cap_msgs);
   hipLaunchKernelGGL(k_tcp_fire, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, t, d.sc, cur, d.cap_msgs, d.o_src, d.o_dst,
                      d.o_seq, d.o_t, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // loss episodes of the connections whose timer fired: their resends' timers join the kept list
+  return launch_tcp_conn_release(d, t, kRelLoss, cur ^ 1u, true, 0);
 }
 
 }  // namespace tgsim

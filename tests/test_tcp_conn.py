@@ -66,22 +66,44 @@ def case_slow_start(b):
 
 
 def case_timeout_then_congestion_avoidance(b):
-    """The first 10 segments are lost twice (the link drops everything until 300 ms): the 200 ms
-    timeout halves ssthresh to 5 and resets cwnd to 1; at 600 ms the third attempt gets through;
-    its 10 ACKs (621 ms) grow cwnd 1 -> 5 in slow start, then one step in congestion avoidance:
-    6 segments leave at 622 ms, their 6 ACKs make it 7, the last 4 leave at 644 ms."""
+    """The first 10 segments are lost (the link drops everything until 300 ms). The 200 ms timeout
+    starts a loss episode: ssthresh 5, cwnd 1, all 10 marked lost and only the oldest resent (lost
+    again); its 600 ms timeout is the same episode (ssthresh stays 5) and its third attempt gets
+    through (610 ms). Every ACK round then resends under cwnd: 2 (cwnd 2), 4 (4), then cwnd 5 in
+    congestion avoidance: the last 3 lost ones and 2 new (676 ms), 6 (698 ms), the last 2 (720 ms)."""
     s = sim(b)
     s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS, loss=100.0), make_shape(latency_ns=10 * MS)])
     s.tcp_connect([0], [1])
     out = run(s, 300 * MS, writes={0: [(0, 20 * MSS)]})
     s.set_shape(0, make_shape(latency_ns=10 * MS))
-    out += run(s, 700 * MS)
-    assert data_arrivals(out, 0) == [(610 * MS, 10), (632 * MS, 6), (654 * MS, 4)]
+    out += run(s, 750 * MS)
+    assert data_arrivals(out, 0) == [(610 * MS, 1), (632 * MS, 2), (654 * MS, 4), (676 * MS, 5), (698 * MS, 6),
+                                     (720 * MS, 2)]
     st, t = s.tcp_writes()
-    assert list(st) == [A.TCP_DELIVERED] and list(t) == [654 * MS]
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [720 * MS]
     cs = s.tcp_conns()
     assert cs["cwnd"].tolist() == [7] and cs["acked"].tolist() == [20]
-    assert s.tcp_stats()["retransmissions"] == 20
+    assert cs["flight"].tolist() == [0] and cs["queued"].tolist() == [0]
+    assert s.tcp_stats()["retransmissions"] == 11
+    s.close()
+
+
+def case_loss_recovery_under_cwnd(b):
+    """DESIGN.md 2.11b's hand case: 10 segments lost once (the link drops everything until 100 ms).
+    The 200 ms timeout marks all 10 lost; they are resent 1, 2, 4, 3 per 22 ms ACK round (cwnd 1,
+    2, 4, then 5 = ssthresh), not all at once."""
+    s = sim(b)
+    s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS, loss=100.0), make_shape(latency_ns=10 * MS)])
+    s.tcp_connect([0], [1])
+    out = run(s, 100 * MS, writes={0: [(0, 10 * MSS)]})
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    out += run(s, 300 * MS)
+    assert data_arrivals(out, 0) == [(210 * MS, 1), (232 * MS, 2), (254 * MS, 4), (276 * MS, 3)]
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [276 * MS]
+    cs = s.tcp_conns()
+    assert cs["cwnd"].tolist() == [6] and cs["acked"].tolist() == [10] and cs["flight"].tolist() == [0]
+    assert s.tcp_stats()["retransmissions"] == 10
     s.close()
 
 
@@ -120,7 +142,8 @@ def case_errors(b):
     s.close()
 
 
-CASES = [case_slow_start, case_timeout_then_congestion_avoidance, case_queued_writes_and_reset, case_errors]
+CASES = [case_slow_start, case_timeout_then_congestion_avoidance, case_loss_recovery_under_cwnd, case_queued_writes_and_reset,
+         case_errors]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda f: f.__name__)
