@@ -44,7 +44,8 @@ METRIC = "simulated msgs delivered/sec (100k-inst storm) + % HBM roofline, 1/2/4
 #   k_emit_bucket.
 ALG_MODELS = {
     "k_extract_shape": lambda d, n, w: 25 * (d["msgs_in"] - d.get("deferred", 0)) + 48 * n * w,
-    "k_shape_seq": lambda d, n, w: 25 * d.get("deferred", 0),
+    "k_shape_seq": lambda d, n, w: 25 * (d.get("deferred", 0) - d.get("wide", 0)),
+    "k_shape_seq_wide": lambda d, n, w: 25 * d.get("wide", 0),
     "k_tb_bucket": lambda d, n, w: 16 * n * w,
     "k_emit_bucket": lambda d, n, w: 24 * (d["delivered"] - d.get("long_emit", 0)),
     "k_wheel_scatter": lambda d, n, w: 24 * d.get("long_emit", 0),
@@ -79,8 +80,13 @@ BYTE_MODELS = {
     # the sequential lane: per deferred message its 24 B record and 16 B (t, seq) order entry read,
     # its 1 B status and a 32 B copy record written; k_seg_small orders them: per deferred message
     # the (key, index) pair read, (t_send, seq) gathered (12 B), the index written (4 B)
-    "k_shape_seq": lambda d: 73 * d.get("deferred", 0),
+    "k_shape_seq": lambda d: 73 * (d.get("deferred", 0) - d.get("wide", 0)),
     "k_seg_small": lambda d: 24 * d.get("deferred", 0),
+    # the whole-sender closed form: as the sequential lane plus its own ordering (the index read and
+    # written back in place, (t_send, seq) gathered); k_copy_n keeps the group-by's order (4 B read,
+    # 4 B written per deferred message)
+    "k_shape_seq_wide": lambda d: 81 * d.get("wide", 0),
+    "k_copy_n": lambda d: 8 * d.get("deferred", 0),
     # flood (config 5): count reads (dst, src, seq) and writes count + first flag per delivery;
     # emit writes the 24 B staged message per forward after re-reading the 17 B per delivery
     "k_flood_count": lambda d: 21 * d["delivered"],

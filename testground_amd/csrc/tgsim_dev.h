@@ -13,7 +13,7 @@ enum KernelId : int {
   KID_SHAPE = 0, KID_EXTRACT, KID_TB, KID_EMIT, KID_RADIX_HIST, KID_RADIX_ROWS, KID_RADIX_SCATTER,
   KID_KEYS, KID_BOUNDS, KID_REGION_FILL, KID_GEN, KID_SIG, KID_LARGE, KID_BKT_HIST, KID_BKT_SCATTER,
   KID_BKT_SORT, KID_SEG_REST, KID_FLOOD_COUNT, KID_FLOOD_EMIT, KID_SHAPE_SEQ, KID_PROBE, KID_SEG_SMALL, KID_STORM,
-  KID_EXCHANGE, KID_ALLREDUCE, KID_SHAPE_WIDE, KID_COUNT
+  KID_EXCHANGE, KID_ALLREDUCE, KID_SHAPE_WIDE, KID_COPY, KID_COUNT
 };
 extern const char* const kKernelNames[KID_COUNT];
 

@@ -115,6 +115,7 @@ struct DevScalars {
 enum { KC_DEFERRED = 0,   // messages decided in the sequential lane (k_shape_seq)
        KC_LONG_TB = 1,    // token-bucket copies of senders with long runs (k_rest<TB>)
        KC_LONG_EMIT = 2,  // deliveries of long inboxes, written by k_rest<Emit> (the wheel-insert launch)
+       KC_WIDE = 3,       // deferred messages decided by k_shape_seq_wide (the rest: k_shape_seq)
        KC_COUNT = 4 };
 enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_EXTERNAL, ST_DESTDOWN,
        ST_LOCAL, ST_DELIVERED, ST_TB_ITEMS, ST_EXTRACTED, ST_INSERTED };

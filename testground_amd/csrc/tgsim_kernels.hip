@@ -22,7 +22,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_extract_shape", "k_extract", "k_tb_bucket", "k_emit_bucket", "k_radix_hist", "k_radix_rows", "k_radix_scatter",
     "k_keys", "k_bounds", "k_wheel_scatter", "k_gen_storm", "sync_signal", "large_segments",
     "k_bkt_hist", "k_bkt_scatter", "k_bkt_sort", "seg_rest", "k_flood_count", "k_flood_emit",
-    "k_shape_seq", "k_probe", "k_seg_small", "k_storm", "exchange", "allreduce", "k_shape_seq_wide"};
+    "k_shape_seq", "k_probe", "k_seg_small", "k_storm", "exchange", "allreduce", "k_shape_seq_wide", "k_copy_n"};
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
@@ -908,6 +908,10 @@ __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, con
 
 constexpr int kBktMaxKeyBits = 13;  // keys per bucket <= 8192 (32 KB of LDS counters)
 constexpr int kGlobUnroll = 8;      // items in flight per thread where one workgroup walks a whole bucket
+#ifndef TGSIM_OVER_UNROLL
+#define TGSIM_OVER_UNROLL 8
+#endif
+constexpr int kOverUnroll = TGSIM_OVER_UNROLL;  // the same in a fused consumer's oversized bucket
 
 // Bucket of a key: b = k / w by a multiply-shift. m = ceil(2^32 / w) is exact when w is a power of
 // two, and for any w while k * w < 2^32 (nloc <= 2^20, w <= 512 on the fused path).
@@ -1157,20 +1161,20 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv b
 
 // Counting part of bkt_count_keys (h known, cnt[0, h.nk) zeroed and visible): key counts of the
 // bucket's items kin[h.start, +h.nb), exclusive offsets in cnt[], and the longest segment.
-__device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t* cnt, uint32_t* part,
-                                                   const BktHead& h) {
+template <int U = kGlobUnroll, class KeyAt>
+__device__ __forceinline__ uint32_t bkt_count_f(const KeyAt& key_at, uint32_t* cnt, uint32_t* part, const BktHead& h) {
   const uint32_t tid = threadIdx.x;
-  // kGlobUnroll keys in flight per thread: one workgroup walks an oversized bucket alone (a probed
-  // target's 10k-request inbox), and a load per iteration made that a chain of ~40 latencies
-  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
-    uint32_t k[kGlobUnroll];
+  // U keys in flight per thread: one workgroup walks an oversized bucket alone (a probed target's
+  // 10k-request inbox), and a load per iteration made that a chain of ~40 latencies
+  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * U) {
+    uint32_t k[U];
 #pragma unroll
-    for (int u = 0; u < kGlobUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint32_t j = j0 + u * kBlock;
-      k[u] = j < h.nb ? kin[h.start + j] : 0xFFFFFFFFu;
+      k[u] = j < h.nb ? key_at(j) : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int u = 0; u < kGlobUnroll; ++u)
+    for (int u = 0; u < U; ++u)
       if (k[u] != 0xFFFFFFFFu) atomicAdd(&cnt[k[u] - h.k0], 1u);
   }
   __syncthreads();
@@ -1199,15 +1203,19 @@ __device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t
   __syncthreads();
   return m;
 }
+__device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t* cnt, uint32_t* part,
+                                                   const BktHead& h) {
+  return bkt_count_f([&](uint32_t j) { return kin[h.start + j]; }, cnt, part, h);
+}
 
 // Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
 // medium (medium_above < len <= kTile) / large (len > kTile) segment lists.
 constexpr uint32_t kNoMedium = 0xFFFFFFFFu;
-__device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                                uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
-                                                const BktHead& h, uint32_t* off, uint32_t* off2,
-                                                uint32_t medium_above, uint32_t* medium, LargeSeg* large,
-                                                DevScalars* sc) {
+template <int U = kGlobUnroll, class ItemAt>
+__device__ __forceinline__ void bkt_emit_global_f(const ItemAt& item_at, uint32_t* kout, uint32_t* vout, uint32_t B,
+                                                  uint32_t K, uint32_t* cnt, const BktHead& h, uint32_t* off,
+                                                  uint32_t* off2, uint32_t medium_above, uint32_t* medium,
+                                                  LargeSeg* large, DevScalars* sc) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < h.nk; i += kBlock) {
     const uint32_t a = cnt[i];
@@ -1232,23 +1240,29 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
     if (off2) off2[h.k0 + h.nk] = h.start + h.nb;
   }
   __syncthreads();
-  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
-    uint32_t k[kGlobUnroll], v[kGlobUnroll];
+  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * U) {
+    uint2 e[U];
 #pragma unroll
-    for (int u = 0; u < kGlobUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint32_t j = j0 + u * kBlock;
-      const bool in = j < h.nb;
-      k[u] = in ? kin[h.start + j] : 0xFFFFFFFFu;
-      v[u] = in ? vin[h.start + j] : 0u;
+      e[u] = j < h.nb ? item_at(j) : make_uint2(0xFFFFFFFFu, 0u);
     }
 #pragma unroll
-    for (int u = 0; u < kGlobUnroll; ++u) {
-      if (k[u] == 0xFFFFFFFFu) continue;
-      const uint32_t pos = h.start + atomicAdd(&cnt[k[u] - h.k0], 1u);
-      kout[pos] = k[u];
-      vout[pos] = v[u];
+    for (int u = 0; u < U; ++u) {
+      if (e[u].x == 0xFFFFFFFFu) continue;
+      const uint32_t pos = h.start + atomicAdd(&cnt[e[u].x - h.k0], 1u);
+      kout[pos] = e[u].x;
+      vout[pos] = e[u].y;
     }
   }
+}
+__device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
+                                                const BktHead& h, uint32_t* off, uint32_t* off2,
+                                                uint32_t medium_above, uint32_t* medium, LargeSeg* large,
+                                                DevScalars* sc) {
+  bkt_emit_global_f([&](uint32_t j) { return make_uint2(kin[h.start + j], vin[h.start + j]); }, kout, vout, B, K, cnt,
+                    h, off, off2, medium_above, medium, large, sc);
 }
 
 // pass 3: one workgroup per bucket, global form only (signals, and > 2^bs-key fallbacks).
@@ -1918,6 +1932,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
   if (threadIdx.x == 0) sm.maxlen = 0;
   __syncthreads();
   TG_PH(1);
+#ifdef TGSIM_BKT_COPY3
   if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest: contiguous copy first
     for (uint32_t j0 = threadIdx.x; j0 < h.nb; j0 += kBlock * kGlobUnroll) {
       uint2 e[kGlobUnroll];
@@ -1936,6 +1951,20 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     __syncthreads();
     (void)bkt_count_body(kscr, sm.cnt, sm.part, h);
     bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
+    return false;
+  }
+#endif
+  if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest
+    // two passes straight over the partition's chunks (the chunk table stays in LDS): key counts,
+    // then the grouped scatter (a contiguous copy first cost a third pass over the bucket: a probed
+    // target's 10k-request inbox walked by this one workgroup)
+    auto at = [&](uint32_t j) {
+      const uint32_t p = chunk_of(cexcl, j);
+      return kv[csrc[p] + (j - cexcl[p])];
+    };
+    (void)bkt_count_f<kOverUnroll>([&](uint32_t j) { return at(j).x; }, sm.cnt, sm.part, h);
+    bkt_emit_global_f<kOverUnroll>(at, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
+    (void)kscr; (void)vscr;
     return false;
   }
   // this thread's items (strided: consecutive positions used to leave half the threads idle)
@@ -2331,6 +2360,14 @@ __global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const
     keys[j] = src[i] - lo;
     vals[j] = i;
   }
+}
+
+// dst[0, n) = src[0, n), n device-side (the deferred messages' group-by output, which the heavy
+// senders' group-by that follows overwrites, kept for k_shape_seq_wide's per-sender sort)
+__global__ __launch_bounds__(kBlock) void k_copy_n(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                   const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = min(*n_ptr, cap);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) dst[i] = src[i];
 }
 
 struct CorrPolicy {
@@ -3023,7 +3060,7 @@ __device__ __forceinline__ int64_t wide_excl_min(int64_t v, int64_t* red) {
   return ex < pre ? ex : pre;
 }
 
-__global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,
+__global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,  // may alias
                                                           const uint32_t* moff, const uint32_t* hoff,
                                                           const uint32_t* hidx, const tgsim_record* H,
                                                           uint8_t* done) {
@@ -3245,6 +3282,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       if (tl) atomicAdd(&row[ST_LOST], (unsigned long long)tl);
       if (tc) atomicAdd(&row[ST_COPIES], (unsigned long long)tc);
       if (to) atomicAdd(&row[ST_OVERLIMIT], (unsigned long long)to);
+      atomicAdd(&sc->kc[KC_WIDE], (unsigned long long)n);
       done[l] = 1;
     }
     __syncthreads();
@@ -3892,6 +3930,12 @@ __device__ __forceinline__ void count_long(const DevScalars* sc, uint32_t len) {
     atomicAdd(const_cast<unsigned long long*>(&sc->kc[KcLong<P>::v]), (unsigned long long)len);
 }
 
+#ifdef TGSIM_PHASE_PROF
+// debug builds: per task of the last task-parallel long-segment pass, {task | block << 32 | rank << 63,
+// claimed, ready (chunk: sorted; rank: its chunks counted), done} in s_memrealtime ticks (100 MHz)
+__device__ uint64_t g_task_ph[4096][4];
+#endif
+
 template <class P>
 __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, const uint32_t* vals, const uint32_t* off,
                                           const uint32_t* medium, const LargeSeg* large, const DevScalars* sc,
@@ -3921,6 +3965,8 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
   }
   if (!par) return;
   // task table: chunk tasks of segment i at [c1[i], c1[i + 1]), its rank tasks at T1 + [c2[i], c2[i + 1])
+  // (measured: pinning a segment's tasks to the blocks of one XCD, so its chunks stay in that L2,
+  // made the 10k inbox slower - 57 -> 70 us for the launch: a quarter of the chip's CUs per segment)
   {
     const uint32_t i = threadIdx.x;  // nl <= kLargeTab = kBlock
     uint32_t a = 0, b = 0, ta, tb;
@@ -3946,6 +3992,15 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     const uint32_t task = __builtin_amdgcn_readfirstlane(s_task);
     if (task >= T) break;
     const bool chunk = task < T1;
+#ifdef TGSIM_PHASE_PROF
+    const uint64_t tp_claim = __builtin_amdgcn_s_memrealtime();
+#define TASK_PH(ready) do { if (threadIdx.x == 0 && task < 4096) { \
+      g_task_ph[task][0] = task | ((uint64_t)blockIdx.x << 32) | (chunk ? 0ull : 1ull << 63); \
+      g_task_ph[task][1] = tp_claim; g_task_ph[task][2] = (ready); \
+      g_task_ph[task][3] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+#else
+#define TASK_PH(ready) do {} while (0)
+#endif
     const uint32_t* tab = chunk ? s_c1 : s_c2;
     const uint32_t r = chunk ? task : task - T1;
     uint32_t i = 0, hi = nl;  // the segment: last i with tab[i] <= r
@@ -3958,9 +4013,13 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     if (chunk) {
       if (r == s_c1[i]) count_long<P>(sc, L.len);  // the segment's first chunk task counts it
       large_chunk_sort(p, s, L, (r - s_c1[i]) * kParChunk, keys, vals, K1a, K2a, K3a, kParChunk);
+#ifdef TGSIM_PHASE_PROF
+      const uint64_t tp_sorted = __builtin_amdgcn_s_memrealtime();
+#endif
       __threadfence();  // the sorted chunk is visible device-wide before it is counted
       __syncthreads();
       if (threadIdx.x == 0) atomicAdd(&lg[i].pad, 1u);
+      TASK_PH(tp_sorted);
       continue;
     }
     if (threadIdx.x == 0) {
@@ -3977,6 +4036,9 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     }
     __syncthreads();
     __threadfence();
+#ifdef TGSIM_PHASE_PROF
+    const uint64_t tp_ready = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t e = (r - s_c2[i]) * kRankTile + threadIdx.x;
     if (e < L.len) {
       const uint32_t x = L.start + e, c = e / kParChunk;
@@ -3997,6 +4059,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
       }
       large_place(p, L, rank, k1, k2, k3, K1b, K2b, K3b);
     }
+    TASK_PH(tp_ready);
     if (LargeScan<P>::v) {  // compile-time: the segment's last rank task runs the scan
       __threadfence();
       __syncthreads();
@@ -4443,10 +4506,16 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
-  if (!a.heavy.pend) {  // with queue tracking k_shape_seq_wide orders the senders of <= kTile messages
+  if (!a.heavy.pend) {
     ProfScope ps_(d, KID_SEG_SMALL);  // each sender's deferred messages in (t_send, seq) order
     hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
                        d.seg_off, n_dev, d.cap_rec);
+  } else {
+    // with queue tracking, k_shape_seq_wide orders each sender of <= kTile messages itself, in
+    // place in corr_sorted (the H group-by below reuses the group-by's output arrays)
+    ProfScope ps_(d, KID_COPY);
+    hipLaunchKernelGGL(k_copy_n, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, vals, d.corr_sorted, n_dev,
+                       d.cap_rec);
   }
   TG_CHECK(hipGetLastError());
   TG_CHECK(launch_rest(d, p, keys, vals));
@@ -4463,8 +4532,8 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
   if (a.heavy.pend) {  // the whole-sender closed form first (heavy senders without HTB / correlation)
     ProfScope ps_(d, KID_SHAPE_WIDE);
-    hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, vals, d.corr_sorted, d.moff, hoff, hidx,
-                       d.H, d.seq_done);
+    hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
+                       hoff, hidx, d.H, d.seq_done);
   } else {
     TG_CHECK(hipMemsetAsync(d.seq_done, 0, std::max<uint32_t>(d.nloc, 1u), d.stream));
   }
@@ -4722,6 +4791,10 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 // debug builds only: the phase clocks of the last k_tb_bucket / k_emit_bucket launches
 extern "C" int tgsim_debug_phases(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_tg_ph), sizeof(tgsim::g_tg_ph));
+}
+// ... and of the last task-parallel long-segment pass (per task)
+extern "C" int tgsim_debug_task_phases(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_task_ph), sizeof(tgsim::g_task_ph));
 }
 // ... and of the last k_shape_seq launch (per block: its last sender)
 extern "C" int tgsim_debug_seq_phases(uint64_t* out) {
