@@ -1161,6 +1161,7 @@ __device__ __forceinline__ uint32_t bkt_count_keys(const uint32_t* kin, BktDiv b
 
 // Counting part of bkt_count_keys (h known, cnt[0, h.nk) zeroed and visible): key counts of the
 // bucket's items kin[h.start, +h.nb), exclusive offsets in cnt[], and the longest segment.
+__device__ __forceinline__ uint32_t bkt_scan_counts(uint32_t* cnt, uint32_t* part, const BktHead& h);
 template <int U = kGlobUnroll, class KeyAt>
 __device__ __forceinline__ uint32_t bkt_count_f(const KeyAt& key_at, uint32_t* cnt, uint32_t* part, const BktHead& h) {
   const uint32_t tid = threadIdx.x;
@@ -1178,6 +1179,11 @@ __device__ __forceinline__ uint32_t bkt_count_f(const KeyAt& key_at, uint32_t* c
       if (k[u] != 0xFFFFFFFFu) atomicAdd(&cnt[k[u] - h.k0], 1u);
   }
   __syncthreads();
+  return bkt_scan_counts(cnt, part, h);
+}
+// key counts cnt[0, h.nk) -> exclusive offsets; returns the longest segment
+__device__ __forceinline__ uint32_t bkt_scan_counts(uint32_t* cnt, uint32_t* part, const BktHead& h) {
+  const uint32_t tid = threadIdx.x;
   const uint32_t per = (h.nk + kBlock - 1) / kBlock, i0 = tid * per;
   uint32_t sum = 0, mx = 0;
   for (uint32_t i = 0; i < per && i0 + i < h.nk; ++i) {
@@ -1211,11 +1217,36 @@ __device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t
 // Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
 // medium (medium_above < len <= kTile) / large (len > kTile) segment lists.
 constexpr uint32_t kNoMedium = 0xFFFFFFFFu;
+__device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const BktHead& h, uint32_t* off, uint32_t* off2,
+                                                   uint32_t medium_above, uint32_t* medium, LargeSeg* large,
+                                                   DevScalars* sc);
 template <int U = kGlobUnroll, class ItemAt>
 __device__ __forceinline__ void bkt_emit_global_f(const ItemAt& item_at, uint32_t* kout, uint32_t* vout, uint32_t B,
                                                   uint32_t K, uint32_t* cnt, const BktHead& h, uint32_t* off,
                                                   uint32_t* off2, uint32_t medium_above, uint32_t* medium,
                                                   LargeSeg* large, DevScalars* sc) {
+  const uint32_t tid = threadIdx.x;
+  bkt_global_offsets(cnt, h, off, off2, medium_above, medium, large, sc);
+  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * U) {
+    uint2 e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      e[u] = j < h.nb ? item_at(j) : make_uint2(0xFFFFFFFFu, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e[u].x == 0xFFFFFFFFu) continue;
+      const uint32_t pos = h.start + atomicAdd(&cnt[e[u].x - h.k0], 1u);
+      kout[pos] = e[u].x;
+      vout[pos] = e[u].y;
+    }
+  }
+}
+// the global form's key offsets off[k] (+ off2) and its medium / large segment lists
+__device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const BktHead& h, uint32_t* off, uint32_t* off2,
+                                                   uint32_t medium_above, uint32_t* medium, LargeSeg* large,
+                                                   DevScalars* sc) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < h.nk; i += kBlock) {
     const uint32_t a = cnt[i];
@@ -1240,21 +1271,6 @@ __device__ __forceinline__ void bkt_emit_global_f(const ItemAt& item_at, uint32_
     if (off2) off2[h.k0 + h.nk] = h.start + h.nb;
   }
   __syncthreads();
-  for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * U) {
-    uint2 e[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t j = j0 + u * kBlock;
-      e[u] = j < h.nb ? item_at(j) : make_uint2(0xFFFFFFFFu, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (e[u].x == 0xFFFFFFFFu) continue;
-      const uint32_t pos = h.start + atomicAdd(&cnt[e[u].x - h.k0], 1u);
-      kout[pos] = e[u].x;
-      vout[pos] = e[u].y;
-    }
-  }
 }
 __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                                                 uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
@@ -1565,6 +1581,34 @@ __device__ __forceinline__ void span_sort(SortSmem& s, uint32_t m, const uint32_
   __syncthreads();
 }
 
+// The sort keys of (keys, vals)[st, st + cnt) into LDS positions [0, cnt), padding up to npad: four
+// elements per thread with every level of their loads (pair, then the policy's gather) in flight
+// together - a loop of one element at a time was a chain of 2 x 4 dependent round trips per chunk.
+template <class P>
+__device__ __forceinline__ void load_span_keys(const P& p, SortSmem& s, const uint32_t* keys, const uint32_t* vals,
+                                               uint32_t st, uint32_t cnt, uint32_t npad) {
+  constexpr int U = 4;
+  for (uint32_t j0 = threadIdx.x; j0 < npad; j0 += kBlock * U) {
+    uint32_t kk[U], vv[U], sg[U], k3[U];
+    uint64_t k1[U], k2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      kk[u] = j < cnt ? keys[st + j] : 0u;
+      vv[u] = j < cnt ? vals[st + j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (j0 + u * kBlock < cnt) p.key(kk[u], vv[u], sg[u], k1[u], k2[u], k3[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * kBlock;
+      if (j < cnt) { s.sg[j] = sg[u]; s.k1[j] = k1[u]; s.k2[j] = k2[u]; s.k3[j] = k3[u]; }
+      else if (j < npad) pad_key(s, j);
+    }
+  }
+}
+
 template <class P>
 __global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys, const uint32_t* vals,
                                                       const uint32_t* off, const uint32_t* n_ptr,
@@ -1581,10 +1625,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_small(P p, const uint32_t* keys,
     if (off[kl + 1] - off[kl] > (uint32_t)kTile) s_next = off[kl];
     if (s_next <= s_begin) continue;
     const uint32_t m = s_next - s_begin;
-    for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
-      const uint32_t i = s_begin + j;
-      p.key(keys[i], vals[i], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-    }
+    load_span_keys(p, s, keys, vals, s_begin, m, m);
     __syncthreads();
     span_sort(s, m, off, s_begin);
     p.epilogue(s, m, s_begin, off, w);
@@ -1955,15 +1996,36 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
   }
 #endif
   if (h.nb > (uint32_t)kBktCap) {  // every key of the bucket goes to k_rest
-    // two passes straight over the partition's chunks (the chunk table stays in LDS): key counts,
-    // then the grouped scatter (a contiguous copy first cost a third pass over the bucket: a probed
-    // target's 10k-request inbox walked by this one workgroup)
-    auto at = [&](uint32_t j) {
-      const uint32_t p = chunk_of(cexcl, j);
-      return kv[csrc[p] + (j - cexcl[p])];
-    };
-    (void)bkt_count_f<kOverUnroll>([&](uint32_t j) { return at(j).x; }, sm.cnt, sm.part, h);
-    bkt_emit_global_f<kOverUnroll>(at, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
+    // two passes straight over the partition's chunks, thread p walking chunk p's contiguous items
+    // (no item -> chunk search): key counts, then the grouped scatter. A contiguous copy first (and
+    // a search per item) cost a third pass over the bucket: a probed target's 10k-request inbox,
+    // walked by this one workgroup
+    const uint32_t p = threadIdx.x;
+    const uint32_t cn = (p + 1 < (uint32_t)kRadixBlocks ? cexcl[p + 1] : h.nb) - cexcl[p];
+    const uint2* run = kv + csrc[p];
+    for (uint32_t i0 = 0; i0 < cn; i0 += kOverUnroll) {
+      uint32_t k[kOverUnroll];
+#pragma unroll
+      for (int u = 0; u < kOverUnroll; ++u) k[u] = i0 + u < cn ? run[i0 + u].x : 0xFFFFFFFFu;
+#pragma unroll
+      for (int u = 0; u < kOverUnroll; ++u)
+        if (k[u] != 0xFFFFFFFFu) atomicAdd(&sm.cnt[k[u] - h.k0], 1u);
+    }
+    __syncthreads();
+    (void)bkt_scan_counts(sm.cnt, sm.part, h);
+    bkt_global_offsets(sm.cnt, h, off, off2, 0, medium, large, sc);
+    for (uint32_t i0 = 0; i0 < cn; i0 += kOverUnroll) {
+      uint2 e[kOverUnroll];
+#pragma unroll
+      for (int u = 0; u < kOverUnroll; ++u) e[u] = i0 + u < cn ? run[i0 + u] : make_uint2(0xFFFFFFFFu, 0u);
+#pragma unroll
+      for (int u = 0; u < kOverUnroll; ++u) {
+        if (e[u].x == 0xFFFFFFFFu) continue;
+        const uint32_t pos = h.start + atomicAdd(&sm.cnt[e[u].x - h.k0], 1u);
+        kout[pos] = e[u].x;
+        vout[pos] = e[u].y;
+      }
+    }
     (void)kscr; (void)vscr;
     return false;
   }
@@ -3060,6 +3122,38 @@ __device__ __forceinline__ int64_t wide_excl_min(int64_t v, int64_t* red) {
   return ex < pre ? ex : pre;
 }
 
+// Ascending bitonic sort of one 64-bit key per thread over threads [0, np2) of the block (np2 a
+// power of two <= kWide): a stage whose partners are less than 64 apart runs in registers (cross-lane
+// shuffles), only the others go through LDS (`lds`, np2 entries) - 10 of the 55 stages at 1024.
+__device__ __forceinline__ uint64_t wide_bitonic(uint64_t x, uint32_t np2, uint64_t* lds) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t k = 2; k <= np2; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      uint64_t y;
+      if (j >= 64) {  // block-uniform
+        __syncthreads();  // the previous LDS stage's reads are done
+        if (tid < np2) lds[tid] = x;
+        __syncthreads();
+        y = tid < np2 ? lds[tid ^ j] : x;
+      } else {
+        y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), (int)j) << 32) |
+            (uint32_t)__shfl_xor((int)(uint32_t)x, (int)j);
+      }
+      const bool keep_lo = ((tid & k) == 0) == ((tid & j) == 0);
+      const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+      x = keep_lo ? lo : hi;
+    }
+  return x;
+}
+
+#ifdef TGSIM_PHASE_PROF
+// debug builds: per block (its last sender) of the last k_shape_seq_wide launch, s_memrealtime at:
+// start, sorted, K ready, copies drawn, decided, appended, end
+__device__ uint64_t g_wide_ph[4096][8];
+#define WIDE_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_wide_ph[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define WIDE_PH(k) do {} while (0)
+#endif
 __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,  // may alias
                                                           const uint32_t* moff, const uint32_t* hoff,
                                                           const uint32_t* hidx, const tgsim_record* H,
@@ -3080,37 +3174,80 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       if (tid == 0) done[l] = 0;
       continue;
     }
-    // the sender's deferred messages in (t_send, seq) order (k_seg_small<CorrPolicy>'s order, which
-    // this kernel replaces for every sender of at most kWide = kTile of them): one bitonic sort in LDS
-    // over (t_send, seq, index), unique keys
+    WIDE_PH(0);
+    // the sender's deferred messages in (t_send, seq, index) order (k_seg_small<CorrPolicy>'s order,
+    // which this kernel replaces for every sender of at most kWide = kTile of them). Packed: one
+    // 64-bit key (t_send - min << 42 | seq << 10 | position) sorted mostly in registers, when the
+    // send times span less than 2^22 ns and no two messages share (t_send, seq); else the exact sort
+    // over (t_send, seq, index) in LDS.
     {
       const uint32_t np2m = n > 1 ? next_pow2(n) : 1u;
+      uint32_t i = 0, sq = 0;
+      int64_t ts = 0;
       if (tid < n) {
-        const uint32_t i = gvals[j0 + tid];
-        S1[tid] = (uint64_t)a.t[i] ^ 0x8000000000000000ull;
-        S2[tid] = a.seq[i];
+        i = gvals[j0 + tid];
+        ts = a.t[i];
+        sq = a.seq[i];
         S3[tid] = i;
-      } else if (tid < np2m) {
-        S1[tid] = ~0ull; S2[tid] = ~0u; S3[tid] = ~0u;
       }
+      int64_t mn = tid < n ? ts : INT64_MAX, mx = tid < n ? ts : INT64_MIN;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
+        mn = x < mn ? x : mn;
+        mx = y > mx ? y : mx;
+      }
+      if (lane_id() == 0) { rmin[tid >> 6] = mn; rmax[tid >> 6] = mx; }
+      if (tid == 0) s_flag = 0;
       __syncthreads();
-      for (uint32_t k = 2; k <= np2m; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-          if (tid < np2m) {
-            const uint32_t p = tid ^ j;
-            if (p > tid) {
-              const uint64_t x1 = S1[tid], y1 = S1[p];
-              const uint32_t x2 = S2[tid], y2 = S2[p], x3 = S3[tid], y3 = S3[p];
-              const bool gt = x1 != y1 ? x1 > y1 : (x2 != y2 ? x2 > y2 : x3 > y3);
-              if (gt == ((tid & k) == 0)) {
-                S1[tid] = y1; S1[p] = x1; S2[tid] = y2; S2[p] = x2; S3[tid] = y3; S3[p] = x3;
+#pragma unroll
+      for (int w = 0; w < kWideWaves; ++w) {
+        mn = rmin[w] < mn ? rmin[w] : mn;
+        mx = rmax[w] > mx ? rmax[w] : mx;
+      }
+      const bool packed = (uint64_t)(mx - mn) < (1ull << 22);  // block-uniform
+      if (packed) {
+        uint64_t key = tid < n ? ((uint64_t)(ts - mn) << 42) | ((uint64_t)sq << 10) | tid : ~0ull;
+        key = wide_bitonic(key, np2m, S1);
+        __syncthreads();
+        if (tid < np2m) S1[tid] = key;
+        __syncthreads();
+        if (tid > 0 && tid < n && (S1[tid] >> 10) == (S1[tid - 1] >> 10)) s_flag = 1u;  // a (t_send, seq) tie
+        __syncthreads();
+        if (!s_flag && tid < n) S2[tid] = S3[key & 1023u];  // the message at sorted position tid
+        __syncthreads();
+        if (!s_flag && tid < n) S3[tid] = S2[tid];
+      }
+      if (!packed || s_flag) {  // block-uniform
+        if (tid < n) {
+          i = gvals[j0 + tid];
+          S1[tid] = (uint64_t)a.t[i] ^ 0x8000000000000000ull;
+          S2[tid] = a.seq[i];
+          S3[tid] = i;
+        } else if (tid < np2m) {
+          S1[tid] = ~0ull; S2[tid] = ~0u; S3[tid] = ~0u;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= np2m; k <<= 1)
+          for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (tid < np2m) {
+              const uint32_t p = tid ^ j;
+              if (p > tid) {
+                const uint64_t x1 = S1[tid], y1 = S1[p];
+                const uint32_t x2 = S2[tid], y2 = S2[p], x3 = S3[tid], y3 = S3[p];
+                const bool gt = x1 != y1 ? x1 > y1 : (x2 != y2 ? x2 > y2 : x3 > y3);
+                if (gt == ((tid & k) == 0)) {
+                  S1[tid] = y1; S1[p] = x1; S2[tid] = y2; S2[p] = x2; S3[tid] = y3; S3[p] = x3;
+                }
               }
             }
+            __syncthreads();
           }
-          __syncthreads();
-        }
+      }
+      __syncthreads();
       if (tid < n) sorted[j0 + tid] = S3[tid];
     }
+    WIDE_PH(1);
     const ShapeDev sh = a.shape[l];
     const uint32_t h0 = hoff ? hoff[l] : 0u, h1 = hoff ? hoff[l + 1] : 0u, n0 = h1 - h0;
     if (!a.heavy.of(l) || (sh.flags & (kShCorr | kShLimited)) || n0 > (uint32_t)kWide || !hoff) {
@@ -3122,13 +3259,12 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     if (tid == 0) s_flag = 0;
     __syncthreads();
     const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
+    uint64_t kx = ~0ull;
     if (tid < n0) {
       tgsim_record r;
       load_rec(H + hidx[h0 + tid], r);
-      K[tid] = r.t;
+      kx = (uint64_t)r.t ^ 0x8000000000000000ull;
       if (!(r.meta & TGSIM_F_STAGE_D)) atomicOr(&s_flag, 1u);
-    } else if (tid < np2) {
-      K[tid] = INT64_MAX;
     }
     __syncthreads();
     if (s_flag) {
@@ -3136,17 +3272,11 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       __syncthreads();
       continue;
     }
-    for (uint32_t k = 2; k <= np2; k <<= 1)  // bitonic, one element per thread
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        if (tid < np2) {
-          const uint32_t p = tid ^ j;
-          if (p > tid) {
-            const int64_t x = K[tid], y = K[p];
-            if ((x > y) == ((tid & k) == 0)) { K[tid] = y; K[p] = x; }
-          }
-        }
-        __syncthreads();
-      }
+    kx = wide_bitonic(kx, np2, reinterpret_cast<uint64_t*>(K));
+    __syncthreads();
+    if (tid < np2) K[tid] = (int64_t)(kx ^ 0x8000000000000000ull);  // padding: INT64_MAX
+    __syncthreads();
+    WIDE_PH(2);
     const uint32_t pnd = a.heavy.pend[l];
     const int64_t far = pnd > n0 ? (int64_t)(pnd - n0) : 0;
     // this thread's message: its copies (clone first) and netem times, as k_shape_seq's parallel form
@@ -3205,6 +3335,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       }
       base = far + (int64_t)(n0 - upper_idx(K, 0, n0, ts));
     }
+    WIDE_PH(3);
     // the closed form holds when every copy outlives the window's last enqueue
     int64_t emin = INT64_MAX, tmax = INT64_MIN;
     if (valid & 2u) emin = e2[1] < emin ? e2[1] : emin;
@@ -3250,6 +3381,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       prev = cur;
       ++k;
     }
+    WIDE_PH(4);
     uint32_t n_lost = 0, n_copies = 0, n_over = 0;
     tgsim_record r1, r2;
     int q1 = -1, q2 = -1;
@@ -3273,6 +3405,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     const int qs[2] = {q1, q2};
     const tgsim_record rs[2] = {r1, r2};
     a.Q.push_batch<2, kWideWaves>(qs, rs, l + (tid >> 6), true);
+    WIDE_PH(5);
     uint32_t tl, tc, to;
     (void)wide_excl_scan(n_lost, red, tl);
     (void)wide_excl_scan(n_copies, red, tc);
@@ -3286,6 +3419,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       done[l] = 1;
     }
     __syncthreads();
+    WIDE_PH(6);
   }
 }
 
@@ -3740,10 +3874,7 @@ __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uin
   const uint32_t st = L.start + c0;
   const uint32_t cnt = min(chunk, L.len - c0);
   const uint32_t npad = next_pow2(cnt);
-  for (uint32_t j = threadIdx.x; j < npad; j += kBlock) {
-    if (j < cnt) p.key(keys[st + j], vals[st + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
-    else pad_key(s, j);
-  }
+  load_span_keys(p, s, keys, vals, st, cnt, npad);
   __syncthreads();
   if (packed_bitonic(s, cnt, npad)) {  // sorted through perm, the arrays in place
     for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
@@ -3950,7 +4081,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     if (w < nm) {
       const uint32_t g = medium[w];
       const uint32_t a = off[g], m = off[g + 1] - a;
-      for (uint32_t j = threadIdx.x; j < m; j += kBlock) p.key(g, vals[a + j], s.sg[j], s.k1[j], s.k2[j], s.k3[j]);
+      load_span_keys(p, s, keys, vals, a, m, m);  // keys[a, a + m) are g
       __syncthreads();
       span_sort(s, m, off, a);
       p.epilogue(s, m, a, off, w);
@@ -4040,22 +4171,50 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     const uint64_t tp_ready = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint32_t e = (r - s_c2[i]) * kRankTile + threadIdx.x;
+#ifndef TGSIM_RANK_PLAIN
+    // a sampled index of the segment's sorted chunks in LDS (every st-th key of each chunk; the
+    // chunks are complete, their tasks counted): a search first finds its st-key window among the
+    // samples, then needs log2(st) dependent global loads instead of log2(kParChunk)
+    uint32_t st = 16;
+    while (nch * (kParChunk / st) > (uint32_t)kSpan) st <<= 1;  // block-uniform
+    const uint32_t S = kParChunk / st;  // samples of a full chunk
+    for (uint32_t q = threadIdx.x; q < nch * S; q += kBlock) {
+      const uint32_t pos = (q / S) * kParChunk + (q % S) * st;
+      if (pos < L.len) { s.k1[q] = K1a[L.start + pos]; s.k2[q] = K2a[L.start + pos]; s.k3[q] = K3a[L.start + pos]; }
+    }
+    __syncthreads();
+#endif
     if (e < L.len) {
       const uint32_t x = L.start + e, c = e / kParChunk;
       const uint64_t k1 = K1a[x], k2 = K2a[x];
       const uint32_t k3 = K3a[x];
       uint32_t rank = e - c * kParChunk;
       for (uint32_t c0 = 0; c0 < nch; c0 += kRankPar) {
-        uint32_t b[kRankPar], n[kRankPar], lo[kRankPar];
+        uint32_t b[kRankPar], n[kRankPar], lo[kRankPar], base[kRankPar];
 #pragma unroll
         for (int q = 0; q < kRankPar; ++q) {
           const uint32_t cc = c0 + q;
           b[q] = L.start + cc * kParChunk;
           n[q] = (cc < nch && cc != c) ? min(kParChunk, L.len - cc * kParChunk) : 0u;
+          base[q] = 0;
+#ifndef TGSIM_RANK_PLAIN
+          if (n[q]) {  // samples of chunk cc below the key: the count lies in ((m - 1) st, m st]
+            const uint32_t ns = (n[q] + st - 1) / st, s0 = cc * S;
+            uint32_t a = 0, z = ns;
+            while (a < z) {
+              const uint32_t mid = (a + z) >> 1;
+              if (key_less(0, s.k1[s0 + mid], s.k2[s0 + mid], s.k3[s0 + mid], 0, k1, k2, k3)) a = mid + 1; else z = mid;
+            }
+            const uint32_t lo0 = a ? (a - 1) * st + 1 : 0u, hi0 = min(a * st, n[q]);
+            base[q] = lo0;
+            b[q] += lo0;
+            n[q] = hi0 - lo0;
+          }
+#endif
         }
         below_n(K1a, K2a, K3a, b, n, k1, k2, k3, lo);
 #pragma unroll
-        for (int q = 0; q < kRankPar; ++q) rank += lo[q];
+        for (int q = 0; q < kRankPar; ++q) rank += base[q] + lo[q];
       }
       large_place(p, L, rank, k1, k2, k3, K1b, K2b, K3b);
     }
@@ -4791,6 +4950,10 @@ hipError_t launch_gen_storm(Dev& d, uint32_t staged_base, uint32_t round, int64_
 // debug builds only: the phase clocks of the last k_tb_bucket / k_emit_bucket launches
 extern "C" int tgsim_debug_phases(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_tg_ph), sizeof(tgsim::g_tg_ph));
+}
+// ... and of the last k_shape_seq_wide launch (per block)
+extern "C" int tgsim_debug_wide_phases(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_wide_ph), sizeof(tgsim::g_wide_ph));
 }
 // ... and of the last task-parallel long-segment pass (per task)
 extern "C" int tgsim_debug_task_phases(uint64_t* out) {
