@@ -2620,6 +2620,7 @@ __global__ __launch_bounds__(kSeqChunk) void k_shape_seq(ShapeArgs a, const uint
                                                          uint32_t* last4, const int64_t* Xs, const uint8_t* done) {
   __shared__ SeqSmem m;
   DevScalars* sc = a.Q.sc;
+  if (sc->seq_left == 0) return;  // k_shape_seq_wide decided every sender (block-uniform)
   const int64_t t_end = sc->t_end;
   const uint32_t lane = threadIdx.x;
   for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
@@ -3122,34 +3123,49 @@ __device__ __forceinline__ int64_t wide_excl_min(int64_t v, int64_t* red) {
   return ex < pre ? ex : pre;
 }
 
-// Ascending bitonic sort of one 64-bit key per thread over threads [0, np2) of the block (np2 a
-// power of two <= kWide): a stage whose partners are less than 64 apart runs in registers (cross-lane
-// shuffles), only the others go through LDS (`lds`, np2 entries) - 10 of the 55 stages at 1024.
-__device__ __forceinline__ uint64_t wide_bitonic(uint64_t x, uint32_t np2, uint64_t* lds) {
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t k = 2; k <= np2; k <<= 1)
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      uint64_t y;
-      if (j >= 64) {  // block-uniform
-        __syncthreads();  // the previous LDS stage's reads are done
-        if (tid < np2) lds[tid] = x;
-        __syncthreads();
-        y = tid < np2 ? lds[tid ^ j] : x;
-      } else {
-        y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), (int)j) << 32) |
-            (uint32_t)__shfl_xor((int)(uint32_t)x, (int)j);
-      }
-      const bool keep_lo = ((tid & k) == 0) == ((tid & j) == 0);
-      const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
-      x = keep_lo ? lo : hi;
+// Ascending sort of one 64-bit key per thread of the kWide-thread block into LDS: each wave ranks
+// its 64 keys against each other (64 scalar broadcasts, no barrier), then four merge rounds of run
+// pairs (64 -> 1024), each element placing itself by a binary search of the other run (A side:
+// keys below; B side: keys at or below, so equal keys - the padding - keep their order). Returns
+// the buffer that holds the sorted keys (a or b). A register bitonic took ~11 us per sender: its 45
+// cross-lane stages are dependent ds_bpermute round trips.
+static_assert(kWide == 1024, "wide_sort: four merge rounds from 64-key runs");
+__device__ __forceinline__ uint64_t* wide_sort(uint64_t x, uint64_t* a, uint64_t* b) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
+  uint32_t r = 0;
+#pragma unroll 8
+  for (int j = 0; j < 64; ++j) {
+    const uint32_t yh = (uint32_t)__builtin_amdgcn_readlane((int)xh, j), yl = (uint32_t)__builtin_amdgcn_readlane((int)xl, j);
+    const uint64_t y = ((uint64_t)yh << 32) | yl;
+    r += (y < x || (y == x && (uint32_t)j < lane)) ? 1u : 0u;
+  }
+  uint32_t pos = wave * 64u + r;
+  a[pos] = x;
+  uint64_t *src = a, *dst = b;
+  for (uint32_t L = 64; L < (uint32_t)kWide; L <<= 1) {
+    __syncthreads();
+    const uint32_t base = pos & ~(2 * L - 1);
+    const bool in_a = (pos & L) == 0;
+    const uint64_t* other = src + base + (in_a ? L : 0u);
+    uint32_t lo = 0, hi = L;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t y = other[mid];
+      if (in_a ? y < x : y <= x) lo = mid + 1; else hi = mid;
     }
-  return x;
+    pos = base + (pos - base - (in_a ? 0u : L)) + lo;
+    dst[pos] = x;
+    uint64_t* t = src; src = dst; dst = t;
+  }
+  __syncthreads();
+  return src;
 }
 
 #ifdef TGSIM_PHASE_PROF
 // debug builds: per block (its last sender) of the last k_shape_seq_wide launch, s_memrealtime at:
 // start, sorted, K ready, copies drawn, decided, appended, end
-__device__ uint64_t g_wide_ph[4096][8];
+__device__ uint64_t g_wide_ph[4096][12];
 #define WIDE_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_wide_ph[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define WIDE_PH(k) do {} while (0)
@@ -3158,12 +3174,14 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
                                                           const uint32_t* moff, const uint32_t* hoff,
                                                           const uint32_t* hidx, const tgsim_record* H,
                                                           uint8_t* done) {
-  __shared__ int64_t K[kWide];
-  __shared__ uint64_t S1[kWide];
-  __shared__ uint32_t S2[kWide], S3[kWide];
+  __shared__ int64_t K[kWide];                 // the due records' departures, ascending
+  __shared__ uint64_t S1[kWide];               // sort keys
+  __shared__ uint32_t S2[kWide], S3[kWide];    // exact sort: seq, position; then S3 = sorted -> position
+  __shared__ int64_t Mt[kWide];                // the messages by position in the group-by's order
+  __shared__ uint32_t Ms[kWide], Md[kWide], Mz[kWide], Mi[kWide];
   __shared__ uint32_t red[kWideWaves];
   __shared__ int64_t red64[kWideWaves], rmin[kWideWaves], rmax[kWideWaves];
-  __shared__ uint32_t s_flag;
+  __shared__ uint32_t s_flag, s_stage_a, s_tot[3];
   DevScalars* sc = a.Q.sc;
   const int64_t t_end = sc->t_end;
   const uint32_t tid = threadIdx.x;
@@ -3171,111 +3189,126 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     const uint32_t j0 = moff[l], j1 = moff[l + 1], n = j1 - j0;
     if (n == 0) continue;
     if (n > (uint32_t)kWide) {  // k_rest ordered it; k_shape_seq walks it
-      if (tid == 0) done[l] = 0;
+      if (tid == 0) { done[l] = 0; atomicAdd(&sc->seq_left, 1u); }
       continue;
     }
     WIDE_PH(0);
-    // the sender's deferred messages in (t_send, seq, index) order (k_seg_small<CorrPolicy>'s order,
-    // which this kernel replaces for every sender of at most kWide = kTile of them). Packed: one
-    // 64-bit key (t_send - min << 42 | seq << 10 | position) sorted mostly in registers, when the
-    // send times span less than 2^22 ns and no two messages share (t_send, seq); else the exact sort
-    // over (t_send, seq, index) in LDS.
-    {
-      const uint32_t np2m = n > 1 ? next_pow2(n) : 1u;
-      uint32_t i = 0, sq = 0;
-      int64_t ts = 0;
-      if (tid < n) {
-        i = gvals[j0 + tid];
-        ts = a.t[i];
-        sq = a.seq[i];
-        S3[tid] = i;
-      }
-      int64_t mn = tid < n ? ts : INT64_MAX, mx = tid < n ? ts : INT64_MIN;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
-        mn = x < mn ? x : mn;
-        mx = y > mx ? y : mx;
-      }
-      if (lane_id() == 0) { rmin[tid >> 6] = mn; rmax[tid >> 6] = mx; }
-      if (tid == 0) s_flag = 0;
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < kWideWaves; ++w) {
-        mn = rmin[w] < mn ? rmin[w] : mn;
-        mx = rmax[w] > mx ? rmax[w] : mx;
-      }
-      const bool packed = (uint64_t)(mx - mn) < (1ull << 22);  // block-uniform
-      if (packed) {
-        uint64_t key = tid < n ? ((uint64_t)(ts - mn) << 42) | ((uint64_t)sq << 10) | tid : ~0ull;
-        key = wide_bitonic(key, np2m, S1);
-        __syncthreads();
-        if (tid < np2m) S1[tid] = key;
-        __syncthreads();
-        if (tid > 0 && tid < n && (S1[tid] >> 10) == (S1[tid - 1] >> 10)) s_flag = 1u;  // a (t_send, seq) tie
-        __syncthreads();
-        if (!s_flag && tid < n) S2[tid] = S3[key & 1023u];  // the message at sorted position tid
-        __syncthreads();
-        if (!s_flag && tid < n) S3[tid] = S2[tid];
-      }
-      if (!packed || s_flag) {  // block-uniform
-        if (tid < n) {
-          i = gvals[j0 + tid];
-          S1[tid] = (uint64_t)a.t[i] ^ 0x8000000000000000ull;
-          S2[tid] = a.seq[i];
-          S3[tid] = i;
-        } else if (tid < np2m) {
-          S1[tid] = ~0ull; S2[tid] = ~0u; S3[tid] = ~0u;
-        }
-        __syncthreads();
-        for (uint32_t k = 2; k <= np2m; k <<= 1)
-          for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            if (tid < np2m) {
-              const uint32_t p = tid ^ j;
-              if (p > tid) {
-                const uint64_t x1 = S1[tid], y1 = S1[p];
-                const uint32_t x2 = S2[tid], y2 = S2[p], x3 = S3[tid], y3 = S3[p];
-                const bool gt = x1 != y1 ? x1 > y1 : (x2 != y2 ? x2 > y2 : x3 > y3);
-                if (gt == ((tid & k) == 0)) {
-                  S1[tid] = y1; S1[p] = x1; S2[tid] = y2; S2[p] = x2; S3[tid] = y3; S3[p] = x3;
-                }
-              }
-            }
-            __syncthreads();
-          }
-      }
-      __syncthreads();
-      if (tid < n) sorted[j0 + tid] = S3[tid];
-    }
-    WIDE_PH(1);
     const ShapeDev sh = a.shape[l];
     const uint32_t h0 = hoff ? hoff[l] : 0u, h1 = hoff ? hoff[l + 1] : 0u, n0 = h1 - h0;
-    if (!a.heavy.of(l) || (sh.flags & (kShCorr | kShLimited)) || n0 > (uint32_t)kWide || !hoff) {
-      if (tid == 0) done[l] = 0;
-      continue;
-    }
-    // K: the due records' departures, ascending; a stage-A record (queued under an earlier, shaped
-    // Shape) needs the heaps of k_shape_seq
-    if (tid == 0) s_flag = 0;
-    __syncthreads();
-    const uint32_t np2 = n0 > 1 ? next_pow2(n0) : 1u;
+    // block-uniform: the closed form needs queue tracking without HTB or correlation
+    const bool elig = hoff && a.heavy.of(l) && !(sh.flags & (kShCorr | kShLimited)) && n0 <= (uint32_t)kWide;
+    if (tid == 0) { s_flag = 0; s_stage_a = 0; }
+    // every load up front, two dependent levels: (message index, due record index), then (the
+    // message's fields, the due record)
+    uint32_t i = 0, hx = 0;
+    if (tid < n) i = gvals[j0 + tid];
+    if (elig && tid < n0) hx = hidx[h0 + tid];
+    int64_t ts = 0;
+    uint32_t sq = 0;
     uint64_t kx = ~0ull;
-    if (tid < n0) {
-      tgsim_record r;
-      load_rec(H + hidx[h0 + tid], r);
-      kx = (uint64_t)r.t ^ 0x8000000000000000ull;
-      if (!(r.meta & TGSIM_F_STAGE_D)) atomicOr(&s_flag, 1u);
+    if (tid < n) {
+      ts = a.t[i];
+      sq = a.seq[i];
+      Mt[tid] = ts; Ms[tid] = sq; Md[tid] = a.dst[i]; Mz[tid] = a.size[i]; Mi[tid] = i;
     }
+    bool stage_a = false;
+    if (elig && tid < n0) {
+      tgsim_record r;
+      load_rec(H + hx, r);
+      kx = (uint64_t)r.t ^ 0x8000000000000000ull;
+      stage_a = !(r.meta & TGSIM_F_STAGE_D);  // queued under an earlier, shaped Shape: k_shape_seq's heaps
+    }
+#ifdef TGSIM_PHASE_PROF
+    if (tid < n) Mi[tid] += (uint32_t)(kx & 0);  // the loads complete before the clock below
+#endif
+    WIDE_PH(7);
+    // the sender's messages in (t_send, seq, index) order (k_seg_small<CorrPolicy>'s order, which
+    // this kernel replaces for every sender of at most kWide = kTile of them). Packed: one 64-bit
+    // key (t_send - min << 42 | seq << 10 | position) sorted mostly in registers, when the send times
+    // span less than 2^22 ns and no two messages share (t_send, seq); else the exact sort over
+    // (t_send, seq, index) in LDS.
+    const uint32_t np2m = n > 1 ? next_pow2(n) : 1u;
+    int64_t mn = tid < n ? ts : INT64_MAX, mx = tid < n ? ts : INT64_MIN;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
+      mn = x < mn ? x : mn;
+      mx = y > mx ? y : mx;
+    }
+    if (lane_id() == 0) { rmin[tid >> 6] = mn; rmax[tid >> 6] = mx; }
     __syncthreads();
-    if (s_flag) {
-      if (tid == 0) done[l] = 0;
+    if (stage_a) s_stage_a = 1u;
+#pragma unroll
+    for (int w = 0; w < kWideWaves; ++w) {
+      mn = rmin[w] < mn ? rmin[w] : mn;
+      mx = rmax[w] > mx ? rmax[w] : mx;
+    }
+    const bool packed = (uint64_t)(mx - mn) < (1ull << 22);  // block-uniform
+    WIDE_PH(8);
+    if (packed) {
+      const uint64_t key = tid < n ? ((uint64_t)(ts - mn) << 42) | ((uint64_t)sq << 10) | tid : ~0ull;
+      const uint64_t* srt = wide_sort(key, S1, reinterpret_cast<uint64_t*>(K));
+      WIDE_PH(9);
+      S3[tid] = (uint32_t)(srt[tid] & 1023u);
+      if (tid > 0 && tid < n && (srt[tid] >> 10) == (srt[tid - 1] >> 10)) s_flag = 1u;  // a (t_send, seq) tie
       __syncthreads();
+    }
+    if (!packed || s_flag) {  // block-uniform
+      if (tid < n) {
+        S1[tid] = (uint64_t)Mt[tid] ^ 0x8000000000000000ull;
+        S2[tid] = Ms[tid];
+        S3[tid] = tid;
+      } else if (tid < np2m) {
+        S1[tid] = ~0ull; S2[tid] = ~0u; S3[tid] = ~0u;
+      }
+      __syncthreads();
+      for (uint32_t k = 2; k <= np2m; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          if (tid < np2m) {
+            const uint32_t p = tid ^ j;
+            if (p > tid) {
+              const uint64_t x1 = S1[tid], y1 = S1[p];
+              const uint32_t x2 = S2[tid], y2 = S2[p], x3 = S3[tid], y3 = S3[p];
+              const uint32_t xi = x3 < n ? Mi[x3] : ~0u, yi = y3 < n ? Mi[y3] : ~0u;
+              const bool gt = x1 != y1 ? x1 > y1 : (x2 != y2 ? x2 > y2 : xi > yi);
+              if (gt == ((tid & k) == 0)) {
+                S1[tid] = y1; S1[p] = x1; S2[tid] = y2; S2[p] = x2; S3[tid] = y3; S3[p] = x3;
+              }
+            }
+          }
+          __syncthreads();
+        }
+    }
+    if (tid < n) sorted[j0 + tid] = Mi[S3[tid]];
+    WIDE_PH(1);
+    if (!elig || s_stage_a) {  // block-uniform: k_shape_seq walks it
+      if (tid == 0) { done[l] = 0; atomicAdd(&sc->seq_left, 1u); }
+      __syncthreads();  // every thread's reads of this sender's LDS are done
       continue;
     }
-    kx = wide_bitonic(kx, np2, reinterpret_cast<uint64_t*>(K));
+    // |K > t_k| for every message k without sorting K: the messages' send times in (t_send, seq)
+    // order (K's array), each due departure v counted at the first message it has not left by,
+    // lb(v) = first k with t_k >= v (a copy leaving at t has left: occupancy [enqueue, departure)),
+    // then #{K <= t_k} = the inclusive prefix of those counts (S2 as the histogram)
+    if (tid < n) K[tid] = Mt[S3[tid]];
+    S2[tid] = 0;
     __syncthreads();
-    if (tid < np2) K[tid] = (int64_t)(kx ^ 0x8000000000000000ull);  // padding: INT64_MAX
+    if (tid < n0) {
+      const int64_t v = (int64_t)(kx ^ 0x8000000000000000ull);
+      uint32_t lo = 0, hi = n;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (K[mid] < v) lo = mid + 1; else hi = mid;
+      }
+      if (lo < n) atomicAdd(&S2[lo], 1u);
+    }
     __syncthreads();
+    uint32_t gone;  // #{K <= t_k} for this thread's message
+    {
+      uint32_t tk;
+      const uint32_t h = S2[tid];
+      gone = wide_excl_scan(h, red, tk) + h;
+    }
     WIDE_PH(2);
     const uint32_t pnd = a.heavy.pend[l];
     const int64_t far = pnd > n0 ? (int64_t)(pnd - n0) : 0;
@@ -3284,11 +3317,12 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     uint8_t st = 0, valid = 0;
     int64_t e2[2] = {INT64_MIN, INT64_MIN};
     uint32_t meta2[2] = {0, 0}, coff2[2] = {0, 0};
-    int64_t ts = INT64_MIN, base = 0;
+    int64_t base = 0;
+    ts = INT64_MIN;
     uint32_t idx = 0, dst = 0, seq = 0, size = 0;
     if (tid < n) {
-      idx = S3[tid];
-      seq = a.seq[idx]; dst = a.dst[idx]; size = a.size[idx]; ts = a.t[idx];
+      const uint32_t p = S3[tid];  // this thread's message: the tid-th in (t_send, seq) order
+      idx = Mi[p]; seq = Ms[p]; dst = Md[p]; size = Mz[p]; ts = Mt[p];
       uint32_t w0[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, w1[2][3] = {{0, 0, 0}, {0, 0, 0}};
       const bool need_w0 = sh.dup_t || sh.loss_t || sh.reorder_t || sh.sigma;
 #pragma unroll
@@ -3333,7 +3367,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
           valid |= (uint8_t)(1u << c);
         }
       }
-      base = far + (int64_t)(n0 - upper_idx(K, 0, n0, ts));
+      base = far + (int64_t)(n0 - gone);
     }
     WIDE_PH(3);
     // the closed form holds when every copy outlives the window's last enqueue
@@ -3355,7 +3389,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       tmax = rmax[w] > tmax ? rmax[w] : tmax;
     }
     if (!(emin > tmax)) {  // block-uniform: k_shape_seq walks it
-      if (tid == 0) done[l] = 0;
+      if (tid == 0) { done[l] = 0; atomicAdd(&sc->seq_left, 1u); }
       __syncthreads();
       continue;
     }
@@ -3406,11 +3440,20 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     const tgsim_record rs[2] = {r1, r2};
     a.Q.push_batch<2, kWideWaves>(qs, rs, l + (tid >> 6), true);
     WIDE_PH(5);
-    uint32_t tl, tc, to;
-    (void)wide_excl_scan(n_lost, red, tl);
-    (void)wide_excl_scan(n_copies, red, tc);
-    (void)wide_excl_scan(n_over, red, to);
+    // the sender's counters: per wave sums, one LDS atomic each, one barrier
+    if (tid < 3) s_tot[tid] = 0;
+    __syncthreads();
+    {
+      const uint32_t wl = wave_sum(n_lost), wc = wave_sum(n_copies), wo = wave_sum(n_over);
+      if (lane_id() == 0) {
+        if (wl) atomicAdd(&s_tot[0], wl);
+        if (wc) atomicAdd(&s_tot[1], wc);
+        if (wo) atomicAdd(&s_tot[2], wo);
+      }
+    }
+    __syncthreads();
     if (tid == 0) {
+      const uint32_t tl = s_tot[0], tc = s_tot[1], to = s_tot[2];
       unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
       if (tl) atomicAdd(&row[ST_LOST], (unsigned long long)tl);
       if (tc) atomicAdd(&row[ST_COPIES], (unsigned long long)tc);
@@ -4018,7 +4061,10 @@ template <> struct LargeScan<TBPolicy> { static constexpr bool v = true; };
 
 // elements of the sorted chunk (K1, K2, K3)[b, b + n) below the key (k1, k2, k3): kRankPar chunks'
 // binary searches advance together, so their loads are in flight at once
-constexpr int kRankPar = 8;  // chunks whose binary searches a rank thread runs together
+#ifndef TGSIM_RANK_PAR
+#define TGSIM_RANK_PAR 8
+#endif
+constexpr int kRankPar = TGSIM_RANK_PAR;  // chunks whose binary searches a rank thread runs together
 __device__ __forceinline__ void below_n(const uint64_t* K1, const uint64_t* K2, const uint32_t* K3, const uint32_t (&b)[kRankPar],
                                        const uint32_t (&n)[kRankPar], uint64_t k1, uint64_t k2, uint32_t k3, uint32_t (&lo)[kRankPar]) {
   uint32_t hi[kRankPar];
@@ -4040,7 +4086,10 @@ __device__ __forceinline__ void below_n(const uint64_t* K1, const uint64_t* K2, 
 }
 
 constexpr uint32_t kRankTile = kBlock;   // elements of a large segment ranked per task (one per thread)
-constexpr uint32_t kParChunk = 1024;    // chunk of the task-parallel path: half the LDS sort, twice the searches
+#ifndef TGSIM_PAR_CHUNK
+#define TGSIM_PAR_CHUNK 1024
+#endif
+constexpr uint32_t kParChunk = TGSIM_PAR_CHUNK;  // chunk of the task-parallel path
 constexpr uint32_t kLargeTab = 256;      // large segments whose task table fits LDS (else one block each)
 
 // The rest of a group-by's segments. Medium segments: one block each. Large segments (len > kTile)
@@ -4689,6 +4738,8 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     hidx = hv;
   }
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
+  // k_shape_seq skips its launch's work when the closed form left it no sender (seq_left 0)
+  TG_CHECK(hipMemsetAsync(&d.sc->seq_left, a.heavy.pend ? 0 : 1, sizeof(uint32_t), d.stream));
   if (a.heavy.pend) {  // the whole-sender closed form first (heavy senders without HTB / correlation)
     ProfScope ps_(d, KID_SHAPE_WIDE);
     hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
@@ -4952,7 +5003,7 @@ extern "C" int tgsim_debug_phases(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_tg_ph), sizeof(tgsim::g_tg_ph));
 }
 // ... and of the last k_shape_seq_wide launch (per block)
-extern "C" int tgsim_debug_wide_phases(uint64_t* out) {
+extern "C" int tgsim_debug_wide_phases(uint64_t* out) {  // [4096][12]
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_wide_ph), sizeof(tgsim::g_wide_ph));
 }
 // ... and of the last task-parallel long-segment pass (per task)
