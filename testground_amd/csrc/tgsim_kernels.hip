@@ -1877,7 +1877,10 @@ struct EmitPolicy {
 #endif
 constexpr int kBktCap = TG_BKT_CAP;   // items of one bucket held by the workgroup
 constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
-constexpr uint32_t kBktRankMax = 64;  // longest key run ranked in LDS
+#ifndef TGSIM_BKT_RANK_MAX
+#define TGSIM_BKT_RANK_MAX 64
+#endif
+constexpr uint32_t kBktRankMax = TGSIM_BKT_RANK_MAX;  // longest key run ranked in LDS
 constexpr int kIPT = kBktCap / kBlock;  // items per thread
 
 constexpr uint32_t kStageN = TG_STAGE_N;  // records staged per round for the coalesced output (k1 + k2 + k3 area:
@@ -3394,14 +3397,49 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
       continue;
     }
     // copy k (enqueue order: message, clone first) admitted iff A_{k+1} = A_k + 1
+    // k0 = copies before this thread's (exclusive sum of nv) and prev = min over earlier copies of
+    // (L - index - 1), in one barrier: with e the wave-local exclusive sum and K0 the waves before,
+    // an earlier thread's term is (Lp - nv - e) - K0, so each wave publishes its sum and its minimum
+    // of (Lp - nv - e), and every thread folds the earlier waves' entries
     const uint32_t nv = (uint32_t)__popc((uint32_t)valid);
-    uint32_t tot;
-    const uint32_t k0 = wide_excl_scan(nv, red, tot);
     const int64_t lim = (int64_t)TGSIM_NETEM_LIMIT - base;
     const int64_t Lp = lim > 0 ? lim : 0;
-    const int64_t x0 = Lp - (int64_t)k0 - 1, x1 = Lp - (int64_t)k0 - 2;
-    const int64_t lmin = nv == 0 ? INT64_MAX : (nv == 1 ? x0 : (x0 < x1 ? x0 : x1));
-    int64_t prev = wide_excl_min(lmin, red64);
+    uint32_t k0;
+    int64_t prev;
+    {
+      const uint32_t lane = lane_id(), wave = tid >> 6;
+      uint32_t inc = nv;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if ((int)lane >= o) inc += y;
+      }
+      const uint32_t e = inc - nv;
+      const int64_t g = nv ? Lp - (int64_t)nv - (int64_t)e : INT64_MAX;
+      int64_t pm = g;  // inclusive prefix minimum of g in the wave
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(pm, o);
+        if ((int)lane >= o) pm = y < pm ? y : pm;
+      }
+      if (lane == 63) { red[wave] = inc; red64[wave] = pm; }
+      int64_t ex = __shfl_up(pm, 1);
+      if (lane == 0) ex = INT64_MAX;
+      __syncthreads();
+      uint32_t K0 = 0;
+      int64_t P = INT64_MAX;
+#pragma unroll
+      for (int w = 0; w < kWideWaves; ++w) {
+        if (w < (int)wave) {
+          const int64_t G = red64[w];
+          if (G != INT64_MAX && G - (int64_t)K0 < P) P = G - (int64_t)K0;
+          K0 += red[w];
+        }
+      }
+      k0 = K0 + e;
+      const int64_t own = ex == INT64_MAX ? INT64_MAX : ex - (int64_t)K0;
+      prev = own < P ? own : P;
+    }
     uint8_t adm = 0;
     uint32_t k = k0;
 #pragma unroll
@@ -3910,6 +3948,9 @@ __device__ void large_consume(const CorrPolicy& p, SortSmem&, const LargeSeg& L,
 }
 
 // Sort chunk [c0, c0 + kChunk) of a large segment in LDS into (K1a, K2a, K3a) at the same positions.
+#ifdef TGSIM_PHASE_PROF
+__device__ uint64_t g_chunk_ph[2];  // debug: the last chunk sort's keys-loaded and sorted clocks
+#endif
 template <class P>
 __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uint32_t c0, const uint32_t* keys,
                                  const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a,
@@ -3919,6 +3960,9 @@ __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uin
   const uint32_t npad = next_pow2(cnt);
   load_span_keys(p, s, keys, vals, st, cnt, npad);
   __syncthreads();
+#ifdef TGSIM_PHASE_PROF
+  if (threadIdx.x == 0) g_chunk_ph[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (packed_bitonic(s, cnt, npad)) {  // sorted through perm, the arrays in place
     for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) {
       const uint32_t e = s.perm[j];
@@ -3928,6 +3972,9 @@ __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uin
     bitonic_lds(s, npad);
     for (uint32_t j = threadIdx.x; j < cnt; j += kBlock) { K1a[st + j] = s.k1[j]; K2a[st + j] = s.k2[j]; K3a[st + j] = s.k3[j]; }
   }
+#ifdef TGSIM_PHASE_PROF
+  if (threadIdx.x == 0) g_chunk_ph[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   __syncthreads();
 }
 
@@ -5006,9 +5053,11 @@ extern "C" int tgsim_debug_phases(uint64_t* out) {
 extern "C" int tgsim_debug_wide_phases(uint64_t* out) {  // [4096][12]
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_wide_ph), sizeof(tgsim::g_wide_ph));
 }
-// ... and of the last task-parallel long-segment pass (per task)
+// ... and of the last task-parallel long-segment pass (per task; then the last chunk sort's two clocks)
 extern "C" int tgsim_debug_task_phases(uint64_t* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_task_ph), sizeof(tgsim::g_task_ph));
+  const int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_task_ph), sizeof(tgsim::g_task_ph));
+  if (rc) return rc;
+  return (int)hipMemcpyFromSymbol(out + 4 * 4096, HIP_SYMBOL(tgsim::g_chunk_ph), sizeof(tgsim::g_chunk_ph));
 }
 // ... and of the last k_shape_seq launch (per block: its last sender)
 extern "C" int tgsim_debug_seq_phases(uint64_t* out) {

@@ -21,8 +21,10 @@ bench.sb_setup(sim, n, "accept")
 for w in range(windows):
     sim.advance((w + 1) * bench.SB_WINDOW_NS)
     sim.probe_react()
-buf = np.zeros((4096, 4), np.uint64)
-assert hip.cdll.tgsim_debug_task_phases(buf.ctypes.data_as(ctypes.c_void_p)) == 0
+raw = np.zeros(4 * 4096 + 2, np.uint64)
+assert hip.cdll.tgsim_debug_task_phases(raw.ctypes.data_as(ctypes.c_void_p)) == 0
+buf = raw[: 4 * 4096].reshape(4096, 4)
+ck = raw[4 * 4096:].astype(np.int64)
 live = buf[:, 1] != 0
 a = buf[live]
 t0 = a[:, 1].min()
@@ -35,4 +37,8 @@ for name, m in (("chunk", ~rank), ("rank", rank)):
     c, r, d = us(a[m, 1]), us(a[m, 2]), us(a[m, 3])
     print(f"{name:5s} tasks {m.sum():4d}  claim {c.min():6.1f}..{c.max():6.1f}  ready {r.min():6.1f}..{r.max():6.1f}"
           f"  done {d.min():6.1f}..{d.max():6.1f}  work median {np.median(d - r):5.1f} us  xcds {np.unique(blk[m] % 8).size}")
+# the last chunk task: claimed -> keys loaded -> sorted (ck) -> ready
+last = np.argmax(np.where(rank, 0, a[:, 1]))
+print(f"last chunk task: keys loaded {(int(ck[0]) - int(a[last, 1])) / 100:.1f} us after its claim, "
+      f"sorted {(int(ck[1]) - int(ck[0])) / 100:.1f} us later (clocks of the last chunk sort of any launch)")
 sim.close()
