@@ -1878,7 +1878,7 @@ struct EmitPolicy {
 constexpr int kBktCap = TG_BKT_CAP;   // items of one bucket held by the workgroup
 constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
 #ifndef TGSIM_BKT_RANK_MAX
-#define TGSIM_BKT_RANK_MAX 64
+#define TGSIM_BKT_RANK_MAX 512
 #endif
 constexpr uint32_t kBktRankMax = TGSIM_BKT_RANK_MAX;  // longest key run ranked in LDS
 constexpr int kIPT = kBktCap / kBlock;  // items per thread
@@ -4660,7 +4660,13 @@ static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
   // a context whose windows carry bkt_load times the packets per key (TCP acks: an ACK per data
   // packet) splits its keys over as many more buckets, so a bucket still fits kBktCap items
   const uint32_t slots = (uint32_t)TG_BKT_WGS_PER_CU * (uint32_t)d.n_cu * d.bkt_load;
-  uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, std::min<uint32_t>(TG_BKT_MIN_KEYS, K));
+  // No floor when one key per bucket fits the wave of workgroups (K <= slots): a 1000-instance
+  // context (config 2) at 24 keys per bucket made 42 buckets of up to ~11k deliveries (its receivers
+  // get up to ~480 each in a window), every one over kBktCap, so all its deliveries took the global
+  // form and k_rest's medium segments (a floor of K / (4 n_cu) measured the same on config 2 and
+  // slower on config 3's 10k instances)
+  const uint32_t floor_keys = K <= slots ? 1u : std::min<uint32_t>(TG_BKT_MIN_KEYS, K);
+  uint32_t w = std::max<uint32_t>((K + slots - 1) / slots, floor_keys);
   w = std::min<uint32_t>(w, 1u << kBktFusedKeyBits);
   // never more than kMaxBins buckets (the partition's LDS histograms and d.poff rows are that wide)
   w = std::max<uint32_t>(w, (K + kMaxBins - 1) / kMaxBins);
