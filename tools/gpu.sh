@@ -4,9 +4,11 @@
 #   tools/gpu.sh tests <out> [pytest args...]         pytest -m gpu (default: the whole GPU suite)
 #   tools/gpu.sh bench <out> <workload> [bench args]   one bench line
 #   tools/gpu.sh evidence <out> <workload> <round> [bench args]
-#        rocprofv3 kernel trace + stats of the bench (profiles/<round>/<w>_kernel_stats.csv,
-#        <w>_trace_summary.txt), FETCH_SIZE / WRITE_SIZE passes (one counter per run, the guide's HBM
-#        section) -> hash-stamped profiles/<round>/pmc_traffic[_<w>].json, then the bench line
+#        rocprofv3 kernel trace + stats of the bench (<w>_kernel_stats.csv, <w>_trace_summary.txt),
+#        FETCH_SIZE / WRITE_SIZE passes (one counter per run, the guide's HBM section) -> hash-stamped
+#        pmc_traffic[_<w>].json, then the bench line (bench_<w>.json) - all into
+#        gpurun_out/<out>/profiles/<round>/ (only gpurun_out/ comes back from the box: copy that
+#        directory into profiles/<round>/ here)
 #   tools/gpu.sh pmc <out> <workload> [bench args]     SQ / LDS / TCC / HBM counter groups, one run each
 #   tools/gpu.sh ab <out> <rounds> <workload> <name>... interleaved timing of libtgsim_<name>.so builds
 #        (tools/build_variant.sh) against the product library
@@ -28,22 +30,23 @@ bench)
   tail -1 $OUT/bench_$W.log | cut -c1-600;;
 evidence)
   W=$1; R=$2; shift 2
-  mkdir -p profiles/$R
+  P=$OUT/profiles/$R
+  mkdir -p $P
   B="bench.py --workload $W --no-cpu-baseline $(warm $W) $*"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$W -o run --output-format csv \
     -- python3 -u $B --steps 20 > $OUT/bench_${W}_under_rocprof.log 2>&1 || { echo PROF_FAIL; tail -20 $OUT/bench_${W}_under_rocprof.log; exit 1; }
-  cp $OUT/prof_$W/run_kernel_stats.csv profiles/$R/${W}_kernel_stats.csv
-  python3 tools/trace_summary.py $OUT/prof_$W/run_kernel_trace.csv --last 20 --marker k_window_start > profiles/$R/${W}_trace_summary.txt 2>&1
-  head -16 profiles/$R/${W}_trace_summary.txt
+  cp $OUT/prof_$W/run_kernel_stats.csv $P/${W}_kernel_stats.csv
+  python3 tools/trace_summary.py $OUT/prof_$W/run_kernel_trace.csv --last 20 --marker k_window_start > $P/${W}_trace_summary.txt 2>&1
+  head -16 $P/${W}_trace_summary.txt
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KR" -d $OUT/pmc_${W}_$c -o run --output-format csv \
       -- python3 -u $B --steps 5 > $OUT/pmc_${W}_$c.log 2>&1 || { echo PMC_FAIL $c; tail -5 $OUT/pmc_${W}_$c.log; exit 1; }
   done
   python3 tools/pmc_traffic.py $OUT/pmc_${W}_FETCH_SIZE/run_counter_collection.csv $OUT/pmc_${W}_WRITE_SIZE/run_counter_collection.csv \
-    profiles/$R/pmc_traffic$(suffix $W).json $W 1 || exit 1
+    $P/pmc_traffic$(suffix $W).json $W 1 || exit 1
   timeout -k 10 400 python3 -u bench.py --workload $W $(warm $W) "$@" > $OUT/bench_$W.log 2>&1 || { echo BENCH_FAIL; tail -30 $OUT/bench_$W.log; exit 1; }
-  tail -1 $OUT/bench_$W.log > profiles/$R/bench_$W.json
-  cut -c1-600 profiles/$R/bench_$W.json;;
+  tail -1 $OUT/bench_$W.log > $P/bench_$W.json
+  cut -c1-600 $P/bench_$W.json;;
 pmc)
   W=$1; shift
   B="bench.py --workload $W --no-cpu-baseline --steps 5 $(warm $W) $*"
