@@ -1458,11 +1458,13 @@ __device__ __forceinline__ void pad_key(SortSmem& s, uint32_t j) {
 // position -> element), the arrays staying in place; npad = next_pow2(m). Returns false, touching
 // nothing, when k1 spreads too far over the elements to pack.
 __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
-    // k1's spread over the span: below 2^52 the sort runs on (segment rank << 53 | k1 - min,
-    // element) pairs - one u64 compare per step, two arrays swapped instead of four; equal packed
-    // keys (same segment and k1) are ordered by (k2, k3) through the elements. The packed keys
-    // live in k1's array (it has no spare LDS: every kernel that reaches rest_body allocates this
-    // struct) and k1 is restored by element afterwards.
+    // k1's spread over the span: below 2^52 the sort runs on (segment rank | k1 - min | the top
+    // bits of k2, element) pairs - one u64 compare per step, two arrays swapped instead of four - the
+    // rank and k1 fields as wide as the span needs, k2's leading bits in the rest (a probed target's
+    // ~10k requests share their arrival times, and every tie went through the elements' k2 / k3: a
+    // 1024-element chunk took ~40 us). Equal packed keys (same segment, k1 and k2 top) are ordered by
+    // (k2, k3) through the elements. The packed keys live in k1's array (it has no spare LDS: every
+    // kernel that reaches rest_body allocates this struct) and k1 is restored by element afterwards.
     uint64_t mn = ~0ull, mx = 0;
     for (uint32_t j = threadIdx.x; j < m; j += kBlock) {
       mn = s.k1[j] < mn ? s.k1[j] : mn;
@@ -1496,13 +1498,20 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
       }
       uint32_t tot;
       uint32_t r = block_excl_scan(c, s.perm, tot);  // perm is scratch until it is filled below
+      // field widths (block-uniform): rank rb <= 11 bits (tot <= kSpan - 1), k1 b1 <= 52, k2 the rest
+      const uint32_t rb = tot ? 32u - (uint32_t)__builtin_clz(tot) : 0u;
+      const uint64_t spread = mx - mn;
+      const uint32_t b1 = spread ? 64u - (uint32_t)__builtin_clzll(spread) : 0u;
+      const uint32_t lo = 64u - rb - b1;  // >= 1
       uint64_t nk[PER];
       for (uint32_t u = 0; u < PER; ++u) {
         const uint32_t j = p0 + u;
-        nk[u] = ~0ull;  // padding: above every real key (rank <= 2^11 - 1, spread < 2^52)
+        nk[u] = ~0ull;  // padding: sorts after every real key (ties with one go by element, below)
         if (j < m) {
           r += (j > 0 && s.sg[j] != s.sg[j - 1]) ? 1u : 0u;
-          nk[u] = ((uint64_t)r << 53) | (s.k1[j] - mn);
+          const uint64_t hi = rb ? ((uint64_t)r << (64u - rb)) : 0ull;
+          const uint64_t mid = lo < 64u ? ((s.k1[j] - mn) << lo) : 0ull;
+          nk[u] = hi | mid | (s.k2[j] >> (64u - lo));
         }
       }
       __syncthreads();  // every k1 read before the packed keys replace them
@@ -1533,10 +1542,11 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
       }
       // restore k1 by element: sorted position i holds element perm[i]'s key
       uint32_t ee[PER];
+      const uint64_t m1 = b1 ? (~0ull >> (64u - b1)) : 0ull;
       for (uint32_t u = 0; u < PER; ++u) {
         const uint32_t i = p0 + u;
         ee[u] = 0xFFFFFFFFu;
-        if (i < m) { ee[u] = s.perm[i]; nk[u] = (kw[i] & ((1ull << 53) - 1)) + mn; }
+        if (i < m) { ee[u] = s.perm[i]; nk[u] = (lo < 64u ? ((kw[i] >> lo) & m1) : 0ull) + mn; }
       }
       __syncthreads();
       for (uint32_t u = 0; u < PER; ++u)
