@@ -212,6 +212,78 @@ def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender
     return out
 
 
+def run_wide(binding, seed: int, n_inst: int = 16, windows: int = 5, window_ns: int = 8 * MS, counters=None):
+    """The queue-limit lane's whole-sender closed form (k_shape_seq_wide) and each of
+    its ways back to the chunked lane: senders of <= 1024 deferred messages whose copies all outlive
+    the window's last enqueue (40-60 ms of netem against a 1 ms send spread) fill their 1000-packet
+    queues over a few windows; one sender repeats (t_send, seq) pairs (the exact sort), one spreads
+    its sends over more than 2^22 ns (the unpacked sort), one sends more than 1024 messages, one has
+    a token bucket, one a delay shorter than its send spread (the closed form does not hold), and
+    late sends at the horizon come in between."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=3000 + seed, max_msgs_per_window=1 << 16,
+                              max_records=1 << 18), binding=binding)
+    big = make_shape(latency_ns=50 * MS, jitter_ns=10 * MS, duplicate=10.0, loss=2.0, corrupt=1.0)
+    shapes = [big, big, big, big,                                  # closed form (packed sort)
+              make_shape(latency_ns=50 * MS, jitter_ns=10 * MS),   # repeated (t_send, seq): exact sort
+              make_shape(latency_ns=80 * MS),                      # sends spread over 6 ms: unpacked sort
+              make_shape(latency_ns=50 * MS, jitter_ns=5 * MS),    # > 1024 messages: chunked lane
+              make_shape(latency_ns=50 * MS, bandwidth_bps=1_000_000_000),   # token bucket: chunked lane
+              make_shape(latency_ns=200 * 1000, jitter_ns=100 * 1000)]       # short delay: no closed form
+    for g, shp in enumerate(shapes):
+        sim.set_shape(g, shp)
+    seqc = np.zeros(n_inst, np.int64)
+
+    def seqs_for(src):
+        q = np.zeros(len(src), np.int64)
+        for i, g in enumerate(src):
+            q[i] = seqc[g]
+            seqc[g] += 1
+        return q
+
+    out, t0 = [], 0
+    for w in range(windows + 40):
+        src, ts, seqs = [], [], []
+        if w < windows:
+            for g in range(len(shapes)):
+                k = 1100 if g == 6 else int(rng.integers(600, 1000))
+                spread = 6 * MS if g == 5 else MS
+                t = t0 + rng.integers(0, spread, k)
+                q = seqc[g] + np.arange(k)
+                seqc[g] += k
+                if g == 4:  # every tenth message repeats its predecessor's (t_send, seq)
+                    m = len(t[1::10])
+                    t[1::10] = t[0:-1:10][:m]
+                    q[1::10] = q[0:-1:10][:m]
+                src.append(np.full(k, g)); ts.append(t); seqs.append(q)
+            light = rng.integers(len(shapes), n_inst, 40)
+            src.append(light); ts.append(t0 + rng.integers(0, window_ns, 40)); seqs.append(seqs_for(light))
+            if w > 0:   # reactions at the horizon
+                late = rng.integers(0, len(shapes), 60)
+                src.append(late); ts.append(t0 - rng.integers(1, window_ns, 60)); seqs.append(seqs_for(late))
+        src = np.concatenate(src) if src else np.zeros(0, np.int64)
+        ts = np.concatenate(ts) if ts else np.zeros(0, np.int64)
+        seq = np.concatenate(seqs) if seqs else np.zeros(0, np.int64)
+        n = len(src)
+        dst = (src + rng.integers(1, n_inst, n)) % n_inst
+        # a repeated (t_send, seq) pair draws the same netem fate; another receiver keeps the two
+        # deliveries apart (at one receiver their inbox order would be a tie of every key)
+        for i in range(1, n):
+            if src[i] == 4 and src[i - 1] == 4 and ts[i] == ts[i - 1] and seq[i] == seq[i - 1] and dst[i] == dst[i - 1]:
+                dst[i] = (dst[i] + 1) % n_inst if (dst[i] + 1) % n_inst != 4 else (dst[i] + 2) % n_inst
+        size = rng.choice([64, 1000, 1500], n)
+        if n:
+            sim.enqueue(src, dst, seq, size, ts)
+        t0 += window_ns if w < windows else 5 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    if counters is not None:  # HIP only: which lane decided the deferred messages
+        counters.update(sim.kernel_counters())
+    sim.close()
+    return out
+
+
 def run_sync(binding, seed: int, restart=None):
     rng = np.random.default_rng(seed)
     sim = Simulator(SimConfig(n_instances=8, seed=seed, max_states=64), binding=binding)

@@ -42,6 +42,17 @@ def test_queue_limit_bursts(hip, oracle, seed):
     assert a[-1]["stats"]["overlimit"] > 1000
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_queue_limit_whole_sender(hip, oracle, seed):
+    """k_shape_seq_wide and its fallbacks (repeated (t_send, seq), wide send spread, > 1024 messages,
+    token bucket, no closed form) against the oracle's walk."""
+    kc = {}
+    a, b = S.run_wide(hip, seed, counters=kc), S.run_wide(oracle, seed)
+    S.assert_same(a, b)
+    assert a[-1]["stats"]["overlimit"] > 1000
+    assert 0 < kc["wide"] < kc["deferred"]  # both lanes took senders
+
+
 def test_sync_service(hip, oracle):
     S.assert_same(S.run_sync(hip, 3), S.run_sync(oracle, 3))
 
