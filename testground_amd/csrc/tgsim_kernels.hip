@@ -1457,7 +1457,16 @@ __device__ __forceinline__ void pad_key(SortSmem& s, uint32_t j) {
 // Sort the m loaded elements of s (whole segments, contiguous in sg order) into perm[] (sorted
 // position -> element), the arrays staying in place; npad = next_pow2(m). Returns false, touching
 // nothing, when k1 spreads too far over the elements to pack.
+#ifdef TGSIM_PHASE_PROF
+// debug: the last chunk sort's keys-loaded and sorted clocks, then the last 1024-key packed sort's
+// clocks after min/max, packing, the network and the restore, and whether it packed
+__device__ uint64_t g_chunk_ph[8];
+#define PB_PH(i) do { if (threadIdx.x == 0 && m == 1024) g_chunk_ph[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PB_PH(i) do {} while (0)
+#endif
 __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
+    PB_PH(2);
     // k1's spread over the span: below 2^52 the sort runs on (segment rank | k1 - min | the top
     // bits of k2, element) pairs - one u64 compare per step, two arrays swapped instead of four - the
     // rank and k1 fields as wide as the span needs, k2's leading bits in the rest (a probed target's
@@ -1485,6 +1494,7 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
       mx = b > mx ? b : mx;
     }
     __syncthreads();  // scA / scB are free again
+    PB_PH(3);
     if (!(mx - mn < (1ull << 52))) return false;
     {
       uint64_t* kw = s.k1;
@@ -1520,6 +1530,7 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
         if (j < npad) { kw[j] = nk[u]; s.perm[j] = j < m ? j : 0xFFFFFFFFu; }
       }
       __syncthreads();
+      PB_PH(4);
       for (uint32_t k = 2; k <= npad; k <<= 1) {
         for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
           for (uint32_t q = threadIdx.x; q < (npad >> 1); q += kBlock) {
@@ -1540,6 +1551,7 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
           __syncthreads();
         }
       }
+      PB_PH(5);
       // restore k1 by element: sorted position i holds element perm[i]'s key
       uint32_t ee[PER];
       const uint64_t m1 = b1 ? (~0ull >> (64u - b1)) : 0ull;
@@ -1553,6 +1565,7 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
         if (ee[u] != 0xFFFFFFFFu) s.k1[ee[u]] = nk[u];
     }
     __syncthreads();
+    PB_PH(6);
     return true;
 }
 
@@ -3958,9 +3971,6 @@ __device__ void large_consume(const CorrPolicy& p, SortSmem&, const LargeSeg& L,
 }
 
 // Sort chunk [c0, c0 + kChunk) of a large segment in LDS into (K1a, K2a, K3a) at the same positions.
-#ifdef TGSIM_PHASE_PROF
-__device__ uint64_t g_chunk_ph[2];  // debug: the last chunk sort's keys-loaded and sorted clocks
-#endif
 template <class P>
 __device__ void large_chunk_sort(const P& p, SortSmem& s, const LargeSeg& L, uint32_t c0, const uint32_t* keys,
                                  const uint32_t* vals, uint64_t* K1a, uint64_t* K2a, uint32_t* K3a,
@@ -4134,8 +4144,16 @@ __device__ __forceinline__ void below_n(const uint64_t* K1, const uint64_t* K2, 
       if (lo[q] >= hi[q]) continue;
       any = true;
       const uint32_t mid = (lo[q] + hi[q]) >> 1, x = b[q] + mid;
+#ifdef TGSIM_RANK_LAZY
       const uint64_t y1 = K1[x];
       const bool lt = y1 != k1 ? y1 < k1 : key_less(0, y1, K2[x], K3[x], 0, k1, k2, k3);
+#else
+      // all three words in one round trip: a probed target's requests share their arrival time, and
+      // loading (k2, k3) only after k1 tied made every search step two dependent loads
+      const uint64_t y1 = K1[x], y2 = K2[x];
+      const uint32_t y3 = K3[x];
+      const bool lt = key_less(0, y1, y2, y3, 0, k1, k2, k3);
+#endif
       if (lt) lo[q] = mid + 1; else hi[q] = mid;
     }
     if (!any) break;
@@ -4148,6 +4166,12 @@ constexpr uint32_t kRankTile = kBlock;   // elements of a large segment ranked p
 #endif
 constexpr uint32_t kParChunk = TGSIM_PAR_CHUNK;  // chunk of the task-parallel path
 constexpr uint32_t kLargeTab = 256;      // large segments whose task table fits LDS (else one block each)
+#ifndef TGSIM_RANK_ST0
+#define TGSIM_RANK_ST0 4
+#endif
+#ifndef TGSIM_SPIN_SLEEP
+#define TGSIM_SPIN_SLEEP 2               // a waiting rank task's poll period, in units of 64 clocks
+#endif
 
 // The rest of a group-by's segments. Medium segments: one block each. Large segments (len > kTile)
 // are sorted by many blocks at once through a task counter: first every kChunk chunk
@@ -4264,7 +4288,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
       // grained memory can keep hitting this XCD's L2 copy of the line while another XCD counts
       uint32_t spins = 0;
       while ((__hip_atomic_fetch_add(&lg[i].pad, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & 0xFFFFu) < nch) {
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(TGSIM_SPIN_SLEEP);
         if (++spins == (1u << 24)) {  // a bound, never expected: report instead of hanging the device
           atomicOr(const_cast<uint32_t*>(&sc->err), ERR_TASKS);
           break;
@@ -4281,7 +4305,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     // a sampled index of the segment's sorted chunks in LDS (every st-th key of each chunk; the
     // chunks are complete, their tasks counted): a search first finds its st-key window among the
     // samples, then needs log2(st) dependent global loads instead of log2(kParChunk)
-    uint32_t st = 16;
+    uint32_t st = TGSIM_RANK_ST0;  // the densest sampling that fits the LDS arrays
     while (nch * (kParChunk / st) > (uint32_t)kSpan) st <<= 1;  // block-uniform
     const uint32_t S = kParChunk / st;  // samples of a full chunk
     for (uint32_t q = threadIdx.x; q < nch * S; q += kBlock) {

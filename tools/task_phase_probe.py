@@ -21,7 +21,7 @@ bench.sb_setup(sim, n, "accept")
 for w in range(windows):
     sim.advance((w + 1) * bench.SB_WINDOW_NS)
     sim.probe_react()
-raw = np.zeros(4 * 4096 + 2, np.uint64)
+raw = np.zeros(4 * 4096 + 8, np.uint64)
 assert hip.cdll.tgsim_debug_task_phases(raw.ctypes.data_as(ctypes.c_void_p)) == 0
 buf = raw[: 4 * 4096].reshape(4096, 4)
 ck = raw[4 * 4096:].astype(np.int64)
@@ -41,4 +41,7 @@ for name, m in (("chunk", ~rank), ("rank", rank)):
 last = np.argmax(np.where(rank, 0, a[:, 1]))
 print(f"last chunk task: keys loaded {(int(ck[0]) - int(a[last, 1])) / 100:.1f} us after its claim, "
       f"sorted {(int(ck[1]) - int(ck[0])) / 100:.1f} us later (clocks of the last chunk sort of any launch)")
+if ck[2]:
+    print("last 1024-key packed sort: " + ", ".join(f"{n} {(int(ck[i + 1]) - int(ck[i])) / 100:.1f} us" for i, n in
+          ((2, "min/max"), (3, "pack"), (4, "network"), (5, "restore"))))
 sim.close()
