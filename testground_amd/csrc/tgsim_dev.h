@@ -226,6 +226,10 @@ struct Dev {
   uint32_t* corr_idx = nullptr;   // [cap_msgs] deferred message indices (k_shape)
   uint32_t* corr_sorted = nullptr;  // [cap_msgs] the same, grouped by sender in (t_send, seq) order
   bool any_corr = false;          // some local shape has kShCorr
+  // some local sender has ever been bandwidth-limited (kShLimited): only then can a copy reach the
+  // token-bucket batch A (copies of an unlimited sender carry TGSIM_F_STAGE_D from the netem pass,
+  // wheel included), so the window skips the A partition, k_tb_bucket and k_rest<TB> until then
+  bool ever_limited = false;
   uint32_t* moff = nullptr;       // [segK] per local sender: its deferred messages in corr_sorted
 
   // netem queue limit: pend[l] = local sender l's records in the timing wheel

@@ -4897,7 +4897,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     TG_CHECK(hipGetLastError());
     if (d.any_corr || d.heavy.pend) TG_CHECK(run_shape_seq(d, a, n_staged));
   }
-  TG_CHECK(run_token_bucket(d));
+  if (d.ever_limited) TG_CHECK(run_token_bucket(d));  // else A is empty (Dev::ever_limited)
   if (d.S > 1) {
     hipLaunchKernelGGL(k_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, d.xsend, d.S, d.xcap, d.sc);
     TG_CHECK(hipGetLastError());

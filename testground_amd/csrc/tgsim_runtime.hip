@@ -974,6 +974,7 @@ static int upload_tables(tgsim_ctx* c) {
     for (uint32_t l = 0; l < c->nloc; ++l) {
       const ShapeDev& sh = c->shape_h[l];
       d.any_corr |= (sh.flags & kShCorr) != 0;
+      d.ever_limited |= (sh.flags & kShLimited) != 0;  // sticky: its copies may still be in flight
       c->any_dup |= sh.dup_t != 0;
       c->tbs_h[l] = TbShape{sh.tau, sh.mult, sh.shift};
       if (sh.mu == 0 && sh.sigma == 0 && !(sh.flags & kShLimited)) c->zd_h[l >> 5] |= 1u << (l & 31u);
@@ -3452,6 +3453,7 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->now_from_device = false;
   c->max_tsend_h = INT64_MIN;
   c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = true;  // re-uploaded at the next window
+  c->d.ever_limited = true;  // the restored wheel may hold copies of a sender limited before the snapshot
   memcpy(c->d.h_sc, r.p + r.at, sizeof(DevScalars));
   return check_device_errors(c);
 }

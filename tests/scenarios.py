@@ -92,6 +92,47 @@ def run_random(binding, seed: int, n_inst: int = 24, windows: int = 6, msgs_per_
     return out
 
 
+def run_limit_switch(binding, seed: int, n_inst: int = 32, windows: int = 8, window_ns: int = 10 * MS):
+    """Bandwidth limits switched on and off mid-run with copies in flight. A context whose senders
+    have never been limited skips the token-bucket stage (Dev::ever_limited): windows 0-1 run
+    without any limit, windows 2-3 limit a quarter of the senders (their copies then sit in the wheel
+    and in A), and from window 4 on the limits are gone again while those copies are still in flight
+    (the stage must keep running for them)."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=3000 + seed), binding=binding)
+    base = [make_shape(latency_ns=int(rng.integers(5, 36)) * MS, jitter_ns=int(rng.choice([0, 2 * MS])),
+                       loss=float(rng.choice([0.0, 5.0]))) for _ in range(n_inst)]
+    for g in range(n_inst):
+        sim.set_shape(g, base[g])
+    limited = rng.choice(n_inst, size=n_inst // 4, replace=False)
+    out, seqc, t0 = [], np.zeros(n_inst, np.int64), 0
+    for w in range(windows):
+        if w in (2, 4):
+            for g in limited:
+                sh = base[int(g)]
+                sim.set_shape(int(g), make_shape(latency_ns=sh.latency_ns, jitter_ns=sh.jitter_ns,
+                                                 loss=sh.loss, bandwidth_bps=800_000 if w == 2 else 0))
+        n = 200
+        src = rng.integers(0, n_inst, n)
+        dst = (src + rng.integers(1, n_inst, n)) % n_inst
+        seq = np.zeros(n, np.int64)
+        for i in range(n):
+            seq[i] = seqc[src[i]]
+            seqc[src[i]] += 1
+        t = t0 + np.sort(rng.integers(0, window_ns, n))
+        sim.enqueue(src, dst, seq, rng.choice([64, 1000, 4000], n), t)
+        t0 += window_ns
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    for w in range(4):
+        t0 += 20 * window_ns
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_heavy(binding, seed: int, n_inst: int = 64):
     """One sender with a long backlog (token-bucket segment > LDS tile) and one receiver with a large
     inbox (delivery segment > LDS tile): exercises the merge-path large-segment paths. With more

@@ -22,6 +22,13 @@ def test_random_windows_small_wheel(hip, oracle):
     S.assert_same(S.run_random(hip, 11, cfg_kw=kw), S.run_random(oracle, 11, cfg_kw=kw))
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_bandwidth_limits_switched_mid_run(hip, oracle, seed):
+    """The token-bucket stage is skipped until a sender is first limited, and kept after its limit
+    is lifted while its copies are in flight (tests/scenarios.py run_limit_switch)."""
+    S.assert_same(S.run_limit_switch(hip, seed), S.run_limit_switch(oracle, seed))
+
+
 @pytest.mark.parametrize("n_inst", [64, 200, 1000])
 def test_large_segments(hip, oracle, n_inst):
     S.assert_same(S.run_heavy(hip, 7, n_inst), S.run_heavy(oracle, 7, n_inst))
