@@ -83,10 +83,8 @@ BYTE_MODELS = {
     "k_shape_seq": lambda d: 73 * (d.get("deferred", 0) - d.get("wide", 0)),
     "k_seg_small": lambda d: 24 * d.get("deferred", 0),
     # the whole-sender closed form: as the sequential lane plus its own ordering (the index read and
-    # written back in place, (t_send, seq) gathered); k_copy_n keeps the group-by's order (4 B read,
-    # 4 B written per deferred message)
+    # written back in place, (t_send, seq) gathered)
     "k_shape_seq_wide": lambda d: 81 * d.get("wide", 0),
-    "k_copy_n": lambda d: 8 * d.get("deferred", 0),
     # flood (config 5): count reads (dst, src, seq) and writes count + first flag per delivery;
     # emit writes the 24 B staged message per forward after re-reading the 17 B per delivery
     "k_flood_count": lambda d: 21 * d["delivered"],

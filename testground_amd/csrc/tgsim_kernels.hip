@@ -1224,7 +1224,7 @@ template <int U = kGlobUnroll, class ItemAt>
 __device__ __forceinline__ void bkt_emit_global_f(const ItemAt& item_at, uint32_t* kout, uint32_t* vout, uint32_t B,
                                                   uint32_t K, uint32_t* cnt, const BktHead& h, uint32_t* off,
                                                   uint32_t* off2, uint32_t medium_above, uint32_t* medium,
-                                                  LargeSeg* large, DevScalars* sc) {
+                                                  LargeSeg* large, DevScalars* sc, uint32_t* vout2 = nullptr) {
   const uint32_t tid = threadIdx.x;
   bkt_global_offsets(cnt, h, off, off2, medium_above, medium, large, sc);
   for (uint32_t j0 = tid; j0 < h.nb; j0 += kBlock * U) {
@@ -1240,6 +1240,7 @@ __device__ __forceinline__ void bkt_emit_global_f(const ItemAt& item_at, uint32_
       const uint32_t pos = h.start + atomicAdd(&cnt[e[u].x - h.k0], 1u);
       kout[pos] = e[u].x;
       vout[pos] = e[u].y;
+      if (vout2) vout2[pos] = e[u].y;
     }
   }
 }
@@ -1276,22 +1277,23 @@ __device__ __forceinline__ void bkt_emit_global(const uint32_t* kin, const uint3
                                                 uint32_t* vout, uint32_t B, uint32_t K, uint32_t* cnt,
                                                 const BktHead& h, uint32_t* off, uint32_t* off2,
                                                 uint32_t medium_above, uint32_t* medium, LargeSeg* large,
-                                                DevScalars* sc) {
+                                                DevScalars* sc, uint32_t* vout2) {
   bkt_emit_global_f([&](uint32_t j) { return make_uint2(kin[h.start + j], vin[h.start + j]); }, kout, vout, B, K, cnt,
-                    h, off, off2, medium_above, medium, large, sc);
+                    h, off, off2, medium_above, medium, large, sc, vout2);
 }
 
-// pass 3: one workgroup per bucket, global form only (signals, and > 2^bs-key fallbacks).
+// pass 3: one workgroup per bucket, global form only (signals, and > 2^bs-key fallbacks); vout2, if
+// given, receives a second copy of the values.
 __global__ __launch_bounds__(kBlock) void k_bkt_sort(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                                                      uint32_t* vout, BktDiv bd, uint32_t B, uint32_t K,
                                                      const uint32_t* tot, uint32_t* off, uint32_t* off2,
                                                      uint32_t medium_above, uint32_t* medium, LargeSeg* large,
-                                                     DevScalars* sc) {
+                                                     DevScalars* sc, uint32_t* vout2) {
   __shared__ uint32_t cnt[1u << kBktMaxKeyBits];
   __shared__ uint32_t part[kBlock];
   BktHead h;
   bkt_count_keys(kin, bd, K, tot, cnt, part, h);
-  bkt_emit_global(kin, vin, kout, vout, B, K, cnt, h, off, off2, medium_above, medium, large, sc);
+  bkt_emit_global(kin, vin, kout, vout, B, K, cnt, h, off, off2, medium_above, medium, large, sc, vout2);
 }
 
 // Wheel insert with buckets = slots (slots <= kMaxBins): records are copied straight from the L
@@ -2017,7 +2019,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     }
     __syncthreads();
     (void)bkt_count_body(kscr, sm.cnt, sm.part, h);
-    bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc);
+    bkt_emit_global(kscr, vscr, kout, vout, B, K, sm.cnt, h, off, off2, 0, medium, large, sc, nullptr);
     return false;
   }
 #endif
@@ -2439,23 +2441,19 @@ struct SigPolicy {
 
 __global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* src, const uint32_t* n_ptr,
                                                       uint32_t lo, uint32_t* keys, uint32_t* vals,
-                                                      unsigned long long* kc_deferred) {
+                                                      unsigned long long* kc_deferred, uint32_t* seq_left,
+                                                      uint32_t seq_left0) {
   const uint32_t n = *n_ptr;
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(kc_deferred, (unsigned long long)n);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(kc_deferred, (unsigned long long)n);
+    *seq_left = seq_left0;  // k_shape_seq_wide counts up from here (a memset would be a launch of its own)
+  }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
     const uint32_t i = idx[j];
     keys[j] = src[i] - lo;
     vals[j] = i;
   }
-}
-
-// dst[0, n) = src[0, n), n device-side (the deferred messages' group-by output, which the heavy
-// senders' group-by that follows overwrites, kept for k_shape_seq_wide's per-sender sort)
-__global__ __launch_bounds__(kBlock) void k_copy_n(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                                   const uint32_t* n_ptr, uint32_t cap) {
-  const uint32_t n = min(*n_ptr, cap);
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) dst[i] = src[i];
 }
 
 struct CorrPolicy {
@@ -4735,7 +4733,7 @@ static hipError_t bkt_local(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
 // Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
 // d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
 static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t medium_above, uint32_t* off2,
-                               uint32_t** keys, uint32_t** vals, bool fine = false) {
+                               uint32_t** keys, uint32_t** vals, bool fine = false, uint32_t* vals_copy = nullptr) {
   const int bs = bkt_shift(K, fine);
   if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
   const uint32_t B = (K + (1u << bs) - 1) >> bs;
@@ -4744,7 +4742,7 @@ static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t m
   {
     ProfScope ps_(d, KID_BKT_SORT);
     hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bd, B, K,
-                       d.tot, d.seg_off, off2, medium_above, d.medium, d.large, d.sc);
+                       d.tot, d.seg_off, off2, medium_above, d.medium, d.large, d.sc, vals_copy);
   }
   TG_CHECK(hipGetLastError());
   *keys = d.keys0;
@@ -4793,24 +4791,21 @@ static hipError_t run_token_bucket(Dev& d) {
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
   hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.m_src, n_dev,
-                     d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED]);
+                     d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
   TG_CHECK(hipGetLastError());
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
   uint32_t *keys, *vals;
-  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true));
+  // with queue tracking the grouped values also go to corr_sorted, where k_shape_seq_wide orders each
+  // sender of <= kTile messages in place (the H group-by below reuses the group-by's output arrays)
+  TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true,
+                        a.heavy.pend ? d.corr_sorted : nullptr));
   CorrPolicy p;
   p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
   if (!a.heavy.pend) {
     ProfScope ps_(d, KID_SEG_SMALL);  // each sender's deferred messages in (t_send, seq) order
     hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
                        d.seg_off, n_dev, d.cap_rec);
-  } else {
-    // with queue tracking, k_shape_seq_wide orders each sender of <= kTile messages itself, in
-    // place in corr_sorted (the H group-by below reuses the group-by's output arrays)
-    ProfScope ps_(d, KID_COPY);
-    hipLaunchKernelGGL(k_copy_n, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, vals, d.corr_sorted, n_dev,
-                       d.cap_rec);
   }
   TG_CHECK(hipGetLastError());
   TG_CHECK(launch_rest(d, p, keys, vals));
@@ -4825,8 +4820,8 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     hidx = hv;
   }
   const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
-  // k_shape_seq skips its launch's work when the closed form left it no sender (seq_left 0)
-  TG_CHECK(hipMemsetAsync(&d.sc->seq_left, a.heavy.pend ? 0 : 1, sizeof(uint32_t), d.stream));
+  // k_shape_seq skips its launch's work when the closed form left it no sender (seq_left 0, set by
+  // k_keys_corr above)
   if (a.heavy.pend) {  // the whole-sender closed form first (heavy senders without HTB / correlation)
     ProfScope ps_(d, KID_SHAPE_WIDE);
     hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
