@@ -196,6 +196,23 @@ __host__ __device__ inline uint32_t shard_of(uint32_t g, uint32_t N, uint32_t S)
   return (uint32_t)((((uint64_t)g + 1) * S - 1) / N);
 }
 
+// One-sided agent-scope fences: a producer that publishes data through a counter needs only the
+// release half (its XCD's L2 written back), a consumer only the acquire half (stale lines dropped);
+// __threadfence() does both in every workgroup that runs it.
+__device__ inline void fence_release_agent() {
+#ifdef TGSIM_FULL_FENCE
+  __threadfence();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+}
+__device__ inline void fence_acquire_agent() {
+#ifdef TGSIM_FULL_FENCE
+  __threadfence();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ inline uint32_t mask_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -4275,7 +4275,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
 #ifdef TGSIM_PHASE_PROF
       const uint64_t tp_sorted = __builtin_amdgcn_s_memrealtime();
 #endif
-      __threadfence();  // the sorted chunk is visible device-wide before it is counted
+      fence_release_agent();  // the sorted chunk is visible device-wide before it is counted
       __syncthreads();
       if (threadIdx.x == 0) atomicAdd(&lg[i].pad, 1u);
       TASK_PH(tp_sorted);
@@ -4294,7 +4294,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
       }
     }
     __syncthreads();
-    __threadfence();
+    fence_acquire_agent();  // the counted chunks' keys, written by other workgroups
 #ifdef TGSIM_PHASE_PROF
     const uint64_t tp_ready = __builtin_amdgcn_s_memrealtime();
 #endif

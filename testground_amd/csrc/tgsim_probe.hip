@@ -224,12 +224,12 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
   }
   // the last workgroup to finish proposes the next window's end (the former k_probe_end launch)
   __shared__ uint32_t s_last;
-  __threadfence();
+  fence_release_agent();
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&p.sc->done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
-    __threadfence();
+    fence_acquire_agent();
     probe_end(p, sc);
   }
 }

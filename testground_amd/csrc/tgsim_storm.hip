@@ -474,12 +474,12 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, TcpDev t, Dev
   }
   // the last workgroup to finish proposes the next window's end
   __shared__ uint32_t s_last;
-  __threadfence();
+  fence_release_agent();
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&s.sc->done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
-    __threadfence();
+    fence_acquire_agent();
     storm_end(s, t, sc, t_end);
   }
 }

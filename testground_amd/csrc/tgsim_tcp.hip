@@ -139,9 +139,9 @@ __device__ __forceinline__ uint32_t tcp_arrived(TcpDev& t, uint32_t sw, int64_t 
   // running max, then the count; the last segment reads the max back after its count (the fences
   // order each thread's max before its count, and the counts are totally ordered)
   atomicMax(reinterpret_cast<long long*>(&t.w_tmax[w]), (long long)arr);
-  __threadfence();
+  fence_release_agent();
   if (atomicSub(&t.w_rem[w], 1u) != 1u) return 0u;
-  __threadfence();
+  fence_acquire_agent();
   const long long m = atomicMax(reinterpret_cast<long long*>(&t.w_tmax[w]), (long long)arr);
   t.w_tarr[w] = m > (long long)arr ? (int64_t)m : arr;
   return 1u;
