@@ -348,24 +348,63 @@ def cpu_baseline(args, shapes):
 
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv=None, script=None) -> int:
+    """`python bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start the N
+    ranks as child processes of this one, one per GPU, with the variables torch.distributed.run would
+    set, and forward rank 0's output. This process never touches the GPU (no torch.cuda call, no
+    libtgsim.so load: it imports neither), so nothing here is initialised when the children start.
+    Returns the exit status: the first failing rank's, else 0. A rank that fails makes the others'
+    collectives fail or hang, so after the first failure the rest get a grace period and are killed."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = None if r == 0 else subprocess.DEVNULL  # rank 0 prints the JSON line; others' stdout is quiet
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] +
+                                      list(sys.argv[1:] if argv is None else argv), env=env,
+                                      stdout=out, start_new_session=True))
+    rc = 0
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            code = p.poll()
+            if code not in (None, 0) and rc == 0:
+                rc, failed_at = code, time.monotonic()
+                print(f"bench: rank {r} exited with {code}", file=sys.stderr, flush=True)
+        if failed_at is not None and time.monotonic() - failed_at > 30:
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGKILL)
+        time.sleep(0.2)
+    for r, p in enumerate(procs):
+        if p.returncode and rc == 0:
+            rc = p.returncode
+            print(f"bench: rank {r} exited with {p.returncode}", file=sys.stderr, flush=True)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.workload in ("a2a", "splitbrain"):
+            raise SystemExit(f"--workload {args.workload} is a single-GPU configuration")
+        sys.exit(spawn_ranks(args.gpus))
     if args.workload == "flood":
         return main_flood(args)
     if args.workload == "a2a":
         return main_a2a(args)
     if args.workload == "splitbrain":
         return main_splitbrain(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    import torch
-    import torch.distributed as dist
-    from testground_amd._abi import T_NOW
-    from testground_amd.sim import Simulator
-
     torch, dist, world, rank, local, rehearsal, stream = _dist_setup(args)
     from testground_amd._abi import T_NOW
     from testground_amd.sim import Simulator

@@ -222,6 +222,7 @@ struct tgo_ctx {
   uint32_t* tpend; size_t tpend_n, tpend_cap;
   struct otack* tack; size_t tack_n, tack_cap;  /* acks = 1: ACK packets for the next window */
   struct otcpc* tc; size_t tc_n, tc_cap;        /* connections (tgsim_tcp_connect) */
+  uint64_t sm_conn_lo, sm_conn_hi;               /* a TCP storm's connections: host writes refused */
   tgsim_tcp_stats tstats;
   /* sequential probes (tgsim_probe_*) */
   struct oprobe* pr; uint32_t* pr_order; uint8_t* pr_out; uint32_t pr_n; tgsim_probe_config pr_cfg;
@@ -1813,6 +1814,8 @@ int tgo_tcp_write(tgo_ctx* c, const uint32_t* conn, const uint32_t* size, const 
   size_t nseg = 0;
   for (size_t i = 0; i < n; ++i) {
     if (conn[i] >= c->tc_n) return fail(c, TGSIM_EINVAL, "write %zu: no connection %u", i, conn[i]);
+    if (conn[i] >= c->sm_conn_lo && conn[i] < c->sm_conn_hi)  /* its queue ends where the reactor left it */
+      return fail(c, TGSIM_ESTATE, "write %zu: connection %u was a storm reactor's", i, conn[i]);
     if (t[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
     if (size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
     nseg += size[i] ? (size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;
@@ -2344,8 +2347,10 @@ int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, con
     for (uint64_t h = 0; h < n_conn; ++h) src[h] = (uint32_t)(h / O);
     ostorm* keep = c->sm;
     c->sm = NULL;  /* tgo_tcp_connect refuses while a reactor owns the connections */
+    const uint64_t lo = c->tc_n;
     int rc = tgo_tcp_connect(c, src, dst, n_conn, NULL);
     c->sm = keep;
+    if (!rc) { c->sm_conn_lo = lo; c->sm_conn_hi = c->tc_n; }
     free(src);
     if (rc) { sm_free(c); return rc; }
     if (grow((void**)&c->tw, &c->tw_cap, c->tw_n + tot_w + 1, sizeof(otcpw)) ||
@@ -2411,9 +2416,16 @@ static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_e
       const uint32_t ws = c->tw[sm_wid(s, h, 0)].state;
       uint8_t out = c->tc[h].acked >= 1 ? TGSIM_PROBE_OK
                   : ws == TGSIM_TCP_TIMEOUT ? TGSIM_PROBE_TIMEOUT : ws == TGSIM_TCP_REFUSED ? TGSIM_PROBE_REFUSED : TGSIM_PROBE_NONE;
+      int64_t te = t_end;
+      if (out == TGSIM_PROBE_NONE && x->t_start + timeout < t_end) {  /* net.DialTimeout (storm.go:144): */
+        size_t unused = 0;                                             /* the SYN write fails at the deadline */
+        te = x->t_start + timeout;
+        out = TGSIM_PROBE_TIMEOUT;
+        tcp_finish(c, sm_wid(s, h, 0), TGSIM_TCP_TIMEOUT, te, &unused);
+      }
       if (out != TGSIM_PROBE_NONE) {
-        x->state = SM_DONE; x->res = out; x->t_done = t_end;
-        s->slot_t[(size_t)g * C + x->slot] = t_end;
+        x->state = SM_DONE; x->res = out; x->t_done = te;
+        s->slot_t[(size_t)g * C + x->slot] = te;
       } else {
         ++*act; ++*waiting;
       }
@@ -2608,6 +2620,16 @@ int tgo_storm_start(tgo_ctx* c) {
   return sm_step(c, 0, c->now, c->now, NULL, NULL);
 }
 
+/* The connection of a chunk packet (src -> dst, chunk id cj = k * nchunks + j), or -1 when no chunk
+ * the storm has written matches it (a message the host staged beside the reactor: ADVICE r4) */
+static int64_t sm_chunk_conn(const ostorm* s, uint32_t src, uint32_t dst, uint32_t cj) {
+  if (s->nchunks == 0) return -1;
+  const uint32_t k = cj / s->nchunks, j = cj - k * s->nchunks;
+  const uint64_t h = (uint64_t)src * s->O + k;
+  if (k >= s->O || h >= s->n_conn || s->conn[h].dst != dst || j >= s->nchunks - s->conn[h].rem) return -1;
+  return (int64_t)h;
+}
+
 int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   ostorm* s = c->sm;
   if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
@@ -2622,12 +2644,16 @@ int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   for (size_t i = 0; i < c->n_status; ++i) {
     const uint32_t sq = st->seq[i], tag = sq >> 30, code = c->status[i] & 0x0Fu;
     if (tag == 1u) {
-      ostorm_conn* x = &s->conn[(size_t)st->src[i] * O + (sq & PR_MASK)];
+      const size_t h = (size_t)st->src[i] * O + (sq & PR_MASK);
+      if ((sq & PR_MASK) >= O || h >= s->n_conn) continue;
+      ostorm_conn* x = &s->conn[h];
       if ((code == TGSIM_ST_DROPPED || code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) &&
           x->state == SM_WAIT && x->dst == st->dst[i])
         x->flags |= 1u;
     } else if (tag == 2u && sm_failed_code(c->status[i])) {
-      s->conn[(size_t)st->src[i] * O + (sq & PR_MASK) / s->nchunks].infl--;
+      const int64_t h = sm_chunk_conn(s, st->src[i], st->dst[i], sq & PR_MASK);
+      if (h < 0) continue;
+      s->conn[h].infl--;
       s->failed[st->src[i]] = 1;
       s->failed_chunks++;
     }
@@ -2637,7 +2663,9 @@ int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
     const tgsim_record* r = &c->out.v[i];
     const uint32_t tag = r->seq >> 30;
     if (tag == 1u) {
-      ostorm_conn* x = &s->conn[(size_t)r->src * O + (r->seq & PR_MASK)];
+      const size_t h = (size_t)r->src * O + (r->seq & PR_MASK);
+      if ((r->seq & PR_MASK) >= O || h >= s->n_conn) continue;
+      ostorm_conn* x = &s->conn[h];
       if (x->state == SM_WAIT && x->dst == r->dst && r->t < x->t_synarr) x->t_synarr = r->t;
     } else if (tag == 3u) {
       const size_t h = r->seq & PR_MASK;
@@ -2646,8 +2674,10 @@ int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
         if (x->dst == r->src && x->state == SM_WAIT && (x->flags & 2u) && r->t < x->t_ackarr) x->t_ackarr = r->t;
       }
     } else if (tag == 2u) {
-      const uint32_t cj = r->seq & PR_MASK, k = cj / s->nchunks;
-      const size_t h = (size_t)r->src * O + k;
+      const uint32_t cj = r->seq & PR_MASK;
+      const int64_t h = sm_chunk_conn(s, r->src, r->dst, cj);
+      if (h < 0) continue;
+      const uint32_t k = cj / s->nchunks;
       const uint64_t bit = (uint64_t)h * s->nchunks + (cj - k * s->nchunks);
       if (!s->claim[bit]) { s->claim[bit] = 1; s->conn[h].infl--; s->delivered++; }
     }

@@ -273,7 +273,7 @@ struct Dev {
   int grid_shape = 2048;          // k_shape / k_gen_storm grids (init_launch_geometry)
   int grid_gen = 2048;
   uint32_t* bstart = nullptr;     // [kMaxBins + 1] bucket starts of the last partition pass
-  uint32_t* qc = nullptr;         // [3][kNSub][32] append counters (128 B apart)
+  uint32_t* qc = nullptr;         // [kQcLines][32] append counters (128 B apart): A / D / L, exchange
   uint32_t* seg_off = nullptr;    // [max(nloc, slots, max_states) + 1]
   LargeSeg* large = nullptr;
   uint32_t* medium = nullptr;     // [segK] ids of segments kThreadSeg < len <= kTile

@@ -20,6 +20,7 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kNSub = 64;                // append sub-queues per batch (contention sharding)
 constexpr int kRankSortMax = 64;         // segments up to this length are rank-sorted in LDS
 constexpr int kMaxShards = 64;
+constexpr int kQcLines = 3 * kNSub + kMaxShards;  // A / D / L sub-queue counters, then exchange cursors
 constexpr int kMaxRegions = 8192;        // live timing-wheel regions (one per window)
 constexpr int kStreamBlocks = 2048;      // grid of grid-stride streaming kernels
 constexpr int64_t kNegInf = INT64_MIN / 4;
@@ -83,7 +84,7 @@ struct DevScalars {
   int64_t H;                         // reaction horizon: earliest admissible t_send
   int64_t base_slot;                 // t_end / slot_ns: timing-wheel slot 0 of this window's insertions
   // ---- per-window block: zeroed by one memset at window start ----
-  uint32_t q[Q_X0 + kMaxShards];     // exchange cursors per peer (q[Q_X0 + p]); q[0..2] unused
+  uint32_t q[Q_X0 + kMaxShards];     // unused (round 4's exchange cursors; now lines of qc, Queues::xctr)
   uint32_t qpre[3][kNSub + 1];       // A, D, L: prefix over sub-queues (after k_qfinal)
   uint32_t qn[3];                    // A, D, L: totals (after k_qfinal)
   uint32_t n_extract;                // records extracted from the wheel this window

@@ -106,6 +106,7 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
 struct Queues {
   DevScalars* sc;
   uint32_t* qc;
+  uint32_t* xq;              // exchange cursor of queue q >= Q_X0 at xq[q << 5] (lines 3 * kNSub.. of qc)
   tgsim_record *A, *D, *L, *X;
   uint32_t* K[3];            // group-by key of each appended record, same physical index (A, D, L)
   uint32_t subcap, xcap, lo, slots;
@@ -120,6 +121,10 @@ struct Queues {
     for (int j = 0; j < 7; ++j) g += key >= gb[j] ? 1u : 0u;
     return g;
   }
+  // Exchange cursor of peer p: a 128-B line of its own after the A / D / L sub-queue counters (round
+  // 4 kept every peer's cursor in one DevScalars line; one per wave and item serialised a sharded
+  // token bucket on that address: k_tb_bucket 20 -> 165 us per 50k shard)
+  __device__ __forceinline__ uint32_t* xctr(uint32_t p) const { return xq + ((p + Q_X0) << 5); }
   // A: local sender; D: local receiver; L: timing-wheel slot relative to this window's end
   __device__ __forceinline__ uint32_t key_of(int q, const tgsim_record& r) const {
     if (q == Q_A) return r.src - lo;
@@ -143,7 +148,7 @@ struct Queues {
         cap = subcap;
         eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
       } else {
-        ctr = &sc->q[q];
+        ctr = xq + ((uint32_t)q << 5);
         buf = X + (size_t)(q - Q_X0) * xcap + 1;
         cap = xcap - 1;
         eb = ERR_CAP_X;
@@ -229,7 +234,7 @@ struct Queues {
       }
       pL += (uint32_t)__popcll(mL[u]);
     }
-    if (__ballot(any_x)) {
+    if (__ballot(any_x)) {  // per item: one reservation per (wave, peer) on the peer's cursor
 #pragma unroll
       for (int u = 0; u < U; ++u) push(q[u] >= Q_X0 ? q[u] : -1, r[u], salt + u);
     }
@@ -309,7 +314,7 @@ __device__ __forceinline__ void window_start_block(const WindowArgs& a) {
   const int64_t t_end_arg = a.t_end_arg, offset = a.offset, slot_ns = a.slot_ns;
   const int64_t* src = a.src;
   __shared__ int64_t s_tend;
-  for (uint32_t i = threadIdx.x; i < 3u * kNSub; i += kBlock) qc[i << 5] = 0;  // one counter per 128-B line
+  for (uint32_t i = threadIdx.x; i < kQcLines; i += kBlock) qc[i << 5] = 0;  // one counter per 128-B line
   uint32_t* w = sc->q;  // the per-window block [q, err) of DevScalars
   const uint32_t nw = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
   for (uint32_t i = threadIdx.x; i < nw; i += kBlock) w[i] = 0;
@@ -809,7 +814,8 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
 // A / D / L queues, through reservations), so a window with staged messages runs them as one
 // launch: blocks [0, ne) extract, the rest shape. ne is a multiple of 8, so every block keeps the
 // XCD (blockIdx mod 8) its sub-queue choice assumes.
-__global__ __launch_bounds__(kBlock) void k_extract_shape(const RegionDev* regions, const uint32_t* plan_start,
+// five waves per SIMD (<= 96 VGPRs, as before the exchange cursors moved; 98 made it four)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_extract_shape(const RegionDev* regions, const uint32_t* plan_start,
                                                           const uint32_t* plan_off, const tgsim_record* arena,
                                                           Queues Q, ShapeArgs a, uint32_t ne, HeavyOut ho) {
   if (blockIdx.x < ne) extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, ne, ho);
@@ -2255,8 +2261,14 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     wL += (uint32_t)__popcll(mL[u]);
   }
   const uint32_t wave = threadIdx.x >> 6;
+  // cross-shard copies (S > 1): per peer an LDS count (each copy's rank in it) and one reservation
+  // per workgroup on the peer's cursor, sm.part[64 + p] / sm.part[128 + p]
+  uint32_t* xcnt = sm.part + 64;
+  uint32_t* xbase = sm.part + 128;
+  static_assert(kBlock >= 128 + kMaxShards, "exchange counts fit sm.part");
   if (threadIdx.x == 0) sm.flag = 0;
   if (threadIdx.x < 8) gcnt[threadIdx.x] = 0;
+  if (threadIdx.x < kMaxShards) xcnt[threadIdx.x] = 0;
   if ((threadIdx.x & 63) == 0) sm.part[kBlock / 64 + wave] = wL;
   __syncthreads();
 #pragma unroll
@@ -2265,6 +2277,8 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     if (code[u] == Q_D) {
       const uint32_t g = Q.group_of(rec[u].dst - p.lo);
       rkD[u] = (g << 24) | atomicAdd(&gcnt[g], 1u);
+    } else if (code[u] >= Q_X0) {
+      rkD[u] = atomicAdd(&xcnt[code[u] - Q_X0], 1u);
     }
   }
   // this workgroup owns its senders' counters for the launch (long runs: k_rest, later)
@@ -2290,6 +2304,10 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
   if (threadIdx.x == 0) {
     sm.part[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
     sm.part[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
+  }
+  if (sm.flag && threadIdx.x >= 64 && threadIdx.x < 64 + p.geo.S) {  // another wave: in parallel
+    const uint32_t pr = threadIdx.x - 64, c = xcnt[pr];
+    xbase[pr] = c ? atomicAdd(Q.xctr(pr), c) : 0u;
   }
   // the routed copies pass through LDS in append order (the D run, then the L run), kStageN per
   // round, so that every wave store covers consecutive records: whole lines, no reliance on L2
@@ -2331,9 +2349,15 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     }
     __syncthreads();
   }
-  if (sm.flag) {  // cross-shard copies (S > 1): wave appends onto the peer blocks
+  if (sm.flag) {  // cross-shard copies: straight into the peer blocks at the reserved positions
+    __syncthreads();  // xbase visible (the staging loop may have had no round)
 #pragma unroll
-    for (int u = 0; u < kIPT; ++u) Q.push(code[u] >= Q_X0 ? code[u] : -1, rec[u], (uint32_t)u);
+    for (int u = 0; u < kIPT; ++u) {
+      if (code[u] < Q_X0) continue;
+      const uint32_t pr = (uint32_t)(code[u] - Q_X0), pos = xbase[pr] + rkD[u];
+      if (pos < Q.xcap - 1) store_rec(Q.X + (size_t)pr * Q.xcap + 1 + pos, rec[u]);
+      else atomicOr(&Q.sc->err, ERR_CAP_X);
+    }
   }
   TG_PH_END(0, h.nb);
 }
@@ -3754,7 +3778,7 @@ __global__ __launch_bounds__(kBlock) void k_window_start_commit(SigState g, uint
     r_cons = rp->consumed; r_n = rp->n; r_base = rp->base_slot; r_dir = rp->dir; r_aoff = rp->arena_off;
   }
   // the per-window counters (nothing below reads them before the barriers)
-  for (uint32_t i = tid; i < 3u * kNSub; i += kBlock) w.qc[i << 5] = 0;
+  for (uint32_t i = tid; i < kQcLines; i += kBlock) w.qc[i << 5] = 0;
   {
     uint32_t* wb = sc->q;
     const uint32_t nwb = (uint32_t)((offsetof(DevScalars, err) - offsetof(DevScalars, q)) / sizeof(uint32_t));
@@ -4393,11 +4417,11 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
 // exchange (sharded runs)
 // ============================================================================================
 
-__global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const DevScalars* sc) {
+__global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const uint32_t* qc) {
   const uint32_t p = threadIdx.x;
   if (p >= S) return;
   tgsim_record h;
-  const uint32_t n = min(sc->q[Q_X0 + p], xcap - 1);
+  const uint32_t n = min(qc[(3u * kNSub + p) << 5], xcap - 1);
   h.t = (int64_t)n; h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
   store_rec(xsend + (size_t)p * xcap, h);
 }
@@ -4656,7 +4680,7 @@ static inline unsigned grid_for(uint64_t n) {
 static uint32_t bkt_width_fused(const Dev& d, uint32_t K);
 static Queues make_queues(Dev& d) {
   Queues Q;
-  Q.sc = d.sc; Q.qc = d.qc; Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
+  Q.sc = d.sc; Q.qc = d.qc; Q.xq = d.qc + ((size_t)(3 * kNSub - Q_X0) << 5); Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
   Q.K[0] = d.KA; Q.K[1] = d.KD; Q.K[2] = d.KL; Q.lo = d.lo; Q.slots = d.slots; Q.slot_ns = d.slot_ns;
   // the fused consumers' buckets (bkt_width_fused over the local keys) in xcd_major order: XCD x
   // runs buckets [x q + min(x, r), (x+1) q + min(x+1, r)) with q = B / 8, r = B % 8
@@ -4894,7 +4918,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
   }
   if (d.ever_limited) TG_CHECK(run_token_bucket(d));  // else A is empty (Dev::ever_limited)
   if (d.S > 1) {
-    hipLaunchKernelGGL(k_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, d.xsend, d.S, d.xcap, d.sc);
+    hipLaunchKernelGGL(k_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, d.xsend, d.S, d.xcap, d.qc);
     TG_CHECK(hipGetLastError());
   }
   return hipSuccess;

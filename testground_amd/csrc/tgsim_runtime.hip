@@ -167,6 +167,9 @@ struct tgsim_ctx {
   // opens the next window (it reads the window's staged rows and deliveries)
   bool probe_need_react = false;
   bool storm_on = false;    // tgsim_storm_setup done, not ended
+  // a TCP storm's connections [lo, hi): host writes are refused on them, also after tgsim_storm_end
+  // (their queues end at the last chunk the reactor linked, which the host does not track)
+  uint64_t storm_conn_lo = 0, storm_conn_hi = 0;
   bool storm_need_react = false;
 };
 
@@ -504,7 +507,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.hist, (size_t)kMaxBins * kRadixBlocks);
   rc |= dalloc(c, &d.tot, kMaxBins);
   rc |= dalloc(c, &d.bstart, kMaxBins + 1);
-  rc |= dalloc(c, &d.qc, (size_t)3 * kNSub * 32);
+  rc |= dalloc(c, &d.qc, (size_t)kQcLines * 32);
   rc |= dalloc(c, &d.sig_red, 4);
   rc |= dalloc(c, &d.sig_part, 2 * 4096);
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
@@ -2273,8 +2276,11 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
   if (c->tcp_on) {
     std::vector<uint32_t> src(n_conn);
     for (uint64_t h = 0; h < n_conn; ++h) src[h] = (uint32_t)(h / O);
+    const uint64_t conn_lo = c->td.n_conn;
     int rc = tgsim_tcp_connect_body(c, src.data(), dst, n_conn, nullptr);  // connection ids 0 .. n_conn - 1
     if (rc) { storm_free(c); return rc; }
+    c->storm_conn_lo = conn_lo;
+    c->storm_conn_hi = c->td.n_conn;
     s.tcp = 1;
     s.mss = c->td.mss;
     s.spc = (uint32_t)spc;
@@ -3126,6 +3132,8 @@ static int tgsim_tcp_write_body(tgsim_ctx* c, const uint32_t* conn, const uint32
   size_t nseg = 0;
   for (size_t i = 0; i < n; ++i) {
     if (conn[i] >= td.n_conn) return fail(c, TGSIM_EINVAL, "write %zu: no connection %u", i, conn[i]);
+    if (conn[i] >= c->storm_conn_lo && conn[i] < c->storm_conn_hi)
+      return fail(c, TGSIM_ESTATE, "write %zu: connection %u was a storm reactor's", i, conn[i]);
     if (t_send[i] < c->horizon) return fail(c, TGSIM_ECAUSALITY, "write %zu: t_send before the horizon", i);
     if (size[i] >= 0x80000000u) return fail(c, TGSIM_EINVAL, "write %zu: size too large", i);
     nseg += size[i] ? (size[i] + c->tcp.mss - 1) / c->tcp.mss : 1;

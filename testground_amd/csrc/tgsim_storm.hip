@@ -54,6 +54,19 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long
   __syncthreads();
 }
 
+// The connection a chunk packet (src -> dst, chunk id c = k * nchunks + j) belongs to, or kNoConn
+// when no written chunk of the storm matches it (a message the host staged beside the
+// reactor with the chunk tag must not index past the tables or free another chunk's buffer slot).
+// rem[h] is not written before k_storm_step, so "written" is the count before this reaction.
+constexpr size_t kNoConn = ~(size_t)0;
+__device__ __forceinline__ size_t chunk_conn(const StormDev& s, uint32_t src, uint32_t dst, uint32_t c) {
+  if (s.nchunks == 0) return kNoConn;
+  const uint32_t k = c / s.nchunks, j = c - k * s.nchunks;
+  const size_t h = (size_t)src * s.O + k;
+  if (k >= s.O || h >= s.n_conn || s.dst[h] != dst || j >= s.nchunks - s.rem[h]) return kNoConn;
+  return h;
+}
+
 __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict__ status,
                                                       const uint32_t* __restrict__ m_src,
                                                       const uint32_t* __restrict__ m_dst,
@@ -80,13 +93,15 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
       const uint32_t sq = m_seq[i], tag = sq >> 30;
       if (tag == 1u) {  // a SYN: refused by the dialler's route
         if (!refused_code(status[i])) continue;
-        const size_t h = (size_t)m_src[i] * O + (sq & kTagMask);
-        if (s.state[h] == kWait && s.dst[h] == m_dst[i]) s.flags[h] |= 1u;
+        const uint32_t k = sq & kTagMask;
+        const size_t h = (size_t)m_src[i] * O + k;
+        if (k < O && h < s.n_conn && s.state[h] == kWait && s.dst[h] == m_dst[i]) s.flags[h] |= 1u;
       } else if (tag == 2u) {  // a chunk that no copy of entered the egress queue
         if (!failed_code(status[i])) continue;
-        const uint32_t g = m_src[i], k = (sq & kTagMask) / s.nchunks;
-        atomicSub(&s.infl[(size_t)g * O + k], 1u);
-        s.failed[g] = 1;
+        const size_t h = chunk_conn(s, m_src[i], m_dst[i], sq & kTagMask);
+        if (h == kNoConn) continue;
+        atomicSub(&s.infl[h], 1u);
+        s.failed[m_src[i]] = 1;
         ++cnt;
       }
     }
@@ -96,16 +111,19 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
     for (uint32_t i = (blockIdx.x - nb) * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
       const uint32_t sq = o_seq[i], tag = sq >> 30;
       if (tag == 1u) {  // a SYN at its listener
-        const size_t h = (size_t)o_src[i] * O + (sq & kTagMask);
-        if (s.state[h] == kWait && s.dst[h] == o_dst[i])
+        const uint32_t k = sq & kTagMask;
+        const size_t h = (size_t)o_src[i] * O + k;
+        if (k < O && h < s.n_conn && s.state[h] == kWait && s.dst[h] == o_dst[i])
           atomicMin(reinterpret_cast<long long*>(&s.t_synarr[h]), (long long)o_t[i]);
       } else if (tag == 3u) {  // a SYN-ACK at its dialler
         const size_t h = sq & kTagMask;
         if (h < s.n_conn && h / O == o_dst[i] && s.dst[h] == o_src[i] && s.state[h] == kWait && (s.flags[h] & 2u))
           atomicMin(reinterpret_cast<long long*>(&s.t_ackarr[h]), (long long)o_t[i]);
       } else if (tag == 2u) {  // a chunk: its first copy frees a buffer slot
-        const uint32_t c = sq & kTagMask, k = c / s.nchunks;
-        const size_t h = (size_t)o_src[i] * O + k;
+        const uint32_t c = sq & kTagMask;
+        const size_t h = chunk_conn(s, o_src[i], o_dst[i], c);
+        if (h == kNoConn) continue;
+        const uint32_t k = c / s.nchunks;
         const uint64_t bit = (uint64_t)h * s.nchunks + (c - k * s.nchunks);
         const uint32_t m = 1u << (bit & 31u);
         if (!(atomicOr(&s.claim[bit >> 5], m) & m)) {
@@ -199,17 +217,29 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l
     if (!resolve || s.state[h] != kWait) continue;
     if (s.tcp) {  // the SYN write: ACKed (connect() returned, seen at the window's end) or failed
       uint8_t out = TGSIM_PROBE_NONE;
+      int64_t te = t_end;
       if (t.c_acked[h] >= 1) {
         out = TGSIM_PROBE_OK;
       } else {
-        const uint32_t ws = tcp_write_state(t, tcp_wid(s, h, 0));
+        const uint32_t w = tcp_wid(s, h, 0);
+        const uint32_t ws = tcp_write_state(t, w);
         out = ws == TGSIM_TCP_TIMEOUT ? TGSIM_PROBE_TIMEOUT : ws == TGSIM_TCP_REFUSED ? TGSIM_PROBE_REFUSED : out;
+        const int64_t dl = s.t_start[h] + s.timeout;
+        if (out == TGSIM_PROBE_NONE && dl < t_end) {  // net.DialTimeout (storm.go:144): the SYN write fails
+          out = TGSIM_PROBE_TIMEOUT;                  // at the deadline, its slot frees then
+          te = dl;
+          atomicMin(reinterpret_cast<long long*>(&t.w_fail[w]), (long long)(dl * 2 + 1));
+          if (atomicCAS(&t.w_state[w], (uint32_t)TGSIM_TCP_PENDING, (uint32_t)TGSIM_TCP_TIMEOUT) == TGSIM_TCP_PENDING) {
+            atomicAdd(&t.sc->done, 1u);
+            atomicAdd(&t.sc->failed, 1ull);
+          }
+        }
       }
       if (out != TGSIM_PROBE_NONE) {
         s.state[h] = kDone;
         s.res[h] = out;
-        s.t_done[h] = t_end;
-        s.slot_t[(size_t)l * C + s.slot[h]] = t_end;
+        s.t_done[h] = te;
+        s.slot_t[(size_t)l * C + s.slot[h]] = te;
       } else {
         ++act;
         ++waiting;

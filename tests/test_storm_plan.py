@@ -183,6 +183,75 @@ def test_storm_protocol_hip(hip):
     _protocol_case(hip)
 
 
+def _foreign_case(b, foreign=True):
+    """messages the host stages beside the reactor with the storm's tags - a SYN to a
+    connection index past `outgoing`, a chunk id past every connection, a chunk not yet written, a
+    chunk whose destination is not its connection's, a SYN-ACK past every connection - are not the
+    storm's: they leave every table in range and every count unchanged (unshaped links, so they
+    take nothing from the storm's packets either). Returns the dial and write results."""
+    n, O = 8, 2
+    s = Simulator(SimConfig(n_instances=n, seed=3), binding=b)
+    src = np.repeat(np.arange(n), O)
+    dst = (src + 1 + np.arange(len(src)) % 3) % n
+    s.storm_setup(dst, np.zeros(len(src), np.int64), outgoing=O, concurrent=1, data_bytes=3 * 4096,
+                  msg_window=1, window_ns=W)
+    nchunks = 3
+
+    def inject():
+        if not foreign:
+            return
+        t = s.horizon
+        g = np.array([0, 1, 2, 3, 4, 5], np.uint32)
+        seq = np.array([A.STORM_SYN | O, A.STORM_DATA | (O * nchunks + 7), A.STORM_DATA | (nchunks - 1),
+                        A.STORM_DATA | 0, A.STORM_SYNACK | (n * O + 3), A.STORM_DATA | 0x3FFFFFFF], np.uint32)
+        d = (g + 1) % n
+        d[3] = (g[3] + 5) % n      # not connection 3.0's destination
+        s.enqueue(g, d, seq, np.full(len(g), 66, np.uint32), np.full(len(g), t, np.int64))
+
+    def run():
+        ne, w = s.now + W, 0
+        while True:
+            s.advance(ne)
+            ne, act = s.storm_react()
+            w += 1
+            if act == 0:
+                return w
+            inject()
+
+    s.storm_start()
+    inject()
+    wd = run()
+    res, t_done = s.storm_dials()
+    s.storm_write_start(s.now)
+    inject()
+    ww = run()
+    failed, t_last, tot = s.storm_results()
+    s.storm_end()
+    s.close()
+    return dict(wd=wd, res=res, t_done=t_done, ww=ww, failed=failed, t_last=t_last, tot=tot)
+
+
+def _assert_foreign_ignored(b):
+    a, ref = _foreign_case(b), _foreign_case(b, foreign=False)
+    assert (a["res"] == A.PROBE_OK).all()
+    for k in ("res", "t_done", "failed", "t_last"):
+        assert np.array_equal(a[k], ref[k]), k
+    assert a["tot"] == ref["tot"] and (a["wd"], a["ww"]) == (ref["wd"], ref["ww"])
+    return a
+
+
+def test_storm_foreign_messages_oracle(oracle):
+    _assert_foreign_ignored(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_foreign_messages_hip(hip, oracle):
+    a, b = _assert_foreign_ignored(hip), _foreign_case(oracle)
+    for k in ("res", "t_done", "failed", "t_last"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["tot"] == b["tot"]
+
+
 def random_run(b, seed, n=60, keep=True):
     """Shaped, lossy, duplicating links, a few blackhole / prohibit rules and a disabled instance:
     dials refused, timed out and OK; then (on a second context, lossless while it dials) the write
@@ -351,6 +420,13 @@ def _tcp_hand_case(b):
     st = s.tcp_stats()
     assert st["writes"] == 8 and st["delivered"] == 8 and st["retransmissions"] == 0
     s.storm_end()
+    # the reactor's connections stay closed to host writes (their queues end where the
+    # reactor left them); a new connection takes writes
+    with pytest.raises(A.TgsimError) as e:
+        s.tcp_write([0], [100], [s.now])
+    assert e.value.code == A.ESTATE
+    (c,) = s.tcp_connect([0], [1])
+    s.tcp_write([c], [100], [s.now])
     s.close()
 
 
@@ -361,6 +437,42 @@ def test_storm_tcp_hand_oracle(oracle):
 @pytest.mark.gpu
 def test_storm_tcp_hand_hip(hip):
     _tcp_hand_case(hip)
+
+
+def _tcp_dial_timeout_case(b):
+    """in TCP mode a dial also ends at net.DialTimeout (storm.go:144), not only when its
+    SYN write gives up (16 attempts from a 20 ms RTO: hours). 3 instances x 2 connections, one dial
+    slot, zero latency, 1 ms windows, DialTimeout 50 ms; instance 1's link drops everything, so its
+    SYNs and its ACKs are lost. 0.0 -> 1 and 1.0 -> 0 time out at 50 ms (seen after the window
+    ending at 51 ms); their second dials start at 51 ms: 0.1 -> 2 is ACKed in [52, 53) ms, OK at
+    53 ms; 1.1 -> 2 times out at 101 ms. 2.0 -> 0 is OK at 2 ms (the hand case's timing), 2.1 -> 1
+    starts at 2 ms and times out at 52 ms. Each timed-out SYN write fails at its deadline."""
+    s = Simulator(SimConfig(n_instances=3, seed=5), binding=b)
+    s.tcp_enable(acks=True, rto_ns=20 * MS, max_attempts=16)
+    s.set_shapes([1], [make_shape(loss=100.0)])
+    s.storm_setup([1, 2, 0, 2, 0, 1], [0] * 6, outgoing=2, concurrent=1, data_bytes=4096,
+                  dial_timeout_ns=50 * MS, window_ns=W)
+    s.storm_start()
+    _, w = drive_tcp(s, keep=False)
+    res, t_done = s.storm_dials()
+    T, OK = A.PROBE_TIMEOUT, A.PROBE_OK
+    assert res.tolist() == [T, OK, T, T, OK, T]
+    assert t_done.tolist() == [50 * MS, 53 * MS, 50 * MS, 101 * MS, 2 * MS, 52 * MS]
+    assert w == 102 and s.now == 102 * MS  # 1.1 resolved after the window ending at 102 ms
+    st = s.tcp_stats()
+    s.storm_end()
+    s.close()
+    return res, t_done, st
+
+
+def test_storm_tcp_dial_timeout_oracle(oracle):
+    _tcp_dial_timeout_case(oracle)
+
+
+@pytest.mark.gpu
+def test_storm_tcp_dial_timeout_hip(hip, oracle):
+    a, b = _tcp_dial_timeout_case(hip), _tcp_dial_timeout_case(oracle)
+    assert a[2] == b[2]
 
 
 def random_tcp_run(b, seed, n=40, keep=True):

@@ -5,5 +5,5 @@
 #  tools/build_variant.sh phase -DTGSIM_PHASE_PROF is the phase-clock build of tools/phase_probe.py)
 set -e
 name=$1; shift
-make -s -B -C "$(dirname "$0")/../testground_amd/csrc" ARCH=gfx950 OUT=../libtgsim_$name.so \
-  CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result $*"
+make -s -j8 -C "$(dirname "$0")/../testground_amd/csrc" ARCH=gfx950 OUT=../libtgsim_$name.so OBJDIR=build_$name \
+  EXTRA="$*"
