@@ -2262,23 +2262,39 @@ struct ostorm {
   int tcp;
   uint32_t W0, S0, spc, spcon;
   uint32_t *settled, *wsegs;
+  /* the listener's side of connection h (its shard is dst[h]'s): SYN answered, the SYN's first
+   * arrival, and the connections answered in this reaction (sharded reactor) */
+  uint8_t* ans;
+  int64_t* lsyn;
+  uint64_t* alist;
+  size_t alist_n;
 };
+/* Notices from the listener's shard to the dialer's (records: t = value, src = connection, seq = kind):
+ * the SYN-ACK the listener staged (value: its send time) and a chunk's arrival (value: chunk j). On
+ * one shard they are applied in place; sharded, they cross in the exchange blocks (tgsim_transport). */
+enum { SMN_SYNACK = 1u, SMN_CHUNK = 2u };
 
 static void sm_free(tgo_ctx* c) {
   ostorm* s = c->sm;
   if (!s) return;
   free(s->conn); free(s->order); free(s->claim); free(s->dq); free(s->qh); free(s->ql); free(s->nh);
   free(s->ring); free(s->hold); free(s->slot_t); free(s->failed); free(s->t_last); free(s->settled); free(s->wsegs);
+  free(s->ans); free(s->lsyn); free(s->alist);
   free(s);
   c->sm = NULL;
   c->sm_need_react = 0;
 }
 
-static const int64_t* g_sm_tr;
-static int cmp_sm_order(const void* a, const void* b) {
-  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
-  if (g_sm_tr[x] != g_sm_tr[y]) return g_sm_tr[x] < g_sm_tr[y] ? -1 : 1;
-  return x < y ? -1 : x > y;
+/* per instance, its connections in (t_ready, k) order: a stable insertion sort (no comparator state
+ * shared between contexts - shards may be set up on several threads at once) */
+static void sm_sort_order(uint32_t* o, const int64_t* tr, uint32_t O) {
+  for (uint32_t k = 0; k < O; ++k) o[k] = k;
+  for (uint32_t i = 1; i < O; ++i) {
+    const uint32_t v = o[i];
+    uint32_t j = i;
+    while (j > 0 && tr[o[j - 1]] > tr[v]) { o[j] = o[j - 1]; --j; }
+    o[j] = v;
+  }
 }
 
 int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, const tgsim_storm_config* cfg) {
@@ -2288,7 +2304,8 @@ int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, con
       (uint64_t)cfg->chunk_bytes + cfg->header_bytes >= 0x80000000ull)
     return fail(c, TGSIM_EINVAL, "bad storm configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
+  if (c->S != 1 && (c->tcp_on || !c->has_tr))
+    return fail(c, TGSIM_ENOTSUP, "a sharded storm reactor needs message mode and a transport");
   if (c->fl_off || c->pr) return fail(c, TGSIM_ESTATE, "the storm reactor runs without a flood graph or probes");
   if (c->tcp_on && (!c->tcp.acks || c->tc_n || c->tw_n))
     return fail(c, TGSIM_ESTATE, "a TCP storm needs acks = 1 and a context without connections or writes yet");
@@ -2323,8 +2340,10 @@ int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, con
   s->dq = (uint32_t*)calloc(nl, 4); s->qh = (uint32_t*)calloc(nl, 4); s->ql = (uint32_t*)calloc(nl, 4);
   s->nh = (uint32_t*)calloc(nl, 4); s->ring = (uint32_t*)calloc(nc, 4); s->hold = (uint32_t*)calloc(nl * Hc, 4);
   s->slot_t = (int64_t*)malloc(nl * C * 8); s->failed = (uint8_t*)calloc(nl, 1); s->t_last = (int64_t*)malloc(nl * 8);
+  s->ans = (uint8_t*)calloc(nc, 1); s->lsyn = (int64_t*)malloc(nc * 8); s->alist = (uint64_t*)malloc(nc * 8);
   if (!s->conn || !s->order || !s->claim || !s->dq || !s->qh || !s->ql || !s->nh || !s->ring || !s->hold ||
-      !s->slot_t || !s->failed || !s->t_last) { sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
+      !s->slot_t || !s->failed || !s->t_last || !s->ans || !s->lsyn || !s->alist) { sm_free(c); return fail(c, TGSIM_ENOMEM, "oom"); }
+  for (size_t i = 0; i < nc; ++i) s->lsyn[i] = SM_NONE;
   for (size_t i = 0; i < nl * C; ++i) s->slot_t[i] = INT64_MIN;
   for (size_t i = 0; i < nl; ++i) s->t_last[i] = INT64_MIN;
   for (uint64_t h = 0; h < n_conn; ++h) {
@@ -2332,12 +2351,7 @@ int tgo_storm_setup(tgo_ctx* c, const uint32_t* dst, const int64_t* t_ready, con
     s->conn[h].t_ready = t_ready[h];
     s->conn[h].t_done = INT64_MIN;
   }
-  for (uint32_t g = 0; g < c->N; ++g) {
-    uint32_t* o = s->order + (size_t)g * O;
-    for (uint32_t k = 0; k < O; ++k) o[k] = k;
-    g_sm_tr = t_ready + (size_t)g * O;
-    qsort(o, O, 4, cmp_sm_order);
-  }
+  for (uint32_t g = 0; g < c->N; ++g) sm_sort_order(s->order + (size_t)g * O, t_ready + (size_t)g * O, O);
   s->cfg = *cfg; s->O = O; s->C = C; s->nchunks = (uint32_t)nchunks; s->n_conn = n_conn; s->phase = 0;
   if (c->tcp_on) {  /* the connections, then the reserved writes and segments as tgo_tcp_write builds them */
     uint32_t* src = (uint32_t*)malloc(nc * 4);
@@ -2405,7 +2419,7 @@ static int sm_failed_code(uint8_t st) {
 static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_end, pbuf* b, int64_t* dl_min,
                      int64_t* ns_min, uint32_t* act, uint32_t* waiting) {
   ostorm* s = c->sm;
-  const uint32_t O = s->O, C = s->C;
+  const uint32_t O = s->O, C = s->C, l = g - c->lo;
   const int64_t timeout = s->cfg.dial_timeout_ns;
   ostorm_conn* cn = s->conn + (size_t)g * O;
   for (uint32_t k = 0; k < O && resolve; ++k) {
@@ -2425,21 +2439,17 @@ static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_e
       }
       if (out != TGSIM_PROBE_NONE) {
         x->state = SM_DONE; x->res = out; x->t_done = te;
-        s->slot_t[(size_t)g * C + x->slot] = te;
+        s->slot_t[(size_t)l * C + x->slot] = te;
       } else {
         ++*act; ++*waiting;
       }
       continue;
     }
     const int64_t dl = x->t_start + timeout;
-    int reply_pending = 0;
-    if (x->t_synarr != SM_NONE && !(x->flags & 2u)) {  /* the listener answers the SYN's first arrival */
-      const int64_t trep = x->t_synarr > H ? x->t_synarr : H;
-      pr_stage(b, x->dst, g, TGSIM_STORM_SYNACK | (uint32_t)((size_t)g * O + k), s->cfg.syn_bytes, trep);
-      x->flags |= 2u;
-      reply_pending = trep < dl;
-    }
-    x->t_synarr = SM_NONE;
+    /* the listener answered the SYN's first arrival in this reaction (its notice): the SYN-ACK may
+     * still beat the deadline, so a timeout waits one more window */
+    const int reply_pending = (x->flags & 8u) && x->t_rep < dl;
+    x->flags &= ~8u;
     uint8_t out = TGSIM_PROBE_NONE;
     int64_t te = 0;
     if (x->flags & 1u) { out = TGSIM_PROBE_REFUSED; te = x->t_start; }
@@ -2447,19 +2457,19 @@ static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_e
     else if (dl < t_end && !reply_pending) { out = TGSIM_PROBE_TIMEOUT; te = dl; }
     if (out != TGSIM_PROBE_NONE) {
       x->state = SM_DONE; x->res = out; x->t_done = te;
-      s->slot_t[(size_t)g * C + x->slot] = te;
+      s->slot_t[(size_t)l * C + x->slot] = te;
     } else {
       ++*act; ++*waiting;
       if (dl < *dl_min) *dl_min = dl;
     }
   }
   if (s->tcp && t_end > H) H = t_end;  /* TCP: the reaction saw the previous dial end at the window's end */
-  uint32_t q = s->dq[g];
+  uint32_t q = s->dq[l];
   while (q < O) {
     uint32_t best = C;
     int64_t bt = SM_BUSY;
     for (uint32_t j = 0; j < C; ++j)
-      if (s->slot_t[(size_t)g * C + j] < bt) { bt = s->slot_t[(size_t)g * C + j]; best = j; }
+      if (s->slot_t[(size_t)l * C + j] < bt) { bt = s->slot_t[(size_t)l * C + j]; best = j; }
     if (best == C) break;
     const uint32_t k = s->order[(size_t)g * O + q];
     ostorm_conn* x = &cn[k];
@@ -2467,7 +2477,7 @@ static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_e
     if (bt > t0) t0 = bt;
     if (H > t0) t0 = H;
     if (t0 >= t_end + s->cfg.window_ns) { if (t0 < *ns_min) *ns_min = t0; break; }
-    s->slot_t[(size_t)g * C + best] = SM_BUSY;
+    s->slot_t[(size_t)l * C + best] = SM_BUSY;
     x->slot = best; x->state = SM_WAIT; x->t_start = t0; x->flags = 0;
     ++*act; ++*waiting;
     ++q;
@@ -2477,11 +2487,11 @@ static void sm_dials(tgo_ctx* c, uint32_t g, int resolve, int64_t H, int64_t t_e
       s->wsegs[h] = 1;
       continue;
     }
-    x->t_synarr = x->t_ackarr = SM_NONE;
+    x->t_ackarr = SM_NONE;
     pr_stage(b, g, x->dst, TGSIM_STORM_SYN | k, s->cfg.syn_bytes, t0);
     if (t0 + timeout < *dl_min) *dl_min = t0 + timeout;
   }
-  s->dq[g] = q;
+  s->dq[l] = q;
   *act += O - q;
 }
 
@@ -2520,11 +2530,11 @@ static int sm_room(tgo_ctx* c, const ostorm* s, uint64_t h, uint32_t wrote_now) 
 /* Write phase of instance g at t: one writesem round (storm.go:158-183). */
 static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act) {
   ostorm* s = c->sm;
-  const uint32_t O = s->O, C = s->C, Hc = C < O ? C : O, win = s->cfg.msg_window;
+  const uint32_t O = s->O, C = s->C, Hc = C < O ? C : O, win = s->cfg.msg_window, l = g - c->lo;
   ostorm_conn* cn = s->conn + (size_t)g * O;
   uint32_t* ring = s->ring + (size_t)g * O;
-  uint32_t* hold = s->hold + (size_t)g * Hc;
-  uint32_t qh = s->qh[g], ql = s->ql[g], nh = s->nh[g], wrote = 0;
+  uint32_t* hold = s->hold + (size_t)l * Hc;
+  uint32_t qh = s->qh[l], ql = s->ql[l], nh = s->nh[l], wrote = 0;
   uint8_t now_[1024];  /* TCP: connections written in this round (one chunk per reaction) */
   uint8_t* now = O <= sizeof(now_) ? now_ : (uint8_t*)malloc(O);
   memset(now, 0, O);
@@ -2537,7 +2547,7 @@ static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act)
         const uint32_t st = c->tw[sm_wid(s, h, 1 + s->settled[h])].state;
         if (st == TGSIM_TCP_PENDING) break;
         if (st == TGSIM_TCP_DELIVERED) s->delivered++;
-        else { s->failed_chunks++; s->failed[g] = 1; }
+        else { s->failed_chunks++; s->failed[l] = 1; }
         s->settled[h]++;
       }
     }
@@ -2567,8 +2577,8 @@ static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act)
       }
     }
   }
-  s->qh[g] = qh; s->ql[g] = ql; s->nh[g] = nh;
-  if (wrote) s->t_last[g] = t;
+  s->qh[l] = qh; s->ql[l] = ql; s->nh[l] = nh;
+  if (wrote) s->t_last[l] = t;
   for (uint32_t k = 0; k < O; ++k) {
     const uint64_t h = (uint64_t)g * O + k;
     *act += (cn[k].rem || (s->tcp ? s->settled[h] < s->nchunks - cn[k].rem : cn[k].infl != 0)) ? 1u : 0u;
@@ -2577,14 +2587,18 @@ static void sm_writes(tgo_ctx* c, uint32_t g, int64_t t, pbuf* b, uint32_t* act)
 }
 
 /* one reaction frame (H, t_end): every instance's step, then the proposal of the next window's end */
-static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* next_end, uint32_t* n_active) {
+/* one reaction frame (H, t_end): every local instance's step, then the proposal of the next window's
+ * end. propose: sharded, the proposal is collective (every shard's busy flag, active count and
+ * earliest deadline / dial start gathered over the transport; the one-shard rule over the whole). */
+static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* next_end, uint32_t* n_active,
+                   int propose) {
   ostorm* s = c->sm;
   pbuf b;
   const size_t cap = s->phase ? (size_t)s->n_conn * s->cfg.msg_window + 1 : 2 * (size_t)s->n_conn + 1;
   if (pr_alloc(&b, cap)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
   int64_t dl = SM_NONE, ns = SM_NONE;
   uint32_t act = 0, waiting = 0;
-  for (uint32_t g = 0; g < c->N; ++g) {
+  for (uint32_t g = c->lo; g < c->hi; ++g) {
     if (s->phase) sm_writes(c, g, t_end, &b, &act);
     else sm_dials(c, g, resolve, H, t_end, &b, &dl, &ns, &act, &waiting);
   }
@@ -2601,14 +2615,29 @@ static int sm_step(tgo_ctx* c, int resolve, int64_t H, int64_t t_end, int64_t* n
     const int rc2 = ostage_flush(c, &q);
     if (rc || rc2) return rc ? fail(c, rc, "oom") : rc2;
   }
-  int64_t ne = t_end + s->cfg.window_ns;
-  if (!staged_before && !c->heap.n && act && (!s->tcp || !waiting)) {  /* idle: jump to the next deadline or dial */
-    int64_t cand = dl != SM_NONE ? dl + 1 : SM_NONE;
-    if (ns < cand) cand = ns;
-    if (cand != SM_NONE && cand > ne) ne = cand;
+  int64_t cand = dl != SM_NONE ? dl + 1 : SM_NONE;
+  if (ns < cand) cand = ns;
+  int64_t busy = staged_before || c->heap.n || (s->tcp && waiting), tot = act;
+  if (propose && c->S > 1) {
+    int64_t mine[3] = {busy, (int64_t)act, cand};
+    int64_t* all = (int64_t*)malloc((size_t)c->S * 3 * 8);
+    if (!all) return fail(c, TGSIM_ENOMEM, "oom");
+    if (c->tr.allgather(c->tr.user, mine, all, sizeof(mine), NULL) != 0) {
+      free(all);
+      return fail(c, TGSIM_EHIP, "transport all-gather failed");
+    }
+    busy = 0; tot = 0; cand = SM_NONE;
+    for (uint32_t k = 0; k < c->S; ++k) {
+      busy |= all[3 * k];
+      tot += all[3 * k + 1];
+      if (all[3 * k + 2] < cand) cand = all[3 * k + 2];
+    }
+    free(all);
   }
+  int64_t ne = t_end + s->cfg.window_ns;
+  if (!busy && tot && cand != SM_NONE && cand > ne) ne = cand;  /* idle: jump to the next deadline or dial */
   if (next_end) *next_end = ne;
-  if (n_active) *n_active = act;
+  if (n_active) *n_active = (uint32_t)tot;
   return TGSIM_OK;
 }
 
@@ -2617,11 +2646,12 @@ int tgo_storm_start(tgo_ctx* c) {
   if (c->sm->phase != 0) return fail(c, TGSIM_ESTATE, "the storm's dials have started");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (react_owed(c)) return TGSIM_ESTATE;
-  return sm_step(c, 0, c->now, c->now, NULL, NULL);
+  return sm_step(c, 0, c->now, c->now, NULL, NULL, 0);
 }
 
-/* The connection of a chunk packet (src -> dst, chunk id cj = k * nchunks + j), or -1 when no chunk
- * the storm has written matches it (a message the host staged beside the reactor: ADVICE r4) */
+/* The connection of a chunk packet (src -> dst, chunk id cj = k * nchunks + j) on its dialer's shard,
+ * or -1 when no chunk the storm has written matches it (a message the host staged beside the
+ * reactor: ADVICE r4). */
 static int64_t sm_chunk_conn(const ostorm* s, uint32_t src, uint32_t dst, uint32_t cj) {
   if (s->nchunks == 0) return -1;
   const uint32_t k = cj / s->nchunks, j = cj - k * s->nchunks;
@@ -2630,17 +2660,68 @@ static int64_t sm_chunk_conn(const ostorm* s, uint32_t src, uint32_t dst, uint32
   return (int64_t)h;
 }
 
-int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+/* A notice on the dialer's shard: the SYN-ACK its listener staged (sent at v), or the arrival of
+ * chunk j = v (the first copy of a written chunk frees its buffer slot) */
+static void sm_notice_apply(tgo_ctx* c, uint64_t h, uint32_t kind, int64_t v) {
+  ostorm* s = c->sm;
+  if (h >= s->n_conn) return;
+  ostorm_conn* x = &s->conn[h];
+  if (kind == SMN_SYNACK) {
+    x->flags |= 2u | 8u;
+    x->t_rep = v;
+  } else if (kind == SMN_CHUNK) {
+    const int64_t hh = sm_chunk_conn(s, (uint32_t)(h / s->O), x->dst, (uint32_t)((h % s->O) * s->nchunks + v));
+    if (hh < 0 || v < 0 || (uint64_t)v >= s->nchunks) return;
+    const uint64_t bit = h * s->nchunks + (uint64_t)v;
+    if (!s->claim[bit]) { s->claim[bit] = 1; x->infl--; s->delivered++; }
+  }
+}
+static int sm_notice(tgo_ctx* c, uint64_t h, uint32_t kind, int64_t v) {
+  const uint32_t p = shard_of(c, (uint32_t)(h / c->sm->O));
+  if (p == c->cfg.shard_id) { sm_notice_apply(c, h, kind, v); return TGSIM_OK; }
+  tgsim_record r;
+  memset(&r, 0, sizeof(r));
+  r.t = v; r.src = (uint32_t)h; r.seq = kind;
+  return recs_push(&c->outbox[p], &r) ? fail(c, TGSIM_ENOMEM, "oom") : TGSIM_OK;
+}
+
+/* Sharded: the notices cross in the exchange blocks (peer-major, header .t = count), then apply */
+static int sm_notice_exchange(tgo_ctx* c) {
+  memset(c->xsend, 0, (size_t)c->S * c->xcap * sizeof(tgsim_record));
+  for (uint32_t p = 0; p < c->S; ++p) {
+    orecs* o = &c->outbox[p];
+    if (p == c->cfg.shard_id) continue;
+    if (o->n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "storm notices exceed the exchange capacity (%zu to peer %u)", o->n, p);
+    c->xsend[(size_t)p * c->xcap].t = (int64_t)o->n;
+    memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
+    o->n = 0;
+  }
+  if (c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-to-all failed");
+  for (uint32_t p = 0; p < c->S; ++p) {
+    if (p == c->cfg.shard_id) continue;
+    const tgsim_record* blk = &c->xrecv[(size_t)p * c->xcap];
+    const size_t n = (size_t)blk[0].t;
+    if (n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "corrupt exchange header");
+    for (size_t i = 0; i < n; ++i) sm_notice_apply(c, blk[1 + i].src, blk[1 + i].seq, blk[1 + i].t);
+  }
+  return TGSIM_OK;
+}
+
+static int storm_react_impl(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   ostorm* s = c->sm;
   if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->sm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react before storm_react");
+  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "the transport was aborted (a shard failed)");
   c->sm_need_react = 0;
-  if (s->tcp) return sm_step(c, 1, c->horizon, c->now, next_end, n_active);  /* the TCP reaction settled the window */
+  if (s->tcp) return sm_step(c, 1, c->horizon, c->now, next_end, n_active, 1);  /* the TCP reaction settled the window */
   const omsgs* st = &c->staged;
   const uint32_t O = s->O;
-  /* 1. the window's packets: refused SYNs, chunks no copy of entered the egress queue */
+  int rc = TGSIM_OK;
+  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
+  /* 1. the window's packets (local dialers): refused SYNs, chunks no copy of entered the egress queue */
   for (size_t i = 0; i < c->n_status; ++i) {
     const uint32_t sq = st->seq[i], tag = sq >> 30, code = c->status[i] & 0x0Fu;
     if (tag == 1u) {
@@ -2654,45 +2735,67 @@ int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
       const int64_t h = sm_chunk_conn(s, st->src[i], st->dst[i], sq & PR_MASK);
       if (h < 0) continue;
       s->conn[h].infl--;
-      s->failed[st->src[i]] = 1;
+      s->failed[st->src[i] - c->lo] = 1;
       s->failed_chunks++;
     }
   }
-  /* 2. the window's deliveries: first arrivals of SYNs and SYN-ACKs, the first copy of each chunk */
-  for (size_t i = 0; i < c->out.n; ++i) {
+  /* 2. the window's deliveries (local receivers): a SYN at its listener (first arrival of the
+   *    connection's SYN: answered in this reaction), a SYN-ACK at its dialer, a chunk at its listener
+   *    (the dialer's shard claims its first copy) */
+  s->alist_n = 0;
+  for (size_t i = 0; i < c->out.n && !rc; ++i) {
     const tgsim_record* r = &c->out.v[i];
     const uint32_t tag = r->seq >> 30;
     if (tag == 1u) {
-      const size_t h = (size_t)r->src * O + (r->seq & PR_MASK);
-      if ((r->seq & PR_MASK) >= O || h >= s->n_conn) continue;
-      ostorm_conn* x = &s->conn[h];
-      if (x->state == SM_WAIT && x->dst == r->dst && r->t < x->t_synarr) x->t_synarr = r->t;
+      const uint64_t h = (uint64_t)r->src * O + (r->seq & PR_MASK);
+      if ((r->seq & PR_MASK) >= O || h >= s->n_conn || s->conn[h].dst != r->dst || s->ans[h] == 1) continue;
+      if (s->ans[h] == 0) { s->ans[h] = 2; s->alist[s->alist_n++] = h; }  /* 2: answered in this reaction */
+      if (r->t < s->lsyn[h]) s->lsyn[h] = r->t;
     } else if (tag == 3u) {
       const size_t h = r->seq & PR_MASK;
       if (h < s->n_conn && h / O == r->dst) {
         ostorm_conn* x = &s->conn[h];
-        if (x->dst == r->src && x->state == SM_WAIT && (x->flags & 2u) && r->t < x->t_ackarr) x->t_ackarr = r->t;
+        if (x->dst == r->src && x->state == SM_WAIT && r->t < x->t_ackarr) x->t_ackarr = r->t;
       }
-    } else if (tag == 2u) {
-      const uint32_t cj = r->seq & PR_MASK;
-      const int64_t h = sm_chunk_conn(s, r->src, r->dst, cj);
-      if (h < 0) continue;
-      const uint32_t k = cj / s->nchunks;
-      const uint64_t bit = (uint64_t)h * s->nchunks + (cj - k * s->nchunks);
-      if (!s->claim[bit]) { s->claim[bit] = 1; s->conn[h].infl--; s->delivered++; }
+    } else if (tag == 2u && s->nchunks) {
+      const uint32_t cj = r->seq & PR_MASK, k = cj / s->nchunks;
+      const uint64_t h = (uint64_t)r->src * O + k;
+      if (k >= O || h >= s->n_conn || s->conn[h].dst != r->dst) continue;
+      rc = sm_notice(c, h, SMN_CHUNK, cj - k * s->nchunks);
     }
   }
-  /* 3. per instance: dials or writes, then the proposal */
-  return sm_step(c, 1, c->horizon, c->now, next_end, n_active);
+  /* 3. the listeners answer: a SYN-ACK at max(first arrival, horizon) per connection answered now */
+  pbuf b;
+  if (!rc && pr_alloc(&b, s->alist_n + 1)) { pr_free(&b); rc = fail(c, TGSIM_ENOMEM, "oom"); }
+  if (rc) return rc;
+  for (size_t i = 0; i < s->alist_n && !rc; ++i) {
+    const uint64_t h = s->alist[i];
+    const int64_t trep = s->lsyn[h] > c->horizon ? s->lsyn[h] : c->horizon;
+    s->ans[h] = 1;
+    pr_stage(&b, s->conn[h].dst, (uint32_t)(h / O), TGSIM_STORM_SYNACK | (uint32_t)h, s->cfg.syn_bytes, trep);
+    rc = sm_notice(c, h, SMN_SYNACK, trep);
+  }
+  if (rc) { pr_free(&b); return rc; }
+  rc = pr_flush(c, &b);
+  if (rc) return rc;
+  /* 4. sharded: the notices to the dialers' shards */
+  if (c->S > 1 && (rc = sm_notice_exchange(c))) return rc;
+  /* 5. per local instance: dials or writes, then the proposal */
+  return sm_step(c, 1, c->horizon, c->now, next_end, n_active, 1);
+}
+int tgo_storm_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  return shard_failed(c, storm_react_impl(c, next_end, n_active));
 }
 
+/* the local instances' connections: [lo * O, hi * O) */
 int tgo_storm_dials(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
   ostorm* s = c->sm;
   if (!s) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  if ((outcome || t_done) && cap < s->n_conn) return fail(c, TGSIM_ECAPACITY, "dial capacity");
-  for (uint64_t h = 0; h < s->n_conn; ++h) {
-    if (outcome) outcome[h] = s->conn[h].res;
-    if (t_done) t_done[h] = s->conn[h].t_done;
+  const uint64_t h0 = (uint64_t)c->lo * s->O, n = (uint64_t)c->nloc * s->O;
+  if ((outcome || t_done) && cap < n) return fail(c, TGSIM_ECAPACITY, "dial capacity");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (outcome) outcome[i] = s->conn[h0 + i].res;
+    if (t_done) t_done[i] = s->conn[h0 + i].t_done;
   }
   return TGSIM_OK;
 }
@@ -2704,19 +2807,26 @@ int tgo_storm_write_start(tgo_ctx* c, int64_t t0) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (react_owed(c)) return TGSIM_ESTATE;
   if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
-  for (uint64_t h = 0; h < s->n_conn; ++h)
-    if (s->conn[h].res != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %llu has not dialled successfully", (unsigned long long)h);
+  /* storm.go:156: every dial of every instance OK (sharded: agreed over the transport) */
+  int64_t bad = -1;
+  for (uint64_t h = (uint64_t)c->lo * s->O; h < (uint64_t)c->hi * s->O && bad < 0; ++h)
+    if (s->conn[h].res != TGSIM_PROBE_OK) bad = (int64_t)h;
+  if (c->S > 1) {
+    if (!c->has_tr) return fail(c, TGSIM_ESTATE, "the transport was aborted (a shard failed)");
+    if (c->tr.allreduce_max_i64(c->tr.user, &bad, 1, NULL) != 0) return shard_failed(c, fail(c, TGSIM_EHIP, "transport all-reduce failed"));
+  }
+  if (bad >= 0) return fail(c, TGSIM_ESTATE, "connection %lld has not dialled successfully", (long long)bad);
   s->phase = 1;
-  for (uint32_t g = 0; g < c->N; ++g) {
+  for (uint32_t g = c->lo; g < c->hi; ++g) {
     uint32_t n = 0;
     for (uint32_t k = 0; k < s->O; ++k) {
       ostorm_conn* x = &s->conn[(size_t)g * s->O + k];
       x->rem = s->nchunks; x->infl = 0;
       if (s->nchunks) s->ring[(size_t)g * s->O + n++] = k;
     }
-    s->qh[g] = 0; s->ql[g] = n; s->nh[g] = 0;
+    s->qh[g - c->lo] = 0; s->ql[g - c->lo] = n; s->nh[g - c->lo] = 0;
   }
-  return sm_step(c, 0, t0, t0, NULL, NULL);
+  return sm_step(c, 0, t0, t0, NULL, NULL, 0);
 }
 
 int tgo_storm_results(tgo_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, tgsim_storm_totals* tot) {
@@ -2726,7 +2836,7 @@ int tgo_storm_results(tgo_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, 
   for (uint32_t g = 0; g < c->nloc; ++g) {
     uint8_t f = s->failed[g];
     for (uint32_t k = 0; k < s->O; ++k) {
-      const uint64_t h = (uint64_t)g * s->O + k;
+      const uint64_t h = (uint64_t)(c->lo + g) * s->O + k;
       const ostorm_conn* x = &s->conn[h];
       f |= (s->phase == 1 && x->rem) ? 1 : 0;
       f |= (s->tcp ? (s->phase == 1 && s->settled[h] < s->nchunks - x->rem) : x->infl != 0) ? 1 : 0;
@@ -2738,7 +2848,7 @@ int tgo_storm_results(tgo_ctx* c, uint8_t* failed, int64_t* t_last, size_t cap, 
     memset(tot, 0, sizeof(*tot));
     tot->chunks_written = s->written; tot->chunks_delivered = s->delivered;
     tot->chunks_failed = s->failed_chunks; tot->bytes_written = s->bytes;
-    for (uint64_t h = 0; h < s->n_conn; ++h) {
+    for (uint64_t h = (uint64_t)c->lo * s->O; h < (uint64_t)c->hi * s->O; ++h) {  /* the local connections */
       const ostorm_conn* x = &s->conn[h];
       tot->dials_ok += x->res == TGSIM_PROBE_OK;
       tot->dials_failed += x->res == TGSIM_PROBE_REFUSED || x->res == TGSIM_PROBE_TIMEOUT;

@@ -154,6 +154,9 @@ struct StormScalars {
   uint32_t done, waiting;         // k_storm_step workgroups finished (the last proposes the window end);
                                   // dials holding a semaphore slot
   unsigned long long written, delivered, failed, bytes;  // chunks (cumulative)
+  uint32_t n_ans, pad_ans;        // connections whose SYN the local listeners answer in this reaction
+  int64_t prop[3];                // this shard's proposal inputs: busy, active connections, earliest deadline
+                                  // + 1 / dial start (sharded: gathered, then reduced by k_storm_prop)
 };
 struct StormDev {
   uint32_t O = 0, C = 0, Hc = 0;  // connections per instance, semaphore width, holder capacity min(C, O)
@@ -171,7 +174,8 @@ struct StormDev {
   uint32_t* dst = nullptr;
   int64_t* t_ready = nullptr;
   uint8_t* state = nullptr;       // sleeping / waiting / done (dial) - kept through the write phase
-  uint8_t* flags = nullptr;       // bit 0 refused, bit 1 the peer answered the SYN
+  uint8_t* flags = nullptr;       // bit 0 refused, bit 1 the peer answered the SYN, bit 3 it did in this
+                                  // reaction (the listener's notice: t_rep is the SYN-ACK's send time)
   uint8_t* res = nullptr;         // TGSIM_PROBE_* dial outcome
   uint32_t* slot = nullptr;       // the dial semaphore slot a waiting dial holds
   int64_t *t_start = nullptr, *t_synarr = nullptr, *t_ackarr = nullptr, *t_done = nullptr, *t_rep = nullptr;
@@ -180,7 +184,17 @@ struct StormDev {
   uint32_t* infl = nullptr;       // chunks in the send buffer (neither arrived nor failed)
   uint32_t* order = nullptr;      // per instance its connections k in dial FIFO order (t_ready, k)
   uint32_t* ring = nullptr;       // per instance the writesem FIFO (O entries, a ring)
-  uint32_t* claim = nullptr;      // bit per chunk (h * nchunks + j): first arrival seen
+  uint32_t* claim = nullptr;      // bit per chunk (h * nchunks + j): first arrival seen (dialer's shard)
+  // the listener's side of connection h (on dst[h]'s shard): t_synarr = the SYN's first arrival;
+  // ans[h] 0 / 2 (first arrival in this reaction, listed in alist) / 1 (answered)
+  uint32_t* ans = nullptr;
+  uint32_t* alist = nullptr;
+  // sharding: local instances [lo, lo + nloc) of N on shard `shard` of S; notices to a
+  // dialer's shard go into the exchange blocks (cursor of peer p at xq[p << 5])
+  uint32_t lo = 0, N = 0, S = 1, shard = 0, xcap = 0;
+  uint32_t* xq = nullptr;
+  tgsim_record *xsend = nullptr, *xrecv = nullptr;
+  int64_t* prop_all = nullptr;    // [S * 3] the shards' proposal inputs (all-gathered)
   // [nloc]
   uint32_t *dq = nullptr, *qh = nullptr, *ql = nullptr, *nh = nullptr;
   int64_t* slot_t = nullptr;      // [nloc * C] time each semaphore slot fell free (kBusy: held)
@@ -259,7 +273,8 @@ struct Dev {
 
   // sort scratch
   uint32_t *keys0 = nullptr, *keys1 = nullptr, *vals0 = nullptr, *vals1 = nullptr;
-  uint32_t* hist = nullptr;       // [kMaxBins * kRadixBlocks]
+  uint32_t* hist = nullptr;       // [kRadixBlocks * kMaxBins] per-partition-block histogram rows
+  uint32_t* histx = nullptr;      // [kMaxBins * kRadixBlocks] per bin the blocks' exclusive offsets
   uint2* kv1 = nullptr;           // k_bkt_local output: (key, physical index) per item
   uint32_t* poff = nullptr;       // [kRadixBlocks * (kMaxBins + 1)] per-block bucket offsets (k_bkt_local)
   uint32_t* keys2 = nullptr;      // oversized fused buckets: contiguous copy for the global path
@@ -433,6 +448,13 @@ hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_
 // and deliveries, then per instance its dials / writes (staged behind sc->n_msgs_dev, set from
 // base_host unless base_dev) and the next window's proposed end (StormScalars::next_end).
 hipError_t launch_storm_start(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, int64_t t_now);
+// Message mode, in three parts around the collectives of a sharded run: _pre (packets, deliveries, the
+// listeners' answers, notices into the exchange blocks), the notice exchange (runtime, S > 1), _post
+// (notices applied, the step); then, S > 1, the proposal all-gather (runtime) and launch_storm_prop.
+hipError_t launch_storm_react_pre(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                                  const uint32_t* n_status_dev);
+hipError_t launch_storm_react_post(Dev& d, const TcpDev& td);
+hipError_t launch_storm_prop(Dev& d);
 hipError_t launch_storm_react(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev);
 // the write phase: every connection queued on its instance's writesem, first round at t0

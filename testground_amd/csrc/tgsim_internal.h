@@ -214,6 +214,38 @@ __device__ inline void fence_acquire_agent() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
 }
+// A workgroup publishes its stores through a counter one lane updates (MI355X_MICROARCH.md
+// § visibility, valid producer form): every storing wave waits for its stores, the barrier, then ONE
+// agent-scope release by the counting lane and a second wait (ROCm 7.2 can drop the fence's own),
+// then that lane's atomic. One L2 write-back per workgroup instead of one per wave, and correct by
+// the model: the release covers the other waves' stores because they completed before the barrier
+// (VERDICT r4 item 9). Call from every thread; returns true on the counting lane (thread 0).
+__device__ inline bool block_release_for_count() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+#ifdef TGSIM_FULL_FENCE
+  __threadfence();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return true;
+}
+// The consumer side: the polling lane (thread 0) has seen the count; ONE agent-scope acquire drops
+// this CU's stale lines, its wait holds the barrier until the invalidate is done, then every wave
+// loads. Call from every thread.
+__device__ inline void block_acquire_after_poll() {
+  if (threadIdx.x == 0) {
+#ifdef TGSIM_FULL_FENCE
+    __threadfence();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ inline uint32_t mask_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -862,35 +862,18 @@ __device__ void region_alloc(DevScalars* sc, RegionDev* regions, uint64_t cap_ar
 // per digit to scan its per-block counts, wave64 ballot ranking in the scatter (stable).
 // ============================================================================================
 
-__device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_t& end) {
+// Bijection of [0, n): block i -> the (i / 8)-th item of XCD i % 8's contiguous share.
+__device__ __forceinline__ uint32_t xcd_major(uint32_t i, uint32_t n) {
+  const uint32_t q = n >> 3, r = n & 7u, x = i & 7u;
+  return x * q + (x < r ? x : r) + (i >> 3);
+}
+
+__device__ __forceinline__ void radix_range(uint32_t n, uint32_t& start, uint32_t& end, uint32_t bid) {
   uint32_t chunk = (n + kRadixBlocks - 1) / kRadixBlocks;
   chunk = (chunk + kBlock - 1) & ~(uint32_t)(kBlock - 1);
-  start = blockIdx.x * chunk;
+  start = bid * chunk;
   if (start > n) start = n;
   end = min(start + chunk, n);
-}
-
-// one block per digit: exclusive scan of that digit's per-block counts, digit total to tot[d]
-__device__ __forceinline__ void radix_rows_body(uint32_t* hist, uint32_t* tot, uint32_t d) {
-  __shared__ uint32_t ws[kRadixBlocks / 64];
-  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint32_t v = hist[d * kRadixBlocks + t];
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if ((int)lane >= o) x += y;
-  }
-  if (lane == 63) ws[wave] = x;
-  __syncthreads();
-  uint32_t pre = 0;
-  for (uint32_t w = 0; w < wave; ++w) pre += ws[w];
-  hist[d * kRadixBlocks + t] = pre + x - v;
-  if (t == kRadixBlocks - 1) tot[d] = pre + x;
-}
-
-__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(uint32_t* hist, uint32_t* tot) {
-  radix_rows_body(hist, tot, blockIdx.x);
 }
 
 __global__ __launch_bounds__(kBlock) void k_keys_sig(const uint32_t* states, const uint32_t* n_ptr, uint32_t kmin,
@@ -949,11 +932,11 @@ static_assert(kRadixBlocks == 4 * kNSub, "partition blocks map onto sub-queue qu
 // bid: the partition block (blockIdx.x unless the pass shares its launch; queue mode only then)
 __device__ __forceinline__ void bkt_block_range(const BktSrc& s, uint32_t& start, uint32_t& end,
                                                 uint32_t bid = 0xFFFFFFFFu) {
+  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
   if (s.mode == 3) {
-    radix_range(clamp_n(s.n_ptr, s.cap), start, end);
+    radix_range(clamp_n(s.n_ptr, s.cap), start, end, bid);
     return;
   }
-  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
   const uint32_t sub = bid >> 2, part = bid & 3;
   uint32_t c = s.qc[((uint32_t)s.q * kNSub + sub) << 5];
   c = c < s.subcap ? c : s.subcap;
@@ -985,6 +968,7 @@ __device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc,
   __syncthreads();
   uint32_t start, end;
   bkt_block_range(src, start, end, bid);
+  if (start == end) return;  // the scans read no row of an empty block (radix_rows_body)
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll];
 #pragma unroll
@@ -997,7 +981,8 @@ __device__ __forceinline__ void bkt_hist_body(const BktSrc& src, DevScalars* sc,
       if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[bd.of(k[u])], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < B; d += kBlock) hist[d * kRadixBlocks + bid] = h[d];
+  uint32_t* row = hist + (size_t)bid * B;
+  for (uint32_t d = threadIdx.x; d < B; d += kBlock) row[d] = h[d];
 }
 
 __global__ __launch_bounds__(kBlock) void k_bkt_hist(BktSrc src, DevScalars* sc, BktDiv bd, uint32_t B,
@@ -1012,6 +997,47 @@ __device__ __forceinline__ void bkt_range_of(const BktSrc& s, uint32_t p, uint32
   c = c < s.subcap ? c : s.subcap;
   start = sub * s.subcap + (uint32_t)(((uint64_t)c * part) >> 2);
   end = sub * s.subcap + (uint32_t)(((uint64_t)c * (part + 1)) >> 2);
+}
+
+// Partition block p's element range is non-empty.
+__device__ __forceinline__ bool bkt_block_nonempty(const BktSrc& s, uint32_t p) {
+  uint32_t a, e;
+  bkt_block_range(s, a, e, p);
+  return a < e;
+}
+
+// Per-block histograms are rows, hist[block * B + bin] (a partition block writes its own row, whole
+// lines, and only when its element range is non-empty); the scan of bin d reads that column from the
+// non-empty blocks only and writes the exclusive per-block offsets as row d of histx[bin *
+// kRadixBlocks + block], only when the bin has items (nothing reads the offsets of an empty bin).
+// Round 4 wrote every block's counts into [bin][block] columns, 4 B per line from blocks on eight
+// XCDs: 8.9 MB of partial-line write-back per splitbrain window for a nearly empty wheel batch
+// (VERDICT r4 item 4). bid / nbid: the scan's block index and count; bins go to XCDs in contiguous
+// runs, so a line of the rows is read by one XCD.
+__device__ __forceinline__ void radix_rows_body(const BktSrc& src, const uint32_t* hist, uint32_t* histx, uint32_t* tot,
+                                                uint32_t B, uint32_t bid, uint32_t nbid) {
+  __shared__ uint32_t ws[kRadixBlocks / 64];
+  const uint32_t d = xcd_major(bid, nbid);
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t v = bkt_block_nonempty(src, t) ? hist[(size_t)t * B + d] : 0u;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kRadixBlocks / 64; ++w) { pre += w < wave ? ws[w] : 0u; all += ws[w]; }
+  if (all) histx[(size_t)d * kRadixBlocks + t] = pre + x - v;
+  if (t == kRadixBlocks - 1) tot[d] = all;
+}
+
+__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(BktSrc src, const uint32_t* hist, uint32_t* histx,
+                                                             uint32_t* tot, uint32_t B) {
+  radix_rows_body(src, hist, histx, tot, B, blockIdx.x, gridDim.x);
 }
 
 // One-kernel partition for the fused consumers (queue sources only): each block counting-sorts
@@ -1033,6 +1059,7 @@ __device__ __forceinline__ void bkt_local_body(const BktSrc& src, DevScalars* sc
   __syncthreads();
   uint32_t start, end;
   bkt_block_range(src, start, end);
+  if (start == end) return;  // no row: the consumers take an empty block's offsets as 0 (bkt_fused_load)
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll];
 #pragma unroll
@@ -1092,7 +1119,7 @@ __global__ __launch_bounds__(kBlock) void k_local_hist(BktSrc srcD, DevScalars* 
 }
 
 // Bucket bases for this block: exclusive scan of the bucket totals + this block's offset in each.
-__device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, const uint32_t* tot, uint32_t* base,
+__device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* histx, const uint32_t* tot, uint32_t* base,
                                           uint32_t* part) {
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (B + kBlock - 1) / kBlock;
@@ -1102,24 +1129,26 @@ __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* hist, cons
   uint32_t total;
   uint32_t run = block_excl_scan(s, part, total);
   for (uint32_t k = 0; k < per && d0 + k < B; ++k) {
-    base[d0 + k] = run + (hist ? hist[(d0 + k) * kRadixBlocks + blockIdx.x] : 0u);
-    run += tot[d0 + k];
+    const uint32_t tk = tot[d0 + k];
+    base[d0 + k] = run + (histx && tk ? histx[(size_t)(d0 + k) * kRadixBlocks + blockIdx.x] : 0u);
+    run += tk;
   }
   __syncthreads();
 }
 
 // pass 2: scatter (key, physical index) into bucket order (kout, vout); ranks from LDS atomics.
 __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
-                                                        const uint32_t* hist, const uint32_t* tot, uint32_t* bstart) {
+                                                        const uint32_t* histx, const uint32_t* tot, uint32_t* bstart) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
-  bkt_bases(B, hist, tot, base, part);
+  uint32_t start, end;
+  bkt_block_range(src, start, end);
+  if (start == end && blockIdx.x != 0) return;  // block-uniform: nothing to place
+  bkt_bases(B, histx, tot, base, part);
   if (blockIdx.x == 0) {  // block 0's bases are the bucket starts (its per-block offsets are 0)
     for (uint32_t d = threadIdx.x; d < B; d += kBlock) bstart[d] = base[d];
     if (threadIdx.x == 0) bstart[B] = base[B - 1] + tot[B - 1];
   }
-  uint32_t start, end;
-  bkt_block_range(src, start, end);
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll], v[kBktUnroll];
 #pragma unroll
@@ -1357,7 +1386,7 @@ __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const
 
 __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars* sc, const tgsim_record* L,
                                                    tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                   const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                   const uint32_t* histx, const uint32_t* tot, uint32_t* pend,
                                                    uint32_t lo, uint32_t nloc) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
@@ -1382,9 +1411,10 @@ __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars
     }
   }
   if (off == ~0ull) return;  // region allocation failed (error bit set)
-  bkt_bases(slots, hist, tot, base, part);
   uint32_t start, end;
   bkt_block_range(src, start, end);
+  if (start == end) return;  // block-uniform: nothing to insert
+  bkt_bases(slots, histx, tot, base, part);
   // kWheelUnroll records in flight per thread; out-of-range lanes load a clamped (valid) record so
   // the arrays stay in registers (a conditional load, or HIP's uint4 wrapper, left them in scratch)
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kWheelUnroll) {
@@ -1953,11 +1983,6 @@ __device__ __forceinline__ bool k3less(uint64_t a1, uint64_t a2, uint32_t a3, ui
 // (true): slot[u] is item u's LDS slot, sm.cnt[k] the END of key k's run, sm.ord the sorted order
 // of every key run of length <= kBktRankMax (by_pos: position -> slot, else slot -> position); longer runs are written out (kout, vout,
 // off) and listed. false: the bucket was too big and went to the global form (k_rest).
-// Bijection of [0, n): block i -> the (i / 8)-th item of XCD i % 8's contiguous share.
-__device__ __forceinline__ uint32_t xcd_major(uint32_t i, uint32_t n) {
-  const uint32_t q = n >> 3, r = n & 7u, x = i & 7u;
-  return x * q + (x < r ? x : r) + (i >> 3);
-}
 
 // chunk of item j: the last chunk p with cexcl[p] <= j (cexcl ascending, cexcl[0] = 0)
 __device__ __forceinline__ uint32_t chunk_of(const uint32_t* cexcl, uint32_t j) {
@@ -1995,7 +2020,8 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     uint32_t ps, pe;
     bkt_range_of(src, p, ps, pe);
     const uint32_t* row = poff + (size_t)p * (B + 1);
-    const uint32_t lo = row[b], hi = row[b + 1];
+    const bool live = ps < pe;  // an empty partition block wrote no row (bkt_local_body)
+    const uint32_t lo = live ? row[b] : 0u, hi = live ? row[b + 1] : 0u;
     uint32_t c = hi - lo, l = lo, tc, tl;
     block_scan2(c, l, sm.part, tc, tl);  // c: items before chunk p; tc: bucket size; tl: bucket start
     cexcl[p] = c;
@@ -2376,11 +2402,12 @@ __global__ __launch_bounds__(kBlock) void k_emit_bucket(EmitPolicy p, BktSrc src
                                                         uint32_t* vscr, uint32_t* kout, uint32_t* vout, BktDiv bd,
                                                         uint32_t B, uint32_t K, uint32_t* off, uint32_t* off2,
                                                         uint32_t* medium, LargeSeg* large, DevScalars* sc,
-                                                        uint32_t* hist, uint32_t* tot) {
+                                                        BktSrc srcL, const uint32_t* hist, uint32_t* histx,
+                                                        uint32_t* tot, uint32_t slots) {
   // blocks [B, B + slots): the wheel insert's per-slot scans of the L histogram (k_local_hist made it;
-  // nothing here reads it), one slot row each - they share this launch instead of a dependent one
+  // nothing here reads it), one slot each - they share this launch instead of a dependent one
   if (blockIdx.x >= B) {
-    radix_rows_body(hist, tot, blockIdx.x - B);
+    radix_rows_body(srcL, hist, histx, tot, slots, blockIdx.x - B, slots);
     return;
   }
   __shared__ BktFusedSmem sm;
@@ -4299,9 +4326,8 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
 #ifdef TGSIM_PHASE_PROF
       const uint64_t tp_sorted = __builtin_amdgcn_s_memrealtime();
 #endif
-      fence_release_agent();  // the sorted chunk is visible device-wide before it is counted
-      __syncthreads();
-      if (threadIdx.x == 0) atomicAdd(&lg[i].pad, 1u);
+      // the sorted chunk is visible device-wide before it is counted
+      if (block_release_for_count()) atomicAdd(&lg[i].pad, 1u);
       TASK_PH(tp_sorted);
       continue;
     }
@@ -4317,8 +4343,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
         }
       }
     }
-    __syncthreads();
-    fence_acquire_agent();  // the counted chunks' keys, written by other workgroups
+    block_acquire_after_poll();  // the counted chunks' keys, written by other workgroups
 #ifdef TGSIM_PHASE_PROF
     const uint64_t tp_ready = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -4737,12 +4762,12 @@ static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B
   }
   {
     ProfScope ps_(d, KID_RADIX_ROWS);
-    hipLaunchKernelGGL(k_radix_rows, dim3(B), dim3(kRadixBlocks), 0, d.stream, d.hist, d.tot);
+    hipLaunchKernelGGL(k_radix_rows, dim3(B), dim3(kRadixBlocks), 0, d.stream, src, d.hist, d.histx, d.tot, B);
   }
   {
     ProfScope ps_(d, KID_BKT_SCATTER);
     hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bd, B,
-                       d.hist, d.tot, d.bstart);
+                       d.histx, d.tot, d.bstart);
   }
   return hipGetLastError();
 }
@@ -4960,8 +4985,8 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
   {
     ProfScope ps_(d, KID_EMIT);
     hipLaunchKernelGGL(k_emit_bucket, dim3(B + d.slots), dim3(kBlock), 0, d.stream, p, srcD, d.poff, d.kv1, d.keys2,
-                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc, d.hist,
-                       d.tot);
+                       d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.inbox, d.medium, d.large, d.sc, srcL,
+                       d.hist, d.histx, d.tot, d.slots);
   }
   TG_CHECK(hipGetLastError());
   if (spec_round) {
@@ -4970,13 +4995,13 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
     const uint64_t threads = (uint64_t)d.nloc * 8;
     const uint32_t g = (uint32_t)std::min<uint64_t>((threads + kBlock - 1) / kBlock, kSpecGenBlocks);
     hipLaunchKernelGGL(k_wheel_scatter_gen, dim3(kRadixBlocks + g + kListBlocks), dim3(kBlock), 0, d.stream, srcL,
-                       d.sc, d.L, d.arena, d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0,
+                       d.sc, d.L, d.arena, d.dirs, d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0,
                        d.seg_off, d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b, ga, sig_state(d), g);
     *spec_parts = g;
   } else {
     ProfScope ps_(d, KID_REGION_FILL);
     hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L,
-                       d.arena, d.dirs, d.slots, d.hist, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
+                       d.arena, d.dirs, d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
                        d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   }
   return hipGetLastError();

@@ -224,9 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
   }
   // the last workgroup to finish proposes the next window's end (the former k_probe_end launch)
   __shared__ uint32_t s_last;
-  fence_release_agent();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&p.sc->done, 1u) == gridDim.x - 1;
+  if (block_release_for_count()) s_last = atomicAdd(&p.sc->done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
     fence_acquire_agent();

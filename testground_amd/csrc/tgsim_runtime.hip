@@ -505,6 +505,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.vals2, phys_rec);
   rc |= dalloc(c, &d.poff, (size_t)kRadixBlocks * (kMaxBins + 1));
   rc |= dalloc(c, &d.hist, (size_t)kMaxBins * kRadixBlocks);
+  rc |= dalloc(c, &d.histx, (size_t)kMaxBins * kRadixBlocks);
   rc |= dalloc(c, &d.tot, kMaxBins);
   rc |= dalloc(c, &d.bstart, kMaxBins + 1);
   rc |= dalloc(c, &d.qc, (size_t)kQcLines * 32);
@@ -2172,7 +2173,8 @@ static void storm_free(tgsim_ctx* c) {
                   (void*)s.t_start, (void*)s.t_synarr, (void*)s.t_ackarr, (void*)s.t_done, (void*)s.t_rep,
                   (void*)s.emit, (void*)s.rem, (void*)s.infl, (void*)s.order, (void*)s.ring, (void*)s.claim,
                   (void*)s.dq, (void*)s.qh, (void*)s.ql, (void*)s.nh, (void*)s.slot_t, (void*)s.hold,
-                  (void*)s.failed, (void*)s.t_last, (void*)s.sc, (void*)s.settled, (void*)s.wsegs})
+                  (void*)s.failed, (void*)s.t_last, (void*)s.sc, (void*)s.settled, (void*)s.wsegs, (void*)s.ans,
+                  (void*)s.alist, (void*)s.prop_all})
     dfree(c, q);
   s = StormDev{};
   c->storm_on = false;
@@ -2190,7 +2192,8 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
       (uint64_t)cfg->chunk_bytes + cfg->header_bytes >= 0x80000000ull)
     return fail(c, TGSIM_EINVAL, "bad storm configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "the storm reactor needs a single-shard context");
+  if (c->S != 1 && c->tcp_on) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
+  if (int rc = need_transport(c)) return rc;  // sharded: the notices and the proposal are collective
   if (!c->fl_off.empty() || c->probes)
     return fail(c, TGSIM_ESTATE, "the storm reactor runs without a flood graph or probes");
   if (c->tcp_on && (!c->tcp.acks || c->td.n_conn || c->tw_n))
@@ -2241,18 +2244,21 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
       dalloc(c, &s.claim, claim_words) || dalloc(c, &s.dq, nl) || dalloc(c, &s.qh, nl) || dalloc(c, &s.ql, nl) ||
       dalloc(c, &s.nh, nl) || dalloc(c, &s.slot_t, nl * C) || dalloc(c, &s.hold, nl * Hc) ||
       dalloc(c, &s.failed, nl) || dalloc(c, &s.t_last, nl) || dalloc(c, &s.sc, 1) ||
+      dalloc(c, &s.ans, nc) || dalloc(c, &s.alist, nc) || dalloc(c, &s.prop_all, (size_t)3 * c->S) ||
       (c->tcp_on && (dalloc(c, &s.settled, nc) || dalloc(c, &s.wsegs, nc)))) {
     storm_free(c);
     return TGSIM_ENOMEM;
   }
   hipStream_t st = c->d.stream;
-  std::vector<int64_t> tmin(std::max(nl * C, nc), INT64_MIN);
+  std::vector<int64_t> tmin(std::max(nl * C, nc), INT64_MIN), tmax(nc, INT64_MAX);
   HIPCK(c, hipMemcpyAsync(s.dst, dst, n_conn * 4, hipMemcpyHostToDevice, st), "storm setup");
   HIPCK(c, hipMemcpyAsync(s.t_ready, t_ready, n_conn * 8, hipMemcpyHostToDevice, st), "storm setup");
   HIPCK(c, hipMemcpyAsync(s.order, order.data(), n_conn * 4, hipMemcpyHostToDevice, st), "storm setup");
   HIPCK(c, hipMemcpyAsync(s.slot_t, tmin.data(), nl * C * 8, hipMemcpyHostToDevice, st), "storm setup");
   HIPCK(c, hipMemcpyAsync(s.t_last, tmin.data(), nl * 8, hipMemcpyHostToDevice, st), "storm setup");
   HIPCK(c, hipMemcpyAsync(s.t_done, tmin.data(), nc * 8, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemcpyAsync(s.t_synarr, tmax.data(), nc * 8, hipMemcpyHostToDevice, st), "storm setup");
+  HIPCK(c, hipMemsetAsync(s.ans, 0, nc * 4, st), "storm setup");
   for (void* z : {(void*)s.state, (void*)s.flags, (void*)s.res}) HIPCK(c, hipMemsetAsync(z, 0, nc, st), "storm setup");
   for (void* z : {(void*)s.rem, (void*)s.infl, (void*)s.emit}) HIPCK(c, hipMemsetAsync(z, 0, nc * 4, st), "storm setup");
   HIPCK(c, hipMemsetAsync(s.claim, 0, claim_words * 4, st), "storm setup");
@@ -2273,6 +2279,9 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
   s.window = cfg->window_ns;
   s.n_conn = (uint32_t)n_conn;
   s.phase = 0;
+  s.lo = c->lo; s.N = c->N; s.S = c->S; s.shard = c->shard; s.xcap = c->d.xcap;
+  s.xq = c->d.qc + ((size_t)3 * kNSub << 5);  // the exchange cursors' lines (idle between windows)
+  s.xsend = c->d.xsend; s.xrecv = c->d.xrecv;
   if (c->tcp_on) {
     std::vector<uint32_t> src(n_conn);
     for (uint64_t h = 0; h < n_conn; ++h) src[h] = (uint32_t)(h / O);
@@ -2365,10 +2374,27 @@ static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_a
   if (!c->storm_need_react) return fail(c, TGSIM_ESTATE, "storm: no window since the last reaction");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react before tgsim_storm_react");
   const bool on_dev = c->n_status_last == kStatusOnDevice;
-  HIPCK(c, launch_storm_react(c->d, c->td, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
-                              on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
-  storm_staged(c);
+  if (int rc = need_transport(c)) return rc;
   c->storm_need_react = false;
+  if (c->d.sm.tcp) {
+    HIPCK(c, launch_storm_react(c->d, c->td, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                                on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
+  } else {
+    int rc = TGSIM_OK;
+    HIPCK(c, launch_storm_react_pre(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                                    on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
+    if (c->S > 1 && c->tr.alltoall(c->tr.user, c->d.xsend, c->d.xrecv, (size_t)c->d.xcap * sizeof(tgsim_record),
+                                   c->d.stream) != 0)  // the notices to the diallers' shards
+      rc = fail(c, TGSIM_EHIP, "transport all-to-all failed");
+    if (!rc) HIPCK(c, launch_storm_react_post(c->d, c->td), "storm react");
+    if (!rc && c->S > 1) {  // the proposal over every shard
+      if (c->tr.allgather(c->tr.user, c->d.sm.sc->prop, c->d.sm.prop_all, 3 * sizeof(int64_t), c->d.stream) != 0)
+        rc = fail(c, TGSIM_EHIP, "transport all-gather failed");
+      else HIPCK(c, launch_storm_prop(c->d), "storm react");
+    }
+    if (rc) return shard_failed(c, rc);
+  }
+  storm_staged(c);
   if (int rc = storm_tcp_release(c)) return rc;
   if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
   return storm_read_scalars(c, next_end, n_active);
@@ -2393,12 +2419,13 @@ extern "C" int tgsim_storm_dials(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done
 static int tgsim_storm_dials_body(tgsim_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {
   if (!c) return TGSIM_EINVAL;
   if (!c->storm_on) return fail(c, TGSIM_ESTATE, "no storm reactor set up");
-  const size_t n = c->d.sm.n_conn;
+  // the local instances' connections [lo * O, hi * O)
+  const size_t h0 = (size_t)c->lo * c->d.sm.O, n = (size_t)c->nloc * c->d.sm.O;
   if ((outcome || t_done) && cap < n) return fail(c, TGSIM_ECAPACITY, "dial capacity %zu < %zu", cap, n);
   int rc = sync_and_check(c);
   if (rc) return rc;
-  if (outcome && n) HIPCK(c, hipMemcpy(outcome, c->d.sm.res, n, hipMemcpyDeviceToHost), "storm dials");
-  if (t_done && n) HIPCK(c, hipMemcpy(t_done, c->d.sm.t_done, n * 8, hipMemcpyDeviceToHost), "storm dials");
+  if (outcome && n) HIPCK(c, hipMemcpy(outcome, c->d.sm.res + h0, n, hipMemcpyDeviceToHost), "storm dials");
+  if (t_done && n) HIPCK(c, hipMemcpy(t_done, c->d.sm.t_done + h0, n * 8, hipMemcpyDeviceToHost), "storm dials");
   return TGSIM_OK;
 }
 
@@ -2417,10 +2444,21 @@ static int tgsim_storm_write_start_body(tgsim_ctx* c, int64_t t0) {
   if (t0 < c->horizon) return fail(c, TGSIM_ECAUSALITY, "t0 before the reaction horizon");
   // a goroutine writes only after its dial succeeded and "outgoing-dials-done" released, which needs
   // every dial (storm.go:156): the write phase starts once all of them are OK
-  std::vector<uint8_t> res(c->d.sm.n_conn);
-  if (!res.empty()) HIPCK(c, hipMemcpy(res.data(), c->d.sm.res, res.size(), hipMemcpyDeviceToHost), "storm write start");
-  for (size_t h = 0; h < res.size(); ++h)
-    if (res[h] != TGSIM_PROBE_OK) return fail(c, TGSIM_ESTATE, "connection %zu has not dialled successfully", h);
+  const size_t h0 = (size_t)c->lo * c->d.sm.O;
+  std::vector<uint8_t> res((size_t)c->nloc * c->d.sm.O);
+  if (!res.empty()) HIPCK(c, hipMemcpy(res.data(), c->d.sm.res + h0, res.size(), hipMemcpyDeviceToHost), "storm write start");
+  int64_t bad = -1;
+  for (size_t i = 0; i < res.size() && bad < 0; ++i)
+    if (res[i] != TGSIM_PROBE_OK) bad = (int64_t)(h0 + i);
+  if (c->S > 1) {  // every shard's dials (agreed: the phase starts everywhere or nowhere)
+    if (int rc2 = need_transport(c)) return rc2;
+    HIPCK(c, hipMemcpy(c->d_red2, &bad, 8, hipMemcpyHostToDevice), "storm write start");
+    if (c->tr.allreduce_max_i64(c->tr.user, c->d_red2, 1, c->d.stream) != 0)
+      return shard_failed(c, fail(c, TGSIM_EHIP, "transport all-reduce failed"));
+    HIPCK(c, hipMemcpyAsync(&bad, c->d_red2, 8, hipMemcpyDeviceToHost, c->d.stream), "storm write start");
+    HIPCK(c, hipStreamSynchronize(c->d.stream), "storm write start");
+  }
+  if (bad >= 0) return fail(c, TGSIM_ESTATE, "connection %lld has not dialled successfully", (long long)bad);
   c->d.sm.phase = 1;
   HIPCK(c, launch_storm_write_start(c->d, c->td, c->staged_dev, c->n_staged, t0), "storm write start");
   storm_staged(c);
@@ -2438,20 +2476,20 @@ static int tgsim_storm_results_body(tgsim_ctx* c, uint8_t* failed, int64_t* t_la
   int rc = sync_and_check(c);
   if (rc) return rc;
   const StormDev& s = c->d.sm;
-  const size_t n = s.n_conn;
+  const size_t h0 = (size_t)c->lo * s.O, n = (size_t)c->nloc * s.O;  // the local connections
   std::vector<uint32_t> infl(n), rem(n);
   std::vector<uint8_t> res(n), fl(c->nloc);
   if (n) {
     // "in flight": message mode, chunks in the buffer; TCP, written chunks not yet settled
     if (s.tcp) {
-      HIPCK(c, hipMemcpy(infl.data(), s.settled, n * 4, hipMemcpyDeviceToHost), "storm results");
-      HIPCK(c, hipMemcpy(rem.data(), s.rem, n * 4, hipMemcpyDeviceToHost), "storm results");
+      HIPCK(c, hipMemcpy(infl.data(), s.settled + h0, n * 4, hipMemcpyDeviceToHost), "storm results");
+      HIPCK(c, hipMemcpy(rem.data(), s.rem + h0, n * 4, hipMemcpyDeviceToHost), "storm results");
       for (size_t h = 0; h < n; ++h) infl[h] = s.phase == 1 ? (s.nchunks - rem[h]) - infl[h] : 0u;
     } else {
-      HIPCK(c, hipMemcpy(infl.data(), s.infl, n * 4, hipMemcpyDeviceToHost), "storm results");
+      HIPCK(c, hipMemcpy(infl.data(), s.infl + h0, n * 4, hipMemcpyDeviceToHost), "storm results");
     }
-    HIPCK(c, hipMemcpy(rem.data(), s.rem, n * 4, hipMemcpyDeviceToHost), "storm results");
-    HIPCK(c, hipMemcpy(res.data(), s.res, n, hipMemcpyDeviceToHost), "storm results");
+    HIPCK(c, hipMemcpy(rem.data(), s.rem + h0, n * 4, hipMemcpyDeviceToHost), "storm results");
+    HIPCK(c, hipMemcpy(res.data(), s.res + h0, n, hipMemcpyDeviceToHost), "storm results");
   }
   if (c->nloc) HIPCK(c, hipMemcpy(fl.data(), s.failed, c->nloc, hipMemcpyDeviceToHost), "storm results");
   for (size_t h = 0; h < n; ++h)

@@ -3,19 +3,26 @@
 // run costs the host O(1) per window whatever its instance count. Oracle twin: tgo_storm_*.
 //
 // After each window, with no host round trip:
-//   k_storm_pre   blocks [0, nb): the window's staged packets - a SYN its dialler's route refused,
-//                 a chunk that failed (no copy queued: its buffer slot frees, its instance failed);
-//                 blocks [nb, 2 nb): the window's deliveries - first arrivals of SYNs (at the
-//                 listener) and SYN-ACKs (at the dialler) by atomicMin, the first copy of each chunk
-//                 by a claim bit (its buffer slot frees); block 0 also resets the step's reductions
-//   k_storm_step  one thread per instance: dial phase - the SYN-ACKs its peers owe, each waiting
-//                 dial's end (refused / SYN-ACK before the deadline / deadline passed), then the
-//                 dial semaphore's FIFO admits dials into the free slots (those due before the next
-//                 window's end); write phase - the writesem round (storm.go:158-183) over the room
-//                 the buffers have; the staged slots reserved once per block behind sc->n_msgs_dev;
-//                 the last workgroup proposes the next window's end
-// A connection's state lives in its own slots, written by its instance's thread; the only shared
-// updates are the arrival minima, the claim bits, the buffer counts and the per-block reductions.
+//   k_storm_pre    blocks [0, nb): the window's staged packets - a SYN its dialler's route refused,
+//                  a chunk that failed (no copy queued: its buffer slot frees, its instance failed);
+//                  blocks [nb, 2 nb): the window's deliveries - a SYN's first arrival at its listener
+//                  (atomicMin; the connection listed to be answered), a SYN-ACK's at its dialler, a
+//                  chunk's arrival (to its dialler: the first copy of a written chunk frees a buffer
+//                  slot, by a claim bit); block 0 also resets the step's reductions
+//   k_storm_answer the listeners answer the listed SYNs: a SYN-ACK at max(first arrival, horizon) each,
+//                  and a notice of it to the dialler (its timeout waits a window if the SYN-ACK may
+//                  still beat the deadline)
+//   (sharded: the notices for other shards' diallers cross in the exchange blocks, k_storm_notices
+//    applies them; on one shard a notice is applied where it is made)
+//   k_storm_step   one thread per instance: dial phase - each waiting dial's end (refused / SYN-ACK
+//                  before the deadline / deadline passed), then the dial semaphore's FIFO admits dials
+//                  into the free slots (those due before the next window's end); write phase - the
+//                  writesem round (storm.go:158-183) over the room the buffers have; the staged slots
+//                  reserved once per block behind sc->n_msgs_dev; the last workgroup proposes the next
+//                  window's end (sharded: every shard's proposal inputs are gathered, k_storm_prop)
+// A connection's dialler state lives on its instance's shard, written by its instance's thread; its
+// listener state (the SYN's first arrival, answered) on its peer's. The only shared updates are the
+// arrival minima, the claim bits, the buffer counts, the notices and the per-block reductions.
 #include <algorithm>
 
 #include "tgsim_dev.h"
@@ -28,7 +35,7 @@ constexpr uint32_t kTagMask = 0x3FFFFFFFu;
 constexpr int64_t kNone = INT64_MAX;
 constexpr int64_t kBusy = INT64_MAX;  // a held semaphore slot
 enum : uint8_t { kSleep = 0, kWait = 1, kDone = 2 };
-enum : uint32_t { kEmitSynAck = 1u, kEmitSyn = 2u };
+enum : uint32_t { kEmitSyn = 2u };  // (the listener's SYN-ACKs are staged by k_storm_answer)
 enum : uint32_t { kModeStart = 0, kModeReact = 1, kModeWrites = 2 };
 
 __device__ __forceinline__ bool failed_code(uint32_t st) {
@@ -54,10 +61,11 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long
   __syncthreads();
 }
 
-// The connection a chunk packet (src -> dst, chunk id c = k * nchunks + j) belongs to, or kNoConn
-// when no written chunk of the storm matches it (a message the host staged beside the
-// reactor with the chunk tag must not index past the tables or free another chunk's buffer slot).
-// rem[h] is not written before k_storm_step, so "written" is the count before this reaction.
+// The connection a chunk packet (src -> dst, chunk id c = k * nchunks + j) belongs to on its
+// dialler's shard, or kNoConn when no written chunk of the storm matches it (a message the
+// host staged beside the reactor with the chunk tag must not index past the tables or free another
+// chunk's buffer slot). rem[h] is not written before k_storm_step, so "written" is the count before
+// this reaction.
 constexpr size_t kNoConn = ~(size_t)0;
 __device__ __forceinline__ size_t chunk_conn(const StormDev& s, uint32_t src, uint32_t dst, uint32_t c) {
   if (s.nchunks == 0) return kNoConn;
@@ -65,6 +73,58 @@ __device__ __forceinline__ size_t chunk_conn(const StormDev& s, uint32_t src, ui
   const size_t h = (size_t)src * s.O + k;
   if (k >= s.O || h >= s.n_conn || s.dst[h] != dst || j >= s.nchunks - s.rem[h]) return kNoConn;
   return h;
+}
+
+// Notices to a connection's dialler (records: t = value, src = connection, seq = kind)
+enum : uint32_t { kNoticeSynAck = 1u, kNoticeChunk = 2u };
+
+// on the dialler's shard: chunk j of connection h arrived (its first copy frees a buffer slot);
+// returns 1 when it counted
+__device__ __forceinline__ uint32_t chunk_arrived(StormDev& s, size_t h, uint32_t j) {
+  if (h >= s.n_conn || s.nchunks == 0 || j >= s.nchunks) return 0u;
+  if (chunk_conn(s, (uint32_t)(h / s.O), s.dst[h], (uint32_t)(h % s.O) * s.nchunks + j) == kNoConn) return 0u;
+  const uint64_t bit = (uint64_t)h * s.nchunks + j;
+  const uint32_t m = 1u << (bit & 31u);
+  if (atomicOr(&s.claim[bit >> 5], m) & m) return 0u;
+  atomicSub(&s.infl[h], 1u);
+  return 1u;
+}
+// on the dialler's shard: the listener staged connection h's SYN-ACK at trep
+__device__ __forceinline__ void synack_staged(StormDev& s, size_t h, int64_t trep) {
+  if (h >= s.n_conn) return;
+  s.t_rep[h] = trep;
+  s.flags[h] |= 2u | 8u;
+}
+
+// Wave-collective: a notice to the dialler's shard p (one reservation per wave and peer on the
+// peer's exchange cursor); p == kNoPeer: none. Overflow sets ERR_CAP_X (ECAPACITY at the next check).
+constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
+__device__ __forceinline__ void notice_push(StormDev& s, DevScalars* sc, uint32_t p, uint32_t h, uint32_t kind, int64_t v) {
+  bool pending = p != kNoPeer;
+  for (;;) {
+    const uint64_t m = __ballot(pending);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lp = __shfl(p, leader);
+    const bool mine = pending && p == lp;
+    const uint64_t mm = __ballot(mine);
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(s.xq + (lp << 5), (uint32_t)__popcll(mm));
+    base = __shfl(base, leader);
+    if (mine) {
+      const uint32_t pos = base + mask_rank(mm);
+      if (pos < s.xcap - 1) {
+        tgsim_record* r = s.xsend + (size_t)p * s.xcap + 1 + pos;
+        r->t = v; r->src = h; r->dst = 0; r->seq = kind; r->size = 0; r->meta = 0; r->corrupt_off = 0;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_X);
+      }
+      pending = false;
+    }
+  }
+}
+__device__ __forceinline__ uint32_t dialler_shard(const StormDev& s, size_t h) {
+  return s.S == 1 ? 0u : shard_of((uint32_t)(h / s.O), s.N, s.S);
 }
 
 __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict__ status,
@@ -101,39 +161,124 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
         const size_t h = chunk_conn(s, m_src[i], m_dst[i], sq & kTagMask);
         if (h == kNoConn) continue;
         atomicSub(&s.infl[h], 1u);
-        s.failed[m_src[i]] = 1;
+        s.failed[m_src[i] - s.lo] = 1;
         ++cnt;
       }
     }
     block_add(&s.sc->failed, cnt, red);
-  } else {  // the window's deliveries
+  } else {  // the window's deliveries (local receivers)
     const uint32_t n = sc->n_out;
-    for (uint32_t i = (blockIdx.x - nb) * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
-      const uint32_t sq = o_seq[i], tag = sq >> 30;
-      if (tag == 1u) {  // a SYN at its listener
-        const uint32_t k = sq & kTagMask;
-        const size_t h = (size_t)o_src[i] * O + k;
-        if (k < O && h < s.n_conn && s.state[h] == kWait && s.dst[h] == o_dst[i])
-          atomicMin(reinterpret_cast<long long*>(&s.t_synarr[h]), (long long)o_t[i]);
-      } else if (tag == 3u) {  // a SYN-ACK at its dialler
-        const size_t h = sq & kTagMask;
-        if (h < s.n_conn && h / O == o_dst[i] && s.dst[h] == o_src[i] && s.state[h] == kWait && (s.flags[h] & 2u))
-          atomicMin(reinterpret_cast<long long*>(&s.t_ackarr[h]), (long long)o_t[i]);
-      } else if (tag == 2u) {  // a chunk: its first copy frees a buffer slot
-        const uint32_t c = sq & kTagMask;
-        const size_t h = chunk_conn(s, o_src[i], o_dst[i], c);
-        if (h == kNoConn) continue;
-        const uint32_t k = c / s.nchunks;
-        const uint64_t bit = (uint64_t)h * s.nchunks + (c - k * s.nchunks);
-        const uint32_t m = 1u << (bit & 31u);
-        if (!(atomicOr(&s.claim[bit >> 5], m) & m)) {
-          atomicSub(&s.infl[h], 1u);
-          ++cnt;
+    for (uint32_t i0 = (blockIdx.x - nb) * kBlock; i0 < n; i0 += nb * kBlock) {  // wave-uniform trip count
+      const uint32_t i = i0 + threadIdx.x;
+      uint32_t peer = kNoPeer, nh = 0, nj = 0;
+      bool listed = false;
+      if (i < n) {
+        const uint32_t sq = o_seq[i], tag = sq >> 30;
+        if (tag == 1u) {  // a SYN at its listener: the connection's first arrival is answered
+          const uint32_t k = sq & kTagMask;
+          const size_t h = (size_t)o_src[i] * O + k;
+          if (k < O && h < s.n_conn && s.dst[h] == o_dst[i] && s.ans[h] != 1u) {
+            atomicMin(reinterpret_cast<long long*>(&s.t_synarr[h]), (long long)o_t[i]);
+            if (atomicCAS(&s.ans[h], 0u, 2u) == 0u) { listed = true; nh = (uint32_t)h; }
+          }
+        } else if (tag == 3u) {  // a SYN-ACK at its dialler
+          const size_t h = sq & kTagMask;
+          if (h < s.n_conn && h / O == o_dst[i] && s.dst[h] == o_src[i] && s.state[h] == kWait)
+            atomicMin(reinterpret_cast<long long*>(&s.t_ackarr[h]), (long long)o_t[i]);
+        } else if (tag == 2u && s.nchunks) {  // a chunk at its listener: to its dialler
+          const uint32_t c = sq & kTagMask, k = c / s.nchunks;
+          const size_t h = (size_t)o_src[i] * O + k;
+          if (k < O && h < s.n_conn && s.dst[h] == o_dst[i]) {
+            const uint32_t p = dialler_shard(s, h);
+            if (p == s.shard) cnt += chunk_arrived(s, h, c - k * s.nchunks);
+            else { peer = p; nh = (uint32_t)h; nj = c - k * s.nchunks; }
+          }
         }
       }
+      const uint64_t lm = __ballot(listed);  // the SYNs to answer: one reservation per wave
+      if (lm) {
+        const int leader = __ffsll((unsigned long long)lm) - 1;
+        uint32_t base = 0;
+        if ((int)lane_id() == leader) base = atomicAdd(&s.sc->n_ans, (uint32_t)__popcll(lm));
+        base = __shfl(base, leader);
+        if (listed) s.alist[base + mask_rank(lm)] = nh;
+      }
+      if (s.S > 1) notice_push(s, sc, peer, nh, kNoticeChunk, nj);
     }
     block_add(&s.sc->delivered, cnt, red);
   }
+}
+
+// The listeners answer the connections listed by k_storm_pre: the SYN-ACK at max(first arrival,
+// horizon), staged behind the device-side count (one reservation per block), and its notice to the
+// dialler (applied here on one shard)
+__global__ __launch_bounds__(kBlock) void k_storm_answer(DevScalars* sc, StormDev s, uint32_t cap,
+                                                         uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
+                                                         uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
+                                                         int64_t* __restrict__ m_t) {
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t sbase;
+  const uint32_t n = s.sc->n_ans;
+  const int64_t H = sc->T;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
+    const uint32_t i = b0 + threadIdx.x;
+    uint32_t h = 0, peer = kNoPeer;
+    int64_t trep = 0;
+    if (i < n) {
+      h = s.alist[i];
+      const int64_t sa = s.t_synarr[h];
+      trep = sa > H ? sa : H;
+      s.ans[h] = 1u;
+      const uint32_t p = dialler_shard(s, h);
+      if (p == s.shard) synack_staged(s, h, trep);
+      else peer = p;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(i < n ? 1u : 0u, red, tot);
+    if (threadIdx.x == 0) sbase = tot ? reserve_staged(&sc->n_msgs_dev, tot, cap) : 0u;
+    __syncthreads();
+    if (i < n) {
+      const uint32_t w = sbase + ex;
+      if (w < cap) {  // from the listener, on the dialler's connection id
+        m_src[w] = s.dst[h]; m_dst[w] = h / s.O; m_seq[w] = TGSIM_STORM_SYNACK | h; m_size[w] = s.syn; m_t[w] = trep;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_M);
+      }
+    }
+    if (s.S > 1) notice_push(s, sc, peer, h, kNoticeSynAck, trep);
+    __syncthreads();  // sbase is rewritten by the next round
+  }
+}
+
+// Sharded: the headers of the notice blocks (counts from the cursors), as k_xheaders does for a window
+__global__ void k_storm_xheaders(StormDev s) {
+  const uint32_t p = threadIdx.x;
+  if (p >= s.S) return;
+  const uint32_t n = min(s.xq[p << 5], s.xcap - 1);
+  tgsim_record h;
+  h.t = (int64_t)n; h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
+  s.xsend[(size_t)p * s.xcap] = h;
+}
+
+// Sharded: the notices the other shards sent this shard's diallers
+__global__ __launch_bounds__(kBlock) void k_storm_notices(DevScalars* sc, StormDev s) {
+  __shared__ unsigned long long red[kBlock / 64];
+  unsigned long long cnt = 0;
+  const uint64_t total = (uint64_t)s.S * s.xcap;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t p = (uint32_t)(j / s.xcap), i = (uint32_t)(j % s.xcap);
+    if (p == s.shard || i == 0) continue;
+    const int64_t n = s.xrecv[(size_t)p * s.xcap].t;
+    if (n < 0 || n >= (int64_t)s.xcap) {
+      if (i == 1) atomicOr(&sc->err, ERR_EXCH_HDR);
+      continue;
+    }
+    if ((int64_t)i > n) continue;
+    const tgsim_record r = s.xrecv[j];
+    if (r.seq == kNoticeSynAck) synack_staged(s, r.src, r.t);
+    else if (r.seq == kNoticeChunk) cnt += chunk_arrived(s, r.src, (uint32_t)r.t);
+  }
+  block_add(&s.sc->delivered, cnt, red);
 }
 
 // per block: the minimum deadline / start time of its instances and the active count
@@ -247,17 +392,11 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l
       continue;
     }
     const int64_t dl = s.t_start[h] + s.timeout;
-    bool reply_pending = false;
-    const int64_t sa = s.t_synarr[h];
-    if (sa != kNone && !(s.flags[h] & 2u)) {  // the listener answers the SYN's first arrival
-      const int64_t trep = sa > H ? sa : H;
-      s.t_rep[h] = trep;
-      s.emit[h] = kEmitSynAck;
-      s.flags[h] |= 2u;
-      reply_pending = trep < dl;
-      ++cnt;
-    }
-    s.t_synarr[h] = kNone;
+    // the listener answered the SYN's first arrival in this reaction (its notice): the SYN-ACK may
+    // still beat the deadline, so a timeout waits one more window
+    const uint8_t fl = s.flags[h];
+    const bool reply_pending = (fl & 8u) && s.t_rep[h] < dl;
+    s.flags[h] = (uint8_t)(fl & ~8u);
     const int64_t aa = s.t_ackarr[h];
     uint8_t out = TGSIM_PROBE_NONE;
     int64_t te = 0;
@@ -309,7 +448,6 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l
       continue;
     }
     s.flags[h] = 0;
-    s.t_synarr[h] = kNone;
     s.t_ackarr[h] = kNone;
     s.emit[h] |= kEmitSyn;
     ++cnt;
@@ -470,15 +608,6 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, TcpDev t, Dev
             }
           }
         } else {
-          if (e & kEmitSynAck) {  // from the listener, on the dialler's connection id
-            if (w < cap) {
-              m_src[w] = s.dst[h]; m_dst[w] = g; m_seq[w] = TGSIM_STORM_SYNACK | (uint32_t)h; m_size[w] = s.syn;
-              m_t[w] = s.t_rep[h];
-            } else {
-              atomicOr(&sc->err, ERR_CAP_M);
-            }
-            ++w;
-          }
           if (e & kEmitSyn) {
             if (w < cap) {
               m_src[w] = g; m_dst[w] = s.dst[h]; m_seq[w] = TGSIM_STORM_SYN | k; m_size[w] = s.syn;
@@ -504,9 +633,7 @@ __global__ __launch_bounds__(kBlock) void k_storm_step(StormDev s, TcpDev t, Dev
   }
   // the last workgroup to finish proposes the next window's end
   __shared__ uint32_t s_last;
-  fence_release_agent();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&s.sc->done, 1u) == gridDim.x - 1;
+  if (block_release_for_count()) s_last = atomicAdd(&s.sc->done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(s_last) && threadIdx.x == 0) {
     fence_acquire_agent();
@@ -527,13 +654,31 @@ __device__ __forceinline__ void storm_end(StormDev& s, const TcpDev& t, const De
   const int64_t q = __hip_atomic_load(&s.sc->next_start, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t staged = __hip_atomic_load(const_cast<uint32_t*>(&sc->n_msgs_dev), __ATOMIC_ACQUIRE,
                                             __HIP_MEMORY_SCOPE_AGENT);
-  if (staged == 0 && sc->arena_used == 0 && act && tcp_idle) {  // idle: jump to the next deadline or dial
-    int64_t cand = m != kNone ? m + 1 : kNone;
-    cand = q < cand ? q : cand;
-    if (cand != kNone && cand > ne) ne = cand;
-  }
+  int64_t cand = m != kNone ? m + 1 : kNone;
+  cand = q < cand ? q : cand;
+  const bool busy = staged != 0 || sc->arena_used != 0 || !tcp_idle;
+  if (!busy && act && cand != kNone && cand > ne) ne = cand;  // idle: jump to the next deadline or dial
   s.sc->next_end = ne;
   s.sc->n_active = act;
+  s.sc->prop[0] = busy ? 1 : 0;  // sharded: the same rule over every shard's inputs (k_storm_prop)
+  s.sc->prop[1] = act;
+  s.sc->prop[2] = cand;
+}
+
+// Sharded: the proposal from every shard's (busy, active, earliest deadline + 1 / dial start), all-
+// gathered into prop_all - the one-shard rule over the whole run
+__global__ void k_storm_prop(StormDev s, const DevScalars* sc) {
+  if (threadIdx.x != 0) return;
+  int64_t busy = 0, act = 0, cand = kNone;
+  for (uint32_t k = 0; k < s.S; ++k) {
+    busy |= s.prop_all[3 * k];
+    act += s.prop_all[3 * k + 1];
+    cand = s.prop_all[3 * k + 2] < cand ? s.prop_all[3 * k + 2] : cand;
+  }
+  int64_t ne = sc->t_end + s.window;
+  if (!busy && act && cand != kNone && cand > ne) ne = cand;
+  s.sc->next_end = ne;
+  s.sc->n_active = (uint32_t)act;
 }
 
 __global__ void k_storm_reset(StormDev s, DevScalars* sc, uint32_t set_base, uint32_t base_host) {
@@ -605,16 +750,48 @@ hipError_t launch_storm_write_start(Dev& d, const TcpDev& td, bool base_dev, uin
   return hipGetLastError();
 }
 
+hipError_t launch_storm_react_pre(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                                  const uint32_t* n_status_dev) {
+  ProfScope ps_(d, KID_STORM);
+  constexpr uint32_t nb = kStreamBlocks / 2;
+  StormDev& s = d.sm;
+  if (hipMemsetAsync(&s.sc->n_ans, 0, sizeof(uint32_t), d.stream) != hipSuccess) return hipGetLastError();
+  if (s.S > 1 && hipMemsetAsync(s.xq, 0, (size_t)s.S * 128, d.stream) != hipSuccess) return hipGetLastError();
+  hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
+                     n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, s, nb,
+                     base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_storm_answer, dim3(grid_for(std::max<uint32_t>(s.n_conn, 1u))), dim3(kBlock), 0, d.stream,
+                     d.sc, s, d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  if (s.S > 1) hipLaunchKernelGGL(k_storm_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_react_post(Dev& d, const TcpDev& td) {
+  ProfScope ps_(d, KID_STORM);
+  const StormDev& s = d.sm;
+  if (s.S > 1) {
+    const uint64_t total = (uint64_t)s.S * s.xcap;
+    hipLaunchKernelGGL(k_storm_notices, dim3(grid_for((uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFu))), dim3(kBlock),
+                       0, d.stream, d.sc, s);
+  }
+  hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, td, d.sc, d.lo,
+                     d.nloc, (uint32_t)kModeReact, (int64_t)0, (int64_t)0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq,
+                     d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_storm_prop(Dev& d) {
+  hipLaunchKernelGGL(k_storm_prop, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc);
+  return hipGetLastError();
+}
+
+// TCP mode (one shard): the TCP reaction has settled the window's packets and deliveries
 hipError_t launch_storm_react(Dev& d, const TcpDev& td, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev) {
   ProfScope ps_(d, KID_STORM);
-  constexpr uint32_t nb = kStreamBlocks / 2;
-  if (d.sm.tcp)  // the TCP reaction has settled the window's packets and deliveries
-    hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
-  else
-    hipLaunchKernelGGL(k_storm_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
-                       n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, d.sm, nb,
-                       base_dev ? 0u : 1u, base_host);
+  (void)n_status_host;
+  (void)n_status_dev;
+  hipLaunchKernelGGL(k_storm_reset, dim3(1), dim3(64), 0, d.stream, d.sm, d.sc, base_dev ? 0u : 1u, base_host);
   hipLaunchKernelGGL(k_storm_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, d.sm, td, d.sc, d.lo,
                      d.nloc, (uint32_t)kModeReact, (int64_t)0, (int64_t)0, d.cap_msgs, d.m_src, d.m_dst, d.m_seq,
                      d.m_size, d.m_t);

@@ -539,7 +539,7 @@ class Simulator:
         d = np.ascontiguousarray(dst, dtype=np.uint32)
         t = np.ascontiguousarray(t_ready, dtype=np.int64)
         assert len(d) == len(t) == self.cfg.n_instances * outgoing
-        self._storm_n = len(d)
+        self._storm_n = (self.hi - self.lo) * outgoing  # the local instances' connections (sharded)
         cfg = A.StormConfig(outgoing, concurrent, chunk_bytes, header_bytes, data_bytes, syn_bytes, msg_window,
                             dial_timeout_ns, window_ns)
         self._check(self.lib.storm_setup(self._ctx, _ptr(d), _ptr(t), C.byref(cfg)))
@@ -562,7 +562,8 @@ class Simulator:
         return a.value, b.value
 
     def storm_dials(self) -> tuple[np.ndarray, np.ndarray]:
-        """(outcome TGSIM_PROBE_* per connection, its end time)."""
+        """(outcome TGSIM_PROBE_* per connection, its end time): the local instances' connections,
+        lo * outgoing .. hi * outgoing."""
         out = np.zeros(self._storm_n, np.uint8)
         t = np.zeros(self._storm_n, np.int64)
         self._check(self.lib.storm_dials(self._ctx, _ptr(out), _ptr(t), self._storm_n))

@@ -114,9 +114,11 @@ def _worker(rank, world, port, seed, q):
         outs, _ = S.run_random_sharded(_with_transport(ob, tr), None, world, seed, local=[rank])
         storm = S.run_storm(ob, n_inst=600, rounds=3, cfg_kw=S.shard_cfg(world, rank, exchange_cap=1 << 14),
                             setup=lambda sim: sim.set_transport(tr))
+        from tests.test_storm_plan import random_run
+        reactor = random_run(ob, seed, shard=(rank, world, lambda ph: tr))  # the storm plan's reactor
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, outs[0], storm))
+        q.put((rank, outs[0], (storm, reactor)))
     except Exception:  # surface the failure in the parent
         import traceback
         q.put((rank, "ERR", traceback.format_exc()))
@@ -141,7 +143,9 @@ def test_sharded_gloo(oracle, world):
         p.join(timeout=60)
     _, srcs = S.run_random_sharded(lambda c: Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
     S.assert_sharded_matches([got[r][0] for r in range(world)], srcs, S.run_random(oracle, seed), world)
-    S.assert_storm_sharded([got[r][1] for r in range(world)], S.run_storm(oracle, n_inst=600, rounds=3), world, 600)
+    S.assert_storm_sharded([got[r][1][0] for r in range(world)], S.run_storm(oracle, n_inst=600, rounds=3), world, 600)
+    from tests.test_storm_plan import assert_storm_shards_match, random_run
+    assert_storm_shards_match([got[r][1][1] for r in range(world)], random_run(oracle, seed))
 
 
 def _failing_shard_run(binding, device=False, world=3):

@@ -252,15 +252,19 @@ def test_storm_foreign_messages_hip(hip, oracle):
     assert a["tot"] == b["tot"]
 
 
-def random_run(b, seed, n=60, keep=True):
+def random_run(b, seed, n=60, keep=True, shard=None):
     """Shaped, lossy, duplicating links, a few blackhole / prohibit rules and a disabled instance:
     dials refused, timed out and OK; then (on a second context, lossless while it dials) the write
-    phase with blocking writers and lost chunks."""
+    phase with blocking writers and lost chunks. shard = (k, world, make_transport): shard k of a
+    sharded run (configuration calls go to every shard; results are the shard's own)."""
     rng = np.random.default_rng(seed)
     out = {}
     for phase in ("dials", "writes"):
-        s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17),
+        kw = dict(shard_id=shard[0], n_shards=shard[1], exchange_cap=1 << 13) if shard else {}
+        s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17, **kw),
                       binding=b)
+        if shard:
+            s.set_transport(shard[2](phase))
         kw = [dict(latency_ns=int(rng.integers(0, 4)) * MS, jitter_ns=int(rng.integers(0, 3)) * MS // 2,
                    loss=float(rng.choice([0.0, 0.0, 3.0])), duplicate=float(rng.choice([0.0, 5.0])),
                    bandwidth_bps=int(rng.choice([0, 0, 50_000_000]))) for _ in range(n)]
@@ -322,6 +326,139 @@ def test_storm_random_hip_matches_oracle(hip, oracle, seed):
     S.assert_same(a["write_obs"], b["write_obs"])
     assert np.array_equal(a["failed"], b["failed"]) and np.array_equal(a["t_last"], b["t_last"])
     assert a["totals"] == b["totals"]
+
+
+def sharded_random_run(b, seed, world, device=False):
+    """random_run on `world` shards, one thread each over the thread-group transport (one group per
+    phase: each phase is a fresh set of contexts)."""
+    from testground_amd.exchange import ThreadGroup, run_threads
+    groups = {ph: ThreadGroup(world, device=device) for ph in ("dials", "writes")}
+    return run_threads([lambda k=k: random_run(b, seed, shard=(k, world, lambda ph, k=k: groups[ph].member(k)))
+                        for k in range(world)])
+
+
+def assert_storm_shards_match(outs, single):
+    """The shards' observations against the single-context run: the same windows, proposals and
+    active counts; statuses as one multiset; deliveries, dial outcomes and per-instance results
+    concatenated in shard order; counters summed."""
+    cat = lambda xs: np.concatenate(xs)
+    for k in ("dials", "writes"):
+        assert all(o[k]["w"] == single[k]["w"] for o in outs), f"{k}: window count"
+        for w, ref in enumerate(single[k]["obs"]):
+            obs = [o[k]["obs"][w] for o in outs]
+            assert all((x["ne"], x["act"]) == (ref["ne"], ref["act"]) for x in obs), f"{k} window {w}: proposal"
+            S.assert_same(np.sort(cat([x["status"] for x in obs])), ref["status"], f"{k} window {w} status")
+            for f in ref["deliv"]:
+                S.assert_same(cat([x["deliv"][f] for x in obs]), ref["deliv"][f], f"{k} window {w} deliv.{f}")
+        assert np.array_equal(cat([o[k]["res"] for o in outs]), single[k]["res"])
+        assert np.array_equal(cat([o[k]["t_done"] for o in outs]), single[k]["t_done"])
+    assert all(o["write_w"] == single["write_w"] for o in outs)
+    for w, ref in enumerate(single["write_obs"]):
+        obs = [o["write_obs"][w] for o in outs]
+        assert all((x["ne"], x["act"]) == (ref["ne"], ref["act"]) for x in obs), f"write window {w}: proposal"
+        S.assert_same(np.sort(cat([x["status"] for x in obs])), ref["status"], f"write window {w} status")
+        for f in ref["deliv"]:
+            S.assert_same(cat([x["deliv"][f] for x in obs]), ref["deliv"][f], f"write window {w} deliv.{f}")
+    assert np.array_equal(cat([o["failed"] for o in outs]), single["failed"])
+    assert np.array_equal(cat([o["t_last"] for o in outs]), single["t_last"])
+    for k in single["totals"]:
+        assert sum(o["totals"][k] for o in outs) == single["totals"][k], k
+    for ph in ("dials_stats", "writes_stats"):
+        for k in single[ph]:
+            assert sum(o[ph][k] for o in outs) == single[ph][k], (ph, k)
+
+
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2), (4, 3)])
+def test_storm_sharded_threads_oracle(oracle, world, seed):
+    """The storm reactor sharded: every instance's dials and writes on its own
+    shard, SYNs and requests reach the peer's shard through the window's exchange, the listener's
+    answers and chunk arrivals reach the dialer's shard as notices, the proposal is collective -
+    equal to the single context window by window."""
+    assert_storm_shards_match(sharded_random_run(oracle, seed, world), random_run(oracle, seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2), (4, 3)])
+def test_storm_sharded_threads_hip(hip, oracle, world, seed):
+    """The sharded reactor on the device: `world` HIP contexts on one GPU (thread-group transport,
+    device buffers) equal the single oracle context window by window."""
+    assert_storm_shards_match(sharded_random_run(hip, seed, world, device=True), random_run(oracle, seed))
+
+
+def storm_reactor_run(b, n, shard=None, outgoing=5, delay_ms=2000, limit=3, size=8 * 1024):
+    """The storm plan's reactor calls (plans.storm at conn_outgoing 5, conn_delay_ms 2000,
+    concurrent_dials 3, data_size_kb 8, message mode): dials until none is active, the write phase
+    from the last dial's end, writes until none is active. shard = (k, world, transport)."""
+    rng = np.random.default_rng(0)
+    src = np.repeat(np.arange(n), outgoing)
+    dst = (src + rng.integers(1, n, len(src))) % n
+    t_ready = rng.integers(0, delay_ms, len(src)) * MS
+    kw = dict(shard_id=shard[0], n_shards=shard[1], exchange_cap=1 << 16) if shard else {}
+    s = Simulator(SimConfig(n_instances=n, seed=1, max_msgs_per_window=max(1 << 18, 64 * n),
+                            max_records=max(1 << 20, 128 * n), **kw), binding=b)
+    if shard:
+        s.set_transport(shard[2])
+    s.storm_setup(dst, t_ready, outgoing=outgoing, concurrent=limit, data_bytes=size, window_ns=W)
+    s.storm_start()
+    props = []
+
+    def windows():
+        ne = s.now + W
+        while True:
+            s.advance(ne)
+            ne, act = s.storm_react()
+            props.append((ne, act))
+            if act == 0:
+                return
+
+    windows()
+    res, t_done = s.storm_dials()
+    s.storm_write_start(s.now)
+    windows()
+    failed, t_last, tot = s.storm_results()
+    out = dict(props=props, res=res, t_done=t_done, failed=failed, t_last=t_last, tot=tot, now=s.now,
+               stats=S.parity_stats(s))
+    s.storm_end()
+    s.close()
+    return out
+
+
+def assert_reactor_shards_match(outs, single):
+    assert all(o["props"] == single["props"] and o["now"] == single["now"] for o in outs)
+    for k in ("res", "t_done", "failed", "t_last"):
+        assert np.array_equal(np.concatenate([o[k] for o in outs]), single[k]), k
+    for k in single["tot"]:
+        assert sum(o["tot"][k] for o in outs) == single["tot"][k], k
+    for k in single["stats"]:
+        assert sum(o["stats"][k] for o in outs) == single["stats"][k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_storm_reactor_20k_sharded_hip(hip, oracle, world):
+    """the storm plan's reactor at 20k instances as 2 and 4 HIP contexts on one GPU
+    (thread-group transport) equals the single HIP context, which equals the oracle."""
+    from testground_amd.exchange import ThreadGroup, run_threads
+    single = storm_reactor_run(hip, 20_000)
+    assert (single["res"] == A.PROBE_OK).all() and single["tot"]["chunks_delivered"] == 20_000 * 5 * 2
+    if world == 2:
+        ref = storm_reactor_run(oracle, 20_000)
+        assert single["props"] == ref["props"] and single["tot"] == ref["tot"] and single["stats"] == ref["stats"]
+        for k in ("res", "t_done", "failed", "t_last"):
+            assert np.array_equal(single[k], ref[k]), k
+    g = ThreadGroup(world, device=True)
+    outs = run_threads([lambda k=k: storm_reactor_run(hip, 20_000, shard=(k, world, g.member(k)))
+                        for k in range(world)])
+    assert_reactor_shards_match(outs, single)
+
+
+def test_storm_reactor_sharded_threads_oracle(oracle):
+    """The same on the oracle at 2,000 instances over 3 shards."""
+    from testground_amd.exchange import ThreadGroup, run_threads
+    single = storm_reactor_run(oracle, 2000)
+    g = ThreadGroup(3)
+    outs = run_threads([lambda k=k: storm_reactor_run(oracle, 2000, shard=(k, 3, g.member(k))) for k in range(3)])
+    assert_reactor_shards_match(outs, single)
 
 
 def storm_plan_run(b, n, params, seed=1):
