@@ -226,6 +226,10 @@ struct tgo_ctx {
   tgsim_tcp_stats tstats;
   /* sequential probes (tgsim_probe_*) */
   struct oprobe* pr; uint32_t* pr_order; uint8_t* pr_out; uint32_t pr_n; tgsim_probe_config pr_cfg;
+  /* the answering side of the probes (per prober g, on every shard: the requests its peers on this
+   * shard received): last position answered + 1, the position being answered in this reaction + 1,
+   * its requests' first arrival; the probers answered in this reaction */
+  uint32_t *pr_ans, *pr_cur, *pr_list; int64_t* pr_rqa; size_t pr_list_n;
   int pr_need_react;  /* a window ended with probes set up: tgo_probe_react before staging or the next window */
   /* storm plan reactor (tgsim_storm_*) */
   struct ostorm* sm;
@@ -365,6 +369,7 @@ void tgo_destroy(tgo_ctx* c) {
   free(c->fl_off); free(c->fl_nbr); free(c->fl_seen);
   free(c->tw); free(c->tsg); free(c->tpend); free(c->tack); free(c->tc);
   free(c->pr); free(c->pr_order); free(c->pr_out);
+  free(c->pr_ans); free(c->pr_cur); free(c->pr_list); free(c->pr_rqa);
   sm_free(c);
   free(c->cl); free(c->epoch);
   for (size_t i = 0; i < c->n_topics; ++i) {
@@ -1412,8 +1417,8 @@ enum { PR_IDLE = 0, PR_WAIT = 1, PR_DONE = 2 };
 #define PR_NONE INT64_MAX
 #define PR_MASK 0x3FFFFFFFu
 typedef struct oprobe {
-  uint32_t pos, state, refused, replied;
-  int64_t t_req, t_reqarr, t_reparr, t_done;
+  uint32_t pos, state, refused, replied;  /* replied: 0, 1, 2 = the peer's notice came in this reaction */
+  int64_t t_req, t_rep, t_reparr, t_done;
 } oprobe;
 
 int tgo_probe_setup(tgo_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg) {
@@ -1421,7 +1426,7 @@ int tgo_probe_setup(tgo_ctx* c, const uint32_t* order, uint32_t n_order, const t
   if (cfg->timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->request_bytes >= 0x80000000u || cfg->reply_bytes >= 0x80000000u)
     return fail(c, TGSIM_EINVAL, "bad probe configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "probes need a single-shard context");
+  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "a sharded context needs a transport for probes");
   if (c->N > PR_MASK) return fail(c, TGSIM_ENOTSUP, "too many instances for probe tags");
   if (c->tcp_on || c->fl_off) return fail(c, TGSIM_ESTATE, "probes run in message mode, without a flood graph");
   if (c->sm) return fail(c, TGSIM_ESTATE, "a storm reactor is set up: it owns the deliveries");
@@ -1434,6 +1439,11 @@ int tgo_probe_setup(tgo_ctx* c, const uint32_t* order, uint32_t n_order, const t
   memcpy(ord, order, (size_t)n_order * 4);
   for (uint32_t l = 0; l < c->nloc; ++l) pr[l].t_done = INT64_MIN;
   free(c->pr); free(c->pr_order); free(c->pr_out);
+  free(c->pr_ans); free(c->pr_cur); free(c->pr_list); free(c->pr_rqa);
+  c->pr_ans = (uint32_t*)calloc(c->N, 4); c->pr_cur = (uint32_t*)calloc(c->N, 4);
+  c->pr_list = (uint32_t*)calloc(c->N, 4); c->pr_rqa = (int64_t*)malloc((size_t)c->N * 8);
+  if (!c->pr_ans || !c->pr_cur || !c->pr_list || !c->pr_rqa) return fail(c, TGSIM_ENOMEM, "oom");
+  for (uint32_t g = 0; g < c->N; ++g) c->pr_rqa[g] = PR_NONE;
   c->pr = pr; c->pr_order = ord; c->pr_out = out; c->pr_n = n_order; c->pr_cfg = *cfg;
   c->pr_need_react = 0;
   return TGSIM_OK;
@@ -1456,7 +1466,7 @@ static void pr_begin(tgo_ctx* c, uint32_t l, uint32_t pos, int64_t te, int64_t H
   if (pos >= c->pr_n) { p->state = PR_DONE; p->t_done = te; p->pos = c->pr_n; return; }
   const int64_t t = te > H ? te : H;
   p->state = PR_WAIT; p->pos = pos; p->t_req = t;
-  p->refused = p->replied = 0; p->t_reqarr = p->t_reparr = PR_NONE;
+  p->refused = p->replied = 0; p->t_rep = p->t_reparr = PR_NONE;
   pr_stage(b, c->lo + l, c->pr_order[pos], TGSIM_PROBE_REQ | pos, c->pr_cfg.request_bytes, t);
 }
 static int pr_alloc(pbuf* b, size_t cap) {
@@ -1485,14 +1495,27 @@ int tgo_probe_start(tgo_ctx* c, int64_t t0) {
   return pr_flush(c, &b);
 }
 
-int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+/* Notices to a prober's shard: its peer answered request `pos` with a reply sent at t (record: t,
+ * src = prober, dst = position, seq = PRN_REPLY) */
+enum { PRN_REPLY = 3u };
+static void pr_notice_apply(tgo_ctx* c, uint32_t g, uint32_t pos, int64_t t) {
+  if (g < c->lo || g >= c->hi) return;
+  oprobe* p = &c->pr[g - c->lo];
+  if (p->state != PR_WAIT || p->pos != pos) return;  /* a request the prober has moved past */
+  p->replied = 2;                                       /* 2: answered in this reaction */
+  p->t_rep = t;
+}
+
+static int probe_react_impl(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   if (!c->pr) return fail(c, TGSIM_ESTATE, "no probes set up");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->pr_need_react) return fail(c, TGSIM_ESTATE, "probes: no window since the last reaction");
+  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "the transport was aborted (a shard failed)");
   c->pr_need_react = 0;  /* the window's staged rows are read exactly once */
   const omsgs* s = &c->staged;
   const int64_t H = c->horizon, t_end = c->now, timeout = c->pr_cfg.timeout_ns;
-  /* 1. the window's requests: a route that refused one ends the probe at once */
+  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
+  /* 1. the window's requests (local probers): a route that refused one ends the probe at once */
   for (size_t i = 0; i < c->n_status; ++i) {
     const uint32_t sq = s->seq[i];
     if ((sq >> 30) != 1u) continue;
@@ -1502,36 +1525,74 @@ int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
         p->pos == (sq & PR_MASK) && c->pr_order[p->pos] == s->dst[i])
       p->refused = 1;
   }
-  /* 2. the window's deliveries: first arrivals of the current request at its peer and of its reply */
+  /* 2. the window's deliveries (local receivers): a request at its peer - a position of the prober
+   *    beyond the last one answered here (the highest such position; its copies' earliest arrival) -
+   *    and a reply at its prober */
+  c->pr_list_n = 0;
   for (size_t i = 0; i < c->out.n; ++i) {
     const tgsim_record* r = &c->out.v[i];
     const uint32_t tag = r->seq >> 30;
     if (tag == 1u) {
-      oprobe* p = &c->pr[r->src - c->lo];
-      if (p->state == PR_WAIT && p->pos == (r->seq & PR_MASK) && c->pr_order[p->pos] == r->dst && r->t < p->t_reqarr)
-        p->t_reqarr = r->t;
+      const uint32_t g = r->src, j = r->seq & PR_MASK;
+      if (g >= c->N || j >= c->pr_n || c->pr_order[j] != r->dst || j + 1 <= c->pr_ans[g]) continue;
+      if (!c->pr_cur[g]) c->pr_list[c->pr_list_n++] = g;
+      if (j + 1 > c->pr_cur[g]) c->pr_cur[g] = j + 1;
+      if (r->t < c->pr_rqa[g]) c->pr_rqa[g] = r->t;
     } else if (tag == 3u && (r->seq & PR_MASK) == r->dst) {
       oprobe* p = &c->pr[r->dst - c->lo];
       if (p->state == PR_WAIT && p->replied && c->pr_order[p->pos] == r->src && r->t < p->t_reparr) p->t_reparr = r->t;
     }
   }
-  /* 3. per prober: the peer's reply, then the probe's end and the next request */
+  /* 3. the peers answer: the reply at max(first arrival, horizon), and its notice to the prober */
   pbuf b;
-  if (pr_alloc(&b, 2 * (size_t)c->nloc + 1)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  if (pr_alloc(&b, 2 * (size_t)c->nloc + c->pr_list_n + 1)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  for (size_t i = 0; i < c->pr_list_n; ++i) {
+    const uint32_t g = c->pr_list[i], j = c->pr_cur[g] - 1;
+    const int64_t trep = c->pr_rqa[g] > H ? c->pr_rqa[g] : H;
+    pr_stage(&b, c->pr_order[j], g, TGSIM_PROBE_REP | g, c->pr_cfg.reply_bytes, trep);
+    c->pr_ans[g] = j + 1;
+    c->pr_cur[g] = 0;
+    c->pr_rqa[g] = PR_NONE;
+    const uint32_t k = shard_of(c, g);
+    if (k == c->cfg.shard_id) { pr_notice_apply(c, g, j, trep); continue; }
+    tgsim_record r;
+    memset(&r, 0, sizeof(r));
+    r.t = trep; r.src = g; r.dst = j; r.seq = PRN_REPLY;
+    if (recs_push(&c->outbox[k], &r)) { pr_free(&b); return fail(c, TGSIM_ENOMEM, "oom"); }
+  }
+  /* sharded: the notices to the probers' shards */
+  if (c->S > 1) {
+    memset(c->xsend, 0, (size_t)c->S * c->xcap * sizeof(tgsim_record));
+    for (uint32_t p = 0; p < c->S; ++p) {
+      orecs* o = &c->outbox[p];
+      if (p == c->cfg.shard_id) continue;
+      if (o->n + 1 > c->xcap) { pr_free(&b); return fail(c, TGSIM_ECAPACITY, "probe notices exceed the exchange capacity"); }
+      c->xsend[(size_t)p * c->xcap].t = (int64_t)o->n;
+      memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
+      o->n = 0;
+    }
+    if (c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0) {
+      pr_free(&b);
+      return fail(c, TGSIM_EHIP, "transport all-to-all failed");
+    }
+    for (uint32_t p = 0; p < c->S; ++p) {
+      if (p == c->cfg.shard_id) continue;
+      const tgsim_record* blk = &c->xrecv[(size_t)p * c->xcap];
+      const size_t n = (size_t)blk[0].t;
+      if (n + 1 > c->xcap) { pr_free(&b); return fail(c, TGSIM_ECAPACITY, "corrupt exchange header"); }
+      for (size_t i = 0; i < n; ++i) pr_notice_apply(c, blk[1 + i].src, blk[1 + i].dst, blk[1 + i].t);
+    }
+  }
+  /* 4. per local prober: the probe's end, then the next request */
   int64_t min_dl = INT64_MAX;
   uint32_t active = 0;
   for (uint32_t l = 0; l < c->nloc; ++l) {
     oprobe* p = &c->pr[l];
     if (p->state != PR_WAIT) continue;
     const int64_t dl = p->t_req + timeout;
-    int reply_pending = 0;  /* a reply staged now before the deadline can still beat it */
-    if (p->t_reqarr != PR_NONE && !p->replied) {
-      const int64_t trep = p->t_reqarr > H ? p->t_reqarr : H;
-      pr_stage(&b, c->pr_order[p->pos], c->lo + l, TGSIM_PROBE_REP | (c->lo + l), c->pr_cfg.reply_bytes, trep);
-      p->replied = 1;
-      reply_pending = trep < dl;
-    }
-    p->t_reqarr = PR_NONE;
+    /* a reply staged now before the deadline can still beat it */
+    const int reply_pending = p->replied == 2 && p->t_rep < dl;
+    if (p->replied == 2) p->replied = 1;
     uint8_t outc = TGSIM_PROBE_NONE;
     int64_t te = 0;
     if (p->refused) { outc = TGSIM_PROBE_REFUSED; te = p->t_req; }
@@ -1549,13 +1610,33 @@ int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
   }
   int rc = pr_flush(c, &b);
   if (rc) return rc;
-  /* 4. the next window: one window_ns while anything is staged or in flight, else up to the
-   *    earliest deadline */
+  /* 5. the next window: one window_ns while anything is staged or in flight (on any shard), else
+   *    up to the earliest deadline */
+  int64_t busy = c->staged.n || c->heap.n, tot = active, m = min_dl;
+  if (c->S > 1) {
+    int64_t mine[3] = {busy, (int64_t)active, min_dl};
+    int64_t* all = (int64_t*)malloc((size_t)c->S * 3 * 8);
+    if (!all) return fail(c, TGSIM_ENOMEM, "oom");
+    if (c->tr.allgather(c->tr.user, mine, all, sizeof(mine), NULL) != 0) {
+      free(all);
+      return fail(c, TGSIM_EHIP, "transport all-gather failed");
+    }
+    busy = 0; tot = 0; m = INT64_MAX;
+    for (uint32_t k = 0; k < c->S; ++k) {
+      busy |= all[3 * k];
+      tot += all[3 * k + 1];
+      if (all[3 * k + 2] < m) m = all[3 * k + 2];
+    }
+    free(all);
+  }
   int64_t ne = t_end + c->pr_cfg.window_ns;
-  if (!c->staged.n && !c->heap.n && active && min_dl != INT64_MAX && min_dl + 1 > ne) ne = min_dl + 1;
+  if (!busy && tot && m != INT64_MAX && m + 1 > ne) ne = m + 1;
   if (next_end) *next_end = ne;
-  if (n_active) *n_active = active;
+  if (n_active) *n_active = (uint32_t)tot;
   return TGSIM_OK;
+}
+int tgo_probe_react(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
+  return shard_failed(c, probe_react_impl(c, next_end, n_active));
 }
 
 int tgo_probe_results(tgo_ctx* c, uint8_t* outcome, int64_t* t_done, size_t cap) {

@@ -129,19 +129,32 @@ struct ProbeScalars {
   int64_t min_dl;                 // running min over waiting probers of their deadline (k_probe_step)
   uint32_t active;                // probers still waiting (k_probe_step -> snapshot n_active)
   uint32_t n_active;
-  uint32_t done, pad;             // k_probe_step workgroups finished (the last one proposes the window end)
+  uint32_t done, n_ans;           // k_probe_step workgroups finished (the last one proposes the window end);
+                                  // probers whose requests the local peers answer in this reaction (sharded)
+  int64_t prop[3];                // this shard's proposal inputs: busy, waiting probers, earliest deadline
 };
 struct ProbeDev {
   uint32_t* order = nullptr;      // [n_order]
   uint32_t* pos = nullptr;        // [nloc] the current probe's position
   uint8_t* state = nullptr;       // [nloc] idle / waiting / done
   uint8_t* refused = nullptr;     // [nloc] the current request was refused by the prober's route
-  uint8_t* replied = nullptr;     // [nloc] the peer has answered the current request
-  int64_t *t_req = nullptr, *t_reqarr = nullptr, *t_reparr = nullptr, *t_done = nullptr;  // [nloc]
+  uint8_t* replied = nullptr;     // [nloc] the peer has answered the current request (2: in this reaction,
+                                  // its reply sent at t_rep)
+  int64_t *t_req = nullptr, *t_rep = nullptr, *t_reparr = nullptr, *t_done = nullptr;  // [nloc]
   uint8_t* out = nullptr;         // [nloc * n_order] TGSIM_PROBE_*
   ProbeScalars* sc = nullptr;
   uint32_t n_order = 0, req_bytes = 0, rep_bytes = 0;
   int64_t timeout = 0, window = 0;
+  // the answering side, per prober g [N] (the requests that peers on this shard received): the last
+  // position answered + 1, the position answered in this reaction + 1 (the highest new one), its
+  // requests' first arrival; the probers to answer (sharded: k_probe_answer)
+  uint32_t *ans = nullptr, *cur = nullptr, *alist = nullptr;
+  int64_t* rqa = nullptr;
+  // sharding (as StormDev): notices to a prober's shard go into the exchange blocks
+  uint32_t lo = 0, nloc = 0, N = 0, S = 1, shard = 0, xcap = 0;
+  uint32_t* xq = nullptr;
+  tgsim_record *xsend = nullptr, *xrecv = nullptr;
+  int64_t* prop_all = nullptr;
 };
 
 // Storm plan reactor (tgsim_storm_*): per connection h (instance * O + k) its dial
@@ -441,6 +454,11 @@ hipError_t launch_probe_start(Dev& d, bool base_dev, uint32_t base_host, int64_t
 // *n_dev), first arrivals of requests and replies (deliveries), then per prober the reply it owes,
 // the end of its probe and the next request (staged behind sc->n_msgs_dev), and the next window's
 // proposed end (ProbeScalars::next_end)
+// sharded (S > 1), around the runtime's notice exchange and proposal all-gather
+hipError_t launch_probe_react_pre(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                                  const uint32_t* n_status_dev);
+hipError_t launch_probe_react_post(Dev& d);
+hipError_t launch_probe_prop(Dev& d);
 hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
                               const uint32_t* n_status_dev);
 
@@ -468,5 +486,35 @@ hipError_t launch_subscribe(Dev& d, const TopicIndex& ti, uint32_t n, const uint
                             const int64_t* until, uint32_t cap_each, uint64_t* cnt, void* scan_tmp, size_t scan_bytes,
                             uint64_t* offsets, uint32_t* entries, uint64_t entries_cap);
 size_t subscribe_scan_bytes(uint32_t n);
+
+// Wave-collective: a reactor's notice to shard p's exchange block (one reservation per wave and
+// peer on the peer's cursor xq[p << 5]); p == kNoPeer: none. The record carries t = v, src = a,
+// dst = b, seq = kind. Overflow sets ERR_CAP_X (ECAPACITY at the next check).
+constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
+__device__ __forceinline__ void notice_push(uint32_t* xq, tgsim_record* xsend, uint32_t xcap, DevScalars* sc,
+                                            uint32_t p, uint32_t a, uint32_t b, uint32_t kind, int64_t v) {
+  bool pending = p != kNoPeer;
+  for (;;) {
+    const uint64_t m = __ballot(pending);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lp = __shfl(p, leader);
+    const bool mine = pending && p == lp;
+    const uint64_t mm = __ballot(mine);
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(xq + (lp << 5), (uint32_t)__popcll(mm));
+    base = __shfl(base, leader);
+    if (mine) {
+      const uint32_t pos = base + mask_rank(mm);
+      if (pos < xcap - 1) {
+        tgsim_record* r = xsend + (size_t)p * xcap + 1 + pos;
+        r->t = v; r->src = a; r->dst = b; r->seq = kind; r->size = 0; r->meta = 0; r->corrupt_off = 0;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_X);
+      }
+      pending = false;
+    }
+  }
+}
 
 }  // namespace tgsim

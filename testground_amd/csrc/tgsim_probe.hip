@@ -3,17 +3,20 @@
 // does with one httpclient.Get after another (Timeout: 1 minute). Oracle twin: tgo_probe_*.
 //
 // After each window, with no host round trip:
-//   k_probe_status  per staged packet of the window: a request its prober's route refused
-//                   (blackhole / prohibit / no route) ends the probe at its send time
-//   k_probe_arrive  per delivery: the first arrival of the current request at its peer and of the
-//                   reply at the prober (atomicMin: the earliest copy whatever thread sees it)
-//   k_probe_step    per prober: the reply its peer owes (at max(arrival, horizon)), the probe's end
-//                   (refused / reply before the deadline / deadline passed), the next request; the
-//                   staged slots reserved once per block behind sc->n_msgs_dev
-//   k_probe_end     one thread: the next window's proposed end (one window_ns while messages are
-//                   staged or in flight, else the earliest deadline + 1)
-// A prober's state lives in its own slots (one thread writes them in k_probe_step); the only shared
-// updates are the arrival minima and the per-block reservation.
+//   k_probe_pre     per staged packet of the window: a request its prober's route refused
+//                   (blackhole / prohibit / no route) ends the probe at its send time; per delivery:
+//                   a request at its peer - a position of its prober beyond the last one answered
+//                   here: the highest such position and its copies' first arrival (atomicMax /
+//                   atomicMin) - and the reply's first arrival at its prober
+//   k_probe_step    per prober: the reply its peer owes (at max(arrival, horizon); on one shard the
+//                   prober's thread answers for the peer), the probe's end (refused / reply before the
+//                   deadline / deadline passed), the next request; the staged slots reserved once per
+//                   block behind sc->n_msgs_dev; the last workgroup proposes the next window's end (one
+//                   window_ns while messages are staged or in flight, else the earliest deadline + 1)
+//   sharded: k_probe_answer (the peers answer, listed by k_probe_pre) before the step, its notices
+//   to the probers' shards through the exchange blocks (k_probe_notices), the proposal collective
+// A prober's state lives in its own slots on its shard; the answering state per prober on every
+// shard. The only shared updates are the arrival extrema, the notices and the reservations.
 #include <algorithm>
 
 #include "tgsim_dev.h"
@@ -102,7 +105,6 @@ __device__ __forceinline__ void begin_probe(ProbeDev& p, uint32_t l, uint32_t g,
   p.t_req[l] = t;
   p.refused[l] = 0;
   p.replied[l] = 0;
-  p.t_reqarr[l] = kNone;
   p.t_reparr[l] = kNone;
   st.add(g, p.order[pos], TGSIM_PROBE_REQ | pos, p.req_bytes, t);
 }
@@ -141,16 +143,33 @@ __device__ __forceinline__ void probe_arrive(const uint32_t* __restrict__ o_src,
                                              const DevScalars* sc, ProbeDev& p, uint32_t lo, uint32_t bid,
                                              uint32_t nb) {
   const uint32_t n = sc->n_out;
-  for (uint32_t i = bid * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
-    const uint32_t sq = o_seq[i], tag = sq >> 30;
-    if (tag == 1u) {  // a request at its peer
-      const uint32_t l = o_src[i] - lo, j = sq & kTagMask;
-      if (p.state[l] == kWait && p.pos[l] == j && p.order[j] == o_dst[i])
-        atomicMin(reinterpret_cast<long long*>(&p.t_reqarr[l]), (long long)o_t[i]);
-    } else if (tag == 3u && (sq & kTagMask) == o_dst[i]) {  // a reply at its prober
-      const uint32_t l = o_dst[i] - lo;
-      if (p.state[l] == kWait && p.replied[l] && p.order[p.pos[l]] == o_src[i])
-        atomicMin(reinterpret_cast<long long*>(&p.t_reparr[l]), (long long)o_t[i]);
+  for (uint32_t i0 = bid * kBlock; i0 < n; i0 += nb * kBlock) {  // wave-uniform trip count
+    const uint32_t i = i0 + threadIdx.x;
+    bool listed = false;
+    uint32_t g = 0;
+    if (i < n) {
+      const uint32_t sq = o_seq[i], tag = sq >> 30;
+      if (tag == 1u) {  // a request at its peer (a position beyond the last one answered here)
+        const uint32_t j = sq & kTagMask;
+        g = o_src[i];
+        if (g < p.N && j < p.n_order && p.order[j] == o_dst[i] && j + 1u > p.ans[g]) {
+          const uint32_t old = atomicMax(&p.cur[g], j + 1u);
+          atomicMin(reinterpret_cast<long long*>(&p.rqa[g]), (long long)o_t[i]);
+          listed = old == 0u && p.S > 1;
+        }
+      } else if (tag == 3u && (sq & kTagMask) == o_dst[i]) {  // a reply at its prober
+        const uint32_t l = o_dst[i] - lo;
+        if (p.state[l] == kWait && p.replied[l] && p.order[p.pos[l]] == o_src[i])
+          atomicMin(reinterpret_cast<long long*>(&p.t_reparr[l]), (long long)o_t[i]);
+      }
+    }
+    const uint64_t lm = __ballot(listed);  // sharded: the probers to answer, one reservation per wave
+    if (lm) {
+      const int leader = __ffsll((unsigned long long)lm) - 1;
+      uint32_t base = 0;
+      if ((int)lane_id() == leader) base = atomicAdd(&p.sc->n_ans, (uint32_t)__popcll(lm));
+      base = __shfl(base, leader);
+      if (listed) p.alist[base + mask_rank(lm)] = g;
     }
   }
 }
@@ -179,6 +198,83 @@ __global__ __launch_bounds__(kBlock) void k_probe_pre(const uint8_t* __restrict_
 
 __device__ __forceinline__ void probe_end(ProbeDev& p, const DevScalars* sc);
 
+// On the prober's shard: its current request `pos` was answered with a reply sent at t
+__device__ __forceinline__ void reply_staged(ProbeDev& p, uint32_t g, uint32_t pos, int64_t t) {
+  const uint32_t l = g - p.lo;
+  if (g < p.lo || l >= p.nloc || p.state[l] != kWait || p.pos[l] != pos) return;  // moved past it
+  p.replied[l] = 2;
+  p.t_rep[l] = t;
+}
+
+// The peer answers prober g's highest new request: the reply at max(first arrival, horizon), staged
+// in st; returns the answered position. The prober's shard learns of it (reply_staged) here on one
+// shard, by a notice when sharded.
+__device__ __forceinline__ uint32_t answer(ProbeDev& p, uint32_t g, int64_t H, Staged& st) {
+  const uint32_t j = p.cur[g] - 1u;
+  const int64_t ra = p.rqa[g];
+  const int64_t trep = ra > H ? ra : H;
+  st.add(p.order[j], g, TGSIM_PROBE_REP | g, p.rep_bytes, trep);
+  p.ans[g] = j + 1u;
+  p.cur[g] = 0;
+  p.rqa[g] = kNone;
+  if (p.S == 1) reply_staged(p, g, j, trep);
+  return j;
+}
+
+constexpr uint32_t kNoticeReply = 3u;
+
+// Sharded: the local peers answer the probers listed by k_probe_pre; notices to their shards
+__global__ __launch_bounds__(kBlock) void k_probe_answer(ProbeDev p, DevScalars* sc, uint32_t cap,
+                                                         uint32_t* __restrict__ m_src, uint32_t* __restrict__ m_dst,
+                                                         uint32_t* __restrict__ m_seq, uint32_t* __restrict__ m_size,
+                                                         int64_t* __restrict__ m_t) {
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t sbase;
+  const uint32_t n = p.sc->n_ans;
+  const int64_t H = sc->T;
+  for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
+    const uint32_t i = b0 + threadIdx.x;
+    Staged st;
+    uint32_t g = 0, j = 0, peer = kNoPeer;
+    int64_t trep = 0;
+    if (i < n) {
+      g = p.alist[i];
+      j = answer(p, g, H, st);
+      trep = st.t[0];
+      const uint32_t k = shard_of(g, p.N, p.S);
+      if (k == p.shard) reply_staged(p, g, j, trep);
+      else peer = k;
+    }
+    notice_push(p.xq, p.xsend, p.xcap, sc, peer, g, j, kNoticeReply, trep);
+    flush_block(st, red, &sbase, sc, cap, m_src, m_dst, m_seq, m_size, m_t);
+  }
+}
+
+__global__ void k_probe_xheaders(ProbeDev p) {
+  const uint32_t k = threadIdx.x;
+  if (k >= p.S) return;
+  const uint32_t n = min(p.xq[k << 5], p.xcap - 1);
+  tgsim_record h;
+  h.t = (int64_t)n; h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
+  p.xsend[(size_t)k * p.xcap] = h;
+}
+
+__global__ __launch_bounds__(kBlock) void k_probe_notices(DevScalars* sc, ProbeDev p) {
+  const uint64_t total = (uint64_t)p.S * p.xcap;
+  for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < total; x += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t k = (uint32_t)(x / p.xcap), i = (uint32_t)(x % p.xcap);
+    if (k == p.shard || i == 0) continue;
+    const int64_t n = p.xrecv[(size_t)k * p.xcap].t;
+    if (n < 0 || n >= (int64_t)p.xcap) {
+      if (i == 1) atomicOr(&sc->err, ERR_EXCH_HDR);
+      continue;
+    }
+    if ((int64_t)i > n) continue;
+    const tgsim_record r = p.xrecv[x];
+    if (r.seq == kNoticeReply) reply_staged(p, r.src, r.dst, r.t);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* sc, uint32_t lo, uint32_t nloc,
                                                        uint32_t cap, uint32_t* __restrict__ m_src,
                                                        uint32_t* __restrict__ m_dst, uint32_t* __restrict__ m_seq,
@@ -191,20 +287,15 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
     Staged st;
     int64_t dl_wait = kNone;
     uint32_t waiting = 0;
+    if (l < nloc && p.S == 1 && p.cur[l]) answer(p, lo + l, H, st);  // one shard: for the peer
     if (l < nloc && p.state[l] == kWait) {
       const uint32_t g = lo + l, pos = p.pos[l];
-      const int64_t rq = p.t_reqarr[l];
       const int64_t tr = p.t_req[l], dl = tr + p.timeout, ra = p.t_reparr[l];
       // a reply staged now, before the deadline, may still beat it: its arrival decides next window
       // (a request arriving within one window of the deadline is not a timeout)
-      bool reply_pending = false;
-      if (rq != kNone && !p.replied[l]) {  // the peer answers the request's first arrival
-        const int64_t trep = rq > H ? rq : H;
-        st.add(p.order[pos], g, TGSIM_PROBE_REP | g, p.rep_bytes, trep);
-        p.replied[l] = 1;
-        reply_pending = trep < dl;
-      }
-      p.t_reqarr[l] = kNone;
+      const uint8_t rp = p.replied[l];
+      const bool reply_pending = rp == 2 && p.t_rep[l] < dl;
+      if (rp == 2) p.replied[l] = 1;
       uint8_t out = TGSIM_PROBE_NONE;
       int64_t te = 0;
       if (p.refused[l]) { out = TGSIM_PROBE_REFUSED; te = tr; }
@@ -241,9 +332,27 @@ __device__ __forceinline__ void probe_end(ProbeDev& p, const DevScalars* sc) {
   const int64_t m = __hip_atomic_load(&p.sc->min_dl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t staged = __hip_atomic_load(const_cast<uint32_t*>(&sc->n_msgs_dev), __ATOMIC_ACQUIRE,
                                             __HIP_MEMORY_SCOPE_AGENT);
-  if (staged == 0 && sc->arena_used == 0 && act && m != kNone && m + 1 > ne) ne = m + 1;
+  const bool busy = staged != 0 || sc->arena_used != 0;
+  if (!busy && act && m != kNone && m + 1 > ne) ne = m + 1;
   p.sc->next_end = ne;
   p.sc->n_active = act;
+  p.sc->prop[0] = busy ? 1 : 0;  // sharded: the same rule over every shard's inputs (k_probe_prop)
+  p.sc->prop[1] = act;
+  p.sc->prop[2] = m;
+}
+
+__global__ void k_probe_prop(ProbeDev p, const DevScalars* sc) {
+  if (threadIdx.x != 0) return;
+  int64_t busy = 0, act = 0, m = kNone;
+  for (uint32_t k = 0; k < p.S; ++k) {
+    busy |= p.prop_all[3 * k];
+    act += p.prop_all[3 * k + 1];
+    m = p.prop_all[3 * k + 2] < m ? p.prop_all[3 * k + 2] : m;
+  }
+  int64_t ne = sc->t_end + p.window;
+  if (!busy && act && m != kNone && m + 1 > ne) ne = m + 1;
+  p.sc->next_end = ne;
+  p.sc->n_active = (uint32_t)act;
 }
 
 unsigned grid_for(uint32_t n) {
@@ -269,6 +378,38 @@ hipError_t launch_probe_react(Dev& d, bool base_dev, uint32_t base_host, uint32_
                      base_dev ? 0u : 1u, base_host);
   hipLaunchKernelGGL(k_probe_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, p, d.sc, d.lo, d.nloc,
                      d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_react_pre(Dev& d, bool base_dev, uint32_t base_host, uint32_t n_status_host,
+                                  const uint32_t* n_status_dev) {
+  ProbeDev& p = d.pr;
+  ProfScope ps_(d, KID_PROBE);
+  constexpr uint32_t nb = kStreamBlocks / 2;
+  if (hipMemsetAsync(&p.sc->n_ans, 0, sizeof(uint32_t), d.stream) != hipSuccess) return hipGetLastError();
+  if (hipMemsetAsync(p.xq, 0, (size_t)p.S * 128, d.stream) != hipSuccess) return hipGetLastError();
+  hipLaunchKernelGGL(k_probe_pre, dim3(2 * nb), dim3(kBlock), 0, d.stream, d.status, d.m_src, d.m_dst, d.m_seq,
+                     n_status_host, n_status_dev, d.o_src, d.o_dst, d.o_seq, d.o_t, d.sc, p, d.lo, nb,
+                     base_dev ? 0u : 1u, base_host);
+  hipLaunchKernelGGL(k_probe_answer, dim3(grid_for(p.N)), dim3(kBlock), 0, d.stream, p, d.sc, d.cap_msgs, d.m_src,
+                     d.m_dst, d.m_seq, d.m_size, d.m_t);
+  hipLaunchKernelGGL(k_probe_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_react_post(Dev& d) {
+  ProbeDev& p = d.pr;
+  ProfScope ps_(d, KID_PROBE);
+  const uint64_t total = (uint64_t)p.S * p.xcap;
+  hipLaunchKernelGGL(k_probe_notices, dim3(grid_for((uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFu))), dim3(kBlock), 0,
+                     d.stream, d.sc, p);
+  hipLaunchKernelGGL(k_probe_step, dim3(grid_for(d.nloc)), dim3(kBlock), 0, d.stream, p, d.sc, d.lo, d.nloc,
+                     d.cap_msgs, d.m_src, d.m_dst, d.m_seq, d.m_size, d.m_t);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_prop(Dev& d) {
+  hipLaunchKernelGGL(k_probe_prop, dim3(1), dim3(64), 0, d.stream, d.pr, d.sc);
   return hipGetLastError();
 }
 

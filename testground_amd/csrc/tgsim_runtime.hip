@@ -2045,7 +2045,7 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   if (cfg->timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->request_bytes >= 0x80000000u || cfg->reply_bytes >= 0x80000000u)
     return fail(c, TGSIM_EINVAL, "bad probe configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "probes need a single-shard context");
+  if (int rc = need_transport(c)) return rc;  // sharded: the notices and the proposal are collective
   if (c->N > 0x3FFFFFFFu) return fail(c, TGSIM_ENOTSUP, "too many instances for probe tags");
   if (c->tcp_on || !c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "probes run in message mode, without a flood graph");
   if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor is set up: it owns the deliveries");
@@ -2054,17 +2054,27 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   ProbeDev& p = c->d.pr;
   for (void* q : {(void*)p.order, (void*)p.pos, (void*)p.state, (void*)p.refused, (void*)p.replied,
-                  (void*)p.t_req, (void*)p.t_reqarr, (void*)p.t_reparr, (void*)p.t_done, (void*)p.out, (void*)p.sc})
+                  (void*)p.t_req, (void*)p.t_rep, (void*)p.t_reparr, (void*)p.t_done, (void*)p.out, (void*)p.sc,
+                  (void*)p.ans, (void*)p.cur, (void*)p.alist, (void*)p.rqa, (void*)p.prop_all})
     dfree(c, q);
   p = ProbeDev{};
   c->probes = false;
   c->probe_need_react = false;
-  const size_t nl = std::max<uint32_t>(c->nloc, 1);
+  const size_t nl = std::max<uint32_t>(c->nloc, 1), nn = std::max<uint32_t>(c->N, 1);
   if (dalloc(c, &p.order, n_order) || dalloc(c, &p.pos, nl) || dalloc(c, &p.state, nl) || dalloc(c, &p.refused, nl) ||
-      dalloc(c, &p.replied, nl) || dalloc(c, &p.t_req, nl) || dalloc(c, &p.t_reqarr, nl) || dalloc(c, &p.t_reparr, nl) ||
-      dalloc(c, &p.t_done, nl) || dalloc(c, &p.out, nl * n_order) || dalloc(c, &p.sc, 1))
+      dalloc(c, &p.replied, nl) || dalloc(c, &p.t_req, nl) || dalloc(c, &p.t_rep, nl) || dalloc(c, &p.t_reparr, nl) ||
+      dalloc(c, &p.t_done, nl) || dalloc(c, &p.out, nl * n_order) || dalloc(c, &p.sc, 1) ||
+      dalloc(c, &p.ans, nn) || dalloc(c, &p.cur, nn) || dalloc(c, &p.alist, nn) || dalloc(c, &p.rqa, nn) ||
+      dalloc(c, &p.prop_all, (size_t)3 * c->S))
     return TGSIM_ENOMEM;
   hipStream_t st = c->d.stream;
+  HIPCK(c, hipMemsetAsync(p.ans, 0, nn * 4, st), "probe setup");
+  HIPCK(c, hipMemsetAsync(p.cur, 0, nn * 4, st), "probe setup");
+  {
+    std::vector<int64_t> tmax(nn, INT64_MAX);
+    HIPCK(c, hipMemcpyAsync(p.rqa, tmax.data(), nn * 8, hipMemcpyHostToDevice, st), "probe setup");
+    HIPCK(c, hipStreamSynchronize(st), "probe setup");
+  }
   HIPCK(c, hipMemcpyAsync(p.order, order, (size_t)n_order * 4, hipMemcpyHostToDevice, st), "probe setup");
   HIPCK(c, hipMemsetAsync(p.state, 0, nl, st), "probe setup");
   HIPCK(c, hipMemsetAsync(p.out, 0, nl * n_order, st), "probe setup");
@@ -2073,6 +2083,9 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   HIPCK(c, hipMemcpyAsync(p.t_done, tmin.data(), nl * 8, hipMemcpyHostToDevice, st), "probe setup");
   HIPCK(c, hipStreamSynchronize(st), "probe setup");  // tmin goes out of scope
   p.n_order = n_order;
+  p.lo = c->lo; p.nloc = c->nloc; p.N = c->N; p.S = c->S; p.shard = c->shard; p.xcap = c->d.xcap;
+  p.xq = c->d.qc + ((size_t)3 * kNSub << 5);  // the exchange cursors' lines (idle between windows)
+  p.xsend = c->d.xsend; p.xrecv = c->d.xrecv;
   p.req_bytes = cfg->request_bytes;
   p.rep_bytes = cfg->reply_bytes;
   p.timeout = cfg->timeout_ns;
@@ -2117,10 +2130,24 @@ static int tgsim_probe_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_a
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->probe_need_react) return fail(c, TGSIM_ESTATE, "probes: no window since the last reaction");
   const bool on_dev = c->n_status_last == kStatusOnDevice;
-  HIPCK(c, launch_probe_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
-                              on_dev ? &c->d.sc->n_msgs_last : nullptr), "probe react");
-  probes_staged(c);
+  if (int rc = need_transport(c)) return rc;
   c->probe_need_react = false;
+  if (c->S == 1) {
+    HIPCK(c, launch_probe_react(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                                on_dev ? &c->d.sc->n_msgs_last : nullptr), "probe react");
+  } else {  // the peers' answers reach the probers' shards as notices; the proposal over every shard
+    int rc = TGSIM_OK;
+    HIPCK(c, launch_probe_react_pre(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
+                                    on_dev ? &c->d.sc->n_msgs_last : nullptr), "probe react");
+    if (c->tr.alltoall(c->tr.user, c->d.xsend, c->d.xrecv, (size_t)c->d.xcap * sizeof(tgsim_record), c->d.stream) != 0)
+      rc = fail(c, TGSIM_EHIP, "transport all-to-all failed");
+    if (!rc) HIPCK(c, launch_probe_react_post(c->d), "probe react");
+    if (!rc && c->tr.allgather(c->tr.user, c->d.pr.sc->prop, c->d.pr.prop_all, 3 * sizeof(int64_t), c->d.stream) != 0)
+      rc = fail(c, TGSIM_EHIP, "transport all-gather failed");
+    if (!rc) HIPCK(c, launch_probe_prop(c->d), "probe react");
+    if (rc) return shard_failed(c, rc);
+  }
+  probes_staged(c);
   if (!next_end && !n_active) return TGSIM_OK;  // asynchronous
   ProbeScalars ps;
   HIPCK(c, hipMemcpyAsync(&ps, c->d.pr.sc, sizeof(ps), hipMemcpyDeviceToHost, c->d.stream), "probe react");

@@ -96,33 +96,6 @@ __device__ __forceinline__ void synack_staged(StormDev& s, size_t h, int64_t tre
   s.flags[h] |= 2u | 8u;
 }
 
-// Wave-collective: a notice to the dialler's shard p (one reservation per wave and peer on the
-// peer's exchange cursor); p == kNoPeer: none. Overflow sets ERR_CAP_X (ECAPACITY at the next check).
-constexpr uint32_t kNoPeer = 0xFFFFFFFFu;
-__device__ __forceinline__ void notice_push(StormDev& s, DevScalars* sc, uint32_t p, uint32_t h, uint32_t kind, int64_t v) {
-  bool pending = p != kNoPeer;
-  for (;;) {
-    const uint64_t m = __ballot(pending);
-    if (m == 0) break;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    const uint32_t lp = __shfl(p, leader);
-    const bool mine = pending && p == lp;
-    const uint64_t mm = __ballot(mine);
-    uint32_t base = 0;
-    if ((int)lane_id() == leader) base = atomicAdd(s.xq + (lp << 5), (uint32_t)__popcll(mm));
-    base = __shfl(base, leader);
-    if (mine) {
-      const uint32_t pos = base + mask_rank(mm);
-      if (pos < s.xcap - 1) {
-        tgsim_record* r = s.xsend + (size_t)p * s.xcap + 1 + pos;
-        r->t = v; r->src = h; r->dst = 0; r->seq = kind; r->size = 0; r->meta = 0; r->corrupt_off = 0;
-      } else {
-        atomicOr(&sc->err, ERR_CAP_X);
-      }
-      pending = false;
-    }
-  }
-}
 __device__ __forceinline__ uint32_t dialler_shard(const StormDev& s, size_t h) {
   return s.S == 1 ? 0u : shard_of((uint32_t)(h / s.O), s.N, s.S);
 }
@@ -203,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_storm_pre(const uint8_t* __restrict_
         base = __shfl(base, leader);
         if (listed) s.alist[base + mask_rank(lm)] = nh;
       }
-      if (s.S > 1) notice_push(s, sc, peer, nh, kNoticeChunk, nj);
+      if (s.S > 1) notice_push(s.xq, s.xsend, s.xcap, sc, peer, nh, 0u, kNoticeChunk, nj);
     }
     block_add(&s.sc->delivered, cnt, red);
   }
@@ -245,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_storm_answer(DevScalars* sc, StormDe
         atomicOr(&sc->err, ERR_CAP_M);
       }
     }
-    if (s.S > 1) notice_push(s, sc, peer, h, kNoticeSynAck, trep);
+    if (s.S > 1) notice_push(s.xq, s.xsend, s.xcap, sc, peer, h, 0u, kNoticeSynAck, trep);
     __syncthreads();  // sbase is rewritten by the next round
   }
 }

@@ -69,9 +69,15 @@ def test_probe_hand_hip(hip):
     _hand_case(hip)
 
 
-def _random_run(b, seed, n=40, keep=True):
+def _random_run(b, seed, n=40, keep=True, shard=None):
+    """shard = (k, world, transport): shard k of a sharded run (configuration calls to every shard;
+    results are the shard's own probers)."""
     rng = np.random.default_rng(seed)
-    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 14, max_records=1 << 16), binding=b)
+    kw = dict(shard_id=shard[0], n_shards=shard[1], exchange_cap=1 << 12) if shard else {}
+    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 14, max_records=1 << 16, **kw),
+                  binding=b)
+    if shard:
+        s.set_transport(shard[2])
     shapes = [make_shape(latency_ns=int(rng.integers(0, 3)) * MS, jitter_ns=int(rng.integers(0, 2)) * MS // 2,
                          loss=float(rng.choice([0.0, 0.0, 5.0])), duplicate=float(rng.choice([0.0, 10.0])))
               for _ in range(n)]
@@ -106,6 +112,43 @@ def test_probe_random_hip_matches_oracle(hip, oracle, seed):
     S.assert_same(a[0], b[0])
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     assert a[4] == b[4]
+
+
+def _sharded_random_run(b, seed, world, device=False):
+    from testground_amd.exchange import ThreadGroup, run_threads
+    g = ThreadGroup(world, device=device)
+    return run_threads([lambda k=k: _random_run(b, seed, shard=(k, world, g.member(k))) for k in range(world)])
+
+
+def _assert_probe_shards_match(outs, single):
+    """Per window: the same proposal and active count on every shard; statuses as one multiset,
+    deliveries concatenated in shard order; outcomes and end times concatenated; counters summed."""
+    out1, res1, td1, w1, st1, _ = single
+    assert all(o[3] == w1 for o in outs), "window count"
+    for w, ref in enumerate(out1):
+        obs = [o[0][w] for o in outs]
+        assert all((x["ne"], x["act"]) == (ref["ne"], ref["act"]) for x in obs), f"window {w}: proposal"
+        S.assert_same(np.sort(np.concatenate([x["status"] for x in obs])), ref["status"], f"window {w} status")
+        for f in ref["deliv"]:
+            S.assert_same(np.concatenate([x["deliv"][f] for x in obs]), ref["deliv"][f], f"window {w} deliv.{f}")
+    assert np.array_equal(np.concatenate([o[1] for o in outs]), res1)
+    assert np.array_equal(np.concatenate([o[2] for o in outs]), td1)
+    for k in st1:
+        assert sum(o[4][k] for o in outs) == st1[k], k
+
+
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2), (4, 3)])
+def test_probe_sharded_threads_oracle(oracle, world, seed):
+    """The probes sharded: every prober on its own shard, a request reaching its
+    peer's shard through the window's exchange, the peer's answer reaching the prober's shard as a
+    notice, the proposal collective - equal to the single context window by window."""
+    _assert_probe_shards_match(_sharded_random_run(oracle, seed, world), _random_run(oracle, seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2), (4, 3)])
+def test_probe_sharded_threads_hip(hip, oracle, world, seed):
+    _assert_probe_shards_match(_sharded_random_run(hip, seed, world, device=True), _random_run(oracle, seed))
 
 
 def test_probe_errors(oracle):
