@@ -2305,6 +2305,9 @@ int tgo_tcp_writes_range(tgo_ctx* c, uint64_t first, size_t n, uint8_t* state, i
 int tgo_tcp_get_stats(tgo_ctx* c, tgsim_tcp_stats* out) {
   if (!out) return TGSIM_EINVAL;
   *out = c->tstats;
+  /* packets = every segment once + the retransmissions released (the device's definition: a
+   * reserved segment counts whether or not its write was reached, e.g. a storm whose dials failed) */
+  out->packets = c->tstats.segments + c->tstats.retransmissions - c->tstats.pending_retx;
   return TGSIM_OK;
 }
 

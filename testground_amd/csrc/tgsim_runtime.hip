@@ -2390,6 +2390,7 @@ static int storm_read_scalars(tgsim_ctx* c, int64_t* next_end, uint32_t* n_activ
   return TGSIM_OK;
 }
 
+static int tcp_snapshot(tgsim_ctx* c);
 static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active);
 extern "C" int tgsim_storm_react(tgsim_ctx* c, int64_t* next_end, uint32_t* n_active) {
   return abi_guard(c, [&] { return tgsim_storm_react_body(c, next_end, n_active); });
@@ -2406,6 +2407,8 @@ static int tgsim_storm_react_body(tgsim_ctx* c, int64_t* next_end, uint32_t* n_a
   if (c->d.sm.tcp) {
     HIPCK(c, launch_storm_react(c->d, c->td, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
                                 on_dev ? &c->d.sc->n_msgs_last : nullptr), "storm react");
+    // the step can fail SYN writes (DialTimeout): the TCP counters as they stand after it
+    if (int rc = tcp_snapshot(c)) return rc;
   } else {
     int rc = TGSIM_OK;
     HIPCK(c, launch_storm_react_pre(c->d, c->staged_dev, c->n_staged, on_dev ? 0u : c->n_status_last,
@@ -2945,6 +2948,18 @@ static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done);
 extern "C" int tgsim_tcp_react(tgsim_ctx* c, size_t* n_done) {
   return abi_guard(c, [&] { return tgsim_tcp_react_body(c, n_done); });
 }
+// The TCP counters into the next pinned snapshot, behind the work queued on the stream
+static int tcp_snapshot(tgsim_ctx* c) {
+  const uint32_t k = c->tcp_snap_slot;
+  HIPCK(c, hipMemcpyAsync(&c->tcp_snap[k], c->td.sc, sizeof(TcpScalars), hipMemcpyDeviceToHost, c->d.stream),
+        "tcp snapshot");
+  HIPCK(c, hipEventRecord(c->tcp_ev[k], c->d.stream), "tcp snapshot");
+  c->tcp_snap_cur[k] = c->tcp_cur;
+  c->tcp_snap_live[k] = true;
+  c->tcp_snap_slot = k ^ 1u;
+  return TGSIM_OK;
+}
+
 static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   if (n_done) *n_done = 0;
   if (!c) return TGSIM_EINVAL;
@@ -2960,14 +2975,8 @@ static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   }
   c->tcp_fill = ~0u;
   c->tcp_need_react = false;
-  // the counters into the next pinned snapshot, behind the reaction on the stream
   const uint32_t k = c->tcp_snap_slot;
-  HIPCK(c, hipMemcpyAsync(&c->tcp_snap[k], c->td.sc, sizeof(TcpScalars), hipMemcpyDeviceToHost, c->d.stream),
-        "tcp react");
-  HIPCK(c, hipEventRecord(c->tcp_ev[k], c->d.stream), "tcp react");
-  c->tcp_snap_cur[k] = c->tcp_cur;
-  c->tcp_snap_live[k] = true;
-  c->tcp_snap_slot = k ^ 1u;
+  if (int rc = tcp_snapshot(c)) return rc;
   if (!n_done) return TGSIM_OK;  // asynchronous: the counters arrive with a later synchronising call
   int rc = sync_and_check(c);
   if (rc) return rc;

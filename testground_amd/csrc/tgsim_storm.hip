@@ -346,10 +346,13 @@ __device__ __forceinline__ uint32_t dial_step(StormDev& s, TcpDev& t, uint32_t l
         if (out == TGSIM_PROBE_NONE && dl < t_end) {  // net.DialTimeout (storm.go:144): the SYN write fails
           out = TGSIM_PROBE_TIMEOUT;                  // at the deadline, its slot frees then
           te = dl;
-          atomicMin(reinterpret_cast<long long*>(&t.w_fail[w]), (long long)(dl * 2 + 1));
-          if (atomicCAS(&t.w_state[w], (uint32_t)TGSIM_TCP_PENDING, (uint32_t)TGSIM_TCP_TIMEOUT) == TGSIM_TCP_PENDING) {
-            atomicAdd(&t.sc->done, 1u);
-            atomicAdd(&t.sc->failed, 1ull);
+          // a SYN that arrived (its ACK did not) is a delivered write: only a pending one fails
+          if (ws == TGSIM_TCP_PENDING) {
+            atomicMin(reinterpret_cast<long long*>(&t.w_fail[w]), (long long)(dl * 2 + 1));
+            if (atomicCAS(&t.w_state[w], (uint32_t)TGSIM_TCP_PENDING, (uint32_t)TGSIM_TCP_TIMEOUT) == TGSIM_TCP_PENDING) {
+              atomicAdd(&t.sc->done, 1u);
+              atomicAdd(&t.sc->failed, 1ull);
+            }
           }
         }
       }
