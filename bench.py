@@ -50,6 +50,14 @@ ALG_MODELS = {
     "k_emit_bucket": lambda d, n, w: 24 * (d["delivered"] - d.get("long_emit", 0)),
     "k_wheel_scatter": lambda d, n, w: 24 * d.get("long_emit", 0),
     "k_gen_storm": lambda d, n, w: 24 * d["msgs_in"],
+    # the plans' reactions after a window: the flood reads every delivery once
+    # (k_flood_count) and writes every forward, the next window's input message (k_flood_emit); the
+    # probe / storm reactors read the window's statuses and deliveries and write the messages they
+    # stage (requests, replies, SYNs, chunks: the next window's inputs)
+    "k_flood_count": lambda d, n, w: 24 * d["delivered"],
+    "k_flood_emit": lambda d, n, w: 24 * d["msgs_in"],
+    "k_probe": lambda d, n, w: 24 * d["delivered"] + 25 * d["msgs_in"],
+    "k_storm": lambda d, n, w: 24 * d["delivered"] + 25 * d["msgs_in"],
 }
 
 

@@ -2287,11 +2287,12 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     wL += (uint32_t)__popcll(mL[u]);
   }
   const uint32_t wave = threadIdx.x >> 6;
-  // cross-shard copies (S > 1): per peer an LDS count (each copy's rank in it) and one reservation
-  // per workgroup on the peer's cursor, sm.part[64 + p] / sm.part[128 + p]
+  // cross-shard copies (S > 1): per peer an LDS count (each copy's rank in it), its offset in the
+  // block's X run and one reservation per workgroup on the peer's cursor, sm.part[64 / 128 / 192 + p]
   uint32_t* xcnt = sm.part + 64;
   uint32_t* xbase = sm.part + 128;
-  static_assert(kBlock >= 128 + kMaxShards, "exchange counts fit sm.part");
+  uint32_t* xoff = sm.part + 192;
+  static_assert(kBlock >= 192 + kMaxShards, "exchange counts fit sm.part");
   if (threadIdx.x == 0) sm.flag = 0;
   if (threadIdx.x < 8) gcnt[threadIdx.x] = 0;
   if (threadIdx.x < kMaxShards) xcnt[threadIdx.x] = 0;
@@ -2316,9 +2317,14 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     uint32_t run = 0;
     for (int g = 0; g < 8; ++g) { const uint32_t v = gcnt[g]; gcnt[8 + g] = run; run += v; }
     gcnt[16] = run;
+    run = 0;
+    if (sm.flag)
+      for (uint32_t k = 0; k < p.geo.S; ++k) { xoff[k] = run; run += xcnt[k]; }
+    gcnt[17] = run;
   }
   __syncthreads();
   uint32_t tD = gcnt[16], tL = 0, bL = 0;
+  const uint32_t tX = gcnt[17];
 #pragma unroll
   for (uint32_t w = 0; w < kBlock / 64; ++w) {
     const uint32_t c = sm.part[kBlock / 64 + w];
@@ -2335,11 +2341,11 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     const uint32_t pr = threadIdx.x - 64, c = xcnt[pr];
     xbase[pr] = c ? atomicAdd(Q.xctr(pr), c) : 0u;
   }
-  // the routed copies pass through LDS in append order (the D run, then the L run), kStageN per
-  // round, so that every wave store covers consecutive records: whole lines, no reliance on L2
-  // merging partial writes
+  // the routed copies pass through LDS in append order (the D run, the L run, then the X runs peer
+  // by peer), kStageN per round, so that every wave store covers consecutive records: whole lines,
+  // no reliance on L2 merging partial writes
   uint4* st = reinterpret_cast<uint4*>(sm.k1);
-  const uint32_t nst = tD + tL;
+  const uint32_t tDL = tD + tL, nst = tDL + tX;
   for (uint32_t r0 = 0; r0 < nst; r0 += kStageN) {
     uint32_t cL = tD + bL;
 #pragma unroll
@@ -2347,8 +2353,8 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
       const uint32_t qD = gcnt[8 + (rkD[u] >> 24)] + (rkD[u] & 0xFFFFFFu);
       const uint32_t qL = cL + mask_rank(mL[u]);
       cL += (uint32_t)__popcll(mL[u]);
-      if (code[u] != Q_D && code[u] != Q_L) continue;
-      const uint32_t q = code[u] == Q_D ? qD : qL;
+      if (code[u] < 0) continue;
+      const uint32_t q = code[u] == Q_D ? qD : (code[u] == Q_L ? qL : tDL + xoff[code[u] - Q_X0] + rkD[u]);
       if (q < r0 || q >= r0 + kStageN) continue;
       const uint32_t i = q - r0;
       st[2 * i] = make_uint4((uint32_t)rec[u].t, (uint32_t)((uint64_t)rec[u].t >> 32), rec[u].src, rec[u].dst);
@@ -2358,9 +2364,23 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     const uint32_t n = min(kStageN, nst - r0);
     for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
       const uint32_t q = r0 + i;
+      const uint4 a = st[2 * i], b = st[2 * i + 1];
+      if (q >= tDL) {  // a cross-shard copy: its peer's run (S is small: a linear search)
+        const uint32_t x = q - tDL;
+        uint32_t pr = 0;
+        while (pr + 1 < p.geo.S && xoff[pr + 1] <= x) ++pr;
+        const uint32_t pos = xbase[pr] + (x - xoff[pr]);
+        if (pos < Q.xcap - 1) {
+          uint4* dst = reinterpret_cast<uint4*>(Q.X + (size_t)pr * Q.xcap + 1 + pos);
+          st4(dst, a.x, a.y, a.z, a.w);
+          st4(dst + 1, b.x, b.y, b.z, b.w);
+        } else {
+          atomicOr(&Q.sc->err, ERR_CAP_X);
+        }
+        continue;
+      }
       const bool isD = q < tD;
       const uint32_t pos = isD ? sm.part[0] + q : sm.part[1] + (q - tD);
-      const uint4 a = st[2 * i], b = st[2 * i + 1];
       if (pos < Q.subcap) {
         const size_t at = (size_t)sub * Q.subcap + pos;
         uint4* dst = reinterpret_cast<uint4*>((isD ? Q.D : Q.L) + at);
@@ -2374,16 +2394,6 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
       }
     }
     __syncthreads();
-  }
-  if (sm.flag) {  // cross-shard copies: straight into the peer blocks at the reserved positions
-    __syncthreads();  // xbase visible (the staging loop may have had no round)
-#pragma unroll
-    for (int u = 0; u < kIPT; ++u) {
-      if (code[u] < Q_X0) continue;
-      const uint32_t pr = (uint32_t)(code[u] - Q_X0), pos = xbase[pr] + rkD[u];
-      if (pos < Q.xcap - 1) store_rec(Q.X + (size_t)pr * Q.xcap + 1 + pos, rec[u]);
-      else atomicOr(&Q.sc->err, ERR_CAP_X);
-    }
   }
   TG_PH_END(0, h.nb);
 }
