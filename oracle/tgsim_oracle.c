@@ -252,6 +252,8 @@ typedef struct otcpc {
   int64_t tloss;            /* the window's earliest expired timer (INT64_MAX: none): a loss episode */
   uint32_t una;             /* no segment before it is outstanding (advanced lazily at a timeout) */
   uint32_t facks;           /* the window's first ACKs of segments in flight (not marked lost) */
+  int64_t tack;             /* the window's latest first-ACK arrival (INT64_MIN: none) */
+  uint32_t fr;              /* the segment last fast-retransmitted (TCP_NOSEG: none) */
 } otcpc;
 #define TCP_NOSEG 0xFFFFFFFFu
 #define TCP_IW 10u
@@ -1879,7 +1881,8 @@ int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t
   if (c->tc_n + n > c->tcp.max_writes) return fail(c, TGSIM_ECAPACITY, "connection capacity");
   if (grow((void**)&c->tc, &c->tc_cap, c->tc_n + n + 1, sizeof(otcpc))) return fail(c, TGSIM_ENOMEM, "oom");
   for (size_t i = 0; i < n; ++i) {
-    otcpc q = {src[i], dst[i], TCP_IW, 0x7FFFFFFFu, 0, 0, 0, TCP_NOSEG, TCP_NOSEG, 0, 0, 0, INT64_MAX, TCP_NOSEG, 0};
+    otcpc q = {src[i], dst[i], TCP_IW, 0x7FFFFFFFu, 0, 0, 0, TCP_NOSEG, TCP_NOSEG, 0, 0, 0, INT64_MAX, TCP_NOSEG, 0,
+               INT64_MIN, TCP_NOSEG};
     if (conn_out) conn_out[i] = (uint32_t)c->tc_n;
     c->tc[c->tc_n++] = q;
   }
@@ -2054,8 +2057,8 @@ int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
 }
 
 /* acks = 1: the window's packets only refuse (a timer handles every other failure); its deliveries
- * are data (first intact arrival, and an ACK back for every intact copy at max(arrival, the next
- * window's start)) or ACKs (an intact one acknowledges its segment). */
+ * are data (first intact arrival, and an ACK back for every intact copy at max(arrival, horizon):
+ * when it arrived, a late send) or ACKs (an intact one acknowledges its segment). */
 static int tcp_react_acks(tgo_ctx* c, size_t* done) {
   const omsgs* s = &c->staged;
   for (size_t i = 0; i < c->n_status; ++i) {
@@ -2085,6 +2088,7 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
         if (k != TCP_NOSEG) {
           c->tc[k].acks++;
           if (!g->lost) c->tc[k].facks++;  /* a segment marked lost holds no flight slot */
+          if (r->t > c->tc[k].tack) c->tc[k].tack = r->t;
         }
       }
       continue;
@@ -2092,7 +2096,7 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     if (!intact) continue;
     if (r->t < g->arrival) g->arrival = r->t;
     if (!g->touched) { g->touched = 1; touched[nt++] = (r->seq >> 4); }
-    otack a = {r->dst, r->src, TGSIM_TCP_ACK_BIT | r->seq, r->t > c->t_end ? r->t : c->t_end};
+    otack a = {r->dst, r->src, TGSIM_TCP_ACK_BIT | r->seq, r->t > c->horizon ? r->t : c->horizon};
     c->tack[c->tack_n++] = a;
   }
   for (size_t k = 0; k < nt; ++k) {
@@ -2106,12 +2110,17 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     if (--w->remaining == 0) tcp_finish(c, g->w, TGSIM_TCP_DELIVERED, w->t, done);
   }
   free(touched);
-  /* connections: the window's first ACKs free flight and open cwnd; the window's end releases what
-   * now fits; a reset connection fails its queued writes */
+  /* connections: the window's first ACKs free flight and open cwnd, and what now fits leaves at
+   * max(the latest of them's arrival, horizon) (the window's end without ACKs); fast retransmit
+   * [EXT RFC 5681 3.2]: once three segments after the oldest outstanding one have been ACKed (three
+   * duplicate ACKs in a cumulative-ACK stack) and it has not, it is resent then (its next attempt,
+   * once per segment, keeping its flight slot), ssthresh = max(flight / 2, 2), cwnd = ssthresh; a
+   * reset connection fails its queued writes at the window's end */
   ostage b = {0};
   int rc = TGSIM_OK;
   for (uint32_t k = 0; k < c->tc_n && !rc; ++k) {
     otcpc* q = &c->tc[k];
+    int64_t t0 = c->t_end;
     q->flight -= q->facks;
     q->facks = 0;
     q->acked += q->acks;
@@ -2119,6 +2128,29 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
       if (q->cwnd < q->ssthresh) ++q->cwnd;
       else if (++q->cnt >= q->cwnd) { ++q->cwnd; q->cnt = 0; }
       if (q->cwnd > TCP_CWND_CLAMP) q->cwnd = TCP_CWND_CLAMP;
+    }
+    if (q->acks) {
+      t0 = q->tack > c->horizon ? q->tack : c->horizon;
+      q->tack = INT64_MIN;
+      uint32_t u = q->una;
+      while (u != q->head && (c->tsg[u].acked || c->tsg[u].gave_up)) u = c->tsg[u].next;
+      q->una = u;
+      if (u != q->head && !q->broken && !c->tsg[u].lost && q->fr != u && c->tsg[u].attempt + 1 < c->tcp.max_attempts) {
+        otcps* g = &c->tsg[u];
+        const uint32_t st = c->tw[g->w].state;
+        uint32_t dup = 0;
+        for (uint32_t x = g->next; x != q->head && dup < 3; x = c->tsg[x].next) dup += c->tsg[x].acked;
+        if (dup >= 3 && st != TGSIM_TCP_TIMEOUT && st != TGSIM_TCP_REFUSED) {
+          q->fr = u;
+          q->ssthresh = q->flight / 2 > 2 ? q->flight / 2 : 2;
+          q->cwnd = q->ssthresh;
+          q->cnt = 0;
+          g->attempt++;
+          g->t_att = t0;
+          c->tstats.retransmissions++;
+          if (ostage_push(&b, q->src, q->dst, (u << 4) | g->attempt, g->wire, t0)) rc = TGSIM_ENOMEM;
+        }
+      }
     }
     q->acks = 0;
     if (q->broken) {
@@ -2132,7 +2164,7 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
       q->queued = 0;
       continue;
     }
-    rc = conn_release(c, k, c->t_end, &b, done);
+    if (!rc) rc = conn_release(c, k, t0, &b, done);
   }
   const int rc2 = ostage_flush(c, &b);
   return rc ? fail(c, rc, "oom") : rc2;

@@ -110,8 +110,10 @@ struct TcpDev {
   uint32_t *c_flight = nullptr, *c_queued = nullptr, *c_head = nullptr, *c_acks = nullptr, *c_broken = nullptr;
   unsigned long long* c_acked = nullptr;  // cumulative first ACKs
   int64_t* c_tloss = nullptr;     // the window's earliest expired timer (INT64_MAX: none): a loss episode
-  uint32_t* c_una = nullptr;      // no segment before it is outstanding (advanced at a loss episode)
+  uint32_t* c_una = nullptr;      // no segment before it is outstanding (advanced after ACKs and at a loss episode)
   uint32_t* c_fack = nullptr;     // the window's first ACKs of segments in flight (not marked lost)
+  int64_t* c_tack = nullptr;      // the window's latest first-ACK arrival (INT64_MIN: none)
+  uint32_t* c_fr = nullptr;       // the segment last fast-retransmitted (kNoSeg: none)
   uint32_t* w_conn = nullptr;     // [W] the write's connection (kNoSeg: tgsim_tcp_send writes)
   uint32_t* s_next = nullptr;     // [S] the connection's next segment
   uint32_t* s_ack1 = nullptr;     // [S] first-ACK claim (a segment frees one flight slot once)

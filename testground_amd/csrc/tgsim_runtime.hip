@@ -3128,10 +3128,11 @@ static int conn_grow(tgsim_ctx* c, uint32_t need) {
   const uint32_t cap = std::max<uint32_t>({need, 2 * c->conn_cap, 1024u});
   HIPCK(c, hipStreamSynchronize(c->d.stream), "sync");
   uint32_t** u32[] = {&t.c_src, &t.c_dst, &t.c_cwnd, &t.c_ssth, &t.c_cnt, &t.c_flight, &t.c_queued, &t.c_head,
-                      &t.c_acks, &t.c_broken, &t.c_una, &t.c_fack};
+                      &t.c_acks, &t.c_broken, &t.c_una, &t.c_fack, &t.c_fr};
   for (uint32_t** a : u32)
     if (dgrow(c, a, t.n_conn, cap)) return TGSIM_ENOMEM;
-  if (dgrow(c, &t.c_acked, t.n_conn, cap) || dgrow(c, &t.c_tloss, t.n_conn, cap)) return TGSIM_ENOMEM;
+  if (dgrow(c, &t.c_acked, t.n_conn, cap) || dgrow(c, &t.c_tloss, t.n_conn, cap) || dgrow(c, &t.c_tack, t.n_conn, cap))
+    return TGSIM_ENOMEM;
   c->conn_cap = cap;
   return TGSIM_OK;
 }
@@ -3166,7 +3167,7 @@ static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint3
   int rc = conn_grow(c, n1);
   if (rc) return rc;
   std::vector<uint32_t> a(src, src + n), b(dst, dst + n), iw(n, 10u), ss(n, 0x7FFFFFFFu), none(n, 0xFFFFFFFFu);
-  std::vector<int64_t> never(n, INT64_MAX);
+  std::vector<int64_t> never(n, INT64_MAX), none_t(n, INT64_MIN);
   hipStream_t st = c->d.stream;
   HIPCK(c, hipMemcpyAsync(t.c_src + n0, a.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_dst + n0, b.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
@@ -3175,6 +3176,8 @@ static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint3
   HIPCK(c, hipMemcpyAsync(t.c_head + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_una + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
   HIPCK(c, hipMemcpyAsync(t.c_tloss + n0, never.data(), n * 8, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_fr + n0, none.data(), n * 4, hipMemcpyHostToDevice, st), "tcp connect");
+  HIPCK(c, hipMemcpyAsync(t.c_tack + n0, none_t.data(), n * 8, hipMemcpyHostToDevice, st), "tcp connect");
   for (uint32_t* z : {t.c_cnt, t.c_flight, t.c_queued, t.c_acks, t.c_broken, t.c_fack})
     HIPCK(c, hipMemsetAsync(z + n0, 0, n * 4, st), "tcp connect");
   HIPCK(c, hipMemsetAsync(t.c_acked + n0, 0, n * 8, st), "tcp connect");

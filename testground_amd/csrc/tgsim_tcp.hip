@@ -169,6 +169,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
             if (k != kNoSeg) {
               atomicAdd(&t.c_acks[k], 1u);
               if (!t.s_lost[sid]) atomicAdd(&t.c_fack[k], 1u);  // a segment marked lost holds no slot
+              atomicMax(reinterpret_cast<long long*>(&t.c_tack[k]), (long long)ti);  // what it releases leaves then
             }
           }
         }
@@ -430,14 +431,15 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
                                                      uint32_t* __restrict__ m_size, int64_t* __restrict__ m_t) {
   __shared__ uint32_t red[kBlock / 64];
   __shared__ uint32_t sb_f, sb_k;
-  const int64_t H = sc->T, t_end = sc->t_end;  // the window [T, t_end) (k_window_start: H is the one before)
+  const int64_t H = sc->T, t_end = sc->t_end;  // the window [T, t_end)
+  const int64_t Hr = sc->H;                     // the reaction horizon: the last window's start
   const uint32_t nxt = cur ^ 1u, stride = gridDim.x * kBlock;
   const uint32_t na = t.sc->ack_n, ab = t.sc->ack_base;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < na; i += stride) {
     const uint32_t d = t.ack_idx[i], p = ab + i;
-    if (p < cap) {
+    if (p < cap) {  // an ACK leaves when its segment arrived (a late send, at or after the horizon)
       m_src[p] = o_dst[d]; m_dst[p] = o_src[d]; m_seq[p] = TGSIM_TCP_ACK_BIT | o_seq[d]; m_size[p] = t.hdr;
-      m_t[p] = o_t[d] > H ? o_t[d] : H;
+      m_t[p] = o_t[d] > Hr ? o_t[d] : Hr;
     }
   }
   const uint32_t np = t.sc->plan_n, nb = t.sc->plan_total, total = nb + t.sc->pend_n[cur];
@@ -584,7 +586,11 @@ __global__ __launch_bounds__(kBlock) void k_tcp_link(TcpDev t, const uint32_t* _
 // of a failed write or out of attempts gives up), then new ones. Modes (kRel*):
 //   at a write: t0 = the write times;
 //   after a window: first the window's ACKs (flight, slow start / congestion avoidance) and resets (a
-//     reset connection fails its queued writes), t0 = the window's end;
+//     reset connection fails its queued writes at the window's end), t0 = max(the window's latest
+//     first-ACK arrival, horizon) - what the ACKs let out leaves when they arrived, not at the window's
+//     end; then fast retransmit [EXT RFC 5681 3.2]: once three segments after the oldest outstanding
+//     one have been ACKed (three duplicate ACKs in a cumulative-ACK stack) and it has not, it is resent
+//     at t0 (next attempt; once per segment), ssthresh = max(flight / 2, 2) and cwnd = ssthresh;
 //   loss: at a window start, the connections whose timer expired in the window just begun (k_tcp_fire:
 //     c_tloss) [EXT Linux tcp_enter_loss, RFC 5681 3.1]: ssthresh = max(cwnd / 2, 2) unless cwnd is
 //     already 1 (the same episode), cwnd = 1, every outstanding segment marked lost and the queue
@@ -604,8 +610,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
   unsigned long long nretx = 0;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
     const uint32_t k = b0 + threadIdx.x;
-    uint32_t go = 0, nent = 0, head = kNoSeg, end = kNoSeg;
+    uint32_t go = 0, nent = 0, head = kNoSeg, end = kNoSeg, fr = kNoSeg;
     bool slow = false;
+    const int64_t tfail = sc->t_end;
     int64_t t0 = mode == kRelAfterWindow ? sc->t_end : INT64_MIN;
     bool act = k < n;
     if (act && mode == kRelLoss) {
@@ -634,8 +641,11 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
         const uint32_t acks = t.c_acks[k];
         if (acks) {
           const uint32_t fa = t.c_fack[k];
+          const int64_t ta = t.c_tack[k];
           t.c_acks[k] = 0u;
           t.c_fack[k] = 0u;
+          t.c_tack[k] = INT64_MIN;
+          t0 = ta > H ? ta : H;
           fl -= fa;
           t.c_acked[k] += acks;
           uint32_t ss = t.c_ssth[k], cnt = t.c_cnt[k];
@@ -643,6 +653,25 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
             if (cw < ss) ++cw;
             else if (++cnt >= cw) { ++cw; cnt = 0u; }
             cw = cw > kCwndClamp ? kCwndClamp : cw;
+          }
+          // fast retransmit: the oldest outstanding segment, past three ACKed ones
+          const uint32_t h0 = t.c_head[k];
+          uint32_t u = t.c_una[k];
+          while (u != h0 && t.s_done[u]) u = t.s_next[u];
+          t.c_una[k] = u;
+          if (u != h0 && !t.c_broken[k] && !t.s_lost[u] && t.c_fr[k] != u && t.s_att[u] + 1u < t.max_att) {
+            const uint32_t ws = t.w_state[t.s_w[u] & kWMask];
+            uint32_t dup = 0;
+            for (uint32_t x = t.s_next[u]; x != h0 && dup < 3u; x = t.s_next[x]) dup += t.s_done[x] == 1;
+            if (dup >= 3u && ws != TGSIM_TCP_TIMEOUT && ws != TGSIM_TCP_REFUSED) {
+              fr = u;
+              t.c_fr[k] = u;
+              ss = fl / 2u > 2u ? fl / 2u : 2u;
+              cw = ss;
+              cnt = 0u;
+              t.c_ssth[k] = ss;
+              nent += t.s_tq[u] ? 0u : 1u;
+            }
           }
           t.c_cwnd[k] = cw;
           t.c_cnt[k] = cnt;
@@ -653,7 +682,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
             const int64_t tw = t.s_tatt[sid];
             const uint32_t w = t.s_w[sid] & kWMask;
             t.s_done[sid] = 2;
-            if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, tw > t0 ? tw : t0, TGSIM_TCP_REFUSED);
+            if (t.w_tarr[w] == INT64_MIN) tcp_fail(t, w, tw > tfail ? tw : tfail, TGSIM_TCP_REFUSED);
           }
           t.c_head[k] = kNoSeg;
           t.c_queued[k] = 0u;
@@ -691,15 +720,34 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
       }
     }
     uint32_t tm, tp;
-    const uint32_t pm = block_excl_scan(go, red, tm);
+    const uint32_t nfr = fr != kNoSeg ? 1u : 0u;
+    const uint32_t pm = block_excl_scan(go + nfr, red, tm);
     const uint32_t pp = block_excl_scan(nent, red, tp);
     if (threadIdx.x == 0) {
       sb_m = tm ? reserve_staged(&sc->n_msgs_dev, tm, cap) : 0u;
       sb_p = tp ? atomicAdd(&t.sc->pend_n[list], tp) : 0u;
     }
     __syncthreads();
+    uint32_t e = 0;
+    if (nfr) {  // the fast retransmission, first; it keeps its flight slot
+      const uint32_t src = t.c_src[k], a = t.s_att[fr] + 1u, p = sb_m + pm;
+      t.s_att[fr] = a;
+      t.s_tatt[fr] = t0;
+      t.s_w[fr] |= kRetxBit;
+      atomicAdd(&t.pend_by[src], 1u);
+      ++nretx;
+      if (p < cap) {
+        m_src[p] = src; m_dst[p] = t.c_dst[k]; m_seq[p] = (fr << 4) | a; m_size[p] = t.s_wire[fr]; m_t[p] = t0;
+      } else {
+        atomicOr(&sc->err, ERR_CAP_M);
+      }
+      if (!t.s_tq[fr]) {
+        t.s_tq[fr] = 1;
+        t.pend[list][sb_p + pp + e++] = fr;
+      }
+    }
     if (go) {
-      uint32_t sid = head, sent = 0, qd = 0, e = 0;
+      uint32_t sid = head, sent = 0, qd = 0;
       const uint32_t src = t.c_src[k], dst = t.c_dst[k];
       while (sent < go) {
         const uint32_t nx = t.s_next[sid];
@@ -718,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
             ++qd;
           }
           t.s_tatt[sid] = ts;
-          const uint32_t p = sb_m + pm + sent;
+          const uint32_t p = sb_m + pm + nfr + sent;
           if (p < cap) {
             m_src[p] = src; m_dst[p] = dst; m_seq[p] = seq; m_size[p] = t.s_wire[sid]; m_t[p] = ts;
           } else {

@@ -124,8 +124,8 @@ def _run_windows(s, until_ms, step_ms=10):
 
 
 def case_ack_clean(b):
-    """The data arrives at 10 ms; its ACK leaves at the next window start (20 ms) and arrives at
-    30 ms, before the 200 ms timer: nothing is retransmitted."""
+    """The data arrives at 10 ms; its ACK leaves then (a late send from the reaction after that
+    window) and arrives at 20 ms, before the 200 ms timer: nothing is retransmitted."""
     s = sim(b)
     s.tcp_enable(acks=True)
     for g in range(4):
@@ -133,7 +133,7 @@ def case_ack_clean(b):
     s.tcp_send([0], [1], [0], [100], [0])
     d = _run_windows(s, 400)
     acks = (d["seq"] & A.TCP_ACK_BIT) != 0
-    assert d["t_deliver"][~acks].tolist() == [10 * MS] and d["t_deliver"][acks].tolist() == [30 * MS]
+    assert d["t_deliver"][~acks].tolist() == [10 * MS] and d["t_deliver"][acks].tolist() == [20 * MS]
     assert d["src"][acks].tolist() == [1] and d["dst"][acks].tolist() == [0]
     assert d["size"][acks].tolist() == [52]
     st, t = s.tcp_writes()
@@ -179,7 +179,7 @@ def case_ack_data_lost(b):
 
 def case_ack_slow_path(b):
     """A 300 ms data path is slower than the 200 ms timer: a spurious retransmission leaves at 200 ms
-    (arriving at 500 ms); the original's ACK (sent at 310, arriving at 315 ms) stops the next timer."""
+    (arriving at 500 ms); the original's ACK (sent at 300, arriving at 305 ms) stops the next timer."""
     s = sim(b)
     s.tcp_enable(acks=True)
     s.set_shape(0, make_shape(latency_ns=300 * MS))
@@ -188,7 +188,7 @@ def case_ack_slow_path(b):
     d = _run_windows(s, 1000)
     data = (d["seq"] & A.TCP_ACK_BIT) == 0
     assert d["t_deliver"][data].tolist() == [300 * MS, 500 * MS]
-    assert sorted(d["t_deliver"][~data].tolist()) == [315 * MS, 515 * MS]
+    assert sorted(d["t_deliver"][~data].tolist()) == [305 * MS, 505 * MS]
     st, t = s.tcp_writes()
     assert st[0] == A.TCP_DELIVERED and t[0] == 300 * MS
     assert s.tcp_stats()["retransmissions"] == 1

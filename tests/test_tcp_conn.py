@@ -48,17 +48,17 @@ def data_arrivals(out, src):
 
 
 def case_slow_start(b):
-    """100 segments on one connection, 10 ms each way: IW10 at 0; every ACK round (a data
-    arrival at 10 ms + k*22 ms, its ACK leaving at the next window start, 11 ms back) doubles the
-    window: 10, 20, 40, then the last 30."""
+    """100 segments on one connection, 10 ms each way: IW10 at 0; every ACK round (a data arrival
+    at 10 ms + k*20 ms, its ACK leaving as it arrives and back 10 ms later, where the segments it
+    lets out leave) doubles the window: 10, 20, 40, then the last 30 - 20 ms rounds, one RTT each."""
     s = sim(b)
     s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS)] * 2)
     c = s.tcp_connect([0], [1])
     assert list(c) == [0]
     out = run(s, 100 * MS, writes={0: [(0, 100 * MSS)]})
-    assert data_arrivals(out, 0) == [(10 * MS, 10), (32 * MS, 20), (54 * MS, 40), (76 * MS, 30)]
+    assert data_arrivals(out, 0) == [(10 * MS, 10), (30 * MS, 20), (50 * MS, 40), (70 * MS, 30)]
     st, t = s.tcp_writes()
-    assert list(st) == [A.TCP_DELIVERED] and list(t) == [76 * MS]
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [70 * MS]
     cs = s.tcp_conns()
     assert cs["acked"].tolist() == [100] and cs["cwnd"].tolist() == [110]
     assert cs["flight"].tolist() == [0] and cs["queued"].tolist() == [0]
@@ -69,18 +69,18 @@ def case_timeout_then_congestion_avoidance(b):
     """The first 10 segments are lost (the link drops everything until 300 ms). The 200 ms timeout
     starts a loss episode: ssthresh 5, cwnd 1, all 10 marked lost and only the oldest resent (lost
     again); its 600 ms timeout is the same episode (ssthresh stays 5) and its third attempt gets
-    through (610 ms). Every ACK round then resends under cwnd: 2 (cwnd 2), 4 (4), then cwnd 5 in
-    congestion avoidance: the last 3 lost ones and 2 new (676 ms), 6 (698 ms), the last 2 (720 ms)."""
+    through (610 ms). Every 20 ms ACK round then resends under cwnd: 2 (cwnd 2), 4 (4), then cwnd 5
+    in congestion avoidance: the last 3 lost ones and 2 new (670 ms), 6 (690 ms), the last 2 (710 ms)."""
     s = sim(b)
     s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS, loss=100.0), make_shape(latency_ns=10 * MS)])
     s.tcp_connect([0], [1])
     out = run(s, 300 * MS, writes={0: [(0, 20 * MSS)]})
     s.set_shape(0, make_shape(latency_ns=10 * MS))
     out += run(s, 750 * MS)
-    assert data_arrivals(out, 0) == [(610 * MS, 1), (632 * MS, 2), (654 * MS, 4), (676 * MS, 5), (698 * MS, 6),
-                                     (720 * MS, 2)]
+    assert data_arrivals(out, 0) == [(610 * MS, 1), (630 * MS, 2), (650 * MS, 4), (670 * MS, 5), (690 * MS, 6),
+                                     (710 * MS, 2)]
     st, t = s.tcp_writes()
-    assert list(st) == [A.TCP_DELIVERED] and list(t) == [720 * MS]
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [710 * MS]
     cs = s.tcp_conns()
     assert cs["cwnd"].tolist() == [7] and cs["acked"].tolist() == [20]
     assert cs["flight"].tolist() == [0] and cs["queued"].tolist() == [0]
@@ -90,7 +90,7 @@ def case_timeout_then_congestion_avoidance(b):
 
 def case_loss_recovery_under_cwnd(b):
     """DESIGN.md 2.11b's hand case: 10 segments lost once (the link drops everything until 100 ms).
-    The 200 ms timeout marks all 10 lost; they are resent 1, 2, 4, 3 per 22 ms ACK round (cwnd 1,
+    The 200 ms timeout marks all 10 lost; they are resent 1, 2, 4, 3 per 20 ms ACK round (cwnd 1,
     2, 4, then 5 = ssthresh), not all at once."""
     s = sim(b)
     s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS, loss=100.0), make_shape(latency_ns=10 * MS)])
@@ -98,12 +98,38 @@ def case_loss_recovery_under_cwnd(b):
     out = run(s, 100 * MS, writes={0: [(0, 10 * MSS)]})
     s.set_shape(0, make_shape(latency_ns=10 * MS))
     out += run(s, 300 * MS)
-    assert data_arrivals(out, 0) == [(210 * MS, 1), (232 * MS, 2), (254 * MS, 4), (276 * MS, 3)]
+    assert data_arrivals(out, 0) == [(210 * MS, 1), (230 * MS, 2), (250 * MS, 4), (270 * MS, 3)]
     st, t = s.tcp_writes()
-    assert list(st) == [A.TCP_DELIVERED] and list(t) == [276 * MS]
+    assert list(st) == [A.TCP_DELIVERED] and list(t) == [270 * MS]
     cs = s.tcp_conns()
     assert cs["cwnd"].tolist() == [6] and cs["acked"].tolist() == [10] and cs["flight"].tolist() == [0]
     assert s.tcp_stats()["retransmissions"] == 10
+    s.close()
+
+
+def case_fast_retransmit(b):
+    """One mid-flight loss is recovered in about one RTT, not one RTO. Ten 1-segment writes leave
+    at 0..9 ms (10 ms each way); the sender's link drops everything during [3, 4) ms, so segment 3
+    alone is lost. The ACKs of 4, 5 and 6 (arriving at 24, 25, 26 ms) are three duplicate ACKs: at
+    26 ms segment 3 is resent (ssthresh = max(flight 4 / 2, 2) = 2, cwnd 2) and arrives at 36 ms -
+    the 200 ms timer would have resent it at 203 ms. cwnd then grows in congestion avoidance to 3."""
+    s = sim(b)
+    s.set_shapes([0, 1], [make_shape(latency_ns=10 * MS)] * 2)
+    s.tcp_connect([0], [1])
+    writes = {i * MS: [(0, MSS)] for i in range(10)}
+    out = run(s, 3 * MS, writes=writes)
+    s.set_shape(0, make_shape(latency_ns=10 * MS, loss=100.0))
+    out += run(s, 4 * MS, writes=writes)
+    s.set_shape(0, make_shape(latency_ns=10 * MS))
+    out += run(s, 100 * MS, writes=writes)
+    assert data_arrivals(out, 0) == [((i + 10) * MS, 1) for i in (0, 1, 2, 4, 5, 6, 7, 8, 9)] + [(36 * MS, 1)]
+    retx = [(t, d["seq"][(d["src"] == 0)].tolist()) for t, d in out if np.any((d["src"] == 0) & ((d["seq"] & 15) != 0))]
+    assert retx == [(36 * MS, [(3 << 4) | 1])]        # the resent attempt, delivered in the window [36, 37) ms
+    st, t = s.tcp_writes()
+    assert list(st) == [A.TCP_DELIVERED] * 10 and list(t) == [(i + 10) * MS if i != 3 else 36 * MS for i in range(10)]
+    cs = s.tcp_conns()
+    assert cs["cwnd"].tolist() == [3] and cs["acked"].tolist() == [10] and cs["flight"].tolist() == [0]
+    assert s.tcp_stats()["retransmissions"] == 1
     s.close()
 
 
@@ -142,7 +168,8 @@ def case_errors(b):
     s.close()
 
 
-CASES = [case_slow_start, case_timeout_then_congestion_avoidance, case_loss_recovery_under_cwnd, case_queued_writes_and_reset,
+CASES = [case_slow_start, case_timeout_then_congestion_avoidance, case_loss_recovery_under_cwnd, case_fast_retransmit,
+         case_queued_writes_and_reset,
          case_errors]
 
 
@@ -187,7 +214,9 @@ def random_conn_run(b, seed, n=16, windows=160):
 def test_conn_random_oracle_properties(oracle):
     r = random_conn_run(oracle, 1)
     st, _ = r["writes"]
-    assert np.count_nonzero(st == A.TCP_DELIVERED) > 0.6 * len(st)
+    # Reno at 10 % loss holds cwnd near 1.22 / sqrt(p) ~ 4 segments (fast retransmit halves it at
+    # every hole), so some writes are still queued behind their connection's window at 160 ms
+    assert np.count_nonzero(st == A.TCP_DELIVERED) > 0.5 * len(st)
     cs = r["conns"]
     assert np.all(cs["cwnd"] >= 1) and cs["acked"].sum() > 0
 
