@@ -196,6 +196,14 @@ __host__ __device__ inline void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 __host__ __device__ inline uint32_t shard_of(uint32_t g, uint32_t N, uint32_t S) {
   return (uint32_t)((((uint64_t)g + 1) * S - 1) / N);
 }
+// The same division by a multiply-high: inv = floor(2^64 / N) + 1 makes floor(x * inv / 2^64) =
+// floor(x / N) exact for every x with x * N < 2^64 (x = (g + 1) S - 1 < 2^38 here). A 64-bit integer
+// division is a ~100-instruction software routine on the GPU; per routed copy it made a sharded
+// token bucket 40 % slower than the same shard alone (20.6 -> 28-30 us at 50k instances).
+inline uint64_t shard_inv(uint32_t N) { return N ? (uint64_t)(((unsigned __int128)1 << 64) / N) + 1 : 0; }
+__device__ __forceinline__ uint32_t shard_of_inv(uint32_t g, uint32_t S, uint64_t inv) {
+  return (uint32_t)__umul64hi(((uint64_t)g + 1) * S - 1, inv);
+}
 
 // One-sided agent-scope fences: a producer that publishes data through a counter needs only the
 // release half (its XCD's L2 written back), a consumer only the acquire half (stale lines dropped);

@@ -241,7 +241,11 @@ struct Queues {
   }
 };
 
-struct Geo { uint32_t N, S, shard; };
+struct Geo {
+  uint32_t N, S, shard;
+  uint64_t inv;  // shard_inv(N)
+};
+static Geo make_geo(const Dev& d) { return Geo{d.N, d.S, d.shard, shard_inv(d.N)}; }
 
 // Queue of a stage-D record (its t is the delivery time): delivered now (here, or on the receiver's
 // shard through the exchange) or later from this shard's wheel. A record crosses shards only in the
@@ -250,7 +254,7 @@ struct Geo { uint32_t N, S, shard; };
 __device__ __forceinline__ int qid_stage_d(const Geo& g, uint32_t dst, int64_t t, int64_t t_end) {
   if (t >= t_end) return Q_L;
   if (g.S > 1) {
-    const uint32_t p = shard_of(dst, g.N, g.S);
+    const uint32_t p = shard_of_inv(dst, g.S, g.inv);
     if (p != g.shard) return Q_X0 + (int)p;
   }
   return Q_D;
@@ -1136,9 +1140,20 @@ __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* histx, con
   __syncthreads();
 }
 
+// One key per bucket (a fine group-by of <= 2^kMaxDigitBits keys): pass 2's buckets are the groups,
+// so the scatter writes the final arrays and block 0 the key offsets and segment lists that pass 3
+// (k_bkt_sort, then skipped) would have written.
+struct BktDirect {
+  uint32_t *off = nullptr, *off2 = nullptr, *vout2 = nullptr, *medium = nullptr;
+  LargeSeg* large = nullptr;
+  DevScalars* sc = nullptr;
+  uint32_t medium_above = 0, on = 0;
+};
+
 // pass 2: scatter (key, physical index) into bucket order (kout, vout); ranks from LDS atomics.
 __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
-                                                        const uint32_t* histx, const uint32_t* tot, uint32_t* bstart) {
+                                                        const uint32_t* histx, const uint32_t* tot, uint32_t* bstart,
+                                                        BktDirect g) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   uint32_t start, end;
@@ -1146,8 +1161,28 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
   if (start == end && blockIdx.x != 0) return;  // block-uniform: nothing to place
   bkt_bases(B, histx, tot, base, part);
   if (blockIdx.x == 0) {  // block 0's bases are the bucket starts (its per-block offsets are 0)
+    const uint32_t total = base[B - 1] + tot[B - 1];
     for (uint32_t d = threadIdx.x; d < B; d += kBlock) bstart[d] = base[d];
-    if (threadIdx.x == 0) bstart[B] = base[B - 1] + tot[B - 1];
+    if (threadIdx.x == 0) bstart[B] = total;
+    if (g.on) {  // the key offsets and segment lists (bkt_global_offsets' outputs)
+      for (uint32_t k = threadIdx.x; k < B; k += kBlock) {
+        const uint32_t run = base[k], len = tot[k];
+        g.off[k] = run;
+        if (g.off2) g.off2[k] = run;
+        if (len > (uint32_t)kTile) {
+          LargeSeg L;
+          L.seg = k; L.start = run; L.len = len; L.pad = 0;
+          g.large[atomicAdd(&g.sc->n_large, 1u)] = L;
+          atomicMax(&g.sc->max_large, len);
+        } else if (len > g.medium_above) {
+          g.medium[atomicAdd(&g.sc->n_medium, 1u)] = k;
+        }
+      }
+      if (threadIdx.x == 0) {
+        g.off[B] = total;
+        if (g.off2) g.off2[B] = total;
+      }
+    }
   }
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll], v[kBktUnroll];
@@ -1163,6 +1198,7 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
       const uint32_t pos = atomicAdd(&base[bd.of(k[u])], 1u);
       kout[pos] = k[u];
       vout[pos] = v[u];
+      if (g.vout2) g.vout2[pos] = v[u];
     }
   }
 }
@@ -3247,6 +3283,48 @@ __device__ __forceinline__ uint64_t* wide_sort(uint64_t x, uint64_t* a, uint64_t
   return src;
 }
 
+// Bucket sort of one packed key per thread (key >> 42 = t_send - min, below it seq and the position,
+// so keys are distinct) for send times spread over < 2^22 ns: bucket = (t_send - min) >> sh, with
+// sh the least shift that leaves < 1024 buckets. One LDS atomic per key claims a slot in its bucket,
+// a block scan of the bucket counts places the buckets, and each key ranks itself among its bucket
+// mates (a few for send times spread evenly). Writes inv[rank] = this thread's position and raises
+// *tie when two keys share (t_send, seq). Returns false (nothing written) when some bucket holds more
+// than kWideBucketMax keys - clustered send times - where the merge sort above is the better form.
+constexpr uint32_t kWideBucketMax = 32;
+__device__ __forceinline__ bool wide_bucket_sort(uint64_t key, bool live, uint32_t sh, uint32_t* cnt, uint64_t* tmp,
+                                                 uint32_t* inv, uint32_t* red, uint32_t* big, uint32_t* tie) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b = live ? (uint32_t)(key >> (42 + sh)) : 0u;
+  cnt[tid] = 0u;
+  __syncthreads();
+  const uint32_t slot = live ? atomicAdd(&cnt[b], 1u) : 0u;
+  __syncthreads();
+  const uint32_t c = cnt[tid];
+  if (c > kWideBucketMax) *big = 1u;
+  uint32_t tot;
+  const uint32_t start = wide_excl_scan(c, red, tot);  // its barriers publish *big
+  if (*big) return false;                             // block-uniform
+  cnt[tid] = start;
+  __syncthreads();
+  const uint32_t s = live ? cnt[b] : 0u;
+  const uint32_t e = live ? (b + 1u < (uint32_t)kWide ? cnt[b + 1] : tot) : 0u;
+  if (live) tmp[s + slot] = key;
+  __syncthreads();
+  if (live) {
+    uint32_t r = 0;
+    bool t = false;
+    for (uint32_t j = s; j < e; ++j) {
+      const uint64_t y = tmp[j];
+      r += y < key ? 1u : 0u;
+      t |= y != key && (y >> 10) == (key >> 10);
+    }
+    inv[s + r] = tid;
+    if (t) *tie = 1u;
+  }
+  __syncthreads();
+  return true;
+}
+
 #ifdef TGSIM_PHASE_PROF
 // debug builds: per block (its last sender) of the last k_shape_seq_wide launch, s_memrealtime at:
 // start, sorted, K ready, copies drawn, decided, appended, end
@@ -3266,7 +3344,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
   __shared__ uint32_t Ms[kWide], Md[kWide], Mz[kWide], Mi[kWide];
   __shared__ uint32_t red[kWideWaves];
   __shared__ int64_t red64[kWideWaves], rmin[kWideWaves], rmax[kWideWaves];
-  __shared__ uint32_t s_flag, s_stage_a, s_tot[3];
+  __shared__ uint32_t s_flag, s_stage_a, s_big, s_tot[3];
   DevScalars* sc = a.Q.sc;
   const int64_t t_end = sc->t_end;
   const uint32_t tid = threadIdx.x;
@@ -3282,7 +3360,7 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     const uint32_t h0 = hoff ? hoff[l] : 0u, h1 = hoff ? hoff[l + 1] : 0u, n0 = h1 - h0;
     // block-uniform: the closed form needs queue tracking without HTB or correlation
     const bool elig = hoff && a.heavy.of(l) && !(sh.flags & (kShCorr | kShLimited)) && n0 <= (uint32_t)kWide;
-    if (tid == 0) { s_flag = 0; s_stage_a = 0; }
+    if (tid == 0) { s_flag = 0; s_stage_a = 0; s_big = 0; }
     // every load up front, two dependent levels: (message index, due record index), then (the
     // message's fields, the due record)
     uint32_t i = 0, hx = 0;
@@ -3332,11 +3410,15 @@ __global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uin
     WIDE_PH(8);
     if (packed) {
       const uint64_t key = tid < n ? ((uint64_t)(ts - mn) << 42) | ((uint64_t)sq << 10) | tid : ~0ull;
-      const uint64_t* srt = wide_sort(key, S1, reinterpret_cast<uint64_t*>(K));
+      const uint32_t span = (uint32_t)(mx - mn), bits = span ? 32u - (uint32_t)__builtin_clz(span) : 0u;
+      const uint32_t sh = bits > 10u ? bits - 10u : 0u;  // (span >> sh) < 1024
+      if (!wide_bucket_sort(key, tid < n, sh, S2, S1, S3, red, &s_big, &s_flag)) {  // block-uniform
+        const uint64_t* srt = wide_sort(key, S1, reinterpret_cast<uint64_t*>(K));
+        S3[tid] = (uint32_t)(srt[tid] & 1023u);
+        if (tid > 0 && tid < n && (srt[tid] >> 10) == (srt[tid - 1] >> 10)) s_flag = 1u;  // a (t_send, seq) tie
+        __syncthreads();
+      }
       WIDE_PH(9);
-      S3[tid] = (uint32_t)(srt[tid] & 1023u);
-      if (tid > 0 && tid < n && (srt[tid] >> 10) == (srt[tid - 1] >> 10)) s_flag = 1u;  // a (t_send, seq) tie
-      __syncthreads();
     }
     if (!packed || s_flag) {  // block-uniform
       if (tid < n) {
@@ -4764,8 +4846,9 @@ static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
   return std::max<uint32_t>(w, 1u);
 }
 
-// Passes 1-2 of the bucketed group-by: (keys1, vals1) in bucket order, bucket totals in d.tot.
-static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
+// Passes 1-2 of the bucketed group-by: (keys1, vals1) in bucket order, bucket totals in d.tot; with
+// g.on (one key per bucket) the final (keys0, vals0) and the key offsets instead.
+static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B, const BktDirect& g = BktDirect()) {
   {
     ProfScope ps_(d, KID_BKT_HIST);
     hipLaunchKernelGGL(k_bkt_hist, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.sc, bd, B, d.hist);
@@ -4776,8 +4859,8 @@ static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B
   }
   {
     ProfScope ps_(d, KID_BKT_SCATTER);
-    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bd, B,
-                       d.histx, d.tot, d.bstart);
+    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, g.on ? d.keys0 : d.keys1,
+                       g.on ? d.vals0 : d.vals1, bd, B, d.histx, d.tot, d.bstart, g);
   }
   return hipGetLastError();
 }
@@ -4797,16 +4880,21 @@ static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t m
   if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
   const uint32_t B = (K + (1u << bs) - 1) >> bs;
   const BktDiv bd = bkt_div(1u << bs);
+  *keys = d.keys0;
+  *vals = d.vals0;
+  if (bs == 0) {  // one key per bucket: the scatter writes the groups and the offsets (no pass 3)
+    BktDirect g;
+    g.on = 1; g.off = d.seg_off; g.off2 = off2; g.vout2 = vals_copy; g.medium = d.medium; g.large = d.large;
+    g.sc = d.sc; g.medium_above = medium_above;
+    return bkt_partition(d, src, bd, B, g);
+  }
   TG_CHECK(bkt_partition(d, src, bd, B));
   {
     ProfScope ps_(d, KID_BKT_SORT);
     hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bd, B, K,
                        d.tot, d.seg_off, off2, medium_above, d.medium, d.large, d.sc, vals_copy);
   }
-  TG_CHECK(hipGetLastError());
-  *keys = d.keys0;
-  *vals = d.vals0;
-  return hipSuccess;
+  return hipGetLastError();
 }
 
 static BktSrc bkt_queue(Dev& d, int q) {
@@ -4829,7 +4917,7 @@ static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const ui
 // and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
 static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
-  p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = Geo{d.N, d.S, d.shard}; p.Q = make_queues(d);
+  p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = make_geo(d); p.Q = make_queues(d);
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= kMaxBins (bkt_width_fused)
@@ -4922,7 +5010,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
   if (n_dev) n_staged = d.cap_msgs;  // device-counted: size the launches for the capacity (grid-stride)
   HeavyOut ho;
   ho.hv = n_staged ? d.heavy : Heavy{};  // H feeds only the staged messages' sequential lane
-  ho.geo = Geo{d.N, d.S, d.shard}; ho.H = d.H; ho.hkeys = d.hkeys; ho.hvals = d.hvals; ho.hcap = d.h_cap;
+  ho.geo = make_geo(d); ho.H = d.H; ho.hkeys = d.hkeys; ho.hvals = d.hvals; ho.hcap = d.h_cap;
   ho.lo = d.lo;
   if (!n_staged) {
     ProfScope ps_(d, KID_EXTRACT);
@@ -4935,7 +5023,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     a.src = d.m_src; a.dst = d.m_dst; a.seq = d.m_seq; a.size = d.m_size; a.t = d.m_t; a.n = n_staged; a.n_dev = n_dev;
     a.status = d.status; a.shape = d.shape; a.ipf = d.ipf; a.en_bits = d.en_bits; a.rule_off = d.rule_off;
     a.rules = d.rules; a.lo = d.lo; a.nloc = d.nloc; a.data_net = d.data_net; a.data_mask = d.data_mask;
-    a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = Geo{d.N, d.S, d.shard}; a.Q = Q;
+    a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = make_geo(d); a.Q = Q;
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
     a.heavy = d.heavy;

@@ -136,12 +136,11 @@ __device__ __forceinline__ uint32_t tcp_arrived(TcpDev& t, uint32_t sw, int64_t 
     t.w_tarr[w] = arr;
     return 1u;
   }
-  // running max, then the count; the last segment reads the max back after its count (the fences
-  // order each thread's max before its count, and the counts are totally ordered)
+  // running max, then the count as one acq_rel RMW (the hand-off: it releases this thread's max and,
+  // for the last segment, acquires every other segment's; the counts are totally ordered); the last
+  // segment reads the max back
   atomicMax(reinterpret_cast<long long*>(&t.w_tmax[w]), (long long)arr);
-  fence_release_agent();
-  if (atomicSub(&t.w_rem[w], 1u) != 1u) return 0u;
-  fence_acquire_agent();
+  if (__hip_atomic_fetch_sub(&t.w_rem[w], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != 1u) return 0u;
   const long long m = atomicMax(reinterpret_cast<long long*>(&t.w_tmax[w]), (long long)arr);
   t.w_tarr[w] = m > (long long)arr ? (int64_t)m : arr;
   return 1u;

@@ -5,7 +5,8 @@
 #   tools/gpu.sh bench <out> <workload> [bench args]   one bench line
 #   tools/gpu.sh evidence <out> <workload> <round> [bench args]
 #        rocprofv3 kernel trace + stats of the bench (<w>_kernel_stats.csv, <w>_trace_summary.txt),
-#        FETCH_SIZE / WRITE_SIZE passes (one counter per run, the guide's HBM section) -> hash-stamped
+#        FETCH_SIZE / WRITE_SIZE passes over every tgsim kernel (one counter per run, the guide's HBM
+#        section) -> hash-stamped
 #        pmc_traffic[_<w>].json, then the bench line (bench_<w>.json) - all into
 #        gpurun_out/<out>/profiles/<round>/ (only gpurun_out/ comes back from the box: copy that
 #        directory into profiles/<round>/ here)
@@ -39,7 +40,7 @@ evidence)
   python3 tools/trace_summary.py $OUT/prof_$W/run_kernel_trace.csv --last 20 --marker k_window_start > $P/${W}_trace_summary.txt 2>&1
   head -16 $P/${W}_trace_summary.txt
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KR" -d $OUT/pmc_${W}_$c -o run --output-format csv \
+    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "k_" -d $OUT/pmc_${W}_$c -o run --output-format csv \
       -- python3 -u $B --steps 5 > $OUT/pmc_${W}_$c.log 2>&1 || { echo PMC_FAIL $c; tail -5 $OUT/pmc_${W}_$c.log; exit 1; }
   done
   python3 tools/pmc_traffic.py $OUT/pmc_${W}_FETCH_SIZE/run_counter_collection.csv $OUT/pmc_${W}_WRITE_SIZE/run_counter_collection.csv \
