@@ -4847,7 +4847,7 @@ static uint32_t bkt_width_fused(const Dev& d, uint32_t K) {
 }
 
 // Passes 1-2 of the bucketed group-by: (keys1, vals1) in bucket order, bucket totals in d.tot; with
-// g.on (one key per bucket) the final (keys0, vals0) and the key offsets instead.
+// g.on (one key per bucket) that is the final grouping, and the scatter writes the key offsets too.
 static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B, const BktDirect& g = BktDirect()) {
   {
     ProfScope ps_(d, KID_BKT_HIST);
@@ -4859,8 +4859,8 @@ static hipError_t bkt_partition(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B
   }
   {
     ProfScope ps_(d, KID_BKT_SCATTER);
-    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, g.on ? d.keys0 : d.keys1,
-                       g.on ? d.vals0 : d.vals1, bd, B, d.histx, d.tot, d.bstart, g);
+    hipLaunchKernelGGL(k_bkt_scatter, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, src, d.keys1, d.vals1, bd, B,
+                       d.histx, d.tot, d.bstart, g);
   }
   return hipGetLastError();
 }
@@ -4872,7 +4872,8 @@ static hipError_t bkt_local(Dev& d, const BktSrc& src, BktDiv bd, uint32_t B) {
   return hipGetLastError();
 }
 
-// Group a batch by key (unstable; see k_bkt_hist): results in (d.keys0, d.vals0), segment offsets in
+// Group a batch by key (unstable; see k_bkt_hist): results in *keys / *vals ((d.keys0, d.vals0), or
+// (d.keys1, d.vals1) for one key per bucket), segment offsets in
 // d.seg_off (and off2), medium / large lists in d.medium / d.large. K <= 2^24 (checked at create).
 static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t medium_above, uint32_t* off2,
                                uint32_t** keys, uint32_t** vals, bool fine = false, uint32_t* vals_copy = nullptr) {
@@ -4880,9 +4881,10 @@ static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t m
   if (bs > kBktMaxKeyBits) return hipErrorInvalidValue;
   const uint32_t B = (K + (1u << bs) - 1) >> bs;
   const BktDiv bd = bkt_div(1u << bs);
-  *keys = d.keys0;
-  *vals = d.vals0;
-  if (bs == 0) {  // one key per bucket: the scatter writes the groups and the offsets (no pass 3)
+  if (bs == 0) {  // one key per bucket: the scatter writes the groups and the offsets (no pass 3);
+    // the result stays in (keys1, vals1) - the source may be (keys0, vals0) (k_keys_corr's output)
+    *keys = d.keys1;
+    *vals = d.vals1;
     BktDirect g;
     g.on = 1; g.off = d.seg_off; g.off2 = off2; g.vout2 = vals_copy; g.medium = d.medium; g.large = d.large;
     g.sc = d.sc; g.medium_above = medium_above;
@@ -4894,6 +4896,8 @@ static hipError_t group_by_bkt(Dev& d, const BktSrc& src, uint32_t K, uint32_t m
     hipLaunchKernelGGL(k_bkt_sort, dim3(B), dim3(kBlock), 0, d.stream, d.keys1, d.vals1, d.keys0, d.vals0, bd, B, K,
                        d.tot, d.seg_off, off2, medium_above, d.medium, d.large, d.sc, vals_copy);
   }
+  *keys = d.keys0;
+  *vals = d.vals0;
   return hipGetLastError();
 }
 
