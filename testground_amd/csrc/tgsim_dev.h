@@ -270,6 +270,10 @@ struct Dev {
   tgsim_record* H = nullptr;
   uint32_t *hkeys = nullptr, *hvals = nullptr;
   uint32_t h_cap = 0;
+  // the H list's own group-by (it shares its launches with the deferred messages' one): output
+  // (hkeys1, hvals1), per-sender offsets hoff [nloc + 1], partition tables as hist / histx / tot / bstart
+  uint32_t *hkeys1 = nullptr, *hvals1 = nullptr, *hoff = nullptr;
+  uint32_t *hhist = nullptr, *hhistx = nullptr, *htot = nullptr, *hbstart = nullptr;
   uint8_t* seq_done = nullptr;     // [nloc] k_shape_seq_wide decided the sender's deferred messages
 
   // staged messages (SoA) + per-message status

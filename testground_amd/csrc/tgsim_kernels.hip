@@ -1124,7 +1124,8 @@ __global__ __launch_bounds__(kBlock) void k_local_hist(BktSrc srcD, DevScalars* 
 
 // Bucket bases for this block: exclusive scan of the bucket totals + this block's offset in each.
 __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* histx, const uint32_t* tot, uint32_t* base,
-                                          uint32_t* part) {
+                                          uint32_t* part, uint32_t bid = 0xFFFFFFFFu) {
+  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (B + kBlock - 1) / kBlock;
   const uint32_t d0 = tid * per;
@@ -1134,7 +1135,7 @@ __device__ __forceinline__ void bkt_bases(uint32_t B, const uint32_t* histx, con
   uint32_t run = block_excl_scan(s, part, total);
   for (uint32_t k = 0; k < per && d0 + k < B; ++k) {
     const uint32_t tk = tot[d0 + k];
-    base[d0 + k] = run + (histx && tk ? histx[(size_t)(d0 + k) * kRadixBlocks + blockIdx.x] : 0u);
+    base[d0 + k] = run + (histx && tk ? histx[(size_t)(d0 + k) * kRadixBlocks + bid] : 0u);
     run += tk;
   }
   __syncthreads();
@@ -1147,20 +1148,21 @@ struct BktDirect {
   uint32_t *off = nullptr, *off2 = nullptr, *vout2 = nullptr, *medium = nullptr;
   LargeSeg* large = nullptr;
   DevScalars* sc = nullptr;
-  uint32_t medium_above = 0, on = 0;
+  uint32_t medium_above = 0, on = 0, lists = 1;  // lists = 0: no medium / large segment lists
 };
 
 // pass 2: scatter (key, physical index) into bucket order (kout, vout); ranks from LDS atomics.
-__global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
-                                                        const uint32_t* histx, const uint32_t* tot, uint32_t* bstart,
-                                                        BktDirect g) {
+// bid: the partition block (the pass may share its launch).
+__device__ __forceinline__ void bkt_scatter_body(const BktSrc& src, uint32_t* kout, uint32_t* vout, const BktDiv& bd,
+                                                 uint32_t B, const uint32_t* histx, const uint32_t* tot,
+                                                 uint32_t* bstart, const BktDirect& g, uint32_t bid) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   uint32_t start, end;
-  bkt_block_range(src, start, end);
-  if (start == end && blockIdx.x != 0) return;  // block-uniform: nothing to place
-  bkt_bases(B, histx, tot, base, part);
-  if (blockIdx.x == 0) {  // block 0's bases are the bucket starts (its per-block offsets are 0)
+  bkt_block_range(src, start, end, bid);
+  if (start == end && bid != 0) return;  // block-uniform: nothing to place
+  bkt_bases(B, histx, tot, base, part, bid);
+  if (bid == 0) {  // block 0's bases are the bucket starts (its per-block offsets are 0)
     const uint32_t total = base[B - 1] + tot[B - 1];
     for (uint32_t d = threadIdx.x; d < B; d += kBlock) bstart[d] = base[d];
     if (threadIdx.x == 0) bstart[B] = total;
@@ -1169,6 +1171,7 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
         const uint32_t run = base[k], len = tot[k];
         g.off[k] = run;
         if (g.off2) g.off2[k] = run;
+        if (!g.lists) continue;
         if (len > (uint32_t)kTile) {
           LargeSeg L;
           L.seg = k; L.start = run; L.len = len; L.pad = 0;
@@ -1201,6 +1204,37 @@ __global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* ko
       if (g.vout2) g.vout2[pos] = v[u];
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bkt_scatter(BktSrc src, uint32_t* kout, uint32_t* vout, BktDiv bd, uint32_t B,
+                                                        const uint32_t* histx, const uint32_t* tot, uint32_t* bstart,
+                                                        BktDirect g) {
+  bkt_scatter_body(src, kout, vout, bd, B, histx, tot, bstart, g, blockIdx.x);
+}
+
+// Two independent one-key-per-bucket group-bys sharing their three launches (blocks split by
+// index): the queue-limit lane's deferred messages and due wheel records, both by local sender
+// (six dependent launches became three).
+struct BktPass {
+  BktSrc src;
+  BktDiv bd;
+  uint32_t B;
+  uint32_t *hist, *histx, *tot, *bstart, *kout, *vout;
+  BktDirect g;
+};
+__global__ __launch_bounds__(kBlock) void k_bkt_hist_pair(BktPass a, BktPass b, DevScalars* sc) {
+  if (blockIdx.x < (uint32_t)kRadixBlocks) bkt_hist_body(a.src, sc, a.bd, a.B, a.hist, blockIdx.x);
+  else bkt_hist_body(b.src, sc, b.bd, b.B, b.hist, blockIdx.x - kRadixBlocks);
+}
+__global__ __launch_bounds__(kRadixBlocks) void k_radix_rows_pair(BktPass a, BktPass b) {
+  if (blockIdx.x < a.B) radix_rows_body(a.src, a.hist, a.histx, a.tot, a.B, blockIdx.x, a.B);
+  else radix_rows_body(b.src, b.hist, b.histx, b.tot, b.B, blockIdx.x - a.B, b.B);
+}
+__global__ __launch_bounds__(kBlock) void k_bkt_scatter_pair(BktPass a, BktPass b) {
+  if (blockIdx.x < (uint32_t)kRadixBlocks)
+    bkt_scatter_body(a.src, a.kout, a.vout, a.bd, a.B, a.histx, a.tot, a.bstart, a.g, blockIdx.x);
+  else
+    bkt_scatter_body(b.src, b.kout, b.vout, b.bd, b.B, b.histx, b.tot, b.bstart, b.g, blockIdx.x - kRadixBlocks);
 }
 
 // pass 3 pieces. bkt_count_keys: the bucket's start / size (sum of the totals before it) and the
@@ -4947,12 +4981,51 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
   uint32_t *keys, *vals;
+  CorrPolicy p;
+  p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
+  BktSrc hs = bkt_queue(d, Q_A);
+  hs.keys = d.hkeys; hs.vals = d.hvals; hs.qc = nullptr; hs.mode = 3; hs.n_ptr = &d.sc->n_hrec; hs.cap = d.h_cap;
+  if (a.heavy.pend && bits_for(d.nloc) <= kMaxDigitBits) {
+    // both group-bys one key per bucket: their passes share three launches; the deferred messages'
+    // values also go to corr_sorted (k_shape_seq_wide orders each sender there in place), the H
+    // list's groups to its own arrays
+    BktPass pc, ph;
+    pc.src = src; pc.bd = bkt_div(1); pc.B = d.nloc; pc.hist = d.hist; pc.histx = d.histx; pc.tot = d.tot;
+    pc.bstart = d.bstart; pc.kout = d.keys1; pc.vout = d.vals1;
+    pc.g.on = 1; pc.g.off = d.seg_off; pc.g.off2 = d.moff; pc.g.vout2 = d.corr_sorted; pc.g.medium = d.medium;
+    pc.g.large = d.large; pc.g.sc = d.sc; pc.g.medium_above = kNoMedium;
+    ph.src = hs; ph.bd = pc.bd; ph.B = d.nloc; ph.hist = d.hhist; ph.histx = d.hhistx; ph.tot = d.htot;
+    ph.bstart = d.hbstart; ph.kout = d.hkeys1; ph.vout = d.hvals1;
+    ph.g.on = 1; ph.g.off = d.hoff; ph.g.sc = d.sc; ph.g.lists = 0;
+    {
+      ProfScope ps_(d, KID_BKT_HIST);
+      hipLaunchKernelGGL(k_bkt_hist_pair, dim3(2 * kRadixBlocks), dim3(kBlock), 0, d.stream, pc, ph, d.sc);
+    }
+    {
+      ProfScope ps_(d, KID_RADIX_ROWS);
+      hipLaunchKernelGGL(k_radix_rows_pair, dim3(2 * d.nloc), dim3(kRadixBlocks), 0, d.stream, pc, ph);
+    }
+    {
+      ProfScope ps_(d, KID_BKT_SCATTER);
+      hipLaunchKernelGGL(k_bkt_scatter_pair, dim3(2 * kRadixBlocks), dim3(kBlock), 0, d.stream, pc, ph);
+    }
+    TG_CHECK(hipGetLastError());
+    TG_CHECK(launch_rest(d, p, d.keys1, d.vals1));
+    const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
+    {
+      ProfScope ps_(d, KID_SHAPE_WIDE);
+      hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
+                         d.hoff, d.hvals1, d.H, d.seq_done);
+    }
+    ProfScope ps_(d, KID_SHAPE_SEQ);
+    hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, d.hoff, d.hvals1,
+                       d.H, d.cor_rho, d.cor_last, d.X, d.seq_done);
+    return hipGetLastError();
+  }
   // with queue tracking the grouped values also go to corr_sorted, where k_shape_seq_wide orders each
   // sender of <= kTile messages in place (the H group-by below reuses the group-by's output arrays)
   TG_CHECK(group_by_bkt(d, src, d.nloc, kNoMedium, d.moff, &keys, &vals, true,
                         a.heavy.pend ? d.corr_sorted : nullptr));
-  CorrPolicy p;
-  p.t = d.m_t; p.seq = d.m_seq; p.sorted = d.corr_sorted;
   if (!a.heavy.pend) {
     ProfScope ps_(d, KID_SEG_SMALL);  // each sender's deferred messages in (t_send, seq) order
     hipLaunchKernelGGL(k_seg_small<CorrPolicy>, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, p, keys, vals,
@@ -4963,8 +5036,6 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   const uint32_t* hoff = nullptr;
   const uint32_t* hidx = nullptr;
   if (a.heavy.pend) {
-    BktSrc hs = bkt_queue(d, Q_A);
-    hs.keys = d.hkeys; hs.vals = d.hvals; hs.qc = nullptr; hs.mode = 3; hs.n_ptr = &d.sc->n_hrec; hs.cap = d.h_cap;
     uint32_t *hk, *hv;
     TG_CHECK(group_by_bkt(d, hs, d.nloc, kNoMedium, nullptr, &hk, &hv, true));
     hoff = d.seg_off;

@@ -1187,7 +1187,11 @@ static int plan_queue_limit(tgsim_ctx* c) {
     if (!d.H) {  // first window that needs the H list: room for every due record of a window
       HIPCK(c, hipStreamSynchronize(d.stream), "sync");
       const size_t cap = (size_t)kNSub * d.subcap;
-      if (dalloc(c, &d.H, cap) || dalloc(c, &d.hkeys, cap) || dalloc(c, &d.hvals, cap)) return TGSIM_ENOMEM;
+      if (dalloc(c, &d.H, cap) || dalloc(c, &d.hkeys, cap) || dalloc(c, &d.hvals, cap) || dalloc(c, &d.hkeys1, cap) ||
+          dalloc(c, &d.hvals1, cap) || dalloc(c, &d.hoff, (size_t)d.nloc + 2) ||
+          dalloc(c, &d.hhist, (size_t)kMaxBins * kRadixBlocks) || dalloc(c, &d.hhistx, (size_t)kMaxBins * kRadixBlocks) ||
+          dalloc(c, &d.htot, kMaxBins) || dalloc(c, &d.hbstart, kMaxBins + 1))
+        return TGSIM_ENOMEM;
       d.h_cap = (uint32_t)cap;
     }
     d.heavy.pend = d.pend;
