@@ -1186,6 +1186,7 @@ __device__ __forceinline__ void bkt_scatter_body(const BktSrc& src, uint32_t* ko
         if (g.off2) g.off2[B] = total;
       }
     }
+    __syncthreads();  // every base read above before the placement's atomics move them
   }
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll], v[kBktUnroll];
