@@ -2081,14 +2081,17 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
     const int intact = !(r->meta & TGSIM_F_CORRUPT);
     otcps* g = &c->tsg[(r->seq & ~TGSIM_TCP_ACK_BIT) >> 4];
     if (r->seq & TGSIM_TCP_ACK_BIT) {
-      /* the first intact ACK of a segment that has not given up settles it (its flight slot) */
-      if (intact && !g->acked && !g->gave_up) {
-        g->acked = 1;
+      /* the first intact ACK of a segment that has not given up settles it (its flight slot); what
+       * the window's ACKs release leaves at the latest intact one's arrival (duplicates included) */
+      if (intact && !g->gave_up) {
         const uint32_t k = c->tw[g->w].conn;
-        if (k != TCP_NOSEG) {
-          c->tc[k].acks++;
-          if (!g->lost) c->tc[k].facks++;  /* a segment marked lost holds no flight slot */
-          if (r->t > c->tc[k].tack) c->tc[k].tack = r->t;
+        if (k != TCP_NOSEG && r->t > c->tc[k].tack) c->tc[k].tack = r->t;
+        if (!g->acked) {
+          g->acked = 1;
+          if (k != TCP_NOSEG) {
+            c->tc[k].acks++;
+            if (!g->lost) c->tc[k].facks++;  /* a segment marked lost holds no flight slot */
+          }
         }
       }
       continue;

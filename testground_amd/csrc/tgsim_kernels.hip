@@ -1574,6 +1574,104 @@ __device__ uint64_t g_chunk_ph[8];
 #else
 #define PB_PH(i) do {} while (0)
 #endif
+// Bucket sort of the packed keys nk (this thread's elements p0 .. p0 + PER - 1, < m real) when they
+// spread evenly: bucket = (key - min) >> sh over 1024 buckets (counts in scA / scB), one LDS atomic
+// per element for its slot, a block scan of the counts, each element's id at its bucket slot in
+// perm, then every element ranks itself among its bucket mates (packed key, then (k2, k3) as the
+// network's ties) and takes its place. Leaves perm = sorted order and k1 restored by element, as
+// packed_bitonic does; returns false - having written only scA / scB and perm - when some bucket
+// holds more than kBucketMax elements (clustered keys: the network is the better form). The network
+// took ~22 us per 1024-key chunk (55 stages, a barrier each: DESIGN.md 5, splitbrain's long inbox).
+constexpr uint32_t kBucketMax = 32;
+constexpr uint32_t kBuckets = 2 * kBlock * sizeof(int64_t) / sizeof(uint32_t);  // scA + scB as u32
+static_assert(kBuckets == 1024, "1024 buckets in scA / scB");
+__device__ __forceinline__ bool packed_bucket(SortSmem& s, uint32_t m, const uint64_t (&nk)[kSpan / kBlock],
+                                              uint32_t p0, uint32_t lo, uint32_t b1, uint64_t mn) {
+  constexpr uint32_t PER = kSpan / kBlock, BPT = kBuckets / kBlock;
+  __shared__ uint32_t s_big;
+  uint64_t kmn = ~0ull, kmx = 0;
+  for (uint32_t u = 0; u < PER; ++u)
+    if (p0 + u < m) { kmn = nk[u] < kmn ? nk[u] : kmn; kmx = nk[u] > kmx ? nk[u] : kmx; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(kmn, o), b = __shfl_xor(kmx, o);
+    kmn = a < kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+  }
+  if ((threadIdx.x & 63) == 0) { s.scA[threadIdx.x >> 6] = (int64_t)kmn; s.scB[threadIdx.x >> 6] = (int64_t)kmx; }
+  if (threadIdx.x == 0) s_big = 0;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) {
+    const uint64_t a = (uint64_t)s.scA[w], b = (uint64_t)s.scB[w];
+    kmn = a < kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+  }
+  __syncthreads();  // scA / scB become the counts
+  const uint64_t d = kmx - kmn;
+  const uint32_t bits = d ? 64u - (uint32_t)__builtin_clzll(d) : 0u;
+  const uint32_t sh = bits > 10u ? bits - 10u : 0u;  // (d >> sh) < 1024
+  uint32_t* C = reinterpret_cast<uint32_t*>(s.scA);
+  for (uint32_t i = 0; i < BPT; ++i) C[threadIdx.x * BPT + i] = 0;
+  __syncthreads();
+  uint32_t bk[PER], sl[PER];
+  for (uint32_t u = 0; u < PER; ++u) {
+    bk[u] = p0 + u < m ? (uint32_t)((nk[u] - kmn) >> sh) : 0u;
+    sl[u] = p0 + u < m ? atomicAdd(&C[bk[u]], 1u) : 0u;
+  }
+  __syncthreads();
+  uint32_t c4 = 0;
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t c = C[threadIdx.x * BPT + i];
+    c4 += c;
+    if (c > kBucketMax) s_big = 1u;
+  }
+  uint32_t tot;
+  uint32_t run = block_excl_scan(c4, s.perm, tot);  // its barriers publish s_big
+  if (s_big) {
+    __syncthreads();  // perm (the scan's scratch) is rewritten by the network's setup
+    return false;     // block-uniform
+  }
+  __syncthreads();  // the scan's reads of perm are done
+  for (uint32_t i = 0; i < BPT; ++i) {
+    const uint32_t c = C[threadIdx.x * BPT + i];
+    C[threadIdx.x * BPT + i] = run;
+    run += c;
+  }
+  uint64_t* kw = s.k1;  // the packed keys, by element
+  for (uint32_t u = 0; u < PER; ++u)
+    if (p0 + u < m) kw[p0 + u] = nk[u];
+  __syncthreads();
+  for (uint32_t u = 0; u < PER; ++u)
+    if (p0 + u < m) s.perm[C[bk[u]] + sl[u]] = p0 + u;
+  __syncthreads();
+  uint32_t pos[PER];
+  for (uint32_t u = 0; u < PER; ++u) {
+    const uint32_t j = p0 + u;
+    pos[u] = 0xFFFFFFFFu;
+    if (j >= m) continue;
+    const uint32_t a = C[bk[u]], e = bk[u] + 1u < kBuckets ? C[bk[u] + 1u] : m;
+    const uint64_t x = nk[u], x2 = s.k2[j];
+    const uint32_t x3 = s.k3[j];
+    uint32_t r = 0;
+    for (uint32_t i = a; i < e; ++i) {
+      const uint32_t q = s.perm[i];
+      const uint64_t y = kw[q];
+      r += (y < x || (y == x && (s.k2[q] < x2 || (s.k2[q] == x2 && s.k3[q] < x3)))) ? 1u : 0u;
+    }
+    pos[u] = a + r;
+  }
+  __syncthreads();  // every bucket read before the places are written
+  const uint64_t m1 = b1 ? (~0ull >> (64u - b1)) : 0ull;
+  for (uint32_t u = 0; u < PER; ++u) {
+    if (pos[u] == 0xFFFFFFFFu) continue;
+    s.perm[pos[u]] = p0 + u;
+    kw[p0 + u] = (lo < 64u ? ((nk[u] >> lo) & m1) : 0ull) + mn;  // k1 restored by element
+  }
+  __syncthreads();
+  return true;
+}
+
 __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
     PB_PH(2);
     // k1's spread over the span: below 2^52 the sort runs on (segment rank | k1 - min | the top
@@ -1634,6 +1732,10 @@ __device__ bool packed_bitonic(SortSmem& s, uint32_t m, uint32_t npad) {
         }
       }
       __syncthreads();  // every k1 read before the packed keys replace them
+      if (packed_bucket(s, m, nk, p0, lo, b1, mn)) {
+        PB_PH(6);
+        return true;
+      }
       for (uint32_t u = 0; u < PER; ++u) {
         const uint32_t j = p0 + u;
         if (j < npad) { kw[j] = nk[u]; s.perm[j] = j < m ? j : 0xFFFFFFFFu; }
@@ -3346,13 +3448,13 @@ __device__ __forceinline__ bool wide_bucket_sort(uint64_t key, bool live, uint32
   if (live) tmp[s + slot] = key;
   __syncthreads();
   if (live) {
-    uint32_t r = 0;
-    bool t = false;
+    uint32_t r = 0, t = 0;  // t: a count, not a bool (see the fast-retransmit walk, tgsim_tcp.hip)
     for (uint32_t j = s; j < e; ++j) {
       const uint64_t y = tmp[j];
       r += y < key ? 1u : 0u;
-      t |= y != key && (y >> 10) == (key >> 10);
+      t += (y != key && (y >> 10) == (key >> 10)) ? 1u : 0u;
     }
+    __asm__ volatile("" : "+v"(t));
     inv[s + r] = tid;
     if (t) *tie = 1u;
   }

@@ -160,15 +160,17 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
       bool ack = false, dup = false;
       if (sq & TGSIM_TCP_ACK_BIT) {
         const uint32_t sid = (sq & ~TGSIM_TCP_ACK_BIT) >> 4;
-        // the first intact ACK of a segment that has not given up frees its connection a flight slot
+        // the first intact ACK of a segment that has not given up frees its connection a flight slot;
+        // what the window's ACKs release leaves at the latest intact one's arrival (every ACK counts
+        // there, so which of a segment's duplicate ACKs claims it does not matter)
         if (!corrupt && t.s_done[sid] != 2) {
           t.s_done[sid] = 1;
-          if (t.n_conn && atomicExch(&t.s_ack1[sid], 1u) == 0u) {
-            const uint32_t k = t.w_conn[t.s_w[sid] & kWMask];
-            if (k != kNoSeg) {
+          const uint32_t k = t.n_conn ? t.w_conn[t.s_w[sid] & kWMask] : kNoSeg;
+          if (k != kNoSeg) {
+            atomicMax(reinterpret_cast<long long*>(&t.c_tack[k]), (long long)ti);
+            if (atomicExch(&t.s_ack1[sid], 1u) == 0u) {
               atomicAdd(&t.c_acks[k], 1u);
               if (!t.s_lost[sid]) atomicAdd(&t.c_fack[k], 1u);  // a segment marked lost holds no slot
-              atomicMax(reinterpret_cast<long long*>(&t.c_tack[k]), (long long)ti);  // what it releases leaves then
             }
           }
         }
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_link(TcpDev t, const uint32_t* _
 //   at a write: t0 = the write times;
 //   after a window: first the window's ACKs (flight, slow start / congestion avoidance) and resets (a
 //     reset connection fails its queued writes at the window's end), t0 = max(the window's latest
-//     first-ACK arrival, horizon) - what the ACKs let out leaves when they arrived, not at the window's
+//     intact ACK arrival, horizon) - what the ACKs let out leaves when they arrived, not at the window's
 //     end; then fast retransmit [EXT RFC 5681 3.2]: once three segments after the oldest outstanding
 //     one have been ACKed (three duplicate ACKs in a cumulative-ACK stack) and it has not, it is resent
 //     at t0 (next attempt; once per segment), ssthresh = max(flight / 2, 2) and cwnd = ssthresh;
@@ -658,10 +660,15 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
           uint32_t u = t.c_una[k];
           while (u != h0 && t.s_done[u]) u = t.s_next[u];
           t.c_una[k] = u;
+
           if (u != h0 && !t.c_broken[k] && !t.s_lost[u] && t.c_fr[k] != u && t.s_att[u] + 1u < t.max_att) {
             const uint32_t ws = t.w_state[t.s_w[u] & kWMask];
             uint32_t dup = 0;
             for (uint32_t x = t.s_next[u]; x != h0 && dup < 3u; x = t.s_next[x]) dup += t.s_done[x] == 1;
+            // the count leaves the loop as a value: this compiler (ROCm 7.2) otherwise reused the exit
+            // test's lane mask of the last iteration for `dup >= 3`, losing it for every lane that left
+            // earlier (a wave of connections where one walks further than another: no fast retransmit)
+            __asm__ volatile("" : "+v"(dup));
             if (dup >= 3u && ws != TGSIM_TCP_TIMEOUT && ws != TGSIM_TCP_REFUSED) {
               fr = u;
               t.c_fr[k] = u;
@@ -693,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
       const uint32_t room = fl < cw && !t.c_broken[k] ? cw - fl : 0u;
       if (room && head != kNoSeg && !t.s_lost[head] && !t.s_done[head]) {  // only new segments from here
         go = min(room, t.c_queued[k]);
-        nent = go;
+        nent += go;
       } else if (room) {  // segments marked lost first: count the sends, give up the hopeless ones
         slow = true;
         uint32_t sid = head;

@@ -531,8 +531,8 @@ def drive_tcp(sim, keep=True, max_windows=100_000):
 
 def _tcp_hand_case(b):
     """2 instances x 1 connection, zero latency, 1 ms windows, 3 chunks of 4 KiB (3 segments each).
-    The SYN leaves at 0 and arrives at 0; its ACK leaves at the next window's start (1 ms) and
-    arrives in [1, 2) ms, so both dials end at that window's end, 2 ms. From the write start at 2 ms
+    The SYN leaves at 0 and arrives at 0; its ACK leaves then (a late send from the reaction) and
+    is delivered in the window [1, 2) ms, so both dials end at that window's end, 2 ms. From the write start at 2 ms
     a connection writes one chunk per reaction while 2 x cwnd (IW10) covers the unACKed segments:
     chunk 0 at 2 ms, 1 at 3 ms, 2 at 4 ms, each delivered in the window it is sent in; every write
     settles DELIVERED and the last conn.Write returned at 4 ms."""
