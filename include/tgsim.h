@@ -253,7 +253,10 @@ int tgsim_advance_async(tgsim_ctx* ctx, int64_t t_end);
 int tgsim_advance_to_barrier(tgsim_ctx* ctx, uint32_t waiter, int64_t offset_ns);
 /* ---- cross-shard transport: one exchange per window, inside tgsim_advance* -----
  * The exchange buffers are peer-major blocks of exchange_cap records; record 0 of a block is a header
- * whose .t holds the count, and only records due in the window cross shards. Blocks travel whole
+ * and only records due in the window cross shards. A block of at least 8 * 64 + 1 records is eight
+ * slices of (exchange_cap - 1) / 8 records, each filled by the producers of one XCD, and the header's
+ * eight 32-bit words are the slices' counts; a smaller block is one slice whose count is the header's
+ * .t. The layout is the library's own: a transport only moves whole blocks. Blocks travel whole
  * (their capacity is the device-known bound), so no count is read back by the host.
  * Native: RCCL over xGMI, one communicator rank per shard, owned by the ctx. unique_id comes from
  * tgsim_comm_unique_id on one rank and is distributed by the caller; tgsim_comm_init is collective
@@ -286,7 +289,7 @@ int tgsim_comm_abort(tgsim_ctx* ctx);
 
 /* Sharded window protocol without a transport: begin (sender side) -> caller all-to-alls the exchange buffers
  * (n_shards * exchange_cap records each way, peer-major; the first record of each peer block is a
- * header whose .t holds the record count) on the same stream -> end (receiver side). */
+ * header, above) on the same stream -> end (receiver side). */
 int tgsim_advance_begin(tgsim_ctx* ctx, int64_t t_end);
 int tgsim_exchange_buffers(tgsim_ctx* ctx, void** send_device, void** recv_device, size_t* bytes);
 /* Use caller-owned device buffers (e.g. tensors a collective library reads/writes in place) for the

@@ -20,7 +20,16 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kNSub = 64;                // append sub-queues per batch (contention sharding)
 constexpr int kRankSortMax = 64;         // segments up to this length are rank-sorted in LDS
 constexpr int kMaxShards = 64;
-constexpr int kQcLines = 3 * kNSub + kMaxShards;  // A / D / L sub-queue counters, then exchange cursors
+// Exchange blocks (sharded runs): peer p's block of xcap records is a header and kXSlices slices of
+// x_slice_cap(xcap) records, slice g written only by workgroups of XCD g (blockIdx % 8) through its
+// own cursor, so a window's ~1000 token-bucket workgroups no longer serialise on one cursor per peer
+// (DESIGN.md 6); the header record's eight 32-bit words are the slices' counts. A block too small to
+// split (xcap - 1 < 8 * 64) is one slice: the header's t is its count, as before.
+constexpr uint32_t kXSlices = 8;
+__host__ __device__ inline uint32_t x_slices(uint32_t xcap) { return xcap - 1u >= kXSlices * 64u ? kXSlices : 1u; }
+__host__ __device__ inline uint32_t x_slice_cap(uint32_t xcap) { return (xcap - 1u) / x_slices(xcap); }
+// A / D / L sub-queue counters, then the exchange cursors (peer p, slice g) at line 3 kNSub + p kXSlices + g
+constexpr int kQcLines = 3 * kNSub + kXSlices * kMaxShards;
 constexpr int kMaxRegions = 8192;        // live timing-wheel regions (one per window)
 constexpr int kStreamBlocks = 2048;      // grid of grid-stride streaming kernels
 constexpr int64_t kNegInf = INT64_MIN / 4;
@@ -199,7 +208,8 @@ __host__ __device__ inline uint32_t shard_of(uint32_t g, uint32_t N, uint32_t S)
 // The same division by a multiply-high: inv = floor(2^64 / N) + 1 makes floor(x * inv / 2^64) =
 // floor(x / N) exact for every x with x * N < 2^64 (x = (g + 1) S - 1 < 2^38 here). A 64-bit integer
 // division is a ~100-instruction software routine on the GPU; per routed copy it made a sharded
-// token bucket 40 % slower than the same shard alone (20.6 -> 28-30 us at 50k instances).
+// token bucket slower than the same shard alone (50k instances: 28-30 us -> 26.8 against 20.6; the
+// rest was the single exchange cursor per peer, now sliced: kXSlices).
 inline uint64_t shard_inv(uint32_t N) { return N ? (uint64_t)(((unsigned __int128)1 << 64) / N) + 1 : 0; }
 __device__ __forceinline__ uint32_t shard_of_inv(uint32_t g, uint32_t S, uint64_t inv) {
   return (uint32_t)__umul64hi(((uint64_t)g + 1) * S - 1, inv);

@@ -106,10 +106,11 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
 struct Queues {
   DevScalars* sc;
   uint32_t* qc;
-  uint32_t* xq;              // exchange cursor of queue q >= Q_X0 at xq[q << 5] (lines 3 * kNSub.. of qc)
+  uint32_t* xq;              // exchange cursors: (peer p, slice g) at xq[(p * kXSlices + g) << 5] (qc lines 3 kNSub..)
   tgsim_record *A, *D, *L, *X;
   uint32_t* K[3];            // group-by key of each appended record, same physical index (A, D, L)
   uint32_t subcap, xcap, lo, slots;
+  uint32_t xg, xcs;          // exchange slices per peer block and records per slice (x_slices / x_slice_cap)
   int64_t slot_ns;
   // consumer groups of A / D keys: the fused consumers give XCD x a contiguous run of buckets
   // (xcd_major), i.e. keys [gb[x-1], gb[x]); producers order each wave's A / D slots by group, so a
@@ -121,10 +122,14 @@ struct Queues {
     for (int j = 0; j < 7; ++j) g += key >= gb[j] ? 1u : 0u;
     return g;
   }
-  // Exchange cursor of peer p: a 128-B line of its own after the A / D / L sub-queue counters (round
-  // 4 kept every peer's cursor in one DevScalars line; one per wave and item serialised a sharded
-  // token bucket on that address: k_tb_bucket 20 -> 165 us per 50k shard)
-  __device__ __forceinline__ uint32_t* xctr(uint32_t p) const { return xq + ((p + Q_X0) << 5); }
+  // Exchange cursor of peer p for this workgroup's slice: a 128-B line of its own after the A / D / L
+  // sub-queue counters (round 4 kept every peer's cursor in one DevScalars line; one per wave and
+  // item serialised a sharded token bucket on that address: k_tb_bucket 20 -> 165 us per 50k shard,
+  // VERDICT r4 item 1; one line per peer still took every workgroup's reservation in turn)
+  __device__ __forceinline__ uint32_t xslice() const { return blockIdx.x & (xg - 1u); }  // xg is 1 or 8
+  __device__ __forceinline__ uint32_t* xctr(uint32_t p, uint32_t g) const { return xq + ((p * kXSlices + g) << 5); }
+  // (32-bit offsets: S * xcap < 2^32 is checked at create)
+  __device__ __forceinline__ tgsim_record* xslot(uint32_t p, uint32_t g) const { return X + (p * xcap + 1u + g * xcs); }
   // A: local sender; D: local receiver; L: timing-wheel slot relative to this window's end
   __device__ __forceinline__ uint32_t key_of(int q, const tgsim_record& r) const {
     if (q == Q_A) return r.src - lo;
@@ -148,9 +153,11 @@ struct Queues {
         cap = subcap;
         eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
       } else {
-        ctr = xq + ((uint32_t)q << 5);
-        buf = X + (size_t)(q - Q_X0) * xcap + 1;
-        cap = xcap - 1;
+        // slice 0: the per-wave path is the rare one (due stage-D copies the extraction routes to a
+        // peer); choosing a slice here spilled k_extract_shape's registers at its 96-VGPR cap
+        ctr = xctr((uint32_t)(q - Q_X0), 0u);
+        buf = xslot((uint32_t)(q - Q_X0), 0u);
+        cap = xcs;
         eb = ERR_CAP_X;
       }
     }
@@ -2510,9 +2517,10 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     sm.part[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
     sm.part[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
   }
+  const uint32_t xg = Q.xslice();
   if (sm.flag && threadIdx.x >= 64 && threadIdx.x < 64 + p.geo.S) {  // another wave: in parallel
     const uint32_t pr = threadIdx.x - 64, c = xcnt[pr];
-    xbase[pr] = c ? atomicAdd(Q.xctr(pr), c) : 0u;
+    xbase[pr] = c ? atomicAdd(Q.xctr(pr, xg), c) : 0u;
   }
   // the routed copies pass through LDS in append order (the D run, the L run, then the X runs peer
   // by peer), kStageN per round, so that every wave store covers consecutive records: whole lines,
@@ -2543,8 +2551,8 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
         uint32_t pr = 0;
         while (pr + 1 < p.geo.S && xoff[pr + 1] <= x) ++pr;
         const uint32_t pos = xbase[pr] + (x - xoff[pr]);
-        if (pos < Q.xcap - 1) {
-          uint4* dst = reinterpret_cast<uint4*>(Q.X + (size_t)pr * Q.xcap + 1 + pos);
+        if (pos < Q.xcs) {
+          uint4* dst = reinterpret_cast<uint4*>(Q.xslot(pr, xg) + pos);
           st4(dst, a.x, a.y, a.z, a.w);
           st4(dst + 1, b.x, b.y, b.z, b.w);
         } else {
@@ -4671,13 +4679,17 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
 // exchange (sharded runs)
 // ============================================================================================
 
+// Peer p's header: the count of each slice in the record's eight 32-bit words (one slice: t = count)
 __global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const uint32_t* qc) {
   const uint32_t p = threadIdx.x;
   if (p >= S) return;
-  tgsim_record h;
-  const uint32_t n = min(qc[(3u * kNSub + p) << 5], xcap - 1);
-  h.t = (int64_t)n; h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
-  store_rec(xsend + (size_t)p * xcap, h);
+  const uint32_t G = x_slices(xcap), cs = x_slice_cap(xcap);
+  uint32_t w[8];
+#pragma unroll
+  for (uint32_t g = 0; g < 8; ++g) w[g] = g < G ? min(qc[(3u * kNSub + p * kXSlices + g) << 5], cs) : 0u;
+  uint4* h = reinterpret_cast<uint4*>(xsend + (size_t)p * xcap);
+  h[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  h[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
 // Receive: every exchanged record is due this window (only due records cross shards) and joins the
@@ -4686,25 +4698,30 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, cons
                                                  uint32_t shard, uint32_t xcap, Queues Q, uint32_t* pend,
                                                  uint32_t lo, uint32_t nloc) {
   const int64_t t_end = Q.sc->t_end;
+  const uint32_t G = x_slices(xcap), cs = x_slice_cap(xcap);
   const uint64_t total = (uint64_t)S * xcap;
   const uint32_t stride = gridDim.x * blockDim.x;
   uint32_t it = 0;
   for (uint64_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += stride, ++it) {
     const uint32_t p = (uint32_t)(j / xcap), i = (uint32_t)(j % xcap);
+    const uint32_t g = i ? (i - 1u) / cs : 0u, o = i ? (i - 1u) - g * cs : 0u;  // slice, position in it
     int q = -1;
     tgsim_record rec;
-    if (p != shard && i > 0) {
-      const int64_t n = xrecv[(size_t)p * xcap].t;
-      if (n < 0 || n >= (int64_t)xcap) {
-        if (i == 1) atomicOr(&Q.sc->err, ERR_EXCH_HDR);
-      } else if ((int64_t)i <= n) {
+    if (p != shard && i > 0 && g < G) {
+      // the slice's count: a header word (G > 1), or the whole t (one slice)
+      const uint32_t* hr = reinterpret_cast<const uint32_t*>(xrecv + (size_t)p * xcap);
+      const int64_t n = G > 1 ? (int64_t)hr[g] : xrecv[(size_t)p * xcap].t;
+      if (n < 0 || n > (int64_t)cs) {
+        if (o == 0) atomicOr(&Q.sc->err, ERR_EXCH_HDR);
+      } else if ((int64_t)o < n) {
         load_rec(xrecv + j, rec);
         rec.meta &= ~(uint32_t)TGSIM_F_WHEEL;
         if (rec.t < t_end) q = Q_D;
         else atomicOr(&Q.sc->err, ERR_EXCH_HDR);
       }
-      const int64_t ns = xsend[(size_t)p * xcap].t;
-      if (ns > 0 && ns < (int64_t)xcap && (int64_t)i <= ns) {
+      const uint32_t* hs = reinterpret_cast<const uint32_t*>(xsend + (size_t)p * xcap);
+      const int64_t ns = G > 1 ? (int64_t)hs[g] : xsend[(size_t)p * xcap].t;
+      if (ns > 0 && ns <= (int64_t)cs && (int64_t)o < ns) {
         const uint4 b = reinterpret_cast<const uint4*>(xsend + j)[1];
         if (b.z & TGSIM_F_WHEEL) {
           const uint32_t src = reinterpret_cast<const uint4*>(xsend + j)[0].z;
@@ -4934,7 +4951,7 @@ static inline unsigned grid_for(uint64_t n) {
 static uint32_t bkt_width_fused(const Dev& d, uint32_t K);
 static Queues make_queues(Dev& d) {
   Queues Q;
-  Q.sc = d.sc; Q.qc = d.qc; Q.xq = d.qc + ((size_t)(3 * kNSub - Q_X0) << 5); Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
+  Q.sc = d.sc; Q.qc = d.qc; Q.xq = d.qc + ((size_t)(3 * kNSub) << 5); Q.xg = x_slices(d.xcap); Q.xcs = x_slice_cap(d.xcap); Q.A = d.A; Q.D = d.D; Q.L = d.L; Q.X = d.xsend; Q.subcap = d.subcap; Q.xcap = d.xcap;
   Q.K[0] = d.KA; Q.K[1] = d.KD; Q.K[2] = d.KL; Q.lo = d.lo; Q.slots = d.slots; Q.slot_ns = d.slot_ns;
   // the fused consumers' buckets (bkt_width_fused over the local keys) in xcd_major order: XCD x
   // runs buckets [x q + min(x, r), (x+1) q + min(x+1, r)) with q = B / 8, r = B % 8

@@ -443,7 +443,10 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   d.subcap = (uint32_t)(cap_rec / kNSub + 4096);  // per sub-queue, with headroom for imbalance
   const size_t phys_rec = (size_t)kNSub * d.subcap;
   d.cap_arena = 2 * cap_rec;
-  d.xcap = c->S > 1 ? (uint32_t)(cfg->exchange_cap ? cfg->exchange_cap : 65536) : 1;
+  const uint64_t xcap = c->S > 1 ? (cfg->exchange_cap ? cfg->exchange_cap : 65536) : 1;
+  // a header and a record per peer block; slot offsets in 32 bits (Queues::xslot)
+  if ((c->S > 1 && xcap < 2) || (uint64_t)c->S * xcap >= (1ull << 32)) return TGSIM_EINVAL;
+  d.xcap = (uint32_t)xcap;
   d.max_states = cfg->max_states ? cfg->max_states : 4096;
   d.max_waiters = cfg->max_waiters ? cfg->max_waiters : 65536;
   d.max_signals = cfg->max_signals ? cfg->max_signals : (1ull << 24);
