@@ -126,7 +126,9 @@ struct Queues {
   // sub-queue counters (round 4 kept every peer's cursor in one DevScalars line; one per wave and
   // item serialised a sharded token bucket on that address: k_tb_bucket 20 -> 165 us per 50k shard,
   // VERDICT r4 item 1; one line per peer still took every workgroup's reservation in turn)
-  __device__ __forceinline__ uint32_t xslice() const { return blockIdx.x & (xg - 1u); }  // xg is 1 or 8
+  __device__ __forceinline__ uint32_t xslice() const {  // xg is 1 or 8
+    return __builtin_amdgcn_readfirstlane(blockIdx.x & (xg - 1u));
+  }
   __device__ __forceinline__ uint32_t* xctr(uint32_t p, uint32_t g) const { return xq + ((p * kXSlices + g) << 5); }
   // (32-bit offsets: S * xcap < 2^32 is checked at create)
   __device__ __forceinline__ tgsim_record* xslot(uint32_t p, uint32_t g) const { return X + (p * xcap + 1u + g * xcs); }
@@ -153,10 +155,11 @@ struct Queues {
         cap = subcap;
         eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
       } else {
-        // slice 0: the per-wave path is the rare one (due stage-D copies the extraction routes to a
-        // peer); choosing a slice here spilled k_extract_shape's registers at its 96-VGPR cap
-        ctr = xctr((uint32_t)(q - Q_X0), 0u);
-        buf = xslot((uint32_t)(q - Q_X0), 0u);
+        // the slice as a scalar (readfirstlane) and 32-bit offsets: anything else spilled
+        // k_extract_shape's registers at its 96-VGPR cap
+        const uint32_t g = __builtin_amdgcn_readfirstlane(blockIdx.x & (xg - 1u));
+        ctr = xq + ((((uint32_t)(q - Q_X0)) * kXSlices + g) << 5);
+        buf = X + (((uint32_t)(q - Q_X0)) * xcap + (1u + g * xcs));
         cap = xcs;
         eb = ERR_CAP_X;
       }
