@@ -33,7 +33,10 @@ evidence)
   W=$1; R=$2; shift 2
   P=$OUT/profiles/$R
   mkdir -p $P
-  B="bench.py --workload $W --no-cpu-baseline $(warm $W) $*"
+  # the profiled runs leave out the storm line's flood beside it (its windows would mix into the
+  # storm's trace and counters); the bench line at the end keeps it
+  NB=""; [ "$W" = storm ] && NB="--no-beside"
+  B="bench.py --workload $W --no-cpu-baseline $NB $(warm $W) $*"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$W -o run --output-format csv \
     -- python3 -u $B --steps 20 > $OUT/bench_${W}_under_rocprof.log 2>&1 || { echo PROF_FAIL; tail -20 $OUT/bench_${W}_under_rocprof.log; exit 1; }
   cp $OUT/prof_$W/run_kernel_stats.csv $P/${W}_kernel_stats.csv
