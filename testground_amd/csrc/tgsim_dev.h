@@ -266,6 +266,7 @@ struct Dev {
   // test (heavy.pend == nullptr: the host proved no sender can reach the limit); H = due wheel
   // records of heavy senders (copies, grouped by sender for k_shape_seq)
   uint32_t* pend = nullptr;
+  uint32_t* pend_part = nullptr;   // [kRadixBlocks] k_pend_max's per-block maxima
   Heavy heavy{};
   tgsim_record* H = nullptr;
   uint32_t *hkeys = nullptr, *hvals = nullptr;
@@ -385,7 +386,8 @@ hipError_t launch_set_window_barrier_commit(Dev& d, uint32_t waiter, int64_t off
 hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
 // retx: TCP pending per sender; inbox_mult: acks mode, packets per delivery of the sender's last inbox
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult);
+// per-block maxima into d.pend_part, then copied to host[kRadixBlocks] (pinned) on the stream
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult, uint32_t* host);
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part
 hipError_t launch_storm_red(Dev& d, uint32_t nparts, int64_t* red2);

@@ -1440,13 +1440,14 @@ __device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uin
   }
 }
 
-// The host's exact refresh of its occupancy bound: max over local senders of pend -> sc->pend_max
-// (zeroed by the host's memset first). TCP mode: mult * (pend + pending retransmissions), which
+// The host's exact refresh of its occupancy bound: max over local senders of pend, per block into
+// part[blockIdx.x] (the host folds the kRadixBlocks partials; one atomicMax per block on one address
+// serialised ~1000 blocks: 14.7 us plus a memset per refresh, config 5). TCP mode: mult * (pend + pending retransmissions), which
 // bounds mult * the sender's unsettled segments (tgsim_tcp.hip). TCP acks mode (refreshed every
 // window): pend + mult * (retransmissions released into the window + the deliveries the sender got
 // last window, each answered by at most one ACK).
 __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const uint32_t* retx, const uint32_t* inbox,
-                                                     uint32_t inbox_mult, uint32_t mult, uint32_t nloc, uint32_t* out) {
+                                                     uint32_t inbox_mult, uint32_t mult, uint32_t nloc, uint32_t* part) {
   __shared__ uint32_t red[kBlock / 64];
   uint32_t mx = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nloc; i += gridDim.x * kBlock) {
@@ -1458,11 +1459,7 @@ __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const
   mx = wave_max(mx);
   if (lane_id() == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
-  // one atomic per block: same-address atomics from every wave serialise (95 us at 1M senders)
-  if (threadIdx.x == 0) {
-    mx = max(max(red[0], red[1]), max(red[2], red[3]));
-    if (mx) atomicMax(out, mx);
-  }
+  if (threadIdx.x == 0) part[blockIdx.x] = max(max(red[0], red[1]), max(red[2], red[3]));
 }
 
 __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars* sc, const tgsim_record* L,
@@ -5189,11 +5186,11 @@ hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
   return hipGetLastError();
 }
 
-hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult) {
-  TG_CHECK(hipMemsetAsync(&d.sc->pend_max, 0, sizeof(uint32_t), d.stream));
-  hipLaunchKernelGGL(k_pend_max, dim3(std::min<unsigned>(grid_for(d.nloc), 1024u)), dim3(kBlock), 0, d.stream, d.pend,
-                     retx, inbox_mult ? d.inbox : nullptr, inbox_mult, mult, d.nloc, &d.sc->pend_max);
-  return hipGetLastError();
+hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult, uint32_t* host) {
+  hipLaunchKernelGGL(k_pend_max, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, d.pend, retx,
+                     inbox_mult ? d.inbox : nullptr, inbox_mult, mult, d.nloc, d.pend_part);
+  TG_CHECK(hipGetLastError());
+  return hipMemcpyAsync(host, d.pend_part, kRadixBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream);
 }
 
 hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {

@@ -94,6 +94,16 @@ struct tgsim_ctx {
   // far) bounds its forwards in any window without reading the device
   uint32_t fl_npubs = 0;
   std::vector<uint8_t> fl_pub_seen;
+  // A lifetime bound on any sender's queued + staged copies while the flood is the only reactor: every
+  // message it ever staged from the host (life_host: the per-window maxima summed) plus at most D per
+  // publication (a node publishes or forwards a publication once), times the largest duplication
+  // multiplier seen. While that stays within the queue limit no window needs the exact refresh (a
+  // host sync every few windows of config 5). life_ok clears for good when probes, a storm reactor
+  // or TCP mode stage traffic the bound does not count.
+  uint64_t life_host = 0;
+  uint64_t life_mult = 1;
+  bool life_ok = true;
+  uint32_t* pend_host = nullptr;     // [kRadixBlocks] pinned: k_pend_max's per-block maxima
   // device-counted staging: after an asynchronous flood reaction the staged count is
   // sc->n_msgs_dev; host / device enqueues then append behind it on the device
   bool staged_dev = false;
@@ -372,6 +382,7 @@ extern "C" void tgsim_destroy(tgsim_ctx* c) {
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->d.h_sc) (void)hipHostFree(c->d.h_sc);
   if (c->tcp_snap) (void)hipHostFree(c->tcp_snap);
+  if (c->pend_host) (void)hipHostFree(c->pend_host);
   for (hipEvent_t e : c->tcp_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream && c->d.stream) (void)hipStreamDestroy(c->d.stream);
@@ -512,6 +523,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.tot, kMaxBins);
   rc |= dalloc(c, &d.bstart, kMaxBins + 1);
   rc |= dalloc(c, &d.qc, (size_t)kQcLines * 32);
+  rc |= dalloc(c, &d.pend_part, kRadixBlocks);
   rc |= dalloc(c, &d.sig_red, 4);
   rc |= dalloc(c, &d.sig_part, 2 * 4096);
   rc |= dalloc(c, &d.stats, (size_t)kNSub * 16);
@@ -1177,11 +1189,22 @@ static int plan_queue_limit(tgsim_ctx* c) {
   bool gate = zd_only ? c->pend_bound >= TGSIM_NETEM_LIMIT : c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   // inconclusive: refresh the bound with the exact maximum (one sync) - unless the window's own
   // staging bound already reaches the limit, when no refresh can close the gate
+  c->life_host = std::min<uint64_t>(c->life_host + m_uniform, 1ull << 40);
+  c->life_mult = std::max<uint64_t>(c->life_mult, mult);
+  if (c->tcp_on || c->win_inbox_max) c->life_ok = false;  // probes / storm reactor / TCP traffic
+  if (gate && c->life_ok && !zd_only &&
+      c->life_mult * ((uint64_t)c->d.fl.D * c->fl_npubs + c->life_host) <= TGSIM_NETEM_LIMIT)
+    gate = false;  // no sender can ever have queued and staged more than the limit
   if (gate && !c->pend_exact && (zd_only || mult * m_max <= TGSIM_NETEM_LIMIT)) {
+    if (!c->pend_host &&
+        hipHostMalloc((void**)&c->pend_host, kRadixBlocks * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+      return fail(c, TGSIM_ENOMEM, "pinned pend maxima");
     HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks ? tcp_inbox_mult(c) : 0u,
-                             (uint32_t)mult), "pend max");
+                             (uint32_t)mult, c->pend_host), "pend max");
     HIPCK(c, sync_scalars(d), "sync");
-    c->pend_bound = d.h_sc->pend_max;
+    uint32_t mx = 0;
+    for (int b = 0; b < kRadixBlocks; ++b) mx = std::max(mx, c->pend_host[b]);
+    c->pend_bound = mx;
     c->pend_exact = true;
     gate = zd_only ? c->pend_bound >= TGSIM_NETEM_LIMIT : c->pend_bound + mult * m_max > TGSIM_NETEM_LIMIT;
   }
@@ -1962,6 +1985,7 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
     f.cap = cap;
   }
   c->fl_pub_seen.swap(pub_seen);
+  if (c->fl_npubs) c->life_ok = false;  // the earlier graph's publications may still be queued
   c->fl_npubs = 0;
   return TGSIM_OK;
 }
@@ -3542,6 +3566,7 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->rules_h.swap(rules);
   c->now = now; c->horizon = horizon; c->n_status_last = n_status_last;
   c->pend_bound = pend_bound; c->pend_exact = pend_exact;
+  c->life_ok = false;  // the restored wheel's copies predate this context's lifetime counts
   c->now_from_device = false;
   c->max_tsend_h = INT64_MIN;
   c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = true;  // re-uploaded at the next window
