@@ -267,6 +267,12 @@ struct Dev {
   // records of heavy senders (copies, grouped by sender for k_shape_seq)
   uint32_t* pend = nullptr;
   uint32_t* pend_part = nullptr;   // [kRadixBlocks] k_pend_max's per-block maxima
+  // the window's wheel insert on a side stream (contexts with a flood graph): side_ev marks its end,
+  // main_ev the point of the context stream it starts from; side_pending until the context stream
+  // has been made to wait for it (join_side)
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev = nullptr, main_ev = nullptr;
+  bool side_pending = false;
   Heavy heavy{};
   tgsim_record* H = nullptr;
   uint32_t *hkeys = nullptr, *hvals = nullptr;
@@ -387,6 +393,7 @@ hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // sc->pend_max = max over local senders of their queued copies (the host's exact occupancy bound)
 // retx: TCP pending per sender; inbox_mult: acks mode, packets per delivery of the sender's last inbox
 // per-block maxima into d.pend_part, then copied to host[kRadixBlocks] (pinned) on the stream
+hipError_t join_side(Dev& d);
 hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult, uint32_t* host);
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part

@@ -26,7 +26,12 @@ const char* const kKernelNames[KID_COUNT] = {
 
 // after a stream synchronisation: fold completed event pairs into the per-kernel totals
 static void prof_resolve(Dev& d) {
+  size_t keep = 0;
   for (auto& p : d.prof.pending) {
+    if (hipEventQuery(p.b) == hipErrorNotReady) {  // a scope on the side stream still running
+      d.prof.pending[keep++] = p;
+      continue;
+    }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       d.prof.ms[p.kid] += ms;
@@ -35,7 +40,7 @@ static void prof_resolve(Dev& d) {
     d.prof.pool.push_back(p.a);
     d.prof.pool.push_back(p.b);
   }
-  d.prof.pending.clear();
+  d.prof.pending.resize(keep);
 }
 
 // ============================================================================================
@@ -1462,24 +1467,29 @@ __global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const
   if (threadIdx.x == 0) part[blockIdx.x] = max(max(red[0], red[1]), max(red[2], red[3]));
 }
 
+// The window's counters close once the window end's passes have run: the deliveries, the staged
+// count the next netem pass reads, the statistics (first block of the insert launch, or of the
+// long-inbox launch when the insert runs on the side stream).
+__device__ __forceinline__ void close_window_counters(DevScalars* sc) {
+  const uint32_t n = sc->qn[Q_D];
+  sc->n_out = n;
+  sc->n_msgs_last = sc->n_msgs_dev;  // the shape pass of this window has read it
+  sc->n_msgs_dev = 0;
+  sc->st[ST_DELIVERED] += n;
+  sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
+  sc->st[ST_EXTRACTED] += sc->n_extract;
+  sc->st[ST_INSERTED] += sc->qn[Q_L];
+}
+
 __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars* sc, const tgsim_record* L,
                                                    tgsim_record* arena, uint32_t* dirs, uint32_t slots,
                                                    const uint32_t* histx, const uint32_t* tot, uint32_t* pend,
-                                                   uint32_t lo, uint32_t nloc) {
+                                                   uint32_t lo, uint32_t nloc, bool close = true) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
   const uint64_t off = sc->ins_off;
   if (blockIdx.x == 0) {
-    if (threadIdx.x == 0) {
-      const uint32_t n = sc->qn[Q_D];
-      sc->n_out = n;
-      sc->n_msgs_last = sc->n_msgs_dev;  // the shape pass of this window has read it
-      sc->n_msgs_dev = 0;
-      sc->st[ST_DELIVERED] += n;
-      sc->st[ST_TB_ITEMS] += sc->qn[Q_A];
-      sc->st[ST_EXTRACTED] += sc->n_extract;
-      sc->st[ST_INSERTED] += sc->qn[Q_L];
-    }
+    if (close && threadIdx.x == 0) close_window_counters(sc);
     if (off != ~0ull) {
       bkt_bases(slots, nullptr, tot, base, part);
       const uint32_t dir = (sc->reg_head - 1) % kMaxRegions;
@@ -4675,6 +4685,25 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
               gridDim.x - kRadixBlocks);
 }
 
+// The same split over two streams (Dev::side): the wheel insert alone on the side
+// stream - nothing after the window reads the wheel before the next window starts - and the long
+// inboxes with the counters' close on the context stream, where the reactions that read the
+// deliveries follow at once.
+__global__ __launch_bounds__(kBlock) void k_wheel_insert(BktSrc src, DevScalars* sc, const tgsim_record* L,
+                                                         tgsim_record* arena, uint32_t* dirs, uint32_t slots,
+                                                         const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                         uint32_t lo, uint32_t nloc) {
+  wheel_scatter_body(src, sc, L, arena, dirs, slots, hist, tot, pend, lo, nloc, false);
+}
+__global__ __launch_bounds__(kBlock) void k_inbox_rest(DevScalars* sc, EmitPolicy p, const uint32_t* keys,
+                                                       const uint32_t* vals, const uint32_t* off,
+                                                       const uint32_t* medium, const LargeSeg* large, uint64_t* K1a,
+                                                       uint64_t* K2a, uint32_t* K3a, uint64_t* K1b, uint64_t* K2b,
+                                                       uint32_t* K3b) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) close_window_counters(sc);
+  rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x, gridDim.x);
+}
+
 // ============================================================================================
 // exchange (sharded runs)
 // ============================================================================================
@@ -5291,6 +5320,20 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
                        d.sc, d.L, d.arena, d.dirs, d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0,
                        d.seg_off, d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b, ga, sig_state(d), g);
     *spec_parts = g;
+  } else if (d.side) {  // the insert beside what follows the window (the flood's reaction)
+    TG_CHECK(hipEventRecord(d.main_ev, d.stream));
+    TG_CHECK(hipStreamWaitEvent(d.side, d.main_ev, 0));
+    {
+      ProfScope ps_(d, KID_REGION_FILL, d.side);
+      hipLaunchKernelGGL(k_wheel_insert, dim3(kRadixBlocks), dim3(kBlock), 0, d.side, srcL, d.sc, d.L, d.arena, d.dirs,
+                         d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc);
+    }
+    TG_CHECK(hipGetLastError());
+    TG_CHECK(hipEventRecord(d.side_ev, d.side));
+    d.side_pending = true;
+    ProfScope ps_(d, KID_SEG_REST);
+    hipLaunchKernelGGL(k_inbox_rest, dim3(kListBlocks), dim3(kBlock), 0, d.stream, d.sc, p, d.keys0, d.vals0,
+                       d.seg_off, d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   } else {
     ProfScope ps_(d, KID_REGION_FILL);
     hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L,
@@ -5298,6 +5341,14 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
                        d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   }
   return hipGetLastError();
+}
+
+// The context stream waits for the side stream's insert (every entry point but the ones that may run
+// beside it does this first)
+hipError_t join_side(Dev& d) {
+  if (!d.side_pending) return hipSuccess;
+  d.side_pending = false;
+  return hipStreamWaitEvent(d.stream, d.side_ev, 0);
 }
 
 hipError_t window_end(Dev& d) { return window_end_impl(d, nullptr, 0, 0, nullptr); }

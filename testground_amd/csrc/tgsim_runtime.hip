@@ -227,9 +227,16 @@ static int fail(tgsim_ctx* c, int code, const char* fmt, ...) {
 // side (std::vector / std::string growth, std::unordered_map) crosses extern "C" into a Go or
 // Python caller. An allocation failure is TGSIM_ENOMEM and leaves the context usable: the tables
 // are rebuilt into temporaries and swapped in only once complete.
+// It also makes the context stream wait for a wheel insert still running on the side stream
+// (Dev::side) - join = false only for the calls that may run beside it (the flood's reaction and
+// publications touch neither the wheel nor the insert's inputs).
 template <class F>
-static int abi_guard(tgsim_ctx* c, F&& body) noexcept {
+static int abi_guard(tgsim_ctx* c, F&& body, bool join = true) noexcept {
   try {
+    if (join && c && c->d.side_pending) {
+      const hipError_t e = join_side(c->d);
+      if (e != hipSuccess) return fail(c, TGSIM_EHIP, "side stream: %s", hipGetErrorString(e));
+    }
     return body();
   } catch (const std::bad_alloc&) {
     return fail(c, TGSIM_ENOMEM, "out of host memory");
@@ -373,6 +380,7 @@ extern "C" int tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
 
 extern "C" void tgsim_destroy(tgsim_ctx* c) {
   if (!c) return;
+  if (c->d.side) (void)hipStreamSynchronize(c->d.side);
   if (c->d.stream) (void)hipStreamSynchronize(c->d.stream);
   for (tgsim_ctx::Pinned* b : {&c->pin_msgs, &c->pin_marks, &c->pin_tcp}) {
     if (b->p) (void)hipHostFree(b->p);
@@ -386,6 +394,9 @@ extern "C" void tgsim_destroy(tgsim_ctx* c) {
   for (hipEvent_t e : c->tcp_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own_stream && c->d.stream) (void)hipStreamDestroy(c->d.stream);
+  if (c->d.side) (void)hipStreamDestroy(c->d.side);
+  for (hipEvent_t e : {c->d.side_ev, c->d.main_ev})
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -1984,6 +1995,11 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
       return TGSIM_ENOMEM;
     f.cap = cap;
   }
+  if (!c->d.side) {  // the wheel insert runs beside the flood's reaction from now on
+    HIPCK(c, hipStreamCreateWithFlags(&c->d.side, hipStreamNonBlocking), "side stream");
+    HIPCK(c, hipEventCreateWithFlags(&c->d.side_ev, hipEventDisableTiming), "side stream");
+    HIPCK(c, hipEventCreateWithFlags(&c->d.main_ev, hipEventDisableTiming), "side stream");
+  }
   c->fl_pub_seen.swap(pub_seen);
   if (c->fl_npubs) c->life_ok = false;  // the earlier graph's publications may still be queued
   c->fl_npubs = 0;
@@ -1994,7 +2010,7 @@ static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const ui
                                    size_t n, uint32_t size);
 extern "C" int tgsim_flood_publish(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
                                    size_t n, uint32_t size) {
-  return abi_guard(c, [&] { return tgsim_flood_publish_body(c, inst, pubs, t, n, size); });
+  return abi_guard(c, [&] { return tgsim_flood_publish_body(c, inst, pubs, t, n, size); }, false);
 }
 static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const uint32_t* pubs, const int64_t* t,
                                    size_t n, uint32_t size) {
@@ -2020,7 +2036,7 @@ static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const ui
     pairs.push_back(l); pairs.push_back(pubs[i]);
   }
   tgsim_msg_soa m{src.data(), dst.data(), seq.data(), sz.data(), ts.data()};
-  int rc = tgsim_enqueue(c, &m, src.size());
+  int rc = tgsim_enqueue_body(c, &m, src.size());  // (not the entry point: it would join the side stream)
   if (rc) return rc;
   const uint32_t np = (uint32_t)(pairs.size() / 2);
   if (!np) return TGSIM_OK;
@@ -2041,7 +2057,7 @@ static int tgsim_flood_publish_body(tgsim_ctx* c, const uint32_t* inst, const ui
 
 static int tgsim_flood_react_body(tgsim_ctx* c, uint32_t size, size_t* n_fwd);
 extern "C" int tgsim_flood_react(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
-  return abi_guard(c, [&] { return tgsim_flood_react_body(c, size, n_fwd); });
+  return abi_guard(c, [&] { return tgsim_flood_react_body(c, size, n_fwd); }, false);
 }
 static int tgsim_flood_react_body(tgsim_ctx* c, uint32_t size, size_t* n_fwd) {
   if (!c) return TGSIM_EINVAL;
