@@ -1995,7 +1995,10 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
       return TGSIM_ENOMEM;
     f.cap = cap;
   }
-  if (!c->d.side) {  // the wheel insert runs beside the flood's reaction from now on
+  // TGSIM_SIDE_INSERT=1: the wheel insert on a side stream beside the flood's reaction - measured
+  // slower (config 5: 0.400 -> 0.447 ms per window), so off unless asked for
+  const char* si = getenv("TGSIM_SIDE_INSERT");
+  if (!c->d.side && si && *si == '1') {
     HIPCK(c, hipStreamCreateWithFlags(&c->d.side, hipStreamNonBlocking), "side stream");
     HIPCK(c, hipEventCreateWithFlags(&c->d.side_ev, hipEventDisableTiming), "side stream");
     HIPCK(c, hipEventCreateWithFlags(&c->d.main_ev, hipEventDisableTiming), "side stream");
