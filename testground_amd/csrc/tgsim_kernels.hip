@@ -4723,16 +4723,18 @@ __global__ void k_xheaders(tgsim_record* xsend, uint32_t S, uint32_t xcap, const
 
 // Receive: every exchanged record is due this window (only due records cross shards) and joins the
 // deliveries. Send side: a wheel copy the extraction sent to a peer leaves its sender's queue.
-// kRecvSplit blocks per (peer, slice) walk only the slice's counted records (the header's words),
-// not the whole block capacity (a grid over S * xcap slots: 7.2 us per window at 50k-instance
-// shards, most threads idle).
-constexpr uint32_t kRecvSplit = 8;
+// `split` blocks per (peer, slice), about two slots of the slice's capacity per thread, walk only the
+// slice's counted records (the header's words) - the capacity slots past the count are not touched.
+__host__ __device__ inline uint32_t recv_split(uint32_t xcap) {
+  const uint32_t cs = x_slice_cap(xcap);
+  return cs > 2u * kBlock ? (cs + 2u * kBlock - 1u) / (2u * kBlock) : 1u;
+}
 __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, const tgsim_record* xsend, uint32_t S,
                                                  uint32_t shard, uint32_t xcap, Queues Q, uint32_t* pend,
                                                  uint32_t lo, uint32_t nloc) {
   const int64_t t_end = Q.sc->t_end;
-  const uint32_t G = x_slices(xcap), cs = x_slice_cap(xcap);
-  const uint32_t b = blockIdx.x / kRecvSplit, part = blockIdx.x % kRecvSplit;
+  const uint32_t G = x_slices(xcap), cs = x_slice_cap(xcap), split = recv_split(xcap);
+  const uint32_t b = blockIdx.x / split, part = blockIdx.x % split;
   const uint32_t p = b / G, g = b % G;  // block-uniform
   if (p >= S || p == shard) return;
   const size_t h = (size_t)p * xcap;
@@ -4745,7 +4747,7 @@ __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, cons
   const uint32_t top = cr > cn ? cr : cn;
   const size_t base = h + 1 + (size_t)g * cs;
   uint32_t it = 0;
-  for (uint32_t o0 = part * kBlock; o0 < top; o0 += kBlock * kRecvSplit, ++it) {  // block-uniform trip count
+  for (uint32_t o0 = part * kBlock; o0 < top; o0 += kBlock * split, ++it) {  // block-uniform trip count
     const uint32_t o = o0 + threadIdx.x;
     int q = -1;
     tgsim_record rec;
@@ -5290,7 +5292,7 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
                                   uint32_t* spec_parts) {
   if (d.S > 1) {
     Queues Q = make_queues(d);
-    const uint32_t nb = d.S * x_slices(d.xcap) * kRecvSplit;
+    const uint32_t nb = d.S * x_slices(d.xcap) * recv_split(d.xcap);
     hipLaunchKernelGGL(k_recv, dim3(nb), dim3(kBlock), 0, d.stream, d.xrecv, d.xsend, d.S, d.shard,
                        d.xcap, Q, d.pend, d.lo, d.nloc);
     TG_CHECK(hipGetLastError());
