@@ -161,8 +161,10 @@ struct Queues {
         eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
       } else {
         // the slice as a scalar (readfirstlane) and 32-bit offsets: anything else spilled
-        // k_extract_shape's registers at its 96-VGPR cap
-        const uint32_t g = __builtin_amdgcn_readfirstlane(blockIdx.x & (xg - 1u));
+        // k_extract_shape's registers at its 96-VGPR cap. The salt (the caller's round / item)
+        // turns a workgroup's successive pushes to successive slices, so one busy workgroup does
+        // not fill one slice alone
+        const uint32_t g = __builtin_amdgcn_readfirstlane((blockIdx.x + salt) & (xg - 1u));
         ctr = xq + ((((uint32_t)(q - Q_X0)) * kXSlices + g) << 5);
         buf = X + (((uint32_t)(q - Q_X0)) * xcap + (1u + g * xcs));
         cap = xcs;
@@ -2527,10 +2529,22 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
     sm.part[0] = tD ? atomicAdd(Q.qc + (((uint32_t)Q_D * kNSub + sub) << 5), tD) : 0u;
     sm.part[1] = tL ? atomicAdd(Q.qc + (((uint32_t)Q_L * kNSub + sub) << 5), tL) : 0u;
   }
-  const uint32_t xg = Q.xslice();
+  // a peer's run goes into this workgroup's slice; what does not fit there goes on into the next
+  // slice (xb1: its base there), so a slice that fills up early (few producers, uneven traffic)
+  // costs no capacity the block still has
+  __shared__ uint32_t xb1[kMaxShards];
+  const uint32_t xg = Q.xslice(), xg1 = (xg + 1u) & (Q.xg - 1u);
   if (sm.flag && threadIdx.x >= 64 && threadIdx.x < 64 + p.geo.S) {  // another wave: in parallel
     const uint32_t pr = threadIdx.x - 64, c = xcnt[pr];
-    xbase[pr] = c ? atomicAdd(Q.xctr(pr, xg), c) : 0u;
+    uint32_t b0 = 0, fit = 0, b1 = 0;
+    if (c) {
+      b0 = atomicAdd(Q.xctr(pr, xg), c);
+      fit = b0 < Q.xcs ? min(c, Q.xcs - b0) : 0u;
+      if (fit < c) b1 = Q.xg > 1u ? atomicAdd(Q.xctr(pr, xg1), c - fit) : Q.xcs;  // one slice: no room
+    }
+    xbase[pr] = b0;
+    xcnt[pr] = fit;
+    xb1[pr] = b1;
   }
   // the routed copies pass through LDS in append order (the D run, the L run, then the X runs peer
   // by peer), kStageN per round, so that every wave store covers consecutive records: whole lines,
@@ -2560,9 +2574,10 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
         const uint32_t x = q - tDL;
         uint32_t pr = 0;
         while (pr + 1 < p.geo.S && xoff[pr + 1] <= x) ++pr;
-        const uint32_t pos = xbase[pr] + (x - xoff[pr]);
+        const uint32_t xi = x - xoff[pr], fit = xcnt[pr];
+        const uint32_t pos = xi < fit ? xbase[pr] + xi : xb1[pr] + (xi - fit);
         if (pos < Q.xcs) {
-          uint4* dst = reinterpret_cast<uint4*>(Q.xslot(pr, xg) + pos);
+          uint4* dst = reinterpret_cast<uint4*>(Q.xslot(pr, xi < fit ? xg : xg1) + pos);
           st4(dst, a.x, a.y, a.z, a.w);
           st4(dst + 1, b.x, b.y, b.z, b.w);
         } else {

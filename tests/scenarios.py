@@ -405,7 +405,7 @@ def shard_range(n, k, s):
 
 
 def run_random_sharded(make_sim, exchange, world: int, seed: int, n_inst: int = 24, windows: int = 6,
-                       msgs_per_window: int = 300, window_ns: int = 40 * MS, local=None):
+                       msgs_per_window: int = 300, window_ns: int = 40 * MS, local=None, exchange_cap: int = 4096):
     """run_random's workload split over `world` shards. make_sim(cfg) -> Simulator of one shard;
     exchange(sims) moves every shard's send blocks to the peers' receive blocks (an all-to-all)
     between advance_begin and advance_end; exchange=None: the shards carry a transport and each
@@ -415,7 +415,7 @@ def run_random_sharded(make_sim, exchange, world: int, seed: int, n_inst: int = 
     rng = np.random.default_rng(seed)
     local = list(range(world)) if local is None else list(local)
     sims = [make_sim(SimConfig(n_instances=n_inst, seed=1000 + seed, shard_id=k, n_shards=world,
-                               exchange_cap=4096)) for k in local]
+                               exchange_cap=exchange_cap)) for k in local]
     outs = [[] for _ in local]
     srcs = []
     seqc = np.zeros(n_inst, np.int64)

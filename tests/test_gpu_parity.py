@@ -142,6 +142,18 @@ def test_transport_on_one_device(hip, oracle, world, seed):
     S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
 
 
+@pytest.mark.parametrize("world,seed", [(2, 1), (3, 2)])
+def test_transport_tight_exchange_on_one_device(hip, oracle, world, seed):
+    """As above with the smallest sliced exchange block (exchange_cap 513: eight slices of 64
+    records, include/tgsim.h): a few busy workgroups overrun their slices, and the token bucket's
+    run spills into the next slice and the per-wave pushes rotate slices, so the capacity the block
+    has is usable - no ECAPACITY, equal to the oracle."""
+    outs = S.sharded_threads(world, lambda k, tr: S.run_random_sharded(
+        _hip_with_transport(tr), None, world, seed, local=[k], exchange_cap=513)[0][0], device=True)
+    _, srcs = S.run_random_sharded(lambda c: S.Simulator(c, binding=oracle), S.memmove_exchange, world, seed)
+    S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_storm_transport_on_one_device(hip, oracle, world):
     """bench.py's storm step on HIP shards: the storm batch's MAX all-reduce and the exchange go

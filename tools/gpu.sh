@@ -67,7 +67,8 @@ ab)
   for r in $(seq 1 $R); do
     for v in product "$@"; do
       if [ $v = product ]; then L=$PWD/testground_amd/libtgsim.so; else L=$PWD/testground_amd/libtgsim_$v.so; fi
-      TGSIM_LIB=$L timeout -k 10 200 python3 -u bench.py --workload $W --no-cpu-baseline --steps 30 > $OUT/${W}_${v}_$r.log 2>&1 || { echo FAIL $v; tail -5 $OUT/${W}_${v}_$r.log; exit 1; }
+      NB=""; [ "$W" = storm ] && NB="--no-beside"
+      TGSIM_LIB=$L timeout -k 10 200 python3 -u bench.py --workload $W --no-cpu-baseline $NB --steps 30 > $OUT/${W}_${v}_$r.log 2>&1 || { echo FAIL $v; tail -5 $OUT/${W}_${v}_$r.log; exit 1; }
       python3 -c "import json; j=json.loads(open('$OUT/${W}_${v}_$r.log').read().strip().splitlines()[-1]); print('$v', 'round $r', j['value'], 'msgs/s', round(j['ms_per_step'],5), 'ms/step', ' '.join('%s=%.1f' % (k, v['avg_us']) for k, v in sorted(j['kernels_probe'].items())))"
     done
   done;;
