@@ -173,6 +173,18 @@ def test_flood_async_reaction_matches_oracle(hip, oracle):
 
 
 @pytest.mark.gpu
+def test_flood_side_stream_insert_matches_oracle(hip, oracle, monkeypatch):
+    """TGSIM_SIDE_INSERT=1 (read when the graph is installed): the window's wheel insert runs on a
+    second stream beside the asynchronous reaction, and every other entry point first makes the
+    context stream wait for it. Measured slower, so off by default; still bit-exact."""
+    monkeypatch.setenv("TGSIM_SIDE_INSERT", "1")
+    n = 3000
+    a = S.run_flood(hip, n_inst=n, windows=40, count=False)
+    monkeypatch.delenv("TGSIM_SIDE_INSERT")
+    S.assert_same(a, S.run_flood(oracle, n_inst=n, windows=40, count=False))
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_flood_full_size(hip, oracle):
     """config 5 at full size: 1M instances, 8-regular, heterogeneous shapes; two publications, the
