@@ -265,7 +265,7 @@ struct Dev {
   // (maintained by k_wheel_scatter +, k_tb_bucket / k_emit_bucket / k_recv -); heavy = this window's
   // test (heavy.pend == nullptr: the host proved no sender can reach the limit); H = due wheel
   // records of heavy senders (copies, grouped by sender for k_shape_seq)
-  uint32_t* pend = nullptr;
+  uint32_t* pend = nullptr;        // [nloc << pend_shift(nloc)]: use pend_ref
   uint32_t* pend_part = nullptr;   // [kRadixBlocks] k_pend_max's per-block maxima
   // the window's wheel insert on a side stream (contexts with a flood graph): side_ev marks its end,
   // main_ev the point of the context stream it starts from; side_pending until the context stream
@@ -394,6 +394,7 @@ hipError_t launch_reset_tb(Dev& d, const uint32_t* locals_dev, uint32_t n);
 // retx: TCP pending per sender; inbox_mult: acks mode, packets per delivery of the sender's last inbox
 // per-block maxima into d.pend_part, then copied to host[kRadixBlocks] (pinned) on the stream
 hipError_t join_side(Dev& d);
+inline PendRef pend_ref(const Dev& d) { return PendRef{d.pend, pend_shift(d.nloc)}; }
 hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult, uint32_t* host);
 // sharded storm batch: generator partials -> red2 = {last, -first} (for a MAX all-reduce) -> the
 // batch's single partial in sig_part

@@ -142,8 +142,25 @@ constexpr int ST_OVERLIMIT = 13;  // a row counter only ([kNSub][16] rows; ST_DE
 // queued at the window start (pend) can count, and it is heavy only when they alone reach the limit
 // (zd: bit per local sender, from the shape table). The splitbrain target that receives 10k requests
 // in a window then answers them in the parallel netem pass instead of one wave's chunk walk.
+// Per-sender queue occupancy (pend): local sender l's count is word l << sh. The deliveries
+// decrement the counts with memory-side atomics, which serialise per line: a small shard's counts
+// in a few lines (config 2: 1000 senders in 32 lines, ~250k decrements per window) queued every
+// delivery workgroup behind the others, so up to kPendSpreadMax senders each count gets a 128-B
+// line of its own.
+#ifndef TG_PEND_SPREAD_MAX
+#define TG_PEND_SPREAD_MAX 16384u
+#endif
+constexpr uint32_t kPendSpreadMax = TG_PEND_SPREAD_MAX;
+__host__ __device__ constexpr uint32_t pend_shift(uint32_t nloc) { return nloc <= kPendSpreadMax ? 5u : 0u; }
+struct PendRef {
+  uint32_t* p;
+  uint32_t sh;
+  __host__ __device__ uint32_t& operator[](uint32_t l) const { return p[(size_t)l << sh]; }
+  __host__ __device__ explicit operator bool() const { return p != nullptr; }
+};
+
 struct Heavy {
-  const uint32_t* pend;   // nullptr: the host proved no sender can reach the limit this window
+  PendRef pend;           // null: the host proved no sender can reach the limit this window
   const uint32_t* inbox;  // [nloc + 1] the last window's inbox offsets (flood forwards), or nullptr
   const uint32_t* retx;   // TCP mode: [nloc] retransmissions pending or released into this window
   const uint32_t* zd;     // [nloc / 32 + 1] zero-delay unshaped senders

@@ -1431,7 +1431,7 @@ constexpr int kWheelUnroll = TG_WHEEL_UNROLL;
 // TGSIM_F_WHEEL) is counted in its sender's pend and marked; runs of one sender among a wave's 64
 // consecutive records share one atomic (the token bucket stages its output grouped by sender). The
 // atomics return nothing, so no wave waits on them.
-__device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uint32_t nloc, uint32_t src, bool add) {
+__device__ __forceinline__ void pend_count_wave(PendRef pend, uint32_t lo, uint32_t nloc, uint32_t src, bool add) {
   const uint32_t lane = lane_id();
   const uint32_t key = add && src - lo < nloc ? src - lo : 0xFFFFFFFFu;
   const uint32_t prev = __shfl_up(key, 1);
@@ -1453,7 +1453,7 @@ __device__ __forceinline__ void pend_count_wave(uint32_t* pend, uint32_t lo, uin
 // bounds mult * the sender's unsettled segments (tgsim_tcp.hip). TCP acks mode (refreshed every
 // window): pend + mult * (retransmissions released into the window + the deliveries the sender got
 // last window, each answered by at most one ACK).
-__global__ __launch_bounds__(kBlock) void k_pend_max(const uint32_t* pend, const uint32_t* retx, const uint32_t* inbox,
+__global__ __launch_bounds__(kBlock) void k_pend_max(PendRef pend, const uint32_t* retx, const uint32_t* inbox,
                                                      uint32_t inbox_mult, uint32_t mult, uint32_t nloc, uint32_t* part) {
   __shared__ uint32_t red[kBlock / 64];
   uint32_t mx = 0;
@@ -1485,7 +1485,7 @@ __device__ __forceinline__ void close_window_counters(DevScalars* sc) {
 
 __device__ __forceinline__ void wheel_scatter_body(const BktSrc& src, DevScalars* sc, const tgsim_record* L,
                                                    tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                   const uint32_t* histx, const uint32_t* tot, uint32_t* pend,
+                                                   const uint32_t* histx, const uint32_t* tot, PendRef pend,
                                                    uint32_t lo, uint32_t nloc, bool close = true) {
   __shared__ uint32_t base[kMaxBins];
   __shared__ uint32_t part[kBlock];
@@ -1928,7 +1928,7 @@ struct TBPolicy {
   const tgsim_record* A;
   const TbShape* shape;
   int64_t* X;
-  uint32_t* pend;  // queue occupancy: a wheel copy leaving now (D / X) no longer counts
+  PendRef pend;  // queue occupancy: a wheel copy leaving now (D / X) no longer counts
   uint32_t lo;
   Geo geo;
   Queues Q;
@@ -2077,7 +2077,7 @@ __device__ __forceinline__ void block_scan2(uint32_t& v0, uint32_t& v1, uint32_t
 
 struct EmitPolicy {
   const tgsim_record* D;
-  uint32_t* pend;  // queue occupancy: a delivered wheel copy of a local sender no longer counts
+  PendRef pend;  // queue occupancy: a delivered wheel copy of a local sender no longer counts
   uint32_t lo, nloc;
   int64_t* o_t;
   uint32_t *o_src, *o_dst, *o_seq, *o_size, *o_flags, *o_coff;
@@ -4686,7 +4686,7 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
 // (DESIGN.md 5). The scatter runs one workgroup per CU, so rest_body's LDS costs it no occupancy.
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                           tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                          const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                          const uint32_t* hist, const uint32_t* tot, PendRef pend,
                                                           uint32_t lo, uint32_t nloc, EmitPolicy p,
                                                           const uint32_t* keys, const uint32_t* vals,
                                                           const uint32_t* off, const uint32_t* medium,
@@ -4706,7 +4706,7 @@ __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars
 // deliveries follow at once.
 __global__ __launch_bounds__(kBlock) void k_wheel_insert(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                          tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                         const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                         const uint32_t* hist, const uint32_t* tot, PendRef pend,
                                                          uint32_t lo, uint32_t nloc) {
   wheel_scatter_body(src, sc, L, arena, dirs, slots, hist, tot, pend, lo, nloc, false);
 }
@@ -4745,7 +4745,7 @@ __host__ __device__ inline uint32_t recv_split(uint32_t xcap) {
   return cs > 2u * kBlock ? (cs + 2u * kBlock - 1u) / (2u * kBlock) : 1u;
 }
 __global__ __launch_bounds__(kBlock) void k_recv(const tgsim_record* xrecv, const tgsim_record* xsend, uint32_t S,
-                                                 uint32_t shard, uint32_t xcap, Queues Q, uint32_t* pend,
+                                                 uint32_t shard, uint32_t xcap, Queues Q, PendRef pend,
                                                  uint32_t lo, uint32_t nloc) {
   const int64_t t_end = Q.sc->t_end;
   const uint32_t G = x_slices(xcap), cs = x_slice_cap(xcap), split = recv_split(xcap);
@@ -4901,7 +4901,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_storm(StormArgs a, SigState sg) 
 // pass) and the signal partials (consumed by this window's start).
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter_gen(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                               tgsim_record* arena, uint32_t* dirs, uint32_t slots,
-                                                              const uint32_t* hist, const uint32_t* tot, uint32_t* pend,
+                                                              const uint32_t* hist, const uint32_t* tot, PendRef pend,
                                                               uint32_t lo, uint32_t nloc, EmitPolicy p,
                                                               const uint32_t* keys, const uint32_t* vals,
                                                               const uint32_t* off, const uint32_t* medium,
@@ -5125,7 +5125,7 @@ static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const ui
 // and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
 static hipError_t run_token_bucket(Dev& d) {
   TBPolicy p;
-  p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = d.pend; p.lo = d.lo; p.geo = make_geo(d); p.Q = make_queues(d);
+  p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = pend_ref(d); p.lo = d.lo; p.geo = make_geo(d); p.Q = make_queues(d);
   p.sc = d.sc;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= kMaxBins (bkt_width_fused)
@@ -5237,7 +5237,7 @@ hipError_t launch_storm_unpack(Dev& d, const int64_t* red2) {
 }
 
 hipError_t launch_pend_max(Dev& d, const uint32_t* retx, uint32_t inbox_mult, uint32_t mult, uint32_t* host) {
-  hipLaunchKernelGGL(k_pend_max, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, d.pend, retx,
+  hipLaunchKernelGGL(k_pend_max, dim3(kRadixBlocks), dim3(kBlock), 0, d.stream, pend_ref(d), retx,
                      inbox_mult ? d.inbox : nullptr, inbox_mult, mult, d.nloc, d.pend_part);
   TG_CHECK(hipGetLastError());
   return hipMemcpyAsync(host, d.pend_part, kRadixBlocks * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream);
@@ -5309,11 +5309,11 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
     Queues Q = make_queues(d);
     const uint32_t nb = d.S * x_slices(d.xcap) * recv_split(d.xcap);
     hipLaunchKernelGGL(k_recv, dim3(nb), dim3(kBlock), 0, d.stream, d.xrecv, d.xsend, d.S, d.shard,
-                       d.xcap, Q, d.pend, d.lo, d.nloc);
+                       d.xcap, Q, pend_ref(d), d.lo, d.nloc);
     TG_CHECK(hipGetLastError());
   }
   EmitPolicy p;
-  p.D = d.D; p.pend = d.pend; p.lo = d.lo; p.nloc = d.nloc; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
+  p.D = d.D; p.pend = pend_ref(d); p.lo = d.lo; p.nloc = d.nloc; p.o_t = d.o_t; p.o_src = d.o_src; p.o_dst = d.o_dst; p.o_seq = d.o_seq;
   p.o_size = d.o_size; p.o_flags = d.o_flags; p.o_coff = d.o_coff;
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
@@ -5338,7 +5338,7 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
     const uint64_t threads = (uint64_t)d.nloc * 8;
     const uint32_t g = (uint32_t)std::min<uint64_t>((threads + kBlock - 1) / kBlock, kSpecGenBlocks);
     hipLaunchKernelGGL(k_wheel_scatter_gen, dim3(kRadixBlocks + g + kListBlocks), dim3(kBlock), 0, d.stream, srcL,
-                       d.sc, d.L, d.arena, d.dirs, d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0,
+                       d.sc, d.L, d.arena, d.dirs, d.slots, d.histx, d.tot, pend_ref(d), d.lo, d.nloc, p, d.keys0, d.vals0,
                        d.seg_off, d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b, ga, sig_state(d), g);
     *spec_parts = g;
   } else if (d.side) {  // the insert beside what follows the window (the flood's reaction)
@@ -5347,7 +5347,7 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
     {
       ProfScope ps_(d, KID_REGION_FILL, d.side);
       hipLaunchKernelGGL(k_wheel_insert, dim3(kRadixBlocks), dim3(kBlock), 0, d.side, srcL, d.sc, d.L, d.arena, d.dirs,
-                         d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc);
+                         d.slots, d.histx, d.tot, pend_ref(d), d.lo, d.nloc);
     }
     TG_CHECK(hipGetLastError());
     TG_CHECK(hipEventRecord(d.side_ev, d.side));
@@ -5358,7 +5358,7 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
   } else {
     ProfScope ps_(d, KID_REGION_FILL);
     hipLaunchKernelGGL(k_wheel_scatter, dim3(kRadixBlocks + kListBlocks), dim3(kBlock), 0, d.stream, srcL, d.sc, d.L,
-                       d.arena, d.dirs, d.slots, d.histx, d.tot, d.pend, d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
+                       d.arena, d.dirs, d.slots, d.histx, d.tot, pend_ref(d), d.lo, d.nloc, p, d.keys0, d.vals0, d.seg_off,
                        d.medium, d.large, d.K1a, d.K2a, d.K3a, d.K1b, d.K2b, d.K3b);
   }
   return hipGetLastError();

@@ -488,7 +488,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.tbs, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &d.zd, (size_t)c->nloc / 32 + 1);
   rc |= dalloc(c, &d.X, std::max<size_t>(c->nloc, 1));
-  rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1));
+  rc |= dalloc(c, &d.pend, std::max<size_t>(c->nloc, 1) << pend_shift(c->nloc));
   rc |= dalloc(c, &d.seq_done, std::max<size_t>(c->nloc, 1));
   rc |= dalloc(c, &c->d_red2, 2);
   rc |= dalloc(c, &d.moff, segK);
@@ -581,7 +581,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
             hipMemsetAsync(d.st_last, 0, d.max_states * sizeof(int64_t), s) == hipSuccess &&
             hipMemsetAsync(d.rule_off, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
             hipMemsetAsync(d.inbox, 0, nl1 * sizeof(uint32_t), s) == hipSuccess &&
-            hipMemsetAsync(d.pend, 0, std::max<size_t>(c->nloc, 1) * sizeof(uint32_t), s) == hipSuccess;
+            hipMemsetAsync(d.pend, 0, (std::max<size_t>(c->nloc, 1) << pend_shift(c->nloc)) * sizeof(uint32_t), s) == hipSuccess;
   if (!ok) return TGSIM_EHIP;
 
   // initial state = after the sidecar's Config{Network:"default", Enable:true} (sidecar_handler.go:26-29)
@@ -1231,7 +1231,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
         return TGSIM_ENOMEM;
       d.h_cap = (uint32_t)cap;
     }
-    d.heavy.pend = d.pend;
+    d.heavy.pend = pend_ref(d);
     d.heavy.zd = d.zd;
     d.heavy.inbox = c->win_m_inbox ? d.inbox : nullptr;
     d.heavy.retx = c->tcp_on ? c->td.pend_by : nullptr;  // single shard: local = global ids
@@ -3438,7 +3438,7 @@ std::vector<std::pair<void*, size_t>> snap_regions(tgsim_ctx* c) {
   return {
       {d.sc, sizeof(DevScalars)},
       {d.X, 8 * nl},
-      {d.pend, 4 * nl},
+      {d.pend, (4 * nl) << pend_shift(c->nloc)},
       {d.cor_last, 16 * nl},
       {d.arena, sizeof(tgsim_record) * d.cap_arena},
       {d.regions, sizeof(RegionDev) * kMaxRegions},
