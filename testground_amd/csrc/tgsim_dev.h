@@ -252,7 +252,7 @@ struct Dev {
   // netem correlations: per local sender (dup, corrupt, reorder, -) rho and crandom state
   uint32_t* cor_rho = nullptr;    // [4 * nloc]
   uint32_t* cor_last = nullptr;   // [4 * nloc]
-  uint32_t* corr_idx = nullptr;   // [cap_msgs] deferred message indices (k_shape)
+  uint32_t* corr_idx = nullptr;   // [kDeferSub][defer_seg_cap(cap_msgs)] deferred message indices (k_shape)
   uint32_t* corr_sorted = nullptr;  // [cap_msgs] the same, grouped by sender in (t_send, seq) order
   bool any_corr = false;          // some local shape has kShCorr
   // some local sender has ever been bandwidth-limited (kShLimited): only then can a copy reach the

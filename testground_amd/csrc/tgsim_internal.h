@@ -28,8 +28,16 @@ constexpr int kMaxShards = 64;
 constexpr uint32_t kXSlices = 8;
 __host__ __device__ inline uint32_t x_slices(uint32_t xcap) { return xcap - 1u >= kXSlices * 64u ? kXSlices : 1u; }
 __host__ __device__ inline uint32_t x_slice_cap(uint32_t xcap) { return (xcap - 1u) / x_slices(xcap); }
-// A / D / L sub-queue counters, then the exchange cursors (peer p, slice g) at line 3 kNSub + p kXSlices + g
-constexpr int kQcLines = 3 * kNSub + kXSlices * kMaxShards;
+// A / D / L sub-queue counters, then the exchange cursors (peer p, slice g) at line 3 kNSub + p kXSlices + g,
+// then the deferred-message sub-lists' counters (k_shape: message chunk c appends to sub-list c % kDeferSub)
+constexpr int kDeferSub = 16;
+constexpr int kQcDefer = 3 * kNSub + kXSlices * kMaxShards;
+constexpr int kQcLines = kQcDefer + kDeferSub;
+// capacity of one deferred-message sub-list: sub-list s takes chunks s, s + kDeferSub, ... of 256
+// messages, at most ceil(chunks / kDeferSub) of them
+__host__ __device__ inline uint32_t defer_seg_cap(uint32_t cap_msgs) {
+  return ((cap_msgs + 255u) / 256u + (uint32_t)kDeferSub - 1u) / (uint32_t)kDeferSub * 256u;
+}
 constexpr int kMaxRegions = 8192;        // live timing-wheel regions (one per window)
 constexpr int kStreamBlocks = 2048;      // grid of grid-stride streaming kernels
 constexpr int64_t kNegInf = INT64_MIN / 4;

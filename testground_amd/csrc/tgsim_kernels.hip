@@ -410,7 +410,8 @@ struct ShapeArgs {
   Geo geo;
   Queues Q;
   unsigned long long* stats;  // [kNSub][16] sharded counters
-  uint32_t* corr_idx;         // deferred messages of correlated / queue-heavy senders (count sc->n_corr)
+  uint32_t* corr_idx;         // deferred messages of correlated / queue-heavy senders: kDeferSub sub-lists of
+  uint32_t corr_seg;          // corr_seg entries each, counted on qc lines kQcDefer + s (k_keys_corr joins them)
   Heavy heavy;                // the window's queue-limit test
   uint32_t may_defer;         // some shape is correlated or the queue-limit test is on
 };
@@ -538,7 +539,10 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   // an iteration pays one load round trip, not two.
   // Deferred messages (correlated / queue-heavy senders) are listed with one reservation per block
   // and round: an all-to-all round defers every message, and a reservation per wave serialised ~16k
-  // atomics on sc->n_corr (~160 us). The loop is block-uniform for it; lanes past n idle.
+  // atomics on one counter (~160 us); one per block still made a chain of ~4k memory-side atomics
+  // on one line (~11 ns each: most of config 2's netem launch), so the round's chunk picks one of
+  // kDeferSub sub-lists, each counter on a line of its own. The loop is block-uniform for it; lanes
+  // past n idle.
   __shared__ uint32_t s_cred[kBlock / 64];
   __shared__ uint32_t s_cbase;
   uint32_t i = bid * blockDim.x + threadIdx.x;
@@ -637,9 +641,14 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
       uint32_t tot;
       const uint32_t pos = block_excl_scan(deferred ? 1u : 0u, s_cred, tot);
       if (tot) {  // block-uniform
-        if (threadIdx.x == 0) s_cbase = atomicAdd(&sc->n_corr, tot);
+        const uint32_t ds = (b0 >> 8) % (uint32_t)kDeferSub;
+        if (threadIdx.x == 0) {
+          const uint32_t at = atomicAdd(a.Q.qc + ((uint32_t)(kQcDefer + ds) << 5), tot);
+          if (at + tot > a.corr_seg) atomicOr(&sc->err, ERR_CAP_M);  // cannot happen: n <= cap_msgs
+          s_cbase = at + tot <= a.corr_seg ? ds * a.corr_seg + at : 0xFFFFFFFFu;
+        }
         __syncthreads();
-        if (deferred) a.corr_idx[s_cbase + pos] = i;
+        if (deferred && s_cbase != 0xFFFFFFFFu) a.corr_idx[s_cbase + pos] = i;
         __syncthreads();  // s_cbase is rewritten by the next round
       }
     }
@@ -2706,18 +2715,31 @@ struct SigPolicy {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* src, const uint32_t* n_ptr,
+// The deferred messages' sub-lists joined into one (key = local sender, value = message index);
+// their total goes to *n_out (the group-by's count)
+__global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* qc, uint32_t seg,
+                                                      const uint32_t* src, uint32_t* n_out,
                                                       uint32_t lo, uint32_t* keys, uint32_t* vals,
                                                       unsigned long long* kc_deferred, uint32_t* seq_left,
                                                       uint32_t seq_left0) {
-  const uint32_t n = *n_ptr;
+  __shared__ uint32_t pre[kDeferSub + 1];
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int s = 0; s < kDeferSub; ++s) { pre[s] = run; run += min(qc[(uint32_t)(kQcDefer + s) << 5], seg); }
+    pre[kDeferSub] = run;
+  }
+  __syncthreads();
+  const uint32_t n = pre[kDeferSub];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *n_out = n;
     atomicAdd(kc_deferred, (unsigned long long)n);
     *seq_left = seq_left0;  // k_shape_seq_wide counts up from here (a memset would be a launch of its own)
   }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-    const uint32_t i = idx[j];
+    uint32_t s = 0;
+    while (pre[s + 1] <= j) ++s;
+    const uint32_t i = idx[s * seg + (j - pre[s])];
     keys[j] = src[i] - lo;
     vals[j] = i;
   }
@@ -5145,8 +5167,8 @@ static hipError_t run_token_bucket(Dev& d) {
 // (t_send, seq); the heavy senders' due wheel records (H) grouped by sender; then k_shape_seq.
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
-  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.m_src, n_dev,
-                     d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
+  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.qc,
+                     defer_seg_cap(d.cap_msgs), d.m_src, n_dev, d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
   TG_CHECK(hipGetLastError());
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
@@ -5271,6 +5293,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = make_geo(d); a.Q = Q;
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
+    a.corr_seg = defer_seg_cap(d.cap_msgs);
     a.heavy = d.heavy;
     a.may_defer = (d.any_corr || d.heavy.pend) ? 1u : 0u;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups

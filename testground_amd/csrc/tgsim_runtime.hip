@@ -502,7 +502,7 @@ static int create_impl(const tgsim_config* cfg, tgsim_ctx** out) {
   rc |= dalloc(c, &d.m_size, d.cap_msgs);
   rc |= dalloc(c, &d.m_t, d.cap_msgs);
   rc |= dalloc(c, &d.status, d.cap_msgs);
-  rc |= dalloc(c, &d.corr_idx, d.cap_msgs);
+  rc |= dalloc(c, &d.corr_idx, (size_t)kDeferSub * defer_seg_cap(d.cap_msgs));
   rc |= dalloc(c, &d.corr_sorted, d.cap_msgs);
   rc |= dalloc(c, &d.cor_rho, 4 * (size_t)std::max<uint32_t>(c->nloc, 1));
   rc |= dalloc(c, &d.cor_last, 4 * (size_t)std::max<uint32_t>(c->nloc, 1));
