@@ -128,9 +128,15 @@ def pmc_traffic(kernel: str, workload: str, n_gpus: int):
             continue
         if j.get("source_hash") != want or j.get("workload") != workload or j.get("n_gpus") != n_gpus:
             continue
-        k = j.get("kernels", {}).get(kernel)
+        ks = j.get("kernels", {})
+        k = ks.get(kernel)
         if k:
             return k["traffic_bytes"], os.path.relpath(path, ROOT)
+        # a templated kernel (k_extract_shape<false> / <true>): the launch-weighted mean of its forms
+        forms = [v for name, v in ks.items() if name.startswith(kernel + "<") and v.get("launches")]
+        if forms:
+            n = sum(v["launches"] for v in forms)
+            return sum(v["traffic_bytes"] * v["launches"] for v in forms) / n, os.path.relpath(path, ROOT)
     return None, None
 
 

@@ -411,7 +411,7 @@ struct ShapeArgs {
   Queues Q;
   unsigned long long* stats;  // [kNSub][16] sharded counters
   uint32_t* corr_idx;         // deferred messages of correlated / queue-heavy senders: kDeferSub sub-lists of
-  uint32_t corr_seg;          // corr_seg entries each, counted on qc lines kQcDefer + s (k_keys_corr joins them)
+                              // defer_seg_cap(n) entries, counted on qc lines kQcDefer + s (k_keys_corr joins them)
   Heavy heavy;                // the window's queue-limit test
   uint32_t may_defer;         // some shape is correlated or the queue-limit test is on
 };
@@ -525,6 +525,10 @@ __device__ __forceinline__ int qid_copy(const Geo& geo, const tgsim_record& r, i
   return r.t < t_end ? Q_A : Q_L;
 }
 
+// The deferred messages' list (a.may_defer): kSharded, kDeferSub sub-lists (a queue-limit window,
+// where an all-to-all round defers every message); else one list behind one counter (sc->n_corr:
+// correlated senders only, few messages). Both are complete forms; the host picks by the window.
+template <bool kSharded>
 __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uint32_t nblocks) {
   DevScalars* sc = a.Q.sc;
   const int64_t H = sc->H, t_end = sc->t_end;
@@ -641,14 +645,14 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
       uint32_t tot;
       const uint32_t pos = block_excl_scan(deferred ? 1u : 0u, s_cred, tot);
       if (tot) {  // block-uniform
-        const uint32_t ds = (b0 >> 8) % (uint32_t)kDeferSub;
-        if (threadIdx.x == 0) {
-          const uint32_t at = atomicAdd(a.Q.qc + ((uint32_t)(kQcDefer + ds) << 5), tot);
-          if (at + tot > a.corr_seg) atomicOr(&sc->err, ERR_CAP_M);  // cannot happen: n <= cap_msgs
-          s_cbase = at + tot <= a.corr_seg ? ds * a.corr_seg + at : 0xFFFFFFFFu;
+        if (!kSharded) {
+          if (threadIdx.x == 0) s_cbase = atomicAdd(&sc->n_corr, tot);
+        } else if (threadIdx.x == 0) {  // the sub-list holds its chunks of the n messages (defer_seg_cap)
+          const uint32_t ds = (b0 >> 8) % (uint32_t)kDeferSub;
+          s_cbase = ds * defer_seg_cap(n) + atomicAdd(a.Q.qc + ((uint32_t)(kQcDefer + ds) << 5), tot);
         }
         __syncthreads();
-        if (deferred && s_cbase != 0xFFFFFFFFu) a.corr_idx[s_cbase + pos] = i;
+        if (deferred) a.corr_idx[s_cbase + pos] = i;
         __syncthreads();  // s_cbase is rewritten by the next round
       }
     }
@@ -673,7 +677,7 @@ __device__ __forceinline__ void shape_body(const ShapeArgs& a, uint32_t bid, uin
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) { shape_body(a, blockIdx.x, gridDim.x); }
+__global__ __launch_bounds__(kBlock) void k_shape(ShapeArgs a) { shape_body<false>(a, blockIdx.x, gridDim.x); }
 
 // ============================================================================================
 // timing wheel: plan (which slot prefixes of which live regions are due), extract, insert
@@ -845,11 +849,12 @@ __global__ __launch_bounds__(kBlock) void k_extract(const RegionDev* regions, co
 // launch: blocks [0, ne) extract, the rest shape. ne is a multiple of 8, so every block keeps the
 // XCD (blockIdx mod 8) its sub-queue choice assumes.
 // five waves per SIMD (<= 96 VGPRs, as before the exchange cursors moved; 98 made it four)
+template <bool kSharded>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_extract_shape(const RegionDev* regions, const uint32_t* plan_start,
                                                           const uint32_t* plan_off, const tgsim_record* arena,
                                                           Queues Q, ShapeArgs a, uint32_t ne, HeavyOut ho) {
   if (blockIdx.x < ne) extract_body(regions, plan_start, plan_off, arena, Q, blockIdx.x, ne, ho);
-  else shape_body(a, blockIdx.x - ne, gridDim.x - ne);
+  else shape_body<kSharded>(a, blockIdx.x - ne, gridDim.x - ne);
 }
 
 // Allocate this window's region in the arena ring (one thread).
@@ -2716,22 +2721,27 @@ struct SigPolicy {
 };
 
 // The deferred messages' sub-lists joined into one (key = local sender, value = message index);
-// their total goes to *n_out (the group-by's count)
-__global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, const uint32_t* qc, uint32_t seg,
-                                                      const uint32_t* src, uint32_t* n_out,
+// their total goes to *n_out (the group-by's count). sharded 0: one list, *n_out already its count.
+__global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, uint32_t sharded, const uint32_t* qc,
+                                                      const uint32_t* n_dev, uint32_t n_cap, const uint32_t* src,
+                                                      uint32_t* n_out,
                                                       uint32_t lo, uint32_t* keys, uint32_t* vals,
                                                       unsigned long long* kc_deferred, uint32_t* seq_left,
                                                       uint32_t seq_left0) {
   __shared__ uint32_t pre[kDeferSub + 1];
+  const uint32_t seg = defer_seg_cap(n_dev ? min(*n_dev, n_cap) : n_cap);  // as the shape pass sized it
   if (threadIdx.x == 0) {
     uint32_t run = 0;
-    for (int s = 0; s < kDeferSub; ++s) { pre[s] = run; run += min(qc[(uint32_t)(kQcDefer + s) << 5], seg); }
+    for (int s = 0; s < kDeferSub; ++s) {
+      pre[s] = run;
+      run += sharded ? min(qc[(uint32_t)(kQcDefer + s) << 5], seg) : (s == 0 ? *n_out : 0u);
+    }
     pre[kDeferSub] = run;
   }
   __syncthreads();
   const uint32_t n = pre[kDeferSub];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *n_out = n;
+    if (sharded) *n_out = n;
     atomicAdd(kc_deferred, (unsigned long long)n);
     *seq_left = seq_left0;  // k_shape_seq_wide counts up from here (a memset would be a launch of its own)
   }
@@ -3525,7 +3535,12 @@ __device__ uint64_t g_wide_ph[4096][12];
 #else
 #define WIDE_PH(k) do {} while (0)
 #endif
-__global__ __launch_bounds__(kWide) void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,  // may alias
+#ifdef TG_WIDE_WPE
+#define TG_WIDE_ATTR __attribute__((amdgpu_waves_per_eu(TG_WIDE_WPE)))
+#else
+#define TG_WIDE_ATTR
+#endif
+__global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs a, const uint32_t* gvals, uint32_t* sorted,  // may alias
                                                           const uint32_t* moff, const uint32_t* hoff,
                                                           const uint32_t* hidx, const tgsim_record* H,
                                                           uint8_t* done) {
@@ -5167,8 +5182,8 @@ static hipError_t run_token_bucket(Dev& d) {
 // (t_send, seq); the heavy senders' due wheel records (H) grouped by sender; then k_shape_seq.
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
-  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx, d.qc,
-                     defer_seg_cap(d.cap_msgs), d.m_src, n_dev, d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
+  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx,
+                     a.heavy.pend ? 1u : 0u, d.qc, a.n_dev, n_staged, d.m_src, n_dev, d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
   TG_CHECK(hipGetLastError());
   BktSrc src = bkt_queue(d, Q_A);
   src.keys = d.keys0; src.vals = d.vals0; src.qc = nullptr; src.mode = 3; src.n_ptr = n_dev;
@@ -5293,7 +5308,6 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     a.data_len = d.data_len; a.key0 = d.key0; a.key1 = d.key1; a.geo = make_geo(d); a.Q = Q;
     a.stats = d.stats;
     a.corr_idx = d.corr_idx;
-    a.corr_seg = defer_seg_cap(d.cap_msgs);
     a.heavy = d.heavy;
     a.may_defer = (d.any_corr || d.heavy.pend) ? 1u : 0u;
     const unsigned g = std::min<unsigned>(grid_for(n_staged), (unsigned)d.grid_shape);  // one wave of workgroups
@@ -5301,7 +5315,7 @@ hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
     static_assert(ne % 8 == 0, "extract blocks keep their XCD");
     {
       ProfScope ps_(d, KID_SHAPE);  // extraction + netem
-      hipLaunchKernelGGL(k_extract_shape, dim3(ne + g), dim3(kBlock), 0, d.stream, d.regions,
+      hipLaunchKernelGGL(d.heavy.pend ? k_extract_shape<true> : k_extract_shape<false>, dim3(ne + g), dim3(kBlock), 0, d.stream, d.regions,
                          d.plan_start, d.plan_off, d.arena, Q, a, ne, ho);
     }
     TG_CHECK(hipGetLastError());
