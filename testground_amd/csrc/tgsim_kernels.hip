@@ -3551,43 +3551,77 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
   __shared__ uint32_t Ms[kWide], Md[kWide], Mz[kWide], Mi[kWide];
   __shared__ uint32_t red[kWideWaves];
   __shared__ int64_t red64[kWideWaves], rmin[kWideWaves], rmax[kWideWaves];
-  __shared__ uint32_t s_flag, s_stage_a, s_big, s_tot[3];
+  __shared__ uint32_t s_flag, s_stage_a, s_big, s_wtot[kWideWaves][3];
   DevScalars* sc = a.Q.sc;
   const int64_t t_end = sc->t_end;
   const uint32_t tid = threadIdx.x;
+  // A block walks its senders one ahead: the next sender's loads - two dependent levels, (message
+  // index, due record index), then (the message's fields, the due record) - are in flight while
+  // this sender sorts and decides (the first level from the top of the iteration, the second from
+  // the end of the due-record count; 3.6 us of a ~19-us sender were these loads, waited for).
+  struct Meta { uint32_t j0, n, h0, n0; bool elig; };
+  struct Pf { int64_t ts; uint64_t kx; uint32_t i, sq, dst, size; bool stage_a; };
+  auto meta_of = [&](uint32_t l) {
+    Meta m{0u, 0u, 0u, 0u, false};
+    if (l >= a.nloc) return m;
+    m.j0 = moff[l];
+    m.n = moff[l + 1] - m.j0;
+    if (m.n == 0 || m.n > (uint32_t)kWide) return m;
+    const ShapeDev sh = a.shape[l];
+    m.h0 = hoff ? hoff[l] : 0u;
+    m.n0 = (hoff ? hoff[l + 1] : 0u) - m.h0;
+    // block-uniform: the closed form needs queue tracking without HTB or correlation
+    m.elig = hoff && a.heavy.of(l) && !(sh.flags & (kShCorr | kShLimited)) && m.n0 <= (uint32_t)kWide;
+    return m;
+  };
+  auto load1 = [&](const Meta& m, uint32_t& qi, uint32_t& qhx) {
+    qi = 0;
+    qhx = 0;
+    if (m.n > (uint32_t)kWide) return;
+    if (tid < m.n) qi = gvals[m.j0 + tid];
+    if (m.elig && tid < m.n0) qhx = hidx[m.h0 + tid];
+  };
+  auto load2 = [&](const Meta& m, uint32_t qi, uint32_t qhx, Pf& p) {
+    p.ts = 0; p.kx = ~0ull; p.i = qi; p.sq = 0; p.dst = 0; p.size = 0; p.stage_a = false;
+    if (m.n > (uint32_t)kWide) return;
+    if (tid < m.n) { p.ts = a.t[qi]; p.sq = a.seq[qi]; p.dst = a.dst[qi]; p.size = a.size[qi]; }
+    if (m.elig && tid < m.n0) {
+      tgsim_record r;
+      load_rec(H + qhx, r);
+      p.kx = (uint64_t)r.t ^ 0x8000000000000000ull;
+      p.stage_a = !(r.meta & TGSIM_F_STAGE_D);  // queued under an earlier, shaped Shape: k_shape_seq's heaps
+    }
+  };
+  Meta nm = meta_of(blockIdx.x);
+  Pf pf;
+  {
+    uint32_t qi, qhx;
+    load1(nm, qi, qhx);
+    load2(nm, qi, qhx, pf);
+  }
   for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
-    const uint32_t j0 = moff[l], j1 = moff[l + 1], n = j1 - j0;
-    if (n == 0) continue;
+    const Meta cm = nm;
+    const uint32_t j0 = cm.j0, n = cm.n, n0 = cm.n0;
+    const bool elig = cm.elig;
+    const uint32_t i = pf.i;
+    int64_t ts = pf.ts;
+    uint32_t sq = pf.sq;
+    const uint32_t mdst = pf.dst, msize = pf.size;
+    uint64_t kx = pf.kx;
+    const bool stage_a = pf.stage_a;
+    nm = meta_of(l + gridDim.x);
+    uint32_t qi, qhx;
+    load1(nm, qi, qhx);
+    if (n == 0) { load2(nm, qi, qhx, pf); continue; }
     if (n > (uint32_t)kWide) {  // k_rest ordered it; k_shape_seq walks it
       if (tid == 0) { done[l] = 0; atomicAdd(&sc->seq_left, 1u); }
+      load2(nm, qi, qhx, pf);
       continue;
     }
     WIDE_PH(0);
     const ShapeDev sh = a.shape[l];
-    const uint32_t h0 = hoff ? hoff[l] : 0u, h1 = hoff ? hoff[l + 1] : 0u, n0 = h1 - h0;
-    // block-uniform: the closed form needs queue tracking without HTB or correlation
-    const bool elig = hoff && a.heavy.of(l) && !(sh.flags & (kShCorr | kShLimited)) && n0 <= (uint32_t)kWide;
     if (tid == 0) { s_flag = 0; s_stage_a = 0; s_big = 0; }
-    // every load up front, two dependent levels: (message index, due record index), then (the
-    // message's fields, the due record)
-    uint32_t i = 0, hx = 0;
-    if (tid < n) i = gvals[j0 + tid];
-    if (elig && tid < n0) hx = hidx[h0 + tid];
-    int64_t ts = 0;
-    uint32_t sq = 0;
-    uint64_t kx = ~0ull;
-    if (tid < n) {
-      ts = a.t[i];
-      sq = a.seq[i];
-      Mt[tid] = ts; Ms[tid] = sq; Md[tid] = a.dst[i]; Mz[tid] = a.size[i]; Mi[tid] = i;
-    }
-    bool stage_a = false;
-    if (elig && tid < n0) {
-      tgsim_record r;
-      load_rec(H + hx, r);
-      kx = (uint64_t)r.t ^ 0x8000000000000000ull;
-      stage_a = !(r.meta & TGSIM_F_STAGE_D);  // queued under an earlier, shaped Shape: k_shape_seq's heaps
-    }
+    if (tid < n) { Mt[tid] = ts; Ms[tid] = sq; Md[tid] = mdst; Mz[tid] = msize; Mi[tid] = i; }
 #ifdef TGSIM_PHASE_PROF
     if (tid < n) Mi[tid] += (uint32_t)(kx & 0);  // the loads complete before the clock below
 #endif
@@ -3657,6 +3691,7 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
     WIDE_PH(1);
     if (!elig || s_stage_a) {  // block-uniform: k_shape_seq walks it
       if (tid == 0) { done[l] = 0; atomicAdd(&sc->seq_left, 1u); }
+      load2(nm, qi, qhx, pf);
       __syncthreads();  // every thread's reads of this sender's LDS are done
       continue;
     }
@@ -3684,6 +3719,7 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
       gone = wide_excl_scan(h, red, tk) + h;
     }
     WIDE_PH(2);
+    load2(nm, qi, qhx, pf);  // the next sender's second level, in flight through the decisions
     const uint32_t pnd = a.heavy.pend[l];
     const int64_t far = pnd > n0 ? (int64_t)(pnd - n0) : 0;
     // this thread's message: its copies (clone first) and netem times, as k_shape_seq's parallel form
@@ -3849,20 +3885,18 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
     const tgsim_record rs[2] = {r1, r2};
     a.Q.push_batch<2, kWideWaves>(qs, rs, l + (tid >> 6), true);
     WIDE_PH(5);
-    // the sender's counters: per wave sums, one LDS atomic each, one barrier
-    if (tid < 3) s_tot[tid] = 0;
-    __syncthreads();
+    // the sender's counters: per wave sums into the wave's LDS slots, one barrier, thread 0 folds
+    // them. No barrier after: the slots are next written at the next sender's tail, and every other
+    // LDS array of this sender was last read before the barrier above.
     {
       const uint32_t wl = wave_sum(n_lost), wc = wave_sum(n_copies), wo = wave_sum(n_over);
-      if (lane_id() == 0) {
-        if (wl) atomicAdd(&s_tot[0], wl);
-        if (wc) atomicAdd(&s_tot[1], wc);
-        if (wo) atomicAdd(&s_tot[2], wo);
-      }
+      if (lane_id() == 0) { s_wtot[tid >> 6][0] = wl; s_wtot[tid >> 6][1] = wc; s_wtot[tid >> 6][2] = wo; }
     }
     __syncthreads();
     if (tid == 0) {
-      const uint32_t tl = s_tot[0], tc = s_tot[1], to = s_tot[2];
+      uint32_t tl = 0, tc = 0, to = 0;
+#pragma unroll
+      for (int w = 0; w < kWideWaves; ++w) { tl += s_wtot[w][0]; tc += s_wtot[w][1]; to += s_wtot[w][2]; }
       unsigned long long* row = a.stats + (size_t)(l & (kNSub - 1)) * 16;
       if (tl) atomicAdd(&row[ST_LOST], (unsigned long long)tl);
       if (tc) atomicAdd(&row[ST_COPIES], (unsigned long long)tc);
@@ -3870,7 +3904,6 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
       atomicAdd(&sc->kc[KC_WIDE], (unsigned long long)n);
       done[l] = 1;
     }
-    __syncthreads();
     WIDE_PH(6);
   }
 }
@@ -5178,6 +5211,13 @@ static hipError_t run_token_bucket(Dev& d) {
   return launch_rest(d, p, d.keys0, d.vals0);
 }
 
+// k_shape_seq_wide's grid: one workgroup per CU (its 16 waves at <= 128 VGPRs fill the CU), each
+// walking its senders one ahead (the next sender's loads in flight); a workgroup per sender left
+// every first sender's loads exposed
+static uint32_t wide_grid(const Dev& d) {
+  return std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), (uint32_t)std::max(d.n_cu, 1));
+}
+
 // The deferred messages (k_shape: correlated or queue-heavy senders): group by sender, order
 // (t_send, seq); the heavy senders' due wheel records (H) grouped by sender; then k_shape_seq.
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
@@ -5221,8 +5261,8 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
     const unsigned g = (unsigned)std::min<uint32_t>(std::max<uint32_t>(d.nloc, 1u), 4096u);
     {
       ProfScope ps_(d, KID_SHAPE_WIDE);
-      hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
-                         d.hoff, d.hvals1, d.H, d.seq_done);
+      hipLaunchKernelGGL(k_shape_seq_wide, dim3(wide_grid(d)), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted,
+                         d.moff, d.hoff, d.hvals1, d.H, d.seq_done);
     }
     ProfScope ps_(d, KID_SHAPE_SEQ);
     hipLaunchKernelGGL(k_shape_seq, dim3(g), dim3(kSeqChunk), 0, d.stream, a, d.corr_sorted, d.moff, d.hoff, d.hvals1,
@@ -5253,8 +5293,8 @@ static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   // k_keys_corr above)
   if (a.heavy.pend) {  // the whole-sender closed form first (heavy senders without HTB / correlation)
     ProfScope ps_(d, KID_SHAPE_WIDE);
-    hipLaunchKernelGGL(k_shape_seq_wide, dim3(g), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted, d.moff,
-                       hoff, hidx, d.H, d.seq_done);
+    hipLaunchKernelGGL(k_shape_seq_wide, dim3(wide_grid(d)), dim3(kWide), 0, d.stream, a, d.corr_sorted, d.corr_sorted,
+                       d.moff, hoff, hidx, d.H, d.seq_done);
   } else {
     TG_CHECK(hipMemsetAsync(d.seq_done, 0, std::max<uint32_t>(d.nloc, 1u), d.stream));
   }
