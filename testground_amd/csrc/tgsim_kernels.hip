@@ -3551,6 +3551,7 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
   __shared__ uint32_t Ms[kWide], Md[kWide], Mz[kWide], Mi[kWide];
   __shared__ uint32_t red[kWideWaves];
   __shared__ int64_t red64[kWideWaves], rmin[kWideWaves], rmax[kWideWaves];
+  __shared__ int64_t rnmin[kWideWaves], rnmax[kWideWaves];  // the next sender's send-time range, per wave
   __shared__ uint32_t s_flag, s_stage_a, s_big, s_wtot[kWideWaves][3];
   DevScalars* sc = a.Q.sc;
   const int64_t t_end = sc->t_end;
@@ -3599,7 +3600,12 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
     load1(nm, qi, qhx);
     load2(nm, qi, qhx, pf);
   }
+  // true: the last sender's tail published this sender's send-time range (rnmin / rnmax) and reset
+  // the flags, so the sort starts without a barrier of its own (block-uniform)
+  bool mm_ready = false;
   for (uint32_t l = blockIdx.x; l < a.nloc; l += gridDim.x) {  // block-uniform
+    const bool mm = mm_ready;
+    mm_ready = false;
     const Meta cm = nm;
     const uint32_t j0 = cm.j0, n = cm.n, n0 = cm.n0;
     const bool elig = cm.elig;
@@ -3620,7 +3626,7 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
     }
     WIDE_PH(0);
     const ShapeDev sh = a.shape[l];
-    if (tid == 0) { s_flag = 0; s_stage_a = 0; s_big = 0; }
+    if (!mm && tid == 0) { s_flag = 0; s_stage_a = 0; s_big = 0; }
     if (tid < n) { Mt[tid] = ts; Ms[tid] = sq; Md[tid] = mdst; Mz[tid] = msize; Mi[tid] = i; }
 #ifdef TGSIM_PHASE_PROF
     if (tid < n) Mi[tid] += (uint32_t)(kx & 0);  // the loads complete before the clock below
@@ -3632,21 +3638,31 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
     // span less than 2^22 ns and no two messages share (t_send, seq); else the exact sort over
     // (t_send, seq, index) in LDS.
     const uint32_t np2m = n > 1 ? next_pow2(n) : 1u;
-    int64_t mn = tid < n ? ts : INT64_MAX, mx = tid < n ? ts : INT64_MIN;
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    if (mm) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const int64_t x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
-      mn = x < mn ? x : mn;
-      mx = y > mx ? y : mx;
-    }
-    if (lane_id() == 0) { rmin[tid >> 6] = mn; rmax[tid >> 6] = mx; }
-    __syncthreads();
-    if (stage_a) s_stage_a = 1u;
+      for (int w = 0; w < kWideWaves; ++w) {
+        mn = rnmin[w] < mn ? rnmin[w] : mn;
+        mx = rnmax[w] > mx ? rnmax[w] : mx;
+      }
+    } else {
+      mn = tid < n ? ts : INT64_MAX;
+      mx = tid < n ? ts : INT64_MIN;
 #pragma unroll
-    for (int w = 0; w < kWideWaves; ++w) {
-      mn = rmin[w] < mn ? rmin[w] : mn;
-      mx = rmax[w] > mx ? rmax[w] : mx;
+      for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
+        mn = x < mn ? x : mn;
+        mx = y > mx ? y : mx;
+      }
+      if (lane_id() == 0) { rmin[tid >> 6] = mn; rmax[tid >> 6] = mx; }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kWideWaves; ++w) {
+        mn = rmin[w] < mn ? rmin[w] : mn;
+        mx = rmax[w] > mx ? rmax[w] : mx;
+      }
     }
+    if (stage_a) s_stage_a = 1u;  // read after the sort's barriers
     const bool packed = (uint64_t)(mx - mn) < (1ull << 22);  // block-uniform
     WIDE_PH(8);
     if (packed) {
@@ -3892,6 +3908,19 @@ __global__ __launch_bounds__(kWide) TG_WIDE_ATTR void k_shape_seq_wide(ShapeArgs
       const uint32_t wl = wave_sum(n_lost), wc = wave_sum(n_copies), wo = wave_sum(n_over);
       if (lane_id() == 0) { s_wtot[tid >> 6][0] = wl; s_wtot[tid >> 6][1] = wc; s_wtot[tid >> 6][2] = wo; }
     }
+    {  // the next sender's send-time range (its loads have landed by now) and flags, for its sort
+      const bool nv = tid < nm.n && nm.n <= (uint32_t)kWide;
+      int64_t nmn = nv ? pf.ts : INT64_MAX, nmx = nv ? pf.ts : INT64_MIN;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(nmn, o), y = __shfl_xor(nmx, o);
+        nmn = x < nmn ? x : nmn;
+        nmx = y > nmx ? y : nmx;
+      }
+      if (lane_id() == 0) { rnmin[tid >> 6] = nmn; rnmax[tid >> 6] = nmx; }
+      if (tid == 0) { s_flag = 0; s_stage_a = 0; s_big = 0; }
+    }
+    mm_ready = true;
     __syncthreads();
     if (tid == 0) {
       uint32_t tl = 0, tc = 0, to = 0;
