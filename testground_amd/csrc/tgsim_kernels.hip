@@ -2745,13 +2745,14 @@ __global__ __launch_bounds__(kBlock) void k_keys_corr(const uint32_t* idx, uint3
     atomicAdd(kc_deferred, (unsigned long long)n);
     *seq_left = seq_left0;  // k_shape_seq_wide counts up from here (a memset would be a launch of its own)
   }
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-    uint32_t s = 0;
-    while (pre[s + 1] <= j) ++s;
-    const uint32_t i = idx[s * seg + (j - pre[s])];
-    keys[j] = src[i] - lo;
-    vals[j] = i;
+  // sharded: block b walks sub-list b % kDeferSub (gridDim a multiple of it), contiguous reads
+  const uint32_t S = sharded ? (uint32_t)kDeferSub : 1u, s = blockIdx.x % S, nb = gridDim.x / S;
+  const uint32_t cnt = pre[s + 1] - pre[s], out = pre[s];
+  const uint32_t* in = idx + (size_t)s * seg;
+  for (uint32_t j = blockIdx.x / S * blockDim.x + threadIdx.x; j < cnt; j += nb * blockDim.x) {
+    const uint32_t i = in[j];
+    keys[out + j] = src[i] - lo;
+    vals[out + j] = i;
   }
 }
 
@@ -5251,7 +5252,8 @@ static uint32_t wide_grid(const Dev& d) {
 // (t_send, seq); the heavy senders' due wheel records (H) grouped by sender; then k_shape_seq.
 static hipError_t run_shape_seq(Dev& d, const ShapeArgs& a, uint32_t n_staged) {
   uint32_t* n_dev = &d.sc->n_corr;
-  hipLaunchKernelGGL(k_keys_corr, dim3(grid_for(n_staged)), dim3(kBlock), 0, d.stream, d.corr_idx,
+  const uint32_t gk = (grid_for(n_staged) + kDeferSub - 1) / kDeferSub * kDeferSub;  // whole sub-list rows
+  hipLaunchKernelGGL(k_keys_corr, dim3(gk), dim3(kBlock), 0, d.stream, d.corr_idx,
                      a.heavy.pend ? 1u : 0u, d.qc, a.n_dev, n_staged, d.m_src, n_dev, d.lo, d.keys0, d.vals0, &d.sc->kc[KC_DEFERRED], &d.sc->seq_left, a.heavy.pend ? 0u : 1u);
   TG_CHECK(hipGetLastError());
   BktSrc src = bkt_queue(d, Q_A);
