@@ -212,32 +212,33 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
   block_partial(ndel, t.part);
 }
 
-// duplicated deliveries (bm_d), one thread per segment and epoch; an arrived segment is never
-// settled again. Few: these take direct list slots
+// duplicated deliveries (bm_d), one thread per delivery (a word's 64 deliveries walked by one thread
+// made chains of dependent atomics where retransmitted attempts pile up: acks mode 19 us), the
+// segment claimed once per epoch; an arrived segment is never settled again. The delivered count goes
+// into the block's k_tcp_arrive partial (same grid), not into one shared line per wave.
 __global__ __launch_bounds__(kBlock) void k_tcp_settle(const uint32_t* __restrict__ o_seq, const DevScalars* sc,
                                                        TcpDev t, uint32_t epoch, uint32_t cur) {
-  const uint32_t nw = (sc->n_out + 63u) >> 6;
+  const uint32_t n = sc->n_out;
   uint32_t ndel = 0;
-  for (uint32_t wi = blockIdx.x * kBlock + threadIdx.x; wi < nw; wi += gridDim.x * kBlock) {
-    for (uint64_t m = t.bm_d[wi]; m; m &= m - 1) {
-      const uint32_t sid = o_seq[wi * 64u + (uint32_t)__builtin_ctzll(m)] >> 4;
-      if (atomicMax(&t.s_mark[sid], epoch) >= epoch) continue;
-      const int64_t arr = t.s_arr[sid];
-      if (arr != INT64_MAX) {
-        t.s_mark[sid] = kArrived;
-        ndel += tcp_arrived(t, t.s_w[sid], arr);
-      } else if (!t.acks && t.s_out[sid] == 0 && tcp_next(t, sid, t.s_tlast[sid])) {
-        t.pend[cur][atomicAdd(&t.sc->pend_n[cur], 1u)] = sid;
-        atomicAdd(&t.sc->retx, 1ull);
-      }
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    if (!((t.bm_d[i >> 6] >> (i & 63u)) & 1ull)) continue;
+    const uint32_t sid = o_seq[i] >> 4;
+    if (atomicMax(&t.s_mark[sid], epoch) >= epoch) continue;
+    const int64_t arr = t.s_arr[sid];
+    if (arr != INT64_MAX) {
+      t.s_mark[sid] = kArrived;
+      ndel += tcp_arrived(t, t.s_w[sid], arr);
+    } else if (!t.acks && t.s_out[sid] == 0 && tcp_next(t, sid, t.s_tlast[sid])) {
+      t.pend[cur][atomicAdd(&t.sc->pend_n[cur], 1u)] = sid;
+      atomicAdd(&t.sc->retx, 1ull);
     }
   }
+  __shared__ uint32_t red[kBlock / 64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) ndel += (uint32_t)__shfl_xor(ndel, o);
-  if (lane_id() == 0 && ndel) {
-    atomicAdd(&t.sc->done, ndel);
-    atomicAdd(&t.sc->delivered, (unsigned long long)ndel);
-  }
+  if (lane_id() == 0) red[threadIdx.x >> 6] = ndel;
+  __syncthreads();
+  if (threadIdx.x == 0) t.part[blockIdx.x] += red[0] + red[1] + red[2] + red[3];  // after k_tcp_arrive's store
 }
 
 // The window's retransmissions (bits over the packets, then over the deliveries) into the pending
@@ -840,13 +841,16 @@ hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, uint32_t mode, uint32_t cu
   return hipGetLastError();
 }
 
+#ifndef TG_TCP_COLLECT_BLOCKS
+#define TG_TCP_COLLECT_BLOCKS 256  // a thread walks one bitmap word's retransmissions (64 blocks: 18.6 us)
+#endif
 hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch,
                             uint32_t fill) {
   hipLaunchKernelGGL(k_tcp_reset, dim3(1), dim3(kBlock), 0, d.stream, t, cur, d.sc, fill);
   hipLaunchKernelGGL(k_tcp_status, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.status, d.m_seq, n_host, n_dev, t);
   hipLaunchKernelGGL(k_tcp_arrive, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_seq, d.o_t, d.o_flags, d.sc, t);
-  hipLaunchKernelGGL(k_tcp_settle, dim3(64), dim3(kBlock), 0, d.stream, d.o_seq, d.sc, t, epoch, cur);
-  hipLaunchKernelGGL(k_tcp_collect, dim3(64), dim3(kBlock), 0, d.stream, d.m_seq, n_host, n_dev, d.o_seq, d.sc, t, cur,
+  hipLaunchKernelGGL(k_tcp_settle, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_seq, d.sc, t, epoch, cur);
+  hipLaunchKernelGGL(k_tcp_collect, dim3(TG_TCP_COLLECT_BLOCKS), dim3(kBlock), 0, d.stream, d.m_seq, n_host, n_dev, d.o_seq, d.sc, t, cur,
                      (uint32_t)kTcpArriveBlocks);
   return hipGetLastError();
 }
