@@ -101,7 +101,10 @@ typedef struct tgsim_config {
   uint32_t reserved0;
   uint64_t max_msgs_per_window;/* staged-message capacity per window */
   uint64_t max_records;        /* capacity of every per-window record batch and of the wheel arena */
-  uint64_t exchange_cap;       /* records per peer in one window's all-to-all (n_shards > 1) */
+  uint64_t exchange_cap;       /* records per peer block of one window's all-to-all (n_shards > 1): a
+                                  header + up to exchange_cap - 1 due copies to that peer (at least
+                                  513: 8 slices of (exchange_cap - 1) / 8, any producer may fill any
+                                  slice); more is TGSIM_ECAPACITY */
   uint32_t max_states;         /* sync states (dense ids 0..max_states-1); 0 = default 4096 */
   uint32_t max_waiters;        /* barrier waiters; 0 = default 65536 */
   uint64_t max_signals;        /* signal log capacity over the run; 0 = default 2^24 */

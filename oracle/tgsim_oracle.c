@@ -960,11 +960,14 @@ int tgo_advance_begin(tgo_ctx* c, int64_t t_end) {
     r.meta |= TGSIM_F_STAGE_D;
     if (route_record(c, &r)) return TGSIM_ENOMEM;
   }
-  /* 4. pack the exchange (peer-major blocks, header record .t = count) */
+  /* 4. pack the exchange (peer-major blocks, header record .t = count). The per-peer bound is the
+   * device block's usable records: below 513 records one slice of xcap - 1, else 8 slices of
+   * (xcap - 1) / 8 (include/tgsim.h exchange_cap), so both refuse the same windows. */
   memset(c->xsend, 0, (size_t)c->S * c->xcap * sizeof(tgsim_record));
+  const size_t xslices = c->xcap - 1 >= 8 * 64 ? 8 : 1, xusable = (c->xcap - 1) / xslices * xslices;
   for (uint32_t p = 0; p < c->S; ++p) {
     orecs* o = &c->outbox[p];
-    if (o->n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "exchange capacity exceeded (%zu records to peer %u)", o->n, p);
+    if (o->n > xusable) return fail(c, TGSIM_ECAPACITY, "exchange capacity exceeded (%zu records to peer %u)", o->n, p);
     c->xsend[(size_t)p * c->xcap].t = (int64_t)o->n;
     memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
   }

@@ -147,39 +147,48 @@ struct Queues {
   }
   // Wave-collective: every lane of the wave calls it; salt must be wave-uniform.
   __device__ __forceinline__ void push(int q, const tgsim_record& r, uint32_t salt) const {
+    const bool loc = q >= 0 && q < Q_X0;
     uint32_t* ctr = nullptr;
     tgsim_record* buf = nullptr;
-    uint32_t cap = 0, eb = 0;
-    if (q >= 0) {
-      if (q < Q_X0) {
-        // sub-queue: blocks b and b+8 share an XCD under round-robin dispatch, so counters
-        // 8x..8x+7 are only touched from one XCD's L2 (a speed choice; any mapping is correct)
-        const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
-        ctr = qc + (((uint32_t)q * kNSub + sub) << 5);
-        buf = (q == Q_A ? A : (q == Q_D ? D : L)) + (size_t)sub * subcap;
-        cap = subcap;
-        eb = q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L);
-      } else {
-        // the slice as a scalar (readfirstlane) and 32-bit offsets: anything else spilled
-        // k_extract_shape's registers at its 96-VGPR cap. The salt (the caller's round / item)
-        // turns a workgroup's successive pushes to successive slices, so one busy workgroup does
-        // not fill one slice alone
-        const uint32_t g = __builtin_amdgcn_readfirstlane((blockIdx.x + salt) & (xg - 1u));
-        ctr = xq + ((((uint32_t)(q - Q_X0)) * kXSlices + g) << 5);
-        buf = X + (((uint32_t)(q - Q_X0)) * xcap + (1u + g * xcs));
-        cap = xcs;
-        eb = ERR_CAP_X;
-      }
+    if (loc) {
+      // sub-queue: blocks b and b+8 share an XCD under round-robin dispatch, so counters
+      // 8x..8x+7 are only touched from one XCD's L2 (a speed choice; any mapping is correct)
+      const uint32_t sub = ((blockIdx.x & 7u) << 3) | ((salt + (blockIdx.x >> 3) * 4u + (threadIdx.x >> 6)) & 7u);
+      ctr = qc + (((uint32_t)q * kNSub + sub) << 5);
+      buf = (q == Q_A ? A : (q == Q_D ? D : L)) + (size_t)sub * subcap;
     }
     const uint32_t pos = wave_append(ctr);
-    if (q >= 0) {
-      if (pos < cap) {
+    if (loc) {
+      if (pos < subcap) {
         store_rec(buf + pos, r);
-        if (q < Q_X0) K[q][(size_t)(buf - (q == Q_A ? A : (q == Q_D ? D : L))) + pos] = key_of(q, r);
+        K[q][(size_t)(buf - (q == Q_A ? A : (q == Q_D ? D : L))) + pos] = key_of(q, r);
       } else {
-        atomicOr(&sc->err, eb);
+        atomicOr(&sc->err, q == Q_A ? ERR_CAP_A : (q == Q_D ? ERR_CAP_D : ERR_CAP_L));
       }
     }
+    if (__ballot(q >= Q_X0)) push_x(q, r, salt);
+  }
+
+  // Exchange append (wave-collective; lanes with q < Q_X0 take no part). The salt (the caller's
+  // round / item) turns a workgroup's successive pushes to successive slices, so one busy workgroup
+  // does not fill one slice alone; a lane whose slice is full goes on through the peer's other
+  // slices, so the per-peer bound is the whole block, xg * xcs records (a skewed
+  // producer overflowed its one slice far below it). The slice is a scalar (readfirstlane) and the
+  // offsets 32-bit: anything else spilled k_extract_shape's registers at its 96-VGPR cap. A full
+  // slice's cursor runs past xcs; k_xheaders clamps the counts.
+  __device__ __forceinline__ void push_x(int q, const tgsim_record& r, uint32_t salt) const {
+    bool pend = q >= Q_X0;
+    const uint32_t p = pend ? (uint32_t)(q - Q_X0) : 0u;
+    const uint32_t g0 = __builtin_amdgcn_readfirstlane((blockIdx.x + salt) & (xg - 1u));
+    for (uint32_t a = 0; a < xg && __ballot(pend); ++a) {
+      const uint32_t g = (g0 + a) & (xg - 1u);
+      const uint32_t pos = wave_append(pend ? xq + ((p * kXSlices + g) << 5) : nullptr);
+      if (pend && pos < xcs) {
+        store_rec(X + (p * xcap + (1u + g * xcs)) + pos, r);
+        pend = false;
+      }
+    }
+    if (pend) atomicOr(&sc->err, ERR_CAP_X);
   }
 
   // Wave-collective append of U records per lane (q[u] < 0: none). The local queues A / D / L take
@@ -2589,9 +2598,16 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
         uint32_t pr = 0;
         while (pr + 1 < p.geo.S && xoff[pr + 1] <= x) ++pr;
         const uint32_t xi = x - xoff[pr], fit = xcnt[pr];
-        const uint32_t pos = xi < fit ? xbase[pr] + xi : xb1[pr] + (xi - fit);
+        uint32_t pos = xi < fit ? xbase[pr] + xi : xb1[pr] + (xi - fit);
+        uint32_t g = xi < fit ? xg : xg1;
+        // both slices full (a skewed window): each remaining copy takes one slot in the peer's
+        // other slices by an atomic of its own (rare), so the per-peer bound is the whole block
+        for (uint32_t k = 2; pos >= Q.xcs && k < Q.xg; ++k) {
+          g = (xg + k) & (Q.xg - 1u);
+          pos = atomicAdd(Q.xctr(pr, g), 1u);
+        }
         if (pos < Q.xcs) {
-          uint4* dst = reinterpret_cast<uint4*>(Q.xslot(pr, xi < fit ? xg : xg1) + pos);
+          uint4* dst = reinterpret_cast<uint4*>(Q.xslot(pr, g) + pos);
           st4(dst, a.x, a.y, a.z, a.w);
           st4(dst + 1, b.x, b.y, b.z, b.w);
         } else {

@@ -644,6 +644,31 @@ def sharded_threads(world: int, fn, device: bool = False):
     return run_threads([lambda k=k: fn(k, g.member(k)) for k in range(world)])
 
 
+def run_skewed_exchange(binding, n_msgs: int, device: bool = False, exchange_cap: int = 513):
+    """one sender of shard 0 sends an unshaped (zero-delay) burst of n_msgs to shard 1's
+    receivers in one window, so one or two workgroups of the netem pass append every record to one
+    peer - far more than a slice's (exchange_cap - 1) / 8. Returns per shard ("ok", statuses or
+    deliveries) or ("err", code)."""
+    from testground_amd.exchange import ThreadGroup, run_threads
+    g = ThreadGroup(2, device=device, timeout=120.0)
+
+    def shard(k):
+        sim = Simulator(SimConfig(n_instances=16, seed=7, shard_id=k, n_shards=2, exchange_cap=exchange_cap),
+                        binding=binding)
+        sim.set_transport(g.member(k))
+        try:
+            if k == 0:
+                i = np.arange(n_msgs, dtype=np.int64)
+                sim.enqueue(np.zeros(n_msgs, np.int64), 8 + i % 8, i, np.full(n_msgs, 100), np.zeros(n_msgs, np.int64))
+            sim.advance(1 * MS)
+            return ("ok", sim.status() if k == 0 else sim.deliveries())
+        except A.TgsimError as e:
+            return ("err", e.code)
+        finally:
+            sim.close()
+    return run_threads([lambda k=k: shard(k) for k in range(2)])
+
+
 def shard_cfg(world: int, k: int, **kw):
     return dict(shard_id=k, n_shards=world, **kw)
 

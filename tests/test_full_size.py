@@ -306,15 +306,29 @@ def test_cfg4_storm_full(hip, oracle, n=100_000, rounds=8):
     assert sum(len(x["deliv"]["dst"]) for x in a[:-1]) > n * 8
 
 
+def _bench_storm_cfg(n: int, k: int, world: int) -> dict:
+    """bench.sim_config's context for shard k of `world` (the test proves the
+    bench's own peer blocks, 1.25 x N x 8 / S^2 + 4096 records, not a roomier capacity)."""
+    import argparse
+    import dataclasses
+    import bench
+    a = argparse.Namespace(instances=n, fanout=8, seed=4, max_records=1 << 23, tcp=False, tcp_acks=False)
+    c = dataclasses.asdict(bench.sim_config(a, k, world))
+    for f in ("n_instances", "seed", "device"):
+        c.pop(f)
+    return c
+
+
 def test_cfg4_storm_sharded_full(hip, n=100_000, rounds=10, world=8):
     """config 4 as bench.py shards it: the 100k storm over 8 HIP contexts (one thread each, one GPU,
-    the exchange and the barrier's all-reduce through the transport) equals the single-context run
-    bit for bit (which test_cfg4_storm_full pins to the oracle)."""
+    the exchange and the barrier's all-reduce through the transport), each built by bench.sim_config
+    (its exchange blocks of 19.7k records at 8 shards), equals the single-context run bit for bit
+    (which test_cfg4_storm_full pins to the oracle), with no ECAPACITY over the rounds."""
     kw = dict(max_records=1 << 23, data_prefix_len=12)
     single = S.run_storm(hip, n_inst=n, rounds=rounds, cfg_kw=kw)
-    skw = dict(max_records=1 << 21, data_prefix_len=12, exchange_cap=1 << 15)
+    assert _bench_storm_cfg(n, 0, world)["exchange_cap"] == int(1.25 * n * 8 / world ** 2) + 4096
     outs = S.sharded_threads(world, lambda k, tr: S.run_storm(
-        hip, n_inst=n, rounds=rounds, cfg_kw=S.shard_cfg(world, k, **skw),
+        hip, n_inst=n, rounds=rounds, cfg_kw=_bench_storm_cfg(n, k, world),
         setup=lambda sim: sim.set_transport(tr)), device=True)
     S.assert_storm_sharded(outs, single, world, n)
     assert sum(len(x["deliv"]["dst"]) for x in single[:-1]) > n * 8

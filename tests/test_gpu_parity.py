@@ -154,6 +154,19 @@ def test_transport_tight_exchange_on_one_device(hip, oracle, world, seed):
     S.assert_sharded_matches(outs, srcs, S.run_random(oracle, seed), world)
 
 
+@pytest.mark.parametrize("n_msgs,ok", [(448, True), (512, True), (513, False)])
+def test_skewed_exchange_on_one_device(hip, oracle, n_msgs, ok):
+    """one or two netem workgroups send every record of a window to one peer, 7-8x a
+    slice's 64 records (exchange_cap 513). Each overflowing wave goes on through the peer's other
+    slices, so the device takes the whole block's 512 like the oracle (bit-exact) and refuses 513."""
+    a, b = S.run_skewed_exchange(hip, n_msgs, device=True), S.run_skewed_exchange(oracle, n_msgs)
+    if ok:
+        assert [x[0] for x in a] == ["ok", "ok"], a
+        S.assert_same(a, b)
+    else:
+        assert a[0] == ("err", A.ECAPACITY) and b[0] == ("err", A.ECAPACITY)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_storm_transport_on_one_device(hip, oracle, world):
     """bench.py's storm step on HIP shards: the storm batch's MAX all-reduce and the exchange go

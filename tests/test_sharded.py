@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 
 from tests import scenarios as S
+from testground_amd import _abi as A
 from testground_amd.sim import SimConfig, Simulator
 
 
@@ -233,3 +234,16 @@ def test_bench_spawns_its_own_ranks(tmp_path, capfd):
         assert bench.spawn_ranks(3, argv=[], script=str(script)) == 7
     finally:
         del os.environ["FAIL_RANK"], os.environ["FAIL_RANK_CODE"]
+
+
+@pytest.mark.parametrize("n_msgs,ok", [(448, True), (512, True), (513, False)])
+def test_skewed_exchange_bound_oracle(oracle, n_msgs, ok):
+    """The per-peer exchange bound is the block's usable records (exchange_cap 513: 8 slices of 64 =
+    512), whichever producers fill it: 512 records to one peer pass, 513 are ECAPACITY."""
+    res = S.run_skewed_exchange(oracle, n_msgs)
+    if ok:
+        assert res[0][0] == "ok" and res[1][0] == "ok"
+        assert len(res[1][1]["dst"]) == n_msgs
+    else:
+        assert res[0] == ("err", A.ECAPACITY)
+
