@@ -259,10 +259,13 @@ __device__ inline void fence_acquire_agent() {
 }
 // A workgroup publishes its stores through a counter one lane updates (MI355X_MICROARCH.md
 // § visibility, valid producer form): every storing wave waits for its stores, the barrier, then ONE
-// agent-scope release by the counting lane and a second wait (ROCm 7.2 can drop the fence's own),
-// then that lane's atomic. One L2 write-back per workgroup instead of one per wave, and correct by
-// the model: the release covers the other waves' stores because they completed before the barrier
-// (VERDICT r4 item 9). Call from every thread; returns true on the counting lane (thread 0).
+// agent-scope release by the counting lane, then that lane's atomic. One L2 write-back per workgroup
+// instead of one per wave, and correct by the model: the release covers the other waves' stores
+// because they completed before the barrier. The release lowers to
+// `buffer_wbl2 sc1; s_waitcnt vmcnt(0)` on gfx950 (ROCm 7.2): round 5 added a second wait after it
+// on the suspicion that the compiler could drop its own; tools/fence_isa.sh checks every write-back
+// of the product kernels is followed by its wait (profiles/r06/fence_isa.txt), so that wait is gone.
+// Call from every thread; returns true on the counting lane (thread 0).
 __device__ inline bool block_release_for_count() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -272,7 +275,6 @@ __device__ inline bool block_release_for_count() {
 #else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return true;
 }
 // The consumer side: the polling lane (thread 0) has seen the count; ONE agent-scope acquire drops

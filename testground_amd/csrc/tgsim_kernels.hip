@@ -4775,12 +4775,13 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     }
     TASK_PH(tp_ready);
     if (LargeScan<P>::v) {  // compile-time: the segment's last rank task runs the scan
-      __threadfence();
-      __syncthreads();
-      if (threadIdx.x == 0) s_last = (atomicAdd(&lg[i].pad, 1u << 16) >> 16) == nrk - 1;
+      // the placed keys are published by one release on the counting lane, and the last task
+      // takes one acquire before it reads every task's placements (this was a
+      // full fence in every thread on both sides)
+      if (block_release_for_count()) s_last = (atomicAdd(&lg[i].pad, 1u << 16) >> 16) == nrk - 1;
       __syncthreads();
       if (__builtin_amdgcn_readfirstlane(s_last)) {
-        __threadfence();
+        block_acquire_after_poll();
         large_consume(p, s, L, K1b, K3b, i * 131u);
       }
       __syncthreads();

@@ -668,8 +668,13 @@ __global__ __launch_bounds__(kBlock) void k_tcp_conn_release(TcpDev t, DevScalar
             for (uint32_t x = t.s_next[u]; x != h0 && dup < 3u; x = t.s_next[x]) dup += t.s_done[x] == 1;
             // the count leaves the loop as a value: this compiler (ROCm 7.2) otherwise reused the exit
             // test's lane mask of the last iteration for `dup >= 3`, losing it for every lane that left
-            // earlier (a wave of connections where one walks further than another: no fast retransmit)
+            // earlier (a wave of connections where one walks further than another: no fast retransmit).
+            // Reproduced standalone by tools/loopexit_repro.hip (25.6k of 65.5k lanes wrong without the
+            // asm, none with it; profiles/r06/loopexit_repro.txt) and found statically by
+            // tools/loopexit_audit.py, which finds no other such loop exit in the product kernels
+#ifndef TGSIM_NO_WALK_ASM  // experiment build: the walk without the asm (tools/loopexit_repro.hip)
             __asm__ volatile("" : "+v"(dup));
+#endif
             if (dup >= 3u && ws != TGSIM_TCP_TIMEOUT && ws != TGSIM_TCP_REFUSED) {
               fr = u;
               t.c_fr[k] = u;

@@ -4,6 +4,7 @@ fixtures, on identical seeded inputs. Bit-exact on every observable: statuses, d
 import numpy as np
 import pytest
 
+from testground_amd import _abi as A
 from tests import golden_check as GC
 from tests import scenarios as S
 from tests import semantics_cases as SC
