@@ -1541,8 +1541,11 @@ static int probe_react_impl(tgo_ctx* c, int64_t* next_end, uint32_t* n_active) {
       const uint32_t g = r->src, j = r->seq & PR_MASK;
       if (g >= c->N || j >= c->pr_n || c->pr_order[j] != r->dst || j + 1 <= c->pr_ans[g]) continue;
       if (!c->pr_cur[g]) c->pr_list[c->pr_list_n++] = g;
-      if (j + 1 > c->pr_cur[g]) c->pr_cur[g] = j + 1;
-      if (r->t < c->pr_rqa[g]) c->pr_rqa[g] = r->t;
+      /* the reply answers the highest position, at the first arrival of THAT position's request: a
+       * request delayed past its timeout and arriving in its successor's window does not stamp the
+       * successor's reply before the successor arrived */
+      if (j + 1 > c->pr_cur[g]) { c->pr_cur[g] = j + 1; c->pr_rqa[g] = r->t; }
+      else if (j + 1 == c->pr_cur[g] && r->t < c->pr_rqa[g]) c->pr_rqa[g] = r->t;
     } else if (tag == 3u && (r->seq & PR_MASK) == r->dst) {
       oprobe* p = &c->pr[r->dst - c->lo];
       if (p->state == PR_WAIT && p->replied && c->pr_order[p->pos] == r->src && r->t < p->t_reparr) p->t_reparr = r->t;

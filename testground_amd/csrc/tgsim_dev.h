@@ -149,9 +149,11 @@ struct ProbeDev {
   int64_t timeout = 0, window = 0;
   // the answering side, per prober g [N] (the requests that peers on this shard received): the last
   // position answered + 1, the position answered in this reaction + 1 (the highest new one), its
-  // requests' first arrival; the probers to answer (sharded: k_probe_answer)
+  // first arrival of that position's request (only the highest position's), packed as
+  // (position + 1) << 40 | (t_end - 1 - arrival) so one 64-bit atomicMax keeps both
+  // (0 = none); the probers to answer (sharded: k_probe_answer)
   uint32_t *ans = nullptr, *cur = nullptr, *alist = nullptr;
-  int64_t* rqa = nullptr;
+  uint64_t* rqa = nullptr;
   // sharding (as StormDev): notices to a prober's shard go into the exchange blocks
   uint32_t lo = 0, nloc = 0, N = 0, S = 1, shard = 0, xcap = 0;
   uint32_t* xq = nullptr;

@@ -55,7 +55,8 @@ enum : uint32_t {
   ERR_BAD_MSG = 1u << 12, ERR_STATE_CHUNKS = 1u << 13, ERR_UNSORTED_TARGET = 1u << 14,
   ERR_QUEUE_CAP = 1u << 15,  // a sender's queue bookkeeping outgrew kSeqCap (cannot happen with limit 1000)
   ERR_CAP_M = 1u << 16,      // device-counted staging (flood forwards, appends after them) outgrew cap_msgs
-  ERR_TCP_TIMERS = 1u << 17  // TCP acks mode: more live timer batches than the ring holds
+  ERR_TCP_TIMERS = 1u << 17, // TCP acks mode: more live timer batches than the ring holds
+  ERR_PROBE_SPAN = 1u << 18  // probe reaction: a request arrival more than 2^40 ns before the window end
   // ERR_TASKS: a large-segment rank task waited past its bound for its chunks (k_rest; never expected)
 };
 

@@ -26,6 +26,7 @@ namespace tgsim {
 namespace {
 
 constexpr uint32_t kTagMask = 0x3FFFFFFFu;
+constexpr uint64_t kArrSpan = 1ull << 40;  // request arrivals packed relative to the window end (answer)
 constexpr int64_t kNone = INT64_MAX;
 enum : uint8_t { kIdle = 0, kWait = 1, kDone = 2 };
 
@@ -154,7 +155,13 @@ __device__ __forceinline__ void probe_arrive(const uint32_t* __restrict__ o_src,
         g = o_src[i];
         if (g < p.N && j < p.n_order && p.order[j] == o_dst[i] && j + 1u > p.ans[g]) {
           const uint32_t old = atomicMax(&p.cur[g], j + 1u);
-          atomicMin(reinterpret_cast<long long*>(&p.rqa[g]), (long long)o_t[i]);
+          // the highest position, and the first arrival of that position's request only: a request
+          // j delayed past its timeout that lands in the window of request j + 1 does not stamp
+          // j + 1's reply before j + 1 arrived
+          const uint64_t off = (uint64_t)(sc->t_end - 1 - o_t[i]);  // >= 0: delivered in this window
+          if (off >= kArrSpan) atomicOr(const_cast<uint32_t*>(&sc->err), ERR_PROBE_SPAN);
+          atomicMax(reinterpret_cast<unsigned long long*>(&p.rqa[g]),
+                    (unsigned long long)(((uint64_t)(j + 1u) << 40) | min(off, kArrSpan - 1u)));  // max off = first
           listed = old == 0u && p.S > 1;
         }
       } else if (tag == 3u && (sq & kTagMask) == o_dst[i]) {  // a reply at its prober
@@ -209,14 +216,15 @@ __device__ __forceinline__ void reply_staged(ProbeDev& p, uint32_t g, uint32_t p
 // The peer answers prober g's highest new request: the reply at max(first arrival, horizon), staged
 // in st; returns the answered position. The prober's shard learns of it (reply_staged) here on one
 // shard, by a notice when sharded.
-__device__ __forceinline__ uint32_t answer(ProbeDev& p, uint32_t g, int64_t H, Staged& st) {
-  const uint32_t j = p.cur[g] - 1u;
-  const int64_t ra = p.rqa[g];
+__device__ __forceinline__ uint32_t answer(ProbeDev& p, uint32_t g, int64_t H, int64_t t_end, Staged& st) {
+  const uint64_t key = p.rqa[g];  // (position + 1, first arrival) of the highest position (probe_arrive)
+  const uint32_t j = (uint32_t)(key >> 40) - 1u;
+  const int64_t ra = t_end - 1 - (int64_t)(key & (kArrSpan - 1u));
   const int64_t trep = ra > H ? ra : H;
   st.add(p.order[j], g, TGSIM_PROBE_REP | g, p.rep_bytes, trep);
   p.ans[g] = j + 1u;
   p.cur[g] = 0;
-  p.rqa[g] = kNone;
+  p.rqa[g] = 0;
   if (p.S == 1) reply_staged(p, g, j, trep);
   return j;
 }
@@ -231,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_answer(ProbeDev p, DevScalars*
   __shared__ uint32_t red[kBlock / 64];
   __shared__ uint32_t sbase;
   const uint32_t n = p.sc->n_ans;
-  const int64_t H = sc->T;
+  const int64_t H = sc->T, t_end = sc->t_end;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform
     const uint32_t i = b0 + threadIdx.x;
     Staged st;
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_answer(ProbeDev p, DevScalars*
     int64_t trep = 0;
     if (i < n) {
       g = p.alist[i];
-      j = answer(p, g, H, st);
+      j = answer(p, g, H, t_end, st);
       trep = st.t[0];
       const uint32_t k = shard_of(g, p.N, p.S);
       if (k == p.shard) reply_staged(p, g, j, trep);
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_step(ProbeDev p, DevScalars* s
     Staged st;
     int64_t dl_wait = kNone;
     uint32_t waiting = 0;
-    if (l < nloc && p.S == 1 && p.cur[l]) answer(p, lo + l, H, st);  // one shard: for the peer
+    if (l < nloc && p.S == 1 && p.cur[l]) answer(p, lo + l, H, t_end, st);  // one shard: for the peer
     if (l < nloc && p.state[l] == kWait) {
       const uint32_t g = lo + l, pos = p.pos[l];
       const int64_t tr = p.t_req[l], dl = tr + p.timeout, ra = p.t_reparr[l];

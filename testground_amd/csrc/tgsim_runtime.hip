@@ -644,6 +644,8 @@ static int check_device_errors(tgsim_ctx* c) {
   if (e & ERR_UNSORTED_TARGET)
     return fail(c, TGSIM_ENOTSUP, "barrier target falls inside a count-only signal batch (only its first/last member is known)");
   if (e & ERR_UNRELEASED) return fail(c, TGSIM_ESTATE, "advance_to_barrier: barrier not released");
+  if (e & ERR_PROBE_SPAN)
+    return fail(c, TGSIM_ENOTSUP, "probe reaction: a request arrived more than 2^40 ns before its window's end");
   return fail(c, TGSIM_EINVAL, "device error bits 0x%x", e);
 }
 
@@ -1186,6 +1188,15 @@ static int tgsim_enqueue_device_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_
 // and with connections up to two segments more per ACK (slow start: a flight slot and a cwnd step)
 static uint32_t tcp_inbox_mult(const tgsim_ctx* c) { return c->td.n_conn ? 3u : 1u; }
 
+// The lifetime bound (life_host, fl_npubs) counts host and device enqueues (win_m_host / win_m_extra,
+// every window) and flood forwards (at most D per publication). Every other device reactor stages
+// traffic it does not count; this is the one list of them, checked every window, that turns the
+// bound off for good (a new reactor must be added here, or the queue-limit test would be
+// skipped for its traffic - test_flood_queue_limit_reopens_* pins the flood side)
+static bool uncounted_staging(const tgsim_ctx* c) {
+  return c->tcp_on || c->probes || c->storm_on || c->win_inbox_max != 0;
+}
+
 // The window's queue-limit test. The kernels test every sender only when the host
 // cannot prove that none can reach the limit: pend_bound (queued copies of any sender at this
 // window's start) + mult * (the most messages one sender can have staged) <= TGSIM_NETEM_LIMIT.
@@ -1202,7 +1213,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
   // staging bound already reaches the limit, when no refresh can close the gate
   c->life_host = std::min<uint64_t>(c->life_host + m_uniform, 1ull << 40);
   c->life_mult = std::max<uint64_t>(c->life_mult, mult);
-  if (c->tcp_on || c->win_inbox_max) c->life_ok = false;  // probes / storm reactor / TCP traffic
+  if (uncounted_staging(c)) c->life_ok = false;
   if (gate && c->life_ok && !zd_only &&
       c->life_mult * ((uint64_t)c->d.fl.D * c->fl_npubs + c->life_host) <= TGSIM_NETEM_LIMIT)
     gate = false;  // no sender can ever have queued and staged more than the limit
@@ -2091,7 +2102,8 @@ extern "C" int tgsim_probe_setup(tgsim_ctx* c, const uint32_t* order, uint32_t n
   return abi_guard(c, [&] { return tgsim_probe_setup_body(c, order, n_order, cfg); });
 }
 static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t n_order, const tgsim_probe_config* cfg) {
-  if (!c || !order || !cfg || n_order == 0 || n_order > 0x3FFFFFFFu) return fail(c, TGSIM_EINVAL, "bad arguments");
+  // positions < 2^24: the reaction packs (position, arrival) into one 64-bit key (tgsim_probe.hip)
+  if (!c || !order || !cfg || n_order == 0 || n_order >= (1u << 24)) return fail(c, TGSIM_EINVAL, "bad arguments");
   if (cfg->timeout_ns <= 0 || cfg->window_ns <= 0 || cfg->request_bytes >= 0x80000000u || cfg->reply_bytes >= 0x80000000u)
     return fail(c, TGSIM_EINVAL, "bad probe configuration");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
@@ -2120,11 +2132,7 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   hipStream_t st = c->d.stream;
   HIPCK(c, hipMemsetAsync(p.ans, 0, nn * 4, st), "probe setup");
   HIPCK(c, hipMemsetAsync(p.cur, 0, nn * 4, st), "probe setup");
-  {
-    std::vector<int64_t> tmax(nn, INT64_MAX);
-    HIPCK(c, hipMemcpyAsync(p.rqa, tmax.data(), nn * 8, hipMemcpyHostToDevice, st), "probe setup");
-    HIPCK(c, hipStreamSynchronize(st), "probe setup");
-  }
+  HIPCK(c, hipMemsetAsync(p.rqa, 0, nn * 8, st), "probe setup");  // no request arrived
   HIPCK(c, hipMemcpyAsync(p.order, order, (size_t)n_order * 4, hipMemcpyHostToDevice, st), "probe setup");
   HIPCK(c, hipMemsetAsync(p.state, 0, nl, st), "probe setup");
   HIPCK(c, hipMemsetAsync(p.out, 0, nl * n_order, st), "probe setup");
@@ -3385,7 +3393,10 @@ static int tgsim_tcp_conns_body(tgsim_ctx* c, uint32_t first, size_t n, uint64_t
 // mirrors are re-uploaded at the next window. Randomness needs no state (Philox is counter-based).
 namespace {
 
-constexpr uint64_t kSnapMagic = 0x3130504E53475454ull;  // "TTGSNP01"
+// "TTGSNP" + a two-digit layout version: bump it whenever snap_regions changes (round 5
+// changed the pend layout under version 01, so an older image was refused only by its byte total)
+constexpr uint64_t kSnapMagic = 0x3230504E53475454ull;  // "TTGSNP02": pend at one line per sender (nloc <= 16384)
+constexpr uint64_t kSnapMagicMask = 0x0000FFFFFFFFFFFFull;  // "TTGSNP" without the version
 
 struct SnapHeader {
   uint64_t magic, bytes;
@@ -3534,6 +3545,9 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   if (c->storm_pending) return fail(c, TGSIM_ESTATE, "restore: a storm round is pending");
   SnapReader r{static_cast<const uint8_t*>(buf), n};
   const SnapHeader h = r.val<SnapHeader>(), want = snap_header(c);
+  if (r.ok && h.magic != kSnapMagic && (h.magic & kSnapMagicMask) == (kSnapMagic & kSnapMagicMask))
+    return fail(c, TGSIM_EINVAL, "restore: snapshot layout version %.2s, this library reads %.2s",
+                reinterpret_cast<const char*>(&h.magic) + 6, reinterpret_cast<const char*>(&kSnapMagic) + 6);
   if (!r.ok || h.magic != kSnapMagic || h.bytes != n) return fail(c, TGSIM_EINVAL, "restore: not a snapshot image");
   SnapHeader hc = h;
   hc.bytes = 0;

@@ -252,3 +252,30 @@ def test_flood_sharded_full_size(hip):
             cfg_kw=dict(skw, **S.shard_cfg(world, k)), setup=lambda sim: sim.set_transport(tr)), device=True)
         S.assert_same(S.combine_flood_shards(outs), want)
         print(f"  flood 1M x {world} shards == single", flush=True)
+
+
+def _hub_shapes(n):
+    """Two slow hubs (2 s latency; one also at 1 Mbit/s) among 1-ms links: every publication reaches
+    a hub within a few windows and the hub forwards it to 7 neighbours, whose copies stay queued for
+    2 s - past netem's 1000-packet limit within the run."""
+    sh = [make_shape(latency_ns=1 * MS)] * n
+    sh[0] = make_shape(latency_ns=2000 * MS)
+    sh[5] = make_shape(latency_ns=2000 * MS, bandwidth_bps=1_000_000)
+    return sh
+
+
+def test_flood_queue_limit_reopens_oracle(oracle):
+    """a flood-only context skips the exact queue-limit refresh while its lifetime bound
+    (host-staged messages + D per publication) stays under the limit. Here the bound is exceeded and
+    two senders' queues do reach 1000: the gate re-opens and tail drops happen - only on the hubs."""
+    out = S.run_flood(oracle, n_inst=64, pubs_per_wave=60, waves=10, wave_gap_windows=1, shapes=_hub_shapes(64),
+                      windows=30)
+    assert out[-1]["stats"]["overlimit"] > 1000
+
+
+@pytest.mark.gpu
+def test_flood_queue_limit_reopens_hip(hip, oracle):
+    kw = dict(n_inst=64, pubs_per_wave=60, waves=10, wave_gap_windows=1, shapes=_hub_shapes(64), windows=30)
+    a, b = S.run_flood(hip, **kw), S.run_flood(oracle, **kw)
+    S.assert_same(a, b)
+    assert a[-1]["stats"]["overlimit"] > 1000

@@ -221,3 +221,40 @@ def test_probe_react_owed_oracle(oracle):
 @pytest.mark.gpu
 def test_probe_react_owed_hip(hip):
     _react_owed_case(hip)
+
+
+def _late_request_case(b):
+    """prober 0's first request (to 1) is slower than the timeout (150 ms latency, 100 ms
+    timeout): the probe times out at 100 ms and the second request (to 2) leaves at 100 ms over a
+    60 ms link (the shape changed meanwhile). Both requests arrive in the window [150, 200) ms, the
+    first at 150, the second at 160. The reply answers the second request: it must leave at its own
+    request's arrival (160), not at the earlier arrival of the first (150), so the probe ends OK at
+    160 ms (the reply's zero-latency arrival), not 150."""
+    s = Simulator(SimConfig(n_instances=3, seed=1), binding=b)
+    s.set_shape(0, make_shape(latency_ns=150 * MS))
+    s.probe_setup(np.arange(3), 66, 66, 100 * MS, 50 * MS)
+    s.probe_start(0)
+    ne, out, changed = 50 * MS, [], False
+    for _ in range(100):
+        s.advance(ne)
+        out.append(dict(status=np.sort(s.status()), deliv=s.deliveries()))
+        ne, act = s.probe_react()
+        if not changed and s.now >= 150 * MS:
+            s.set_shape(0, make_shape(latency_ns=60 * MS))
+            changed = True
+        if act == 0:
+            break
+    res, t_done = s.probe_results()
+    s.close()
+    assert res[0].tolist() == [0, A.PROBE_TIMEOUT, A.PROBE_OK]
+    assert t_done[0] == 160 * MS
+    return out, res, t_done
+
+
+def test_probe_late_request_reply_time_oracle(oracle):
+    _late_request_case(oracle)
+
+
+@pytest.mark.gpu
+def test_probe_late_request_reply_time_hip(hip, oracle):
+    S.assert_same(_late_request_case(hip), _late_request_case(oracle))

@@ -79,6 +79,11 @@ def test_snapshot_refusals(hip):
     with pytest.raises(A.TgsimError) as e:     # truncated image: refused, the context unchanged
         same.restore(image[:-8])
     assert e.value.code == A.EINVAL
+    old = bytearray(image)                     # an image of an older layout (version 01): named as such
+    old[6:8] = b"01"
+    with pytest.raises(A.TgsimError) as e:
+        same.restore(bytes(old))
+    assert e.value.code == A.EINVAL and "version 01" in str(e.value)
     same.enqueue([2], [3], [0], [10], [0])
     same.advance(1 * MS)
     assert same.deliveries()["dst"].tolist() == [3]
