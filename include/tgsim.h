@@ -240,7 +240,11 @@ int tgsim_get_ip(const tgsim_ctx* ctx, uint32_t instance, uint32_t* ip);
 /* ---- data path (replaces the host kernel's HTB/netem/FIB per packet) ----------------------------- */
 /* Stage messages for the next window (host SoA, copied). t_send must be >= tgsim_horizon(). */
 int tgsim_enqueue(tgsim_ctx* ctx, const tgsim_msg_soa* msgs, size_t n);
-/* Stage messages already in device memory (SoA arrays of n elements). */
+/* Stage messages already in device memory (SoA arrays of n elements, on this device, complete on the
+ * context's stream). When they are the first messages staged for the window (and no probe or storm
+ * reactor is set up) they are not copied: the window reads them in place, so the arrays must stay
+ * unchanged until that window's work on the context's stream has run (stream order, or the next
+ * synchronising call); otherwise they are copied during the call. */
 int tgsim_enqueue_device(tgsim_ctx* ctx, const tgsim_msg_soa* dev_msgs, size_t n);
 /* Run one window [now, t_end): shape + route staged messages, token-bucket the copies whose netem
  * time is < t_end, deliver everything due before t_end. A sharded ctx needs a transport

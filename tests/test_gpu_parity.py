@@ -267,3 +267,53 @@ def test_shared_torch_stream_ordering(hip, oracle):
     assert np.array_equal(hs.deliveries()["seq"], want["seq"])
     for sm in sims:
         sm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix", ["device", "device+device", "device+host", "host+device"])
+def test_enqueue_device_in_place(hip, oracle, mix):
+    """a tgsim_enqueue_device batch that is the window's only staging is read in
+    place (no copy); one followed by more staging is copied in front of it at the window start; one
+    after a host batch is copied during the call. Every mix equals the oracle fed the same messages,
+    window by window, with the queue limit on (the sequential lane reads the batch too)."""
+    import torch
+    from testground_amd.sim import SimConfig, Simulator, make_shape
+    dev = torch.device("cuda:0")
+    n_inst, n = 4, 2500     # ~600 per sender per window, queued for 1-4 ms: the queue limit decides
+    sims = [Simulator(SimConfig(n_instances=n_inst, seed=5, max_msgs_per_window=1 << 14, max_records=1 << 16),
+                      binding=b) for b in (hip, oracle)]
+    for sm in sims:
+        for g in range(n_inst):
+            sm.set_shape(g, make_shape(latency_ns=(1 + g % 4) * 1_000_000, jitter_ns=300_000, loss=2.0))
+    rng = np.random.default_rng(11)
+    outs = [[], []]
+    seqc = np.zeros(n_inst, np.int64)
+    for w in range(4):
+        parts = []
+        for kind in mix.split("+"):
+            src = rng.integers(0, n_inst, n)
+            dst = rng.integers(0, n_inst, n)
+            seq = np.zeros(n, np.int64)
+            for i in range(n):
+                seq[i] = seqc[src[i]]
+                seqc[src[i]] += 1
+            t = w * 2_000_000 + np.sort(rng.integers(0, 2_000_000, n))
+            parts.append((kind, src, dst, seq, np.full(n, 1500), t))
+        keep = []
+        for kind, src, dst, seq, size, t in parts:
+            if kind == "device":
+                cols = [torch.from_numpy(x.astype(np.int32)).to(dev) for x in (src, dst, seq, size)]
+                cols.append(torch.from_numpy(t.astype(np.int64)).to(dev))
+                torch.cuda.synchronize()
+                keep.append(cols)   # read in place by the window: alive until it has run
+                sims[0].enqueue_device(*(c.data_ptr() for c in cols), n)
+            else:
+                sims[0].enqueue(src, dst, seq, size, t)
+            sims[1].enqueue(src, dst, seq, size, t)
+        for k, sm in enumerate(sims):
+            sm.advance((w + 1) * 2_000_000)
+            outs[k].append(dict(status=sm.status(), deliv=sm.deliveries(), stats=S.parity_stats(sm)))
+        del keep
+    S.assert_same(outs[0], outs[1])
+    for sm in sims:
+        sm.close()

@@ -46,8 +46,10 @@ evidence)
     timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "k_" -d $OUT/pmc_${W}_$c -o run --output-format csv \
       -- python3 -u $B --steps 5 > $OUT/pmc_${W}_$c.log 2>&1 || { echo PMC_FAIL $c; tail -5 $OUT/pmc_${W}_$c.log; exit 1; }
   done
+  # the flood publishes every 4 windows: its per-window sums average two whole cycles
+  LAST=5; [ "$W" = flood ] && LAST=8
   python3 tools/pmc_traffic.py $OUT/pmc_${W}_FETCH_SIZE/run_counter_collection.csv $OUT/pmc_${W}_WRITE_SIZE/run_counter_collection.csv \
-    $P/pmc_traffic$(suffix $W).json $W 1 || exit 1
+    $P/pmc_traffic$(suffix $W).json $W 1 --last $LAST || exit 1
   timeout -k 10 400 python3 -u bench.py --workload $W $(warm $W) "$@" > $OUT/bench_$W.log 2>&1 || { echo BENCH_FAIL; tail -30 $OUT/bench_$W.log; exit 1; }
   tail -1 $OUT/bench_$W.log > $P/bench_$W.json
   cut -c1-600 $P/bench_$W.json;;
