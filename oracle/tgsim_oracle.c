@@ -198,6 +198,7 @@ struct tgo_ctx {
   uint32_t* inbox;    /* [nloc+1] */
   tgsim_record* xsend; tgsim_record* xrecv; size_t xcap;
   orecs* outbox;      /* [S] */
+  orecs tcp_rx;       /* sharded TCP: data copies other shards delivered for this shard's writers */
   tgsim_stats stats;
   otimes* sig;        /* per state: signal times in seq order */
   size_t n_states;
@@ -216,6 +217,7 @@ struct tgo_ctx {
   int has_tr, replicated_batch, tr_aborted;
   /* TCP mode: writes, segments, segments with a retransmission scheduled */
   int tcp_on, tcp_need_react;
+  uint32_t tcp_F;     /* sharded TCP: the generated storm rounds' fanout (tcp_wire / tcp_local) */
   tgsim_tcp_config tcp;
   struct otcpw* tw; size_t tw_n, tw_cap;
   struct otcps* tsg; size_t tsg_n, tsg_cap;
@@ -386,6 +388,7 @@ void tgo_destroy(tgo_ctx* c) {
   free(c->id_of); free(c->inbox); free(c->outbox); free(c->xsend); free(c->xrecv);
   free(c->staged.src); free(c->staged.dst); free(c->staged.seq); free(c->staged.size); free(c->staged.t);
   free(c->status); free(c->heap.v); free(c->A.v); free(c->D.v); free(c->pend); free(c->out.v);
+  free(c->tcp_rx.v);
   free(c);
 }
 
@@ -1239,9 +1242,17 @@ int tgo_tcp_gen_storm_round(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fan
                             int64_t spread_ns, uint32_t state) {
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (size > c->tcp.mss) return fail(c, TGSIM_EINVAL, "a storm write must fit one segment");
+  if (c->S != 1) {  /* the wire ids: every round of one fanout, and within the packets' 27/28 bits */
+    if (c->tcp_F && c->tcp_F != fanout) return fail(c, TGSIM_ENOTSUP, "sharded TCP storms keep one fanout");
+    const uint64_t rounds = (uint64_t)c->tsg_n / ((uint64_t)c->nloc * fanout) + 1;
+    if (rounds * c->N * fanout > (c->tcp.acks ? (1ull << 27) : (1ull << 28)))
+      return fail(c, TGSIM_ECAPACITY, "TCP segment ids beyond the packets' seq bits");
+    c->tcp_F = fanout;
+  }
   return gen_storm_impl(c, round, t0, fanout, size, spread_ns, state, 1);
 }
 
+static int tcp_send_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n);
 static int gen_storm_impl(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanout, uint32_t size,
                           int64_t spread_ns, uint32_t state, int tcp) {
   if (fanout == 0 || fanout >= c->N || fanout > 32) return fail(c, TGSIM_EINVAL, "bad fanout");
@@ -1281,7 +1292,7 @@ static int gen_storm_impl(tgo_ctx* c, uint32_t round, int64_t t0, uint32_t fanou
     sst[l] = state; sin[l] = g; stt[l] = tmax;
   }
   tgsim_msg_soa m = {src, dst, seq, sz, ts};
-  rc = tcp ? tgo_tcp_send(c, &m, n) : enqueue_impl(c, &m, n);
+  rc = tcp ? tcp_send_impl(c, &m, n) : enqueue_impl(c, &m, n);
   /* single shard, or sharded with a transport (the batch is gathered: replicated sync state) */
   if (!rc && (c->S == 1 || c->has_tr)) rc = tgo_sync_signal(c, sst, sin, stt, c->nloc, NULL);
   if (!rc && c->S > 1 && !c->has_tr) { /* sharded: the caller MAX-reduces the local release across shards */
@@ -1745,7 +1756,7 @@ int tgo_sync_subscribe(tgo_ctx* c, uint32_t topic, uint32_t from, int64_t until_
 
 int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   if (!cfg) return fail(c, TGSIM_EINVAL, "bad arguments");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
+  if (c->S != 1 && !c->has_tr) return fail(c, TGSIM_ESTATE, "a sharded context needs a transport for TCP mode");
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->staged.n) return fail(c, TGSIM_ESTATE, "messages already staged");
   if (c->fl_off) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
@@ -1766,7 +1777,28 @@ int tgo_tcp_enable(tgo_ctx* c, const tgsim_tcp_config* cfg) {
   return TGSIM_OK;
 }
 
+/* Segment ids on the wire (packet seq = id * 16 + attempt, the Philox counter of its netem draws) must
+ * not depend on the shard count. A shard numbers its own segments 0, 1, ... (its state arrays); a
+ * sharded context carries generated storm rounds only, each round n * F writes of one segment in
+ * (instance, k) order, so the single run's id of local segment `sid` is the round's base plus the
+ * shard's offset in it - an affine map per round, the identity on one shard. */
+static uint32_t tcp_wire(const tgo_ctx* c, uint32_t sid) {
+  if (c->S == 1) return sid;
+  const uint32_t per = c->nloc * c->tcp_F, r = sid / per;
+  return r * c->N * c->tcp_F + c->lo * c->tcp_F + sid % per;
+}
+static uint32_t tcp_local(const tgo_ctx* c, uint32_t wid) {
+  if (c->S == 1) return wid;
+  const uint32_t per = c->N * c->tcp_F, r = wid / per;
+  return r * c->nloc * c->tcp_F + (wid % per - c->lo * c->tcp_F);
+}
+
+static int tcp_send_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n);
 int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "sharded TCP mode carries generated storm rounds (tcp_gen_storm_round) only");
+  return tcp_send_impl(c, m, n);
+}
+static int tcp_send_impl(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (c->tc_n) return fail(c, TGSIM_ESTATE, "a context with connections writes through tcp_write");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tcp_react after every window");
@@ -1798,7 +1830,7 @@ int tgo_tcp_send(tgo_ctx* c, const tgsim_msg_soa* m, size_t n) {
       const uint32_t sid = (uint32_t)c->tsg_n++;
       otcps g = {wi, pay + c->tcp.header_bytes, 0, 0, 0, 0, m->t_send[i], INT64_MAX, INT64_MIN, 0, 0, TCP_NOSEG, 0, 0};
       c->tsg[sid] = g;
-      src[k] = w.src; dst[k] = w.dst; seq[k] = sid << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
+      src[k] = w.src; dst[k] = w.dst; seq[k] = tcp_wire(c, sid) << 4; sz[k] = g.wire; ts[k] = m->t_send[i];
     }
   }
   tgsim_msg_soa p = {src, dst, seq, sz, ts};
@@ -1878,6 +1910,7 @@ static int conn_release(tgo_ctx* c, uint32_t k, int64_t t0, ostage* b, size_t* d
 
 int tgo_tcp_connect(tgo_ctx* c, const uint32_t* src, const uint32_t* dst, size_t n, uint32_t* conn_out) {
   if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "connections (their ACK clock) need a single-shard context");
   if (c->sm) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->tw_n && !c->tc_n) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
@@ -2003,12 +2036,61 @@ static uint32_t tcp_copies(uint8_t st) {
 
 static int tcp_react_acks(tgo_ctx* c, size_t* done);
 
+/* Sharded TCP: a write's segments live on its writer's shard
+ * (its packets were staged and shaped there: egress), while a data copy is delivered on its receiver's
+ * shard. After each window every shard forwards the data copies it delivered for another shard's
+ * writers to that shard as their delivery records (one all-to-all of the exchange blocks), and
+ * collects those delivered elsewhere for its own writers into c->tcp_rx. ACKs (acks = 1) leave from
+ * the receiver's shard and are delivered on the writer's: they need no forwarding. */
+static int tcp_forward(tgo_ctx* c) {
+  c->tcp_rx.n = 0;
+  if (c->S == 1) return TGSIM_OK;
+  if (!c->has_tr) return fail(c, TGSIM_ESTATE, "the transport was aborted (a shard failed)");
+  const uint32_t me = c->cfg.shard_id;
+  for (uint32_t p = 0; p < c->S; ++p) c->outbox[p].n = 0;
+  for (size_t i = 0; i < c->out.n; ++i) {
+    const tgsim_record* r = &c->out.v[i];
+    if (c->tcp.acks && (r->seq & TGSIM_TCP_ACK_BIT)) continue;
+    const uint32_t p = shard_of(c, r->src);
+    if (p != me && recs_push(&c->outbox[p], r)) return fail(c, TGSIM_ENOMEM, "oom");
+  }
+  memset(c->xsend, 0, (size_t)c->S * c->xcap * sizeof(tgsim_record));
+  for (uint32_t p = 0; p < c->S; ++p) {
+    orecs* o = &c->outbox[p];
+    if (p == me) continue;
+    if (o->n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "TCP arrivals exceed the exchange capacity (%zu to peer %u)", o->n, p);
+    c->xsend[(size_t)p * c->xcap].t = (int64_t)o->n;
+    memcpy(&c->xsend[(size_t)p * c->xcap + 1], o->v, o->n * sizeof(tgsim_record));
+    o->n = 0;
+  }
+  if (c->tr.alltoall(c->tr.user, c->xsend, c->xrecv, c->xcap * sizeof(tgsim_record), NULL) != 0)
+    return fail(c, TGSIM_EHIP, "transport all-to-all failed");
+  for (uint32_t p = 0; p < c->S; ++p) {
+    if (p == me) continue;
+    const tgsim_record* blk = &c->xrecv[(size_t)p * c->xcap];
+    const size_t n = (size_t)blk[0].t;
+    if (n + 1 > c->xcap) return fail(c, TGSIM_ECAPACITY, "corrupt exchange header");
+    for (size_t i = 0; i < n; ++i)
+      if (recs_push(&c->tcp_rx, &blk[1 + i])) return fail(c, TGSIM_ENOMEM, "oom");
+  }
+  return TGSIM_OK;
+}
+
+/* a data copy this shard settles: delivered here to a local writer's segment, or forwarded (tcp_rx) */
+static int tcp_mine(const tgo_ctx* c, const tgsim_record* r) {
+  return c->S == 1 || shard_of(c, r->src) == c->cfg.shard_id;
+}
+
 int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
   size_t done = 0;
   if (n_done) *n_done = 0;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->tcp_need_react) return TGSIM_OK;
+  {
+    const int rc = tcp_forward(c);
+    if (rc) return rc;
+  }
   if (c->tcp.acks) {
     int rc = tcp_react_acks(c, &done);
     if (rc) return rc;
@@ -2019,7 +2101,7 @@ int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
   /* 1. the window's packets (staged arrays are intact until the next staging) */
   const omsgs* s = &c->staged;
   for (size_t i = 0; i < c->n_status; ++i) {
-    const uint32_t sid = s->seq[i] >> 4;
+    const uint32_t sid = tcp_local(c, s->seq[i] >> 4);
     otcps* g = &c->tsg[sid];
     const uint32_t q = tcp_copies(c->status[i]);
     if (q) { g->outstanding += q; continue; }
@@ -2027,13 +2109,15 @@ int tgo_tcp_react(tgo_ctx* c, size_t* n_done) {
     if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, &done);
     else if (tcp_schedule(c, sid, g->t_att, &done)) return fail(c, TGSIM_ENOMEM, "oom");
   }
-  /* 2. the window's deliveries: first intact arrival, copies accounted */
-  uint32_t* touched = (uint32_t*)malloc((c->out.n + 1) * 4);
+  /* 2. the window's deliveries: first intact arrival, copies accounted - the copies of this shard's
+   *    writers delivered here, then those forwarded from the receivers' shards */
+  uint32_t* touched = (uint32_t*)malloc((c->out.n + c->tcp_rx.n + 1) * 4);
   if (!touched) return fail(c, TGSIM_ENOMEM, "oom");
   size_t nt = 0;
-  for (size_t i = 0; i < c->out.n; ++i) {
-    const tgsim_record* r = &c->out.v[i];
-    const uint32_t sid = r->seq >> 4;
+  for (size_t i = 0; i < c->out.n + c->tcp_rx.n; ++i) {
+    const tgsim_record* r = i < c->out.n ? &c->out.v[i] : &c->tcp_rx.v[i - c->out.n];
+    if (i < c->out.n && !tcp_mine(c, r)) continue;
+    const uint32_t sid = tcp_local(c, r->seq >> 4);
     otcps* g = &c->tsg[sid];
     if (!(r->meta & TGSIM_F_CORRUPT) && r->t < g->arrival) g->arrival = r->t;
     if (r->t > g->t_last) g->t_last = r->t;
@@ -2070,23 +2154,28 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
   for (size_t i = 0; i < c->n_status; ++i) {
     if (s->seq[i] & TGSIM_TCP_ACK_BIT) continue;
     const uint8_t code = c->status[i] & 0x0Fu;
-    otcps* g = &c->tsg[s->seq[i] >> 4];
+    otcps* g = &c->tsg[tcp_local(c, s->seq[i] >> 4)];
     if (code == TGSIM_ST_REJECTED || code == TGSIM_ST_UNREACHABLE) {
       tcp_finish(c, g->w, TGSIM_TCP_REFUSED, g->t_att, done);
       if (c->tw[g->w].conn != TCP_NOSEG) c->tc[c->tw[g->w].conn].broken = 1;  /* the connection is reset */
     }
   }
-  uint32_t* touched = (uint32_t*)malloc((c->out.n + 1) * 4);
+  uint32_t* touched = (uint32_t*)malloc((c->out.n + c->tcp_rx.n + 1) * 4);
   if (!touched || grow((void**)&c->tack, &c->tack_cap, c->tack_n + c->out.n + 1, sizeof(otack))) {
     free(touched);
     return fail(c, TGSIM_ENOMEM, "oom");
   }
   size_t nt = 0;
-  for (size_t i = 0; i < c->out.n; ++i) {
-    const tgsim_record* r = &c->out.v[i];
+  /* the deliveries here (ACKs of this shard's writers' segments; data: answered from here, settled
+   * here for a local writer), then the data copies of this shard's writers delivered elsewhere */
+  for (size_t i = 0; i < c->out.n + c->tcp_rx.n; ++i) {
+    const int rx = i >= c->out.n;
+    const tgsim_record* r = rx ? &c->tcp_rx.v[i - c->out.n] : &c->out.v[i];
     const int intact = !(r->meta & TGSIM_F_CORRUPT);
-    otcps* g = &c->tsg[(r->seq & ~TGSIM_TCP_ACK_BIT) >> 4];
+    /* this shard's segment: an ACK's always, a data copy's once its writer is known to be local */
+    const uint32_t sid = tcp_local(c, (r->seq & ~TGSIM_TCP_ACK_BIT) >> 4);
     if (r->seq & TGSIM_TCP_ACK_BIT) {
+      otcps* g = &c->tsg[sid];  /* an ACK arrives at the writer: always this shard's */
       /* the first intact ACK of a segment that has not given up settles it (its flight slot); what
        * the window's ACKs release leaves at the latest intact one's arrival (duplicates included) */
       if (intact && !g->gave_up) {
@@ -2103,10 +2192,14 @@ static int tcp_react_acks(tgo_ctx* c, size_t* done) {
       continue;
     }
     if (!intact) continue;
+    if (!rx) {  /* the receiver answers every intact data copy it got */
+      otack a = {r->dst, r->src, TGSIM_TCP_ACK_BIT | r->seq, r->t > c->horizon ? r->t : c->horizon};
+      c->tack[c->tack_n++] = a;
+      if (!tcp_mine(c, r)) continue;  /* its writer's shard settles the segment */
+    }
+    otcps* g = &c->tsg[sid];
     if (r->t < g->arrival) g->arrival = r->t;
-    if (!g->touched) { g->touched = 1; touched[nt++] = (r->seq >> 4); }
-    otack a = {r->dst, r->src, TGSIM_TCP_ACK_BIT | r->seq, r->t > c->horizon ? r->t : c->horizon};
-    c->tack[c->tack_n++] = a;
+    if (!g->touched) { g->touched = 1; touched[nt++] = sid; }
   }
   for (size_t k = 0; k < nt; ++k) {
     otcps* g = &c->tsg[touched[k]];
@@ -2212,7 +2305,7 @@ static int tcp_release(tgo_ctx* c, int64_t t_end) {
     if (!src || !dst || !seq || !sz || !ts) rc = TGSIM_ENOMEM;
     for (size_t i = 0; i < nd && !rc; ++i) {
       const otcps* g = &c->tsg[due[i].sid];
-      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (due[i].sid << 4) | g->attempt;
+      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (tcp_wire(c, due[i].sid) << 4) | g->attempt;
       sz[i] = g->wire; ts[i] = g->t_att;
     }
     if (!rc) {
@@ -2284,7 +2377,7 @@ static int tcp_release_acks(tgo_ctx* c, int64_t t_end) {
     if (!src || !dst || !seq || !sz || !ts) rc = TGSIM_ENOMEM;
     for (size_t i = 0; i < nd && !rc; ++i) {
       const otcps* g = &c->tsg[due[i].sid];
-      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (due[i].sid << 4) | g->attempt;
+      src[i] = c->tw[g->w].src; dst[i] = c->tw[g->w].dst; seq[i] = (tcp_wire(c, due[i].sid) << 4) | g->attempt;
       sz[i] = g->wire; ts[i] = g->t_att;
     }
     if (!rc) {

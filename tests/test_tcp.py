@@ -11,6 +11,7 @@ import pytest
 from testground_amd import _abi as A
 from testground_amd import tcp as T
 from testground_amd.sim import SimConfig, Simulator, make_rule, make_shape
+from tests import scenarios as S
 
 MS = 1_000_000
 
@@ -383,17 +384,23 @@ def test_lossy_rpc_over_tcp_hip(hip, oracle):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 * MS):
+def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 * MS, cfg_kw=None, setup=None):
     """The storm plan over TCP mode (plans/benchmarks/storm.go dials and writes 1 KiB per peer):
     tgsim_tcp_gen_storm_round generates each round as writes on the device, SignalAndWait ends
-    the window, and the reaction recovers the 10 % lost segments. Drained afterwards."""
+    the window, and the reaction recovers the 10 % lost segments. Drained afterwards. Sharded
+    (cfg_kw shard_id / n_shards, setup attaching a transport): the same calls on every shard, each
+    collective; a shard reports its own writers' writes (each round's block of its instances) and
+    its own counters."""
     rng = np.random.default_rng(seed)
     # a window stages the round's writes, the ACKs of every intact data copy of the last window
     # (retransmitted ones included) and the fired timers: with a 30 ms RTO nearly every segment is
     # retransmitted once, spuriously
     per_window = max(1 << 16, 5 * n * 8)
     s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=per_window,
-                            max_records=max(1 << 18, 16 * n * 8), max_states=64, data_prefix_len=12), binding=b)
+                            max_records=max(1 << 18, 16 * n * 8), max_states=64, data_prefix_len=12,
+                            **(cfg_kw or {})), binding=b)
+    if setup is not None:
+        setup(s)
     s.tcp_enable(max_attempts=5, rto_ns=rto_ns, acks=acks, max_writes=rounds * n * 8, max_segments=rounds * n * 8)
     for g in range(n):
         s.set_shape(g, make_shape(latency_ns=int(rng.integers(5, 21)) * MS, jitter_ns=2 * MS, loss=10.0,
@@ -469,3 +476,39 @@ def test_tcp_storm_acks_full_size(hip, oracle):
     b = run_tcp_storm(oracle, n=100_000, rounds=4, acks=True, rto_ns=200 * MS)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
     assert a[2]["retransmissions"] > 0.05 * a[2]["writes"] and (a[0] == A.TCP_DELIVERED).mean() > 0.99
+
+
+def tcp_storm_sharded(b, world, device=False, exchange_cap=1 << 14, **kw):
+    """run_tcp_storm over `world` shards (one thread each, ThreadGroup transport), recombined into the
+    single run's form: every round's writes in instance order (shard k owns instances [lo, hi)), the
+    counters summed."""
+    n, rounds = kw.get("n", 400), kw.get("rounds", 6)
+    outs = S.sharded_threads(world, lambda k, tr: run_tcp_storm(
+        b, cfg_kw=S.shard_cfg(world, k, exchange_cap=exchange_cap), setup=lambda sim: sim.set_transport(tr), **kw),
+        device=device)
+    per_round = lambda k: (S.shard_range(n, k, world)[1] - S.shard_range(n, k, world)[0]) * 8
+    st = np.concatenate([outs[k][0].reshape(rounds, per_round(k)) for k in range(world)], axis=1).ravel()
+    t = np.concatenate([outs[k][1].reshape(rounds, per_round(k)) for k in range(world)], axis=1).ravel()
+    stats = {f: sum(o[2][f] for o in outs) for f in outs[0][2]}
+    return st, t, stats, sum(o[3] for o in outs)
+
+
+@pytest.mark.parametrize("world,acks", [(2, False), (3, False), (2, True), (3, True)])
+def test_tcp_storm_sharded_oracle(oracle, world, acks):
+    """TCP mode sharded. A data copy is settled on its writer's shard (forwarded
+    there after the window through the exchange blocks), its ACK leaves from the receiver's shard:
+    the sharded oracle run equals the single one (write outcomes and times, counters)."""
+    a = tcp_storm_sharded(oracle, world, acks=acks)
+    b = run_tcp_storm(oracle, acks=acks)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
+    assert b[2]["retransmissions"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,acks", [(2, False), (4, False), (2, True), (4, True)])
+def test_tcp_storm_sharded_hip(hip, oracle, world, acks):
+    """The same on HIP shards on one GPU (thread transport): equal to the single HIP context and the
+    oracle, with the reactions queued without a read-back (bench.py --tcp's loop)."""
+    a = tcp_storm_sharded(hip, world, device=True, acks=acks, wait=False)
+    b = run_tcp_storm(oracle, acks=acks)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
