@@ -323,7 +323,7 @@ def sim_config(args, shard=0, n_shards=1, device=0):
     return SimConfig(n_instances=args.instances, seed=args.seed, shard_id=shard, n_shards=n_shards, device=device,
                      data_prefix_len=12, max_msgs_per_window=max(1 << 20, per_window),
                      max_records=args.max_records * (2 if acks else 1) // max(1, n_shards // 2), max_states=4096,
-                     exchange_cap=exchange_cap(args.instances * args.fanout, n_shards))
+                     exchange_cap=exchange_cap(per_window, n_shards))
 
 
 def cpu_baseline(args, shapes):
@@ -431,11 +431,10 @@ def main():
     spread, rtt = int(args.spread_ms * MS), int(args.rtt_ms * MS)
     N, F = args.instances, args.fanout
 
-    if args.tcp:
-        if world > 1:
-            raise SystemExit("--tcp: TCP mode needs a single-shard context")
+    if args.tcp:  # sharded: each rank's writers (arrivals forwarded to the writer's shard)
         rounds = args.warmup + probe_steps(args) + args.steps + 1
-        sim.tcp_enable(max_writes=rounds * N * F, max_segments=rounds * N * F, acks=args.tcp_acks)
+        nl = sim.hi - sim.lo
+        sim.tcp_enable(max_writes=rounds * nl * F, max_segments=rounds * nl * F, acks=args.tcp_acks)
 
     def step(r: int):
         # t0 / t_wait = TGSIM_T_NOW: the round starts where the device's last window ended, so a
@@ -500,16 +499,26 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.tcp:
         cpu = cpu_baseline(args, shapes)
 
-    if rank == 0 and args.tcp:
+    if args.tcp:
         dt = {k: tcp1[k] - tcp0[k] for k in tcp1}
-        print(json.dumps({
-            "metric": "TCP writes delivered/sec (100k-inst storm over TCP mode, DESIGN.md 2.11)"
-                      + (", ACKs on the reverse path" if args.tcp_acks else ""),
-            "value": dt["delivered"] / elapsed, "unit": "writes/s", "n_gpus": 1, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "packets_delivered_per_s": delivered / elapsed, "tcp_in_timed_steps": dt,
-            "dtype": "int64", "data": "synthetic", "kernels_probe": warm_kernels}), flush=True)
+        if world > 1:  # every rank's writers' counters (gloo: host tensors)
+            keys = sorted(dt)
+            v = torch.tensor([dt[k] for k in keys], dtype=torch.int64)
+            dist.all_reduce(v, op=dist.ReduceOp.SUM)
+            dt = {k: int(x) for k, x in zip(keys, v.tolist())}
+        if rank == 0:
+            print(json.dumps({
+                "metric": "TCP writes delivered/sec (100k-inst storm over TCP mode, DESIGN.md 2.11)"
+                          + (", ACKs on the reverse path" if args.tcp_acks else ""),
+                "value": dt["delivered"] / elapsed, "unit": "writes/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "strong", "parallelism": f"shard{world}{transport}",
+                "packets_delivered_per_s": delivered / elapsed, "tcp_in_timed_steps": dt,
+                "collectives": coll, "dtype": "int64", "data": "synthetic", "kernels_probe": warm_kernels}),
+                flush=True)
         sim.close()
+        if world > 1:
+            dist.destroy_process_group()
         return
     if rank == 0:
         line = {

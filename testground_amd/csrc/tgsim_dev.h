@@ -77,6 +77,8 @@ struct TcpScalars {
   uint32_t ack_base;              // ... their first staged slot at the release
   uint32_t tb_tail;               // ... oldest live timer batch
   uint32_t plan_n, plan_total;    // ... batches due at this release and their segments
+  uint32_t n_in;                  // the reaction's deliveries: the window's own (n_out) + the copies other
+                                  // shards delivered for this shard's writers (sharded: k_tcp_rx)
   unsigned long long retx, delivered, failed, released;
 };
 struct TcpDev {
@@ -122,6 +124,13 @@ struct TcpDev {
   uint32_t mss = 0, hdr = 0, max_att = 0;
   int64_t rto = 0;
   uint64_t cap_w = 0, cap_s = 0;
+  // sharded: instances [lo, lo + nloc) of N on shard `shard` of S; segment ids on the
+  // wire are the single run's (generated storm rounds of fanout F: tgsim_tcp.hip tcp_wire / tcp_local);
+  // data copies delivered here for another shard's writers go there through the exchange blocks
+  uint32_t S = 1, shard = 0, N = 0, lo = 0, nloc = 0, F = 0, xcap = 0;
+  uint64_t inv = 0;               // shard_inv(N)
+  uint32_t* xq = nullptr;
+  tgsim_record *xsend = nullptr, *xrecv = nullptr;
 };
 
 // Sequential probes (tgsim_probe_*): per local prober its position in order,
@@ -456,6 +465,8 @@ hipError_t launch_tcp_release_acks(Dev& d, TcpDev& t, uint32_t cur, bool base_de
                                    bool reg, uint32_t lo, uint32_t hi);
 // TCP mode: the staged storm round [base, base + n) adopted as writes wbase.. / segments sbase..
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase);
+// sharded: the window's data copies for other shards' writers into the exchange blocks (+ headers)
+hipError_t launch_tcp_fwd(Dev& d, TcpDev& t);
 // connections: new segments linked to their queues (links: n quads conn, old tail, first, count),
 // then every connection sends what its window has room for, at max(written, t0) (t0 = INT64_MIN:
 // at the write times; after_window: first apply the window's ACKs and resets, t0 = the window's

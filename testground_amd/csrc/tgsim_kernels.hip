@@ -2152,7 +2152,10 @@ struct EmitPolicy {
 #define TG_BKT_WGS_PER_CU 4
 #endif
 constexpr int kBktCap = TG_BKT_CAP;   // items of one bucket held by the workgroup
-constexpr int kBktFusedKeyBits = 9;   // keys per bucket on the fused path
+#ifndef TG_BKT_KEY_BITS
+#define TG_BKT_KEY_BITS 9
+#endif
+constexpr int kBktFusedKeyBits = TG_BKT_KEY_BITS;   // keys per bucket on the fused path (log2)
 #ifndef TGSIM_BKT_RANK_MAX
 #define TGSIM_BKT_RANK_MAX 512
 #endif

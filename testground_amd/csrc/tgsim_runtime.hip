@@ -1238,7 +1238,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
     if (!c->pend_host &&
         hipHostMalloc((void**)&c->pend_host, kRadixBlocks * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
       return fail(c, TGSIM_ENOMEM, "pinned pend maxima");
-    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by : nullptr, c->tcp_on && c->tcp.acks ? tcp_inbox_mult(c) : 0u,
+    HIPCK(c, launch_pend_max(d, c->tcp_on ? c->td.pend_by + c->lo : nullptr, c->tcp_on && c->tcp.acks ? tcp_inbox_mult(c) : 0u,
                              (uint32_t)mult, c->pend_host), "pend max");
     HIPCK(c, sync_scalars(d), "sync");
     uint32_t mx = 0;
@@ -1262,7 +1262,7 @@ static int plan_queue_limit(tgsim_ctx* c) {
     d.heavy.pend = pend_ref(d);
     d.heavy.zd = d.zd;
     d.heavy.inbox = c->win_m_inbox ? d.inbox : nullptr;
-    d.heavy.retx = c->tcp_on ? c->td.pend_by : nullptr;  // single shard: local = global ids
+    d.heavy.retx = c->tcp_on ? c->td.pend_by + c->lo : nullptr;  // [N] by instance: the local senders' part
     d.heavy.m_uniform = (uint32_t)m_uniform;
     d.heavy.m_inbox = c->win_m_inbox;
     if (c->tcp_on && c->tcp.acks) {  // ACKs: at most one per delivery the sender got last window
@@ -2904,7 +2904,7 @@ extern "C" int tgsim_tcp_enable(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
 }
 static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   if (!c || !cfg) return fail(c, TGSIM_EINVAL, "bad arguments");
-  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "TCP mode needs a single-shard context");
+  if (int rc = need_transport(c)) return rc;  // sharded: every reaction forwards arrivals (collective)
   if (c->in_window || c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode already on or inside a window");
   if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "messages already staged");
   if (!c->fl_off.empty()) return fail(c, TGSIM_ESTATE, "a flood graph is installed: TCP mode and floods exclude each other");
@@ -2959,6 +2959,9 @@ static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
     return fail(c, TGSIM_ENOMEM, "pinned TCP snapshots");
   for (hipEvent_t& e : c->tcp_ev) HIPCK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "tcp init");
   d.mss = t.mss; d.hdr = t.header_bytes; d.max_att = t.max_attempts; d.rto = t.rto_ns; d.cap_w = W; d.cap_s = S;
+  d.S = c->S; d.shard = c->shard; d.N = c->N; d.lo = c->lo; d.nloc = c->nloc; d.xcap = c->d.xcap; d.inv = shard_inv(c->N);
+  d.xq = c->d.qc + ((size_t)3 * kNSub << 5);  // the exchange cursors' lines (idle between windows)
+  d.xsend = c->d.xsend; d.xrecv = c->d.xrecv;
   c->tcp = t;
   c->tcp_on = true;
   return TGSIM_OK;
@@ -2972,6 +2975,7 @@ static int tgsim_tcp_send_body(tgsim_ctx* c, const tgsim_msg_soa* m, size_t n) {
   if (!c || !m) return TGSIM_EINVAL;
   c->spec.valid = false;
   if (!c->tcp_on) return fail(c, TGSIM_ESTATE, "TCP mode is off");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "sharded TCP mode carries generated storm rounds (tgsim_tcp_gen_storm_round) only");
   if (c->td.n_conn) return fail(c, TGSIM_ESTATE, "a context with connections writes through tgsim_tcp_write");
   if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "TCP mode: tgsim_tcp_react after every window");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
@@ -3059,6 +3063,12 @@ static int tgsim_tcp_react_body(tgsim_ctx* c, size_t* n_done) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (!c->tcp_need_react) return TGSIM_OK;
   const bool on_dev = c->n_status_last == kStatusOnDevice;
+  if (c->S > 1) {  // the data copies delivered here for other shards' writers go to them (collective)
+    if (int rc = need_transport(c)) return rc;
+    HIPCK(c, launch_tcp_fwd(c->d, c->td), "tcp forward");
+    if (c->tr.alltoall(c->tr.user, c->d.xsend, c->d.xrecv, (size_t)c->d.xcap * sizeof(tgsim_record), c->d.stream) != 0)
+      return shard_failed(c, fail(c, TGSIM_EHIP, "transport all-to-all failed"));
+  }
   HIPCK(c, launch_tcp_react(c->d, c->td, c->tcp_cur, on_dev ? 0u : c->n_status_last,
                             on_dev ? &c->d.sc->n_msgs_last : nullptr, ++c->tcp_epoch, c->tcp_fill), "tcp react");
   if (c->td.n_conn) {  // the window's ACKs open the connections' windows: send what fits, at its end
@@ -3169,6 +3179,13 @@ static int tgsim_tcp_gen_storm_round_body(tgsim_ctx* c, uint32_t round, int64_t 
   const uint64_t n = (uint64_t)c->nloc * fanout;
   if (c->tw_n + n > c->tcp.max_writes || c->tsg_n + n > c->tcp.max_segments)
     return fail(c, TGSIM_ECAPACITY, "TCP write / segment capacity");
+  if (c->S != 1) {  // the single run's segment ids on the wire (tgsim_tcp.hip tcp_wire): one fanout, 27/28 bits
+    if (c->td.F && c->td.F != fanout) return fail(c, TGSIM_ENOTSUP, "sharded TCP storms keep one fanout");
+    const uint64_t rounds = c->tsg_n / n + 1;
+    if (rounds * c->N * fanout > (c->tcp.acks ? (1ull << 27) : (1ull << 28)))
+      return fail(c, TGSIM_ECAPACITY, "TCP segment ids beyond the packets' seq bits");
+    c->td.F = fanout;
+  }
   const uint32_t base = c->n_staged;
   int rc = gen_storm_impl(c, round, t0, fanout, size, spread_ns, state);
   if (rc) return rc;
@@ -3237,6 +3254,7 @@ static int tgsim_tcp_connect_body(tgsim_ctx* c, const uint32_t* src, const uint3
   if (!c) return TGSIM_EINVAL;
   if (c->storm_on) return fail(c, TGSIM_ESTATE, "a storm reactor owns the connections");
   if (!c->tcp_on || !c->tcp.acks) return fail(c, TGSIM_ESTATE, "connections need TCP mode with acks = 1");
+  if (c->S != 1) return fail(c, TGSIM_ENOTSUP, "connections (their ACK clock) need a single-shard context");
   if (c->in_window) return fail(c, TGSIM_ESTATE, "inside a window");
   if (c->tw_n && !c->td.n_conn) return fail(c, TGSIM_ESTATE, "tcp_send writes exist: a context uses one or the other");
   if (n && (!src || !dst)) return fail(c, TGSIM_EINVAL, "bad arguments");

@@ -54,6 +54,24 @@ __device__ __forceinline__ uint32_t tcp_copies(uint8_t st) {
   return q;
 }
 
+// Sharded TCP: a shard numbers its own segments 0, 1, ... (its state arrays), while a
+// packet's seq carries the single run's segment id, so that its netem draws (Philox keyed by (seq,
+// src)) do not depend on the shard count. A sharded context carries generated storm rounds of one
+// fanout F, n * F one-segment writes per round in (instance, k) order: an affine map per round, the
+// identity on one shard (oracle twin: tgsim_oracle.c tcp_wire / tcp_local).
+__device__ __forceinline__ uint32_t tcp_local(const TcpDev& t, uint32_t w) {
+  if (t.S == 1) return w;
+  const uint32_t per = t.N * t.F, r = w / per;
+  return r * t.nloc * t.F + (w % per - t.lo * t.F);
+}
+__device__ __forceinline__ uint32_t tcp_wire(const TcpDev& t, uint32_t sid) {
+  if (t.S == 1) return sid;
+  const uint32_t per = t.nloc * t.F, r = sid / per;
+  return r * t.N * t.F + t.lo * t.F + sid % per;
+}
+// a data copy whose writer (its src) lives on this shard: settled here
+__device__ __forceinline__ bool tcp_mine(const TcpDev& t, uint32_t src) { return t.S == 1 || src - t.lo < t.nloc; }
+
 // the write fails (earliest failure kept; the first transition from pending counts it)
 __device__ __forceinline__ void tcp_fail(TcpDev& t, uint32_t w, int64_t tf, uint32_t state) {
   atomicMin(reinterpret_cast<long long*>(&t.w_fail[w]), (long long)(tf * 2 + (state == TGSIM_TCP_TIMEOUT ? 1 : 0)));
@@ -104,9 +122,10 @@ __global__ __launch_bounds__(kBlock) void k_tcp_status(const uint8_t* __restrict
                                                        const uint32_t* n_dev, TcpDev t) {
   const uint32_t n = n_dev ? *n_dev : n_host;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t sq = seq[i], sid = sq >> 4;
+    const uint32_t sq = seq[i];
     bool retx = false;
     if (!(t.acks && (sq & TGSIM_TCP_ACK_BIT))) {  // acks mode: an ACK packet's fate concerns nobody
+      const uint32_t sid = tcp_local(t, sq >> 4);
       const uint8_t st = status[i];
       const uint32_t q = tcp_copies(st), code = st & 0x0Fu;
       // a released retransmission leaves its sender's pending count once its packet is accounted
@@ -146,20 +165,25 @@ __device__ __forceinline__ uint32_t tcp_arrived(TcpDev& t, uint32_t sw, int64_t 
   return 1u;
 }
 
-__global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restrict__ o_seq,
+// Sharded, the inputs are the window's own deliveries [0, n_out) and then the data copies of this
+// shard's writers delivered on other shards (k_tcp_rx, [n_out, n_in)): a data copy delivered here for
+// another shard's writer is only answered (its ACK leaves from here), a forwarded one only settled.
+__global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restrict__ o_src,
+                                                       const uint32_t* __restrict__ o_seq,
                                                        const int64_t* __restrict__ o_t,
                                                        const uint32_t* __restrict__ o_flags, const DevScalars* sc,
                                                        TcpDev t) {
-  const uint32_t n = sc->n_out;
+  const uint32_t n = t.sc->n_in, nl = sc->n_out;
   uint32_t ndel = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t sq = o_seq[i];
     const int64_t ti = o_t[i];
     const bool corrupt = o_flags[i] & TGSIM_F_CORRUPT;
+    const bool here = i < nl, mine = !here || tcp_mine(t, o_src[i]);
     if (t.acks) {  // acks mode: ACKs settle segments, intact data is answered; timers decide the rest
       bool ack = false, dup = false;
       if (sq & TGSIM_TCP_ACK_BIT) {
-        const uint32_t sid = (sq & ~TGSIM_TCP_ACK_BIT) >> 4;
+        const uint32_t sid = tcp_local(t, (sq & ~TGSIM_TCP_ACK_BIT) >> 4);
         // the first intact ACK of a segment that has not given up frees its connection a flight slot;
         // what the window's ACKs release leaves at the latest intact one's arrival (every ACK counts
         // there, so which of a segment's duplicate ACKs claims it does not matter)
@@ -174,9 +198,11 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
             }
           }
         }
+      } else if (!corrupt && !mine) {
+        ack = true;  // answered here; the writer's shard settles it from the forwarded copy
       } else if (!corrupt) {
-        ack = true;
-        const uint32_t sid = sq >> 4, sw = t.s_w[sid];
+        ack = here;
+        const uint32_t sid = tcp_local(t, sq >> 4), sw = t.s_w[sid];
         // the first attempt's only copy is the segment's only delivery (a later attempt - and with
         // it another copy - would have set kRetxBit): this thread settles it
         if (((sw >> kQShift) & 3u) == 1u && !(sw & kRetxBit)) {
@@ -192,7 +218,12 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
       put_bits(t.bm_a, i, ack);
       continue;
     }
-    const uint32_t sid = sq >> 4;
+    if (!mine) {  // another shard's writer: forwarded there (k_tcp_fwd)
+      put_bits(t.bm_r, i, false);
+      put_bits(t.bm_d, i, false);
+      continue;
+    }
+    const uint32_t sid = tcp_local(t, sq >> 4);
     const uint32_t sw = t.s_w[sid];
     const bool sole = ((sw >> kQShift) & 3u) == 1u;
     bool retx = false;
@@ -218,11 +249,11 @@ __global__ __launch_bounds__(kBlock) void k_tcp_arrive(const uint32_t* __restric
 // into the block's k_tcp_arrive partial (same grid), not into one shared line per wave.
 __global__ __launch_bounds__(kBlock) void k_tcp_settle(const uint32_t* __restrict__ o_seq, const DevScalars* sc,
                                                        TcpDev t, uint32_t epoch, uint32_t cur) {
-  const uint32_t n = sc->n_out;
+  const uint32_t n = t.sc->n_in;
   uint32_t ndel = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     if (!((t.bm_d[i >> 6] >> (i & 63u)) & 1ull)) continue;
-    const uint32_t sid = o_seq[i] >> 4;
+    const uint32_t sid = tcp_local(t, o_seq[i] >> 4);
     if (atomicMax(&t.s_mark[sid], epoch) >= epoch) continue;
     const int64_t arr = t.s_arr[sid];
     if (arr != INT64_MAX) {
@@ -250,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_collect(const uint32_t* __restri
                                                         uint32_t nparts) {
   __shared__ uint32_t red[kBlock / 64];
   __shared__ uint32_t sbase;
-  const uint32_t ws = ((n_dev ? *n_dev : n_host) + 63u) >> 6, wr = (sc->n_out + 63u) >> 6, nw = ws + wr;
+  const uint32_t ws = ((n_dev ? *n_dev : n_host) + 63u) >> 6, wr = (t.sc->n_in + 63u) >> 6, nw = ws + wr;
   uint32_t nretx = 0;
   for (uint32_t b0 = blockIdx.x * kBlock; b0 < nw; b0 += gridDim.x * kBlock) {  // uniform per block
     const uint32_t wi = b0 + threadIdx.x;
@@ -269,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_collect(const uint32_t* __restri
     if (threadIdx.x == 0 && tot) sbase = atomicAdd(&t.sc->pend_n[cur], tot);
     __syncthreads();
     p += sbase;
-    for (; m; m &= m - 1) t.pend[cur][p++] = seq[i0 + (uint32_t)__builtin_ctzll(m)] >> 4;
+    for (; m; m &= m - 1) t.pend[cur][p++] = tcp_local(t, seq[i0 + (uint32_t)__builtin_ctzll(m)] >> 4);
     nretx += tot;
     __syncthreads();  // sbase is rewritten by the next round
   }
@@ -303,6 +334,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_reset(TcpDev t, uint32_t cur, co
     t.sc->done = 0;
     t.sc->pend_n[cur ^ 1u] = 0;
     t.sc->ack_n = 0;
+    t.sc->n_in = sc->n_out;  // sharded: k_tcp_rx adds the forwarded copies
     if (fill != ~0u) {  // acks mode: the window's new segments sent in [T, t_end): timers in [T, t_end) + rto
       TcpBatch& b = t.tb[fill % kTcpBatches];
       b.t_lo = sc->T + t.rto;
@@ -355,7 +387,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_release(TcpDev t, uint32_t cur, 
     if (rel) {
       const uint32_t p = sb_r + pr;
       if (p < cap) {
-        m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | t.s_att[sid]; m_size[p] = t.s_wire[sid];
+        m_src[p] = t.w_src[w]; m_dst[p] = t.w_dst[w]; m_seq[p] = (tcp_wire(t, sid) << 4) | t.s_att[sid];
+        m_size[p] = t.s_wire[sid];
         m_t[p] = ta;
       } else {
         atomicOr(&sc->err, ERR_CAP_M);
@@ -554,7 +587,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_fire(TcpDev t, DevScalars* sc, u
       const uint32_t w = t.s_w[sid] & kWMask, src = t.w_src[w];
       const uint32_t p = qf++;
       if (p < cap) {
-        m_src[p] = src; m_dst[p] = t.w_dst[w]; m_seq[p] = (sid << 4) | t.s_att[sid]; m_size[p] = t.s_wire[sid];
+        m_src[p] = src; m_dst[p] = t.w_dst[w]; m_seq[p] = (tcp_wire(t, sid) << 4) | t.s_att[sid];
+        m_size[p] = t.s_wire[sid];
         m_t[p] = t.s_tatt[sid];
       } else {
         atomicOr(&sc->err, ERR_CAP_M);
@@ -815,12 +849,108 @@ __global__ __launch_bounds__(kBlock) void k_tcp_adopt(TcpDev t, uint32_t base, u
     const uint32_t m = base + i, w = wbase + i, sid = sbase + i;
     t.w_src[w] = m_src[m]; t.w_dst[w] = m_dst[m]; t.w_rem[w] = 1u;
     t.s_w[sid] = w | kSoleSeg; t.s_wire[sid] = m_size[m] + t.hdr; t.s_tatt[sid] = m_t[m];
-    m_seq[m] = sid << 4;
+    m_seq[m] = tcp_wire(t, sid) << 4;
     m_size[m] += t.hdr;
   }
 }
 
+// Sharded: the window's data copies delivered here for another shard's writers, each to its writer's
+// shard as its delivery record (t, src, dst, seq; meta = the delivery flags), one reservation per wave
+// and peer on the peer's cursor (xq[p << 5], zeroed by the host before)
+__global__ __launch_bounds__(kBlock) void k_tcp_fwd(const uint32_t* __restrict__ o_src,
+                                                    const uint32_t* __restrict__ o_dst,
+                                                    const uint32_t* __restrict__ o_seq,
+                                                    const int64_t* __restrict__ o_t,
+                                                    const uint32_t* __restrict__ o_flags, DevScalars* sc, TcpDev t) {
+  const uint32_t n = sc->n_out;
+  for (uint32_t i0 = blockIdx.x * kBlock; i0 < n; i0 += gridDim.x * kBlock) {  // wave-uniform trip count
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t p = kNoPeer;
+    if (i < n) {
+      const uint32_t sq = o_seq[i], src = o_src[i];
+      if (!(t.acks && (sq & TGSIM_TCP_ACK_BIT)) && !tcp_mine(t, src)) p = shard_of_inv(src, t.S, t.inv);
+    }
+    bool pending = p != kNoPeer;
+    for (;;) {  // the lanes of one peer share a reservation
+      const uint64_t m = __ballot(pending);
+      if (m == 0) break;
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      const uint32_t lp = __shfl(p, leader);
+      const bool mine = pending && p == lp;
+      const uint64_t mm = __ballot(mine);
+      uint32_t base = 0;
+      if ((int)lane_id() == leader) base = atomicAdd(t.xq + (lp << 5), (uint32_t)__popcll(mm));
+      base = __shfl(base, leader);
+      if (mine) {
+        const uint32_t pos = base + mask_rank(mm);
+        if (pos < t.xcap - 1u) {
+          tgsim_record r;
+          r.t = o_t[i]; r.src = o_src[i]; r.dst = o_dst[i]; r.seq = o_seq[i]; r.size = 0; r.meta = o_flags[i];
+          r.corrupt_off = 0;
+          t.xsend[(size_t)p * t.xcap + 1 + pos] = r;
+        } else {
+          atomicOr(&sc->err, ERR_CAP_X);
+        }
+        pending = false;
+      }
+    }
+  }
+}
+
+// Sharded: the forward blocks' headers (counts from the cursors)
+__global__ void k_tcp_xheaders(TcpDev t) {
+  const uint32_t p = threadIdx.x;
+  if (p >= t.S) return;
+  tgsim_record h;
+  h.t = (int64_t)min(t.xq[p << 5], t.xcap - 1u);
+  h.src = h.dst = h.seq = h.size = h.meta = h.corrupt_off = 0;
+  t.xsend[(size_t)p * t.xcap] = h;
+}
+
+// Sharded: the copies other shards delivered for this shard's writers join the reaction's inputs
+// behind the window's own deliveries (o_* from n_out on: the delivery API reads [0, n_out)); every
+// block takes the peers' counts (S <= 64) and their prefix itself
+__global__ __launch_bounds__(kBlock) void k_tcp_rx(DevScalars* sc, TcpDev t, uint32_t cap, uint32_t* __restrict__ o_src,
+                                                   uint32_t* __restrict__ o_dst, uint32_t* __restrict__ o_seq,
+                                                   int64_t* __restrict__ o_t, uint32_t* __restrict__ o_flags) {
+  __shared__ uint32_t off[kMaxShards + 1];
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    bool bad = false;
+    for (uint32_t p = 0; p < t.S; ++p) {
+      off[p] = a;
+      const int64_t np = p == t.shard ? 0 : t.xrecv[(size_t)p * t.xcap].t;
+      bad |= np < 0 || np >= (int64_t)t.xcap;
+      a += (np < 0 || np >= (int64_t)t.xcap) ? 0u : (uint32_t)np;
+    }
+    off[t.S] = a;
+    if (bad && blockIdx.x == 0) atomicOr(&sc->err, ERR_EXCH_HDR);
+  }
+  __syncthreads();
+  const uint32_t base = sc->n_out, tot = off[t.S];
+  const uint32_t room = cap > base ? cap - base : 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    t.sc->n_in = base + min(tot, room);
+    if (tot > room) atomicOr(&sc->err, ERR_CAP_D);
+  }
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < min(tot, room); j += gridDim.x * kBlock) {
+    uint32_t p = 0;
+    while (p + 1 < t.S && off[p + 1] <= j) ++p;
+    const tgsim_record r = t.xrecv[(size_t)p * t.xcap + 1 + (j - off[p])];
+    const uint32_t k = base + j;
+    o_src[k] = r.src; o_dst[k] = r.dst; o_seq[k] = r.seq; o_t[k] = r.t; o_flags[k] = r.meta;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_tcp_fwd(Dev& d, TcpDev& t) {
+  if (hipMemsetAsync(t.xq, 0, (size_t)t.S * 128, d.stream) != hipSuccess) return hipGetLastError();
+  hipLaunchKernelGGL(k_tcp_fwd, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_src, d.o_dst, d.o_seq, d.o_t,
+                     d.o_flags, d.sc, t);
+  hipLaunchKernelGGL(k_tcp_xheaders, dim3(1), dim3(kMaxShards), 0, d.stream, t);
+  return hipGetLastError();
+}
 
 hipError_t launch_tcp_adopt(Dev& d, TcpDev& t, uint32_t base, uint32_t n, uint32_t wbase, uint32_t sbase) {
   if (!n) return hipSuccess;
@@ -852,8 +982,12 @@ hipError_t launch_tcp_conn_release(Dev& d, TcpDev& t, uint32_t mode, uint32_t cu
 hipError_t launch_tcp_react(Dev& d, TcpDev& t, uint32_t cur, uint32_t n_host, const uint32_t* n_dev, uint32_t epoch,
                             uint32_t fill) {
   hipLaunchKernelGGL(k_tcp_reset, dim3(1), dim3(kBlock), 0, d.stream, t, cur, d.sc, fill);
+  if (t.S > 1)  // after the forward exchange (launch_tcp_fwd + the transport's all-to-all)
+    hipLaunchKernelGGL(k_tcp_rx, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.sc, t, (uint32_t)kNSub * d.subcap,
+                       d.o_src, d.o_dst, d.o_seq, d.o_t, d.o_flags);
   hipLaunchKernelGGL(k_tcp_status, dim3(kStreamBlocks), dim3(kBlock), 0, d.stream, d.status, d.m_seq, n_host, n_dev, t);
-  hipLaunchKernelGGL(k_tcp_arrive, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_seq, d.o_t, d.o_flags, d.sc, t);
+  hipLaunchKernelGGL(k_tcp_arrive, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_src, d.o_seq, d.o_t, d.o_flags,
+                     d.sc, t);
   hipLaunchKernelGGL(k_tcp_settle, dim3(kTcpArriveBlocks), dim3(kBlock), 0, d.stream, d.o_seq, d.sc, t, epoch, cur);
   hipLaunchKernelGGL(k_tcp_collect, dim3(TG_TCP_COLLECT_BLOCKS), dim3(kBlock), 0, d.stream, d.m_seq, n_host, n_dev, d.o_seq, d.sc, t, cur,
                      (uint32_t)kTcpArriveBlocks);

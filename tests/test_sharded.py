@@ -117,9 +117,12 @@ def _worker(rank, world, port, seed, q):
                             setup=lambda sim: sim.set_transport(tr))
         from tests.test_storm_plan import random_run
         reactor = random_run(ob, seed, shard=(rank, world, lambda ph: tr))  # the storm plan's reactor
+        from tests.test_tcp import run_tcp_storm  # TCP mode: arrivals forwarded to the writers' shards
+        tcp = run_tcp_storm(ob, n=400, rounds=4, acks=True, cfg_kw=S.shard_cfg(world, rank, exchange_cap=1 << 14),
+                            setup=lambda sim: sim.set_transport(tr))
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, outs[0], (storm, reactor)))
+        q.put((rank, outs[0], (storm, reactor, tcp)))
     except Exception:  # surface the failure in the parent
         import traceback
         q.put((rank, "ERR", traceback.format_exc()))
@@ -147,6 +150,10 @@ def test_sharded_gloo(oracle, world):
     S.assert_storm_sharded([got[r][1][0] for r in range(world)], S.run_storm(oracle, n_inst=600, rounds=3), world, 600)
     from tests.test_storm_plan import assert_storm_shards_match, random_run
     assert_storm_shards_match([got[r][1][1] for r in range(world)], random_run(oracle, seed))
+    from tests.test_tcp import combine_tcp_storm, run_tcp_storm
+    a = combine_tcp_storm([got[r][1][2] for r in range(world)], world, 400, 4)
+    b = run_tcp_storm(oracle, n=400, rounds=4, acks=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
 
 
 def _failing_shard_run(binding, device=False, world=3):

@@ -482,10 +482,14 @@ def tcp_storm_sharded(b, world, device=False, exchange_cap=1 << 14, **kw):
     """run_tcp_storm over `world` shards (one thread each, ThreadGroup transport), recombined into the
     single run's form: every round's writes in instance order (shard k owns instances [lo, hi)), the
     counters summed."""
-    n, rounds = kw.get("n", 400), kw.get("rounds", 6)
     outs = S.sharded_threads(world, lambda k, tr: run_tcp_storm(
         b, cfg_kw=S.shard_cfg(world, k, exchange_cap=exchange_cap), setup=lambda sim: sim.set_transport(tr), **kw),
         device=device)
+    return combine_tcp_storm(outs, world, kw.get("n", 400), kw.get("rounds", 6))
+
+
+def combine_tcp_storm(outs, world, n, rounds):
+    """Per-shard run_tcp_storm outputs -> the single run's form."""
     per_round = lambda k: (S.shard_range(n, k, world)[1] - S.shard_range(n, k, world)[0]) * 8
     st = np.concatenate([outs[k][0].reshape(rounds, per_round(k)) for k in range(world)], axis=1).ravel()
     t = np.concatenate([outs[k][1].reshape(rounds, per_round(k)) for k in range(world)], axis=1).ravel()
