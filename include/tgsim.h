@@ -437,8 +437,10 @@ int tgsim_restore(tgsim_ctx* ctx, const void* buf, size_t n);
  *     own routes drop, a disabled peer);
  * and the next probe leaves at max(end, horizon). Call tgsim_probe_react after every window. It
  * also proposes the next window's end: one window_ns later while anything is staged or in flight,
- * else the earliest pending deadline + 1 (idle stretches cost one window). Single-shard contexts;
- * message mode (not with TCP mode or a flood graph). */
+ * else the earliest pending deadline + 1 (idle stretches cost one window). Message mode (not with TCP
+ * mode or a flood graph). Sharded (a transport attached): setup, start and react are collective; a
+ * prober's state lives on its shard, the answer to it on its peer's, the reply's notice crosses in
+ * the exchange blocks and the window proposal is folded over every shard. */
 #define TGSIM_PROBE_REQ 0x40000000u
 #define TGSIM_PROBE_REP 0xC0000000u
 typedef struct tgsim_probe_config {
@@ -483,7 +485,9 @@ int tgsim_probe_results(tgsim_ctx* ctx, uint8_t* outcome, int64_t* t_done, size_
  * writesem round at the window's end over the room the window's arrivals and failures freed, all
  * staged on the device behind the device-side staged count. It proposes the next window's end
  * (window_ns later while anything is staged or in flight, else the next deadline + 1 or the next
- * dial's start). Single-shard contexts, message mode (not with probes, a flood graph or TCP mode).
+ * dial's start). Message mode (not with probes or a flood graph); sharded contexts (a transport
+ * attached) run the reactor collectively, each shard its own instances' dials and writes
+ * (DESIGN.md 2.14); TCP mode (acks = 1, below) needs a single-shard context.
  * Like probes, it owns each window's statuses and deliveries: staging or the next window before the
  * reaction is ESTATE. */
 #define TGSIM_STORM_SYN 0x40000000u
@@ -534,9 +538,13 @@ int tgsim_storm_end(tgsim_ctx* ctx);
  * it); attempt a + 1 is then sent at max(t_a + rto * 2^a, the time the failure is known), up to
  * max_attempts attempts (then the write fails). A route that refuses the packet (prohibit / no
  * route) fails the write at once. A segment arrives with its first intact copy; a write completes
- * when its last segment arrives. Single-shard contexts; while TCP mode is on, all traffic is TCP
- * (tgsim_enqueue is refused). Packet seq = segment id * 16 + attempt (segment ids count from 0 in
- * send order, < 2^28).
+ * when its last segment arrives. While TCP mode is on, all traffic is TCP (tgsim_enqueue is
+ * refused). Packet seq = segment id * 16 + attempt (segment ids count from 0 in send order, < 2^28).
+ * Sharded contexts (a transport attached) carry generated storm rounds (tgsim_tcp_gen_storm_round, one
+ * fanout) and react collectively: a data copy delivered on another shard is forwarded to its writer's
+ * shard after the window and settled there, its ACK leaves from the receiver's shard, and the
+ * segment ids on the wire are the single-shard run's, so a sharded run equals it;
+ * tgsim_tcp_send and connections need a single-shard context (TGSIM_ENOTSUP).
  *
  * acks = 1 adds the reverse path: every intact data copy the receiver gets is answered by an ACK
  * packet (header_bytes, seq = TGSIM_TCP_ACK_BIT | the data packet's seq) sent at max(arrival, the
@@ -546,8 +554,8 @@ int tgsim_storm_end(tgsim_ctx* ctx);
  * earlier window: attempt a + 1 leaves at max(timer, window start) (spurious retransmissions
  * included), and after max_attempts attempts the segment gives up (the write fails, TIMEOUT at the
  * timer, if it has not completed). A write's outcome is its first event in window order: a write
- * that failed stays failed. Segment ids < 2^27. Not modelled: congestion window (IW10 never binds
- * for writes below 14.5 KB), delayed ACKs, fast retransmit. */
+ * that failed stays failed. Segment ids < 2^27. The congestion window and fast retransmit are the
+ * connections' (below); not modelled: delayed ACKs, SACK. */
 #define TGSIM_TCP_ACK_BIT 0x80000000u
 typedef struct tgsim_tcp_config {
   uint32_t mss;           /* payload bytes per segment; 0 = 1448 */
