@@ -372,7 +372,8 @@ const char* tgsim_kernel_name(int kernel_class);
  * kernels that move them: [0] messages decided in the sequential queue-limit / correlation lane
  * (k_shape_seq), [1] token-bucket copies of senders with long runs (k_rest), [2] deliveries of long
  * inboxes (written by the wheel-insert launch's k_rest part), [3] deferred messages decided by the whole-sender
- * closed form (k_shape_seq_wide). *n = the count (4). */
+ * closed form (k_shape_seq_wide), [4] of [2], deliveries of long inboxes sorted whole by one workgroup in
+ * LDS (experiment builds with -DTGSIM_WHOLE_SORT only; 0 in the product). *n = the count (5). */
 int tgsim_kernel_counters(tgsim_ctx* ctx, uint64_t* out, size_t cap, size_t* n);
 /* Test hook: the nth host allocation point from now (tgsim_add_rules, tgsim_flood_set_graph) throws
  * std::bad_alloc inside the library; the entry point returns TGSIM_ENOMEM and the context stays

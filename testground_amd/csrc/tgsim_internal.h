@@ -130,13 +130,14 @@ struct DevScalars {
   unsigned long long st[13];
   // cumulative implementation counters (tgsim_kernel_counters; bench.py attributes SURVEY.md 8(d)
   // bytes to the kernels that move them): KC_*
-  unsigned long long kc[4];
+  unsigned long long kc[5];
 };
 enum { KC_DEFERRED = 0,   // messages decided in the sequential lane (k_shape_seq)
        KC_LONG_TB = 1,    // token-bucket copies of senders with long runs (k_rest<TB>)
        KC_LONG_EMIT = 2,  // deliveries of long inboxes, written by k_rest<Emit> (the wheel-insert launch)
        KC_WIDE = 3,       // deferred messages decided by k_shape_seq_wide (the rest: k_shape_seq)
-       KC_COUNT = 4 };
+       KC_WHOLE = 4,      // of KC_LONG_EMIT: inboxes sorted whole by one workgroup (whole_sort, -DTGSIM_WHOLE_SORT)
+       KC_COUNT = 5 };
 enum { ST_MSGS = 0, ST_COPIES, ST_LOST, ST_DROPPED, ST_REJECTED, ST_UNREACH, ST_EXTERNAL, ST_DESTDOWN,
        ST_LOCAL, ST_DELIVERED, ST_TB_ITEMS, ST_EXTRACTED, ST_INSERTED };
 constexpr int ST_OVERLIMIT = 13;  // a row counter only ([kNSub][16] rows; ST_DELIVERED.. live in DevScalars::st)

@@ -780,27 +780,31 @@ __device__ __forceinline__ void extract_body(const RegionDev* regions, const uin
   uint32_t it = 0;
   for (uint32_t base = bid * kBlock * kExtractUnroll; base < total; base += step, ++it) {  // block-uniform
     tgsim_record rec[kExtractUnroll];
+    // every record's place first, then every gather: a search loop after a gather starts with a wait
+    // for all loads in flight (s_waitcnt vmcnt(0) at its header), which made the kExtractUnroll
+    // gathers one round trip each
+    uint64_t at[kExtractUnroll];
 #pragma unroll
     for (int u = 0; u < kExtractUnroll; ++u) {
       uint32_t j = base + u * kBlock + threadIdx.x;
       j = j < total ? j : total - 1;  // clamped: the load stays valid, the push is skipped
       uint32_t lo = 0, hi = nl;
-      uint64_t at;
       if (lds) {
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
           if (s_off[mid] <= j) lo = mid; else hi = mid;
         }
-        at = s_src[lo] + (j - s_off[lo]);
+        at[u] = s_src[lo] + (j - s_off[lo]);
       } else {
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
           if (plan_off[mid] <= j) lo = mid; else hi = mid;
         }
-        at = regions[(tail + lo) % kMaxRegions].arena_off + plan_start[lo] + (j - plan_off[lo]);
+        at[u] = regions[(tail + lo) % kMaxRegions].arena_off + plan_start[lo] + (j - plan_off[lo]);
       }
-      load_rec(arena + at, rec[u]);
     }
+#pragma unroll
+    for (int u = 0; u < kExtractUnroll; ++u) load_rec(arena + at[u], rec[u]);
     int qs[kExtractUnroll];
 #pragma unroll
     for (int u = 0; u < kExtractUnroll; ++u) {
@@ -1864,18 +1868,24 @@ template <class P>
 __device__ __forceinline__ void load_span_keys(const P& p, SortSmem& s, const uint32_t* keys, const uint32_t* vals,
                                                uint32_t st, uint32_t cnt, uint32_t npad) {
   constexpr int U = 4;
+  if (cnt == 0) {
+    for (uint32_t j = threadIdx.x; j < npad; j += kBlock) pad_key(s, j);
+    return;
+  }
   for (uint32_t j0 = threadIdx.x; j0 < npad; j0 += kBlock * U) {
     uint32_t kk[U], vv[U], sg[U], k3[U];
     uint64_t k1[U], k2[U];
+    // unconditional loads (a lane past the end re-reads the last element): behind a branch per
+    // element, each gather waited for every load before it (s_waitcnt vmcnt(0)) - U serial round
+    // trips instead of one
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t j = j0 + u * kBlock;
-      kk[u] = j < cnt ? keys[st + j] : 0u;
-      vv[u] = j < cnt ? vals[st + j] : 0u;
+      const uint32_t j = min(j0 + u * kBlock, cnt - 1);
+      kk[u] = keys[st + j];
+      vv[u] = vals[st + j];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (j0 + u * kBlock < cnt) p.key(kk[u], vv[u], sg[u], k1[u], k2[u], k3[u]);
+    for (int u = 0; u < U; ++u) p.key(kk[u], vv[u], sg[u], k1[u], k2[u], k3[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = j0 + u * kBlock;
@@ -2117,6 +2127,9 @@ struct EmitPolicy {
   __device__ __forceinline__ void write(uint32_t pos, uint32_t k3) const {
     tgsim_record r;
     load_rec(D + (k3 & 0x7FFFFFFFu), r);
+    put(pos, r);
+  }
+  __device__ __forceinline__ void put(uint32_t pos, const tgsim_record& r) const {
     if ((r.meta & TGSIM_F_WHEEL) && r.src - lo < nloc) atomicSub(&pend[r.src - lo], 1u);
     o_t[pos] = r.t; o_src[pos] = r.src; o_dst[pos] = r.dst; o_seq[pos] = r.seq; o_size[pos] = r.size;
     o_flags[pos] = r.meta & ~(uint32_t)(TGSIM_F_STAGE_D | TGSIM_F_WHEEL); o_coff[pos] = r.corrupt_off;
@@ -4621,6 +4634,217 @@ __device__ __forceinline__ void count_long(const DevScalars* sc, uint32_t len) {
     atomicAdd(const_cast<unsigned long long*>(&sc->kc[KcLong<P>::v]), (unsigned long long)len);
 }
 
+// EXPERIMENT BUILD ONLY (-DTGSIM_WHOLE_SORT; the product sorts every long inbox with the tasks).
+// One workgroup sorts a whole long inbox of up to kWholeMax deliveries in LDS (VERDICT r5 item 5:
+// config 3's ~10k requests at one probed node take chunk tasks plus rank searches through global
+// memory, 34 us of its 83 busy us per window):
+//   A  the records are gathered for the block's minimum and maximum of t, src and seq. The key packs
+//      into 32 bits when the three offsets from their minimums and the clone bit fit: t | src | seq |
+//      !clone, most significant first - the order key_less gives (k1, k2, k3 >> 31);
+//   B  the records again (from this XCD's L2 now): each thread keeps its 40 packed keys in registers
+//      and counts them into kWholeBkt LDS buckets by their top bits, then the counts are scanned;
+//   C  every packed key is slotted into its bucket (LDS);
+//   D  a delivery's sorted place is its bucket's start plus its bucket mates below it; it is written
+//      there from its record.
+// Measured on config 3 (a 9,993-request inbox, tools/gpu.sh ab): the insert launch took 67-72 us
+// with it against 35 us with the tasks. One CU gathers the 10k scattered 32-B records three times
+// (A, B, D) through its own L1 - ~20k line requests per pass - where the tasks spread them over 10
+// chunk and 40 rank workgroups; batching 8 gathers per thread (whole_gather_idx: the first version's
+// per-element branches made them ~100 dependent round trips, 85 us) did not change that bound.
+// The workgroup hands the segment back to the chunk and rank tasks, before writing any delivery,
+// when the key needs more than 32 bits, a bucket holds more than kWholeMate keys (D is O(mates)), or
+// two packed keys are equal (two deliveries with one (src, seq, clone): the contract excludes it,
+// and the tasks then order them by record index as always). Its verdict goes to LargeSeg::pad bits
+// 30/31, which the segment's chunk and rank tasks wait for.
+#ifndef TGSIM_WHOLE_MAX
+#define TGSIM_WHOLE_MAX 10240
+#endif
+#ifndef TGSIM_WHOLE_BATCH
+#define TGSIM_WHOLE_BATCH 8
+#endif
+constexpr uint32_t kWholeMax = TGSIM_WHOLE_MAX;  // longest inbox one workgroup sorts
+constexpr uint32_t kWholeBits = 12, kWholeBkt = 1u << kWholeBits;
+constexpr uint32_t kWholeMate = 64;    // a fuller bucket gives the segment back to the tasks
+constexpr uint32_t kWholeBatch = TGSIM_WHOLE_BATCH;    // gathers a thread keeps in flight
+constexpr uint32_t kWholePer = kWholeMax / kBlock;  // elements per thread
+static_assert(kWholeMax % (kBlock * kWholeBatch) == 0, "whole-inbox batches tile kWholeMax");
+constexpr uint32_t kWholeDone = 1u << 30, kWholeBack = 1u << 31;  // LargeSeg::pad verdict bits
+static_assert(sizeof(SortSmem) >= sizeof(uint32_t) * (kWholeBkt + kWholeMax), "whole-inbox sort fits SortSmem");
+static_assert(kWholeBkt % kBlock == 0, "buckets are scanned kWholeBkt / kBlock per thread");
+template <class P> struct WholeSort { static constexpr bool v = false; };
+#ifdef TGSIM_WHOLE_SORT  // experiment build only: measured slower than the tasks (see above)
+template <> struct WholeSort<EmitPolicy> { static constexpr bool v = true; };
+#endif
+
+struct WholePack {  // key = (t - t0) << sh_t | (src - s0) << sh_s | (seq - q0) << 1 | !clone
+  uint64_t t0;
+  uint32_t s0, q0, sh_t, sh_s;
+  __device__ __forceinline__ uint32_t key(uint64_t t, uint32_t src, uint32_t seq, uint32_t not_clone) const {
+    return (uint32_t)(((t - t0) << sh_t) | ((uint64_t)(src - s0) << sh_s) | ((uint64_t)(seq - q0) << 1) | not_clone);
+  }
+};
+__device__ __forceinline__ uint32_t bit_width64(uint64_t x) { return x ? 64u - (uint32_t)__clzll((long long)x) : 0u; }
+
+// Returns false (nothing written) when the segment goes back to the tasks; on true
+// the deliveries are written and kWholeDone is set. Every thread calls it; the verdict is uniform.
+#ifdef TGSIM_PHASE_PROF
+// debug builds: the last whole sort - [0] = n | bits << 32, [1..6] s_memrealtime at its start and
+// after A, B (scan), C, the equal-key check and D
+__device__ uint64_t g_whole_ph[8];
+#define WHOLE_PH(i, v) do { if (threadIdx.x == 0) g_whole_ph[i] = (v); } while (0)
+#else
+#define WHOLE_PH(i, v) do {} while (0)
+#endif
+// The record indices of a thread's batch: unconditional loads (a lane past the end re-reads the
+// last element), so the batch's loads issue back to back - with a branch per element each one waited
+// for every load before it (s_waitcnt vmcnt(0)), ~80 serial round trips per pass
+__device__ __forceinline__ void whole_gather_idx(const uint32_t* v, uint32_t j0, uint32_t n, uint32_t (&x)[kWholeBatch]) {
+#pragma unroll
+  for (uint32_t q = 0; q < kWholeBatch; ++q) x[q] = v[min(j0 + q * kBlock, n - 1)];
+}
+__device__ __forceinline__ bool whole_sort(const EmitPolicy& p, SortSmem& s, const LargeSeg& L, const uint32_t* vals,
+                                           uint32_t* verdict) {
+  __shared__ uint64_t w_t[2];         // t min, max
+  __shared__ uint32_t w_u[6];         // src min, max; seq min, max; fullest bucket; equal keys seen
+  __shared__ uint32_t w_red[kBlock / 64];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(&s);  // bucket counts -> starts -> ends
+  uint32_t* slot = cnt + kWholeBkt;                 // packed keys: element order (B), bucket order (C)
+  const uint32_t n = L.len, b0 = L.start;
+  if (threadIdx.x == 0) {
+    w_t[0] = ~0ull; w_t[1] = 0;
+    w_u[0] = ~0u; w_u[1] = 0; w_u[2] = ~0u; w_u[3] = 0; w_u[4] = 0; w_u[5] = 0;
+  }
+  for (uint32_t b = threadIdx.x; b < kWholeBkt; b += kBlock) cnt[b] = 0;
+  WHOLE_PH(1, __builtin_amdgcn_s_memrealtime());
+  // A: the ranges of t, src and seq; each thread keeps kWholeBatch gathers in flight
+  uint64_t tlo = ~0ull, thi = 0;
+  uint32_t slo = ~0u, shi = 0, qlo = ~0u, qhi = 0;
+#pragma unroll 1
+  for (uint32_t j0 = threadIdx.x; j0 < n; j0 += kBlock * kWholeBatch) {
+    uint4 a[kWholeBatch];
+    uint32_t sq[kWholeBatch];
+    uint32_t x[kWholeBatch];
+    whole_gather_idx(vals + b0, j0, n, x);
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q) {
+      a[q] = reinterpret_cast<const uint4*>(p.D + x[q])[0];
+      sq[q] = p.D[x[q]].seq;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q)
+      if (j0 + q * kBlock < n) {
+        const uint64_t t = ((uint64_t)a[q].y << 32) | a[q].x;
+        tlo = min(tlo, t); thi = max(thi, t);
+        slo = min(slo, a[q].z); shi = max(shi, a[q].z);
+        qlo = min(qlo, sq[q]); qhi = max(qhi, sq[q]);
+      }
+  }
+  __syncthreads();  // the initial values above are in place
+  atomicMin(&w_t[0], tlo); atomicMax(&w_t[1], thi);
+  atomicMin(&w_u[0], slo); atomicMax(&w_u[1], shi);
+  atomicMin(&w_u[2], qlo); atomicMax(&w_u[3], qhi);
+  __syncthreads();
+  const uint32_t bt = bit_width64(w_t[1] - w_t[0]), bs = bit_width64(w_u[1] - w_u[0]),
+                 bq = bit_width64(w_u[3] - w_u[2]);
+  const uint32_t bits = bt + bs + bq + 1;
+  WHOLE_PH(0, n | (uint64_t)bits << 32);
+  WHOLE_PH(2, __builtin_amdgcn_s_memrealtime());
+  if (bits > 32) return false;  // block-uniform: from LDS after the barrier
+  WholePack k;
+  k.t0 = w_t[0]; k.s0 = w_u[0]; k.q0 = w_u[2]; k.sh_s = 1 + bq; k.sh_t = 1 + bq + bs;
+  const uint32_t shift = bits > kWholeBits ? bits - kWholeBits : 0u;
+  // B: the packed keys (the records again, from this XCD's L2 now) into LDS in element order, and
+  // their bucket counts
+#pragma unroll 1
+  for (uint32_t j0 = threadIdx.x; j0 < n; j0 += kBlock * kWholeBatch) {
+    uint4 a[kWholeBatch], b[kWholeBatch];
+    uint32_t x[kWholeBatch];
+    whole_gather_idx(vals + b0, j0, n, x);
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q) {
+      a[q] = reinterpret_cast<const uint4*>(p.D + x[q])[0];
+      b[q] = reinterpret_cast<const uint4*>(p.D + x[q])[1];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q)
+      if (j0 + q * kBlock < n) {
+        const uint64_t t = ((uint64_t)a[q].y << 32) | a[q].x;
+        const uint32_t v = k.key(t, a[q].z, b[q].x, (b[q].z & TGSIM_F_CLONE) ? 0u : 1u);
+        slot[j0 + q * kBlock] = v;
+        atomicAdd(&cnt[v >> shift], 1u);
+      }
+  }
+  __syncthreads();
+  {
+    constexpr uint32_t per = kWholeBkt / kBlock;
+    uint32_t c[per], sum = 0, big = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < per; ++q) {
+      c[q] = cnt[threadIdx.x * per + q];
+      sum += c[q];
+      big = max(big, c[q]);
+    }
+    uint32_t tot;
+    uint32_t pre = block_excl_scan(sum, w_red, tot);
+#pragma unroll
+    for (uint32_t q = 0; q < per; ++q) { cnt[threadIdx.x * per + q] = pre; pre += c[q]; }
+    if (big > kWholeMate) atomicMax(&w_u[4], big);
+  }
+  __syncthreads();
+  WHOLE_PH(3, __builtin_amdgcn_s_memrealtime());
+  if (w_u[4] > kWholeMate) return false;
+  // C: the keys into bucket order in place (all read before any is moved); cnt[b] ends as the end
+  // of bucket b (= the start of b + 1)
+  {
+    uint32_t v[kWholePer];
+#pragma unroll
+    for (uint32_t q = 0; q < kWholePer; ++q)
+      if (q * kBlock + threadIdx.x < n) v[q] = slot[q * kBlock + threadIdx.x];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kWholePer; ++q)
+      if (q * kBlock + threadIdx.x < n) slot[atomicAdd(&cnt[v[q] >> shift], 1u)] = v[q];
+  }
+  __syncthreads();
+  WHOLE_PH(4, __builtin_amdgcn_s_memrealtime());
+  for (uint32_t x = threadIdx.x; x < n; x += kBlock) {  // equal packed keys: each pair seen by its first
+    const uint32_t u = slot[x], e = cnt[u >> shift];
+    bool eq = false;
+    for (uint32_t y = x + 1; y < e; ++y) eq |= slot[y] == u;
+    if (eq) w_u[5] = 1;
+  }
+  __syncthreads();
+  WHOLE_PH(5, __builtin_amdgcn_s_memrealtime());
+  if (w_u[5]) return false;
+  if (threadIdx.x == 0) atomicOr(verdict, kWholeDone);  // the tasks need nothing of this block's
+  // D: every delivery's place (its bucket's start + its mates below it), written from its record
+#pragma unroll 1
+  for (uint32_t j0 = threadIdx.x; j0 < n; j0 += kBlock * kWholeBatch) {
+    uint4 a[kWholeBatch], b[kWholeBatch];
+    uint32_t x[kWholeBatch];
+    whole_gather_idx(vals + b0, j0, n, x);
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q) {
+      a[q] = reinterpret_cast<const uint4*>(p.D + x[q])[0];
+      b[q] = reinterpret_cast<const uint4*>(p.D + x[q])[1];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kWholeBatch; ++q) {
+      if (j0 + q * kBlock >= n) continue;
+      tgsim_record r;
+      r.t = (int64_t)(((uint64_t)a[q].y << 32) | a[q].x);
+      r.src = a[q].z; r.dst = a[q].w; r.seq = b[q].x; r.size = b[q].y; r.meta = b[q].z; r.corrupt_off = b[q].w;
+      const uint32_t u = k.key((uint64_t)r.t, r.src, r.seq, (r.meta & TGSIM_F_CLONE) ? 0u : 1u);
+      const uint32_t bk = u >> shift, e = cnt[bk];
+      uint32_t y = bk ? cnt[bk - 1] : 0u, rank = y;
+      for (; y < e; ++y) rank += slot[y] < u;
+      p.put(b0 + rank, r);
+    }
+  }
+  WHOLE_PH(6, __builtin_amdgcn_s_memrealtime());
+  return true;
+}
+
 #ifdef TGSIM_PHASE_PROF
 // debug builds: per task of the last task-parallel long-segment pass, {task | block << 32 | rank << 63,
 // claimed, ready (chunk: sorted; rank: its chunks counted), done} in s_memrealtime ticks (100 MHz)
@@ -4671,7 +4895,9 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     if (i == 0) { s_c1[nl] = ta; s_c2[nl] = tb; }
     __syncthreads();
   }
-  const uint32_t T1 = s_c1[nl], T = T1 + s_c2[nl];
+  // whole tasks (WholeSort policies) first: task i < T0 is segment i's one-workgroup sort when it is
+  // short enough, so the chunk tasks that wait for its verdict wait only on claimed tasks
+  const uint32_t T0 = WholeSort<P>::v ? nl : 0u, T1 = T0 + s_c1[nl], T = T1 + s_c2[nl];
   LargeSeg* lg = const_cast<LargeSeg*>(large);
   uint32_t* ctr = const_cast<uint32_t*>(&sc->n_chunks);  // the launch's task counter (zeroed with the lists)
   for (;;) {
@@ -4682,6 +4908,19 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     // (and the barriers inside) stays uniform control flow
     const uint32_t task = __builtin_amdgcn_readfirstlane(s_task);
     if (task >= T) break;
+    if (task < T0) {
+      const LargeSeg L = large[task];
+      if constexpr (WholeSort<P>::v) {
+        if (L.len > kWholeMax) continue;
+        if (whole_sort(p, s, L, vals, &lg[task].pad)) {
+          count_long<P>(sc, L.len);
+          if (threadIdx.x == 0) atomicAdd(const_cast<unsigned long long*>(&sc->kc[KC_WHOLE]), (unsigned long long)L.len);
+        }
+        else if (threadIdx.x == 0)  // it wrote nothing
+          atomicOr(&lg[task].pad, kWholeBack);
+      }
+      continue;
+    }
     const bool chunk = task < T1;
 #ifdef TGSIM_PHASE_PROF
     const uint64_t tp_claim = __builtin_amdgcn_s_memrealtime();
@@ -4693,7 +4932,7 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
 #define TASK_PH(ready) do {} while (0)
 #endif
     const uint32_t* tab = chunk ? s_c1 : s_c2;
-    const uint32_t r = chunk ? task : task - T1;
+    const uint32_t r = chunk ? task - T0 : task - T1;
     uint32_t i = 0, hi = nl;  // the segment: last i with tab[i] <= r
     while (hi - i > 1) {
       const uint32_t mid = (i + hi) >> 1;
@@ -4701,7 +4940,25 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     }
     const LargeSeg L = large[i];
     const uint32_t nch = s_c1[i + 1] - s_c1[i], nrk = s_c2[i + 1] - s_c2[i];
+    const bool whole = WholeSort<P>::v && L.len <= kWholeMax;  // its verdict decides who sorts it
     if (chunk) {
+      if (whole) {
+        if (threadIdx.x == 0) {
+          uint32_t spins = 0, v;
+          while (!((v = __hip_atomic_fetch_add(&lg[i].pad, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+                   (kWholeDone | kWholeBack))) {
+            __builtin_amdgcn_s_sleep(TGSIM_SPIN_SLEEP);
+            if (++spins == (1u << 24)) {
+              atomicOr(const_cast<uint32_t*>(&sc->err), ERR_TASKS);
+              v = kWholeDone;
+              break;
+            }
+          }
+          s_last = v & kWholeDone;
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(s_last)) continue;  // sorted whole
+      }
       if (r == s_c1[i]) count_long<P>(sc, L.len);  // the segment's first chunk task counts it
       large_chunk_sort(p, s, L, (r - s_c1[i]) * kParChunk, keys, vals, K1a, K2a, K3a, kParChunk);
 #ifdef TGSIM_PHASE_PROF
@@ -4715,16 +4972,19 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
     if (threadIdx.x == 0) {
       // the count is read with an atomic read-modify-write: a plain (even atomic) load of coarse-
       // grained memory can keep hitting this XCD's L2 copy of the line while another XCD counts
-      uint32_t spins = 0;
-      while ((__hip_atomic_fetch_add(&lg[i].pad, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & 0xFFFFu) < nch) {
+      uint32_t spins = 0, v;
+      while (((v = __hip_atomic_fetch_add(&lg[i].pad, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) & 0xFFFFu) < nch &&
+             !(whole && (v & kWholeDone))) {
         __builtin_amdgcn_s_sleep(TGSIM_SPIN_SLEEP);
         if (++spins == (1u << 24)) {  // a bound, never expected: report instead of hanging the device
           atomicOr(const_cast<uint32_t*>(&sc->err), ERR_TASKS);
           break;
         }
       }
+      if (whole) s_last = v & kWholeDone;
     }
     block_acquire_after_poll();  // the counted chunks' keys, written by other workgroups
+    if (whole && __builtin_amdgcn_readfirstlane(s_last)) continue;  // sorted whole
 #ifdef TGSIM_PHASE_PROF
     const uint64_t tp_ready = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -5635,6 +5895,10 @@ extern "C" int tgsim_debug_task_phases(uint64_t* out) {
   const int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_task_ph), sizeof(tgsim::g_task_ph));
   if (rc) return rc;
   return (int)hipMemcpyFromSymbol(out + 4 * 4096, HIP_SYMBOL(tgsim::g_chunk_ph), sizeof(tgsim::g_chunk_ph));
+}
+// ... and of the last whole-inbox sort (whole_sort)
+extern "C" int tgsim_debug_whole_phases(uint64_t* out) {  // [8]
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tgsim::g_whole_ph), sizeof(tgsim::g_whole_ph));
 }
 // ... and of the last k_shape_seq launch (per block: its last sender)
 extern "C" int tgsim_debug_seq_phases(uint64_t* out) {

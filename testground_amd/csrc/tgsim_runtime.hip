@@ -3447,7 +3447,7 @@ namespace {
 
 // "TTGSNP" + a two-digit layout version: bump it whenever snap_regions changes (round 5
 // changed the pend layout under version 01, so an older image was refused only by its byte total)
-constexpr uint64_t kSnapMagic = 0x3230504E53475454ull;  // "TTGSNP02": pend at one line per sender (nloc <= 16384)
+constexpr uint64_t kSnapMagic = 0x3330504E53475454ull;  // "TTGSNP03": 02 + a fifth implementation counter
 constexpr uint64_t kSnapMagicMask = 0x0000FFFFFFFFFFFFull;  // "TTGSNP" without the version
 
 struct SnapHeader {

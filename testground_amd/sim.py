@@ -372,7 +372,7 @@ class Simulator:
         self._check(self.lib.profile_read(self._ctx, _ptr(ms), _ptr(cnt), k, C.byref(n)))
         return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(self.kernel_names())}
 
-    KERNEL_COUNTERS = ("deferred", "long_tb", "long_emit", "wide")
+    KERNEL_COUNTERS = ("deferred", "long_tb", "long_emit", "wide", "long_whole")
 
     def kernel_counters(self) -> dict[str, int]:
         """Cumulative implementation counters (tgsim_kernel_counters; HIP library only)."""

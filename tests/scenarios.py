@@ -197,6 +197,58 @@ def run_many_large(binding, seed: int, n_inst: int = 64, n: int = 40_000):
     return out
 
 
+def run_whole_inbox(binding, seed: int, n_inst: int = 4000, counters=None):
+    """Long inboxes of up to 10240 deliveries are sorted by one workgroup in LDS when their keys
+    pack into 32 bits (whole_sort); the others go back to the chunk and rank tasks.
+    Window 0: two ~5k inboxes whose deliveries share one arrival time (duplicates: clone ties) next
+    to a 12k inbox (tasks); window 1: arrivals spread over 1 us (packed key of ~25 bits); window 2:
+    90 % of arrivals at one instant, the rest over 60 us (a bucket over its mate bound: tasks);
+    window 3: arrivals over 20 ms (key wider than 32 bits: tasks). counters (HIP): the kernel
+    counters after each window."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, max_msgs_per_window=1 << 16), binding=binding)
+    for g in range(n_inst):
+        sim.set_shape(g, make_shape(latency_ns=MS, duplicate=30.0))
+    snd = np.arange(3, n_inst, dtype=np.int64)
+    out = []
+    t0 = 0
+    sent = np.zeros(n_inst, np.int64)
+
+    def window(src, dst, t, span):
+        nonlocal t0
+        # per-sender sequence numbers (one (src, seq) per message): narrow seq ranges per inbox
+        order = np.argsort(src, kind="stable")
+        s_sorted = src[order]
+        first = np.r_[0, np.flatnonzero(np.diff(s_sorted)) + 1]
+        occ = np.empty(len(src), np.int64)
+        occ[order] = np.arange(len(src)) - np.repeat(first, np.diff(np.r_[first, len(src)]))
+        seq = sent[src] + occ
+        np.add.at(sent, src, 1)
+        sim.enqueue(src, dst, seq, rng.choice([64, 1500], len(src)), t)
+        t0 += span
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if counters is not None:
+            counters.append(sim.kernel_counters())
+
+    # the window's sends: every sender to 0 and 1; 12k to 2 (three per sender)
+    src = np.concatenate([snd, snd, np.repeat(snd, 3)])
+    dst = np.concatenate([np.zeros_like(snd), np.ones_like(snd), np.full(3 * len(snd), 2)])
+    window(src, dst, np.full(len(src), t0), 5 * MS)
+    src = rng.permutation(np.concatenate([snd, snd[::2]]))
+    window(src, np.zeros_like(src), t0 + rng.integers(0, 1000, len(src)), 5 * MS)
+    src = rng.permutation(snd)
+    t = np.where(rng.random(len(src)) < 0.9, t0, t0 + rng.integers(0, 60_000, len(src)))
+    window(src, np.ones_like(src), t, 5 * MS)
+    window(src, np.zeros_like(src), t0 + rng.integers(0, 20 * MS, len(src)), 25 * MS)
+    t0 += 100 * MS
+    sim.advance(t0)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
               window_ns: int = 4 * MS, restart=None):
     """Senders whose bursts overrun netem's 1000-packet queue under every kind of

@@ -42,6 +42,24 @@ def test_many_large_segments(hip, oracle):
     assert max(np.diff(x["inbox"]).max() for x in a[:3]) > 8192
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_whole_inbox_sort(hip, oracle, seed):
+    """Several long inboxes in one window - arrival ties with clone ties, arrivals over 1 us, a
+    clustered one, arrivals over 20 ms, one of 15k - through k_rest's tasks. In the experiment build
+    (-DTGSIM_WHOLE_SORT, loaded with TGSIM_LIB) the narrow ones are sorted by one workgroup in LDS
+    instead (whole_sort) and the others handed back to the tasks: same outputs."""
+    kc = []
+    a = S.run_whole_inbox(hip, seed, counters=kc)
+    S.assert_same(a, S.run_whole_inbox(oracle, seed))
+    whole = np.diff([0] + [k["long_whole"] for k in kc])
+    emit = np.diff([0] + [k["long_emit"] for k in kc])
+    assert emit[0] > 25000 and emit[1] > 7000 and emit[2] > 3000 and emit[3] > 3000
+    if whole.any():  # the experiment build
+        assert whole[0] > 7000 and emit[0] > whole[0] + 12000   # two ~5k inboxes whole, the 15k one by tasks
+        assert whole[1] == emit[1]                              # spread over 1 us: whole
+        assert whole[2] == 0 and whole[3] == 0                  # clustered / wide keys: handed back
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_queue_limit_bursts(hip, oracle, seed):
     """netem's 1000-packet queue under every shape kind, across windows."""
