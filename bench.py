@@ -285,6 +285,9 @@ def parse():
                    help="publications per wave (flood; distinct publishers; SURVEY's literal 1%% of 1M "
                         "instances = 10000 floods per wave does not fit in memory: DESIGN.md 5.4)")
     p.add_argument("--window-ms", type=float, default=10.0, help="window length (flood)")
+    p.add_argument("--flood-records-per-pub", type=int, default=1 << 25,
+                   help="flood: max_records per publication of a wave (the wheel arena is twice it; "
+                        "heavier waves need more than the default's headroom: tools/flood_load.sh)")
     p.add_argument("--no-beside", action="store_true",
                    help="storm: skip config 5 (the 1M flood, same GPU count) reported beside the headline")
     a = p.parse_args()
@@ -680,7 +683,7 @@ def flood_config(args, shard=0, n_shards=1, device=0):
     from testground_amd.sim import SimConfig
     return SimConfig(n_instances=args.flood_instances, seed=args.seed, shard_id=shard, n_shards=n_shards,
                      device=device, data_prefix_len=11, max_msgs_per_window=(1 << 23) * args.pubs_per_wave,
-                     max_records=(1 << 25) * args.pubs_per_wave,
+                     max_records=args.flood_records_per_pub * args.pubs_per_wave,
                      exchange_cap=exchange_cap(3 << 20, n_shards))
 
 

@@ -1367,6 +1367,14 @@ __device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t
 // Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
 // medium (medium_above < len <= kTile) / large (len > kTile) segment lists.
 constexpr uint32_t kNoMedium = 0xFFFFFFFFu;
+// medium_above = kMediumSpans: the keys of at most kTile items go to k_rest as spans, not one by one:
+// the keys starting in one kTile stretch of the bucket (up to a long key) are one medium entry,
+// g | (keys - 1) << kSpanKeyShift, sorted by one block in LDS (<= kSpan items, span_sort handles
+// several segments). An overflowing fused bucket listed every key alone: a flood of two
+// publications per wave put ~10^6 keys of 2-30 items through k_rest one block each, 8 ms a window.
+constexpr uint32_t kMediumSpans = 0xFFFFFFFEu;
+constexpr uint32_t kSpanKeyShift = 21;  // keys < 2^21 (nloc <= 2^20); <= 2^11 keys per span
+constexpr uint32_t kSpanKeyMask = (1u << kSpanKeyShift) - 1u;
 __device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const BktHead& h, uint32_t* off, uint32_t* off2,
                                                    uint32_t medium_above, uint32_t* medium, LargeSeg* large,
                                                    DevScalars* sc);
@@ -1399,9 +1407,10 @@ __device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const Bk
                                                    uint32_t medium_above, uint32_t* medium, LargeSeg* large,
                                                    DevScalars* sc) {
   const uint32_t tid = threadIdx.x;
+  const auto len_of = [&](uint32_t i) { return (i + 1 < h.nk ? cnt[i + 1] : h.nb) - cnt[i]; };
   for (uint32_t i = tid; i < h.nk; i += kBlock) {
     const uint32_t a = cnt[i];
-    const uint32_t len = (i + 1 < h.nk ? cnt[i + 1] : h.nb) - a;
+    const uint32_t len = len_of(i);
     const uint32_t k = h.k0 + i, run = h.start + a;
     off[k] = run;
     if (off2) off2[k] = run;
@@ -1411,6 +1420,15 @@ __device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const Bk
       L.seg = k; L.start = run; L.len = len; L.pad = 0;
       large[li] = L;
       atomicMax(&sc->max_large, len);
+    } else if (medium_above == kMediumSpans) {
+      // the head of a span: the first key of its stretch, or the first after a long key
+      const uint32_t st = a / (uint32_t)kTile;
+      if (i == 0 || cnt[i - 1] / (uint32_t)kTile != st || len_of(i - 1) > (uint32_t)kTile) {
+        uint32_t e = i + 1;
+        while (e < h.nk && cnt[e] / (uint32_t)kTile == st && len_of(e) <= (uint32_t)kTile) ++e;
+        const uint32_t items = (e < h.nk ? cnt[e] : h.nb) - a;  // <= kTile + kTile - 1
+        if (items) medium[atomicAdd(&sc->n_medium, 1u)] = k | ((e - i - 1) << kSpanKeyShift);
+      }
     } else if (len > medium_above) {  // kNoMedium: never
       medium[atomicAdd(&sc->n_medium, 1u)] = k;
     }
@@ -2304,7 +2322,7 @@ __device__ __forceinline__ bool bkt_fused_load(const BktSrc& src, const uint32_t
     }
     __syncthreads();
     (void)bkt_scan_counts(sm.cnt, sm.part, h);
-    bkt_global_offsets(sm.cnt, h, off, off2, 0, medium, large, sc);
+    bkt_global_offsets(sm.cnt, h, off, off2, kMediumSpans, medium, large, sc);
     for (uint32_t i0 = 0; i0 < cn; i0 += kOverUnroll) {
       uint2 e[kOverUnroll];
 #pragma unroll
@@ -4863,9 +4881,10 @@ __device__ __forceinline__ void rest_body(const P& p, const uint32_t* keys, cons
   const bool par = nl > 0 && nl <= kLargeTab && sc->max_large < (1u << 24);  // launch-uniform
   for (uint32_t w = bid; w < nm + (par ? 0u : nl); w += nblocks) {
     if (w < nm) {
-      const uint32_t g = medium[w];
-      const uint32_t a = off[g], m = off[g + 1] - a;
-      load_span_keys(p, s, keys, vals, a, m, m);  // keys[a, a + m) are g
+      // one key, or a span of several (kMediumSpans): keys[a, a + m) are g .. g + nk - 1
+      const uint32_t e = medium[w], g = e & kSpanKeyMask, nk = (e >> kSpanKeyShift) + 1u;
+      const uint32_t a = off[g], m = off[g + nk] - a;
+      load_span_keys(p, s, keys, vals, a, m, m);
       __syncthreads();
       span_sort(s, m, off, a);
       p.epilogue(s, m, a, off, w);

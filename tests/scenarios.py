@@ -249,6 +249,42 @@ def run_whole_inbox(binding, seed: int, n_inst: int = 4000, counters=None):
     return out
 
 
+def run_bucket_overflow(binding, seed: int, n_inst: int = 4096, per_sender: int = 80, windows: int = 3,
+                        counters=None):
+    """More items per fused bucket than it holds (kBktCap) on both group-bys: 4096 instances (24
+    keys per bucket), every sender 80 messages a window to random receivers, every sender
+    bandwidth-limited - ~1900 items per bucket, so most buckets take the global form and their keys
+    go to k_rest in spans of several keys (kMediumSpans). counters (HIP): kernel counters per window."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, max_msgs_per_window=1 << 20, max_records=1 << 21),
+                    binding=binding)
+    for g in range(n_inst):
+        sim.set_shape(g, make_shape(latency_ns=int(rng.choice([1, 2, 3])) * MS, jitter_ns=int(rng.choice([0, 2 * MS])),
+                                    bandwidth_bps=int(rng.choice([50_000_000, 400_000_000])), duplicate=5.0,
+                                    loss=1.0))
+    out = []
+    t0 = 0
+    for w in range(windows):
+        n = n_inst * per_sender
+        src = np.repeat(np.arange(n_inst), per_sender)
+        dst = rng.integers(0, n_inst, n)
+        dst[dst == src] = (dst[dst == src] + 1) % n_inst
+        seq = np.tile(np.arange(per_sender), n_inst) + w * per_sender
+        t = t0 + rng.integers(0, 4 * MS, n)
+        sim.enqueue(src, dst, seq, rng.choice([100, 1000], n), t)
+        t0 += 4 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if counters is not None:
+            counters.append(sim.kernel_counters())
+    t0 += 50 * MS
+    sim.advance(t0)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
               window_ns: int = 4 * MS, restart=None):
     """Senders whose bursts overrun netem's 1000-packet queue under every kind of

@@ -60,6 +60,16 @@ def test_whole_inbox_sort(hip, oracle, seed):
         assert whole[2] == 0 and whole[3] == 0                  # clustered / wide keys: handed back
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_bucket_overflow_spans(hip, oracle, seed):
+    """Fused buckets over their item capacity on the token bucket and the deliveries: their keys go
+    to k_rest in spans of several keys (kMediumSpans), HIP = oracle."""
+    kc = []
+    a = S.run_bucket_overflow(hip, seed, counters=kc)
+    S.assert_same(a, S.run_bucket_overflow(oracle, seed))
+    assert kc[-1]["long_emit"] > 100_000 and kc[-1]["long_tb"] > 10_000  # the global form ran on both
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_queue_limit_bursts(hip, oracle, seed):
     """netem's 1000-packet queue under every shape kind, across windows."""
