@@ -1367,11 +1367,14 @@ __device__ __forceinline__ uint32_t bkt_count_body(const uint32_t* kin, uint32_t
 // Global form of pass 3 (after bkt_count_keys): (kout, vout) grouped by key, off[k] (+ off2),
 // medium (medium_above < len <= kTile) / large (len > kTile) segment lists.
 constexpr uint32_t kNoMedium = 0xFFFFFFFFu;
-// medium_above = kMediumSpans: the keys of at most kTile items go to k_rest as spans, not one by one:
-// the keys starting in one kTile stretch of the bucket (up to a long key) are one medium entry,
-// g | (keys - 1) << kSpanKeyShift, sorted by one block in LDS (<= kSpan items, span_sort handles
-// several segments). An overflowing fused bucket listed every key alone: a flood of two
+// medium_above = kMediumSpans: the bucket's keys go to k_rest in groups of G consecutive keys, G the
+// power of two that puts about kTile / 2 items in a group at the bucket's mean run length: a group of
+// at most kTile items is one medium entry, g | (G' - 1) << kSpanKeyShift, sorted by one block in LDS
+// (span_sort handles several segments); a fuller group lists its keys one by one (its long keys are
+// large segments as always). An overflowing fused bucket listed every key alone: a flood of two
 // publications per wave put ~10^6 keys of 2-30 items through k_rest one block each, 8 ms a window.
+// (A first form grew each span key by key up to a kTile stretch: that serial walk cost config 3's
+// probed-target bucket 1.5 us.)
 constexpr uint32_t kMediumSpans = 0xFFFFFFFEu;
 constexpr uint32_t kSpanKeyShift = 21;  // keys < 2^21 (nloc <= 2^20); <= 2^11 keys per span
 constexpr uint32_t kSpanKeyMask = (1u << kSpanKeyShift) - 1u;
@@ -1408,6 +1411,11 @@ __device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const Bk
                                                    DevScalars* sc) {
   const uint32_t tid = threadIdx.x;
   const auto len_of = [&](uint32_t i) { return (i + 1 < h.nk ? cnt[i + 1] : h.nb) - cnt[i]; };
+  uint32_t G = 1;  // keys per span group (kMediumSpans)
+  if (medium_above == kMediumSpans && h.nk) {
+    const uint32_t mean = max(h.nb / h.nk, 1u);
+    while (G < 512u && 2u * G * mean <= (uint32_t)kTile / 2u) G <<= 1;
+  }
   for (uint32_t i = tid; i < h.nk; i += kBlock) {
     const uint32_t a = cnt[i];
     const uint32_t len = len_of(i);
@@ -1420,17 +1428,19 @@ __device__ __forceinline__ void bkt_global_offsets(const uint32_t* cnt, const Bk
       L.seg = k; L.start = run; L.len = len; L.pad = 0;
       large[li] = L;
       atomicMax(&sc->max_large, len);
-    } else if (medium_above == kMediumSpans) {
-      // the head of a span: the first key of its stretch, or the first after a long key
-      const uint32_t st = a / (uint32_t)kTile;
-      if (i == 0 || cnt[i - 1] / (uint32_t)kTile != st || len_of(i - 1) > (uint32_t)kTile) {
-        uint32_t e = i + 1;
-        while (e < h.nk && cnt[e] / (uint32_t)kTile == st && len_of(e) <= (uint32_t)kTile) ++e;
-        const uint32_t items = (e < h.nk ? cnt[e] : h.nb) - a;  // <= kTile + kTile - 1
-        if (items) medium[atomicAdd(&sc->n_medium, 1u)] = k | ((e - i - 1) << kSpanKeyShift);
-      }
-    } else if (len > medium_above) {  // kNoMedium: never
+    } else if (medium_above != kMediumSpans && len > medium_above) {  // kNoMedium: never
       medium[atomicAdd(&sc->n_medium, 1u)] = k;
+    }
+    if (medium_above == kMediumSpans && (i & (G - 1u)) == 0) {  // the group's head lists it
+      const uint32_t e = min(i + G, h.nk), items = (e < h.nk ? cnt[e] : h.nb) - a;
+      if (G > 1 && items <= (uint32_t)kTile) {
+        if (items) medium[atomicAdd(&sc->n_medium, 1u)] = k | ((e - i - 1) << kSpanKeyShift);
+      } else {
+        for (uint32_t j = i; j < e; ++j) {
+          const uint32_t l = len_of(j);
+          if (l && l <= (uint32_t)kTile) medium[atomicAdd(&sc->n_medium, 1u)] = h.k0 + j;
+        }
+      }
     }
   }
   // the end of this bucket's last segment: a neighbouring bucket on the fused path writes offsets
