@@ -180,6 +180,10 @@ struct tgsim_ctx {
   size_t sub_cap = 0, sub_scan_bytes = 0;
   // flood workload (tgsim_flood_*): host copy of the local rows (publish builds its messages here)
   std::vector<uint32_t> fl_off, fl_nbr;
+  // fingerprints of the flood graph (rows, max_pubs) and of the probe setup (order, configuration):
+  // a snapshot taken with either restores only into a context set up the same way
+  uint64_t fl_hash = 0, probe_hash = 0;
+  uint32_t snap_staged = 0;  // the staged messages a snapshot image holds (sizes snap_regions)
   uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
   bool probes = false;      // tgsim_probe_setup done
   // a window ended with probes set up: tgsim_probe_react must run before anything stages messages or
@@ -198,6 +202,13 @@ static int react_owed(tgsim_ctx* c) {
   if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "probes: tgsim_probe_react after every window");
   if (c->storm_need_react) return fail(c, TGSIM_ESTATE, "storm: tgsim_storm_react after every window");
   return 0;
+}
+
+// FNV-1a over bytes, for the setup fingerprints the snapshot header carries
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+  return h;
 }
 
 // An allocation point of a host-side table (tgsim_debug_fail_alloc makes the chosen one throw, so
@@ -2051,6 +2062,9 @@ static int tgsim_flood_set_graph_body(tgsim_ctx* c, const uint32_t* off, const u
   c->fl_pub_seen.swap(pub_seen);
   if (c->fl_npubs) c->life_ok = false;  // the earlier graph's publications may still be queued
   c->fl_npubs = 0;
+  uint64_t h = fnv1a(0xCBF29CE484222325ull, c->fl_off.data(), c->fl_off.size() * 4);
+  h = fnv1a(h, c->fl_nbr.data(), c->fl_nbr.size() * 4);
+  c->fl_hash = fnv1a(h, &max_pubs, 4) | 1u;  // nonzero: a graph is set
   return TGSIM_OK;
 }
 
@@ -2183,6 +2197,10 @@ static int tgsim_probe_setup_body(tgsim_ctx* c, const uint32_t* order, uint32_t 
   p.timeout = cfg->timeout_ns;
   p.window = cfg->window_ns;
   c->probes = true;
+  uint64_t h = fnv1a(0xCBF29CE484222325ull, order, (size_t)n_order * 4);
+  h = fnv1a(h, &cfg->request_bytes, 4); h = fnv1a(h, &cfg->reply_bytes, 4);
+  h = fnv1a(h, &cfg->timeout_ns, 8); h = fnv1a(h, &cfg->window_ns, 8);
+  c->probe_hash = h | 1u;
   return TGSIM_OK;
 }
 
@@ -3440,20 +3458,22 @@ static int tgsim_tcp_conns_body(tgsim_ctx* c, uint32_t first, size_t n, uint64_t
 // opaque image - device: scalars (clock, wheel ring, counters), token buckets, queue occupancy,
 // correlation states, the timing-wheel arena with its regions and slot directories, the last
 // window's deliveries, the sync service (counts, times, chunks, the used part of the signal log and
-// of the waiter table); host: the configuration mirrors (shapes, correlations, flags, addresses,
-// rules, pending resets), the clock, the queue-limit bound. Device tables compiled from the host
+// of the waiter table), the next window's staged messages, a flood's first-receipt bits, the probers'
+// state; host: the configuration mirrors (shapes, correlations, flags, addresses, rules, pending
+// resets), the clock, the queue-limit bound and the staging counters, the flood's publication set. Device tables compiled from the host
 // mirrors are re-uploaded at the next window. Randomness needs no state (Philox is counter-based).
 namespace {
 
 // "TTGSNP" + a two-digit layout version: bump it whenever snap_regions changes (round 5
 // changed the pend layout under version 01, so an older image was refused only by its byte total)
-constexpr uint64_t kSnapMagic = 0x3330504E53475454ull;  // "TTGSNP03": 02 + a fifth implementation counter
+constexpr uint64_t kSnapMagic = 0x3430504E53475454ull;  // "TTGSNP04": 03 + staged messages, floods, probes
 constexpr uint64_t kSnapMagicMask = 0x0000FFFFFFFFFFFFull;  // "TTGSNP" without the version
 
 struct SnapHeader {
   uint64_t magic, bytes;
   uint32_t dev_scalars, N, S, shard, nloc, slots, cap_rec, cap_msgs, max_states, max_waiters;
   uint64_t max_signals, seed, cap_arena;
+  uint64_t fl_hash, probe_hash;  // the flood graph / probe setup the image needs (0: none)
 };
 
 struct SnapWriter {  // sizing pass when p == nullptr
@@ -3520,6 +3540,26 @@ std::vector<std::pair<void*, size_t>> snap_regions(tgsim_ctx* c) {
       {d.w_twait, 8ull * c->n_waiters}, {d.w_release, 8ull * c->n_waiters},
   };
 }
+// ... then the staged messages (a reactor stages the next window's between windows), the flood's
+// first-receipt bits and the probers' state
+void snap_regions_more(tgsim_ctx* c, std::vector<std::pair<void*, size_t>>& v) {
+  Dev& d = c->d;
+  const size_t k = c->snap_staged;
+  for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+           {d.m_t, 8 * k}, {d.m_src, 4 * k}, {d.m_dst, 4 * k}, {d.m_seq, 4 * k}, {d.m_size, 4 * k}})
+    v.push_back(r);
+  if (!c->fl_off.empty()) v.push_back({d.fl.seen, 4ull * d.fl.max_pubs * d.fl.wpp});
+  if (c->probes) {
+    const ProbeDev& p = d.pr;
+    const size_t nl = std::max<uint32_t>(c->nloc, 1), nn = std::max<uint32_t>(c->N, 1);
+    for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+             {p.order, 4ull * p.n_order}, {p.pos, 4 * nl}, {p.state, nl}, {p.refused, nl}, {p.replied, nl},
+             {p.t_req, 8 * nl}, {p.t_rep, 8 * nl}, {p.t_reparr, 8 * nl}, {p.t_done, 8 * nl},
+             {p.out, nl * p.n_order}, {p.sc, sizeof(ProbeScalars)},
+             {p.ans, 4 * nn}, {p.cur, 4 * nn}, {p.alist, 4 * nn}, {p.rqa, 8 * nn}})
+      v.push_back(r);
+  }
+}
 
 SnapHeader snap_header(tgsim_ctx* c) {
   SnapHeader h{};
@@ -3529,6 +3569,8 @@ SnapHeader snap_header(tgsim_ctx* c) {
   h.cap_rec = c->d.cap_rec; h.cap_msgs = c->d.cap_msgs; h.max_states = c->d.max_states;
   h.max_waiters = c->d.max_waiters; h.max_signals = c->d.max_signals; h.seed = c->cfg.seed;
   h.cap_arena = c->d.cap_arena;
+  h.fl_hash = c->fl_off.empty() ? 0 : c->fl_hash;
+  h.probe_hash = c->probes ? c->probe_hash : 0;
   return h;
 }
 
@@ -3542,13 +3584,20 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
   for (const auto& r : c->rules_h) w.vec(r);
   w.val(c->now); w.val(c->horizon); w.val(c->n_status_last); w.val(c->sig_log_used); w.val(c->n_waiters);
   w.val(c->pend_bound); w.val(c->pend_exact);
+  // staging between windows (round 6: the reactors' staged messages are captured, not refused)
+  w.val(c->snap_staged); w.val(c->n_staged); w.val(c->staged_dev);
+  w.val(c->win_m_host); w.val(c->win_m_extra); w.val(c->win_m_inbox); w.val(c->win_inbox_max); w.val(c->max_tsend_h);
+  w.vec(c->hcnt); w.vec(c->hcnt_touched);
+  w.val(c->fl_npubs); w.vec(c->fl_pub_seen); w.val(c->life_host); w.val(c->life_mult);
 }
 
 int snap_refusal(tgsim_ctx* c) {
   if (c->in_window) return fail(c, TGSIM_ESTATE, "snapshot/restore: inside a window");
-  if (c->n_staged || c->staged_dev) return fail(c, TGSIM_ESTATE, "snapshot/restore: messages are staged");
-  if (c->tcp_on || c->tp_n || !c->fl_off.empty() || c->probes || c->storm_on)
-    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics, flood graphs and probes are not captured");
+  if (c->ext.n)  // read in place by the next window: the caller's buffers are not the context's
+    return fail(c, TGSIM_ESTATE, "snapshot/restore: a device batch is staged in place (tgsim_enqueue_device)");
+  if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: probes: tgsim_probe_react first");
+  if (c->tcp_on || c->tp_n || c->storm_on)
+    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics and the storm reactor are not captured");
   return TGSIM_OK;
 }
 
@@ -3564,7 +3613,9 @@ static int tgsim_snapshot_body(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
   if (rc) return rc;
   rc = sync_and_check(c);  // commits a deferred storm batch, settles the device clock
   if (rc) return rc;
-  const auto regs = snap_regions(c);
+  c->snap_staged = c->staged_dev ? std::min<uint32_t>(c->d.h_sc->n_msgs_dev, c->d.cap_msgs) : c->n_staged;
+  auto regs = snap_regions(c);
+  snap_regions_more(c, regs);
   SnapWriter sz{nullptr};
   sz.val(SnapHeader{});
   snap_host(c, sz);
@@ -3625,18 +3676,38 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   const uint32_t n_waiters = r.val<uint32_t>();
   const uint64_t pend_bound = r.val<uint64_t>();
   const bool pend_exact = r.val<bool>();
-  if (!r.ok || sig_used > c->d.max_signals || n_waiters > c->d.max_waiters)
+  const uint32_t snap_staged = r.val<uint32_t>(), n_staged = r.val<uint32_t>();
+  const bool staged_dev = r.val<bool>();
+  const uint32_t win_m_host = r.val<uint32_t>();
+  const uint64_t win_m_extra = r.val<uint64_t>();
+  const uint32_t win_m_inbox = r.val<uint32_t>();
+  const uint64_t win_inbox_max = r.val<uint64_t>();
+  const int64_t max_tsend_h = r.val<int64_t>();
+  std::vector<uint32_t> hcnt, hcnt_touched;
+  r.vec(hcnt, c->hcnt.size()); r.vec(hcnt_touched);
+  const uint32_t fl_npubs = r.val<uint32_t>();
+  std::vector<uint8_t> fl_pub_seen;
+  r.vec(fl_pub_seen, c->fl_pub_seen.size());
+  const uint64_t life_host = r.val<uint64_t>(), life_mult = r.val<uint64_t>();
+  if (!r.ok || sig_used > c->d.max_signals || n_waiters > c->d.max_waiters || snap_staged > c->d.cap_msgs ||
+      n_staged > c->d.cap_msgs || (!staged_dev && snap_staged != n_staged))
     return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
+  for (uint32_t l : hcnt_touched)
+    if (l >= hcnt.size()) return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
   const uint64_t sig_used0 = c->sig_log_used;
   const uint32_t n_waiters0 = c->n_waiters;
-  c->sig_log_used = sig_used;  // sizes the log / waiter regions below
+  const uint32_t snap_staged0 = c->snap_staged;
+  c->sig_log_used = sig_used;  // sizes the log / waiter / staged regions below
   c->n_waiters = n_waiters;
-  const auto regs = snap_regions(c);
+  c->snap_staged = snap_staged;
+  auto regs = snap_regions(c);
+  snap_regions_more(c, regs);
   size_t need = r.at;
   for (const auto& g : regs) need += g.second;
   if (need != n) {
     c->sig_log_used = sig_used0;
     c->n_waiters = n_waiters0;
+    c->snap_staged = snap_staged0;
     return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
   }
   HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
@@ -3651,9 +3722,15 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->rules_h.swap(rules);
   c->now = now; c->horizon = horizon; c->n_status_last = n_status_last;
   c->pend_bound = pend_bound; c->pend_exact = pend_exact;
+  c->n_staged = n_staged; c->staged_dev = staged_dev;
+  c->win_m_host = win_m_host; c->win_m_extra = win_m_extra; c->win_m_inbox = win_m_inbox;
+  c->win_inbox_max = win_inbox_max; c->max_tsend_h = max_tsend_h;
+  c->hcnt.swap(hcnt); c->hcnt_touched.swap(hcnt_touched);
+  c->fl_npubs = fl_npubs; c->fl_pub_seen.swap(fl_pub_seen);
+  c->life_host = life_host; c->life_mult = life_mult;
+  c->probe_need_react = false;
   c->life_ok = false;  // the restored wheel's copies predate this context's lifetime counts
   c->now_from_device = false;
-  c->max_tsend_h = INT64_MIN;
   c->shape_dirty = c->flags_dirty = c->ip_dirty = c->rules_dirty = true;  // re-uploaded at the next window
   c->d.ever_limited = true;  // the restored wheel may hold copies of a sender limited before the snapshot
   memcpy(c->d.h_sc, r.p + r.at, sizeof(DevScalars));

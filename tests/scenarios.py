@@ -629,13 +629,14 @@ def memmove_exchange(sims):
 
 def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4, window_ns=10 * MS, size=512,
               seed=5, degree=8, shapes=None, keep=True, on_window=None, cfg_kw=None, max_windows=2000,
-              windows=None, setup=None, count=True):
+              windows=None, setup=None, count=True, restart=()):
     """Waves of publications flooding the graph; every window: advance, read the deliveries, then
     tgsim_flood_react stages the first-receipt forwards for the next window. Returns per-window
     observables (keep=True) and the totals. windows: run exactly that many windows (a sharded run
     driven through a transport, whose shards cannot see the global end condition); setup(sim)
     attaches that transport. count=False: the reaction stays asynchronous (no forward counts; give
-    `windows`)."""
+    `windows`). restart: windows after whose reaction the run is snapshotted and restored into a
+    fresh context with the same graph (checkpoint / resume)."""
     from testground_amd import workloads as W
     assert count or windows is not None
     kw = dict(max_msgs_per_window=1 << 20, max_records=1 << 22, data_prefix_len=12)
@@ -665,6 +666,15 @@ def run_flood(binding, n_inst=3000, pubs_per_wave=3, waves=2, wave_gap_windows=4
             on_window(w, d, fwd)
         if keep:
             out.append(dict(status=sim.status(), deliv=d, inbox=sim.inbox_offsets(), fwd=fwd))
+        if w in restart:
+            image = sim.snapshot()
+            cfg = sim.cfg
+            sim.close()
+            sim = Simulator(cfg, binding=binding)
+            if setup is not None:
+                setup(sim)
+            sim.flood_set_graph(off, nbr, pubs_per_wave * waves)
+            sim.restore(image)
         w += 1
     tot["windows"] = w
     out.append(dict(stats=parity_stats(sim), tot=tot))

@@ -65,10 +65,17 @@ def test_sync_resumed_matches_oracle(hip, oracle):
 def test_snapshot_refusals(hip):
     s = Simulator(SimConfig(n_instances=8, seed=1), binding=hip)
     s.set_shape(0, make_shape(latency_ns=5 * MS))
-    s.enqueue([0], [1], [0], [100], [0])
-    with pytest.raises(A.TgsimError) as e:     # staged messages: not a window boundary
+    s.advance(1 * MS)
+    s.probe_setup([0, 1], 66, 66, 60_000 * MS, 100_000)
+    s.probe_start(s.now)
+    s.advance(2 * MS)
+    with pytest.raises(A.TgsimError) as e:     # a probe reaction owed: not a window boundary
         s.snapshot()
     assert e.value.code == A.ESTATE
+    s.close()
+    s = Simulator(SimConfig(n_instances=8, seed=1), binding=hip)
+    s.set_shape(0, make_shape(latency_ns=5 * MS))
+    s.enqueue([0], [1], [0], [100], [0])
     s.advance(1 * MS)
     image = s.snapshot()
     other = Simulator(SimConfig(n_instances=9, seed=1), binding=hip)
@@ -98,3 +105,119 @@ def test_snapshot_refusals(hip):
     assert e.value.code == A.ENOTSUP
     for x in (s, other, same):
         x.close()
+
+
+def _staged_run(b, restore_at=None):
+    """Host and device-generated staging across the checkpoint: each window's messages are staged
+    (and, at restore_at, snapshotted with them staged) before the window runs."""
+    rng = np.random.default_rng(7)
+    n = 64
+    sim = Simulator(SimConfig(n_instances=n, seed=7), binding=b)
+    for g in range(n):
+        sim.set_shape(g, make_shape(latency_ns=int(rng.integers(1, 30)) * MS, jitter_ns=2 * MS, duplicate=10.0,
+                                    bandwidth_bps=int(rng.choice([0, 1_000_000]))))
+    out, t = [], 0
+    for w in range(6):
+        k = 400
+        sim.enqueue(rng.integers(0, n, k), rng.integers(0, n, k), np.arange(k) + w * k, rng.choice([100, 1500], k),
+                    t + rng.integers(0, 10 * MS, k))
+        if restore_at is not None and w in restore_at:  # the window's messages are staged
+            image = sim.snapshot()
+            cfg = sim.cfg
+            sim.close()
+            sim = Simulator(cfg, binding=b)
+            sim.restore(image)
+        t += 10 * MS
+        sim.advance(t)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    t += 200 * MS
+    sim.advance(t)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=S.parity_stats(sim)))
+    sim.close()
+    return out
+
+
+@pytest.mark.gpu
+def test_staged_resumed_matches_oracle(hip, oracle):
+    """a snapshot with the next window's messages staged (round 6: captured, no longer refused)"""
+    S.assert_same(_staged_run(hip, restore_at={1, 4}), _staged_run(oracle))
+
+
+@pytest.mark.gpu
+def test_flood_resumed_matches_oracle(hip, oracle):
+    """a flood checkpointed after its reactions (the forwards staged, publications in flight) and
+    restored into a context with the same graph; a context without it refuses the image"""
+    a = S.run_flood(hip, n_inst=1500, waves=3, restart={2, 6})
+    b = S.run_flood(oracle, n_inst=1500, waves=3)
+    S.assert_same(a[:-1], b[:-1])
+    assert a[-1]["stats"] == b[-1]["stats"] and a[-1]["tot"] == b[-1]["tot"]
+
+
+@pytest.mark.gpu
+def test_flood_image_needs_the_graph(hip):
+    from testground_amd import workloads as W
+    cfg = SimConfig(n_instances=200, seed=5)
+    s = Simulator(cfg, binding=hip)
+    off, nbr = W.random_regular_graph(200, 4, 5)
+    s.flood_set_graph(off, nbr, 4)
+    s.flood_publish([3], [0], 0, 100)
+    s.advance(10 * MS)
+    s.flood_react(100)
+    image = s.snapshot()
+    for setup in (None, (W.random_regular_graph(200, 4, 6), 4), ((off, nbr), 8)):
+        f = Simulator(cfg, binding=hip)
+        if setup:
+            f.flood_set_graph(*setup[0], setup[1])
+        with pytest.raises(A.TgsimError) as e:
+            f.restore(image)
+        assert e.value.code == A.EINVAL
+        f.close()
+    s.close()
+
+
+def _probe_run(b, restore_at=()):
+    """splitbrain-style probes (tests/test_probe.py) checkpointed between reactions"""
+    from testground_amd.network import int_to_ip
+    from testground_amd.sim import make_rule
+    rng = np.random.default_rng(3)
+    n, W = 30, 100_000
+    cfg = SimConfig(n_instances=n, seed=3, max_msgs_per_window=1 << 14, max_records=1 << 16)
+    sim = Simulator(cfg, binding=b)
+    sim.set_shapes(np.arange(n), [make_shape(latency_ns=int(rng.integers(0, 3)) * MS, loss=float(rng.choice([0.0, 5.0])))
+                                  for _ in range(n)])
+    ip = [int_to_ip(sim.get_ip(g)) + "/32" for g in range(n)]
+    for g in rng.choice(n, n // 4, replace=False):
+        sim.add_rules(int(g), [make_rule(ip[int(t)], A.FILTER_DROP) for t in rng.choice(n, 4, replace=False) if t != g])
+    order = rng.permutation(n)
+    args = (order, 66, 66, 80 * MS, W)
+    sim.probe_setup(*args)
+    sim.probe_start(0)
+    out, ne, w = [], W, 0
+    while w < 100_000:
+        sim.advance(ne)
+        st, d = sim.status(), sim.deliveries()
+        ne, act = sim.probe_react()
+        out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+        w += 1
+        if act == 0:
+            break
+        if w in restore_at:  # the next requests and replies are staged
+            image = sim.snapshot()
+            sim.close()
+            sim = Simulator(cfg, binding=b)
+            sim.probe_setup(*args)
+            sim.restore(image)
+    res, t_done = sim.probe_results()
+    stats = S.parity_stats(sim)
+    sim.close()
+    return out, res, t_done, stats
+
+
+@pytest.mark.gpu
+def test_probes_resumed_matches_oracle(hip, oracle):
+    a = _probe_run(hip, restore_at={3, 10, 40})
+    b = _probe_run(oracle)
+    assert len(a[0]) == len(b[0]) > 40
+    S.assert_same(a[0], b[0])
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
