@@ -3459,7 +3459,7 @@ static int tgsim_tcp_conns_body(tgsim_ctx* c, uint32_t first, size_t n, uint64_t
 // correlation states, the timing-wheel arena with its regions and slot directories, the last
 // window's deliveries, the sync service (counts, times, chunks, the used part of the signal log and
 // of the waiter table), the next window's staged messages, a flood's first-receipt bits, the probers'
-// state; host: the configuration mirrors (shapes, correlations, flags, addresses, rules, pending
+// state, the topic logs; host: the configuration mirrors (shapes, correlations, flags, addresses, rules, pending
 // resets), the clock, the queue-limit bound and the staging counters, the flood's publication set. Device tables compiled from the host
 // mirrors are re-uploaded at the next window. Randomness needs no state (Philox is counter-based).
 namespace {
@@ -3549,6 +3549,11 @@ void snap_regions_more(tgsim_ctx* c, std::vector<std::pair<void*, size_t>>& v) {
            {d.m_t, 8 * k}, {d.m_src, 4 * k}, {d.m_dst, 4 * k}, {d.m_seq, 4 * k}, {d.m_size, 4 * k}})
     v.push_back(r);
   if (!c->fl_off.empty()) v.push_back({d.fl.seen, 4ull * d.fl.max_pubs * d.fl.wpp});
+  if (c->tp_n)
+    for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+             {c->tp_inst, 4 * c->tp_n}, {c->tp_t, 8 * c->tp_n}, {c->tp_off, 8 * c->tp_n}, {c->tp_len, 4 * c->tp_n},
+             {c->tp_bytes, c->tp_nbytes}})
+      v.push_back(r);
   if (c->probes) {
     const ProbeDev& p = d.pr;
     const size_t nl = std::max<uint32_t>(c->nloc, 1), nn = std::max<uint32_t>(c->N, 1);
@@ -3589,6 +3594,9 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
   w.val(c->win_m_host); w.val(c->win_m_extra); w.val(c->win_m_inbox); w.val(c->win_inbox_max); w.val(c->max_tsend_h);
   w.vec(c->hcnt); w.vec(c->hcnt_touched);
   w.val(c->fl_npubs); w.vec(c->fl_pub_seen); w.val(c->life_host); w.val(c->life_mult);
+  w.val(c->tp_n); w.val(c->tp_nbytes);  // topics: the entry arenas (regions) and each topic's runs
+  w.val<uint64_t>(c->topic_runs.size());
+  for (const auto& v : c->topic_runs) w.vec(v);
 }
 
 int snap_refusal(tgsim_ctx* c) {
@@ -3596,8 +3604,8 @@ int snap_refusal(tgsim_ctx* c) {
   if (c->ext.n)  // read in place by the next window: the caller's buffers are not the context's
     return fail(c, TGSIM_ESTATE, "snapshot/restore: a device batch is staged in place (tgsim_enqueue_device)");
   if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: probes: tgsim_probe_react first");
-  if (c->tcp_on || c->tp_n || c->storm_on)
-    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode, topics and the storm reactor are not captured");
+  if (c->tcp_on || c->storm_on)
+    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode and the storm reactor are not captured");
   return TGSIM_OK;
 }
 
@@ -3689,6 +3697,13 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   std::vector<uint8_t> fl_pub_seen;
   r.vec(fl_pub_seen, c->fl_pub_seen.size());
   const uint64_t life_host = r.val<uint64_t>(), life_mult = r.val<uint64_t>();
+  const uint64_t tp_n = r.val<uint64_t>(), tp_nbytes = r.val<uint64_t>();
+  std::vector<std::vector<tgsim_ctx::TopicRun>> runs(std::min<uint64_t>(r.val<uint64_t>(), r.ok ? (uint64_t)c->d.max_states : 0));
+  for (auto& v : runs) {
+    r.vec(v);
+    for (const auto& x : v)
+      if (x.entry + x.len > tp_n) r.ok = false;
+  }
   if (!r.ok || sig_used > c->d.max_signals || n_waiters > c->d.max_waiters || snap_staged > c->d.cap_msgs ||
       n_staged > c->d.cap_msgs || (!staged_dev && snap_staged != n_staged))
     return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
@@ -3696,10 +3711,24 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
     if (l >= hcnt.size()) return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
   const uint64_t sig_used0 = c->sig_log_used;
   const uint32_t n_waiters0 = c->n_waiters;
+  if (tp_n > 0xFFFFFFFFull || tp_nbytes > (n - r.at)) return fail(c, TGSIM_EINVAL, "restore: truncated or inconsistent image");
+  // the topic arenas grow to the image's (keeping their entries: a failure below changes nothing)
+  if (tp_n > c->tp_cap) {
+    if (dgrow(c, &c->tp_inst, c->tp_n, tp_n) || dgrow(c, &c->tp_t, c->tp_n, tp_n) ||
+        dgrow(c, &c->tp_off, c->tp_n, tp_n) || dgrow(c, &c->tp_len, c->tp_n, tp_n))
+      return TGSIM_ENOMEM;
+    c->tp_cap = tp_n;
+  }
+  if (tp_nbytes > c->tp_bytes_cap) {
+    if (dgrow(c, &c->tp_bytes, c->tp_nbytes, tp_nbytes)) return TGSIM_ENOMEM;
+    c->tp_bytes_cap = tp_nbytes;
+  }
   const uint32_t snap_staged0 = c->snap_staged;
-  c->sig_log_used = sig_used;  // sizes the log / waiter / staged regions below
+  const uint64_t tp_n0 = c->tp_n, tp_nbytes0 = c->tp_nbytes;
+  c->sig_log_used = sig_used;  // sizes the log / waiter / staged / topic regions below
   c->n_waiters = n_waiters;
   c->snap_staged = snap_staged;
+  c->tp_n = tp_n; c->tp_nbytes = tp_nbytes;
   auto regs = snap_regions(c);
   snap_regions_more(c, regs);
   size_t need = r.at;
@@ -3708,6 +3737,7 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
     c->sig_log_used = sig_used0;
     c->n_waiters = n_waiters0;
     c->snap_staged = snap_staged0;
+    c->tp_n = tp_n0; c->tp_nbytes = tp_nbytes0;
     return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
   }
   HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
@@ -3728,6 +3758,8 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->hcnt.swap(hcnt); c->hcnt_touched.swap(hcnt_touched);
   c->fl_npubs = fl_npubs; c->fl_pub_seen.swap(fl_pub_seen);
   c->life_host = life_host; c->life_mult = life_mult;
+  c->topic_runs.swap(runs);
+  c->tp_index_dirty = true;
   c->probe_need_react = false;
   c->life_ok = false;  // the restored wheel's copies predate this context's lifetime counts
   c->now_from_device = false;

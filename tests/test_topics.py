@@ -42,11 +42,13 @@ def test_topics_known_answers_hip(hip):
     _known_answers(hip)
 
 
-def _random_topics(binding, seed, n_inst=500, batches=40):
+def _random_topics(binding, seed, n_inst=500, batches=40, restart=()):
     """Mixed batches over several topics (and a signal state), payloads of 0..300 bytes; every
-    position returned and every subscription (several from / until cuts) is recorded."""
+    position returned and every subscription (several from / until cuts) is recorded. restart:
+    batches after which the run is snapshotted and restored into a fresh context."""
     rng = np.random.default_rng(seed)
-    sim = Simulator(SimConfig(n_instances=n_inst, max_states=64), binding=binding)
+    cfg = SimConfig(n_instances=n_inst, max_states=64)
+    sim = Simulator(cfg, binding=binding)
     out, t = [], 0
     for b in range(batches):
         n = int(rng.integers(1, 400))
@@ -58,6 +60,11 @@ def _random_topics(binding, seed, n_inst=500, batches=40):
         t = int(tt.max())
         if b % 7 == 3:
             out.append(sim.signal(np.full(5, 7), rng.integers(0, n_inst, 5), np.full(5, t)))
+        if b in restart:
+            image = sim.snapshot()
+            sim.close()
+            sim = Simulator(cfg, binding=binding)
+            sim.restore(image)
     for topic in range(7):
         for frm in (1, 2, 50, 10_000):
             for until in (t // 3, t, (1 << 63) - 1):
@@ -89,6 +96,13 @@ def test_random_topics_properties_oracle(oracle):
 @pytest.mark.parametrize("seed", [1, 2])
 def test_random_topics_hip_matches_oracle(hip, oracle, seed):
     _same(_random_topics(hip, seed), _random_topics(oracle, seed))
+
+
+@pytest.mark.gpu
+def test_random_topics_resumed_matches_oracle(hip, oracle):
+    """topic arenas and runs through tgsim_snapshot / tgsim_restore (a fresh context's arenas grow
+    to the image's)"""
+    _same(_random_topics(hip, 3, restart={0, 11, 25}), _random_topics(oracle, 3))
 
 
 def _publish_random(sim, rng, n_inst, batches):
