@@ -492,8 +492,10 @@ def main():
         v = torch.tensor([delivered, b_total], dtype=torch.int64)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         delivered, b_total = int(v[0].item()), int(v[1].item())
-    roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, "storm", world, b_total,
-                    elapsed)
+    # (TCP lines: the PMC summaries are the message storm's, so their traffic is looked up under
+    # their own workload name, which no committed summary carries: null)
+    wl = ("tcp_acks" if args.tcp_acks else "tcp") if args.tcp else "storm"
+    roof = roofline(dominant, delta, kern_ms, kern_n, sim.hi - sim.lo, args.steps, wl, world, b_total, elapsed)
     roof["kernels"] = kernel_fracs(warm_kernels, delta, sim.hi - sim.lo, args.steps, probe)
     coll = collective_stats(sim, dist, world, base_all, args.steps, transport)
     if coll:
@@ -517,7 +519,8 @@ def main():
                 "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                 "scaling": "strong", "parallelism": f"shard{world}{transport}",
                 "packets_delivered_per_s": delivered / elapsed, "tcp_in_timed_steps": dt,
-                "collectives": coll, "dtype": "int64", "data": "synthetic", "kernels_probe": warm_kernels}),
+                "collectives": coll, "dtype": "int64", "data": "synthetic", "roofline": roof,
+                "cpu_baseline": None, "kernels_probe": warm_kernels}),
                 flush=True)
         sim.close()
         if world > 1:
