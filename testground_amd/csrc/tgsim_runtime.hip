@@ -182,7 +182,7 @@ struct tgsim_ctx {
   std::vector<uint32_t> fl_off, fl_nbr;
   // fingerprints of the flood graph (rows, max_pubs) and of the probe setup (order, configuration):
   // a snapshot taken with either restores only into a context set up the same way
-  uint64_t fl_hash = 0, probe_hash = 0;
+  uint64_t fl_hash = 0, probe_hash = 0, storm_hash = 0;
   uint32_t snap_staged = 0;  // the staged messages a snapshot image holds (sizes snap_regions)
   uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
   bool probes = false;      // tgsim_probe_setup done
@@ -2445,6 +2445,9 @@ static int tgsim_storm_setup_body(tgsim_ctx* c, const uint32_t* dst, const int64
   }
   c->storm_on = true;
   c->storm_need_react = false;
+  uint64_t h = fnv1a(0xCBF29CE484222325ull, dst, n_conn * 4);
+  h = fnv1a(h, t_ready, n_conn * 8);
+  c->storm_hash = fnv1a(h, cfg, sizeof(*cfg)) | 1u;
   return TGSIM_OK;
 }
 
@@ -3473,7 +3476,7 @@ struct SnapHeader {
   uint64_t magic, bytes;
   uint32_t dev_scalars, N, S, shard, nloc, slots, cap_rec, cap_msgs, max_states, max_waiters;
   uint64_t max_signals, seed, cap_arena;
-  uint64_t fl_hash, probe_hash;  // the flood graph / probe setup the image needs (0: none)
+  uint64_t fl_hash, probe_hash, storm_hash;  // the flood graph / probe / storm setup the image needs (0: none)
 };
 
 struct SnapWriter {  // sizing pass when p == nullptr
@@ -3549,6 +3552,19 @@ void snap_regions_more(tgsim_ctx* c, std::vector<std::pair<void*, size_t>>& v) {
            {d.m_t, 8 * k}, {d.m_src, 4 * k}, {d.m_dst, 4 * k}, {d.m_seq, 4 * k}, {d.m_size, 4 * k}})
     v.push_back(r);
   if (!c->fl_off.empty()) v.push_back({d.fl.seen, 4ull * d.fl.max_pubs * d.fl.wpp});
+  if (c->storm_on) {
+    const StormDev& m = d.sm;
+    const size_t nc = std::max<uint32_t>(m.n_conn, 1), nl = std::max<uint32_t>(c->nloc, 1);
+    const size_t claim_words = std::max<uint64_t>(((uint64_t)m.n_conn * m.nchunks + 31) / 32, 1);
+    for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+             {m.dst, 4 * nc}, {m.t_ready, 8 * nc}, {m.state, nc}, {m.flags, nc}, {m.res, nc}, {m.slot, 4 * nc},
+             {m.t_start, 8 * nc}, {m.t_synarr, 8 * nc}, {m.t_ackarr, 8 * nc}, {m.t_done, 8 * nc}, {m.t_rep, 8 * nc},
+             {m.emit, 4 * nc}, {m.rem, 4 * nc}, {m.infl, 4 * nc}, {m.order, 4 * nc}, {m.ring, 4 * nc},
+             {m.claim, 4 * claim_words}, {m.dq, 4 * nl}, {m.qh, 4 * nl}, {m.ql, 4 * nl}, {m.nh, 4 * nl},
+             {m.slot_t, 8 * nl * m.C}, {m.hold, 4 * nl * m.Hc}, {m.failed, nl}, {m.t_last, 8 * nl},
+             {m.sc, sizeof(StormScalars)}, {m.ans, 4 * nc}, {m.alist, 4 * nc}})
+      v.push_back(r);
+  }
   if (c->tp_n)
     for (auto r : std::initializer_list<std::pair<void*, size_t>>{
              {c->tp_inst, 4 * c->tp_n}, {c->tp_t, 8 * c->tp_n}, {c->tp_off, 8 * c->tp_n}, {c->tp_len, 4 * c->tp_n},
@@ -3576,6 +3592,7 @@ SnapHeader snap_header(tgsim_ctx* c) {
   h.cap_arena = c->d.cap_arena;
   h.fl_hash = c->fl_off.empty() ? 0 : c->fl_hash;
   h.probe_hash = c->probes ? c->probe_hash : 0;
+  h.storm_hash = c->storm_on ? c->storm_hash : 0;
   return h;
 }
 
@@ -3594,6 +3611,7 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
   w.val(c->win_m_host); w.val(c->win_m_extra); w.val(c->win_m_inbox); w.val(c->win_inbox_max); w.val(c->max_tsend_h);
   w.vec(c->hcnt); w.vec(c->hcnt_touched);
   w.val(c->fl_npubs); w.vec(c->fl_pub_seen); w.val(c->life_host); w.val(c->life_mult);
+  w.val(c->d.sm.phase);  // the storm reactor's phase (dials / writes; its tables are regions)
   w.val(c->tp_n); w.val(c->tp_nbytes);  // topics: the entry arenas (regions) and each topic's runs
   w.val<uint64_t>(c->topic_runs.size());
   for (const auto& v : c->topic_runs) w.vec(v);
@@ -3604,8 +3622,8 @@ int snap_refusal(tgsim_ctx* c) {
   if (c->ext.n)  // read in place by the next window: the caller's buffers are not the context's
     return fail(c, TGSIM_ESTATE, "snapshot/restore: a device batch is staged in place (tgsim_enqueue_device)");
   if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: probes: tgsim_probe_react first");
-  if (c->tcp_on || c->storm_on)
-    return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode and the storm reactor are not captured");
+  if (c->storm_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: storm: tgsim_storm_react first");
+  if (c->tcp_on) return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode is not captured");
   return TGSIM_OK;
 }
 
@@ -3697,6 +3715,7 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   std::vector<uint8_t> fl_pub_seen;
   r.vec(fl_pub_seen, c->fl_pub_seen.size());
   const uint64_t life_host = r.val<uint64_t>(), life_mult = r.val<uint64_t>();
+  const uint32_t storm_phase = r.val<uint32_t>();
   const uint64_t tp_n = r.val<uint64_t>(), tp_nbytes = r.val<uint64_t>();
   std::vector<std::vector<tgsim_ctx::TopicRun>> runs(std::min<uint64_t>(r.val<uint64_t>(), r.ok ? (uint64_t)c->d.max_states : 0));
   for (auto& v : runs) {
@@ -3760,6 +3779,8 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->life_host = life_host; c->life_mult = life_mult;
   c->topic_runs.swap(runs);
   c->tp_index_dirty = true;
+  if (c->storm_on) c->d.sm.phase = storm_phase;
+  c->storm_need_react = false;
   c->probe_need_react = false;
   c->life_ok = false;  // the restored wheel's copies predate this context's lifetime counts
   c->now_from_device = false;

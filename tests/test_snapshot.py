@@ -221,3 +221,63 @@ def test_probes_resumed_matches_oracle(hip, oracle):
     assert len(a[0]) == len(b[0]) > 40
     S.assert_same(a[0], b[0])
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+
+
+def _storm_reactor_run(b, seed, restore_at=()):
+    """the storm plan reactor (dial semaphore, DialTimeout, writesem, send buffers) checkpointed
+    between reactions in both phases; a restoring context repeats tgsim_storm_setup first"""
+    rng = np.random.default_rng(seed)
+    n = 40
+    cfg = SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17)
+    kw = [dict(latency_ns=int(rng.integers(0, 4)) * MS, jitter_ns=int(rng.integers(0, 3)) * MS // 2,
+               loss=float(rng.choice([0.0, 0.0, 3.0])), duplicate=float(rng.choice([0.0, 5.0])),
+               bandwidth_bps=int(rng.choice([0, 0, 50_000_000]))) for _ in range(n)]
+    shapes = [make_shape(**k) for k in kw]
+    lossless = [make_shape(**{**k, "loss": 0.0}) for k in kw]  # every dial succeeds; the writes lose chunks
+    O = 3
+    src = np.repeat(np.arange(n), O)
+    dst = (src + rng.integers(1, n, len(src))) % n
+    t_ready = rng.integers(0, 40, len(src)) * MS // 3
+    args = dict(outgoing=O, concurrent=2, data_bytes=5 * 1500 + 4096, msg_window=2, dial_timeout_ns=60 * MS,
+                window_ns=MS)
+    sim = Simulator(cfg, binding=b)
+    sim.set_shapes(np.arange(n), lossless)
+    sim.storm_setup(dst, t_ready, **args)
+    sim.storm_start()
+    out, w = [], 0
+    for phase in ("dials", "writes"):
+        if phase == "writes":
+            sim.set_shapes(np.arange(n), shapes)
+            sim.storm_write_start(sim.now)
+        ne = sim.now + MS
+        while True:
+            sim.advance(ne)
+            st, d = sim.status(), sim.deliveries()
+            ne, act = sim.storm_react()
+            out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+            w += 1
+            if act == 0:
+                break
+            if w in restore_at:
+                image = sim.snapshot()
+                sim.close()
+                sim = Simulator(cfg, binding=b)
+                sim.storm_setup(dst, t_ready, **args)
+                sim.restore(image)
+    res, t_done = sim.storm_dials()
+    failed, t_last, tot = sim.storm_results()
+    stats = S.parity_stats(sim)
+    sim.storm_end()
+    sim.close()
+    return out, res, t_done, failed, t_last, tot, stats
+
+
+@pytest.mark.gpu
+def test_storm_reactor_resumed_matches_oracle(hip, oracle):
+    a = _storm_reactor_run(hip, 2, restore_at={2, 5, 9, 14, 20})
+    b = _storm_reactor_run(oracle, 2)
+    assert len(a[0]) == len(b[0]) > 20
+    S.assert_same(a[0], b[0])
+    for x, y in zip(a[1:5], b[1:5]):
+        assert np.array_equal(x, y)
+    assert a[5] == b[5] and a[6] == b[6]
