@@ -422,11 +422,12 @@ int tgsim_flood_react(tgsim_ctx* ctx, uint32_t size, size_t* n_forwarded);
  * every shard and sets the transport of the restored contexts again. The staged messages of the
  * next window are part of the image (host or device enqueues, a flood reaction's forwards, the probes'
  * requests), and so are the topic logs, a flood's first-receipt state, the probers' state and the
- * storm reactor's: the restoring context must have the same flood graph (tgsim_flood_set_graph, same
- * max_pubs), probe setup (tgsim_probe_setup, same order and configuration) or storm setup
- * (tgsim_storm_setup, same arguments) before tgsim_restore, else EINVAL. Both calls need a window
- * boundary (ESTATE: inside a window, a probe or storm reaction owed, or a tgsim_enqueue_device batch
- * staged in place) and are ENOTSUP in TCP mode. A malformed
+ * storm reactor's, and in TCP mode the writes, segments, retransmission timers, ACK clock and connections:
+ * the restoring context must have the same flood graph (tgsim_flood_set_graph, same max_pubs), probe
+ * setup (tgsim_probe_setup, same order and configuration), storm setup (tgsim_storm_setup, same
+ * arguments) or TCP mode (tgsim_tcp_enable, same configuration; tgsim_tcp_connect, same pairs) before
+ * tgsim_restore, else EINVAL. Both calls need a window boundary (ESTATE: inside a window, a probe,
+ * storm or TCP reaction owed, or a tgsim_enqueue_device batch staged in place). A malformed
  * or foreign image is EINVAL and leaves the context unchanged. */
 int tgsim_snapshot(tgsim_ctx* ctx, void* buf, size_t cap, size_t* n);
 int tgsim_restore(tgsim_ctx* ctx, const void* buf, size_t n);

@@ -182,8 +182,9 @@ struct tgsim_ctx {
   std::vector<uint32_t> fl_off, fl_nbr;
   // fingerprints of the flood graph (rows, max_pubs) and of the probe setup (order, configuration):
   // a snapshot taken with either restores only into a context set up the same way
-  uint64_t fl_hash = 0, probe_hash = 0, storm_hash = 0;
+  uint64_t fl_hash = 0, probe_hash = 0, storm_hash = 0, tcp_hash = 0;
   uint32_t snap_staged = 0;  // the staged messages a snapshot image holds (sizes snap_regions)
+  uint32_t snap_acks = 0;    // TCP acks mode: the last reaction's ACKs (ack_idx entries) it holds
   uint32_t fail_alloc = 0;  // tgsim_debug_fail_alloc: the n-th allocation point throws std::bad_alloc
   bool probes = false;      // tgsim_probe_setup done
   // a window ended with probes set up: tgsim_probe_react must run before anything stages messages or
@@ -2985,6 +2986,7 @@ static int tgsim_tcp_enable_body(tgsim_ctx* c, const tgsim_tcp_config* cfg) {
   d.xsend = c->d.xsend; d.xrecv = c->d.xrecv;
   c->tcp = t;
   c->tcp_on = true;
+  c->tcp_hash = fnv1a(0xCBF29CE484222325ull, &t, sizeof(t)) | 1u;
   return TGSIM_OK;
 }
 
@@ -3477,6 +3479,7 @@ struct SnapHeader {
   uint32_t dev_scalars, N, S, shard, nloc, slots, cap_rec, cap_msgs, max_states, max_waiters;
   uint64_t max_signals, seed, cap_arena;
   uint64_t fl_hash, probe_hash, storm_hash;  // the flood graph / probe / storm setup the image needs (0: none)
+  uint64_t tcp_hash, conn_hash;  // TCP mode's configuration and its connections (0: off)
 };
 
 struct SnapWriter {  // sizing pass when p == nullptr
@@ -3552,6 +3555,29 @@ void snap_regions_more(tgsim_ctx* c, std::vector<std::pair<void*, size_t>>& v) {
            {d.m_t, 8 * k}, {d.m_src, 4 * k}, {d.m_dst, 4 * k}, {d.m_seq, 4 * k}, {d.m_size, 4 * k}})
     v.push_back(r);
   if (!c->fl_off.empty()) v.push_back({d.fl.seen, 4ull * d.fl.max_pubs * d.fl.wpp});
+  if (c->tcp_on) {
+    const TcpDev& t = c->td;
+    const size_t W = c->tw_n, S = c->tsg_n, nc = t.n_conn;
+    for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+             {t.w_src, 4 * W}, {t.w_dst, 4 * W}, {t.w_rem, 4 * W}, {t.w_state, 4 * W}, {t.w_tarr, 8 * W},
+             {t.w_tmax, 8 * W}, {t.w_fail, 8 * W}, {t.s_w, 4 * S}, {t.s_wire, 4 * S}, {t.s_att, 4 * S},
+             {t.s_out, 4 * S}, {t.s_mark, 4 * S}, {t.s_tatt, 8 * S}, {t.s_arr, 8 * S}, {t.s_tlast, 8 * S},
+             {t.pend[0], 4 * S}, {t.pend[1], 4 * S}, {t.pend_by, 4ull * c->N}, {t.sc, sizeof(TcpScalars)}})
+      v.push_back(r);
+    if (t.acks)  // the timer ring, and the last reaction's ACKs (released at the next window start)
+      for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+               {t.s_done, S}, {t.tb, sizeof(TcpBatch) * kTcpBatches}, {t.plan_lo, 4ull * (kTcpBatches + 1)},
+               {t.plan_off, 4ull * (kTcpBatches + 1)}, {t.ack_idx, 4ull * c->snap_acks}})
+        v.push_back(r);
+    if (t.w_conn)
+      for (auto r : std::initializer_list<std::pair<void*, size_t>>{
+               {t.w_conn, 4 * W}, {t.s_next, 4 * S}, {t.s_ack1, 4 * S}, {t.s_lost, S}, {t.s_tq, S},
+               {t.c_src, 4 * nc}, {t.c_dst, 4 * nc}, {t.c_cwnd, 4 * nc}, {t.c_ssth, 4 * nc}, {t.c_cnt, 4 * nc},
+               {t.c_flight, 4 * nc}, {t.c_queued, 4 * nc}, {t.c_head, 4 * nc}, {t.c_acks, 4 * nc},
+               {t.c_broken, 4 * nc}, {t.c_acked, 8 * nc}, {t.c_tloss, 8 * nc}, {t.c_una, 4 * nc},
+               {t.c_fack, 4 * nc}, {t.c_tack, 8 * nc}, {t.c_fr, 4 * nc}})
+        v.push_back(r);
+  }
   if (c->storm_on) {
     const StormDev& m = d.sm;
     const size_t nc = std::max<uint32_t>(m.n_conn, 1), nl = std::max<uint32_t>(c->nloc, 1);
@@ -3564,6 +3590,10 @@ void snap_regions_more(tgsim_ctx* c, std::vector<std::pair<void*, size_t>>& v) {
              {m.slot_t, 8 * nl * m.C}, {m.hold, 4 * nl * m.Hc}, {m.failed, nl}, {m.t_last, 8 * nl},
              {m.sc, sizeof(StormScalars)}, {m.ans, 4 * nc}, {m.alist, 4 * nc}})
       v.push_back(r);
+    if (m.tcp) {
+      v.push_back({m.settled, 4 * nc});
+      v.push_back({m.wsegs, 4 * nc});
+    }
   }
   if (c->tp_n)
     for (auto r : std::initializer_list<std::pair<void*, size_t>>{
@@ -3593,6 +3623,12 @@ SnapHeader snap_header(tgsim_ctx* c) {
   h.fl_hash = c->fl_off.empty() ? 0 : c->fl_hash;
   h.probe_hash = c->probes ? c->probe_hash : 0;
   h.storm_hash = c->storm_on ? c->storm_hash : 0;
+  h.tcp_hash = c->tcp_on ? c->tcp_hash : 0;
+  h.conn_hash = 0;
+  if (c->tcp_on) {
+    uint64_t k = fnv1a(0xCBF29CE484222325ull, c->conn_src.data(), c->conn_src.size() * 4);
+    h.conn_hash = fnv1a(k, c->conn_dst.data(), c->conn_dst.size() * 4) ^ c->td.n_conn;
+  }
   return h;
 }
 
@@ -3612,6 +3648,11 @@ void snap_host(tgsim_ctx* c, SnapWriter& w) {
   w.vec(c->hcnt); w.vec(c->hcnt_touched);
   w.val(c->fl_npubs); w.vec(c->fl_pub_seen); w.val(c->life_host); w.val(c->life_mult);
   w.val(c->d.sm.phase);  // the storm reactor's phase (dials / writes; its tables are regions)
+  // TCP mode: the write / segment counts (they size the regions), the reaction's list parity and
+  // epoch, the timer ring's cursors, the connections' queue tails, the counters the host keeps
+  w.val(c->tw_n); w.val(c->tsg_n); w.val(c->tcp_cur); w.val(c->tcp_epoch); w.val(c->tcp_nb); w.val(c->tcp_fill);
+  w.val(c->tcp_seg_batched); w.vec(c->conn_tail); w.val(c->tstats); w.val(c->storm_conn_lo); w.val(c->storm_conn_hi);
+  w.val(c->snap_acks);
   w.val(c->tp_n); w.val(c->tp_nbytes);  // topics: the entry arenas (regions) and each topic's runs
   w.val<uint64_t>(c->topic_runs.size());
   for (const auto& v : c->topic_runs) w.vec(v);
@@ -3623,7 +3664,7 @@ int snap_refusal(tgsim_ctx* c) {
     return fail(c, TGSIM_ESTATE, "snapshot/restore: a device batch is staged in place (tgsim_enqueue_device)");
   if (c->probe_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: probes: tgsim_probe_react first");
   if (c->storm_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: storm: tgsim_storm_react first");
-  if (c->tcp_on) return fail(c, TGSIM_ENOTSUP, "snapshot/restore: TCP mode is not captured");
+  if (c->tcp_need_react) return fail(c, TGSIM_ESTATE, "snapshot/restore: TCP mode: tgsim_tcp_react first");
   return TGSIM_OK;
 }
 
@@ -3640,6 +3681,12 @@ static int tgsim_snapshot_body(tgsim_ctx* c, void* buf, size_t cap, size_t* n) {
   rc = sync_and_check(c);  // commits a deferred storm batch, settles the device clock
   if (rc) return rc;
   c->snap_staged = c->staged_dev ? std::min<uint32_t>(c->d.h_sc->n_msgs_dev, c->d.cap_msgs) : c->n_staged;
+  c->snap_acks = 0;
+  if (c->tcp_on && c->td.acks) {
+    TcpScalars ts;
+    HIPCK(c, hipMemcpy(&ts, c->td.sc, sizeof(ts), hipMemcpyDeviceToHost), "snapshot");
+    c->snap_acks = std::min<uint32_t>(ts.ack_n, (uint32_t)(kNSub * c->d.subcap));
+  }
   auto regs = snap_regions(c);
   snap_regions_more(c, regs);
   SnapWriter sz{nullptr};
@@ -3716,6 +3763,17 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   r.vec(fl_pub_seen, c->fl_pub_seen.size());
   const uint64_t life_host = r.val<uint64_t>(), life_mult = r.val<uint64_t>();
   const uint32_t storm_phase = r.val<uint32_t>();
+  const uint64_t tw_n = r.val<uint64_t>(), tsg_n = r.val<uint64_t>();
+  const uint32_t tcp_cur = r.val<uint32_t>(), tcp_epoch = r.val<uint32_t>(), tcp_nb = r.val<uint32_t>(),
+                 tcp_fill = r.val<uint32_t>();
+  const uint64_t tcp_seg_batched = r.val<uint64_t>();
+  std::vector<uint32_t> conn_tail;
+  r.vec(conn_tail, c->conn_tail.size());
+  const tgsim_tcp_stats tstats = r.val<tgsim_tcp_stats>();
+  const uint64_t storm_conn_lo = r.val<uint64_t>(), storm_conn_hi = r.val<uint64_t>();
+  const uint32_t snap_acks = r.val<uint32_t>();
+  if (snap_acks > (uint64_t)kNSub * c->d.subcap || (snap_acks && !(c->tcp_on && c->td.acks))) r.ok = false;
+  if (c->tcp_on && (tw_n > c->tcp.max_writes || tsg_n > c->tcp.max_segments)) r.ok = false;
   const uint64_t tp_n = r.val<uint64_t>(), tp_nbytes = r.val<uint64_t>();
   std::vector<std::vector<tgsim_ctx::TopicRun>> runs(std::min<uint64_t>(r.val<uint64_t>(), r.ok ? (uint64_t)c->d.max_states : 0));
   for (auto& v : runs) {
@@ -3743,7 +3801,10 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
     c->tp_bytes_cap = tp_nbytes;
   }
   const uint32_t snap_staged0 = c->snap_staged;
-  const uint64_t tp_n0 = c->tp_n, tp_nbytes0 = c->tp_nbytes;
+  const uint64_t tp_n0 = c->tp_n, tp_nbytes0 = c->tp_nbytes, tw_n0 = c->tw_n, tsg_n0 = c->tsg_n;
+  c->tw_n = tw_n; c->tsg_n = tsg_n;
+  const uint32_t snap_acks0 = c->snap_acks;
+  c->snap_acks = snap_acks;
   c->sig_log_used = sig_used;  // sizes the log / waiter / staged / topic regions below
   c->n_waiters = n_waiters;
   c->snap_staged = snap_staged;
@@ -3757,6 +3818,8 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
     c->n_waiters = n_waiters0;
     c->snap_staged = snap_staged0;
     c->tp_n = tp_n0; c->tp_nbytes = tp_nbytes0;
+    c->tw_n = tw_n0; c->tsg_n = tsg_n0;
+    c->snap_acks = snap_acks0;
     return fail(c, TGSIM_EINVAL, "restore: image size mismatch");
   }
   HIPCK(c, hipStreamSynchronize(c->d.stream), "restore");
@@ -3781,6 +3844,14 @@ static int tgsim_restore_body(tgsim_ctx* c, const void* buf, size_t n) {
   c->tp_index_dirty = true;
   if (c->storm_on) c->d.sm.phase = storm_phase;
   c->storm_need_react = false;
+  if (c->tcp_on) {
+    c->tcp_cur = tcp_cur; c->tcp_epoch = tcp_epoch; c->tcp_nb = tcp_nb; c->tcp_fill = tcp_fill;
+    c->tcp_seg_batched = tcp_seg_batched; c->conn_tail.swap(conn_tail); c->tstats = tstats;
+    c->storm_conn_lo = storm_conn_lo; c->storm_conn_hi = storm_conn_hi;
+    c->tcp_need_react = false;
+    c->tcp_snap_live[0] = c->tcp_snap_live[1] = false;
+    if (int rc2 = tcp_snapshot(c)) return rc2;  // the restored counters, for tgsim_tcp_stats
+  }
   c->probe_need_react = false;
   c->life_ok = false;  // the restored wheel's copies predate this context's lifetime counts
   c->now_from_device = false;

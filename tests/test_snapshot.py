@@ -100,9 +100,10 @@ def test_snapshot_refusals(hip):
     d = same.deliveries()
     assert d["src"].tolist() == [0] and d["t_deliver"].tolist() == [5 * MS]
     s.tcp_enable()
-    with pytest.raises(A.TgsimError) as e:
-        s.snapshot()
-    assert e.value.code == A.ENOTSUP
+    image2 = s.snapshot()                      # TCP mode is captured too: its image restores only
+    with pytest.raises(A.TgsimError) as e:     # into a context with the same TCP configuration
+        same.restore(image2)
+    assert e.value.code == A.EINVAL
     for x in (s, other, same):
         x.close()
 
@@ -281,3 +282,34 @@ def test_storm_reactor_resumed_matches_oracle(hip, oracle):
     for x, y in zip(a[1:5], b[1:5]):
         assert np.array_equal(x, y)
     assert a[5] == b[5] and a[6] == b[6]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("acks", [False, True])
+def test_tcp_random_resumed_matches_oracle(hip, oracle, acks):
+    """TCP mode across checkpoints: writes, segments, retransmission lists, the acks-mode timer ring"""
+    from tests import test_tcp as T
+    w = 120 if acks else 60
+    T._same(T.run_random(hip, 2, acks=acks, windows=w, restart={5, 17, 40}),
+            T.run_random(oracle, 2, acks=acks, windows=w))
+
+
+@pytest.mark.gpu
+def test_tcp_storm_resumed_matches_oracle(hip, oracle):
+    from tests import test_tcp as T
+    a = T.run_tcp_storm(hip, n=300, rounds=5, acks=True, restart={1, 3})
+    b = T.run_tcp_storm(oracle, n=300, rounds=5, acks=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
+
+
+@pytest.mark.gpu
+def test_tcp_connections_resumed_matches_oracle(hip, oracle):
+    """connections (Reno windows, queued writes, loss episodes) across checkpoints; the restoring
+    context opens the same connections first"""
+    from tests import test_tcp_conn as T
+    a, b = T.random_conn_run(hip, 2, restart={20, 55, 90}), T.random_conn_run(oracle, 2)
+    S.assert_same(a["deliv"], b["deliv"])
+    assert np.array_equal(a["writes"][0], b["writes"][0]) and np.array_equal(a["writes"][1], b["writes"][1])
+    for k in a["conns"]:
+        assert np.array_equal(a["conns"][k], b["conns"][k]), k
+    assert a["stats"] == b["stats"] and a["tcp"] == b["tcp"]

@@ -612,12 +612,15 @@ def test_storm_tcp_dial_timeout_hip(hip, oracle):
     assert a[2] == b[2]
 
 
-def random_tcp_run(b, seed, n=40, keep=True):
+def random_tcp_run(b, seed, n=40, keep=True, restart=()):
     """TCP storm on shaped, lossy, duplicating, corrupting links: SYN and data retransmissions, the
-    Reno window's collapses, writes blocked on the socket buffer; window by window."""
+    Reno window's collapses, writes blocked on the socket buffer; window by window. restart: window
+    counts after whose reactions the run is snapshotted and restored into a fresh context."""
     rng = np.random.default_rng(seed)
-    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17), binding=b)
-    s.tcp_enable(acks=True, rto_ns=30 * MS, max_attempts=6, max_writes=1 << 16, max_segments=1 << 18)
+    cfg = SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 15, max_records=1 << 17)
+    enable = dict(acks=True, rto_ns=30 * MS, max_attempts=6, max_writes=1 << 16, max_segments=1 << 18)
+    s = Simulator(cfg, binding=b)
+    s.tcp_enable(**enable)
     s.set_shapes(np.arange(n), [make_shape(latency_ns=int(rng.integers(1, 4)) * MS, jitter_ns=int(rng.integers(0, 2)) * MS // 2,
                                            loss=float(rng.choice([0.0, 2.0])), duplicate=float(rng.choice([0.0, 5.0])),
                                            corrupt=float(rng.choice([0.0, 1.0])),
@@ -625,15 +628,40 @@ def random_tcp_run(b, seed, n=40, keep=True):
     O = int(rng.integers(1, 4))
     src = np.repeat(np.arange(n), O)
     dst = (src + rng.integers(1, n, len(src))) % n
-    s.storm_setup(dst, rng.integers(0, 30, len(src)) * MS // 2, outgoing=O, concurrent=int(rng.integers(1, 3)),
-                  data_bytes=int(rng.integers(1, 6)) * 4096 + int(rng.integers(0, 2)) * 1000, window_ns=W)
+    t_ready = rng.integers(0, 30, len(src)) * MS // 2
+    setup = dict(outgoing=O, concurrent=int(rng.integers(1, 3)),
+                 data_bytes=int(rng.integers(1, 6)) * 4096 + int(rng.integers(0, 2)) * 1000, window_ns=W)
+    s.storm_setup(dst, t_ready, **setup)
     s.storm_start()
-    dial_obs, dial_w = drive_tcp(s, keep=keep)
+    windows = [0]
+
+    def drive(s):
+        out, ne, w = [], s.now + W, 0
+        while True:
+            s.advance(ne)
+            st, d = s.status(), s.deliveries()
+            s.tcp_react()
+            ne, act = s.storm_react()
+            if keep:
+                out.append(dict(status=np.sort(st), deliv=d, ne=ne, act=act))
+            w += 1
+            windows[0] += 1
+            if act == 0:
+                return out, w, s
+            if windows[0] in restart:
+                image = s.snapshot()
+                s.close()
+                s = Simulator(cfg, binding=b)
+                s.tcp_enable(**enable)
+                s.storm_setup(dst, t_ready, **setup)
+                s.restore(image)
+
+    dial_obs, dial_w, s = drive(s)
     res, t_done = s.storm_dials()
     out = dict(dial_obs=dial_obs, dial_w=dial_w, res=res, t_done=t_done)
     if (res == A.PROBE_OK).all():
         s.storm_write_start(s.now)
-        out["write_obs"], out["write_w"] = drive_tcp(s, keep=keep)
+        out["write_obs"], out["write_w"], s = drive(s)
         out["failed"], out["t_last"], out["totals"] = s.storm_results()
     out["tcp"] = s.tcp_stats()
     out["stats"] = S.parity_stats(s)
@@ -650,9 +678,11 @@ def test_storm_tcp_random_oracle(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_storm_tcp_random_hip_matches_oracle(hip, oracle, seed):
-    a, b = random_tcp_run(hip, seed), random_tcp_run(oracle, seed)
+@pytest.mark.parametrize("seed,restart", [(1, ()), (2, ()), (3, ()), (1, (3, 9, 20, 31))],
+                         ids=["1", "2", "3", "1-resumed"])
+def test_storm_tcp_random_hip_matches_oracle(hip, oracle, seed, restart):
+    """(1-resumed: the TCP storm reactor snapshotted and restored four times; tgsim_snapshot)"""
+    a, b = random_tcp_run(hip, seed, restart=restart), random_tcp_run(oracle, seed)
     assert a["dial_w"] == b["dial_w"]
     S.assert_same(a["dial_obs"], b["dial_obs"])
     assert np.array_equal(a["res"], b["res"]) and np.array_equal(a["t_done"], b["t_done"])

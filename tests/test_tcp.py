@@ -247,14 +247,16 @@ def test_in_order_view():
     assert list(s3) == [T.REFUSED, T.REFUSED] and list(t3) == [3, 3]   # the reset fails what follows
 
 
-def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True, acks=False):
+def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True, acks=False, restart=()):
     """Lossy, corrupting, duplicating, reordering links with jitter and rate limits; writes of 0 to
     9000 B over the first 30 windows. Per window: deliveries and the statuses as a sorted multiset;
-    at the end the write outcomes and counters."""
+    at the end the write outcomes and counters. restart: windows after whose reaction the run is
+    snapshotted and restored into a fresh context (checkpoint / resume)."""
     rng = np.random.default_rng(seed)
-    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18),
-                  binding=b)
-    s.tcp_enable(max_attempts=int(rng.integers(3, 8)), rto_ns=int(rng.integers(20, 80)) * MS, acks=acks)
+    cfg = SimConfig(n_instances=n, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 18)
+    s = Simulator(cfg, binding=b)
+    enable = dict(max_attempts=int(rng.integers(3, 8)), rto_ns=int(rng.integers(20, 80)) * MS, acks=acks)
+    s.tcp_enable(**enable)
     for g in range(n):
         s.set_shape(g, make_shape(latency_ns=int(rng.integers(1, 60)) * MS, jitter_ns=int(rng.integers(0, 5)) * MS,
                                   bandwidth_bps=int(rng.choice([0, 2_000_000, 20_000_000])),
@@ -273,6 +275,12 @@ def run_random(b, seed, n=300, windows=60, window_ns=10 * MS, wait=True, acks=Fa
         d = s.deliveries()
         s.tcp_react(wait=wait)
         out.append(dict(deliv=d, status=np.sort(st)))
+        if w in restart:
+            image = s.snapshot()
+            s.close()
+            s = Simulator(cfg, binding=b)
+            s.tcp_enable(**enable)
+            s.restore(image)
     ws, wt = s.tcp_writes()
     out.append(dict(writes=(ws, wt), stats=s.tcp_stats()))
     s.close()
@@ -384,7 +392,8 @@ def test_lossy_rpc_over_tcp_hip(hip, oracle):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 * MS, cfg_kw=None, setup=None):
+def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 * MS, cfg_kw=None, setup=None,
+                  restart=()):
     """The storm plan over TCP mode (plans/benchmarks/storm.go dials and writes 1 KiB per peer):
     tgsim_tcp_gen_storm_round generates each round as writes on the device, SignalAndWait ends
     the window, and the reaction recovers the 10 % lost segments. Drained afterwards. Sharded
@@ -396,12 +405,13 @@ def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 *
     # (retransmitted ones included) and the fired timers: with a 30 ms RTO nearly every segment is
     # retransmitted once, spuriously
     per_window = max(1 << 16, 5 * n * 8)
-    s = Simulator(SimConfig(n_instances=n, seed=seed, max_msgs_per_window=per_window,
-                            max_records=max(1 << 18, 16 * n * 8), max_states=64, data_prefix_len=12,
-                            **(cfg_kw or {})), binding=b)
+    cfg = SimConfig(n_instances=n, seed=seed, max_msgs_per_window=per_window, max_records=max(1 << 18, 16 * n * 8),
+                    max_states=64, data_prefix_len=12, **(cfg_kw or {}))
+    s = Simulator(cfg, binding=b)
     if setup is not None:
         setup(s)
-    s.tcp_enable(max_attempts=5, rto_ns=rto_ns, acks=acks, max_writes=rounds * n * 8, max_segments=rounds * n * 8)
+    enable = dict(max_attempts=5, rto_ns=rto_ns, acks=acks, max_writes=rounds * n * 8, max_segments=rounds * n * 8)
+    s.tcp_enable(**enable)
     for g in range(n):
         s.set_shape(g, make_shape(latency_ns=int(rng.integers(5, 21)) * MS, jitter_ns=2 * MS, loss=10.0,
                                   bandwidth_bps=10_000_000))
@@ -410,6 +420,14 @@ def run_tcp_storm(b, seed=4, n=400, rounds=6, wait=True, acks=False, rto_ns=30 *
         w = s.barrier(r, n, A.T_NOW)
         s.advance_to_barrier(w, 1 * MS)
         s.tcp_react(wait=wait)
+        if r in restart:
+            image = s.snapshot()
+            s.close()
+            s = Simulator(cfg, binding=b)
+            if setup is not None:
+                setup(s)
+            s.tcp_enable(**enable)
+            s.restore(image)
     for _ in range(40):
         s.advance(s.now + 20 * MS, wait=wait)
         s.tcp_react(wait=wait)

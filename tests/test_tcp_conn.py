@@ -184,7 +184,7 @@ def test_conn_hip(hip, case):
     case(hip)
 
 
-def random_conn_run(b, seed, n=16, windows=160):
+def random_conn_run(b, seed, n=16, windows=160, restart=()):
     """Connections between random pairs (some twice), lossy / duplicating / corrupting links of a
     few ms, writes of 1 B .. 40 segments arriving over the first 60 windows, a prohibit route."""
     rng = np.random.default_rng(seed)
@@ -203,7 +203,21 @@ def random_conn_run(b, seed, n=16, windows=160):
         if k:
             t = w * MS + int(rng.integers(0, MS))
             writes[t] = [(int(rng.choice(conns)), int(rng.integers(1, 40 * MSS))) for _ in range(k)]
-    out = run(s, windows * MS, writes=writes)
+    if restart:  # checkpoint / resume: after the windows ending at the given ms, a fresh context
+        cfg = s.cfg
+        out = []
+        for stop in sorted(restart) + [windows]:
+            out += run(s, stop * MS, writes=writes)
+            if stop == windows:
+                break
+            image = s.snapshot()
+            s.close()
+            s = Simulator(cfg, binding=b)
+            s.tcp_enable(acks=True)
+            s.tcp_connect(src, dst)
+            s.restore(image)
+    else:
+        out = run(s, windows * MS, writes=writes)
     st, t = s.tcp_writes()
     res = dict(deliv=[d for _, d in out], status=None, writes=(st, t), conns=s.tcp_conns(), stats=S.parity_stats(s),
                tcp=s.tcp_stats())
