@@ -270,6 +270,9 @@ struct Dev {
   // token-bucket batch A (copies of an unlimited sender carry TGSIM_F_STAGE_D from the netem pass,
   // wheel included), so the window skips the A partition, k_tb_bucket and k_rest<TB> until then
   bool ever_limited = false;
+  // single-shard contexts: this window's k_rest<TB> rides in the window end's first launch
+  // (k_rest_local_hist) instead of a launch of its own
+  bool tb_rest_owed = false;
   uint32_t* moff = nullptr;       // [segK] per local sender: its deferred messages in corr_sorted
 
   // netem queue limit: pend[l] = local sender l's records in the timing wheel

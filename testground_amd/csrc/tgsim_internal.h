@@ -113,6 +113,8 @@ struct DevScalars {
   uint32_t n_corr;                   // messages deferred by k_shape (correlated or queue-heavy senders)
   uint32_t n_hrec;                   // due wheel records of queue-heavy senders copied to the H list
   uint32_t seq_left;                 // senders k_shape_seq_wide left to k_shape_seq (0: it has nothing to do)
+  uint32_t rest_tb;                  // k_tb_bucket listed long senders for k_rest<TB> (k_rest_local_hist)
+  uint32_t rest_ticket, rest_done;   // k_rest_local_hist: role tickets claimed, rest roles finished
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits
   uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)

@@ -1095,18 +1095,20 @@ __global__ __launch_bounds__(kRadixBlocks) void k_radix_rows(BktSrc src, const u
 // one XCD's L2). The consumer of bucket b finds its items as 256 chunks and its global start as
 // sum_p poff[p][b] (every block's offsets are prefix sums of its own counts). The first block
 // also closes the queue (queue_final) and resets the segment lists.
+// bid: the partition block (blockIdx.x unless the pass shares its launch).
 __device__ __forceinline__ void bkt_local_body(const BktSrc& src, DevScalars* sc, const BktDiv& bd, uint32_t B,
-                                               uint2* kv, uint32_t* poff) {
+                                               uint2* kv, uint32_t* poff, uint32_t bid = 0xFFFFFFFFu) {
   __shared__ uint32_t h[kMaxBins + 1];
   __shared__ uint32_t red[kBlock / 64];
+  if (bid == 0xFFFFFFFFu) bid = blockIdx.x;
   for (uint32_t d = threadIdx.x; d <= B; d += kBlock) h[d] = 0;
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     if (threadIdx.x == 0) { sc->n_large = 0; sc->max_large = 0; sc->n_chunks = 0; sc->n_medium = 0; }
     if (threadIdx.x < kNSub) queue_final(sc, src.qc, src.q, src.subcap);
   }
   __syncthreads();
   uint32_t start, end;
-  bkt_block_range(src, start, end);
+  bkt_block_range(src, start, end, bid);
   if (start == end) return;  // no row: the consumers take an empty block's offsets as 0 (bkt_fused_load)
   for (uint32_t j0 = start + threadIdx.x; j0 < end; j0 += kBlock * kBktUnroll) {
     uint32_t k[kBktUnroll];
@@ -1126,7 +1128,7 @@ __device__ __forceinline__ void bkt_local_body(const BktSrc& src, DevScalars* sc
   for (uint32_t i = 0; i < per && d0 + i < B; ++i) sum += h[d0 + i];
   uint32_t total;
   uint32_t run = block_excl_scan(sum, red, total);
-  uint32_t* row = poff + (size_t)blockIdx.x * (B + 1);
+  uint32_t* row = poff + (size_t)bid * (B + 1);
   for (uint32_t i = 0; i < per && d0 + i < B; ++i) {
     const uint32_t c = h[d0 + i];
     h[d0 + i] = run;
@@ -2483,8 +2485,11 @@ __global__ __launch_bounds__(kBlock) void k_tb_bucket(TBPolicy p, BktSrc src, co
   tgsim_record rec[kIPT];
   uint32_t slot[kIPT];
   if (!bkt_fused_load<true>(src, poff, kv, kscr, vscr, kout, vout, bd, B, K, off, nullptr, medium, large, sc,
-                            sm, h, p.A, TBKey{}, rec, slot))
+                            sm, h, p.A, TBKey{}, rec, slot)) {
+    if (threadIdx.x == 0) sc->rest_tb = 1u;  // the bucket's keys are listed for k_rest<TB>
     return;
+  }
+  if (sm.maxlen > kBktRankMax && threadIdx.x == 0) sc->rest_tb = 1u;  // so are its long keys
   // the GCRA along each sender's run (one thread per sender); departures replace k1
   for (uint32_t i = threadIdx.x; i < h.nk; i += kBlock) {
     const uint32_t a = i ? sm.cnt[i - 1] : 0u, e = sm.cnt[i];
@@ -5089,6 +5094,56 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
   rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, blockIdx.x, gridDim.x);
 }
 
+// Window end, first pass of a single-shard context whose window ran the token bucket: k_rest<TB>
+// (the senders with long runs) shares the launch with k_local_hist's partition of D and histogram of
+// L, which read what it appends - a launch of its own cost ~4.5 us at the dependent-launch boundary
+// even with nothing to do, which is nearly every window. sc->rest_tb (set by
+// k_tb_bucket, constant in this launch) says whether it has work: if not, the first kRestRoles blocks
+// leave at once and blocks [kRestRoles, kRestRoles + 2 kRadixBlocks) are the partition and histogram
+// blocks, as in k_local_hist. If so, roles go by ticket: tickets [0, kRestRoles) run rest_body, then
+// count themselves done after a release; a partition or histogram block (a later ticket) waits for all
+// of them, so it only waits on roles that running workgroups hold (whatever the dispatch order).
+constexpr uint32_t kRestRoles = 256;
+__global__ __launch_bounds__(kBlock) void k_rest_local_hist(TBPolicy p, const uint32_t* keys, const uint32_t* vals,
+                                                            const uint32_t* off, const uint32_t* medium,
+                                                            const LargeSeg* large, DevScalars* sc, uint64_t* K1a,
+                                                            uint64_t* K2a, uint32_t* K3a, uint64_t* K1b, uint64_t* K2b,
+                                                            uint32_t* K3b, BktSrc srcD, BktDiv bdD, uint32_t BD,
+                                                            uint2* kv, uint32_t* poff, BktSrc srcL, BktDiv bdL,
+                                                            uint32_t BL, uint32_t* hist) {
+  __shared__ uint32_t s_role;
+  const bool busy = sc->rest_tb != 0u;  // launch-uniform: written by k_tb_bucket, read-only here
+  uint32_t role = blockIdx.x;
+  if (busy) {
+    if (threadIdx.x == 0) s_role = atomicAdd(&sc->rest_ticket, 1u);
+    __syncthreads();
+    role = __builtin_amdgcn_readfirstlane(s_role);
+  }
+  if (role < kRestRoles) {
+    if (!busy) return;
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, role, kRestRoles);
+    // its departures (D, L), token state and queue counts are visible device-wide before it counts
+    if (block_release_for_count()) atomicAdd(&sc->rest_done, 1u);
+    return;
+  }
+  role -= kRestRoles;
+  if (busy) {
+    if (threadIdx.x == 0) {
+      uint32_t spins = 0;
+      while (__hip_atomic_fetch_add(&sc->rest_done, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < kRestRoles) {
+        __builtin_amdgcn_s_sleep(TGSIM_SPIN_SLEEP);
+        if (++spins == (1u << 24)) {  // a bound, never expected: report instead of hanging the device
+          atomicOr(&sc->err, ERR_TASKS);
+          break;
+        }
+      }
+    }
+    block_acquire_after_poll();
+  }
+  if (role < (uint32_t)kRadixBlocks) bkt_local_body(srcD, sc, bdD, BD, kv, poff, role);
+  else bkt_hist_body(srcL, sc, bdL, BL, hist, role - kRadixBlocks);
+}
+
 // Window end, last pass: the wheel insert (blocks [0, kRadixBlocks)) and the deliveries' long
 // inboxes (k_rest<Emit>, the other blocks) are independent after k_emit_bucket, so they share one
 // launch: a launch that finds nothing to do still costs ~4.5 us at a dependent-launch boundary
@@ -5532,10 +5587,15 @@ static hipError_t launch_rest(Dev& d, const P& p, const uint32_t* keys, const ui
 
 // Token bucket: partition the due copies by sender bucket, then one workgroup per bucket groups
 // and runs the GCRA in LDS (k_tb_bucket); long senders finish in k_rest.
-static hipError_t run_token_bucket(Dev& d) {
+static TBPolicy tb_policy(Dev& d) {
   TBPolicy p;
   p.A = d.A; p.shape = d.tbs; p.X = d.X; p.pend = pend_ref(d); p.lo = d.lo; p.geo = make_geo(d); p.Q = make_queues(d);
   p.sc = d.sc;
+  return p;
+}
+
+static hipError_t run_token_bucket(Dev& d) {
+  const TBPolicy p = tb_policy(d);
   const BktDiv bd = bkt_div(bkt_width_fused(d, d.nloc));
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;  // <= kMaxBins (bkt_width_fused)
   if (B > (uint32_t)kMaxBins) return hipErrorInvalidValue;
@@ -5547,8 +5607,15 @@ static hipError_t run_token_bucket(Dev& d) {
                        d.vals2, d.keys0, d.vals0, bd, B, d.nloc, d.seg_off, d.medium, d.large, d.sc);
   }
   TG_CHECK(hipGetLastError());
-  return launch_rest(d, p, d.keys0, d.vals0);
+#ifndef TGSIM_REST_OWN_LAUNCH  // experiment build: k_rest<TB> in a launch of its own (the round-5 form)
+  if (d.S == 1) {  // nothing reads its outputs before the window end's first launch, which runs it
+    d.tb_rest_owed = true;
+    return hipSuccess;
+  }
+#endif
+  return launch_rest(d, p, d.keys0, d.vals0);  // sharded: the exchange headers read its copies
 }
+
 
 // k_shape_seq_wide's grid: one workgroup per CU (its 16 waves at <= 128 VGPRs fill the CU), each
 // walking its senders one ahead (the next sender's loads in flight); a workgroup per sender left
@@ -5668,6 +5735,7 @@ hipError_t launch_reset_corr(Dev& d, const uint32_t* pairs_dev, uint32_t n) {
 }
 
 hipError_t window_begin(Dev& d, uint32_t n_staged, const uint32_t* n_dev) {
+  d.tb_rest_owed = false;
   Queues Q = make_queues(d);  // the extraction plan was made by k_window_start
   if (n_dev) n_staged = d.cap_msgs;  // device-counted: size the launches for the capacity (grid-stride)
   HeavyOut ho;
@@ -5736,7 +5804,13 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
   const uint32_t B = (d.nloc + bd.w - 1) / bd.w;
   if (B > (uint32_t)kMaxBins) return hipErrorInvalidValue;
   const BktSrc srcD = bkt_queue(d, Q_D), srcL = bkt_queue(d, Q_L);
-  {
+  if (d.tb_rest_owed) {
+    d.tb_rest_owed = false;
+    ProfScope ps_(d, KID_BKT_SCATTER);
+    hipLaunchKernelGGL(k_rest_local_hist, dim3(kRestRoles + 2 * kRadixBlocks), dim3(kBlock), 0, d.stream,
+                       tb_policy(d), d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.sc, d.K1a, d.K2a, d.K3a,
+                       d.K1b, d.K2b, d.K3b, srcD, bd, B, d.kv1, d.poff, srcL, bkt_div(1), d.slots, d.hist);
+  } else {
     ProfScope ps_(d, KID_BKT_SCATTER);
     hipLaunchKernelGGL(k_local_hist, dim3(2 * kRadixBlocks), dim3(kBlock), 0, d.stream, srcD, d.sc, bd, B, d.kv1,
                        d.poff, srcL, bkt_div(1), d.slots, d.hist);
