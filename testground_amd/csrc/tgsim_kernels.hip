@@ -5147,7 +5147,9 @@ __global__ __launch_bounds__(kBlock) void k_rest_local_hist(TBPolicy p, const ui
 // Window end, last pass: the wheel insert (blocks [0, kRadixBlocks)) and the deliveries' long
 // inboxes (k_rest<Emit>, the other blocks) are independent after k_emit_bucket, so they share one
 // launch: a launch that finds nothing to do still costs ~4.5 us at a dependent-launch boundary
-// (DESIGN.md 5). The scatter runs one workgroup per CU, so rest_body's LDS costs it no occupancy.
+// (DESIGN.md 5). The scatter runs one workgroup per CU, so rest_body's LDS costs it no occupancy;
+// the storm generator's blocks beside it do lose some (two workgroups per CU: a build without the
+// long-inbox role measured 22.4 against 25.3 us for k_wheel_scatter_gen, less than a launch's ~4.5).
 __global__ __launch_bounds__(kBlock) void k_wheel_scatter(BktSrc src, DevScalars* sc, const tgsim_record* L,
                                                           tgsim_record* arena, uint32_t* dirs, uint32_t slots,
                                                           const uint32_t* hist, const uint32_t* tot, PendRef pend,
