@@ -32,7 +32,8 @@ __host__ __device__ inline uint32_t x_slice_cap(uint32_t xcap) { return (xcap - 
 // then the deferred-message sub-lists' counters (k_shape: message chunk c appends to sub-list c % kDeferSub)
 constexpr int kDeferSub = 16;
 constexpr int kQcDefer = 3 * kNSub + kXSlices * kMaxShards;
-constexpr int kQcLines = kQcDefer + kDeferSub;
+constexpr int kQcRest = kQcDefer + kDeferSub;  // k_rest_local_hist: role tickets, then rest roles done
+constexpr int kQcLines = kQcRest + 2;
 // capacity of one deferred-message sub-list: sub-list s takes chunks s, s + kDeferSub, ... of 256
 // messages, at most ceil(chunks / kDeferSub) of them
 __host__ __device__ inline uint32_t defer_seg_cap(uint32_t cap_msgs) {
@@ -114,7 +115,6 @@ struct DevScalars {
   uint32_t n_hrec;                   // due wheel records of queue-heavy senders copied to the H list
   uint32_t seq_left;                 // senders k_shape_seq_wide left to k_shape_seq (0: it has nothing to do)
   uint32_t rest_tb;                  // k_tb_bucket listed long senders for k_rest<TB> (k_rest_local_hist)
-  uint32_t rest_ticket, rest_done;   // k_rest_local_hist: role tickets claimed, rest roles finished
   // ---- persistent ----
   uint32_t err;                      // sticky ERR_* bits
   uint32_t reg_head, reg_tail;       // region ring (monotonic counters; slot = counter % kMaxRegions)
@@ -122,7 +122,7 @@ struct DevScalars {
   uint64_t arena_head, arena_tail, arena_used, ins_off;  // arena ring (records)
   uint64_t sig_log_used;             // signal log entries used
   uint32_t pend_max;                 // max over local senders of queued copies (k_pend_max, host gate)
-  uint32_t pad_pm;
+  uint32_t rest_tb_last;             // the last window end's rest_tb (a host hint, read at sync points)
   // device-counted staging: once the flood reaction stages its forwards, the staged
   // count lives here (appends go after it); the window's shape pass reads it, window end moves it
   // to n_msgs_last (the status count of that window) and clears it

@@ -1164,6 +1164,7 @@ __global__ __launch_bounds__(kBlock) void k_bkt_local(BktSrc src, DevScalars* sc
 __global__ __launch_bounds__(kBlock) void k_local_hist(BktSrc srcD, DevScalars* sc, BktDiv bdD, uint32_t BD,
                                                        uint2* kv, uint32_t* poff, BktSrc srcL, BktDiv bdL,
                                                        uint32_t BL, uint32_t* hist) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->rest_tb_last = sc->rest_tb;  // 0 here unless k_rest<TB> ran alone
   if (blockIdx.x < (uint32_t)kRadixBlocks) bkt_local_body(srcD, sc, bdD, BD, kv, poff);
   else bkt_hist_body(srcL, sc, bdL, BL, hist, blockIdx.x - kRadixBlocks);
 }
@@ -5098,41 +5099,53 @@ __global__ __launch_bounds__(kBlock) void k_rest(P p, const uint32_t* keys, cons
 // (the senders with long runs) shares the launch with k_local_hist's partition of D and histogram of
 // L, which read what it appends - a launch of its own cost ~4.5 us at the dependent-launch boundary
 // even with nothing to do, which is nearly every window. sc->rest_tb (set by
-// k_tb_bucket, constant in this launch) says whether it has work: if not, the first kRestRoles blocks
-// leave at once and blocks [kRestRoles, kRestRoles + 2 kRadixBlocks) are the partition and histogram
-// blocks, as in k_local_hist. If so, roles go by ticket: tickets [0, kRestRoles) run rest_body, then
-// count themselves done after a release; a partition or histogram block (a later ticket) waits for all
-// of them, so it only waits on roles that running workgroups hold (whatever the dispatch order).
-constexpr uint32_t kRestRoles = 256;
+// k_tb_bucket, constant in this launch) says whether it has work. If not, blocks [0, 2 kRadixBlocks)
+// are the partition and histogram blocks, as in k_local_hist, and the kRestRoles blocks after them
+// leave at once. If so, roles go by ticket: tickets [0, kRestRoles) run rest_body (the launch's two
+// workgroups per CU all start as rest roles) and count themselves done after a release; a partition
+// or histogram block (a later ticket) waits for all of them, so it only waits on roles that running
+// workgroups hold, whatever the dispatch order. The ticket and the count have 128-B lines of their
+// own, and a waiting block polls every ~8k clocks: polling every 128 clocks from every waiting block,
+// on the line of the rest tasks' own counters, made the rest 2.2x slower (config 5 at two floods per
+// wave).
+#ifndef TG_REST_ROLES
+#define TG_REST_ROLES 512
+#endif
+constexpr uint32_t kRestRoles = TG_REST_ROLES;
 __global__ __launch_bounds__(kBlock) void k_rest_local_hist(TBPolicy p, const uint32_t* keys, const uint32_t* vals,
                                                             const uint32_t* off, const uint32_t* medium,
                                                             const LargeSeg* large, DevScalars* sc, uint64_t* K1a,
                                                             uint64_t* K2a, uint32_t* K3a, uint64_t* K1b, uint64_t* K2b,
                                                             uint32_t* K3b, BktSrc srcD, BktDiv bdD, uint32_t BD,
                                                             uint2* kv, uint32_t* poff, BktSrc srcL, BktDiv bdL,
-                                                            uint32_t BL, uint32_t* hist) {
+                                                            uint32_t BL, uint32_t* hist, uint32_t* qc) {
   __shared__ uint32_t s_role;
   const bool busy = sc->rest_tb != 0u;  // launch-uniform: written by k_tb_bucket, read-only here
-  uint32_t role = blockIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->rest_tb_last = busy ? 1u : 0u;
+  uint32_t* ticket = qc + ((uint32_t)kQcRest << 5);
+  uint32_t* done = qc + ((uint32_t)(kQcRest + 1) << 5);
+  uint32_t role;  // [0, 2 kRadixBlocks): partition / histogram; above: rest
   if (busy) {
-    if (threadIdx.x == 0) s_role = atomicAdd(&sc->rest_ticket, 1u);
+    if (threadIdx.x == 0) s_role = atomicAdd(ticket, 1u);
     __syncthreads();
-    role = __builtin_amdgcn_readfirstlane(s_role);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(s_role);
+    role = t < kRestRoles ? 2u * kRadixBlocks + t : t - kRestRoles;
+  } else {
+    role = blockIdx.x;
   }
-  if (role < kRestRoles) {
+  if (role >= 2u * kRadixBlocks) {
     if (!busy) return;
-    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, role, kRestRoles);
+    rest_body(p, keys, vals, off, medium, large, sc, K1a, K2a, K3a, K1b, K2b, K3b, role - 2u * kRadixBlocks, kRestRoles);
     // its departures (D, L), token state and queue counts are visible device-wide before it counts
-    if (block_release_for_count()) atomicAdd(&sc->rest_done, 1u);
+    if (block_release_for_count()) atomicAdd(done, 1u);
     return;
   }
-  role -= kRestRoles;
   if (busy) {
     if (threadIdx.x == 0) {
       uint32_t spins = 0;
-      while (__hip_atomic_fetch_add(&sc->rest_done, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < kRestRoles) {
-        __builtin_amdgcn_s_sleep(TGSIM_SPIN_SLEEP);
-        if (++spins == (1u << 24)) {  // a bound, never expected: report instead of hanging the device
+      while (__hip_atomic_fetch_add(done, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < kRestRoles) {
+        __builtin_amdgcn_s_sleep(127);
+        if (++spins == (1u << 20)) {  // a bound, never expected: report instead of hanging the device
           atomicOr(&sc->err, ERR_TASKS);
           break;
         }
@@ -5610,7 +5623,11 @@ static hipError_t run_token_bucket(Dev& d) {
   }
   TG_CHECK(hipGetLastError());
 #ifndef TGSIM_REST_OWN_LAUNCH  // experiment build: k_rest<TB> in a launch of its own (the round-5 form)
-  if (d.S == 1) {  // nothing reads its outputs before the window end's first launch, which runs it
+  // nothing reads its outputs before the window end's first launch, which then runs it - unless the
+  // last window the host saw (a sync point) had long senders: a busy k_rest<TB> runs faster in a launch
+  // of its own (config 5 at two floods per wave: 1.07 against 1.13 ms per window), and such windows
+  // come in runs (the hint only picks the launch; both forms give the same results)
+  if (d.S == 1 && !d.h_sc->rest_tb_last) {
     d.tb_rest_owed = true;
     return hipSuccess;
   }
@@ -5811,7 +5828,7 @@ static hipError_t window_end_impl(Dev& d, const uint32_t* spec_round, uint32_t s
     ProfScope ps_(d, KID_BKT_SCATTER);
     hipLaunchKernelGGL(k_rest_local_hist, dim3(kRestRoles + 2 * kRadixBlocks), dim3(kBlock), 0, d.stream,
                        tb_policy(d), d.keys0, d.vals0, d.seg_off, d.medium, d.large, d.sc, d.K1a, d.K2a, d.K3a,
-                       d.K1b, d.K2b, d.K3b, srcD, bd, B, d.kv1, d.poff, srcL, bkt_div(1), d.slots, d.hist);
+                       d.K1b, d.K2b, d.K3b, srcD, bd, B, d.kv1, d.poff, srcL, bkt_div(1), d.slots, d.hist, d.qc);
   } else {
     ProfScope ps_(d, KID_BKT_SCATTER);
     hipLaunchKernelGGL(k_local_hist, dim3(2 * kRadixBlocks), dim3(kBlock), 0, d.stream, srcD, d.sc, bd, B, d.kv1,
