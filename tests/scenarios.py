@@ -285,6 +285,50 @@ def run_bucket_overflow(binding, seed: int, n_inst: int = 4096, per_sender: int 
     return out
 
 
+def run_rest_hint(binding, seed: int, n_inst: int = 512, pattern=(1, 1, 0, 1, 0, 0, 1, 1), heavy: int = 4,
+                  burst: int = 700, counters=None):
+    """Token-bucket windows that do and do not leave long senders to k_rest<TB>, in runs: a window
+    whose `pattern` entry is 1 has `heavy` bandwidth-limited senders send `burst` messages each (a key
+    run past kBktRankMax in their bucket), every other sender 3. With a sync after every window, a
+    busy window after a quiet one runs k_rest<TB> inside the window end's first launch
+    (k_rest_local_hist, busy roles by ticket), one after a busy one in a launch of its own (the host
+    hint), and a quiet one after a busy one resets the hint - every form against the oracle."""
+    rng = np.random.default_rng(seed)
+    sim = Simulator(SimConfig(n_instances=n_inst, seed=seed, max_msgs_per_window=1 << 16, max_records=1 << 19),
+                    binding=binding)
+    # no duplicates and heavy senders that drain within the window: a burst stays under netem's
+    # 1000-packet limit, so the queue-limit lane (k_shape_seq) never takes it from the token bucket
+    hv = rng.choice(n_inst, heavy, replace=False)
+    for g in range(n_inst):
+        bw = 4_000_000_000 if g in hv else int(rng.choice([20_000_000, 200_000_000]))
+        sim.set_shape(g, make_shape(latency_ns=int(rng.choice([0, 1])) * MS, jitter_ns=int(rng.choice([0, MS // 2])),
+                                    bandwidth_bps=bw, loss=1.0))
+    out = []
+    t0 = 0
+    for w, busy in enumerate(pattern):
+        per = np.full(n_inst, 3)
+        if busy:
+            per[hv] = burst
+        src = np.repeat(np.arange(n_inst), per)
+        n = len(src)
+        dst = rng.integers(0, n_inst, n)
+        dst[dst == src] = (dst[dst == src] + 1) % n_inst
+        seq = np.concatenate([np.arange(k) for k in per]) + w * burst
+        t = t0 + rng.integers(0, 2 * MS, n)
+        sim.enqueue(src, dst, seq, rng.choice([200, 1200], n), t)
+        t0 += 4 * MS
+        sim.advance(t0)
+        out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+        if counters is not None:
+            counters.append(sim.kernel_counters())
+    t0 += 200 * MS
+    sim.advance(t0)
+    out.append(dict(status=sim.status(), deliv=sim.deliveries(), inbox=sim.inbox_offsets()))
+    out.append(dict(stats=parity_stats(sim)))
+    sim.close()
+    return out
+
+
 def run_burst(binding, seed: int, n_inst: int = 10, windows: int = 5, per_sender: int = 1400,
               window_ns: int = 4 * MS, restart=None):
     """Senders whose bursts overrun netem's 1000-packet queue under every kind of

@@ -70,6 +70,17 @@ def test_bucket_overflow_spans(hip, oracle, seed):
     assert kc[-1]["long_emit"] > 100_000 and kc[-1]["long_tb"] > 10_000  # the global form ran on both
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_token_bucket_rest_forms(hip, oracle, seed):
+    """Busy and quiet token-bucket windows in runs: k_rest<TB> inside the window end's first launch
+    and in a launch of its own (the host hint after a busy window), HIP = oracle."""
+    kc = []
+    a = S.run_rest_hint(hip, seed, counters=kc)
+    S.assert_same(a, S.run_rest_hint(oracle, seed))
+    longs = [kc[0]["long_tb"]] + [y["long_tb"] - x["long_tb"] for x, y in zip(kc, kc[1:])]
+    assert all(v > 0 for v, b in zip(longs, (1, 1, 0, 1, 0, 0, 1, 1)) if b)  # every busy window went to k_rest
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_queue_limit_bursts(hip, oracle, seed):
     """netem's 1000-packet queue under every shape kind, across windows."""
